@@ -1,0 +1,224 @@
+"""ctypes front end of the CPU oracle (oracle/kle_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker.  The product never imports it.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_gauss.argtypes = [C.c_int, f64p, f64p]
+        L.orc_lobatto.argtypes = [C.c_int, f64p, f64p]
+        L.orc_spectral_order.argtypes = [C.c_int, C.c_int, i32p]
+        L.orc_elem_create.restype = C.c_void_p
+        L.orc_elem_create.argtypes = [C.c_int, C.c_int]
+        L.orc_elem_destroy.argtypes = [C.c_void_p]
+        L.orc_elem_table.argtypes = [C.c_void_p, C.c_int, C.c_int, f64p]
+        L.orc_elem_npoints.argtypes = [C.c_void_p, C.c_int]
+        L.orc_elem_kle.argtypes = [C.c_void_p, f64p, f64p, f64p, f64p]
+        L.orc_elem_ops.argtypes = [C.c_void_p, f64p, f64p, f64p, f64p, f64p]
+        L.orc_mesh_box.restype = C.c_void_p
+        L.orc_mesh_box.argtypes = [C.c_int, i64p, f64p, f64p, C.c_int]
+        L.orc_mesh_destroy.argtypes = [C.c_void_p]
+        L.orc_mesh_nnodes.restype = C.c_int64
+        L.orc_mesh_nnodes.argtypes = [C.c_void_p]
+        L.orc_mesh_nelems.restype = C.c_int64
+        L.orc_mesh_nelems.argtypes = [C.c_void_p]
+        L.orc_mesh_conn.argtypes = [C.c_void_p, i64p]
+        L.orc_mesh_corners.argtypes = [C.c_void_p, f64p]
+        L.orc_mesh_coords.argtypes = [C.c_void_p, f64p]
+        L.orc_assemble_fs.argtypes = [C.c_void_p, u8p, C.POINTER(C.c_void_p),
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.orc_csr_destroy.argtypes = [C.c_void_p]
+        L.orc_csr_nnz.restype = C.c_int64
+        L.orc_csr_nnz.argtypes = [C.c_void_p]
+        L.orc_csr_rows.restype = C.c_int64
+        L.orc_csr_rows.argtypes = [C.c_void_p]
+        L.orc_csr_export.argtypes = [C.c_void_p, i64p, i64p, f64p]
+        L.orc_csr_from.restype = C.c_void_p
+        L.orc_csr_from.argtypes = [C.c_int64, C.c_int64, i64p, i64p, f64p]
+        L.orc_spmv.argtypes = [C.c_void_p, f64p, f64p]
+        L.orc_cg.restype = C.c_int
+        L.orc_cg.argtypes = [C.c_void_p, f64p, f64p, C.c_double, C.c_double, C.c_int,
+                             C.c_int, C.c_int, C.POINTER(C.c_double)]
+        L.orc_num_threads.restype = C.c_int
+        L.orc_set_num_threads.argtypes = [C.c_int]
+        _LIB = L
+    return _LIB
+
+
+def gauss(n):
+    x, w = np.zeros(n), np.zeros(n)
+    lib().orc_gauss(n, x, w)
+    return x, w
+
+
+def lobatto(n):
+    x, w = np.zeros(n), np.zeros(n)
+    lib().orc_lobatto(n, x, w)
+    return x, w
+
+
+def spectral_order(dim, n):
+    out = np.zeros(n ** dim, dtype=np.int32)
+    lib().orc_spectral_order(dim, n, out)
+    return out
+
+
+SETS = {"full": 0, "red": 1, "op": 2, "coo": 3, "cooRed": 4, "cooOp": 5}
+
+
+class Element:
+    """Restated Spectral(ngl, dim) (spectral.py:17-90)."""
+
+    def __init__(self, ngl, dim):
+        self.ngl, self.dim = ngl, dim
+        self.nn = ngl ** dim
+        self.dim_w = 1 if dim == 2 else 3
+        self.dim_s = 3 if dim == 2 else 6
+        self._h = lib().orc_elem_create(dim, ngl)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_elem_destroy(self._h)
+
+    def table(self, which, what):
+        s = SETS[which]
+        nq = lib().orc_elem_npoints(self._h, s)
+        nn = 2 ** self.dim if which.startswith("coo") else self.nn
+        shape = {0: (nq, nn), 1: (nq, self.dim, nn), 2: (nq,), 3: (nq, self.dim)}[what]
+        out = np.zeros(int(np.prod(shape)))
+        lib().orc_elem_table(self._h, s, what, out)
+        return out.reshape(shape)
+
+    def kle(self, X):
+        nd = self.dim * self.nn
+        K = np.zeros((nd, nd))
+        Rw = np.zeros((nd, self.dim_w * self.nn))
+        Rd = np.zeros((nd, self.nn))
+        lib().orc_elem_kle(self._h, np.ascontiguousarray(X, dtype=float), K, Rw, Rd)
+        return K, Rw, Rd
+
+    def ops(self, X):
+        nd, nn = self.dim * self.nn, self.nn
+        SrT = np.zeros((self.dim_s * nn, nd))
+        Div = np.zeros((nd, self.dim_s * nn))
+        Curl = np.zeros((self.dim_w * nn, nd))
+        W = np.zeros(nn)
+        lib().orc_elem_ops(self._h, np.ascontiguousarray(X, dtype=float), SrT, Div, Curl, W)
+        return SrT, Div, Curl, W
+
+
+class CSR:
+    def __init__(self, handle, ncols=None):
+        self._h = handle
+        L = lib()
+        self.m = L.orc_csr_rows(handle)
+        self.nnz = L.orc_csr_nnz(handle)
+        self.indptr = np.zeros(self.m + 1, dtype=np.int64)
+        self.indices = np.zeros(max(self.nnz, 1), dtype=np.int64)
+        self.data = np.zeros(max(self.nnz, 1))
+        L.orc_csr_export(handle, self.indptr, self.indices, self.data)
+        self.indices = self.indices[: self.nnz]
+        self.data = self.data[: self.nnz]
+        self.n = ncols
+
+    @classmethod
+    def from_arrays(cls, indptr, indices, data, ncols):
+        h = lib().orc_csr_from(len(indptr) - 1, ncols, np.ascontiguousarray(indptr, np.int64),
+                               np.ascontiguousarray(indices, np.int64),
+                               np.ascontiguousarray(data, np.float64))
+        return cls(h, ncols)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_csr_destroy(self._h)
+
+    def mult(self, x):
+        y = np.zeros(self.m)
+        lib().orc_spmv(self._h, np.ascontiguousarray(x, np.float64), y)
+        return y
+
+    def cg(self, b, rtol=1e-10, atol=0.0, maxit=100000, jacobi=True, fixed_iters=False):
+        x = np.zeros(self.m)
+        rr = C.c_double(0)
+        it = lib().orc_cg(self._h, np.ascontiguousarray(b, np.float64), x, rtol, atol, maxit,
+                          int(jacobi), int(fixed_iters), C.byref(rr))
+        return x, it, rr.value
+
+    def dense(self):
+        d = np.zeros((self.m, self.n))
+        for r in range(self.m):
+            d[r, self.indices[self.indptr[r]:self.indptr[r + 1]]] = \
+                self.data[self.indptr[r]:self.indptr[r + 1]]
+        return d
+
+
+class BoxMesh:
+    """Structured box mesh in the canonical numbering (see kle_oracle.c)."""
+
+    def __init__(self, dim, nelem, lower, upper, ngl):
+        self.dim, self.ngl = dim, ngl
+        self.nn = ngl ** dim
+        self._h = lib().orc_mesh_box(dim, np.array(list(nelem) + [1] * (3 - dim), np.int64),
+                                     np.array(list(lower) + [0.0] * (3 - dim), float),
+                                     np.array(list(upper) + [1.0] * (3 - dim), float), ngl)
+        self.N = lib().orc_mesh_nnodes(self._h)
+        self.E = lib().orc_mesh_nelems(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_mesh_destroy(self._h)
+
+    def conn(self):
+        out = np.zeros(self.E * self.nn, dtype=np.int64)
+        lib().orc_mesh_conn(self._h, out)
+        return out.reshape(self.E, self.nn)
+
+    def corners(self):
+        out = np.zeros(self.E * 2 ** self.dim * self.dim)
+        lib().orc_mesh_corners(self._h, out)
+        return out.reshape(self.E, 2 ** self.dim, self.dim)
+
+    def coords(self):
+        out = np.zeros(self.N * self.dim)
+        lib().orc_mesh_coords(self._h, out)
+        return out.reshape(self.N, self.dim)
+
+    def assemble_fs(self, dir_flag):
+        K, Kr, Rw = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        lib().orc_assemble_fs(self._h, np.ascontiguousarray(dir_flag, np.uint8),
+                              C.byref(K), C.byref(Kr), C.byref(Rw))
+        dw = 1 if self.dim == 2 else 3
+        return (CSR(K.value, self.N * self.dim), CSR(Kr.value, self.N * self.dim),
+                CSR(Rw.value, self.N * dw))
+
+
+def set_threads(n):
+    lib().orc_set_num_threads(int(n))
+
+
+def num_threads():
+    return lib().orc_num_threads()
