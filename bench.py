@@ -1,0 +1,262 @@
+"""Benchmark: KLE CG iterations/s + SpMV GB/s vs the HBM roofline on the
+BASELINE.json config 2 workload (3-D KLE Laplacian, structured hex mesh
+[20,16,16], p=4 / ngl=5, ~1M DoF, Taylor-Green-3D Dirichlet data).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+A "step" is one CG iteration (SpMV + fused dot, Jacobi z/p update, x/r
+update, two deterministic reductions) on the assembled device matrix; the
+K steps are timed between barriers, max over ranks.  Assembly (device
+element kernels + gather) is untimed setup.  A full solve to rtol 1e-10 is
+run once for the convergence record.  The roofline uses HIP-event timings of
+the SpMV kernel inside the timed region and the algorithmic bytes of the
+node-block format; `traffic` comes from the rocprofv3 PMC pass recorded in
+profiles/ (or null).  cpu_baseline: the C oracle's CSR CG on the same
+matrix, OpenMP on the host cores, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+METRIC = "KLE CG iters/sec + SpMV GB/s (vs HBM roofline), 1M-DoF p=4 hex mesh"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--nelem", type=str, default="20,16,16")
+    ap.add_argument("--ngl", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-solve", action="store_true")
+    ap.add_argument("--aij", action="store_true", help="also time the scalar-CSR (aij) SpMV")
+    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def init_dist(n):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        return dist
+    if n > 1:
+        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    return None
+
+
+def main():
+    args = parse()
+    dist = init_dist(args.gpus)
+    import numpy as np
+
+    import pynama_amd as pa
+    from pynama_amd import fields
+    from pynama_amd.petsc import KSP, PC
+
+    ctx = pa.get_ctx()
+    rank, nranks = ctx.rank, ctx.nranks
+    nelem = [int(v) for v in args.nelem.split(",")]
+    dim = len(nelem)
+    cfg = {"domain": {"ngl": args.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * dim, "upper": [1.0] * dim}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d" if dim == 3 else "taylor_green"}}}
+    t0 = time.perf_counter()
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    mat.build()
+    ctx.synchronize()
+    t_asm = time.perf_counter() - t1
+    sol = pa.KleSolver()
+    sol.setMat(mat)
+    sol.setUp()
+    f = fields.get(cfg["boundary-conditions"]["custom-func"]["name"])
+    nu = 0.01 / 0.5  # taylor-green3d.yaml material (rho 0.5, mu 0.01)
+    vort = mat.Rw.createVecRight()
+    vort.setArray(f.vorticity(dom.getFullCoordArray(), f.alpha(nu, 0.0)))
+    vel = sol.getSolution()
+    dom.applyBoundaryConditions(vel, "velocity", 0.0, nu)
+    b = sol.rhs(vort).copy()
+    t_setup = time.perf_counter() - t0
+
+    K = mat.K
+    n_global = K.getSize()[0]
+    info = K.getInfo()
+    nnz_local = info["nz_used"]
+    spmv_bytes_local = K.spmvBytes()
+
+    # --- full solve to convergence (correctness record, untimed for the metric)
+    solve = {}
+    if not args.no_solve:
+        ksp = sol.getKSP()
+        ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=200000)
+        ctx.barrier()
+        ts = time.perf_counter()
+        sol.solve(vort)
+        ctx.barrier()
+        solve = {"rtol": 1e-10, "iterations": ksp.getIterationNumber(), "reason": ksp.getConvergedReason(),
+                 "true_rel_residual": ksp.getTrueRelativeResidual(), "seconds": time.perf_counter() - ts}
+
+    # --- timed fixed-iteration CG
+    kb = KSP().create()
+    kb.setType("cg")
+    pc = PC()
+    pc.setType("jacobi")
+    kb.setPC(pc)
+    kb.setOperators(K)
+    kb.setUp()
+    x = K.createVecRight()
+    if args.warmup > 0:
+        kb.setFixedIterations(args.warmup)
+        kb.solve(b, x)
+    kb.setFixedIterations(args.steps)
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    ctx.barrier()
+    if dist is not None:
+        dist.barrier()
+    t_start = time.perf_counter()
+    kb.solve(b, x)
+    ctx.barrier()
+    t_loc = time.perf_counter() - t_start
+    ctx.set_profiling(False)
+    spmv_cnt, spmv_ms = ctx.kernel_stats("spmv")
+    upd_cnt, upd_ms = ctx.kernel_stats("cg_update")
+    p_cnt, p_ms = ctx.kernel_stats("p_update")
+    red_cnt, red_ms = ctx.kernel_stats("reduce")
+    halo_cnt, halo_ms = ctx.kernel_stats("halo")
+    t_max = t_loc
+    tot_bytes = spmv_bytes_local
+    tot_nnz = nnz_local
+    spmv_avg_ms = spmv_ms / max(spmv_cnt, 1)
+    if dist is not None:
+        import torch
+        tt = torch.tensor([t_loc, spmv_avg_ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max, spmv_avg_max = float(tt[0]), float(tt[1])
+        sb = torch.tensor([spmv_bytes_local, float(nnz_local)], dtype=torch.float64)
+        dist.all_reduce(sb, op=dist.ReduceOp.SUM)
+        tot_bytes, tot_nnz = float(sb[0]), int(sb[1])
+    else:
+        spmv_avg_max = spmv_avg_ms
+    if "torch" in sys.modules:  # torch is only the launcher's plumbing here
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    iters_per_s = args.steps / t_max
+    achieved = tot_bytes / (spmv_avg_max * 1e-3) / 1e9 if spmv_avg_max > 0 else None
+
+    aij = None
+    if args.aij and nranks == 1:
+        A = K.convert("aij")
+        xa = A.createVecRight()
+        ya = A.createVecLeft()
+        xa.setArray(np.random.default_rng(0).uniform(-1, 1, xa.getLocalSize()))
+        for _ in range(5):
+            A.mult(xa, ya)
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        for _ in range(50):
+            A.mult(xa, ya)
+        ctx.synchronize()
+        c, ms = ctx.kernel_stats("spmv")
+        ctx.set_profiling(False)
+        ab = A.spmvBytes()
+        aij = {"format": "aij (scalar CSR, int32 cols)", "bytes_per_spmv": ab, "avg_ms": ms / c,
+               "gbps": ab / (ms / c * 1e-3) / 1e9, "frac": ab / (ms / c * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        del A
+
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            key = f"{nelem}-{args.ngl}-{nranks}"
+            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and nranks == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(K, b, args.cpu_seconds)
+
+    if rank == 0:
+        stream = ctx.stream_copy_gbps(1 << 30, 10)
+        line = {
+            "metric": METRIC,
+            "value": iters_per_s,
+            "unit": "CG iters/s",
+            "n_gpus": nranks,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Taylor-Green-3D vorticity + Dirichlet velocity on a generated box mesh)",
+            "config": {"workload": f"KLE Laplacian {dim}-D box {nelem} ngl={args.ngl} (p={args.ngl - 1}), "
+                                   f"TG-{dim}D Dirichlet on all faces; one CG(+Jacobi) iteration per step",
+                       "nelem": nelem, "ngl": args.ngl, "n_dof": n_global, "nnz_K": tot_nnz,
+                       "ksp": "cg", "pc": "jacobi", "matrix_format": info["format"],
+                       "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                         "kernel": "k_nb_spmv<3,3,true>", "bytes_per_launch": tot_bytes,
+                         "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt},
+            "cpu_baseline": cpu,
+            "spmv_gbps": achieved,
+            "stream_copy_gbps": stream,
+            "breakdown_ms_per_iter": {"spmv": spmv_ms / max(args.steps, 1), "cg_update": upd_ms / max(args.steps, 1),
+                                      "p_update": p_ms / max(args.steps, 1), "reduce": red_ms / max(args.steps, 1),
+                                      "halo": halo_ms / max(args.steps, 1)},
+            "assembly_s": t_asm,
+            "setup_s": t_setup,
+            "solve": solve,
+            "aij_spmv": aij,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(K, b, seconds):
+    """Oracle CSR CG (OpenMP) on the same matrix: bounded sample of ~`seconds`."""
+    import numpy as np
+
+    from oracle import oracle as O
+    ip, ix, d = K.getValuesCSR()
+    A = O.CSR.from_arrays(ip, ix, d, int(ip.shape[0] - 1))
+    del ip, ix, d
+    bb = b.getArray()
+    threads = O.num_threads()
+    # calibrate: 2 iterations, then size the sample to ~seconds
+    t = time.perf_counter()
+    A.cg(bb, fixed_iters=True, maxit=2)
+    per = (time.perf_counter() - t) / 2
+    its = max(3, int(seconds / max(per, 1e-6)))
+    t = time.perf_counter()
+    A.cg(bb, fixed_iters=True, maxit=its)
+    el = time.perf_counter() - t
+    return {"value": its / el, "unit": "CG iters/s", "cores": threads, "kind": "port",
+            "sample": f"{its} fixed CG+Jacobi iterations of oracle/kle_oracle.c (CSR, OpenMP) on the same "
+                      f"assembled K ({A.nnz} nnz), {el:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,224 @@
+/*
+ * kle.h -- C ABI of libkle.so, the MI355X-native KLE assembly + Krylov library.
+ *
+ * This is the drop-in boundary.  It replaces, for Pynama's hot path, the
+ * petsc4py objects the reference creates and the Python element loops that
+ * fill them (paths are under the reference's src/):
+ *
+ *   PETSc Mat (AIJ)  createAIJ/setValues/assemble/mult/diagonalScale
+ *                      matrices/mat_fs.py:102-106,115-120,175-186,245-267
+ *   PETSc Vec          createMPI/setValues/axpy/scale/dot/norm/...
+ *                      matrices/mat_fs.py:228-236, cases/base_problem.py:129-154
+ *   PETSc KSP/PC       KspSolver.createSolver / KleSolver.solve
+ *                      solver/kle_solver.py:33-41,54-64
+ *   MatFS.build element loops (buildFS, buildOperators)
+ *                      matrices/mat_fs.py:131-201  -> kle_assemble_kle()
+ *   DMPlex box mesh + FEM section numbering
+ *                      domain/dmplex.py:31-49,193-196,382-388 -> kle_mesh_*
+ *
+ * Conventions (PETSc-like):
+ *   - every function returns int: 0 = success, a KLE_ERR_* code otherwise;
+ *     kle_last_error() returns a thread-local message for the last failure.
+ *   - handles are opaque; plain pointers/sizes only, no torch types.
+ *   - all device work is ordered on the context's HIP stream.
+ *   - one process per GPU; ranks partition the mesh into slabs along the
+ *     slowest lattice axis (z in 3-D, y in 2-D).  Collectives (halo exchange,
+ *     Krylov dot products) go over RCCL inside the library.
+ *   - handles are not thread-safe (same as PETSc objects).
+ */
+#ifndef KLE_H
+#define KLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    KLE_OK = 0,
+    KLE_ERR_ARG = 62,        /* PETSC_ERR_ARG_WRONG          */
+    KLE_ERR_SIZ = 60,        /* PETSC_ERR_ARG_SIZ            */
+    KLE_ERR_OUTOFRANGE = 63, /* PETSC_ERR_ARG_OUTOFRANGE     */
+    KLE_ERR_MEM = 55,        /* PETSC_ERR_MEM                */
+    KLE_ERR_SUP = 56,        /* PETSC_ERR_SUP (not supported) */
+    KLE_ERR_STATE = 73,      /* PETSC_ERR_ARG_WRONGSTATE     */
+    KLE_ERR_DEVICE = 76,     /* HIP runtime failure          */
+    KLE_ERR_COMM = 98,       /* RCCL failure                 */
+    KLE_ERR_NEWNZ = 77       /* insertion outside the preallocated pattern */
+};
+
+/* KSP converged reasons (same numeric values as PETSc's KSPConvergedReason). */
+enum {
+    KLE_CONVERGED_RTOL = 2,
+    KLE_CONVERGED_ATOL = 3,
+    KLE_CONVERGED_ITS = 4,
+    KLE_DIVERGED_ITS = -3,
+    KLE_DIVERGED_DTOL = -4,
+    KLE_DIVERGED_BREAKDOWN = -5,
+    KLE_DIVERGED_NANORINF = -9,
+    KLE_CONVERGED_ITERATING = 0
+};
+
+typedef struct kle_ctx kle_ctx;
+typedef struct kle_mesh kle_mesh;
+typedef struct kle_vec kle_vec;
+typedef struct kle_mat kle_mat;
+typedef struct kle_ksp kle_ksp;
+
+const char *kle_last_error(void);
+int kle_version(void);
+
+/* ---------------------------------------------------------------- context */
+/* 128-byte RCCL unique id, produced on rank 0 and broadcast by the caller. */
+int kle_get_unique_id(unsigned char out[128]);
+/* device: HIP ordinal; nranks==1 needs no unique id (pass NULL). */
+int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id,
+                   kle_ctx **out);
+int kle_ctx_destroy(kle_ctx *ctx);
+int kle_ctx_synchronize(kle_ctx *ctx);
+int kle_ctx_barrier(kle_ctx *ctx); /* device-side RCCL barrier + stream sync */
+/* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */
+int kle_ctx_set_profiling(kle_ctx *ctx, int on);
+/* name: "spmv" | "cg_update" | "p_update" | "reduce" | "halo" | "allreduce" */
+int kle_ctx_get_kernel_stats(kle_ctx *ctx, const char *name, int64_t *count, double *total_ms);
+int kle_ctx_reset_kernel_stats(kle_ctx *ctx);
+
+/* ------------------------------------------------------------------- mesh */
+/* Structured box mesh (replaces BoxDom.create + DMPlexDom.setFemIndexing,
+ * dmplex.py:31-49,382-388).  Host-only: usable without a GPU.  Node ids are
+ * lattice-lexicographic (x fastest); cells x-fastest; element-local nodes in
+ * tensor order (kle_mesh_local_order gives the reference spectral order). */
+int kle_mesh_create_box(int dim, const int64_t nelem[3], const double lower[3],
+                        const double upper[3], int ngl, int rank, int nranks, kle_mesh **out);
+int kle_mesh_destroy(kle_mesh *m);
+
+typedef struct {
+    int dim, ngl, rank, nranks;
+    int64_t nelem[3];
+    int64_t lattice[3];     /* nodes per axis                                */
+    int64_t n_nodes;        /* global                                        */
+    int64_t n_elems;        /* global                                        */
+    int64_t node_begin;     /* owned node range [node_begin, node_end)       */
+    int64_t node_end;
+    int64_t ext_begin;      /* owned + ghost node range [ext_begin, ext_end) */
+    int64_t ext_end;
+    int64_t elem_begin;     /* local (owned + ghost) element range           */
+    int64_t elem_end;
+} kle_mesh_info;
+
+int kle_mesh_get_info(const kle_mesh *m, kle_mesh_info *info);
+/* element->global node ids for local elements, tensor order [elem][ngl^dim]. */
+int kle_mesh_get_conn(const kle_mesh *m, int64_t *conn);
+/* cell corners in DMPlex closure order [elem][2^dim][dim] (dmplex.py:93-100). */
+int kle_mesh_get_corners(const kle_mesh *m, double *xyz);
+/* coordinates of the owned nodes [node][dim] (computeFullCoordinates). */
+int kle_mesh_get_coords(const kle_mesh *m, double *xyz);
+/* Boundary nodes of named faces: face bit f follows the reference's naming
+ * (dmplex.py:27-30): 3-D 0 back(z-) 1 front(z+) 2 down(y-) 3 up(y+) 4 right(x+)
+ * 5 left(x-); 2-D 0 down 1 right 2 up 3 left.  Fills the owned boundary
+ * nodes (sorted) and returns their count in *n (pass nodes=NULL to count). */
+int kle_mesh_face_nodes(const kle_mesh *m, unsigned face_mask, int64_t *nodes, int64_t *n);
+/* Dirichlet (free-slip) node set: faces by mask, or explicit global ids. */
+int kle_mesh_set_dirichlet_faces(kle_mesh *m, unsigned face_mask);
+int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n);
+/* Symbolic node-block pattern (host).  which: 0 K, 1 Krhs, 2 Rw.
+ * row_ptr[n_owned+1] (block offsets, unpadded) and col[] (global node ids). */
+int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks);
+int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *cols);
+/* Halo plan of this rank: ghost node counts below/above and neighbour ranks. */
+int kle_mesh_halo(const kle_mesh *m, int64_t *lo_count, int64_t *hi_count, int *lo_rank,
+                  int *hi_rank);
+
+/* -------------------------------------------------------------------- vec */
+/* Mesh vector with bs components per node, ghosted over the ext range. */
+int kle_vec_create_mesh(kle_ctx *ctx, const kle_mesh *m, int bs, kle_vec **out);
+/* Plain distributed vector (no ghosts). */
+int kle_vec_create(kle_ctx *ctx, int64_t n_local, int64_t n_global, kle_vec **out);
+int kle_vec_duplicate(const kle_vec *v, kle_vec **out);
+int kle_vec_destroy(kle_vec *v);
+int kle_vec_get_sizes(const kle_vec *v, int64_t *n_local, int64_t *n_global);
+int kle_vec_get_ownership_range(const kle_vec *v, int64_t *lo, int64_t *hi);
+int kle_vec_set(kle_vec *v, double alpha);
+int kle_vec_copy(const kle_vec *x, kle_vec *y);                 /* y = x          */
+int kle_vec_axpy(kle_vec *y, double alpha, const kle_vec *x);   /* y += a x       */
+int kle_vec_aypx(kle_vec *y, double beta, const kle_vec *x);    /* y = x + b y    */
+int kle_vec_waxpy(kle_vec *w, double alpha, const kle_vec *x, const kle_vec *y); /* w = a x + y */
+int kle_vec_scale(kle_vec *v, double alpha);
+int kle_vec_pointwise_mult(kle_vec *w, const kle_vec *x, const kle_vec *y);
+int kle_vec_reciprocal(kle_vec *v);
+int kle_vec_dot(const kle_vec *x, const kle_vec *y, double *out);
+int kle_vec_norm2(const kle_vec *x, double *out);
+/* Host <-> device.  Indices are GLOBAL; only owned entries may be set.
+ * addv: 0 INSERT_VALUES, 1 ADD_VALUES (applied in index order). */
+int kle_vec_set_values(kle_vec *v, int64_t n, const int64_t *idx, const double *vals, int addv);
+int kle_vec_get_values(const kle_vec *v, int64_t n, const int64_t *idx, double *vals);
+int kle_vec_get_array(const kle_vec *v, double *host_local);     /* owned part */
+int kle_vec_set_array(kle_vec *v, const double *host_local);
+int kle_vec_ghost_update(kle_vec *v);                             /* halo fill  */
+/* raw device pointer to the owned part (for zero-copy interop). */
+int kle_vec_device_ptr(const kle_vec *v, double **dptr);
+
+/* -------------------------------------------------------------------- mat */
+/* Batch device assembly of the KLE system: replaces MatFS.build / buildFS
+ * (mat_fs.py:131-192).  Produces node-block matrices K (dim x dim blocks),
+ * Krhs (dim x dim) and Rw (dim x dim_w) with PETSc's pattern and ADD order. */
+int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw);
+/* Element matrices of local element e in tensor order (parity tests):
+ * K_e [dim n][dim n], Rw_e [dim n][dim_w n] (row-major, n = ngl^dim). */
+int kle_element_kle(kle_ctx *ctx, kle_mesh *m, int64_t e, double *Ke, double *Rwe);
+
+/* Generic AIJ (petsc4py Mat().createAIJ + setValues + assemble). */
+int kle_mat_create_aij(kle_ctx *ctx, int64_t m_local, int64_t n_local, int64_t m_global,
+                       int64_t n_global, const int32_t *d_nnz, const int32_t *o_nnz,
+                       kle_mat **out);
+int kle_mat_set_values(kle_mat *A, int32_t nr, const int64_t *rows, int32_t nc,
+                       const int64_t *cols, const double *v_rowmajor, int addv);
+int kle_mat_assemble(kle_mat *A);
+int kle_mat_destroy(kle_mat *A);
+int kle_mat_get_size(const kle_mat *A, int64_t *m_global, int64_t *n_global);
+int kle_mat_get_ownership_range(const kle_mat *A, int64_t *lo, int64_t *hi);
+int kle_mat_get_local_nnz(const kle_mat *A, int64_t *nnz);
+int kle_mat_mult(kle_mat *A, kle_vec *x, kle_vec *y);            /* y = A x */
+int kle_mat_mult_add(kle_mat *A, kle_vec *x, kle_vec *y, kle_vec *z); /* z = y + A x */
+int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *R);
+int kle_mat_get_diagonal(const kle_mat *A, kle_vec *d);
+/* Y += a X where X's pattern is a subset of, or equal to, Y's. */
+int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X);
+int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out);
+/* Scalar CSR of the owned rows with GLOBAL column ids, PETSc pattern. */
+int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz);
+int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double *data);
+/* Convert (single rank) to the scalar-CSR device format (the AIJ kernel). */
+int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
+/* "nb" (node-block) or "aij". */
+int kle_mat_get_format(const kle_mat *A, char *buf, int buflen);
+/* Bytes one SpMV with this matrix moves (algorithmic: matrix + x + y). */
+int kle_mat_spmv_bytes(const kle_mat *A, double *bytes);
+
+/* -------------------------------------------------------------------- ksp */
+int kle_ksp_create(kle_ctx *ctx, kle_ksp **out);
+int kle_ksp_destroy(kle_ksp *k);
+int kle_ksp_set_type(kle_ksp *k, const char *type);      /* "cg" | "gmres" | "preonly" */
+int kle_ksp_set_pc_type(kle_ksp *k, const char *type);   /* "none" | "jacobi" | "lu"   */
+int kle_ksp_set_tolerances(kle_ksp *k, double rtol, double atol, double dtol, int maxit);
+int kle_ksp_set_gmres_restart(kle_ksp *k, int restart);
+/* Run exactly n iterations, no convergence test (benchmarks); 0 = off. */
+int kle_ksp_set_fixed_iterations(kle_ksp *k, int n);
+int kle_ksp_set_operators(kle_ksp *k, kle_mat *A);
+int kle_ksp_set_up(kle_ksp *k);
+int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x);
+int kle_ksp_get_iteration_number(const kle_ksp *k, int *its);
+int kle_ksp_get_residual_norm(const kle_ksp *k, double *rnorm);
+int kle_ksp_get_converged_reason(const kle_ksp *k, int *reason);
+/* ||b - A x|| / ||b|| recomputed after the last solve. */
+int kle_ksp_get_true_relative_residual(const kle_ksp *k, double *rel);
+
+/* ------------------------------------------------------------ diagnostics */
+/* Streaming read/copy microbenchmark (HBM ceiling for the roofline). */
+int kle_stream_copy_bench(kle_ctx *ctx, int64_t bytes, int reps, double *gbps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,563 @@
+// kle_assemble.hip -- batch device assembly of the KLE system on gfx950.
+//
+// Replaces MatFS.build -> buildFS (mat_fs.py:131-192): the per-cell Python
+// loop that calls Spectral.getElemKLEMatrices (spectral.py:92-160) and
+// inserts the element blocks with MatSetValues(ADD_VALUES).
+//
+// Three kernels:
+//   k_geometry   one thread per (element, Gauss point): Jacobian of the
+//                trilinear map, c_q = w_q det J, inv(J)          (spectral.py:117-120)
+//   k_element    one element x (32x32 node-pair tile) per 256-thread workgroup.
+//                Gauss-point loops staged through LDS in chunks of QC points;
+//                factored form of the element matrices:
+//                  K_e(la,mb) = d_ab G + a_d D_ab + a_w (d_ab tr D - D_ba)
+//                  G   = sum_full c grad N_l . grad N_m
+//                  D_ab= sum_red  c dN_l/dx_a dN_m/dx_b
+//                  Rw_e from E_d = sum_full c N_l dN_m/dx_d and F_d = sum_red c dN_l/dx_d N_m
+//                (algebraically identical to B_gr^T B_gr + a_d B_div^T B_div +
+//                 a_w B_curl^T B_curl of spectral.py:134,155-156)
+//   k_gather     one wavefront per owned node row: for every block column the
+//                lanes sum the element blocks of the cells containing both
+//                nodes in ascending cell order (PETSc single-rank ADD order),
+//                no atomics -> bitwise deterministic.  Dirichlet masking as
+//                mat_fs.py:158-189.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "kle_basis.hpp"
+#include "kle_internal.hpp"
+
+namespace kle {
+
+constexpr double ALPHA_W = 1e2;  // spectral.py:96
+constexpr double ALPHA_D = 1e3;  // spectral.py:97
+constexpr int TL = 32;           // node tile of k_element
+constexpr int QC = 32;           // Gauss points per LDS chunk
+
+struct Tables1D {
+    int np1;          // 1-D points
+    const double *x;  // [np1]
+    const double *w;  // [np1]
+    const double *h;  // [np1][ngl]
+    const double *dh; // [np1][ngl]
+};
+
+// ------------------------------------------------------------- geometry
+template <int DIM>
+__global__ void k_geometry(int64_t nel, int ngl, Tables1D T, const double *__restrict__ corners,
+                           double *__restrict__ geo)
+{
+    const int nq = DIM == 2 ? T.np1 * T.np1 : T.np1 * T.np1 * T.np1;
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= nel * nq) return;
+    const int64_t e = t / nq;
+    const int q = (int)(t % nq);
+    int qi[3] = {q % T.np1, (q / T.np1) % T.np1, DIM == 3 ? q / (T.np1 * T.np1) : 0};
+    double xi[3], wq = 1.0;
+    for (int d = 0; d < DIM; ++d) {
+        xi[d] = T.x[qi[d]];
+        wq *= T.w[qi[d]];
+    }
+    constexpr int NC = 1 << DIM;
+    // closure order of the corners (kle_mesh.cpp CORN2/CORN3)
+    const int c2[4][2] = {{0, 0}, {1, 0}, {1, 1}, {0, 1}};
+    const int c3[8][3] = {{0, 0, 0}, {0, 1, 0}, {1, 1, 0}, {1, 0, 0},
+                          {0, 0, 1}, {1, 0, 1}, {1, 1, 1}, {0, 1, 1}};
+    double J[DIM][DIM] = {};
+    const double *X = corners + e * NC * DIM;
+    for (int c = 0; c < NC; ++c) {
+        double s[3], f[3];
+        for (int d = 0; d < DIM; ++d) {
+            s[d] = 2.0 * (DIM == 2 ? c2[c][d] : c3[c][d]) - 1.0;
+            f[d] = 0.5 * (1.0 + s[d] * xi[d]);
+        }
+        for (int k = 0; k < DIM; ++k) {
+            double dn = 0.5 * s[k];
+            for (int d = 0; d < DIM; ++d)
+                if (d != k) dn *= f[d];
+            for (int j = 0; j < DIM; ++j) J[k][j] += dn * X[c * DIM + j];
+        }
+    }
+    double det, Ji[DIM][DIM];
+    if constexpr (DIM == 2) {
+        det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+        Ji[0][0] = J[1][1] / det;
+        Ji[0][1] = -J[0][1] / det;
+        Ji[1][0] = -J[1][0] / det;
+        Ji[1][1] = J[0][0] / det;
+    } else {
+        const double a00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+        const double a01 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+        const double a02 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+        det = J[0][0] * a00 + J[0][1] * a01 + J[0][2] * a02;
+        Ji[0][0] = a00 / det;
+        Ji[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / det;
+        Ji[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / det;
+        Ji[1][0] = a01 / det;
+        Ji[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / det;
+        Ji[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / det;
+        Ji[2][0] = a02 / det;
+        Ji[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / det;
+        Ji[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / det;
+    }
+    double *g = geo + t * (1 + DIM * DIM);
+    g[0] = wq * det;  // signed det J, as spectral.py:120
+    for (int i = 0; i < DIM; ++i)
+        for (int k = 0; k < DIM; ++k) g[1 + i * DIM + k] = Ji[i][k];
+}
+
+// Fill one LDS chunk: for points q0..q0+QC-1 and the 32 nodes of a tile,
+// value H and physical gradient, optionally scaled by c_q.
+template <int DIM>
+__device__ __forceinline__ void fill_chunk(int ngl, int ne, int nq, const Tables1D &T,
+                                           const double *__restrict__ geo, int q0, int n0,
+                                           bool scale, double (*sH)[TL], double (*sG)[DIM][TL],
+                                           const double (*sgeo)[1 + DIM * DIM], int tid)
+{
+    for (int it = tid; it < QC * TL; it += 256) {
+        const int qq = it / TL, nl = it % TL;
+        const int q = q0 + qq, l = n0 + nl;
+        double hv = 0, g[DIM] = {};
+        if (q < nq && l < ne) {
+            const int qi[3] = {q % T.np1, (q / T.np1) % T.np1, DIM == 3 ? q / (T.np1 * T.np1) : 0};
+            const int li[3] = {l % ngl, (l / ngl) % ngl, DIM == 3 ? l / (ngl * ngl) : 0};
+            double hh[3], dd[3];
+            for (int d = 0; d < DIM; ++d) {
+                hh[d] = T.h[qi[d] * ngl + li[d]];
+                dd[d] = T.dh[qi[d] * ngl + li[d]];
+            }
+            double dref[DIM];
+            if constexpr (DIM == 2) {
+                hv = hh[0] * hh[1];
+                dref[0] = dd[0] * hh[1];
+                dref[1] = hh[0] * dd[1];
+            } else {
+                hv = hh[0] * hh[1] * hh[2];
+                dref[0] = dd[0] * hh[1] * hh[2];
+                dref[1] = hh[0] * dd[1] * hh[2];
+                dref[2] = hh[0] * hh[1] * dd[2];
+            }
+            const double *gq = sgeo[qq];
+            for (int i = 0; i < DIM; ++i) {
+                double s = 0;
+                for (int k = 0; k < DIM; ++k) s += gq[1 + i * DIM + k] * dref[k];
+                g[i] = s;
+            }
+            if (scale) {
+                hv *= gq[0];
+                for (int i = 0; i < DIM; ++i) g[i] *= gq[0];
+            }
+        }
+        sH[qq][nl] = hv;
+        for (int i = 0; i < DIM; ++i) sG[qq][i][nl] = g[i];
+    }
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_element(int ngl, Tables1D TF, Tables1D TR,
+                                                 const double *__restrict__ geoF,
+                                                 const double *__restrict__ geoR,
+                                                 double *__restrict__ Ke, double *__restrict__ Rwe)
+{
+    constexpr int DW = DIM == 2 ? 1 : 3;
+    constexpr int G1 = 1 + DIM * DIM;
+    const int ne = DIM == 2 ? ngl * ngl : ngl * ngl * ngl;
+    const int nqF = DIM == 2 ? TF.np1 * TF.np1 : TF.np1 * TF.np1 * TF.np1;
+    const int nqR = DIM == 2 ? TR.np1 * TR.np1 : TR.np1 * TR.np1 * TR.np1;
+    const int64_t e = blockIdx.z;
+    const int l0 = blockIdx.x * TL, m0 = blockIdx.y * TL;
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+
+    __shared__ double sHL[QC][TL], sHM[QC][TL];
+    __shared__ double sGL[QC][DIM][TL], sGM[QC][DIM][TL];
+    __shared__ double sgeo[QC][G1];
+
+    double G[4] = {}, E[DIM][4] = {}, D[DIM][DIM][4] = {}, F[DIM][4] = {};
+
+    // full integration (GLL if ngl > 3 else Gauss): G and E
+    for (int q0 = 0; q0 < nqF; q0 += QC) {
+        for (int it = tid; it < QC * G1; it += 256) {
+            int qq = it / G1, k = it % G1;
+            sgeo[qq][k] = (q0 + qq < nqF) ? geoF[(e * nqF + q0 + qq) * G1 + k] : 0.0;
+        }
+        __syncthreads();
+        fill_chunk<DIM>(ngl, ne, nqF, TF, geoF, q0, l0, true, sHL, sGL, sgeo, tid);
+        fill_chunk<DIM>(ngl, ne, nqF, TF, geoF, q0, m0, false, sHM, sGM, sgeo, tid);
+        __syncthreads();
+        const int qn = min(QC, nqF - q0);
+        for (int qq = 0; qq < qn; ++qq) {
+            double gl[2][DIM], hl[2], gm[2][DIM];
+            for (int u = 0; u < 2; ++u) {
+                hl[u] = sHL[qq][tx + 16 * u];
+                for (int i = 0; i < DIM; ++i) {
+                    gl[u][i] = sGL[qq][i][tx + 16 * u];
+                    gm[u][i] = sGM[qq][i][ty + 16 * u];
+                }
+            }
+            for (int u = 0; u < 2; ++u)
+                for (int v = 0; v < 2; ++v) {
+                    double s = 0;
+                    for (int i = 0; i < DIM; ++i) s += gl[u][i] * gm[v][i];
+                    G[u * 2 + v] += s;
+                    for (int d = 0; d < DIM; ++d) E[d][u * 2 + v] += hl[u] * gm[v][d];
+                }
+        }
+        __syncthreads();
+    }
+    // reduced integration (Gauss ngl-1): D and F
+    for (int q0 = 0; q0 < nqR; q0 += QC) {
+        for (int it = tid; it < QC * G1; it += 256) {
+            int qq = it / G1, k = it % G1;
+            sgeo[qq][k] = (q0 + qq < nqR) ? geoR[(e * nqR + q0 + qq) * G1 + k] : 0.0;
+        }
+        __syncthreads();
+        fill_chunk<DIM>(ngl, ne, nqR, TR, geoR, q0, l0, true, sHL, sGL, sgeo, tid);
+        fill_chunk<DIM>(ngl, ne, nqR, TR, geoR, q0, m0, false, sHM, sGM, sgeo, tid);
+        __syncthreads();
+        const int qn = min(QC, nqR - q0);
+        for (int qq = 0; qq < qn; ++qq) {
+            double gl[2][DIM], gm[2][DIM], hm[2];
+            for (int u = 0; u < 2; ++u) {
+                hm[u] = sHM[qq][ty + 16 * u];
+                for (int i = 0; i < DIM; ++i) {
+                    gl[u][i] = sGL[qq][i][tx + 16 * u];
+                    gm[u][i] = sGM[qq][i][ty + 16 * u];
+                }
+            }
+            for (int u = 0; u < 2; ++u)
+                for (int v = 0; v < 2; ++v) {
+                    for (int a = 0; a < DIM; ++a)
+                        for (int b = 0; b < DIM; ++b) D[a][b][u * 2 + v] += gl[u][a] * gm[v][b];
+                    for (int d = 0; d < DIM; ++d) F[d][u * 2 + v] += gl[u][d] * hm[v];
+                }
+        }
+        __syncthreads();
+    }
+    // compose and store the blocks: Ke[e][l][m][a][b], Rwe[e][l][m][a][c]
+    for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 2; ++v) {
+            const int l = l0 + tx + 16 * u, m = m0 + ty + 16 * v;
+            if (l >= ne || m >= ne) continue;
+            const int pv = u * 2 + v;
+            double tr = 0;
+            for (int c = 0; c < DIM; ++c) tr += D[c][c][pv];
+            double *kb = Ke + ((e * ne + l) * (int64_t)ne + m) * (DIM * DIM);
+            for (int a = 0; a < DIM; ++a)
+                for (int b = 0; b < DIM; ++b) {
+                    double val = ALPHA_D * D[a][b][pv] - ALPHA_W * D[b][a][pv];
+                    if (a == b) val += G[pv] + ALPHA_W * tr;
+                    kb[a * DIM + b] = val;
+                }
+            double rw[DIM][DW] = {};
+            if constexpr (DIM == 3) {
+                // (row, col, derivative) of B_curl / Bw_curl, sign (-1)^t
+                // (indCurl == indWCurl, spectral.py:31-32)
+                const int ind[6][3] = {{0, 2, 1}, {0, 1, 2}, {1, 0, 2}, {1, 2, 0}, {2, 1, 0}, {2, 0, 1}};
+                for (int t = 0; t < 6; ++t) {
+                    const double s = (t & 1) ? -1.0 : 1.0;
+                    const int r0 = ind[t][0], r1 = ind[t][1], d = ind[t][2];
+                    rw[r0][r1] += s * E[d][pv];             // H^T Bw_curl  (full)
+                    rw[r1][r0] += ALPHA_W * s * F[d][pv];   // a_w B_curl^T H (reduced)
+                }
+            } else {
+                // indWCurl 2-D [[0,0,1],[1,0,0]] ; indCurl 2-D [[0,1,0],[0,0,1]]
+                rw[0][0] += E[1][pv] - ALPHA_W * F[1][pv];
+                rw[1][0] += -E[0][pv] + ALPHA_W * F[0][pv];
+            }
+            double *rb = Rwe + ((e * ne + l) * (int64_t)ne + m) * (DIM * DW);
+            for (int a = 0; a < DIM; ++a)
+                for (int c = 0; c < DW; ++c) rb[a * DW + c] = rw[a][c];
+        }
+}
+
+// ---------------------------------------------------------------- gather
+struct MeshDev {
+    int dim, p, ngl, ne;
+    int64_t nel[3], L[3];
+    int64_t node_begin, ext_begin, elem_begin;
+};
+
+// MODE 0: K (free cols, +K_e), 1: Krhs (Dirichlet cols, -K_e), 2: Rw (+Rw_e)
+template <int R, int C, int MODE>
+__global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const int *__restrict__ rowptr,
+                                                const int *__restrict__ bcol,
+                                                const uint8_t *__restrict__ dir,
+                                                const double *__restrict__ Eblk, double *__restrict__ val)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (row >= nrows) return;
+    const int64_t gi = M.node_begin + row;
+    const int b0 = rowptr[row], m = rowptr[row + 1] - b0;
+    double *v = val + (int64_t)b0 * R * C;
+    if (dir[gi - M.ext_begin]) {
+        // K[dir,dir] = 0 + ... + 0 + 1 and Krhs[dir,dir] = 1 (mat_fs.py:115-120,182-183)
+        if (MODE != 2 && lane == 0 && m == 1)
+            for (int a = 0; a < R; ++a)
+                for (int b = 0; b < C; ++b) v[a * C + b] = (a == b) ? 1.0 : 0.0;
+        return;
+    }
+    int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], M.dim == 3 ? gi / (M.L[0] * M.L[1]) : 0};
+    int64_t elo[3], ehi[3];
+    for (int d = 0; d < 3; ++d) {
+        if (d >= M.dim) {
+            elo[d] = ehi[d] = 0;
+            continue;
+        }
+        int64_t c = ci[d];
+        elo[d] = (c % M.p == 0) ? max((int64_t)0, c / M.p - 1) : c / M.p;
+        ehi[d] = min(M.nel[d] - 1, c / M.p);
+    }
+    const int ngl = M.ngl, ne = M.ne;
+    for (int k = lane; k < m; k += 64) {
+        const int64_t gj = M.ext_begin + bcol[b0 + k];
+        int64_t cj[3] = {gj % M.L[0], (gj / M.L[0]) % M.L[1], M.dim == 3 ? gj / (M.L[0] * M.L[1]) : 0};
+        double acc[R * C];
+#pragma unroll
+        for (int t = 0; t < R * C; ++t) acc[t] = 0.0;
+        for (int64_t ez = elo[2]; ez <= ehi[2]; ++ez)
+            for (int64_t ey = elo[1]; ey <= ehi[1]; ++ey)
+                for (int64_t ex = elo[0]; ex <= ehi[0]; ++ex) {
+                    const int64_t eo[3] = {ex * M.p, ey * M.p, ez * M.p};
+                    bool in = true;
+                    int oj[3] = {0, 0, 0}, oi[3] = {0, 0, 0};
+                    for (int d = 0; d < M.dim; ++d) {
+                        int64_t o = cj[d] - eo[d];
+                        in = in && o >= 0 && o <= M.p;
+                        oj[d] = (int)o;
+                        oi[d] = (int)(ci[d] - eo[d]);
+                    }
+                    if (!in) continue;
+                    const int64_t e = ex + M.nel[0] * (ey + M.nel[1] * ez) - M.elem_begin;
+                    const int li = oi[0] + ngl * (oi[1] + ngl * oi[2]);
+                    const int lj = oj[0] + ngl * (oj[1] + ngl * oj[2]);
+                    const double *blk = Eblk + ((e * ne + li) * (int64_t)ne + lj) * (R * C);
+#pragma unroll
+                    for (int t = 0; t < R * C; ++t) acc[t] += (MODE == 1) ? -blk[t] : blk[t];
+                }
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < C; ++b) v[(a * C + b) * (int64_t)m + k] = acc[a * C + b];
+    }
+}
+
+static MeshDev mesh_dev(const kle_mesh *m)
+{
+    MeshDev M;
+    M.dim = m->dim;
+    M.p = m->p;
+    M.ngl = m->ngl;
+    M.ne = m->nn();
+    for (int d = 0; d < 3; ++d) {
+        M.nel[d] = m->nel[d];
+        M.L[d] = m->L[d];
+    }
+    M.node_begin = m->node_begin;
+    M.ext_begin = m->ext_begin;
+    M.elem_begin = m->elem_begin;
+    return M;
+}
+
+// Device node-block matrix with the symbolic pattern `which` of the mesh.
+int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat **out)
+{
+    const int64_t nrows = m->node_end - m->node_begin;
+    std::vector<int64_t> rp(nrows + 1);
+    int64_t nb;
+    KLE_TRY(kle_mesh_pattern_size(m, which, &nb));
+    if (nb >= (1ll << 31) / 1) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
+    std::vector<int64_t> cols(std::max<int64_t>(nb, 1));
+    KLE_TRY(kle_mesh_pattern(m, which, rp.data(), cols.data()));
+    std::vector<int> rp32(nrows + 1), c32(std::max<int64_t>(nb, 1));
+    for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
+    for (int64_t k = 0; k < nb; ++k) c32[k] = (int)(cols[k] - m->ext_begin);
+    kle_mat *A = new kle_mat;
+    A->ctx = ctx;
+    A->kind = 0;
+    A->R = R;
+    A->C = C;
+    A->nrows = nrows;
+    A->nblocks = nb;
+    A->node_begin = m->node_begin;
+    A->ext_begin = m->ext_begin;
+    A->ext_nodes = m->ext_end - m->ext_begin;
+    A->m_local = nrows * R;
+    A->n_local = nrows * C;
+    A->m_global = m->N * R;
+    A->n_global = m->N * C;
+    A->row_lo = m->node_begin * R;
+    A->col_lo = m->node_begin * C;
+    A->lo_rank = m->halo_lo_rank;
+    A->hi_rank = m->halo_hi_rank;
+    A->ghost_lo = (m->node_begin - m->ext_begin) * C;
+    A->ghost_hi = (m->ext_end - m->node_end) * C;
+    A->send_lo = m->send_lo_nodes * C;
+    A->send_hi = m->send_hi_nodes * C;
+    A->diag_only_row.assign(nrows, 0);
+    if (which != 2)
+        for (int64_t i = 0; i < nrows; ++i) A->diag_only_row[i] = m->dir[m->node_begin + i - m->ext_begin];
+    if (hipMalloc(&A->d_rowptr, sizeof(int) * (nrows + 1)) != hipSuccess ||
+        hipMalloc(&A->d_bcol, sizeof(int) * std::max<int64_t>(nb, 1)) != hipSuccess ||
+        hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nb * R * C, 1)) != hipSuccess) {
+        kle_mat_destroy(A);
+        return fail(KLE_ERR_MEM, "out of device memory for a %lld-block matrix", (long long)nb);
+    }
+    KLE_HIP(hipMemcpyAsync(A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1), hipMemcpyHostToDevice,
+                           ctx->stream));
+    KLE_HIP(hipMemcpyAsync(A->d_bcol, c32.data(), sizeof(int) * std::max<int64_t>(nb, 1),
+                           hipMemcpyHostToDevice, ctx->stream));
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    *out = A;
+    return 0;
+}
+
+struct DevTables {
+    double *buf = nullptr;
+    Tables1D F, R;
+    ~DevTables() { hipFree(buf); }
+};
+
+static int upload_tables(kle_ctx *ctx, int ngl, DevTables &T)
+{
+    PointSet1D full, red, op;
+    element_sets(ngl, full, red, op);
+    std::vector<double> h;
+    auto put = [&](const std::vector<double> &v) {
+        size_t o = h.size();
+        h.insert(h.end(), v.begin(), v.end());
+        return o;
+    };
+    size_t fx = put(full.x), fw = put(full.w), fh = put(full.h), fd = put(full.dh);
+    size_t rx = put(red.x), rw = put(red.w), rh = put(red.h), rd = put(red.dh);
+    KLE_HIP(hipMalloc(&T.buf, sizeof(double) * h.size()));
+    KLE_HIP(hipMemcpyAsync(T.buf, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, ctx->stream));
+    T.F = {(int)full.x.size(), T.buf + fx, T.buf + fw, T.buf + fh, T.buf + fd};
+    T.R = {(int)red.x.size(), T.buf + rx, T.buf + rw, T.buf + rh, T.buf + rd};
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+// Compute K_e and Rw_e of all local elements into device buffers.
+static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, double **dRwe)
+{
+    const int dim = m->dim, ne = m->nn(), dw = dim == 2 ? 1 : 3, nc = 1 << dim;
+    const int64_t nel = m->elem_end - m->elem_begin;
+    DevTables T;
+    KLE_TRY(upload_tables(ctx, m->ngl, T));
+    std::vector<double> corners(nel * nc * dim);
+    KLE_TRY(kle_mesh_get_corners(m, corners.data()));
+    double *dX = nullptr, *gF = nullptr, *gR = nullptr;
+    const int nqF = dim == 2 ? T.F.np1 * T.F.np1 : T.F.np1 * T.F.np1 * T.F.np1;
+    const int nqR = dim == 2 ? T.R.np1 * T.R.np1 : T.R.np1 * T.R.np1 * T.R.np1;
+    const int G1 = 1 + dim * dim;
+    KLE_HIP(hipMalloc(&dX, sizeof(double) * corners.size()));
+    KLE_HIP(hipMalloc(&gF, sizeof(double) * nel * nqF * G1));
+    KLE_HIP(hipMalloc(&gR, sizeof(double) * nel * nqR * G1));
+    KLE_HIP(hipMemcpyAsync(dX, corners.data(), sizeof(double) * corners.size(), hipMemcpyHostToDevice,
+                           ctx->stream));
+    const size_t keN = (size_t)nel * ne * ne * dim * dim, rwN = (size_t)nel * ne * ne * dim * dw;
+    if (hipMalloc(dKe, sizeof(double) * keN) != hipSuccess ||
+        hipMalloc(dRwe, sizeof(double) * rwN) != hipSuccess) {
+        hipFree(dX); hipFree(gF); hipFree(gR);
+        return fail(KLE_ERR_MEM, "element matrix workspace (%.2f GB) does not fit",
+                    (keN + rwN) * 8.0 / 1e9);
+    }
+    const int64_t nF = nel * nqF, nR = nel * nqR;
+    dim3 eg((ne + TL - 1) / TL, (ne + TL - 1) / TL, (unsigned)nel);
+    if (dim == 2) {
+        hipLaunchKernelGGL(k_geometry<2>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
+        hipLaunchKernelGGL(k_geometry<2>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
+        hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe);
+    } else {
+        hipLaunchKernelGGL(k_geometry<3>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
+        hipLaunchKernelGGL(k_geometry<3>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
+        hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe);
+    }
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    hipFree(dX);
+    hipFree(gF);
+    hipFree(gR);
+    return 0;
+}
+
+template <int R, int C, int MODE>
+static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint8_t *dir, const double *E)
+{
+    const int64_t threads = A->nrows * 64;
+    hipLaunchKernelGGL((k_gather<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
+                       A->nrows, A->d_rowptr, A->d_bcol, dir, E, A->d_val);
+}
+
+}  // namespace kle
+
+using namespace kle;
+
+extern "C" {
+
+int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw)
+{
+    KLE_ARG(ctx && m && K && Krhs && Rw, "null arg");
+    KLE_ARG(m->rank == ctx->rank && m->nranks == ctx->nranks, "mesh partition does not match ctx");
+    KLE_ARG(m->dir_set, "Dirichlet nodes not set (kle_mesh_set_dirichlet_*)");
+    const int dim = m->dim, dw = dim == 2 ? 1 : 3;
+    KLE_HIP(hipSetDevice(ctx->device));
+    kle_mat *mK = nullptr, *mKr = nullptr, *mRw = nullptr;
+    KLE_TRY(nb_create(ctx, m, 0, dim, dim, &mK));
+    KLE_TRY(nb_create(ctx, m, 1, dim, dim, &mKr));
+    KLE_TRY(nb_create(ctx, m, 2, dim, dw, &mRw));
+    double *dKe = nullptr, *dRwe = nullptr;
+    KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe));
+    uint8_t *ddir = nullptr;
+    KLE_HIP(hipMalloc(&ddir, m->dir.size()));
+    KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
+    MeshDev M = mesh_dev(m);
+    if (dim == 3) {
+        launch_gather<3, 3, 0>(ctx, M, mK, ddir, dKe);
+        launch_gather<3, 3, 1>(ctx, M, mKr, ddir, dKe);
+        launch_gather<3, 3, 2>(ctx, M, mRw, ddir, dRwe);
+    } else {
+        launch_gather<2, 2, 0>(ctx, M, mK, ddir, dKe);
+        launch_gather<2, 2, 1>(ctx, M, mKr, ddir, dKe);
+        launch_gather<2, 1, 2>(ctx, M, mRw, ddir, dRwe);
+    }
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    hipFree(dKe);
+    hipFree(dRwe);
+    hipFree(ddir);
+    *K = mK;
+    *Krhs = mKr;
+    *Rw = mRw;
+    return 0;
+}
+
+int kle_element_kle(kle_ctx *ctx, kle_mesh *m, int64_t e, double *Ke, double *Rwe)
+{
+    KLE_ARG(ctx && m && Ke && Rwe, "null arg");
+    const int64_t nel = m->elem_end - m->elem_begin;
+    KLE_ARG(e >= 0 && e < nel, "element %lld out of local range", (long long)e);
+    KLE_HIP(hipSetDevice(ctx->device));
+    double *dKe = nullptr, *dRwe = nullptr;
+    KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe));
+    const int dim = m->dim, ne = m->nn(), dw = dim == 2 ? 1 : 3;
+    std::vector<double> kb((size_t)ne * ne * dim * dim), rb((size_t)ne * ne * dim * dw);
+    KLE_HIP(hipMemcpy(kb.data(), dKe + (size_t)e * kb.size(), sizeof(double) * kb.size(), hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(rb.data(), dRwe + (size_t)e * rb.size(), sizeof(double) * rb.size(), hipMemcpyDeviceToHost));
+    hipFree(dKe);
+    hipFree(dRwe);
+    // block layout [l][m][a][b] -> row-major [l a][m b]
+    for (int l = 0; l < ne; ++l)
+        for (int mm = 0; mm < ne; ++mm)
+            for (int a = 0; a < dim; ++a) {
+                for (int b = 0; b < dim; ++b)
+                    Ke[(size_t)(l * dim + a) * ne * dim + mm * dim + b] = kb[(((size_t)l * ne + mm) * dim + a) * dim + b];
+                for (int c = 0; c < dw; ++c)
+                    Rwe[(size_t)(l * dim + a) * ne * dw + mm * dw + c] = rb[(((size_t)l * ne + mm) * dim + a) * dw + c];
+            }
+    return 0;
+}
+
+}  // extern "C"

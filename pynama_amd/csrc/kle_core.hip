@@ -1,0 +1,728 @@
+// kle_core.hip -- context, errors, profiling, device vectors (BLAS-1 with
+// deterministic two-stage reductions), halo exchange over RCCL.
+//
+// Replaces the PETSc Vec traffic of the hot path:
+// Vec.__add__ (kle_solver.py:35), axpy/scale (base_problem.py:129-134),
+// setValues+assemble (boundary_conditions.py:252-260), reciprocal
+// (mat_fs.py:256), dot/norm (base_problem.py:334,389).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "kle_internal.hpp"
+
+namespace kle {
+
+static thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+void clear_error() { g_err.clear(); }
+
+int grid_for(int64_t work, int per_block, int max_blocks)
+{
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > max_blocks) g = max_blocks;
+    return (int)g;
+}
+
+// ------------------------------------------------------------ wave utilities
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide sum of one value per thread (blockDim.x <= 1024), result valid
+// in thread 0.  Fixed combination order -> bitwise reproducible.
+__device__ __forceinline__ double block_sum(double v, double *lds)
+{
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) lds[w] = v;
+    __syncthreads();
+    double s = 0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < nw; ++i) s += lds[i];
+    return s;
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ void k_set(int64_t n, double a, double *__restrict__ y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = a;
+}
+
+__global__ void k_axpy(int64_t n, double a, const double *__restrict__ x, double *__restrict__ y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] += a * x[i];
+}
+
+__global__ void k_aypx(int64_t n, double b, const double *__restrict__ x, double *__restrict__ y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = x[i] + b * y[i];
+}
+
+__global__ void k_waxpy(int64_t n, double a, const double *__restrict__ x,
+                        const double *__restrict__ y, double *__restrict__ w)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        w[i] = a * x[i] + y[i];
+}
+
+__global__ void k_scale(int64_t n, double a, double *__restrict__ y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] *= a;
+}
+
+__global__ void k_pmult(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
+                        double *__restrict__ w)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        w[i] = x[i] * y[i];
+}
+
+__global__ void k_recip(int64_t n, double *__restrict__ y)
+{
+    // VecReciprocal: zero entries stay zero (PETSc semantics)
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = y[i] != 0.0 ? 1.0 / y[i] : 0.0;
+}
+
+__global__ void k_dot_partial(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
+                              double *__restrict__ partials)
+{
+    __shared__ double lds[16];
+    double s = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        s += x[i] * y[i];
+    s = block_sum(s, lds);
+    if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// Sum nq quantities of nparts partials each (stride RED_BLOCKS) into out[q].
+__global__ void k_reduce(const double *__restrict__ partials, int nparts, int nq,
+                         double *__restrict__ out)
+{
+    __shared__ double lds[16];
+    for (int q = 0; q < nq; ++q) {
+        double s = 0;
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partials[q * RED_BLOCKS + i];
+        s = block_sum(s, lds);
+        if (threadIdx.x == 0) out[q] = s;
+        __syncthreads();
+    }
+}
+
+__global__ void k_scatter_values(int64_t n, const int64_t *__restrict__ idx,
+                                 const double *__restrict__ v, double *__restrict__ y, int addv)
+{
+    // addv: applied sequentially by one thread when indices may repeat
+    if (addv) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            for (int64_t i = 0; i < n; ++i) y[idx[i]] += v[i];
+        return;
+    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[idx[i]] = v[i];
+}
+
+__global__ void k_gather_values(int64_t n, const int64_t *__restrict__ idx,
+                                const double *__restrict__ y, double *__restrict__ v)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        v[i] = y[idx[i]];
+}
+
+__global__ void k_stream_copy(int64_t n4, const double4 *__restrict__ a, double4 *__restrict__ b)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
+int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out)
+{
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, ctx->stream, partials, nparts, nq, out);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+static constexpr int VB = 256;      // vector kernel block
+static constexpr int VMAX = 2048;   // vector kernel max grid (8 WG per CU)
+
+int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64_t glo,
+              int64_t ghi, kle_vec **out)
+{
+    kle_vec *v = new kle_vec;
+    v->ctx = ctx;
+    v->n_local = n_local;
+    v->n_global = n_global;
+    v->lo = lo;
+    v->ghost_lo = glo;
+    v->ghost_hi = ghi;
+    int64_t tot = glo + n_local + ghi;
+    if (hipMalloc(&v->base, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess) {
+        delete v;
+        return fail(KLE_ERR_MEM, "hipMalloc of %lld doubles failed", (long long)tot);
+    }
+    if (hipMemsetAsync(v->base, 0, sizeof(double) * std::max<int64_t>(tot, 1), ctx->stream) !=
+        hipSuccess) {
+        hipFree(v->base);
+        delete v;
+        return fail(KLE_ERR_DEVICE, "hipMemsetAsync failed");
+    }
+    v->d = v->base + glo;
+    *out = v;
+    return 0;
+}
+
+int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
+                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi)
+{
+    if (ctx->nranks == 1 || (lo_rank < 0 && hi_rank < 0)) return 0;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(ctx->tic("halo", &ev));
+    double *own = base + ghost_lo;
+    KLE_NCCL(ncclGroupStart());
+    if (lo_rank >= 0) {
+        // my lowest send_lo owned entries are the lower neighbour's upper ghosts
+        KLE_NCCL(ncclSend(own, send_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
+        KLE_NCCL(ncclRecv(base, ghost_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
+    }
+    if (hi_rank >= 0) {
+        KLE_NCCL(ncclSend(own + n_local - send_hi, send_hi, ncclDouble, hi_rank, ctx->comm,
+                          ctx->stream));
+        KLE_NCCL(ncclRecv(own + n_local, ghost_hi, ncclDouble, hi_rank, ctx->comm, ctx->stream));
+    }
+    KLE_NCCL(ncclGroupEnd());
+    KLE_TRY(ctx->toc("halo", &ev));
+    return 0;
+}
+
+}  // namespace kle
+
+using namespace kle;
+
+// ----------------------------------------------------------- ctx profiling
+hipEvent_t kle_ctx::get_event()
+{
+    if (!event_pool.empty()) {
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int kle_ctx::tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev)
+{
+    (void)name;
+    if (!profiling) return 0;
+    ev->first = get_event();
+    ev->second = get_event();
+    if (!ev->first || !ev->second) return fail(KLE_ERR_DEVICE, "hipEventCreate failed");
+    KLE_HIP(hipEventRecord(ev->first, stream));
+    return 0;
+}
+
+int kle_ctx::toc(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev)
+{
+    if (!profiling) return 0;
+    KLE_HIP(hipEventRecord(ev->second, stream));
+    Stat &s = stats[name];
+    s.pending.push_back(*ev);
+    if (s.pending.size() > 8192) return resolve_stats();
+    return 0;
+}
+
+int kle_ctx::resolve_stats()
+{
+    for (auto &kv : stats) {
+        for (auto &pr : kv.second.pending) {
+            KLE_HIP(hipEventSynchronize(pr.second));
+            float ms = 0;
+            KLE_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+            kv.second.ms += ms;
+            kv.second.count += 1;
+            event_pool.push_back(pr.first);
+            event_pool.push_back(pr.second);
+        }
+        kv.second.pending.clear();
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char *kle_last_error(void) { return g_err.c_str(); }
+int kle_version(void) { return 1; }
+
+int kle_get_unique_id(unsigned char out[128])
+{
+    ncclUniqueId id;
+    KLE_NCCL(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(out, &id, 128);
+    return 0;
+}
+
+int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, kle_ctx **out)
+{
+    KLE_ARG(out, "null output");
+    KLE_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank %d / nranks %d", rank, nranks);
+    KLE_ARG(nranks == 1 || unique_id, "nranks > 1 needs an RCCL unique id");
+    int ndev = 0;
+    KLE_HIP(hipGetDeviceCount(&ndev));
+    KLE_ARG(device >= 0 && device < ndev, "device %d not present (%d visible)", device, ndev);
+    KLE_HIP(hipSetDevice(device));
+    kle_ctx *c = new kle_ctx;
+    c->device = device;
+    c->rank = rank;
+    c->nranks = nranks;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(KLE_ERR_DEVICE, "hipStreamCreate failed");
+    }
+    if (hipMalloc(&c->d_partials, sizeof(double) * 4 * RED_BLOCKS) != hipSuccess ||
+        hipMalloc(&c->d_scal, sizeof(double) * NSCAL) != hipSuccess ||
+        hipMalloc(&c->d_istate, sizeof(int) * I_COUNT) != hipSuccess ||
+        hipHostMalloc(&c->h_scal, sizeof(double) * NSCAL) != hipSuccess ||
+        hipHostMalloc(&c->h_istate, sizeof(int) * I_COUNT) != hipSuccess) {
+        kle_ctx_destroy(c);
+        return fail(KLE_ERR_MEM, "context scratch allocation failed");
+    }
+    hipMemset(c->d_scal, 0, sizeof(double) * NSCAL);
+    hipMemset(c->d_istate, 0, sizeof(int) * I_COUNT);
+    if (nranks > 1) {
+        ncclUniqueId id;
+        memcpy(&id, unique_id, 128);
+        ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+        if (r != ncclSuccess) {
+            kle_ctx_destroy(c);
+            return fail(KLE_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+    }
+    *out = c;
+    return 0;
+}
+
+int kle_ctx_destroy(kle_ctx *c)
+{
+    if (!c) return 0;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    c->resolve_stats();
+    for (auto e : c->event_pool) hipEventDestroy(e);
+    if (c->comm) ncclCommDestroy(c->comm);
+    hipFree(c->d_partials);
+    hipFree(c->d_scal);
+    hipFree(c->d_istate);
+    hipHostFree(c->h_scal);
+    hipHostFree(c->h_istate);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int kle_ctx_synchronize(kle_ctx *c)
+{
+    KLE_ARG(c, "null ctx");
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int kle_ctx_barrier(kle_ctx *c)
+{
+    KLE_ARG(c, "null ctx");
+    if (c->nranks > 1) {
+        // a one-double allreduce on the stream is the device-side barrier
+        KLE_NCCL(ncclAllReduce(c->d_scal + S_TMP1, c->d_scal + S_TMP1, 1, ncclDouble, ncclSum,
+                               c->comm, c->stream));
+    }
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int kle_ctx_set_profiling(kle_ctx *c, int on)
+{
+    KLE_ARG(c, "null ctx");
+    c->profiling = on != 0;
+    return 0;
+}
+
+int kle_ctx_get_kernel_stats(kle_ctx *c, const char *name, int64_t *count, double *total_ms)
+{
+    KLE_ARG(c && name, "null arg");
+    KLE_TRY(c->resolve_stats());
+    auto it = c->stats.find(name);
+    *count = it == c->stats.end() ? 0 : it->second.count;
+    *total_ms = it == c->stats.end() ? 0 : it->second.ms;
+    return 0;
+}
+
+int kle_ctx_reset_kernel_stats(kle_ctx *c)
+{
+    KLE_ARG(c, "null ctx");
+    KLE_TRY(c->resolve_stats());
+    for (auto &kv : c->stats) {
+        kv.second.count = 0;
+        kv.second.ms = 0;
+    }
+    return 0;
+}
+
+// --------------------------------------------------------------------- vec
+int kle_vec_create(kle_ctx *ctx, int64_t n_local, int64_t n_global, kle_vec **out)
+{
+    KLE_ARG(ctx && out, "null arg");
+    KLE_ARG(n_local >= 0, "negative size");
+    int64_t lo = 0;
+    if (ctx->nranks > 1) {
+        // ownership ranges follow rank order: prefix sum over ranks
+        int64_t *d;
+        KLE_HIP(hipMalloc(&d, sizeof(int64_t)));
+        KLE_HIP(hipMemcpyAsync(d, &n_local, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+        std::vector<int64_t> all(ctx->nranks);
+        int64_t *dall;
+        KLE_HIP(hipMalloc(&dall, sizeof(int64_t) * ctx->nranks));
+        KLE_NCCL(ncclAllGather(d, dall, 1, ncclInt64, ctx->comm, ctx->stream));
+        KLE_HIP(hipMemcpyAsync(all.data(), dall, sizeof(int64_t) * ctx->nranks,
+                               hipMemcpyDeviceToHost, ctx->stream));
+        KLE_HIP(hipStreamSynchronize(ctx->stream));
+        hipFree(d);
+        hipFree(dall);
+        int64_t tot = 0;
+        for (int r = 0; r < ctx->nranks; ++r) {
+            if (r == ctx->rank) lo = tot;
+            tot += all[r];
+        }
+        if (n_global < 0) n_global = tot;
+        KLE_ARG(n_global == tot, "global size %lld != sum of local sizes %lld",
+                (long long)n_global, (long long)tot);
+    } else {
+        if (n_global < 0) n_global = n_local;
+        KLE_ARG(n_global == n_local, "single rank: global size must equal local size");
+    }
+    return vec_alloc(ctx, n_local, n_global, lo, 0, 0, out);
+}
+
+int kle_vec_create_mesh(kle_ctx *ctx, const kle_mesh *m, int bs, kle_vec **out)
+{
+    KLE_ARG(ctx && m && out, "null arg");
+    KLE_ARG(bs >= 1 && bs <= 16, "bad block size %d", bs);
+    KLE_ARG(m->nranks == ctx->nranks && m->rank == ctx->rank, "mesh partition does not match ctx");
+    int64_t own = (m->node_end - m->node_begin) * bs;
+    KLE_TRY(vec_alloc(ctx, own, m->N * bs, m->node_begin * bs,
+                      (m->node_begin - m->ext_begin) * bs, (m->ext_end - m->node_end) * bs, out));
+    kle_vec *v = *out;
+    v->bs = bs;
+    v->lo_rank = m->halo_lo_rank;
+    v->hi_rank = m->halo_hi_rank;
+    v->send_lo = m->send_lo_nodes * bs;
+    v->send_hi = m->send_hi_nodes * bs;
+    return 0;
+}
+
+int kle_vec_duplicate(const kle_vec *v, kle_vec **out)
+{
+    KLE_ARG(v && out, "null arg");
+    KLE_TRY(vec_alloc(v->ctx, v->n_local, v->n_global, v->lo, v->ghost_lo, v->ghost_hi, out));
+    kle_vec *w = *out;
+    w->bs = v->bs;
+    w->lo_rank = v->lo_rank;
+    w->hi_rank = v->hi_rank;
+    w->send_lo = v->send_lo;
+    w->send_hi = v->send_hi;
+    return 0;
+}
+
+int kle_vec_destroy(kle_vec *v)
+{
+    if (!v) return 0;
+    if (v->owns) hipFree(v->base);
+    delete v;
+    return 0;
+}
+
+int kle_vec_get_sizes(const kle_vec *v, int64_t *nl, int64_t *ng)
+{
+    KLE_ARG(v, "null vec");
+    if (nl) *nl = v->n_local;
+    if (ng) *ng = v->n_global;
+    return 0;
+}
+
+int kle_vec_get_ownership_range(const kle_vec *v, int64_t *lo, int64_t *hi)
+{
+    KLE_ARG(v, "null vec");
+    *lo = v->lo;
+    *hi = v->lo + v->n_local;
+    return 0;
+}
+
+#define VGRID(n) kle::grid_for((n), VB, VMAX)
+
+int kle_vec_set(kle_vec *v, double a)
+{
+    KLE_ARG(v, "null vec");
+    hipLaunchKernelGGL(k_set, dim3(VGRID(v->n_local)), dim3(VB), 0, v->ctx->stream, v->n_local, a,
+                       v->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+static int same_layout(const kle_vec *a, const kle_vec *b)
+{
+    if (a->n_local != b->n_local || a->n_global != b->n_global)
+        return fail(KLE_ERR_SIZ, "vector sizes differ (%lld/%lld vs %lld/%lld)",
+                    (long long)a->n_local, (long long)a->n_global, (long long)b->n_local,
+                    (long long)b->n_global);
+    return 0;
+}
+
+int kle_vec_copy(const kle_vec *x, kle_vec *y)
+{
+    KLE_ARG(x && y, "null vec");
+    KLE_TRY(same_layout(x, y));
+    KLE_HIP(hipMemcpyAsync(y->d, x->d, sizeof(double) * x->n_local, hipMemcpyDeviceToDevice,
+                           x->ctx->stream));
+    return 0;
+}
+
+int kle_vec_axpy(kle_vec *y, double a, const kle_vec *x)
+{
+    KLE_ARG(x && y, "null vec");
+    KLE_TRY(same_layout(x, y));
+    hipLaunchKernelGGL(k_axpy, dim3(VGRID(y->n_local)), dim3(VB), 0, y->ctx->stream, y->n_local, a,
+                       x->d, y->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_aypx(kle_vec *y, double b, const kle_vec *x)
+{
+    KLE_ARG(x && y, "null vec");
+    KLE_TRY(same_layout(x, y));
+    hipLaunchKernelGGL(k_aypx, dim3(VGRID(y->n_local)), dim3(VB), 0, y->ctx->stream, y->n_local, b,
+                       x->d, y->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_waxpy(kle_vec *w, double a, const kle_vec *x, const kle_vec *y)
+{
+    KLE_ARG(w && x && y, "null vec");
+    KLE_TRY(same_layout(x, y));
+    KLE_TRY(same_layout(x, w));
+    hipLaunchKernelGGL(k_waxpy, dim3(VGRID(w->n_local)), dim3(VB), 0, w->ctx->stream, w->n_local,
+                       a, x->d, y->d, w->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_scale(kle_vec *v, double a)
+{
+    KLE_ARG(v, "null vec");
+    hipLaunchKernelGGL(k_scale, dim3(VGRID(v->n_local)), dim3(VB), 0, v->ctx->stream, v->n_local, a,
+                       v->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_pointwise_mult(kle_vec *w, const kle_vec *x, const kle_vec *y)
+{
+    KLE_ARG(w && x && y, "null vec");
+    KLE_TRY(same_layout(x, y));
+    KLE_TRY(same_layout(x, w));
+    hipLaunchKernelGGL(k_pmult, dim3(VGRID(w->n_local)), dim3(VB), 0, w->ctx->stream, w->n_local,
+                       x->d, y->d, w->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_reciprocal(kle_vec *v)
+{
+    KLE_ARG(v, "null vec");
+    hipLaunchKernelGGL(k_recip, dim3(VGRID(v->n_local)), dim3(VB), 0, v->ctx->stream, v->n_local,
+                       v->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_dot(const kle_vec *x, const kle_vec *y, double *out)
+{
+    KLE_ARG(x && y && out, "null arg");
+    KLE_TRY(same_layout(x, y));
+    kle_ctx *c = x->ctx;
+    int g = VGRID(x->n_local);
+    hipLaunchKernelGGL(k_dot_partial, dim3(g), dim3(VB), 0, c->stream, x->n_local, x->d, y->d,
+                       c->d_partials);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(reduce_partials(c, c->d_partials, g, 1, c->d_scal + S_TMP0));
+    if (c->nranks > 1)
+        KLE_NCCL(ncclAllReduce(c->d_scal + S_TMP0, c->d_scal + S_TMP0, 1, ncclDouble, ncclSum,
+                               c->comm, c->stream));
+    KLE_HIP(hipMemcpyAsync(c->h_scal + S_TMP0, c->d_scal + S_TMP0, sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream));
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    *out = c->h_scal[S_TMP0];
+    return 0;
+}
+
+int kle_vec_norm2(const kle_vec *x, double *out)
+{
+    double d;
+    KLE_TRY(kle_vec_dot(x, x, &d));
+    *out = std::sqrt(d);
+    return 0;
+}
+
+int kle_vec_set_values(kle_vec *v, int64_t n, const int64_t *idx, const double *vals, int addv)
+{
+    KLE_ARG(v && (n == 0 || (idx && vals)), "null arg");
+    if (n == 0) return 0;
+    std::vector<int64_t> loc(n);
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t l = idx[i] - v->lo;
+        if (l < 0 || l >= v->n_local)
+            return fail(KLE_ERR_OUTOFRANGE, "index %lld not owned ([%lld,%lld))",
+                        (long long)idx[i], (long long)v->lo, (long long)(v->lo + v->n_local));
+        loc[i] = l;
+    }
+    int64_t *di;
+    double *dv;
+    KLE_HIP(hipMalloc(&di, sizeof(int64_t) * n));
+    KLE_HIP(hipMalloc(&dv, sizeof(double) * n));
+    KLE_HIP(hipMemcpyAsync(di, loc.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice,
+                           v->ctx->stream));
+    KLE_HIP(hipMemcpyAsync(dv, vals, sizeof(double) * n, hipMemcpyHostToDevice, v->ctx->stream));
+    hipLaunchKernelGGL(k_scatter_values, dim3(VGRID(n)), dim3(VB), 0, v->ctx->stream, n, di, dv,
+                       v->d, addv);
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(v->ctx->stream));
+    hipFree(di);
+    hipFree(dv);
+    return 0;
+}
+
+int kle_vec_get_values(const kle_vec *v, int64_t n, const int64_t *idx, double *vals)
+{
+    KLE_ARG(v && (n == 0 || (idx && vals)), "null arg");
+    if (n == 0) return 0;
+    std::vector<int64_t> loc(n);
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t l = idx[i] - v->lo;
+        if (l < -v->ghost_lo || l >= v->n_local + v->ghost_hi)
+            return fail(KLE_ERR_OUTOFRANGE, "index %lld not local", (long long)idx[i]);
+        loc[i] = l;
+    }
+    int64_t *di;
+    double *dv;
+    KLE_HIP(hipMalloc(&di, sizeof(int64_t) * n));
+    KLE_HIP(hipMalloc(&dv, sizeof(double) * n));
+    KLE_HIP(hipMemcpyAsync(di, loc.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice,
+                           v->ctx->stream));
+    hipLaunchKernelGGL(k_gather_values, dim3(VGRID(n)), dim3(VB), 0, v->ctx->stream, n, di, v->d,
+                       dv);
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipMemcpyAsync(vals, dv, sizeof(double) * n, hipMemcpyDeviceToHost, v->ctx->stream));
+    KLE_HIP(hipStreamSynchronize(v->ctx->stream));
+    hipFree(di);
+    hipFree(dv);
+    return 0;
+}
+
+int kle_vec_get_array(const kle_vec *v, double *host)
+{
+    KLE_ARG(v && host, "null arg");
+    KLE_HIP(hipMemcpyAsync(host, v->d, sizeof(double) * v->n_local, hipMemcpyDeviceToHost,
+                           v->ctx->stream));
+    KLE_HIP(hipStreamSynchronize(v->ctx->stream));
+    return 0;
+}
+
+int kle_vec_set_array(kle_vec *v, const double *host)
+{
+    KLE_ARG(v && host, "null arg");
+    KLE_HIP(hipMemcpyAsync(v->d, host, sizeof(double) * v->n_local, hipMemcpyHostToDevice,
+                           v->ctx->stream));
+    KLE_HIP(hipStreamSynchronize(v->ctx->stream));
+    return 0;
+}
+
+int kle_vec_ghost_update(kle_vec *v)
+{
+    KLE_ARG(v, "null vec");
+    return halo_exchange(v->ctx, v->base, v->ghost_lo, v->n_local, v->ghost_hi, v->lo_rank,
+                         v->hi_rank, v->send_lo, v->send_hi);
+}
+
+int kle_vec_device_ptr(const kle_vec *v, double **p)
+{
+    KLE_ARG(v && p, "null arg");
+    *p = v->d;
+    return 0;
+}
+
+int kle_stream_copy_bench(kle_ctx *ctx, int64_t bytes, int reps, double *gbps)
+{
+    KLE_ARG(ctx && gbps && bytes >= 64 && reps >= 1, "bad arg");
+    int64_t n4 = bytes / 32;
+    double4 *a, *b;
+    KLE_HIP(hipMalloc(&a, n4 * 32));
+    KLE_HIP(hipMalloc(&b, n4 * 32));
+    KLE_HIP(hipMemsetAsync(a, 0, n4 * 32, ctx->stream));
+    int g = ctx->num_cus * 8;
+    hipLaunchKernelGGL(k_stream_copy, dim3(g), dim3(256), 0, ctx->stream, n4, a, b);
+    hipEvent_t e0, e1;
+    KLE_HIP(hipEventCreate(&e0));
+    KLE_HIP(hipEventCreate(&e1));
+    KLE_HIP(hipEventRecord(e0, ctx->stream));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(k_stream_copy, dim3(g), dim3(256), 0, ctx->stream, n4, a, b);
+    KLE_HIP(hipEventRecord(e1, ctx->stream));
+    KLE_HIP(hipEventSynchronize(e1));
+    float ms;
+    KLE_HIP(hipEventElapsedTime(&ms, e0, e1));
+    *gbps = 2.0 * n4 * 32 * reps / (ms * 1e-3) / 1e9;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipFree(a);
+    hipFree(b);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+// kle_internal.hpp -- shared internals of libkle.so (MI355X / gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/kle.h"
+
+namespace kle {
+
+int fail(int code, const char *fmt, ...);
+void clear_error();
+
+constexpr int WAVE = 64;
+
+#define KLE_HIP(call)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (call);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return kle::fail(KLE_ERR_DEVICE, "%s failed: %s (%s:%d)", #call,             \
+                             hipGetErrorString(e_), __FILE__, __LINE__);                 \
+    } while (0)
+
+#define KLE_NCCL(call)                                                                   \
+    do {                                                                                 \
+        ncclResult_t r_ = (call);                                                        \
+        if (r_ != ncclSuccess)                                                           \
+            return kle::fail(KLE_ERR_COMM, "%s failed: %s", #call, ncclGetErrorString(r_)); \
+    } while (0)
+
+#define KLE_TRY(call)                                                                    \
+    do {                                                                                 \
+        int rc_ = (call);                                                                \
+        if (rc_) return rc_;                                                             \
+    } while (0)
+
+#define KLE_ARG(cond, ...)                                                               \
+    do {                                                                                 \
+        if (!(cond)) return kle::fail(KLE_ERR_ARG, __VA_ARGS__);                         \
+    } while (0)
+
+// Deterministic two-stage reductions: kernels write one partial per
+// workgroup; a single-workgroup kernel sums them in a fixed order.
+constexpr int RED_BLOCKS = 2048;   // max partial slots per quantity
+constexpr int NSCAL = 32;          // device scalar slots
+
+// Device scalar slots used by the Krylov kernels.
+enum Scal {
+    S_RHO = 0, S_RHO_OLD, S_PQ, S_ALPHA, S_BETA, S_RR, S_TOL, S_BNORM,
+    S_SUM0, S_SUM1, S_SUM2, S_SUM3,  // raw reduction outputs
+    S_TMP0, S_TMP1
+};
+// Device integer state: [0] reason (0 iterating), [1] iterations done,
+// [2] fixed-iteration mode, [3] maxit.
+enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_COUNT = 8 };
+
+}  // namespace kle
+
+struct kle_ctx {
+    int device = 0, rank = 0, nranks = 1;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    bool profiling = false;
+    struct Stat {
+        int64_t count = 0;
+        double ms = 0;
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    };
+    std::map<std::string, Stat> stats;
+    std::vector<hipEvent_t> event_pool;
+    // reduction scratch
+    double *d_partials = nullptr;  // [4][RED_BLOCKS]
+    double *d_scal = nullptr;      // [NSCAL]
+    int *d_istate = nullptr;       // [I_COUNT]
+    double *h_scal = nullptr;      // pinned mirror
+    int *h_istate = nullptr;
+    int num_cus = 256;
+
+    // timing helpers (no-ops unless profiling)
+    int tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev);
+    int toc(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev);
+    int resolve_stats();
+    hipEvent_t get_event();
+};
+
+struct kle_mesh {
+    int dim = 3, ngl = 2, p = 1, rank = 0, nranks = 1;
+    int64_t nel[3] = {1, 1, 1}, L[3] = {1, 1, 1};
+    int64_t N = 1, E = 1;
+    double lower[3] = {0, 0, 0}, upper[3] = {1, 1, 1}, h[3] = {1, 1, 1};
+    std::vector<double> xi;  // GLL nodes on [0,1], ascending
+    int axis = 2;            // partition axis (slowest lattice axis)
+    int64_t plane = 1;       // nodes per lattice plane of the partition axis
+    int64_t pl0 = 0, pl1 = 0, xl0 = 0, xl1 = 0, el0 = 0, el1 = 0;  // planes / element layers
+    int64_t node_begin = 0, node_end = 0, ext_begin = 0, ext_end = 0;
+    int64_t elem_begin = 0, elem_end = 0;
+    int64_t elem_layer = 1;  // elements per layer of the partition axis
+    std::vector<uint8_t> dir;  // Dirichlet flag per ext node (index - ext_begin)
+    bool dir_set = false;
+    int halo_lo_rank = -1, halo_hi_rank = -1;
+    int64_t halo_lo_nodes = 0, halo_hi_nodes = 0;   // ghost nodes received
+    int64_t send_lo_nodes = 0, send_hi_nodes = 0;   // owned nodes sent to neighbours
+    int nn() const { return dim == 2 ? ngl * ngl : ngl * ngl * ngl; }
+    void lattice_of(int64_t id, int64_t *c) const {
+        c[0] = id % L[0];
+        id /= L[0];
+        c[1] = id % L[1];
+        c[2] = id / L[1];
+        if (dim == 2) c[2] = 0;
+    }
+    int64_t id_of(const int64_t *c) const { return c[0] + L[0] * (c[1] + L[1] * c[2]); }
+};
+
+struct kle_vec {
+    kle_ctx *ctx = nullptr;
+    int64_t n_local = 0, n_global = 0, lo = 0;  // owned [lo, lo + n_local)
+    int64_t ghost_lo = 0, ghost_hi = 0;         // ghost entries before / after owned
+    int bs = 1;
+    double *base = nullptr;                     // allocation (ghost_lo + n_local + ghost_hi)
+    double *d = nullptr;                        // = base + ghost_lo
+    // halo plan (entries, not nodes)
+    int lo_rank = -1, hi_rank = -1;
+    int64_t send_lo = 0, send_hi = 0;
+    bool owns = true;
+};
+
+struct kle_mat {
+    kle_ctx *ctx = nullptr;
+    int kind = 0;  // 0 node-block, 1 scalar AIJ
+    int64_t m_global = 0, n_global = 0, m_local = 0, n_local = 0, row_lo = 0, col_lo = 0;
+    // ---- node-block (kind 0)
+    int R = 1, C = 1;
+    int64_t nrows = 0;         // owned node rows
+    int64_t nblocks = 0;
+    int64_t node_begin = 0, ext_begin = 0, ext_nodes = 0;
+    int *d_rowptr = nullptr;   // [nrows+1] block offsets
+    int *d_bcol = nullptr;     // [nblocks] local ext node index
+    double *d_val = nullptr;   // [nblocks*R*C], per row SoA [a][b][k]
+    std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
+    // halo plan of the column space
+    int lo_rank = -1, hi_rank = -1;
+    int64_t ghost_lo = 0, ghost_hi = 0, send_lo = 0, send_hi = 0;  // entries
+    // ---- scalar AIJ (kind 1)
+    int64_t nnz = 0;
+    int64_t *d_aptr = nullptr;   // [m_local+1]
+    int *d_acol = nullptr;       // [nnz] local column
+    double *d_aval = nullptr;
+    // host staging for setValues (PETSc stash semantics)
+    std::vector<int64_t> h_ptr;  // preallocated pattern (after first assembly)
+    std::vector<int64_t> h_col;
+    std::vector<double> h_val;
+    struct StashEnt {
+        int64_t col;
+        double v;
+        int add;
+    };
+    std::vector<std::vector<StashEnt>> stash;  // per row, before first assembly
+    std::vector<int32_t> d_nnz_hint;
+    bool assembled = false, dirty = false;
+};
+
+namespace kle {
+// vec helpers used across translation units
+int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64_t glo,
+              int64_t ghi, kle_vec **out);
+int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
+                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi);
+int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials,
+         int *nparts, const int *istate);
+int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
+int grid_for(int64_t work, int per_block, int max_blocks);
+}  // namespace kle

@@ -1,0 +1,669 @@
+// kle_ksp.hip -- Krylov solvers on the device (KSP replacement).
+//
+// Replaces KspSolver / KSPSolve (solver/kle_solver.py:33-41,54-64).  The
+// reference configures gmres + PC lu and the makefile forces preonly + lu
+// (makefile:7); K is SPD (identity on Dirichlet rows, SPD free block), so the
+// hot path is (Jacobi-)preconditioned CG:
+//   * every scalar (alpha, beta, rho, norms) stays in device memory; kernels
+//     read them directly -> no host round trip inside an iteration;
+//   * convergence is decided on the device: the scalar kernel sets a reason
+//     word and every later kernel of the solve turns into a no-op, so the
+//     host only polls every few iterations and the iteration count is exact;
+//   * the dot(p, A p) partials are fused into the SpMV epilogue, the x/r
+//     update and the r.z / r.r partials are one kernel;
+//   * deterministic two-stage reductions (per-workgroup partials, fixed-order
+//     final sum), RCCL allreduce of the 1-2 scalars across ranks.
+// GMRES(m) (classical Gram-Schmidt, right Jacobi preconditioning) is the
+// general fallback; its tiny Hessenberg least-squares update runs on the host.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "kle_internal.hpp"
+
+namespace kle {
+
+__device__ __forceinline__ double wsum2(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block sum of 1..3 values, lane 0 of wave 0 holds the result
+template <int NQ>
+__device__ __forceinline__ void block_sums(double (&v)[NQ], double *partials, int stride)
+{
+    __shared__ double lds[NQ][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = wsum2(v[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) lds[q][w] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            double s = 0;
+            for (int i = 0; i < nw; ++i) s += lds[q][i];
+            partials[q * stride + blockIdx.x] = s;
+        }
+}
+
+constexpr int KB = 256;
+
+// x = 0, r = b, p = 0 ; partials: [0] r.z, [1] r.r
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_cg_start(int64_t n, const double *__restrict__ b,
+                                                 const double *__restrict__ dinv, double *__restrict__ x,
+                                                 double *__restrict__ r, double *__restrict__ p,
+                                                 double *__restrict__ partials)
+{
+    double s[2] = {0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double ri = b[i];
+        x[i] = 0.0;
+        r[i] = ri;
+        p[i] = 0.0;
+        const double zi = JAC ? dinv[i] * ri : ri;
+        s[0] += ri * zi;
+        s[1] += ri * ri;
+    }
+    block_sums<2>(s, partials, RED_BLOCKS);
+}
+
+// p = z + beta p,  z = D^-1 r
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_cg_p(int64_t n, const double *__restrict__ r, const double *__restrict__ dinv,
+                                             double *__restrict__ p, const double *__restrict__ scal,
+                                             const int *__restrict__ ist)
+{
+    if (ist[I_REASON] != 0) return;
+    const double beta = scal[S_BETA];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double zi = JAC ? dinv[i] * r[i] : r[i];
+        p[i] = zi + beta * p[i];
+    }
+}
+
+// x += alpha p ; r -= alpha q ; partials: [0] r.z, [1] r.r
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_cg_update(int64_t n, const double *__restrict__ p, const double *__restrict__ q,
+                                                  const double *__restrict__ dinv, double *__restrict__ x,
+                                                  double *__restrict__ r, double *__restrict__ partials,
+                                                  const double *__restrict__ scal, const int *__restrict__ ist)
+{
+    if (ist[I_REASON] != 0) return;
+    const double alpha = scal[S_ALPHA];
+    double s[2] = {0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        x[i] += alpha * p[i];
+        const double ri = r[i] - alpha * q[i];
+        r[i] = ri;
+        const double zi = JAC ? dinv[i] * ri : ri;
+        s[0] += ri * zi;
+        s[1] += ri * ri;
+    }
+    block_sums<2>(s, partials, RED_BLOCKS);
+}
+
+enum Stage { ST_START = 0, ST_ALPHA = 1, ST_BETA = 2 };
+
+__device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, double atol)
+{
+    if (stage == ST_START) {
+        const double rz = scal[S_SUM0], rr = scal[S_SUM1];
+        const double bn = sqrt(rr);
+        scal[S_BNORM] = bn;
+        scal[S_TOL] = fmax(rtol * bn, atol);
+        scal[S_RHO] = rz;
+        scal[S_RR] = rr;
+        scal[S_BETA] = 0.0;
+        ist[I_ITS] = 0;
+        ist[I_REASON] = 0;
+        if (!ist[I_FIXED] && bn <= scal[S_TOL]) ist[I_REASON] = bn <= atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+        if (!isfinite(bn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
+        return;
+    }
+    if (ist[I_REASON] != 0) return;
+    if (stage == ST_ALPHA) {
+        const double pq = scal[S_SUM0];
+        scal[S_PQ] = pq;
+        if (!isfinite(pq)) {
+            ist[I_REASON] = KLE_DIVERGED_NANORINF;
+            return;
+        }
+        if (pq <= 0.0 && !ist[I_FIXED]) {
+            ist[I_REASON] = -8;  // KSP_DIVERGED_INDEFINITE_MAT
+            return;
+        }
+        scal[S_ALPHA] = scal[S_RHO] / pq;
+        return;
+    }
+    // ST_BETA
+    const double rz = scal[S_SUM0], rr = scal[S_SUM1];
+    scal[S_RHO_OLD] = scal[S_RHO];
+    scal[S_RHO] = rz;
+    scal[S_BETA] = rz / scal[S_RHO_OLD];
+    scal[S_RR] = rr;
+    const int its = ++ist[I_ITS];
+    const double rn = sqrt(rr);
+    if (ist[I_FIXED]) {
+        if (its >= ist[I_FIXED]) ist[I_REASON] = KLE_CONVERGED_ITS;
+        return;
+    }
+    if (!isfinite(rn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
+    else if (rn <= scal[S_TOL]) ist[I_REASON] = rn <= atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+    else if (its >= ist[I_MAXIT]) ist[I_REASON] = KLE_DIVERGED_ITS;
+}
+
+// Sum nq partial arrays (fixed order) into scal[S_SUM0..]; optionally apply
+// the stage's scalar update in the same launch (single rank).
+__global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict__ partials, int nparts, int nq,
+                                                       double *__restrict__ scal, int *__restrict__ ist, int stage,
+                                                       int fuse, double rtol, double atol)
+{
+    if (stage != ST_START && ist[I_REASON] != 0) return;
+    __shared__ double lds[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int q = 0; q < nq; ++q) {
+        double s = 0;
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partials[q * RED_BLOCKS + i];
+        s = wsum2(s);
+        __syncthreads();
+        if (lane == 0) lds[w] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0;
+            for (int i = 0; i < nw; ++i) t += lds[i];
+            scal[S_SUM0 + q] = t;
+        }
+    }
+    if (fuse && threadIdx.x == 0) cg_scalars(stage, scal, ist, rtol, atol);
+}
+
+__global__ void k_scalars(double *scal, int *ist, int stage, double rtol, double atol)
+{
+    cg_scalars(stage, scal, ist, rtol, atol);
+}
+
+__global__ void k_invert_diag(int64_t n, const double *__restrict__ d, double *__restrict__ dinv)
+{
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) dinv[i] = d[i] != 0.0 ? 1.0 / d[i] : 1.0;
+}
+
+// y = b - y (true residual)
+__global__ void k_bmy(int64_t n, const double *__restrict__ b, double *__restrict__ y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = b[i] - y[i];
+}
+
+// ------------------------------------------------------------- GMRES kernels
+// h[j] partials of V[:,j] . w for j < k (classical Gram-Schmidt, one pass)
+__global__ __launch_bounds__(KB) void k_mdot(int64_t n, int k, const double *const *__restrict__ V,
+                                             const double *__restrict__ w, double *__restrict__ partials)
+{
+    __shared__ double lds[16];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int j = 0; j < k; ++j) {
+        double s = 0;
+        const double *v = V[j];
+        for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+            s += v[i] * w[i];
+        s = wsum2(s);
+        __syncthreads();
+        if (lane == 0) lds[wv] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0;
+            for (int i = 0; i < nw; ++i) t += lds[i];
+            partials[j * RED_BLOCKS + blockIdx.x] = t;
+        }
+    }
+}
+
+// w -= sum_j h[j] V[:,j]
+__global__ __launch_bounds__(KB) void k_maxpy(int64_t n, int k, const double *const *__restrict__ V,
+                                              const double *__restrict__ h, double *__restrict__ w)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double s = w[i];
+        for (int j = 0; j < k; ++j) s -= h[j] * V[j][i];
+        w[i] = s;
+    }
+}
+
+__global__ void k_reduce_many(const double *__restrict__ partials, int nparts, int nq, double *__restrict__ out)
+{
+    __shared__ double lds[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int q = 0; q < nq; ++q) {
+        double s = 0;
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partials[q * RED_BLOCKS + i];
+        s = wsum2(s);
+        __syncthreads();
+        if (lane == 0) lds[w] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0;
+            for (int i = 0; i < nw; ++i) t += lds[i];
+            out[q] = t;
+        }
+    }
+}
+
+}  // namespace kle
+
+using namespace kle;
+
+struct kle_ksp {
+    kle_ctx *ctx = nullptr;
+    std::string type = "cg", pc = "jacobi";
+    double rtol = 1e-5, atol = 1e-50, dtol = 1e5;
+    int maxit = 10000, restart = 30, fixed = 0, check_every = 8;
+    kle_mat *A = nullptr;
+    kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
+    std::vector<kle_vec *> V;  // GMRES basis
+    double **d_Vptr = nullptr;
+    double *d_h = nullptr;
+    bool setup = false;
+    int its = 0, reason = 0;
+    double rnorm = 0, true_rel = -1;
+};
+
+static void free_work(kle_ksp *k)
+{
+    kle_vec_destroy(k->r);
+    kle_vec_destroy(k->p);
+    kle_vec_destroy(k->q);
+    kle_vec_destroy(k->dinv);
+    for (auto v : k->V) kle_vec_destroy(v);
+    k->V.clear();
+    hipFree(k->d_Vptr);
+    hipFree(k->d_h);
+    k->r = k->p = k->q = k->dinv = nullptr;
+    k->d_Vptr = nullptr;
+    k->d_h = nullptr;
+    k->setup = false;
+}
+
+static int make_vec_like_cols(kle_ksp *k, kle_vec **out)
+{
+    // a vector in the column space of A (ghosted for nb matrices)
+    kle_mat *A = k->A;
+    KLE_TRY(vec_alloc(k->ctx, A->n_local, A->n_global, A->col_lo, A->kind == 0 ? A->ghost_lo : 0,
+                      A->kind == 0 ? A->ghost_hi : 0, out));
+    (*out)->bs = A->C;
+    (*out)->lo_rank = A->lo_rank;
+    (*out)->hi_rank = A->hi_rank;
+    (*out)->send_lo = A->send_lo;
+    (*out)->send_hi = A->send_hi;
+    return 0;
+}
+
+static int reduce_stage(kle_ksp *k, int nparts, int nq, int stage)
+{
+    kle_ctx *c = k->ctx;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(c->tic("reduce", &ev));
+    const int fuse = c->nranks == 1;
+    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, c->stream, c->d_partials, nparts, nq, c->d_scal,
+                       c->d_istate, stage, fuse, k->rtol, k->atol);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(c->toc("reduce", &ev));
+    if (!fuse) {
+        KLE_TRY(c->tic("allreduce", &ev));
+        KLE_NCCL(ncclAllReduce(c->d_scal + S_SUM0, c->d_scal + S_SUM0, nq, ncclDouble, ncclSum, c->comm, c->stream));
+        KLE_TRY(c->toc("allreduce", &ev));
+        hipLaunchKernelGGL(k_scalars, dim3(1), dim3(1), 0, c->stream, c->d_scal, c->d_istate, stage, k->rtol, k->atol);
+        KLE_HIP(hipGetLastError());
+    }
+    return 0;
+}
+
+static int poll_state(kle_ksp *k)
+{
+    kle_ctx *c = k->ctx;
+    KLE_HIP(hipMemcpyAsync(c->h_istate, c->d_istate, sizeof(int) * I_COUNT, hipMemcpyDeviceToHost, c->stream));
+    KLE_HIP(hipMemcpyAsync(c->h_scal, c->d_scal, sizeof(double) * NSCAL, hipMemcpyDeviceToHost, c->stream));
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+static int true_residual(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    kle_ctx *c = k->ctx;
+    // q = A x ; q = b - q ; ||q|| / ||b||
+    KLE_HIP(hipMemcpyAsync(k->p->d, x->d, sizeof(double) * x->n_local, hipMemcpyDeviceToDevice, c->stream));
+    KLE_TRY(spmv(k->A, k->p, k->q, nullptr, nullptr, nullptr, nullptr));
+    hipLaunchKernelGGL(k_bmy, dim3(grid_for(b->n_local, KB, RED_BLOCKS)), dim3(KB), 0, c->stream, b->n_local, b->d,
+                       k->q->d);
+    KLE_HIP(hipGetLastError());
+    double rn, bn;
+    KLE_TRY(kle_vec_norm2(k->q, &rn));
+    KLE_TRY(kle_vec_norm2(b, &bn));
+    k->true_rel = bn > 0 ? rn / bn : rn;
+    return 0;
+}
+
+static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    kle_ctx *c = k->ctx;
+    const int64_t n = b->n_local;
+    const bool jac = k->pc == "jacobi";
+    const double *dinv = jac ? k->dinv->d : nullptr;
+    const int g = grid_for(n, KB, RED_BLOCKS);
+    int host_fixed[I_COUNT] = {0, 0, k->fixed, k->fixed ? k->fixed : k->maxit, 0, 0, 0, 0};
+    KLE_HIP(hipMemcpyAsync(c->d_istate, host_fixed, sizeof(int) * I_COUNT, hipMemcpyHostToDevice, c->stream));
+    if (jac)
+        hipLaunchKernelGGL(k_cg_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->p->d,
+                           c->d_partials);
+    else
+        hipLaunchKernelGGL(k_cg_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->p->d,
+                           c->d_partials);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(reduce_stage(k, g, 2, ST_START));
+    const int limit = k->fixed ? k->fixed : k->maxit;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    for (int it = 0; it < limit; ++it) {
+        KLE_TRY(c->tic("p_update", &ev));
+        if (jac)
+            hipLaunchKernelGGL(k_cg_p<true>, dim3(g), dim3(KB), 0, c->stream, n, k->r->d, dinv, k->p->d, c->d_scal,
+                               c->d_istate);
+        else
+            hipLaunchKernelGGL(k_cg_p<false>, dim3(g), dim3(KB), 0, c->stream, n, k->r->d, dinv, k->p->d, c->d_scal,
+                               c->d_istate);
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(c->toc("p_update", &ev));
+        int np = 0;
+        KLE_TRY(spmv(k->A, k->p, k->q, k->p, c->d_partials, &np, c->d_istate));
+        KLE_TRY(reduce_stage(k, np, 1, ST_ALPHA));
+        KLE_TRY(c->tic("cg_update", &ev));
+        if (jac)
+            hipLaunchKernelGGL(k_cg_update<true>, dim3(g), dim3(KB), 0, c->stream, n, k->p->d, k->q->d, dinv, x->d,
+                               k->r->d, c->d_partials, c->d_scal, c->d_istate);
+        else
+            hipLaunchKernelGGL(k_cg_update<false>, dim3(g), dim3(KB), 0, c->stream, n, k->p->d, k->q->d, dinv, x->d,
+                               k->r->d, c->d_partials, c->d_scal, c->d_istate);
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(c->toc("cg_update", &ev));
+        KLE_TRY(reduce_stage(k, g, 2, ST_BETA));
+        if (!k->fixed && ((it + 1) % k->check_every == 0)) {
+            KLE_TRY(poll_state(k));
+            if (c->h_istate[I_REASON] != 0) break;
+        }
+    }
+    KLE_TRY(poll_state(k));
+    k->its = c->h_istate[I_ITS];
+    k->reason = c->h_istate[I_REASON];
+    if (k->reason == 0) k->reason = KLE_DIVERGED_ITS;
+    k->rnorm = std::sqrt(c->h_scal[S_RR]);
+    return 0;
+}
+
+// ------------------------------------------------------------------ GMRES
+static int gmres_dots(kle_ksp *k, int kk, const kle_vec *w, double *h)
+{
+    kle_ctx *c = k->ctx;
+    const int64_t n = w->n_local;
+    const int g = grid_for(n, KB, RED_BLOCKS);
+    hipLaunchKernelGGL(k_mdot, dim3(g), dim3(KB), 0, c->stream, n, kk, (const double *const *)k->d_Vptr, w->d,
+                       c->d_partials);
+    hipLaunchKernelGGL(k_reduce_many, dim3(1), dim3(1024), 0, c->stream, c->d_partials, g, kk, k->d_h);
+    KLE_HIP(hipGetLastError());
+    if (c->nranks > 1) KLE_NCCL(ncclAllReduce(k->d_h, k->d_h, kk, ncclDouble, ncclSum, c->comm, c->stream));
+    KLE_HIP(hipMemcpyAsync(h, k->d_h, sizeof(double) * kk, hipMemcpyDeviceToHost, c->stream));
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+static int solve_gmres(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    // right-preconditioned GMRES(m): A M^-1 u = b, x = M^-1 u; the residual
+    // norm is the true (unpreconditioned) one, as for CG.
+    kle_ctx *c = k->ctx;
+    const int m = k->restart;
+    const bool jac = k->pc == "jacobi";
+    const int64_t n = b->n_local;
+    KLE_TRY(kle_vec_set(x, 0.0));
+    double bn;
+    KLE_TRY(kle_vec_norm2(b, &bn));
+    const double tol = std::max(k->rtol * bn, k->atol);
+    std::vector<double> H((m + 1) * m), cs(m), sn(m), gvec(m + 1), hcol(m + 1);
+    k->its = 0;
+    k->reason = 0;
+    double rn = bn;
+    if (rn <= tol) {
+        k->reason = rn <= k->atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+        k->rnorm = rn;
+        return 0;
+    }
+    kle_vec *z = k->q;  // scratch for M^-1 v
+    while (true) {
+        // r = b - A x  -> V0
+        KLE_HIP(hipMemcpyAsync(k->p->d, x->d, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+        KLE_TRY(spmv(k->A, k->p, k->V[0], nullptr, nullptr, nullptr, nullptr));
+        hipLaunchKernelGGL(k_bmy, dim3(grid_for(n, KB, RED_BLOCKS)), dim3(KB), 0, c->stream, n, b->d, k->V[0]->d);
+        KLE_TRY(kle_vec_norm2(k->V[0], &rn));
+        if (rn <= tol) break;
+        KLE_TRY(kle_vec_scale(k->V[0], 1.0 / rn));
+        std::fill(gvec.begin(), gvec.end(), 0.0);
+        gvec[0] = rn;
+        int j = 0;
+        for (; j < m && k->its < k->maxit; ++j) {
+            // w = A M^-1 v_j
+            if (jac) KLE_TRY(kle_vec_pointwise_mult(z, k->dinv, k->V[j]));
+            else KLE_TRY(kle_vec_copy(k->V[j], z));
+            KLE_TRY(spmv(k->A, z, k->V[j + 1], nullptr, nullptr, nullptr, nullptr));
+            // two passes of classical Gram-Schmidt (CGS2)
+            std::fill(hcol.begin(), hcol.end(), 0.0);
+            for (int pass = 0; pass < 2; ++pass) {
+                std::vector<double> h(j + 1);
+                KLE_TRY(gmres_dots(k, j + 1, k->V[j + 1], h.data()));
+                KLE_HIP(hipMemcpyAsync(k->d_h, h.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, c->stream));
+                hipLaunchKernelGGL(k_maxpy, dim3(grid_for(n, KB, RED_BLOCKS)), dim3(KB), 0, c->stream, n, j + 1,
+                                   (const double *const *)k->d_Vptr, k->d_h, k->V[j + 1]->d);
+                KLE_HIP(hipGetLastError());
+                for (int i = 0; i <= j; ++i) hcol[i] += h[i];
+            }
+            double hn;
+            KLE_TRY(kle_vec_norm2(k->V[j + 1], &hn));
+            hcol[j + 1] = hn;
+            if (hn > 0) KLE_TRY(kle_vec_scale(k->V[j + 1], 1.0 / hn));
+            for (int i = 0; i < j; ++i) {  // apply previous rotations
+                double t = cs[i] * hcol[i] + sn[i] * hcol[i + 1];
+                hcol[i + 1] = -sn[i] * hcol[i] + cs[i] * hcol[i + 1];
+                hcol[i] = t;
+            }
+            double den = std::hypot(hcol[j], hcol[j + 1]);
+            cs[j] = den > 0 ? hcol[j] / den : 1.0;
+            sn[j] = den > 0 ? hcol[j + 1] / den : 0.0;
+            hcol[j] = den;
+            hcol[j + 1] = 0;
+            gvec[j + 1] = -sn[j] * gvec[j];
+            gvec[j] = cs[j] * gvec[j];
+            for (int i = 0; i <= j; ++i) H[i * m + j] = hcol[i];
+            ++k->its;
+            rn = std::fabs(gvec[j + 1]);
+            if (rn <= tol || hn == 0) {
+                ++j;
+                break;
+            }
+        }
+        // solve H y = g, x += M^-1 V y
+        std::vector<double> y(j);
+        for (int i = j - 1; i >= 0; --i) {
+            double s = gvec[i];
+            for (int l = i + 1; l < j; ++l) s -= H[i * m + l] * y[l];
+            y[i] = s / H[i * m + i];
+        }
+        KLE_HIP(hipMemcpyAsync(k->d_h, y.data(), sizeof(double) * j, hipMemcpyHostToDevice, c->stream));
+        // z = - sum y_i v_i  (k_maxpy subtracts), then x += M^-1 (-z)
+        KLE_TRY(kle_vec_set(z, 0.0));
+        hipLaunchKernelGGL(k_maxpy, dim3(grid_for(n, KB, RED_BLOCKS)), dim3(KB), 0, c->stream, n, j,
+                           (const double *const *)k->d_Vptr, k->d_h, z->d);
+        KLE_HIP(hipGetLastError());
+        if (jac) KLE_TRY(kle_vec_pointwise_mult(z, k->dinv, z));
+        KLE_TRY(kle_vec_axpy(x, -1.0, z));
+        if (rn <= tol) break;
+        if (k->its >= k->maxit) {
+            k->reason = KLE_DIVERGED_ITS;
+            break;
+        }
+    }
+    if (!k->reason) k->reason = rn <= k->atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+    k->rnorm = rn;
+    return 0;
+}
+
+extern "C" {
+
+int kle_ksp_create(kle_ctx *ctx, kle_ksp **out)
+{
+    KLE_ARG(ctx && out, "null arg");
+    kle_ksp *k = new kle_ksp;
+    k->ctx = ctx;
+    *out = k;
+    return 0;
+}
+
+int kle_ksp_destroy(kle_ksp *k)
+{
+    if (!k) return 0;
+    free_work(k);
+    delete k;
+    return 0;
+}
+
+int kle_ksp_set_type(kle_ksp *k, const char *t)
+{
+    KLE_ARG(k && t, "null arg");
+    std::string s(t);
+    KLE_ARG(s == "cg" || s == "gmres" || s == "preonly", "unknown KSP type '%s' (cg|gmres|preonly)", t);
+    k->type = s;
+    k->setup = false;
+    return 0;
+}
+
+int kle_ksp_set_pc_type(kle_ksp *k, const char *t)
+{
+    KLE_ARG(k && t, "null arg");
+    std::string s(t);
+    KLE_ARG(s == "none" || s == "jacobi" || s == "lu", "unknown PC type '%s' (none|jacobi|lu)", t);
+    k->pc = s;
+    k->setup = false;
+    return 0;
+}
+
+int kle_ksp_set_tolerances(kle_ksp *k, double rtol, double atol, double dtol, int maxit)
+{
+    KLE_ARG(k, "null ksp");
+    if (rtol >= 0) k->rtol = rtol;
+    if (atol >= 0) k->atol = atol;
+    if (dtol >= 0) k->dtol = dtol;
+    if (maxit > 0) k->maxit = maxit;
+    return 0;
+}
+
+int kle_ksp_set_gmres_restart(kle_ksp *k, int restart)
+{
+    KLE_ARG(k && restart >= 1 && restart <= 200, "bad restart");
+    k->restart = restart;
+    k->setup = false;
+    return 0;
+}
+
+int kle_ksp_set_fixed_iterations(kle_ksp *k, int n)
+{
+    KLE_ARG(k && n >= 0, "bad arg");
+    k->fixed = n;
+    return 0;
+}
+
+int kle_ksp_set_operators(kle_ksp *k, kle_mat *A)
+{
+    KLE_ARG(k && A, "null arg");
+    KLE_ARG(A->m_global == A->n_global, "KSP needs a square operator");
+    k->A = A;
+    k->setup = false;
+    return 0;
+}
+
+int kle_ksp_set_up(kle_ksp *k)
+{
+    KLE_ARG(k && k->A, "operators not set");
+    if (k->setup) return 0;
+    if (k->pc == "lu" || k->type == "preonly")
+        return fail(KLE_ERR_SUP,
+                    "PC 'lu' / KSP 'preonly' (the reference's direct LU, makefile:7) has no device "
+                    "implementation; use -ksp_type cg -pc_type jacobi (K is SPD)");
+    free_work(k);
+    KLE_TRY(make_vec_like_cols(k, &k->r));
+    KLE_TRY(make_vec_like_cols(k, &k->p));
+    KLE_TRY(make_vec_like_cols(k, &k->q));
+    if (k->pc == "jacobi") {
+        KLE_TRY(make_vec_like_cols(k, &k->dinv));
+        KLE_TRY(kle_mat_get_diagonal(k->A, k->q));
+        hipLaunchKernelGGL(k_invert_diag, dim3((k->A->m_local + 255) / 256), dim3(256), 0, k->ctx->stream,
+                           k->A->m_local, k->q->d, k->dinv->d);
+        KLE_HIP(hipGetLastError());
+    }
+    if (k->type == "gmres") {
+        k->V.resize(k->restart + 1);
+        for (auto &v : k->V) KLE_TRY(make_vec_like_cols(k, &v));
+        std::vector<double *> ptrs(k->V.size());
+        for (size_t i = 0; i < ptrs.size(); ++i) ptrs[i] = k->V[i]->d;
+        KLE_HIP(hipMalloc(&k->d_Vptr, sizeof(double *) * ptrs.size()));
+        KLE_HIP(hipMalloc(&k->d_h, sizeof(double) * (k->restart + 2)));
+        KLE_HIP(hipMemcpy(k->d_Vptr, ptrs.data(), sizeof(double *) * ptrs.size(), hipMemcpyHostToDevice));
+    }
+    KLE_HIP(hipStreamSynchronize(k->ctx->stream));
+    k->setup = true;
+    return 0;
+}
+
+int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    KLE_ARG(k && b && x, "null arg");
+    KLE_TRY(kle_ksp_set_up(k));
+    KLE_ARG(b->n_local == k->A->m_local && x->n_local == k->A->n_local, "b/x sizes do not match the operator");
+    k->true_rel = -1;
+    if (k->type == "cg") KLE_TRY(solve_cg(k, b, x));
+    else KLE_TRY(solve_gmres(k, b, x));
+    if (!k->fixed) KLE_TRY(true_residual(k, b, x));
+    return 0;
+}
+
+int kle_ksp_get_iteration_number(const kle_ksp *k, int *its)
+{
+    KLE_ARG(k && its, "null arg");
+    *its = k->its;
+    return 0;
+}
+
+int kle_ksp_get_residual_norm(const kle_ksp *k, double *rn)
+{
+    KLE_ARG(k && rn, "null arg");
+    *rn = k->rnorm;
+    return 0;
+}
+
+int kle_ksp_get_converged_reason(const kle_ksp *k, int *reason)
+{
+    KLE_ARG(k && reason, "null arg");
+    *reason = k->reason;
+    return 0;
+}
+
+int kle_ksp_get_true_relative_residual(const kle_ksp *k, double *rel)
+{
+    KLE_ARG(k && rel, "null arg");
+    *rel = k->true_rel;
+    return 0;
+}
+
+}  // extern "C"

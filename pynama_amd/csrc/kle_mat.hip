@@ -1,0 +1,702 @@
+// kle_mat.hip -- device sparse matrices and SpMV kernels for gfx950.
+//
+// Two formats:
+//  * node-block ("nb"): the KLE operators couple whole nodes, so every row of
+//    nodes shares one column list.  Per node row i: m_i block columns (int32,
+//    local ghosted node index) and R*C value streams laid out [a][b][k]
+//    (structure of arrays inside the row), so lane k of a wavefront reads
+//    value (a,b) of block k with unit stride: every load instruction is a
+//    fully coalesced 512-byte sweep and the column index costs 4/(R*C)
+//    bytes per value instead of 4.  Values keep PETSc's pattern (explicit
+//    zeros included), only the index storage is shared.
+//  * scalar CSR ("aij"): MatSeqAIJ layout (int64 row pointers, int32
+//    columns), used by the generic petsc4py-style setValues/assemble path.
+//
+// SpMV = MatMult (MatMult_SeqAIJ / MatMult_MPIAIJ; kle_solver.py:35-41,
+// base_problem.py:123-136): one 64-lane wavefront per node row (per scalar row
+// for aij), matrix streams read with non-temporal loads so they do not evict
+// the ghosted x vector from L2, shuffle reductions, optional fused dot(y, p)
+// partials for the Krylov loop.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+
+#include "kle_internal.hpp"
+
+namespace kle {
+
+__device__ __forceinline__ double wsum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <class T>
+__device__ __forceinline__ T ntload(const T *p)
+{
+    return __builtin_nontemporal_load(p);
+}
+
+constexpr int SPMV_BLOCK = 256;
+constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
+
+template <int R, int C, bool DOT>
+__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int *__restrict__ rowptr,
+                                                        const int *__restrict__ bcol,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x,
+                                                        double *__restrict__ y,
+                                                        const double *__restrict__ pd,
+                                                        double *__restrict__ partials,
+                                                        const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave0 = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
+    double dotacc = 0.0;
+    for (int64_t i = wave0; i < nrows; i += nwaves) {
+        const int b0 = rowptr[i];
+        const int m = rowptr[i + 1] - b0;
+        const double *v = val + (int64_t)b0 * (R * C);
+        const int *cj = bcol + b0;
+        double acc[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[a] = 0.0;
+        for (int k = lane; k < m; k += 64) {
+            const int64_t j = ntload(cj + k);
+            double xv[C];
+#pragma unroll
+            for (int b = 0; b < C; ++b) xv[b] = x[j * C + b];
+#pragma unroll
+            for (int a = 0; a < R; ++a)
+#pragma unroll
+                for (int b = 0; b < C; ++b) acc[a] += ntload(v + (int64_t)(a * C + b) * m + k) * xv[b];
+        }
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[a] = wsum(acc[a]);
+        if (lane < R) {
+            double mine = acc[0];
+#pragma unroll
+            for (int a = 1; a < R; ++a)
+                if (lane == a) mine = acc[a];
+            y[i * R + lane] = mine;
+            if (DOT) dotacc += mine * pd[i * R + lane];
+        }
+    }
+    if (DOT) {
+        __shared__ double lds[SPMV_WAVES];
+        dotacc = wsum(dotacc);
+        if (lane == 0) lds[threadIdx.x >> 6] = dotacc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 0;
+            for (int w = 0; w < SPMV_WAVES; ++w) s += lds[w];
+            partials[blockIdx.x] = s;
+        }
+    }
+}
+
+template <bool DOT>
+__global__ __launch_bounds__(SPMV_BLOCK) void k_aij_spmv(int64_t nrows, const int64_t *__restrict__ ptr,
+                                                         const int *__restrict__ col,
+                                                         const double *__restrict__ val,
+                                                         const double *__restrict__ x, double *__restrict__ y,
+                                                         const double *__restrict__ pd,
+                                                         double *__restrict__ partials,
+                                                         const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave0 = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
+    double dotacc = 0.0;
+    for (int64_t i = wave0; i < nrows; i += nwaves) {
+        const int64_t s = ptr[i], e = ptr[i + 1];
+        double acc = 0.0;
+        for (int64_t k = s + lane; k < e; k += 64) acc += ntload(val + k) * x[ntload(col + k)];
+        acc = wsum(acc);
+        if (lane == 0) {
+            y[i] = acc;
+            if (DOT) dotacc += acc * pd[i];
+        }
+    }
+    if (DOT) {
+        __shared__ double lds[SPMV_WAVES];
+        dotacc = wsum(dotacc);
+        if (lane == 0) lds[threadIdx.x >> 6] = dotacc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 0;
+            for (int w = 0; w < SPMV_WAVES; ++w) s += lds[w];
+            partials[blockIdx.x] = s;
+        }
+    }
+}
+
+// diagonal position of each node row (for Jacobi / get_diagonal)
+__global__ void k_diagpos(int64_t nrows, int64_t row_off, const int *__restrict__ rowptr,
+                          const int *__restrict__ bcol, int *__restrict__ pos)
+{
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    int lo = rowptr[i], hi = rowptr[i + 1] - 1, want = (int)(i + row_off), found = -1;
+    while (lo <= hi) {
+        int mid = (lo + hi) >> 1;
+        int c = bcol[mid];
+        if (c == want) {
+            found = mid;
+            break;
+        }
+        if (c < want) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    pos[i] = found < 0 ? -1 : found - rowptr[i];
+}
+
+template <int R, int C>
+__global__ void k_nb_scale(int64_t nrows, const int *__restrict__ rowptr, const int *__restrict__ bcol,
+                           double *__restrict__ val, const double *__restrict__ L,
+                           const double *__restrict__ Rx)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (i >= nrows) return;
+    const int b0 = rowptr[i], m = rowptr[i + 1] - b0;
+    double *v = val + (int64_t)b0 * R * C;
+    for (int k = lane; k < m; k += 64) {
+        const int64_t j = bcol[b0 + k];
+        for (int a = 0; a < R; ++a)
+            for (int b = 0; b < C; ++b) {
+                double s = 1.0;
+                if (L) s *= L[i * R + a];
+                if (Rx) s *= Rx[j * C + b];
+                v[(int64_t)(a * C + b) * m + k] *= s;
+            }
+    }
+}
+
+__global__ void k_nb_diag(int64_t nrows, int R, int C, const int *__restrict__ rowptr,
+                          const int *__restrict__ pos, const double *__restrict__ val, double *__restrict__ d)
+{
+    int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= nrows * R) return;
+    int64_t i = t / R;
+    int a = (int)(t % R);
+    const int b0 = rowptr[i], m = rowptr[i + 1] - b0;
+    d[t] = pos[i] < 0 ? 0.0 : val[(int64_t)b0 * R * C + (int64_t)(a * C + a) * m + pos[i]];
+}
+
+__global__ void k_aij_scale(int64_t nrows, const int64_t *__restrict__ ptr, const int *__restrict__ col,
+                            double *__restrict__ val, const double *__restrict__ L,
+                            const double *__restrict__ Rx)
+{
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+        double s = 1.0;
+        if (L) s *= L[i];
+        if (Rx) s *= Rx[col[k]];
+        val[k] *= s;
+    }
+}
+
+__global__ void k_aij_diag(int64_t nrows, int64_t col_off, const int64_t *__restrict__ ptr,
+                           const int *__restrict__ col, const double *__restrict__ val, double *__restrict__ d)
+{
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    double v = 0.0;
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+        if (col[k] == i + col_off) v = val[k];
+    d[i] = v;
+}
+
+__global__ void k_axpy_same(int64_t n, double a, const double *__restrict__ x, double *__restrict__ y)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] += a * x[i];
+}
+
+int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials, int *nparts,
+         const int *istate)
+{
+    kle_ctx *c = A->ctx;
+    const bool dot = dotvec != nullptr;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    if (A->kind == 0) {
+        if (c->nranks > 1)
+            KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
+                                  x->send_lo, x->send_hi));
+        const int grid = grid_for(A->nrows, SPMV_WAVES, RED_BLOCKS);
+        if (nparts) *nparts = grid;
+        const double *pd = dot ? dotvec->d : nullptr;
+        KLE_TRY(c->tic("spmv", &ev));
+#define NB_CASE(RR, CC)                                                                             \
+    if (A->R == RR && A->C == CC) {                                                                 \
+        if (dot)                                                                                    \
+            hipLaunchKernelGGL((k_nb_spmv<RR, CC, true>), dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, \
+                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, partials, istate); \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_nb_spmv<RR, CC, false>), dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, \
+                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, partials, istate); \
+    } else
+        NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
+        NB_CASE(3, 6) NB_CASE(1, 1) {
+            return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
+        }
+#undef NB_CASE
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(c->toc("spmv", &ev));
+        return 0;
+    }
+    const int grid = grid_for(A->m_local, SPMV_WAVES, RED_BLOCKS);
+    if (nparts) *nparts = grid;
+    KLE_TRY(c->tic("spmv", &ev));
+    if (dot)
+        hipLaunchKernelGGL(k_aij_spmv<true>, dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, A->m_local, A->d_aptr,
+                           A->d_acol, A->d_aval, x->d, y->d, dotvec->d, partials, istate);
+    else
+        hipLaunchKernelGGL(k_aij_spmv<false>, dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, A->m_local, A->d_aptr,
+                           A->d_acol, A->d_aval, x->d, y->d, nullptr, partials, istate);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(c->toc("spmv", &ev));
+    return 0;
+}
+
+static int check_mult_layout(const kle_mat *A, const kle_vec *x, const kle_vec *y)
+{
+    if (A->kind == 0) {
+        if (x->n_local != A->n_local || x->ghost_lo != A->ghost_lo || x->ghost_hi != A->ghost_hi)
+            return fail(KLE_ERR_SIZ, "x layout does not match the matrix column space "
+                                     "(need a mesh vector with bs=%d)", A->C);
+    } else if (x->n_local != A->n_local) {
+        return fail(KLE_ERR_SIZ, "x has %lld local entries, matrix has %lld columns", (long long)x->n_local,
+                    (long long)A->n_local);
+    }
+    if (y->n_local != A->m_local)
+        return fail(KLE_ERR_SIZ, "y has %lld local entries, matrix has %lld rows", (long long)y->n_local,
+                    (long long)A->m_local);
+    return 0;
+}
+
+// host copy of an nb matrix
+struct NBHost {
+    std::vector<int> rp, bc;
+    std::vector<double> v;
+};
+
+static int nb_download(const kle_mat *A, NBHost &h)
+{
+    h.rp.resize(A->nrows + 1);
+    h.bc.resize(std::max<int64_t>(A->nblocks, 1));
+    h.v.resize(std::max<int64_t>(A->nblocks * A->R * A->C, 1));
+    KLE_HIP(hipMemcpy(h.rp.data(), A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(h.bc.data(), A->d_bcol, sizeof(int) * h.bc.size(), hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(h.v.data(), A->d_val, sizeof(double) * h.v.size(), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+static int aij_upload(kle_mat *A)
+{
+    kle_ctx *c = A->ctx;
+    hipFree(A->d_aptr);
+    hipFree(A->d_acol);
+    hipFree(A->d_aval);
+    A->d_aptr = nullptr;
+    A->d_acol = nullptr;
+    A->d_aval = nullptr;
+    A->nnz = A->h_ptr.back();
+    std::vector<int> c32(std::max<int64_t>(A->nnz, 1));
+    for (int64_t k = 0; k < A->nnz; ++k) c32[k] = (int)(A->h_col[k] - A->col_lo);
+    KLE_HIP(hipMalloc(&A->d_aptr, sizeof(int64_t) * A->h_ptr.size()));
+    KLE_HIP(hipMalloc(&A->d_acol, sizeof(int) * c32.size()));
+    KLE_HIP(hipMalloc(&A->d_aval, sizeof(double) * std::max<int64_t>(A->nnz, 1)));
+    KLE_HIP(hipMemcpyAsync(A->d_aptr, A->h_ptr.data(), sizeof(int64_t) * A->h_ptr.size(), hipMemcpyHostToDevice, c->stream));
+    KLE_HIP(hipMemcpyAsync(A->d_acol, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice, c->stream));
+    if (A->nnz)
+        KLE_HIP(hipMemcpyAsync(A->d_aval, A->h_val.data(), sizeof(double) * A->nnz, hipMemcpyHostToDevice, c->stream));
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+}  // namespace kle
+
+using namespace kle;
+
+extern "C" {
+
+int kle_mat_create_aij(kle_ctx *ctx, int64_t m_local, int64_t n_local, int64_t m_global, int64_t n_global,
+                       const int32_t *d_nnz, const int32_t *o_nnz, kle_mat **out)
+{
+    KLE_ARG(ctx && out, "null arg");
+    KLE_ARG(m_local >= 0 && n_local >= 0, "negative size");
+    if (ctx->nranks > 1) return fail(KLE_ERR_SUP, "generic AIJ is single-rank; use kle_assemble_kle for MPI layouts");
+    if (m_global < 0) m_global = m_local;
+    if (n_global < 0) n_global = n_local;
+    KLE_ARG(m_global == m_local && n_global == n_local, "single rank: global size must equal local size");
+    kle_mat *A = new kle_mat;
+    A->ctx = ctx;
+    A->kind = 1;
+    A->m_local = m_local;
+    A->n_local = n_local;
+    A->m_global = m_global;
+    A->n_global = n_global;
+    A->stash.resize(m_local);
+    if (d_nnz) A->d_nnz_hint.assign(d_nnz, d_nnz + m_local);
+    (void)o_nnz;
+    *out = A;
+    return 0;
+}
+
+int kle_mat_set_values(kle_mat *A, int32_t nr, const int64_t *rows, int32_t nc, const int64_t *cols,
+                       const double *v, int addv)
+{
+    KLE_ARG(A && rows && cols && v, "null arg");
+    if (A->kind != 1) return fail(KLE_ERR_SUP, "setValues on a node-block matrix: assemble with kle_assemble_kle");
+    for (int32_t r = 0; r < nr; ++r) {
+        const int64_t row = rows[r] - A->row_lo;
+        if (rows[r] < 0) continue;  // PETSc ignores negative indices
+        if (row < 0 || row >= A->m_local)
+            return fail(KLE_ERR_OUTOFRANGE, "row %lld out of range [0,%lld)", (long long)rows[r], (long long)A->m_local);
+        for (int32_t c = 0; c < nc; ++c) {
+            if (cols[c] < 0) continue;
+            if (cols[c] >= A->n_global)
+                return fail(KLE_ERR_OUTOFRANGE, "column %lld out of range", (long long)cols[c]);
+            const double val = v[(int64_t)r * nc + c];
+            if (!A->assembled) {
+                A->stash[row].push_back({cols[c], val, addv ? 1 : 0});
+            } else {
+                auto b = A->h_col.begin() + A->h_ptr[row], e = A->h_col.begin() + A->h_ptr[row + 1];
+                auto it = std::lower_bound(b, e, cols[c]);
+                if (it == e || *it != cols[c])
+                    return fail(KLE_ERR_NEWNZ, "new nonzero at (%lld,%lld) caused a malloc", (long long)rows[r],
+                                (long long)cols[c]);
+                double &slot = A->h_val[it - A->h_col.begin()];
+                slot = addv ? slot + val : val;
+                A->dirty = true;
+            }
+        }
+    }
+    return 0;
+}
+
+int kle_mat_assemble(kle_mat *A)
+{
+    KLE_ARG(A, "null mat");
+    if (A->kind != 1) return 0;
+    if (!A->assembled) {
+        // build the pattern: entries in call order, ADD sums from 0 in that
+        // order, INSERT overwrites (MatSetValues_SeqAIJ semantics)
+        A->h_ptr.assign(A->m_local + 1, 0);
+        A->h_col.clear();
+        A->h_val.clear();
+        for (int64_t r = 0; r < A->m_local; ++r) {
+            std::map<int64_t, double> row;
+            for (auto &en : A->stash[r]) {
+                if (en.add) row[en.col] += en.v;
+                else row[en.col] = en.v;
+            }
+            for (auto &kv : row) {
+                A->h_col.push_back(kv.first);
+                A->h_val.push_back(kv.second);
+            }
+            A->h_ptr[r + 1] = (int64_t)A->h_col.size();
+            std::vector<kle_mat::StashEnt>().swap(A->stash[r]);
+        }
+        A->assembled = true;
+        return aij_upload(A);
+    }
+    if (A->dirty) {
+        KLE_HIP(hipMemcpy(A->d_aval, A->h_val.data(), sizeof(double) * A->nnz, hipMemcpyHostToDevice));
+        A->dirty = false;
+    }
+    return 0;
+}
+
+int kle_mat_destroy(kle_mat *A)
+{
+    if (!A) return 0;
+    hipFree(A->d_rowptr);
+    hipFree(A->d_bcol);
+    hipFree(A->d_val);
+    hipFree(A->d_aptr);
+    hipFree(A->d_acol);
+    hipFree(A->d_aval);
+    delete A;
+    return 0;
+}
+
+int kle_mat_get_size(const kle_mat *A, int64_t *m, int64_t *n)
+{
+    KLE_ARG(A, "null mat");
+    if (m) *m = A->m_global;
+    if (n) *n = A->n_global;
+    return 0;
+}
+
+int kle_mat_get_ownership_range(const kle_mat *A, int64_t *lo, int64_t *hi)
+{
+    KLE_ARG(A && lo && hi, "null arg");
+    *lo = A->row_lo;
+    *hi = A->row_lo + A->m_local;
+    return 0;
+}
+
+int kle_mat_get_local_nnz(const kle_mat *A, int64_t *nnz)
+{
+    KLE_ARG(A && nnz, "null arg");
+    if (A->kind == 1) {
+        *nnz = A->nnz;
+        return 0;
+    }
+    int64_t m, z;
+    KLE_TRY(kle_mat_get_csr_size(A, &m, &z));
+    *nnz = z;
+    return 0;
+}
+
+int kle_mat_mult(kle_mat *A, kle_vec *x, kle_vec *y)
+{
+    KLE_ARG(A && x && y, "null arg");
+    if (A->kind == 1 && !A->assembled) return fail(KLE_ERR_STATE, "matrix not assembled");
+    KLE_TRY(check_mult_layout(A, x, y));
+    return spmv(A, x, y, nullptr, nullptr, nullptr, nullptr);
+}
+
+int kle_mat_mult_add(kle_mat *A, kle_vec *x, kle_vec *y, kle_vec *z)
+{
+    KLE_ARG(A && x && y && z, "null arg");
+    kle_vec *t;
+    KLE_TRY(kle_vec_duplicate(z, &t));
+    KLE_TRY(kle_mat_mult(A, x, t));
+    KLE_TRY(kle_vec_waxpy(z, 1.0, t, y));
+    KLE_HIP(hipStreamSynchronize(A->ctx->stream));
+    kle_vec_destroy(t);
+    return 0;
+}
+
+int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *Rv)
+{
+    KLE_ARG(A, "null mat");
+    kle_ctx *c = A->ctx;
+    if (L && L->n_local != A->m_local) return fail(KLE_ERR_SIZ, "left scaling vector size mismatch");
+    if (A->kind == 0) {
+        const double *rx = nullptr;
+        if (Rv) {
+            if (Rv->n_local != A->n_local || Rv->ghost_lo != A->ghost_lo || Rv->ghost_hi != A->ghost_hi)
+                return fail(KLE_ERR_SIZ, "right scaling vector must be a ghosted mesh vector of the column space");
+            KLE_TRY(halo_exchange(c, Rv->base, Rv->ghost_lo, Rv->n_local, Rv->ghost_hi, Rv->lo_rank, Rv->hi_rank,
+                                  Rv->send_lo, Rv->send_hi));
+            rx = Rv->base;
+        }
+        const int64_t th = A->nrows * 64;
+#define SC_CASE(RR, CC)                                                                                    \
+    if (A->R == RR && A->C == CC)                                                                          \
+        hipLaunchKernelGGL((k_nb_scale<RR, CC>), dim3((th + 255) / 256), dim3(256), 0, c->stream, A->nrows, \
+                           A->d_rowptr, A->d_bcol, A->d_val, L ? L->d : nullptr, rx);                      \
+    else
+        SC_CASE(3, 3) SC_CASE(2, 2) SC_CASE(2, 1) SC_CASE(1, 2) SC_CASE(3, 1) SC_CASE(1, 3) SC_CASE(6, 3)
+        SC_CASE(3, 6) SC_CASE(1, 1) return fail(KLE_ERR_SUP, "no scale kernel for %dx%d", A->R, A->C);
+#undef SC_CASE
+    } else {
+        if (Rv && Rv->n_local != A->n_local) return fail(KLE_ERR_SIZ, "right scaling vector size mismatch");
+        hipLaunchKernelGGL(k_aij_scale, dim3((A->m_local + 255) / 256), dim3(256), 0, c->stream, A->m_local,
+                           A->d_aptr, A->d_acol, A->d_aval, L ? L->d : nullptr, Rv ? Rv->d : nullptr);
+        // keep the host mirror in step for later setValues
+        KLE_HIP(hipMemcpyAsync(A->h_val.data(), A->d_aval, sizeof(double) * A->nnz, hipMemcpyDeviceToHost, c->stream));
+    }
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int kle_mat_get_diagonal(const kle_mat *A, kle_vec *d)
+{
+    KLE_ARG(A && d, "null arg");
+    KLE_ARG(d->n_local == A->m_local, "diagonal vector size mismatch");
+    kle_ctx *c = A->ctx;
+    if (A->kind == 0) {
+        KLE_ARG(A->R == A->C, "get_diagonal needs square blocks");
+        int *pos;
+        KLE_HIP(hipMalloc(&pos, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
+        hipLaunchKernelGGL(k_diagpos, dim3((A->nrows + 255) / 256), dim3(256), 0, c->stream, A->nrows,
+                           A->node_begin - A->ext_begin, A->d_rowptr, A->d_bcol, pos);
+        hipLaunchKernelGGL(k_nb_diag, dim3((A->nrows * A->R + 255) / 256), dim3(256), 0, c->stream, A->nrows, A->R,
+                           A->C, A->d_rowptr, pos, A->d_val, d->d);
+        KLE_HIP(hipGetLastError());
+        KLE_HIP(hipStreamSynchronize(c->stream));
+        hipFree(pos);
+        return 0;
+    }
+    hipLaunchKernelGGL(k_aij_diag, dim3((A->m_local + 255) / 256), dim3(256), 0, c->stream, A->m_local, A->row_lo - A->col_lo,
+                       A->d_aptr, A->d_acol, A->d_aval, d->d);
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz)
+{
+    KLE_ARG(A && m_local && nnz, "null arg");
+    *m_local = A->m_local;
+    if (A->kind == 1) {
+        *nnz = A->assembled ? A->nnz : 0;
+        return 0;
+    }
+    std::vector<int> rp(A->nrows + 1);
+    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToHost));
+    int64_t z = 0;
+    for (int64_t i = 0; i < A->nrows; ++i)
+        z += A->diag_only_row[i] ? std::min(A->R, A->C) : (int64_t)(rp[i + 1] - rp[i]) * A->R * A->C;
+    *nnz = z;
+    return 0;
+}
+
+int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double *data)
+{
+    KLE_ARG(A && indptr && indices && data, "null arg");
+    if (A->kind == 1) {
+        KLE_HIP(hipMemcpy(data, A->d_aval, sizeof(double) * A->nnz, hipMemcpyDeviceToHost));
+        memcpy(indptr, A->h_ptr.data(), sizeof(int64_t) * (A->m_local + 1));
+        memcpy(indices, A->h_col.data(), sizeof(int64_t) * A->nnz);
+        return 0;
+    }
+    NBHost h;
+    KLE_TRY(nb_download(A, h));
+    const int R = A->R, C = A->C;
+    int64_t z = 0;
+    indptr[0] = 0;
+    for (int64_t i = 0; i < A->nrows; ++i) {
+        const int b0 = h.rp[i], m = h.rp[i + 1] - b0;
+        const double *v = h.v.data() + (int64_t)b0 * R * C;
+        for (int a = 0; a < R; ++a) {
+            if (A->diag_only_row[i]) {
+                // Dirichlet row: PETSc stores the diagonal only (mat_fs.py:44-45,115-120)
+                if (a < C) {
+                    indices[z] = (A->node_begin + i) * C + a;
+                    data[z++] = v[(a * C + a) * (int64_t)m + 0];
+                }
+            } else {
+                for (int k = 0; k < m; ++k)
+                    for (int b = 0; b < C; ++b) {
+                        indices[z] = (A->ext_begin + h.bc[b0 + k]) * C + b;
+                        data[z++] = v[(int64_t)(a * C + b) * m + k];
+                    }
+            }
+            indptr[i * R + a + 1] = z;
+        }
+    }
+    return 0;
+}
+
+int kle_mat_convert_aij(const kle_mat *A, kle_mat **out)
+{
+    KLE_ARG(A && out, "null arg");
+    KLE_ARG(A->ctx->nranks == 1, "convert_aij is single-rank");
+    int64_t m, z;
+    KLE_TRY(kle_mat_get_csr_size(A, &m, &z));
+    kle_mat *B;
+    KLE_TRY(kle_mat_create_aij(A->ctx, A->m_local, A->n_local, A->m_global, A->n_global, nullptr, nullptr, &B));
+    B->h_ptr.resize(m + 1);
+    B->h_col.resize(std::max<int64_t>(z, 1));
+    B->h_val.resize(std::max<int64_t>(z, 1));
+    KLE_TRY(kle_mat_get_csr(A, B->h_ptr.data(), B->h_col.data(), B->h_val.data()));
+    B->h_col.resize(z);
+    B->h_val.resize(z);
+    B->assembled = true;
+    B->stash.clear();
+    KLE_TRY(aij_upload(B));
+    *out = B;
+    return 0;
+}
+
+int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X)
+{
+    KLE_ARG(Y && X, "null arg");
+    KLE_ARG(Y->kind == X->kind && Y->m_local == X->m_local && Y->n_local == X->n_local, "layout mismatch");
+    kle_ctx *c = Y->ctx;
+    if (Y->kind == 0) {
+        KLE_ARG(Y->R == X->R && Y->C == X->C && Y->nblocks == X->nblocks, "axpy needs the same pattern");
+        NBHost hy, hx;
+        KLE_TRY(nb_download(Y, hy));
+        KLE_TRY(nb_download(X, hx));
+        if (hy.rp != hx.rp || hy.bc != hx.bc) return fail(KLE_ERR_SUP, "axpy needs the same pattern");
+        const int64_t n = Y->nblocks * Y->R * Y->C;
+        hipLaunchKernelGGL(k_axpy_same, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, n, a, X->d_val, Y->d_val);
+        KLE_HIP(hipGetLastError());
+        KLE_HIP(hipStreamSynchronize(c->stream));
+        return 0;
+    }
+    // aij: subset pattern, merged on the host (setup-time operation)
+    for (int64_t r = 0; r < X->m_local; ++r)
+        for (int64_t k = X->h_ptr[r]; k < X->h_ptr[r + 1]; ++k) {
+            auto b = Y->h_col.begin() + Y->h_ptr[r], e = Y->h_col.begin() + Y->h_ptr[r + 1];
+            auto it = std::lower_bound(b, e, X->h_col[k]);
+            if (it == e || *it != X->h_col[k]) return fail(KLE_ERR_SUP, "axpy: X pattern not a subset of Y");
+        }
+    std::vector<double> xv(std::max<int64_t>(X->nnz, 1));
+    KLE_HIP(hipMemcpy(Y->h_val.data(), Y->d_aval, sizeof(double) * Y->nnz, hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(xv.data(), X->d_aval, sizeof(double) * X->nnz, hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < X->m_local; ++r)
+        for (int64_t k = X->h_ptr[r]; k < X->h_ptr[r + 1]; ++k) {
+            auto b = Y->h_col.begin() + Y->h_ptr[r], e = Y->h_col.begin() + Y->h_ptr[r + 1];
+            auto it = std::lower_bound(b, e, X->h_col[k]);
+            Y->h_val[it - Y->h_col.begin()] += a * xv[k];
+        }
+    KLE_HIP(hipMemcpy(Y->d_aval, Y->h_val.data(), sizeof(double) * Y->nnz, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
+{
+    KLE_ARG(A && out, "null arg");
+    kle_mat *B = new kle_mat(*A);
+    B->d_rowptr = nullptr;
+    B->d_bcol = nullptr;
+    B->d_val = nullptr;
+    B->d_aptr = nullptr;
+    B->d_acol = nullptr;
+    B->d_aval = nullptr;
+    if (A->kind == 0) {
+        const size_t nv = std::max<int64_t>(A->nblocks * A->R * A->C, 1);
+        KLE_HIP(hipMalloc(&B->d_rowptr, sizeof(int) * (A->nrows + 1)));
+        KLE_HIP(hipMalloc(&B->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1)));
+        KLE_HIP(hipMalloc(&B->d_val, sizeof(double) * nv));
+        KLE_HIP(hipMemcpy(B->d_rowptr, A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToDevice));
+        KLE_HIP(hipMemcpy(B->d_bcol, A->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1), hipMemcpyDeviceToDevice));
+        if (copy_values) KLE_HIP(hipMemcpy(B->d_val, A->d_val, sizeof(double) * nv, hipMemcpyDeviceToDevice));
+        else KLE_HIP(hipMemset(B->d_val, 0, sizeof(double) * nv));
+    } else {
+        if (!copy_values) std::fill(B->h_val.begin(), B->h_val.end(), 0.0);
+        if (A->assembled) {
+            if (copy_values) KLE_HIP(hipMemcpy(B->h_val.data(), A->d_aval, sizeof(double) * A->nnz, hipMemcpyDeviceToHost));
+            KLE_TRY(aij_upload(B));
+        }
+    }
+    *out = B;
+    return 0;
+}
+
+int kle_mat_get_format(const kle_mat *A, char *buf, int buflen)
+{
+    KLE_ARG(A && buf && buflen > 3, "bad arg");
+    snprintf(buf, buflen, "%s", A->kind == 0 ? "nb" : "aij");
+    return 0;
+}
+
+int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
+{
+    KLE_ARG(A && bytes, "null arg");
+    if (A->kind == 0) {
+        *bytes = (double)A->nblocks * (A->R * A->C * 8.0 + 4.0) + (A->nrows + 1) * 4.0 +
+                 (double)A->ext_nodes * A->C * 8.0 + (double)A->m_local * 8.0;
+    } else {
+        *bytes = (double)A->nnz * 12.0 + (A->m_local + 1) * 8.0 + A->n_local * 8.0 + A->m_local * 8.0;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+"""Structured box mesh + slab partition (host side of libkle, no GPU needed).
+
+Replaces for the hot path the reference's DMPlex box mesh and FEM section
+numbering (domain/dmplex.py:18-49,193-196,352-372,382-388).  Canonical
+numbering: node id = ix + Lx*(iy + Ly*iz) on the GLL lattice, cells
+x-fastest, element-local nodes in tensor order; ranks own slabs of whole
+element layers along the slowest axis (z in 3-D, y in 2-D).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import MeshInfo, call
+
+# face names in the reference's order (dmplex.py:27-30): bit i of a face mask
+FACES = {2: ["down", "right", "up", "left"],
+         3: ["back", "front", "down", "up", "right", "left"]}
+
+
+class BoxMesh:
+    def __init__(self, dim, nelem, lower, upper, ngl, rank=0, nranks=1):
+        self.dim, self.ngl = int(dim), int(ngl)
+        ne = np.array(list(nelem) + [1] * (3 - dim), dtype=np.int64)
+        lo = np.array(list(lower) + [0.0] * (3 - dim), dtype=np.float64)
+        hi = np.array(list(upper) + [1.0] * (3 - dim), dtype=np.float64)
+        h = C.c_void_p()
+        call("kle_mesh_create_box", self.dim, ne, lo, hi, self.ngl, int(rank), int(nranks), C.byref(h))
+        self._h = h
+        info = MeshInfo()
+        call("kle_mesh_get_info", h, C.byref(info))
+        self.info = info
+        self.rank, self.nranks = info.rank, info.nranks
+        self.N = info.n_nodes
+        self.E = info.n_elems
+        self.node_range = (info.node_begin, info.node_end)
+        self.ext_range = (info.ext_begin, info.ext_end)
+        self.elem_range = (info.elem_begin, info.elem_end)
+        self.lattice = tuple(info.lattice[:dim])
+        self.nelem = tuple(info.nelem[:dim])
+        self.nn = self.ngl ** self.dim
+        self.dim_w = 1 if dim == 2 else 3
+        self.dim_s = 3 if dim == 2 else 6
+
+    def __del__(self):
+        try:
+            if self._h:
+                call("kle_mesh_destroy", self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    @property
+    def n_owned(self):
+        return self.node_range[1] - self.node_range[0]
+
+    def conn(self):
+        ne = self.elem_range[1] - self.elem_range[0]
+        out = np.zeros(ne * self.nn, dtype=np.int64)
+        call("kle_mesh_get_conn", self._h, out)
+        return out.reshape(ne, self.nn)
+
+    def corners(self):
+        ne = self.elem_range[1] - self.elem_range[0]
+        out = np.zeros(ne * 2 ** self.dim * self.dim)
+        call("kle_mesh_get_corners", self._h, out)
+        return out.reshape(ne, 2 ** self.dim, self.dim)
+
+    def coords(self):
+        out = np.zeros(self.n_owned * self.dim)
+        call("kle_mesh_get_coords", self._h, out)
+        return out.reshape(self.n_owned, self.dim)
+
+    def face_mask(self, names):
+        faces = FACES[self.dim]
+        m = 0
+        for n in names:
+            m |= 1 << faces.index(n)
+        return m
+
+    def face_nodes(self, names):
+        """Owned nodes on the named faces, sorted (getBorderNodes, dmplex.py:160-166)."""
+        mask = self.face_mask(names) if not isinstance(names, int) else names
+        n = C.c_int64()
+        call("kle_mesh_face_nodes", self._h, mask, None, C.byref(n))
+        out = np.zeros(max(n.value, 1), dtype=np.int64)
+        call("kle_mesh_face_nodes", self._h, mask, out.ctypes.data, C.byref(n))
+        return out[: n.value]
+
+    def set_dirichlet_faces(self, names):
+        call("kle_mesh_set_dirichlet_faces", self._h, self.face_mask(names))
+
+    def set_dirichlet_nodes(self, nodes):
+        nodes = np.ascontiguousarray(np.asarray(sorted(nodes), dtype=np.int64))
+        call("kle_mesh_set_dirichlet_nodes", self._h, nodes if len(nodes) else np.zeros(1, np.int64),
+             len(nodes))
+
+    def pattern(self, which):
+        """Symbolic node-block pattern: 0 K, 1 Krhs, 2 Rw -> (row_ptr, global cols)."""
+        nb = C.c_int64()
+        call("kle_mesh_pattern_size", self._h, int(which), C.byref(nb))
+        rp = np.zeros(self.n_owned + 1, dtype=np.int64)
+        cols = np.zeros(max(nb.value, 1), dtype=np.int64)
+        call("kle_mesh_pattern", self._h, int(which), rp, cols.ctypes.data)
+        return rp, cols[: nb.value]
+
+    def halo(self):
+        lo, hi, lr, hr = C.c_int64(), C.c_int64(), C.c_int(), C.c_int()
+        call("kle_mesh_halo", self._h, C.byref(lo), C.byref(hi), C.byref(lr), C.byref(hr))
+        return {"lo_nodes": lo.value, "hi_nodes": hi.value, "lo_rank": lr.value, "hi_rank": hr.value}

@@ -1,0 +1,593 @@
+"""petsc4py-shaped Mat / Vec / KSP / PC / Options over libkle (device-resident).
+
+Mirrors exactly the petsc4py subset Pynama's hot path uses:
+  Mat: createAIJ, setUp, setName/getName, setValues(addv), assemble,
+       diagonalScale(L=), createVecLeft/Right, getOwnershipRange, mult,
+       Mat*Vec, Mat+Mat, destroy                 (mat_fs.py, kle_solver.py)
+  Vec: createMPI, setValues(addv), setValue, assemble, set, reciprocal,
+       duplicate, copy, getArray, axpy, scale, *=, +, -, *, dot, norm
+                                                 (base_problem.py, mat_fs.py)
+  KSP: create, setType, setPC, setFromOptions, setOperators, setUp, solve,
+       __call__(b, x)                            (kle_solver.py:49-64)
+  PC:  create, setType
+  Options: getString/getInt/getReal              (run_case.py:9-13)
+Errors raise ``Error`` (ierr = PETSc-style code).  Differences from petsc4py:
+Vec.getArray() returns a host COPY of the owned part (device memory), use
+setArray() to write back.
+"""
+import ctypes as C
+import sys
+
+import numpy as np
+
+from ._lib import Error, call
+from .runtime import COMM_WORLD, get_ctx
+
+INSERT_VALUES, ADD_VALUES = 0, 1
+
+
+def _h(obj):
+    return obj._h if obj is not None else None
+
+
+def _i64(a):
+    return np.ascontiguousarray(np.atleast_1d(np.asarray(a, dtype=np.int64)))
+
+
+def _f64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+class Options(dict):
+    """PETSc options database (-key value pairs from argv + programmatic)."""
+
+    _db = None
+
+    def __new__(cls, prefix=None):
+        if Options._db is None:
+            db = dict.__new__(cls)
+            dict.__init__(db)
+            argv = sys.argv[1:]
+            i = 0
+            while i < len(argv):
+                a = argv[i]
+                if a.startswith("-") and len(a) > 1 and not a[1:2].isdigit():
+                    key = a.lstrip("-")
+                    if i + 1 < len(argv) and not (argv[i + 1].startswith("-") and not argv[i + 1][1:2].isdigit()):
+                        db[key] = argv[i + 1]
+                        i += 1
+                    else:
+                        db[key] = "true"
+                i += 1
+            Options._db = db
+        return Options._db
+
+    def __init__(self, prefix=None):
+        pass
+
+    def getString(self, key, default=None):
+        return str(self[key]) if key in self else default
+
+    def getInt(self, key, default=None):
+        return int(self[key]) if key in self else default
+
+    def getReal(self, key, default=None):
+        return float(self[key]) if key in self else default
+
+    def getBool(self, key, default=None):
+        if key not in self:
+            return default
+        return str(self[key]).lower() in ("1", "true", "yes", "on")
+
+    def setValue(self, key, value):
+        self[key.lstrip("-")] = value
+
+    def delValue(self, key):
+        self.pop(key.lstrip("-"), None)
+
+
+class Vec:
+    def __init__(self):
+        self._h = None
+        self._name = ""
+        self._ctx = None
+
+    # ------------------------------------------------------------ creation
+    @classmethod
+    def _wrap(cls, handle, ctx):
+        v = cls()
+        v._h = handle
+        v._ctx = ctx
+        return v
+
+    def createMPI(self, size, comm=None):
+        if isinstance(size, (tuple, list)):
+            nl, ng = size[0], size[1] if len(size) > 1 else None
+        else:
+            nl, ng = size, None
+        ctx = get_ctx()
+        if nl is None:
+            nl = ng // ctx.nranks + (1 if ctx.rank < ng % ctx.nranks else 0)
+        h = C.c_void_p()
+        call("kle_vec_create", ctx.h, int(nl), -1 if ng is None else int(ng), C.byref(h))
+        self._h, self._ctx = h, ctx
+        return self
+
+    def createSeq(self, n, comm=None):
+        return self.createMPI((n, n))
+
+    def createWithArray(self, array, size=None, comm=None):
+        a = _f64(array).ravel()
+        self.createMPI((len(a), None))
+        self.setArray(a)
+        return self
+
+    @classmethod
+    def fromMesh(cls, mesh, bs):
+        ctx = get_ctx()
+        h = C.c_void_p()
+        call("kle_vec_create_mesh", ctx.h, mesh._h, int(bs), C.byref(h))
+        return cls._wrap(h, ctx)
+
+    def duplicate(self):
+        h = C.c_void_p()
+        call("kle_vec_duplicate", self._h, C.byref(h))
+        return Vec._wrap(h, self._ctx)
+
+    def copy(self, result=None):
+        if result is None:
+            result = self.duplicate()
+        call("kle_vec_copy", self._h, result._h)
+        return result
+
+    def destroy(self):
+        if self._h:
+            call("kle_vec_destroy", self._h)
+            self._h = None
+        return self
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------- sizes
+    def setName(self, name):
+        self._name = name
+
+    def getName(self):
+        return self._name
+
+    def getSizes(self):
+        nl, ng = C.c_int64(), C.c_int64()
+        call("kle_vec_get_sizes", self._h, C.byref(nl), C.byref(ng))
+        return nl.value, ng.value
+
+    def getSize(self):
+        return self.getSizes()[1]
+
+    def getLocalSize(self):
+        return self.getSizes()[0]
+
+    def getOwnershipRange(self):
+        lo, hi = C.c_int64(), C.c_int64()
+        call("kle_vec_get_ownership_range", self._h, C.byref(lo), C.byref(hi))
+        return lo.value, hi.value
+
+    @property
+    def owner_range(self):
+        return self.getOwnershipRange()
+
+    @property
+    def size(self):
+        return self.getSize()
+
+    # -------------------------------------------------------------- values
+    def setValues(self, indices, values, addv=False):
+        idx = _i64(indices)
+        vals = _f64(np.broadcast_to(np.asarray(values, dtype=np.float64), idx.shape))
+        call("kle_vec_set_values", self._h, len(idx), idx, vals, int(bool(addv)))
+
+    def setValue(self, index, value, addv=False):
+        self.setValues([index], [value], addv)
+
+    def getValues(self, indices):
+        idx = _i64(indices)
+        out = np.zeros(len(idx))
+        call("kle_vec_get_values", self._h, len(idx), idx, out)
+        return out
+
+    def assemble(self):
+        pass
+
+    assemblyBegin = assemble
+    assemblyEnd = assemble
+
+    def set(self, alpha):
+        call("kle_vec_set", self._h, float(alpha))
+
+    def zeroEntries(self):
+        self.set(0.0)
+
+    def getArray(self, readonly=False):
+        out = np.zeros(self.getLocalSize())
+        call("kle_vec_get_array", self._h, out)
+        return out
+
+    def setArray(self, array):
+        a = _f64(array).ravel()
+        if len(a) != self.getLocalSize():
+            raise Error(60, f"setArray: {len(a)} values for {self.getLocalSize()} local entries")
+        call("kle_vec_set_array", self._h, a)
+
+    @property
+    def array(self):
+        return self.getArray()
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.getArray()
+        return a.astype(dtype) if dtype is not None else a
+
+    def ghostUpdate(self, *args, **kw):
+        call("kle_vec_ghost_update", self._h)
+
+    # ------------------------------------------------------------- BLAS-1
+    def axpy(self, alpha, x):
+        call("kle_vec_axpy", self._h, float(alpha), x._h)
+
+    def aypx(self, alpha, x):
+        call("kle_vec_aypx", self._h, float(alpha), x._h)
+
+    def waxpy(self, alpha, x, y):
+        call("kle_vec_waxpy", self._h, float(alpha), x._h, y._h)
+
+    def scale(self, alpha):
+        call("kle_vec_scale", self._h, float(alpha))
+
+    def pointwiseMult(self, x, y):
+        call("kle_vec_pointwise_mult", self._h, x._h, y._h)
+
+    def reciprocal(self):
+        call("kle_vec_reciprocal", self._h)
+
+    def dot(self, v):
+        out = C.c_double()
+        call("kle_vec_dot", self._h, v._h, C.byref(out))
+        return out.value
+
+    def norm(self, norm_type=2):
+        if norm_type not in (2, None, "2", "NORM_2"):
+            raise Error(56, "only the 2-norm is provided")
+        out = C.c_double()
+        call("kle_vec_norm2", self._h, C.byref(out))
+        return out.value
+
+    def __imul__(self, alpha):
+        self.scale(alpha)
+        return self
+
+    def __add__(self, other):
+        out = self.copy()
+        out.axpy(1.0, other)
+        return out
+
+    def __sub__(self, other):
+        out = self.copy()
+        out.axpy(-1.0, other)
+        return out
+
+    def __mul__(self, other):
+        out = self.copy()
+        if isinstance(other, Vec):
+            out.pointwiseMult(self, other)
+        else:
+            out.scale(other)
+        return out
+
+    __rmul__ = __mul__
+
+
+class Mat:
+    def __init__(self):
+        self._h = None
+        self._name = ""
+        self._ctx = None
+        self._mesh = None    # node-block matrices: (mesh, row bs, col bs)
+        self._rbs = self._cbs = 1
+
+    @classmethod
+    def _wrap(cls, handle, ctx, mesh=None, rbs=1, cbs=1):
+        m = cls()
+        m._h, m._ctx, m._mesh, m._rbs, m._cbs = handle, ctx, mesh, rbs, cbs
+        return m
+
+    def createAIJ(self, size, bsize=None, nnz=None, csr=None, comm=None):
+        (ml, mg), (nl, ng) = size
+        ctx = get_ctx()
+        if ml is None:
+            ml = mg
+        if nl is None:
+            nl = ng
+        d = None
+        if nnz is not None:
+            dn = nnz[0] if isinstance(nnz, (tuple, list)) else nnz
+            if dn is not None:
+                d = np.ascontiguousarray(np.asarray(dn, dtype=np.int32))
+        h = C.c_void_p()
+        call("kle_mat_create_aij", ctx.h, int(ml), int(nl), -1 if mg is None else int(mg),
+             -1 if ng is None else int(ng), d.ctypes.data if d is not None else None, None, C.byref(h))
+        self._h, self._ctx = h, ctx
+        self._keep = d
+        return self
+
+    def setUp(self):
+        return self
+
+    def setName(self, name):
+        self._name = name
+
+    def getName(self):
+        return self._name
+
+    def destroy(self):
+        if self._h:
+            call("kle_mat_destroy", self._h)
+            self._h = None
+        return self
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    def setValues(self, rows, cols, values, addv=False):
+        r, c = _i64(rows), _i64(cols)
+        v = _f64(np.broadcast_to(np.asarray(values, dtype=np.float64), (len(r), len(c))))
+        call("kle_mat_set_values", self._h, len(r), r, len(c), c, v, int(bool(addv)))
+
+    def setValue(self, row, col, value, addv=False):
+        self.setValues([row], [col], [[value]], addv)
+
+    def assemble(self, assembly=None):
+        call("kle_mat_assemble", self._h)
+
+    assemblyBegin = assemble
+    assemblyEnd = assemble
+
+    def getSize(self):
+        m, n = C.c_int64(), C.c_int64()
+        call("kle_mat_get_size", self._h, C.byref(m), C.byref(n))
+        return m.value, n.value
+
+    def getOwnershipRange(self):
+        lo, hi = C.c_int64(), C.c_int64()
+        call("kle_mat_get_ownership_range", self._h, C.byref(lo), C.byref(hi))
+        return lo.value, hi.value
+
+    @property
+    def owner_range(self):
+        return self.getOwnershipRange()
+
+    def getFormat(self):
+        buf = C.create_string_buffer(16)
+        call("kle_mat_get_format", self._h, buf, 16)
+        return buf.value.decode()
+
+    def getInfo(self):
+        nz = C.c_int64()
+        call("kle_mat_get_local_nnz", self._h, C.byref(nz))
+        b = C.c_double()
+        call("kle_mat_spmv_bytes", self._h, C.byref(b))
+        return {"nz_used": nz.value, "nz_allocated": nz.value, "nz_unneeded": 0,
+                "spmv_bytes": b.value, "format": self.getFormat()}
+
+    def spmvBytes(self):
+        b = C.c_double()
+        call("kle_mat_spmv_bytes", self._h, C.byref(b))
+        return b.value
+
+    def createVecLeft(self):
+        if self._mesh is not None:
+            return Vec.fromMesh(self._mesh, self._rbs)
+        lo, hi = self.getOwnershipRange()
+        return Vec().createMPI((hi - lo, self.getSize()[0]))
+
+    def createVecRight(self):
+        if self._mesh is not None:
+            return Vec.fromMesh(self._mesh, self._cbs)
+        m, n = self.getSize()
+        return Vec().createMPI((n, n))
+
+    def createVecs(self):
+        return self.createVecRight(), self.createVecLeft()
+
+    def mult(self, x, y):
+        call("kle_mat_mult", self._h, x._h, y._h)
+
+    def multAdd(self, x, v2, v3):
+        call("kle_mat_mult_add", self._h, x._h, v2._h, v3._h)
+
+    def __mul__(self, x):
+        y = self.createVecLeft()
+        self.mult(x, y)
+        return y
+
+    def diagonalScale(self, L=None, R=None):
+        call("kle_mat_diagonal_scale", self._h, _h(L), _h(R))
+
+    def getDiagonal(self, result=None):
+        if result is None:
+            result = self.createVecLeft()
+        call("kle_mat_get_diagonal", self._h, result._h)
+        return result
+
+    def duplicate(self, copy=False):
+        h = C.c_void_p()
+        call("kle_mat_duplicate", self._h, int(bool(copy)), C.byref(h))
+        return Mat._wrap(h, self._ctx, self._mesh, self._rbs, self._cbs)
+
+    def axpy(self, alpha, X, structure=None):
+        call("kle_mat_axpy", self._h, float(alpha), X._h)
+
+    def __add__(self, other):
+        out = self.duplicate(copy=True)
+        out.axpy(1.0, other)
+        return out
+
+    def convert(self, mat_type="aij"):
+        if mat_type not in ("aij", "seqaij", "mpiaij"):
+            raise Error(56, f"convert to {mat_type}")
+        h = C.c_void_p()
+        call("kle_mat_convert_aij", self._h, C.byref(h))
+        m, n = self.getSize()
+        return Mat._wrap(h, self._ctx)
+
+    def getValuesCSR(self):
+        """(indptr, indices, data) of the owned rows, global column ids."""
+        m, nz = C.c_int64(), C.c_int64()
+        call("kle_mat_get_csr_size", self._h, C.byref(m), C.byref(nz))
+        ip = np.zeros(m.value + 1, dtype=np.int64)
+        ix = np.zeros(max(nz.value, 1), dtype=np.int64)
+        d = np.zeros(max(nz.value, 1))
+        call("kle_mat_get_csr", self._h, ip, ix, d)
+        return ip, ix[: nz.value], d[: nz.value]
+
+
+class PC:
+    def __init__(self):
+        self._type = "jacobi"
+
+    def create(self, comm=None):
+        return self
+
+    def setType(self, t):
+        self._type = str(t).lower()
+
+    def getType(self):
+        return self._type
+
+    def destroy(self):
+        return self
+
+
+class KSP:
+    """Krylov solver on the device.  Default type cg, PC jacobi."""
+
+    def __init__(self):
+        self._h = None
+        self._pc = PC()
+        self._type = "cg"
+        self._A = None
+
+    def create(self, comm=None):
+        ctx = get_ctx()
+        h = C.c_void_p()
+        call("kle_ksp_create", ctx.h, C.byref(h))
+        self._h = h
+        self._ctx = ctx
+        return self
+
+    def _ensure(self):
+        if self._h is None:
+            self.create()
+
+    def setType(self, t):
+        self._ensure()
+        self._type = str(t).lower()
+        call("kle_ksp_set_type", self._h, self._type.encode())
+
+    def getType(self):
+        return self._type
+
+    def setPC(self, pc):
+        self._ensure()
+        self._pc = pc
+        call("kle_ksp_set_pc_type", self._h, pc.getType().encode())
+
+    def getPC(self):
+        return self._pc
+
+    def setTolerances(self, rtol=None, atol=None, divtol=None, max_it=None):
+        self._ensure()
+        call("kle_ksp_set_tolerances", self._h, -1.0 if rtol is None else float(rtol),
+             -1.0 if atol is None else float(atol), -1.0 if divtol is None else float(divtol),
+             -1 if max_it is None else int(max_it))
+
+    def setFixedIterations(self, n):
+        self._ensure()
+        call("kle_ksp_set_fixed_iterations", self._h, int(n))
+
+    def setGMRESRestart(self, m):
+        self._ensure()
+        call("kle_ksp_set_gmres_restart", self._h, int(m))
+
+    def setFromOptions(self):
+        self._ensure()
+        o = Options()
+        if "ksp_type" in o:
+            self.setType(o["ksp_type"])
+        if "pc_type" in o:
+            pc = PC()
+            pc.setType(o["pc_type"])
+            self.setPC(pc)
+        self.setTolerances(o.getReal("ksp_rtol"), o.getReal("ksp_atol"), o.getReal("ksp_divtol"),
+                           o.getInt("ksp_max_it"))
+        if "ksp_gmres_restart" in o:
+            self.setGMRESRestart(o.getInt("ksp_gmres_restart"))
+
+    def setOperators(self, A, P=None):
+        self._ensure()
+        self._A = A
+        call("kle_ksp_set_operators", self._h, A._h)
+
+    def setUp(self):
+        self._ensure()
+        call("kle_ksp_set_up", self._h)
+
+    def solve(self, b, x):
+        call("kle_ksp_solve", self._h, b._h, x._h)
+
+    def __call__(self, b, x=None):
+        if x is None:
+            x = self._A.createVecRight()
+        self.solve(b, x)
+        return x
+
+    def getIterationNumber(self):
+        v = C.c_int()
+        call("kle_ksp_get_iteration_number", self._h, C.byref(v))
+        return v.value
+
+    its = property(getIterationNumber)
+
+    def getResidualNorm(self):
+        v = C.c_double()
+        call("kle_ksp_get_residual_norm", self._h, C.byref(v))
+        return v.value
+
+    def getConvergedReason(self):
+        v = C.c_int()
+        call("kle_ksp_get_converged_reason", self._h, C.byref(v))
+        return v.value
+
+    def getTrueRelativeResidual(self):
+        v = C.c_double()
+        call("kle_ksp_get_true_relative_residual", self._h, C.byref(v))
+        return v.value
+
+    def destroy(self):
+        if self._h:
+            call("kle_ksp_destroy", self._h)
+            self._h = None
+        return self
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+__all__ = ["Mat", "Vec", "KSP", "PC", "Options", "Error", "COMM_WORLD", "INSERT_VALUES", "ADD_VALUES"]

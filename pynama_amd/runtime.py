@@ -1,0 +1,134 @@
+"""Process-level runtime: one kle context (HIP device + stream + RCCL comm)
+per process, one process per GPU.
+
+Rank/world come from torch.distributed when it is initialised (torchrun sets
+RANK / LOCAL_RANK / WORLD_SIZE), otherwise from the environment, otherwise a
+single rank.  The RCCL unique id is made on rank 0 by libkle and broadcast
+over torch.distributed -- PyTorch is only the bootstrap here.
+"""
+import ctypes as C
+import os
+import sys
+
+from ._lib import call, load
+
+
+def _dist():
+    # import torch only when a multi-rank launch can have initialised it
+    if "torch" not in sys.modules and int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist
+    except Exception:  # torch absent or broken: single rank
+        pass
+    return None
+
+
+def world():
+    """(rank, size) without touching the GPU."""
+    d = _dist()
+    if d is not None:
+        return d.get_rank(), d.get_world_size()
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+class Comm:
+    """petsc4py COMM_WORLD stand-in (rank / size only)."""
+
+    @property
+    def rank(self):
+        return world()[0]
+
+    @property
+    def size(self):
+        return world()[1]
+
+    def tompi4py(self):
+        return self
+
+    def barrier(self):
+        ctx = get_ctx()
+        call("kle_ctx_barrier", ctx.h)
+
+
+COMM_WORLD = Comm()
+
+
+class Context:
+    def __init__(self, device=None, rank=None, nranks=None):
+        load()
+        r, n = world()
+        self.rank = r if rank is None else rank
+        self.nranks = n if nranks is None else nranks
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", self.rank if self.nranks > 1 else 0))
+        self.device = device
+        uid = None
+        if self.nranks > 1:
+            uid = self._bcast_unique_id()
+        h = C.c_void_p()
+        call("kle_ctx_create", device, self.rank, self.nranks, uid, C.byref(h))
+        self.h = h
+
+    def _bcast_unique_id(self):
+        d = _dist()
+        if d is None:
+            raise RuntimeError("nranks > 1 needs torch.distributed initialised for the RCCL bootstrap")
+        buf = [None]
+        if self.rank == 0:
+            raw = C.create_string_buffer(128)
+            call("kle_get_unique_id", raw)
+            buf[0] = bytes(raw.raw)
+        d.broadcast_object_list(buf, src=0)
+        return buf[0]
+
+    def synchronize(self):
+        call("kle_ctx_synchronize", self.h)
+
+    def barrier(self):
+        call("kle_ctx_barrier", self.h)
+
+    def set_profiling(self, on=True):
+        call("kle_ctx_set_profiling", self.h, int(bool(on)))
+
+    def kernel_stats(self, name):
+        cnt, ms = C.c_int64(), C.c_double()
+        call("kle_ctx_get_kernel_stats", self.h, name.encode(), C.byref(cnt), C.byref(ms))
+        return cnt.value, ms.value
+
+    def reset_stats(self):
+        call("kle_ctx_reset_kernel_stats", self.h)
+
+    def stream_copy_gbps(self, nbytes=1 << 30, reps=20):
+        g = C.c_double()
+        call("kle_stream_copy_bench", self.h, int(nbytes), int(reps), C.byref(g))
+        return g.value
+
+    def destroy(self):
+        if self.h:
+            call("kle_ctx_destroy", self.h)
+            self.h = None
+
+
+_CTX = None
+
+
+def get_ctx():
+    global _CTX
+    if _CTX is None:
+        _CTX = Context()
+    return _CTX
+
+
+def set_ctx(ctx):
+    global _CTX
+    _CTX = ctx
+
+
+def finalize():
+    global _CTX
+    if _CTX is not None:
+        _CTX.destroy()
+        _CTX = None

@@ -1,0 +1,73 @@
+"""KleSolver / KspSolver: the KLE velocity solve on the device.
+
+Mirror of the reference's solver/kle_solver.py:5-64 (same methods and
+behaviour): ``solve(vort)`` forms b = Rw*vort + Krhs*vel (vel carries the
+Dirichlet values, written beforehand by applyBoundaryConditions) and solves
+K vel = b in place.  The reference's KSP is gmres + PC lu, overridden to
+preonly + lu by the makefile (makefile:7); K is SPD, so the device default is
+CG + Jacobi at rtol 1e-10 (the north-star tolerance), overridable with the
+usual -ksp_type / -pc_type / -ksp_rtol / -ksp_max_it options.  PC 'lu' raises
+(no device direct solver): there is no silent CPU fallback.
+"""
+from .petsc import KSP, PC, Options
+
+DEFAULT_RTOL = 1e-10
+
+
+class KspSolver(KSP):
+    def createSolver(self, mat):
+        self.create()
+        self.setType("cg")
+        pc = PC().create()
+        pc.setType("jacobi")
+        self.setPC(pc)
+        self.setTolerances(rtol=DEFAULT_RTOL, atol=0.0, max_it=100000)
+        self.setFromOptions()
+        self.setOperators(mat)
+        self.setUp()
+
+
+class KleSolver:
+    def __init__(self):
+        self.mat = None
+        self._b = None
+
+    def setMat(self, mat):
+        self.mat = mat
+
+    def setUp(self):
+        K = self.mat.K
+        self.solver = KspSolver()
+        self.solver.createSolver(K)
+        self.__vel = K.createVecRight()
+        self.__vel.setName("velocity")
+        self._b = K.createVecLeft()
+        self._wtmp = K.createVecLeft()
+        self.__isNS = False
+        if self.mat.bcType == "NS":
+            raise NotImplementedError("no-slip KLE solve (solveFS) is the next row of the scope table")
+
+    def isNS(self):
+        return self.__isNS
+
+    def rhs(self, vort, vec=None):
+        """b = Rw * vort + Krhs * vel (kle_solver.py:35) without temporaries."""
+        vel = self.__vel if vec is None else vec
+        self.mat.Rw.mult(vort, self._b)
+        self.mat.Krhs.mult(vel, self._wtmp)
+        self._b.axpy(1.0, self._wtmp)
+        return self._b
+
+    def solve(self, vort, vec=None):
+        vel = self.__vel if vec is None else vec
+        b = self.rhs(vort, vel)
+        self.solver(b, vel)
+
+    def getSolution(self):
+        return self.__vel
+
+    def getKSP(self):
+        return self.solver
+
+    def getFreeSlipSolution(self):
+        raise NotImplementedError("no-slip path not provided yet")

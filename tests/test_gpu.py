@@ -1,0 +1,299 @@
+"""GPU parity tests: libkle.so (HIP, gfx950) against the CPU oracle and the
+golden fixtures produced by the reference's own code.
+
+Tolerances (fp64):
+  * connectivity / patterns: bit-exact
+  * element + assembled matrices: max|diff| <= 1e-12 * max|ref| (different
+    but equivalent fp64 summation orders: factored vs B^T B form)
+  * SpMV: <= 1e-13 relative in the 2-norm
+  * KLE solution vs the reference direct solve: <= 1e-9 relative at
+    rtol 1e-13 (CG stops on ||r|| <= rtol ||b||)
+  * known answers: uniform < 1e-12, Taylor-Green 2-D p=4 < 1e-5
+    (test_solver.py:18-37)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+CASES = ["uniform2d", "tg2d", "tg2d_small", "tg3d", "tg3d_p4"]
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import pynama_amd
+    pynama_amd.load()
+    return pynama_amd
+
+
+def _golden(case):
+    return np.load(os.path.join(G, f"case_{case}.npz"))
+
+
+def _my_index(loc2lat, ngl):
+    """reference local node l -> tensor index of libkle's element order"""
+    idx = np.zeros(len(loc2lat), dtype=np.int64)
+    for d in range(loc2lat.shape[1]):
+        idx += loc2lat[:, d] * ngl ** d
+    return idx
+
+
+def _domain(pa, g):
+    dim = int(g["dim"])
+    cfg = {"domain": {"ngl": int(g["ngl"]), "box-mesh": {"nelem": list(g["nelem"]),
+                                                          "lower": list(g["lower"]), "upper": list(g["upper"])}},
+           "boundary-conditions": {"uniform": {"velocity": [4, 0]}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    dom.mesh.set_dirichlet_nodes(g["dir_nodes"])
+    return dom
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_assembly_matches_golden(pa, case):
+    g = _golden(case)
+    dom = _domain(pa, g)
+    # bit-exact connectivity (reference local order via the golden loc2lat)
+    conn = dom.mesh.conn()
+    np.testing.assert_array_equal(conn[:, _my_index(g["loc2lat"], int(g["ngl"]))], g["conn"])
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    for nm in ("K", "Krhs", "Rw"):
+        ip, ix, d = getattr(mat, nm).getValuesCSR()
+        np.testing.assert_array_equal(ip, g[nm + "_indptr"])
+        np.testing.assert_array_equal(ix, g[nm + "_indices"])
+        ref = g[nm + "_data"]
+        assert np.abs(d - ref).max() <= 1e-12 * np.abs(ref).max(), nm
+
+
+@pytest.mark.parametrize("dim,ngl", [(2, 2), (2, 3), (2, 5), (2, 7), (3, 2), (3, 3), (3, 5)])
+def test_element_kernel_vs_oracle(pa, dim, ngl):
+    import ctypes as C
+    from pynama_amd._lib import call
+    mesh = pa.BoxMesh(dim, [2] * dim, [0.1] * dim, [0.7, 0.5, 0.4][:dim], ngl)
+    ctx = pa.get_ctx()
+    n = ngl ** dim
+    dw = 1 if dim == 2 else 3
+    Ke = np.zeros((dim * n, dim * n))
+    Rwe = np.zeros((dim * n, dw * n))
+    call("kle_element_kle", ctx.h, mesh._h, 1, Ke, Rwe)
+    el = O.Element(ngl, dim)
+    X = mesh.corners()[1]
+    Kr, Rwr, _ = el.kle(X.ravel())
+    # oracle (reference local order) -> tensor order via geometry
+    om = O.BoxMesh(dim, [2] * dim, [0.1] * dim, [0.7, 0.5, 0.4][:dim], ngl)
+    ref_conn = om.conn()[1]
+    my_conn = mesh.conn()[1]
+    perm = np.array([np.where(my_conn == c)[0][0] for c in ref_conn])
+    pv = (perm[:, None] * dim + np.arange(dim)[None, :]).ravel()
+    pw = (perm[:, None] * dw + np.arange(dw)[None, :]).ravel()
+    Kt = np.zeros_like(Kr)
+    Kt[np.ix_(pv, pv)] = Kr
+    Rt = np.zeros_like(Rwr)
+    Rt[np.ix_(pv, pw)] = Rwr
+    assert np.abs(Ke - Kt).max() <= 1e-12 * np.abs(Kt).max()
+    assert np.abs(Rwe - Rt).max() <= 1e-12 * np.abs(Rt).max()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_spmv_and_solve(pa, case):
+    g = _golden(case)
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    K = O.CSR.from_arrays(g["K_indptr"], g["K_indices"], g["K_data"], int(g["K_shape"][1]))
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-1, 1, K.m)
+    xv = mat.K.createVecRight()
+    xv.setArray(x)
+    yv = mat.K * xv
+    y = K.mult(x)
+    assert np.linalg.norm(yv.getArray() - y) <= 1e-13 * np.linalg.norm(y)
+    # KLE solve: b = Rw w + Krhs vel0 ; K u = b
+    sol = pa.KleSolver()
+    sol.setMat(mat)
+    sol.setUp()
+    ksp = sol.getKSP()
+    ksp.setTolerances(rtol=1e-13)
+    vort = mat.Rw.createVecRight()
+    vort.setArray(g["vort0"])
+    vel = sol.getSolution()
+    vel.setArray(g["vel0"])
+    b = sol.rhs(vort)
+    np.testing.assert_allclose(b.getArray(), g["b"], rtol=0, atol=1e-12 * np.abs(g["b"]).max())
+    sol.solve(vort)
+    u = vel.getArray()
+    assert ksp.getConvergedReason() > 0
+    assert ksp.getTrueRelativeResidual() < 1e-12
+    assert np.linalg.norm(u - g["u"]) <= 1e-9 * np.linalg.norm(g["u"])
+    if case == "uniform2d":
+        assert np.linalg.norm(u - g["u_exact"]) < 1e-12  # test_solver.py:25
+    if case == "tg2d":
+        assert np.linalg.norm(u - g["u_exact"]) < 1e-5   # test_solver.py:37
+
+
+@pytest.mark.parametrize("case", ["tg2d", "tg3d_p4"])
+def test_cg_iterations_match_oracle(pa, case):
+    g = _golden(case)
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    K = O.CSR.from_arrays(g["K_indptr"], g["K_indices"], g["K_data"], int(g["K_shape"][1]))
+    xo, it_o, rr_o = K.cg(g["b"], rtol=1e-10, jacobi=True)
+    ksp = pa.petsc.KSP().create()
+    ksp.setType("cg")
+    pc = pa.petsc.PC()
+    pc.setType("jacobi")
+    ksp.setPC(pc)
+    ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+    ksp.setOperators(mat.K)
+    b = mat.K.createVecLeft()
+    b.setArray(g["b"])
+    x = mat.K.createVecRight()
+    ksp.solve(b, x)
+    assert abs(ksp.getIterationNumber() - it_o) <= 1
+    assert ksp.getTrueRelativeResidual() <= 1.01e-10 * 1.5
+    assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
+
+
+def test_gmres_and_aij(pa):
+    g = _golden("tg2d_small")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    A = mat.K.convert("aij")
+    assert A.getFormat() == "aij"
+    ip, ix, d = A.getValuesCSR()
+    np.testing.assert_array_equal(ip, g["K_indptr"])
+    x = mat.K.createVecRight()
+    x.setArray(np.random.default_rng(1).uniform(-1, 1, x.getLocalSize()))
+    xa = A.createVecRight()
+    xa.setArray(x.getArray())
+    np.testing.assert_allclose((A * xa).getArray(), (mat.K * x).getArray(), rtol=1e-13, atol=1e-11)
+    ksp = pa.petsc.KSP().create()
+    ksp.setType("gmres")
+    ksp.setTolerances(rtol=1e-12, max_it=5000)
+    ksp.setOperators(mat.K)
+    b = mat.K.createVecLeft()
+    b.setArray(g["b"])
+    u = mat.K.createVecRight()
+    ksp.solve(b, u)
+    assert ksp.getConvergedReason() > 0
+    assert np.linalg.norm(u.getArray() - g["u"]) <= 1e-9 * np.linalg.norm(g["u"])
+
+
+def test_generic_aij_setvalues(pa):
+    P = pa.petsc
+    n = 7
+    A = P.Mat().createAIJ(((n, None), (n, None)), nnz=([3] * n, None))
+    A.setUp()
+    rng = np.random.default_rng(3)
+    dense = np.zeros((n, n))
+    for _ in range(20):  # ADD_VALUES in call order, explicit zeros kept
+        r = rng.integers(0, n, 2)
+        c = rng.integers(0, n, 2)
+        v = rng.uniform(-1, 1, (2, 2))
+        A.setValues(r, c, v, addv=True)
+        for i in range(2):
+            for j in range(2):
+                dense[r[i], c[j]] += v[i, j]
+    A.setValues([0], [0], [[5.0]], addv=False)
+    dense[0, 0] = 5.0
+    A.assemble()
+    x = P.Vec().createSeq(n)
+    xv = rng.uniform(-1, 1, n)
+    x.setArray(xv)
+    y = A * x
+    np.testing.assert_allclose(y.getArray(), dense @ xv, rtol=1e-14, atol=1e-14)
+    pattern = {(r, c) for r in range(n) for c in range(n)}
+    A_ip, A_ix, _ = A.getValuesCSR()
+    present = {(r, int(c)) for r in range(n) for c in A_ix[A_ip[r]:A_ip[r + 1]]}
+    free = sorted(pattern - present)
+    if free:  # inserting outside the assembled pattern raises (MAT_NEW_NONZERO_ALLOCATION_ERR)
+        with pytest.raises(P.Error):
+            A.setValues([free[0][0]], [free[0][1]], [[1.0]], addv=True)
+
+
+def test_vec_ops(pa):
+    P = pa.petsc
+    rng = np.random.default_rng(5)
+    n = 10001
+    a, b = rng.uniform(-1, 1, n), rng.uniform(-1, 1, n)
+    x = P.Vec().createWithArray(a)
+    y = P.Vec().createWithArray(b)
+    assert abs(x.dot(y) - a @ b) < 1e-12
+    assert abs(x.norm() - np.linalg.norm(a)) < 1e-12
+    z = x + y
+    np.testing.assert_allclose(z.getArray(), a + b, rtol=1e-15)
+    z.axpy(2.0, x)
+    np.testing.assert_allclose(z.getArray(), a + b + 2 * a, rtol=1e-14)
+    z *= 0.5
+    np.testing.assert_allclose(z.getArray(), 0.5 * (3 * a + b), rtol=1e-14)
+    w = x * y
+    np.testing.assert_allclose(w.getArray(), a * b, rtol=1e-15)
+    x.setValues([3, 5], [7.0, 8.0])
+    x.setValues([3], [1.0], addv=True)
+    assert x.getValues([3, 5]).tolist() == [8.0, 8.0]
+    r = P.Vec().createWithArray(np.array([2.0, 0.0, 4.0]))
+    r.reciprocal()
+    assert r.getArray().tolist() == [0.5, 0.0, 0.25]
+
+
+def test_lu_raises(pa):
+    g = _golden("uniform2d")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    ksp = pa.petsc.KSP().create()
+    pc = pa.petsc.PC()
+    pc.setType("lu")
+    ksp.setPC(pc)
+    ksp.setOperators(mat.K)
+    with pytest.raises(pa.Error):
+        ksp.setUp()
+
+
+def test_larger_mesh_properties(pa):
+    """Size-independent properties on a 3-D p=4 mesh (the bench config family):
+    symmetry of K, linearity of SpMV, CG true residual, Dirichlet rows."""
+    cfg = {"domain": {"ngl": 5, "box-mesh": {"nelem": [6, 5, 4], "lower": [0, 0, 0], "upper": [1, 1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    rng = np.random.default_rng(11)
+    x = mat.K.createVecRight()
+    y = mat.K.createVecRight()
+    xa, ya = rng.uniform(-1, 1, x.getLocalSize()), rng.uniform(-1, 1, y.getLocalSize())
+    x.setArray(xa)
+    y.setArray(ya)
+    Ax, Ay = mat.K * x, mat.K * y
+    s = x + y
+    As = mat.K * s
+    np.testing.assert_allclose(As.getArray(), Ax.getArray() + Ay.getArray(), rtol=1e-12, atol=1e-9)
+    assert abs(y.dot(Ax) - x.dot(Ay)) <= 1e-12 * abs(y.dot(Ax)) + 1e-9
+    # Dirichlet rows are identity
+    bn = sorted(dom.getNodesDirichlet())
+    idx = (np.array(bn)[:, None] * 3 + np.arange(3)).ravel()
+    np.testing.assert_array_equal(Ax.getArray()[idx], xa[idx])
+    ksp = pa.petsc.KSP().create()
+    ksp.setTolerances(rtol=1e-10, max_it=20000)
+    ksp.setOperators(mat.K)
+    u = mat.K.createVecRight()
+    ksp.solve(Ax, u)
+    assert ksp.getTrueRelativeResidual() <= 2e-10
+    assert np.linalg.norm(u.getArray() - xa) <= 1e-5 * np.linalg.norm(xa)
