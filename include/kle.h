@@ -88,7 +88,7 @@ int kle_ctx_reset_kernel_stats(kle_ctx *ctx);
 /* Structured box mesh (replaces BoxDom.create + DMPlexDom.setFemIndexing,
  * dmplex.py:31-49,382-388).  Host-only: usable without a GPU.  Node ids are
  * lattice-lexicographic (x fastest); cells x-fastest; element-local nodes in
- * tensor order (kle_mesh_local_order gives the reference spectral order). */
+ * tensor order. */
 int kle_mesh_create_box(int dim, const int64_t nelem[3], const double lower[3],
                         const double upper[3], int ngl, int rank, int nranks, kle_mesh **out);
 int kle_mesh_destroy(kle_mesh *m);
@@ -126,9 +126,10 @@ int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n);
  * row_ptr[n_owned+1] (block offsets, unpadded) and col[] (global node ids). */
 int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks);
 int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *cols);
-/* Halo plan of this rank: ghost node counts below/above and neighbour ranks. */
-int kle_mesh_halo(const kle_mesh *m, int64_t *lo_count, int64_t *hi_count, int *lo_rank,
-                  int *hi_rank);
+/* Halo plan of this rank (node counts): ghosts received from below/above,
+ * owned nodes sent to the lower/upper neighbour, neighbour ranks (-1: none). */
+int kle_mesh_halo(const kle_mesh *m, int64_t *lo_count, int64_t *hi_count, int64_t *send_lo,
+                  int64_t *send_hi, int *lo_rank, int *hi_rank);
 
 /* -------------------------------------------------------------------- vec */
 /* Mesh vector with bs components per node, ghosted over the ext range. */
@@ -191,6 +192,9 @@ int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz);
 int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double *data);
 /* Convert (single rank) to the scalar-CSR device format (the AIJ kernel). */
 int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
+/* SpMV kernel variant of a node-block matrix (tuning): lanes per node row
+ * (64|32|16), block columns per lane in flight (1|2), persistent grid (0|1). */
+int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent);
 /* "nb" (node-block) or "aij". */
 int kle_mat_get_format(const kle_mat *A, char *buf, int buflen);
 /* Bytes one SpMV with this matrix moves (algorithmic: matrix + x + y). */
@@ -217,6 +221,8 @@ int kle_ksp_get_true_relative_residual(const kle_ksp *k, double *rel);
 /* ------------------------------------------------------------ diagnostics */
 /* Streaming read/copy microbenchmark (HBM ceiling for the roofline). */
 int kle_stream_copy_bench(kle_ctx *ctx, int64_t bytes, int reps, double *gbps);
+/* mode 0: copy (read+write bytes counted), 1: read-only (non-temporal). */
+int kle_stream_bench(kle_ctx *ctx, int64_t bytes, int reps, int mode, double *gbps);
 
 #ifdef __cplusplus
 }

@@ -57,8 +57,8 @@ _SIGS = {
     "kle_mesh_set_dirichlet_nodes": [vp, i64p, C.c_int64],
     "kle_mesh_pattern_size": [vp, C.c_int, C.POINTER(C.c_int64)],
     "kle_mesh_pattern": [vp, C.c_int, i64p, vp],
-    "kle_mesh_halo": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int),
-                      C.POINTER(C.c_int)],
+    "kle_mesh_halo": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                      C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "kle_vec_create_mesh": [vp, vp, C.c_int, pvp],
     "kle_vec_create": [vp, C.c_int64, C.c_int64, pvp],
     "kle_vec_duplicate": [vp, pvp],
@@ -99,6 +99,7 @@ _SIGS = {
     "kle_mat_get_csr_size": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "kle_mat_get_csr": [vp, i64p, i64p, f64p],
     "kle_mat_convert_aij": [vp, pvp],
+    "kle_mat_set_spmv_variant": [vp, C.c_int, C.c_int, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],
     "kle_mat_spmv_bytes": [vp, C.POINTER(C.c_double)],
     "kle_ksp_create": [vp, pvp],
@@ -116,6 +117,7 @@ _SIGS = {
     "kle_ksp_get_converged_reason": [vp, C.POINTER(C.c_int)],
     "kle_ksp_get_true_relative_residual": [vp, C.POINTER(C.c_double)],
     "kle_stream_copy_bench": [vp, C.c_int64, C.c_int, C.POINTER(C.c_double)],
+    "kle_stream_bench": [vp, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double)],
 }
 
 _lib = None

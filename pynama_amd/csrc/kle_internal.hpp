@@ -47,7 +47,8 @@ constexpr int WAVE = 64;
 
 // Deterministic two-stage reductions: kernels write one partial per
 // workgroup; a single-workgroup kernel sums them in a fixed order.
-constexpr int RED_BLOCKS = 2048;   // max partial slots per quantity
+constexpr int RED_BLOCKS = 2048;   // max workgroups of the grid-stride vector kernels
+constexpr int PART_STRIDE = 1 << 18;  // partial slots per reduced quantity
 constexpr int NSCAL = 32;          // device scalar slots
 
 // Device scalar slots used by the Krylov kernels.
@@ -75,7 +76,7 @@ struct kle_ctx {
     std::map<std::string, Stat> stats;
     std::vector<hipEvent_t> event_pool;
     // reduction scratch
-    double *d_partials = nullptr;  // [4][RED_BLOCKS]
+    double *d_partials = nullptr;  // [4][PART_STRIDE]
     double *d_scal = nullptr;      // [NSCAL]
     int *d_istate = nullptr;       // [I_COUNT]
     double *h_scal = nullptr;      // pinned mirror
@@ -133,6 +134,7 @@ struct kle_vec {
 struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
+    int spmv_lpr = 64, spmv_unroll = 1, spmv_persistent = 0;  // SpMV kernel variant
     int64_t m_global = 0, n_global = 0, m_local = 0, n_local = 0, row_lo = 0, col_lo = 0;
     // ---- node-block (kind 0)
     int R = 1, C = 1;

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(KB) void k_cg_start(int64_t n, const double *__rest
         s[0] += ri * zi;
         s[1] += ri * ri;
     }
-    block_sums<2>(s, partials, RED_BLOCKS);
+    block_sums<2>(s, partials, PART_STRIDE);
 }
 
 // p = z + beta p,  z = D^-1 r
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(KB) void k_cg_update(int64_t n, const double *__res
         s[0] += ri * zi;
         s[1] += ri * ri;
     }
-    block_sums<2>(s, partials, RED_BLOCKS);
+    block_sums<2>(s, partials, PART_STRIDE);
 }
 
 enum Stage { ST_START = 0, ST_ALPHA = 1, ST_BETA = 2 };
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int q = 0; q < nq; ++q) {
         double s = 0;
-        for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partials[q * RED_BLOCKS + i];
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partials[q * PART_STRIDE + i];
         s = wsum2(s);
         __syncthreads();
         if (lane == 0) lds[w] = s;
@@ -270,6 +270,7 @@ struct kle_ksp {
     std::vector<kle_vec *> V;  // GMRES basis
     double **d_Vptr = nullptr;
     double *d_h = nullptr;
+    double *d_gpart = nullptr;  // GMRES dot partials [restart+2][RED_BLOCKS]
     bool setup = false;
     int its = 0, reason = 0;
     double rnorm = 0, true_rel = -1;
@@ -285,6 +286,8 @@ static void free_work(kle_ksp *k)
     k->V.clear();
     hipFree(k->d_Vptr);
     hipFree(k->d_h);
+    hipFree(k->d_gpart);
+    k->d_gpart = nullptr;
     k->r = k->p = k->q = k->dinv = nullptr;
     k->d_Vptr = nullptr;
     k->d_h = nullptr;
@@ -412,8 +415,8 @@ static int gmres_dots(kle_ksp *k, int kk, const kle_vec *w, double *h)
     const int64_t n = w->n_local;
     const int g = grid_for(n, KB, RED_BLOCKS);
     hipLaunchKernelGGL(k_mdot, dim3(g), dim3(KB), 0, c->stream, n, kk, (const double *const *)k->d_Vptr, w->d,
-                       c->d_partials);
-    hipLaunchKernelGGL(k_reduce_many, dim3(1), dim3(1024), 0, c->stream, c->d_partials, g, kk, k->d_h);
+                       k->d_gpart);
+    hipLaunchKernelGGL(k_reduce_many, dim3(1), dim3(1024), 0, c->stream, k->d_gpart, g, kk, k->d_h);
     KLE_HIP(hipGetLastError());
     if (c->nranks > 1) KLE_NCCL(ncclAllReduce(k->d_h, k->d_h, kk, ncclDouble, ncclSum, c->comm, c->stream));
     KLE_HIP(hipMemcpyAsync(h, k->d_h, sizeof(double) * kk, hipMemcpyDeviceToHost, c->stream));
@@ -619,6 +622,7 @@ int kle_ksp_set_up(kle_ksp *k)
         for (size_t i = 0; i < ptrs.size(); ++i) ptrs[i] = k->V[i]->d;
         KLE_HIP(hipMalloc(&k->d_Vptr, sizeof(double *) * ptrs.size()));
         KLE_HIP(hipMalloc(&k->d_h, sizeof(double) * (k->restart + 2)));
+        KLE_HIP(hipMalloc(&k->d_gpart, sizeof(double) * (k->restart + 2) * RED_BLOCKS));
         KLE_HIP(hipMemcpy(k->d_Vptr, ptrs.data(), sizeof(double *) * ptrs.size(), hipMemcpyHostToDevice));
     }
     KLE_HIP(hipStreamSynchronize(k->ctx->stream));

@@ -42,7 +42,10 @@ __device__ __forceinline__ T ntload(const T *p)
 constexpr int SPMV_BLOCK = 256;
 constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
 
-template <int R, int C, bool DOT>
+// LPR lanes per node row (64: one row per wavefront, 32/16: 2/4 rows per
+// wavefront), UNR block columns per lane issued before the FMAs (memory-level
+// parallelism), persistent: grid-stride over rows with a resident-size grid.
+template <int R, int C, bool DOT, int LPR, int UNR>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int *__restrict__ rowptr,
                                                         const int *__restrict__ bcol,
                                                         const double *__restrict__ val,
@@ -53,37 +56,58 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
                                                         const int *__restrict__ istate)
 {
     if (istate && istate[I_REASON] != 0) return;
+    constexpr int RPW = 64 / LPR;  // rows per wavefront
     const int lane = threadIdx.x & 63;
+    const int sub = lane / LPR, sl = lane % LPR;
     const int64_t wave0 = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
     double dotacc = 0.0;
-    for (int64_t i = wave0; i < nrows; i += nwaves) {
-        const int b0 = rowptr[i];
-        const int m = rowptr[i + 1] - b0;
+    for (int64_t base = wave0 * RPW; base < nrows; base += nwaves * RPW) {
+        const int64_t i = base + sub;
+        int b0 = 0, m = 0;
+        if (i < nrows) {
+            b0 = rowptr[i];
+            m = rowptr[i + 1] - b0;
+        }
         const double *v = val + (int64_t)b0 * (R * C);
         const int *cj = bcol + b0;
         double acc[R];
 #pragma unroll
         for (int a = 0; a < R; ++a) acc[a] = 0.0;
-        for (int k = lane; k < m; k += 64) {
-            const int64_t j = ntload(cj + k);
-            double xv[C];
+        for (int k = sl; k < m; k += LPR * UNR) {
+            int64_t j[UNR];
+            double vv[UNR][R * C];
+            bool on[UNR];
 #pragma unroll
-            for (int b = 0; b < C; ++b) xv[b] = x[j * C + b];
+            for (int u = 0; u < UNR; ++u) {
+                const int ku = k + u * LPR;
+                on[u] = ku < m;
+                j[u] = on[u] ? ntload(cj + ku) : 0;
 #pragma unroll
-            for (int a = 0; a < R; ++a)
+                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ntload(v + (int64_t)t * m + ku) : 0.0;
+            }
 #pragma unroll
-                for (int b = 0; b < C; ++b) acc[a] += ntload(v + (int64_t)(a * C + b) * m + k) * xv[b];
+            for (int u = 0; u < UNR; ++u) {
+                double xv[C];
+#pragma unroll
+                for (int b = 0; b < C; ++b) xv[b] = on[u] ? x[j[u] * C + b] : 0.0;
+#pragma unroll
+                for (int a = 0; a < R; ++a)
+#pragma unroll
+                    for (int b = 0; b < C; ++b) acc[a] += vv[u][a * C + b] * xv[b];
+            }
         }
 #pragma unroll
-        for (int a = 0; a < R; ++a) acc[a] = wsum(acc[a]);
-        if (lane < R) {
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int o = LPR / 2; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+        if (sl < R && i < nrows) {
             double mine = acc[0];
 #pragma unroll
             for (int a = 1; a < R; ++a)
-                if (lane == a) mine = acc[a];
-            y[i * R + lane] = mine;
-            if (DOT) dotacc += mine * pd[i * R + lane];
+                if (sl == a) mine = acc[a];
+            y[i * R + sl] = mine;
+            if (DOT) dotacc += mine * pd[i * R + sl];
         }
     }
     if (DOT) {
@@ -230,29 +254,55 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (c->nranks > 1)
             KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
                                   x->send_lo, x->send_hi));
-        const int grid = grid_for(A->nrows, SPMV_WAVES, RED_BLOCKS);
+        const int rpb = SPMV_WAVES * (64 / A->spmv_lpr);  // rows per workgroup
+        int grid;
+        if (A->spmv_persistent) {
+            int occ = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_nb_spmv<3, 3, true, 64, 1>,
+                                                             SPMV_BLOCK, 0) != hipSuccess || occ < 1)
+                occ = 4;
+            grid = grid_for(A->nrows, rpb, c->num_cus * occ);
+        } else {
+            grid = grid_for(A->nrows, rpb, PART_STRIDE);
+        }
         if (nparts) *nparts = grid;
         const double *pd = dot ? dotvec->d : nullptr;
         KLE_TRY(c->tic("spmv", &ev));
-#define NB_CASE(RR, CC)                                                                             \
-    if (A->R == RR && A->C == CC) {                                                                 \
-        if (dot)                                                                                    \
-            hipLaunchKernelGGL((k_nb_spmv<RR, CC, true>), dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, \
-                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, partials, istate); \
-        else                                                                                        \
-            hipLaunchKernelGGL((k_nb_spmv<RR, CC, false>), dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, \
-                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, partials, istate); \
+#define NB_LAUNCH(RR, CC, LPR, UNR)                                                                     \
+    do {                                                                                                \
+        if (dot)                                                                                        \
+            hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
+                               c->stream, A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, \
+                               partials, istate);                                                       \
+        else                                                                                            \
+            hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR>), dim3(grid), dim3(SPMV_BLOCK), 0,   \
+                               c->stream, A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, \
+                               partials, istate);                                                       \
+    } while (0)
+#define NB_VARIANTS(RR, CC)                                                                             \
+    if (A->spmv_lpr == 64 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 64, 1);                             \
+    else if (A->spmv_lpr == 64) NB_LAUNCH(RR, CC, 64, 2);                                               \
+    else if (A->spmv_lpr == 32 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 32, 1);                        \
+    else if (A->spmv_lpr == 32) NB_LAUNCH(RR, CC, 32, 2);                                               \
+    else if (A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 16, 1);                                             \
+    else NB_LAUNCH(RR, CC, 16, 2);
+#define NB_CASE(RR, CC)                                                                                 \
+    if (A->R == RR && A->C == CC) {                                                                     \
+        if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1);                                                      \
+        else { NB_VARIANTS(RR, CC) }                                                                    \
     } else
         NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
         NB_CASE(3, 6) NB_CASE(1, 1) {
             return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
         }
 #undef NB_CASE
+#undef NB_VARIANTS
+#undef NB_LAUNCH
         KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
     }
-    const int grid = grid_for(A->m_local, SPMV_WAVES, RED_BLOCKS);
+    const int grid = grid_for(A->m_local, SPMV_WAVES, PART_STRIDE);
     if (nparts) *nparts = grid;
     KLE_TRY(c->tic("spmv", &ev));
     if (dot)
@@ -677,6 +727,17 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         }
     }
     *out = B;
+    return 0;
+}
+
+int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent)
+{
+    KLE_ARG(A, "null mat");
+    KLE_ARG(lanes_per_row == 64 || lanes_per_row == 32 || lanes_per_row == 16, "lanes_per_row must be 64/32/16");
+    KLE_ARG(unroll == 1 || unroll == 2, "unroll must be 1 or 2");
+    A->spmv_lpr = lanes_per_row;
+    A->spmv_unroll = unroll;
+    A->spmv_persistent = persistent != 0;
     return 0;
 }
 

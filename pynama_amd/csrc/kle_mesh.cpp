@@ -315,11 +315,14 @@ int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *co
     return 0;
 }
 
-int kle_mesh_halo(const kle_mesh *m, int64_t *lo_count, int64_t *hi_count, int *lo_rank, int *hi_rank)
+int kle_mesh_halo(const kle_mesh *m, int64_t *lo_count, int64_t *hi_count, int64_t *send_lo,
+                  int64_t *send_hi, int *lo_rank, int *hi_rank)
 {
     KLE_ARG(m, "null mesh");
     if (lo_count) *lo_count = m->halo_lo_nodes;
     if (hi_count) *hi_count = m->halo_hi_nodes;
+    if (send_lo) *send_lo = m->send_lo_nodes;
+    if (send_hi) *send_hi = m->send_hi_nodes;
     if (lo_rank) *lo_rank = m->halo_lo_rank;
     if (hi_rank) *hi_rank = m->halo_hi_rank;
     return 0;

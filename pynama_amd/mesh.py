@@ -104,6 +104,9 @@ class BoxMesh:
         return rp, cols[: nb.value]
 
     def halo(self):
-        lo, hi, lr, hr = C.c_int64(), C.c_int64(), C.c_int(), C.c_int()
-        call("kle_mesh_halo", self._h, C.byref(lo), C.byref(hi), C.byref(lr), C.byref(hr))
-        return {"lo_nodes": lo.value, "hi_nodes": hi.value, "lo_rank": lr.value, "hi_rank": hr.value}
+        lo, hi, sl, sh = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        lr, hr = C.c_int(), C.c_int()
+        call("kle_mesh_halo", self._h, C.byref(lo), C.byref(hi), C.byref(sl), C.byref(sh), C.byref(lr),
+             C.byref(hr))
+        return {"lo_nodes": lo.value, "hi_nodes": hi.value, "send_lo_nodes": sl.value,
+                "send_hi_nodes": sh.value, "lo_rank": lr.value, "hi_rank": hr.value}

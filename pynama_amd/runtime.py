@@ -103,7 +103,12 @@ class Context:
 
     def stream_copy_gbps(self, nbytes=1 << 30, reps=20):
         g = C.c_double()
-        call("kle_stream_copy_bench", self.h, int(nbytes), int(reps), C.byref(g))
+        call("kle_stream_bench", self.h, int(nbytes), int(reps), 0, C.byref(g))
+        return g.value
+
+    def stream_read_gbps(self, nbytes=1 << 31, reps=20):
+        g = C.c_double()
+        call("kle_stream_bench", self.h, int(nbytes), int(reps), 1, C.byref(g))
         return g.value
 
     def destroy(self):

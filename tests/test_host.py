@@ -1,0 +1,168 @@
+"""CPU-only tests of libkle's host side: the C ABI exports, the structured
+mesh / numbering / symbolic patterns against the golden fixtures (bit-exact),
+the reference's domain facts, and the slab partition + halo plan."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "tests", "golden")
+CASES = ["uniform2d", "tg2d", "tg2d_small", "tg3d", "tg3d_p4", "cavity2d"]
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import pynama_amd
+    pynama_amd.load()
+    return pynama_amd
+
+
+def test_library_exports_every_header_symbol(pa):
+    hdr = open(os.path.join(ROOT, "include", "kle.h")).read()
+    names = sorted(set(re.findall(r"\b(kle_[a-z0-9_]+)\s*\(", hdr)))
+    assert len(names) > 60
+    lib = C.CDLL(pa._lib.LIBPATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes binding declares all of them
+    bound = set(pa._lib.exported_symbols())
+    assert not (set(names) - bound), sorted(set(names) - bound)
+
+
+def _mesh(pa, g):
+    return pa.BoxMesh(int(g["dim"]), list(g["nelem"]), list(g["lower"]), list(g["upper"]), int(g["ngl"]))
+
+
+def _tensor_index(loc2lat, ngl):
+    idx = np.zeros(len(loc2lat), dtype=np.int64)
+    for d in range(loc2lat.shape[1]):
+        idx += loc2lat[:, d] * ngl ** d
+    return idx
+
+
+def _expand(rp, cols, R, C, dir_rows=None):
+    """node-block pattern -> scalar CSR pattern in PETSc layout"""
+    ip, ix = [0], []
+    for i in range(len(rp) - 1):
+        c = cols[rp[i]:rp[i + 1]]
+        for a in range(R):
+            if dir_rows is not None and dir_rows[i]:
+                ix.append(c[0] * C + a)
+            else:
+                ix.extend((c[:, None] * C + np.arange(C)[None, :]).ravel().tolist())
+            ip.append(len(ix))
+    return np.array(ip), np.array(ix, dtype=np.int64)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_mesh_conn_coords_patterns(pa, case):
+    g = np.load(os.path.join(G, f"case_{case}.npz"))
+    m = _mesh(pa, g)
+    ngl, dim = int(g["ngl"]), int(g["dim"])
+    conn = m.conn()
+    np.testing.assert_array_equal(conn[:, _tensor_index(g["loc2lat"], ngl)], g["conn"])
+    np.testing.assert_allclose(m.coords(), g["coords"], rtol=0, atol=1e-15)
+    np.testing.assert_array_equal(m.corners(), g["corners"])
+    if case == "cavity2d":
+        return  # no-slip sets differ (next row); conn/coords still pinned
+    m.set_dirichlet_nodes(g["dir_nodes"])
+    dirf = np.zeros(m.N, bool)
+    dirf[g["dir_nodes"]] = True
+    dw = 1 if dim == 2 else 3
+    for which, nm, C_ in ((0, "K", dim), (1, "Krhs", dim), (2, "Rw", dw)):
+        rp, cols = m.pattern(which)
+        ip, ix = _expand(rp, cols, dim, C_, dirf if which < 2 else None)
+        np.testing.assert_array_equal(ip, g[nm + "_indptr"])
+        np.testing.assert_array_equal(ix, g[nm + "_indices"])
+
+
+def test_domain_facts_from_reference_tests(pa):
+    # test_domain.py:30-39: 2x2 box, ngl=3 -> 25 nodes, 4 cells
+    m = pa.BoxMesh(2, [2, 2], [0, 0], [1, 1], 3)
+    assert (m.N, m.E) == (25, 4)
+    # test_domain.py:52-62: ngl=7 -> (7*2-1)^2 nodes
+    assert pa.BoxMesh(2, [2, 2], [0, 0], [1, 1], 7).N == 13 * 13
+    # test_domain.py:223-227 / ngl=2: x-fastest lexicographic numbering
+    m = pa.BoxMesh(2, [2, 2], [0, 0], [1, 1], 2)
+    xy = m.coords()
+    np.testing.assert_array_equal(xy[:, 0], np.tile([0, 0.5, 1], 3))
+    np.testing.assert_array_equal(xy[:, 1], np.repeat([0, 0.5, 1], 3))
+    # test_dmplex_wrapper.py:24-27 cell-0 corners (2-D), closure order
+    m = pa.BoxMesh(2, [3, 4], [0, 0], [0.6, 0.8], 3)
+    np.testing.assert_allclose(m.corners()[0].ravel(), [0, 0, 0.2, 0, 0.2, 0.2, 0, 0.2], atol=1e-13)
+    # test_dmplex_wrapper.py:29-47 border node counts (2-D [3,4], ngl=3)
+    assert len(m.face_nodes(["down", "right", "up", "left"])) == 28
+    for b in ("up", "down"):
+        assert len(m.face_nodes([b])) == 7
+    for b in ("left", "right"):
+        assert len(m.face_nodes([b])) == 9
+    # test_dmplex_wrapper.py:100-115 (3-D [3,4,5], ngl=3)
+    m3 = pa.BoxMesh(3, [3, 4, 5], [0, 0, 0], [0.6, 0.8, 1], 3)
+    np.testing.assert_allclose(m3.corners()[0].ravel(),
+                               np.array([[0, 0, 0], [0, .2, 0], [.2, .2, 0], [.2, 0, 0], [0, 0, .2], [.2, 0, .2],
+                                         [.2, .2, .2], [0, .2, .2]]).ravel(), atol=1e-13)
+    assert m3.E == 60
+    assert len(m3.face_nodes(["back", "front", "down", "up", "right", "left"])) == 28 * 11 + 35 * 2
+    # TestNglIndexing2D (test_dmplex_wrapper.py:61-88)
+    for ngl in range(2, 10, 2):
+        if ngl > 8:
+            continue
+        mm = pa.BoxMesh(2, [2, 3], [0, 0], [0.6, 0.8], ngl)
+        assert len(mm.face_nodes(["down", "right", "up", "left"])) == 10 + 10 * (ngl - 2)
+        for b in ("up", "down"):
+            assert len(mm.face_nodes([b])) == 3 + 2 * (ngl - 2)
+        for b in ("left", "right"):
+            assert len(mm.face_nodes([b])) == 4 + 3 * (ngl - 2)
+
+
+def test_bench_config_counts(pa):
+    """Config 2 of BASELINE.json: n = 1,026,675, nnz(K) = 561,335,085."""
+    m = pa.BoxMesh(3, [20, 16, 16], [0, 0, 0], [1, 1, 1], 5)
+    m.set_dirichlet_faces(["back", "front", "down", "up", "right", "left"])
+    assert m.N * 3 == 1026675
+    rp, cols = m.pattern(0)
+    ndir = len(m.face_nodes(["back", "front", "down", "up", "right", "left"]))
+    assert len(cols) * 9 - 6 * ndir == 561335085
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4, 8])
+def test_slab_partition_and_halo_plan(pa, nranks):
+    dims = ([20, 16, 16], 5)
+    ms = [pa.BoxMesh(3, dims[0], [0, 0, 0], [1, 1, 1], dims[1], r, nranks) for r in range(nranks)]
+    for m in ms:
+        m.set_dirichlet_faces(["back", "front", "down", "up", "right", "left"])
+    # owned ranges tile [0, N) in rank order
+    assert ms[0].node_range[0] == 0 and ms[-1].node_range[1] == ms[0].N
+    for a, b in zip(ms, ms[1:]):
+        assert a.node_range[1] == b.node_range[0]
+    serial = pa.BoxMesh(3, dims[0], [0, 0, 0], [1, 1, 1], dims[1])
+    serial.set_dirichlet_faces(["back", "front", "down", "up", "right", "left"])
+    for which in (0, 1, 2):
+        rp_s, cols_s = serial.pattern(which)
+        for m in ms:
+            rp, cols = m.pattern(which)
+            lo, hi = m.node_range
+            # the partitioned rows are exactly the serial rows
+            np.testing.assert_array_equal(cols, cols_s[rp_s[lo]:rp_s[hi]])
+            # every column lies in the ghosted ext range
+            if len(cols):
+                assert cols.min() >= m.ext_range[0] and cols.max() < m.ext_range[1]
+    # halo plan: what r sends down is what r-1 receives from above, and v.v.
+    plane = ms[0].lattice[0] * ms[0].lattice[1]
+    for r in range(nranks):
+        h = ms[r].halo()
+        if r > 0:
+            assert h["lo_rank"] == r - 1
+            assert h["lo_nodes"] == ms[r].node_range[0] - ms[r].ext_range[0]
+            assert ms[r - 1].halo()["hi_nodes"] == plane  # one ghost plane above
+        if r < nranks - 1:
+            assert h["hi_rank"] == r + 1
+    # local elements cover every element touching an owned row
+    for m in ms:
+        lo, hi = m.node_range
+        sconn = serial.conn()
+        need = np.nonzero(((sconn >= lo) & (sconn < hi)).any(1))[0]
+        assert need.min() >= m.elem_range[0] and need.max() < m.elem_range[1]
