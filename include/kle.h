@@ -75,6 +75,21 @@ int kle_get_unique_id(unsigned char out[128]);
 /* device: HIP ordinal; nranks==1 needs no unique id (pass NULL). */
 int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id,
                    kle_ctx **out);
+/* Host-staged transport (testing / debugging): the same distributed code
+ * paths with the collectives delegated to caller callbacks on host buffers
+ * (e.g. gloo), so several ranks can share one GPU.  Production runs use RCCL.
+ *   allreduce: in-place sum of n doubles over all ranks.
+ *   halo: send n_send_lo doubles to lo_rank and n_send_hi to hi_rank, receive
+ *         n_recv_lo from lo_rank and n_recv_hi from hi_rank (ranks < 0: none). */
+typedef struct {
+    int (*allreduce)(double *buf, int n, void *user);
+    int (*halo)(const double *send_lo, int64_t n_send_lo, int lo_rank, const double *send_hi,
+                int64_t n_send_hi, int hi_rank, double *recv_lo, int64_t n_recv_lo,
+                double *recv_hi, int64_t n_recv_hi, void *user);
+    void *user;
+} kle_host_comm;
+int kle_ctx_create_host_comm(int device, int rank, int nranks, const kle_host_comm *comm,
+                             kle_ctx **out);
 int kle_ctx_destroy(kle_ctx *ctx);
 int kle_ctx_synchronize(kle_ctx *ctx);
 int kle_ctx_barrier(kle_ctx *ctx); /* device-side RCCL barrier + stream sync */

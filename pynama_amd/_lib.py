@@ -36,10 +36,20 @@ class MeshInfo(C.Structure):
                 ("elem_end", C.c_int64)]
 
 
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
+HALO_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.c_int, C.POINTER(C.c_double), C.c_int64,
+                      C.c_int, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
+
+
+class HostComm(C.Structure):
+    _fields_ = [("allreduce", ALLREDUCE_FN), ("halo", HALO_FN), ("user", C.c_void_p)]
+
+
 _SIGS = {
     "kle_version": [],
     "kle_get_unique_id": [C.c_char_p],
     "kle_ctx_create": [C.c_int, C.c_int, C.c_int, C.c_char_p, pvp],
+    "kle_ctx_create_host_comm": [C.c_int, C.c_int, C.c_int, C.POINTER(HostComm), pvp],
     "kle_ctx_destroy": [vp],
     "kle_ctx_synchronize": [vp],
     "kle_ctx_barrier": [vp],

@@ -217,6 +217,56 @@ int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64
     return 0;
 }
 
+static int stage_reserve(kle_ctx *ctx, int64_t n)
+{
+    if (ctx->h_stage_n >= n) return 0;
+    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    ctx->h_stage = nullptr;
+    ctx->h_stage_n = 0;
+    KLE_HIP(hipHostMalloc(&ctx->h_stage, sizeof(double) * std::max<int64_t>(n, 64)));
+    ctx->h_stage_n = std::max<int64_t>(n, 64);
+    return 0;
+}
+
+int allreduce_sum(kle_ctx *ctx, double *dbuf, int n)
+{
+    if (ctx->nranks == 1) return 0;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(ctx->tic("allreduce", &ev));
+    if (ctx->comm) {
+        KLE_NCCL(ncclAllReduce(dbuf, dbuf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+    } else {
+        KLE_TRY(stage_reserve(ctx, n));
+        KLE_HIP(hipMemcpyAsync(ctx->h_stage, dbuf, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+        KLE_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->hcomm.allreduce(ctx->h_stage, n, ctx->hcomm.user))
+            return fail(KLE_ERR_COMM, "host allreduce callback failed");
+        KLE_HIP(hipMemcpyAsync(dbuf, ctx->h_stage, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+        KLE_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    KLE_TRY(ctx->toc("allreduce", &ev));
+    return 0;
+}
+
+int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all)
+{
+    // one-hot sum (exact for integers < 2^53)
+    all.assign(ctx->nranks, 0);
+    std::vector<double> h(ctx->nranks, 0.0);
+    h[ctx->rank] = (double)mine;
+    double *d;
+    KLE_HIP(hipMalloc(&d, sizeof(double) * ctx->nranks));
+    KLE_HIP(hipMemcpyAsync(d, h.data(), sizeof(double) * ctx->nranks, hipMemcpyHostToDevice, ctx->stream));
+    int rc = allreduce_sum(ctx, d, ctx->nranks);
+    if (!rc) {
+        KLE_HIP(hipMemcpyAsync(h.data(), d, sizeof(double) * ctx->nranks, hipMemcpyDeviceToHost, ctx->stream));
+        KLE_HIP(hipStreamSynchronize(ctx->stream));
+        for (int r = 0; r < ctx->nranks; ++r) all[r] = (int64_t)h[r];
+    }
+    hipFree(d);
+    return rc;
+}
+
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
                   int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi)
 {
@@ -224,18 +274,36 @@ int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local,
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("halo", &ev));
     double *own = base + ghost_lo;
-    KLE_NCCL(ncclGroupStart());
-    if (lo_rank >= 0) {
-        // my lowest send_lo owned entries are the lower neighbour's upper ghosts
-        KLE_NCCL(ncclSend(own, send_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
-        KLE_NCCL(ncclRecv(base, ghost_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
+    if (ctx->comm) {
+        KLE_NCCL(ncclGroupStart());
+        if (lo_rank >= 0) {
+            // my lowest send_lo owned entries are the lower neighbour's upper ghosts
+            KLE_NCCL(ncclSend(own, send_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
+            KLE_NCCL(ncclRecv(base, ghost_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
+        }
+        if (hi_rank >= 0) {
+            KLE_NCCL(ncclSend(own + n_local - send_hi, send_hi, ncclDouble, hi_rank, ctx->comm,
+                              ctx->stream));
+            KLE_NCCL(ncclRecv(own + n_local, ghost_hi, ncclDouble, hi_rank, ctx->comm, ctx->stream));
+        }
+        KLE_NCCL(ncclGroupEnd());
+    } else {
+        const int64_t sl = lo_rank >= 0 ? send_lo : 0, sh = hi_rank >= 0 ? send_hi : 0;
+        const int64_t rl = lo_rank >= 0 ? ghost_lo : 0, rh = hi_rank >= 0 ? ghost_hi : 0;
+        KLE_TRY(stage_reserve(ctx, sl + sh + rl + rh));
+        double *hs_lo = ctx->h_stage, *hs_hi = hs_lo + sl, *hr_lo = hs_hi + sh, *hr_hi = hr_lo + rl;
+        if (sl) KLE_HIP(hipMemcpyAsync(hs_lo, own, sizeof(double) * sl, hipMemcpyDeviceToHost, ctx->stream));
+        if (sh)
+            KLE_HIP(hipMemcpyAsync(hs_hi, own + n_local - sh, sizeof(double) * sh, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        KLE_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->hcomm.halo(hs_lo, sl, lo_rank, hs_hi, sh, hi_rank, hr_lo, rl, hr_hi, rh, ctx->hcomm.user))
+            return fail(KLE_ERR_COMM, "host halo callback failed");
+        if (rl) KLE_HIP(hipMemcpyAsync(base, hr_lo, sizeof(double) * rl, hipMemcpyHostToDevice, ctx->stream));
+        if (rh)
+            KLE_HIP(hipMemcpyAsync(own + n_local, hr_hi, sizeof(double) * rh, hipMemcpyHostToDevice, ctx->stream));
+        KLE_HIP(hipStreamSynchronize(ctx->stream));
     }
-    if (hi_rank >= 0) {
-        KLE_NCCL(ncclSend(own + n_local - send_hi, send_hi, ncclDouble, hi_rank, ctx->comm,
-                          ctx->stream));
-        KLE_NCCL(ncclRecv(own + n_local, ghost_hi, ncclDouble, hi_rank, ctx->comm, ctx->stream));
-    }
-    KLE_NCCL(ncclGroupEnd());
     KLE_TRY(ctx->toc("halo", &ev));
     return 0;
 }
@@ -310,11 +378,10 @@ int kle_get_unique_id(unsigned char out[128])
     return 0;
 }
 
-int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, kle_ctx **out)
+static int ctx_init(int device, int rank, int nranks, kle_ctx **out)
 {
     KLE_ARG(out, "null output");
     KLE_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank %d / nranks %d", rank, nranks);
-    KLE_ARG(nranks == 1 || unique_id, "nranks > 1 needs an RCCL unique id");
     int ndev = 0;
     KLE_HIP(hipGetDeviceCount(&ndev));
     KLE_ARG(device >= 0 && device < ndev, "device %d not present (%d visible)", device, ndev);
@@ -339,6 +406,15 @@ int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique
     }
     hipMemset(c->d_scal, 0, sizeof(double) * NSCAL);
     hipMemset(c->d_istate, 0, sizeof(int) * I_COUNT);
+    *out = c;
+    return 0;
+}
+
+int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, kle_ctx **out)
+{
+    KLE_ARG(nranks == 1 || unique_id, "nranks > 1 needs an RCCL unique id");
+    kle_ctx *c;
+    KLE_TRY(ctx_init(device, rank, nranks, &c));
     if (nranks > 1) {
         ncclUniqueId id;
         memcpy(&id, unique_id, 128);
@@ -348,6 +424,16 @@ int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique
             return fail(KLE_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
         }
     }
+    *out = c;
+    return 0;
+}
+
+int kle_ctx_create_host_comm(int device, int rank, int nranks, const kle_host_comm *comm, kle_ctx **out)
+{
+    KLE_ARG(comm && comm->allreduce && comm->halo, "host transport needs allreduce and halo callbacks");
+    kle_ctx *c;
+    KLE_TRY(ctx_init(device, rank, nranks, &c));
+    c->hcomm = *comm;
     *out = c;
     return 0;
 }
@@ -365,6 +451,7 @@ int kle_ctx_destroy(kle_ctx *c)
     hipFree(c->d_istate);
     hipHostFree(c->h_scal);
     hipHostFree(c->h_istate);
+    if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -380,11 +467,8 @@ int kle_ctx_synchronize(kle_ctx *c)
 int kle_ctx_barrier(kle_ctx *c)
 {
     KLE_ARG(c, "null ctx");
-    if (c->nranks > 1) {
-        // a one-double allreduce on the stream is the device-side barrier
-        KLE_NCCL(ncclAllReduce(c->d_scal + S_TMP1, c->d_scal + S_TMP1, 1, ncclDouble, ncclSum,
-                               c->comm, c->stream));
-    }
+    // a one-double allreduce on the stream is the device-side barrier
+    KLE_TRY(allreduce_sum(c, c->d_scal + S_TMP1, 1));
     KLE_HIP(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -425,18 +509,8 @@ int kle_vec_create(kle_ctx *ctx, int64_t n_local, int64_t n_global, kle_vec **ou
     int64_t lo = 0;
     if (ctx->nranks > 1) {
         // ownership ranges follow rank order: prefix sum over ranks
-        int64_t *d;
-        KLE_HIP(hipMalloc(&d, sizeof(int64_t)));
-        KLE_HIP(hipMemcpyAsync(d, &n_local, sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
-        std::vector<int64_t> all(ctx->nranks);
-        int64_t *dall;
-        KLE_HIP(hipMalloc(&dall, sizeof(int64_t) * ctx->nranks));
-        KLE_NCCL(ncclAllGather(d, dall, 1, ncclInt64, ctx->comm, ctx->stream));
-        KLE_HIP(hipMemcpyAsync(all.data(), dall, sizeof(int64_t) * ctx->nranks,
-                               hipMemcpyDeviceToHost, ctx->stream));
-        KLE_HIP(hipStreamSynchronize(ctx->stream));
-        hipFree(d);
-        hipFree(dall);
+        std::vector<int64_t> all;
+        KLE_TRY(allgather_i64(ctx, n_local, all));
         int64_t tot = 0;
         for (int r = 0; r < ctx->nranks; ++r) {
             if (r == ctx->rank) lo = tot;
@@ -605,9 +679,7 @@ int kle_vec_dot(const kle_vec *x, const kle_vec *y, double *out)
                        c->d_partials);
     KLE_HIP(hipGetLastError());
     KLE_TRY(reduce_partials(c, c->d_partials, g, 1, c->d_scal + S_TMP0));
-    if (c->nranks > 1)
-        KLE_NCCL(ncclAllReduce(c->d_scal + S_TMP0, c->d_scal + S_TMP0, 1, ncclDouble, ncclSum,
-                               c->comm, c->stream));
+    KLE_TRY(allreduce_sum(c, c->d_scal + S_TMP0, 1));
     KLE_HIP(hipMemcpyAsync(c->h_scal + S_TMP0, c->d_scal + S_TMP0, sizeof(double),
                            hipMemcpyDeviceToHost, c->stream));
     KLE_HIP(hipStreamSynchronize(c->stream));

@@ -67,6 +67,9 @@ struct kle_ctx {
     int device = 0, rank = 0, nranks = 1;
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
+    kle_host_comm hcomm = {};         // host-staged transport (testing), used when comm == nullptr
+    double *h_stage = nullptr;        // pinned staging for the host transport
+    int64_t h_stage_n = 0;
     bool profiling = false;
     struct Stat {
         int64_t count = 0;
@@ -134,7 +137,7 @@ struct kle_vec {
 struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
-    int spmv_lpr = 64, spmv_unroll = 1, spmv_persistent = 0;  // SpMV kernel variant
+    int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
     int64_t m_global = 0, n_global = 0, m_local = 0, n_local = 0, row_lo = 0, col_lo = 0;
     // ---- node-block (kind 0)
     int R = 1, C = 1;
@@ -171,6 +174,8 @@ namespace kle {
 // vec helpers used across translation units
 int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64_t glo,
               int64_t ghi, kle_vec **out);
+int allreduce_sum(kle_ctx *ctx, double *dbuf, int n);  // in place, device buffer
+int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all);
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
                   int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi);
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials,

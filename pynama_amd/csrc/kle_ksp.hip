@@ -308,20 +308,52 @@ static int make_vec_like_cols(kle_ksp *k, kle_vec **out)
     return 0;
 }
 
+// First level of a two-level reduction: 64 workgroups each sum a contiguous
+// chunk of the partials (fixed order) into partials[q*PART_STRIDE + PART2 + g].
+constexpr int PART2_OFF = PART_STRIDE - 128;
+constexpr int PART2_N = 64;
+__global__ __launch_bounds__(1024) void k_reduce_l1(double *__restrict__ partials, int nparts, int nq,
+                                                    const int *__restrict__ ist, int stage)
+{
+    if (stage != ST_START && ist[I_REASON] != 0) return;
+    __shared__ double lds[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int chunk = (nparts + PART2_N - 1) / PART2_N;
+    const int lo = blockIdx.x * chunk, hi = min(nparts, lo + chunk);
+    for (int q = 0; q < nq; ++q) {
+        double s = 0;
+        for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s += partials[q * PART_STRIDE + i];
+        s = wsum2(s);
+        __syncthreads();
+        if (lane == 0) lds[w] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0;
+            for (int i = 0; i < nw; ++i) t += lds[i];
+            partials[q * PART_STRIDE + PART2_OFF + blockIdx.x] = t;
+        }
+    }
+}
+
 static int reduce_stage(kle_ksp *k, int nparts, int nq, int stage)
 {
     kle_ctx *c = k->ctx;
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(c->tic("reduce", &ev));
+    const double *parts = c->d_partials;
+    if (nparts > 4096) {
+        hipLaunchKernelGGL(k_reduce_l1, dim3(PART2_N), dim3(1024), 0, c->stream, c->d_partials, nparts, nq,
+                           c->d_istate, stage);
+        parts = c->d_partials + PART2_OFF;
+        nparts = PART2_N;
+    }
     const int fuse = c->nranks == 1;
-    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, c->stream, c->d_partials, nparts, nq, c->d_scal,
+    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, c->stream, parts, nparts, nq, c->d_scal,
                        c->d_istate, stage, fuse, k->rtol, k->atol);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("reduce", &ev));
     if (!fuse) {
-        KLE_TRY(c->tic("allreduce", &ev));
-        KLE_NCCL(ncclAllReduce(c->d_scal + S_SUM0, c->d_scal + S_SUM0, nq, ncclDouble, ncclSum, c->comm, c->stream));
-        KLE_TRY(c->toc("allreduce", &ev));
+        KLE_TRY(allreduce_sum(c, c->d_scal + S_SUM0, nq));
         hipLaunchKernelGGL(k_scalars, dim3(1), dim3(1), 0, c->stream, c->d_scal, c->d_istate, stage, k->rtol, k->atol);
         KLE_HIP(hipGetLastError());
     }
@@ -418,7 +450,7 @@ static int gmres_dots(kle_ksp *k, int kk, const kle_vec *w, double *h)
                        k->d_gpart);
     hipLaunchKernelGGL(k_reduce_many, dim3(1), dim3(1024), 0, c->stream, k->d_gpart, g, kk, k->d_h);
     KLE_HIP(hipGetLastError());
-    if (c->nranks > 1) KLE_NCCL(ncclAllReduce(k->d_h, k->d_h, kk, ncclDouble, ncclSum, c->comm, c->stream));
+    KLE_TRY(allreduce_sum(c, k->d_h, kk));
     KLE_HIP(hipMemcpyAsync(h, k->d_h, sizeof(double) * kk, hipMemcpyDeviceToHost, c->stream));
     KLE_HIP(hipStreamSynchronize(c->stream));
     return 0;

@@ -263,7 +263,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 occ = 4;
             grid = grid_for(A->nrows, rpb, c->num_cus * occ);
         } else {
-            grid = grid_for(A->nrows, rpb, PART_STRIDE);
+            grid = grid_for(A->nrows, rpb, PART_STRIDE - 256);
         }
         if (nparts) *nparts = grid;
         const double *pd = dot ? dotvec->d : nullptr;
@@ -302,7 +302,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
     }
-    const int grid = grid_for(A->m_local, SPMV_WAVES, PART_STRIDE);
+    const int grid = grid_for(A->m_local, SPMV_WAVES, PART_STRIDE - 256);
     if (nparts) *nparts = grid;
     KLE_TRY(c->tic("spmv", &ev));
     if (dot)

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 import sys
 
-from ._lib import call, load
+from ._lib import ALLREDUCE_FN, HALO_FN, HostComm, call, load
 
 
 def _dist():
@@ -57,20 +57,75 @@ COMM_WORLD = Comm()
 
 
 class Context:
-    def __init__(self, device=None, rank=None, nranks=None):
+    """transport: "rccl" (default, one GPU per rank) or "host" (collectives
+    staged through host memory over torch.distributed/gloo; several ranks may
+    share one GPU -- used to test the distributed path on a single device)."""
+
+    def __init__(self, device=None, rank=None, nranks=None, transport=None):
         load()
         r, n = world()
         self.rank = r if rank is None else rank
         self.nranks = n if nranks is None else nranks
+        self.transport = transport or os.environ.get("KLE_TRANSPORT", "rccl")
         if device is None:
-            device = int(os.environ.get("LOCAL_RANK", self.rank if self.nranks > 1 else 0))
+            default = 0 if self.transport == "host" else (self.rank if self.nranks > 1 else 0)
+            device = int(os.environ.get("KLE_DEVICE", os.environ.get("LOCAL_RANK", default)))
+            if self.transport == "host":
+                device = int(os.environ.get("KLE_DEVICE", 0))
         self.device = device
-        uid = None
-        if self.nranks > 1:
-            uid = self._bcast_unique_id()
         h = C.c_void_p()
-        call("kle_ctx_create", device, self.rank, self.nranks, uid, C.byref(h))
+        if self.nranks > 1 and self.transport == "host":
+            self._hc = self._host_comm()
+            call("kle_ctx_create_host_comm", device, self.rank, self.nranks, C.byref(self._hc), C.byref(h))
+        else:
+            uid = self._bcast_unique_id() if self.nranks > 1 else None
+            call("kle_ctx_create", device, self.rank, self.nranks, uid, C.byref(h))
         self.h = h
+
+    def _host_comm(self):
+        import numpy as np
+        import torch
+        d = _dist()
+        if d is None:
+            raise RuntimeError("host transport needs torch.distributed initialised")
+
+        def allreduce(buf, n, user):
+            try:
+                a = np.ctypeslib.as_array(buf, (n,))
+                t = torch.from_numpy(a.copy())
+                d.all_reduce(t)
+                a[:] = t.numpy()
+                return 0
+            except Exception:
+                return 1
+
+        def halo(s_lo, n_slo, lo_rank, s_hi, n_shi, hi_rank, r_lo, n_rlo, r_hi, n_rhi, user):
+            try:
+                reqs, bufs = [], []
+                if lo_rank >= 0:
+                    if n_slo:
+                        reqs.append(d.isend(torch.from_numpy(np.ctypeslib.as_array(s_lo, (n_slo,)).copy()), lo_rank))
+                    if n_rlo:
+                        t = torch.zeros(n_rlo, dtype=torch.float64)
+                        reqs.append(d.irecv(t, lo_rank))
+                        bufs.append((r_lo, n_rlo, t))
+                if hi_rank >= 0:
+                    if n_shi:
+                        reqs.append(d.isend(torch.from_numpy(np.ctypeslib.as_array(s_hi, (n_shi,)).copy()), hi_rank))
+                    if n_rhi:
+                        t = torch.zeros(n_rhi, dtype=torch.float64)
+                        reqs.append(d.irecv(t, hi_rank))
+                        bufs.append((r_hi, n_rhi, t))
+                for q in reqs:
+                    q.wait()
+                for ptr, n, t in bufs:
+                    np.ctypeslib.as_array(ptr, (n,))[:] = t.numpy()
+                return 0
+            except Exception:
+                return 1
+
+        self._cb = (ALLREDUCE_FN(allreduce), HALO_FN(halo))
+        return HostComm(self._cb[0], self._cb[1], None)
 
     def _bcast_unique_id(self):
         d = _dist()
