@@ -210,6 +210,8 @@ int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
 /* SpMV kernel variant of a node-block matrix (tuning): lanes per node row
  * (64|32|16), block columns per lane in flight (1|2), persistent grid (0|1). */
 int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent);
+/* Row -> workgroup mapping: XCD-contiguous chunks (0|1), (x,y)-tiled row order (0|1). */
+int kle_mat_set_spmv_layout(kle_mat *A, int xcd_chunks, int tiled_order);
 /* "nb" (node-block) or "aij". */
 int kle_mat_get_format(const kle_mat *A, char *buf, int buflen);
 /* Bytes one SpMV with this matrix moves (algorithmic: matrix + x + y). */
@@ -236,7 +238,8 @@ int kle_ksp_get_true_relative_residual(const kle_ksp *k, double *rel);
 /* ------------------------------------------------------------ diagnostics */
 /* Streaming read/copy microbenchmark (HBM ceiling for the roofline). */
 int kle_stream_copy_bench(kle_ctx *ctx, int64_t bytes, int reps, double *gbps);
-/* mode 0: copy (read+write bytes counted), 1: read-only (non-temporal). */
+/* mode 0: copy (read+write bytes counted), 1: read-only 32 B/lane non-temporal,
+ * 2: read-only 8 B/lane non-temporal, 3: read-only 8 B/lane plain. */
 int kle_stream_bench(kle_ctx *ctx, int64_t bytes, int reps, int mode, double *gbps);
 
 #ifdef __cplusplus

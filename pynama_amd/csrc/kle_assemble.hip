@@ -389,6 +389,9 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->n_global = m->N * C;
     A->row_lo = m->node_begin * R;
     A->col_lo = m->node_begin * C;
+    A->row_lat[0] = m->L[0];
+    A->row_lat[1] = m->dim == 3 ? m->L[1] : (m->node_end - m->node_begin) / m->L[0];
+    A->row_lat[2] = m->dim == 3 ? (m->node_end - m->node_begin) / (m->L[0] * m->L[1]) : 1;
     A->lo_rank = m->halo_lo_rank;
     A->hi_rank = m->halo_hi_rank;
     A->ghost_lo = (m->node_begin - m->ext_begin) * C;

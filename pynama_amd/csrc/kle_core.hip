@@ -181,6 +181,17 @@ __global__ void k_stream_read(int64_t n4, const double4 *__restrict__ a4, double
     if (s == 1.2345e-300) out[0] = s;  // keep the loads alive
 }
 
+// 8-byte-per-lane read (the SpMV's access width); nt: non-temporal
+template <bool NT>
+__global__ void k_stream_read8(int64_t n, const double *__restrict__ a, double *__restrict__ out)
+{
+    double s = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        s += NT ? __builtin_nontemporal_load(a + i) : a[i];
+    if (s == 1.2345e-300) out[0] = s;
+}
+
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out)
 {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, ctx->stream, partials, nparts, nq, out);
@@ -793,7 +804,11 @@ int kle_stream_bench(kle_ctx *ctx, int64_t bytes, int reps, int mode, double *gb
     int g = ctx->num_cus * 8;
     auto launch = [&]() {
         if (mode == 0) hipLaunchKernelGGL(k_stream_copy, dim3(g), dim3(256), 0, ctx->stream, n4, a, b);
-        else hipLaunchKernelGGL(k_stream_read, dim3(g), dim3(256), 0, ctx->stream, n4, a, (double *)b);
+        else if (mode == 1) hipLaunchKernelGGL(k_stream_read, dim3(g), dim3(256), 0, ctx->stream, n4, a, (double *)b);
+        else if (mode == 2)
+            hipLaunchKernelGGL(k_stream_read8<true>, dim3(g), dim3(256), 0, ctx->stream, n4 * 4, (const double *)a, (double *)b);
+        else
+            hipLaunchKernelGGL(k_stream_read8<false>, dim3(g), dim3(256), 0, ctx->stream, n4 * 4, (const double *)a, (double *)b);
     };
     launch();
     hipEvent_t e0, e1;

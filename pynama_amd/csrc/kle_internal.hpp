@@ -138,6 +138,10 @@ struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
     int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
+    int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping
+    int spmv_order = 0;        // 0 natural row order, 1 (x,y)-tiled z-columns
+    int *d_order = nullptr;    // processing order of node rows (spmv_order 1)
+    int64_t row_lat[3] = {1, 1, 1};  // lattice of the owned rows (x, y, z extents)
     int64_t m_global = 0, n_global = 0, m_local = 0, n_local = 0, row_lo = 0, col_lo = 0;
     // ---- node-block (kind 0)
     int R = 1, C = 1;

@@ -45,6 +45,10 @@ constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
 // LPR lanes per node row (64: one row per wavefront, 32/16: 2/4 rows per
 // wavefront), UNR block columns per lane issued before the FMAs (memory-level
 // parallelism), persistent: grid-stride over rows with a resident-size grid.
+// xcd: the dispatcher deals workgroups round-robin over the 8 XCDs (b, b+8 on
+// one XCD; MI355X_MICROARCH.md); remapping b -> (b%8)*(G/8) + b/8 gives each
+// XCD one contiguous chunk of the row order, so the x lines a chunk gathers
+// stay in that XCD's L2.  order: optional row permutation (spatially tiled).
 template <int R, int C, bool DOT, int LPR, int UNR>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int *__restrict__ rowptr,
                                                         const int *__restrict__ bcol,
@@ -53,17 +57,19 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
                                                         double *__restrict__ y,
                                                         const double *__restrict__ pd,
                                                         double *__restrict__ partials,
-                                                        const int *__restrict__ istate)
+                                                        const int *__restrict__ istate,
+                                                        const int *__restrict__ order, int xcd)
 {
     if (istate && istate[I_REASON] != 0) return;
     constexpr int RPW = 64 / LPR;  // rows per wavefront
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR, sl = lane % LPR;
-    const int64_t wave0 = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    const int64_t lb = xcd ? (int64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+    const int64_t wave0 = lb * SPMV_WAVES + (threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
     double dotacc = 0.0;
     for (int64_t base = wave0 * RPW; base < nrows; base += nwaves * RPW) {
-        const int64_t i = base + sub;
+        const int64_t i = (order && base + sub < nrows) ? order[base + sub] : base + sub;
         int b0 = 0, m = 0;
         if (i < nrows) {
             b0 = rowptr[i];
@@ -244,6 +250,25 @@ __global__ void k_axpy_same(int64_t n, double a, const double *__restrict__ x, d
         y[i] += a * x[i];
 }
 
+// Row processing order: (x,y) tiles of TX x TY nodes, each swept through all
+// owned z planes, so consecutive workgroups reuse the same x window in L2.
+static int nb_build_order(kle_mat *A)
+{
+    const int64_t LX = A->row_lat[0], LY = A->row_lat[1], LZ = A->row_lat[2];
+    if (LX * LY * LZ != A->nrows) return fail(KLE_ERR_STATE, "row lattice does not match the matrix");
+    const int64_t TX = 16, TY = 8;
+    std::vector<int> ord;
+    ord.reserve(A->nrows);
+    for (int64_t ty = 0; ty < LY; ty += TY)
+        for (int64_t tx = 0; tx < LX; tx += TX)
+            for (int64_t z = 0; z < LZ; ++z)
+                for (int64_t yy = ty; yy < std::min(LY, ty + TY); ++yy)
+                    for (int64_t xx = tx; xx < std::min(LX, tx + TX); ++xx) ord.push_back((int)(xx + LX * (yy + LY * z)));
+    KLE_HIP(hipMalloc(&A->d_order, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
+    KLE_HIP(hipMemcpy(A->d_order, ord.data(), sizeof(int) * A->nrows, hipMemcpyHostToDevice));
+    return 0;
+}
+
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials, int *nparts,
          const int *istate)
 {
@@ -258,13 +283,17 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         int grid;
         if (A->spmv_persistent) {
             int occ = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_nb_spmv<3, 3, true, 64, 1>,
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_nb_spmv<3, 3, true, 64, 2>,
                                                              SPMV_BLOCK, 0) != hipSuccess || occ < 1)
                 occ = 4;
             grid = grid_for(A->nrows, rpb, c->num_cus * occ);
         } else {
             grid = grid_for(A->nrows, rpb, PART_STRIDE - 256);
+            if (A->spmv_xcd) grid = (grid + 7) / 8 * 8;  // whole XCD chunks
         }
+        if (A->spmv_order && !A->d_order) KLE_TRY(nb_build_order(A));
+        const int *order = A->spmv_order ? A->d_order : nullptr;
+        const int xcd = A->spmv_xcd && !A->spmv_persistent;
         if (nparts) *nparts = grid;
         const double *pd = dot ? dotvec->d : nullptr;
         KLE_TRY(c->tic("spmv", &ev));
@@ -273,11 +302,11 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (dot)                                                                                        \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
                                c->stream, A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, \
-                               partials, istate);                                                       \
+                               partials, istate, order, xcd);                                           \
         else                                                                                            \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR>), dim3(grid), dim3(SPMV_BLOCK), 0,   \
                                c->stream, A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, \
-                               partials, istate);                                                       \
+                               partials, istate, order, xcd);                                           \
     } while (0)
 #define NB_VARIANTS(RR, CC)                                                                             \
     if (A->spmv_lpr == 64 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 64, 1);                             \
@@ -469,6 +498,7 @@ int kle_mat_assemble(kle_mat *A)
 int kle_mat_destroy(kle_mat *A)
 {
     if (!A) return 0;
+    hipFree(A->d_order);
     hipFree(A->d_rowptr);
     hipFree(A->d_bcol);
     hipFree(A->d_val);
@@ -704,6 +734,7 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
 {
     KLE_ARG(A && out, "null arg");
     kle_mat *B = new kle_mat(*A);
+    B->d_order = nullptr;
     B->d_rowptr = nullptr;
     B->d_bcol = nullptr;
     B->d_val = nullptr;
@@ -727,6 +758,14 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         }
     }
     *out = B;
+    return 0;
+}
+
+int kle_mat_set_spmv_layout(kle_mat *A, int xcd_chunks, int tiled_order)
+{
+    KLE_ARG(A && A->kind == 0, "node-block matrix expected");
+    A->spmv_xcd = xcd_chunks != 0;
+    A->spmv_order = tiled_order != 0;
     return 0;
 }
 

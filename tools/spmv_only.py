@@ -20,6 +20,8 @@ mat.build()
 K = mat.K
 if len(sys.argv) > 4:
     K.setSpmvVariant(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+if len(sys.argv) > 6:
+    K.setSpmvLayout(int(sys.argv[5]), int(sys.argv[6]))
 x = K.createVecRight()
 x.setArray(np.random.default_rng(0).uniform(-1, 1, x.getLocalSize()))
 y = K.createVecLeft()

@@ -33,8 +33,11 @@ def main():
     out = {"n": K.getSize()[0], "bytes": nbytes, "stream_copy_gbps": ctx.stream_copy_gbps(),
            "stream_read_gbps": ctx.stream_read_gbps(), "variants": []}
     ref = None
-    for lpr, unr, pers in itertools.product((64, 32, 16), (1, 2), (0, 1)):
+    combos = [(64, u, 0, xcd, order) for u in (1, 2) for xcd in (0, 1) for order in (0, 1)]
+    combos += [(64, 2, 1, 0, 0), (32, 2, 0, 1, 1)]
+    for lpr, unr, pers, xcd, order in combos:
         K.setSpmvVariant(lpr, unr, pers)
+        K.setSpmvLayout(xcd, order)
         for _ in range(5):
             K.mult(x, y)
         ctx.synchronize()
@@ -63,7 +66,8 @@ def main():
         ctx.synchronize()
         it_ms = (time.perf_counter() - t) / 50 * 1e3
         avg = ms / c
-        out["variants"].append({"lpr": lpr, "unroll": unr, "persistent": pers, "spmv_ms": avg,
+        out["variants"].append({"lpr": lpr, "unroll": unr, "persistent": pers, "xcd": xcd, "order": order,
+                                "spmv_ms": avg,
                                 "gbps": nbytes / (avg * 1e-3) / 1e9, "cg_iter_ms": it_ms, "maxdiff": err})
         print(json.dumps(out["variants"][-1]), flush=True)
     print(json.dumps(out))
