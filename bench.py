@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--aij", action="store_true", help="also time the scalar-CSR (aij) SpMV")
+    ap.add_argument("--classic-cg", action="store_true",
+                    help="two reductions per iteration instead of the single-reduction (Chronopoulos-Gear) CG")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -104,6 +106,7 @@ def main():
     if not args.no_solve:
         ksp = sol.getKSP()
         ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=200000)
+        ksp.setCGSingleReduction(not args.classic_cg)
         ctx.barrier()
         ts = time.perf_counter()
         sol.solve(vort)
@@ -117,6 +120,7 @@ def main():
     pc = PC()
     pc.setType("jacobi")
     kb.setPC(pc)
+    kb.setCGSingleReduction(not args.classic_cg)
     kb.setOperators(K)
     kb.setUp()
     x = K.createVecRight()
@@ -212,7 +216,8 @@ def main():
             "config": {"workload": f"KLE Laplacian {dim}-D box {nelem} ngl={args.ngl} (p={args.ngl - 1}), "
                                    f"TG-{dim}D Dirichlet on all faces; one CG(+Jacobi) iteration per step",
                        "nelem": nelem, "ngl": args.ngl, "n_dof": n_global, "nnz_K": tot_nnz,
-                       "ksp": "cg", "pc": "jacobi", "matrix_format": info["format"],
+                       "ksp": "cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)",
+                       "pc": "jacobi", "matrix_format": info["format"],
                        "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
@@ -245,14 +250,13 @@ def cpu_baseline(K, b, seconds):
     del ip, ix, d
     bb = b.getArray()
     threads = O.num_threads()
-    # calibrate: 2 iterations, then size the sample to ~seconds
-    t = time.perf_counter()
-    A.cg(bb, fixed_iters=True, maxit=2)
-    per = (time.perf_counter() - t) / 2
-    its = max(3, int(seconds / max(per, 1e-6)))
-    t = time.perf_counter()
-    A.cg(bb, fixed_iters=True, maxit=its)
-    el = time.perf_counter() - t
+    A.cg(bb, fixed_iters=True, maxit=3)  # first touch of the host pages
+    its, el = 0, 0.0
+    while el < seconds:  # bounded sample: chunks of 10 iterations until ~seconds
+        t = time.perf_counter()
+        A.cg(bb, fixed_iters=True, maxit=10)
+        el += time.perf_counter() - t
+        its += 10
     return {"value": its / el, "unit": "CG iters/s", "cores": threads, "kind": "port",
             "sample": f"{its} fixed CG+Jacobi iterations of oracle/kle_oracle.c (CSR, OpenMP) on the same "
                       f"assembled K ({A.nnz} nnz), {el:.1f} s"}

@@ -224,6 +224,9 @@ int kle_ksp_set_type(kle_ksp *k, const char *type);      /* "cg" | "gmres" | "pr
 int kle_ksp_set_pc_type(kle_ksp *k, const char *type);   /* "none" | "jacobi" | "lu"   */
 int kle_ksp_set_tolerances(kle_ksp *k, double rtol, double atol, double dtol, int maxit);
 int kle_ksp_set_gmres_restart(kle_ksp *k, int restart);
+/* CG with one reduction per iteration (Chronopoulos-Gear), as PETSc's
+ * -ksp_cg_single_reduction. */
+int kle_ksp_set_cg_single_reduction(kle_ksp *k, int flag);
 /* Run exactly n iterations, no convergence test (benchmarks); 0 = off. */
 int kle_ksp_set_fixed_iterations(kle_ksp *k, int n);
 int kle_ksp_set_operators(kle_ksp *k, kle_mat *A);

@@ -109,10 +109,104 @@ __global__ __launch_bounds__(KB) void k_cg_update(int64_t n, const double *__res
     block_sums<2>(s, partials, PART_STRIDE);
 }
 
-enum Stage { ST_START = 0, ST_ALPHA = 1, ST_BETA = 2 };
+// x = 0, r = b, u = M r, p = s = 0 ; partials: [0] r.u, [1] r.r
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_sr_start(int64_t n, const double *__restrict__ b,
+                                                 const double *__restrict__ dinv, double *__restrict__ x,
+                                                 double *__restrict__ r, double *__restrict__ u, double *__restrict__ p,
+                                                 double *__restrict__ sv, double *__restrict__ partials)
+{
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double ri = b[i];
+        const double ui = JAC ? dinv[i] * ri : ri;
+        x[i] = 0.0;
+        r[i] = ri;
+        u[i] = ui;
+        p[i] = 0.0;
+        sv[i] = 0.0;
+        acc[0] += ri * ui;
+        acc[1] += ri * ri;
+    }
+    block_sums<2>(acc, partials, PART_STRIDE);
+}
+
+// p = u + beta p ; s = w + beta s ; x += alpha p ; r -= alpha s ; u = M r
+// partials: [0] r.u, [1] r.r   (one pass over 7 inputs, 5 outputs)
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_sr_update(int64_t n, const double *__restrict__ dinv,
+                                                  const double *__restrict__ w, double *__restrict__ u,
+                                                  double *__restrict__ p, double *__restrict__ sv,
+                                                  double *__restrict__ x, double *__restrict__ r,
+                                                  double *__restrict__ partials, const double *__restrict__ scal,
+                                                  const int *__restrict__ ist)
+{
+    if (ist[I_REASON] != 0) return;
+    const double alpha = scal[S_ALPHA], beta = scal[S_BETA];
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double pi = u[i] + beta * p[i];
+        const double si = w[i] + beta * sv[i];
+        p[i] = pi;
+        sv[i] = si;
+        x[i] += alpha * pi;
+        const double ri = r[i] - alpha * si;
+        r[i] = ri;
+        const double ui = JAC ? dinv[i] * ri : ri;
+        u[i] = ui;
+        acc[0] += ri * ui;
+        acc[1] += ri * ri;
+    }
+    block_sums<2>(acc, partials, PART_STRIDE);
+}
+
+enum Stage { ST_START = 0, ST_ALPHA = 1, ST_BETA = 2, ST_SR_START = 3, ST_SR = 4 };
 
 __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, double atol)
 {
+    if (stage == ST_SR_START || stage == ST_SR) {
+        // Chronopoulos-Gear single-reduction CG: sums = (r,u), (r,r), (w,u)
+        const double g = scal[S_SUM0], rr = scal[S_SUM1], d = scal[S_SUM2];
+        const double rn = sqrt(rr);
+        scal[S_RR] = rr;
+        if (stage == ST_SR_START) {
+            scal[S_BNORM] = rn;
+            scal[S_TOL] = fmax(rtol * rn, atol);
+            ist[I_ITS] = 0;
+            ist[I_REASON] = 0;
+            scal[S_BETA] = 0.0;
+            scal[S_RHO] = g;
+            scal[S_ALPHA] = g / d;
+            if (!ist[I_FIXED] && rn <= scal[S_TOL]) ist[I_REASON] = rn <= atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+            else if (!isfinite(rn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
+            else if (d <= 0.0 && !ist[I_FIXED]) ist[I_REASON] = -8;
+            return;
+        }
+        if (ist[I_REASON] != 0) return;
+        const int its = ++ist[I_ITS];
+        if (ist[I_FIXED]) {
+            if (its >= ist[I_FIXED]) ist[I_REASON] = KLE_CONVERGED_ITS;
+        } else if (!isfinite(rn)) {
+            ist[I_REASON] = KLE_DIVERGED_NANORINF;
+            return;
+        } else if (rn <= scal[S_TOL]) {
+            ist[I_REASON] = rn <= atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+            return;
+        } else if (its >= ist[I_MAXIT]) {
+            ist[I_REASON] = KLE_DIVERGED_ITS;
+            return;
+        }
+        const double beta = g / scal[S_RHO];
+        const double den = d - beta * g / scal[S_ALPHA];
+        if (den <= 0.0 && !ist[I_FIXED]) {
+            ist[I_REASON] = -8;
+            return;
+        }
+        scal[S_BETA] = beta;
+        scal[S_ALPHA] = g / den;
+        scal[S_RHO] = g;
+        return;
+    }
     if (stage == ST_START) {
         const double rz = scal[S_SUM0], rr = scal[S_SUM1];
         const double bn = sqrt(rr);
@@ -161,15 +255,20 @@ __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, doubl
 
 // Sum nq partial arrays (fixed order) into scal[S_SUM0..]; optionally apply
 // the stage's scalar update in the same launch (single rank).
-__global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict__ partials, int nparts, int nq,
+struct NParts {
+    int n[4];
+};
+
+__global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict__ partials, NParts np, int nq,
                                                        double *__restrict__ scal, int *__restrict__ ist, int stage,
                                                        int fuse, double rtol, double atol)
 {
-    if (stage != ST_START && ist[I_REASON] != 0) return;
+    if (stage != ST_START && stage != ST_SR_START && ist[I_REASON] != 0) return;
     __shared__ double lds[16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int q = 0; q < nq; ++q) {
         double s = 0;
+        const int nparts = np.n[q];
         for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partials[q * PART_STRIDE + i];
         s = wsum2(s);
         __syncthreads();
@@ -267,6 +366,8 @@ struct kle_ksp {
     int maxit = 10000, restart = 30, fixed = 0, check_every = 8;
     kle_mat *A = nullptr;
     kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
+    kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
+    int single_reduction = 0;
     std::vector<kle_vec *> V;  // GMRES basis
     double **d_Vptr = nullptr;
     double *d_h = nullptr;
@@ -282,6 +383,10 @@ static void free_work(kle_ksp *k)
     kle_vec_destroy(k->p);
     kle_vec_destroy(k->q);
     kle_vec_destroy(k->dinv);
+    kle_vec_destroy(k->u);
+    kle_vec_destroy(k->w);
+    kle_vec_destroy(k->s);
+    k->u = k->w = k->s = nullptr;
     for (auto v : k->V) kle_vec_destroy(v);
     k->V.clear();
     hipFree(k->d_Vptr);
@@ -312,15 +417,16 @@ static int make_vec_like_cols(kle_ksp *k, kle_vec **out)
 // chunk of the partials (fixed order) into partials[q*PART_STRIDE + PART2 + g].
 constexpr int PART2_OFF = PART_STRIDE - 128;
 constexpr int PART2_N = 64;
-__global__ __launch_bounds__(1024) void k_reduce_l1(double *__restrict__ partials, int nparts, int nq,
+__global__ __launch_bounds__(1024) void k_reduce_l1(double *__restrict__ partials, NParts np, int nq,
                                                     const int *__restrict__ ist, int stage)
 {
-    if (stage != ST_START && ist[I_REASON] != 0) return;
+    if (stage != ST_START && stage != ST_SR_START && ist[I_REASON] != 0) return;
     __shared__ double lds[16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int chunk = (nparts + PART2_N - 1) / PART2_N;
-    const int lo = blockIdx.x * chunk, hi = min(nparts, lo + chunk);
     for (int q = 0; q < nq; ++q) {
+        const int nparts = np.n[q];
+        const int chunk = (nparts + PART2_N - 1) / PART2_N;
+        const int lo = blockIdx.x * chunk, hi = min(nparts, lo + chunk);
         double s = 0;
         for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s += partials[q * PART_STRIDE + i];
         s = wsum2(s);
@@ -335,20 +441,23 @@ __global__ __launch_bounds__(1024) void k_reduce_l1(double *__restrict__ partial
     }
 }
 
-static int reduce_stage(kle_ksp *k, int nparts, int nq, int stage)
+static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage)
 {
     kle_ctx *c = k->ctx;
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(c->tic("reduce", &ev));
     const double *parts = c->d_partials;
-    if (nparts > 4096) {
-        hipLaunchKernelGGL(k_reduce_l1, dim3(PART2_N), dim3(1024), 0, c->stream, c->d_partials, nparts, nq,
+    int big = 0;
+    for (int q = 0; q < nq; ++q) big |= np.n[q] > 4096;
+    if (big) {
+        // first level per quantity (small quantities just copy through)
+        hipLaunchKernelGGL(k_reduce_l1, dim3(PART2_N), dim3(1024), 0, c->stream, c->d_partials, np, nq,
                            c->d_istate, stage);
         parts = c->d_partials + PART2_OFF;
-        nparts = PART2_N;
+        for (int q = 0; q < nq; ++q) np.n[q] = PART2_N;
     }
     const int fuse = c->nranks == 1;
-    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, c->stream, parts, nparts, nq, c->d_scal,
+    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, c->stream, parts, np, nq, c->d_scal,
                        c->d_istate, stage, fuse, k->rtol, k->atol);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("reduce", &ev));
@@ -401,7 +510,7 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
         hipLaunchKernelGGL(k_cg_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->p->d,
                            c->d_partials);
     KLE_HIP(hipGetLastError());
-    KLE_TRY(reduce_stage(k, g, 2, ST_START));
+    KLE_TRY(reduce_stage(k, NParts{{g, g, 0, 0}}, 2, ST_START));
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
     for (int it = 0; it < limit; ++it) {
@@ -416,7 +525,7 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
         KLE_TRY(c->toc("p_update", &ev));
         int np = 0;
         KLE_TRY(spmv(k->A, k->p, k->q, k->p, c->d_partials, &np, c->d_istate));
-        KLE_TRY(reduce_stage(k, np, 1, ST_ALPHA));
+        KLE_TRY(reduce_stage(k, NParts{{np, 0, 0, 0}}, 1, ST_ALPHA));
         KLE_TRY(c->tic("cg_update", &ev));
         if (jac)
             hipLaunchKernelGGL(k_cg_update<true>, dim3(g), dim3(KB), 0, c->stream, n, k->p->d, k->q->d, dinv, x->d,
@@ -426,7 +535,56 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
                                k->r->d, c->d_partials, c->d_scal, c->d_istate);
         KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("cg_update", &ev));
-        KLE_TRY(reduce_stage(k, g, 2, ST_BETA));
+        KLE_TRY(reduce_stage(k, NParts{{g, g, 0, 0}}, 2, ST_BETA));
+        if (!k->fixed && ((it + 1) % k->check_every == 0)) {
+            KLE_TRY(poll_state(k));
+            if (c->h_istate[I_REASON] != 0) break;
+        }
+    }
+    KLE_TRY(poll_state(k));
+    k->its = c->h_istate[I_ITS];
+    k->reason = c->h_istate[I_REASON];
+    if (k->reason == 0) k->reason = KLE_DIVERGED_ITS;
+    k->rnorm = std::sqrt(c->h_scal[S_RR]);
+    return 0;
+}
+
+// Chronopoulos-Gear CG (PETSc -ksp_cg_single_reduction): one fused update
+// kernel + one SpMV (with fused (w,u)) + one reduction (three sums) per
+// iteration -> one allreduce per iteration across ranks.
+static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    kle_ctx *c = k->ctx;
+    const int64_t n = b->n_local;
+    const bool jac = k->pc == "jacobi";
+    const double *dinv = jac ? k->dinv->d : nullptr;
+    const int g = grid_for(n, KB, RED_BLOCKS);
+    int host_fixed[I_COUNT] = {0, 0, k->fixed, k->fixed ? k->fixed : k->maxit, 0, 0, 0, 0};
+    KLE_HIP(hipMemcpyAsync(c->d_istate, host_fixed, sizeof(int) * I_COUNT, hipMemcpyHostToDevice, c->stream));
+    if (jac)
+        hipLaunchKernelGGL(k_sr_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
+                           k->p->d, k->s->d, c->d_partials);
+    else
+        hipLaunchKernelGGL(k_sr_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
+                           k->p->d, k->s->d, c->d_partials);
+    KLE_HIP(hipGetLastError());
+    int np = 0;
+    KLE_TRY(spmv(k->A, k->u, k->w, k->u, c->d_partials + 2 * PART_STRIDE, &np, nullptr));
+    KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR_START));
+    const int limit = k->fixed ? k->fixed : k->maxit;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    for (int it = 0; it < limit; ++it) {
+        KLE_TRY(c->tic("cg_update", &ev));
+        if (jac)
+            hipLaunchKernelGGL(k_sr_update<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d, k->p->d,
+                               k->s->d, x->d, k->r->d, c->d_partials, c->d_scal, c->d_istate);
+        else
+            hipLaunchKernelGGL(k_sr_update<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d, k->p->d,
+                               k->s->d, x->d, k->r->d, c->d_partials, c->d_scal, c->d_istate);
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(c->toc("cg_update", &ev));
+        KLE_TRY(spmv(k->A, k->u, k->w, k->u, c->d_partials + 2 * PART_STRIDE, &np, c->d_istate));
+        KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR));
         if (!k->fixed && ((it + 1) % k->check_every == 0)) {
             KLE_TRY(poll_state(k));
             if (c->h_istate[I_REASON] != 0) break;
@@ -612,6 +770,14 @@ int kle_ksp_set_gmres_restart(kle_ksp *k, int restart)
     return 0;
 }
 
+int kle_ksp_set_cg_single_reduction(kle_ksp *k, int flag)
+{
+    KLE_ARG(k, "null ksp");
+    k->single_reduction = flag != 0;
+    k->setup = false;
+    return 0;
+}
+
 int kle_ksp_set_fixed_iterations(kle_ksp *k, int n)
 {
     KLE_ARG(k && n >= 0, "bad arg");
@@ -640,6 +806,11 @@ int kle_ksp_set_up(kle_ksp *k)
     KLE_TRY(make_vec_like_cols(k, &k->r));
     KLE_TRY(make_vec_like_cols(k, &k->p));
     KLE_TRY(make_vec_like_cols(k, &k->q));
+    if (k->type == "cg" && k->single_reduction) {
+        KLE_TRY(make_vec_like_cols(k, &k->u));
+        KLE_TRY(make_vec_like_cols(k, &k->w));
+        KLE_TRY(make_vec_like_cols(k, &k->s));
+    }
     if (k->pc == "jacobi") {
         KLE_TRY(make_vec_like_cols(k, &k->dinv));
         KLE_TRY(kle_mat_get_diagonal(k->A, k->q));
@@ -668,7 +839,8 @@ int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(kle_ksp_set_up(k));
     KLE_ARG(b->n_local == k->A->m_local && x->n_local == k->A->n_local, "b/x sizes do not match the operator");
     k->true_rel = -1;
-    if (k->type == "cg") KLE_TRY(solve_cg(k, b, x));
+    if (k->type == "cg" && k->single_reduction) KLE_TRY(solve_cg_single(k, b, x));
+    else if (k->type == "cg") KLE_TRY(solve_cg(k, b, x));
     else KLE_TRY(solve_gmres(k, b, x));
     if (!k->fixed) KLE_TRY(true_residual(k, b, x));
     return 0;

@@ -525,6 +525,10 @@ class KSP:
         self._ensure()
         call("kle_ksp_set_fixed_iterations", self._h, int(n))
 
+    def setCGSingleReduction(self, flag=True):
+        self._ensure()
+        call("kle_ksp_set_cg_single_reduction", self._h, int(bool(flag)))
+
     def setGMRESRestart(self, m):
         self._ensure()
         call("kle_ksp_set_gmres_restart", self._h, int(m))
@@ -540,6 +544,8 @@ class KSP:
             self.setPC(pc)
         self.setTolerances(o.getReal("ksp_rtol"), o.getReal("ksp_atol"), o.getReal("ksp_divtol"),
                            o.getInt("ksp_max_it"))
+        if "ksp_cg_single_reduction" in o:
+            self.setCGSingleReduction(o.getBool("ksp_cg_single_reduction", True))
         if "ksp_gmres_restart" in o:
             self.setGMRESRestart(o.getInt("ksp_gmres_restart"))
 

@@ -140,8 +140,9 @@ def test_spmv_and_solve(pa, case):
         assert np.linalg.norm(u - g["u_exact"]) < 1e-5   # test_solver.py:37
 
 
+@pytest.mark.parametrize("single", [False, True])
 @pytest.mark.parametrize("case", ["tg2d", "tg3d_p4"])
-def test_cg_iterations_match_oracle(pa, case):
+def test_cg_iterations_match_oracle(pa, case, single):
     g = _golden(case)
     dom = _domain(pa, g)
     mat = pa.MatFS()
@@ -155,12 +156,13 @@ def test_cg_iterations_match_oracle(pa, case):
     pc.setType("jacobi")
     ksp.setPC(pc)
     ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+    ksp.setCGSingleReduction(single)  # Chronopoulos-Gear: same iterates in exact arithmetic
     ksp.setOperators(mat.K)
     b = mat.K.createVecLeft()
     b.setArray(g["b"])
     x = mat.K.createVecRight()
     ksp.solve(b, x)
-    assert abs(ksp.getIterationNumber() - it_o) <= 1
+    assert abs(ksp.getIterationNumber() - it_o) <= (2 if single else 1)
     assert ksp.getTrueRelativeResidual() <= 1.01e-10 * 1.5
     assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
 
