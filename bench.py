@@ -159,7 +159,7 @@ def main():
         spmv_avg_max = spmv_avg_ms
     if "torch" in sys.modules:  # torch is only the launcher's plumbing here
         import torch
-        if torch.cuda.is_available():
+        if torch.cuda.is_initialized():  # never create a torch context just to sync it
             torch.cuda.synchronize()
 
     iters_per_s = args.steps / t_max
