@@ -210,6 +210,10 @@ int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
 /* SpMV kernel variant of a node-block matrix (tuning): lanes per node row
  * (64|32|16), block columns per lane in flight (1|2), persistent grid (0|1). */
 int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent);
+/* Buffer-descriptor SpMV variants (cache-policy study): 0 off, 1 aux 0, 2 nt,
+ * 3 sc0|nt, 4 sc1, 5 sc1|nt, 6 sc1|sc0|nt, 7 sc1|sc0, 8 nt with the x gather
+ * dropped (timing diagnostic only: wrong results). */
+int kle_mat_set_spmv_buffer_variant(kle_mat *A, int variant);
 /* Row -> workgroup mapping: XCD-contiguous chunks (0|1), (x,y)-tiled row order (0|1). */
 int kle_mat_set_spmv_layout(kle_mat *A, int xcd_chunks, int tiled_order);
 /* "nb" (node-block) or "aij". */

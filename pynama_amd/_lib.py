@@ -111,6 +111,7 @@ _SIGS = {
     "kle_mat_convert_aij": [vp, pvp],
     "kle_mat_set_spmv_variant": [vp, C.c_int, C.c_int, C.c_int],
     "kle_mat_set_spmv_layout": [vp, C.c_int, C.c_int],
+    "kle_mat_set_spmv_buffer_variant": [vp, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],
     "kle_mat_spmv_bytes": [vp, C.POINTER(C.c_double)],
     "kle_ksp_create": [vp, pvp],

@@ -139,6 +139,7 @@ struct kle_mat {
     int kind = 0;  // 0 node-block, 1 scalar AIJ
     int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
     int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping
+    int spmv_buf = 0;          // buffer-load variant (0 off; cache-policy experiments)
     int spmv_order = 0;        // 0 natural row order, 1 (x,y)-tiled z-columns
     int *d_order = nullptr;    // processing order of node rows (spmv_order 1)
     int64_t row_lat[3] = {1, 1, 1};  // lattice of the owned rows (x, y, z extents)

@@ -129,6 +129,87 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
     }
 }
 
+// Buffer-load variant of the node-block SpMV (one row per wavefront, two
+// block columns per lane in flight): the matrix streams go through a per-row
+// buffer descriptor so the cache-policy bits (aux: bit0 sc0, bit1 nt,
+// bit4 sc1) can be chosen; XDROP=1 prices the x gather (descriptor with 0
+// records: the gathers return 0 -- wrong y, timing diagnostic only).
+template <int R, int C, bool DOT, int AUX, bool XDROP>
+__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_buf(int64_t nrows, const int *__restrict__ rowptr,
+                                                            const int *__restrict__ bcol,
+                                                            const double *__restrict__ val,
+                                                            const double *__restrict__ x, int64_t xbytes,
+                                                            double *__restrict__ y,
+                                                            const double *__restrict__ pd,
+                                                            double *__restrict__ partials,
+                                                            const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    double dotacc = 0.0;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, XDROP ? 0 : (int)min(xbytes, (int64_t)0x7fffffff), 0x00020000);
+    if (i < nrows) {
+        const int b0 = __builtin_amdgcn_readfirstlane(rowptr[i]);
+        const int m = __builtin_amdgcn_readfirstlane(rowptr[i + 1]) - b0;
+        const __amdgpu_buffer_rsrc_t vr =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(val + (int64_t)b0 * (R * C)), 0, m * R * C * 8, 0x00020000);
+        const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc((void *)(bcol + b0), 0, m * 4, 0x00020000);
+        double acc[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[a] = 0.0;
+        for (int k = lane; k < m; k += 128) {
+            int j[2];
+            double vv[2][R * C];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int ku = k + 64 * u;  // out-of-range offsets read 0 (bounds-checked descriptor)
+                j[u] = __builtin_amdgcn_raw_buffer_load_b32(cr, ku * 4, 0, AUX);
+#pragma unroll
+                for (int t = 0; t < R * C; ++t) {
+                    vv[u][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vr, (t * m + ku) * 8, 0, AUX));
+                }
+                if (ku >= m) {
+#pragma unroll
+                    for (int t = 0; t < R * C; ++t) vv[u][t] = 0.0;
+                    j[u] = 0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int b = 0; b < C; ++b) {
+                    const double xv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (j[u] * C + b) * 8, 0, 0));
+#pragma unroll
+                    for (int a = 0; a < R; ++a) acc[a] += vv[u][a * C + b] * xv;
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[a] = wsum(acc[a]);
+        if (lane < R) {
+            double mine = acc[0];
+#pragma unroll
+            for (int a = 1; a < R; ++a)
+                if (lane == a) mine = acc[a];
+            y[i * R + lane] = mine;
+            if (DOT) dotacc += mine * pd[i * R + lane];
+        }
+    }
+    if (DOT) {
+        __shared__ double lds[SPMV_WAVES];
+        dotacc = wsum(dotacc);
+        if (lane == 0) lds[threadIdx.x >> 6] = dotacc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = 0;
+            for (int w = 0; w < SPMV_WAVES; ++w) s += lds[w];
+            partials[blockIdx.x] = s;
+        }
+    }
+}
+
 template <bool DOT>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_aij_spmv(int64_t nrows, const int64_t *__restrict__ ptr,
                                                          const int *__restrict__ col,
@@ -290,6 +371,41 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         } else {
             grid = grid_for(A->nrows, rpb, PART_STRIDE - 256);
             if (A->spmv_xcd) grid = (grid + 7) / 8 * 8;  // whole XCD chunks
+        }
+        if (A->spmv_buf && A->R == 3 && A->C == 3 && A->spmv_lpr == 64 && !A->spmv_persistent && !A->spmv_order &&
+            !A->spmv_xcd) {
+            const int64_t xbytes = (int64_t)(x->ghost_lo + x->n_local + x->ghost_hi) * 8;
+            const int g2 = (int)((A->nrows + SPMV_WAVES - 1) / SPMV_WAVES);
+            if (g2 > PART_STRIDE - 256) return fail(KLE_ERR_SUP, "buffer SpMV variant: matrix too large");
+            if (nparts) *nparts = g2;
+            const double *pd = dot ? dotvec->d : nullptr;
+            KLE_TRY(c->tic("spmv", &ev));
+#define BUF_LAUNCH(AUXV, XD)                                                                              \
+    do {                                                                                                  \
+        if (dot)                                                                                          \
+            hipLaunchKernelGGL((k_nb_spmv_buf<3, 3, true, AUXV, XD>), dim3(g2), dim3(SPMV_BLOCK), 0, c->stream, \
+                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
+                               istate);                                                                   \
+        else                                                                                              \
+            hipLaunchKernelGGL((k_nb_spmv_buf<3, 3, false, AUXV, XD>), dim3(g2), dim3(SPMV_BLOCK), 0, c->stream, \
+                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
+                               istate);                                                                   \
+    } while (0)
+            switch (A->spmv_buf) {
+            case 1: BUF_LAUNCH(0, false); break;
+            case 2: BUF_LAUNCH(2, false); break;
+            case 3: BUF_LAUNCH(3, false); break;
+            case 4: BUF_LAUNCH(16, false); break;
+            case 5: BUF_LAUNCH(18, false); break;
+            case 6: BUF_LAUNCH(19, false); break;
+            case 7: BUF_LAUNCH(17, false); break;
+            case 8: BUF_LAUNCH(2, true); break;
+            default: return fail(KLE_ERR_ARG, "unknown buffer SpMV variant %d", A->spmv_buf);
+            }
+#undef BUF_LAUNCH
+            KLE_HIP(hipGetLastError());
+            KLE_TRY(c->toc("spmv", &ev));
+            return 0;
         }
         if (A->spmv_order && !A->d_order) KLE_TRY(nb_build_order(A));
         const int *order = A->spmv_order ? A->d_order : nullptr;
@@ -758,6 +874,13 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         }
     }
     *out = B;
+    return 0;
+}
+
+int kle_mat_set_spmv_buffer_variant(kle_mat *A, int variant)
+{
+    KLE_ARG(A && A->kind == 0 && variant >= 0 && variant <= 8, "bad buffer variant");
+    A->spmv_buf = variant;
     return 0;
 }
 

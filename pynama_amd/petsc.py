@@ -373,6 +373,9 @@ class Mat:
     def setSpmvVariant(self, lanes_per_row=64, unroll=1, persistent=False):
         call("kle_mat_set_spmv_variant", self._h, int(lanes_per_row), int(unroll), int(bool(persistent)))
 
+    def setSpmvBufferVariant(self, v):
+        call("kle_mat_set_spmv_buffer_variant", self._h, int(v))
+
     def setSpmvLayout(self, xcd_chunks=False, tiled_order=False):
         call("kle_mat_set_spmv_layout", self._h, int(bool(xcd_chunks)), int(bool(tiled_order)))
 
