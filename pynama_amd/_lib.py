@@ -112,6 +112,8 @@ _SIGS = {
     "kle_mat_set_spmv_variant": [vp, C.c_int, C.c_int, C.c_int],
     "kle_mat_set_spmv_layout": [vp, C.c_int, C.c_int],
     "kle_mat_set_spmv_buffer_variant": [vp, C.c_int],
+    "kle_set_nb_pad": [C.c_int],
+    "kle_mat_set_spmv_nontemporal": [vp, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],
     "kle_mat_spmv_bytes": [vp, C.POINTER(C.c_double)],
     "kle_ksp_create": [vp, pvp],

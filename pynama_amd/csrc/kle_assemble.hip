@@ -281,7 +281,7 @@ struct MeshDev {
 // MODE 0: K (free cols, +K_e), 1: Krhs (Dirichlet cols, -K_e), 2: Rw (+Rw_e)
 template <int R, int C, int MODE>
 __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const int *__restrict__ rowptr,
-                                                const int *__restrict__ bcol,
+                                                const int *__restrict__ rowcnt, const int *__restrict__ bcol,
                                                 const uint8_t *__restrict__ dir,
                                                 const double *__restrict__ Eblk, double *__restrict__ val)
 {
@@ -289,13 +289,13 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
     const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (row >= nrows) return;
     const int64_t gi = M.node_begin + row;
-    const int b0 = rowptr[row], m = rowptr[row + 1] - b0;
+    const int b0 = rowptr[row], mp = rowptr[row + 1] - b0, m = rowcnt ? rowcnt[row] : mp;
     double *v = val + (int64_t)b0 * R * C;
     if (dir[gi - M.ext_begin]) {
         // K[dir,dir] = 0 + ... + 0 + 1 and Krhs[dir,dir] = 1 (mat_fs.py:115-120,182-183)
         if (MODE != 2 && lane == 0 && m == 1)
             for (int a = 0; a < R; ++a)
-                for (int b = 0; b < C; ++b) v[a * C + b] = (a == b) ? 1.0 : 0.0;
+                for (int b = 0; b < C; ++b) v[(a * C + b) * (int64_t)mp] = (a == b) ? 1.0 : 0.0;
         return;
     }
     int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], M.dim == 3 ? gi / (M.L[0] * M.L[1]) : 0};
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
 #pragma unroll
         for (int a = 0; a < R; ++a)
 #pragma unroll
-            for (int b = 0; b < C; ++b) v[(a * C + b) * (int64_t)m + k] = acc[a * C + b];
+            for (int b = 0; b < C; ++b) v[(a * C + b) * (int64_t)mp + k] = acc[a * C + b];
     }
 }
 
@@ -370,16 +370,28 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     if (nb >= (1ll << 31) / 1) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
     std::vector<int64_t> cols(std::max<int64_t>(nb, 1));
     KLE_TRY(kle_mesh_pattern(m, which, rp.data(), cols.data()));
-    std::vector<int> rp32(nrows + 1), c32(std::max<int64_t>(nb, 1));
-    for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
-    for (int64_t k = 0; k < nb; ++k) c32[k] = (int)(cols[k] - m->ext_begin);
+    const int pad = std::max(1, g_nb_pad);
+    std::vector<int> rp32(nrows + 1), cnt(nrows);
+    int64_t nbp = 0;
+    for (int64_t i = 0; i < nrows; ++i) {
+        cnt[i] = (int)(rp[i + 1] - rp[i]);
+        rp32[i] = (int)nbp;
+        nbp += (cnt[i] + pad - 1) / pad * pad;
+    }
+    rp32[nrows] = (int)nbp;
+    if (nbp >= (1ll << 31)) return fail(KLE_ERR_SUP, "padded pattern too large for int32 block offsets");
+    std::vector<int> c32(std::max<int64_t>(nbp, 1), 0);
+    for (int64_t i = 0; i < nrows; ++i)
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) c32[rp32[i] + (k - rp[i])] = (int)(cols[k] - m->ext_begin);
     kle_mat *A = new kle_mat;
     A->ctx = ctx;
     A->kind = 0;
     A->R = R;
     A->C = C;
     A->nrows = nrows;
-    A->nblocks = nb;
+    A->nblocks = nbp;
+    A->nblocks_real = nb;
+    A->pad = pad;
     A->node_begin = m->node_begin;
     A->ext_begin = m->ext_begin;
     A->ext_nodes = m->ext_end - m->ext_begin;
@@ -402,15 +414,20 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     if (which != 2)
         for (int64_t i = 0; i < nrows; ++i) A->diag_only_row[i] = m->dir[m->node_begin + i - m->ext_begin];
     if (hipMalloc(&A->d_rowptr, sizeof(int) * (nrows + 1)) != hipSuccess ||
-        hipMalloc(&A->d_bcol, sizeof(int) * std::max<int64_t>(nb, 1)) != hipSuccess ||
-        hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nb * R * C, 1)) != hipSuccess) {
+        (pad > 1 && hipMalloc(&A->d_rowcnt, sizeof(int) * std::max<int64_t>(nrows, 1)) != hipSuccess) ||
+        hipMalloc(&A->d_bcol, sizeof(int) * std::max<int64_t>(nbp, 1)) != hipSuccess ||
+        hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nbp * R * C, 1)) != hipSuccess) {
         kle_mat_destroy(A);
         return fail(KLE_ERR_MEM, "out of device memory for a %lld-block matrix", (long long)nb);
     }
     KLE_HIP(hipMemcpyAsync(A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1), hipMemcpyHostToDevice,
                            ctx->stream));
-    KLE_HIP(hipMemcpyAsync(A->d_bcol, c32.data(), sizeof(int) * std::max<int64_t>(nb, 1),
+    KLE_HIP(hipMemcpyAsync(A->d_bcol, c32.data(), sizeof(int) * std::max<int64_t>(nbp, 1),
                            hipMemcpyHostToDevice, ctx->stream));
+    if (A->d_rowcnt)
+        KLE_HIP(hipMemcpyAsync(A->d_rowcnt, cnt.data(), sizeof(int) * std::max<int64_t>(nrows, 1), hipMemcpyHostToDevice,
+                               ctx->stream));
+    if (pad > 1) KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(nbp * R * C, 1), ctx->stream));
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     *out = A;
     return 0;
@@ -491,7 +508,7 @@ static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint
 {
     const int64_t threads = A->nrows * 64;
     hipLaunchKernelGGL((k_gather<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
-                       A->nrows, A->d_rowptr, A->d_bcol, dir, E, A->d_val);
+                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, dir, E, A->d_val);
 }
 
 }  // namespace kle

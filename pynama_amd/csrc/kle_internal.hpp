@@ -138,6 +138,7 @@ struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
     int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
+    int spmv_nt = 0;  // non-temporal value/column loads (plain loads fetch fewer bytes: profiles/r01)
     int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping
     int spmv_buf = 0;          // buffer-load variant (0 off; cache-policy experiments)
     int spmv_order = 0;        // 0 natural row order, 1 (x,y)-tiled z-columns
@@ -149,7 +150,10 @@ struct kle_mat {
     int64_t nrows = 0;         // owned node rows
     int64_t nblocks = 0;
     int64_t node_begin = 0, ext_begin = 0, ext_nodes = 0;
-    int *d_rowptr = nullptr;   // [nrows+1] block offsets
+    int *d_rowptr = nullptr;   // [nrows+1] block offsets (rows padded to `pad` blocks)
+    int *d_rowcnt = nullptr;   // [nrows] real block count per row (null when pad == 1)
+    int64_t nblocks_real = 0;
+    int pad = 1;
     int *d_bcol = nullptr;     // [nblocks] local ext node index
     double *d_val = nullptr;   // [nblocks*R*C], per row SoA [a][b][k]
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
@@ -187,4 +191,5 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
          int *nparts, const int *istate);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
+extern int g_nb_pad;  // row padding quantum (blocks) of new node-block matrices
 }  // namespace kle

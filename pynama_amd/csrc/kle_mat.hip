@@ -26,6 +26,8 @@
 
 namespace kle {
 
+int g_nb_pad = 1;
+
 __device__ __forceinline__ double wsum(double v)
 {
 #pragma unroll
@@ -39,6 +41,13 @@ __device__ __forceinline__ T ntload(const T *p)
     return __builtin_nontemporal_load(p);
 }
 
+template <bool NT, class T>
+__device__ __forceinline__ T ldv(const T *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
 constexpr int SPMV_BLOCK = 256;
 constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
 
@@ -49,8 +58,9 @@ constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
 // one XCD; MI355X_MICROARCH.md); remapping b -> (b%8)*(G/8) + b/8 gives each
 // XCD one contiguous chunk of the row order, so the x lines a chunk gathers
 // stay in that XCD's L2.  order: optional row permutation (spatially tiled).
-template <int R, int C, bool DOT, int LPR, int UNR>
+template <int R, int C, bool DOT, int LPR, int UNR, bool NT>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int *__restrict__ rowptr,
+                                                        const int *__restrict__ rowcnt,
                                                         const int *__restrict__ bcol,
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x,
@@ -70,10 +80,11 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
     double dotacc = 0.0;
     for (int64_t base = wave0 * RPW; base < nrows; base += nwaves * RPW) {
         const int64_t i = (order && base + sub < nrows) ? order[base + sub] : base + sub;
-        int b0 = 0, m = 0;
+        int b0 = 0, m = 0, mp = 0;
         if (i < nrows) {
             b0 = rowptr[i];
-            m = rowptr[i + 1] - b0;
+            mp = rowptr[i + 1] - b0;
+            m = rowcnt ? rowcnt[i] : mp;
         }
         const double *v = val + (int64_t)b0 * (R * C);
         const int *cj = bcol + b0;
@@ -88,9 +99,9 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
             for (int u = 0; u < UNR; ++u) {
                 const int ku = k + u * LPR;
                 on[u] = ku < m;
-                j[u] = on[u] ? ntload(cj + ku) : 0;
+                j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
 #pragma unroll
-                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ntload(v + (int64_t)t * m + ku) : 0.0;
+                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + (int64_t)t * mp + ku) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
@@ -136,6 +147,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
 // records: the gathers return 0 -- wrong y, timing diagnostic only).
 template <int R, int C, bool DOT, int AUX, bool XDROP>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_buf(int64_t nrows, const int *__restrict__ rowptr,
+                                                            const int *__restrict__ rowcnt,
                                                             const int *__restrict__ bcol,
                                                             const double *__restrict__ val,
                                                             const double *__restrict__ x, int64_t xbytes,
@@ -152,9 +164,10 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_buf(int64_t nrows, const
         __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, XDROP ? 0 : (int)min(xbytes, (int64_t)0x7fffffff), 0x00020000);
     if (i < nrows) {
         const int b0 = __builtin_amdgcn_readfirstlane(rowptr[i]);
-        const int m = __builtin_amdgcn_readfirstlane(rowptr[i + 1]) - b0;
+        const int mp = __builtin_amdgcn_readfirstlane(rowptr[i + 1]) - b0;
+        const int m = rowcnt ? __builtin_amdgcn_readfirstlane(rowcnt[i]) : mp;
         const __amdgpu_buffer_rsrc_t vr =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(val + (int64_t)b0 * (R * C)), 0, m * R * C * 8, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void *)(val + (int64_t)b0 * (R * C)), 0, mp * R * C * 8, 0x00020000);
         const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc((void *)(bcol + b0), 0, m * 4, 0x00020000);
         double acc[R];
 #pragma unroll
@@ -168,7 +181,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_buf(int64_t nrows, const
                 j[u] = __builtin_amdgcn_raw_buffer_load_b32(cr, ku * 4, 0, AUX);
 #pragma unroll
                 for (int t = 0; t < R * C; ++t) {
-                    vv[u][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vr, (t * m + ku) * 8, 0, AUX));
+                    vv[u][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vr, (t * mp + ku) * 8, 0, AUX));
                 }
                 if (ku >= m) {
 #pragma unroll
@@ -249,11 +262,11 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_aij_spmv(int64_t nrows, const in
 
 // diagonal position of each node row (for Jacobi / get_diagonal)
 __global__ void k_diagpos(int64_t nrows, int64_t row_off, const int *__restrict__ rowptr,
-                          const int *__restrict__ bcol, int *__restrict__ pos)
+                          const int *__restrict__ rowcnt, const int *__restrict__ bcol, int *__restrict__ pos)
 {
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= nrows) return;
-    int lo = rowptr[i], hi = rowptr[i + 1] - 1, want = (int)(i + row_off), found = -1;
+    int lo = rowptr[i], hi = lo + (rowcnt ? rowcnt[i] : rowptr[i + 1] - lo) - 1, want = (int)(i + row_off), found = -1;
     while (lo <= hi) {
         int mid = (lo + hi) >> 1;
         int c = bcol[mid];
@@ -268,14 +281,14 @@ __global__ void k_diagpos(int64_t nrows, int64_t row_off, const int *__restrict_
 }
 
 template <int R, int C>
-__global__ void k_nb_scale(int64_t nrows, const int *__restrict__ rowptr, const int *__restrict__ bcol,
-                           double *__restrict__ val, const double *__restrict__ L,
+__global__ void k_nb_scale(int64_t nrows, const int *__restrict__ rowptr, const int *__restrict__ rowcnt,
+                           const int *__restrict__ bcol, double *__restrict__ val, const double *__restrict__ L,
                            const double *__restrict__ Rx)
 {
     const int lane = threadIdx.x & 63;
     const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (i >= nrows) return;
-    const int b0 = rowptr[i], m = rowptr[i + 1] - b0;
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
     double *v = val + (int64_t)b0 * R * C;
     for (int k = lane; k < m; k += 64) {
         const int64_t j = bcol[b0 + k];
@@ -284,7 +297,7 @@ __global__ void k_nb_scale(int64_t nrows, const int *__restrict__ rowptr, const 
                 double s = 1.0;
                 if (L) s *= L[i * R + a];
                 if (Rx) s *= Rx[j * C + b];
-                v[(int64_t)(a * C + b) * m + k] *= s;
+                v[(int64_t)(a * C + b) * mp + k] *= s;
             }
     }
 }
@@ -296,8 +309,8 @@ __global__ void k_nb_diag(int64_t nrows, int R, int C, const int *__restrict__ r
     if (t >= nrows * R) return;
     int64_t i = t / R;
     int a = (int)(t % R);
-    const int b0 = rowptr[i], m = rowptr[i + 1] - b0;
-    d[t] = pos[i] < 0 ? 0.0 : val[(int64_t)b0 * R * C + (int64_t)(a * C + a) * m + pos[i]];
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0;
+    d[t] = pos[i] < 0 ? 0.0 : val[(int64_t)b0 * R * C + (int64_t)(a * C + a) * mp + pos[i]];
 }
 
 __global__ void k_aij_scale(int64_t nrows, const int64_t *__restrict__ ptr, const int *__restrict__ col,
@@ -364,7 +377,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         int grid;
         if (A->spmv_persistent) {
             int occ = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_nb_spmv<3, 3, true, 64, 2>,
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_nb_spmv<3, 3, true, 64, 2, false>,
                                                              SPMV_BLOCK, 0) != hipSuccess || occ < 1)
                 occ = 4;
             grid = grid_for(A->nrows, rpb, c->num_cus * occ);
@@ -384,11 +397,11 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
     do {                                                                                                  \
         if (dot)                                                                                          \
             hipLaunchKernelGGL((k_nb_spmv_buf<3, 3, true, AUXV, XD>), dim3(g2), dim3(SPMV_BLOCK), 0, c->stream, \
-                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
+                               A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
                                istate);                                                                   \
         else                                                                                              \
             hipLaunchKernelGGL((k_nb_spmv_buf<3, 3, false, AUXV, XD>), dim3(g2), dim3(SPMV_BLOCK), 0, c->stream, \
-                               A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
+                               A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
                                istate);                                                                   \
     } while (0)
             switch (A->spmv_buf) {
@@ -413,27 +426,29 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (nparts) *nparts = grid;
         const double *pd = dot ? dotvec->d : nullptr;
         KLE_TRY(c->tic("spmv", &ev));
-#define NB_LAUNCH(RR, CC, LPR, UNR)                                                                     \
+#define NB_LAUNCH(RR, CC, LPR, UNR, NT)                                                                   \
     do {                                                                                                \
         if (dot)                                                                                        \
-            hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
-                               c->stream, A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, \
-                               partials, istate, order, xcd);                                           \
+            hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
+                               c->stream, A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, \
+                               y->d, pd, partials, istate, order, xcd);                                 \
         else                                                                                            \
-            hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR>), dim3(grid), dim3(SPMV_BLOCK), 0,   \
-                               c->stream, A->nrows, A->d_rowptr, A->d_bcol, A->d_val, x->base, y->d, pd, \
-                               partials, istate, order, xcd);                                           \
+            hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0, \
+                               c->stream, A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, \
+                               y->d, pd, partials, istate, order, xcd);                                 \
     } while (0)
 #define NB_VARIANTS(RR, CC)                                                                             \
-    if (A->spmv_lpr == 64 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 64, 1);                             \
-    else if (A->spmv_lpr == 64) NB_LAUNCH(RR, CC, 64, 2);                                               \
-    else if (A->spmv_lpr == 32 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 32, 1);                        \
-    else if (A->spmv_lpr == 32) NB_LAUNCH(RR, CC, 32, 2);                                               \
-    else if (A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 16, 1);                                             \
-    else NB_LAUNCH(RR, CC, 16, 2);
+    if (A->spmv_lpr == 64 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 1, true);         \
+    else if (A->spmv_lpr == 64 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 64, 1, false);                 \
+    else if (A->spmv_lpr == 64 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 2, true);                           \
+    else if (A->spmv_lpr == 64) NB_LAUNCH(RR, CC, 64, 2, false);                                        \
+    else if (A->spmv_lpr == 32 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 32, 1, false);                 \
+    else if (A->spmv_lpr == 32) NB_LAUNCH(RR, CC, 32, 2, false);                                        \
+    else if (A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 16, 1, false);                                      \
+    else NB_LAUNCH(RR, CC, 16, 2, false);
 #define NB_CASE(RR, CC)                                                                                 \
     if (A->R == RR && A->C == CC) {                                                                     \
-        if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1);                                                      \
+        if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1, false);                                                      \
         else { NB_VARIANTS(RR, CC) }                                                                    \
     } else
         NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
@@ -479,7 +494,7 @@ static int check_mult_layout(const kle_mat *A, const kle_vec *x, const kle_vec *
 
 // host copy of an nb matrix
 struct NBHost {
-    std::vector<int> rp, bc;
+    std::vector<int> rp, bc, cnt;
     std::vector<double> v;
 };
 
@@ -491,6 +506,10 @@ static int nb_download(const kle_mat *A, NBHost &h)
     KLE_HIP(hipMemcpy(h.rp.data(), A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToHost));
     KLE_HIP(hipMemcpy(h.bc.data(), A->d_bcol, sizeof(int) * h.bc.size(), hipMemcpyDeviceToHost));
     KLE_HIP(hipMemcpy(h.v.data(), A->d_val, sizeof(double) * h.v.size(), hipMemcpyDeviceToHost));
+    h.cnt.resize(A->nrows);
+    if (A->d_rowcnt) KLE_HIP(hipMemcpy(h.cnt.data(), A->d_rowcnt, sizeof(int) * A->nrows, hipMemcpyDeviceToHost));
+    else
+        for (int64_t i = 0; i < A->nrows; ++i) h.cnt[i] = h.rp[i + 1] - h.rp[i];
     return 0;
 }
 
@@ -615,6 +634,7 @@ int kle_mat_destroy(kle_mat *A)
 {
     if (!A) return 0;
     hipFree(A->d_order);
+    hipFree(A->d_rowcnt);
     hipFree(A->d_rowptr);
     hipFree(A->d_bcol);
     hipFree(A->d_val);
@@ -692,7 +712,7 @@ int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *Rv)
 #define SC_CASE(RR, CC)                                                                                    \
     if (A->R == RR && A->C == CC)                                                                          \
         hipLaunchKernelGGL((k_nb_scale<RR, CC>), dim3((th + 255) / 256), dim3(256), 0, c->stream, A->nrows, \
-                           A->d_rowptr, A->d_bcol, A->d_val, L ? L->d : nullptr, rx);                      \
+                           A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, L ? L->d : nullptr, rx);         \
     else
         SC_CASE(3, 3) SC_CASE(2, 2) SC_CASE(2, 1) SC_CASE(1, 2) SC_CASE(3, 1) SC_CASE(1, 3) SC_CASE(6, 3)
         SC_CASE(3, 6) SC_CASE(1, 1) return fail(KLE_ERR_SUP, "no scale kernel for %dx%d", A->R, A->C);
@@ -719,7 +739,7 @@ int kle_mat_get_diagonal(const kle_mat *A, kle_vec *d)
         int *pos;
         KLE_HIP(hipMalloc(&pos, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
         hipLaunchKernelGGL(k_diagpos, dim3((A->nrows + 255) / 256), dim3(256), 0, c->stream, A->nrows,
-                           A->node_begin - A->ext_begin, A->d_rowptr, A->d_bcol, pos);
+                           A->node_begin - A->ext_begin, A->d_rowptr, A->d_rowcnt, A->d_bcol, pos);
         hipLaunchKernelGGL(k_nb_diag, dim3((A->nrows * A->R + 255) / 256), dim3(256), 0, c->stream, A->nrows, A->R,
                            A->C, A->d_rowptr, pos, A->d_val, d->d);
         KLE_HIP(hipGetLastError());
@@ -742,11 +762,14 @@ int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz)
         *nnz = A->assembled ? A->nnz : 0;
         return 0;
     }
-    std::vector<int> rp(A->nrows + 1);
+    std::vector<int> rp(A->nrows + 1), cnt(A->nrows);
     KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToHost));
+    if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * A->nrows, hipMemcpyDeviceToHost));
+    else
+        for (int64_t i = 0; i < A->nrows; ++i) cnt[i] = rp[i + 1] - rp[i];
     int64_t z = 0;
     for (int64_t i = 0; i < A->nrows; ++i)
-        z += A->diag_only_row[i] ? std::min(A->R, A->C) : (int64_t)(rp[i + 1] - rp[i]) * A->R * A->C;
+        z += A->diag_only_row[i] ? std::min(A->R, A->C) : (int64_t)cnt[i] * A->R * A->C;
     *nnz = z;
     return 0;
 }
@@ -766,20 +789,20 @@ int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double 
     int64_t z = 0;
     indptr[0] = 0;
     for (int64_t i = 0; i < A->nrows; ++i) {
-        const int b0 = h.rp[i], m = h.rp[i + 1] - b0;
+        const int b0 = h.rp[i], mp = h.rp[i + 1] - b0, m = h.cnt[i];
         const double *v = h.v.data() + (int64_t)b0 * R * C;
         for (int a = 0; a < R; ++a) {
             if (A->diag_only_row[i]) {
                 // Dirichlet row: PETSc stores the diagonal only (mat_fs.py:44-45,115-120)
                 if (a < C) {
                     indices[z] = (A->node_begin + i) * C + a;
-                    data[z++] = v[(a * C + a) * (int64_t)m + 0];
+                    data[z++] = v[(a * C + a) * (int64_t)mp + 0];
                 }
             } else {
                 for (int k = 0; k < m; ++k)
                     for (int b = 0; b < C; ++b) {
                         indices[z] = (A->ext_begin + h.bc[b0 + k]) * C + b;
-                        data[z++] = v[(int64_t)(a * C + b) * m + k];
+                        data[z++] = v[(int64_t)(a * C + b) * mp + k];
                     }
             }
             indptr[i * R + a + 1] = z;
@@ -819,7 +842,7 @@ int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X)
         NBHost hy, hx;
         KLE_TRY(nb_download(Y, hy));
         KLE_TRY(nb_download(X, hx));
-        if (hy.rp != hx.rp || hy.bc != hx.bc) return fail(KLE_ERR_SUP, "axpy needs the same pattern");
+        if (hy.rp != hx.rp || hy.bc != hx.bc || hy.cnt != hx.cnt) return fail(KLE_ERR_SUP, "axpy needs the same pattern");
         const int64_t n = Y->nblocks * Y->R * Y->C;
         hipLaunchKernelGGL(k_axpy_same, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, n, a, X->d_val, Y->d_val);
         KLE_HIP(hipGetLastError());
@@ -851,6 +874,7 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     KLE_ARG(A && out, "null arg");
     kle_mat *B = new kle_mat(*A);
     B->d_order = nullptr;
+    B->d_rowcnt = nullptr;
     B->d_rowptr = nullptr;
     B->d_bcol = nullptr;
     B->d_val = nullptr;
@@ -863,6 +887,10 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         KLE_HIP(hipMalloc(&B->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1)));
         KLE_HIP(hipMalloc(&B->d_val, sizeof(double) * nv));
         KLE_HIP(hipMemcpy(B->d_rowptr, A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToDevice));
+        if (A->d_rowcnt) {
+            KLE_HIP(hipMalloc(&B->d_rowcnt, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
+            KLE_HIP(hipMemcpy(B->d_rowcnt, A->d_rowcnt, sizeof(int) * A->nrows, hipMemcpyDeviceToDevice));
+        }
         KLE_HIP(hipMemcpy(B->d_bcol, A->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1), hipMemcpyDeviceToDevice));
         if (copy_values) KLE_HIP(hipMemcpy(B->d_val, A->d_val, sizeof(double) * nv, hipMemcpyDeviceToDevice));
         else KLE_HIP(hipMemset(B->d_val, 0, sizeof(double) * nv));
@@ -874,6 +902,20 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         }
     }
     *out = B;
+    return 0;
+}
+
+int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt)
+{
+    KLE_ARG(A, "null matrix");
+    A->spmv_nt = nt != 0;
+    return 0;
+}
+
+int kle_set_nb_pad(int quantum)
+{
+    KLE_ARG(quantum >= 1 && quantum <= 64, "pad quantum must be in [1,64]");
+    g_nb_pad = quantum;
     return 0;
 }
 
@@ -914,7 +956,8 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
 {
     KLE_ARG(A && bytes, "null arg");
     if (A->kind == 0) {
-        *bytes = (double)A->nblocks * (A->R * A->C * 8.0 + 4.0) + (A->nrows + 1) * 4.0 +
+        // useful bytes: real blocks only (row padding is not counted)
+        *bytes = (double)A->nblocks_real * (A->R * A->C * 8.0 + 4.0) + (A->nrows + 1) * 4.0 +
                  (double)A->ext_nodes * A->C * 8.0 + (double)A->m_local * 8.0;
     } else {
         *bytes = (double)A->nnz * 12.0 + (A->m_local + 1) * 8.0 + A->n_local * 8.0 + A->m_local * 8.0;

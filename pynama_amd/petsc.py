@@ -376,6 +376,9 @@ class Mat:
     def setSpmvBufferVariant(self, v):
         call("kle_mat_set_spmv_buffer_variant", self._h, int(v))
 
+    def setSpmvNontemporal(self, nt=True):
+        call("kle_mat_set_spmv_nontemporal", self._h, int(bool(nt)))
+
     def setSpmvLayout(self, xcd_chunks=False, tiled_order=False):
         call("kle_mat_set_spmv_layout", self._h, int(bool(xcd_chunks)), int(bool(tiled_order)))
 

@@ -178,8 +178,16 @@ _CTX = None
 def get_ctx():
     global _CTX
     if _CTX is None:
+        if os.environ.get("KLE_NB_PAD"):
+            set_row_padding(int(os.environ["KLE_NB_PAD"]))
         _CTX = Context()
     return _CTX
+
+
+def set_row_padding(quantum):
+    """Row padding quantum (blocks) for node-block matrices created afterwards
+    (KLE_NB_PAD in the environment sets the initial value)."""
+    call("kle_set_nb_pad", int(quantum))
 
 
 def set_ctx(ctx):
