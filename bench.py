@@ -5,7 +5,7 @@ BASELINE.json config 2 workload (3-D KLE Laplacian, structured hex mesh
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-A "step" is one CG iteration (SpMV + fused dot, Jacobi z/p update, x/r
+A "step" is one CG iteration (SpMV + dot, Jacobi z/p update, x/r
 update, two deterministic reductions) on the assembled device matrix; the
 K steps are timed between barriers, max over ranks.  Assembly (device
 element kernels + gather) is untimed setup.  A full solve to rtol 1e-10 is
@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--aij", action="store_true", help="also time the scalar-CSR (aij) SpMV")
+    ap.add_argument("--pad", type=int, default=16, help="row padding quantum of K's value streams (blocks)")
+    ap.add_argument("--fused-dot", action="store_true", help="form the CG dot inside the SpMV kernel")
+    ap.add_argument("--loads", choices=["nt", "plain"], default="nt", help="SpMV value/column load policy")
     ap.add_argument("--classic-cg", action="store_true",
                     help="two reductions per iteration instead of the single-reduction (Chronopoulos-Gear) CG")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -67,6 +70,7 @@ def main():
     from pynama_amd.petsc import KSP, PC
 
     ctx = pa.get_ctx()
+    pa.runtime.set_row_padding(args.pad)
     rank, nranks = ctx.rank, ctx.nranks
     nelem = [int(v) for v in args.nelem.split(",")]
     dim = len(nelem)
@@ -96,6 +100,7 @@ def main():
     t_setup = time.perf_counter() - t0
 
     K = mat.K
+    K.setSpmvNontemporal(args.loads == "nt")
     n_global = K.getSize()[0]
     info = K.getInfo()
     nnz_local = info["nz_used"]
@@ -121,6 +126,7 @@ def main():
     pc.setType("jacobi")
     kb.setPC(pc)
     kb.setCGSingleReduction(not args.classic_cg)
+    kb.setFusedDot(args.fused_dot)
     kb.setOperators(K)
     kb.setUp()
     x = K.createVecRight()
@@ -143,6 +149,7 @@ def main():
     p_cnt, p_ms = ctx.kernel_stats("p_update")
     red_cnt, red_ms = ctx.kernel_stats("reduce")
     halo_cnt, halo_ms = ctx.kernel_stats("halo")
+    dot_cnt, dot_ms = ctx.kernel_stats("dot")
     t_max = t_loc
     tot_bytes = spmv_bytes_local
     tot_nnz = nnz_local
@@ -189,7 +196,7 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
-            key = f"{nelem}-{args.ngl}-{nranks}"
+            key = f"{nelem}-{args.ngl}-{nranks}-pad{args.pad}-{args.loads}" + ("-fused" if args.fused_dot else "")
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -217,18 +224,19 @@ def main():
                                    f"TG-{dim}D Dirichlet on all faces; one CG(+Jacobi) iteration per step",
                        "nelem": nelem, "ngl": args.ngl, "n_dof": n_global, "nnz_K": tot_nnz,
                        "ksp": "cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)",
-                       "pc": "jacobi", "matrix_format": info["format"],
+                       "pc": "jacobi", "matrix_format": info["format"], "row_pad_blocks": args.pad,
+                       "spmv_loads": args.loads, "spmv_fused_dot": args.fused_dot,
                        "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                         "kernel": "k_nb_spmv<3,3,true>", "bytes_per_launch": tot_bytes,
+                         "kernel": "k_nb_spmv<3,3,%s>" % ("true" if args.fused_dot else "false"), "bytes_per_launch": tot_bytes,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt},
             "cpu_baseline": cpu,
             "spmv_gbps": achieved,
             "stream_copy_gbps": stream,
             "breakdown_ms_per_iter": {"spmv": spmv_ms / max(args.steps, 1), "cg_update": upd_ms / max(args.steps, 1),
                                       "p_update": p_ms / max(args.steps, 1), "reduce": red_ms / max(args.steps, 1),
-                                      "halo": halo_ms / max(args.steps, 1)},
+                                      "halo": halo_ms / max(args.steps, 1), "dot": dot_ms / max(args.steps, 1)},
             "assembly_s": t_asm,
             "setup_s": t_setup,
             "solve": solve,

@@ -238,6 +238,9 @@ int kle_ksp_set_gmres_restart(kle_ksp *k, int restart);
 /* CG with one reduction per iteration (Chronopoulos-Gear), as PETSc's
  * -ksp_cg_single_reduction. */
 int kle_ksp_set_cg_single_reduction(kle_ksp *k, int flag);
+/* 1: the CG dot (p, Ap) is formed inside the SpMV kernel; 0 (default): by a
+ * separate streaming pass over p and Ap after a plain SpMV. */
+int kle_ksp_set_fused_dot(kle_ksp *k, int flag);
 /* Run exactly n iterations, no convergence test (benchmarks); 0 = off. */
 int kle_ksp_set_fixed_iterations(kle_ksp *k, int n);
 int kle_ksp_set_operators(kle_ksp *k, kle_mat *A);

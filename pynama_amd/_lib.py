@@ -124,6 +124,7 @@ _SIGS = {
     "kle_ksp_set_gmres_restart": [vp, C.c_int],
     "kle_ksp_set_fixed_iterations": [vp, C.c_int],
     "kle_ksp_set_cg_single_reduction": [vp, C.c_int],
+    "kle_ksp_set_fused_dot": [vp, C.c_int],
     "kle_ksp_set_operators": [vp, vp],
     "kle_ksp_set_up": [vp],
     "kle_ksp_solve": [vp, vp, vp],

@@ -283,6 +283,16 @@ __global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict_
     if (fuse && threadIdx.x == 0) cg_scalars(stage, scal, ist, rtol, atol);
 }
 
+// partials[blockIdx] = sum x.y over this block's grid-stride slice; no-op once converged
+__global__ __launch_bounds__(KB) void k_dot_part(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
+                                                 double *__restrict__ partials, const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    double s[1] = {0.0};
+    for (int64_t i = blockIdx.x * (int64_t)KB + threadIdx.x; i < n; i += (int64_t)gridDim.x * KB) s[0] += x[i] * y[i];
+    block_sums<1>(s, partials, 0);
+}
+
 __global__ void k_scalars(double *scal, int *ist, int stage, double rtol, double atol)
 {
     cg_scalars(stage, scal, ist, rtol, atol);
@@ -368,6 +378,7 @@ struct kle_ksp {
     kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
     kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
     int single_reduction = 0;
+    int fused_dot = 0;  // 1: SpMV also forms the dot with its input (DOT variant)
     std::vector<kle_vec *> V;  // GMRES basis
     double **d_Vptr = nullptr;
     double *d_h = nullptr;
@@ -439,6 +450,23 @@ __global__ __launch_bounds__(1024) void k_reduce_l1(double *__restrict__ partial
             partials[q * PART_STRIDE + PART2_OFF + blockIdx.x] = t;
         }
     }
+}
+
+// y = A x and partials of (x, y): fused into the SpMV (DOT variant) or as a
+// separate streaming pass over x and y (cheaper on gfx950: profiles/r01)
+static int spmv_dot(kle_ksp *k, kle_vec *x, kle_vec *y, double *partials, int *np, const int *istate)
+{
+    if (k->fused_dot) return spmv(k->A, x, y, x, partials, np, istate);
+    KLE_TRY(spmv(k->A, x, y, nullptr, nullptr, nullptr, istate));
+    kle_ctx *c = k->ctx;
+    const int g = grid_for(x->n_local, KB, RED_BLOCKS);
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(c->tic("dot", &ev));
+    hipLaunchKernelGGL(k_dot_part, dim3(g), dim3(KB), 0, c->stream, x->n_local, x->d, y->d, partials, istate);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(c->toc("dot", &ev));
+    *np = g;
+    return 0;
 }
 
 static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage)
@@ -524,7 +552,7 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
         KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("p_update", &ev));
         int np = 0;
-        KLE_TRY(spmv(k->A, k->p, k->q, k->p, c->d_partials, &np, c->d_istate));
+        KLE_TRY(spmv_dot(k, k->p, k->q, c->d_partials, &np, c->d_istate));
         KLE_TRY(reduce_stage(k, NParts{{np, 0, 0, 0}}, 1, ST_ALPHA));
         KLE_TRY(c->tic("cg_update", &ev));
         if (jac)
@@ -569,7 +597,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
                            k->p->d, k->s->d, c->d_partials);
     KLE_HIP(hipGetLastError());
     int np = 0;
-    KLE_TRY(spmv(k->A, k->u, k->w, k->u, c->d_partials + 2 * PART_STRIDE, &np, nullptr));
+    KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, nullptr));
     KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR_START));
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
@@ -583,7 +611,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
                                k->s->d, x->d, k->r->d, c->d_partials, c->d_scal, c->d_istate);
         KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("cg_update", &ev));
-        KLE_TRY(spmv(k->A, k->u, k->w, k->u, c->d_partials + 2 * PART_STRIDE, &np, c->d_istate));
+        KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, c->d_istate));
         KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR));
         if (!k->fixed && ((it + 1) % k->check_every == 0)) {
             KLE_TRY(poll_state(k));
@@ -775,6 +803,13 @@ int kle_ksp_set_cg_single_reduction(kle_ksp *k, int flag)
     KLE_ARG(k, "null ksp");
     k->single_reduction = flag != 0;
     k->setup = false;
+    return 0;
+}
+
+int kle_ksp_set_fused_dot(kle_ksp *k, int flag)
+{
+    KLE_ARG(k, "null ksp");
+    k->fused_dot = flag != 0;
     return 0;
 }
 

@@ -535,6 +535,11 @@ class KSP:
         self._ensure()
         call("kle_ksp_set_cg_single_reduction", self._h, int(bool(flag)))
 
+    def setFusedDot(self, flag=True):
+        """Form the CG dot (p, Ap) inside the SpMV kernel instead of a separate pass."""
+        self._ensure()
+        call("kle_ksp_set_fused_dot", self._h, int(bool(flag)))
+
     def setGMRESRestart(self, m):
         self._ensure()
         call("kle_ksp_set_gmres_restart", self._h, int(m))
