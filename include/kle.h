@@ -137,7 +137,8 @@ int kle_mesh_face_nodes(const kle_mesh *m, unsigned face_mask, int64_t *nodes, i
 /* Dirichlet (free-slip) node set: faces by mask, or explicit global ids. */
 int kle_mesh_set_dirichlet_faces(kle_mesh *m, unsigned face_mask);
 int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n);
-/* Symbolic node-block pattern (host).  which: 0 K, 1 Krhs, 2 Rw.
+/* Symbolic node-block pattern (host).  which: 0 K, 1 Krhs, 2 Rw, 3 operators
+ * (Curl/SrT/DivSrT: every node x every node sharing a cell).
  * row_ptr[n_owned+1] (block offsets, unpadded) and col[] (global node ids). */
 int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks);
 int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *cols);
@@ -162,6 +163,10 @@ int kle_vec_aypx(kle_vec *y, double beta, const kle_vec *x);    /* y = x + b y  
 int kle_vec_waxpy(kle_vec *w, double alpha, const kle_vec *x, const kle_vec *y); /* w = a x + y */
 int kle_vec_scale(kle_vec *v, double alpha);
 int kle_vec_pointwise_mult(kle_vec *w, const kle_vec *x, const kle_vec *y);
+/* out[node] = v v^T of the dim-vector at each node, components xx,xy,yy
+ * (2-D) or xx,xy,yy,yz,zz,zx (3-D): BaseProblem.computeVtensV
+ * (base_problem.py:138-154). */
+int kle_vec_tensor_square(const kle_vec *v, int dim, kle_vec *out);
 int kle_vec_reciprocal(kle_vec *v);
 int kle_vec_dot(const kle_vec *x, const kle_vec *y, double *out);
 int kle_vec_norm2(const kle_vec *x, double *out);
@@ -183,6 +188,12 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
 /* Element matrices of local element e in tensor order (parity tests):
  * K_e [dim n][dim n], Rw_e [dim n][dim_w n] (row-major, n = ngl^dim). */
 int kle_element_kle(kle_ctx *ctx, kle_mesh *m, int64_t e, double *Ke, double *Rwe);
+/* Operators (replaces MatFS.buildOperators + Operators.setValues/assembleAll,
+ * mat_fs.py:194-271, with Spectral.getElemKLEOperators spectral.py:162-228):
+ * Curl [dim_w N x dim N], SrT [dim_s N x dim N], DivSrT [dim N x dim_s N],
+ * each already scaled by the inverse lumped nodal weight.  Node-block CSR on
+ * the full node adjacency (pattern 3), explicit zeros kept as PETSc does. */
+int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **SrT, kle_mat **DivSrT);
 
 /* Generic AIJ (petsc4py Mat().createAIJ + setValues + assemble). */
 int kle_mat_create_aij(kle_ctx *ctx, int64_t m_local, int64_t n_local, int64_t m_global,

@@ -904,6 +904,91 @@ int orc_assemble_fs(const orc_mesh *m, const uint8_t *dir_flag, orc_csr **Kout,
     return 0;
 }
 
+/* a12: Operators (mat_fs.py:194-271).  Curl [dw N x dim N], SrT [ds N x dim N],
+ * DivSrT [dim N x ds N] on the full node adjacency (explicit zeros kept),
+ * element blocks of Spectral.getElemKLEOperators added in ascending cell order
+ * (Operators.setValues, mat_fs.py:238-251); the lumped weights are summed per
+ * node in the same order, inverted (Vec.reciprocal) and applied as a left
+ * diagonal scaling (Mat.diagonalScale(L=), mat_fs.py:253-271). */
+static orc_csr *ops_pattern(int64_t N, const int *deg, int64_t *const *adj, int R, int C)
+{
+    orc_csr *A = calloc(1, sizeof(orc_csr));
+    A->m = N * R;
+    A->n = N * C;
+    A->indptr = calloc(A->m + 1, sizeof(int64_t));
+    for (int64_t i = 0; i < N; ++i)
+        for (int a = 0; a < R; ++a) A->indptr[i * R + a + 1] = (int64_t)deg[i] * C;
+    for (int64_t r = 0; r < A->m; ++r) A->indptr[r + 1] += A->indptr[r];
+    A->nnz = A->indptr[A->m];
+    A->indices = malloc(sizeof(int64_t) * (A->nnz ? A->nnz : 1));
+    A->data = calloc(A->nnz ? A->nnz : 1, sizeof(double));
+    for (int64_t i = 0; i < N; ++i)
+        for (int a = 0; a < R; ++a) {
+            int64_t p = A->indptr[i * R + a];
+            for (int k = 0; k < deg[i]; ++k)
+                for (int b = 0; b < C; ++b) A->indices[p++] = adj[i][k] * C + b;
+        }
+    return A;
+}
+
+static void ops_add(orc_csr *A, const int64_t *cn, int nn, int R, int C, const double *Ae)
+{
+    for (int li = 0; li < nn; ++li)
+        for (int a = 0; a < R; ++a) {
+            int64_t r = cn[li] * R + a;
+            for (int lj = 0; lj < nn; ++lj) {
+                int64_t p = find_col(A, r, cn[lj] * C);
+                for (int b = 0; b < C; ++b) A->data[p + b] += Ae[(size_t)(li * R + a) * nn * C + lj * C + b];
+            }
+        }
+}
+
+static void ops_scale(orc_csr *A, int R, const double *winv)
+{
+    for (int64_t r = 0; r < A->m; ++r)
+        for (int64_t k = A->indptr[r]; k < A->indptr[r + 1]; ++k) A->data[k] *= winv[r / R];
+}
+
+int orc_assemble_ops(const orc_mesh *m, orc_csr **Curl, orc_csr **SrT, orc_csr **DivSrT, double *Wout)
+{
+    const int dim = m->dim, dw = dim == 2 ? 1 : 3, ds = dim == 2 ? 3 : 6;
+    const int nn = dim == 2 ? m->ngl * m->ngl : m->ngl * m->ngl * m->ngl;
+    const int64_t N = m->N;
+    int64_t *conn = malloc(sizeof(int64_t) * m->E * nn);
+    orc_mesh_conn(m, conn);
+    int *deg = malloc(sizeof(int) * N);
+    int64_t **adj = node_adjacency(m, conn, deg);
+    orc_csr *Cu = ops_pattern(N, deg, adj, dw, dim), *S = ops_pattern(N, deg, adj, ds, dim),
+            *D = ops_pattern(N, deg, adj, dim, ds);
+    double *W = calloc(N, sizeof(double));
+    orc_elem *el = orc_elem_create(dim, m->ngl);
+    const int nd = dim * nn, nc = 1 << dim;
+    double *X = malloc(sizeof(double) * m->E * nc * dim);
+    orc_mesh_corners(m, X);
+    double *Se = malloc(sizeof(double) * ds * nn * nd), *De = malloc(sizeof(double) * nd * ds * nn),
+           *Ce = malloc(sizeof(double) * dw * nn * nd), *We = malloc(sizeof(double) * nn);
+    for (int64_t e = 0; e < m->E; ++e) {
+        orc_elem_ops(el, X + e * nc * dim, Se, De, Ce, We);
+        const int64_t *cn = conn + e * nn;
+        ops_add(Cu, cn, nn, dw, dim, Ce);
+        ops_add(S, cn, nn, ds, dim, Se);
+        ops_add(D, cn, nn, dim, ds, De);
+        for (int l = 0; l < nn; ++l) W[cn[l]] += We[l];
+    }
+    double *winv = calloc(N ? N : 1, sizeof(double));
+    for (int64_t i = 0; i < N; ++i) winv[i] = 1.0 / W[i];
+    ops_scale(S, ds, winv);
+    ops_scale(D, dim, winv);
+    ops_scale(Cu, dw, winv);
+    if (Wout) memcpy(Wout, W, sizeof(double) * N);
+    orc_elem_destroy(el);
+    free(X); free(Se); free(De); free(Ce); free(We); free(W); free(winv); free(conn);
+    for (int64_t i = 0; i < N; ++i) free(adj[i]);
+    free(adj); free(deg);
+    *Curl = Cu; *SrT = S; *DivSrT = D;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* a14/a15: CSR SpMV and PETSc-3.12-style KSPCG                               */
 /* ------------------------------------------------------------------------ */

@@ -51,6 +51,7 @@ def lib():
         L.orc_mesh_coords.argtypes = [C.c_void_p, f64p]
         L.orc_assemble_fs.argtypes = [C.c_void_p, u8p, C.POINTER(C.c_void_p),
                                       C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.orc_assemble_ops.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 3 + [f64p]
         L.orc_csr_destroy.argtypes = [C.c_void_p]
         L.orc_csr_nnz.restype = C.c_int64
         L.orc_csr_nnz.argtypes = [C.c_void_p]
@@ -214,6 +215,38 @@ class BoxMesh:
         dw = 1 if self.dim == 2 else 3
         return (CSR(K.value, self.N * self.dim), CSR(Kr.value, self.N * self.dim),
                 CSR(Rw.value, self.N * dw))
+
+
+    def assemble_ops(self):
+        """Operators Curl, SrT, DivSrT (weights applied) and the lumped nodal weights W."""
+        Cu, S, D = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        W = np.zeros(self.N)
+        lib().orc_assemble_ops(self._h, C.byref(Cu), C.byref(S), C.byref(D), W)
+        dw, ds = (1, 3) if self.dim == 2 else (3, 6)
+        return (CSR(Cu.value, self.N * self.dim), CSR(S.value, self.N * self.dim),
+                CSR(D.value, self.N * ds), W)
+
+
+def vtensv(vel, dim):
+    """BaseProblem.computeVtensV (base_problem.py:138-154)."""
+    v = np.asarray(vel).reshape(-1, dim)
+    x, y = v[:, 0], v[:, 1]
+    if dim == 2:
+        return np.stack([x ** 2, x * y, y ** 2], 1).ravel()
+    z = v[:, 2]
+    return np.stack([x ** 2, x * y, y ** 2, y * z, z ** 2, z * x], 1).ravel()
+
+
+def eval_rhs_chain(Curl, SrT, DivSrT, vel, rho, mu, dim):
+    """The operator part of BaseProblem.evalRHS (base_problem.py:127-136) after
+    the KLE solve: returns (VtensV, Aux1, f)."""
+    vt = vtensv(vel, dim)
+    aux = SrT.mult(vel)
+    aux *= (2.0 * mu)
+    aux += (-1.0 * rho) * vt
+    rhs = DivSrT.mult(aux)
+    rhs *= (1 / rho)
+    return vt, aux, Curl.mult(rhs)
 
 
 def set_threads(n):

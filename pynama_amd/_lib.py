@@ -82,6 +82,7 @@ _SIGS = {
     "kle_vec_waxpy": [vp, C.c_double, vp, vp],
     "kle_vec_scale": [vp, C.c_double],
     "kle_vec_pointwise_mult": [vp, vp, vp],
+    "kle_vec_tensor_square": [vp, C.c_int, vp],
     "kle_vec_reciprocal": [vp],
     "kle_vec_dot": [vp, vp, C.POINTER(C.c_double)],
     "kle_vec_norm2": [vp, C.POINTER(C.c_double)],
@@ -93,6 +94,7 @@ _SIGS = {
     "kle_vec_device_ptr": [vp, C.POINTER(C.c_void_p)],
     "kle_assemble_kle": [vp, vp, pvp, pvp, pvp],
     "kle_element_kle": [vp, vp, C.c_int64, f64p, f64p],
+    "kle_assemble_operators": [vp, vp, pvp, pvp, pvp],
     "kle_mat_create_aij": [vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp, vp, pvp],
     "kle_mat_set_values": [vp, C.c_int32, i64p, C.c_int32, i64p, f64p, C.c_int],
     "kle_mat_assemble": [vp],

@@ -411,7 +411,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->send_lo = m->send_lo_nodes * C;
     A->send_hi = m->send_hi_nodes * C;
     A->diag_only_row.assign(nrows, 0);
-    if (which != 2)
+    if (which <= 1)
         for (int64_t i = 0; i < nrows; ++i) A->diag_only_row[i] = m->dir[m->node_begin + i - m->ext_begin];
     if (hipMalloc(&A->d_rowptr, sizeof(int) * (nrows + 1)) != hipSuccess ||
         (pad > 1 && hipMalloc(&A->d_rowcnt, sizeof(int) * std::max<int64_t>(nrows, 1)) != hipSuccess) ||
@@ -435,7 +435,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
 
 struct DevTables {
     double *buf = nullptr;
-    Tables1D F, R;
+    Tables1D F, R, O;
     ~DevTables() { hipFree(buf); }
 };
 
@@ -451,10 +451,12 @@ static int upload_tables(kle_ctx *ctx, int ngl, DevTables &T)
     };
     size_t fx = put(full.x), fw = put(full.w), fh = put(full.h), fd = put(full.dh);
     size_t rx = put(red.x), rw = put(red.w), rh = put(red.h), rd = put(red.dh);
+    size_t ox = put(op.x), ow = put(op.w), oh = put(op.h), od = put(op.dh);
     KLE_HIP(hipMalloc(&T.buf, sizeof(double) * h.size()));
     KLE_HIP(hipMemcpyAsync(T.buf, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, ctx->stream));
     T.F = {(int)full.x.size(), T.buf + fx, T.buf + fw, T.buf + fh, T.buf + fd};
     T.R = {(int)red.x.size(), T.buf + rx, T.buf + rw, T.buf + rh, T.buf + rd};
+    T.O = {(int)op.x.size(), T.buf + ox, T.buf + ow, T.buf + oh, T.buf + od};
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     return 0;
 }
@@ -501,6 +503,157 @@ static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, doubl
     hipFree(gF);
     hipFree(gR);
     return 0;
+}
+
+
+// ---------------------------------------------------------------- operators
+// Operators (mat_fs.py:194-271, spectral.py:162-228) are collocation operators
+// on the GLL nodes: at op point l of cell e only node l's basis is nonzero
+// (H = delta), so the element block of (row node n = local l, col node m) is
+//   c_{e,l} * B_{e,l}[a][(m, b)],  c = w_l det J,  Hxy = inv(J) dN_m/dxi at l,
+// with B_curl / B_srt / B_div the sparse maps of spectral.py:205-228.
+// dN_m/dxi_k at node l is D[l_k][m_k] when m and l agree on the other axes,
+// else exactly 0.  The global entry is the ascending-cell sum of those blocks
+// times 1/W_n, W_n = sum_e c_{e,l(n)} (Vec.reciprocal + diagonalScale(L)).
+struct OpsOut {
+    double *curl, *srt, *div;
+    const int *rp_c, *rp_s, *rp_d;  // padded row offsets of each matrix
+};
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_ops_weights(MeshDev M, int64_t nrows, const double *__restrict__ geo,
+                                                     double *__restrict__ winv)
+{
+    const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    constexpr int G1 = 1 + DIM * DIM;
+    const int64_t gi = M.node_begin + row;
+    const int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], DIM == 3 ? gi / (M.L[0] * M.L[1]) : 0};
+    int64_t elo[3] = {0, 0, 0}, ehi[3] = {0, 0, 0};
+    for (int d = 0; d < DIM; ++d) {
+        elo[d] = (ci[d] % M.p == 0) ? max((int64_t)0, ci[d] / M.p - 1) : ci[d] / M.p;
+        ehi[d] = min(M.nel[d] - 1, ci[d] / M.p);
+    }
+    double W = 0.0;
+    for (int64_t ez = elo[2]; ez <= ehi[2]; ++ez)
+        for (int64_t ey = elo[1]; ey <= ehi[1]; ++ey)
+            for (int64_t ex = elo[0]; ex <= ehi[0]; ++ex) {
+                const int64_t eo[3] = {ex * M.p, ey * M.p, ez * M.p};
+                int l = 0;
+                for (int d = DIM - 1; d >= 0; --d) l = l * M.ngl + (int)(ci[d] - eo[d]);
+                const int64_t e = ex + M.nel[0] * (ey + M.nel[1] * ez) - M.elem_begin;
+                W += geo[(e * M.ne + l) * G1];
+            }
+    winv[row] = 1.0 / W;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_ops_gather(MeshDev M, int64_t nrows, const int *__restrict__ rowcnt,
+                                                    const int *__restrict__ bcol, const double *__restrict__ geo,
+                                                    const double *__restrict__ dh, const double *__restrict__ winv,
+                                                    OpsOut out)
+{
+    constexpr int DW = DIM == 2 ? 1 : 3, DS = DIM == 2 ? 3 : 6, G1 = 1 + DIM * DIM;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (row >= nrows) return;
+    const int64_t gi = M.node_begin + row;
+    const int m = rowcnt[row];
+    const int bc0 = out.rp_c[row];  // block offset in the (shared) column list
+    const int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], DIM == 3 ? gi / (M.L[0] * M.L[1]) : 0};
+    int64_t elo[3] = {0, 0, 0}, ehi[3] = {0, 0, 0};
+    for (int d = 0; d < DIM; ++d) {
+        elo[d] = (ci[d] % M.p == 0) ? max((int64_t)0, ci[d] / M.p - 1) : ci[d] / M.p;
+        ehi[d] = min(M.nel[d] - 1, ci[d] / M.p);
+    }
+    const double wi = winv[row];
+    const int mpc = out.rp_c[row + 1] - out.rp_c[row], mps = out.rp_s[row + 1] - out.rp_s[row],
+              mpd = out.rp_d[row + 1] - out.rp_d[row];
+    double *vc = out.curl + (int64_t)out.rp_c[row] * DW * DIM;
+    double *vs = out.srt + (int64_t)out.rp_s[row] * DS * DIM;
+    double *vd = out.div + (int64_t)out.rp_d[row] * DIM * DS;
+    for (int k = lane; k < m; k += 64) {
+        const int64_t gj = M.ext_begin + bcol[bc0 + k];
+        const int64_t cj[3] = {gj % M.L[0], (gj / M.L[0]) % M.L[1], DIM == 3 ? gj / (M.L[0] * M.L[1]) : 0};
+        double C[DW * DIM], S[DS * DIM], D[DIM * DS];
+        for (int t = 0; t < DW * DIM; ++t) C[t] = 0.0;
+        for (int t = 0; t < DS * DIM; ++t) S[t] = D[t] = 0.0;
+        for (int64_t ez = elo[2]; ez <= ehi[2]; ++ez)
+            for (int64_t ey = elo[1]; ey <= ehi[1]; ++ey)
+                for (int64_t ex = elo[0]; ex <= ehi[0]; ++ex) {
+                    const int64_t eo[3] = {ex * M.p, ey * M.p, ez * M.p};
+                    int oi[3] = {0, 0, 0}, oj[3] = {0, 0, 0};
+                    bool in = true;
+                    for (int d = 0; d < DIM; ++d) {
+                        const int64_t o = cj[d] - eo[d];
+                        in = in && o >= 0 && o <= M.p;
+                        oj[d] = (int)o;
+                        oi[d] = (int)(ci[d] - eo[d]);
+                    }
+                    if (!in) continue;
+                    int l = 0;
+                    for (int d = DIM - 1; d >= 0; --d) l = l * M.ngl + oi[d];
+                    const int64_t e = ex + M.nel[0] * (ey + M.nel[1] * ez) - M.elem_begin;
+                    const double *g = geo + (e * M.ne + l) * G1;
+                    const double c = g[0];
+                    double Hrs[DIM];
+                    for (int kk = 0; kk < DIM; ++kk) {
+                        bool line = true;
+                        for (int j = 0; j < DIM; ++j)
+                            if (j != kk) line = line && oj[j] == oi[j];
+                        Hrs[kk] = line ? dh[oi[kk] * M.ngl + oj[kk]] : 0.0;
+                    }
+                    double H[DIM];
+                    for (int d = 0; d < DIM; ++d) {
+                        double acc = 0.0;
+                        for (int kk = 0; kk < DIM; ++kk) acc += g[1 + d * DIM + kk] * Hrs[kk];
+                        H[d] = acc;
+                    }
+                    if constexpr (DIM == 3) {
+                        // curl: indCurl (spectral.py:31), signs (-1)^i
+                        C[0 * 3 + 2] += c * H[1];
+                        C[0 * 3 + 1] += c * -H[2];
+                        C[1 * 3 + 0] += c * H[2];
+                        C[1 * 3 + 2] += c * -H[0];
+                        C[2 * 3 + 1] += c * H[0];
+                        C[2 * 3 + 0] += c * -H[1];
+                        // strain rate xx,xy,yy,yz,zz,zx (B_srt *= 0.5, spectral.py:209-220)
+                        S[0 * 3 + 0] += c * H[0];
+                        S[1 * 3 + 1] += c * (0.5 * H[0]);
+                        S[5 * 3 + 2] += c * (0.5 * H[0]);
+                        S[2 * 3 + 1] += c * H[1];
+                        S[1 * 3 + 0] += c * (0.5 * H[1]);
+                        S[3 * 3 + 2] += c * (0.5 * H[1]);
+                        S[4 * 3 + 2] += c * H[2];
+                        S[5 * 3 + 0] += c * (0.5 * H[2]);
+                        S[3 * 3 + 1] += c * (0.5 * H[2]);
+                        // divergence of the symmetric tensor: indBdiv (spectral.py:33)
+                        D[0 * 6 + 0] += c * H[0];
+                        D[0 * 6 + 1] += c * H[1];
+                        D[0 * 6 + 5] += c * H[2];
+                        D[1 * 6 + 1] += c * H[0];
+                        D[1 * 6 + 2] += c * H[1];
+                        D[1 * 6 + 3] += c * H[2];
+                        D[2 * 6 + 5] += c * H[0];
+                        D[2 * 6 + 3] += c * H[1];
+                        D[2 * 6 + 4] += c * H[2];
+                    } else {
+                        C[1] += c * H[0];  // indCurl 2-D (spectral.py:27)
+                        C[0] += c * -H[1];
+                        S[0 * 2 + 0] += c * H[0];
+                        S[1 * 2 + 1] += c * (0.5 * H[0]);
+                        S[2 * 2 + 1] += c * H[1];
+                        S[1 * 2 + 0] += c * (0.5 * H[1]);
+                        D[0 * 3 + 0] += c * H[0];
+                        D[0 * 3 + 1] += c * H[1];
+                        D[1 * 3 + 1] += c * H[0];
+                        D[1 * 3 + 2] += c * H[1];
+                    }
+                }
+        for (int t = 0; t < DW * DIM; ++t) vc[(int64_t)t * mpc + k] = C[t] * wi;
+        for (int t = 0; t < DS * DIM; ++t) vs[(int64_t)t * mps + k] = S[t] * wi;
+        for (int t = 0; t < DIM * DS; ++t) vd[(int64_t)t * mpd + k] = D[t] * wi;
+    }
 }
 
 template <int R, int C, int MODE>
@@ -551,6 +704,65 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     *K = mK;
     *Krhs = mKr;
     *Rw = mRw;
+    return 0;
+}
+
+int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **SrT, kle_mat **DivSrT)
+{
+    KLE_ARG(ctx && m && Curl && SrT && DivSrT, "null arg");
+    KLE_ARG(m->rank == ctx->rank && m->nranks == ctx->nranks, "mesh partition does not match ctx");
+    const int dim = m->dim, dw = dim == 2 ? 1 : 3, ds = dim == 2 ? 3 : 6, nc = 1 << dim, G1 = 1 + dim * dim;
+    KLE_HIP(hipSetDevice(ctx->device));
+    kle_mat *mc = nullptr, *ms = nullptr, *md = nullptr;
+    KLE_TRY(nb_create(ctx, m, 3, dw, dim, &mc));
+    KLE_TRY(nb_create(ctx, m, 3, ds, dim, &ms));
+    KLE_TRY(nb_create(ctx, m, 3, dim, ds, &md));
+    const int64_t nel = m->elem_end - m->elem_begin, nrows = mc->nrows;
+    DevTables T;
+    KLE_TRY(upload_tables(ctx, m->ngl, T));
+    std::vector<double> corners(nel * nc * dim);
+    KLE_TRY(kle_mesh_get_corners(m, corners.data()));
+    std::vector<int> cnt(nrows);
+    {
+        std::vector<int> rp(nrows + 1);
+        KLE_HIP(hipMemcpy(rp.data(), mc->d_rowptr, sizeof(int) * (nrows + 1), hipMemcpyDeviceToHost));
+        if (mc->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), mc->d_rowcnt, sizeof(int) * nrows, hipMemcpyDeviceToHost));
+        else
+            for (int64_t i = 0; i < nrows; ++i) cnt[i] = rp[i + 1] - rp[i];
+    }
+    double *dX = nullptr, *geo = nullptr, *winv = nullptr;
+    int *dcnt = nullptr;
+    const int64_t nq = nel * m->nn();
+    KLE_HIP(hipMalloc(&dX, sizeof(double) * std::max<size_t>(corners.size(), 1)));
+    KLE_HIP(hipMalloc(&geo, sizeof(double) * std::max<int64_t>(nq * G1, 1)));
+    KLE_HIP(hipMalloc(&winv, sizeof(double) * std::max<int64_t>(nrows, 1)));
+    KLE_HIP(hipMalloc(&dcnt, sizeof(int) * std::max<int64_t>(nrows, 1)));
+    KLE_HIP(hipMemcpyAsync(dX, corners.data(), sizeof(double) * corners.size(), hipMemcpyHostToDevice, ctx->stream));
+    KLE_HIP(hipMemcpyAsync(dcnt, cnt.data(), sizeof(int) * nrows, hipMemcpyHostToDevice, ctx->stream));
+    MeshDev M = mesh_dev(m);
+    OpsOut o{mc->d_val, ms->d_val, md->d_val, mc->d_rowptr, ms->d_rowptr, md->d_rowptr};
+    const unsigned gq = (unsigned)((nq + 255) / 256), gr = (unsigned)((nrows + 255) / 256),
+                   gw = (unsigned)((nrows * 64 + 255) / 256);
+    if (dim == 3) {
+        hipLaunchKernelGGL(k_geometry<3>, dim3(gq), dim3(256), 0, ctx->stream, nel, m->ngl, T.O, dX, geo);
+        hipLaunchKernelGGL(k_ops_weights<3>, dim3(gr), dim3(256), 0, ctx->stream, M, nrows, geo, winv);
+        hipLaunchKernelGGL(k_ops_gather<3>, dim3(gw), dim3(256), 0, ctx->stream, M, nrows, dcnt, mc->d_bcol, geo,
+                           T.O.dh, winv, o);
+    } else {
+        hipLaunchKernelGGL(k_geometry<2>, dim3(gq), dim3(256), 0, ctx->stream, nel, m->ngl, T.O, dX, geo);
+        hipLaunchKernelGGL(k_ops_weights<2>, dim3(gr), dim3(256), 0, ctx->stream, M, nrows, geo, winv);
+        hipLaunchKernelGGL(k_ops_gather<2>, dim3(gw), dim3(256), 0, ctx->stream, M, nrows, dcnt, mc->d_bcol, geo,
+                           T.O.dh, winv, o);
+    }
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    hipFree(dX);
+    hipFree(geo);
+    hipFree(winv);
+    hipFree(dcnt);
+    *Curl = mc;
+    *SrT = ms;
+    *DivSrT = md;
     return 0;
 }
 

@@ -97,6 +97,27 @@ __global__ void k_scale(int64_t n, double a, double *__restrict__ y)
         y[i] *= a;
 }
 
+// computeVtensV (base_problem.py:138-154): the symmetric tensor v v^T per node,
+// components xx, xy, yy (2-D) or xx, xy, yy, yz, zz, zx (3-D)
+template <int DIM>
+__global__ void k_vtensv(int64_t nodes, const double *__restrict__ v, double *__restrict__ o)
+{
+    constexpr int DS = DIM == 2 ? 3 : 6;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nodes; i += (int64_t)gridDim.x * blockDim.x) {
+        const double x = v[i * DIM], y = v[i * DIM + 1];
+        double *t = o + i * DS;
+        t[0] = x * x;
+        t[1] = x * y;
+        t[2] = y * y;
+        if constexpr (DIM == 3) {
+            const double z = v[i * DIM + 2];
+            t[3] = y * z;
+            t[4] = z * z;
+            t[5] = z * x;
+        }
+    }
+}
+
 __global__ void k_pmult(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
                         double *__restrict__ w)
 {
@@ -667,6 +688,21 @@ int kle_vec_pointwise_mult(kle_vec *w, const kle_vec *x, const kle_vec *y)
     KLE_TRY(same_layout(x, w));
     hipLaunchKernelGGL(k_pmult, dim3(VGRID(w->n_local)), dim3(VB), 0, w->ctx->stream, w->n_local,
                        x->d, y->d, w->d);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+int kle_vec_tensor_square(const kle_vec *v, int dim, kle_vec *out)
+{
+    KLE_ARG(v && out, "null vec");
+    KLE_ARG(dim == 2 || dim == 3, "dim must be 2 or 3");
+    const int ds = dim == 2 ? 3 : 6;
+    KLE_ARG(v->n_local % dim == 0 && out->n_local == v->n_local / dim * ds, "sizes do not match dim %d", dim);
+    const int64_t nodes = v->n_local / dim;
+    if (dim == 2)
+        hipLaunchKernelGGL(k_vtensv<2>, dim3(VGRID(nodes)), dim3(VB), 0, v->ctx->stream, nodes, v->d, out->d);
+    else
+        hipLaunchKernelGGL(k_vtensv<3>, dim3(VGRID(nodes)), dim3(VB), 0, v->ctx->stream, nodes, v->d, out->d);
     KLE_HIP(hipGetLastError());
     return 0;
 }

@@ -451,7 +451,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1, false);                                                      \
         else { NB_VARIANTS(RR, CC) }                                                                    \
     } else
-        NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
+        NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3) NB_CASE(3, 2) NB_CASE(2, 3)
         NB_CASE(3, 6) NB_CASE(1, 1) {
             return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
         }

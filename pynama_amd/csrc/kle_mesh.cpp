@@ -48,12 +48,13 @@ inline bool is_dir(const kle_mesh *m, int64_t node) { return m->dir[node - m->ex
 }  // namespace
 
 // which: 0 K (free x free, Dirichlet rows diagonal), 1 Krhs (free x Dirichlet,
-// Dirichlet rows diagonal), 2 Rw (free x all, Dirichlet rows empty).
+// Dirichlet rows diagonal), 2 Rw (free x all, Dirichlet rows empty),
+// 3 operators Curl/SrT/DivSrT (all x all, mat_fs.py:215-236).
 // Enumerates the columns of owned node row i in ascending order.
 template <class F>
 static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
 {
-    const bool di = is_dir(m, i);
+    const bool di = which != 3 && is_dir(m, i);
     if (di) {
         if (which != 2) emit(i);
         return;
@@ -66,7 +67,7 @@ static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
         for (q[1] = lo[1]; q[1] <= hi[1]; ++q[1])
             for (q[0] = lo[0]; q[0] <= hi[0]; ++q[0]) {
                 int64_t j = m->id_of(q);
-                if (which == 2 || (which == 0) == !is_dir(m, j)) emit(j);
+                if (which >= 2 || (which == 0) == !is_dir(m, j)) emit(j);
             }
 }
 
@@ -293,7 +294,7 @@ int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n)
 
 int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks)
 {
-    KLE_ARG(m && nblocks && which >= 0 && which <= 2, "bad arg");
+    KLE_ARG(m && nblocks && which >= 0 && which <= 3, "bad arg");
     int64_t tot = 0;
     for (int64_t i = m->node_begin; i < m->node_end; ++i) row_cols(m, which, i, [&](int64_t) { ++tot; });
     *nblocks = tot;
@@ -302,7 +303,7 @@ int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks)
 
 int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *cols)
 {
-    KLE_ARG(m && row_ptr && which >= 0 && which <= 2, "bad arg");
+    KLE_ARG(m && row_ptr && which >= 0 && which <= 3, "bad arg");
     int64_t k = 0;
     row_ptr[0] = 0;
     for (int64_t i = m->node_begin; i < m->node_end; ++i) {

@@ -25,7 +25,7 @@ class MatFS:
     def setDomain(self, dom):
         self.dom = dom
 
-    def build(self, buildKLE=True, buildOperators=False):
+    def build(self, buildKLE=True, buildOperators=True):
         if self.dom.getBoundaryType() != "FS":
             raise Error(56, "MatFS needs free-slip (Dirichlet) boundaries")
         if buildKLE:
@@ -47,12 +47,41 @@ class MatFS:
         self.kle = [self.K, self.Krhs, self.Rw]
 
     def buildOperators(self):
-        # Curl / SrT / DivSrT (mat_fs.py:194-271) are the next row of the
-        # scope table; not provided in this build.
-        raise Error(56, "Operators (Curl/SrT/DivSrT) are not provided yet")
+        """Curl / SrT / DivSrT on the device (mat_fs.py:194-201)."""
+        self.operator = Operators()
+        self.operator.setDimensions(self.dom.getDimensions())
+        self.operator.build(self.dom.getMesh())
 
     def getOperators(self):
         return self.operator
 
     def assembleAll(self):
         pass
+
+
+class Operators:
+    """Mirror of the reference's Operators (mat_fs.py:211-271): the collocation
+    operators Curl [dim_w N x dim N], SrT [dim_s N x dim N] and DivSrT
+    [dim N x dim_s N], each left-scaled by the inverse lumped nodal weight.
+    Assembled in one device pass (libkle kle_assemble_operators) instead of
+    the per-cell setValues loop; same pattern (explicit zeros kept) and the
+    same ascending-cell ADD order."""
+
+    def __init__(self):
+        self.Curl = self.SrT = self.DivSrT = None
+
+    def setDimensions(self, dims):
+        self.dim, self.dim_w, self.dim_s = dims
+
+    def build(self, mesh):
+        ctx = get_ctx()
+        hc, hs, hd = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        call("kle_assemble_operators", ctx.h, mesh._h, C.byref(hc), C.byref(hs), C.byref(hd))
+        self.Curl = Mat._wrap(hc, ctx, mesh, self.dim_w, self.dim)
+        self.SrT = Mat._wrap(hs, ctx, mesh, self.dim_s, self.dim)
+        self.DivSrT = Mat._wrap(hd, ctx, mesh, self.dim, self.dim_s)
+        for m, n in ((self.Curl, "Curl"), (self.SrT, "SrT"), (self.DivSrT, "DivSrT")):
+            m.setName(n)
+
+    def assembleAll(self):
+        pass  # assembled (and weight-scaled) on the device by build()

@@ -1,0 +1,155 @@
+"""The caller of the KLE path: the vorticity right-hand side.
+
+Host mirror of the part of the reference's BaseProblem / BaseProblemTest
+(cases/base_problem.py:17-420) that drives the KLE solve and the operator
+chain: setUpDomain, readMaterialData, setUpSolver, setUpInitialConditions,
+evalRHS, computeVtensV, generateExactVecs, getKLEError, getConvective and
+getDiffusive.  Same names, arguments and in-place semantics; everything
+runs on the device through libkle (the KLE solve, the Curl / SrT / DivSrT
+SpMVs, the v v^T tensor and the BLAS-1 updates).  The viewer, the PETSc TS
+time integrator and the timers are not part of this path.
+"""
+import numpy as np
+
+from . import fields
+from ._lib import call
+from .domain import Domain
+from .matrices import MatFS
+from .solver import KleSolver
+
+
+class BaseProblem:
+    def __init__(self, config, **kwargs):
+        self.config = config
+        self.opts = kwargs
+        self.case = kwargs.get("case", "uniform")
+        self.caseName = config.get("name")
+        self.readMaterialData()
+        ts = config.get("time-solver") or {}
+        self.initTime = float(kwargs.get("initTime", ts.get("start-time", 0.0)))
+
+    def setUp(self):
+        self.setUpDomain()
+
+    def setUpDomain(self):
+        self.dom = Domain()
+        self.dom.configure(self.config)
+        self.dom.setOptions(**{k: v for k, v in self.opts.items() if k in ("ngl", "nelem", "lower", "upper")})
+        self.dom.setUp()
+        self.dim = self.dom.getDimension()
+        self.dim_w = 1 if self.dim == 2 else 3
+        self.dim_s = 3 if self.dim == 2 else 6
+
+    def readMaterialData(self):
+        materialData = self.config.get("material-properties")
+        self.rho = materialData["rho"]
+        self.mu = materialData["mu"]
+        self.nu = self.mu / self.rho
+
+    def setUpSolver(self):
+        """base_problem.py:156-179 (free-slip / Dirichlet boundaries)."""
+        if self.dom.getBoundaryType() != "FS":
+            raise NotImplementedError("no-slip (MatNS) is the next row of the scope table")
+        mat = MatFS()
+        mat.setDomain(self.dom)
+        mat.build()
+        self.mat = mat
+        self.solverKLE = KleSolver()
+        self.solverKLE.setMat(mat)
+        self.solverKLE.setUp()
+        self.operator = mat.getOperators()
+        self._VtensV = self.operator.SrT.createVecLeft()
+        self._Aux1 = self._VtensV.duplicate()
+        assert "initial-conditions" in self.config, "Initial conditions not defined"
+        self.setUpInitialConditions()
+
+    def setUpInitialConditions(self):
+        """base_problem.py:181-222."""
+        vort = self.operator.Curl.createVecLeft()
+        vort.setName("vorticity")
+        vel = self.solverKLE.getSolution()
+        ic = self.config["initial-conditions"]
+        if "custom-func" in ic:
+            f = fields.get(ic["custom-func"]["name"])
+            alpha = f.alpha(self.nu, self.initTime)
+            coords = self.dom.getFullCoordArray()
+            vort.setArray(np.asarray(f.vorticity(coords, alpha), dtype=np.float64).ravel())
+            vel.setArray(np.asarray(f.velocity(coords, alpha), dtype=np.float64).ravel())
+        elif "velocity" in ic and "vorticity" not in ic:
+            nodes = self.dom.getAllNodes()
+            vel.setArray(np.tile(np.asarray(ic["velocity"], dtype=np.float64), len(nodes)))
+        self.vort = vort
+
+    def evalRHS(self, ts, t, vort, f):
+        """Evaluate the KLE right-hand side (base_problem.py:111-136):
+        f = Curl( DivSrT( 2 mu SrT u - rho u u^T ) / rho ), u = KLE(vort).
+        As in the reference, the KLE solve uses self.vort (with its boundary
+        values refreshed), not the stage vector `vort`."""
+        self.dom.applyBoundaryConditions(self.vort, "vorticity", t, self.nu)
+        vel = self.solverKLE.getSolution()
+        self.dom.applyBoundaryConditions(vel, "velocity", t, self.nu)
+        self.solverKLE.solve(self.vort)
+        self.computeVtensV(vel)
+        self.operator.SrT.mult(vel, self._Aux1)
+        self._Aux1 *= (2.0 * self.mu)
+        self._Aux1.axpy(-1.0 * self.rho, self._VtensV)
+        rhs = vel.duplicate()
+        self.operator.DivSrT.mult(self._Aux1, rhs)
+        rhs.scale(1 / self.rho)
+        self.operator.Curl.mult(rhs, f)
+
+    def computeVtensV(self, vec):
+        """base_problem.py:138-154 as one device kernel."""
+        call("kle_vec_tensor_square", vec._h, self.dim, self._VtensV._h)
+
+
+class BaseProblemTest(BaseProblem):
+    """Known-answer helpers of the reference's BaseProblemTest (base_problem.py:232-420)."""
+
+    def generateExactVecs(self, vel=None, vort=None, time=None):
+        exactVel = self.mat.K.createVecRight()
+        exactVort = self.mat.Rw.createVecRight()
+        n = len(self.dom.getAllNodes())
+        if vel and vort:
+            arrVel, arrVort = np.tile(vel, n), np.tile(vort, n)
+        else:
+            f = fields.get(self.config["tests"]["custom-func"]["name"])
+            alpha = f.alpha(self.nu, time)
+            coords = self.dom.getFullCoordArray()
+            arrVel, arrVort = f.velocity(coords, alpha), f.vorticity(coords, alpha)
+        exactVort.setArray(np.asarray(arrVort, dtype=np.float64).ravel())
+        exactVel.setArray(np.asarray(arrVel, dtype=np.float64).ravel())
+        return exactVel, exactVort
+
+    def getKLEError(self, viscousTimes=None, startTime=0.0, endTime=1.0, steps=10):
+        if viscousTimes is None:
+            viscousTimes = np.arange(startTime, endTime, (endTime - startTime) / steps)
+        errors = []
+        for time in [(tau ** 2) / (4 * self.nu) for tau in viscousTimes]:
+            exactVel, exactVort = self.generateExactVecs(time=time)
+            self.dom.applyBoundaryConditions(self.vort, "vorticity", time, self.nu)
+            vel = self.solverKLE.getSolution()
+            self.dom.applyBoundaryConditions(vel, "velocity", time, self.nu)
+            self.solverKLE.solve(exactVort)
+            errors.append((exactVel - vel).norm())
+        return errors
+
+    def getConvective(self, exactVel, exactConv):
+        convective = exactConv.copy()
+        vel = self.solverKLE.getSolution()
+        self.computeVtensV(vel)
+        aux = vel.copy()
+        self.operator.DivSrT.mult(self._VtensV, aux)
+        self.operator.Curl.mult(aux, convective)
+        return convective
+
+    def getDiffusive(self, exactVel, exactDiff):
+        diffusive = exactDiff.copy()
+        vel = self.solverKLE.getSolution()
+        self.operator.SrT.mult(exactVel, self._Aux1)
+        aux = vel.copy()
+        self._Aux1 *= (2.0 * self.mu)
+        self.operator.DivSrT.mult(self._Aux1, aux)
+        aux.scale(1 / self.rho)
+        self.operator.Curl.mult(aux, diffusive)
+        return diffusive

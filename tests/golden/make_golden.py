@@ -338,6 +338,16 @@ from boundaries.boundary_conditions import BoundaryConditions  # noqa: E402
 import functions.taylor_green as tg2d  # noqa: E402
 import functions.taylor_green3d as tg3d  # noqa: E402
 
+# BaseProblem.evalRHS (cases/base_problem.py:111-154) is called unbound on a
+# namespace; the module's imports that are not on that path (viewer, TS, DMPlex
+# domain, timers) are replaced by empty modules so it can be imported.
+for _name in ("domain.domain", "viewer.paraviewer", "solver.ts_solver", "common.timer"):
+    _m = types.ModuleType(_name)
+    for _attr in ("Domain", "Paraviewer", "TsSolver", "Timer"):
+        setattr(_m, _attr, object)
+    sys.modules[_name] = _m
+from cases.base_problem import BaseProblem  # noqa: E402
+
 CORNERS = {
     2: [(0, 0), (1, 0), (1, 1), (0, 1)],
     3: [(0, 0, 0), (0, 1, 0), (1, 1, 0), (1, 0, 0),
@@ -540,6 +550,23 @@ def element_fixtures():
     np.savez_compressed(os.path.join(OUT, "elements.npz"), **out)
 
 
+def eval_rhs(dom, mat, solver, vort0, rho, mu, dim, t):
+    """One reference evalRHS call at time t from the initial vorticity."""
+    op = mat.getOperators()
+    ns = types.SimpleNamespace(dom=dom, solverKLE=solver, operator=op, rho=rho, mu=mu, nu=mu / rho,
+                               dim=dim, dim_w=1 if dim == 2 else 3, dim_s=3 if dim == 2 else 6)
+    ns.vort = vort0.copy()
+    ns._VtensV = op.SrT.createVecLeft()
+    ns._Aux1 = ns._VtensV.duplicate()
+    ns.computeVtensV = lambda vec: BaseProblem.computeVtensV(ns, vec)
+    rec = {"rhs_t": t, "rhs_vort_in": ns.vort.a.copy()}
+    f = op.Curl.createVecLeft()
+    BaseProblem.evalRHS(ns, None, t, ns.vort, f)
+    rec.update(rhs_vort_bc=ns.vort.a.copy(), rhs_vel=solver.getSolution().a.copy(), rhs_VtensV=ns._VtensV.a.copy(),
+               rhs_Aux1=ns._Aux1.a.copy(), rhs_f=f.a.copy())
+    return rec
+
+
 def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True):
     lower = [0.0] * dim
     upper = [1.0] * dim
@@ -601,6 +628,9 @@ def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True):
     b = (mat.Rw * vort + mat.Krhs * vel).a.copy()
     solver.solve(vort)
     u = solver.getSolution().a.copy()
+    if ops and not ns:
+        out.update(eval_rhs(dom, mat, solver, vort, rho, mu, dim, 0.25))
+        solver.solve(vort)  # restore the t=0 solution
     out["b"] = b
     out["u"] = u
     out["u_exact"] = u_ex

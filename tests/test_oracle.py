@@ -122,3 +122,36 @@ def test_assembly_and_solve(case):
         assert np.linalg.norm(x - g["u_exact"]) < 1e-12
     if case == "tg2d":
         assert np.linalg.norm(x - g["u_exact"]) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["uniform2d", "tg2d_small", "tg3d", "cavity2d"])
+def test_operators_golden(case):
+    """Operators (mat_fs.py:194-271): pattern bit-exact, values to a few ulps of
+    the reference's assembled Curl / SrT / DivSrT."""
+    g = np.load(os.path.join(G, f"case_{case}.npz"))
+    dim = int(g["dim"])
+    m = O.BoxMesh(dim, list(g["nelem"]), list(g["lower"]), list(g["upper"]), int(g["ngl"]))
+    Cu, S, D, W = m.assemble_ops()
+    for nm, A in (("Curl", Cu), ("SrT", S), ("DivSrT", D)):
+        np.testing.assert_array_equal(A.indptr, g[nm + "_indptr"])
+        np.testing.assert_array_equal(A.indices, g[nm + "_indices"])
+        ref = g[nm + "_data"]
+        assert np.abs(A.data - ref).max() <= 1e-14 * np.abs(ref).max(), nm
+    # lumped weights sum to the domain measure
+    assert abs(W.sum() - np.prod(np.asarray(g["upper"]) - np.asarray(g["lower"]))) < 1e-12
+
+
+@pytest.mark.parametrize("case", ["uniform2d", "tg2d_small", "tg3d"])
+def test_eval_rhs_chain_golden(case):
+    """The operator chain of BaseProblem.evalRHS (base_problem.py:111-136),
+    restated on the oracle's operators, reproduces the reference's own evalRHS
+    output from the same KLE velocity."""
+    g = np.load(os.path.join(G, f"case_{case}.npz"))
+    dim = int(g["dim"])
+    m = O.BoxMesh(dim, list(g["nelem"]), list(g["lower"]), list(g["upper"]), int(g["ngl"]))
+    Cu, S, D, _ = m.assemble_ops()
+    vt, aux, f = O.eval_rhs_chain(Cu, S, D, g["rhs_vel"], float(g["rho"]), float(g["mu"]), dim)
+    np.testing.assert_array_equal(vt, g["rhs_VtensV"])
+    assert np.abs(aux - g["rhs_Aux1"]).max() <= 1e-12 * max(1.0, np.abs(g["rhs_Aux1"]).max())
+    scale = max(1.0, np.abs(g["rhs_f"]).max())
+    assert np.abs(f - g["rhs_f"]).max() <= 1e-10 * scale
