@@ -40,12 +40,66 @@ def parse():
     ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--aij", action="store_true", help="also time the scalar-CSR (aij) SpMV")
     ap.add_argument("--pad", type=int, default=16, help="row padding quantum of K's value streams (blocks)")
+    ap.add_argument("--ops", action="store_true",
+                    help="also assemble Curl/SrT/DivSrT and time their SpMVs and the evalRHS operator chain")
     ap.add_argument("--fused-dot", action="store_true", help="form the CG dot inside the SpMV kernel")
     ap.add_argument("--loads", choices=["nt", "plain"], default="nt", help="SpMV value/column load policy")
     ap.add_argument("--classic-cg", action="store_true",
                     help="two reductions per iteration instead of the single-reduction (Chronopoulos-Gear) CG")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
+
+
+def bench_operators(pa, mat, ctx, sol, dim, reps=20):
+    """Operators row: device assembly time, per-operator SpMV
+    time / useful GB/s, and the evalRHS operator chain (base_problem.py:127-136)
+    after the KLE solve: VtensV, SrT, scale/axpy, DivSrT, scale, Curl."""
+    import numpy as np
+    from pynama_amd._lib import call
+    ctx.synchronize()
+    t = time.perf_counter()
+    mat.buildOperators()
+    ctx.synchronize()
+    out = {"assembly_s": time.perf_counter() - t}
+    op = mat.getOperators()
+    rng = np.random.default_rng(1)
+    for nm in ("Curl", "SrT", "DivSrT"):
+        A = getattr(op, nm)
+        x, y = A.createVecRight(), A.createVecLeft()
+        x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
+        A.mult(x, y)
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        for _ in range(reps):
+            A.mult(x, y)
+        c, ms = ctx.kernel_stats("spmv")
+        ctx.set_profiling(False)
+        nb = A.spmvBytes()
+        out[nm] = {"avg_ms": ms / c, "bytes": nb, "gbps": nb / (ms / c * 1e-3) / 1e9,
+                   "frac": nb / (ms / c * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    vel = sol.getSolution()
+    vt = op.SrT.createVecLeft()
+    aux = vt.duplicate()
+    rhs = vel.duplicate()
+    f = op.Curl.createVecLeft()
+    rho, mu = 0.5, 0.01
+
+    def chain():
+        call("kle_vec_tensor_square", vel._h, dim, vt._h)
+        op.SrT.mult(vel, aux)
+        aux.scale(2.0 * mu)
+        aux.axpy(-rho, vt)
+        op.DivSrT.mult(aux, rhs)
+        rhs.scale(1 / rho)
+        op.Curl.mult(rhs, f)
+    chain()
+    ctx.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        chain()
+    ctx.synchronize()
+    out["evalRHS_chain_ms"] = (time.perf_counter() - t) / reps * 1e3
+    return out
 
 
 def init_dist(n):
@@ -84,7 +138,7 @@ def main():
     mat.setDomain(dom)
     ctx.synchronize()
     t1 = time.perf_counter()
-    mat.build()
+    mat.build(buildOperators=False)
     ctx.synchronize()
     t_asm = time.perf_counter() - t1
     sol = pa.KleSolver()
@@ -201,6 +255,10 @@ def main():
         except Exception:
             traffic = None
 
+    ops = None
+    if args.ops:
+        ops = bench_operators(pa, mat, ctx, sol, dim)
+
     cpu = None
     if rank == 0 and nranks == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(K, b, args.cpu_seconds)
@@ -241,6 +299,7 @@ def main():
             "setup_s": t_setup,
             "solve": solve,
             "aij_spmv": aij,
+            "operators": ops,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

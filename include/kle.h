@@ -222,12 +222,13 @@ int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
  * (64|32|16), block columns per lane in flight (1|2), persistent grid (0|1). */
 int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent);
 /* Non-temporal (nt) loads for the value/column streams of the node-block SpMV
- * (default off: plain loads measured fewer HBM bytes, profiles/r01). */
+ * (default on: fastest together with 128-B row padding, profiles/r01). */
 int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt);
 /* Row padding quantum (in blocks) of node-block matrices created afterwards:
  * every value stream of a row starts on a multiple of `quantum` doubles
  * (16 = one 128-B line) so adjacent streams never share a cache line. */
-int kle_set_nb_pad(int quantum);
+int kle_set_nb_pad(int quantum);  /* default 16 */
+int kle_get_nb_pad(void);
 /* Buffer-descriptor SpMV variants (cache-policy study): 0 off, 1 aux 0, 2 nt,
  * 3 sc0|nt, 4 sc1, 5 sc1|nt, 6 sc1|sc0|nt, 7 sc1|sc0, 8 nt with the x gather
  * dropped (timing diagnostic only: wrong results). */

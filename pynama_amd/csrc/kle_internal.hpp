@@ -138,7 +138,7 @@ struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
     int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
-    int spmv_nt = 0;  // non-temporal value/column loads (plain loads fetch fewer bytes: profiles/r01)
+    int spmv_nt = 1;  // non-temporal value/column loads (fastest with padded rows: profiles/r01)
     int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping
     int spmv_buf = 0;          // buffer-load variant (0 off; cache-policy experiments)
     int spmv_order = 0;        // 0 natural row order, 1 (x,y)-tiled z-columns

@@ -26,7 +26,7 @@
 
 namespace kle {
 
-int g_nb_pad = 1;
+int g_nb_pad = 16;  // 128-B aligned row streams (profiles/r01/spmv_sweep_pad.jsonl)
 
 __device__ __forceinline__ double wsum(double v)
 {
@@ -911,6 +911,8 @@ int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt)
     A->spmv_nt = nt != 0;
     return 0;
 }
+
+int kle_get_nb_pad(void) { return g_nb_pad; }
 
 int kle_set_nb_pad(int quantum)
 {

@@ -190,6 +190,10 @@ def set_row_padding(quantum):
     call("kle_set_nb_pad", int(quantum))
 
 
+def get_row_padding():
+    return int(load().kle_get_nb_pad())
+
+
 def set_ctx(ctx):
     global _CTX
     _CTX = ctx

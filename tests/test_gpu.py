@@ -306,9 +306,10 @@ def test_row_padding_and_nt_loads_are_exact(pa, pad):
     """Padded row streams (every stream 128-B aligned) and non-temporal loads
     change only the memory layout / cache policy: export, diagonal, scaling and
     SpMV must be bit-identical to the unpadded plain-load matrix."""
-    from pynama_amd.runtime import set_row_padding
+    from pynama_amd.runtime import get_row_padding, set_row_padding
     g = _golden("tg3d_p4")
     mats = []
+    old = get_row_padding()
     try:
         for q in (1, pad):
             set_row_padding(q)
@@ -318,8 +319,9 @@ def test_row_padding_and_nt_loads_are_exact(pa, pad):
             mat.build()
             mats.append(mat)
     finally:
-        set_row_padding(1)
+        set_row_padding(old)
     a, b = mats
+    a.K.setSpmvNontemporal(False)
     for nm in ("K", "Krhs", "Rw"):
         for u, v in zip(getattr(a, nm).getValuesCSR(), getattr(b, nm).getValuesCSR()):
             np.testing.assert_array_equal(u, v)
