@@ -137,6 +137,13 @@ int kle_mesh_face_nodes(const kle_mesh *m, unsigned face_mask, int64_t *nodes, i
 /* Dirichlet (free-slip) node set: faces by mask, or explicit global ids. */
 int kle_mesh_set_dirichlet_faces(kle_mesh *m, unsigned face_mask);
 int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n);
+/* No-slip walls (BoundaryConditions.getNoSlipTangDofs / getNoSlipNormalDofs,
+ * boundary_conditions.py:214-241): global velocity DoF ids; a DoF in both
+ * lists is normal (mat_ns.py:60-62).  Their nodes become the fixed nodes. */
+int kle_mesh_set_noslip_dofs(kle_mesh *m, const int64_t *tang, int64_t nt, const int64_t *normal, int64_t nn);
+/* Same, from the no-slip faces (face bits as kle_mesh_set_dirichlet_faces) in
+ * the order the configuration lists them (that order decides corner DoFs). */
+int kle_mesh_set_noslip_faces(kle_mesh *m, const int *faces, int nfaces);
 /* Symbolic node-block pattern (host).  which: 0 K, 1 Krhs, 2 Rw, 3 operators
  * (Curl/SrT/DivSrT: every node x every node sharing a cell).
  * row_ptr[n_owned+1] (block offsets, unpadded) and col[] (global node ids). */
@@ -188,6 +195,13 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
 /* Element matrices of local element e in tensor order (parity tests):
  * K_e [dim n][dim n], Rw_e [dim n][dim_w n] (row-major, n = ngl^dim). */
 int kle_element_kle(kle_ctx *ctx, kle_mesh *m, int64_t e, double *Ke, double *Rwe);
+/* No-slip assembly (replaces MatNS.build / buildNS, mat_ns.py:47-161):
+ * K, Krhs, Rw as kle_assemble_kle on the no-slip nodes, plus Kfs, Krhsfs,
+ * Rwfs with PETSc's DoF-level patterns, and Ksum = K + Kfs (the operator of
+ * KleSolver.solverFS, kle_solver.py:22-28) assembled directly.  Rd / Rdfs are
+ * filled by the reference but read by nothing on the KLE path: not built. */
+int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw, kle_mat **Kfs,
+                    kle_mat **Krhsfs, kle_mat **Rwfs, kle_mat **Ksum);
 /* Operators (replaces MatFS.buildOperators + Operators.setValues/assembleAll,
  * mat_fs.py:194-271, with Spectral.getElemKLEOperators spectral.py:162-228):
  * Curl [dim_w N x dim N], SrT [dim_s N x dim N], DivSrT [dim N x dim_s N],
@@ -199,6 +213,10 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
 int kle_mat_create_aij(kle_ctx *ctx, int64_t m_local, int64_t n_local, int64_t m_global,
                        int64_t n_global, const int32_t *d_nnz, const int32_t *o_nnz,
                        kle_mat **out);
+/* createAIJ(csr=(indptr, indices, data)): assembled scalar CSR (single rank),
+ * strictly ascending columns per row. */
+int kle_mat_create_aij_csr(kle_ctx *ctx, int64_t m, int64_t n, const int64_t *indptr, const int64_t *indices,
+                           const double *data, kle_mat **out);
 int kle_mat_set_values(kle_mat *A, int32_t nr, const int64_t *rows, int32_t nc,
                        const int64_t *cols, const double *v_rowmajor, int addv);
 int kle_mat_assemble(kle_mat *A);

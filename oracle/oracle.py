@@ -182,6 +182,7 @@ class BoxMesh:
 
     def __init__(self, dim, nelem, lower, upper, ngl):
         self.dim, self.ngl = dim, ngl
+        self.nelem = [int(v) for v in nelem]
         self.nn = ngl ** dim
         self._h = lib().orc_mesh_box(dim, np.array(list(nelem) + [1] * (3 - dim), np.int64),
                                      np.array(list(lower) + [0.0] * (3 - dim), float),
@@ -255,3 +256,105 @@ def set_threads(n):
 
 def num_threads():
     return lib().orc_num_threads()
+
+
+# ------------------------------------------------------------------ no-slip
+FACE_AXIS = {"left": (0, 0), "right": (0, 1), "down": (1, 0), "up": (1, 1), "back": (2, 0), "front": (2, 1)}
+
+
+def noslip_dofs(mesh, walls):
+    """Tangential / normal DoF sets of the no-slip walls, in configuration order:
+    Boundary.getTangDofs / getNormalDofs (boundary.py:98-115) collected by
+    BoundaryConditions.getNoSlipTangDofs / getNoSlipNormalDofs(allGather=True)
+    (boundary_conditions.py:205-238, incl. its left/right corner rule)."""
+    dim = mesh.dim
+    L = [int(n) * (mesh.ngl - 1) + 1 for n in mesh.nelem]
+    lat = np.stack(np.meshgrid(*[np.arange(n) for n in L[::-1]], indexing="ij")[::-1], -1).reshape(-1, dim)
+    tang, normal, remove = set(), set(), set()
+    for name in walls:
+        ax, side = FACE_AXIS[name]
+        nodes = np.nonzero(lat[:, ax] == (0 if side == 0 else L[ax] - 1))[0]
+        loc = set((nodes * dim + ax).tolist())
+        if name in ("left", "right"):
+            remove |= {i for i in loc if i + 1 in normal}
+        normal |= loc
+        for t in range(dim):
+            if t != ax:
+                tang |= set((nodes * dim + t).tolist())
+    return tang, normal - remove
+
+
+def _dok_csr(dok, m, n):
+    rows = sorted(dok)
+    ip = np.zeros(m + 1, np.int64)
+    ix, dv = [], []
+    for r in range(m):
+        cols = sorted(dok.get(r, {}))
+        ip[r + 1] = ip[r] + len(cols)
+        ix += cols
+        dv += [dok[r][c] for c in cols]
+    del rows
+    return CSR.from_arrays(ip, np.array(ix, np.int64), np.array(dv, float), n)
+
+
+def assemble_ns(mesh, tang, normal):
+    """MatNS.buildNS (mat_ns.py:47-145) restated on dict-of-keys matrices with
+    PETSc ADD/INSERT semantics, cells ascending (single rank).  Small meshes
+    only.  Returns dict of CSR: K, Krhs, Rw, Kfs, Krhsfs, Rwfs."""
+    dim, nn = mesh.dim, mesh.nn
+    dw = 1 if dim == 2 else 3
+    el = Element(mesh.ngl, dim)
+    conn, X = mesh.conn(), mesh.corners()
+    mats = {k: {} for k in ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs")}
+
+    def add(name, rows, cols, vals, addv=True):
+        d = mats[name]
+        for i, r in enumerate(rows):
+            row = d.setdefault(r, {})
+            for j, c in enumerate(cols):
+                v = vals[i][j] if np.ndim(vals) else vals
+                row[c] = (row.get(c, 0.0) + v) if addv else v
+
+    ind1, ind1fs = set(), set()
+    for e in range(mesh.E):
+        Ke, Rwe, _ = el.kle(X[e].ravel())
+        nodes = conn[e].tolist()
+        iv = [n * dim + d for n in nodes for d in range(dim)]
+        iw = [n * dw + d for n in nodes for d in range(dw)]
+        ivs = set(iv)
+        nd_ = normal & ivs
+        td = (tang & ivs) - nd_
+        gfree = list(ivs - nd_ - td)
+        dfree = [iv.index(i) for i in gfree]
+        lnorm = [iv.index(i) for i in nd_]
+        ltang = [iv.index(i) for i in td]
+        gnorm, gtang = list(nd_), list(td)
+        d2set = list(set(ltang) | set(lnorm))
+        g2set = [iv[i] for i in d2set]
+        if nd_ | td:
+            add("Krhs", gfree, g2set, -Ke[np.ix_(dfree, d2set)])
+            ind1.update(g2set)
+            for i in g2set:
+                add("Krhs", [i], [i], 0.0)
+            add("Kfs", gtang, gfree, Ke[np.ix_(ltang, dfree)])
+            add("Kfs", gfree, gtang, Ke[np.ix_(dfree, ltang)])
+            add("Kfs", gtang, gtang, Ke[np.ix_(ltang, ltang)])
+            ind1fs.update(gtang)
+            add("Rwfs", gtang, iw, Rwe[ltang, :])
+            add("Krhsfs", gtang, gnorm, -Ke[np.ix_(ltang, lnorm)])
+            add("Krhsfs", gfree, gnorm, -Ke[np.ix_(dfree, lnorm)])
+            for i in gnorm:
+                add("Krhsfs", [i], [i], 0.0)
+        add("K", gfree, gfree, Ke[np.ix_(dfree, dfree)])
+        for i in g2set:
+            add("K", [i], [i], 0.0)
+        add("Rw", gfree, iw, Rwe[np.ix_(dfree, range(len(iw)))])
+    for i in ind1:  # setIndices2One (mat_fs.py:115-120)
+        add("Krhs", [i], [i], 1.0)
+        add("K", [i], [i], 1.0)
+    for i in ind1fs:
+        add("Kfs", [i], [i], -1.0)
+    for i in ind1 - ind1fs:
+        add("Krhsfs", [i], [i], 1.0, addv=False)
+    n = mesh.N * dim
+    return {k: _dok_csr(v, n, mesh.N * dw if k in ("Rw", "Rwfs") else n) for k, v in mats.items()}

@@ -6,7 +6,7 @@ and the petsc4py Mat/Vec/KSP objects they use; the compute runs in libkle.so
 """
 from ._lib import Error, load  # noqa: F401
 from .domain import Domain  # noqa: F401
-from .matrices import MatFS, Operators  # noqa: F401
+from .matrices import MatFS, MatNS, Operators  # noqa: F401
 from .problem import BaseProblem, BaseProblemTest  # noqa: F401
 from .mesh import BoxMesh  # noqa: F401
 from .runtime import COMM_WORLD, get_ctx, finalize  # noqa: F401

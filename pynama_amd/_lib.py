@@ -64,6 +64,8 @@ _SIGS = {
     "kle_mesh_get_coords": [vp, f64p],
     "kle_mesh_face_nodes": [vp, C.c_uint, vp, C.POINTER(C.c_int64)],
     "kle_mesh_set_dirichlet_faces": [vp, C.c_uint],
+    "kle_mesh_set_noslip_dofs": [vp, i64p, C.c_int64, i64p, C.c_int64],
+    "kle_mesh_set_noslip_faces": [vp, i32p, C.c_int],
     "kle_mesh_set_dirichlet_nodes": [vp, i64p, C.c_int64],
     "kle_mesh_pattern_size": [vp, C.c_int, C.POINTER(C.c_int64)],
     "kle_mesh_pattern": [vp, C.c_int, i64p, vp],
@@ -95,7 +97,9 @@ _SIGS = {
     "kle_assemble_kle": [vp, vp, pvp, pvp, pvp],
     "kle_element_kle": [vp, vp, C.c_int64, f64p, f64p],
     "kle_assemble_operators": [vp, vp, pvp, pvp, pvp],
+    "kle_assemble_ns": [vp, vp, pvp, pvp, pvp, pvp, pvp, pvp, pvp],
     "kle_mat_create_aij": [vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp, vp, pvp],
+    "kle_mat_create_aij_csr": [vp, C.c_int64, C.c_int64, i64p, i64p, f64p, pvp],
     "kle_mat_set_values": [vp, C.c_int32, i64p, C.c_int32, i64p, f64p, C.c_int],
     "kle_mat_assemble": [vp],
     "kle_mat_destroy": [vp],

@@ -656,6 +656,96 @@ __global__ __launch_bounds__(256) void k_ops_gather(MeshDev M, int64_t nrows, co
     }
 }
 
+
+// ---------------------------------------------------------------- no-slip
+// MatNS.buildNS (mat_ns.py:47-145) on the device.  DoF classes F (free),
+// T (tangential), N (normal) per velocity DoF (ext range, cls[]).  Per entry
+// (row DoF r, col DoF c) the ascending-cell sum S of the element blocks:
+//   MODE 3 Kfs    : S on (T,F),(F,T),(T,T); T diagonal S + (-1)   (:104-116,124-125)
+//   MODE 4 Krhsfs : -S on (F|T, N); N diagonal 1 (INSERT)        (:118-122,130-131)
+//   MODE 5 Rwfs   : S of Rw_e on T rows                          (:110-111)
+//   MODE 6 K+Kfs  : S on (F|T, F|T); T diagonal 1 + (S + (-1)); N diagonal 1
+//                   (the matrix KleSolver.setUp hands to solverFS, kle_solver.py:25)
+// Entries outside those sets are stored as exact zeros (node blocks) and
+// left out of the exported CSR (kle_mat.mask_rule).
+template <int R, int C, int MODE>
+__global__ __launch_bounds__(256) void k_gather_ns(MeshDev M, int64_t nrows, const int *__restrict__ rowptr,
+                                                   const int *__restrict__ rowcnt, const int *__restrict__ bcol,
+                                                   const uint8_t *__restrict__ cls, const double *__restrict__ Eblk,
+                                                   double *__restrict__ val)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (row >= nrows) return;
+    const int64_t gi = M.node_begin + row, il = gi - M.ext_begin;
+    const int b0 = rowptr[row], mp = rowptr[row + 1] - b0, m = rowcnt ? rowcnt[row] : mp;
+    double *v = val + (int64_t)b0 * R * C;
+    int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], M.dim == 3 ? gi / (M.L[0] * M.L[1]) : 0};
+    int64_t elo[3], ehi[3];
+    for (int d = 0; d < 3; ++d) {
+        if (d >= M.dim) {
+            elo[d] = ehi[d] = 0;
+            continue;
+        }
+        const int64_t c = ci[d];
+        elo[d] = (c % M.p == 0) ? max((int64_t)0, c / M.p - 1) : c / M.p;
+        ehi[d] = min(M.nel[d] - 1, c / M.p);
+    }
+    const int ngl = M.ngl, ne = M.ne;
+    for (int k = lane; k < m; k += 64) {
+        const int64_t jl = bcol[b0 + k], gj = M.ext_begin + jl;
+        int64_t cj[3] = {gj % M.L[0], (gj / M.L[0]) % M.L[1], M.dim == 3 ? gj / (M.L[0] * M.L[1]) : 0};
+        double acc[R * C];
+#pragma unroll
+        for (int t = 0; t < R * C; ++t) acc[t] = 0.0;
+        for (int64_t ez = elo[2]; ez <= ehi[2]; ++ez)
+            for (int64_t ey = elo[1]; ey <= ehi[1]; ++ey)
+                for (int64_t ex = elo[0]; ex <= ehi[0]; ++ex) {
+                    const int64_t eo[3] = {ex * M.p, ey * M.p, ez * M.p};
+                    bool in = true;
+                    int oj[3] = {0, 0, 0}, oi[3] = {0, 0, 0};
+                    for (int d = 0; d < M.dim; ++d) {
+                        const int64_t o = cj[d] - eo[d];
+                        in = in && o >= 0 && o <= M.p;
+                        oj[d] = (int)o;
+                        oi[d] = (int)(ci[d] - eo[d]);
+                    }
+                    if (!in) continue;
+                    const int64_t e = ex + M.nel[0] * (ey + M.nel[1] * ez) - M.elem_begin;
+                    const int li = oi[0] + ngl * (oi[1] + ngl * oi[2]);
+                    const int lj = oj[0] + ngl * (oj[1] + ngl * oj[2]);
+                    const double *blk = Eblk + ((e * ne + li) * (int64_t)ne + lj) * (R * C);
+#pragma unroll
+                    for (int t = 0; t < R * C; ++t) acc[t] += (MODE == 4) ? -blk[t] : blk[t];
+                }
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < C; ++b) {
+                const int rc = cls[il * R + a];
+                const int cc = MODE == 5 ? DOF_FREE : cls[jl * C + b];
+                const bool diag = jl == il && a == b;
+                const int rule = MODE == 3 ? MASK_KFS : MODE == 4 ? MASK_KRHSFS : MODE == 5 ? MASK_TANG_ROWS : MASK_KSUM;
+                double out = mask_entry(rule, rc, cc, diag) ? acc[a * C + b] : 0.0;
+                if (diag) {
+                    if (MODE == 3 && rc == DOF_TANG) out = acc[a * C + b] + (-1.0);
+                    if (MODE == 4 && rc == DOF_NORMAL) out = 1.0;
+                    if (MODE == 6 && rc == DOF_TANG) out = 1.0 + (acc[a * C + b] + (-1.0));
+                    if (MODE == 6 && rc == DOF_NORMAL) out = 1.0;
+                }
+                v[(a * C + b) * (int64_t)mp + k] = out;
+            }
+    }
+}
+
+template <int R, int C, int MODE>
+static void launch_gather_ns(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint8_t *cls, const double *E)
+{
+    const int64_t threads = A->nrows * 64;
+    hipLaunchKernelGGL((k_gather_ns<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
+                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, cls, E, A->d_val);
+}
+
 template <int R, int C, int MODE>
 static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint8_t *dir, const double *E)
 {
@@ -763,6 +853,57 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
     *Curl = mc;
     *SrT = ms;
     *DivSrT = md;
+    return 0;
+}
+
+int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw, kle_mat **Kfs,
+                    kle_mat **Krhsfs, kle_mat **Rwfs, kle_mat **Ksum)
+{
+    KLE_ARG(ctx && m && K && Krhs && Rw && Kfs && Krhsfs && Rwfs && Ksum, "null arg");
+    KLE_ARG(m->rank == ctx->rank && m->nranks == ctx->nranks, "mesh partition does not match ctx");
+    KLE_ARG(!m->dof_cls.empty(), "no-slip DoFs not set (kle_mesh_set_noslip_dofs)");
+    // K, Krhs, Rw of MatNS are the free-slip ones with the no-slip nodes fixed
+    // (mat_ns.py:124-141 + setIndices2One)
+    KLE_TRY(kle_assemble_kle(ctx, m, K, Krhs, Rw));
+    const int dim = m->dim, dw = dim == 2 ? 1 : 3;
+    kle_mat *mf = nullptr, *mr = nullptr, *mw = nullptr, *ms = nullptr;
+    KLE_TRY(nb_create(ctx, m, 4, dim, dim, &mf));
+    KLE_TRY(nb_create(ctx, m, 5, dim, dim, &mr));
+    KLE_TRY(nb_create(ctx, m, 6, dim, dw, &mw));
+    KLE_TRY(nb_create(ctx, m, 3, dim, dim, &ms));
+    const int rules[4] = {MASK_KFS, MASK_KRHSFS, MASK_TANG_ROWS, MASK_KSUM};
+    kle_mat *all[4] = {mf, mr, mw, ms};
+    for (int t = 0; t < 4; ++t) {
+        all[t]->mask_rule = rules[t];
+        all[t]->dof_cls = m->dof_cls;
+        all[t]->diag_only_row.assign(all[t]->nrows, 0);
+    }
+    double *dKe = nullptr, *dRwe = nullptr;
+    KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe));
+    uint8_t *dcls = nullptr;
+    KLE_HIP(hipMalloc(&dcls, m->dof_cls.size()));
+    KLE_HIP(hipMemcpyAsync(dcls, m->dof_cls.data(), m->dof_cls.size(), hipMemcpyHostToDevice, ctx->stream));
+    MeshDev M = mesh_dev(m);
+    if (dim == 3) {
+        launch_gather_ns<3, 3, 3>(ctx, M, mf, dcls, dKe);
+        launch_gather_ns<3, 3, 4>(ctx, M, mr, dcls, dKe);
+        launch_gather_ns<3, 3, 5>(ctx, M, mw, dcls, dRwe);
+        launch_gather_ns<3, 3, 6>(ctx, M, ms, dcls, dKe);
+    } else {
+        launch_gather_ns<2, 2, 3>(ctx, M, mf, dcls, dKe);
+        launch_gather_ns<2, 2, 4>(ctx, M, mr, dcls, dKe);
+        launch_gather_ns<2, 1, 5>(ctx, M, mw, dcls, dRwe);
+        launch_gather_ns<2, 2, 6>(ctx, M, ms, dcls, dKe);
+    }
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    hipFree(dKe);
+    hipFree(dRwe);
+    hipFree(dcls);
+    *Kfs = mf;
+    *Krhsfs = mr;
+    *Rwfs = mw;
+    *Ksum = ms;
     return 0;
 }
 

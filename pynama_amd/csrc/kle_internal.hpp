@@ -107,6 +107,9 @@ struct kle_mesh {
     int64_t elem_layer = 1;  // elements per layer of the partition axis
     std::vector<uint8_t> dir;  // Dirichlet flag per ext node (index - ext_begin)
     bool dir_set = false;
+    // no-slip: class of every velocity DoF of the ext range (DOF_FREE /
+    // DOF_TANG / DOF_NORMAL, mat_ns.py:58-70); empty for free-slip meshes
+    std::vector<uint8_t> dof_cls;
     int halo_lo_rank = -1, halo_hi_rank = -1;
     int64_t halo_lo_nodes = 0, halo_hi_nodes = 0;   // ghost nodes received
     int64_t send_lo_nodes = 0, send_hi_nodes = 0;   // owned nodes sent to neighbours
@@ -157,6 +160,10 @@ struct kle_mat {
     int *d_bcol = nullptr;     // [nblocks] local ext node index
     double *d_val = nullptr;   // [nblocks*R*C], per row SoA [a][b][k]
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
+    // export: DoF-level entry rule inside the node blocks (no-slip matrices,
+    // MASK_* below) and the ext-range DoF classes it reads
+    int mask_rule = 0;
+    std::vector<uint8_t> dof_cls;
     // halo plan of the column space
     int lo_rank = -1, hi_rank = -1;
     int64_t ghost_lo = 0, ghost_hi = 0, send_lo = 0, send_hi = 0;  // entries
@@ -191,5 +198,18 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
          int *nparts, const int *istate);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
-extern int g_nb_pad;  // row padding quantum (blocks) of new node-block matrices
+extern int g_nb_pad;
+enum DofClass : uint8_t { DOF_FREE = 0, DOF_TANG = 1, DOF_NORMAL = 2 };
+// which PETSc entries of a node block exist (MatNS.buildNS, mat_ns.py:47-145)
+enum MaskRule { MASK_NONE = 0, MASK_KFS = 1, MASK_KRHSFS = 2, MASK_TANG_ROWS = 3, MASK_KSUM = 4 };
+__host__ __device__ inline bool mask_entry(int rule, int rc, int cc, bool diag)
+{
+    switch (rule) {
+    case MASK_KFS: return (rc == DOF_TANG && cc != DOF_NORMAL) || (rc == DOF_FREE && cc == DOF_TANG);
+    case MASK_KRHSFS: return rc == DOF_NORMAL ? diag : cc == DOF_NORMAL;
+    case MASK_TANG_ROWS: return rc == DOF_TANG;
+    case MASK_KSUM: return rc == DOF_NORMAL ? diag : cc != DOF_NORMAL;
+    default: return true;
+    }
+}  // row padding quantum (blocks) of new node-block matrices
 }  // namespace kle

@@ -493,6 +493,17 @@ static int check_mult_layout(const kle_mat *A, const kle_vec *x, const kle_vec *
 }
 
 // host copy of an nb matrix
+// Does PETSc hold entry (row node i (owned-local), comp a) x (col node jl
+// (ext-local), comp b)?  No-slip matrices keep DoF-level patterns.
+static bool nb_entry_exists(const kle_mat *A, int64_t i, int a, int64_t jl, int b)
+{
+    if (A->mask_rule == MASK_NONE) return true;
+    const int64_t il = A->node_begin - A->ext_begin + i;
+    const int rc = A->dof_cls[il * A->R + a];
+    const int cc = A->mask_rule == MASK_TANG_ROWS ? DOF_FREE : A->dof_cls[jl * A->C + b];
+    return mask_entry(A->mask_rule, rc, cc, jl == il && a == b);
+}
+
 struct NBHost {
     std::vector<int> rp, bc, cnt;
     std::vector<double> v;
@@ -561,6 +572,36 @@ int kle_mat_create_aij(kle_ctx *ctx, int64_t m_local, int64_t n_local, int64_t m
     A->stash.resize(m_local);
     if (d_nnz) A->d_nnz_hint.assign(d_nnz, d_nnz + m_local);
     (void)o_nnz;
+    *out = A;
+    return 0;
+}
+
+int kle_mat_create_aij_csr(kle_ctx *ctx, int64_t m, int64_t n, const int64_t *indptr, const int64_t *indices,
+                           const double *data, kle_mat **out)
+{
+    KLE_ARG(ctx && indptr && out, "null arg");
+    KLE_ARG(indptr[0] == 0, "indptr[0] must be 0");
+    for (int64_t r = 0; r < m; ++r) {
+        KLE_ARG(indptr[r + 1] >= indptr[r], "indptr not monotone at row %lld", (long long)r);
+        for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k) {
+            KLE_ARG(indices[k] >= 0 && indices[k] < n, "column %lld out of range", (long long)indices[k]);
+            KLE_ARG(k == indptr[r] || indices[k] > indices[k - 1], "columns of row %lld not strictly ascending",
+                    (long long)r);
+        }
+    }
+    kle_mat *A;
+    KLE_TRY(kle_mat_create_aij(ctx, m, n, m, n, nullptr, nullptr, &A));
+    const int64_t z = indptr[m];
+    A->h_ptr.assign(indptr, indptr + m + 1);
+    A->h_col.assign(indices, indices + z);
+    A->h_val.assign(data, data + z);
+    A->assembled = true;
+    A->stash.clear();
+    int rc = aij_upload(A);
+    if (rc) {
+        kle_mat_destroy(A);
+        return rc;
+    }
     *out = A;
     return 0;
 }
@@ -762,6 +803,17 @@ int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz)
         *nnz = A->assembled ? A->nnz : 0;
         return 0;
     }
+    if (A->mask_rule != MASK_NONE) {
+        NBHost h;
+        KLE_TRY(nb_download(A, h));
+        int64_t z = 0;
+        for (int64_t i = 0; i < A->nrows; ++i)
+            for (int a = 0; a < A->R; ++a)
+                for (int k = 0; k < h.cnt[i]; ++k)
+                    for (int b = 0; b < A->C; ++b) z += nb_entry_exists(A, i, a, h.bc[h.rp[i] + k], b);
+        *nnz = z;
+        return 0;
+    }
     std::vector<int> rp(A->nrows + 1), cnt(A->nrows);
     KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToHost));
     if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * A->nrows, hipMemcpyDeviceToHost));
@@ -801,6 +853,7 @@ int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double 
             } else {
                 for (int k = 0; k < m; ++k)
                     for (int b = 0; b < C; ++b) {
+                        if (A->mask_rule != MASK_NONE && !nb_entry_exists(A, i, a, h.bc[b0 + k], b)) continue;
                         indices[z] = (A->ext_begin + h.bc[b0 + k]) * C + b;
                         data[z++] = v[(int64_t)(a * C + b) * mp + k];
                     }

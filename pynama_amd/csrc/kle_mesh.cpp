@@ -49,13 +49,16 @@ inline bool is_dir(const kle_mesh *m, int64_t node) { return m->dir[node - m->ex
 
 // which: 0 K (free x free, Dirichlet rows diagonal), 1 Krhs (free x Dirichlet,
 // Dirichlet rows diagonal), 2 Rw (free x all, Dirichlet rows empty),
-// 3 operators Curl/SrT/DivSrT (all x all, mat_fs.py:215-236).
+// 3 operators Curl/SrT/DivSrT (all x all, mat_fs.py:215-236); no-slip
+// (dir = no-slip nodes): 4 Kfs (free rows x no-slip nodes, no-slip rows x all),
+// 5 Krhsfs (all rows x no-slip nodes), 6 Rwfs (no-slip rows x all), mat_ns.py:7-45,86-122.
 // Enumerates the columns of owned node row i in ascending order.
 template <class F>
 static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
 {
-    const bool di = which != 3 && is_dir(m, i);
-    if (di) {
+    const bool di = is_dir(m, i);
+    if (which == 6 && !di) return;
+    if (which <= 2 && di) {
         if (which != 2) emit(i);
         return;
     }
@@ -67,7 +70,15 @@ static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
         for (q[1] = lo[1]; q[1] <= hi[1]; ++q[1])
             for (q[0] = lo[0]; q[0] <= hi[0]; ++q[0]) {
                 int64_t j = m->id_of(q);
-                if (which >= 2 || (which == 0) == !is_dir(m, j)) emit(j);
+                bool keep;
+                switch (which) {
+                case 0: keep = !is_dir(m, j); break;
+                case 1: keep = is_dir(m, j); break;
+                case 4: keep = di || is_dir(m, j); break;
+                case 5: keep = is_dir(m, j); break;
+                default: keep = true;  // 2, 3, 6
+                }
+                if (keep) emit(j);
             }
 }
 
@@ -292,9 +303,67 @@ int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n)
     return 0;
 }
 
+int kle_mesh_set_noslip_dofs(kle_mesh *m, const int64_t *tang, int64_t nt, const int64_t *normal, int64_t nnorm)
+{
+    KLE_ARG(m && (nt == 0 || tang) && (nnorm == 0 || normal), "null arg");
+    const int64_t next = m->ext_end - m->ext_begin, d0 = m->ext_begin * m->dim, d1 = m->ext_end * m->dim;
+    m->dof_cls.assign(next * m->dim, DOF_FREE);
+    std::fill(m->dir.begin(), m->dir.end(), 0);
+    auto mark = [&](const int64_t *dofs, int64_t n, uint8_t c) -> int {
+        for (int64_t k = 0; k < n; ++k) {
+            if (dofs[k] < 0 || dofs[k] >= m->N * m->dim) return fail(KLE_ERR_OUTOFRANGE, "dof %lld", (long long)dofs[k]);
+            if (dofs[k] < d0 || dofs[k] >= d1) continue;
+            // a DoF both normal and tangential is normal (mat_ns.py:60-62)
+            uint8_t &slot = m->dof_cls[dofs[k] - d0];
+            slot = std::max(slot, c);
+            m->dir[dofs[k] / m->dim - m->ext_begin] = 1;
+        }
+        return 0;
+    };
+    KLE_TRY(mark(tang, nt, DOF_TANG));
+    KLE_TRY(mark(normal, nnorm, DOF_NORMAL));
+    m->dir_set = true;
+    return 0;
+}
+
+int kle_mesh_set_noslip_faces(kle_mesh *m, const int *faces, int nfaces)
+{
+    KLE_ARG(m && (nfaces == 0 || faces), "null arg");
+    int axes[6];
+    for (int k = 0; k < nfaces; ++k) {
+        int side;
+        if (!face_axis(m->dim, faces[k], axes[k], side)) return fail(KLE_ERR_ARG, "bad face %d", faces[k]);
+    }
+    const int64_t next = m->ext_end - m->ext_begin;
+    m->dof_cls.assign(next * m->dim, DOF_FREE);
+    for (int64_t i = 0; i < next; ++i) {
+        const int64_t node = m->ext_begin + i;
+        bool normal[3] = {false, false, false}, tang[3] = {false, false, false}, drop_x = false, y_normal = false;
+        bool on_any = false;
+        for (int k = 0; k < nfaces; ++k) {
+            if (!on_faces(m, node, 1u << faces[k])) continue;
+            on_any = true;
+            // getNoSlipNormalDofs(allGather=True) (boundary_conditions.py:222-238): a
+            // left/right x-normal DoF is dropped when the node's y DoF is already
+            // normal from an earlier (up/down) wall
+            if (axes[k] == 0 && y_normal) drop_x = true;
+            normal[axes[k]] = true;
+            if (axes[k] == 1) y_normal = true;
+            for (int d = 0; d < m->dim; ++d)
+                if (d != axes[k]) tang[d] = true;
+        }
+        if (drop_x) normal[0] = false;
+        for (int d = 0; d < m->dim; ++d)
+            m->dof_cls[i * m->dim + d] = normal[d] ? DOF_NORMAL : tang[d] ? DOF_TANG : DOF_FREE;
+        m->dir[i] = on_any;
+    }
+    m->dir_set = true;
+    return 0;
+}
+
 int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks)
 {
-    KLE_ARG(m && nblocks && which >= 0 && which <= 3, "bad arg");
+    KLE_ARG(m && nblocks && which >= 0 && which <= 6, "bad arg");
     int64_t tot = 0;
     for (int64_t i = m->node_begin; i < m->node_end; ++i) row_cols(m, which, i, [&](int64_t) { ++tot; });
     *nblocks = tot;
@@ -303,7 +372,7 @@ int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks)
 
 int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *cols)
 {
-    KLE_ARG(m && row_ptr && which >= 0 && which <= 3, "bad arg");
+    KLE_ARG(m && row_ptr && which >= 0 && which <= 6, "bad arg");
     int64_t k = 0;
     row_ptr[0] = 0;
     for (int64_t i = m->node_begin; i < m->node_end; ++i) {

@@ -102,14 +102,27 @@ class Domain:
                     self._bcs.append(_Boundary(n, "free-slip", dict(v)))
                 else:
                     self._bcs.append(_Boundary(n, "free-slip", {"velocity": v}))
+        elif "no-slip" in bc and "free-slip" not in bc:
+            # walls with constant velocity (BoundaryConditions.__setBoundary,
+            # boundary_conditions.py:115-136); dict order = processing order
+            self._type = "NS"
+            zero_w = [0] if self.dim == 2 else [0, 0, 0]
+            for n, v in bc["no-slip"].items():
+                vals = dict(v) if isinstance(v, dict) else {"velocity": v}
+                vals.setdefault("vorticity", zero_w)
+                self._bcs.append(_Boundary(n, "no-slip", vals))
         else:
-            # no-slip walls (MatNS, mat_ns.py) are the next row of the scope table
-            raise NotImplementedError("no-slip boundary conditions (MatNS) are not provided yet")
+            # mixed free-slip + no-slip: the reference has no matrix for it either
+            # (base_problem.py:161-162, "FSNS Mat not implemented")
+            raise NotImplementedError("mixed free-slip / no-slip boundaries (FS-NS)")
         for b in self._bcs:
             b.nodes = self.mesh.face_nodes([b.name])
             lo = self.mesh.node_range[0]
             b.coords = self._coords[b.nodes - lo] if len(b.nodes) else np.zeros((0, self.dim))
-        self.mesh.set_dirichlet_faces([b.name for b in self._bcs])
+        if self._type == "NS":
+            self.mesh.set_noslip_faces([b.name for b in self._bcs])
+        else:
+            self.mesh.set_dirichlet_faces([b.name for b in self._bcs])
 
     # ------------------------------------------------------------ queries
     def getMesh(self):
@@ -149,10 +162,42 @@ class Domain:
     def getBorderNodes(self, name):
         return self.mesh.face_nodes([name])
 
+    # no-slip DoF sets (BoundaryConditions.getNoSlip*, boundary_conditions.py:205-238)
+    _AXIS = {"left": 0, "right": 0, "up": 1, "down": 1, "front": 2, "back": 2}
+
+    def _ns(self):
+        return [b for b in self._bcs if b.kind == "no-slip"]
+
+    def getNodesNoSlip(self, collect=False):
+        nodes = set()
+        for b in self._ns():
+            nodes |= set(b.nodes.tolist())
+        return nodes
+
+    def getTangDofs(self, collect=False):
+        dofs = set()
+        for b in self._ns():
+            ax = self._AXIS[b.name]
+            for t in range(self.dim):
+                if t != ax:
+                    dofs |= set((b.nodes * self.dim + t).tolist())
+        return dofs
+
+    def getNormalDofs(self, collect=False):
+        dofs, remove = set(), set()
+        for b in self._ns():
+            ax = self._AXIS[b.name]
+            loc = set((b.nodes * self.dim + ax).tolist())
+            if collect and b.name in ("left", "right"):
+                remove |= {i for i in loc if i + 1 in dofs}
+            dofs |= loc
+        return dofs - remove
+
     def getNodesDirichlet(self, collect=False):
         nodes = set()
         for b in self._bcs:
-            nodes |= set(b.nodes.tolist())
+            if b.kind == "free-slip":
+                nodes |= set(b.nodes.tolist())
         return nodes
 
     # -------------------------------------------------------------- BCs
@@ -168,4 +213,17 @@ class Domain:
                 comps = self.dim
                 inds = (b.nodes[:, None] * comps + np.arange(comps)[None, :]).ravel()
             vec.setValues(inds, vals, addv=False)
+        vec.assemble()
+
+    def applyBoundaryConditionsNS(self, vec, varName, t=None, nu=None):
+        """BoundaryConditions.setTangentialValuesToVec (boundary_conditions.py:262-278):
+        the tangential wall velocity on every no-slip wall."""
+        for b in self._ns():
+            if len(b.nodes) == 0:
+                continue
+            vel = np.asarray(b.values["velocity"], dtype=np.float64)
+            ax = self._AXIS[b.name]
+            for t_ in range(self.dim):
+                if t_ != ax:
+                    vec.setValues(b.nodes * self.dim + t_, np.repeat(vel[t_], len(b.nodes)), addv=False)
         vec.assemble()

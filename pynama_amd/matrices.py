@@ -59,6 +59,45 @@ class MatFS:
         pass
 
 
+class MatNS(MatFS):
+    """Mirror of the reference's MatNS (matrices/mat_ns.py:5-161): no-slip walls.
+    K, Krhs, Rw fix the no-slip nodes; Kfs, Krhsfs, Rwfs free their tangential
+    DoFs for the free-slip pre-solve (solveFS).  One device pass
+    (kle_assemble_ns) with PETSc's DoF-level patterns; K + Kfs, the operator of
+    KleSolver.solverFS, is assembled directly (getKplusKfs).  Rd / Rdfs are
+    filled by the reference but read by nothing downstream: left as None."""
+    bcType = "NS"
+
+    def __init__(self):
+        super().__init__()
+        self.Kfs = self.Krhsfs = self.Rwfs = self.Rdfs = None
+        self._Ksum = None
+
+    def build(self, buildKLE=True, buildOperators=True):
+        if self.dom.getBoundaryType() != "NS":
+            raise Error(56, "MatNS needs no-slip boundaries")
+        if buildKLE:
+            self.buildNS()
+        if buildOperators:
+            self.buildOperators()
+
+    def buildNS(self):
+        ctx = get_ctx()
+        mesh = self.dom.getMesh()
+        h = [C.c_void_p() for _ in range(7)]
+        call("kle_assemble_ns", ctx.h, mesh._h, *[C.byref(x) for x in h])
+        dim, dim_w, _ = self.dom.getDimensions()
+        shapes = [(dim, dim), (dim, dim), (dim, dim_w), (dim, dim), (dim, dim), (dim, dim_w), (dim, dim)]
+        mats = [Mat._wrap(x, ctx, mesh, r, c) for x, (r, c) in zip(h, shapes)]
+        self.K, self.Krhs, self.Rw, self.Kfs, self.Krhsfs, self.Rwfs, self._Ksum = mats
+        for m, n in zip(mats, ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs", "K+Kfs")):
+            m.setName(n)
+        self.kle = mats[:6]
+
+    def getKplusKfs(self):
+        return self._Ksum
+
+
 class Operators:
     """Mirror of the reference's Operators (mat_fs.py:211-271): the collocation
     operators Curl [dim_w N x dim N], SrT [dim_s N x dim N] and DivSrT

@@ -89,6 +89,11 @@ class BoxMesh:
     def set_dirichlet_faces(self, names):
         call("kle_mesh_set_dirichlet_faces", self._h, self.face_mask(names))
 
+    def set_noslip_faces(self, names):
+        """No-slip walls, in configuration order (fixes the corner DoF classes)."""
+        faces = np.array([FACES[self.dim].index(n) for n in names], dtype=np.int32)
+        call("kle_mesh_set_noslip_faces", self._h, faces if len(faces) else np.zeros(1, np.int32), len(faces))
+
     def set_dirichlet_nodes(self, nodes):
         nodes = np.ascontiguousarray(np.asarray(sorted(nodes), dtype=np.int64))
         call("kle_mesh_set_dirichlet_nodes", self._h, nodes if len(nodes) else np.zeros(1, np.int64),

@@ -309,6 +309,13 @@ class Mat:
             ml = mg
         if nl is None:
             nl = ng
+        if csr is not None:
+            ip, ix, v = (np.ascontiguousarray(np.asarray(a, dtype=t)) for a, t in zip(csr, (np.int64, np.int64, np.float64)))
+            h = C.c_void_p()
+            call("kle_mat_create_aij_csr", ctx.h, int(ml), int(nl), ip, ix if len(ix) else np.zeros(1, np.int64),
+                 v if len(v) else np.zeros(1), C.byref(h))
+            self._h, self._ctx = h, ctx
+            return self
         d = None
         if nnz is not None:
             dn = nnz[0] if isinstance(nnz, (tuple, list)) else nnz
@@ -444,9 +451,33 @@ class Mat:
         call("kle_mat_axpy", self._h, float(alpha), X._h)
 
     def __add__(self, other):
-        out = self.duplicate(copy=True)
-        out.axpy(1.0, other)
-        return out
+        """Mat + Mat.  Same pattern: device axpy.  Different patterns: PETSc's
+        MatAXPY(DIFFERENT_NONZERO_PATTERN) on the union of the two CSR
+        patterns (y + 1*x where both exist), as a device AIJ matrix."""
+        try:
+            out = self.duplicate(copy=True)
+            out.axpy(1.0, other)
+            return out
+        except Error:
+            pass
+        a, b = self.getValuesCSR(), other.getValuesCSR()
+        m = len(a[0]) - 1
+        rows = np.concatenate([np.repeat(np.arange(m), np.diff(a[0])), np.repeat(np.arange(m), np.diff(b[0]))])
+        cols = np.concatenate([a[1], b[1]])
+        vals = np.concatenate([a[2], 1.0 * b[2]])
+        first = np.concatenate([np.ones(len(a[1]), bool), np.zeros(len(b[1]), bool)])
+        order = np.lexsort((~first, cols, rows))  # per (row, col): Y's entry first, then X's
+        rows, cols, vals = rows[order], cols[order], vals[order]
+        key = np.ones(len(rows), bool)
+        key[1:] = (rows[1:] != rows[:-1]) | (cols[1:] != cols[:-1])
+        grp = np.cumsum(key) - 1
+        out_v = np.zeros(key.sum())
+        np.add.at(out_v, grp, vals)  # y + x, in that order (at most two terms)
+        ip = np.zeros(m + 1, np.int64)
+        np.add.at(ip, rows[key] + 1, 1)
+        ip = np.cumsum(ip)
+        _, n = self.getSize()
+        return Mat().createAIJ(((m, m), (n, n)), csr=(ip, cols[key], out_v))
 
     def convert(self, mat_type="aij"):
         if mat_type not in ("aij", "seqaij", "mpiaij"):

@@ -14,7 +14,7 @@ import numpy as np
 from . import fields
 from ._lib import call
 from .domain import Domain
-from .matrices import MatFS
+from .matrices import MatFS, MatNS
 from .solver import KleSolver
 
 
@@ -48,9 +48,13 @@ class BaseProblem:
 
     def setUpSolver(self):
         """base_problem.py:156-179 (free-slip / Dirichlet boundaries)."""
-        if self.dom.getBoundaryType() != "FS":
-            raise NotImplementedError("no-slip (MatNS) is the next row of the scope table")
-        mat = MatFS()
+        bcType = self.dom.getBoundaryType()
+        if bcType == "FS":
+            mat = MatFS()
+        elif bcType == "NS":
+            mat = MatNS()
+        else:
+            raise Exception("FSNS Mat not implemented")
         mat.setDomain(self.dom)
         mat.build()
         self.mat = mat
@@ -88,6 +92,11 @@ class BaseProblem:
         self.dom.applyBoundaryConditions(self.vort, "vorticity", t, self.nu)
         vel = self.solverKLE.getSolution()
         self.dom.applyBoundaryConditions(vel, "velocity", t, self.nu)
+        if self.solverKLE.isNS():
+            self.solverKLE.solveFS(self.vort)
+            velFS = self.solverKLE.getFreeSlipSolution()
+            self.dom.applyBoundaryConditionsNS(velFS, "velocity", t, self.nu)
+            self.operator.Curl.mult(velFS, self.vort)
         self.solverKLE.solve(self.vort)
         self.computeVtensV(vel)
         self.operator.SrT.mult(vel, self._Aux1)

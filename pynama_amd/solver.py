@@ -45,7 +45,14 @@ class KleSolver:
         self._wtmp = K.createVecLeft()
         self.__isNS = False
         if self.mat.bcType == "NS":
-            raise NotImplementedError("no-slip KLE solve (solveFS) is the next row of the scope table")
+            # solverFS on K + Kfs (kle_solver.py:22-28); MatNS assembles the sum
+            # on the device with PETSc's union pattern and rounding
+            self.solverFS = KspSolver()
+            self.solverFS.createSolver(self.mat.getKplusKfs())
+            self.__velFS = K.createVecRight()
+            self.__velFS.setName("free-slip")
+            self._bfs = K.createVecLeft()
+            self.__isNS = True
 
     def isNS(self):
         return self.__isNS
@@ -69,5 +76,17 @@ class KleSolver:
     def getKSP(self):
         return self.solver
 
+    def rhsFS(self, vort):
+        """b = Rw * vort + Rwfs * vort + Krhsfs * vel (kle_solver.py:39-41)."""
+        self.mat.Rw.mult(vort, self._bfs)
+        self.mat.Rwfs.mult(vort, self._wtmp)
+        self._bfs.axpy(1.0, self._wtmp)
+        self.mat.Krhsfs.mult(self.__vel, self._wtmp)
+        self._bfs.axpy(1.0, self._wtmp)
+        return self._bfs
+
+    def solveFS(self, vort):
+        self.solverFS(self.rhsFS(vort), self.__velFS)
+
     def getFreeSlipSolution(self):
-        raise NotImplementedError("no-slip path not provided yet")
+        return self.__velFS

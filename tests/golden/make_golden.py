@@ -564,6 +564,8 @@ def eval_rhs(dom, mat, solver, vort0, rho, mu, dim, t):
     BaseProblem.evalRHS(ns, None, t, ns.vort, f)
     rec.update(rhs_vort_bc=ns.vort.a.copy(), rhs_vel=solver.getSolution().a.copy(), rhs_VtensV=ns._VtensV.a.copy(),
                rhs_Aux1=ns._Aux1.a.copy(), rhs_f=f.a.copy())
+    if solver.isNS():
+        rec["rhs_velFS"] = solver.getFreeSlipSolution().a.copy()
     return rec
 
 
@@ -628,9 +630,9 @@ def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True):
     b = (mat.Rw * vort + mat.Krhs * vel).a.copy()
     solver.solve(vort)
     u = solver.getSolution().a.copy()
-    if ops and not ns:
+    if ops:
         out.update(eval_rhs(dom, mat, solver, vort, rho, mu, dim, 0.25))
-        solver.solve(vort)  # restore the t=0 solution
+        solver.getSolution().a[:] = u  # restore the t=0 solution
     out["b"] = b
     out["u"] = u
     out["u_exact"] = u_ex

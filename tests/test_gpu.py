@@ -73,7 +73,7 @@ def test_assembly_matches_golden(pa, case):
         assert np.abs(d - ref).max() <= 1e-12 * np.abs(ref).max(), nm
 
 
-@pytest.mark.parametrize("dim,ngl", [(2, 2), (2, 3), (2, 5), (2, 7), (3, 2), (3, 3), (3, 5)])
+@pytest.mark.parametrize("dim,ngl", [(2, 2), (2, 3), (2, 5), (2, 7), (3, 2), (3, 3), (3, 5), (3, 6), (3, 7)])
 def test_element_kernel_vs_oracle(pa, dim, ngl):
     import ctypes as C
     from pynama_amd._lib import call

@@ -166,3 +166,19 @@ def test_slab_partition_and_halo_plan(pa, nranks):
         sconn = serial.conn()
         need = np.nonzero(((sconn >= lo) & (sconn < hi)).any(1))[0]
         assert need.min() >= m.elem_range[0] and need.max() < m.elem_range[1]
+
+
+def test_noslip_dof_sets_match_reference():
+    """Domain no-slip DoF sets (getTangDofs / getNormalDofs(collect=True)) equal
+    the reference BoundaryConditions' sets on the cavity fixture."""
+    import pynama_amd as pa
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "case_cavity2d.npz"))
+    cfg = {"domain": {"ngl": 3, "box-mesh": {"nelem": [4, 4], "lower": [0, 0], "upper": [1, 1]}},
+           "boundary-conditions": {"no-slip": {"up": [2, 0], "down": [0, 0], "left": [0, 0], "right": [0, 0]}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    assert dom.getBoundaryType() == "NS"
+    assert sorted(dom.getTangDofs(collect=True)) == sorted(g["tang_dofs"].tolist())
+    assert sorted(dom.getNormalDofs(collect=True)) == sorted(g["normal_dofs"].tolist())
+    assert dom.getNodesNoSlip() == set(int(d) // 2 for d in g["tang_dofs"])

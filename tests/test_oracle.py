@@ -155,3 +155,23 @@ def test_eval_rhs_chain_golden(case):
     assert np.abs(aux - g["rhs_Aux1"]).max() <= 1e-12 * max(1.0, np.abs(g["rhs_Aux1"]).max())
     scale = max(1.0, np.abs(g["rhs_f"]).max())
     assert np.abs(f - g["rhs_f"]).max() <= 1e-10 * scale
+
+
+NS_MATS = ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs")
+
+
+def test_noslip_golden():
+    """MatNS.buildNS restated (oracle.assemble_ns) against the reference's own
+    no-slip matrices (cavity, 4x4, ngl=3): DoF sets and patterns exact, values
+    to a few ulps."""
+    g = np.load(os.path.join(G, "case_cavity2d.npz"))
+    m = O.BoxMesh(2, [4, 4], [0, 0], [1, 1], 3)
+    T, N = O.noslip_dofs(m, ["up", "down", "left", "right"])
+    assert sorted(T) == sorted(g["tang_dofs"].tolist())
+    assert sorted(N) == sorted(g["normal_dofs"].tolist())
+    mats = O.assemble_ns(m, T, N)
+    for k in NS_MATS:
+        A = mats[k]
+        np.testing.assert_array_equal(A.indptr, g[k + "_indptr"])
+        np.testing.assert_array_equal(A.indices, g[k + "_indices"])
+        assert np.abs(A.data - g[k + "_data"]).max() <= 1e-14 * np.abs(g[k + "_data"]).max(), k
