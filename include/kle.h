@@ -95,6 +95,9 @@ int kle_ctx_synchronize(kle_ctx *ctx);
 int kle_ctx_barrier(kle_ctx *ctx); /* device-side RCCL barrier + stream sync */
 /* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */
 int kle_ctx_set_profiling(kle_ctx *ctx, int on);
+/* Time only the launches tagged `name` ("spmv", "dot", "cg_update", "reduce",
+ * "halo", "allreduce"); NULL or "" times all of them. */
+int kle_ctx_set_profiling_filter(kle_ctx *ctx, const char *name);
 /* name: "spmv" | "cg_update" | "p_update" | "reduce" | "halo" | "allreduce" */
 int kle_ctx_get_kernel_stats(kle_ctx *ctx, const char *name, int64_t *count, double *total_ms);
 int kle_ctx_reset_kernel_stats(kle_ctx *ctx);
@@ -242,6 +245,9 @@ int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int pers
 /* Non-temporal (nt) loads for the value/column streams of the node-block SpMV
  * (default on: fastest together with 128-B row padding, profiles/r01). */
 int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt);
+/* N > 1: run the rows that read no ghost entry while the halo exchange is in
+ * flight on a second stream (default on; needs the unfused CG dot). */
+int kle_mat_set_halo_overlap(kle_mat *A, int on);
 /* Row padding quantum (in blocks) of node-block matrices created afterwards:
  * every value stream of a row starts on a multiple of `quantum` doubles
  * (16 = one 128-B line) so adjacent streams never share a cache line. */

@@ -54,6 +54,7 @@ _SIGS = {
     "kle_ctx_synchronize": [vp],
     "kle_ctx_barrier": [vp],
     "kle_ctx_set_profiling": [vp, C.c_int],
+    "kle_ctx_set_profiling_filter": [vp, C.c_char_p],
     "kle_ctx_get_kernel_stats": [vp, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)],
     "kle_ctx_reset_kernel_stats": [vp],
     "kle_mesh_create_box": [C.c_int, i64p, f64p, f64p, C.c_int, C.c_int, C.c_int, pvp],
@@ -119,6 +120,7 @@ _SIGS = {
     "kle_mat_set_spmv_layout": [vp, C.c_int, C.c_int],
     "kle_mat_set_spmv_buffer_variant": [vp, C.c_int],
     "kle_set_nb_pad": [C.c_int],
+    "kle_mat_set_halo_overlap": [vp, C.c_int],
     "kle_get_nb_pad": [],
     "kle_mat_set_spmv_nontemporal": [vp, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],

@@ -22,6 +22,7 @@
 //                no atomics -> bitwise deterministic.  Dirichlet masking as
 //                mat_fs.py:158-189.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -383,6 +384,16 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     std::vector<int> c32(std::max<int64_t>(nbp, 1), 0);
     for (int64_t i = 0; i < nrows; ++i)
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) c32[rp32[i] + (k - rp[i])] = (int)(cols[k] - m->ext_begin);
+    // interior rows (no ghost column): [int_lo, int_hi) between the last row
+    // reading a lower ghost and the first row reading an upper ghost
+    const int64_t glo = m->node_begin - m->ext_begin;
+    int64_t last_lo = -1, first_hi = nrows;
+    for (int64_t i = 0; i < nrows; ++i)
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            const int64_t cl = cols[k] - m->ext_begin;
+            if (cl < glo) last_lo = std::max(last_lo, i);
+            if (cl >= glo + nrows) first_hi = std::min(first_hi, i);
+        }
     kle_mat *A = new kle_mat;
     A->ctx = ctx;
     A->kind = 0;
@@ -392,6 +403,9 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->nblocks = nbp;
     A->nblocks_real = nb;
     A->pad = pad;
+    A->int_lo = last_lo + 1;
+    A->int_hi = first_hi;
+    if (const char *e = getenv("KLE_HALO_OVERLAP")) A->halo_overlap = atoi(e) != 0;
     A->node_begin = m->node_begin;
     A->ext_begin = m->ext_begin;
     A->ext_nodes = m->ext_end - m->ext_begin;

@@ -300,23 +300,24 @@ int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all)
 }
 
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
-                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi)
+                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st)
 {
     if (ctx->nranks == 1 || (lo_rank < 0 && hi_rank < 0)) return 0;
+    if (!st) st = ctx->stream;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    KLE_TRY(ctx->tic("halo", &ev));
+    KLE_TRY(ctx->tic("halo", &ev, st));
     double *own = base + ghost_lo;
     if (ctx->comm) {
         KLE_NCCL(ncclGroupStart());
         if (lo_rank >= 0) {
             // my lowest send_lo owned entries are the lower neighbour's upper ghosts
-            KLE_NCCL(ncclSend(own, send_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
-            KLE_NCCL(ncclRecv(base, ghost_lo, ncclDouble, lo_rank, ctx->comm, ctx->stream));
+            KLE_NCCL(ncclSend(own, send_lo, ncclDouble, lo_rank, ctx->comm, st));
+            KLE_NCCL(ncclRecv(base, ghost_lo, ncclDouble, lo_rank, ctx->comm, st));
         }
         if (hi_rank >= 0) {
             KLE_NCCL(ncclSend(own + n_local - send_hi, send_hi, ncclDouble, hi_rank, ctx->comm,
-                              ctx->stream));
-            KLE_NCCL(ncclRecv(own + n_local, ghost_hi, ncclDouble, hi_rank, ctx->comm, ctx->stream));
+                              st));
+            KLE_NCCL(ncclRecv(own + n_local, ghost_hi, ncclDouble, hi_rank, ctx->comm, st));
         }
         KLE_NCCL(ncclGroupEnd());
     } else {
@@ -324,19 +325,19 @@ int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local,
         const int64_t rl = lo_rank >= 0 ? ghost_lo : 0, rh = hi_rank >= 0 ? ghost_hi : 0;
         KLE_TRY(stage_reserve(ctx, sl + sh + rl + rh));
         double *hs_lo = ctx->h_stage, *hs_hi = hs_lo + sl, *hr_lo = hs_hi + sh, *hr_hi = hr_lo + rl;
-        if (sl) KLE_HIP(hipMemcpyAsync(hs_lo, own, sizeof(double) * sl, hipMemcpyDeviceToHost, ctx->stream));
+        if (sl) KLE_HIP(hipMemcpyAsync(hs_lo, own, sizeof(double) * sl, hipMemcpyDeviceToHost, st));
         if (sh)
             KLE_HIP(hipMemcpyAsync(hs_hi, own + n_local - sh, sizeof(double) * sh, hipMemcpyDeviceToHost,
-                                   ctx->stream));
-        KLE_HIP(hipStreamSynchronize(ctx->stream));
+                                   st));
+        KLE_HIP(hipStreamSynchronize(st));
         if (ctx->hcomm.halo(hs_lo, sl, lo_rank, hs_hi, sh, hi_rank, hr_lo, rl, hr_hi, rh, ctx->hcomm.user))
             return fail(KLE_ERR_COMM, "host halo callback failed");
-        if (rl) KLE_HIP(hipMemcpyAsync(base, hr_lo, sizeof(double) * rl, hipMemcpyHostToDevice, ctx->stream));
+        if (rl) KLE_HIP(hipMemcpyAsync(base, hr_lo, sizeof(double) * rl, hipMemcpyHostToDevice, st));
         if (rh)
-            KLE_HIP(hipMemcpyAsync(own + n_local, hr_hi, sizeof(double) * rh, hipMemcpyHostToDevice, ctx->stream));
-        KLE_HIP(hipStreamSynchronize(ctx->stream));
+            KLE_HIP(hipMemcpyAsync(own + n_local, hr_hi, sizeof(double) * rh, hipMemcpyHostToDevice, st));
+        KLE_HIP(hipStreamSynchronize(st));
     }
-    KLE_TRY(ctx->toc("halo", &ev));
+    KLE_TRY(ctx->toc("halo", &ev, st));
     return 0;
 }
 
@@ -357,24 +358,25 @@ hipEvent_t kle_ctx::get_event()
     return e;
 }
 
-int kle_ctx::tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev)
+int kle_ctx::tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev, hipStream_t s)
 {
-    (void)name;
-    if (!profiling) return 0;
+    if (!s) s = stream;
+    ev->first = ev->second = nullptr;
+    if (!profiling || (!prof_only.empty() && prof_only != name)) return 0;
     ev->first = get_event();
     ev->second = get_event();
     if (!ev->first || !ev->second) return fail(KLE_ERR_DEVICE, "hipEventCreate failed");
-    KLE_HIP(hipEventRecord(ev->first, stream));
+    KLE_HIP(hipEventRecord(ev->first, s));
     return 0;
 }
 
-int kle_ctx::toc(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev)
+int kle_ctx::toc(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev, hipStream_t s)
 {
-    if (!profiling) return 0;
-    KLE_HIP(hipEventRecord(ev->second, stream));
-    Stat &s = stats[name];
-    s.pending.push_back(*ev);
-    if (s.pending.size() > 8192) return resolve_stats();
+    if (!profiling || !ev->first) return 0;
+    KLE_HIP(hipEventRecord(ev->second, s ? s : stream));
+    Stat &st = stats[name];
+    st.pending.push_back(*ev);
+    if (st.pending.size() > 8192) return resolve_stats();
     return 0;
 }
 
@@ -424,9 +426,12 @@ static int ctx_init(int device, int rank, int nranks, kle_ctx **out)
     c->nranks = nranks;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return fail(KLE_ERR_DEVICE, "hipStreamCreate failed");
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_x_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_halo_done, hipEventDisableTiming) != hipSuccess) {
+        kle_ctx_destroy(c);
+        return fail(KLE_ERR_DEVICE, "hipStreamCreate / hipEventCreate failed");
     }
     if (hipMalloc(&c->d_partials, sizeof(double) * 4 * PART_STRIDE) != hipSuccess ||
         hipMalloc(&c->d_scal, sizeof(double) * NSCAL) != hipSuccess ||
@@ -485,6 +490,9 @@ int kle_ctx_destroy(kle_ctx *c)
     hipHostFree(c->h_istate);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->comm_stream) hipStreamDestroy(c->comm_stream);
+    if (c->ev_x_ready) hipEventDestroy(c->ev_x_ready);
+    if (c->ev_halo_done) hipEventDestroy(c->ev_halo_done);
     delete c;
     return 0;
 }
@@ -509,6 +517,13 @@ int kle_ctx_set_profiling(kle_ctx *c, int on)
 {
     KLE_ARG(c, "null ctx");
     c->profiling = on != 0;
+    return 0;
+}
+
+int kle_ctx_set_profiling_filter(kle_ctx *c, const char *name)
+{
+    KLE_ARG(c, "null ctx");
+    c->prof_only = name ? name : "";
     return 0;
 }
 

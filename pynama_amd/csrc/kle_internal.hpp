@@ -66,11 +66,14 @@ enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_COUNT = 8 };
 struct kle_ctx {
     int device = 0, rank = 0, nranks = 1;
     hipStream_t stream = nullptr;
+    hipStream_t comm_stream = nullptr;        // halo exchange overlapped with interior SpMV rows
+    hipEvent_t ev_x_ready = nullptr, ev_halo_done = nullptr;
     ncclComm_t comm = nullptr;
     kle_host_comm hcomm = {};         // host-staged transport (testing), used when comm == nullptr
     double *h_stage = nullptr;        // pinned staging for the host transport
     int64_t h_stage_n = 0;
     bool profiling = false;
+    std::string prof_only;  // time only this kernel tag (empty: all)
     struct Stat {
         int64_t count = 0;
         double ms = 0;
@@ -87,8 +90,8 @@ struct kle_ctx {
     int num_cus = 256;
 
     // timing helpers (no-ops unless profiling)
-    int tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev);
-    int toc(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev);
+    int tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev, hipStream_t s = nullptr);
+    int toc(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev, hipStream_t s = nullptr);
     int resolve_stats();
     hipEvent_t get_event();
 };
@@ -141,7 +144,9 @@ struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
     int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
-    int spmv_nt = 1;  // non-temporal value/column loads (fastest with padded rows: profiles/r01)
+    int spmv_nt = 1;
+    int halo_overlap = 1;          // N>1: interior rows run while the halo is in flight
+    int64_t int_lo = 0, int_hi = 0;  // rows [int_lo, int_hi) read no ghost entries  // non-temporal value/column loads (fastest with padded rows: profiles/r01)
     int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping
     int spmv_buf = 0;          // buffer-load variant (0 off; cache-policy experiments)
     int spmv_order = 0;        // 0 natural row order, 1 (x,y)-tiled z-columns
@@ -193,7 +198,7 @@ int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64
 int allreduce_sum(kle_ctx *ctx, double *dbuf, int n);  // in place, device buffer
 int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all);
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
-                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi);
+                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t s = nullptr);
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials,
          int *nparts, const int *istate);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);

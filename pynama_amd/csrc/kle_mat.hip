@@ -58,8 +58,14 @@ constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
 // one XCD; MI355X_MICROARCH.md); remapping b -> (b%8)*(G/8) + b/8 gives each
 // XCD one contiguous chunk of the row order, so the x lines a chunk gathers
 // stay in that XCD's L2.  order: optional row permutation (spatially tiled).
+// rows [a0, a0 + na) then [b0, b0 + nb): the whole matrix, or the interior /
+// ghost-dependent split used to overlap the halo exchange (N > 1)
+struct RowMap {
+    int64_t a0, na, b0, nb;
+};
+
 template <int R, int C, bool DOT, int LPR, int UNR, bool NT>
-__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int *__restrict__ rowptr,
+__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__restrict__ rowptr,
                                                         const int *__restrict__ rowcnt,
                                                         const int *__restrict__ bcol,
                                                         const double *__restrict__ val,
@@ -78,10 +84,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
     const int64_t wave0 = lb * SPMV_WAVES + (threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
     double dotacc = 0.0;
+    const int64_t nrows = rm.na + rm.nb;
     for (int64_t base = wave0 * RPW; base < nrows; base += nwaves * RPW) {
-        const int64_t i = (order && base + sub < nrows) ? order[base + sub] : base + sub;
+        const int64_t r = base + sub;
+        const bool valid = r < nrows;
+        const int64_t i = !valid ? 0 : order ? order[r] : r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
         int b0 = 0, m = 0, mp = 0;
-        if (i < nrows) {
+        if (valid) {
             b0 = rowptr[i];
             mp = rowptr[i + 1] - b0;
             m = rowcnt ? rowcnt[i] : mp;
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(int64_t nrows, const int
         for (int a = 0; a < R; ++a)
 #pragma unroll
             for (int o = LPR / 2; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-        if (sl < R && i < nrows) {
+        if (sl < R && valid) {
             double mine = acc[0];
 #pragma unroll
             for (int a = 1; a < R; ++a)
@@ -370,7 +379,12 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
     const bool dot = dotvec != nullptr;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (A->kind == 0) {
-        if (c->nranks > 1)
+        // N > 1: rows [int_lo, int_hi) read no ghost entry, so they run while the
+        // halo is in flight on the comm stream; the ghost-dependent rows follow
+        const bool overlap = c->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi && !dot &&
+                             !A->spmv_order && !A->spmv_buf && !A->spmv_persistent &&
+                             (x->lo_rank >= 0 || x->hi_rank >= 0);
+        if (c->nranks > 1 && !overlap)
             KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
                                   x->send_lo, x->send_hi));
         const int rpb = SPMV_WAVES * (64 / A->spmv_lpr);  // rows per workgroup
@@ -426,15 +440,32 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (nparts) *nparts = grid;
         const double *pd = dot ? dotvec->d : nullptr;
         KLE_TRY(c->tic("spmv", &ev));
+        RowMap rm{0, A->nrows, 0, 0};
+        if (overlap) {
+            rm = RowMap{A->int_lo, A->int_hi - A->int_lo, 0, 0};
+            grid = grid_for(rm.na, rpb, PART_STRIDE - 256);
+            KLE_HIP(hipEventRecord(c->ev_x_ready, c->stream));
+            KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
+        }
+        for (int pass = 0; pass < (overlap ? 2 : 1); ++pass) {
+            if (pass == 1) {
+                // interior rows are queued; exchange the halo beside them
+                KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
+                                      x->send_lo, x->send_hi, c->comm_stream));
+                KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
+                KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
+                rm = RowMap{0, A->int_lo, A->int_hi, A->nrows - A->int_hi};
+                grid = grid_for(rm.na + rm.nb, rpb, PART_STRIDE - 256);
+            }
 #define NB_LAUNCH(RR, CC, LPR, UNR, NT)                                                                   \
     do {                                                                                                \
         if (dot)                                                                                        \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
-                               c->stream, A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, \
+                               c->stream, rm, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base,   \
                                y->d, pd, partials, istate, order, xcd);                                 \
         else                                                                                            \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0, \
-                               c->stream, A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, \
+                               c->stream, rm, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base,   \
                                y->d, pd, partials, istate, order, xcd);                                 \
     } while (0)
 #define NB_VARIANTS(RR, CC)                                                                             \
@@ -451,14 +482,15 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1, false);                                                      \
         else { NB_VARIANTS(RR, CC) }                                                                    \
     } else
-        NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3) NB_CASE(3, 2) NB_CASE(2, 3)
-        NB_CASE(3, 6) NB_CASE(1, 1) {
-            return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
+            NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
+            NB_CASE(3, 2) NB_CASE(2, 3) NB_CASE(3, 6) NB_CASE(1, 1) {
+                return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
+            }
+            KLE_HIP(hipGetLastError());
         }
 #undef NB_CASE
 #undef NB_VARIANTS
 #undef NB_LAUNCH
-        KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
     }
@@ -966,6 +998,13 @@ int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt)
 }
 
 int kle_get_nb_pad(void) { return g_nb_pad; }
+
+int kle_mat_set_halo_overlap(kle_mat *A, int on)
+{
+    KLE_ARG(A, "null matrix");
+    A->halo_overlap = on != 0;
+    return 0;
+}
 
 int kle_set_nb_pad(int quantum)
 {

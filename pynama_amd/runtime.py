@@ -145,7 +145,9 @@ class Context:
     def barrier(self):
         call("kle_ctx_barrier", self.h)
 
-    def set_profiling(self, on=True):
+    def set_profiling(self, on=True, only=None):
+        """Event-time device launches; `only` restricts it to one kernel tag."""
+        call("kle_ctx_set_profiling_filter", self.h, only.encode() if only else None)
         call("kle_ctx_set_profiling", self.h, int(bool(on)))
 
     def kernel_stats(self, name):

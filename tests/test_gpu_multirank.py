@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, size, port, nelem, ngl, q):
+def _worker(rank, size, port, nelem, ngl, q, overlap=True):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="host",
@@ -40,6 +40,13 @@ def _worker(rank, size, port, nelem, ngl, q):
         mat = pa.MatFS()
         mat.setDomain(dom)
         mat.build()
+        # halo exchange overlapped with the interior rows == plain exchange, bitwise
+        xv = mat.K.createVecRight()
+        xv.setArray(np.sin(np.arange(*mat.K.getOwnershipRange(), dtype=np.float64)))
+        y_ov = (mat.K * xv).getArray()
+        mat.K.setHaloOverlap(False)
+        y_pl = (mat.K * xv).getArray()
+        mat.K.setHaloOverlap(overlap)
         sol = pa.KleSolver()
         sol.setMat(mat)
         sol.setUp()
@@ -57,7 +64,9 @@ def _worker(rank, size, port, nelem, ngl, q):
         dn = pa.petsc.Vec().createMPI((7, None))  # exercise the allgather-based layout
         res = {"rank": rank, "lo": lo, "hi": hi, "u": u, "its": ksp.getIterationNumber(),
                "true": ksp.getTrueRelativeResidual(), "ip": ip, "ix": ix, "d": d,
-               "vec_range": dn.getOwnershipRange(), "dot": vort.dot(vort)}
+               "vec_range": dn.getOwnershipRange(), "dot": vort.dot(vort),
+               "overlap_equal": bool(np.array_equal(y_ov, y_pl)), "y": y_ov,
+               "ov_diff": (np.nonzero(y_ov != y_pl)[0][:12].tolist(), len(y_ov))}
         q.put(res)
     except Exception as e:  # report instead of hanging the peer
         import traceback
@@ -66,15 +75,16 @@ def _worker(rank, size, port, nelem, ngl, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 4), (3, [2, 3, 3], 3)])
-def test_partitioned_solve_matches_serial(size, nelem, ngl):
+def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap)) for r in range(size)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=600) for _ in range(size)], key=lambda r: r["rank"])
@@ -82,6 +92,8 @@ def test_partitioned_solve_matches_serial(size, nelem, ngl):
         p.join(timeout=120)
     for r in res:
         assert "error" not in r, r.get("error")
+    for r in res:
+        assert r["overlap_equal"], (r["rank"], r["ov_diff"])
     # serial oracle system on the same numbering
     dim = len(nelem)
     om = O.BoxMesh(dim, nelem, [0] * dim, [1] * dim, ngl)
@@ -112,5 +124,8 @@ def test_partitioned_solve_matches_serial(size, nelem, ngl):
         np.testing.assert_array_equal(r["ix"], K.indices[ip0:K.indptr[r["hi"]]])
         assert np.abs(r["d"] - K.data[ip0:K.indptr[r["hi"]]]).max() <= 1e-12 * np.abs(K.data).max()
         assert r["dot"] == res[0]["dot"]  # allreduced
+        assert r["overlap_equal"]
+        np.testing.assert_allclose(r["y"], K.mult(np.sin(np.arange(K.m, dtype=np.float64)))[r["lo"]:r["hi"]],
+                                   rtol=1e-13, atol=1e-10)
     ranges = [r["vec_range"] for r in res]
     assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
