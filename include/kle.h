@@ -199,12 +199,12 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
  * K_e [dim n][dim n], Rw_e [dim n][dim_w n] (row-major, n = ngl^dim). */
 int kle_element_kle(kle_ctx *ctx, kle_mesh *m, int64_t e, double *Ke, double *Rwe);
 /* No-slip assembly (replaces MatNS.build / buildNS, mat_ns.py:47-161):
- * K, Krhs, Rw as kle_assemble_kle on the no-slip nodes, plus Kfs, Krhsfs,
- * Rwfs with PETSc's DoF-level patterns, and Ksum = K + Kfs (the operator of
- * KleSolver.solverFS, kle_solver.py:22-28) assembled directly.  Rd / Rdfs are
- * filled by the reference but read by nothing on the KLE path: not built. */
-int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw, kle_mat **Kfs,
-                    kle_mat **Krhsfs, kle_mat **Rwfs, kle_mat **Ksum);
+ * K, Krhs, Rw as kle_assemble_kle on the no-slip nodes, Rd (free rows x
+ * cell nodes), plus Kfs, Krhsfs, Rwfs, Rdfs with PETSc's DoF-level patterns,
+ * and Ksum = K + Kfs (the operator of KleSolver.solverFS, kle_solver.py:22-28)
+ * assembled directly. */
+int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw, kle_mat **Rd,
+                    kle_mat **Kfs, kle_mat **Krhsfs, kle_mat **Rwfs, kle_mat **Rdfs, kle_mat **Ksum);
 /* Operators (replaces MatFS.buildOperators + Operators.setValues/assembleAll,
  * mat_fs.py:194-271, with Spectral.getElemKLEOperators spectral.py:162-228):
  * Curl [dim_w N x dim N], SrT [dim_s N x dim N], DivSrT [dim N x dim_s N],

@@ -300,12 +300,12 @@ def _dok_csr(dok, m, n):
 def assemble_ns(mesh, tang, normal):
     """MatNS.buildNS (mat_ns.py:47-145) restated on dict-of-keys matrices with
     PETSc ADD/INSERT semantics, cells ascending (single rank).  Small meshes
-    only.  Returns dict of CSR: K, Krhs, Rw, Kfs, Krhsfs, Rwfs."""
+    only.  Returns dict of CSR: K, Krhs, Rw, Rd, Kfs, Krhsfs, Rwfs, Rdfs."""
     dim, nn = mesh.dim, mesh.nn
     dw = 1 if dim == 2 else 3
     el = Element(mesh.ngl, dim)
     conn, X = mesh.conn(), mesh.corners()
-    mats = {k: {} for k in ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs")}
+    mats = {k: {} for k in ("K", "Krhs", "Rw", "Rd", "Kfs", "Krhsfs", "Rwfs", "Rdfs")}
 
     def add(name, rows, cols, vals, addv=True):
         d = mats[name]
@@ -317,7 +317,7 @@ def assemble_ns(mesh, tang, normal):
 
     ind1, ind1fs = set(), set()
     for e in range(mesh.E):
-        Ke, Rwe, _ = el.kle(X[e].ravel())
+        Ke, Rwe, Rde = el.kle(X[e].ravel())
         nodes = conn[e].tolist()
         iv = [n * dim + d for n in nodes for d in range(dim)]
         iw = [n * dw + d for n in nodes for d in range(dw)]
@@ -341,6 +341,7 @@ def assemble_ns(mesh, tang, normal):
             add("Kfs", gtang, gtang, Ke[np.ix_(ltang, ltang)])
             ind1fs.update(gtang)
             add("Rwfs", gtang, iw, Rwe[ltang, :])
+            add("Rdfs", gtang, nodes, Rde[ltang, :])
             add("Krhsfs", gtang, gnorm, -Ke[np.ix_(ltang, lnorm)])
             add("Krhsfs", gfree, gnorm, -Ke[np.ix_(dfree, lnorm)])
             for i in gnorm:
@@ -349,6 +350,7 @@ def assemble_ns(mesh, tang, normal):
         for i in g2set:
             add("K", [i], [i], 0.0)
         add("Rw", gfree, iw, Rwe[np.ix_(dfree, range(len(iw)))])
+        add("Rd", gfree, nodes, Rde[np.ix_(dfree, range(len(nodes)))])
     for i in ind1:  # setIndices2One (mat_fs.py:115-120)
         add("Krhs", [i], [i], 1.0)
         add("K", [i], [i], 1.0)
@@ -357,4 +359,5 @@ def assemble_ns(mesh, tang, normal):
     for i in ind1 - ind1fs:
         add("Krhsfs", [i], [i], 1.0, addv=False)
     n = mesh.N * dim
-    return {k: _dok_csr(v, n, mesh.N * dw if k in ("Rw", "Rwfs") else n) for k, v in mats.items()}
+    ncols = {"Rw": mesh.N * dw, "Rwfs": mesh.N * dw, "Rd": mesh.N, "Rdfs": mesh.N}
+    return {k: _dok_csr(v, n, ncols.get(k, n)) for k, v in mats.items()}

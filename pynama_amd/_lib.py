@@ -98,7 +98,7 @@ _SIGS = {
     "kle_assemble_kle": [vp, vp, pvp, pvp, pvp],
     "kle_element_kle": [vp, vp, C.c_int64, f64p, f64p],
     "kle_assemble_operators": [vp, vp, pvp, pvp, pvp],
-    "kle_assemble_ns": [vp, vp, pvp, pvp, pvp, pvp, pvp, pvp, pvp],
+    "kle_assemble_ns": [vp, vp] + [pvp] * 9,
     "kle_mat_create_aij": [vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, vp, vp, pvp],
     "kle_mat_create_aij_csr": [vp, C.c_int64, C.c_int64, i64p, i64p, f64p, pvp],
     "kle_mat_set_values": [vp, C.c_int32, i64p, C.c_int32, i64p, f64p, C.c_int],

@@ -159,7 +159,8 @@ template <int DIM>
 __global__ __launch_bounds__(256) void k_element(int ngl, Tables1D TF, Tables1D TR,
                                                  const double *__restrict__ geoF,
                                                  const double *__restrict__ geoR,
-                                                 double *__restrict__ Ke, double *__restrict__ Rwe)
+                                                 double *__restrict__ Ke, double *__restrict__ Rwe,
+                                                 double *__restrict__ Rde)
 {
     constexpr int DW = DIM == 2 ? 1 : 3;
     constexpr int G1 = 1 + DIM * DIM;
@@ -269,6 +270,11 @@ __global__ __launch_bounds__(256) void k_element(int ngl, Tables1D TF, Tables1D 
             double *rb = Rwe + ((e * ne + l) * (int64_t)ne + m) * (DIM * DW);
             for (int a = 0; a < DIM; ++a)
                 for (int c = 0; c < DW; ++c) rb[a * DW + c] = rw[a][c];
+            if (Rde) {
+                // Rd_e = -H^T B_div (full) + a_d B_div^T H (reduced)   (spectral.py:136-137,157)
+                double *db = Rde + ((e * ne + l) * (int64_t)ne + m) * DIM;
+                for (int a = 0; a < DIM; ++a) db[a] = -E[a][pv] + ALPHA_D * F[a][pv];
+            }
         }
 }
 
@@ -476,7 +482,7 @@ static int upload_tables(kle_ctx *ctx, int ngl, DevTables &T)
 }
 
 // Compute K_e and Rw_e of all local elements into device buffers.
-static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, double **dRwe)
+static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, double **dRwe, double **dRde = nullptr)
 {
     const int dim = m->dim, ne = m->nn(), dw = dim == 2 ? 1 : 3, nc = 1 << dim;
     const int64_t nel = m->elem_end - m->elem_begin;
@@ -500,16 +506,21 @@ static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, doubl
         return fail(KLE_ERR_MEM, "element matrix workspace (%.2f GB) does not fit",
                     (keN + rwN) * 8.0 / 1e9);
     }
+    if (dRde && hipMalloc(dRde, sizeof(double) * std::max<size_t>((size_t)nel * ne * ne * dim, 1)) != hipSuccess) {
+        hipFree(dX); hipFree(gF); hipFree(gR); hipFree(*dKe); hipFree(*dRwe);
+        return fail(KLE_ERR_MEM, "element Rd workspace does not fit");
+    }
+    double *Rd_out = dRde ? *dRde : nullptr;
     const int64_t nF = nel * nqF, nR = nel * nqR;
     dim3 eg((ne + TL - 1) / TL, (ne + TL - 1) / TL, (unsigned)nel);
     if (dim == 2) {
         hipLaunchKernelGGL(k_geometry<2>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
         hipLaunchKernelGGL(k_geometry<2>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
-        hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe);
+        hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
     } else {
         hipLaunchKernelGGL(k_geometry<3>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
         hipLaunchKernelGGL(k_geometry<3>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
-        hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe);
+        hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
     }
     KLE_HIP(hipGetLastError());
     KLE_HIP(hipStreamSynchronize(ctx->stream));
@@ -870,30 +881,35 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
     return 0;
 }
 
-int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw, kle_mat **Kfs,
-                    kle_mat **Krhsfs, kle_mat **Rwfs, kle_mat **Ksum)
+int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_mat **Rw, kle_mat **Rd,
+                    kle_mat **Kfs, kle_mat **Krhsfs, kle_mat **Rwfs, kle_mat **Rdfs, kle_mat **Ksum)
 {
-    KLE_ARG(ctx && m && K && Krhs && Rw && Kfs && Krhsfs && Rwfs && Ksum, "null arg");
+    KLE_ARG(ctx && m && K && Krhs && Rw && Rd && Kfs && Krhsfs && Rwfs && Rdfs && Ksum, "null arg");
     KLE_ARG(m->rank == ctx->rank && m->nranks == ctx->nranks, "mesh partition does not match ctx");
     KLE_ARG(!m->dof_cls.empty(), "no-slip DoFs not set (kle_mesh_set_noslip_dofs)");
     // K, Krhs, Rw of MatNS are the free-slip ones with the no-slip nodes fixed
     // (mat_ns.py:124-141 + setIndices2One)
     KLE_TRY(kle_assemble_kle(ctx, m, K, Krhs, Rw));
     const int dim = m->dim, dw = dim == 2 ? 1 : 3;
-    kle_mat *mf = nullptr, *mr = nullptr, *mw = nullptr, *ms = nullptr;
+    kle_mat *mf = nullptr, *mr = nullptr, *mw = nullptr, *ms = nullptr, *md = nullptr, *mdf = nullptr;
     KLE_TRY(nb_create(ctx, m, 4, dim, dim, &mf));
     KLE_TRY(nb_create(ctx, m, 5, dim, dim, &mr));
     KLE_TRY(nb_create(ctx, m, 6, dim, dw, &mw));
     KLE_TRY(nb_create(ctx, m, 3, dim, dim, &ms));
-    const int rules[4] = {MASK_KFS, MASK_KRHSFS, MASK_TANG_ROWS, MASK_KSUM};
-    kle_mat *all[4] = {mf, mr, mw, ms};
-    for (int t = 0; t < 4; ++t) {
+    KLE_TRY(nb_create(ctx, m, 2, dim, 1, &md));   // Rd: free rows x cell nodes (mat_ns.py:139-141)
+    KLE_TRY(nb_create(ctx, m, 6, dim, 1, &mdf));  // Rdfs: tangential rows x cell nodes (:113-114)
+    const int rules[5] = {MASK_KFS, MASK_KRHSFS, MASK_TANG_ROWS, MASK_KSUM, MASK_TANG_ROWS};
+    kle_mat *all[5] = {mf, mr, mw, ms, mdf};
+    for (int t = 0; t < 5; ++t) {
         all[t]->mask_rule = rules[t];
         all[t]->dof_cls = m->dof_cls;
         all[t]->diag_only_row.assign(all[t]->nrows, 0);
     }
-    double *dKe = nullptr, *dRwe = nullptr;
-    KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe));
+    double *dKe = nullptr, *dRwe = nullptr, *dRde = nullptr;
+    KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe, &dRde));
+    uint8_t *ddir = nullptr;
+    KLE_HIP(hipMalloc(&ddir, m->dir.size()));
+    KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
     uint8_t *dcls = nullptr;
     KLE_HIP(hipMalloc(&dcls, m->dof_cls.size()));
     KLE_HIP(hipMemcpyAsync(dcls, m->dof_cls.data(), m->dof_cls.size(), hipMemcpyHostToDevice, ctx->stream));
@@ -903,17 +919,25 @@ int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_
         launch_gather_ns<3, 3, 4>(ctx, M, mr, dcls, dKe);
         launch_gather_ns<3, 3, 5>(ctx, M, mw, dcls, dRwe);
         launch_gather_ns<3, 3, 6>(ctx, M, ms, dcls, dKe);
+        launch_gather<3, 1, 2>(ctx, M, md, ddir, dRde);
+        launch_gather_ns<3, 1, 5>(ctx, M, mdf, dcls, dRde);
     } else {
         launch_gather_ns<2, 2, 3>(ctx, M, mf, dcls, dKe);
         launch_gather_ns<2, 2, 4>(ctx, M, mr, dcls, dKe);
         launch_gather_ns<2, 1, 5>(ctx, M, mw, dcls, dRwe);
         launch_gather_ns<2, 2, 6>(ctx, M, ms, dcls, dKe);
+        launch_gather<2, 1, 2>(ctx, M, md, ddir, dRde);
+        launch_gather_ns<2, 1, 5>(ctx, M, mdf, dcls, dRde);
     }
     KLE_HIP(hipGetLastError());
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     hipFree(dKe);
     hipFree(dRwe);
+    hipFree(dRde);
     hipFree(dcls);
+    hipFree(ddir);
+    *Rd = md;
+    *Rdfs = mdf;
     *Kfs = mf;
     *Krhsfs = mr;
     *Rwfs = mw;

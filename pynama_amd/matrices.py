@@ -64,8 +64,7 @@ class MatNS(MatFS):
     K, Krhs, Rw fix the no-slip nodes; Kfs, Krhsfs, Rwfs free their tangential
     DoFs for the free-slip pre-solve (solveFS).  One device pass
     (kle_assemble_ns) with PETSc's DoF-level patterns; K + Kfs, the operator of
-    KleSolver.solverFS, is assembled directly (getKplusKfs).  Rd / Rdfs are
-    filled by the reference but read by nothing downstream: left as None."""
+    KleSolver.solverFS, is assembled directly (getKplusKfs)."""
     bcType = "NS"
 
     def __init__(self):
@@ -84,15 +83,16 @@ class MatNS(MatFS):
     def buildNS(self):
         ctx = get_ctx()
         mesh = self.dom.getMesh()
-        h = [C.c_void_p() for _ in range(7)]
+        h = [C.c_void_p() for _ in range(9)]
         call("kle_assemble_ns", ctx.h, mesh._h, *[C.byref(x) for x in h])
         dim, dim_w, _ = self.dom.getDimensions()
-        shapes = [(dim, dim), (dim, dim), (dim, dim_w), (dim, dim), (dim, dim), (dim, dim_w), (dim, dim)]
+        shapes = [(dim, dim), (dim, dim), (dim, dim_w), (dim, 1), (dim, dim), (dim, dim), (dim, dim_w), (dim, 1),
+                  (dim, dim)]
         mats = [Mat._wrap(x, ctx, mesh, r, c) for x, (r, c) in zip(h, shapes)]
-        self.K, self.Krhs, self.Rw, self.Kfs, self.Krhsfs, self.Rwfs, self._Ksum = mats
-        for m, n in zip(mats, ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs", "K+Kfs")):
+        (self.K, self.Krhs, self.Rw, self.Rd, self.Kfs, self.Krhsfs, self.Rwfs, self.Rdfs, self._Ksum) = mats
+        for m, n in zip(mats, ("K", "Krhs", "Rw", "Rd", "Kfs", "Krhsfs", "Rwfs", "Rdfs", "K+Kfs")):
             m.setName(n)
-        self.kle = mats[:6]
+        self.kle = mats[:8]
 
     def getKplusKfs(self):
         return self._Ksum

@@ -18,7 +18,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 G = os.path.join(os.path.dirname(__file__), "golden")
-NS_MATS = ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs")
+NS_MATS = ("K", "Krhs", "Rw", "Rd", "Kfs", "Krhsfs", "Rwfs", "Rdfs")
 CAVITY = {"up": [2, 0], "down": [0, 0], "left": [0, 0], "right": [0, 0]}
 
 

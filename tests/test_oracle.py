@@ -157,7 +157,7 @@ def test_eval_rhs_chain_golden(case):
     assert np.abs(f - g["rhs_f"]).max() <= 1e-10 * scale
 
 
-NS_MATS = ("K", "Krhs", "Rw", "Kfs", "Krhsfs", "Rwfs")
+NS_MATS = ("K", "Krhs", "Rw", "Rd", "Kfs", "Krhsfs", "Rwfs", "Rdfs")
 
 
 def test_noslip_golden():
