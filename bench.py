@@ -254,7 +254,7 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
-            key = f"{nelem}-{args.ngl}-{nranks}-pad{args.pad}-{args.loads}" + ("-fused" if args.fused_dot else "")
+            key = f"{nelem}-{args.ngl}-{nranks}-pad{args.pad}-{args.loads}-u1" + ("-fused" if args.fused_dot else "")
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -291,7 +291,9 @@ def main():
                        "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                         "kernel": "k_nb_spmv<3,3,%s>" % ("true" if args.fused_dot else "false"), "bytes_per_launch": tot_bytes,
+                         "kernel": "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
+                                                                   "true" if args.loads == "nt" else "false"),
+                         "bytes_per_launch": tot_bytes,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt},
             "cpu_baseline": cpu,
             "spmv_gbps": achieved,

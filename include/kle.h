@@ -245,6 +245,9 @@ int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int pers
 /* Non-temporal (nt) loads for the value/column streams of the node-block SpMV
  * (default on: fastest together with 128-B row padding, profiles/r01). */
 int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt);
+/* SpMV rows per wavefront (3x3 blocks, unfused): > 1 selects the kernel that
+ * prefetches the next row's extent while streaming the current row. */
+int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on; needs the unfused CG dot). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

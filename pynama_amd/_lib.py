@@ -121,6 +121,7 @@ _SIGS = {
     "kle_mat_set_spmv_buffer_variant": [vp, C.c_int],
     "kle_set_nb_pad": [C.c_int],
     "kle_mat_set_halo_overlap": [vp, C.c_int],
+    "kle_mat_set_spmv_rows_per_wave": [vp, C.c_int],
     "kle_get_nb_pad": [],
     "kle_mat_set_spmv_nontemporal": [vp, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],

@@ -143,8 +143,9 @@ struct kle_vec {
 struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
-    int spmv_lpr = 64, spmv_unroll = 2, spmv_persistent = 0;  // SpMV kernel variant
+    int spmv_lpr = 64, spmv_unroll = 1, spmv_persistent = 0;  // SpMV kernel variant (profiles/r01/spmv_ab.jsonl)
     int spmv_nt = 1;
+    int spmv_seq = 1;              // rows per wavefront (k_nb_spmv_seq when > 1)
     int halo_overlap = 1;          // N>1: interior rows run while the halo is in flight
     int64_t int_lo = 0, int_hi = 0;  // rows [int_lo, int_hi) read no ghost entries  // non-temporal value/column loads (fastest with padded rows: profiles/r01)
     int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping

@@ -149,6 +149,82 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
     }
 }
 
+
+// Variant: each wave takes `seq` consecutive rows and prefetches the next
+// row's (offset, length) while it streams the current one, so the row-start
+// latency overlaps the previous row's loads.  No fused dot / order / XCD map.
+template <int R, int C, int UNR, bool NT>
+__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_seq(RowMap rm, int seq, const int *__restrict__ rowptr,
+                                                            const int *__restrict__ rowcnt,
+                                                            const int *__restrict__ bcol,
+                                                            const double *__restrict__ val,
+                                                            const double *__restrict__ x, double *__restrict__ y,
+                                                            const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    const int64_t nrows = rm.na + rm.nb;
+    const int64_t r0 = wave * seq;
+    if (r0 >= nrows) return;
+    const int64_t r1 = min(r0 + (int64_t)seq, nrows);
+    int64_t i = r0 < rm.na ? rm.a0 + r0 : rm.b0 + (r0 - rm.na);
+    int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
+    for (int64_t r = r0; r < r1; ++r) {
+        int64_t ni = i;
+        int nb0 = 0, nmp = 0, nm = 0;
+        if (r + 1 < r1) {
+            ni = r + 1 < rm.na ? rm.a0 + r + 1 : rm.b0 + (r + 1 - rm.na);
+            nb0 = rowptr[ni];
+            nmp = rowptr[ni + 1] - nb0;
+            nm = rowcnt ? rowcnt[ni] : nmp;
+        }
+        const double *v = val + (int64_t)b0 * (R * C);
+        const int *cj = bcol + b0;
+        double acc[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[a] = 0.0;
+        for (int k = lane; k < m; k += 64 * UNR) {
+            int64_t j[UNR];
+            double vv[UNR][R * C];
+            bool on[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int ku = k + u * 64;
+                on[u] = ku < m;
+                j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
+#pragma unroll
+                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + (int64_t)t * mp + ku) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                double xv[C];
+#pragma unroll
+                for (int b = 0; b < C; ++b) xv[b] = on[u] ? x[j[u] * C + b] : 0.0;
+#pragma unroll
+                for (int a = 0; a < R; ++a)
+#pragma unroll
+                    for (int b = 0; b < C; ++b) acc[a] += vv[u][a * C + b] * xv[b];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+        if (lane < R) {
+            double mine = acc[0];
+#pragma unroll
+            for (int a = 1; a < R; ++a)
+                if (lane == a) mine = acc[a];
+            y[i * R + lane] = mine;
+        }
+        i = ni;
+        b0 = nb0;
+        mp = nmp;
+        m = nm;
+    }
+}
+
 // Buffer-load variant of the node-block SpMV (one row per wavefront, two
 // block columns per lane in flight): the matrix streams go through a per-row
 // buffer descriptor so the cache-policy bits (aux: bit0 sc0, bit1 nt,
@@ -434,6 +510,8 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
             KLE_TRY(c->toc("spmv", &ev));
             return 0;
         }
+        const bool seq_ok = A->spmv_seq > 1 && A->R == 3 && A->C == 3 && A->spmv_lpr == 64 && !dot &&
+                            !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
         if (A->spmv_order && !A->d_order) KLE_TRY(nb_build_order(A));
         const int *order = A->spmv_order ? A->d_order : nullptr;
         const int xcd = A->spmv_xcd && !A->spmv_persistent;
@@ -457,6 +535,24 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 rm = RowMap{0, A->int_lo, A->int_hi, A->nrows - A->int_hi};
                 grid = grid_for(rm.na + rm.nb, rpb, PART_STRIDE - 256);
             }
+            if (seq_ok) {
+                const int64_t nr = rm.na + rm.nb;
+                const int gs = (int)((nr + (int64_t)SPMV_WAVES * A->spmv_seq - 1) / ((int64_t)SPMV_WAVES * A->spmv_seq));
+                if (A->spmv_unroll == 1 && A->spmv_nt)
+                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 1, true>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                else if (A->spmv_unroll == 1)
+                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 1, false>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                else if (A->spmv_nt)
+                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 2, true>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                else
+                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 2, false>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                KLE_HIP(hipGetLastError());
+                continue;
+            }
 #define NB_LAUNCH(RR, CC, LPR, UNR, NT)                                                                   \
     do {                                                                                                \
         if (dot)                                                                                        \
@@ -477,9 +573,17 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
     else if (A->spmv_lpr == 32) NB_LAUNCH(RR, CC, 32, 2, false);                                        \
     else if (A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 16, 1, false);                                      \
     else NB_LAUNCH(RR, CC, 16, 2, false);
+#define NB_VARIANTS_33                                                                                  \
+    if (A->spmv_lpr == 32 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(3, 3, 32, 1, true);           \
+    else if (A->spmv_lpr == 32 && A->spmv_nt) NB_LAUNCH(3, 3, 32, 2, true);                             \
+    else if (A->spmv_lpr == 16 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(3, 3, 16, 1, true);      \
+    else if (A->spmv_lpr == 16 && A->spmv_nt) NB_LAUNCH(3, 3, 16, 2, true);                             \
+    else { NB_VARIANTS(3, 3) }
 #define NB_CASE(RR, CC)                                                                                 \
     if (A->R == RR && A->C == CC) {                                                                     \
-        if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1, false);                                                      \
+        if (RR * CC > 9 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 1, true);                                  \
+        else if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1, false);                                          \
+        else if (RR == 3 && CC == 3) { NB_VARIANTS_33 }                                                 \
         else { NB_VARIANTS(RR, CC) }                                                                    \
     } else
             NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
@@ -490,6 +594,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         }
 #undef NB_CASE
 #undef NB_VARIANTS
+#undef NB_VARIANTS_33
 #undef NB_LAUNCH
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
@@ -998,6 +1103,13 @@ int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt)
 }
 
 int kle_get_nb_pad(void) { return g_nb_pad; }
+
+int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq)
+{
+    KLE_ARG(A && seq >= 1 && seq <= 64, "rows per wave must be in [1,64]");
+    A->spmv_seq = seq;
+    return 0;
+}
 
 int kle_mat_set_halo_overlap(kle_mat *A, int on)
 {

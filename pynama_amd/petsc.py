@@ -383,6 +383,9 @@ class Mat:
     def setSpmvBufferVariant(self, v):
         call("kle_mat_set_spmv_buffer_variant", self._h, int(v))
 
+    def setSpmvRowsPerWave(self, seq):
+        call("kle_mat_set_spmv_rows_per_wave", self._h, int(seq))
+
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))
 
