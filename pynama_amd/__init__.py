@@ -8,6 +8,7 @@ from ._lib import Error, load  # noqa: F401
 from .domain import Domain  # noqa: F401
 from .matrices import MatFS, MatNS, Operators  # noqa: F401
 from .problem import BaseProblem, BaseProblemTest  # noqa: F401
+from .ts import TsSolver  # noqa: F401
 from .mesh import BoxMesh  # noqa: F401
 from .runtime import COMM_WORLD, get_ctx, finalize  # noqa: F401
 from .solver import KleSolver, KspSolver  # noqa: F401

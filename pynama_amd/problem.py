@@ -27,6 +27,26 @@ class BaseProblem:
         self.readMaterialData()
         ts = config.get("time-solver") or {}
         self.initTime = float(kwargs.get("initTime", ts.get("start-time", 0.0)))
+        self.ts = None
+        if "time-solver" in config:
+            self.setUpTimeSolver()
+
+    def setUpTimeSolver(self):
+        """base_problem.py:71-80: TS rk/5bs over [start-time, end-time]."""
+        from .ts import TsSolver
+        options = self.config.get("time-solver")
+        self.ts = TsSolver()
+        self.ts.setUpTimes(options["start-time"], options["end-time"], options["max-steps"])
+        self.ts.initSolver(self.evalRHS, self.convergedStepFunction)
+
+    def convergedStepFunction(self, ts):
+        """Post-step hook (base_problem.py:93-101); the reference writes HDF5/XDMF
+        output here, which is outside this path: record the step instead."""
+        self.lastStep = (ts.step_number, ts.time, ts.getTimeStep())
+
+    def startSolver(self):
+        """timeSolving (run_case.py:153-163): integrate the vorticity in place."""
+        self.ts.solve(self.vort)
 
     def setUp(self):
         self.setUpDomain()
