@@ -22,6 +22,7 @@
 //                no atomics -> bitwise deterministic.  Dirichlet masking as
 //                mat_fs.py:158-189.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -371,12 +372,10 @@ static MeshDev mesh_dev(const kle_mesh *m)
 int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat **out)
 {
     const int64_t nrows = m->node_end - m->node_begin;
-    std::vector<int64_t> rp(nrows + 1);
-    int64_t nb;
-    KLE_TRY(kle_mesh_pattern_size(m, which, &nb));
+    std::vector<int64_t> rp, cols;
+    KLE_TRY(pattern_csr(m, which, rp, cols));
+    const int64_t nb = rp[nrows];
     if (nb >= (1ll << 31) / 1) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
-    std::vector<int64_t> cols(std::max<int64_t>(nb, 1));
-    KLE_TRY(kle_mesh_pattern(m, which, rp.data(), cols.data()));
     const int pad = std::max(1, g_nb_pad);
     std::vector<int> rp32(nrows + 1), cnt(nrows);
     int64_t nbp = 0;
@@ -388,18 +387,29 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     rp32[nrows] = (int)nbp;
     if (nbp >= (1ll << 31)) return fail(KLE_ERR_SUP, "padded pattern too large for int32 block offsets");
     std::vector<int> c32(std::max<int64_t>(nbp, 1), 0);
-    for (int64_t i = 0; i < nrows; ++i)
-        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) c32[rp32[i] + (k - rp[i])] = (int)(cols[k] - m->ext_begin);
     // interior rows (no ghost column): [int_lo, int_hi) between the last row
     // reading a lower ghost and the first row reading an upper ghost
     const int64_t glo = m->node_begin - m->ext_begin;
+    std::vector<int64_t> t_lo(host_threads() + 1, -1), t_hi(host_threads() + 1, nrows);
+    std::atomic<int> slot{0};
+    parallel_for(nrows, [&](int64_t lo, int64_t hi) {
+        const int me = slot++;
+        int64_t last_lo = -1, first_hi = nrows;
+        for (int64_t i = lo; i < hi; ++i)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int64_t cl = cols[k] - m->ext_begin;
+                c32[rp32[i] + (k - rp[i])] = (int)cl;
+                if (cl < glo) last_lo = std::max(last_lo, i);
+                if (cl >= glo + nrows) first_hi = std::min(first_hi, i);
+            }
+        t_lo[me] = last_lo;
+        t_hi[me] = first_hi;
+    });
     int64_t last_lo = -1, first_hi = nrows;
-    for (int64_t i = 0; i < nrows; ++i)
-        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-            const int64_t cl = cols[k] - m->ext_begin;
-            if (cl < glo) last_lo = std::max(last_lo, i);
-            if (cl >= glo + nrows) first_hi = std::min(first_hi, i);
-        }
+    for (size_t t = 0; t < t_lo.size(); ++t) {
+        last_lo = std::max(last_lo, t_lo[t]);
+        first_hi = std::min(first_hi, t_hi[t]);
+    }
     kle_mat *A = new kle_mat;
     A->ctx = ctx;
     A->kind = 0;

@@ -6,6 +6,7 @@
 
 #include <cstdarg>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -205,6 +206,13 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
 extern int g_nb_pad;
+// Host worker count for setup loops: OMP_NUM_THREADS if set, else the
+// hardware concurrency, capped at 16 (the GPU box's CPU share per GPU).
+int host_threads();
+// Run f(lo, hi) over [0, n) split into contiguous chunks on host_threads().
+void parallel_for(int64_t n, const std::function<void(int64_t, int64_t)> &f);
+// Symbolic pattern `which` of the owned rows as CSR (row_ptr[n+1], global cols).
+int pattern_csr(const kle_mesh *m, int which, std::vector<int64_t> &row_ptr, std::vector<int64_t> &cols);
 enum DofClass : uint8_t { DOF_FREE = 0, DOF_TANG = 1, DOF_NORMAL = 2 };
 // which PETSc entries of a node block exist (MatNS.buildNS, mat_ns.py:47-145)
 enum MaskRule { MASK_NONE = 0, MASK_KFS = 1, MASK_KRHSFS = 2, MASK_TANG_ROWS = 3, MASK_KSUM = 4 };

@@ -11,6 +11,8 @@
 // Canonical numbering: lattice node id = ix + Lx (iy + Ly iz); cells x-fastest;
 // element-local nodes in tensor order (a along x fastest).
 #include <algorithm>
+#include <cstdlib>
+#include <thread>
 #include <cmath>
 #include <cstring>
 
@@ -81,6 +83,52 @@ static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
                 if (keep) emit(j);
             }
 }
+
+namespace kle {
+
+int host_threads()
+{
+    int n = (int)std::thread::hardware_concurrency();
+    if (const char *e = getenv("OMP_NUM_THREADS")) n = atoi(e);
+    return std::max(1, std::min(n, 16));
+}
+
+void parallel_for(int64_t n, const std::function<void(int64_t, int64_t)> &f)
+{
+    const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 4096));
+    if (nt <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t)
+        pool.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
+    for (auto &th : pool) th.join();
+}
+
+int pattern_csr(const kle_mesh *m, int which, std::vector<int64_t> &rp, std::vector<int64_t> &cols)
+{
+    const int64_t n = m->node_end - m->node_begin;
+    rp.assign(n + 1, 0);
+    parallel_for(n, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            int64_t c = 0;
+            row_cols(m, which, m->node_begin + i, [&](int64_t) { ++c; });
+            rp[i + 1] = c;
+        }
+    });
+    for (int64_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+    cols.resize(std::max<int64_t>(rp[n], 1));
+    parallel_for(n, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            int64_t k = rp[i];
+            row_cols(m, which, m->node_begin + i, [&](int64_t j) { cols[k++] = j; });
+        }
+    });
+    return 0;
+}
+
+}  // namespace kle
 
 extern "C" {
 
@@ -360,6 +408,7 @@ int kle_mesh_set_noslip_faces(kle_mesh *m, const int *faces, int nfaces)
     m->dir_set = true;
     return 0;
 }
+
 
 int kle_mesh_pattern_size(const kle_mesh *m, int which, int64_t *nblocks)
 {
