@@ -44,6 +44,8 @@ def parse():
                     help="also assemble Curl/SrT/DivSrT and time their SpMVs and the evalRHS operator chain")
     ap.add_argument("--fused-dot", action="store_true", help="form the CG dot inside the SpMV kernel")
     ap.add_argument("--loads", choices=["nt", "plain"], default="nt", help="SpMV value/column load policy")
+    ap.add_argument("--ksp", choices=["auto", "cg", "pipecg"], default="auto",
+                    help="auto: single-reduction CG on one GPU, pipelined CG (allreduce beside the SpMV) on N>1")
     ap.add_argument("--classic-cg", action="store_true",
                     help="two reductions per iteration instead of the single-reduction (Chronopoulos-Gear) CG")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -164,6 +166,7 @@ def main():
     solve = {}
     if not args.no_solve:
         ksp = sol.getKSP()
+        ksp.setType("pipecg" if (args.ksp == "pipecg" or (args.ksp == "auto" and nranks > 1)) else "cg")
         ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=200000)
         ksp.setCGSingleReduction(not args.classic_cg)
         ctx.barrier()
@@ -174,8 +177,9 @@ def main():
                  "true_rel_residual": ksp.getTrueRelativeResidual(), "seconds": time.perf_counter() - ts}
 
     # --- timed fixed-iteration CG
+    ksp_type = args.ksp if args.ksp != "auto" else ("pipecg" if nranks > 1 else "cg")
     kb = KSP().create()
-    kb.setType("cg")
+    kb.setType(ksp_type)
     pc = PC()
     pc.setType("jacobi")
     kb.setPC(pc)
@@ -285,7 +289,8 @@ def main():
             "config": {"workload": f"KLE Laplacian {dim}-D box {nelem} ngl={args.ngl} (p={args.ngl - 1}), "
                                    f"TG-{dim}D Dirichlet on all faces; one CG(+Jacobi) iteration per step",
                        "nelem": nelem, "ngl": args.ngl, "n_dof": n_global, "nnz_K": tot_nnz,
-                       "ksp": "cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)",
+                       "ksp": ksp_type if ksp_type == "pipecg" else
+                       ("cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)"),
                        "pc": "jacobi", "matrix_format": info["format"], "row_pad_blocks": args.pad,
                        "spmv_loads": args.loads, "spmv_fused_dot": args.fused_dot,
                        "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},

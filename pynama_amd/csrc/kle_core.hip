@@ -260,23 +260,24 @@ static int stage_reserve(kle_ctx *ctx, int64_t n)
     return 0;
 }
 
-int allreduce_sum(kle_ctx *ctx, double *dbuf, int n)
+int allreduce_sum(kle_ctx *ctx, double *dbuf, int n, hipStream_t st)
 {
     if (ctx->nranks == 1) return 0;
+    if (!st) st = ctx->stream;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    KLE_TRY(ctx->tic("allreduce", &ev));
+    KLE_TRY(ctx->tic("allreduce", &ev, st));
     if (ctx->comm) {
-        KLE_NCCL(ncclAllReduce(dbuf, dbuf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+        KLE_NCCL(ncclAllReduce(dbuf, dbuf, n, ncclDouble, ncclSum, ctx->comm, st));
     } else {
         KLE_TRY(stage_reserve(ctx, n));
-        KLE_HIP(hipMemcpyAsync(ctx->h_stage, dbuf, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
-        KLE_HIP(hipStreamSynchronize(ctx->stream));
+        KLE_HIP(hipMemcpyAsync(ctx->h_stage, dbuf, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+        KLE_HIP(hipStreamSynchronize(st));
         if (ctx->hcomm.allreduce(ctx->h_stage, n, ctx->hcomm.user))
             return fail(KLE_ERR_COMM, "host allreduce callback failed");
-        KLE_HIP(hipMemcpyAsync(dbuf, ctx->h_stage, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
-        KLE_HIP(hipStreamSynchronize(ctx->stream));
+        KLE_HIP(hipMemcpyAsync(dbuf, ctx->h_stage, sizeof(double) * n, hipMemcpyHostToDevice, st));
+        KLE_HIP(hipStreamSynchronize(st));
     }
-    KLE_TRY(ctx->toc("allreduce", &ev));
+    KLE_TRY(ctx->toc("allreduce", &ev, st));
     return 0;
 }
 

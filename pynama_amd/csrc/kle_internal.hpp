@@ -197,12 +197,14 @@ namespace kle {
 // vec helpers used across translation units
 int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64_t glo,
               int64_t ghi, kle_vec **out);
-int allreduce_sum(kle_ctx *ctx, double *dbuf, int n);  // in place, device buffer
+int allreduce_sum(kle_ctx *ctx, double *dbuf, int n, hipStream_t s = nullptr);  // in place, device buffer
 int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all);
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
                   int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t s = nullptr);
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials,
          int *nparts, const int *istate);
+// true when spmv(A, x, ...) without a fused dot exchanges the halo on ctx->comm_stream
+bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
 extern int g_nb_pad;

@@ -160,6 +160,61 @@ __global__ __launch_bounds__(KB) void k_sr_update(int64_t n, const double *__res
     block_sums<2>(acc, partials, PART_STRIDE);
 }
 
+// Pipelined CG (Ghysels & Vanroose 2014; PETSc KSPPIPECG): with w = A u,
+// u = M r kept by recurrence, one fused pass per iteration
+//   z = n + b z, q = m + b q, s = w + b s, p = u + b p,
+//   x += a p, r -= a s, u -= a q, w -= a z, m = M w
+// partials: [0] r.u, [1] r.r, [2] w.u -- reduced while the SpMV n = A m runs.
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_pipe_update(int64_t n, const double *__restrict__ dinv,
+                                                    const double *__restrict__ nv, double *__restrict__ z,
+                                                    double *__restrict__ q, double *__restrict__ sv,
+                                                    double *__restrict__ p, double *__restrict__ x,
+                                                    double *__restrict__ r, double *__restrict__ u,
+                                                    double *__restrict__ w, double *__restrict__ m,
+                                                    double *__restrict__ partials, const double *__restrict__ scal,
+                                                    const int *__restrict__ ist)
+{
+    if (ist[I_REASON] != 0) return;
+    const double alpha = scal[S_ALPHA], beta = scal[S_BETA];
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double zi = nv[i] + beta * z[i];
+        const double qi = m[i] + beta * q[i];
+        const double si = w[i] + beta * sv[i];
+        const double pi = u[i] + beta * p[i];
+        z[i] = zi;
+        q[i] = qi;
+        sv[i] = si;
+        p[i] = pi;
+        x[i] += alpha * pi;
+        const double ri = r[i] - alpha * si;
+        const double ui = u[i] - alpha * qi;
+        const double wi = w[i] - alpha * zi;
+        r[i] = ri;
+        u[i] = ui;
+        w[i] = wi;
+        m[i] = JAC ? dinv[i] * wi : wi;
+        acc[0] += ri * ui;
+        acc[1] += ri * ri;
+        acc[2] += wi * ui;
+    }
+    block_sums<3>(acc, partials, PART_STRIDE);
+}
+
+// m = M w ; z = q = 0 (start of pipelined CG)
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_pipe_init(int64_t n, const double *__restrict__ dinv,
+                                                  const double *__restrict__ w, double *__restrict__ m,
+                                                  double *__restrict__ z, double *__restrict__ q)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        m[i] = JAC ? dinv[i] * w[i] : w[i];
+        z[i] = 0.0;
+        q[i] = 0.0;
+    }
+}
+
 enum Stage { ST_START = 0, ST_ALPHA = 1, ST_BETA = 2, ST_SR_START = 3, ST_SR = 4 };
 
 __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, double atol)
@@ -377,6 +432,7 @@ struct kle_ksp {
     kle_mat *A = nullptr;
     kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
     kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
+    kle_vec *m = nullptr, *nv = nullptr, *z = nullptr;  // pipelined CG
     int single_reduction = 0;
     int fused_dot = 0;  // 1: SpMV also forms the dot with its input (DOT variant)
     std::vector<kle_vec *> V;  // GMRES basis
@@ -397,7 +453,10 @@ static void free_work(kle_ksp *k)
     kle_vec_destroy(k->u);
     kle_vec_destroy(k->w);
     kle_vec_destroy(k->s);
-    k->u = k->w = k->s = nullptr;
+    kle_vec_destroy(k->m);
+    kle_vec_destroy(k->nv);
+    kle_vec_destroy(k->z);
+    k->u = k->w = k->s = k->m = k->nv = k->z = nullptr;
     for (auto v : k->V) kle_vec_destroy(v);
     k->V.clear();
     hipFree(k->d_Vptr);
@@ -469,29 +528,30 @@ static int spmv_dot(kle_ksp *k, kle_vec *x, kle_vec *y, double *partials, int *n
     return 0;
 }
 
-static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage)
+static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage, hipStream_t st = nullptr)
 {
     kle_ctx *c = k->ctx;
+    if (!st) st = c->stream;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    KLE_TRY(c->tic("reduce", &ev));
+    KLE_TRY(c->tic("reduce", &ev, st));
     const double *parts = c->d_partials;
     int big = 0;
     for (int q = 0; q < nq; ++q) big |= np.n[q] > 4096;
     if (big) {
         // first level per quantity (small quantities just copy through)
-        hipLaunchKernelGGL(k_reduce_l1, dim3(PART2_N), dim3(1024), 0, c->stream, c->d_partials, np, nq,
+        hipLaunchKernelGGL(k_reduce_l1, dim3(PART2_N), dim3(1024), 0, st, c->d_partials, np, nq,
                            c->d_istate, stage);
         parts = c->d_partials + PART2_OFF;
         for (int q = 0; q < nq; ++q) np.n[q] = PART2_N;
     }
     const int fuse = c->nranks == 1;
-    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, c->stream, parts, np, nq, c->d_scal,
+    hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, st, parts, np, nq, c->d_scal,
                        c->d_istate, stage, fuse, k->rtol, k->atol);
     KLE_HIP(hipGetLastError());
-    KLE_TRY(c->toc("reduce", &ev));
+    KLE_TRY(c->toc("reduce", &ev, st));
     if (!fuse) {
-        KLE_TRY(allreduce_sum(c, c->d_scal + S_SUM0, nq));
-        hipLaunchKernelGGL(k_scalars, dim3(1), dim3(1), 0, c->stream, c->d_scal, c->d_istate, stage, k->rtol, k->atol);
+        KLE_TRY(allreduce_sum(c, c->d_scal + S_SUM0, nq, st));
+        hipLaunchKernelGGL(k_scalars, dim3(1), dim3(1), 0, st, c->d_scal, c->d_istate, stage, k->rtol, k->atol);
         KLE_HIP(hipGetLastError());
     }
     return 0;
@@ -618,6 +678,99 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
             if (c->h_istate[I_REASON] != 0) break;
         }
     }
+    KLE_TRY(poll_state(k));
+    k->its = c->h_istate[I_ITS];
+    k->reason = c->h_istate[I_REASON];
+    if (k->reason == 0) k->reason = KLE_DIVERGED_ITS;
+    k->rnorm = std::sqrt(c->h_scal[S_RR]);
+    return 0;
+}
+
+
+// Pipelined CG (PETSc KSPPIPECG): the reduction of iteration i (and its
+// allreduce across ranks) runs on the comm stream while the SpMV n = A m of
+// the same iteration runs on the compute stream.  Same scalar recurrence as
+// the single-reduction CG (stages ST_SR_START / ST_SR).
+static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    kle_ctx *c = k->ctx;
+    const int64_t n = b->n_local;
+    const bool jac = k->pc == "jacobi";
+    const double *dinv = jac ? k->dinv->d : nullptr;
+    const int g = grid_for(n, KB, RED_BLOCKS);
+    int host_fixed[I_COUNT] = {0, 0, k->fixed, k->fixed ? k->fixed : k->maxit, 0, 0, 0, 0};
+    KLE_HIP(hipMemcpyAsync(c->d_istate, host_fixed, sizeof(int) * I_COUNT, hipMemcpyHostToDevice, c->stream));
+    if (jac)
+        hipLaunchKernelGGL(k_sr_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
+                           k->p->d, k->s->d, c->d_partials);
+    else
+        hipLaunchKernelGGL(k_sr_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
+                           k->p->d, k->s->d, c->d_partials);
+    KLE_HIP(hipGetLastError());
+    int np = 0;
+    KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, nullptr));  // w = A u, (w,u)
+    KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR_START));
+    if (jac)
+        hipLaunchKernelGGL(k_pipe_init<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d, k->z->d,
+                           k->q->d);
+    else
+        hipLaunchKernelGGL(k_pipe_init<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d, k->z->d,
+                           k->q->d);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, nullptr));  // n = A m
+    // the reduction may run beside the SpMV only where the SpMV's own halo uses
+    // the comm stream too (one RCCL stream: halo, then allreduce)
+    const bool side = spmv_uses_comm_stream(k->A, k->m);
+    hipEvent_t ev_upd = nullptr, ev_red = nullptr;
+    KLE_HIP(hipEventCreateWithFlags(&ev_upd, hipEventDisableTiming));
+    KLE_HIP(hipEventCreateWithFlags(&ev_red, hipEventDisableTiming));
+    const int limit = k->fixed ? k->fixed : k->maxit;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    int rc = 0;
+    for (int it = 0; it < limit && !rc; ++it) {
+        rc = c->tic("cg_update", &ev);
+        if (rc) break;
+        if (jac)
+            hipLaunchKernelGGL(k_pipe_update<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
+                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, c->d_partials,
+                               c->d_scal, c->d_istate);
+        else
+            hipLaunchKernelGGL(k_pipe_update<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
+                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, c->d_partials,
+                               c->d_scal, c->d_istate);
+        if (hipGetLastError() != hipSuccess) { rc = fail(KLE_ERR_DEVICE, "k_pipe_update launch failed"); break; }
+        if ((rc = c->toc("cg_update", &ev))) break;
+        if (side && c->nranks > 1) {
+            if (hipEventRecord(ev_upd, c->stream) != hipSuccess ||
+                hipStreamWaitEvent(c->comm_stream, ev_upd, 0) != hipSuccess) {
+                rc = fail(KLE_ERR_DEVICE, "event record/wait failed");
+                break;
+            }
+            if ((rc = spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, c->d_istate))) break;
+            if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR, c->comm_stream))) break;
+            if (hipEventRecord(ev_red, c->comm_stream) != hipSuccess ||
+                hipStreamWaitEvent(c->stream, ev_red, 0) != hipSuccess) {
+                rc = fail(KLE_ERR_DEVICE, "event record/wait failed");
+                break;
+            }
+        } else if (c->nranks > 1) {
+            // no overlap possible on this rank: same collective order as the
+            // overlapping ranks (halo, then allreduce), all on one stream
+            if ((rc = spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, c->d_istate))) break;
+            if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
+        } else {
+            // one rank: the scalar stage first, the SpMV behind it
+            if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
+            if ((rc = spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, c->d_istate))) break;
+        }
+        if (!k->fixed && ((it + 1) % k->check_every == 0)) {
+            if ((rc = poll_state(k))) break;
+            if (c->h_istate[I_REASON] != 0) break;
+        }
+    }
+    hipEventDestroy(ev_upd);
+    hipEventDestroy(ev_red);
+    if (rc) return rc;
     KLE_TRY(poll_state(k));
     k->its = c->h_istate[I_ITS];
     k->reason = c->h_istate[I_REASON];
@@ -764,7 +917,8 @@ int kle_ksp_set_type(kle_ksp *k, const char *t)
 {
     KLE_ARG(k && t, "null arg");
     std::string s(t);
-    KLE_ARG(s == "cg" || s == "gmres" || s == "preonly", "unknown KSP type '%s' (cg|gmres|preonly)", t);
+    KLE_ARG(s == "cg" || s == "pipecg" || s == "gmres" || s == "preonly", "unknown KSP type '%s' (cg|pipecg|gmres|preonly)",
+            t);
     k->type = s;
     k->setup = false;
     return 0;
@@ -841,10 +995,15 @@ int kle_ksp_set_up(kle_ksp *k)
     KLE_TRY(make_vec_like_cols(k, &k->r));
     KLE_TRY(make_vec_like_cols(k, &k->p));
     KLE_TRY(make_vec_like_cols(k, &k->q));
-    if (k->type == "cg" && k->single_reduction) {
+    if ((k->type == "cg" && k->single_reduction) || k->type == "pipecg") {
         KLE_TRY(make_vec_like_cols(k, &k->u));
         KLE_TRY(make_vec_like_cols(k, &k->w));
         KLE_TRY(make_vec_like_cols(k, &k->s));
+    }
+    if (k->type == "pipecg") {
+        KLE_TRY(make_vec_like_cols(k, &k->m));
+        KLE_TRY(make_vec_like_cols(k, &k->nv));
+        KLE_TRY(make_vec_like_cols(k, &k->z));
     }
     if (k->pc == "jacobi") {
         KLE_TRY(make_vec_like_cols(k, &k->dinv));
@@ -874,7 +1033,8 @@ int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(kle_ksp_set_up(k));
     KLE_ARG(b->n_local == k->A->m_local && x->n_local == k->A->n_local, "b/x sizes do not match the operator");
     k->true_rel = -1;
-    if (k->type == "cg" && k->single_reduction) KLE_TRY(solve_cg_single(k, b, x));
+    if (k->type == "pipecg") KLE_TRY(solve_pipecg(k, b, x));
+    else if (k->type == "cg" && k->single_reduction) KLE_TRY(solve_cg_single(k, b, x));
     else if (k->type == "cg") KLE_TRY(solve_cg(k, b, x));
     else KLE_TRY(solve_gmres(k, b, x));
     if (!k->fixed) KLE_TRY(true_residual(k, b, x));

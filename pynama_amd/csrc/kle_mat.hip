@@ -448,6 +448,12 @@ static int nb_build_order(kle_mat *A)
     return 0;
 }
 
+bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
+{
+    return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi && !A->spmv_order &&
+           !A->spmv_buf && !A->spmv_persistent && (x->lo_rank >= 0 || x->hi_rank >= 0);
+}
+
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials, int *nparts,
          const int *istate)
 {
@@ -457,9 +463,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
     if (A->kind == 0) {
         // N > 1: rows [int_lo, int_hi) read no ghost entry, so they run while the
         // halo is in flight on the comm stream; the ghost-dependent rows follow
-        const bool overlap = c->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi && !dot &&
-                             !A->spmv_order && !A->spmv_buf && !A->spmv_persistent &&
-                             (x->lo_rank >= 0 || x->hi_rank >= 0);
+        const bool overlap = !dot && spmv_uses_comm_stream(A, x);
         if (c->nranks > 1 && !overlap)
             KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
                                   x->send_lo, x->send_hi));

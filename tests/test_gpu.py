@@ -140,7 +140,7 @@ def test_spmv_and_solve(pa, case):
         assert np.linalg.norm(u - g["u_exact"]) < 1e-5   # test_solver.py:37
 
 
-@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("single", [False, True, "pipecg"])
 @pytest.mark.parametrize("case", ["tg2d", "tg3d_p4"])
 def test_cg_iterations_match_oracle(pa, case, single):
     g = _golden(case)
@@ -151,18 +151,21 @@ def test_cg_iterations_match_oracle(pa, case, single):
     K = O.CSR.from_arrays(g["K_indptr"], g["K_indices"], g["K_data"], int(g["K_shape"][1]))
     xo, it_o, rr_o = K.cg(g["b"], rtol=1e-10, jacobi=True)
     ksp = pa.petsc.KSP().create()
-    ksp.setType("cg")
+    ksp.setType("pipecg" if single == "pipecg" else "cg")
     pc = pa.petsc.PC()
     pc.setType("jacobi")
     ksp.setPC(pc)
     ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
-    ksp.setCGSingleReduction(single)  # Chronopoulos-Gear: same iterates in exact arithmetic
+    if single != "pipecg":
+        ksp.setCGSingleReduction(single)  # Chronopoulos-Gear: same iterates in exact arithmetic
     ksp.setOperators(mat.K)
     b = mat.K.createVecLeft()
     b.setArray(g["b"])
     x = mat.K.createVecRight()
     ksp.solve(b, x)
-    assert abs(ksp.getIterationNumber() - it_o) <= (2 if single else 1)
+    # pipelined CG: same iterates in exact arithmetic, recurrences drift more in fp64
+    tol_its = {False: 1, True: 2, "pipecg": 4}[single]
+    assert abs(ksp.getIterationNumber() - it_o) <= tol_its
     assert ksp.getTrueRelativeResidual() <= 1.01e-10 * 1.5
     assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
 

@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, size, port, nelem, ngl, q, overlap=True):
+def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg"):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="host",
@@ -51,6 +51,8 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True):
         sol.setMat(mat)
         sol.setUp()
         ksp = sol.getKSP()
+        if ksp_type != "cg":
+            ksp.setType(ksp_type)
         ksp.setTolerances(rtol=1e-11)
         f = pa.fields.get("taylor_green3d")
         vort = mat.Rw.createVecRight()
@@ -75,19 +77,24 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("overlap,ksp_type", [(True, "cg"), (False, "cg"), (True, "pipecg")])
 @pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 4), (3, [2, 3, 3], 3)])
-def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap):
+def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap, ksp_type):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type)) for r in range(size)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=600) for _ in range(size)], key=lambda r: r["rank"])
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(size)], key=lambda r: r["rank"])
+    except Exception:
+        for p in procs:
+            p.kill()
+        raise
     for p in procs:
         p.join(timeout=120)
     for r in res:
@@ -115,7 +122,7 @@ def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap):
     assert np.linalg.norm(u - xs) <= 1e-8 * np.linalg.norm(xs)
     for r in res:
         # cross-rank sums change the rounding: counts agree to a couple of iterations
-        assert abs(r["its"] - its) <= 3
+        assert abs(r["its"] - its) <= (3 if ksp_type == "cg" else 6)
         assert r["true"] < 1e-10
         # each rank's rows of K: PETSc pattern, oracle values
         rows = slice(r["lo"], r["hi"])

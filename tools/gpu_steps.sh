@@ -3,6 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1  # step logs grow while a step runs
 step() {  # step <name> <timeout-seconds> <cmd...>
   local name=$1 t=$2; shift 2
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
