@@ -236,6 +236,9 @@ int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X);
 int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out);
 /* Scalar CSR of the owned rows with GLOBAL column ids, PETSc pattern. */
 int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz);
+/* Mat.getRow(row) (dmplex.py:332,363): owned global row -> global columns and
+ * values in PETSc's pattern; call with cols = vals = NULL for the length. */
+int kle_mat_get_row(const kle_mat *A, int64_t row, int64_t *ncols, int64_t *cols, double *vals);
 int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double *data);
 /* Convert (single rank) to the scalar-CSR device format (the AIJ kernel). */
 int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);

@@ -114,6 +114,7 @@ _SIGS = {
     "kle_mat_axpy": [vp, C.c_double, vp],
     "kle_mat_duplicate": [vp, C.c_int, pvp],
     "kle_mat_get_csr_size": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
+    "kle_mat_get_row": [vp, C.c_int64, C.POINTER(C.c_int64), vp, vp],
     "kle_mat_get_csr": [vp, i64p, i64p, f64p],
     "kle_mat_convert_aij": [vp, pvp],
     "kle_mat_set_spmv_variant": [vp, C.c_int, C.c_int, C.c_int],

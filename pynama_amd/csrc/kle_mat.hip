@@ -967,6 +967,54 @@ int kle_mat_get_csr_size(const kle_mat *A, int64_t *m_local, int64_t *nnz)
     return 0;
 }
 
+int kle_mat_get_row(const kle_mat *A, int64_t row, int64_t *ncols, int64_t *cols, double *vals)
+{
+    KLE_ARG(A && ncols, "null arg");
+    KLE_ARG(row >= A->row_lo && row < A->row_lo + A->m_local, "row %lld not owned", (long long)row);
+    const int64_t lr = row - A->row_lo;
+    std::vector<int64_t> c;
+    std::vector<double> v;
+    if (A->kind == 1) {
+        KLE_ARG(A->assembled, "matrix not assembled");
+        const int64_t b = A->h_ptr[lr], e = A->h_ptr[lr + 1];
+        c.assign(A->h_col.begin() + b, A->h_col.begin() + e);
+        v.resize(e - b);
+        if (e > b) KLE_HIP(hipMemcpy(v.data(), A->d_aval + b, sizeof(double) * (e - b), hipMemcpyDeviceToHost));
+    } else {
+        const int R = A->R, C = A->C;
+        const int64_t i = lr / R;
+        const int a = (int)(lr % R);
+        int rp[2], cnt = 0;
+        KLE_HIP(hipMemcpy(rp, A->d_rowptr + i, sizeof(int) * 2, hipMemcpyDeviceToHost));
+        if (A->d_rowcnt) KLE_HIP(hipMemcpy(&cnt, A->d_rowcnt + i, sizeof(int), hipMemcpyDeviceToHost));
+        else cnt = rp[1] - rp[0];
+        const int mp = rp[1] - rp[0];
+        std::vector<int> bc(std::max(cnt, 1));
+        std::vector<double> vals_a((size_t)C * std::max(mp, 1));
+        if (cnt) KLE_HIP(hipMemcpy(bc.data(), A->d_bcol + rp[0], sizeof(int) * cnt, hipMemcpyDeviceToHost));
+        if (mp)
+            KLE_HIP(hipMemcpy(vals_a.data(), A->d_val + (int64_t)rp[0] * R * C + (int64_t)a * C * mp,
+                              sizeof(double) * C * mp, hipMemcpyDeviceToHost));
+        if (A->diag_only_row[i]) {
+            if (a < C) {
+                c.push_back((A->node_begin + i) * C + a);
+                v.push_back(vals_a[(size_t)a * mp]);
+            }
+        } else {
+            for (int k = 0; k < cnt; ++k)
+                for (int b = 0; b < C; ++b) {
+                    if (A->mask_rule != MASK_NONE && !nb_entry_exists(A, i, a, bc[k], b)) continue;
+                    c.push_back((A->ext_begin + bc[k]) * C + b);
+                    v.push_back(vals_a[(size_t)b * mp + k]);
+                }
+        }
+    }
+    *ncols = (int64_t)c.size();
+    if (cols) std::copy(c.begin(), c.end(), cols);
+    if (vals) std::copy(v.begin(), v.end(), vals);
+    return 0;
+}
+
 int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double *data)
 {
     KLE_ARG(A && indptr && indices && data, "null arg");

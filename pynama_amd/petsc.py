@@ -493,6 +493,15 @@ class Mat:
         m, n = self.getSize()
         return Mat._wrap(h, self._ctx)
 
+    def getRow(self, row):
+        """(cols, values) of owned global row `row` (PETSc pattern, explicit zeros kept)."""
+        n = C.c_int64()
+        call("kle_mat_get_row", self._h, int(row), C.byref(n), None, None)
+        cols = np.zeros(max(n.value, 1), dtype=np.int64)
+        vals = np.zeros(max(n.value, 1))
+        call("kle_mat_get_row", self._h, int(row), C.byref(n), cols.ctypes.data, vals.ctypes.data)
+        return cols[:n.value], vals[:n.value]
+
     def getValuesCSR(self):
         """(indptr, indices, data) of the owned rows, global column ids."""
         m, nz = C.c_int64(), C.c_int64()

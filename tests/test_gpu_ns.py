@@ -141,3 +141,17 @@ def test_eval_rhs_noslip_matches_reference(pa):
     assert np.linalg.norm(u - g["rhs_vel"]) <= 1e-9 * np.linalg.norm(g["rhs_vel"])
     scale = max(1.0, np.abs(g["rhs_f"]).max())
     assert np.abs(f.getArray() - g["rhs_f"]).max() <= 1e-6 * scale
+
+
+def test_getrow_matches_csr(pa):
+    """Mat.getRow (petsc4py, dmplex.py:332,363) on node-block matrices with and
+    without DoF-level masks, and on a scalar AIJ matrix."""
+    dom, mat = _matns(pa, 2, [4, 4], 3, CAVITY)
+    rng = np.random.default_rng(2)
+    for A in (mat.K, mat.Kfs, mat.Krhsfs, mat.Rwfs, mat.getKplusKfs(), mat.getOperators().SrT, mat.K + mat.Kfs):
+        ip, ix, d = A.getValuesCSR()
+        lo, _ = A.getOwnershipRange()
+        for r in rng.choice(len(ip) - 1, 12, replace=False):
+            cols, vals = A.getRow(lo + r)
+            np.testing.assert_array_equal(cols, ix[ip[r]:ip[r + 1]])
+            np.testing.assert_array_equal(vals, d[ip[r]:ip[r + 1]])
