@@ -251,6 +251,11 @@ int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt);
 /* SpMV rows per wavefront (3x3 blocks, unfused): > 1 selects the kernel that
  * prefetches the next row's extent while streaming the current row. */
 int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq);
+/* Structured columns: when every row's columns form a lattice box (K, Rw and
+ * the operators on box meshes) the SpMV computes them from 8 B per row instead
+ * of streaming 4 B per block (default on; 0 forces the column stream). */
+int kle_mat_set_spmv_structured(kle_mat *A, int on);
+int kle_mat_is_structured(const kle_mat *A, int *on);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on; needs the unfused CG dot). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

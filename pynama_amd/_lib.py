@@ -122,6 +122,8 @@ _SIGS = {
     "kle_mat_set_spmv_buffer_variant": [vp, C.c_int],
     "kle_set_nb_pad": [C.c_int],
     "kle_mat_set_halo_overlap": [vp, C.c_int],
+    "kle_mat_set_spmv_structured": [vp, C.c_int],
+    "kle_mat_is_structured": [vp, C.POINTER(C.c_int)],
     "kle_mat_set_spmv_rows_per_wave": [vp, C.c_int],
     "kle_get_nb_pad": [],
     "kle_mat_set_spmv_nontemporal": [vp, C.c_int],

@@ -23,6 +23,7 @@
 //                mat_fs.py:158-189.
 #include <algorithm>
 #include <atomic>
+#include <thread>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -410,6 +411,33 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
         last_lo = std::max(last_lo, t_lo[t]);
         first_hi = std::min(first_hi, t_hi[t]);
     }
+    // structured columns? each row's column list must be exactly a lattice box
+    const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
+    std::vector<int> box(2 * std::max<int64_t>(nrows, 1), 0);
+    std::atomic<bool> is_box{nrows > 0};
+    parallel_for(nrows, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi && is_box.load(std::memory_order_relaxed); ++i) {
+            const int64_t b = rp[i], e = rp[i + 1];
+            if (e == b) continue;  // empty row (Rw Dirichlet rows): box stays 0 x 0
+            const int64_t c0 = cols[b] - m->ext_begin, c1 = cols[e - 1] - m->ext_begin;
+            const int64_t nx = c1 % Lx - c0 % Lx + 1, ny = (c1 / Lx) % m->L[1] - (c0 / Lx) % m->L[1] + 1,
+                          nz = c1 / Lxy - c0 / Lxy + 1;
+            if (nx < 1 || ny < 1 || nz < 1 || nx > 255 || ny > 255 || nz > 255 || nx * ny * nz != e - b) {
+                is_box = false;
+                return;
+            }
+            int64_t k = b;
+            for (int64_t z = 0; z < nz; ++z)
+                for (int64_t y = 0; y < ny; ++y)
+                    for (int64_t x = 0; x < nx; ++x, ++k)
+                        if (cols[k] - m->ext_begin != c0 + x + Lx * y + Lxy * z) {
+                            is_box = false;
+                            return;
+                        }
+            box[2 * i] = (int)c0;
+            box[2 * i + 1] = (int)(nx | (ny << 8) | (nz << 16));
+        }
+    });
     kle_mat *A = new kle_mat;
     A->ctx = ctx;
     A->kind = 0;
@@ -421,6 +449,8 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->pad = pad;
     A->int_lo = last_lo + 1;
     A->int_hi = first_hi;
+    A->box_lx = Lx;
+    A->box_lxy = Lxy;
     if (const char *e = getenv("KLE_HALO_OVERLAP")) A->halo_overlap = atoi(e) != 0;
     A->node_begin = m->node_begin;
     A->ext_begin = m->ext_begin;
@@ -458,6 +488,10 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
         KLE_HIP(hipMemcpyAsync(A->d_rowcnt, cnt.data(), sizeof(int) * std::max<int64_t>(nrows, 1), hipMemcpyHostToDevice,
                                ctx->stream));
     if (pad > 1) KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(nbp * R * C, 1), ctx->stream));
+    if (is_box) {
+        KLE_HIP(hipMalloc(&A->d_rowbox, sizeof(int) * 2 * nrows));
+        KLE_HIP(hipMemcpyAsync(A->d_rowbox, box.data(), sizeof(int) * 2 * nrows, hipMemcpyHostToDevice, ctx->stream));
+    }
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     *out = A;
     return 0;

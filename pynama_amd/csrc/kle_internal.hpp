@@ -162,6 +162,12 @@ struct kle_mat {
     int64_t node_begin = 0, ext_begin = 0, ext_nodes = 0;
     int *d_rowptr = nullptr;   // [nrows+1] block offsets (rows padded to `pad` blocks)
     int *d_rowcnt = nullptr;   // [nrows] real block count per row (null when pad == 1)
+    // structured columns: every row's columns are the ext-lattice box
+    // base + [0,nx) + Lx [0,ny) + Lx Ly [0,nz) -> the SpMV computes them
+    // instead of streaming bcol (d_rowbox[2*i] = base, [2*i+1] = nx | ny<<8 | nz<<16)
+    int *d_rowbox = nullptr;
+    int64_t box_lx = 0, box_lxy = 0;
+    int spmv_struct = 1;  // use d_rowbox when present
     int64_t nblocks_real = 0;
     int pad = 1;
     int *d_bcol = nullptr;     // [nblocks] local ext node index

@@ -67,6 +67,7 @@ struct RowMap {
 template <int R, int C, bool DOT, int LPR, int UNR, bool NT>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__restrict__ rowptr,
                                                         const int *__restrict__ rowcnt,
+                                                        const int *__restrict__ rowbox, int lx, int lxy,
                                                         const int *__restrict__ bcol,
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x,
@@ -89,11 +90,17 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
         const int64_t r = base + sub;
         const bool valid = r < nrows;
         const int64_t i = !valid ? 0 : order ? order[r] : r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
-        int b0 = 0, m = 0, mp = 0;
+        int b0 = 0, m = 0, mp = 0, bbase = 0, bnx = 1, bnxy = 1;
         if (valid) {
             b0 = rowptr[i];
             mp = rowptr[i + 1] - b0;
             m = rowcnt ? rowcnt[i] : mp;
+            if (rowbox) {
+                bbase = rowbox[2 * i];
+                const int d = rowbox[2 * i + 1];
+                bnx = d & 255;
+                bnxy = bnx * ((d >> 8) & 255);
+            }
         }
         const double *v = val + (int64_t)b0 * (R * C);
         const int *cj = bcol + b0;
@@ -108,7 +115,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
             for (int u = 0; u < UNR; ++u) {
                 const int ku = k + u * LPR;
                 on[u] = ku < m;
-                j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
+                if (rowbox) {
+                    // column of block ku inside the row's lattice box (no bcol stream)
+                    const int kz = ku / bnxy, rem = ku - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
+                    j[u] = on[u] ? bbase + kx + lx * ky + lxy * kz : 0;
+                } else {
+                    j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
+                }
 #pragma unroll
                 for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + (int64_t)t * mp + ku) : 0.0;
             }
@@ -522,6 +535,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (nparts) *nparts = grid;
         const double *pd = dot ? dotvec->d : nullptr;
         KLE_TRY(c->tic("spmv", &ev));
+        const int *rbox = A->spmv_struct ? A->d_rowbox : nullptr;
         RowMap rm{0, A->nrows, 0, 0};
         if (overlap) {
             rm = RowMap{A->int_lo, A->int_hi - A->int_lo, 0, 0};
@@ -561,12 +575,14 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
     do {                                                                                                \
         if (dot)                                                                                        \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
-                               c->stream, rm, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base,   \
-                               y->d, pd, partials, istate, order, xcd);                                 \
+                               c->stream, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,           \
+                               (int)A->box_lxy, A->d_bcol, A->d_val, x->base, y->d, pd, partials,       \
+                               istate, order, xcd);                                                     \
         else                                                                                            \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0, \
-                               c->stream, rm, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base,   \
-                               y->d, pd, partials, istate, order, xcd);                                 \
+                               c->stream, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,           \
+                               (int)A->box_lxy, A->d_bcol, A->d_val, x->base, y->d, pd, partials,       \
+                               istate, order, xcd);                                                     \
     } while (0)
 #define NB_VARIANTS(RR, CC)                                                                             \
     if (A->spmv_lpr == 64 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 1, true);         \
@@ -817,6 +833,7 @@ int kle_mat_destroy(kle_mat *A)
     if (!A) return 0;
     hipFree(A->d_order);
     hipFree(A->d_rowcnt);
+    hipFree(A->d_rowbox);
     hipFree(A->d_rowptr);
     hipFree(A->d_bcol);
     hipFree(A->d_val);
@@ -1117,6 +1134,7 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     kle_mat *B = new kle_mat(*A);
     B->d_order = nullptr;
     B->d_rowcnt = nullptr;
+    B->d_rowbox = nullptr;
     B->d_rowptr = nullptr;
     B->d_bcol = nullptr;
     B->d_val = nullptr;
@@ -1132,6 +1150,10 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         if (A->d_rowcnt) {
             KLE_HIP(hipMalloc(&B->d_rowcnt, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
             KLE_HIP(hipMemcpy(B->d_rowcnt, A->d_rowcnt, sizeof(int) * A->nrows, hipMemcpyDeviceToDevice));
+        }
+        if (A->d_rowbox) {
+            KLE_HIP(hipMalloc(&B->d_rowbox, sizeof(int) * 2 * std::max<int64_t>(A->nrows, 1)));
+            KLE_HIP(hipMemcpy(B->d_rowbox, A->d_rowbox, sizeof(int) * 2 * A->nrows, hipMemcpyDeviceToDevice));
         }
         KLE_HIP(hipMemcpy(B->d_bcol, A->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1), hipMemcpyDeviceToDevice));
         if (copy_values) KLE_HIP(hipMemcpy(B->d_val, A->d_val, sizeof(double) * nv, hipMemcpyDeviceToDevice));
@@ -1160,6 +1182,20 @@ int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq)
 {
     KLE_ARG(A && seq >= 1 && seq <= 64, "rows per wave must be in [1,64]");
     A->spmv_seq = seq;
+    return 0;
+}
+
+int kle_mat_set_spmv_structured(kle_mat *A, int on)
+{
+    KLE_ARG(A, "null matrix");
+    A->spmv_struct = on != 0;
+    return 0;
+}
+
+int kle_mat_is_structured(const kle_mat *A, int *on)
+{
+    KLE_ARG(A && on, "null arg");
+    *on = A->d_rowbox != nullptr;
     return 0;
 }
 
@@ -1214,8 +1250,11 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
 {
     KLE_ARG(A && bytes, "null arg");
     if (A->kind == 0) {
-        // useful bytes: real blocks only (row padding is not counted)
-        *bytes = (double)A->nblocks_real * (A->R * A->C * 8.0 + 4.0) + (A->nrows + 1) * 4.0 +
+        // bytes the SpMV must move: real blocks only (row padding is not counted);
+        // the column stream unless the columns are computed from row boxes
+        const bool sb = A->spmv_struct && A->d_rowbox;
+        *bytes = (double)A->nblocks_real * (A->R * A->C * 8.0 + (sb ? 0.0 : 4.0)) + (A->nrows + 1) * 4.0 +
+                 (A->d_rowcnt ? A->nrows * 4.0 : 0.0) + (sb ? A->nrows * 8.0 : 0.0) +
                  (double)A->ext_nodes * A->C * 8.0 + (double)A->m_local * 8.0;
     } else {
         *bytes = (double)A->nnz * 12.0 + (A->m_local + 1) * 8.0 + A->n_local * 8.0 + A->m_local * 8.0;

@@ -386,6 +386,14 @@ class Mat:
     def setSpmvRowsPerWave(self, seq):
         call("kle_mat_set_spmv_rows_per_wave", self._h, int(seq))
 
+    def setSpmvStructured(self, on=True):
+        call("kle_mat_set_spmv_structured", self._h, int(bool(on)))
+
+    def isStructured(self):
+        v = C.c_int()
+        call("kle_mat_is_structured", self._h, C.byref(v))
+        return bool(v.value)
+
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))
 
