@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--aij", action="store_true", help="also time the scalar-CSR (aij) SpMV")
-    ap.add_argument("--pad", type=int, default=16, help="row padding quantum of K's value streams (blocks)")
+    ap.add_argument("--layout", type=int, choices=[0, 1], default=1,
+                    help="node-block value layout: 1 = 16-block chunks + packed tail, 0 = padded row streams")
+    ap.add_argument("--pad", type=int, default=16, help="row padding quantum of layout 0 (blocks)")
     ap.add_argument("--ops", action="store_true",
                     help="also assemble Curl/SrT/DivSrT and time their SpMVs and the evalRHS operator chain")
     ap.add_argument("--fused-dot", action="store_true", help="form the CG dot inside the SpMV kernel")
@@ -127,6 +129,7 @@ def main():
 
     ctx = pa.get_ctx()
     pa.runtime.set_row_padding(args.pad)
+    pa.runtime.set_value_layout(args.layout)
     rank, nranks = ctx.rank, ctx.nranks
     nelem = [int(v) for v in args.nelem.split(",")]
     dim = len(nelem)
@@ -258,7 +261,8 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
-            key = f"{nelem}-{args.ngl}-{nranks}-pad{args.pad}-{args.loads}-u1" + ("-fused" if args.fused_dot else "")
+            key = (f"{nelem}-{args.ngl}-{nranks}-" + ("chunk" if args.layout == 1 else f"pad{args.pad}") +
+                   f"-{args.loads}-u1" + ("-struct" if K.isStructured() else "") + ("-fused" if args.fused_dot else ""))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -291,7 +295,8 @@ def main():
                        "nelem": nelem, "ngl": args.ngl, "n_dof": n_global, "nnz_K": tot_nnz,
                        "ksp": ksp_type if ksp_type == "pipecg" else
                        ("cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)"),
-                       "pc": "jacobi", "matrix_format": info["format"], "row_pad_blocks": args.pad,
+                       "pc": "jacobi", "matrix_format": info["format"], "value_layout": "chunk16+tail" if args.layout == 1 else f"row streams padded to {args.pad}",
+                       "structured_columns": K.isStructured(),
                        "spmv_loads": args.loads, "spmv_fused_dot": args.fused_dot,
                        "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -264,6 +264,12 @@ int kle_mat_set_halo_overlap(kle_mat *A, int on);
  * (16 = one 128-B line) so adjacent streams never share a cache line. */
 int kle_set_nb_pad(int quantum);  /* default 16 */
 int kle_get_nb_pad(void);
+/* Value layout of node-block matrices created afterwards: 0 = each row's
+ * R*C value streams padded to the pad quantum; 1 = 16-block chunks (each
+ * stream's 128-B line per chunk) + packed tail, rows 128-B aligned (no
+ * per-stream padding). */
+int kle_set_nb_layout(int layout);
+int kle_get_nb_layout(void);
 /* Buffer-descriptor SpMV variants (cache-policy study): 0 off, 1 aux 0, 2 nt,
  * 3 sc0|nt, 4 sc1, 5 sc1|nt, 6 sc1|sc0|nt, 7 sc1|sc0, 8 nt with the x gather
  * dropped (timing diagnostic only: wrong results). */

@@ -126,6 +126,8 @@ _SIGS = {
     "kle_mat_is_structured": [vp, C.POINTER(C.c_int)],
     "kle_mat_set_spmv_rows_per_wave": [vp, C.c_int],
     "kle_get_nb_pad": [],
+    "kle_set_nb_layout": [C.c_int],
+    "kle_get_nb_layout": [],
     "kle_mat_set_spmv_nontemporal": [vp, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],
     "kle_mat_spmv_bytes": [vp, C.POINTER(C.c_double)],

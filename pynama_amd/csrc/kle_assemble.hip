@@ -290,7 +290,8 @@ struct MeshDev {
 // MODE 0: K (free cols, +K_e), 1: Krhs (Dirichlet cols, -K_e), 2: Rw (+Rw_e)
 template <int R, int C, int MODE>
 __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const int *__restrict__ rowptr,
-                                                const int *__restrict__ rowcnt, const int *__restrict__ bcol,
+                                                const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
+                                                int lay, const int *__restrict__ bcol,
                                                 const uint8_t *__restrict__ dir,
                                                 const double *__restrict__ Eblk, double *__restrict__ val)
 {
@@ -299,12 +300,12 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
     if (row >= nrows) return;
     const int64_t gi = M.node_begin + row;
     const int b0 = rowptr[row], mp = rowptr[row + 1] - b0, m = rowcnt ? rowcnt[row] : mp;
-    double *v = val + (int64_t)b0 * R * C;
+    double *v = val + vptr[row];
     if (dir[gi - M.ext_begin]) {
         // K[dir,dir] = 0 + ... + 0 + 1 and Krhs[dir,dir] = 1 (mat_fs.py:115-120,182-183)
         if (MODE != 2 && lane == 0 && m == 1)
             for (int a = 0; a < R; ++a)
-                for (int b = 0; b < C; ++b) v[(a * C + b) * (int64_t)mp] = (a == b) ? 1.0 : 0.0;
+                for (int b = 0; b < C; ++b) v[vofs(lay, R * C, a * C + b, 0, m, mp)] = (a == b) ? 1.0 : 0.0;
         return;
     }
     int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], M.dim == 3 ? gi / (M.L[0] * M.L[1]) : 0};
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
 #pragma unroll
         for (int a = 0; a < R; ++a)
 #pragma unroll
-            for (int b = 0; b < C; ++b) v[(a * C + b) * (int64_t)mp + k] = acc[a * C + b];
+            for (int b = 0; b < C; ++b) v[vofs(lay, R * C, a * C + b, k, m, mp)] = acc[a * C + b];
     }
 }
 
@@ -377,7 +378,8 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     KLE_TRY(pattern_csr(m, which, rp, cols));
     const int64_t nb = rp[nrows];
     if (nb >= (1ll << 31) / 1) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
-    const int pad = std::max(1, g_nb_pad);
+    const int lay = g_nb_layout;
+    const int pad = lay == 1 ? 1 : std::max(1, g_nb_pad);
     std::vector<int> rp32(nrows + 1), cnt(nrows);
     int64_t nbp = 0;
     for (int64_t i = 0; i < nrows; ++i) {
@@ -447,6 +449,13 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->nblocks = nbp;
     A->nblocks_real = nb;
     A->pad = pad;
+    A->vlayout = lay;
+    std::vector<int64_t> vptr(nrows + 1, 0);
+    for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t mi = rp[i + 1] - rp[i];
+        vptr[i + 1] = vptr[i] + (lay == 1 ? (mi * R * C + 15) / 16 * 16 : (int64_t)(rp32[i + 1] - rp32[i]) * R * C);
+    }
+    A->nvals = vptr[nrows];
     A->int_lo = last_lo + 1;
     A->int_hi = first_hi;
     A->box_lx = Lx;
@@ -476,7 +485,8 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     if (hipMalloc(&A->d_rowptr, sizeof(int) * (nrows + 1)) != hipSuccess ||
         (pad > 1 && hipMalloc(&A->d_rowcnt, sizeof(int) * std::max<int64_t>(nrows, 1)) != hipSuccess) ||
         hipMalloc(&A->d_bcol, sizeof(int) * std::max<int64_t>(nbp, 1)) != hipSuccess ||
-        hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nbp * R * C, 1)) != hipSuccess) {
+        hipMalloc(&A->d_vptr, sizeof(int64_t) * (nrows + 1)) != hipSuccess ||
+        hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(A->nvals, 1)) != hipSuccess) {
         kle_mat_destroy(A);
         return fail(KLE_ERR_MEM, "out of device memory for a %lld-block matrix", (long long)nb);
     }
@@ -487,7 +497,9 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     if (A->d_rowcnt)
         KLE_HIP(hipMemcpyAsync(A->d_rowcnt, cnt.data(), sizeof(int) * std::max<int64_t>(nrows, 1), hipMemcpyHostToDevice,
                                ctx->stream));
-    if (pad > 1) KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(nbp * R * C, 1), ctx->stream));
+    KLE_HIP(hipMemcpyAsync(A->d_vptr, vptr.data(), sizeof(int64_t) * (nrows + 1), hipMemcpyHostToDevice, ctx->stream));
+    if (pad > 1 || lay == 1)
+        KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(A->nvals, 1), ctx->stream));
     if (is_box) {
         KLE_HIP(hipMalloc(&A->d_rowbox, sizeof(int) * 2 * nrows));
         KLE_HIP(hipMemcpyAsync(A->d_rowbox, box.data(), sizeof(int) * 2 * nrows, hipMemcpyHostToDevice, ctx->stream));
@@ -586,7 +598,9 @@ static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, doubl
 // times 1/W_n, W_n = sum_e c_{e,l(n)} (Vec.reciprocal + diagonalScale(L)).
 struct OpsOut {
     double *curl, *srt, *div;
-    const int *rp_c, *rp_s, *rp_d;  // padded row offsets of each matrix
+    const int *rp_c, *rp_s, *rp_d;        // block row offsets (padded) of each matrix
+    const int64_t *vp_c, *vp_s, *vp_d;    // value row offsets
+    int lay;
 };
 
 template <int DIM>
@@ -638,9 +652,9 @@ __global__ __launch_bounds__(256) void k_ops_gather(MeshDev M, int64_t nrows, co
     const double wi = winv[row];
     const int mpc = out.rp_c[row + 1] - out.rp_c[row], mps = out.rp_s[row + 1] - out.rp_s[row],
               mpd = out.rp_d[row + 1] - out.rp_d[row];
-    double *vc = out.curl + (int64_t)out.rp_c[row] * DW * DIM;
-    double *vs = out.srt + (int64_t)out.rp_s[row] * DS * DIM;
-    double *vd = out.div + (int64_t)out.rp_d[row] * DIM * DS;
+    double *vc = out.curl + out.vp_c[row];
+    double *vs = out.srt + out.vp_s[row];
+    double *vd = out.div + out.vp_d[row];
     for (int k = lane; k < m; k += 64) {
         const int64_t gj = M.ext_begin + bcol[bc0 + k];
         const int64_t cj[3] = {gj % M.L[0], (gj / M.L[0]) % M.L[1], DIM == 3 ? gj / (M.L[0] * M.L[1]) : 0};
@@ -719,9 +733,9 @@ __global__ __launch_bounds__(256) void k_ops_gather(MeshDev M, int64_t nrows, co
                         D[1 * 3 + 2] += c * H[1];
                     }
                 }
-        for (int t = 0; t < DW * DIM; ++t) vc[(int64_t)t * mpc + k] = C[t] * wi;
-        for (int t = 0; t < DS * DIM; ++t) vs[(int64_t)t * mps + k] = S[t] * wi;
-        for (int t = 0; t < DIM * DS; ++t) vd[(int64_t)t * mpd + k] = D[t] * wi;
+        for (int t = 0; t < DW * DIM; ++t) vc[vofs(out.lay, DW * DIM, t, k, m, mpc)] = C[t] * wi;
+        for (int t = 0; t < DS * DIM; ++t) vs[vofs(out.lay, DS * DIM, t, k, m, mps)] = S[t] * wi;
+        for (int t = 0; t < DIM * DS; ++t) vd[vofs(out.lay, DIM * DS, t, k, m, mpd)] = D[t] * wi;
     }
 }
 
@@ -739,7 +753,8 @@ __global__ __launch_bounds__(256) void k_ops_gather(MeshDev M, int64_t nrows, co
 // left out of the exported CSR (kle_mat.mask_rule).
 template <int R, int C, int MODE>
 __global__ __launch_bounds__(256) void k_gather_ns(MeshDev M, int64_t nrows, const int *__restrict__ rowptr,
-                                                   const int *__restrict__ rowcnt, const int *__restrict__ bcol,
+                                                   const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
+                                                   int lay, const int *__restrict__ bcol,
                                                    const uint8_t *__restrict__ cls, const double *__restrict__ Eblk,
                                                    double *__restrict__ val)
 {
@@ -748,7 +763,7 @@ __global__ __launch_bounds__(256) void k_gather_ns(MeshDev M, int64_t nrows, con
     if (row >= nrows) return;
     const int64_t gi = M.node_begin + row, il = gi - M.ext_begin;
     const int b0 = rowptr[row], mp = rowptr[row + 1] - b0, m = rowcnt ? rowcnt[row] : mp;
-    double *v = val + (int64_t)b0 * R * C;
+    double *v = val + vptr[row];
     int64_t ci[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], M.dim == 3 ? gi / (M.L[0] * M.L[1]) : 0};
     int64_t elo[3], ehi[3];
     for (int d = 0; d < 3; ++d) {
@@ -802,7 +817,7 @@ __global__ __launch_bounds__(256) void k_gather_ns(MeshDev M, int64_t nrows, con
                     if (MODE == 6 && rc == DOF_TANG) out = 1.0 + (acc[a * C + b] + (-1.0));
                     if (MODE == 6 && rc == DOF_NORMAL) out = 1.0;
                 }
-                v[(a * C + b) * (int64_t)mp + k] = out;
+                v[vofs(lay, R * C, a * C + b, k, m, mp)] = out;
             }
     }
 }
@@ -812,7 +827,7 @@ static void launch_gather_ns(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const u
 {
     const int64_t threads = A->nrows * 64;
     hipLaunchKernelGGL((k_gather_ns<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
-                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, cls, E, A->d_val);
+                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, cls, E, A->d_val);
 }
 
 template <int R, int C, int MODE>
@@ -820,7 +835,7 @@ static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint
 {
     const int64_t threads = A->nrows * 64;
     hipLaunchKernelGGL((k_gather<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
-                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, dir, E, A->d_val);
+                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, E, A->d_val);
 }
 
 }  // namespace kle
@@ -899,7 +914,8 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
     KLE_HIP(hipMemcpyAsync(dX, corners.data(), sizeof(double) * corners.size(), hipMemcpyHostToDevice, ctx->stream));
     KLE_HIP(hipMemcpyAsync(dcnt, cnt.data(), sizeof(int) * nrows, hipMemcpyHostToDevice, ctx->stream));
     MeshDev M = mesh_dev(m);
-    OpsOut o{mc->d_val, ms->d_val, md->d_val, mc->d_rowptr, ms->d_rowptr, md->d_rowptr};
+    OpsOut o{mc->d_val,   ms->d_val,   md->d_val,   mc->d_rowptr, ms->d_rowptr,
+             md->d_rowptr, mc->d_vptr, ms->d_vptr, md->d_vptr, mc->vlayout};
     const unsigned gq = (unsigned)((nq + 255) / 256), gr = (unsigned)((nrows + 255) / 256),
                    gw = (unsigned)((nrows * 64 + 255) / 256);
     if (dim == 3) {

@@ -162,6 +162,12 @@ struct kle_mat {
     int64_t node_begin = 0, ext_begin = 0, ext_nodes = 0;
     int *d_rowptr = nullptr;   // [nrows+1] block offsets (rows padded to `pad` blocks)
     int *d_rowcnt = nullptr;   // [nrows] real block count per row (null when pad == 1)
+    // value layout: 0 = per-row SoA streams padded to `pad` blocks
+    // (v[t * mp + k]); 1 = 16-block chunks + packed tail, rows 128-B aligned
+    // (see vofs); d_vptr[i] = first double of row i in d_val
+    int vlayout = 0;
+    int64_t *d_vptr = nullptr;
+    int64_t nvals = 0;
     // structured columns: every row's columns are the ext-lattice box
     // base + [0,nx) + Lx [0,ny) + Lx Ly [0,nz) -> the SpMV computes them
     // instead of streaming bcol (d_rowbox[2*i] = base, [2*i+1] = nx | ny<<8 | nz<<16)
@@ -214,6 +220,18 @@ bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
 extern int g_nb_pad;
+extern int g_nb_layout;  // value layout of new node-block matrices (kle_mat.vlayout)
+// Offset of entry t (0 <= t < RC) of block k inside a row of m blocks
+// (mp = padded length for layout 0).  Layout 1: full 16-block chunks hold the
+// RC streams back to back (t-th 128-B line of chunk c), the m % 16 tail
+// blocks follow as RC packed streams of length m % 16.
+__host__ __device__ inline int64_t vofs(int lay, int RC, int t, int k, int m, int mp)
+{
+    if (lay == 0) return (int64_t)t * mp + k;
+    const int q16 = m & ~15;
+    if (k < q16) return ((int64_t)(k >> 4) * RC + t) * 16 + (k & 15);
+    return (int64_t)q16 * RC + (int64_t)t * (m - q16) + (k - q16);
+}
 // Host worker count for setup loops: OMP_NUM_THREADS if set, else the
 // hardware concurrency, capped at 16 (the GPU box's CPU share per GPU).
 int host_threads();

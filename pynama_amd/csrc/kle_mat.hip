@@ -27,6 +27,7 @@
 namespace kle {
 
 int g_nb_pad = 16;  // 128-B aligned row streams (profiles/r01/spmv_sweep_pad.jsonl)
+int g_nb_layout = 1;  // chunked rows (profiles/r01/layout_ab.jsonl)
 
 __device__ __forceinline__ double wsum(double v)
 {
@@ -68,6 +69,7 @@ template <int R, int C, bool DOT, int LPR, int UNR, bool NT>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__restrict__ rowptr,
                                                         const int *__restrict__ rowcnt,
                                                         const int *__restrict__ rowbox, int lx, int lxy,
+                                                        const int64_t *__restrict__ vptr, int lay,
                                                         const int *__restrict__ bcol,
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x,
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
                 bnxy = bnx * ((d >> 8) & 255);
             }
         }
-        const double *v = val + (int64_t)b0 * (R * C);
+        const double *v = val + (valid ? vptr[i] : 0);
         const int *cj = bcol + b0;
         double acc[R];
 #pragma unroll
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
                     j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
                 }
 #pragma unroll
-                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + (int64_t)t * mp + ku) : 0.0;
+                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + vofs(lay, R * C, t, ku, m, mp)) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
@@ -169,6 +171,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
 template <int R, int C, int UNR, bool NT>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_seq(RowMap rm, int seq, const int *__restrict__ rowptr,
                                                             const int *__restrict__ rowcnt,
+                                                            const int64_t *__restrict__ vptr, int lay,
                                                             const int *__restrict__ bcol,
                                                             const double *__restrict__ val,
                                                             const double *__restrict__ x, double *__restrict__ y,
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_seq(RowMap rm, int seq, 
             nmp = rowptr[ni + 1] - nb0;
             nm = rowcnt ? rowcnt[ni] : nmp;
         }
-        const double *v = val + (int64_t)b0 * (R * C);
+        const double *v = val + vptr[i];
         const int *cj = bcol + b0;
         double acc[R];
 #pragma unroll
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_seq(RowMap rm, int seq, 
                 on[u] = ku < m;
                 j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
 #pragma unroll
-                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + (int64_t)t * mp + ku) : 0.0;
+                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + vofs(lay, R * C, t, ku, m, mp)) : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
@@ -380,14 +383,14 @@ __global__ void k_diagpos(int64_t nrows, int64_t row_off, const int *__restrict_
 
 template <int R, int C>
 __global__ void k_nb_scale(int64_t nrows, const int *__restrict__ rowptr, const int *__restrict__ rowcnt,
-                           const int *__restrict__ bcol, double *__restrict__ val, const double *__restrict__ L,
-                           const double *__restrict__ Rx)
+                           const int64_t *__restrict__ vptr, int lay, const int *__restrict__ bcol,
+                           double *__restrict__ val, const double *__restrict__ L, const double *__restrict__ Rx)
 {
     const int lane = threadIdx.x & 63;
     const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (i >= nrows) return;
     const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
-    double *v = val + (int64_t)b0 * R * C;
+    double *v = val + vptr[i];
     for (int k = lane; k < m; k += 64) {
         const int64_t j = bcol[b0 + k];
         for (int a = 0; a < R; ++a)
@@ -395,20 +398,21 @@ __global__ void k_nb_scale(int64_t nrows, const int *__restrict__ rowptr, const 
                 double s = 1.0;
                 if (L) s *= L[i * R + a];
                 if (Rx) s *= Rx[j * C + b];
-                v[(int64_t)(a * C + b) * mp + k] *= s;
+                v[vofs(lay, R * C, a * C + b, k, m, mp)] *= s;
             }
     }
 }
 
 __global__ void k_nb_diag(int64_t nrows, int R, int C, const int *__restrict__ rowptr,
+                          const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr, int lay,
                           const int *__restrict__ pos, const double *__restrict__ val, double *__restrict__ d)
 {
     int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (t >= nrows * R) return;
     int64_t i = t / R;
     int a = (int)(t % R);
-    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0;
-    d[t] = pos[i] < 0 ? 0.0 : val[(int64_t)b0 * R * C + (int64_t)(a * C + a) * mp + pos[i]];
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
+    d[t] = pos[i] < 0 ? 0.0 : val[vptr[i] + vofs(lay, R * C, a * C + a, pos[i], m, mp)];
 }
 
 __global__ void k_aij_scale(int64_t nrows, const int64_t *__restrict__ ptr, const int *__restrict__ col,
@@ -493,7 +497,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
             if (A->spmv_xcd) grid = (grid + 7) / 8 * 8;  // whole XCD chunks
         }
         if (A->spmv_buf && A->R == 3 && A->C == 3 && A->spmv_lpr == 64 && !A->spmv_persistent && !A->spmv_order &&
-            !A->spmv_xcd) {
+            !A->spmv_xcd && A->vlayout == 0) {
             const int64_t xbytes = (int64_t)(x->ghost_lo + x->n_local + x->ghost_hi) * 8;
             const int g2 = (int)((A->nrows + SPMV_WAVES - 1) / SPMV_WAVES);
             if (g2 > PART_STRIDE - 256) return fail(KLE_ERR_SUP, "buffer SpMV variant: matrix too large");
@@ -558,16 +562,16 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 const int gs = (int)((nr + (int64_t)SPMV_WAVES * A->spmv_seq - 1) / ((int64_t)SPMV_WAVES * A->spmv_seq));
                 if (A->spmv_unroll == 1 && A->spmv_nt)
                     hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 1, true>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
                 else if (A->spmv_unroll == 1)
                     hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 1, false>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
                 else if (A->spmv_nt)
                     hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 2, true>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
                 else
                     hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 2, false>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, y->d, istate);
+                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
                 KLE_HIP(hipGetLastError());
                 continue;
             }
@@ -576,12 +580,14 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         if (dot)                                                                                        \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
                                c->stream, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,           \
-                               (int)A->box_lxy, A->d_bcol, A->d_val, x->base, y->d, pd, partials,       \
+                               (int)A->box_lxy, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base,    \
+                               y->d, pd, partials,                                                      \
                                istate, order, xcd);                                                     \
         else                                                                                            \
             hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0, \
                                c->stream, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,           \
-                               (int)A->box_lxy, A->d_bcol, A->d_val, x->base, y->d, pd, partials,       \
+                               (int)A->box_lxy, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base,    \
+                               y->d, pd, partials,                                                      \
                                istate, order, xcd);                                                     \
     } while (0)
 #define NB_VARIANTS(RR, CC)                                                                             \
@@ -663,14 +669,22 @@ static bool nb_entry_exists(const kle_mat *A, int64_t i, int a, int64_t jl, int 
 
 struct NBHost {
     std::vector<int> rp, bc, cnt;
+    std::vector<int64_t> vp;
     std::vector<double> v;
+    // entry t of block k in row i
+    double at(const kle_mat *A, int64_t i, int t, int k) const
+    {
+        return v[vp[i] + vofs(A->vlayout, A->R * A->C, t, k, cnt[i], rp[i + 1] - rp[i])];
+    }
 };
 
 static int nb_download(const kle_mat *A, NBHost &h)
 {
     h.rp.resize(A->nrows + 1);
     h.bc.resize(std::max<int64_t>(A->nblocks, 1));
-    h.v.resize(std::max<int64_t>(A->nblocks * A->R * A->C, 1));
+    h.v.resize(std::max<int64_t>(A->nvals, 1));
+    h.vp.resize(A->nrows + 1);
+    KLE_HIP(hipMemcpy(h.vp.data(), A->d_vptr, sizeof(int64_t) * (A->nrows + 1), hipMemcpyDeviceToHost));
     KLE_HIP(hipMemcpy(h.rp.data(), A->d_rowptr, sizeof(int) * (A->nrows + 1), hipMemcpyDeviceToHost));
     KLE_HIP(hipMemcpy(h.bc.data(), A->d_bcol, sizeof(int) * h.bc.size(), hipMemcpyDeviceToHost));
     KLE_HIP(hipMemcpy(h.v.data(), A->d_val, sizeof(double) * h.v.size(), hipMemcpyDeviceToHost));
@@ -834,6 +848,7 @@ int kle_mat_destroy(kle_mat *A)
     hipFree(A->d_order);
     hipFree(A->d_rowcnt);
     hipFree(A->d_rowbox);
+    hipFree(A->d_vptr);
     hipFree(A->d_rowptr);
     hipFree(A->d_bcol);
     hipFree(A->d_val);
@@ -911,7 +926,8 @@ int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *Rv)
 #define SC_CASE(RR, CC)                                                                                    \
     if (A->R == RR && A->C == CC)                                                                          \
         hipLaunchKernelGGL((k_nb_scale<RR, CC>), dim3((th + 255) / 256), dim3(256), 0, c->stream, A->nrows, \
-                           A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, L ? L->d : nullptr, rx);         \
+                           A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val,           \
+                           L ? L->d : nullptr, rx);                                                        \
     else
         SC_CASE(3, 3) SC_CASE(2, 2) SC_CASE(2, 1) SC_CASE(1, 2) SC_CASE(3, 1) SC_CASE(1, 3) SC_CASE(6, 3)
         SC_CASE(3, 6) SC_CASE(1, 1) return fail(KLE_ERR_SUP, "no scale kernel for %dx%d", A->R, A->C);
@@ -940,7 +956,7 @@ int kle_mat_get_diagonal(const kle_mat *A, kle_vec *d)
         hipLaunchKernelGGL(k_diagpos, dim3((A->nrows + 255) / 256), dim3(256), 0, c->stream, A->nrows,
                            A->node_begin - A->ext_begin, A->d_rowptr, A->d_rowcnt, A->d_bcol, pos);
         hipLaunchKernelGGL(k_nb_diag, dim3((A->nrows * A->R + 255) / 256), dim3(256), 0, c->stream, A->nrows, A->R,
-                           A->C, A->d_rowptr, pos, A->d_val, d->d);
+                           A->C, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, pos, A->d_val, d->d);
         KLE_HIP(hipGetLastError());
         KLE_HIP(hipStreamSynchronize(c->stream));
         hipFree(pos);
@@ -1007,22 +1023,24 @@ int kle_mat_get_row(const kle_mat *A, int64_t row, int64_t *ncols, int64_t *cols
         else cnt = rp[1] - rp[0];
         const int mp = rp[1] - rp[0];
         std::vector<int> bc(std::max(cnt, 1));
-        std::vector<double> vals_a((size_t)C * std::max(mp, 1));
+        int64_t vp[2];
+        KLE_HIP(hipMemcpy(vp, A->d_vptr + i, sizeof(int64_t) * 2, hipMemcpyDeviceToHost));
+        std::vector<double> rowv(std::max<int64_t>(vp[1] - vp[0], 1));
         if (cnt) KLE_HIP(hipMemcpy(bc.data(), A->d_bcol + rp[0], sizeof(int) * cnt, hipMemcpyDeviceToHost));
-        if (mp)
-            KLE_HIP(hipMemcpy(vals_a.data(), A->d_val + (int64_t)rp[0] * R * C + (int64_t)a * C * mp,
-                              sizeof(double) * C * mp, hipMemcpyDeviceToHost));
+        if (vp[1] > vp[0])
+            KLE_HIP(hipMemcpy(rowv.data(), A->d_val + vp[0], sizeof(double) * (vp[1] - vp[0]), hipMemcpyDeviceToHost));
+        auto val_at = [&](int t, int kk) { return rowv[vofs(A->vlayout, R * C, t, kk, cnt, mp)]; };
         if (A->diag_only_row[i]) {
             if (a < C) {
                 c.push_back((A->node_begin + i) * C + a);
-                v.push_back(vals_a[(size_t)a * mp]);
+                v.push_back(val_at(a * C + a, 0));
             }
         } else {
             for (int k = 0; k < cnt; ++k)
                 for (int b = 0; b < C; ++b) {
                     if (A->mask_rule != MASK_NONE && !nb_entry_exists(A, i, a, bc[k], b)) continue;
                     c.push_back((A->ext_begin + bc[k]) * C + b);
-                    v.push_back(vals_a[(size_t)b * mp + k]);
+                    v.push_back(val_at(a * C + b, k));
                 }
         }
     }
@@ -1047,21 +1065,20 @@ int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double 
     int64_t z = 0;
     indptr[0] = 0;
     for (int64_t i = 0; i < A->nrows; ++i) {
-        const int b0 = h.rp[i], mp = h.rp[i + 1] - b0, m = h.cnt[i];
-        const double *v = h.v.data() + (int64_t)b0 * R * C;
+        const int b0 = h.rp[i], m = h.cnt[i];
         for (int a = 0; a < R; ++a) {
             if (A->diag_only_row[i]) {
                 // Dirichlet row: PETSc stores the diagonal only (mat_fs.py:44-45,115-120)
                 if (a < C) {
                     indices[z] = (A->node_begin + i) * C + a;
-                    data[z++] = v[(a * C + a) * (int64_t)mp + 0];
+                    data[z++] = h.at(A, i, a * C + a, 0);
                 }
             } else {
                 for (int k = 0; k < m; ++k)
                     for (int b = 0; b < C; ++b) {
                         if (A->mask_rule != MASK_NONE && !nb_entry_exists(A, i, a, h.bc[b0 + k], b)) continue;
                         indices[z] = (A->ext_begin + h.bc[b0 + k]) * C + b;
-                        data[z++] = v[(int64_t)(a * C + b) * mp + k];
+                        data[z++] = h.at(A, i, a * C + b, k);
                     }
             }
             indptr[i * R + a + 1] = z;
@@ -1101,8 +1118,9 @@ int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X)
         NBHost hy, hx;
         KLE_TRY(nb_download(Y, hy));
         KLE_TRY(nb_download(X, hx));
-        if (hy.rp != hx.rp || hy.bc != hx.bc || hy.cnt != hx.cnt) return fail(KLE_ERR_SUP, "axpy needs the same pattern");
-        const int64_t n = Y->nblocks * Y->R * Y->C;
+        if (hy.rp != hx.rp || hy.bc != hx.bc || hy.cnt != hx.cnt || hy.vp != hx.vp || Y->vlayout != X->vlayout)
+            return fail(KLE_ERR_SUP, "axpy needs the same pattern");
+        const int64_t n = Y->nvals;
         hipLaunchKernelGGL(k_axpy_same, dim3(grid_for(n, 256, 2048)), dim3(256), 0, c->stream, n, a, X->d_val, Y->d_val);
         KLE_HIP(hipGetLastError());
         KLE_HIP(hipStreamSynchronize(c->stream));
@@ -1135,6 +1153,7 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     B->d_order = nullptr;
     B->d_rowcnt = nullptr;
     B->d_rowbox = nullptr;
+    B->d_vptr = nullptr;
     B->d_rowptr = nullptr;
     B->d_bcol = nullptr;
     B->d_val = nullptr;
@@ -1142,7 +1161,7 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     B->d_acol = nullptr;
     B->d_aval = nullptr;
     if (A->kind == 0) {
-        const size_t nv = std::max<int64_t>(A->nblocks * A->R * A->C, 1);
+        const size_t nv = std::max<int64_t>(A->nvals, 1);
         KLE_HIP(hipMalloc(&B->d_rowptr, sizeof(int) * (A->nrows + 1)));
         KLE_HIP(hipMalloc(&B->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1)));
         KLE_HIP(hipMalloc(&B->d_val, sizeof(double) * nv));
@@ -1151,6 +1170,8 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
             KLE_HIP(hipMalloc(&B->d_rowcnt, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
             KLE_HIP(hipMemcpy(B->d_rowcnt, A->d_rowcnt, sizeof(int) * A->nrows, hipMemcpyDeviceToDevice));
         }
+        KLE_HIP(hipMalloc(&B->d_vptr, sizeof(int64_t) * (A->nrows + 1)));
+        KLE_HIP(hipMemcpy(B->d_vptr, A->d_vptr, sizeof(int64_t) * (A->nrows + 1), hipMemcpyDeviceToDevice));
         if (A->d_rowbox) {
             KLE_HIP(hipMalloc(&B->d_rowbox, sizeof(int) * 2 * std::max<int64_t>(A->nrows, 1)));
             KLE_HIP(hipMemcpy(B->d_rowbox, A->d_rowbox, sizeof(int) * 2 * A->nrows, hipMemcpyDeviceToDevice));
@@ -1177,6 +1198,15 @@ int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt)
 }
 
 int kle_get_nb_pad(void) { return g_nb_pad; }
+
+int kle_set_nb_layout(int layout)
+{
+    KLE_ARG(layout == 0 || layout == 1, "layout must be 0 (padded streams) or 1 (16-block chunks)");
+    g_nb_layout = layout;
+    return 0;
+}
+
+int kle_get_nb_layout(void) { return g_nb_layout; }
 
 int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq)
 {

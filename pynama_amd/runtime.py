@@ -182,6 +182,8 @@ def get_ctx():
     if _CTX is None:
         if os.environ.get("KLE_NB_PAD"):
             set_row_padding(int(os.environ["KLE_NB_PAD"]))
+        if os.environ.get("KLE_NB_LAYOUT"):
+            set_value_layout(int(os.environ["KLE_NB_LAYOUT"]))
         _CTX = Context()
     return _CTX
 
@@ -190,6 +192,16 @@ def set_row_padding(quantum):
     """Row padding quantum (blocks) for node-block matrices created afterwards
     (KLE_NB_PAD in the environment sets the initial value)."""
     call("kle_set_nb_pad", int(quantum))
+
+
+def set_value_layout(layout):
+    """Node-block value layout for matrices created afterwards (0 padded
+    streams, 1 chunked + packed tail); KLE_NB_LAYOUT sets the initial value."""
+    call("kle_set_nb_layout", int(layout))
+
+
+def get_value_layout():
+    return int(load().kle_get_nb_layout())
 
 
 def get_row_padding():

@@ -367,3 +367,53 @@ def test_structured_columns_are_exact(pa):
         A.setSpmvStructured(True)
         np.testing.assert_array_equal(y1, y0)
         assert A.spmvBytes() > 0
+
+
+def test_chunked_value_layout_is_exact(pa):
+    """Layout 1 (16-block chunks + packed tail, no per-stream padding) stores
+    the same entries: CSR exports, getRow, diagonal, scaling and SpMV of the
+    free-slip matrices, the operators and the no-slip matrices are bitwise equal
+    to layout 0."""
+    from pynama_amd.runtime import get_value_layout, set_value_layout
+    old = get_value_layout()
+    g = _golden("tg3d_p4")
+    built = {}
+    try:
+        for lay in (0, 1):
+            set_value_layout(lay)
+            dom = _domain(pa, g)
+            mat = pa.MatFS()
+            mat.setDomain(dom)
+            mat.build()
+            cfg = {"domain": {"ngl": 4, "box-mesh": {"nelem": [3, 3], "lower": [0, 0], "upper": [1, 1]}},
+                   "boundary-conditions": {"no-slip": {"up": [1, 0], "down": [0, 0], "left": [0, 0],
+                                                       "right": [0, 0]}}}
+            dns = pa.Domain()
+            dns.configure(cfg)
+            dns.setUp()
+            mns = pa.MatNS()
+            mns.setDomain(dns)
+            mns.build()
+            op = mat.getOperators()
+            built[lay] = [mat.K, mat.Krhs, mat.Rw, op.Curl, op.SrT, op.DivSrT, mns.Kfs, mns.Krhsfs,
+                          mns.getKplusKfs(), mns.Rdfs]
+    finally:
+        set_value_layout(old)
+    rng = np.random.default_rng(9)
+    for A0, A1 in zip(built[0], built[1]):
+        for u, v in zip(A0.getValuesCSR(), A1.getValuesCSR()):
+            np.testing.assert_array_equal(u, v)
+        x = A0.createVecRight()
+        x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
+        np.testing.assert_array_equal((A0 * x).getArray(), (A1 * x).getArray())
+        r = A0.getOwnershipRange()[0] + 5
+        for u, v in zip(A0.getRow(r), A1.getRow(r)):
+            np.testing.assert_array_equal(u, v)
+    K0, K1 = built[0][0], built[1][0]
+    np.testing.assert_array_equal(K0.getDiagonal().getArray(), K1.getDiagonal().getArray())
+    s = K0.createVecLeft()
+    s.setArray(rng.uniform(0.5, 2, s.getLocalSize()))
+    K0.diagonalScale(L=s)
+    K1.diagonalScale(L=s)
+    for u, v in zip(K0.getValuesCSR(), K1.getValuesCSR()):
+        np.testing.assert_array_equal(u, v)
