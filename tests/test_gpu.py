@@ -309,10 +309,11 @@ def test_row_padding_and_nt_loads_are_exact(pa, pad):
     """Padded row streams (every stream 128-B aligned) and non-temporal loads
     change only the memory layout / cache policy: export, diagonal, scaling and
     SpMV must be bit-identical to the unpadded plain-load matrix."""
-    from pynama_amd.runtime import get_row_padding, set_row_padding
+    from pynama_amd.runtime import get_row_padding, get_value_layout, set_row_padding, set_value_layout
     g = _golden("tg3d_p4")
     mats = []
-    old = get_row_padding()
+    old, old_lay = get_row_padding(), get_value_layout()
+    set_value_layout(0)  # padding is a property of the stream layout
     try:
         for q in (1, pad):
             set_row_padding(q)
@@ -323,6 +324,7 @@ def test_row_padding_and_nt_loads_are_exact(pa, pad):
             mats.append(mat)
     finally:
         set_row_padding(old)
+        set_value_layout(old_lay)
     a, b = mats
     a.K.setSpmvNontemporal(False)
     for nm in ("K", "Krhs", "Rw"):
