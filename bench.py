@@ -237,6 +237,24 @@ def main():
     iters_per_s = args.steps / t_max
     achieved = tot_bytes / (spmv_avg_max * 1e-3) / 1e9 if spmv_avg_max > 0 else None
 
+    # plain SpMV leg: x = uniform[-1,1) from splitmix64 seeded
+    # 0x5EED, 10 warm-ups, 200 timed repetitions of y = K x
+    lo, hi = K.getOwnershipRange()
+    xs = K.createVecRight()
+    xs.setArray(splitmix_uniform(0x5EED, lo, hi))
+    ys = K.createVecLeft()
+    for _ in range(10):
+        K.mult(xs, ys)
+    ctx.set_profiling(True, only="spmv")
+    ctx.reset_stats()
+    for _ in range(200):
+        K.mult(xs, ys)
+    pc_, pms = ctx.kernel_stats("spmv")
+    ctx.set_profiling(False)
+    spmv_plain = {"reps": pc_, "avg_ms": pms / max(pc_, 1), "bytes": spmv_bytes_local,
+                  "gbps": spmv_bytes_local / (pms / max(pc_, 1) * 1e-3) / 1e9,
+                  "x": "uniform[-1,1) from splitmix64(0x5EED), global index order"}
+
     aij = None
     if args.aij and nranks == 1:
         A = K.convert("aij")
@@ -312,6 +330,7 @@ def main():
             "assembly_s": t_asm,
             "setup_s": t_setup,
             "solve": solve,
+            "spmv_plain": spmv_plain,
             "aij_spmv": aij,
             "operators": ops,
         }
@@ -319,6 +338,19 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def splitmix_uniform(seed, lo, hi):
+    """x[i] = uniform[-1, 1) from the splitmix64 stream of `seed` at global
+    index i (same on every rank and on the CPU)."""
+    import numpy as np
+    i = np.arange(lo, hi, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (2.0 / 9007199254740992.0) - 1.0
 
 
 def cpu_baseline(K, b, seconds):

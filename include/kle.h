@@ -256,6 +256,9 @@ int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq);
  * of streaming 4 B per block (default on; 0 forces the column stream). */
 int kle_mat_set_spmv_structured(kle_mat *A, int on);
 int kle_mat_is_structured(const kle_mat *A, int *on);
+/* 1 (default): the default SpMV variant runs the kernel specialised on layout
+ * and structured columns; 0: the generic kernel (same results, bitwise). */
+int kle_mat_set_spmv_fast(kle_mat *A, int on);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on; needs the unfused CG dot). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

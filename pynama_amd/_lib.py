@@ -123,6 +123,7 @@ _SIGS = {
     "kle_set_nb_pad": [C.c_int],
     "kle_mat_set_halo_overlap": [vp, C.c_int],
     "kle_mat_set_spmv_structured": [vp, C.c_int],
+    "kle_mat_set_spmv_fast": [vp, C.c_int],
     "kle_mat_is_structured": [vp, C.POINTER(C.c_int)],
     "kle_mat_set_spmv_rows_per_wave": [vp, C.c_int],
     "kle_get_nb_pad": [],

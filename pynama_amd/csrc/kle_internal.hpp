@@ -174,6 +174,7 @@ struct kle_mat {
     int *d_rowbox = nullptr;
     int64_t box_lx = 0, box_lxy = 0;
     int spmv_struct = 1;  // use d_rowbox when present
+    int spmv_fast = 1;    // specialised default kernel (k_nb_spmv_fast) when the variant allows
     int64_t nblocks_real = 0;
     int pad = 1;
     int *d_bcol = nullptr;     // [nblocks] local ext node index

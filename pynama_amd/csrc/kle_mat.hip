@@ -165,6 +165,90 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
 }
 
 
+
+// Default SpMV (unfused, one row per wavefront, one block per lane in flight,
+// nt streams), specialised on the value layout and on structured columns so
+// the generic variant's branches cost no registers (occupancy 8 at R = C = 3).
+// LAY 1: while the wave's 64 blocks lie inside the row's full 16-block chunks
+// the RC value loads of a lane share one base address (immediate offsets of
+// 128 B); the last, partial pass uses the packed-tail rule of vofs().
+template <int R, int C, int LAY, bool STRUCT>
+__global__ __launch_bounds__(SPMV_BLOCK, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(RowMap rm, const int *__restrict__ rowptr,
+                                                             const int *__restrict__ rowcnt,
+                                                             const int *__restrict__ rowbox, int lx, int lxy,
+                                                             const int64_t *__restrict__ vptr,
+                                                             const int *__restrict__ bcol,
+                                                             const double *__restrict__ val,
+                                                             const double *__restrict__ x, double *__restrict__ y,
+                                                             const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    constexpr int RC = R * C;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    if (r >= rm.na + rm.nb) return;
+    const int64_t i = r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
+    const double *v = val + vptr[i];
+    int bbase = 0, bnx = 1, bnxy = 1;
+    if constexpr (STRUCT) {
+        bbase = rowbox[2 * i];
+        const int d = rowbox[2 * i + 1];
+        bnx = d & 255;
+        bnxy = bnx * ((d >> 8) & 255);
+    }
+    const int q16 = LAY == 1 ? (m & ~15) : 0;
+    double acc[R];
+#pragma unroll
+    for (int a = 0; a < R; ++a) acc[a] = 0.0;
+    for (int kb = 0; kb < m; kb += 64) {
+        const int k = kb + lane;
+        const bool on = k < m;
+        int j = 0;
+        if (on) {
+            if constexpr (STRUCT) {
+                const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
+                j = bbase + kx + lx * ky + lxy * kz;
+            } else {
+                j = __builtin_nontemporal_load(bcol + b0 + k);
+            }
+        }
+        double vv[RC];
+        if (LAY == 1 && kb + 64 <= q16) {
+            // whole wave inside full chunks: stream t at +16 t doubles
+            const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
+#pragma unroll
+            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(p + t * 16);
+        } else if (on) {
+            const int64_t o0 = vofs(LAY, RC, 0, k, m, mp);
+            const int64_t st = LAY == 1 ? (k < q16 ? 16 : m - q16) : mp;
+#pragma unroll
+            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
+        } else {
+#pragma unroll
+            for (int t = 0; t < RC; ++t) vv[t] = 0.0;
+        }
+        double xv[C];
+#pragma unroll
+        for (int b = 0; b < C; ++b) xv[b] = on ? x[(int64_t)j * C + b] : 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xv[b];
+    }
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+    if (lane < R) {
+        double mine = acc[0];
+#pragma unroll
+        for (int a = 1; a < R; ++a)
+            if (lane == a) mine = acc[a];
+        y[i * R + lane] = mine;
+    }
+}
+
 // Variant: each wave takes `seq` consecutive rows and prefetches the next
 // row's (offset, length) while it streams the current one, so the row-start
 // latency overlaps the previous row's loads.  No fused dot / order / XCD map.
@@ -533,6 +617,10 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         }
         const bool seq_ok = A->spmv_seq > 1 && A->R == 3 && A->C == 3 && A->spmv_lpr == 64 && !dot &&
                             !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
+        const bool fast_shape = (A->R == 3 && A->C == 3) || (A->R == 6 && A->C == 3) || (A->R == 3 && A->C == 6) ||
+                                (A->R == 2 && A->C == 2);
+        const bool fast_ok = A->spmv_fast && fast_shape && !dot && A->spmv_lpr == 64 && A->spmv_unroll == 1 &&
+                             A->spmv_nt && A->spmv_seq <= 1 && !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
         if (A->spmv_order && !A->d_order) KLE_TRY(nb_build_order(A));
         const int *order = A->spmv_order ? A->d_order : nullptr;
         const int xcd = A->spmv_xcd && !A->spmv_persistent;
@@ -556,6 +644,27 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
                 rm = RowMap{0, A->int_lo, A->int_hi, A->nrows - A->int_hi};
                 grid = grid_for(rm.na + rm.nb, rpb, PART_STRIDE - 256);
+            }
+            if (fast_ok) {
+                const int gf = grid_for(rm.na + rm.nb, SPMV_WAVES, 1 << 30);
+                const int st_ = rbox ? 1 : 0;
+#define FAST_LAUNCH(RR, CC, LY, SS)                                                                     \
+    hipLaunchKernelGGL((k_nb_spmv_fast<RR, CC, LY, SS>), dim3(gf), dim3(SPMV_BLOCK), 0, c->stream, rm,  \
+                       A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
+                       A->d_bcol, A->d_val, x->base, y->d, istate)
+#define FAST_SHAPE(RR, CC)                                                                              \
+    if (A->vlayout == 1 && st_) FAST_LAUNCH(RR, CC, 1, true);                                           \
+    else if (A->vlayout == 1) FAST_LAUNCH(RR, CC, 1, false);                                            \
+    else if (st_) FAST_LAUNCH(RR, CC, 0, true);                                                         \
+    else FAST_LAUNCH(RR, CC, 0, false);
+                if (A->R == 3 && A->C == 3) { FAST_SHAPE(3, 3) }
+                else if (A->R == 6 && A->C == 3) { FAST_SHAPE(6, 3) }
+                else if (A->R == 3 && A->C == 6) { FAST_SHAPE(3, 6) }
+                else if (A->R == 2 && A->C == 2) { FAST_SHAPE(2, 2) }
+#undef FAST_SHAPE
+#undef FAST_LAUNCH
+                KLE_HIP(hipGetLastError());
+                continue;
             }
             if (seq_ok) {
                 const int64_t nr = rm.na + rm.nb;
@@ -1212,6 +1321,13 @@ int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq)
 {
     KLE_ARG(A && seq >= 1 && seq <= 64, "rows per wave must be in [1,64]");
     A->spmv_seq = seq;
+    return 0;
+}
+
+int kle_mat_set_spmv_fast(kle_mat *A, int on)
+{
+    KLE_ARG(A, "null matrix");
+    A->spmv_fast = on != 0;
     return 0;
 }
 

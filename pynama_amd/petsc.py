@@ -386,6 +386,9 @@ class Mat:
     def setSpmvRowsPerWave(self, seq):
         call("kle_mat_set_spmv_rows_per_wave", self._h, int(seq))
 
+    def setSpmvFast(self, on=True):
+        call("kle_mat_set_spmv_fast", self._h, int(bool(on)))
+
     def setSpmvStructured(self, on=True):
         call("kle_mat_set_spmv_structured", self._h, int(bool(on)))
 

@@ -419,3 +419,34 @@ def test_chunked_value_layout_is_exact(pa):
     K1.diagonalScale(L=s)
     for u, v in zip(K0.getValuesCSR(), K1.getValuesCSR()):
         np.testing.assert_array_equal(u, v)
+
+
+def test_fast_spmv_kernel_matches_generic(pa):
+    """The specialised default SpMV kernel == the generic one, bitwise, for
+    every (layout, structured) combination and the operator shapes."""
+    from pynama_amd.runtime import get_value_layout, set_value_layout
+    g = _golden("tg3d_p4")
+    old = get_value_layout()
+    try:
+        for lay in (0, 1):
+            set_value_layout(lay)
+            dom = _domain(pa, g)
+            mat = pa.MatFS()
+            mat.setDomain(dom)
+            mat.build()
+            op = mat.getOperators()
+            rng = np.random.default_rng(lay)
+            for A in (mat.K, mat.Rw, mat.Krhs, op.SrT, op.DivSrT, op.Curl):
+                x = A.createVecRight()
+                x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
+                for st in (True, False):
+                    A.setSpmvStructured(st)
+                    A.setSpmvFast(True)
+                    y1 = (A * x).getArray()
+                    A.setSpmvFast(False)
+                    y0 = (A * x).getArray()
+                    np.testing.assert_array_equal(y1, y0)
+                A.setSpmvFast(True)
+                A.setSpmvStructured(True)
+    finally:
+        set_value_layout(old)
