@@ -172,7 +172,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
 // LAY 1: while the wave's 64 blocks lie inside the row's full 16-block chunks
 // the RC value loads of a lane share one base address (immediate offsets of
 // 128 B); the last, partial pass uses the packed-tail rule of vofs().
-template <int R, int C, int LAY, bool STRUCT>
+template <int R, int C, int LAY, bool STRUCT, int UNR>
 __global__ __launch_bounds__(SPMV_BLOCK, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(RowMap rm, const int *__restrict__ rowptr,
                                                              const int *__restrict__ rowcnt,
                                                              const int *__restrict__ rowbox, int lx, int lxy,
@@ -201,40 +201,48 @@ __global__ __launch_bounds__(SPMV_BLOCK, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fa
     double acc[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) acc[a] = 0.0;
-    for (int kb = 0; kb < m; kb += 64) {
-        const int k = kb + lane;
-        const bool on = k < m;
-        int j = 0;
-        if (on) {
-            if constexpr (STRUCT) {
-                const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
-                j = bbase + kx + lx * ky + lxy * kz;
+    for (int kb = 0; kb < m; kb += 64 * UNR) {
+        int j[UNR];
+        bool on[UNR];
+        double vv[UNR][RC];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const int kbu = kb + 64 * u, k = kbu + lane;
+            on[u] = k < m;
+            j[u] = 0;
+            if (on[u]) {
+                if constexpr (STRUCT) {
+                    const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
+                    j[u] = bbase + kx + lx * ky + lxy * kz;
+                } else {
+                    j[u] = __builtin_nontemporal_load(bcol + b0 + k);
+                }
+            }
+            if (LAY == 1 && kbu + 64 <= q16) {
+                // whole wave inside full chunks: stream t at +16 t doubles
+                const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
+#pragma unroll
+                for (int t = 0; t < RC; ++t) vv[u][t] = __builtin_nontemporal_load(p + t * 16);
+            } else if (on[u]) {
+                const int64_t o0 = vofs(LAY, RC, 0, k, m, mp);
+                const int64_t st = LAY == 1 ? (k < q16 ? 16 : m - q16) : mp;
+#pragma unroll
+                for (int t = 0; t < RC; ++t) vv[u][t] = __builtin_nontemporal_load(v + o0 + t * st);
             } else {
-                j = __builtin_nontemporal_load(bcol + b0 + k);
+#pragma unroll
+                for (int t = 0; t < RC; ++t) vv[u][t] = 0.0;
             }
         }
-        double vv[RC];
-        if (LAY == 1 && kb + 64 <= q16) {
-            // whole wave inside full chunks: stream t at +16 t doubles
-            const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
 #pragma unroll
-            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(p + t * 16);
-        } else if (on) {
-            const int64_t o0 = vofs(LAY, RC, 0, k, m, mp);
-            const int64_t st = LAY == 1 ? (k < q16 ? 16 : m - q16) : mp;
+        for (int u = 0; u < UNR; ++u) {
+            double xv[C];
 #pragma unroll
-            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
-        } else {
+            for (int b = 0; b < C; ++b) xv[b] = on[u] ? x[(int64_t)j[u] * C + b] : 0.0;
 #pragma unroll
-            for (int t = 0; t < RC; ++t) vv[t] = 0.0;
+            for (int a = 0; a < R; ++a)
+#pragma unroll
+                for (int b = 0; b < C; ++b) acc[a] += vv[u][a * C + b] * xv[b];
         }
-        double xv[C];
-#pragma unroll
-        for (int b = 0; b < C; ++b) xv[b] = on ? x[(int64_t)j * C + b] : 0.0;
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-            for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xv[b];
     }
 #pragma unroll
     for (int a = 0; a < R; ++a)
@@ -619,6 +627,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                             !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
         const bool fast_shape = (A->R == 3 && A->C == 3) || (A->R == 6 && A->C == 3) || (A->R == 3 && A->C == 6) ||
                                 (A->R == 2 && A->C == 2);
+        // (two blocks per lane in flight spill at 8 waves/SIMD: 112 B scratch -> unroll 1 only)
         const bool fast_ok = A->spmv_fast && fast_shape && !dot && A->spmv_lpr == 64 && A->spmv_unroll == 1 &&
                              A->spmv_nt && A->spmv_seq <= 1 && !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
         if (A->spmv_order && !A->d_order) KLE_TRY(nb_build_order(A));
@@ -649,7 +658,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 const int gf = grid_for(rm.na + rm.nb, SPMV_WAVES, 1 << 30);
                 const int st_ = rbox ? 1 : 0;
 #define FAST_LAUNCH(RR, CC, LY, SS)                                                                     \
-    hipLaunchKernelGGL((k_nb_spmv_fast<RR, CC, LY, SS>), dim3(gf), dim3(SPMV_BLOCK), 0, c->stream, rm,  \
+    hipLaunchKernelGGL((k_nb_spmv_fast<RR, CC, LY, SS, 1>), dim3(gf), dim3(SPMV_BLOCK), 0, c->stream, rm, \
                        A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
                        A->d_bcol, A->d_val, x->base, y->d, istate)
 #define FAST_SHAPE(RR, CC)                                                                              \
