@@ -319,8 +319,10 @@ def main():
                        "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-                         "kernel": "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
-                                                                   "true" if args.loads == "nt" else "false"),
+                         "kernel": (("k_nb_spmv_fast<3,3,%d,%s,1>" % (args.layout, "true" if K.isStructured() else "false"))
+                                    if not args.fused_dot and args.loads == "nt" else
+                                    "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
+                                                                  "true" if args.loads == "nt" else "false")),
                          "bytes_per_launch": tot_bytes,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt},
             "cpu_baseline": cpu,
