@@ -1,3 +1,5 @@
+# Round profiling pass (bench + rocprofv3 kernel stats + PMC FETCH/WRITE/TCC):
+#   gpurun --timeout 2400 -- 'bash tools/gpu_profile.sh'
 source tools/gpu_steps.sh
 step bench_default 600 python bench.py --aij --ops
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
