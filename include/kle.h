@@ -110,6 +110,24 @@ int kle_ctx_reset_kernel_stats(kle_ctx *ctx);
 int kle_mesh_create_box(int dim, const int64_t nelem[3], const double lower[3],
                         const double upper[3], int ngl, int rank, int nranks, kle_mesh **out);
 int kle_mesh_destroy(kle_mesh *m);
+/* Unstructured quad (2-D) / hex (3-D) mesh (replaces GmshDom.create +
+ * DMPlexDistribute + setFemIndexing, dmplex.py:18-49,390-395; entity
+ * orientation rules indices.py:70-96).  vxyz: [nverts][3]; cells:
+ * [ncells][2^dim] vertex indices in Gmsh order (quad counter-clockwise, hex
+ * bottom 0-3 then 4-7 above them), cell ids = row order (the ADD order);
+ * facets: [nfacets][2^(dim-1)] boundary faces with their Face Sets value
+ * (tag t >= 1 -> face bit t-1, the reference's name order: dmplex.py:27-30,
+ * 175-178).  Ranks own slabs of cells along the longest axis; node ids are
+ * global, each rank's owned range ordered [lower interface | interior | upper
+ * interface] (see kle_umesh.cpp).  Fails with KLE_ERR_ARG for inverted cells
+ * or slabs too thin for the two-neighbour halo. */
+int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double *vxyz, int64_t ncells,
+                                 const int64_t *cells, int64_t nfacets, const int64_t *facets,
+                                 const int *facet_tags, int rank, int nranks, kle_mesh **out);
+/* Gmsh MSH 4.1 ASCII file (GmshDom.create -> DMPlexCreateFromFile). */
+int kle_mesh_create_gmsh(const char *path, int ngl, int rank, int nranks, kle_mesh **out);
+/* Global cell ids of the local (owned + ghost) elements, ascending. */
+int kle_mesh_get_elements(const kle_mesh *m, int64_t *ids);
 
 typedef struct {
     int dim, ngl, rank, nranks;
@@ -123,6 +141,8 @@ typedef struct {
     int64_t ext_end;
     int64_t elem_begin;     /* local (owned + ghost) element range           */
     int64_t elem_end;
+    int kind;               /* 0 structured box, 1 unstructured              */
+    int axis;               /* partition axis                                */
 } kle_mesh_info;
 
 int kle_mesh_get_info(const kle_mesh *m, kle_mesh_info *info);

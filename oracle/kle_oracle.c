@@ -598,6 +598,8 @@ typedef struct {
     double lower[3], upper[3], h[3];
     int *loc2lat;       /* [nn][dim] lattice offset of local node l */
     double xi[ORC_MAXN];/* GLL nodes mapped to [0,1], ascending        */
+    int64_t *uconn;     /* unstructured: explicit [E][nn] node ids      */
+    double *ucorners;   /* unstructured: [E][2^dim][dim] closure order  */
 } orc_mesh;
 
 static const int CORN2[4][2] = {{0, 0}, {1, 0}, {1, 1}, {0, 1}};
@@ -648,7 +650,28 @@ void orc_mesh_destroy(orc_mesh *m)
 {
     if (!m) return;
     free(m->loc2lat);
+    free(m->uconn);
+    free(m->ucorners);
     free(m);
+}
+
+/* Unstructured mesh from explicit arrays (GmshDom + the section numbering are
+ * restated in oracle.py: nodes identified by coordinates). */
+orc_mesh *orc_mesh_from_arrays(int dim, int ngl, int64_t N, int64_t E, const int64_t *conn,
+                               const double *corners)
+{
+    orc_mesh *m = calloc(1, sizeof(orc_mesh));
+    m->dim = dim;
+    m->ngl = ngl;
+    m->p = ngl - 1;
+    m->N = N;
+    m->E = E;
+    const int nn = dim == 2 ? ngl * ngl : ngl * ngl * ngl, nc = 1 << dim;
+    m->uconn = malloc(sizeof(int64_t) * E * nn);
+    m->ucorners = malloc(sizeof(double) * E * nc * dim);
+    memcpy(m->uconn, conn, sizeof(int64_t) * E * nn);
+    memcpy(m->ucorners, corners, sizeof(double) * E * nc * dim);
+    return m;
 }
 
 int64_t orc_mesh_nnodes(const orc_mesh *m) { return m->N; }
@@ -666,6 +689,10 @@ static void elem_index(const orc_mesh *m, int64_t e, int64_t *ei)
 int orc_mesh_conn(const orc_mesh *m, int64_t *conn)
 {
     int nn = m->dim == 2 ? m->ngl * m->ngl : m->ngl * m->ngl * m->ngl;
+    if (m->uconn) {
+        memcpy(conn, m->uconn, sizeof(int64_t) * m->E * nn);
+        return 0;
+    }
     for (int64_t e = 0; e < m->E; ++e) {
         int64_t ei[3];
         elem_index(m, e, ei);
@@ -683,6 +710,10 @@ int orc_mesh_conn(const orc_mesh *m, int64_t *conn)
 int orc_mesh_corners(const orc_mesh *m, double *X)
 {
     int nc = 1 << m->dim;
+    if (m->ucorners) {
+        memcpy(X, m->ucorners, sizeof(double) * m->E * nc * m->dim);
+        return 0;
+    }
     for (int64_t e = 0; e < m->E; ++e) {
         int64_t ei[3];
         elem_index(m, e, ei);

@@ -42,6 +42,8 @@ def lib():
         L.orc_mesh_box.restype = C.c_void_p
         L.orc_mesh_box.argtypes = [C.c_int, i64p, f64p, f64p, C.c_int]
         L.orc_mesh_destroy.argtypes = [C.c_void_p]
+        L.orc_mesh_from_arrays.restype = C.c_void_p
+        L.orc_mesh_from_arrays.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, i64p, f64p]
         L.orc_mesh_nnodes.restype = C.c_int64
         L.orc_mesh_nnodes.argtypes = [C.c_void_p]
         L.orc_mesh_nelems.restype = C.c_int64
@@ -226,6 +228,185 @@ class BoxMesh:
         dw, ds = (1, 3) if self.dim == 2 else (3, 6)
         return (CSR(Cu.value, self.N * self.dim), CSR(S.value, self.N * self.dim),
                 CSR(D.value, self.N * ds), W)
+
+
+# ------------------------------------------------------------ unstructured
+def read_gmsh(path):
+    """Gmsh MSH 4.1 ASCII -> (dim, vertices [nv,3], cells [nc, 2^dim] (Gmsh
+    order, file order), facets [nf, 2^(dim-1)], facet physical tags [nf]).
+    Restates what DMPlexCreateGmsh keeps of the file for GmshDom
+    (dmplex.py:390-395): quads/hexes as cells, boundary lines/quads with their
+    entity's first physical tag as the "Face Sets" value."""
+    with open(path) as f:
+        tok = f.read().split()
+    i = 0
+    phys = {}
+    verts, index = [], {}
+    blocks = []
+
+    def take(n=1):
+        nonlocal i
+        out = tok[i:i + n]
+        i += n
+        return out if n > 1 else out[0]
+
+    while i < len(tok):
+        t = take()
+        if t == "$Entities":
+            cnt = [int(x) for x in take(4)]
+            for d in range(4):
+                for _ in range(cnt[d]):
+                    tag = int(take())
+                    take(3 if d == 0 else 6)
+                    nph = int(take())
+                    ph = [int(take()) for _ in range(nph)]
+                    if ph:
+                        phys[(d, tag)] = abs(ph[0])
+                    if d > 0:
+                        nb = int(take())
+                        take(nb) if nb > 1 else (take() if nb == 1 else None)
+        elif t == "$Nodes":
+            nblk = int(take())
+            take(3)
+            for _ in range(nblk):
+                edim, _etag, para, n = (int(x) for x in take(4))
+                tags = [int(take()) for _ in range(n)]
+                for tg in tags:
+                    xyz = [float(take()) for _ in range(3)]
+                    if para:
+                        take(edim) if edim > 1 else take()
+                    index[tg] = len(verts)
+                    verts.append(xyz)
+        elif t == "$Elements":
+            nblk = int(take())
+            take(3)
+            for _ in range(nblk):
+                edim, etag, etype, n = (int(x) for x in take(4))
+                nv = {1: 2, 3: 4, 5: 8, 15: 1}[etype]
+                rows = []
+                for _ in range(n):
+                    take()
+                    rows.append([index[int(take())] for _ in range(nv)])
+                blocks.append((edim, etag, etype, rows))
+    dim = 3 if any(b[2] == 5 for b in blocks) else 2
+    ctype, ftype = (5, 3) if dim == 3 else (3, 1)
+    cells = [r for b in blocks if b[2] == ctype for r in b[3]]
+    facets, ftags = [], []
+    for edim, etag, etype, rows in blocks:
+        if etype == ftype and edim == dim - 1:
+            for r in rows:
+                facets.append(r)
+                ftags.append(phys.get((edim, etag), 0))
+    return (dim, np.array(verts, float), np.array(cells, np.int64),
+            np.array(facets, np.int64).reshape(-1, 2 ** (dim - 1)), np.array(ftags, np.int64))
+
+
+# tensor corner t = x + 2y (+4z) -> Gmsh slot; DMPlex closure slot -> tensor corner
+_T2G = {2: [0, 1, 3, 2], 3: [0, 1, 3, 2, 4, 5, 7, 6]}
+_C2T = {2: [0, 1, 3, 2], 3: [0, 2, 3, 1, 4, 5, 7, 6]}
+
+
+class UMesh(BoxMesh):
+    """Unstructured quad/hex mesh for the oracle.  Node numbering is by
+    coordinates: every cell's GLL nodes are placed by its multilinear map
+    (computeFullCoordinates, dmplex.py:62-91) and points closer than `tol`
+    are the same node (ids in order of first appearance) -- independent of
+    the product's topological numbering (kle_umesh.cpp).  Cell frame: Gmsh
+    vertex order, corners handed to the element in DMPlex closure order."""
+
+    def __init__(self, dim, ngl, verts, cells, facets=None, ftags=None, tol=1e-9):
+        from scipy.spatial import cKDTree
+        self.dim, self.ngl = dim, ngl
+        self.nn = ngl ** dim
+        nc = 2 ** dim
+        xi = (1.0 + lobatto(ngl)[0]) / 2.0
+        tv = np.asarray(cells)[:, _T2G[dim]]
+        X = np.asarray(verts, float)[:, :dim]
+        self.E = len(cells)
+        q = np.stack(np.meshgrid(*[np.arange(ngl)] * dim, indexing="ij")[::-1], -1).reshape(-1, dim)
+        # shape functions of tensor corner t at local node l
+        Nw = np.ones((self.nn, nc))
+        for t in range(nc):
+            for k in range(dim):
+                Nw[:, t] *= xi[q[:, k]] if (t >> k) & 1 else 1.0 - xi[q[:, k]]
+        pts = np.einsum("lt,etd->eld", Nw, X[tv]).reshape(-1, dim)
+        scale = max(1.0, np.abs(pts).max())
+        pairs = cKDTree(pts).query_pairs(tol * scale, output_type="ndarray")
+        parent = np.arange(len(pts))
+
+        def root(a):
+            while parent[a] != a:
+                parent[a] = parent[parent[a]]
+                a = parent[a]
+            return a
+
+        for a, b in pairs:
+            ra, rb = root(a), root(b)
+            if ra != rb:
+                parent[max(ra, rb)] = min(ra, rb)
+        roots = np.array([root(a) for a in range(len(pts))])
+        uniq, first = np.unique(roots, return_index=True)
+        order = np.argsort(first)
+        newid = np.empty(len(uniq), np.int64)
+        newid[order] = np.arange(len(uniq))
+        self.conn_ = newid[np.searchsorted(uniq, roots)].reshape(self.E, self.nn)
+        self.N = len(uniq)
+        self.coords_ = np.zeros((self.N, dim))
+        self.coords_[self.conn_.ravel()] = pts  # last cell wins
+        self.corners_ = np.ascontiguousarray(X[tv[:, _C2T[dim]]])
+        # the element routines (restated Spectral) order local nodes as the
+        # reference does (HCooOp of the closure-order corners): tensor index
+        # of reference node q, for the C assembly
+        unit = np.array([[(t >> k) & 1 for k in range(dim)] for t in _C2T[dim]], float)
+        Hc = Element(ngl, dim).table("cooOp", 0)
+        pos = Hc @ unit
+        ti = np.array([[int(np.argmin(np.abs(xi - c))) for c in row] for row in pos])
+        ref_to_tensor = sum(ti[:, k] * ngl ** k for k in range(dim))
+        self.conn_ref_ = np.ascontiguousarray(self.conn_[:, ref_to_tensor])
+        self.tags_ = np.zeros(self.N, np.int64)
+        if facets is not None and len(facets):
+            fmap = {}
+            for f, t in zip(np.asarray(facets), np.asarray(ftags)):
+                if 1 <= t <= 32:
+                    k = tuple(sorted(f.tolist()))
+                    fmap[k] = fmap.get(k, 0) | (1 << (int(t) - 1))
+            for e in range(self.E):
+                for d in range(dim):
+                    for side in (0, 1):
+                        k = tuple(sorted(tv[e, t] for t in range(nc) if ((t >> d) & 1) == side))
+                        if k in fmap:
+                            on = q[:, d] == (ngl - 1 if side else 0)
+                            self.tags_[self.conn_[e, on]] |= fmap[k]
+        self._h = lib().orc_mesh_from_arrays(dim, ngl, self.N, self.E,
+                                             np.ascontiguousarray(self.conn_ref_.ravel()),
+                                             np.ascontiguousarray(self.corners_.ravel()))
+
+    @classmethod
+    def from_gmsh(cls, path, ngl):
+        dim, v, c, f, t = read_gmsh(path)
+        return cls(dim, ngl, v, c, f, t)
+
+    def conn(self):
+        return self.conn_
+
+    def corners(self):
+        return self.corners_
+
+    def coords(self):
+        return self.coords_
+
+    def face_nodes(self, mask):
+        return np.nonzero(self.tags_ & mask)[0]
+
+
+def node_map(coords_a, coords_b, tol=1e-9):
+    """Index map m with coords_b[m[i]] == coords_a[i] (bijection checked)."""
+    from scipy.spatial import cKDTree
+    d, m = cKDTree(coords_b).query(coords_a)
+    assert len(coords_a) == len(coords_b)
+    assert d.max() <= tol * max(1.0, np.abs(coords_b).max()), d.max()
+    assert len(np.unique(m)) == len(m)
+    return m
 
 
 def vtensv(vel, dim):

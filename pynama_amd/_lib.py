@@ -33,7 +33,7 @@ class MeshInfo(C.Structure):
                 ("nelem", C.c_int64 * 3), ("lattice", C.c_int64 * 3), ("n_nodes", C.c_int64),
                 ("n_elems", C.c_int64), ("node_begin", C.c_int64), ("node_end", C.c_int64),
                 ("ext_begin", C.c_int64), ("ext_end", C.c_int64), ("elem_begin", C.c_int64),
-                ("elem_end", C.c_int64)]
+                ("elem_end", C.c_int64), ("kind", C.c_int), ("axis", C.c_int)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
@@ -59,6 +59,10 @@ _SIGS = {
     "kle_ctx_reset_kernel_stats": [vp],
     "kle_mesh_create_box": [C.c_int, i64p, f64p, f64p, C.c_int, C.c_int, C.c_int, pvp],
     "kle_mesh_destroy": [vp],
+    "kle_mesh_create_unstructured": [C.c_int, C.c_int, C.c_int64, f64p, C.c_int64, i64p, C.c_int64, vp, vp,
+                                     C.c_int, C.c_int, pvp],
+    "kle_mesh_create_gmsh": [C.c_char_p, C.c_int, C.c_int, C.c_int, pvp],
+    "kle_mesh_get_elements": [vp, i64p],
     "kle_mesh_get_info": [vp, C.POINTER(MeshInfo)],
     "kle_mesh_get_conn": [vp, i64p],
     "kle_mesh_get_corners": [vp, f64p],

@@ -416,7 +416,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     // structured columns? each row's column list must be exactly a lattice box
     const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
     std::vector<int> box(2 * std::max<int64_t>(nrows, 1), 0);
-    std::atomic<bool> is_box{nrows > 0};
+    std::atomic<bool> is_box{nrows > 0 && m->kind == 0};
     parallel_for(nrows, [&](int64_t lo, int64_t hi) {
         for (int64_t i = lo; i < hi && is_box.load(std::memory_order_relaxed); ++i) {
             const int64_t b = rp[i], e = rp[i + 1];
@@ -470,9 +470,14 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->n_global = m->N * C;
     A->row_lo = m->node_begin * R;
     A->col_lo = m->node_begin * C;
-    A->row_lat[0] = m->L[0];
-    A->row_lat[1] = m->dim == 3 ? m->L[1] : (m->node_end - m->node_begin) / m->L[0];
-    A->row_lat[2] = m->dim == 3 ? (m->node_end - m->node_begin) / (m->L[0] * m->L[1]) : 1;
+    if (m->kind == 0) {
+        A->row_lat[0] = m->L[0];
+        A->row_lat[1] = m->dim == 3 ? m->L[1] : (m->node_end - m->node_begin) / m->L[0];
+        A->row_lat[2] = m->dim == 3 ? (m->node_end - m->node_begin) / (m->L[0] * m->L[1]) : 1;
+    } else {
+        A->row_lat[0] = nrows;
+        A->row_lat[1] = A->row_lat[2] = 1;
+    }
     A->lo_rank = m->halo_lo_rank;
     A->hi_rank = m->halo_hi_rank;
     A->ghost_lo = (m->node_begin - m->ext_begin) * C;
@@ -751,6 +756,31 @@ __global__ __launch_bounds__(256) void k_ops_gather(MeshDev M, int64_t nrows, co
 //                   (the matrix KleSolver.setUp hands to solverFS, kle_solver.py:25)
 // Entries outside those sets are stored as exact zeros (node blocks) and
 // left out of the exported CSR (kle_mat.mask_rule).
+// Write the accumulated block (row node il, column node jl, ext-local) with
+// the MODE's DoF-class rule.
+template <int R, int C, int MODE>
+__device__ __forceinline__ void store_ns(double *v, int lay, int k, int m, int mp, const double *acc, int64_t il,
+                                         int64_t jl, const uint8_t *__restrict__ cls)
+{
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < C; ++b) {
+            const int rc = cls[il * R + a];
+            const int cc = MODE == 5 ? DOF_FREE : cls[jl * C + b];
+            const bool diag = jl == il && a == b;
+            const int rule = MODE == 3 ? MASK_KFS : MODE == 4 ? MASK_KRHSFS : MODE == 5 ? MASK_TANG_ROWS : MASK_KSUM;
+            double out = mask_entry(rule, rc, cc, diag) ? acc[a * C + b] : 0.0;
+            if (diag) {
+                if (MODE == 3 && rc == DOF_TANG) out = acc[a * C + b] + (-1.0);
+                if (MODE == 4 && rc == DOF_NORMAL) out = 1.0;
+                if (MODE == 6 && rc == DOF_TANG) out = 1.0 + (acc[a * C + b] + (-1.0));
+                if (MODE == 6 && rc == DOF_NORMAL) out = 1.0;
+            }
+            v[vofs(lay, R * C, a * C + b, k, m, mp)] = out;
+        }
+}
+
 template <int R, int C, int MODE>
 __global__ __launch_bounds__(256) void k_gather_ns(MeshDev M, int64_t nrows, const int *__restrict__ rowptr,
                                                    const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
@@ -802,23 +832,7 @@ __global__ __launch_bounds__(256) void k_gather_ns(MeshDev M, int64_t nrows, con
 #pragma unroll
                     for (int t = 0; t < R * C; ++t) acc[t] += (MODE == 4) ? -blk[t] : blk[t];
                 }
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-            for (int b = 0; b < C; ++b) {
-                const int rc = cls[il * R + a];
-                const int cc = MODE == 5 ? DOF_FREE : cls[jl * C + b];
-                const bool diag = jl == il && a == b;
-                const int rule = MODE == 3 ? MASK_KFS : MODE == 4 ? MASK_KRHSFS : MODE == 5 ? MASK_TANG_ROWS : MASK_KSUM;
-                double out = mask_entry(rule, rc, cc, diag) ? acc[a * C + b] : 0.0;
-                if (diag) {
-                    if (MODE == 3 && rc == DOF_TANG) out = acc[a * C + b] + (-1.0);
-                    if (MODE == 4 && rc == DOF_NORMAL) out = 1.0;
-                    if (MODE == 6 && rc == DOF_TANG) out = 1.0 + (acc[a * C + b] + (-1.0));
-                    if (MODE == 6 && rc == DOF_NORMAL) out = 1.0;
-                }
-                v[vofs(lay, R * C, a * C + b, k, m, mp)] = out;
-            }
+        store_ns<R, C, MODE>(v, lay, k, m, mp, acc, il, jl, cls);
     }
 }
 
@@ -836,6 +850,263 @@ static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint
     const int64_t threads = A->nrows * 64;
     hipLaunchKernelGGL((k_gather<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
                        A->nrows, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, E, A->d_val);
+}
+
+// ------------------------------------------------------- unstructured
+// Unstructured meshes (kle_umesh.cpp) have no lattice to enumerate a row's
+// cells, so the gather walks the row's incidence list instead: one 64-lane
+// workgroup per node row, the row's incident (cell, local node) pairs in
+// ascending cell order, lanes over the cell's nodes.  Each lane finds its
+// column in the row's sorted column list (binary search; columns outside the
+// pattern -- e.g. Dirichlet columns of K -- are skipped, which is the
+// pattern's own filter) and adds the element block into an LDS window of
+// UW block accumulators.  Within one cell the lanes hit distinct columns;
+// cells are separated by a barrier, so every entry is the ascending-cell sum
+// starting from 0, exactly as the lattice kernels and PETSc's ADD order.
+struct UMeshDev {
+    int ne;
+    const int *conn;      // [e][ne] ext-local node
+    const int64_t *incp;  // owned row -> [incp[i], incp[i+1])
+    const int *inc;       // e * ne + l
+    int64_t glo;          // ext-local id of owned row 0
+};
+
+constexpr int UW = 256;
+
+__device__ __forceinline__ int find_col(const int *__restrict__ cols, int lo, int hi, int j)
+{
+    // cols[lo, hi) ascending; -1 if absent
+    --hi;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const int c = cols[mid];
+        if (c == j) return mid;
+        if (c < j) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return -1;
+}
+
+// MODE as k_gather (0 K, 1 Krhs, 2 Rw) and k_gather_ns (3 Kfs, 4 Krhsfs, 5 Rwfs / Rdfs, 6 K+Kfs)
+template <int R, int C, int MODE>
+__global__ __launch_bounds__(64) void k_gather_u(UMeshDev U, int64_t nrows, const int *__restrict__ rowptr,
+                                                 const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
+                                                 int lay, const int *__restrict__ bcol,
+                                                 const uint8_t *__restrict__ dir, const uint8_t *__restrict__ cls,
+                                                 const double *__restrict__ Eblk, double *__restrict__ val)
+{
+    constexpr int RC = R * C;
+    __shared__ double acc[UW * RC];
+    const int lane = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    if (row >= nrows) return;
+    const int64_t il = row + U.glo;
+    const int b0 = rowptr[row], mp = rowptr[row + 1] - b0, m = rowcnt ? rowcnt[row] : mp;
+    double *v = val + vptr[row];
+    const int *cols = bcol + b0;
+    if (MODE <= 2 && dir[il]) {
+        // K[dir,dir] = 0 + ... + 0 + 1 and Krhs[dir,dir] = 1 (mat_fs.py:115-120,182-183)
+        if (MODE != 2 && lane == 0 && m == 1)
+            for (int a = 0; a < R; ++a)
+                for (int b = 0; b < C; ++b) v[vofs(lay, RC, a * C + b, 0, m, mp)] = (a == b) ? 1.0 : 0.0;
+        return;
+    }
+    const int ne = U.ne;
+    const int64_t q0 = U.incp[row], q1 = U.incp[row + 1];
+    for (int w0 = 0; w0 < m; w0 += UW) {
+        const int wn = min(UW, m - w0);
+        for (int t = lane; t < wn * RC; t += 64) acc[t] = 0.0;
+        __syncthreads();
+        for (int64_t q = q0; q < q1; ++q) {
+            const int ei = U.inc[q];
+            const int e = ei / ne, li = ei - e * ne;
+            const int *ce = U.conn + (int64_t)e * ne;
+            for (int lj = lane; lj < ne; lj += 64) {
+                const int pos = find_col(cols, w0, w0 + wn, ce[lj]);
+                if (pos < 0) continue;
+                const double *blk = Eblk + (((int64_t)e * ne + li) * ne + lj) * RC;
+                double *a = acc + (pos - w0) * RC;
+#pragma unroll
+                for (int t = 0; t < RC; ++t) a[t] += (MODE == 1 || MODE == 4) ? -blk[t] : blk[t];
+            }
+            __syncthreads();
+        }
+        for (int k = lane; k < wn; k += 64) {
+            const double *a = acc + k * RC;
+            if constexpr (MODE <= 2) {
+#pragma unroll
+                for (int t = 0; t < RC; ++t) v[vofs(lay, RC, t, w0 + k, m, mp)] = a[t];
+            } else {
+                double blk[RC];
+#pragma unroll
+                for (int t = 0; t < RC; ++t) blk[t] = a[t];
+                store_ns<R, C, MODE>(v, lay, w0 + k, m, mp, blk, il, cols[w0 + k], cls);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_ops_weights_u(UMeshDev U, int64_t nrows, const double *__restrict__ geo,
+                                                       double *__restrict__ winv)
+{
+    const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    constexpr int G1 = 1 + DIM * DIM;
+    double W = 0.0;
+    for (int64_t q = U.incp[row]; q < U.incp[row + 1]; ++q) W += geo[(int64_t)U.inc[q] * G1];
+    winv[row] = 1.0 / W;
+}
+
+// Collocation operators on an unstructured mesh: per incident (cell, li) only
+// the nodes on the DIM tensor lines through li carry a nonzero block (the
+// other entries of the element block are exact zeros, which do not change an
+// ascending sum), so lanes take the DIM*ngl line candidates.  Block values as
+// k_ops_gather.
+constexpr int UWO = 128;
+template <int DIM>
+__global__ __launch_bounds__(64) void k_ops_gather_u(UMeshDev U, int ngl, int64_t nrows, const int *__restrict__ rowcnt,
+                                                     const int *__restrict__ bcol, const double *__restrict__ geo,
+                                                     const double *__restrict__ dh, const double *__restrict__ winv,
+                                                     OpsOut out)
+{
+    constexpr int DW = DIM == 2 ? 1 : 3, DS = DIM == 2 ? 3 : 6, G1 = 1 + DIM * DIM;
+    constexpr int NC = DW * DIM, NS = DS * DIM, ND = DIM * DS, NB = NC + NS + ND;
+    __shared__ double acc[UWO * NB];
+    const int lane = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    if (row >= nrows) return;
+    const int m = rowcnt[row];
+    const int *cols = bcol + out.rp_c[row];
+    const double wi = winv[row];
+    const int mpc = out.rp_c[row + 1] - out.rp_c[row], mps = out.rp_s[row + 1] - out.rp_s[row],
+              mpd = out.rp_d[row + 1] - out.rp_d[row];
+    double *vc = out.curl + out.vp_c[row];
+    double *vs = out.srt + out.vp_s[row];
+    double *vd = out.div + out.vp_d[row];
+    const int ne = U.ne;
+    const int64_t q0 = U.incp[row], q1 = U.incp[row + 1];
+    for (int w0 = 0; w0 < m; w0 += UWO) {
+        const int wn = min(UWO, m - w0);
+        for (int t = lane; t < wn * NB; t += 64) acc[t] = 0.0;
+        __syncthreads();
+        for (int64_t q = q0; q < q1; ++q) {
+            const int ei = U.inc[q];
+            const int e = ei / ne, li = ei - e * ne;
+            int oi[3] = {li % ngl, (li / ngl) % ngl, DIM == 3 ? li / (ngl * ngl) : 0};
+            for (int cand = lane; cand < DIM * ngl; cand += 64) {
+                const int ax = cand / ngl, t = cand - ax * ngl;
+                if (ax > 0 && t == oi[ax]) continue;  // the row node itself: taken once, on axis 0
+                int oj[3] = {oi[0], oi[1], oi[2]};
+                oj[ax] = t;
+                const int lj = oj[0] + ngl * (oj[1] + ngl * oj[2]);
+                const int pos = find_col(cols, w0, w0 + wn, U.conn[(int64_t)e * ne + lj]);
+                if (pos < 0) continue;
+                const double *g = geo + ((int64_t)e * ne + li) * G1;
+                const double c = g[0];
+                double Hrs[DIM];
+                for (int kk = 0; kk < DIM; ++kk) {
+                    bool line = true;
+                    for (int j = 0; j < DIM; ++j)
+                        if (j != kk) line = line && oj[j] == oi[j];
+                    Hrs[kk] = line ? dh[oi[kk] * ngl + oj[kk]] : 0.0;
+                }
+                double H[DIM];
+                for (int d = 0; d < DIM; ++d) {
+                    double s = 0.0;
+                    for (int kk = 0; kk < DIM; ++kk) s += g[1 + d * DIM + kk] * Hrs[kk];
+                    H[d] = s;
+                }
+                double *Cc = acc + (pos - w0) * NB, *S = Cc + NC, *D = S + NS;
+                if constexpr (DIM == 3) {
+                    Cc[0 * 3 + 2] += c * H[1];
+                    Cc[0 * 3 + 1] += c * -H[2];
+                    Cc[1 * 3 + 0] += c * H[2];
+                    Cc[1 * 3 + 2] += c * -H[0];
+                    Cc[2 * 3 + 1] += c * H[0];
+                    Cc[2 * 3 + 0] += c * -H[1];
+                    S[0 * 3 + 0] += c * H[0];
+                    S[1 * 3 + 1] += c * (0.5 * H[0]);
+                    S[5 * 3 + 2] += c * (0.5 * H[0]);
+                    S[2 * 3 + 1] += c * H[1];
+                    S[1 * 3 + 0] += c * (0.5 * H[1]);
+                    S[3 * 3 + 2] += c * (0.5 * H[1]);
+                    S[4 * 3 + 2] += c * H[2];
+                    S[5 * 3 + 0] += c * (0.5 * H[2]);
+                    S[3 * 3 + 1] += c * (0.5 * H[2]);
+                    D[0 * 6 + 0] += c * H[0];
+                    D[0 * 6 + 1] += c * H[1];
+                    D[0 * 6 + 5] += c * H[2];
+                    D[1 * 6 + 1] += c * H[0];
+                    D[1 * 6 + 2] += c * H[1];
+                    D[1 * 6 + 3] += c * H[2];
+                    D[2 * 6 + 5] += c * H[0];
+                    D[2 * 6 + 3] += c * H[1];
+                    D[2 * 6 + 4] += c * H[2];
+                } else {
+                    Cc[1] += c * H[0];
+                    Cc[0] += c * -H[1];
+                    S[0 * 2 + 0] += c * H[0];
+                    S[1 * 2 + 1] += c * (0.5 * H[0]);
+                    S[2 * 2 + 1] += c * H[1];
+                    S[1 * 2 + 0] += c * (0.5 * H[1]);
+                    D[0 * 3 + 0] += c * H[0];
+                    D[0 * 3 + 1] += c * H[1];
+                    D[1 * 3 + 1] += c * H[0];
+                    D[1 * 3 + 2] += c * H[1];
+                }
+            }
+            __syncthreads();
+        }
+        for (int k = lane; k < wn; k += 64) {
+            const double *Cc = acc + k * NB, *S = Cc + NC, *D = S + NS;
+            for (int t = 0; t < NC; ++t) vc[vofs(out.lay, NC, t, w0 + k, m, mpc)] = Cc[t] * wi;
+            for (int t = 0; t < NS; ++t) vs[vofs(out.lay, NS, t, w0 + k, m, mps)] = S[t] * wi;
+            for (int t = 0; t < ND; ++t) vd[vofs(out.lay, ND, t, w0 + k, m, mpd)] = D[t] * wi;
+        }
+        __syncthreads();
+    }
+}
+
+struct UMeshBuf {
+    int *conn = nullptr, *inc = nullptr;
+    int64_t *incp = nullptr;
+    UMeshDev dev{};
+    ~UMeshBuf()
+    {
+        hipFree(conn);
+        hipFree(inc);
+        hipFree(incp);
+    }
+};
+
+static int upload_umesh(kle_ctx *ctx, const kle_mesh *m, UMeshBuf &U)
+{
+    const int ne = m->nn();
+    std::vector<int> c32(std::max<size_t>(m->u_conn.size(), 1));
+    for (size_t k = 0; k < m->u_conn.size(); ++k) c32[k] = (int)(m->u_conn[k] - m->ext_begin);
+    KLE_HIP(hipMalloc(&U.conn, sizeof(int) * c32.size()));
+    KLE_HIP(hipMalloc(&U.incp, sizeof(int64_t) * m->u_incp.size()));
+    KLE_HIP(hipMalloc(&U.inc, sizeof(int) * std::max<size_t>(m->u_inc.size(), 1)));
+    KLE_HIP(hipMemcpyAsync(U.conn, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice, ctx->stream));
+    KLE_HIP(hipMemcpyAsync(U.incp, m->u_incp.data(), sizeof(int64_t) * m->u_incp.size(), hipMemcpyHostToDevice,
+                           ctx->stream));
+    if (!m->u_inc.empty())
+        KLE_HIP(hipMemcpyAsync(U.inc, m->u_inc.data(), sizeof(int) * m->u_inc.size(), hipMemcpyHostToDevice,
+                               ctx->stream));
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    U.dev = {ne, U.conn, U.incp, U.inc, m->node_begin - m->ext_begin};
+    return 0;
+}
+
+template <int R, int C, int MODE>
+static void launch_gather_u(kle_ctx *ctx, const UMeshDev &U, kle_mat *A, const uint8_t *dir, const uint8_t *cls,
+                            const double *E)
+{
+    if (A->nrows == 0) return;
+    hipLaunchKernelGGL((k_gather_u<R, C, MODE>), dim3((unsigned)A->nrows), dim3(64), 0, ctx->stream, U, A->nrows,
+                       A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, cls, E, A->d_val);
 }
 
 }  // namespace kle
@@ -861,7 +1132,19 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     KLE_HIP(hipMalloc(&ddir, m->dir.size()));
     KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
     MeshDev M = mesh_dev(m);
-    if (dim == 3) {
+    UMeshBuf U;
+    if (m->kind == 1) {
+        KLE_TRY(upload_umesh(ctx, m, U));
+        if (dim == 3) {
+            launch_gather_u<3, 3, 0>(ctx, U.dev, mK, ddir, nullptr, dKe);
+            launch_gather_u<3, 3, 1>(ctx, U.dev, mKr, ddir, nullptr, dKe);
+            launch_gather_u<3, 3, 2>(ctx, U.dev, mRw, ddir, nullptr, dRwe);
+        } else {
+            launch_gather_u<2, 2, 0>(ctx, U.dev, mK, ddir, nullptr, dKe);
+            launch_gather_u<2, 2, 1>(ctx, U.dev, mKr, ddir, nullptr, dKe);
+            launch_gather_u<2, 1, 2>(ctx, U.dev, mRw, ddir, nullptr, dRwe);
+        }
+    } else if (dim == 3) {
         launch_gather<3, 3, 0>(ctx, M, mK, ddir, dKe);
         launch_gather<3, 3, 1>(ctx, M, mKr, ddir, dKe);
         launch_gather<3, 3, 2>(ctx, M, mRw, ddir, dRwe);
@@ -918,7 +1201,22 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
              md->d_rowptr, mc->d_vptr, ms->d_vptr, md->d_vptr, mc->vlayout};
     const unsigned gq = (unsigned)((nq + 255) / 256), gr = (unsigned)((nrows + 255) / 256),
                    gw = (unsigned)((nrows * 64 + 255) / 256);
-    if (dim == 3) {
+    UMeshBuf U;
+    if (m->kind == 1) KLE_TRY(upload_umesh(ctx, m, U));
+    if (m->kind == 1 && nq > 0 && nrows > 0) {
+        if (dim == 3) {
+            hipLaunchKernelGGL(k_geometry<3>, dim3(gq), dim3(256), 0, ctx->stream, nel, m->ngl, T.O, dX, geo);
+            hipLaunchKernelGGL(k_ops_weights_u<3>, dim3(gr), dim3(256), 0, ctx->stream, U.dev, nrows, geo, winv);
+            hipLaunchKernelGGL(k_ops_gather_u<3>, dim3((unsigned)nrows), dim3(64), 0, ctx->stream, U.dev, m->ngl,
+                               nrows, dcnt, mc->d_bcol, geo, T.O.dh, winv, o);
+        } else {
+            hipLaunchKernelGGL(k_geometry<2>, dim3(gq), dim3(256), 0, ctx->stream, nel, m->ngl, T.O, dX, geo);
+            hipLaunchKernelGGL(k_ops_weights_u<2>, dim3(gr), dim3(256), 0, ctx->stream, U.dev, nrows, geo, winv);
+            hipLaunchKernelGGL(k_ops_gather_u<2>, dim3((unsigned)nrows), dim3(64), 0, ctx->stream, U.dev, m->ngl,
+                               nrows, dcnt, mc->d_bcol, geo, T.O.dh, winv, o);
+        }
+    } else if (m->kind == 1) {
+    } else if (dim == 3) {
         hipLaunchKernelGGL(k_geometry<3>, dim3(gq), dim3(256), 0, ctx->stream, nel, m->ngl, T.O, dX, geo);
         hipLaunchKernelGGL(k_ops_weights<3>, dim3(gr), dim3(256), 0, ctx->stream, M, nrows, geo, winv);
         hipLaunchKernelGGL(k_ops_gather<3>, dim3(gw), dim3(256), 0, ctx->stream, M, nrows, dcnt, mc->d_bcol, geo,
@@ -974,7 +1272,25 @@ int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_
     KLE_HIP(hipMalloc(&dcls, m->dof_cls.size()));
     KLE_HIP(hipMemcpyAsync(dcls, m->dof_cls.data(), m->dof_cls.size(), hipMemcpyHostToDevice, ctx->stream));
     MeshDev M = mesh_dev(m);
-    if (dim == 3) {
+    UMeshBuf U;
+    if (m->kind == 1) {
+        KLE_TRY(upload_umesh(ctx, m, U));
+        if (dim == 3) {
+            launch_gather_u<3, 3, 3>(ctx, U.dev, mf, ddir, dcls, dKe);
+            launch_gather_u<3, 3, 4>(ctx, U.dev, mr, ddir, dcls, dKe);
+            launch_gather_u<3, 3, 5>(ctx, U.dev, mw, ddir, dcls, dRwe);
+            launch_gather_u<3, 3, 6>(ctx, U.dev, ms, ddir, dcls, dKe);
+            launch_gather_u<3, 1, 2>(ctx, U.dev, md, ddir, dcls, dRde);
+            launch_gather_u<3, 1, 5>(ctx, U.dev, mdf, ddir, dcls, dRde);
+        } else {
+            launch_gather_u<2, 2, 3>(ctx, U.dev, mf, ddir, dcls, dKe);
+            launch_gather_u<2, 2, 4>(ctx, U.dev, mr, ddir, dcls, dKe);
+            launch_gather_u<2, 1, 5>(ctx, U.dev, mw, ddir, dcls, dRwe);
+            launch_gather_u<2, 2, 6>(ctx, U.dev, ms, ddir, dcls, dKe);
+            launch_gather_u<2, 1, 2>(ctx, U.dev, md, ddir, dcls, dRde);
+            launch_gather_u<2, 1, 5>(ctx, U.dev, mdf, ddir, dcls, dRde);
+        }
+    } else if (dim == 3) {
         launch_gather_ns<3, 3, 3>(ctx, M, mf, dcls, dKe);
         launch_gather_ns<3, 3, 4>(ctx, M, mr, dcls, dKe);
         launch_gather_ns<3, 3, 5>(ctx, M, mw, dcls, dRwe);

@@ -117,6 +117,18 @@ struct kle_mesh {
     int halo_lo_rank = -1, halo_hi_rank = -1;
     int64_t halo_lo_nodes = 0, halo_hi_nodes = 0;   // ghost nodes received
     int64_t send_lo_nodes = 0, send_hi_nodes = 0;   // owned nodes sent to neighbours
+    // kind 1 (unstructured, kle_umesh.cpp): explicit topology.  Local elements
+    // are every cell touching an owned node (owned + ghost cells), ascending
+    // global cell id = the reference's ADD order; node ids are global.
+    int kind = 0;
+    std::vector<int64_t> u_elem;    // global cell id of local element e
+    std::vector<int64_t> u_conn;    // [e][nn] global node id, tensor order
+    std::vector<double> u_corners;  // [e][2^dim][dim] DMPlex closure order
+    std::vector<double> u_coords;   // [ext node][dim]
+    std::vector<uint32_t> u_tags;   // [ext node] Face Sets bits (tag t -> bit t-1)
+    std::vector<int64_t> u_incp;    // owned row i -> u_inc[u_incp[i] .. u_incp[i+1])
+    std::vector<int32_t> u_inc;     // e * nn + l, ascending e
+    int64_t n_local_elems() const { return kind ? (int64_t)u_elem.size() : elem_end - elem_begin; }
     int nn() const { return dim == 2 ? ngl * ngl : ngl * ngl * ngl; }
     void lattice_of(int64_t id, int64_t *c) const {
         c[0] = id % L[0];
@@ -240,6 +252,9 @@ int host_threads();
 void parallel_for(int64_t n, const std::function<void(int64_t, int64_t)> &f);
 // Symbolic pattern `which` of the owned rows as CSR (row_ptr[n+1], global cols).
 int pattern_csr(const kle_mesh *m, int which, std::vector<int64_t> &row_ptr, std::vector<int64_t> &cols);
+// Unstructured mesh (kle_umesh.cpp): sorted unique node neighbours of owned
+// row i (nodes sharing a local cell); on_face: Face Sets bits of an ext node.
+void umesh_row_nodes(const kle_mesh *m, int64_t i, std::vector<int64_t> &out);
 enum DofClass : uint8_t { DOF_FREE = 0, DOF_TANG = 1, DOF_NORMAL = 2 };
 // which PETSc entries of a node block exist (MatNS.buildNS, mat_ns.py:47-145)
 enum MaskRule { MASK_NONE = 0, MASK_KFS = 1, MASK_KRHSFS = 2, MASK_TANG_ROWS = 3, MASK_KSUM = 4 };

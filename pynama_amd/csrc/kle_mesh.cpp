@@ -64,6 +64,22 @@ static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
         if (which != 2) emit(i);
         return;
     }
+    auto filter = [&](int64_t j) {
+        switch (which) {
+        case 0: return !is_dir(m, j);
+        case 1: return is_dir(m, j);
+        case 4: return di || is_dir(m, j);
+        case 5: return is_dir(m, j);
+        default: return true;  // 2, 3, 6
+        }
+    };
+    if (m->kind == 1) {
+        thread_local std::vector<int64_t> nb;
+        umesh_row_nodes(m, i - m->node_begin, nb);
+        for (int64_t j : nb)
+            if (filter(j)) emit(j);
+        return;
+    }
     int64_t c[3], lo[3], hi[3];
     m->lattice_of(i, c);
     for (int d = 0; d < 3; ++d) nbr_range(m, d, c[d], lo[d], hi[d]);
@@ -71,16 +87,8 @@ static void row_cols(const kle_mesh *m, int which, int64_t i, F &&emit)
     for (q[2] = lo[2]; q[2] <= hi[2]; ++q[2])
         for (q[1] = lo[1]; q[1] <= hi[1]; ++q[1])
             for (q[0] = lo[0]; q[0] <= hi[0]; ++q[0]) {
-                int64_t j = m->id_of(q);
-                bool keep;
-                switch (which) {
-                case 0: keep = !is_dir(m, j); break;
-                case 1: keep = is_dir(m, j); break;
-                case 4: keep = di || is_dir(m, j); break;
-                case 5: keep = is_dir(m, j); break;
-                default: keep = true;  // 2, 3, 6
-                }
-                if (keep) emit(j);
+                const int64_t j = m->id_of(q);
+                if (filter(j)) emit(j);
             }
 }
 
@@ -236,12 +244,28 @@ int kle_mesh_get_info(const kle_mesh *m, kle_mesh_info *info)
     info->ext_end = m->ext_end;
     info->elem_begin = m->elem_begin;
     info->elem_end = m->elem_end;
+    info->kind = m->kind;
+    info->axis = m->axis;
+    if (m->kind == 1) info->lattice[0] = info->lattice[1] = info->lattice[2] = 0;
+    return 0;
+}
+
+int kle_mesh_get_elements(const kle_mesh *m, int64_t *ids)
+{
+    KLE_ARG(m && ids, "null arg");
+    if (m->kind == 1) std::copy(m->u_elem.begin(), m->u_elem.end(), ids);
+    else
+        for (int64_t e = m->elem_begin; e < m->elem_end; ++e) ids[e - m->elem_begin] = e;
     return 0;
 }
 
 int kle_mesh_get_conn(const kle_mesh *m, int64_t *conn)
 {
     KLE_ARG(m && conn, "null arg");
+    if (m->kind == 1) {
+        std::copy(m->u_conn.begin(), m->u_conn.end(), conn);
+        return 0;
+    }
     const int ngl = m->ngl, nn = m->nn(), p = m->p;
     for (int64_t e = m->elem_begin; e < m->elem_end; ++e) {
         int64_t ex = e % m->nel[0], ey = (e / m->nel[0]) % m->nel[1], ez = e / (m->nel[0] * m->nel[1]);
@@ -258,6 +282,10 @@ int kle_mesh_get_conn(const kle_mesh *m, int64_t *conn)
 int kle_mesh_get_corners(const kle_mesh *m, double *xyz)
 {
     KLE_ARG(m && xyz, "null arg");
+    if (m->kind == 1) {
+        std::copy(m->u_corners.begin(), m->u_corners.end(), xyz);
+        return 0;
+    }
     const int nc = 1 << m->dim;
     for (int64_t e = m->elem_begin; e < m->elem_end; ++e) {
         int64_t ei[3] = {e % m->nel[0], (e / m->nel[0]) % m->nel[1], e / (m->nel[0] * m->nel[1])};
@@ -274,6 +302,11 @@ int kle_mesh_get_corners(const kle_mesh *m, double *xyz)
 int kle_mesh_get_coords(const kle_mesh *m, double *xyz)
 {
     KLE_ARG(m && xyz, "null arg");
+    if (m->kind == 1) {
+        std::copy(m->u_coords.begin() + (m->node_begin - m->ext_begin) * m->dim,
+                  m->u_coords.begin() + (m->node_end - m->ext_begin) * m->dim, xyz);
+        return 0;
+    }
     for (int64_t n = m->node_begin; n < m->node_end; ++n) {
         int64_t c[3];
         m->lattice_of(n, c);
@@ -307,6 +340,7 @@ static bool face_axis(int dim, int f, int &axis, int &side)
 
 static bool on_faces(const kle_mesh *m, int64_t node, unsigned mask)
 {
+    if (m->kind == 1) return (m->u_tags[node - m->ext_begin] & mask) != 0;
     int64_t c[3];
     m->lattice_of(node, c);
     for (int f = 0; f < 6; ++f) {
@@ -377,6 +411,8 @@ int kle_mesh_set_noslip_dofs(kle_mesh *m, const int64_t *tang, int64_t nt, const
 int kle_mesh_set_noslip_faces(kle_mesh *m, const int *faces, int nfaces)
 {
     KLE_ARG(m && (nfaces == 0 || faces), "null arg");
+    // the wall's normal axis comes from its name (NsWalls, nswalls.py), also on
+    // unstructured meshes, whose Face Sets values map to the same names
     int axes[6];
     for (int k = 0; k < nfaces; ++k) {
         int side;

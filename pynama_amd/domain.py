@@ -6,14 +6,17 @@ Host-side mirror of the subset of the reference's Domain
 configure / setOptions / setUp, getDimension(s), getNodesRange,
 getLocalCellRange, getNodesDirichlet, getFullCoordArray, getAllNodes,
 applyBoundaryConditions.  Same config schema as src/cases/*.yaml.
-Only box meshes ("box-mesh") are provided; gmsh input is out of scope.
+Meshes: "box-mesh" (BoxDom) and "gmsh-file" (GmshDom, MSH 4.1 quads/hexes,
+dmplex.py:390-395); on a Gmsh mesh the boundary names are the Face Sets
+values of the facets' physical tags in the reference's name order (tag 1 ->
+"down" in 2-D, "back" in 3-D; dmplex.py:27-30,175-178).
 """
 import copy
 
 import numpy as np
 
 from . import fields
-from .mesh import FACES, BoxMesh
+from .mesh import FACES, BoxMesh, UnstructuredMesh
 from .runtime import world
 
 
@@ -44,6 +47,7 @@ class Domain:
         self.mesh = None
         self._bcs = []
         self._type = None
+        self._type_mesh = None
 
     # ------------------------------------------------------------ config
     def configure(self, inp):
@@ -59,6 +63,8 @@ class Domain:
                 self.domData["ngl"] = val
             elif key in ("lower", "upper", "nelem"):
                 self.domData["box-mesh"][key] = val
+            elif key == "fileName":
+                self.domData["gmsh-file"] = val
             elif key in ("freeSlip", "noSlip", "constant"):
                 k = {"freeSlip": "free-slip", "noSlip": "no-slip"}.get(key, key)
                 self.bcData[k] = val
@@ -66,15 +72,30 @@ class Domain:
 
     # ------------------------------------------------------------- setup
     def setUp(self):
-        if not self.domData or "box-mesh" not in self.domData:
-            raise ValueError("only 'box-mesh' domains are provided")
-        box = self.domData["box-mesh"]
-        rank, size = world()
-        self.mesh = BoxMesh(len(box["nelem"]), box["nelem"], box["lower"], box["upper"],
-                            self.domData["ngl"], rank, size)
+        self.create()
         self.dim = self.mesh.dim
         self._coords = self.mesh.coords()
         self._setup_bcs()
+
+    def create(self):
+        """Domain.create (domain.py:25-43): the mesh of the 'box-mesh' or
+        'gmsh-file' entry, partitioned over the ranks."""
+        if not self.domData:
+            raise ValueError("Domain not defined")
+        rank, size = world()
+        if "box-mesh" in self.domData:
+            box = self.domData["box-mesh"]
+            self._type_mesh = "box"
+            self.mesh = BoxMesh(len(box["nelem"]), box["nelem"], box["lower"], box["upper"],
+                                self.domData["ngl"], rank, size)
+        elif "gmsh-file" in self.domData:
+            self._type_mesh = "gmsh"
+            self.mesh = UnstructuredMesh.from_gmsh(self.domData["gmsh-file"], self.domData["ngl"], rank, size)
+        else:
+            raise ValueError("Mesh Type not defined")
+
+    def getMeshType(self):
+        return self._type_mesh
 
     def _setup_bcs(self):
         if not self.bcData:

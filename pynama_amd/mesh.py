@@ -1,10 +1,18 @@
-"""Structured box mesh + slab partition (host side of libkle, no GPU needed).
+"""Meshes + slab partition (host side of libkle, no GPU needed).
 
-Replaces for the hot path the reference's DMPlex box mesh and FEM section
-numbering (domain/dmplex.py:18-49,193-196,352-372,382-388).  Canonical
+BoxMesh replaces for the hot path the reference's DMPlex box mesh and FEM
+section numbering (domain/dmplex.py:18-49,193-196,352-372,382-388).  Canonical
 numbering: node id = ix + Lx*(iy + Ly*iz) on the GLL lattice, cells
 x-fastest, element-local nodes in tensor order; ranks own slabs of whole
 element layers along the slowest axis (z in 3-D, y in 2-D).
+
+UnstructuredMesh replaces GmshDom (dmplex.py:390-395) + DMPlexDistribute:
+quads / hexes from a Gmsh 4.1 file or from arrays; GLL nodes numbered by
+topological entity (kle_umesh.cpp), ranks own slabs of cells along the
+longest axis, each rank's nodes ordered [lower interface | interior | upper
+interface] so the halo keeps the box mesh's two-range form.  Boundary faces
+carry the Gmsh physical tag of their facet as the Face Sets value: tag t is
+face name FACES[dim][t-1] (dmplex.py:27-30,175-178).
 """
 import ctypes as C
 
@@ -17,18 +25,15 @@ FACES = {2: ["down", "right", "up", "left"],
          3: ["back", "front", "down", "up", "right", "left"]}
 
 
-class BoxMesh:
-    def __init__(self, dim, nelem, lower, upper, ngl, rank=0, nranks=1):
-        self.dim, self.ngl = int(dim), int(ngl)
-        ne = np.array(list(nelem) + [1] * (3 - dim), dtype=np.int64)
-        lo = np.array(list(lower) + [0.0] * (3 - dim), dtype=np.float64)
-        hi = np.array(list(upper) + [1.0] * (3 - dim), dtype=np.float64)
-        h = C.c_void_p()
-        call("kle_mesh_create_box", self.dim, ne, lo, hi, self.ngl, int(rank), int(nranks), C.byref(h))
+class _Mesh:
+    def _load(self, h):
         self._h = h
         info = MeshInfo()
         call("kle_mesh_get_info", h, C.byref(info))
         self.info = info
+        self.dim, self.ngl = info.dim, info.ngl
+        dim = self.dim
+        self.kind = "box" if info.kind == 0 else "unstructured"
         self.rank, self.nranks = info.rank, info.nranks
         self.N = info.n_nodes
         self.E = info.n_elems
@@ -115,3 +120,48 @@ class BoxMesh:
              C.byref(hr))
         return {"lo_nodes": lo.value, "hi_nodes": hi.value, "send_lo_nodes": sl.value,
                 "send_hi_nodes": sh.value, "lo_rank": lr.value, "hi_rank": hr.value}
+
+
+class BoxMesh(_Mesh):
+    def __init__(self, dim, nelem, lower, upper, ngl, rank=0, nranks=1):
+        dim = int(dim)
+        ne = np.array(list(nelem) + [1] * (3 - dim), dtype=np.int64)
+        lo = np.array(list(lower) + [0.0] * (3 - dim), dtype=np.float64)
+        hi = np.array(list(upper) + [1.0] * (3 - dim), dtype=np.float64)
+        h = C.c_void_p()
+        call("kle_mesh_create_box", dim, ne, lo, hi, int(ngl), int(rank), int(nranks), C.byref(h))
+        self._load(h)
+
+
+class UnstructuredMesh(_Mesh):
+    """Quad / hex mesh: UnstructuredMesh.from_gmsh(path, ngl) (GmshDom.create)
+    or UnstructuredMesh(dim, ngl, vertices, cells, facets, facet_tags)."""
+
+    def __init__(self, dim, ngl, vertices, cells, facets=None, facet_tags=None, rank=0, nranks=1, _handle=None):
+        if _handle is not None:
+            self._load(_handle)
+            return
+        dim = int(dim)
+        v = np.zeros((len(vertices), 3))
+        v[:, :dim] = np.asarray(vertices, dtype=np.float64)[:, :dim]
+        cells = np.ascontiguousarray(cells, dtype=np.int64)
+        assert cells.ndim == 2 and cells.shape[1] == 2 ** dim
+        nf = 0 if facets is None else len(facets)
+        fa = np.ascontiguousarray(facets if nf else np.zeros((1, 2 ** (dim - 1))), dtype=np.int64)
+        ft = np.ascontiguousarray(facet_tags if nf else np.zeros(1), dtype=np.int32)
+        h = C.c_void_p()
+        call("kle_mesh_create_unstructured", dim, int(ngl), len(v), np.ascontiguousarray(v.ravel()), len(cells),
+             cells.ravel(), nf, fa.ctypes.data, ft.ctypes.data, int(rank), int(nranks), C.byref(h))
+        self._load(h)
+
+    @classmethod
+    def from_gmsh(cls, path, ngl, rank=0, nranks=1):
+        h = C.c_void_p()
+        call("kle_mesh_create_gmsh", str(path).encode(), int(ngl), int(rank), int(nranks), C.byref(h))
+        return cls(None, None, None, None, _handle=h)
+
+    def elements(self):
+        """Global cell ids of the local (owned + ghost) elements, ascending."""
+        out = np.zeros(max(self.elem_range[1] - self.elem_range[0], 1), dtype=np.int64)
+        call("kle_mesh_get_elements", self._h, out)
+        return out[: self.elem_range[1] - self.elem_range[0]]

@@ -34,6 +34,9 @@ import numpy as np
 
 REF_SRC = "/root/reference/src"
 OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))  # repo root: oracle, meshgen
+from oracle import oracle as O  # noqa: E402
+from pynama_amd.meshgen import perturbed_box  # noqa: E402
 
 # ---------------------------------------------------------------- stubs ----
 _mpi = types.ModuleType("mpi4py")
@@ -486,6 +489,52 @@ class FakeDomain:
         self.bc.setTangentialValuesToVec(vec, name, t, nu)
 
 
+class FakeUDomain(FakeDomain):
+    """Unstructured quad/hex mesh (GmshDom stand-in) on the oracle's
+    coordinate numbering (oracle.UMesh); the element matrices, assembly, BCs
+    and solve are the reference's own code as for FakeDomain.  Boundary name
+    i = Face Sets value i + 1 (dmplex.py:175-178)."""
+
+    def __init__(self, umesh, bc):
+        dim, ngl = umesh.dim, umesh.ngl
+        self.dim = dim
+        self.dim_w = 1 if dim == 2 else 3
+        self.dim_s = 3 if dim == 2 else 6
+        self.ngl = ngl
+        self.N, self.E = umesh.N, umesh.E
+        self.elem = Spectral(ngl, dim)
+        self.corners = umesh.corners().copy()
+        self.coords = umesh.coords().copy()
+        # the reference's element-local node order (spectral / closure order):
+        # node q of cell e sits at HCooOp[q] @ corners (dmplex.py:62-91)
+        from scipy.spatial import cKDTree
+        tree = cKDTree(self.coords)
+        H = np.array(self.elem.HCooOp)
+        self.conn = np.zeros((self.E, len(H)), dtype=np.int64)
+        for e in range(self.E):
+            d, idx = tree.query(H @ self.corners[e])
+            assert d.max() < 1e-9
+            self.conn[e] = idx
+        self.umesh = umesh
+        self.bc = BoundaryConditions(FACES[dim])
+        self.bc.setBoundaryConditions(bc)
+        for name in self.bc.getNames():
+            self.bc.setBoundaryNodes(name, self.border_nodes(name))
+        for name in self.bc.getBordersNeedsCoords():
+            inds = self.bc.getIndicesByName(name)
+            nodes = inds[:: dim] // dim
+            self.bc.setBoundaryCoords(name, self.coords[nodes].ravel().copy())
+        adj = [set() for _ in range(self.N)]
+        for e in range(self.E):
+            st = set(self.conn[e].tolist())
+            for n in self.conn[e]:
+                adj[n] |= st
+        self.adj = adj
+
+    def border_nodes(self, name):
+        return self.umesh.face_nodes(1 << FACES[self.dim].index(name)).tolist()
+
+
 def csr_dict(prefix, mat):
     ip, ix, d = mat.csr()
     return {f"{prefix}_indptr": ip, f"{prefix}_indices": ix, f"{prefix}_data": d,
@@ -569,10 +618,10 @@ def eval_rhs(dom, mat, solver, vort0, rho, mu, dim, t):
     return rec
 
 
-def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True):
+def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True, umesh=None, extra=None):
     lower = [0.0] * dim
     upper = [1.0] * dim
-    dom = FakeDomain(dim, nelem, lower, upper, ngl, bc)
+    dom = FakeDomain(dim, nelem, lower, upper, ngl, bc) if umesh is None else FakeUDomain(umesh, bc)
     mat = MatNS() if ns else MatFS()
     mat.setDomain(dom)
     if not ops:
@@ -585,7 +634,10 @@ def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True):
     solver.setUp()
     out = {"dim": dim, "nelem": np.array(nelem), "ngl": ngl, "lower": np.array(lower),
            "upper": np.array(upper), "conn": dom.conn, "coords": dom.coords,
-           "loc2lat": dom.loc2lat, "corners": dom.corners, "rho": rho, "mu": mu}
+           "corners": dom.corners, "rho": rho, "mu": mu}
+    if umesh is None:
+        out["loc2lat"] = dom.loc2lat
+    out.update(extra or {})
     for m in ("K", "Krhs", "Rw"):
         out.update(csr_dict(m, getattr(mat, m)))
     if ns:
@@ -641,22 +693,45 @@ def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True):
     print(name, "n =", len(u), "nnz(K) =", len(out["K_data"]), "err =", out["err_l2"])
 
 
-def main():
-    table_fixtures()
-    element_fixtures()
+def main(only=()):
+    """Regenerate every fixture, or only the named cases (e.g. `gmsh2d`)."""
     uni = {"uniform": {"velocity": [4, 0]}}
     tg = {"custom-func": {"name": "taylor_green", "attributes": ["velocity", "vorticity", "alpha"]}}
     tg3 = {"custom-func": {"name": "taylor_green3d", "attributes": ["velocity", "vorticity", "alpha"]}}
-    # test_solver.py:7-25  (uniform, 3x3, ngl=3, rho=1, mu=0.01)
-    assembled_case("uniform2d", 2, [3, 3], 3, uni, 1.0, 0.01, None)
-    # test_solver.py:27-37 (Taylor-Green 2-D, 10x10, ngl=5)
-    assembled_case("tg2d", 2, [10, 10], 5, tg, 0.5, 0.01, tg2d, ops=False)
-    assembled_case("tg2d_small", 2, [4, 3], 4, tg, 0.5, 0.01, tg2d)
-    assembled_case("tg3d", 3, [2, 2, 2], 3, tg3, 0.5, 0.01, tg3d)
-    assembled_case("tg3d_p4", 3, [1, 1, 2], 5, tg3, 0.5, 0.01, tg3d, ops=False)
     cav = {"no-slip": {"up": [2, 0], "down": [0, 0], "left": [0, 0], "right": [0, 0]}}
-    assembled_case("cavity2d", 2, [4, 4], 3, cav, 0.5, 0.01, None, ns=True)
+
+    def unstructured():
+        um = O.UMesh.from_gmsh(os.path.join(OUT, "test.msh"), 3)
+        V, Cc, F, T = perturbed_box(3, [2, 2, 2], seed=11)
+        return um, O.UMesh(3, 3, V, Cc, F, T), {"mesh_vertices": V, "mesh_cells": Cc, "mesh_facets": F,
+                                                 "mesh_tags": T}
+
+    cases = {
+        "tables": table_fixtures,
+        "elements": element_fixtures,
+        # test_solver.py:7-25  (uniform, 3x3, ngl=3, rho=1, mu=0.01)
+        "uniform2d": lambda: assembled_case("uniform2d", 2, [3, 3], 3, uni, 1.0, 0.01, None),
+        # test_solver.py:27-37 (Taylor-Green 2-D, 10x10, ngl=5)
+        "tg2d": lambda: assembled_case("tg2d", 2, [10, 10], 5, tg, 0.5, 0.01, tg2d, ops=False),
+        "tg2d_small": lambda: assembled_case("tg2d_small", 2, [4, 3], 4, tg, 0.5, 0.01, tg2d),
+        "tg3d": lambda: assembled_case("tg3d", 3, [2, 2, 2], 3, tg3, 0.5, 0.01, tg3d),
+        "tg3d_p4": lambda: assembled_case("tg3d_p4", 3, [1, 1, 2], 5, tg3, 0.5, 0.01, tg3d, ops=False),
+        "cavity2d": lambda: assembled_case("cavity2d", 2, [4, 4], 3, cav, 0.5, 0.01, None, ns=True),
+        # unstructured (SURVEY 8(f) #4): the reference's Gmsh fixture
+        # src/tests/test.msh (copied to tests/golden/test.msh) and a rotated /
+        # shuffled / perturbed hex mesh
+        "gmsh2d": lambda: assembled_case("gmsh2d", 2, [0, 0], 3, tg, 0.5, 0.01, tg2d, umesh=unstructured()[0]),
+        "umesh3d": lambda: assembled_case("umesh3d", 3, [0, 0, 0], 3, tg3, 0.5, 0.01, tg3d,
+                                          umesh=unstructured()[1], extra=unstructured()[2]),
+        # no-slip on the unstructured quad mesh: the fixture's single physical
+        # group is the "down" wall (Face Sets value 1)
+        "gmsh2d_ns": lambda: assembled_case("gmsh2d_ns", 2, [0, 0], 3, {"no-slip": {"down": [1, 0]}}, 0.5, 0.01,
+                                            None, ns=True, umesh=unstructured()[0]),
+    }
+    for name, fn in cases.items():
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

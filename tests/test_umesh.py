@@ -1,0 +1,181 @@
+"""Unstructured mesh ingest: Gmsh 4.1 reader, entity numbering
+of the GLL nodes, Face Sets, slab partition -- host-only, no GPU.
+
+Pinned by the reference's own fixture and counts: src/tests/test.msh (copied
+as tests/golden/test.msh) has 33 cells and 153 nodes at ngl = 3, 1688 at
+ngl = 8 (test_domain.py:41-50,64-71).  Everything else is checked against
+the oracle's independent numbering (oracle.UMesh: nodes identified by
+coordinates, not by topology): the maps element -> node must agree up to a
+relabelling, bit-exact, on meshes whose cells are randomly rotated so shared
+edges/faces meet in every relative orientation.  The reference's PETSc
+section numbering itself is not reproducible without PETSc (parity
+unpinned for the labels; the connectivity is pinned)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pynama_amd._lib import Error
+from pynama_amd.mesh import FACES, UnstructuredMesh
+from pynama_amd.meshgen import perturbed_box, write_gmsh
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+MSH = os.path.join(G, "test.msh")
+
+
+@pytest.mark.parametrize("ngl,nodes", [(3, 153), (8, 1688), (2, 44)])
+def test_gmsh_fixture_counts(ngl, nodes):
+    m = UnstructuredMesh.from_gmsh(MSH, ngl)
+    assert m.kind == "unstructured" and m.dim == 2
+    assert m.E == 33 and m.N == nodes
+    assert m.node_range == (0, nodes) and m.ext_range == (0, nodes)
+
+
+def _check_against_oracle(m, u):
+    mp = O.node_map(m.coords(), u.coords())
+    np.testing.assert_array_equal(mp[m.conn()], u.conn())
+    for i, name in enumerate(FACES[m.dim]):
+        np.testing.assert_array_equal(np.sort(mp[m.face_nodes([name])]), u.face_nodes(1 << i))
+    np.testing.assert_allclose(m.corners(), u.corners(), rtol=0, atol=0)
+    return mp
+
+
+@pytest.mark.parametrize("ngl", [2, 3, 5])
+def test_gmsh_fixture_matches_oracle(ngl):
+    m = UnstructuredMesh.from_gmsh(MSH, ngl)
+    u = O.UMesh.from_gmsh(MSH, ngl)
+    _check_against_oracle(m, u)
+    # every boundary facet of the fixture is physical group 1 ("External"),
+    # i.e. Face Sets value 1 = the first name, "down" (dmplex.py:175-178)
+    assert len(m.face_nodes(["down"])) == 20 * (ngl - 1)
+    assert len(m.face_nodes(["up", "left", "right"])) == 0
+
+
+@pytest.mark.parametrize("dim,nelem,ngl,seed", [(2, [5, 4], 4, 1), (3, [3, 3, 2], 3, 2), (3, [3, 2, 2], 5, 3),
+                                                (3, [2, 2, 2], 7, 4)])
+def test_rotated_cells_match_oracle(dim, nelem, ngl, seed):
+    V, C, F, T = perturbed_box(dim, nelem, seed=seed)
+    m = UnstructuredMesh(dim, ngl, V, C, F, T)
+    u = O.UMesh(dim, ngl, V, C, F, T)
+    assert m.N == u.N == int(np.prod([n * (ngl - 1) + 1 for n in nelem]))
+    _check_against_oracle(m, u)
+
+
+def test_gmsh_writer_round_trip(tmp_path):
+    V, C, F, T = perturbed_box(3, [2, 3, 2], seed=5)
+    p = tmp_path / "box.msh"
+    write_gmsh(p, 3, V, C, F, T)
+    a = UnstructuredMesh.from_gmsh(p, 4)
+    b = UnstructuredMesh(3, 4, V, C, F, T)
+    np.testing.assert_array_equal(a.conn(), b.conn())
+    np.testing.assert_array_equal(a.coords(), b.coords())
+    # the oracle's reader sees the same file
+    dim, v2, c2, f2, t2 = O.read_gmsh(p)
+    np.testing.assert_array_equal(c2, C)
+    np.testing.assert_array_equal(t2, T)
+
+
+def test_inverted_cell_is_refused():
+    V, C, F, T = perturbed_box(2, [2, 2], seed=0, rotate=False, shuffle=False)
+    C = C.copy()
+    C[0] = C[0][::-1]  # clockwise quad
+    with pytest.raises(Error):
+        UnstructuredMesh(2, 3, V, C)
+
+
+def test_pattern_is_node_adjacency():
+    """a8 on an unstructured mesh: node rows hold every node sharing a cell."""
+    V, C, F, T = perturbed_box(3, [3, 2, 2], seed=6)
+    m = UnstructuredMesh(3, 3, V, C, F, T)
+    rp, cols = m.pattern(3)
+    conn = m.conn()
+    adj = [set() for _ in range(m.N)]
+    for e in conn:
+        s = set(e.tolist())
+        for n in e:
+            adj[n] |= s
+    for i in range(m.N):
+        assert cols[rp[i]:rp[i + 1]].tolist() == sorted(adj[i])
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_slab_partition(nranks):
+    """Owned ranges tile [0, N); each rank's cells are the cells touching its
+    nodes, with the 1-rank connectivity; ghosts are exactly the two
+    neighbours' interface segments ([lower | interior | upper] order), so
+    every column of a rank's rows lies in its ext range and only the first
+    send_lo / last send_hi owned rows are read by the neighbours."""
+    V, C, F, T = perturbed_box(3, [2, 3, 8], seed=7)
+    ngl = 4
+    one = UnstructuredMesh(3, ngl, V, C, F, T)
+    parts = [UnstructuredMesh(3, ngl, V, C, F, T, rank=r, nranks=nranks) for r in range(nranks)]
+    assert parts[0].node_range[0] == 0 and parts[-1].node_range[1] == one.N
+    for a, b in zip(parts, parts[1:]):
+        assert a.node_range[1] == b.node_range[0]
+    allx = np.concatenate([p.coords() for p in parts])
+    mp = O.node_map(allx, one.coords())   # global id (partitioned) -> 1-rank id
+    for r, p in enumerate(parts):
+        h = p.halo()
+        lo, hi = p.node_range
+        xb, xe = p.ext_range
+        assert xb == lo - h["lo_nodes"] and xe == hi + h["hi_nodes"]
+        if r > 0:
+            assert h["lo_nodes"] == parts[r - 1].halo()["send_hi_nodes"] and h["lo_rank"] == r - 1
+        if r < nranks - 1:
+            assert h["hi_nodes"] == parts[r + 1].halo()["send_lo_nodes"] and h["hi_rank"] == r + 1
+        ids = p.elements()
+        conn = p.conn()
+        np.testing.assert_array_equal(mp[conn], one.conn()[ids])
+        # local cells = cells with an owned node
+        owned = (conn >= lo) & (conn < hi)
+        assert owned.any(axis=1).all()
+        all_cells = one.conn()
+        touch = np.isin(all_cells, mp[lo:hi]).any(axis=1)
+        np.testing.assert_array_equal(np.nonzero(touch)[0], ids)
+        rp, cols = p.pattern(3)
+        assert cols.min() >= xb and cols.max() < xe
+        reads_lo = np.nonzero([(cols[rp[i]:rp[i + 1]] < lo).any() for i in range(hi - lo)])[0]
+        reads_hi = np.nonzero([(cols[rp[i]:rp[i + 1]] >= hi).any() for i in range(hi - lo)])[0]
+        if r > 0:
+            assert reads_lo.max() < h["send_lo_nodes"]
+        if r < nranks - 1:
+            assert reads_hi.min() >= (hi - lo) - h["send_hi_nodes"]
+        # and the lower ghosts are all read
+        if r > 0:
+            assert set(cols[cols < lo].tolist()) == set(range(xb, lo))
+
+
+def test_too_thin_slab_is_refused():
+    V, C, F, T = perturbed_box(3, [2, 2, 3], seed=8)
+    with pytest.raises(Error):
+        UnstructuredMesh(3, 3, V, C, F, T, rank=0, nranks=3)
+
+
+@pytest.mark.parametrize("case", ["gmsh2d", "umesh3d"])
+def test_oracle_umesh_assembly_matches_reference(case):
+    """Pin the oracle's unstructured assembly (used by the GPU tests on larger
+    meshes) to the reference's own MatFS / Operators output on the same mesh
+    (tests/golden/make_golden.py, FakeUDomain)."""
+    g = np.load(os.path.join(G, f"case_{case}.npz"))
+    dim = int(g["dim"])
+    if "mesh_cells" in g:
+        um = O.UMesh(dim, int(g["ngl"]), g["mesh_vertices"], g["mesh_cells"], g["mesh_facets"], g["mesh_tags"])
+    else:
+        um = O.UMesh.from_gmsh(MSH, int(g["ngl"]))
+    mp = O.node_map(um.coords(), g["coords"])
+    flag = ((um.tags_ & (1 << 2 * dim) - 1) != 0).astype(np.uint8)
+    K, Kr, Rw = um.assemble_fs(flag)
+    Cu, S, D, _ = um.assemble_ops()
+    dw, ds = (1, 3) if dim == 2 else (3, 6)
+    for nm, A, R, C in (("K", K, dim, dim), ("Krhs", Kr, dim, dim), ("Rw", Rw, dim, dw), ("Curl", Cu, dw, dim),
+                        ("SrT", S, ds, dim), ("DivSrT", D, dim, ds)):
+        rows = np.repeat(np.arange(A.m), np.diff(A.indptr))
+        shape = g[nm + "_shape"]
+        key = (mp[rows // R] * R + rows % R) * shape[1] + mp[A.indices // C] * C + A.indices % C
+        o = np.argsort(key)
+        ip = g[nm + "_indptr"]
+        rkey = np.repeat(np.arange(len(ip) - 1), np.diff(ip)) * shape[1] + g[nm + "_indices"]
+        np.testing.assert_array_equal(key[o], rkey, err_msg=nm)
+        ref = g[nm + "_data"]
+        assert np.abs(A.data[o] - ref).max() <= 1e-13 * np.abs(ref).max(), nm
