@@ -35,6 +35,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--nelem", type=str, default="20,16,16")
     ap.add_argument("--ngl", type=int, default=5)
+    ap.add_argument("--mesh", choices=["box", "unstructured"], default="box",
+                    help="box: structured box mesh (config 2/3); unstructured: the same box as a Gmsh file of "
+                         "perturbed, randomly rotated and shuffled hexes (config 5's irregular path)")
+    ap.add_argument("--msh", type=str, default=None, help="read this Gmsh 4.1 file instead (implies unstructured)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-solve", action="store_true")
@@ -135,6 +139,20 @@ def main():
     dim = len(nelem)
     cfg = {"domain": {"ngl": args.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * dim, "upper": [1.0] * dim}},
            "boundary-conditions": {"custom-func": {"name": "taylor_green3d" if dim == 3 else "taylor_green"}}}
+    mesh_kind = "box"
+    t_mesh = 0.0
+    if args.msh or args.mesh == "unstructured":
+        mesh_kind = "unstructured"
+        path = args.msh
+        if path is None:
+            import tempfile
+            from pynama_amd.meshgen import perturbed_box, write_gmsh
+            tg = time.perf_counter()
+            V, Cc, F, T = perturbed_box(dim, nelem, seed=5)
+            path = os.path.join(tempfile.mkdtemp(prefix="kle_bench_"), "mesh.msh")
+            write_gmsh(path, dim, V, Cc, F, T)
+            t_mesh = time.perf_counter() - tg
+        cfg["domain"] = {"ngl": args.ngl, "gmsh-file": path}
     t0 = time.perf_counter()
     dom = pa.Domain()
     dom.configure(cfg)
@@ -279,7 +297,8 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tr = json.load(open(args.traffic))
-            key = (f"{nelem}-{args.ngl}-{nranks}-" + ("chunk" if args.layout == 1 else f"pad{args.pad}") +
+            key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
+                   ("chunk" if args.layout == 1 else f"pad{args.pad}") +
                    f"-{args.loads}-u1" + ("-struct" if K.isStructured() else "") + ("-fused" if args.fused_dot else ""))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
@@ -307,16 +326,24 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (Taylor-Green-3D vorticity + Dirichlet velocity on a generated box mesh)",
-            "config": {"workload": f"KLE Laplacian {dim}-D box {nelem} ngl={args.ngl} (p={args.ngl - 1}), "
+            "data": ("synthetic (Taylor-Green-3D vorticity + Dirichlet velocity on a generated box mesh)"
+                     if mesh_kind == "box" else
+                     "synthetic (Taylor-Green-3D vorticity + Dirichlet velocity on a generated unstructured hex "
+                     "mesh: perturbed, rotated, shuffled cells read from Gmsh 4.1)"),
+            "config": {"workload": (f"KLE Laplacian {dim}-D box {nelem} ngl={args.ngl} (p={args.ngl - 1}), "
+                                    if mesh_kind == "box" else
+                                    f"KLE Laplacian {dim}-D unstructured hex mesh ({int(np.prod(nelem))} cells, "
+                                    f"{nelem} box topology) ngl={args.ngl} (p={args.ngl - 1}), ") +
                                    f"TG-{dim}D Dirichlet on all faces; one CG(+Jacobi) iteration per step",
+                       "mesh": mesh_kind,
                        "nelem": nelem, "ngl": args.ngl, "n_dof": n_global, "nnz_K": tot_nnz,
                        "ksp": ksp_type if ksp_type == "pipecg" else
                        ("cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)"),
                        "pc": "jacobi", "matrix_format": info["format"], "value_layout": "chunk16+tail" if args.layout == 1 else f"row streams padded to {args.pad}",
                        "structured_columns": K.isStructured(),
                        "spmv_loads": args.loads, "spmv_fused_dot": args.fused_dot,
-                       "parallelism": f"z-slab x{nranks} (RCCL halo + allreduce)"},
+                       "parallelism": (f"z-slab x{nranks} (RCCL halo + allreduce)" if mesh_kind == "box" else
+                                       f"cell slabs along the most-layered axis x{nranks} (RCCL halo + allreduce)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "kernel": (("k_nb_spmv_fast<3,3,%d,%s,1>" % (args.layout, "true" if K.isStructured() else "false"))
@@ -330,6 +357,7 @@ def main():
             "stream_copy_gbps": stream,
             "breakdown_ms_per_iter": brk,
             "assembly_s": t_asm,
+            "mesh_generation_s": t_mesh,
             "setup_s": t_setup,
             "solve": solve,
             "spmv_plain": spmv_plain,
