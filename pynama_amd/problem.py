@@ -6,8 +6,9 @@ chain: setUpDomain, readMaterialData, setUpSolver, setUpInitialConditions,
 evalRHS, computeVtensV, generateExactVecs, getKLEError, getConvective and
 getDiffusive.  Same names, arguments and in-place semantics; everything
 runs on the device through libkle (the KLE solve, the Curl / SrT / DivSrT
-SpMVs, the v v^T tensor and the BLAS-1 updates).  The viewer, the PETSc TS
-time integrator and the timers are not part of this path.
+SpMVs, the v v^T tensor and the BLAS-1 updates).  Output (Paraviewer,
+XDMF over HDF5, viewer.py) is written when the case names a "save-dir"; the
+reference always writes it (base_problem.py:40-43,65-70,93-101).
 """
 import numpy as np
 
@@ -40,9 +41,14 @@ class BaseProblem:
         self.ts.initSolver(self.evalRHS, self.convergedStepFunction)
 
     def convergedStepFunction(self, ts):
-        """Post-step hook (base_problem.py:93-101); the reference writes HDF5/XDMF
-        output here, which is outside this path: record the step instead."""
+        """Post-step hook (base_problem.py:93-101): velocity and vorticity of
+        the step to HDF5 + the case's XDMF (when a viewer is set up)."""
         self.lastStep = (ts.step_number, ts.time, ts.getTimeStep())
+        if getattr(self, "viewer", None) is not None:
+            vel = self.solverKLE.getSolution()
+            vort = ts.getSolution()
+            self.viewer.saveData(ts.step_number, ts.time, vel, vort)
+            self.viewer.writeXmf(self.caseName)
 
     def startSolver(self):
         """timeSolving (run_case.py:153-163): integrate the vorticity in place."""
@@ -50,6 +56,20 @@ class BaseProblem:
 
     def setUp(self):
         self.setUpDomain()
+        self.viewer = None
+        if self.config.get("save-dir"):
+            self.setUpViewer()
+            self.createMesh()
+
+    def setUpViewer(self):
+        from .viewer import Paraviewer
+        self.viewer = Paraviewer()
+
+    def createMesh(self, saveMesh=True):
+        """base_problem.py:65-70: configure the viewer, save the node coordinates."""
+        self.viewer.configure(self.dim, self.config.get("save-dir"))
+        if saveMesh:
+            self.viewer.saveMesh(self.dom.getFullCoordArray())
 
     def setUpDomain(self):
         self.dom = Domain()
