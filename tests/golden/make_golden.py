@@ -699,6 +699,8 @@ def main(only=()):
     tg = {"custom-func": {"name": "taylor_green", "attributes": ["velocity", "vorticity", "alpha"]}}
     tg3 = {"custom-func": {"name": "taylor_green3d", "attributes": ["velocity", "vorticity", "alpha"]}}
     cav = {"no-slip": {"up": [2, 0], "down": [0, 0], "left": [0, 0], "right": [0, 0]}}
+    NS3 = {"no-slip": {"up": [1, 0, 0.5], "down": [0, 0, 0], "left": [0, 0, 0], "right": [0, 0, 0],
+                       "front": [0, 0, 0], "back": [0, 0, 0]}}
 
     def unstructured():
         um = O.UMesh.from_gmsh(os.path.join(OUT, "test.msh"), 3)
@@ -727,6 +729,9 @@ def main(only=()):
         # group is the "down" wall (Face Sets value 1)
         "gmsh2d_ns": lambda: assembled_case("gmsh2d_ns", 2, [0, 0], 3, {"no-slip": {"down": [1, 0]}}, 0.5, 0.01,
                                             None, ns=True, umesh=unstructured()[0]),
+        # lid-driven cube on the rotated hex mesh (walls by Face Sets name)
+        "umesh3d_ns": lambda: assembled_case("umesh3d_ns", 3, [0, 0, 0], 3, NS3, 0.5, 0.01, None, ns=True,
+                                             umesh=unstructured()[1], extra=unstructured()[2]),
     }
     for name, fn in cases.items():
         if not only or name in only:

@@ -135,15 +135,29 @@ def test_umesh_solve_and_eval_rhs_match_golden(pa, case, tmp_path):
     assert np.abs(f.getArray() - rf).max() <= 1e-6 * max(1.0, np.abs(rf).max())
 
 
-def test_umesh_noslip_matches_golden(pa):
-    g = np.load(os.path.join(G, "case_gmsh2d_ns.npz"))
-    dom = _domain(pa, MSH, 3, {"no-slip": {"down": [1, 0]}})
-    mp = O.node_map(dom.getFullCoordArray().reshape(-1, 2), g["coords"])
+NS3 = {"up": [1, 0, 0.5], "down": [0, 0, 0], "left": [0, 0, 0], "right": [0, 0, 0], "front": [0, 0, 0],
+       "back": [0, 0, 0]}
+
+
+@pytest.mark.parametrize("case,walls", [("gmsh2d_ns", {"down": [1, 0]}), ("umesh3d_ns", NS3)])
+def test_umesh_noslip_matches_golden(pa, case, walls, tmp_path):
+    g = np.load(os.path.join(G, f"case_{case}.npz"))
+    dim = int(g["dim"])
+    dw = 1 if dim == 2 else 3
+    dom = _domain(pa, _msh(g, tmp_path), int(g["ngl"]), {"no-slip": walls})
+    mp = O.node_map(dom.getFullCoordArray().reshape(-1, dim), g["coords"])
+    # the DoF classes (incl. the corner rule) equal the reference's sets
+    inv = np.empty_like(mp)
+    inv[mp] = np.arange(len(mp))
+    for ours, ref in ((dom.getTangDofs(collect=True), g["tang_dofs"]),
+                      (dom.getNormalDofs(collect=True), g["normal_dofs"])):
+        o = np.array(sorted(ours), dtype=np.int64)
+        np.testing.assert_array_equal(np.sort(mp[o // dim] * dim + o % dim), ref)
     mat = pa.MatNS()
     mat.setDomain(dom)
     mat.build()
-    for name, R, C in (("K", 2, 2), ("Krhs", 2, 2), ("Rw", 2, 1), ("Rd", 2, 1), ("Kfs", 2, 2),
-                       ("Krhsfs", 2, 2), ("Rwfs", 2, 1), ("Rdfs", 2, 1)):
+    for name, R, C in (("K", dim, dim), ("Krhs", dim, dim), ("Rw", dim, dw), ("Rd", dim, 1), ("Kfs", dim, dim),
+                       ("Krhsfs", dim, dim), ("Rwfs", dim, dw), ("Rdfs", dim, 1)):
         _check(getattr(mat, name), g, name, mp, R, C)
     sol = pa.KleSolver()
     sol.setMat(mat)
@@ -151,15 +165,15 @@ def test_umesh_noslip_matches_golden(pa):
     sol.getKSP().setTolerances(rtol=1e-13)
     sol.solverFS.setTolerances(rtol=1e-13)
     vort = mat.Rw.createVecRight()
-    vort.setArray(_vec_to_ours(g["vort0"], mp, 1))
+    vort.setArray(_vec_to_ours(g["vort0"], mp, dw))
     vel = sol.getSolution()
-    vel.setArray(_vec_to_ours(g["vel0"], mp, 2))
+    vel.setArray(_vec_to_ours(g["vel0"], mp, dim))
     sol.solveFS(vort)
     vfs = sol.getFreeSlipSolution().getArray()
-    rfs = _vec_to_ours(g["velFS"], mp, 2)
+    rfs = _vec_to_ours(g["velFS"], mp, dim)
     assert np.linalg.norm(vfs - rfs) <= 1e-9 * np.linalg.norm(rfs)
     sol.solve(vort)
-    ru = _vec_to_ours(g["u"], mp, 2)
+    ru = _vec_to_ours(g["u"], mp, dim)
     assert np.linalg.norm(vel.getArray() - ru) <= 1e-9 * max(1.0, np.linalg.norm(ru))
 
 
