@@ -80,13 +80,19 @@ int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique
  * (e.g. gloo), so several ranks can share one GPU.  Production runs use RCCL.
  *   allreduce: in-place sum of n doubles over all ranks.
  *   halo: send n_send_lo doubles to lo_rank and n_send_hi to hi_rank, receive
- *         n_recv_lo from lo_rank and n_recv_hi from hi_rank (ranks < 0: none). */
+ *         n_recv_lo from lo_rank and n_recv_hi from hi_rank (ranks < 0: none).
+ *   exchange: general halo of graph-partitioned meshes: for peer k send
+ *         send_cnt[k] doubles (packed back to back in `send`, peer order) and
+ *         receive recv_cnt[k] (packed in `recv`); may be NULL when no mesh
+ *         with a graph partition is used. */
 typedef struct {
     int (*allreduce)(double *buf, int n, void *user);
     int (*halo)(const double *send_lo, int64_t n_send_lo, int lo_rank, const double *send_hi,
                 int64_t n_send_hi, int hi_rank, double *recv_lo, int64_t n_recv_lo,
                 double *recv_hi, int64_t n_recv_hi, void *user);
     void *user;
+    int (*exchange)(int npeers, const int *peers, const double *send, const int64_t *send_cnt,
+                    double *recv, const int64_t *recv_cnt, void *user);
 } kle_host_comm;
 int kle_ctx_create_host_comm(int device, int rank, int nranks, const kle_host_comm *comm,
                              kle_ctx **out);
@@ -117,15 +123,29 @@ int kle_mesh_destroy(kle_mesh *m);
  * bottom 0-3 then 4-7 above them), cell ids = row order (the ADD order);
  * facets: [nfacets][2^(dim-1)] boundary faces with their Face Sets value
  * (tag t >= 1 -> face bit t-1, the reference's name order: dmplex.py:27-30,
- * 175-178).  Ranks own slabs of cells along the longest axis; node ids are
- * global, each rank's owned range ordered [lower interface | interior | upper
- * interface] (see kle_umesh.cpp).  Fails with KLE_ERR_ARG for inverted cells
- * or slabs too thin for the two-neighbour halo. */
+ * 175-178).  Cells are partitioned by kle_set_partitioner's method; node ids
+ * are global, owned ranges contiguous per rank (see kle_umesh.cpp).  Fails
+ * with KLE_ERR_ARG for inverted cells, ranks without nodes, or slabs too thin
+ * for the two-neighbour halo. */
 int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double *vxyz, int64_t ncells,
                                  const int64_t *cells, int64_t nfacets, const int64_t *facets,
                                  const int *facet_tags, int rank, int nranks, kle_mesh **out);
 /* Gmsh MSH 4.1 ASCII file (GmshDom.create -> DMPlexCreateFromFile). */
 int kle_mesh_create_gmsh(const char *path, int ngl, int rank, int nranks, kle_mesh **out);
+/* Partitioner of the unstructured meshes created afterwards (the role of
+ * DMPlexDistribute's Chaco partitioner, dmplex.py:21): 0 (default) inertial
+ * recursive bisection of the cells -- general partitions, any number of
+ * neighbours per rank, index-list halos; 1 slabs along the longest axis
+ * (two-neighbour halo in contiguous ranges). */
+int kle_set_partitioner(int method);
+int kle_get_partitioner(void);
+/* Halo of a rank: npeers neighbours, per peer its rank, the ghost nodes
+ * received and the owned nodes sent; send_list (optional, sum of send_nodes
+ * entries) holds the owned-local node indices sent, peer by peer. */
+int kle_mesh_get_peers(const kle_mesh *m, int *npeers, int *ranks, int64_t *recv_nodes, int64_t *send_nodes,
+                       int64_t *send_list);
+/* Global node id of every ext (owned + ghost) node, in ext order. */
+int kle_mesh_get_ext_gids(const kle_mesh *m, int64_t *gids);
 /* Global cell ids of the local (owned + ghost) elements, ascending. */
 int kle_mesh_get_elements(const kle_mesh *m, int64_t *ids);
 

@@ -41,8 +41,12 @@ HALO_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.c_int, C.POIN
                       C.c_int, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_int64, C.c_void_p)
 
 
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                          C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_void_p)
+
+
 class HostComm(C.Structure):
-    _fields_ = [("allreduce", ALLREDUCE_FN), ("halo", HALO_FN), ("user", C.c_void_p)]
+    _fields_ = [("allreduce", ALLREDUCE_FN), ("halo", HALO_FN), ("user", C.c_void_p), ("exchange", EXCHANGE_FN)]
 
 
 _SIGS = {
@@ -63,6 +67,10 @@ _SIGS = {
                                      C.c_int, C.c_int, pvp],
     "kle_mesh_create_gmsh": [C.c_char_p, C.c_int, C.c_int, C.c_int, pvp],
     "kle_mesh_get_elements": [vp, i64p],
+    "kle_set_partitioner": [C.c_int],
+    "kle_get_partitioner": [],
+    "kle_mesh_get_peers": [vp, C.POINTER(C.c_int), vp, vp, vp, vp],
+    "kle_mesh_get_ext_gids": [vp, i64p],
     "kle_mesh_get_info": [vp, C.POINTER(MeshInfo)],
     "kle_mesh_get_conn": [vp, i64p],
     "kle_mesh_get_corners": [vp, f64p],

@@ -393,25 +393,35 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     // interior rows (no ghost column): [int_lo, int_hi) between the last row
     // reading a lower ghost and the first row reading an upper ghost
     const int64_t glo = m->node_begin - m->ext_begin;
-    std::vector<int64_t> t_lo(host_threads() + 1, -1), t_hi(host_threads() + 1, nrows);
+    // (slab layouts); graph partitions order the ghost-reading rows last, so
+    // there the range is [0, first row reading any ghost)
+    std::vector<int64_t> t_lo(host_threads() + 1, -1), t_hi(host_threads() + 1, nrows),
+        t_any(host_threads() + 1, nrows);
     std::atomic<int> slot{0};
     parallel_for(nrows, [&](int64_t lo, int64_t hi) {
         const int me = slot++;
-        int64_t last_lo = -1, first_hi = nrows;
+        int64_t last_lo = -1, first_hi = nrows, first_any = nrows;
         for (int64_t i = lo; i < hi; ++i)
             for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
                 const int64_t cl = cols[k] - m->ext_begin;
                 c32[rp32[i] + (k - rp[i])] = (int)cl;
                 if (cl < glo) last_lo = std::max(last_lo, i);
                 if (cl >= glo + nrows) first_hi = std::min(first_hi, i);
+                if (cl < glo || cl >= glo + nrows) first_any = std::min(first_any, i);
             }
         t_lo[me] = last_lo;
         t_hi[me] = first_hi;
+        t_any[me] = first_any;
     });
-    int64_t last_lo = -1, first_hi = nrows;
+    int64_t last_lo = -1, first_hi = nrows, first_any = nrows;
     for (size_t t = 0; t < t_lo.size(); ++t) {
         last_lo = std::max(last_lo, t_lo[t]);
         first_hi = std::min(first_hi, t_hi[t]);
+        first_any = std::min(first_any, t_any[t]);
+    }
+    if (first_hi - (last_lo + 1) < first_any) {
+        last_lo = -1;
+        first_hi = first_any;
     }
     // structured columns? each row's column list must be exactly a lattice box
     const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
@@ -484,6 +494,8 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->ghost_hi = (m->ext_end - m->node_end) * C;
     A->send_lo = m->send_lo_nodes * C;
     A->send_hi = m->send_hi_nodes * C;
+    A->plan = m->plan;
+    A->ext_gid = m->ext_gid;
     A->diag_only_row.assign(nrows, 0);
     if (which <= 1)
         for (int64_t i = 0; i < nrows; ++i) A->diag_only_row[i] = m->dir[m->node_begin + i - m->ext_begin];

@@ -300,11 +300,101 @@ int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all)
     return rc;
 }
 
-int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
-                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st)
+HaloPlan::~HaloPlan()
 {
-    if (ctx->nranks == 1 || (lo_rank < 0 && hi_rank < 0)) return 0;
+    if (d_send_idx) (void)hipFree(d_send_idx);
+    if (d_sbuf) (void)hipFree(d_sbuf);
+}
+
+// sbuf[k] = own[idx[k / bs] * bs + k % bs]: a graph-partition halo's sends
+__global__ void k_halo_pack(int64_t n, int bs, const int32_t *__restrict__ idx, const double *__restrict__ own,
+                            double *__restrict__ sbuf)
+{
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t node = idx[k / bs];
+        sbuf[k] = own[node * bs + k % bs];
+    }
+}
+
+// General halo (HaloPlan): pack the sends, then one grouped send/recv per
+// peer; receives land in the peer's ghost group of the ext layout.
+static int halo_exchange_plan(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local,
+                              const HaloPlan &P_, hipStream_t st)
+{
+    HaloPlan &P = const_cast<HaloPlan &>(P_);
+    if (P.peers.empty()) return 0;
+    if (P.n_owned <= 0 || n_local % P.n_owned)
+        return fail(KLE_ERR_STATE, "halo plan of %lld owned nodes does not fit a vector of %lld entries",
+                    (long long)P.n_owned, (long long)n_local);
+    const int bs = (int)(n_local / P.n_owned);
+    const int64_t ns = (int64_t)P.send_idx.size() * bs;
+    if (!P.d_send_idx && !P.send_idx.empty()) {
+        KLE_HIP(hipMalloc(&P.d_send_idx, sizeof(int32_t) * P.send_idx.size()));
+        KLE_HIP(hipMemcpy(P.d_send_idx, P.send_idx.data(), sizeof(int32_t) * P.send_idx.size(), hipMemcpyHostToDevice));
+    }
+    if (P.sbuf_cap < ns) {
+        KLE_HIP(hipStreamSynchronize(st));
+        if (P.d_sbuf) KLE_HIP(hipFree(P.d_sbuf));
+        P.d_sbuf = nullptr;
+        KLE_HIP(hipMalloc(&P.d_sbuf, sizeof(double) * ns));
+        P.sbuf_cap = ns;
+    }
+    const double *own = base + ghost_lo;
+    if (ns) {
+        const int g = (int)std::min<int64_t>((ns + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_halo_pack, dim3(g), dim3(256), 0, st, ns, bs, P.d_send_idx, own, P.d_sbuf);
+        KLE_HIP(hipGetLastError());
+    }
+    // ghost group of peer k starts at ext node recv_off[k] (relative to base)
+    const size_t np = P.peers.size();
+    if (ctx->comm) {
+        KLE_NCCL(ncclGroupStart());
+        for (size_t k = 0; k < np; ++k) {
+            if (P.send_cnt[k])
+                KLE_NCCL(ncclSend(P.d_sbuf + P.send_off[k] * bs, P.send_cnt[k] * bs, ncclDouble, P.peers[k], ctx->comm, st));
+            if (P.recv_cnt[k])
+                KLE_NCCL(ncclRecv(base + P.recv_off[k] * bs, P.recv_cnt[k] * bs, ncclDouble, P.peers[k], ctx->comm, st));
+        }
+        KLE_NCCL(ncclGroupEnd());
+        return 0;
+    }
+    if (!ctx->hcomm.exchange) return fail(KLE_ERR_COMM, "host transport has no exchange callback (graph-partitioned halo)");
+    int64_t nr = 0;
+    std::vector<int64_t> sc(np), rc(np);
+    for (size_t k = 0; k < np; ++k) {
+        sc[k] = P.send_cnt[k] * bs;
+        rc[k] = P.recv_cnt[k] * bs;
+        nr += rc[k];
+    }
+    KLE_TRY(stage_reserve(ctx, ns + nr));
+    double *hs = ctx->h_stage, *hr = hs + ns;
+    if (ns) KLE_HIP(hipMemcpyAsync(hs, P.d_sbuf, sizeof(double) * ns, hipMemcpyDeviceToHost, st));
+    KLE_HIP(hipStreamSynchronize(st));
+    if (ctx->hcomm.exchange((int)np, P.peers.data(), hs, sc.data(), hr, rc.data(), ctx->hcomm.user))
+        return fail(KLE_ERR_COMM, "host exchange callback failed");
+    int64_t z = 0;
+    for (size_t k = 0; k < np; ++k) {
+        if (rc[k]) KLE_HIP(hipMemcpyAsync(base + P.recv_off[k] * bs, hr + z, sizeof(double) * rc[k], hipMemcpyHostToDevice, st));
+        z += rc[k];
+    }
+    KLE_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
+                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st,
+                  const HaloPlan *plan)
+{
+    if (ctx->nranks == 1) return 0;
     if (!st) st = ctx->stream;
+    if (plan) {
+        std::pair<hipEvent_t, hipEvent_t> ev;
+        KLE_TRY(ctx->tic("halo", &ev, st));
+        KLE_TRY(halo_exchange_plan(ctx, base, ghost_lo, n_local, *plan, st));
+        KLE_TRY(ctx->toc("halo", &ev, st));
+        return 0;
+    }
+    if (lo_rank < 0 && hi_rank < 0) return 0;
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("halo", &ev, st));
     double *own = base + ghost_lo;
@@ -588,6 +678,7 @@ int kle_vec_create_mesh(kle_ctx *ctx, const kle_mesh *m, int bs, kle_vec **out)
     v->hi_rank = m->halo_hi_rank;
     v->send_lo = m->send_lo_nodes * bs;
     v->send_hi = m->send_hi_nodes * bs;
+    v->plan = m->plan;
     return 0;
 }
 
@@ -601,6 +692,7 @@ int kle_vec_duplicate(const kle_vec *v, kle_vec **out)
     w->hi_rank = v->hi_rank;
     w->send_lo = v->send_lo;
     w->send_hi = v->send_hi;
+    w->plan = v->plan;
     return 0;
 }
 
@@ -835,7 +927,7 @@ int kle_vec_ghost_update(kle_vec *v)
 {
     KLE_ARG(v, "null vec");
     return halo_exchange(v->ctx, v->base, v->ghost_lo, v->n_local, v->ghost_hi, v->lo_rank,
-                         v->hi_rank, v->send_lo, v->send_hi);
+                         v->hi_rank, v->send_lo, v->send_hi, nullptr, v->plan.get());
 }
 
 int kle_vec_device_ptr(const kle_vec *v, double **p)

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -51,6 +52,26 @@ constexpr int WAVE = 64;
 constexpr int RED_BLOCKS = 2048;   // max workgroups of the grid-stride vector kernels
 constexpr int PART_STRIDE = 1 << 18;  // partial slots per reduced quantity
 constexpr int NSCAL = 32;          // device scalar slots
+
+// General halo of a graph-partitioned mesh (kle_umesh.cpp, inertial
+// bisection).  The ext layout stays [ghosts of lower ranks | owned | ghosts
+// of higher ranks], each peer's ghosts one contiguous group in ascending
+// global id, so receives land in place; sends gather owned entries through
+// an index list (the peer's order).  Counts and offsets are in nodes; a
+// vector of block size bs moves bs entries per node.
+struct HaloPlan {
+    int64_t n_owned = 0;
+    std::vector<int> peers;                   // ascending rank
+    std::vector<int64_t> recv_off, recv_cnt;  // ghost group of peer k: ext nodes [recv_off, +recv_cnt)
+    std::vector<int64_t> send_off, send_cnt;  // peer k's slice of send_idx
+    std::vector<int32_t> send_idx;            // owned-local node index
+    int32_t *d_send_idx = nullptr;            // device copies (made on first use)
+    double *d_sbuf = nullptr;
+    int64_t sbuf_cap = 0;
+    std::vector<double> h_buf;                // host transport staging
+    ~HaloPlan();
+};
+using PlanPtr = std::shared_ptr<HaloPlan>;
 
 // Device scalar slots used by the Krylov kernels.
 enum Scal {
@@ -128,6 +149,14 @@ struct kle_mesh {
     std::vector<uint32_t> u_tags;   // [ext node] Face Sets bits (tag t -> bit t-1)
     std::vector<int64_t> u_incp;    // owned row i -> u_inc[u_incp[i] .. u_incp[i+1])
     std::vector<int32_t> u_inc;     // e * nn + l, ascending e
+    // graph partitions: u_conn and every ext-indexed array use pseudo ids
+    // ext_begin + (ext position); ext_gid maps a position to the global id
+    // (empty: pseudo id == global id, the slab layouts)
+    kle::PlanPtr plan;
+    std::vector<int64_t> ext_gid;
+    int64_t to_global(int64_t pseudo) const { return ext_gid.empty() ? pseudo : ext_gid[pseudo - ext_begin]; }
+    // global id -> pseudo id, -1 when the node is not in the ext range
+    int64_t to_pseudo(int64_t gid) const;
     int64_t n_local_elems() const { return kind ? (int64_t)u_elem.size() : elem_end - elem_begin; }
     int nn() const { return dim == 2 ? ngl * ngl : ngl * ngl * ngl; }
     void lattice_of(int64_t id, int64_t *c) const {
@@ -150,6 +179,7 @@ struct kle_vec {
     // halo plan (entries, not nodes)
     int lo_rank = -1, hi_rank = -1;
     int64_t send_lo = 0, send_hi = 0;
+    kle::PlanPtr plan;  // general halo (graph partitions); overrides lo/hi ranks
     bool owns = true;
 };
 
@@ -199,6 +229,8 @@ struct kle_mat {
     // halo plan of the column space
     int lo_rank = -1, hi_rank = -1;
     int64_t ghost_lo = 0, ghost_hi = 0, send_lo = 0, send_hi = 0;  // entries
+    kle::PlanPtr plan;                 // general halo of the column space
+    std::vector<int64_t> ext_gid;      // ext column -> global node (graph partitions)
     // ---- scalar AIJ (kind 1)
     int64_t nnz = 0;
     int64_t *d_aptr = nullptr;   // [m_local+1]
@@ -225,7 +257,8 @@ int vec_alloc(kle_ctx *ctx, int64_t n_local, int64_t n_global, int64_t lo, int64
 int allreduce_sum(kle_ctx *ctx, double *dbuf, int n, hipStream_t s = nullptr);  // in place, device buffer
 int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all);
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
-                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t s = nullptr);
+                  int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t s = nullptr,
+                  const HaloPlan *plan = nullptr);
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials,
          int *nparts, const int *istate);
 // true when spmv(A, x, ...) without a fused dot exchanges the halo on ctx->comm_stream
@@ -234,6 +267,7 @@ int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, do
 int grid_for(int64_t work, int per_block, int max_blocks);
 extern int g_nb_pad;
 extern int g_nb_layout;  // value layout of new node-block matrices (kle_mat.vlayout)
+extern int g_partitioner;  // unstructured meshes: 0 inertial bisection, 1 slabs (kle_umesh.cpp)
 // Offset of entry t (0 <= t < RC) of block k inside a row of m blocks
 // (mp = padded length for layout 0).  Layout 1: full 16-block chunks hold the
 // RC streams back to back (t-th 128-B line of chunk c), the m % 16 tail

@@ -480,6 +480,7 @@ static int make_vec_like_cols(kle_ksp *k, kle_vec **out)
     (*out)->hi_rank = A->hi_rank;
     (*out)->send_lo = A->send_lo;
     (*out)->send_hi = A->send_hi;
+    (*out)->plan = A->plan;
     return 0;
 }
 

@@ -560,7 +560,7 @@ static int nb_build_order(kle_mat *A)
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
     return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi && !A->spmv_order &&
-           !A->spmv_buf && !A->spmv_persistent && (x->lo_rank >= 0 || x->hi_rank >= 0);
+           !A->spmv_buf && !A->spmv_persistent && (x->lo_rank >= 0 || x->hi_rank >= 0 || (x->plan && !x->plan->peers.empty()));
 }
 
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials, int *nparts,
@@ -575,7 +575,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
         const bool overlap = !dot && spmv_uses_comm_stream(A, x);
         if (c->nranks > 1 && !overlap)
             KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
-                                  x->send_lo, x->send_hi));
+                                  x->send_lo, x->send_hi, nullptr, x->plan.get()));
         const int rpb = SPMV_WAVES * (64 / A->spmv_lpr);  // rows per workgroup
         int grid;
         if (A->spmv_persistent) {
@@ -648,7 +648,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
             if (pass == 1) {
                 // interior rows are queued; exchange the halo beside them
                 KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
-                                      x->send_lo, x->send_hi, c->comm_stream));
+                                      x->send_lo, x->send_hi, c->comm_stream, x->plan.get()));
                 KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
                 KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
                 rm = RowMap{0, A->int_lo, A->int_hi, A->nrows - A->int_hi};
@@ -1037,7 +1037,7 @@ int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *Rv)
             if (Rv->n_local != A->n_local || Rv->ghost_lo != A->ghost_lo || Rv->ghost_hi != A->ghost_hi)
                 return fail(KLE_ERR_SIZ, "right scaling vector must be a ghosted mesh vector of the column space");
             KLE_TRY(halo_exchange(c, Rv->base, Rv->ghost_lo, Rv->n_local, Rv->ghost_hi, Rv->lo_rank, Rv->hi_rank,
-                                  Rv->send_lo, Rv->send_hi));
+                                  Rv->send_lo, Rv->send_hi, nullptr, Rv->plan.get()));
             rx = Rv->base;
         }
         const int64_t th = A->nrows * 64;
@@ -1157,7 +1157,7 @@ int kle_mat_get_row(const kle_mat *A, int64_t row, int64_t *ncols, int64_t *cols
             for (int k = 0; k < cnt; ++k)
                 for (int b = 0; b < C; ++b) {
                     if (A->mask_rule != MASK_NONE && !nb_entry_exists(A, i, a, bc[k], b)) continue;
-                    c.push_back((A->ext_begin + bc[k]) * C + b);
+                    c.push_back((A->ext_gid.empty() ? A->ext_begin + bc[k] : A->ext_gid[bc[k]]) * C + b);
                     v.push_back(val_at(a * C + b, k));
                 }
         }
@@ -1195,7 +1195,7 @@ int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double 
                 for (int k = 0; k < m; ++k)
                     for (int b = 0; b < C; ++b) {
                         if (A->mask_rule != MASK_NONE && !nb_entry_exists(A, i, a, h.bc[b0 + k], b)) continue;
-                        indices[z] = (A->ext_begin + h.bc[b0 + k]) * C + b;
+                        indices[z] = (A->ext_gid.empty() ? A->ext_begin + h.bc[b0 + k] : A->ext_gid[h.bc[b0 + k]]) * C + b;
                         data[z++] = h.at(A, i, a * C + b, k);
                     }
             }

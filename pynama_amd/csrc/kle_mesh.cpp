@@ -138,6 +138,14 @@ int pattern_csr(const kle_mesh *m, int which, std::vector<int64_t> &rp, std::vec
 
 }  // namespace kle
 
+int64_t kle_mesh::to_pseudo(int64_t gid) const
+{
+    if (ext_gid.empty()) return gid >= ext_begin && gid < ext_end ? gid : -1;
+    // ext_gid ascends (ghost groups ordered by owner, owners number their nodes contiguously)
+    auto it = std::lower_bound(ext_gid.begin(), ext_gid.end(), gid);
+    return it != ext_gid.end() && *it == gid ? ext_begin + (it - ext_gid.begin()) : -1;
+}
+
 extern "C" {
 
 int kle_mesh_create_box(int dim, const int64_t nelem[3], const double lower[3], const double upper[3],
@@ -224,6 +232,58 @@ int kle_mesh_destroy(kle_mesh *m)
     return 0;
 }
 
+int kle_set_partitioner(int method)
+{
+    KLE_ARG(method == 0 || method == 1, "partitioner must be 0 (inertial) or 1 (slab), got %d", method);
+    g_partitioner = method;
+    return 0;
+}
+
+int kle_get_partitioner(void) { return g_partitioner; }
+
+int kle_mesh_get_peers(const kle_mesh *m, int *npeers, int *ranks, int64_t *recv_nodes, int64_t *send_nodes,
+                       int64_t *send_list)
+{
+    KLE_ARG(m && npeers, "null arg");
+    if (!m->plan) {
+        int k = 0;
+        for (int q : {m->halo_lo_rank, m->halo_hi_rank}) {
+            if (q < 0) continue;
+            if (ranks) ranks[k] = q;
+            const bool lo = q == m->halo_lo_rank;
+            if (recv_nodes) recv_nodes[k] = lo ? m->halo_lo_nodes : m->halo_hi_nodes;
+            if (send_nodes) send_nodes[k] = lo ? m->send_lo_nodes : m->send_hi_nodes;
+            ++k;
+        }
+        if (send_list) {  // contiguous ranges: lowest / highest owned nodes
+            int64_t z = 0;
+            const int64_t own = m->node_end - m->node_begin;
+            if (m->halo_lo_rank >= 0)
+                for (int64_t i = 0; i < m->send_lo_nodes; ++i) send_list[z++] = i;
+            if (m->halo_hi_rank >= 0)
+                for (int64_t i = own - m->send_hi_nodes; i < own; ++i) send_list[z++] = i;
+        }
+        *npeers = k;
+        return 0;
+    }
+    const HaloPlan &P = *m->plan;
+    *npeers = (int)P.peers.size();
+    for (size_t k = 0; k < P.peers.size(); ++k) {
+        if (ranks) ranks[k] = P.peers[k];
+        if (recv_nodes) recv_nodes[k] = P.recv_cnt[k];
+        if (send_nodes) send_nodes[k] = P.send_cnt[k];
+    }
+    if (send_list) std::copy(P.send_idx.begin(), P.send_idx.end(), send_list);
+    return 0;
+}
+
+int kle_mesh_get_ext_gids(const kle_mesh *m, int64_t *gids)
+{
+    KLE_ARG(m && gids, "null arg");
+    for (int64_t k = m->ext_begin; k < m->ext_end; ++k) gids[k - m->ext_begin] = m->to_global(k);
+    return 0;
+}
+
 int kle_mesh_get_info(const kle_mesh *m, kle_mesh_info *info)
 {
     KLE_ARG(m && info, "null arg");
@@ -263,7 +323,7 @@ int kle_mesh_get_conn(const kle_mesh *m, int64_t *conn)
 {
     KLE_ARG(m && conn, "null arg");
     if (m->kind == 1) {
-        std::copy(m->u_conn.begin(), m->u_conn.end(), conn);
+        for (size_t k = 0; k < m->u_conn.size(); ++k) conn[k] = m->to_global(m->u_conn[k]);
         return 0;
     }
     const int ngl = m->ngl, nn = m->nn(), p = m->p;
@@ -379,7 +439,8 @@ int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n)
     std::fill(m->dir.begin(), m->dir.end(), 0);
     for (int64_t k = 0; k < n; ++k) {
         if (nodes[k] < 0 || nodes[k] >= m->N) return fail(KLE_ERR_OUTOFRANGE, "node %lld", (long long)nodes[k]);
-        if (nodes[k] >= m->ext_begin && nodes[k] < m->ext_end) m->dir[nodes[k] - m->ext_begin] = 1;
+        const int64_t q = m->to_pseudo(nodes[k]);
+        if (q >= 0) m->dir[q - m->ext_begin] = 1;
     }
     m->dir_set = true;
     return 0;
@@ -388,17 +449,18 @@ int kle_mesh_set_dirichlet_nodes(kle_mesh *m, const int64_t *nodes, int64_t n)
 int kle_mesh_set_noslip_dofs(kle_mesh *m, const int64_t *tang, int64_t nt, const int64_t *normal, int64_t nnorm)
 {
     KLE_ARG(m && (nt == 0 || tang) && (nnorm == 0 || normal), "null arg");
-    const int64_t next = m->ext_end - m->ext_begin, d0 = m->ext_begin * m->dim, d1 = m->ext_end * m->dim;
+    const int64_t next = m->ext_end - m->ext_begin;
     m->dof_cls.assign(next * m->dim, DOF_FREE);
     std::fill(m->dir.begin(), m->dir.end(), 0);
     auto mark = [&](const int64_t *dofs, int64_t n, uint8_t c) -> int {
         for (int64_t k = 0; k < n; ++k) {
             if (dofs[k] < 0 || dofs[k] >= m->N * m->dim) return fail(KLE_ERR_OUTOFRANGE, "dof %lld", (long long)dofs[k]);
-            if (dofs[k] < d0 || dofs[k] >= d1) continue;
+            const int64_t q = m->to_pseudo(dofs[k] / m->dim);
+            if (q < 0) continue;
             // a DoF both normal and tangential is normal (mat_ns.py:60-62)
-            uint8_t &slot = m->dof_cls[dofs[k] - d0];
+            uint8_t &slot = m->dof_cls[(q - m->ext_begin) * m->dim + dofs[k] % m->dim];
             slot = std::max(slot, c);
-            m->dir[dofs[k] / m->dim - m->ext_begin] = 1;
+            m->dir[q - m->ext_begin] = 1;
         }
         return 0;
     };
@@ -462,7 +524,7 @@ int kle_mesh_pattern(const kle_mesh *m, int which, int64_t *row_ptr, int64_t *co
     row_ptr[0] = 0;
     for (int64_t i = m->node_begin; i < m->node_end; ++i) {
         row_cols(m, which, i, [&](int64_t j) {
-            if (cols) cols[k] = j;
+            if (cols) cols[k] = m->to_global(j);  // pseudo order == global order (kle_umesh.cpp)
             ++k;
         });
         row_ptr[i - m->node_begin + 1] = k;

@@ -27,15 +27,24 @@
 // interface segment, Morton order of the coordinates).  Parity tests compare
 // through node coordinates.
 //
-// Partition.  Cells are sorted by centroid along the axis with the most cell
-// layers (bounding-box extent / mean cell extent) and cut into nranks equal slabs (stand-in for the Chaco graph partition).
-// A node belongs to the highest rank among its cells (the box mesh's "upper
-// slab owns the interface" rule).  Inside a rank the owned nodes are ordered
-// [nodes the lower neighbour reads | interior | nodes the upper neighbour
-// reads], so the halo of an unstructured slab is again two contiguous ranges
-// and the box mesh's vector layout, halo exchange and interior/ghost row split
-// apply unchanged.  Slabs must be thick enough that no node touches cells of
-// ranks two apart (checked; the error names the remedy).
+// Partition (DMPlexDistribute with the Chaco partitioner, dmplex.py:21).
+// Default: inertial recursive bisection of the cells -- Chaco's "inertial"
+// method: split the cell centroids at the weighted median of their principal
+// axis of inertia, recursively, rank counts proportional to the halves.  A
+// node belongs to the highest rank among its cells.  Owned nodes are ordered
+// [interior | rows that read ghosts] (Morton inside each), so the SpMV's
+// ghost-free rows are one range that runs while the halo is in flight.  A
+// rank's ghosts are grouped by owner rank in ascending global id, lower ranks
+// before the owned range and higher ranks after it, so the vector layout
+// [ghost_lo | owned | ghost_hi] and in-place receives are unchanged; sends are
+// index lists (HaloPlan), any number of neighbours.  Ghost nodes get pseudo
+// ids ext_begin + (ext position) inside the mesh (ext_gid holds their global
+// ids), so every ext-indexed array and kernel works on either layout.
+// Alternative (kle_set_partitioner(1)): slabs -- cells sorted by centroid
+// along the axis with the most cell layers and cut into equal slabs, owned
+// nodes ordered [read by the lower neighbour | interior | read by the upper],
+// two contiguous halo ranges; slabs must be thick enough that no node touches
+// cells of ranks two apart (checked; the error names the remedy).
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -43,6 +52,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <numeric>
 #include <sstream>
 #include <unordered_map>
@@ -189,9 +199,91 @@ int number_entities(Build &B)
     return 0;
 }
 
+// principal axis (largest eigenvalue) of a symmetric dim x dim matrix, cyclic Jacobi
+void principal_axis(int dim, double A[3][3], double v[3])
+{
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0;
+        for (int i = 0; i < dim; ++i)
+            for (int j = i + 1; j < dim; ++j) off += A[i][j] * A[i][j];
+        if (off < 1e-30) break;
+        for (int pi = 0; pi < dim; ++pi)
+            for (int q = pi + 1; q < dim; ++q) {
+                if (std::fabs(A[pi][q]) < 1e-300) continue;
+                const double th = (A[q][q] - A[pi][pi]) / (2 * A[pi][q]);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
+                const double c = 1 / std::sqrt(t * t + 1), sn = t * c;
+                for (int k = 0; k < dim; ++k) {  // A <- A J
+                    const double a = A[k][pi], b = A[k][q];
+                    A[k][pi] = c * a - sn * b;
+                    A[k][q] = sn * a + c * b;
+                }
+                for (int k = 0; k < dim; ++k) {  // A <- J^T A
+                    const double a = A[pi][k], b = A[q][k];
+                    A[pi][k] = c * a - sn * b;
+                    A[q][k] = sn * a + c * b;
+                }
+                for (int k = 0; k < dim; ++k) {
+                    const double a = V[k][pi], b = V[k][q];
+                    V[k][pi] = c * a - sn * b;
+                    V[k][q] = sn * a + c * b;
+                }
+            }
+    }
+    int best = 0;
+    for (int i = 1; i < dim; ++i)
+        if (A[i][i] > A[best][best] * (1 + 1e-12)) best = i;
+    // sign convention: largest |component| positive (identical on every rank)
+    int big = 0;
+    for (int k = 1; k < dim; ++k)
+        if (std::fabs(V[k][best]) > std::fabs(V[big][best])) big = k;
+    const double sg = V[big][best] < 0 ? -1.0 : 1.0;
+    for (int k = 0; k < 3; ++k) v[k] = k < dim ? sg * V[k][best] : 0.0;
+}
+
+// Chaco-style inertial recursive bisection of the cells idx[lo, hi) into
+// ranks [r0, r0 + nr): split at the centroid count proportional to the rank
+// counts of the two halves along the principal axis of inertia.
+void inertial_bisect(int dim, const std::vector<double> &cen, std::vector<int64_t> &idx, int64_t lo, int64_t hi,
+                     int r0, int nr, std::vector<int> &crank)
+{
+    if (nr == 1) {
+        for (int64_t k = lo; k < hi; ++k) crank[idx[k]] = r0;
+        return;
+    }
+    const int64_t n = hi - lo;
+    double mu[3] = {0, 0, 0}, A[3][3] = {{0}};
+    for (int64_t k = lo; k < hi; ++k)
+        for (int d = 0; d < dim; ++d) mu[d] += cen[idx[k] * dim + d];
+    for (int d = 0; d < dim; ++d) mu[d] /= (double)n;
+    for (int64_t k = lo; k < hi; ++k) {
+        const double *c = &cen[idx[k] * dim];
+        for (int a = 0; a < dim; ++a)
+            for (int b = 0; b < dim; ++b) A[a][b] += (c[a] - mu[a]) * (c[b] - mu[b]);
+    }
+    double ax[3];
+    principal_axis(dim, A, ax);
+    std::vector<std::pair<double, int64_t>> key(n);
+    for (int64_t k = lo; k < hi; ++k) {
+        double s = 0;
+        for (int d = 0; d < dim; ++d) s += (cen[idx[k] * dim + d] - mu[d]) * ax[d];
+        // quantised so that round-off cannot reorder cells on a symmetric mesh
+        key[k - lo] = {std::nearbyint(s * 1e9) / 1e9, idx[k]};
+    }
+    std::sort(key.begin(), key.end());
+    for (int64_t k = 0; k < n; ++k) idx[lo + k] = key[k].second;
+    const int n1 = nr / 2;
+    const int64_t cut = lo + (n * n1 + nr / 2) / nr;
+    inertial_bisect(dim, cen, idx, lo, cut, r0, n1, crank);
+    inertial_bisect(dim, cen, idx, cut, hi, r0 + n1, nr - n1, crank);
+}
+
 }  // namespace
 
 namespace kle {
+
+int g_partitioner = 0;  // 0 inertial bisection, 1 slabs
 
 void umesh_row_nodes(const kle_mesh *m, int64_t i, std::vector<int64_t> &out)
 {
@@ -306,8 +398,9 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
             ax = d;
         }
     }
+    const bool slab = g_partitioner == 1;
     std::vector<int> crank(ncells, 0);
-    if (nranks > 1) {
+    if (nranks > 1 && slab) {
         std::vector<double> cen(ncells, 0.0);
         for (int64_t c = 0; c < ncells; ++c) {
             for (int t = 0; t < nc; ++t) cen[c] += corner(c, t, ax);
@@ -318,8 +411,18 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
         std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return cen[a] < cen[b]; });
         for (int r = 0; r < nranks; ++r)
             for (int64_t k = ncells * r / nranks; k < ncells * (r + 1) / nranks; ++k) crank[ord[k]] = r;
+    } else if (nranks > 1) {
+        std::vector<double> cen((size_t)ncells * dim, 0.0);
+        for (int64_t c = 0; c < ncells; ++c)
+            for (int d = 0; d < dim; ++d) {
+                for (int t = 0; t < nc; ++t) cen[c * dim + d] += corner(c, t, d);
+                cen[c * dim + d] /= nc;
+            }
+        std::vector<int64_t> idx(ncells);
+        std::iota(idx.begin(), idx.end(), 0);
+        inertial_bisect(dim, cen, idx, 0, ncells, 0, nranks, crank);
     }
-    // node owner = highest cell rank; span check
+    // node owner = highest cell rank
     std::vector<int> own(NT, -1), omin(NT, nranks);
     for (int64_t c = 0; c < ncells; ++c)
         for (int l = 0; l < nn; ++l) {
@@ -327,12 +430,13 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
             own[id] = std::max(own[id], crank[c]);
             omin[id] = std::min(omin[id], crank[c]);
         }
-    for (int64_t v = 0; v < NT; ++v)
-        if (used[v] && own[v] - omin[v] > 1)
-            return fail(KLE_ERR_ARG,
-                        "slab partition too thin: a node touches cells of ranks %d and %d (use fewer ranks)",
-                        omin[v], own[v]);
-    // interface segments: 0 read by the lower neighbour, 1 interior, 2 read by the upper
+    if (slab)
+        for (int64_t v = 0; v < NT; ++v)
+            if (used[v] && own[v] - omin[v] > 1)
+                return fail(KLE_ERR_ARG,
+                            "slab partition too thin: a node touches cells of ranks %d and %d (use fewer ranks)",
+                            omin[v], own[v]);
+    // owner range of every cell's nodes
     std::vector<int> emin(ncells, nranks), emax(ncells, -1);
     for (int64_t c = 0; c < ncells; ++c)
         for (int l = 0; l < nn; ++l) {
@@ -340,17 +444,25 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
             emin[c] = std::min(emin[c], o);
             emax[c] = std::max(emax[c], o);
         }
+    // segments.  slab: 0 read by the lower neighbour, 1 interior, 2 read by
+    // the upper.  inertial: 1 interior, 2 the row reads a ghost (a cell of the
+    // node holds a node of another owner)
     std::vector<uint8_t> seglo(NT, 0), seghi(NT, 0);
     for (int64_t c = 0; c < ncells; ++c)
         for (int l = 0; l < nn; ++l) {
             const int64_t id = B.tmp[c * nn + l];
-            if (emin[c] == own[id] - 1) seglo[id] = 1;
-            if (emax[c] == own[id] + 1) seghi[id] = 1;
+            if (slab) {
+                if (emin[c] == own[id] - 1) seglo[id] = 1;
+                if (emax[c] == own[id] + 1) seghi[id] = 1;
+            } else if (emin[c] != own[id] || emax[c] != own[id]) {
+                seghi[id] = 1;
+            }
         }
-    for (int64_t v = 0; v < NT; ++v)
-        if (used[v] && seglo[v] && seghi[v])
-            return fail(KLE_ERR_ARG, "slab partition too thin: rank %d has a node read by both neighbours "
-                                     "(use fewer ranks)", own[v]);
+    if (slab)
+        for (int64_t v = 0; v < NT; ++v)
+            if (used[v] && seglo[v] && seghi[v])
+                return fail(KLE_ERR_ARG, "slab partition too thin: rank %d has a node read by both neighbours "
+                                         "(use fewer ranks)", own[v]);
     // final numbering: (owner, segment, Morton(x), temp id)
     std::vector<int64_t> ord;
     ord.reserve(NT);
@@ -386,6 +498,97 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
     for (int r = 0; r < nranks; ++r)
         if (rbeg[r + 1] == rbeg[r]) return fail(KLE_ERR_ARG, "rank %d owns no node (use fewer ranks)", r);
 
+    // local cells: every cell with a node owned here, ascending id
+    std::vector<int64_t> lcells;
+    for (int64_t c = 0; c < ncells; ++c) {
+        if (emin[c] > rank || emax[c] < rank) continue;
+        bool mine = slab;
+        for (int l = 0; l < nn && !mine; ++l) mine = own[B.tmp[c * nn + l]] == rank;
+        if (mine) lcells.push_back(c);
+    }
+    // ext layout and pseudo ids (tmp id -> pseudo id, -1 outside the ext range)
+    std::vector<int64_t> loc(NT, -1), ext_gid;
+    int64_t ext_begin, ext_end;
+    kle::PlanPtr plan;
+    if (slab || nranks == 1) {
+        ext_begin = rbeg[rank] - (rank > 0 ? nhi[rank - 1] : 0);
+        ext_end = rbeg[rank + 1] + (rank < nranks - 1 ? nlo[rank + 1] : 0);
+        for (int64_t v : ord)
+            if (gid[v] >= ext_begin && gid[v] < ext_end) loc[v] = gid[v];
+    } else {
+        // ghosts: nodes of local cells owned elsewhere, ascending global id
+        // (= grouped by owner rank, since ids are numbered owner-major)
+        std::vector<int64_t> ghosts;
+        for (int64_t c : lcells)
+            for (int l = 0; l < nn; ++l) {
+                const int64_t v = B.tmp[c * nn + l];
+                if (own[v] != rank) ghosts.push_back(gid[v]);
+            }
+        std::sort(ghosts.begin(), ghosts.end());
+        ghosts.erase(std::unique(ghosts.begin(), ghosts.end()), ghosts.end());
+        const int64_t nglo = std::lower_bound(ghosts.begin(), ghosts.end(), rbeg[rank]) - ghosts.begin();
+        ext_begin = rbeg[rank] - nglo;
+        ext_end = rbeg[rank + 1] + ((int64_t)ghosts.size() - nglo);
+        ext_gid.resize(ext_end - ext_begin);
+        for (int64_t k = 0; k < nglo; ++k) ext_gid[k] = ghosts[k];
+        for (int64_t g = rbeg[rank]; g < rbeg[rank + 1]; ++g) ext_gid[nglo + g - rbeg[rank]] = g;
+        for (size_t k = nglo; k < ghosts.size(); ++k) ext_gid[nglo + (rbeg[rank + 1] - rbeg[rank]) + (k - nglo)] = ghosts[k];
+        for (int64_t k = 0; k < (int64_t)ext_gid.size(); ++k) loc[ord[ext_gid[k]]] = ext_begin + k;
+        // halo plan: receive each peer's ghost group in place; send the owned
+        // nodes that sit in the peer's local cells, ascending global id
+        plan = std::make_shared<kle::HaloPlan>();
+        plan->n_owned = rbeg[rank + 1] - rbeg[rank];
+        std::map<int, std::vector<int64_t>> sends;
+        std::vector<int> owners;
+        for (int64_t c = 0; c < ncells; ++c) {
+            if (emin[c] == emax[c] || emin[c] > rank || emax[c] < rank) continue;
+            owners.clear();
+            bool mine = false;
+            for (int l = 0; l < nn; ++l) {
+                const int o = own[B.tmp[c * nn + l]];
+                mine |= o == rank;
+                owners.push_back(o);
+            }
+            if (!mine) continue;
+            std::sort(owners.begin(), owners.end());
+            owners.erase(std::unique(owners.begin(), owners.end()), owners.end());
+            for (int q : owners) {
+                if (q == rank) continue;
+                auto &lst = sends[q];
+                for (int l = 0; l < nn; ++l) {
+                    const int64_t v = B.tmp[c * nn + l];
+                    if (own[v] == rank) lst.push_back(gid[v] - rbeg[rank]);
+                }
+            }
+        }
+        std::map<int, std::pair<int64_t, int64_t>> recvs;  // peer -> (ext offset, count)
+        for (int64_t k = 0; k < (int64_t)ext_gid.size(); ++k) {
+            const int64_t g = ext_gid[k];
+            if (g >= rbeg[rank] && g < rbeg[rank + 1]) continue;
+            const int q = (int)(std::upper_bound(rbeg.begin(), rbeg.end(), g) - rbeg.begin()) - 1;
+            auto it = recvs.find(q);
+            if (it == recvs.end()) recvs[q] = {k, 1};
+            else it->second.second++;
+        }
+        for (auto &kv : sends) {
+            auto &lst = kv.second;
+            std::sort(lst.begin(), lst.end());
+            lst.erase(std::unique(lst.begin(), lst.end()), lst.end());
+            if (!recvs.count(kv.first)) return fail(KLE_ERR_STATE, "halo plan: rank %d sends to %d but receives nothing", rank, kv.first);
+        }
+        for (auto &kv : recvs) {
+            const int q = kv.first;
+            auto it = sends.find(q);
+            if (it == sends.end()) return fail(KLE_ERR_STATE, "halo plan: rank %d receives from %d but sends nothing", rank, q);
+            plan->peers.push_back(q);
+            plan->recv_off.push_back(kv.second.first);
+            plan->recv_cnt.push_back(kv.second.second);
+            plan->send_off.push_back((int64_t)plan->send_idx.size());
+            plan->send_cnt.push_back((int64_t)it->second.size());
+            for (int64_t o : it->second) plan->send_idx.push_back((int32_t)o);
+        }
+    }
+
     kle_mesh *m = new kle_mesh;
     m->kind = 1;
     m->dim = dim;
@@ -403,24 +606,24 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
         m->upper[d] = d < dim ? hi[d] : 0.0;
     }
     m->xi = xi;
-    m->axis = ax;
+    m->axis = slab ? ax : -1;
     m->node_begin = rbeg[rank];
     m->node_end = rbeg[rank + 1];
-    m->ext_begin = m->node_begin - (rank > 0 ? nhi[rank - 1] : 0);
-    m->ext_end = m->node_end + (rank < nranks - 1 ? nlo[rank + 1] : 0);
-    if (rank > 0) {
+    m->ext_begin = ext_begin;
+    m->ext_end = ext_end;
+    m->plan = plan;
+    m->ext_gid = std::move(ext_gid);
+    if (slab && rank > 0) {
         m->halo_lo_rank = rank - 1;
         m->halo_lo_nodes = nhi[rank - 1];
         m->send_lo_nodes = nlo[rank];
     }
-    if (rank < nranks - 1) {
+    if (slab && rank < nranks - 1) {
         m->halo_hi_rank = rank + 1;
         m->halo_hi_nodes = nlo[rank + 1];
         m->send_hi_nodes = nhi[rank];
     }
-    // local cells: every cell with a node owned here, ascending id
-    for (int64_t c = 0; c < ncells; ++c)
-        if (emin[c] <= rank && rank <= emax[c]) m->u_elem.push_back(c);
+    m->u_elem = std::move(lcells);
     const int64_t nle = (int64_t)m->u_elem.size();
     m->elem_begin = 0;
     m->elem_end = nle;
@@ -431,10 +634,10 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
     for (int64_t e = 0; e < nle; ++e) {
         const int64_t c = m->u_elem[e];
         for (int l = 0; l < nn; ++l) {
-            const int64_t g = gid[B.tmp[c * nn + l]];
-            if (g < m->ext_begin || g >= m->ext_end) {
+            const int64_t g = loc[B.tmp[c * nn + l]];
+            if (g < 0) {
                 delete m;
-                return fail(KLE_ERR_STATE, "cell %lld node %lld outside the ext range", (long long)c, (long long)g);
+                return fail(KLE_ERR_STATE, "cell %lld node outside the ext range", (long long)c);
             }
             m->u_conn[e * nn + l] = g;
             if (g >= m->node_begin && g < m->node_end) m->u_incp[g - m->node_begin + 1]++;
@@ -455,8 +658,8 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
     }
     m->u_coords.resize((size_t)next * dim);
     for (int64_t v : ord) {
-        const int64_t g = gid[v];
-        if (g < m->ext_begin || g >= m->ext_end) continue;
+        const int64_t g = loc[v];
+        if (g < 0) continue;
         for (int d = 0; d < dim; ++d) m->u_coords[(g - m->ext_begin) * dim + d] = X[v * dim + d];
     }
     // Face Sets: a cell face (edge in 2-D) matching a tagged facet marks all its nodes
@@ -486,8 +689,8 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
                     for (int l = 0; l < nn; ++l) {
                         const int q = d == 0 ? l % ngl : d == 1 ? (l / ngl) % ngl : l / (ngl * ngl);
                         if (q != (side ? p : 0)) continue;
-                        const int64_t g = gid[B.tmp[c * nn + l]];
-                        if (g >= m->ext_begin && g < m->ext_end) m->u_tags[g - m->ext_begin] |= it->second;
+                        const int64_t g = loc[B.tmp[c * nn + l]];
+                        if (g >= 0) m->u_tags[g - m->ext_begin] |= it->second;
                     }
                 }
         }

@@ -90,7 +90,8 @@ class Domain:
                                 self.domData["ngl"], rank, size)
         elif "gmsh-file" in self.domData:
             self._type_mesh = "gmsh"
-            self.mesh = UnstructuredMesh.from_gmsh(self.domData["gmsh-file"], self.domData["ngl"], rank, size)
+            self.mesh = UnstructuredMesh.from_gmsh(self.domData["gmsh-file"], self.domData["ngl"], rank, size,
+                                                   partitioner=self.domData.get("partitioner", "inertial"))
         else:
             raise ValueError("Mesh Type not defined")
 

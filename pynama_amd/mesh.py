@@ -8,8 +8,10 @@ element layers along the slowest axis (z in 3-D, y in 2-D).
 
 UnstructuredMesh replaces GmshDom (dmplex.py:390-395) + DMPlexDistribute:
 quads / hexes from a Gmsh 4.1 file or from arrays; GLL nodes numbered by
-topological entity (kle_umesh.cpp), ranks own slabs of cells along the
-longest axis, each rank's nodes ordered [lower interface | interior | upper
+topological entity (kle_umesh.cpp).  Cells are partitioned by inertial
+recursive bisection (Chaco's inertial method; any number of neighbours per
+rank, index-list halos) or, with partitioner="slab", into slabs along the
+longest axis whose nodes are ordered [lower interface | interior | upper
 interface] so the halo keeps the box mesh's two-range form.  Boundary faces
 carry the Gmsh physical tag of their facet as the Face Sets value: tag t is
 face name FACES[dim][t-1] (dmplex.py:27-30,175-178).
@@ -18,7 +20,34 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import MeshInfo, call
+from ._lib import MeshInfo, call, load
+
+PARTITIONERS = {"inertial": 0, "chaco": 0, "slab": 1}
+
+
+def set_partitioner(name):
+    """Partitioner of unstructured meshes created afterwards
+    (PetscPartitioner type of DMPlexDistribute, dmplex.py:21)."""
+    call("kle_set_partitioner", PARTITIONERS[name] if isinstance(name, str) else int(name))
+
+
+def get_partitioner():
+    return {0: "inertial", 1: "slab"}[int(load().kle_get_partitioner())]
+
+
+class _partitioner:
+    """Use `name` for one mesh creation (None: the current setting)."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = get_partitioner()
+        if self.name is not None:
+            set_partitioner(self.name)
+
+    def __exit__(self, *exc):
+        set_partitioner(self.prev)
 
 # face names in the reference's order (dmplex.py:27-30): bit i of a face mask
 FACES = {2: ["down", "right", "up", "left"],
@@ -121,6 +150,30 @@ class _Mesh:
         return {"lo_nodes": lo.value, "hi_nodes": hi.value, "send_lo_nodes": sl.value,
                 "send_hi_nodes": sh.value, "lo_rank": lr.value, "hi_rank": hr.value}
 
+    def peers(self):
+        """Halo neighbours: {rank: (ghost nodes received, owned-local node ids sent)}."""
+        n = C.c_int()
+        call("kle_mesh_get_peers", self._h, C.byref(n), None, None, None, None)
+        k = n.value
+        ranks = np.zeros(max(k, 1), np.int32)
+        rn = np.zeros(max(k, 1), np.int64)
+        sn = np.zeros(max(k, 1), np.int64)
+        call("kle_mesh_get_peers", self._h, C.byref(n), ranks.ctypes.data, rn.ctypes.data, sn.ctypes.data, None)
+        sl = np.zeros(max(int(sn[:k].sum()), 1), np.int64)
+        call("kle_mesh_get_peers", self._h, C.byref(n), ranks.ctypes.data, rn.ctypes.data, sn.ctypes.data,
+             sl.ctypes.data)
+        out, o = {}, 0
+        for j in range(k):
+            out[int(ranks[j])] = (int(rn[j]), sl[o:o + sn[j]].copy())
+            o += int(sn[j])
+        return out
+
+    def ext_gids(self):
+        """Global node id of every owned + ghost node, in the vector layout's order."""
+        out = np.zeros(max(self.ext_range[1] - self.ext_range[0], 1), np.int64)
+        call("kle_mesh_get_ext_gids", self._h, out)
+        return out[: self.ext_range[1] - self.ext_range[0]]
+
 
 class BoxMesh(_Mesh):
     def __init__(self, dim, nelem, lower, upper, ngl, rank=0, nranks=1):
@@ -137,7 +190,8 @@ class UnstructuredMesh(_Mesh):
     """Quad / hex mesh: UnstructuredMesh.from_gmsh(path, ngl) (GmshDom.create)
     or UnstructuredMesh(dim, ngl, vertices, cells, facets, facet_tags)."""
 
-    def __init__(self, dim, ngl, vertices, cells, facets=None, facet_tags=None, rank=0, nranks=1, _handle=None):
+    def __init__(self, dim, ngl, vertices, cells, facets=None, facet_tags=None, rank=0, nranks=1, _handle=None,
+                 partitioner=None):
         if _handle is not None:
             self._load(_handle)
             return
@@ -150,14 +204,16 @@ class UnstructuredMesh(_Mesh):
         fa = np.ascontiguousarray(facets if nf else np.zeros((1, 2 ** (dim - 1))), dtype=np.int64)
         ft = np.ascontiguousarray(facet_tags if nf else np.zeros(1), dtype=np.int32)
         h = C.c_void_p()
-        call("kle_mesh_create_unstructured", dim, int(ngl), len(v), np.ascontiguousarray(v.ravel()), len(cells),
-             cells.ravel(), nf, fa.ctypes.data, ft.ctypes.data, int(rank), int(nranks), C.byref(h))
+        with _partitioner(partitioner):
+            call("kle_mesh_create_unstructured", dim, int(ngl), len(v), np.ascontiguousarray(v.ravel()), len(cells),
+                 cells.ravel(), nf, fa.ctypes.data, ft.ctypes.data, int(rank), int(nranks), C.byref(h))
         self._load(h)
 
     @classmethod
-    def from_gmsh(cls, path, ngl, rank=0, nranks=1):
+    def from_gmsh(cls, path, ngl, rank=0, nranks=1, partitioner=None):
         h = C.c_void_p()
-        call("kle_mesh_create_gmsh", str(path).encode(), int(ngl), int(rank), int(nranks), C.byref(h))
+        with _partitioner(partitioner):
+            call("kle_mesh_create_gmsh", str(path).encode(), int(ngl), int(rank), int(nranks), C.byref(h))
         return cls(None, None, None, None, _handle=h)
 
     def elements(self):

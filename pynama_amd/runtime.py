@@ -10,7 +10,7 @@ import ctypes as C
 import os
 import sys
 
-from ._lib import ALLREDUCE_FN, HALO_FN, HostComm, call, load
+from ._lib import ALLREDUCE_FN, EXCHANGE_FN, HALO_FN, HostComm, call, load
 
 
 def _dist():
@@ -124,8 +124,32 @@ class Context:
             except Exception:
                 return 1
 
-        self._cb = (ALLREDUCE_FN(allreduce), HALO_FN(halo))
-        return HostComm(self._cb[0], self._cb[1], None)
+        def exchange(npeers, peers, send, scnt, recv, rcnt, user):
+            # graph-partition halo: packed per-peer slices, peer order
+            try:
+                reqs, bufs, so, ro = [], [], 0, 0
+                for k in range(npeers):
+                    q, ns, nr = peers[k], scnt[k], rcnt[k]
+                    if ns:
+                        reqs.append(d.isend(torch.from_numpy(np.ctypeslib.as_array(send, (so + ns,))[so:].copy()), q))
+                    if nr:
+                        t = torch.zeros(nr, dtype=torch.float64)
+                        reqs.append(d.irecv(t, q))
+                        bufs.append((ro, nr, t))
+                    so += ns
+                    ro += nr
+                for r in reqs:
+                    r.wait()
+                if ro:
+                    out = np.ctypeslib.as_array(recv, (ro,))
+                    for o, n, t in bufs:
+                        out[o:o + n] = t.numpy()
+                return 0
+            except Exception:
+                return 1
+
+        self._cb = (ALLREDUCE_FN(allreduce), HALO_FN(halo), EXCHANGE_FN(exchange))
+        return HostComm(self._cb[0], self._cb[1], None, self._cb[2])
 
     def _bcast_unique_id(self):
         d = _dist()

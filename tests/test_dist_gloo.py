@@ -142,3 +142,114 @@ def test_distributed_cg_matches_serial(size, nelem, ngl):
     for rank, it, its, err in res:
         assert abs(it - its) <= 1, (rank, it, its)
         assert err < 1e-9, (rank, err)
+
+
+def _worker_graph(rank, size, port, nel, ngl, q):
+    """Same rehearsal on an unstructured mesh cut by inertial bisection: any
+    number of neighbours, ghosts grouped by owner, sends through index lists
+    (kle_mesh_get_peers) -- the plan libkle's general halo exchange uses."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    from oracle import oracle as O
+    from pynama_amd.mesh import UnstructuredMesh
+    from pynama_amd.meshgen import perturbed_box
+    V, Cc, F, T = perturbed_box(3, nel, seed=5)
+    m = UnstructuredMesh(3, ngl, V, Cc, F, T, rank=rank, nranks=size, partitioner="inertial")
+    um = O.UMesh(3, ngl, V, Cc, F, T)
+    flag = ((um.tags_ & 0x3f) != 0).astype(np.uint8)
+    K, Kr, Rw = um.assemble_fs(flag)
+    allc = [None] * size
+    dist.all_gather_object(allc, m.coords())
+    to_orc = O.node_map(np.concatenate(allc), um.coords())  # our global id -> oracle id
+    from_orc = np.argsort(to_orc)
+    bs = 3
+    lo, hi = m.node_range
+    g = m.ext_gids()
+    nown, glo = (hi - lo) * bs, (lo - m.ext_range[0]) * bs
+    ip, cols, vals = [0], [], []
+    for node in range(lo, hi):
+        for a in range(bs):
+            row = to_orc[node] * bs + a
+            c = K.indices[K.indptr[row]:K.indptr[row + 1]]
+            gn = from_orc[c // bs]
+            pos = np.searchsorted(g, gn)
+            assert (g[np.minimum(pos, len(g) - 1)] == gn).all(), "column outside the ext range"
+            cols.extend((pos * bs + c % bs).tolist())
+            vals.extend(K.data[K.indptr[row]:K.indptr[row + 1]].tolist())
+            ip.append(len(cols))
+    ip, cols, vals = np.array(ip), np.array(cols), np.array(vals)
+    rows_orc = (to_orc[lo:hi, None] * bs + np.arange(bs)).ravel()
+    diag = np.array([vals[ip[i]:ip[i + 1]][cols[ip[i]:ip[i + 1]] == glo + i][0] for i in range(nown)])
+    peers = m.peers()
+    owner = np.concatenate([[r] * len(c) for r, c in enumerate(allc)])
+
+    def halo(pext):
+        own = pext[glo:glo + nown].reshape(-1, bs)
+        reqs, bufs = [], []
+        for qr, (nrecv, sent) in sorted(peers.items()):
+            reqs.append(dist.isend(torch.from_numpy(own[sent].ravel().copy()), qr))
+            t = torch.zeros(nrecv * bs, dtype=torch.float64)
+            reqs.append(dist.irecv(t, qr))
+            first = int(np.nonzero(owner[g] == qr)[0][0])  # the peer's ghost group
+            bufs.append((first * bs, t))
+        for rq in reqs:
+            rq.wait()
+        for o, t in bufs:
+            pext[o:o + len(t)] = t.numpy()
+
+    def allsum(*v):
+        t = torch.tensor(v, dtype=torch.float64)
+        dist.all_reduce(t)
+        return t.numpy()
+
+    rng = np.random.default_rng(7)
+    b_glob = rng.uniform(-1, 1, K.m)
+    b = b_glob[rows_orc]
+    x, r = np.zeros(nown), b.copy()
+    z = r / diag
+    rz, rr = allsum(r @ z, r @ r)
+    tol = 1e-10 * np.sqrt(rr)
+    pext = np.zeros(len(g) * bs)
+    it = 0
+    while np.sqrt(rr) > tol and it < 5000:
+        pext[glo:glo + nown] = z + (0.0 if it == 0 else rz / rz_old) * pext[glo:glo + nown]
+        halo(pext)
+        w = np.array([vals[ip[i]:ip[i + 1]] @ pext[cols[ip[i]:ip[i + 1]]] for i in range(nown)])
+        (pw,) = allsum(pext[glo:glo + nown] @ w)
+        a = rz / pw
+        x += a * pext[glo:glo + nown]
+        r -= a * w
+        z = r / diag
+        rz_old = rz
+        rz, rr = allsum(r @ z, r @ r)
+        it += 1
+    xs, its, _ = K.cg(b_glob, rtol=1e-10, jacobi=True)
+    err = np.linalg.norm(x - xs[rows_orc]) / max(np.linalg.norm(xs[rows_orc]), 1e-300)
+    q.put((rank, it, its, err, len(peers)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,nel", [(2, [3, 3, 4]), (4, [4, 4, 3])])
+def test_graph_partition_cg_matches_serial(size, nel):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_graph, args=(r, size, port, nel, 3, q)) for r in range(size)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(size)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, it, its, err, npeers in res:
+        assert abs(it - its) <= 1, (rank, it, its)
+        assert err < 1e-9, (rank, err)
+    if size == 4:
+        assert max(r[4] for r in res) >= 3  # more than a slab chain's two neighbours

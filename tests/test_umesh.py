@@ -109,7 +109,7 @@ def test_slab_partition(nranks):
     V, C, F, T = perturbed_box(3, [2, 3, 8], seed=7)
     ngl = 4
     one = UnstructuredMesh(3, ngl, V, C, F, T)
-    parts = [UnstructuredMesh(3, ngl, V, C, F, T, rank=r, nranks=nranks) for r in range(nranks)]
+    parts = [UnstructuredMesh(3, ngl, V, C, F, T, rank=r, nranks=nranks, partitioner="slab") for r in range(nranks)]
     assert parts[0].node_range[0] == 0 and parts[-1].node_range[1] == one.N
     for a, b in zip(parts, parts[1:]):
         assert a.node_range[1] == b.node_range[0]
@@ -146,10 +146,67 @@ def test_slab_partition(nranks):
             assert set(cols[cols < lo].tolist()) == set(range(xb, lo))
 
 
+@pytest.mark.parametrize("nranks,nel", [(2, [3, 3, 4]), (3, [3, 4, 4]), (4, [4, 4, 4]), (8, [4, 4, 4])])
+def test_inertial_partition(nranks, nel):
+    """Graph partition (Chaco's inertial bisection, DMPlexDistribute
+    dmplex.py:21): owned ranges tile [0, N); local cells = cells touching an
+    owned node, with the 1-rank connectivity; ghosts = the other nodes of the
+    local cells, in ascending global id; every peer's send list is exactly
+    what the peer receives (same global ids, same order); rows that read a
+    ghost come after the interior rows."""
+    V, C, F, T = perturbed_box(3, nel, seed=11)
+    ngl = 3
+    one = UnstructuredMesh(3, ngl, V, C, F, T)
+    parts = [UnstructuredMesh(3, ngl, V, C, F, T, rank=r, nranks=nranks, partitioner="inertial")
+             for r in range(nranks)]
+    assert parts[0].node_range[0] == 0 and parts[-1].node_range[1] == one.N
+    for a, b in zip(parts, parts[1:]):
+        assert a.node_range[1] == b.node_range[0]
+    allx = np.concatenate([p.coords() for p in parts])
+    mp = O.node_map(allx, one.coords())
+    owner = np.repeat(np.arange(nranks), [p.n_owned for p in parts])
+    cells_seen = np.zeros(len(C), int)
+    max_peers = 0
+    for r, p in enumerate(parts):
+        lo, hi = p.node_range
+        ids = p.elements()
+        conn = p.conn()
+        np.testing.assert_array_equal(mp[conn], one.conn()[ids])
+        touch = np.isin(one.conn(), mp[lo:hi]).any(axis=1)
+        np.testing.assert_array_equal(np.nonzero(touch)[0], ids)
+        cells_seen[ids] += 1
+        g = p.ext_gids()
+        assert np.all(np.diff(g) > 0)
+        ghosts = np.setdiff1d(np.unique(conn), np.arange(lo, hi))
+        np.testing.assert_array_equal(np.setdiff1d(g, np.arange(lo, hi)), ghosts)
+        xb, xe = p.ext_range
+        assert xe - xb == len(g) and lo - xb == np.count_nonzero(g < lo)
+        peers = p.peers()
+        max_peers = max(max_peers, len(peers))
+        assert sorted(peers) == sorted(set(owner[ghosts].tolist()))
+        for q, (nrecv, sent) in peers.items():
+            qlo = parts[q].node_range[0]
+            got = ghosts[owner[ghosts] == q]
+            assert nrecv == len(got)
+            nq, sent_q = parts[q].peers()[r]
+            np.testing.assert_array_equal(qlo + sent_q, got)
+        # interior rows first: the rows reading a ghost are a suffix
+        rp, cols = p.pattern(3)
+        reads = np.array([((cols[rp[i]:rp[i + 1]] < lo) | (cols[rp[i]:rp[i + 1]] >= hi)).any()
+                          for i in range(hi - lo)])
+        if reads.any():
+            assert reads[np.argmax(reads):].all()
+        if nranks < 8:  # 2x2x2-cell parts at 8 ranks read ghosts in every row
+            assert (~reads).any()
+    assert (cells_seen >= 1).all()
+    if nranks == 8:
+        assert max_peers >= 4  # a genuinely irregular halo, not a slab chain
+
+
 def test_too_thin_slab_is_refused():
     V, C, F, T = perturbed_box(3, [2, 2, 3], seed=8)
     with pytest.raises(Error):
-        UnstructuredMesh(3, 3, V, C, F, T, rank=0, nranks=3)
+        UnstructuredMesh(3, 3, V, C, F, T, rank=0, nranks=3, partitioner="slab")
 
 
 @pytest.mark.parametrize("case", ["gmsh2d", "umesh3d"])
