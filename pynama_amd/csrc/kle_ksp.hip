@@ -13,6 +13,8 @@
 //     update and the r.z / r.r partials are one kernel;
 //   * deterministic two-stage reductions (per-workgroup partials, fixed-order
 //     final sum), RCCL allreduce of the 1-2 scalars across ranks.
+// PC lu (and KSP preonly) are a dense rocSOLVER factorization for the
+// small sequential systems the reference's own cases use (config 1).
 // GMRES(m) (classical Gram-Schmidt, right Jacobi preconditioning) is the
 // general fallback; its tiny Hessenberg least-squares update runs on the host.
 #include <algorithm>
@@ -21,6 +23,9 @@
 #include <string>
 
 #include "kle_internal.hpp"
+
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 namespace kle {
 
@@ -439,6 +444,10 @@ struct kle_ksp {
     double **d_Vptr = nullptr;
     double *d_h = nullptr;
     double *d_gpart = nullptr;  // GMRES dot partials [restart+2][RED_BLOCKS]
+    // PC lu: dense LU factors on the device (rocSOLVER getrf, column major)
+    double *d_lu = nullptr;
+    rocblas_int *d_ipiv = nullptr, *d_info = nullptr;
+    rocblas_handle blas = nullptr;
     bool setup = false;
     int its = 0, reason = 0;
     double rnorm = 0, true_rel = -1;
@@ -463,6 +472,13 @@ static void free_work(kle_ksp *k)
     hipFree(k->d_h);
     hipFree(k->d_gpart);
     k->d_gpart = nullptr;
+    hipFree(k->d_lu);
+    hipFree(k->d_ipiv);
+    hipFree(k->d_info);
+    k->d_lu = nullptr;
+    k->d_ipiv = k->d_info = nullptr;
+    if (k->blas) rocblas_destroy_handle(k->blas);
+    k->blas = nullptr;
     k->r = k->p = k->q = k->dinv = nullptr;
     k->d_Vptr = nullptr;
     k->d_h = nullptr;
@@ -895,6 +911,94 @@ static int solve_gmres(kle_ksp *k, kle_vec *b, kle_vec *x)
     return 0;
 }
 
+// ---------------------------------------------------------------- PC lu
+// The reference's solver is KSPPREONLY + PCLU (makefile:7; kle_solver.py:54-64
+// configures gmres + lu).  On the device: the operator densified column-major
+// and factored once by rocSOLVER (getrf, partial pivoting); every solve is one
+// getrs.  Sequential only -- like PETSc's own LU, which needs an external
+// package (MUMPS, SuperLU_dist) for a parallel matrix -- and dense, so sizes
+// stay below LU_MAX_N (config 1, unit tests); the large systems use CG.
+constexpr int64_t LU_MAX_N = 40000;
+
+__global__ void k_densify_nb(int64_t nrows, int R, int C, int lay, const int *__restrict__ rowptr,
+                             const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
+                             const int *__restrict__ bcol, const double *__restrict__ val, double *__restrict__ D,
+                             int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
+    const double *v = val + vptr[i];
+    for (int k = 0; k < m; ++k) {
+        const int64_t j = bcol[b0 + k];
+        for (int a = 0; a < R; ++a)
+            for (int b = 0; b < C; ++b) D[(j * C + b) * n + i * R + a] += v[vofs(lay, R * C, a * C + b, k, m, mp)];
+    }
+}
+
+__global__ void k_densify_aij(int64_t m, const int64_t *__restrict__ ptr, const int *__restrict__ col,
+                              const double *__restrict__ val, double *__restrict__ D, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) D[(int64_t)col[k] * n + i] += val[k];
+}
+
+static int lu_factor(kle_ksp *k)
+{
+    kle_ctx *c = k->ctx;
+    kle_mat *A = k->A;
+    if (c->nranks > 1)
+        return fail(KLE_ERR_SUP, "PC lu on %d ranks needs a parallel direct solver (PETSc: MUMPS / SuperLU_dist); "
+                                 "use -ksp_type cg -pc_type jacobi (K is SPD)", c->nranks);
+    const int64_t n = A->m_local;
+    if (n > LU_MAX_N)
+        return fail(KLE_ERR_SUP, "PC lu is a dense device factorization: n = %lld exceeds %lld; use -ksp_type cg "
+                                 "-pc_type jacobi (K is SPD)", (long long)n, (long long)LU_MAX_N);
+    KLE_HIP(hipMalloc(&k->d_lu, sizeof(double) * std::max<int64_t>(n * n, 1)));
+    KLE_HIP(hipMalloc(&k->d_ipiv, sizeof(rocblas_int) * std::max<int64_t>(n, 1)));
+    KLE_HIP(hipMalloc(&k->d_info, sizeof(rocblas_int)));
+    KLE_HIP(hipMemsetAsync(k->d_lu, 0, sizeof(double) * n * n, c->stream));
+    if (A->kind == 0) {
+        KLE_ARG(A->R == A->C, "PC lu needs square blocks");
+        hipLaunchKernelGGL(k_densify_nb, dim3((A->nrows + 127) / 128), dim3(128), 0, c->stream, A->nrows, A->R, A->C,
+                           A->vlayout, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->d_bcol, A->d_val, k->d_lu, n);
+    } else {
+        hipLaunchKernelGGL(k_densify_aij, dim3((A->m_local + 127) / 128), dim3(128), 0, c->stream, A->m_local,
+                           A->d_aptr, A->d_acol, A->d_aval, k->d_lu, n);
+    }
+    KLE_HIP(hipGetLastError());
+    if (rocblas_create_handle(&k->blas) != rocblas_status_success) return fail(KLE_ERR_DEVICE, "rocblas_create_handle failed");
+    rocblas_set_stream(k->blas, c->stream);
+    if (rocsolver_dgetrf(k->blas, (rocblas_int)n, (rocblas_int)n, k->d_lu, (rocblas_int)n, k->d_ipiv, k->d_info) !=
+        rocblas_status_success)
+        return fail(KLE_ERR_DEVICE, "rocsolver_dgetrf failed");
+    rocblas_int info = 0;
+    KLE_HIP(hipMemcpyAsync(&info, k->d_info, sizeof(info), hipMemcpyDeviceToHost, c->stream));
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    if (info > 0) return fail(71, "zero pivot in LU factorization: row %d", (int)info);  // PETSC_ERR_MAT_LU_ZRPVT
+    return 0;
+}
+
+// preonly / PC lu: one application of the preconditioner (x = M^-1 b)
+static int solve_direct(kle_ksp *k, kle_vec *b, kle_vec *x)
+{
+    kle_ctx *c = k->ctx;
+    const int64_t n = b->n_local;
+    KLE_HIP(hipMemcpyAsync(x->d, b->d, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+    if (k->pc == "lu") {
+        if (rocsolver_dgetrs(k->blas, rocblas_operation_none, (rocblas_int)n, 1, k->d_lu, (rocblas_int)n, k->d_ipiv,
+                             x->d, (rocblas_int)n) != rocblas_status_success)
+            return fail(KLE_ERR_DEVICE, "rocsolver_dgetrs failed");
+    } else if (k->pc == "jacobi") {
+        KLE_TRY(kle_vec_pointwise_mult(x, x, k->dinv));
+    }
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    k->its = 1;
+    k->reason = 4;  // KSP_CONVERGED_ITS
+    return 0;
+}
+
 extern "C" {
 
 int kle_ksp_create(kle_ctx *ctx, kle_ksp **out)
@@ -988,11 +1092,14 @@ int kle_ksp_set_up(kle_ksp *k)
 {
     KLE_ARG(k && k->A, "operators not set");
     if (k->setup) return 0;
-    if (k->pc == "lu" || k->type == "preonly")
-        return fail(KLE_ERR_SUP,
-                    "PC 'lu' / KSP 'preonly' (the reference's direct LU, makefile:7) has no device "
-                    "implementation; use -ksp_type cg -pc_type jacobi (K is SPD)");
     free_work(k);
+    if (k->pc == "lu") {
+        KLE_TRY(make_vec_like_cols(k, &k->p));
+        KLE_TRY(make_vec_like_cols(k, &k->q));
+        KLE_TRY(lu_factor(k));
+        k->setup = true;
+        return 0;
+    }
     KLE_TRY(make_vec_like_cols(k, &k->r));
     KLE_TRY(make_vec_like_cols(k, &k->p));
     KLE_TRY(make_vec_like_cols(k, &k->q));
@@ -1034,7 +1141,10 @@ int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(kle_ksp_set_up(k));
     KLE_ARG(b->n_local == k->A->m_local && x->n_local == k->A->n_local, "b/x sizes do not match the operator");
     k->true_rel = -1;
-    if (k->type == "pipecg") KLE_TRY(solve_pipecg(k, b, x));
+    // an exact preconditioner makes any Krylov method converge in one step:
+    // PC lu is applied directly whatever the KSP type (gmres + lu, kle_solver.py:57-61)
+    if (k->pc == "lu" || k->type == "preonly") KLE_TRY(solve_direct(k, b, x));
+    else if (k->type == "pipecg") KLE_TRY(solve_pipecg(k, b, x));
     else if (k->type == "cg" && k->single_reduction) KLE_TRY(solve_cg_single(k, b, x));
     else if (k->type == "cg") KLE_TRY(solve_cg(k, b, x));
     else KLE_TRY(solve_gmres(k, b, x));

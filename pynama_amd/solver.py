@@ -6,8 +6,11 @@ Dirichlet values, written beforehand by applyBoundaryConditions) and solves
 K vel = b in place.  The reference's KSP is gmres + PC lu, overridden to
 preonly + lu by the makefile (makefile:7); K is SPD, so the device default is
 CG + Jacobi at rtol 1e-10 (the north-star tolerance), overridable with the
-usual -ksp_type / -pc_type / -ksp_rtol / -ksp_max_it options.  PC 'lu' raises
-(no device direct solver): there is no silent CPU fallback.
+usual -ksp_type / -pc_type / -ksp_rtol / -ksp_max_it options.  The makefile's
+-ksp_type preonly -pc_type lu is a dense device LU (rocSOLVER getrf/getrs) for
+sequential systems up to 40k unknowns (config 1, the unit cases); beyond that,
+or on several ranks, it raises like PETSc without a parallel direct solver --
+there is no CPU fallback.
 """
 from .petsc import KSP, PC, Options
 

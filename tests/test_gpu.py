@@ -254,19 +254,98 @@ def test_vec_ops(pa):
     assert r.getArray().tolist() == [0.5, 0.0, 0.25]
 
 
-def test_lu_raises(pa):
-    g = _golden("uniform2d")
+@pytest.mark.parametrize("case", ["uniform2d", "tg2d"])
+def test_preonly_lu_matches_golden(pa, case):
+    """The makefile's -ksp_type preonly -pc_type lu (makefile:7): a dense device
+    LU (rocSOLVER).  The golden u is the reference's KleSolver.solve with a
+    direct solve standing in for PETSc's LU, so both sides are direct solves:
+    agreement to roundoff, and the reference's known answers
+    (test_solver.py:25,37)."""
+    g = _golden(case)
     dom = _domain(pa, g)
     mat = pa.MatFS()
     mat.setDomain(dom)
     mat.build()
+    opts = pa.petsc.Options()
+    opts.update({"ksp_type": "preonly", "pc_type": "lu"})
+    try:
+        sol = pa.KleSolver()
+        sol.setMat(mat)
+        sol.setUp()
+    finally:
+        opts.pop("ksp_type")
+        opts.pop("pc_type")
+    ksp = sol.getKSP()
+    vort = mat.Rw.createVecRight()
+    vort.setArray(g["vort0"])
+    vel = sol.getSolution()
+    vel.setArray(g["vel0"])
+    sol.solve(vort)
+    u = vel.getArray()
+    assert ksp.getIterationNumber() == 1 and ksp.getConvergedReason() == 4  # KSP_CONVERGED_ITS
+    assert ksp.getTrueRelativeResidual() < 1e-13
+    assert np.linalg.norm(u - g["u"]) <= 1e-12 * np.linalg.norm(g["u"])
+    if case == "uniform2d":
+        assert np.linalg.norm(u - g["u_exact"]) < 1e-12
+    if case == "tg2d":
+        assert np.linalg.norm(u - g["u_exact"]) < 1e-5
+
+
+def test_gmres_lu_is_one_step_and_preonly_jacobi(pa):
+    """KspSolver.createSolver's own gmres + PC lu (kle_solver.py:54-64) takes
+    one step; preonly + jacobi applies D^-1 once, like PETSc."""
+    g = _golden("tg2d_small")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    b = mat.K.createVecLeft()
+    rng = np.random.default_rng(3)
+    b.setArray(rng.uniform(-1, 1, b.getLocalSize()))
     ksp = pa.petsc.KSP().create()
-    pc = pa.petsc.PC()
+    ksp.setType("gmres")
+    pc = pa.petsc.PC().create()
     pc.setType("lu")
     ksp.setPC(pc)
     ksp.setOperators(mat.K)
-    with pytest.raises(pa.Error):
+    ksp.setUp()
+    x = mat.K.createVecRight()
+    ksp.solve(b, x)
+    K = O.CSR.from_arrays(*mat.K.getValuesCSR(), mat.K.getSize()[1])
+    assert ksp.getIterationNumber() == 1
+    assert np.linalg.norm(K.mult(x.getArray()) - b.getArray()) <= 1e-13 * np.linalg.norm(b.getArray())
+    ksp2 = pa.petsc.KSP().create()
+    ksp2.setType("preonly")
+    pc2 = pa.petsc.PC().create()
+    pc2.setType("jacobi")
+    ksp2.setPC(pc2)
+    ksp2.setOperators(mat.K)
+    ksp2.setUp()
+    ksp2.solve(b, x)
+    ip, ix, dv = mat.K.getValuesCSR()
+    d = np.array([dv[ip[i]:ip[i + 1]][ix[ip[i]:ip[i + 1]] == i][0] for i in range(len(ip) - 1)])
+    np.testing.assert_allclose(x.getArray(), b.getArray() / d, rtol=1e-15)
+
+
+def test_lu_too_large_raises(pa):
+    """Dense device LU is for small sequential systems; beyond that PC lu
+    raises (PETSc error 56) -- no CPU fallback."""
+    cfg = {"domain": {"ngl": 5, "box-mesh": {"nelem": [8, 8, 8], "lower": [0, 0, 0], "upper": [1, 1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    ksp = pa.petsc.KSP().create()
+    pc = pa.petsc.PC().create()
+    pc.setType("lu")
+    ksp.setPC(pc)
+    ksp.setOperators(mat.K)
+    with pytest.raises(pa.Error) as e:
         ksp.setUp()
+    assert e.value.ierr == 56
 
 
 def test_larger_mesh_properties(pa):
