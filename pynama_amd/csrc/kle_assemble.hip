@@ -23,6 +23,8 @@
 //                mat_fs.py:158-189.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <thread>
 #include <cstdlib>
 #include <cmath>
@@ -157,6 +159,50 @@ __device__ __forceinline__ void fill_chunk(int ngl, int ne, int nq, const Tables
     }
 }
 
+// K_e, Rw_e (and Rd_e) blocks of node pair (l, m) from the factored sums
+// (G, E_d, D_ab, F_d of k_element's header comment)
+template <int DIM>
+__device__ __forceinline__ void store_elem_blocks(int64_t e, int l, int m, int ne, double G, const double (&E)[DIM],
+                                                  const double (&D)[DIM][DIM], const double (&F)[DIM],
+                                                  double *__restrict__ Ke, double *__restrict__ Rwe,
+                                                  double *__restrict__ Rde)
+{
+    constexpr int DW = DIM == 2 ? 1 : 3;
+    double tr = 0;
+    for (int c = 0; c < DIM; ++c) tr += D[c][c];
+    double *kb = Ke + ((e * ne + l) * (int64_t)ne + m) * (DIM * DIM);
+    for (int a = 0; a < DIM; ++a)
+        for (int b = 0; b < DIM; ++b) {
+            double val = ALPHA_D * D[a][b] - ALPHA_W * D[b][a];
+            if (a == b) val += G + ALPHA_W * tr;
+            kb[a * DIM + b] = val;
+        }
+    double rw[DIM][DW] = {};
+    if constexpr (DIM == 3) {
+        // (row, col, derivative) of B_curl / Bw_curl, sign (-1)^t
+        // (indCurl == indWCurl, spectral.py:31-32)
+        const int ind[6][3] = {{0, 2, 1}, {0, 1, 2}, {1, 0, 2}, {1, 2, 0}, {2, 1, 0}, {2, 0, 1}};
+        for (int t = 0; t < 6; ++t) {
+            const double sg = (t & 1) ? -1.0 : 1.0;
+            const int r0 = ind[t][0], r1 = ind[t][1], d = ind[t][2];
+            rw[r0][r1] += sg * E[d];             // H^T Bw_curl  (full)
+            rw[r1][r0] += ALPHA_W * sg * F[d];   // a_w B_curl^T H (reduced)
+        }
+    } else {
+        // indWCurl 2-D [[0,0,1],[1,0,0]] ; indCurl 2-D [[0,1,0],[0,0,1]]
+        rw[0][0] += E[1] - ALPHA_W * F[1];
+        rw[1][0] += -E[0] + ALPHA_W * F[0];
+    }
+    double *rb = Rwe + ((e * ne + l) * (int64_t)ne + m) * (DIM * DW);
+    for (int a = 0; a < DIM; ++a)
+        for (int c = 0; c < DW; ++c) rb[a * DW + c] = rw[a][c];
+    if (Rde) {
+        // Rd_e = -H^T B_div (full) + a_d B_div^T H (reduced)   (spectral.py:136-137,157)
+        double *db = Rde + ((e * ne + l) * (int64_t)ne + m) * DIM;
+        for (int a = 0; a < DIM; ++a) db[a] = -E[a] + ALPHA_D * F[a];
+    }
+}
+
 template <int DIM>
 __global__ __launch_bounds__(256) void k_element(int ngl, Tables1D TF, Tables1D TR,
                                                  const double *__restrict__ geoF,
@@ -244,40 +290,136 @@ __global__ __launch_bounds__(256) void k_element(int ngl, Tables1D TF, Tables1D 
             const int l = l0 + tx + 16 * u, m = m0 + ty + 16 * v;
             if (l >= ne || m >= ne) continue;
             const int pv = u * 2 + v;
-            double tr = 0;
-            for (int c = 0; c < DIM; ++c) tr += D[c][c][pv];
-            double *kb = Ke + ((e * ne + l) * (int64_t)ne + m) * (DIM * DIM);
-            for (int a = 0; a < DIM; ++a)
-                for (int b = 0; b < DIM; ++b) {
-                    double val = ALPHA_D * D[a][b][pv] - ALPHA_W * D[b][a][pv];
-                    if (a == b) val += G[pv] + ALPHA_W * tr;
-                    kb[a * DIM + b] = val;
-                }
-            double rw[DIM][DW] = {};
-            if constexpr (DIM == 3) {
-                // (row, col, derivative) of B_curl / Bw_curl, sign (-1)^t
-                // (indCurl == indWCurl, spectral.py:31-32)
-                const int ind[6][3] = {{0, 2, 1}, {0, 1, 2}, {1, 0, 2}, {1, 2, 0}, {2, 1, 0}, {2, 0, 1}};
-                for (int t = 0; t < 6; ++t) {
-                    const double s = (t & 1) ? -1.0 : 1.0;
-                    const int r0 = ind[t][0], r1 = ind[t][1], d = ind[t][2];
-                    rw[r0][r1] += s * E[d][pv];             // H^T Bw_curl  (full)
-                    rw[r1][r0] += ALPHA_W * s * F[d][pv];   // a_w B_curl^T H (reduced)
-                }
-            } else {
-                // indWCurl 2-D [[0,0,1],[1,0,0]] ; indCurl 2-D [[0,1,0],[0,0,1]]
-                rw[0][0] += E[1][pv] - ALPHA_W * F[1][pv];
-                rw[1][0] += -E[0][pv] + ALPHA_W * F[0][pv];
+            double d[DIM][DIM], ev[DIM], fv[DIM];
+            for (int a = 0; a < DIM; ++a) {
+                ev[a] = E[a][pv];
+                fv[a] = F[a][pv];
+                for (int b = 0; b < DIM; ++b) d[a][b] = D[a][b][pv];
             }
-            double *rb = Rwe + ((e * ne + l) * (int64_t)ne + m) * (DIM * DW);
-            for (int a = 0; a < DIM; ++a)
-                for (int c = 0; c < DW; ++c) rb[a * DW + c] = rw[a][c];
-            if (Rde) {
-                // Rd_e = -H^T B_div (full) + a_d B_div^T H (reduced)   (spectral.py:136-137,157)
-                double *db = Rde + ((e * ne + l) * (int64_t)ne + m) * DIM;
-                for (int a = 0; a < DIM; ++a) db[a] = -E[a][pv] + ALPHA_D * F[a][pv];
-            }
+            store_elem_blocks<DIM>(e, l, m, ne, G[pv], ev, d, fv, Ke, Rwe, Rde);
         }
+}
+
+// MFMA form of k_element (the default): the Gauss-point sums are GEMMs,
+//   G    = (c grad N_L)^T (grad N_M)   (K = DIM * nq_full)
+//   E_d  = (c N_L)^T (dN_M/dx_d)       (K = nq_full)
+//   D_ab = (c dN_L/dx_a)^T (dN_M/dx_b) (K = nq_red)
+//   F_d  = (c dN_L/dx_d)^T N_M         (K = nq_red)
+// run on v_mfma_f64_16x16x4_f64: each of the 4 waves owns a 16x16 (l, m)
+// sub-tile of the workgroup's 32x32 tile and keeps all 1 + DIM + DIM^2 + DIM
+// accumulators (double4 each) in registers; the A (l side, scaled by c_q) and
+// B (m side) operands come from the same LDS chunks as k_element, four Gauss
+// points per instruction (lane: A[l = lane&15][q = lane>>4], B[q = lane>>4][m
+// = lane&15]; result reg r at l = (lane>>4) + 4r, m = lane&15).
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ dbl4 mfma64(double a, double b, dbl4 c)
+{
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tables1D TR,
+                                                      const double *__restrict__ geoF,
+                                                      const double *__restrict__ geoR,
+                                                      double *__restrict__ Ke, double *__restrict__ Rwe,
+                                                      double *__restrict__ Rde)
+{
+    constexpr int G1 = 1 + DIM * DIM;
+    const int ne = DIM == 2 ? ngl * ngl : ngl * ngl * ngl;
+    const int nqF = DIM == 2 ? TF.np1 * TF.np1 : TF.np1 * TF.np1 * TF.np1;
+    const int nqR = DIM == 2 ? TR.np1 * TR.np1 : TR.np1 * TR.np1 * TR.np1;
+    const int64_t e = blockIdx.z;
+    const int l0 = blockIdx.x * TL, m0 = blockIdx.y * TL;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ls = (wv & 1) * 16, ms = (wv >> 1) * 16;  // this wave's 16x16 sub-tile
+    const int li = lane & 15, kq = lane >> 4;
+
+    __shared__ double sHL[QC][TL], sHM[QC][TL];
+    __shared__ double sGL[QC][DIM][TL], sGM[QC][DIM][TL];
+    __shared__ double sgeo[QC][G1];
+
+    const dbl4 z4 = {0.0, 0.0, 0.0, 0.0};
+    dbl4 G = z4, E[DIM], D[DIM][DIM], F[DIM];
+#pragma unroll
+    for (int a = 0; a < DIM; ++a) {
+        E[a] = z4;
+        F[a] = z4;
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) D[a][b] = z4;
+    }
+
+    // full integration: G and E (the chunk beyond nq is zero-filled)
+    for (int q0 = 0; q0 < nqF; q0 += QC) {
+        for (int it = tid; it < QC * G1; it += 256) {
+            int qq = it / G1, k = it % G1;
+            sgeo[qq][k] = (q0 + qq < nqF) ? geoF[(e * nqF + q0 + qq) * G1 + k] : 0.0;
+        }
+        __syncthreads();
+        fill_chunk<DIM>(ngl, ne, nqF, TF, geoF, q0, l0, true, sHL, sGL, sgeo, tid);
+        fill_chunk<DIM>(ngl, ne, nqF, TF, geoF, q0, m0, false, sHM, sGM, sgeo, tid);
+        __syncthreads();
+        const int qn = min(QC, nqF - q0);
+        for (int qq = 0; qq < qn; qq += 4) {
+            const int q = qq + kq;
+            const double ah = sHL[q][ls + li];
+            double ag[DIM], bg[DIM];
+#pragma unroll
+            for (int i = 0; i < DIM; ++i) {
+                ag[i] = sGL[q][i][ls + li];
+                bg[i] = sGM[q][i][ms + li];
+            }
+#pragma unroll
+            for (int i = 0; i < DIM; ++i) G = mfma64(ag[i], bg[i], G);
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) E[d] = mfma64(ah, bg[d], E[d]);
+        }
+        __syncthreads();
+    }
+    // reduced integration: D and F
+    for (int q0 = 0; q0 < nqR; q0 += QC) {
+        for (int it = tid; it < QC * G1; it += 256) {
+            int qq = it / G1, k = it % G1;
+            sgeo[qq][k] = (q0 + qq < nqR) ? geoR[(e * nqR + q0 + qq) * G1 + k] : 0.0;
+        }
+        __syncthreads();
+        fill_chunk<DIM>(ngl, ne, nqR, TR, geoR, q0, l0, true, sHL, sGL, sgeo, tid);
+        fill_chunk<DIM>(ngl, ne, nqR, TR, geoR, q0, m0, false, sHM, sGM, sgeo, tid);
+        __syncthreads();
+        const int qn = min(QC, nqR - q0);
+        for (int qq = 0; qq < qn; qq += 4) {
+            const int q = qq + kq;
+            const double bh = sHM[q][ms + li];
+            double ag[DIM], bg[DIM];
+#pragma unroll
+            for (int i = 0; i < DIM; ++i) {
+                ag[i] = sGL[q][i][ls + li];
+                bg[i] = sGM[q][i][ms + li];
+            }
+#pragma unroll
+            for (int a = 0; a < DIM; ++a)
+#pragma unroll
+                for (int b = 0; b < DIM; ++b) D[a][b] = mfma64(ag[a], bg[b], D[a][b]);
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) F[d] = mfma64(ag[d], bh, F[d]);
+        }
+        __syncthreads();
+    }
+    const int m = m0 + ms + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int l = l0 + ls + kq + 4 * r;
+        if (l >= ne || m >= ne) continue;
+        double d[DIM][DIM], ev[DIM], fv[DIM];
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) {
+            ev[a] = E[a][r];
+            fv[a] = F[a][r];
+#pragma unroll
+            for (int b = 0; b < DIM; ++b) d[a][b] = D[a][b][r];
+        }
+        store_elem_blocks<DIM>(e, l, m, ne, G[r], ev, d, fv, Ke, Rwe, Rde);
+    }
 }
 
 // ---------------------------------------------------------------- gather
@@ -370,54 +512,303 @@ static MeshDev mesh_dev(const kle_mesh *m)
     return M;
 }
 
+// KLE_TIMING=1: stream-synchronised wall time of each setup phase on stderr
+struct PhaseTimer {
+    kle_ctx *c;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseTimer(kle_ctx *ctx) : c(ctx)
+    {
+        const char *e = getenv("KLE_TIMING");
+        on = e && atoi(e) != 0;
+        t = std::chrono::steady_clock::now();
+    }
+    void lap(const char *what)
+    {
+        if (!on) return;
+        (void)hipStreamSynchronize(c->stream);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[kle timing r%d] %-34s %9.2f ms\n", c->rank, what,
+                std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
+// ------------------------------------------------------ device patterns
+// Box meshes: the symbolic pattern `which` (kle_mesh.cpp row_cols: the
+// preallocation of mat_fs.py:21-94 / mat_ns.py:7-45) built on the device, one
+// wavefront per owned node row.  The lanes walk the row's neighbour box
+// (nodes sharing a cell) in ascending node id, the Dirichlet filter of
+// `which` is a ballot, and the kept columns are compacted with a popcount
+// prefix -> the same ascending column list as the host enumeration, bit for
+// bit, without materialising O(nnz) host arrays.
+struct PatRowInfo {
+    int cnt;   // kept columns
+    int cmin;  // first / last kept column (ext-relative), INT_MAX / -1 when empty
+    int cmax;
+    int box0;  // structured-column box: base column, nx | ny<<8 | nz<<16 (-1: not a box)
+    int box1;
+};
+
+__device__ __forceinline__ bool pat_keep(int which, bool di, bool dj)
+{
+    switch (which) {
+    case 0: return !dj;
+    case 1: return dj;
+    case 4: return di || dj;
+    case 5: return dj;
+    default: return true;  // 2, 3, 6
+    }
+}
+
+// neighbour box of node row gi (kle_mesh.cpp nbr_range); returns false for the
+// rows whose pattern is not a box walk (Dirichlet rows of K/Krhs/Rw, free rows of Rwfs)
+__device__ __forceinline__ bool pat_row_box(const MeshDev &M, int which, int64_t gi, bool di, int64_t lo[3],
+                                            int64_t n[3], int &special)
+{
+    special = -1;
+    if (which == 6 && !di) {
+        special = 0;
+        return false;
+    }
+    if (which <= 2 && di) {
+        special = which != 2 ? 1 : 0;
+        return false;
+    }
+    const int64_t c[3] = {gi % M.L[0], (gi / M.L[0]) % M.L[1], M.dim == 3 ? gi / (M.L[0] * M.L[1]) : 0};
+    for (int d = 0; d < 3; ++d) {
+        int64_t a = 0, b = 0;
+        if (d < M.dim) {
+            if (c[d] % M.p == 0) {
+                a = max((int64_t)0, c[d] - M.p);
+                b = min(M.L[d] - 1, c[d] + M.p);
+            } else {
+                a = (c[d] / M.p) * M.p;
+                b = a + M.p;
+            }
+        }
+        lo[d] = a;
+        n[d] = b - a + 1;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_pat_count(MeshDev M, int64_t nrows, int which,
+                                                   const uint8_t *__restrict__ dir, PatRowInfo *__restrict__ info)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (row >= nrows) return;
+    const int64_t gi = M.node_begin + row;
+    const bool di = dir[gi - M.ext_begin] != 0;
+    int64_t lo[3], n[3];
+    int special;
+    PatRowInfo r{0, 0x7fffffff, -1, 0, 0};
+    if (!pat_row_box(M, which, gi, di, lo, n, special)) {
+        if (special == 1) {
+            const int c = (int)(gi - M.ext_begin);
+            r = PatRowInfo{1, c, c, c, 1 | (1 << 8) | (1 << 16)};
+        }
+        if (lane == 0) info[row] = r;
+        return;
+    }
+    const int64_t vol = n[0] * n[1] * n[2], Lxy = M.L[0] * M.L[1];
+    int cnt = 0;
+    int64_t mn[3] = {INT64_MAX, INT64_MAX, INT64_MAX}, mx[3] = {-1, -1, -1};
+    int64_t first = INT64_MAX, last = -1;
+    for (int64_t k0 = 0; k0 < vol; k0 += 64) {
+        const int64_t k = k0 + lane;
+        bool keep = false;
+        int64_t q[3] = {0, 0, 0}, j = 0;
+        if (k < vol) {
+            q[0] = lo[0] + k % n[0];
+            q[1] = lo[1] + (k / n[0]) % n[1];
+            q[2] = lo[2] + k / (n[0] * n[1]);
+            j = q[0] + M.L[0] * q[1] + Lxy * q[2];
+            keep = pat_keep(which, di, dir[j - M.ext_begin] != 0);
+        }
+        cnt += __popcll(__ballot(keep));
+        if (keep) {
+            for (int d = 0; d < 3; ++d) {
+                mn[d] = min(mn[d], q[d]);
+                mx[d] = max(mx[d], q[d]);
+            }
+            first = min(first, j);
+            last = max(last, j);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int d = 0; d < 3; ++d) {
+            mn[d] = min(mn[d], (int64_t)__shfl_xor(mn[d], o, 64));
+            mx[d] = max(mx[d], (int64_t)__shfl_xor(mx[d], o, 64));
+        }
+        first = min(first, (int64_t)__shfl_xor(first, o, 64));
+        last = max(last, (int64_t)__shfl_xor(last, o, 64));
+    }
+    if (lane) return;
+    r.cnt = cnt;
+    if (cnt) {
+        r.cmin = (int)(first - M.ext_begin);
+        r.cmax = (int)(last - M.ext_begin);
+        const int64_t bx = mx[0] - mn[0] + 1, by = mx[1] - mn[1] + 1, bz = mx[2] - mn[2] + 1;
+        if (bx * by * bz == cnt && bx <= 255 && by <= 255 && bz <= 255) {
+            r.box0 = (int)(mn[0] + M.L[0] * mn[1] + Lxy * mn[2] - M.ext_begin);
+            r.box1 = (int)(bx | (by << 8) | (bz << 16));
+        } else {
+            r.box0 = 0;
+            r.box1 = -1;
+        }
+    }
+    info[row] = r;
+}
+
+__global__ __launch_bounds__(256) void k_pat_fill(MeshDev M, int64_t nrows, int which,
+                                                  const uint8_t *__restrict__ dir, const int *__restrict__ rowptr,
+                                                  int *__restrict__ bcol)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (row >= nrows) return;
+    const int64_t gi = M.node_begin + row;
+    const bool di = dir[gi - M.ext_begin] != 0;
+    int64_t lo[3], n[3];
+    int special;
+    int *out = bcol + rowptr[row];
+    if (!pat_row_box(M, which, gi, di, lo, n, special)) {
+        if (special == 1 && lane == 0) out[0] = (int)(gi - M.ext_begin);
+        return;
+    }
+    const int64_t vol = n[0] * n[1] * n[2], Lxy = M.L[0] * M.L[1];
+    const uint64_t below = (1ull << lane) - 1ull;
+    int pos = 0;
+    for (int64_t k0 = 0; k0 < vol; k0 += 64) {
+        const int64_t k = k0 + lane;
+        bool keep = false;
+        int64_t j = 0;
+        if (k < vol) {
+            j = lo[0] + k % n[0] + M.L[0] * (lo[1] + (k / n[0]) % n[1]) + Lxy * (lo[2] + k / (n[0] * n[1]));
+            keep = pat_keep(which, di, dir[j - M.ext_begin] != 0);
+        }
+        const uint64_t bal = __ballot(keep);
+        if (keep) out[pos + __popcll(bal & below)] = (int)(j - M.ext_begin);
+        pos += __popcll(bal);
+    }
+}
+
+// Per-row pattern summary of `which` on the device (box meshes); dd = device
+// copy of m->dir.
+static int pattern_rows_dev(kle_ctx *ctx, const kle_mesh *m, int which, const uint8_t *dd,
+                            std::vector<PatRowInfo> &info)
+{
+    const int64_t nrows = m->node_end - m->node_begin;
+    info.resize(std::max<int64_t>(nrows, 1));
+    if (nrows == 0) return 0;
+    PatRowInfo *di = nullptr;
+    KLE_HIP(hipMalloc(&di, sizeof(PatRowInfo) * nrows));
+    hipLaunchKernelGGL(k_pat_count, dim3((unsigned)((nrows * 64 + 255) / 256)), dim3(256), 0, ctx->stream,
+                       mesh_dev(m), nrows, which, dd, di);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(info.data(), di, sizeof(PatRowInfo) * nrows, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    hipFree(di);
+    if (e != hipSuccess) return fail(KLE_ERR_DEVICE, "device pattern count failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+// Host-built pattern (unstructured meshes, and box meshes under KLE_HOST_PATTERN=1):
+// the same per-row summary plus the explicit column lists.
+static int pattern_rows_host(const kle_mesh *m, int which, std::vector<PatRowInfo> &info,
+                             std::vector<int64_t> &rp, std::vector<int64_t> &cols)
+{
+    const int64_t nrows = m->node_end - m->node_begin;
+    KLE_TRY(pattern_csr(m, which, rp, cols));
+    info.resize(std::max<int64_t>(nrows, 1));
+    const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
+    parallel_for(nrows, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) {
+            const int64_t b = rp[i], e = rp[i + 1];
+            PatRowInfo r{(int)(e - b), 0x7fffffff, -1, 0, 0};
+            if (e > b) {
+                const int64_t c0 = cols[b] - m->ext_begin, c1 = cols[e - 1] - m->ext_begin;
+                r.cmin = (int)c0;
+                r.cmax = (int)c1;
+                r.box1 = -1;
+                if (m->kind != 0) {  // unstructured: no lattice (and L may be 0)
+                    info[i] = r;
+                    continue;
+                }
+                // structured columns: the list must be exactly a lattice box
+                const int64_t nx = c1 % Lx - c0 % Lx + 1, ny = (c1 / Lx) % m->L[1] - (c0 / Lx) % m->L[1] + 1,
+                              nz = c1 / Lxy - c0 / Lxy + 1;
+                bool ok = nx >= 1 && ny >= 1 && nz >= 1 && nx <= 255 && ny <= 255 && nz <= 255 &&
+                          nx * ny * nz == e - b;
+                int64_t k = b;
+                for (int64_t z = 0; ok && z < nz; ++z)
+                    for (int64_t y = 0; ok && y < ny; ++y)
+                        for (int64_t x = 0; ok && x < nx; ++x, ++k)
+                            ok = cols[k] - m->ext_begin == c0 + x + Lx * y + Lxy * z;
+                if (ok) {
+                    r.box0 = (int)c0;
+                    r.box1 = (int)(nx | (ny << 8) | (nz << 16));
+                }
+            }
+            info[i] = r;
+        }
+    });
+    return 0;
+}
+
 // Device node-block matrix with the symbolic pattern `which` of the mesh.
 int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat **out)
 {
     const int64_t nrows = m->node_end - m->node_begin;
+    PhaseTimer tm(ctx);
+    // symbolic pattern: on the device for box meshes, host enumeration otherwise
+    const char *hp = getenv("KLE_HOST_PATTERN");
+    const bool on_dev = m->kind == 0 && !(hp && atoi(hp) != 0);
+    std::vector<PatRowInfo> info;
     std::vector<int64_t> rp, cols;
-    KLE_TRY(pattern_csr(m, which, rp, cols));
-    const int64_t nb = rp[nrows];
+    struct DirBuf {
+        uint8_t *p = nullptr;
+        ~DirBuf() { if (p) (void)hipFree(p); }
+    } dirbuf;
+    uint8_t *&ddir = dirbuf.p;
+    if (on_dev) {
+        KLE_HIP(hipMalloc(&ddir, std::max<size_t>(m->dir.size(), 1)));
+        KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
+        KLE_TRY(pattern_rows_dev(ctx, m, which, ddir, info));
+    } else {
+        KLE_TRY(pattern_rows_host(m, which, info, rp, cols));
+    }
+    tm.lap(on_dev ? "pattern: device row summary" : "pattern: host enumeration");
+    int64_t nb = 0;
+    for (int64_t i = 0; i < nrows; ++i) nb += info[i].cnt;
     if (nb >= (1ll << 31) / 1) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
     const int lay = g_nb_layout;
     const int pad = lay == 1 ? 1 : std::max(1, g_nb_pad);
     std::vector<int> rp32(nrows + 1), cnt(nrows);
     int64_t nbp = 0;
     for (int64_t i = 0; i < nrows; ++i) {
-        cnt[i] = (int)(rp[i + 1] - rp[i]);
+        cnt[i] = info[i].cnt;
         rp32[i] = (int)nbp;
         nbp += (cnt[i] + pad - 1) / pad * pad;
     }
     rp32[nrows] = (int)nbp;
     if (nbp >= (1ll << 31)) return fail(KLE_ERR_SUP, "padded pattern too large for int32 block offsets");
-    std::vector<int> c32(std::max<int64_t>(nbp, 1), 0);
     // interior rows (no ghost column): [int_lo, int_hi) between the last row
     // reading a lower ghost and the first row reading an upper ghost
-    const int64_t glo = m->node_begin - m->ext_begin;
     // (slab layouts); graph partitions order the ghost-reading rows last, so
     // there the range is [0, first row reading any ghost)
-    std::vector<int64_t> t_lo(host_threads() + 1, -1), t_hi(host_threads() + 1, nrows),
-        t_any(host_threads() + 1, nrows);
-    std::atomic<int> slot{0};
-    parallel_for(nrows, [&](int64_t lo, int64_t hi) {
-        const int me = slot++;
-        int64_t last_lo = -1, first_hi = nrows, first_any = nrows;
-        for (int64_t i = lo; i < hi; ++i)
-            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-                const int64_t cl = cols[k] - m->ext_begin;
-                c32[rp32[i] + (k - rp[i])] = (int)cl;
-                if (cl < glo) last_lo = std::max(last_lo, i);
-                if (cl >= glo + nrows) first_hi = std::min(first_hi, i);
-                if (cl < glo || cl >= glo + nrows) first_any = std::min(first_any, i);
-            }
-        t_lo[me] = last_lo;
-        t_hi[me] = first_hi;
-        t_any[me] = first_any;
-    });
+    const int64_t glo = m->node_begin - m->ext_begin;
     int64_t last_lo = -1, first_hi = nrows, first_any = nrows;
-    for (size_t t = 0; t < t_lo.size(); ++t) {
-        last_lo = std::max(last_lo, t_lo[t]);
-        first_hi = std::min(first_hi, t_hi[t]);
-        first_any = std::min(first_any, t_any[t]);
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (!info[i].cnt) continue;
+        const bool rl = info[i].cmin < glo, rh = info[i].cmax >= glo + nrows;
+        if (rl) last_lo = i;
+        if (rh && first_hi == nrows) first_hi = i;
+        if ((rl || rh) && first_any == nrows) first_any = i;
     }
     if (first_hi - (last_lo + 1) < first_any) {
         last_lo = -1;
@@ -425,31 +816,23 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     }
     // structured columns? each row's column list must be exactly a lattice box
     const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
+    bool is_box = nrows > 0 && m->kind == 0;
     std::vector<int> box(2 * std::max<int64_t>(nrows, 1), 0);
-    std::atomic<bool> is_box{nrows > 0 && m->kind == 0};
-    parallel_for(nrows, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi && is_box.load(std::memory_order_relaxed); ++i) {
-            const int64_t b = rp[i], e = rp[i + 1];
-            if (e == b) continue;  // empty row (Rw Dirichlet rows): box stays 0 x 0
-            const int64_t c0 = cols[b] - m->ext_begin, c1 = cols[e - 1] - m->ext_begin;
-            const int64_t nx = c1 % Lx - c0 % Lx + 1, ny = (c1 / Lx) % m->L[1] - (c0 / Lx) % m->L[1] + 1,
-                          nz = c1 / Lxy - c0 / Lxy + 1;
-            if (nx < 1 || ny < 1 || nz < 1 || nx > 255 || ny > 255 || nz > 255 || nx * ny * nz != e - b) {
-                is_box = false;
-                return;
-            }
-            int64_t k = b;
-            for (int64_t z = 0; z < nz; ++z)
-                for (int64_t y = 0; y < ny; ++y)
-                    for (int64_t x = 0; x < nx; ++x, ++k)
-                        if (cols[k] - m->ext_begin != c0 + x + Lx * y + Lxy * z) {
-                            is_box = false;
-                            return;
-                        }
-            box[2 * i] = (int)c0;
-            box[2 * i + 1] = (int)(nx | (ny << 8) | (nz << 16));
-        }
-    });
+    for (int64_t i = 0; i < nrows && is_box; ++i) {
+        if (info[i].box1 < 0) is_box = false;
+        box[2 * i] = info[i].box0;
+        box[2 * i + 1] = info[i].box1;
+    }
+    std::vector<int> c32;
+    if (!on_dev) {
+        c32.assign(std::max<int64_t>(nbp, 1), 0);
+        parallel_for(nrows, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; ++i)
+                for (int64_t k = rp[i]; k < rp[i + 1]; ++k) c32[rp32[i] + (k - rp[i])] = (int)(cols[k] - m->ext_begin);
+        });
+        std::vector<int64_t>().swap(cols);
+    }
+    tm.lap("pattern: host row offsets / ranges");
     kle_mat *A = new kle_mat;
     A->ctx = ctx;
     A->kind = 0;
@@ -462,7 +845,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->vlayout = lay;
     std::vector<int64_t> vptr(nrows + 1, 0);
     for (int64_t i = 0; i < nrows; ++i) {
-        const int64_t mi = rp[i + 1] - rp[i];
+        const int64_t mi = cnt[i];
         vptr[i + 1] = vptr[i] + (lay == 1 ? (mi * R * C + 15) / 16 * 16 : (int64_t)(rp32[i + 1] - rp32[i]) * R * C);
     }
     A->nvals = vptr[nrows];
@@ -509,8 +892,16 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     }
     KLE_HIP(hipMemcpyAsync(A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1), hipMemcpyHostToDevice,
                            ctx->stream));
-    KLE_HIP(hipMemcpyAsync(A->d_bcol, c32.data(), sizeof(int) * std::max<int64_t>(nbp, 1),
-                           hipMemcpyHostToDevice, ctx->stream));
+    if (on_dev) {
+        KLE_HIP(hipMemsetAsync(A->d_bcol, 0, sizeof(int) * std::max<int64_t>(nbp, 1), ctx->stream));
+        if (nrows)
+            hipLaunchKernelGGL(k_pat_fill, dim3((unsigned)((nrows * 64 + 255) / 256)), dim3(256), 0, ctx->stream,
+                               mesh_dev(m), nrows, which, ddir, A->d_rowptr, A->d_bcol);
+        KLE_HIP(hipGetLastError());
+    } else {
+        KLE_HIP(hipMemcpyAsync(A->d_bcol, c32.data(), sizeof(int) * std::max<int64_t>(nbp, 1),
+                               hipMemcpyHostToDevice, ctx->stream));
+    }
     if (A->d_rowcnt)
         KLE_HIP(hipMemcpyAsync(A->d_rowcnt, cnt.data(), sizeof(int) * std::max<int64_t>(nrows, 1), hipMemcpyHostToDevice,
                                ctx->stream));
@@ -522,6 +913,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
         KLE_HIP(hipMemcpyAsync(A->d_rowbox, box.data(), sizeof(int) * 2 * nrows, hipMemcpyHostToDevice, ctx->stream));
     }
     KLE_HIP(hipStreamSynchronize(ctx->stream));
+    tm.lap("matrix alloc + uploads + column fill");
     *out = A;
     return 0;
 }
@@ -559,10 +951,12 @@ static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, doubl
 {
     const int dim = m->dim, ne = m->nn(), dw = dim == 2 ? 1 : 3, nc = 1 << dim;
     const int64_t nel = m->elem_end - m->elem_begin;
+    PhaseTimer tm(ctx);
     DevTables T;
     KLE_TRY(upload_tables(ctx, m->ngl, T));
     std::vector<double> corners(nel * nc * dim);
     KLE_TRY(kle_mesh_get_corners(m, corners.data()));
+    tm.lap("element: tables + corners");
     double *dX = nullptr, *gF = nullptr, *gR = nullptr;
     const int nqF = dim == 2 ? T.F.np1 * T.F.np1 : T.F.np1 * T.F.np1 * T.F.np1;
     const int nqR = dim == 2 ? T.R.np1 * T.R.np1 : T.R.np1 * T.R.np1 * T.R.np1;
@@ -586,17 +980,29 @@ static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, doubl
     double *Rd_out = dRde ? *dRde : nullptr;
     const int64_t nF = nel * nqF, nR = nel * nqR;
     dim3 eg((ne + TL - 1) / TL, (ne + TL - 1) / TL, (unsigned)nel);
+    // KLE_ELEMENT_VALU=1: the FP64-VALU element kernel instead of the MFMA one
+    const char *ev = getenv("KLE_ELEMENT_VALU");
+    const bool valu = ev && atoi(ev) != 0;
     if (dim == 2) {
         hipLaunchKernelGGL(k_geometry<2>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
         hipLaunchKernelGGL(k_geometry<2>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
-        hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
+        if (valu)
+            hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
+        else
+            hipLaunchKernelGGL(k_element_mfma<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe,
+                               Rd_out);
     } else {
         hipLaunchKernelGGL(k_geometry<3>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
         hipLaunchKernelGGL(k_geometry<3>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
-        hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
+        if (valu)
+            hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
+        else
+            hipLaunchKernelGGL(k_element_mfma<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe,
+                               Rd_out);
     }
     KLE_HIP(hipGetLastError());
     KLE_HIP(hipStreamSynchronize(ctx->stream));
+    tm.lap(valu ? "element: geometry + k_element (VALU)" : "element: geometry + k_element_mfma");
     hipFree(dX);
     hipFree(gF);
     hipFree(gR);
@@ -1135,11 +1541,14 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     const int dim = m->dim, dw = dim == 2 ? 1 : 3;
     KLE_HIP(hipSetDevice(ctx->device));
     kle_mat *mK = nullptr, *mKr = nullptr, *mRw = nullptr;
+    PhaseTimer tm(ctx);
     KLE_TRY(nb_create(ctx, m, 0, dim, dim, &mK));
     KLE_TRY(nb_create(ctx, m, 1, dim, dim, &mKr));
     KLE_TRY(nb_create(ctx, m, 2, dim, dw, &mRw));
+    tm.lap("assemble_kle: three patterns");
     double *dKe = nullptr, *dRwe = nullptr;
     KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe));
+    tm.lap("assemble_kle: element matrices");
     uint8_t *ddir = nullptr;
     KLE_HIP(hipMalloc(&ddir, m->dir.size()));
     KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
@@ -1167,9 +1576,11 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     }
     KLE_HIP(hipGetLastError());
     KLE_HIP(hipStreamSynchronize(ctx->stream));
+    tm.lap("assemble_kle: gathers");
     hipFree(dKe);
     hipFree(dRwe);
     hipFree(ddir);
+    tm.lap("assemble_kle: free element scratch");
     *K = mK;
     *Krhs = mKr;
     *Rw = mRw;

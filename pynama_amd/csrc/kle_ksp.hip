@@ -451,10 +451,25 @@ struct kle_ksp {
     bool setup = false;
     int its = 0, reason = 0;
     double rnorm = 0, true_rel = -1;
+    // single-rank CG: `check_every` iterations captured as one hipGraph,
+    // replayed until the device reason word stops the kernels; valid for the
+    // (b, x) pair it was captured with
+    hipGraphExec_t graph = nullptr;
+    const double *graph_b = nullptr, *graph_x = nullptr;
+    int graph_jac = -1, graph_len = 0;
+    bool graph_off = false;  // capture failed once: stream-launched from then on
 };
+
+static void drop_graph(kle_ksp *k)
+{
+    if (k->graph) (void)hipGraphExecDestroy(k->graph);
+    k->graph = nullptr;
+    k->graph_b = k->graph_x = nullptr;
+}
 
 static void free_work(kle_ksp *k)
 {
+    drop_graph(k);
     kle_vec_destroy(k->r);
     kle_vec_destroy(k->p);
     kle_vec_destroy(k->q);
@@ -678,7 +693,8 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR_START));
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    for (int it = 0; it < limit; ++it) {
+    // one iteration: fused update, SpMV w = A u (+ (w, u) partials), reduction
+    auto iteration = [&]() -> int {
         KLE_TRY(c->tic("cg_update", &ev));
         if (jac)
             hipLaunchKernelGGL(k_sr_update<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d, k->p->d,
@@ -690,9 +706,49 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
         KLE_TRY(c->toc("cg_update", &ev));
         KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, c->d_istate));
         KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR));
-        if (!k->fixed && ((it + 1) % k->check_every == 0)) {
-            KLE_TRY(poll_state(k));
-            if (c->h_istate[I_REASON] != 0) break;
+        return 0;
+    };
+    // hipGraph replay (one rank, no per-launch timing): every kernel of the
+    // loop reads its scalars from device memory and turns into a no-op once
+    // the reason word is set, so a block of check_every iterations is a fixed
+    // launch sequence; capture it once per (b, x), replay it per block
+    const char *ge = getenv("KLE_GRAPH");
+    const bool want_graph = c->nranks == 1 && !c->profiling && !k->graph_off && !(ge && atoi(ge) == 0);
+    if (want_graph && !(k->graph && k->graph_b == b->d && k->graph_x == x->d && k->graph_jac == (int)jac &&
+                        k->graph_len == k->check_every)) {
+        drop_graph(k);
+        hipGraph_t gr = nullptr;
+        int rc = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess ? 0 : 1;
+        for (int j = 0; j < k->check_every && !rc; ++j) rc = iteration();
+        const bool ended = hipStreamEndCapture(c->stream, &gr) == hipSuccess;
+        hipGraphExec_t ex = nullptr;
+        if (!rc && ended && gr && hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0) == hipSuccess) {
+            k->graph = ex;
+            k->graph_b = b->d;
+            k->graph_x = x->d;
+            k->graph_jac = (int)jac;
+            k->graph_len = k->check_every;
+        } else {
+            k->graph_off = true;  // e.g. a matrix whose SpMV path cannot be captured
+            (void)hipGetLastError();
+        }
+        if (gr) (void)hipGraphDestroy(gr);
+    }
+    if (want_graph && k->graph) {
+        for (int it = 0; it < limit; it += k->graph_len) {
+            KLE_HIP(hipGraphLaunch(k->graph, c->stream));
+            if (!k->fixed) {
+                KLE_TRY(poll_state(k));
+                if (c->h_istate[I_REASON] != 0) break;
+            }
+        }
+    } else {
+        for (int it = 0; it < limit; ++it) {
+            KLE_TRY(iteration());
+            if (!k->fixed && ((it + 1) % k->check_every == 0)) {
+                KLE_TRY(poll_state(k));
+                if (c->h_istate[I_REASON] != 0) break;
+            }
         }
     }
     KLE_TRY(poll_state(k));
@@ -1085,6 +1141,7 @@ int kle_ksp_set_operators(kle_ksp *k, kle_mat *A)
     KLE_ARG(A->m_global == A->n_global, "KSP needs a square operator");
     k->A = A;
     k->setup = false;
+    drop_graph(k);
     return 0;
 }
 

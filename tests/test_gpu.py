@@ -73,8 +73,11 @@ def test_assembly_matches_golden(pa, case):
         assert np.abs(d - ref).max() <= 1e-12 * np.abs(ref).max(), nm
 
 
+@pytest.mark.parametrize("kernel", ["mfma", "valu"])
 @pytest.mark.parametrize("dim,ngl", [(2, 2), (2, 3), (2, 5), (2, 7), (3, 2), (3, 3), (3, 5), (3, 6), (3, 7)])
-def test_element_kernel_vs_oracle(pa, dim, ngl):
+def test_element_kernel_vs_oracle(pa, dim, ngl, kernel):
+    """k_element_mfma (FP64 MFMA, the default) and k_element (FP64 VALU,
+    KLE_ELEMENT_VALU=1) against the oracle's element matrices."""
     import ctypes as C
     from pynama_amd._lib import call
     mesh = pa.BoxMesh(dim, [2] * dim, [0.1] * dim, [0.7, 0.5, 0.4][:dim], ngl)
@@ -83,7 +86,11 @@ def test_element_kernel_vs_oracle(pa, dim, ngl):
     dw = 1 if dim == 2 else 3
     Ke = np.zeros((dim * n, dim * n))
     Rwe = np.zeros((dim * n, dw * n))
-    call("kle_element_kle", ctx.h, mesh._h, 1, Ke, Rwe)
+    os.environ["KLE_ELEMENT_VALU"] = "1" if kernel == "valu" else "0"
+    try:
+        call("kle_element_kle", ctx.h, mesh._h, 1, Ke, Rwe)
+    finally:
+        os.environ.pop("KLE_ELEMENT_VALU", None)
     el = O.Element(ngl, dim)
     X = mesh.corners()[1]
     Kr, Rwr, _ = el.kle(X.ravel())
@@ -529,3 +536,65 @@ def test_fast_spmv_kernel_matches_generic(pa):
                 A.setSpmvStructured(True)
     finally:
         set_value_layout(old)
+
+
+@pytest.mark.parametrize("lay", [0, 1])
+def test_device_pattern_matches_host(pa, lay):
+    """Box-mesh patterns built on the device (k_pat_count / k_pat_fill) ==
+    the host enumeration (KLE_HOST_PATTERN=1), bitwise: CSR exports,
+    structured-column detection, interior row range and SpMV, for the
+    free-slip matrices (all-boundary and random Dirichlet sets, 2-D and 3-D,
+    two slab ranks' rows), the operators and the no-slip matrices."""
+    from pynama_amd.runtime import get_value_layout, set_value_layout
+    old_lay = get_value_layout()
+    rng = np.random.default_rng(17)
+    g = _golden("tg3d_p4")
+
+    def build_all():
+        out = []
+        dom = _domain(pa, g)
+        mat = pa.MatFS()
+        mat.setDomain(dom)
+        mat.build()
+        op = mat.getOperators()
+        out += [mat.K, mat.Krhs, mat.Rw, op.Curl, op.SrT, op.DivSrT]
+        for dim, nel, ngl in ((3, [3, 2, 4], 4), (2, [4, 3], 5)):
+            cfg = {"domain": {"ngl": ngl, "box-mesh": {"nelem": nel, "lower": [0] * dim, "upper": [1] * dim}},
+                   "boundary-conditions": {"uniform": {"velocity": [1] * dim}}}
+            d = pa.Domain()
+            d.configure(cfg)
+            d.setUp()
+            N = d.mesh.N
+            sub = np.sort(np.random.default_rng(dim).choice(N, N // 5, replace=False))
+            d.mesh.set_dirichlet_nodes(sub)  # arbitrary Dirichlet set: filtered rows are not boxes
+            mt = pa.MatFS()
+            mt.setDomain(d)
+            mt.build(buildOperators=False)
+            out += [mt.K, mt.Krhs, mt.Rw]
+        cfg = {"domain": {"ngl": 4, "box-mesh": {"nelem": [3, 3], "lower": [0, 0], "upper": [1, 1]}},
+               "boundary-conditions": {"no-slip": {"up": [1, 0], "down": [0, 0], "left": [0, 0], "right": [0, 0]}}}
+        dns = pa.Domain()
+        dns.configure(cfg)
+        dns.setUp()
+        mns = pa.MatNS()
+        mns.setDomain(dns)
+        mns.build()
+        out += [mns.K, mns.Krhs, mns.Rw, mns.Kfs, mns.Krhsfs, mns.Rwfs, mns.getKplusKfs(), mns.Rdfs]
+        return out
+
+    built = {}
+    try:
+        set_value_layout(lay)
+        for host in (1, 0):
+            os.environ["KLE_HOST_PATTERN"] = str(host)
+            built[host] = build_all()
+    finally:
+        os.environ.pop("KLE_HOST_PATTERN", None)
+        set_value_layout(old_lay)
+    for A0, A1 in zip(built[1], built[0]):
+        assert A0.isStructured() == A1.isStructured()
+        for u, v in zip(A0.getValuesCSR(), A1.getValuesCSR()):
+            np.testing.assert_array_equal(u, v)
+        x = A0.createVecRight()
+        x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
+        np.testing.assert_array_equal((A0 * x).getArray(), (A1 * x).getArray())

@@ -85,6 +85,18 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
 @pytest.mark.parametrize("overlap,ksp_type", [(True, "cg"), (False, "cg"), (True, "pipecg")])
 @pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 4), (3, [2, 3, 3], 3)])
 def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap, ksp_type):
+    _check_box(size, nelem, ngl, overlap, ksp_type)
+
+
+@pytest.mark.parametrize("ksp_type", ["cg", "pipecg"])
+def test_eight_slab_solve_matches_serial(ksp_type):
+    """The 8-GPU bench's decomposition (config 3) at small size: 8 ranks of one
+    element layer each (every interior rank exchanges with two neighbours, the
+    lower ghost range is a whole neighbour slab), overlap on."""
+    _check_box(8, [2, 2, 8], 4, True, ksp_type)
+
+
+def _check_box(size, nelem, ngl, overlap, ksp_type):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
@@ -92,18 +104,7 @@ def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap, ksp_type):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type)) for r in range(size)]
-    for p in procs:
-        p.start()
-    try:
-        res = sorted([q.get(timeout=240) for _ in range(size)], key=lambda r: r["rank"])
-    except Exception:
-        for p in procs:
-            p.kill()
-        raise
-    for p in procs:
-        p.join(timeout=120)
-    for r in res:
-        assert "error" not in r, r.get("error")
+    res = _collect(procs, q, size)
     for r in res:
         assert r["overlap_equal"], (r["rank"], r["ov_diff"])
     # serial oracle system on the same numbering
@@ -150,25 +151,43 @@ def _run(size, nelem, ngl, overlap=True, ksp_type="cg", msh=None, partitioner=No
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, msh, partitioner))
              for r in range(size)]
+    return _collect(procs, q, size)
+
+
+def _collect(procs, q, size, timeout=100):
+    """Start the ranks and gather their results; the first rank that reports
+    an error fails the test at once (its peers are killed, not waited for)."""
+    import queue
     for p in procs:
         p.start()
+    import time
+    res = []
+    t_end = time.time() + timeout
     try:
-        res = sorted([q.get(timeout=240) for _ in range(size)], key=lambda r: r["rank"])
-    except Exception:
+        while len(res) < size:
+            try:
+                r = q.get(timeout=2)
+            except queue.Empty:
+                missing = sorted(set(range(size)) - {x["rank"] for x in res})
+                dead = [(i, procs[i].exitcode) for i in missing if procs[i].exitcode is not None]
+                assert not dead, f"ranks died without a result (rank, exit code): {dead}"
+                assert time.time() < t_end, f"ranks {missing} sent nothing within {timeout} s"
+                continue
+            assert "error" not in r, f"rank {r['rank']}: {r['error']}"
+            res.append(r)
+    except BaseException:
         for p in procs:
             p.kill()
         raise
     for p in procs:
-        p.join(timeout=120)
-    for r in res:
-        assert "error" not in r, r.get("error")
-    return res
+        p.join(timeout=60)
+    return sorted(res, key=lambda r: r["rank"])
 
 
 @pytest.mark.parametrize("size,partitioner,nel,ksp_type", [
     (2, "slab", [2, 3, 9], "cg"), (3, "slab", [2, 3, 9], "cg"),
     (2, "inertial", [3, 3, 4], "cg"), (3, "inertial", [3, 4, 4], "cg"), (4, "inertial", [4, 4, 4], "cg"),
-    (4, "inertial", [4, 4, 4], "pipecg")])
+    (4, "inertial", [4, 4, 4], "pipecg"), (8, "inertial", [4, 4, 6], "pipecg")])
 def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type, tmp_path):
     """SURVEY 8(e) on an unstructured mesh (config 5's path): rotated /
     shuffled hexes in Gmsh format, partitioned into slabs (two-range halo)

@@ -1,0 +1,5 @@
+# Full GPU suite, verbose, per-test timeout (a hang names its test and dumps stacks)
+source tools/gpu_steps.sh
+rm -f gpurun_out/steps.txt
+step pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread || exit 1
+tail -n 3 gpurun_out/pytest_gpu.log
