@@ -708,12 +708,14 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
         KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR));
         return 0;
     };
-    // hipGraph replay (one rank, no per-launch timing): every kernel of the
-    // loop reads its scalars from device memory and turns into a no-op once
-    // the reason word is set, so a block of check_every iterations is a fixed
-    // launch sequence; capture it once per (b, x), replay it per block
+    // hipGraph replay (KLE_GRAPH=1; one rank, no per-launch timing): every
+    // kernel of the loop reads its scalars from device memory and turns into a
+    // no-op once the reason word is set, so a block of check_every iterations
+    // is a fixed launch sequence; capture it once per (b, x), replay it per
+    // block.  Off by default: the loop is not launch-bound on MI355X
+    // (tools/graph_ab.py: equal time at 1M and 8M DoF, +0.7 % on a 142k-DoF part)
     const char *ge = getenv("KLE_GRAPH");
-    const bool want_graph = c->nranks == 1 && !c->profiling && !k->graph_off && !(ge && atoi(ge) == 0);
+    const bool want_graph = c->nranks == 1 && !c->profiling && !k->graph_off && ge && atoi(ge) != 0;
     if (want_graph && !(k->graph && k->graph_b == b->d && k->graph_x == x->d && k->graph_jac == (int)jac &&
                         k->graph_len == k->check_every)) {
         drop_graph(k);

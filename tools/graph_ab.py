@@ -58,7 +58,7 @@ def main(nelem, ngl, steps=200, reps=4):
     ctx.set_profiling(False)
     out["spmv_ms"] = ms / c
     for mode in ("1", "0") * reps:
-        os.environ["KLE_GRAPH"] = mode
+        os.environ["KLE_GRAPH"] = mode  # 1: graph replay (opt-in), 0: stream launches
         kb.setFixedIterations(20)
         kb.solve(b, x)
         kb.setFixedIterations(steps)
@@ -71,7 +71,7 @@ def main(nelem, ngl, steps=200, reps=4):
     # converged solve equal either way
     res = {}
     for mode in ("1", "0"):
-        os.environ["KLE_GRAPH"] = mode
+        os.environ["KLE_GRAPH"] = mode  # 1: graph replay (opt-in), 0: stream launches
         ksp = sol.getKSP()
         ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=100000)
         vel.set(0.0)
