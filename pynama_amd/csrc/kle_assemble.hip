@@ -435,7 +435,8 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
                                                 const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
                                                 int lay, const int *__restrict__ bcol,
                                                 const uint8_t *__restrict__ dir,
-                                                const double *__restrict__ Eblk, double *__restrict__ val)
+                                                const double *__restrict__ Eblk, double *__restrict__ val,
+                                                int64_t eb0, int64_t eb1, int accum)
 {
     const int lane = threadIdx.x & 63;
     const int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
     double *v = val + vptr[row];
     if (dir[gi - M.ext_begin]) {
         // K[dir,dir] = 0 + ... + 0 + 1 and Krhs[dir,dir] = 1 (mat_fs.py:115-120,182-183)
-        if (MODE != 2 && lane == 0 && m == 1)
+        if (MODE != 2 && lane == 0 && m == 1 && eb0 == 0)
             for (int a = 0; a < R; ++a)
                 for (int b = 0; b < C; ++b) v[vofs(lay, R * C, a * C + b, 0, m, mp)] = (a == b) ? 1.0 : 0.0;
         return;
@@ -461,13 +462,21 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
         elo[d] = (c % M.p == 0) ? max((int64_t)0, c / M.p - 1) : c / M.p;
         ehi[d] = min(M.nel[d] - 1, c / M.p);
     }
+    // element batch [eb0, eb1) (local ids, ascending = the ADD order): rows
+    // with no cell in it are left as they are
+    const int64_t emin = elo[0] + M.nel[0] * (elo[1] + M.nel[1] * elo[2]) - M.elem_begin;
+    const int64_t emax = ehi[0] + M.nel[0] * (ehi[1] + M.nel[1] * ehi[2]) - M.elem_begin;
+    if (emax < eb0 || emin >= eb1) return;
     const int ngl = M.ngl, ne = M.ne;
     for (int k = lane; k < m; k += 64) {
         const int64_t gj = M.ext_begin + bcol[b0 + k];
         int64_t cj[3] = {gj % M.L[0], (gj / M.L[0]) % M.L[1], M.dim == 3 ? gj / (M.L[0] * M.L[1]) : 0};
         double acc[R * C];
+        // later batches continue the ascending-cell sum from the stored partial
 #pragma unroll
-        for (int t = 0; t < R * C; ++t) acc[t] = 0.0;
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < C; ++b) acc[a * C + b] = accum ? v[vofs(lay, R * C, a * C + b, k, m, mp)] : 0.0;
         for (int64_t ez = elo[2]; ez <= ehi[2]; ++ez)
             for (int64_t ey = elo[1]; ey <= ehi[1]; ++ey)
                 for (int64_t ex = elo[0]; ex <= ehi[0]; ++ex) {
@@ -480,11 +489,11 @@ __global__ __launch_bounds__(256) void k_gather(MeshDev M, int64_t nrows, const 
                         oj[d] = (int)o;
                         oi[d] = (int)(ci[d] - eo[d]);
                     }
-                    if (!in) continue;
                     const int64_t e = ex + M.nel[0] * (ey + M.nel[1] * ez) - M.elem_begin;
+                    if (!in || e < eb0 || e >= eb1) continue;
                     const int li = oi[0] + ngl * (oi[1] + ngl * oi[2]);
                     const int lj = oj[0] + ngl * (oj[1] + ngl * oj[2]);
-                    const double *blk = Eblk + ((e * ne + li) * (int64_t)ne + lj) * (R * C);
+                    const double *blk = Eblk + (((e - eb0) * ne + li) * (int64_t)ne + lj) * (R * C);
 #pragma unroll
                     for (int t = 0; t < R * C; ++t) acc[t] += (MODE == 1) ? -blk[t] : blk[t];
                 }
@@ -533,6 +542,46 @@ struct PhaseTimer {
         t = now;
     }
 };
+
+// Unstructured mesh topology on the device (kle_umesh.cpp arrays, ext-local ids)
+struct UMeshDev {
+    int ne;
+    const int *conn;      // [e][ne] ext-local node
+    const int64_t *incp;  // owned row -> [incp[i], incp[i+1])
+    const int *inc;       // e * ne + l
+    int64_t glo;          // ext-local id of owned row 0
+};
+
+struct UMeshBuf {
+    int *conn = nullptr, *inc = nullptr;
+    int64_t *incp = nullptr;
+    UMeshDev dev{};
+    ~UMeshBuf()
+    {
+        hipFree(conn);
+        hipFree(inc);
+        hipFree(incp);
+    }
+};
+
+static int upload_umesh(kle_ctx *ctx, const kle_mesh *m, UMeshBuf &U)
+{
+    const int ne = m->nn();
+    std::vector<int> c32(std::max<size_t>(m->u_conn.size(), 1));
+    for (size_t k = 0; k < m->u_conn.size(); ++k) c32[k] = (int)(m->u_conn[k] - m->ext_begin);
+    KLE_HIP(hipMalloc(&U.conn, sizeof(int) * c32.size()));
+    KLE_HIP(hipMalloc(&U.incp, sizeof(int64_t) * m->u_incp.size()));
+    KLE_HIP(hipMalloc(&U.inc, sizeof(int) * std::max<size_t>(m->u_inc.size(), 1)));
+    KLE_HIP(hipMemcpyAsync(U.conn, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice, ctx->stream));
+    KLE_HIP(hipMemcpyAsync(U.incp, m->u_incp.data(), sizeof(int64_t) * m->u_incp.size(), hipMemcpyHostToDevice,
+                           ctx->stream));
+    if (!m->u_inc.empty())
+        KLE_HIP(hipMemcpyAsync(U.inc, m->u_inc.data(), sizeof(int) * m->u_inc.size(), hipMemcpyHostToDevice,
+                               ctx->stream));
+    KLE_HIP(hipStreamSynchronize(ctx->stream));
+    U.dev = {ne, U.conn, U.incp, U.inc, m->node_begin - m->ext_begin};
+    return 0;
+}
 
 // ------------------------------------------------------ device patterns
 // Box meshes: the symbolic pattern `which` (kle_mesh.cpp row_cols: the
@@ -696,18 +745,113 @@ __global__ __launch_bounds__(256) void k_pat_fill(MeshDev M, int64_t nrows, int 
     }
 }
 
+// Unstructured meshes: the columns of row i are the sorted unique nodes of
+// its incident cells (kle_umesh.cpp umesh_row_nodes), filtered as row_cols.
+// One wavefront per row gathers the incident cells' node lists into LDS
+// (padded to a power of two), bitonic-sorts them, and keeps the first copy of
+// each node that passes the filter (ballot + popcount prefix).  pass 0:
+// per-row summary; pass 1: the column list at rowptr[row].
+__global__ __launch_bounds__(64) void k_upat(UMeshDev U, int64_t nrows, int which, int P,
+                                             const uint8_t *__restrict__ dir, PatRowInfo *__restrict__ info,
+                                             const int *__restrict__ rowptr, int *__restrict__ bcol)
+{
+    extern __shared__ int sc[];
+    const int lane = threadIdx.x;
+    const int64_t row = blockIdx.x;
+    if (row >= nrows) return;
+    const int il = (int)(row + U.glo);
+    const bool di = dir[il] != 0;
+    const bool pass1 = bcol != nullptr;
+    int *out = pass1 ? bcol + rowptr[row] : nullptr;
+    if ((which == 6 && !di) || (which <= 2 && di)) {
+        const bool one = which <= 2 && which != 2;
+        if (lane == 0) {
+            if (pass1) {
+                if (one) out[0] = il;
+            } else {
+                info[row] = one ? PatRowInfo{1, il, il, 0, -1} : PatRowInfo{0, 0x7fffffff, -1, 0, 0};
+            }
+        }
+        return;
+    }
+    const int ne = U.ne;
+    const int64_t q0 = U.incp[row], q1 = U.incp[row + 1];
+    const int nc = (int)(q1 - q0) * ne;
+    for (int k = lane; k < P; k += 64) {
+        int v = 0x7fffffff;
+        if (k < nc) {
+            const int e = U.inc[q0 + k / ne] / ne;
+            v = U.conn[(int64_t)e * ne + k % ne];
+        }
+        sc[k] = v;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= P; kk <<= 1)
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = lane; i < P; i += 64) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int a = sc[i], b = sc[ixj];
+                    if ((a > b) == ((i & kk) == 0)) {
+                        sc[i] = b;
+                        sc[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const uint64_t below = (1ull << lane) - 1ull;
+    int cnt = 0, first = 0x7fffffff, last = -1;
+    for (int k0 = 0; k0 < nc; k0 += 64) {
+        const int k = k0 + lane;
+        bool keep = false;
+        int v = 0;
+        if (k < nc) {
+            v = sc[k];
+            keep = (k == 0 || sc[k - 1] != v) && pat_keep(which, di, dir[v] != 0);
+        }
+        const uint64_t bal = __ballot(keep);
+        if (keep) {
+            if (pass1) out[cnt + __popcll(bal & below)] = v;
+            first = min(first, v);
+            last = max(last, v);
+        }
+        cnt += __popcll(bal);
+    }
+    if (pass1) return;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        first = min(first, __shfl_xor(first, o, 64));
+        last = max(last, __shfl_xor(last, o, 64));
+    }
+    if (lane == 0) info[row] = PatRowInfo{cnt, first, last, 0, cnt ? -1 : 0};
+}
+
+static int upat_lds(const kle_mesh *m)
+{
+    int64_t mx = 1;
+    for (size_t i = 0; i + 1 < m->u_incp.size(); ++i) mx = std::max<int64_t>(mx, m->u_incp[i + 1] - m->u_incp[i]);
+    int P = 64;
+    while (P < mx * m->nn()) P <<= 1;
+    return P;
+}
+
 // Per-row pattern summary of `which` on the device (box meshes); dd = device
 // copy of m->dir.
 static int pattern_rows_dev(kle_ctx *ctx, const kle_mesh *m, int which, const uint8_t *dd,
-                            std::vector<PatRowInfo> &info)
+                            std::vector<PatRowInfo> &info, const UMeshDev *U = nullptr, int P = 0)
 {
     const int64_t nrows = m->node_end - m->node_begin;
     info.resize(std::max<int64_t>(nrows, 1));
     if (nrows == 0) return 0;
     PatRowInfo *di = nullptr;
     KLE_HIP(hipMalloc(&di, sizeof(PatRowInfo) * nrows));
-    hipLaunchKernelGGL(k_pat_count, dim3((unsigned)((nrows * 64 + 255) / 256)), dim3(256), 0, ctx->stream,
-                       mesh_dev(m), nrows, which, dd, di);
+    if (m->kind == 1)
+        hipLaunchKernelGGL(k_upat, dim3((unsigned)nrows), dim3(64), sizeof(int) * P, ctx->stream, *U, nrows, which, P,
+                           dd, di, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL(k_pat_count, dim3((unsigned)((nrows * 64 + 255) / 256)), dim3(256), 0, ctx->stream,
+                           mesh_dev(m), nrows, which, dd, di);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)
         e = hipMemcpyAsync(info.data(), di, sizeof(PatRowInfo) * nrows, hipMemcpyDeviceToHost, ctx->stream);
@@ -761,13 +905,19 @@ static int pattern_rows_host(const kle_mesh *m, int which, std::vector<PatRowInf
 }
 
 // Device node-block matrix with the symbolic pattern `which` of the mesh.
-int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat **out)
+int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat **out, const UMeshDev *U = nullptr)
 {
     const int64_t nrows = m->node_end - m->node_begin;
     PhaseTimer tm(ctx);
-    // symbolic pattern: on the device for box meshes, host enumeration otherwise
+    // symbolic pattern on the device (KLE_HOST_PATTERN=1: the host enumeration)
     const char *hp = getenv("KLE_HOST_PATTERN");
-    const bool on_dev = m->kind == 0 && !(hp && atoi(hp) != 0);
+    const int P = m->kind == 1 ? upat_lds(m) : 0;
+    const bool on_dev = !(hp && atoi(hp) != 0) && P <= 32768;
+    UMeshBuf Uloc;
+    if (on_dev && m->kind == 1 && !U) {
+        KLE_TRY(upload_umesh(ctx, m, Uloc));
+        U = &Uloc.dev;
+    }
     std::vector<PatRowInfo> info;
     std::vector<int64_t> rp, cols;
     struct DirBuf {
@@ -778,7 +928,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     if (on_dev) {
         KLE_HIP(hipMalloc(&ddir, std::max<size_t>(m->dir.size(), 1)));
         KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
-        KLE_TRY(pattern_rows_dev(ctx, m, which, ddir, info));
+        KLE_TRY(pattern_rows_dev(ctx, m, which, ddir, info, U, P));
     } else {
         KLE_TRY(pattern_rows_host(m, which, info, rp, cols));
     }
@@ -894,7 +1044,10 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
                            ctx->stream));
     if (on_dev) {
         KLE_HIP(hipMemsetAsync(A->d_bcol, 0, sizeof(int) * std::max<int64_t>(nbp, 1), ctx->stream));
-        if (nrows)
+        if (nrows && m->kind == 1)
+            hipLaunchKernelGGL(k_upat, dim3((unsigned)nrows), dim3(64), sizeof(int) * P, ctx->stream, *U, nrows, which,
+                               P, ddir, nullptr, A->d_rowptr, A->d_bcol);
+        else if (nrows)
             hipLaunchKernelGGL(k_pat_fill, dim3((unsigned)((nrows * 64 + 255) / 256)), dim3(256), 0, ctx->stream,
                                mesh_dev(m), nrows, which, ddir, A->d_rowptr, A->d_bcol);
         KLE_HIP(hipGetLastError());
@@ -946,66 +1099,100 @@ static int upload_tables(kle_ctx *ctx, int ngl, DevTables &T)
     return 0;
 }
 
-// Compute K_e and Rw_e of all local elements into device buffers.
-static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, double **dRwe, double **dRde = nullptr)
-{
-    const int dim = m->dim, ne = m->nn(), dw = dim == 2 ? 1 : 3, nc = 1 << dim;
-    const int64_t nel = m->elem_end - m->elem_begin;
-    PhaseTimer tm(ctx);
+// Element-matrix pipeline: tables, corners and the Gauss-point geometry of
+// every local element once (ElemSetup), then K_e / Rw_e (/ Rd_e) of any
+// contiguous range of local elements (element_batch, outputs indexed e - e0).
+struct ElemSetup {
     DevTables T;
-    KLE_TRY(upload_tables(ctx, m->ngl, T));
-    std::vector<double> corners(nel * nc * dim);
-    KLE_TRY(kle_mesh_get_corners(m, corners.data()));
-    tm.lap("element: tables + corners");
     double *dX = nullptr, *gF = nullptr, *gR = nullptr;
-    const int nqF = dim == 2 ? T.F.np1 * T.F.np1 : T.F.np1 * T.F.np1 * T.F.np1;
-    const int nqR = dim == 2 ? T.R.np1 * T.R.np1 : T.R.np1 * T.R.np1 * T.R.np1;
-    const int G1 = 1 + dim * dim;
-    KLE_HIP(hipMalloc(&dX, sizeof(double) * corners.size()));
-    KLE_HIP(hipMalloc(&gF, sizeof(double) * nel * nqF * G1));
-    KLE_HIP(hipMalloc(&gR, sizeof(double) * nel * nqR * G1));
-    KLE_HIP(hipMemcpyAsync(dX, corners.data(), sizeof(double) * corners.size(), hipMemcpyHostToDevice,
+    int nqF = 0, nqR = 0;
+    int64_t nel = 0;
+    bool valu = false;
+    ~ElemSetup()
+    {
+        if (dX) (void)hipFree(dX);
+        if (gF) (void)hipFree(gF);
+        if (gR) (void)hipFree(gR);
+    }
+};
+
+static int element_setup(kle_ctx *ctx, const kle_mesh *m, ElemSetup &S)
+{
+    const int dim = m->dim, nc = 1 << dim, G1 = 1 + dim * dim;
+    const int64_t nel = m->elem_end - m->elem_begin;
+    S.nel = nel;
+    KLE_TRY(upload_tables(ctx, m->ngl, S.T));
+    std::vector<double> corners(std::max<int64_t>(nel * nc * dim, 1));
+    KLE_TRY(kle_mesh_get_corners(m, corners.data()));
+    S.nqF = dim == 2 ? S.T.F.np1 * S.T.F.np1 : S.T.F.np1 * S.T.F.np1 * S.T.F.np1;
+    S.nqR = dim == 2 ? S.T.R.np1 * S.T.R.np1 : S.T.R.np1 * S.T.R.np1 * S.T.R.np1;
+    KLE_HIP(hipMalloc(&S.dX, sizeof(double) * corners.size()));
+    KLE_HIP(hipMalloc(&S.gF, sizeof(double) * std::max<int64_t>(nel * S.nqF * G1, 1)));
+    KLE_HIP(hipMalloc(&S.gR, sizeof(double) * std::max<int64_t>(nel * S.nqR * G1, 1)));
+    KLE_HIP(hipMemcpyAsync(S.dX, corners.data(), sizeof(double) * corners.size(), hipMemcpyHostToDevice,
                            ctx->stream));
-    const size_t keN = (size_t)nel * ne * ne * dim * dim, rwN = (size_t)nel * ne * ne * dim * dw;
-    if (hipMalloc(dKe, sizeof(double) * keN) != hipSuccess ||
-        hipMalloc(dRwe, sizeof(double) * rwN) != hipSuccess) {
-        hipFree(dX); hipFree(gF); hipFree(gR);
-        return fail(KLE_ERR_MEM, "element matrix workspace (%.2f GB) does not fit",
-                    (keN + rwN) * 8.0 / 1e9);
+    const int64_t nF = nel * S.nqF, nR = nel * S.nqR;
+    if (nel > 0) {
+        if (dim == 2) {
+            hipLaunchKernelGGL(k_geometry<2>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, S.T.F, S.dX, S.gF);
+            hipLaunchKernelGGL(k_geometry<2>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, S.T.R, S.dX, S.gR);
+        } else {
+            hipLaunchKernelGGL(k_geometry<3>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, S.T.F, S.dX, S.gF);
+            hipLaunchKernelGGL(k_geometry<3>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, S.T.R, S.dX, S.gR);
+        }
+        KLE_HIP(hipGetLastError());
     }
-    if (dRde && hipMalloc(dRde, sizeof(double) * std::max<size_t>((size_t)nel * ne * ne * dim, 1)) != hipSuccess) {
-        hipFree(dX); hipFree(gF); hipFree(gR); hipFree(*dKe); hipFree(*dRwe);
-        return fail(KLE_ERR_MEM, "element Rd workspace does not fit");
-    }
-    double *Rd_out = dRde ? *dRde : nullptr;
-    const int64_t nF = nel * nqF, nR = nel * nqR;
-    dim3 eg((ne + TL - 1) / TL, (ne + TL - 1) / TL, (unsigned)nel);
     // KLE_ELEMENT_VALU=1: the FP64-VALU element kernel instead of the MFMA one
     const char *ev = getenv("KLE_ELEMENT_VALU");
-    const bool valu = ev && atoi(ev) != 0;
+    S.valu = ev && atoi(ev) != 0;
+    return 0;
+}
+
+static int element_batch(kle_ctx *ctx, const kle_mesh *m, const ElemSetup &S, int64_t e0, int64_t cnt, double *Ke,
+                         double *Rwe, double *Rde)
+{
+    if (cnt <= 0) return 0;
+    const int dim = m->dim, ne = m->nn(), G1 = 1 + dim * dim;
+    const double *gF = S.gF + e0 * S.nqF * G1, *gR = S.gR + e0 * S.nqR * G1;
+    dim3 eg((ne + TL - 1) / TL, (ne + TL - 1) / TL, (unsigned)cnt);
     if (dim == 2) {
-        hipLaunchKernelGGL(k_geometry<2>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
-        hipLaunchKernelGGL(k_geometry<2>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
-        if (valu)
-            hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
+        if (S.valu)
+            hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
         else
-            hipLaunchKernelGGL(k_element_mfma<2>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe,
-                               Rd_out);
+            hipLaunchKernelGGL(k_element_mfma<2>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
     } else {
-        hipLaunchKernelGGL(k_geometry<3>, dim3((nF + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.F, dX, gF);
-        hipLaunchKernelGGL(k_geometry<3>, dim3((nR + 255) / 256), dim3(256), 0, ctx->stream, nel, m->ngl, T.R, dX, gR);
-        if (valu)
-            hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe, Rd_out);
+        if (S.valu)
+            hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
         else
-            hipLaunchKernelGGL(k_element_mfma<3>, eg, dim3(256), 0, ctx->stream, m->ngl, T.F, T.R, gF, gR, *dKe, *dRwe,
-                               Rd_out);
+            hipLaunchKernelGGL(k_element_mfma<3>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
     }
     KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+// K_e and Rw_e (and Rd_e) of all local elements into new device buffers.
+static int element_matrices(kle_ctx *ctx, const kle_mesh *m, double **dKe, double **dRwe, double **dRde = nullptr)
+{
+    const int dim = m->dim, ne = m->nn(), dw = dim == 2 ? 1 : 3;
+    PhaseTimer tm(ctx);
+    ElemSetup S;
+    KLE_TRY(element_setup(ctx, m, S));
+    const int64_t nel = S.nel;
+    const size_t keN = (size_t)nel * ne * ne * dim * dim, rwN = (size_t)nel * ne * ne * dim * dw;
+    *dKe = *dRwe = nullptr;
+    if (hipMalloc(dKe, sizeof(double) * std::max<size_t>(keN, 1)) != hipSuccess ||
+        hipMalloc(dRwe, sizeof(double) * std::max<size_t>(rwN, 1)) != hipSuccess) {
+        if (*dKe) hipFree(*dKe);
+        return fail(KLE_ERR_MEM, "element matrix workspace (%.2f GB) does not fit", (keN + rwN) * 8.0 / 1e9);
+    }
+    if (dRde && hipMalloc(dRde, sizeof(double) * std::max<size_t>((size_t)nel * ne * ne * dim, 1)) != hipSuccess) {
+        hipFree(*dKe);
+        hipFree(*dRwe);
+        return fail(KLE_ERR_MEM, "element Rd workspace does not fit");
+    }
+    KLE_TRY(element_batch(ctx, m, S, 0, nel, *dKe, *dRwe, dRde ? *dRde : nullptr));
     KLE_HIP(hipStreamSynchronize(ctx->stream));
-    tm.lap(valu ? "element: geometry + k_element (VALU)" : "element: geometry + k_element_mfma");
-    hipFree(dX);
-    hipFree(gF);
-    hipFree(gR);
+    tm.lap(S.valu ? "element: geometry + k_element (VALU)" : "element: geometry + k_element_mfma");
     return 0;
 }
 
@@ -1263,11 +1450,13 @@ static void launch_gather_ns(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const u
 }
 
 template <int R, int C, int MODE>
-static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint8_t *dir, const double *E)
+static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint8_t *dir, const double *E,
+                          int64_t eb0 = 0, int64_t eb1 = INT64_MAX, int accum = 0)
 {
     const int64_t threads = A->nrows * 64;
     hipLaunchKernelGGL((k_gather<R, C, MODE>), dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, M,
-                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, E, A->d_val);
+                       A->nrows, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, E, A->d_val,
+                       eb0, eb1, accum);
 }
 
 // ------------------------------------------------------- unstructured
@@ -1281,13 +1470,6 @@ static void launch_gather(kle_ctx *ctx, const MeshDev &M, kle_mat *A, const uint
 // UW block accumulators.  Within one cell the lanes hit distinct columns;
 // cells are separated by a barrier, so every entry is the ascending-cell sum
 // starting from 0, exactly as the lattice kernels and PETSc's ADD order.
-struct UMeshDev {
-    int ne;
-    const int *conn;      // [e][ne] ext-local node
-    const int64_t *incp;  // owned row -> [incp[i], incp[i+1])
-    const int *inc;       // e * ne + l
-    int64_t glo;          // ext-local id of owned row 0
-};
 
 constexpr int UW = 256;
 
@@ -1311,7 +1493,8 @@ __global__ __launch_bounds__(64) void k_gather_u(UMeshDev U, int64_t nrows, cons
                                                  const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
                                                  int lay, const int *__restrict__ bcol,
                                                  const uint8_t *__restrict__ dir, const uint8_t *__restrict__ cls,
-                                                 const double *__restrict__ Eblk, double *__restrict__ val)
+                                                 const double *__restrict__ Eblk, double *__restrict__ val,
+                                                 int64_t eb0, int64_t eb1, int accum)
 {
     constexpr int RC = R * C;
     __shared__ double acc[UW * RC];
@@ -1324,25 +1507,28 @@ __global__ __launch_bounds__(64) void k_gather_u(UMeshDev U, int64_t nrows, cons
     const int *cols = bcol + b0;
     if (MODE <= 2 && dir[il]) {
         // K[dir,dir] = 0 + ... + 0 + 1 and Krhs[dir,dir] = 1 (mat_fs.py:115-120,182-183)
-        if (MODE != 2 && lane == 0 && m == 1)
+        if (MODE != 2 && lane == 0 && m == 1 && eb0 == 0)
             for (int a = 0; a < R; ++a)
                 for (int b = 0; b < C; ++b) v[vofs(lay, RC, a * C + b, 0, m, mp)] = (a == b) ? 1.0 : 0.0;
         return;
     }
     const int ne = U.ne;
     const int64_t q0 = U.incp[row], q1 = U.incp[row + 1];
+    // element batch [eb0, eb1): the incidence list ascends in e
+    if (q0 == q1 || U.inc[q1 - 1] / ne < eb0 || U.inc[q0] / ne >= eb1) return;
     for (int w0 = 0; w0 < m; w0 += UW) {
         const int wn = min(UW, m - w0);
-        for (int t = lane; t < wn * RC; t += 64) acc[t] = 0.0;
+        for (int t = lane; t < wn * RC; t += 64) acc[t] = accum ? v[vofs(lay, RC, t % RC, w0 + t / RC, m, mp)] : 0.0;
         __syncthreads();
         for (int64_t q = q0; q < q1; ++q) {
             const int ei = U.inc[q];
             const int e = ei / ne, li = ei - e * ne;
+            if (e < eb0 || e >= eb1) continue;  // uniform over the workgroup
             const int *ce = U.conn + (int64_t)e * ne;
             for (int lj = lane; lj < ne; lj += 64) {
                 const int pos = find_col(cols, w0, w0 + wn, ce[lj]);
                 if (pos < 0) continue;
-                const double *blk = Eblk + (((int64_t)e * ne + li) * ne + lj) * RC;
+                const double *blk = Eblk + (((int64_t)(e - eb0) * ne + li) * ne + lj) * RC;
                 double *a = acc + (pos - w0) * RC;
 #pragma unroll
                 for (int t = 0; t < RC; ++t) a[t] += (MODE == 1 || MODE == 4) ? -blk[t] : blk[t];
@@ -1487,44 +1673,15 @@ __global__ __launch_bounds__(64) void k_ops_gather_u(UMeshDev U, int ngl, int64_
     }
 }
 
-struct UMeshBuf {
-    int *conn = nullptr, *inc = nullptr;
-    int64_t *incp = nullptr;
-    UMeshDev dev{};
-    ~UMeshBuf()
-    {
-        hipFree(conn);
-        hipFree(inc);
-        hipFree(incp);
-    }
-};
-
-static int upload_umesh(kle_ctx *ctx, const kle_mesh *m, UMeshBuf &U)
-{
-    const int ne = m->nn();
-    std::vector<int> c32(std::max<size_t>(m->u_conn.size(), 1));
-    for (size_t k = 0; k < m->u_conn.size(); ++k) c32[k] = (int)(m->u_conn[k] - m->ext_begin);
-    KLE_HIP(hipMalloc(&U.conn, sizeof(int) * c32.size()));
-    KLE_HIP(hipMalloc(&U.incp, sizeof(int64_t) * m->u_incp.size()));
-    KLE_HIP(hipMalloc(&U.inc, sizeof(int) * std::max<size_t>(m->u_inc.size(), 1)));
-    KLE_HIP(hipMemcpyAsync(U.conn, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice, ctx->stream));
-    KLE_HIP(hipMemcpyAsync(U.incp, m->u_incp.data(), sizeof(int64_t) * m->u_incp.size(), hipMemcpyHostToDevice,
-                           ctx->stream));
-    if (!m->u_inc.empty())
-        KLE_HIP(hipMemcpyAsync(U.inc, m->u_inc.data(), sizeof(int) * m->u_inc.size(), hipMemcpyHostToDevice,
-                               ctx->stream));
-    KLE_HIP(hipStreamSynchronize(ctx->stream));
-    U.dev = {ne, U.conn, U.incp, U.inc, m->node_begin - m->ext_begin};
-    return 0;
-}
 
 template <int R, int C, int MODE>
 static void launch_gather_u(kle_ctx *ctx, const UMeshDev &U, kle_mat *A, const uint8_t *dir, const uint8_t *cls,
-                            const double *E)
+                            const double *E, int64_t eb0 = 0, int64_t eb1 = INT64_MAX, int accum = 0)
 {
     if (A->nrows == 0) return;
     hipLaunchKernelGGL((k_gather_u<R, C, MODE>), dim3((unsigned)A->nrows), dim3(64), 0, ctx->stream, U, A->nrows,
-                       A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, cls, E, A->d_val);
+                       A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, dir, cls, E, A->d_val, eb0, eb1,
+                       accum);
 }
 
 }  // namespace kle
@@ -1538,49 +1695,78 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     KLE_ARG(ctx && m && K && Krhs && Rw, "null arg");
     KLE_ARG(m->rank == ctx->rank && m->nranks == ctx->nranks, "mesh partition does not match ctx");
     KLE_ARG(m->dir_set, "Dirichlet nodes not set (kle_mesh_set_dirichlet_*)");
-    const int dim = m->dim, dw = dim == 2 ? 1 : 3;
+    const int dim = m->dim, dw = dim == 2 ? 1 : 3, ne = m->nn();
     KLE_HIP(hipSetDevice(ctx->device));
     kle_mat *mK = nullptr, *mKr = nullptr, *mRw = nullptr;
     PhaseTimer tm(ctx);
-    KLE_TRY(nb_create(ctx, m, 0, dim, dim, &mK));
-    KLE_TRY(nb_create(ctx, m, 1, dim, dim, &mKr));
-    KLE_TRY(nb_create(ctx, m, 2, dim, dw, &mRw));
-    tm.lap("assemble_kle: three patterns");
-    double *dKe = nullptr, *dRwe = nullptr;
-    KLE_TRY(element_matrices(ctx, m, &dKe, &dRwe));
-    tm.lap("assemble_kle: element matrices");
-    uint8_t *ddir = nullptr;
-    KLE_HIP(hipMalloc(&ddir, m->dir.size()));
-    KLE_HIP(hipMemcpyAsync(ddir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
-    MeshDev M = mesh_dev(m);
     UMeshBuf U;
-    if (m->kind == 1) {
-        KLE_TRY(upload_umesh(ctx, m, U));
-        if (dim == 3) {
-            launch_gather_u<3, 3, 0>(ctx, U.dev, mK, ddir, nullptr, dKe);
-            launch_gather_u<3, 3, 1>(ctx, U.dev, mKr, ddir, nullptr, dKe);
-            launch_gather_u<3, 3, 2>(ctx, U.dev, mRw, ddir, nullptr, dRwe);
-        } else {
-            launch_gather_u<2, 2, 0>(ctx, U.dev, mK, ddir, nullptr, dKe);
-            launch_gather_u<2, 2, 1>(ctx, U.dev, mKr, ddir, nullptr, dKe);
-            launch_gather_u<2, 1, 2>(ctx, U.dev, mRw, ddir, nullptr, dRwe);
+    if (m->kind == 1) KLE_TRY(upload_umesh(ctx, m, U));
+    const UMeshDev *Ud = m->kind == 1 ? &U.dev : nullptr;
+    KLE_TRY(nb_create(ctx, m, 0, dim, dim, &mK, Ud));
+    KLE_TRY(nb_create(ctx, m, 1, dim, dim, &mKr, Ud));
+    KLE_TRY(nb_create(ctx, m, 2, dim, dw, &mRw, Ud));
+    tm.lap("assemble_kle: three patterns");
+    ElemSetup S;
+    KLE_TRY(element_setup(ctx, m, S));
+    const int64_t nel = S.nel;
+    // Element scratch is bounded (KLE_ASM_SCRATCH_GB, default 8 GB): the
+    // local elements are processed in ascending batches and every gather
+    // continues each entry's ascending-cell sum from the stored partial, so
+    // the result is bitwise the single-pass one (same additions, same order)
+    // while config 4 needs 8 GB of scratch instead of 99 GB.
+    const double per_el = (double)ne * ne * (dim * dim + dim * dw) * sizeof(double);
+    double budget = 8e9;
+    if (const char *e = getenv("KLE_ASM_SCRATCH_GB")) budget = atof(e) * 1e9;
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(nel, 1), (int64_t)(budget / per_el)));
+    const int64_t nbatch = (nel + nb - 1) / nb;
+    const int accum = nbatch > 1;
+    struct Scratch {
+        double *ke = nullptr, *rw = nullptr;
+        uint8_t *dir = nullptr;
+        ~Scratch()
+        {
+            if (ke) (void)hipFree(ke);
+            if (rw) (void)hipFree(rw);
+            if (dir) (void)hipFree(dir);
         }
-    } else if (dim == 3) {
-        launch_gather<3, 3, 0>(ctx, M, mK, ddir, dKe);
-        launch_gather<3, 3, 1>(ctx, M, mKr, ddir, dKe);
-        launch_gather<3, 3, 2>(ctx, M, mRw, ddir, dRwe);
-    } else {
-        launch_gather<2, 2, 0>(ctx, M, mK, ddir, dKe);
-        launch_gather<2, 2, 1>(ctx, M, mKr, ddir, dKe);
-        launch_gather<2, 1, 2>(ctx, M, mRw, ddir, dRwe);
+    } sc;
+    if (hipMalloc(&sc.ke, sizeof(double) * (size_t)std::max<int64_t>(nb * ne * ne * dim * dim, 1)) != hipSuccess ||
+        hipMalloc(&sc.rw, sizeof(double) * (size_t)std::max<int64_t>(nb * ne * ne * dim * dw, 1)) != hipSuccess)
+        return fail(KLE_ERR_MEM, "element matrix workspace (%.2f GB) does not fit", nb * per_el / 1e9);
+    KLE_HIP(hipMalloc(&sc.dir, std::max<size_t>(m->dir.size(), 1)));
+    KLE_HIP(hipMemcpyAsync(sc.dir, m->dir.data(), m->dir.size(), hipMemcpyHostToDevice, ctx->stream));
+    if (accum)
+        for (kle_mat *A : {mK, mKr, mRw})
+            KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(A->nvals, 1), ctx->stream));
+    MeshDev M = mesh_dev(m);
+    const uint8_t *ddir = sc.dir;
+    tm.lap("assemble_kle: geometry + scratch");
+    for (int64_t e0 = 0; e0 < std::max<int64_t>(nel, 1); e0 += nb) {
+        const int64_t cnt = std::min(nb, nel - e0), e1 = e0 + std::max<int64_t>(cnt, 0);
+        KLE_TRY(element_batch(ctx, m, S, e0, cnt, sc.ke, sc.rw, nullptr));
+        if (m->kind == 1) {
+            if (dim == 3) {
+                launch_gather_u<3, 3, 0>(ctx, U.dev, mK, ddir, nullptr, sc.ke, e0, e1, accum);
+                launch_gather_u<3, 3, 1>(ctx, U.dev, mKr, ddir, nullptr, sc.ke, e0, e1, accum);
+                launch_gather_u<3, 3, 2>(ctx, U.dev, mRw, ddir, nullptr, sc.rw, e0, e1, accum);
+            } else {
+                launch_gather_u<2, 2, 0>(ctx, U.dev, mK, ddir, nullptr, sc.ke, e0, e1, accum);
+                launch_gather_u<2, 2, 1>(ctx, U.dev, mKr, ddir, nullptr, sc.ke, e0, e1, accum);
+                launch_gather_u<2, 1, 2>(ctx, U.dev, mRw, ddir, nullptr, sc.rw, e0, e1, accum);
+            }
+        } else if (dim == 3) {
+            launch_gather<3, 3, 0>(ctx, M, mK, ddir, sc.ke, e0, e1, accum);
+            launch_gather<3, 3, 1>(ctx, M, mKr, ddir, sc.ke, e0, e1, accum);
+            launch_gather<3, 3, 2>(ctx, M, mRw, ddir, sc.rw, e0, e1, accum);
+        } else {
+            launch_gather<2, 2, 0>(ctx, M, mK, ddir, sc.ke, e0, e1, accum);
+            launch_gather<2, 2, 1>(ctx, M, mKr, ddir, sc.ke, e0, e1, accum);
+            launch_gather<2, 1, 2>(ctx, M, mRw, ddir, sc.rw, e0, e1, accum);
+        }
+        KLE_HIP(hipGetLastError());
     }
-    KLE_HIP(hipGetLastError());
     KLE_HIP(hipStreamSynchronize(ctx->stream));
-    tm.lap("assemble_kle: gathers");
-    hipFree(dKe);
-    hipFree(dRwe);
-    hipFree(ddir);
-    tm.lap("assemble_kle: free element scratch");
+    tm.lap(nbatch > 1 ? "assemble_kle: element batches + gathers" : "assemble_kle: elements + gathers");
     *K = mK;
     *Krhs = mKr;
     *Rw = mRw;
@@ -1594,9 +1780,12 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
     const int dim = m->dim, dw = dim == 2 ? 1 : 3, ds = dim == 2 ? 3 : 6, nc = 1 << dim, G1 = 1 + dim * dim;
     KLE_HIP(hipSetDevice(ctx->device));
     kle_mat *mc = nullptr, *ms = nullptr, *md = nullptr;
-    KLE_TRY(nb_create(ctx, m, 3, dw, dim, &mc));
-    KLE_TRY(nb_create(ctx, m, 3, ds, dim, &ms));
-    KLE_TRY(nb_create(ctx, m, 3, dim, ds, &md));
+    UMeshBuf U;
+    if (m->kind == 1) KLE_TRY(upload_umesh(ctx, m, U));
+    const UMeshDev *Ud = m->kind == 1 ? &U.dev : nullptr;
+    KLE_TRY(nb_create(ctx, m, 3, dw, dim, &mc, Ud));
+    KLE_TRY(nb_create(ctx, m, 3, ds, dim, &ms, Ud));
+    KLE_TRY(nb_create(ctx, m, 3, dim, ds, &md, Ud));
     const int64_t nel = m->elem_end - m->elem_begin, nrows = mc->nrows;
     DevTables T;
     KLE_TRY(upload_tables(ctx, m->ngl, T));
@@ -1624,8 +1813,6 @@ int kle_assemble_operators(kle_ctx *ctx, kle_mesh *m, kle_mat **Curl, kle_mat **
              md->d_rowptr, mc->d_vptr, ms->d_vptr, md->d_vptr, mc->vlayout};
     const unsigned gq = (unsigned)((nq + 255) / 256), gr = (unsigned)((nrows + 255) / 256),
                    gw = (unsigned)((nrows * 64 + 255) / 256);
-    UMeshBuf U;
-    if (m->kind == 1) KLE_TRY(upload_umesh(ctx, m, U));
     if (m->kind == 1 && nq > 0 && nrows > 0) {
         if (dim == 3) {
             hipLaunchKernelGGL(k_geometry<3>, dim3(gq), dim3(256), 0, ctx->stream, nel, m->ngl, T.O, dX, geo);
@@ -1673,12 +1860,15 @@ int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_
     KLE_TRY(kle_assemble_kle(ctx, m, K, Krhs, Rw));
     const int dim = m->dim, dw = dim == 2 ? 1 : 3;
     kle_mat *mf = nullptr, *mr = nullptr, *mw = nullptr, *ms = nullptr, *md = nullptr, *mdf = nullptr;
-    KLE_TRY(nb_create(ctx, m, 4, dim, dim, &mf));
-    KLE_TRY(nb_create(ctx, m, 5, dim, dim, &mr));
-    KLE_TRY(nb_create(ctx, m, 6, dim, dw, &mw));
-    KLE_TRY(nb_create(ctx, m, 3, dim, dim, &ms));
-    KLE_TRY(nb_create(ctx, m, 2, dim, 1, &md));   // Rd: free rows x cell nodes (mat_ns.py:139-141)
-    KLE_TRY(nb_create(ctx, m, 6, dim, 1, &mdf));  // Rdfs: tangential rows x cell nodes (:113-114)
+    UMeshBuf U;
+    if (m->kind == 1) KLE_TRY(upload_umesh(ctx, m, U));
+    const UMeshDev *Ud = m->kind == 1 ? &U.dev : nullptr;
+    KLE_TRY(nb_create(ctx, m, 4, dim, dim, &mf, Ud));
+    KLE_TRY(nb_create(ctx, m, 5, dim, dim, &mr, Ud));
+    KLE_TRY(nb_create(ctx, m, 6, dim, dw, &mw, Ud));
+    KLE_TRY(nb_create(ctx, m, 3, dim, dim, &ms, Ud));
+    KLE_TRY(nb_create(ctx, m, 2, dim, 1, &md, Ud));   // Rd: free rows x cell nodes (mat_ns.py:139-141)
+    KLE_TRY(nb_create(ctx, m, 6, dim, 1, &mdf, Ud));  // Rdfs: tangential rows x cell nodes (:113-114)
     const int rules[5] = {MASK_KFS, MASK_KRHSFS, MASK_TANG_ROWS, MASK_KSUM, MASK_TANG_ROWS};
     kle_mat *all[5] = {mf, mr, mw, ms, mdf};
     for (int t = 0; t < 5; ++t) {
@@ -1695,9 +1885,7 @@ int kle_assemble_ns(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle_
     KLE_HIP(hipMalloc(&dcls, m->dof_cls.size()));
     KLE_HIP(hipMemcpyAsync(dcls, m->dof_cls.data(), m->dof_cls.size(), hipMemcpyHostToDevice, ctx->stream));
     MeshDev M = mesh_dev(m);
-    UMeshBuf U;
     if (m->kind == 1) {
-        KLE_TRY(upload_umesh(ctx, m, U));
         if (dim == 3) {
             launch_gather_u<3, 3, 3>(ctx, U.dev, mf, ddir, dcls, dKe);
             launch_gather_u<3, 3, 4>(ctx, U.dev, mr, ddir, dcls, dKe);

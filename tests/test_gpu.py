@@ -598,3 +598,97 @@ def test_device_pattern_matches_host(pa, lay):
         x = A0.createVecRight()
         x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
         np.testing.assert_array_equal((A0 * x).getArray(), (A1 * x).getArray())
+
+
+@pytest.mark.parametrize("mesh", ["box3", "box2", "umesh3"])
+def test_batched_element_scratch_is_bitwise(pa, mesh, tmp_path):
+    """K / Krhs / Rw assembled in element batches (KLE_ASM_SCRATCH_GB tiny:
+    one element per batch, every gather continuing the stored partial sums)
+    == the single-batch assembly, bitwise."""
+    if mesh == "umesh3":
+        from pynama_amd.meshgen import perturbed_box, write_gmsh
+        V, Cc, F, T = perturbed_box(3, [3, 2, 2], seed=3)
+        msh = str(tmp_path / "b.msh")
+        write_gmsh(msh, 3, V, Cc, F, T)
+        dom_cfg = {"ngl": 4, "gmsh-file": msh}
+        bc = {"custom-func": {"name": "taylor_green3d"}}
+    else:
+        dim = 3 if mesh == "box3" else 2
+        dom_cfg = {"ngl": 5 if dim == 3 else 6, "box-mesh": {"nelem": [3, 2, 3][:dim], "lower": [0] * dim,
+                                                              "upper": [1] * dim}}
+        bc = {"custom-func": {"name": "taylor_green3d" if dim == 3 else "taylor_green"}}
+    out = {}
+    try:
+        for budget in (None, "0.000001"):
+            if budget:
+                os.environ["KLE_ASM_SCRATCH_GB"] = budget
+            d = pa.Domain()
+            d.configure({"domain": dom_cfg, "boundary-conditions": bc})
+            d.setUp()
+            mt = pa.MatFS()
+            mt.setDomain(d)
+            mt.build(buildOperators=False)
+            out[budget] = [A.getValuesCSR() for A in (mt.K, mt.Krhs, mt.Rw)]
+    finally:
+        os.environ.pop("KLE_ASM_SCRATCH_GB", None)
+    for a, b in zip(out[None], out["0.000001"]):
+        for u, v in zip(a, b):
+            np.testing.assert_array_equal(u, v)
+
+
+def test_device_pattern_matches_host_unstructured(pa, tmp_path):
+    """Unstructured meshes: the per-row sort/unique pattern kernel (k_upat) ==
+    the host enumeration, bitwise, for K / Krhs / Rw (boundary and random
+    Dirichlet sets), the operators and the no-slip matrices (2-D wall)."""
+    from pynama_amd.meshgen import perturbed_box, write_gmsh
+    V, Cc, F, T = perturbed_box(3, [3, 3, 2], seed=8)
+    m3 = str(tmp_path / "u3.msh")
+    write_gmsh(m3, 3, V, Cc, F, T)
+    V2, C2, F2, T2 = perturbed_box(2, [4, 3], seed=9)
+    m2 = str(tmp_path / "u2.msh")
+    write_gmsh(m2, 2, V2, C2, F2, T2)
+    rng = np.random.default_rng(21)
+
+    def build_all():
+        out = []
+        d = pa.Domain()
+        d.configure({"domain": {"ngl": 4, "gmsh-file": m3},
+                     "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}})
+        d.setUp()
+        mt = pa.MatFS()
+        mt.setDomain(d)
+        mt.build()
+        op = mt.getOperators()
+        out += [mt.K, mt.Krhs, mt.Rw, op.Curl, op.SrT, op.DivSrT]
+        d = pa.Domain()
+        d.configure({"domain": {"ngl": 3, "gmsh-file": m3},
+                     "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}})
+        d.setUp()
+        N = d.mesh.N
+        d.mesh.set_dirichlet_nodes(np.sort(np.random.default_rng(5).choice(N, N // 4, replace=False)))
+        mt = pa.MatFS()
+        mt.setDomain(d)
+        mt.build(buildOperators=False)
+        out += [mt.K, mt.Krhs, mt.Rw]
+        d = pa.Domain()
+        d.configure({"domain": {"ngl": 4, "gmsh-file": m2}, "boundary-conditions": {"no-slip": {"down": [1, 0]}}})
+        d.setUp()
+        mn = pa.MatNS()
+        mn.setDomain(d)
+        mn.build()
+        out += [mn.K, mn.Krhs, mn.Rw, mn.Kfs, mn.Krhsfs, mn.Rwfs, mn.getKplusKfs(), mn.Rdfs]
+        return out
+
+    built = {}
+    try:
+        for host in (1, 0):
+            os.environ["KLE_HOST_PATTERN"] = str(host)
+            built[host] = build_all()
+    finally:
+        os.environ.pop("KLE_HOST_PATTERN", None)
+    for A0, A1 in zip(built[1], built[0]):
+        for u, v in zip(A0.getValuesCSR(), A1.getValuesCSR()):
+            np.testing.assert_array_equal(u, v)
+        x = A0.createVecRight()
+        x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
+        np.testing.assert_array_equal((A0 * x).getArray(), (A1 * x).getArray())

@@ -1,0 +1,9 @@
+# Full GPU suite, then setup timings of config 4 and the config-5-size unstructured mesh
+source tools/gpu_steps.sh
+rm -f gpurun_out/steps.txt
+step pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread || exit 1
+tail -n 2 gpurun_out/pytest_gpu.log
+KLE_TIMING=1 step bench_cfg4 900 python bench.py --nelem 18,18,18 --ngl 7 --steps 50 --warmup 5 --cpu-seconds 10 || exit 1
+tail -n 1 gpurun_out/bench_cfg4.log | cut -c1-200
+KLE_TIMING=1 step bench_cfg5 900 python bench.py --mesh unstructured --nelem 40,32,32 --steps 50 --warmup 5 --no-cpu-baseline || exit 1
+tail -n 1 gpurun_out/bench_cfg5.log | cut -c1-200
