@@ -314,6 +314,7 @@ def main():
 
     if rank == 0:
         stream = ctx.stream_copy_gbps(1 << 30, 10)
+        stream_rd = ctx.stream_read_gbps(1 << 32, 10)
         line = {
             "metric": METRIC,
             "value": iters_per_s,
@@ -355,6 +356,7 @@ def main():
             "cpu_baseline": cpu,
             "spmv_gbps": achieved,
             "stream_copy_gbps": stream,
+            "stream_read_gbps": stream_rd,  # read-only streaming ceiling (the SpMV is read-dominated)
             "breakdown_ms_per_iter": brk,
             "assembly_s": t_asm,
             "mesh_generation_s": t_mesh,

@@ -203,6 +203,60 @@ __device__ __forceinline__ void store_elem_blocks(int64_t e, int l, int m, int n
     }
 }
 
+// fill_chunk with the index arithmetic hoisted: the 1-D tables (th, tdh:
+// [point][node]) live in LDS and every point / node of the chunk / tile comes
+// pre-decomposed into lattice indices (x | y << 8 | z << 16, -1 outside), so
+// an entry costs a few LDS reads and FMAs instead of six integer divisions
+// and global table loads.  Same arithmetic, same values.
+template <int DIM>
+__device__ __forceinline__ void fill_chunk_lds(int ngl, const double *th, const double *tdh, const int *sq,
+                                               const int *sn, bool scale, double (*sH)[TL], double (*sG)[DIM][TL],
+                                               const double (*sgeo)[1 + DIM * DIM], int tid)
+{
+    for (int it = tid; it < QC * TL; it += 256) {
+        const int qq = it / TL, nl = it % TL;
+        const int qp = sq[qq], lp = sn[nl];
+        double hv = 0, g[DIM] = {};
+        if (qp >= 0 && lp >= 0) {
+            double hh[3], dd[3];
+            for (int d = 0; d < DIM; ++d) {
+                const int t = ((qp >> (8 * d)) & 255) * ngl + ((lp >> (8 * d)) & 255);
+                hh[d] = th[t];
+                dd[d] = tdh[t];
+            }
+            double dref[DIM];
+            if constexpr (DIM == 2) {
+                hv = hh[0] * hh[1];
+                dref[0] = dd[0] * hh[1];
+                dref[1] = hh[0] * dd[1];
+            } else {
+                hv = hh[0] * hh[1] * hh[2];
+                dref[0] = dd[0] * hh[1] * hh[2];
+                dref[1] = hh[0] * dd[1] * hh[2];
+                dref[2] = hh[0] * hh[1] * dd[2];
+            }
+            const double *gq = sgeo[qq];
+            for (int i = 0; i < DIM; ++i) {
+                double s = 0;
+                for (int k = 0; k < DIM; ++k) s += gq[1 + i * DIM + k] * dref[k];
+                g[i] = s;
+            }
+            if (scale) {
+                hv *= gq[0];
+                for (int i = 0; i < DIM; ++i) g[i] *= gq[0];
+            }
+        }
+        sH[qq][nl] = hv;
+        for (int i = 0; i < DIM; ++i) sG[qq][i][nl] = g[i];
+    }
+}
+
+__device__ __forceinline__ int pack_lattice(int v, int n, int dim)
+{
+    const int x = v % n, y = (v / n) % n, z = dim == 3 ? v / (n * n) : 0;
+    return x | (y << 8) | (z << 16);
+}
+
 template <int DIM>
 __global__ __launch_bounds__(256) void k_element(int ngl, Tables1D TF, Tables1D TR,
                                                  const double *__restrict__ geoF,
@@ -338,6 +392,18 @@ __global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tabl
     __shared__ double sHL[QC][TL], sHM[QC][TL];
     __shared__ double sGL[QC][DIM][TL], sGM[QC][DIM][TL];
     __shared__ double sgeo[QC][G1];
+    __shared__ double sTab[4][64];  // full h, dh; reduced h, dh  [point * ngl + node]
+    __shared__ int sLn[TL], sMn[TL], sQ[QC];
+    for (int it = tid; it < 64; it += 256) {
+        sTab[0][it] = it < TF.np1 * ngl ? TF.h[it] : 0.0;
+        sTab[1][it] = it < TF.np1 * ngl ? TF.dh[it] : 0.0;
+        sTab[2][it] = it < TR.np1 * ngl ? TR.h[it] : 0.0;
+        sTab[3][it] = it < TR.np1 * ngl ? TR.dh[it] : 0.0;
+    }
+    if (tid < TL) {
+        sLn[tid] = l0 + tid < ne ? pack_lattice(l0 + tid, ngl, DIM) : -1;
+        sMn[tid] = m0 + tid < ne ? pack_lattice(m0 + tid, ngl, DIM) : -1;
+    }
 
     const dbl4 z4 = {0.0, 0.0, 0.0, 0.0};
     dbl4 G = z4, E[DIM], D[DIM][DIM], F[DIM];
@@ -355,9 +421,10 @@ __global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tabl
             int qq = it / G1, k = it % G1;
             sgeo[qq][k] = (q0 + qq < nqF) ? geoF[(e * nqF + q0 + qq) * G1 + k] : 0.0;
         }
+        if (tid < QC) sQ[tid] = q0 + tid < nqF ? pack_lattice(q0 + tid, TF.np1, DIM) : -1;
         __syncthreads();
-        fill_chunk<DIM>(ngl, ne, nqF, TF, geoF, q0, l0, true, sHL, sGL, sgeo, tid);
-        fill_chunk<DIM>(ngl, ne, nqF, TF, geoF, q0, m0, false, sHM, sGM, sgeo, tid);
+        fill_chunk_lds<DIM>(ngl, sTab[0], sTab[1], sQ, sLn, true, sHL, sGL, sgeo, tid);
+        fill_chunk_lds<DIM>(ngl, sTab[0], sTab[1], sQ, sMn, false, sHM, sGM, sgeo, tid);
         __syncthreads();
         const int qn = min(QC, nqF - q0);
         for (int qq = 0; qq < qn; qq += 4) {
@@ -382,9 +449,10 @@ __global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tabl
             int qq = it / G1, k = it % G1;
             sgeo[qq][k] = (q0 + qq < nqR) ? geoR[(e * nqR + q0 + qq) * G1 + k] : 0.0;
         }
+        if (tid < QC) sQ[tid] = q0 + tid < nqR ? pack_lattice(q0 + tid, TR.np1, DIM) : -1;
         __syncthreads();
-        fill_chunk<DIM>(ngl, ne, nqR, TR, geoR, q0, l0, true, sHL, sGL, sgeo, tid);
-        fill_chunk<DIM>(ngl, ne, nqR, TR, geoR, q0, m0, false, sHM, sGM, sgeo, tid);
+        fill_chunk_lds<DIM>(ngl, sTab[2], sTab[3], sQ, sLn, true, sHL, sGL, sgeo, tid);
+        fill_chunk_lds<DIM>(ngl, sTab[2], sTab[3], sQ, sMn, false, sHM, sGM, sgeo, tid);
         __syncthreads();
         const int qn = min(QC, nqR - q0);
         for (int qq = 0; qq < qn; qq += 4) {
