@@ -345,8 +345,10 @@ def main():
                        "spmv_loads": args.loads, "spmv_fused_dot": args.fused_dot,
                        "parallelism": (f"z-slab x{nranks} (RCCL halo + allreduce)" if mesh_kind == "box" else
                                        f"cell slabs along the most-layered axis x{nranks} (RCCL halo + allreduce)")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+            # N > 1: bytes of all ranks over the slowest rank's SpMV time,
+            # against N x the per-GPU peak
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
+                         "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
                          "kernel": (("k_nb_spmv_fast<3,3,%d,%s,1>" % (args.layout, "true" if K.isStructured() else "false"))
                                     if not args.fused_dot and args.loads == "nt" else
                                     "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
