@@ -38,7 +38,8 @@ namespace kle {
 constexpr double ALPHA_W = 1e2;  // spectral.py:96
 constexpr double ALPHA_D = 1e3;  // spectral.py:97
 constexpr int TL = 32;           // node tile of k_element
-constexpr int QC = 32;           // Gauss points per LDS chunk
+constexpr int QC = 32;           // Gauss points per LDS chunk (k_element)
+constexpr int QM = 16;           // Gauss points per LDS chunk (k_element_mfma: 3 workgroups / CU)
 
 struct Tables1D {
     int np1;          // 1-D points
@@ -208,12 +209,12 @@ __device__ __forceinline__ void store_elem_blocks(int64_t e, int l, int m, int n
 // pre-decomposed into lattice indices (x | y << 8 | z << 16, -1 outside), so
 // an entry costs a few LDS reads and FMAs instead of six integer divisions
 // and global table loads.  Same arithmetic, same values.
-template <int DIM>
+template <int DIM, int NQ = QC>
 __device__ __forceinline__ void fill_chunk_lds(int ngl, const double *th, const double *tdh, const int *sq,
                                                const int *sn, bool scale, double (*sH)[TL], double (*sG)[DIM][TL],
                                                const double (*sgeo)[1 + DIM * DIM], int tid)
 {
-    for (int it = tid; it < QC * TL; it += 256) {
+    for (int it = tid; it < NQ * TL; it += 256) {
         const int qq = it / TL, nl = it % TL;
         const int qp = sq[qq], lp = sn[nl];
         double hv = 0, g[DIM] = {};
@@ -372,8 +373,8 @@ __device__ __forceinline__ dbl4 mfma64(double a, double b, dbl4 c)
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int DIM>
-__global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tables1D TR,
+template <int DIM, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_element_mfma(int ngl, Tables1D TF, Tables1D TR,
                                                       const double *__restrict__ geoF,
                                                       const double *__restrict__ geoR,
                                                       double *__restrict__ Ke, double *__restrict__ Rwe,
@@ -389,11 +390,11 @@ __global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tabl
     const int ls = (wv & 1) * 16, ms = (wv >> 1) * 16;  // this wave's 16x16 sub-tile
     const int li = lane & 15, kq = lane >> 4;
 
-    __shared__ double sHL[QC][TL], sHM[QC][TL];
-    __shared__ double sGL[QC][DIM][TL], sGM[QC][DIM][TL];
-    __shared__ double sgeo[QC][G1];
+    __shared__ double sHL[QM][TL], sHM[QM][TL];
+    __shared__ double sGL[QM][DIM][TL], sGM[QM][DIM][TL];
+    __shared__ double sgeo[QM][G1];
     __shared__ double sTab[4][64];  // full h, dh; reduced h, dh  [point * ngl + node]
-    __shared__ int sLn[TL], sMn[TL], sQ[QC];
+    __shared__ int sLn[TL], sMn[TL], sQ[QM];
     for (int it = tid; it < 64; it += 256) {
         sTab[0][it] = it < TF.np1 * ngl ? TF.h[it] : 0.0;
         sTab[1][it] = it < TF.np1 * ngl ? TF.dh[it] : 0.0;
@@ -416,17 +417,17 @@ __global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tabl
     }
 
     // full integration: G and E (the chunk beyond nq is zero-filled)
-    for (int q0 = 0; q0 < nqF; q0 += QC) {
-        for (int it = tid; it < QC * G1; it += 256) {
+    for (int q0 = 0; q0 < nqF; q0 += QM) {
+        for (int it = tid; it < QM * G1; it += 256) {
             int qq = it / G1, k = it % G1;
             sgeo[qq][k] = (q0 + qq < nqF) ? geoF[(e * nqF + q0 + qq) * G1 + k] : 0.0;
         }
-        if (tid < QC) sQ[tid] = q0 + tid < nqF ? pack_lattice(q0 + tid, TF.np1, DIM) : -1;
+        if (tid < QM) sQ[tid] = q0 + tid < nqF ? pack_lattice(q0 + tid, TF.np1, DIM) : -1;
         __syncthreads();
-        fill_chunk_lds<DIM>(ngl, sTab[0], sTab[1], sQ, sLn, true, sHL, sGL, sgeo, tid);
-        fill_chunk_lds<DIM>(ngl, sTab[0], sTab[1], sQ, sMn, false, sHM, sGM, sgeo, tid);
+        fill_chunk_lds<DIM, QM>(ngl, sTab[0], sTab[1], sQ, sLn, true, sHL, sGL, sgeo, tid);
+        fill_chunk_lds<DIM, QM>(ngl, sTab[0], sTab[1], sQ, sMn, false, sHM, sGM, sgeo, tid);
         __syncthreads();
-        const int qn = min(QC, nqF - q0);
+        const int qn = min(QM, nqF - q0);
         for (int qq = 0; qq < qn; qq += 4) {
             const int q = qq + kq;
             const double ah = sHL[q][ls + li];
@@ -444,17 +445,17 @@ __global__ __launch_bounds__(256) void k_element_mfma(int ngl, Tables1D TF, Tabl
         __syncthreads();
     }
     // reduced integration: D and F
-    for (int q0 = 0; q0 < nqR; q0 += QC) {
-        for (int it = tid; it < QC * G1; it += 256) {
+    for (int q0 = 0; q0 < nqR; q0 += QM) {
+        for (int it = tid; it < QM * G1; it += 256) {
             int qq = it / G1, k = it % G1;
             sgeo[qq][k] = (q0 + qq < nqR) ? geoR[(e * nqR + q0 + qq) * G1 + k] : 0.0;
         }
-        if (tid < QC) sQ[tid] = q0 + tid < nqR ? pack_lattice(q0 + tid, TR.np1, DIM) : -1;
+        if (tid < QM) sQ[tid] = q0 + tid < nqR ? pack_lattice(q0 + tid, TR.np1, DIM) : -1;
         __syncthreads();
-        fill_chunk_lds<DIM>(ngl, sTab[2], sTab[3], sQ, sLn, true, sHL, sGL, sgeo, tid);
-        fill_chunk_lds<DIM>(ngl, sTab[2], sTab[3], sQ, sMn, false, sHM, sGM, sgeo, tid);
+        fill_chunk_lds<DIM, QM>(ngl, sTab[2], sTab[3], sQ, sLn, true, sHL, sGL, sgeo, tid);
+        fill_chunk_lds<DIM, QM>(ngl, sTab[2], sTab[3], sQ, sMn, false, sHM, sGM, sgeo, tid);
         __syncthreads();
-        const int qn = min(QC, nqR - q0);
+        const int qn = min(QM, nqR - q0);
         for (int qq = 0; qq < qn; qq += 4) {
             const int q = qq + kq;
             const double bh = sHM[q][ms + li];
@@ -1176,6 +1177,7 @@ struct ElemSetup {
     int nqF = 0, nqR = 0;
     int64_t nel = 0;
     bool valu = false;
+    int minw = 3;  // k_element_mfma register budget: 3 (default) or 2 waves / SIMD (KLE_ELEMENT_WAVES)
     ~ElemSetup()
     {
         if (dX) (void)hipFree(dX);
@@ -1213,6 +1215,7 @@ static int element_setup(kle_ctx *ctx, const kle_mesh *m, ElemSetup &S)
     // KLE_ELEMENT_VALU=1: the FP64-VALU element kernel instead of the MFMA one
     const char *ev = getenv("KLE_ELEMENT_VALU");
     S.valu = ev && atoi(ev) != 0;
+    if (const char *w = getenv("KLE_ELEMENT_WAVES")) S.minw = atoi(w) == 2 ? 2 : 3;
     return 0;
 }
 
@@ -1223,17 +1226,18 @@ static int element_batch(kle_ctx *ctx, const kle_mesh *m, const ElemSetup &S, in
     const int dim = m->dim, ne = m->nn(), G1 = 1 + dim * dim;
     const double *gF = S.gF + e0 * S.nqF * G1, *gR = S.gR + e0 * S.nqR * G1;
     dim3 eg((ne + TL - 1) / TL, (ne + TL - 1) / TL, (unsigned)cnt);
+#define KLE_ELEM_LAUNCH(KERN) \
+    hipLaunchKernelGGL(KERN, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde)
     if (dim == 2) {
-        if (S.valu)
-            hipLaunchKernelGGL(k_element<2>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
-        else
-            hipLaunchKernelGGL(k_element_mfma<2>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
+        if (S.valu) KLE_ELEM_LAUNCH(k_element<2>);
+        else if (S.minw == 3) KLE_ELEM_LAUNCH((k_element_mfma<2, 3>));
+        else KLE_ELEM_LAUNCH((k_element_mfma<2, 2>));
     } else {
-        if (S.valu)
-            hipLaunchKernelGGL(k_element<3>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
-        else
-            hipLaunchKernelGGL(k_element_mfma<3>, eg, dim3(256), 0, ctx->stream, m->ngl, S.T.F, S.T.R, gF, gR, Ke, Rwe, Rde);
+        if (S.valu) KLE_ELEM_LAUNCH(k_element<3>);
+        else if (S.minw == 3) KLE_ELEM_LAUNCH((k_element_mfma<3, 3>));
+        else KLE_ELEM_LAUNCH((k_element_mfma<3, 2>));
     }
+#undef KLE_ELEM_LAUNCH
     KLE_HIP(hipGetLastError());
     return 0;
 }
