@@ -354,7 +354,13 @@ def main():
                                     "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
                                                                   "true" if args.loads == "nt" else "false")),
                          "bytes_per_launch": tot_bytes,
-                         "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt},
+                         "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
+                         # PMC traffic rate vs this box's measured read-only streaming
+                         # ceiling (per GPU): how close the SpMV is to what HBM delivers here
+                         "read_ceiling_gbps": stream_rd,
+                         "traffic_frac_of_read_ceiling": (traffic / (spmv_avg_max * 1e-3) / 1e9 / stream_rd
+                                                          if traffic and spmv_avg_max > 0 and nranks == 1
+                                                          else None)},
             "cpu_baseline": cpu,
             "spmv_gbps": achieved,
             "stream_copy_gbps": stream,
