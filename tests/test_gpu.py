@@ -731,3 +731,56 @@ def test_graph_replay_matches_stream_launches(pa):
     assert out["1"][0] == out["0"][0] and out["1"][2] == out["0"][2] == 13
     np.testing.assert_array_equal(out["1"][1], out["0"][1])
     np.testing.assert_array_equal(out["1"][3], out["0"][3])
+
+
+def test_config2_full_size_properties(pa):
+    """BASELINE config 2 at full size (1,026,675 DoF, p = 4): size-independent
+    properties of the device-assembled system.  PETSc's nonzero count
+    (SURVEY 8), patterns from the device == the host enumeration (SpMV
+    bitwise equal), symmetry and linearity of K, identity Dirichlet rows, and
+    the Jacobi-CG solve to 1e-10 (true residual)."""
+    cfg = {"domain": {"ngl": 5, "box-mesh": {"nelem": [20, 16, 16], "lower": [0, 0, 0], "upper": [1, 1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    mats = {}
+    try:
+        for host in ("1", "0"):
+            os.environ["KLE_HOST_PATTERN"] = host
+            dom = pa.Domain()
+            dom.configure(cfg)
+            dom.setUp()
+            mat = pa.MatFS()
+            mat.setDomain(dom)
+            mat.build(buildOperators=False)
+            mats[host] = (dom, mat)
+    finally:
+        os.environ.pop("KLE_HOST_PATTERN", None)
+    dom, mat = mats["0"]
+    K = mat.K
+    assert K.getSize()[0] == 1026675
+    assert K.getInfo()["nz_used"] == 561335085
+    assert K.isStructured() and mats["1"][1].K.isStructured()
+    rng = np.random.default_rng(7)
+    x, y = K.createVecRight(), K.createVecRight()
+    xa, ya = rng.uniform(-1, 1, x.getLocalSize()), rng.uniform(-1, 1, y.getLocalSize())
+    x.setArray(xa)
+    y.setArray(ya)
+    for name in ("K", "Krhs", "Rw"):
+        A0, A1 = getattr(mats["1"][1], name), getattr(mat, name)
+        v = A0.createVecRight()
+        v.setArray(rng.uniform(-1, 1, v.getLocalSize()))
+        np.testing.assert_array_equal((A0 * v).getArray(), (A1 * v).getArray())
+    Ax, Ay = K * x, K * y
+    s = x + y
+    np.testing.assert_allclose((K * s).getArray(), Ax.getArray() + Ay.getArray(), rtol=1e-12, atol=1e-9)
+    assert abs(y.dot(Ax) - x.dot(Ay)) <= 1e-12 * abs(y.dot(Ax))
+    bn = np.array(sorted(dom.getNodesDirichlet()))
+    idx = (bn[:, None] * 3 + np.arange(3)).ravel()
+    np.testing.assert_array_equal(Ax.getArray()[idx], xa[idx])
+    ksp = pa.petsc.KSP().create()
+    ksp.setType("cg")
+    ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=20000)
+    ksp.setOperators(K)
+    u = K.createVecRight()
+    ksp.solve(Ax, u)
+    assert ksp.getConvergedReason() > 0
+    assert ksp.getTrueRelativeResidual() <= 2e-10
