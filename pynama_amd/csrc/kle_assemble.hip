@@ -1004,7 +1004,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     tm.lap(on_dev ? "pattern: device row summary" : "pattern: host enumeration");
     int64_t nb = 0;
     for (int64_t i = 0; i < nrows; ++i) nb += info[i].cnt;
-    if (nb >= (1ll << 31) / 1) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
+    if (nb >= (1ll << 31)) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
     const int lay = g_nb_layout;
     const int pad = lay == 1 ? 1 : std::max(1, g_nb_pad);
     std::vector<int> rp32(nrows + 1), cnt(nrows);
@@ -1770,6 +1770,16 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     const int dim = m->dim, dw = dim == 2 ? 1 : 3, ne = m->nn();
     KLE_HIP(hipSetDevice(ctx->device));
     kle_mat *mK = nullptr, *mKr = nullptr, *mRw = nullptr;
+    // on any error below the partially built matrices are released
+    struct Owned {
+        kle_mat **p[3];
+        bool keep = false;
+        ~Owned()
+        {
+            if (!keep)
+                for (auto q : p) kle_mat_destroy(*q);
+        }
+    } owned{{&mK, &mKr, &mRw}};
     PhaseTimer tm(ctx);
     UMeshBuf U;
     if (m->kind == 1) KLE_TRY(upload_umesh(ctx, m, U));
@@ -1839,6 +1849,7 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     }
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     tm.lap(nbatch > 1 ? "assemble_kle: element batches + gathers" : "assemble_kle: elements + gathers");
+    owned.keep = true;
     *K = mK;
     *Krhs = mKr;
     *Rw = mRw;
