@@ -1,0 +1,48 @@
+"""bench.py's output contract (the driver parses this line): one JSON object
+on stdout with the metric / value / roofline / cpu_baseline fields, on a small
+mesh so it runs in seconds."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_line_contract():
+    d = _run("--nelem", "4,4,4", "--ngl", "4", "--steps", "20", "--warmup", "2", "--cpu-seconds", "0.5")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["warmup"] == 2 and d["higher_is_better"] is True
+    assert d["dtype"] == "f64" and d["unit"] == "CG iters/s" and d["value"] > 0
+    assert abs(d["ms_per_step"] - 1e3 / d["value"]) <= 1e-6 * d["ms_per_step"]
+    assert "workload" in d["config"] and "model" not in d["config"]
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["unit"] == d["unit"]
+    s = d["solve"]
+    assert s["reason"] > 0 and s["true_rel_residual"] <= 2e-10
+
+
+def test_bench_unstructured_line():
+    d = _run("--mesh", "unstructured", "--nelem", "3,3,3", "--ngl", "4", "--steps", "10", "--warmup", "1",
+             "--no-cpu-baseline")
+    assert d["config"]["mesh"] == "unstructured" and d["cpu_baseline"] is None and d["value"] > 0
+    assert d["roofline"]["achieved"] > 0
