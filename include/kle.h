@@ -226,6 +226,12 @@ int kle_vec_set_values(kle_vec *v, int64_t n, const int64_t *idx, const double *
 int kle_vec_get_values(const kle_vec *v, int64_t n, const int64_t *idx, double *vals);
 int kle_vec_get_array(const kle_vec *v, double *host_local);     /* owned part */
 int kle_vec_set_array(kle_vec *v, const double *host_local);
+/* petsc4py getArray()/restoreArray pair: kle_vec_get_array copies the owned
+ * part out, kle_vec_restore_array writes a (modified) host copy back. */
+int kle_vec_restore_array(kle_vec *v, const double *host_local);
+/* VecAssemblyBegin/End: set_values writes owned entries immediately, so
+ * assembly only completes the pending device work of the vector's stream. */
+int kle_vec_assemble(kle_vec *v);
 int kle_vec_ghost_update(kle_vec *v);                             /* halo fill  */
 /* raw device pointer to the owned part (for zero-copy interop). */
 int kle_vec_device_ptr(const kle_vec *v, double **dptr);
@@ -267,6 +273,16 @@ int kle_mat_destroy(kle_mat *A);
 int kle_mat_get_size(const kle_mat *A, int64_t *m_global, int64_t *n_global);
 int kle_mat_get_ownership_range(const kle_mat *A, int64_t *lo, int64_t *hi);
 int kle_mat_get_local_nnz(const kle_mat *A, int64_t *nnz);
+/* MatGetInfo (+ sizes): PETSc nonzeros of the owned rows, the storage format
+ * (0 node-block, 1 scalar AIJ), block shape and the SpMV's algorithmic bytes. */
+typedef struct {
+    int64_t m_global, n_global, m_local, n_local;
+    int64_t nz_used;       /* PETSc nonzeros of the owned rows (explicit zeros included) */
+    int format;            /* 0 node-block CSR, 1 scalar AIJ */
+    int block_rows, block_cols;
+    double spmv_bytes;     /* algorithmic bytes of one y = A x on this rank */
+} kle_mat_info;
+int kle_mat_get_info(const kle_mat *A, kle_mat_info *info);
 int kle_mat_mult(kle_mat *A, kle_vec *x, kle_vec *y);            /* y = A x */
 int kle_mat_mult_add(kle_mat *A, kle_vec *x, kle_vec *y, kle_vec *z); /* z = y + A x */
 int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *R);
@@ -329,6 +345,7 @@ int kle_ksp_create(kle_ctx *ctx, kle_ksp **out);
 int kle_ksp_destroy(kle_ksp *k);
 int kle_ksp_set_type(kle_ksp *k, const char *type);      /* "cg" | "gmres" | "preonly" */
 int kle_ksp_set_pc_type(kle_ksp *k, const char *type);   /* "none" | "jacobi" | "lu"   */
+int kle_ksp_set_pc(kle_ksp *k, const char *type);        /* KSPSetPC(PCSetType): same as set_pc_type */
 int kle_ksp_set_tolerances(kle_ksp *k, double rtol, double atol, double dtol, int maxit);
 int kle_ksp_set_gmres_restart(kle_ksp *k, int restart);
 /* CG with one reduction per iteration (Chronopoulos-Gear), as PETSc's

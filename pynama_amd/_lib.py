@@ -105,6 +105,8 @@ _SIGS = {
     "kle_vec_get_values": [vp, C.c_int64, i64p, f64p],
     "kle_vec_get_array": [vp, f64p],
     "kle_vec_set_array": [vp, f64p],
+    "kle_vec_restore_array": [vp, f64p],
+    "kle_vec_assemble": [vp],
     "kle_vec_ghost_update": [vp],
     "kle_vec_device_ptr": [vp, C.POINTER(C.c_void_p)],
     "kle_assemble_kle": [vp, vp, pvp, pvp, pvp],
@@ -119,6 +121,7 @@ _SIGS = {
     "kle_mat_get_size": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "kle_mat_get_ownership_range": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "kle_mat_get_local_nnz": [vp, C.POINTER(C.c_int64)],
+    "kle_mat_get_info": [vp, C.c_void_p],  # kle_mat_info* (MatInfo below)
     "kle_mat_mult": [vp, vp, vp],
     "kle_mat_mult_add": [vp, vp, vp, vp],
     "kle_mat_diagonal_scale": [vp, vp, vp],
@@ -148,6 +151,7 @@ _SIGS = {
     "kle_ksp_destroy": [vp],
     "kle_ksp_set_type": [vp, C.c_char_p],
     "kle_ksp_set_pc_type": [vp, C.c_char_p],
+    "kle_ksp_set_pc": [vp, C.c_char_p],
     "kle_ksp_set_tolerances": [vp, C.c_double, C.c_double, C.c_double, C.c_int],
     "kle_ksp_set_gmres_restart": [vp, C.c_int],
     "kle_ksp_set_fixed_iterations": [vp, C.c_int],
@@ -183,6 +187,13 @@ def load():
     lib.kle_last_error.argtypes = []
     _lib = lib
     return lib
+
+
+class MatInfo(C.Structure):
+    """kle_mat_info (include/kle.h)."""
+    _fields_ = [("m_global", C.c_int64), ("n_global", C.c_int64), ("m_local", C.c_int64),
+                ("n_local", C.c_int64), ("nz_used", C.c_int64), ("format", C.c_int),
+                ("block_rows", C.c_int), ("block_cols", C.c_int), ("spmv_bytes", C.c_double)]
 
 
 def exported_symbols():

@@ -923,6 +923,15 @@ int kle_vec_set_array(kle_vec *v, const double *host)
     return 0;
 }
 
+int kle_vec_restore_array(kle_vec *v, const double *host) { return kle_vec_set_array(v, host); }
+
+int kle_vec_assemble(kle_vec *v)
+{
+    KLE_ARG(v, "null vec");
+    KLE_HIP(hipStreamSynchronize(v->ctx->stream));
+    return 0;
+}
+
 int kle_vec_ghost_update(kle_vec *v)
 {
     KLE_ARG(v, "null vec");

@@ -1087,6 +1087,8 @@ int kle_ksp_set_type(kle_ksp *k, const char *t)
     return 0;
 }
 
+int kle_ksp_set_pc(kle_ksp *k, const char *t) { return kle_ksp_set_pc_type(k, t); }
+
 int kle_ksp_set_pc_type(kle_ksp *k, const char *t)
 {
     KLE_ARG(k && t, "null arg");

@@ -993,6 +993,23 @@ int kle_mat_get_ownership_range(const kle_mat *A, int64_t *lo, int64_t *hi)
     return 0;
 }
 
+int kle_mat_get_info(const kle_mat *A, kle_mat_info *info)
+{
+    KLE_ARG(A && info, "null arg");
+    kle_mat_info r{};
+    r.m_global = A->m_global;
+    r.n_global = A->n_global;
+    r.m_local = A->m_local;
+    r.n_local = A->n_local;
+    KLE_TRY(kle_mat_get_local_nnz(A, &r.nz_used));
+    r.format = A->kind;
+    r.block_rows = A->kind == 0 ? A->R : 1;
+    r.block_cols = A->kind == 0 ? A->C : 1;
+    KLE_TRY(kle_mat_spmv_bytes(A, &r.spmv_bytes));
+    *info = r;
+    return 0;
+}
+
 int kle_mat_get_local_nnz(const kle_mat *A, int64_t *nnz)
 {
     KLE_ARG(A && nnz, "null arg");

@@ -199,7 +199,8 @@ class Vec:
         return out
 
     def assemble(self):
-        pass
+        """VecAssemblyBegin/End: setValues already wrote the owned entries."""
+        call("kle_vec_assemble", self._h)
 
     assemblyBegin = assemble
     assemblyEnd = assemble
@@ -412,12 +413,13 @@ class Mat:
         return buf.value.decode()
 
     def getInfo(self):
-        nz = C.c_int64()
-        call("kle_mat_get_local_nnz", self._h, C.byref(nz))
-        b = C.c_double()
-        call("kle_mat_spmv_bytes", self._h, C.byref(b))
-        return {"nz_used": nz.value, "nz_allocated": nz.value, "nz_unneeded": 0,
-                "spmv_bytes": b.value, "format": self.getFormat()}
+        """MatGetInfo subset (kle_mat_get_info)."""
+        from ._lib import MatInfo
+        inf = MatInfo()
+        call("kle_mat_get_info", self._h, C.byref(inf))
+        return {"nz_used": inf.nz_used, "nz_allocated": inf.nz_used, "nz_unneeded": 0,
+                "spmv_bytes": inf.spmv_bytes, "format": self.getFormat(),
+                "block_size": (inf.block_rows, inf.block_cols)}
 
     def spmvBytes(self):
         b = C.c_double()
