@@ -349,7 +349,8 @@ def main():
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
                          "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
-                         "kernel": (("k_nb_spmv_fast<3,3,%d,%s,1>" % (args.layout, "true" if K.isStructured() else "false"))
+                         "kernel": (("k_nb_spmv_fast<3,3,%d,%s,1,%d>" % (args.layout, "true" if K.isStructured() else "false",
+                                                                          spmv_waves(K, args.layout)))
                                     if not args.fused_dot and args.loads == "nt" else
                                     "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
                                                                   "true" if args.loads == "nt" else "false")),
@@ -378,6 +379,18 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def spmv_waves(K, layout):
+    """Waves per workgroup the default SpMV kernel uses for this rank's K
+    (kle_mat.hip: 8 from 100k node rows up, else 4; KLE_SPMV_WAVES overrides)."""
+    env = int(os.environ.get("KLE_SPMV_WAVES", "0") or 0)
+    if layout != 1:
+        return 4
+    if env in (1, 2, 4, 8, 16):
+        return env
+    lo, hi = K.getOwnershipRange()
+    return 8 if (hi - lo) // 3 >= 100000 else 4
 
 
 def splitmix_uniform(seed, lo, hi):

@@ -172,8 +172,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__
 // LAY 1: while the wave's 64 blocks lie inside the row's full 16-block chunks
 // the RC value loads of a lane share one base address (immediate offsets of
 // 128 B); the last, partial pass uses the packed-tail rule of vofs().
-template <int R, int C, int LAY, bool STRUCT, int UNR>
-__global__ __launch_bounds__(SPMV_BLOCK, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(RowMap rm, const int *__restrict__ rowptr,
+template <int R, int C, int LAY, bool STRUCT, int UNR, int WV = SPMV_WAVES>
+__global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(RowMap rm, const int *__restrict__ rowptr,
                                                              const int *__restrict__ rowcnt,
                                                              const int *__restrict__ rowbox, int lx, int lxy,
                                                              const int64_t *__restrict__ vptr,
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(SPMV_BLOCK, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fa
     if (istate && istate[I_REASON] != 0) return;
     constexpr int RC = R * C;
     const int lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
+    const int64_t r = (int64_t)blockIdx.x * WV + (threadIdx.x >> 6);
     if (r >= rm.na + rm.nb) return;
     const int64_t i = r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
     const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
@@ -655,6 +655,42 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 grid = grid_for(rm.na + rm.nb, rpb, PART_STRIDE - 256);
             }
             if (fast_ok) {
+                // waves per workgroup of the default kernel for the 3x3 node-block
+                // matrices: 8 consecutive rows per workgroup share their x columns in
+                // the CU's L1 -- 2.5 % faster at config 2, 2 % on the unstructured 1M
+                // mesh; 4 stays 0.5 % ahead on small parts (the 1/8 slab), 16 is
+                // slower everywhere (profiles/r01/spmv_waves_ab.jsonl).
+                // KLE_SPMV_WAVES=1/2/4/8/16 overrides.
+                static const int wv_env = [] {
+                    const char *e = getenv("KLE_SPMV_WAVES");
+                    const int w = e ? atoi(e) : 0;
+                    return (w == 1 || w == 2 || w == 4 || w == 8 || w == 16) ? w : 0;
+                }();
+                const int wv = (A->R == 3 && A->C == 3 && A->vlayout == 1)
+                                   ? (wv_env ? wv_env : (A->nrows >= 100000 ? 8 : SPMV_WAVES))
+                                   : SPMV_WAVES;
+                if (wv != SPMV_WAVES) {
+                    const int gw = grid_for(rm.na + rm.nb, wv, 1 << 30);
+                    const bool st = rbox != nullptr;
+#define FAST_W(W)                                                                                               \
+    do {                                                                                                        \
+        if (st)                                                                                                 \
+            hipLaunchKernelGGL((k_nb_spmv_fast<3, 3, 1, true, 1, W>), dim3(gw), dim3(64 * W), 0, c->stream, rm, \
+                               A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
+                               A->d_bcol, A->d_val, x->base, y->d, istate);                                     \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_nb_spmv_fast<3, 3, 1, false, 1, W>), dim3(gw), dim3(64 * W), 0, c->stream, rm, \
+                               A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
+                               A->d_bcol, A->d_val, x->base, y->d, istate);                                     \
+    } while (0)
+                    if (wv == 1) FAST_W(1);
+                    else if (wv == 2) FAST_W(2);
+                    else if (wv == 8) FAST_W(8);
+                    else FAST_W(16);
+#undef FAST_W
+                    KLE_HIP(hipGetLastError());
+                    continue;
+                }
                 const int gf = grid_for(rm.na + rm.nb, SPMV_WAVES, 1 << 30);
                 const int st_ = rbox ? 1 : 0;
 #define FAST_LAUNCH(RR, CC, LY, SS)                                                                     \

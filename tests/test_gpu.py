@@ -770,6 +770,10 @@ def test_config2_full_size_properties(pa):
         v.setArray(rng.uniform(-1, 1, v.getLocalSize()))
         np.testing.assert_array_equal((A0 * v).getArray(), (A1 * v).getArray())
     Ax, Ay = K * x, K * y
+    # the default kernel at this size (8 waves per workgroup) == the generic kernel, bitwise
+    K.setSpmvFast(False)
+    np.testing.assert_array_equal((K * x).getArray(), Ax.getArray())
+    K.setSpmvFast(True)
     s = x + y
     np.testing.assert_allclose((K * s).getArray(), Ax.getArray() + Ay.getArray(), rtol=1e-12, atol=1e-9)
     assert abs(y.dot(Ax) - x.dot(Ay)) <= 1e-12 * abs(y.dot(Ax))
