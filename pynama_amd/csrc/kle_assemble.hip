@@ -4,7 +4,10 @@
 // loop that calls Spectral.getElemKLEMatrices (spectral.py:92-160) and
 // inserts the element blocks with MatSetValues(ADD_VALUES).
 //
-// Three kernels:
+// Kernels (patterns: k_pat_count / k_pat_fill on box meshes, k_upat on
+// unstructured ones; element matrices: k_element_mfma by default, the FP64
+// MFMA form of k_element below; elements are processed in ascending batches
+// bounded by KLE_ASM_SCRATCH_GB):
 //   k_geometry   one thread per (element, Gauss point): Jacobian of the
 //                trilinear map, c_q = w_q det J, inv(J)          (spectral.py:117-120)
 //   k_element    one element x (32x32 node-pair tile) per 256-thread workgroup.
