@@ -383,14 +383,14 @@ def main():
 
 def spmv_waves(K, layout):
     """Waves per workgroup the default SpMV kernel uses for this rank's K
-    (kle_mat.hip: 8 from 100k node rows up, else 4; KLE_SPMV_WAVES overrides)."""
+    (kle_mat.hip: 8 from 64k node rows up, else 4; KLE_SPMV_WAVES overrides)."""
     env = int(os.environ.get("KLE_SPMV_WAVES", "0") or 0)
     if layout != 1:
         return 4
     if env in (1, 2, 4, 8, 16):
         return env
     lo, hi = K.getOwnershipRange()
-    return 8 if (hi - lo) // 3 >= 100000 else 4
+    return 8 if (hi - lo) // 3 >= 64000 else 4
 
 
 def splitmix_uniform(seed, lo, hi):

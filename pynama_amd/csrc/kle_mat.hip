@@ -658,7 +658,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                 // waves per workgroup of the default kernel for the 3x3 node-block
                 // matrices: 8 consecutive rows per workgroup share their x columns in
                 // the CU's L1 -- 2.5 % faster at config 2, 2 % on the unstructured 1M
-                // mesh; 4 stays 0.5 % ahead on small parts (the 1/8 slab), 16 is
+                // mesh, 1 % on its 1/4 part (89k rows); 4 stays 0.5 % ahead on the 1/8 slab (47k), 16 is
                 // slower everywhere (profiles/r01/spmv_waves_ab.jsonl).
                 // KLE_SPMV_WAVES=1/2/4/8/16 overrides.
                 static const int wv_env = [] {
@@ -667,7 +667,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double
                     return (w == 1 || w == 2 || w == 4 || w == 8 || w == 16) ? w : 0;
                 }();
                 const int wv = (A->R == 3 && A->C == 3 && A->vlayout == 1)
-                                   ? (wv_env ? wv_env : (A->nrows >= 100000 ? 8 : SPMV_WAVES))
+                                   ? (wv_env ? wv_env : (A->nrows >= 64000 ? 8 : SPMV_WAVES))
                                    : SPMV_WAVES;
                 if (wv != SPMV_WAVES) {
                     const int gw = grid_for(rm.na + rm.nb, wv, 1 << 30);
