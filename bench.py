@@ -3,11 +3,14 @@ BASELINE.json config 2 workload (3-D KLE Laplacian, structured hex mesh
 [20,16,16], p=4 / ngl=5, ~1M DoF, Taylor-Green-3D Dirichlet data).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
+      (N > 1: starts torch.distributed.run with N ranks itself)
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-A "step" is one CG iteration (SpMV + dot, Jacobi z/p update, x/r
-update, two deterministic reductions) on the assembled device matrix; the
-K steps are timed between barriers, max over ranks.  Assembly (device
+A "step" is one CG iteration on the assembled device matrix (single-
+reduction CG + Jacobi: fused vector update with its dot partials, SpMV with
+the row shares of (u, A u), dot finish + scalar update; pipelined CG on N>1);
+the warm-up solve starts the recurrence and the K timed steps continue it
+(no restart inside the timed region), between barriers, max over ranks.  Assembly (device
 element kernels + gather) is untimed setup.  A full solve to rtol 1e-10 is
 run once for the convergence record.  The roofline uses HIP-event timings of
 the SpMV kernel inside the timed region and the algorithmic bytes of the
@@ -48,8 +51,6 @@ def parse():
     ap.add_argument("--pad", type=int, default=16, help="row padding quantum of layout 0 (blocks)")
     ap.add_argument("--ops", action="store_true",
                     help="also assemble Curl/SrT/DivSrT and time their SpMVs and the evalRHS operator chain")
-    ap.add_argument("--fused-dot", action="store_true", help="form the CG dot inside the SpMV kernel")
-    ap.add_argument("--loads", choices=["nt", "plain"], default="nt", help="SpMV value/column load policy")
     ap.add_argument("--ksp", choices=["auto", "cg", "pipecg"], default="auto",
                     help="auto: single-reduction CG on one GPU, pipelined CG (allreduce beside the SpMV) on N>1")
     ap.add_argument("--classic-cg", action="store_true",
@@ -110,20 +111,83 @@ def bench_operators(pa, mat, ctx, sol, dim, reps=20):
     return out
 
 
+def comm_timeout_s():
+    """Deadline (s) for every rank-to-rank rendezvous: the gloo bootstrap here
+    and ncclCommInitRank inside libkle (KLE_COMM_TIMEOUT_S, default 300)."""
+    return float(os.environ.get("KLE_COMM_TIMEOUT_S", "300"))
+
+
 def init_dist(n):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
+        import datetime
+
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=comm_timeout_s()))
         return dist
-    if n > 1:
-        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
     return None
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, deadline_s=None):
+    """`python bench.py --gpus N` without a torchrun around it: start
+    torch.distributed.run with N ranks (one per GPU, LOCAL_RANK = device) as a
+    child process group, forward rank 0's JSON line, and exit with the
+    children's status.  This process never touches HIP (nothing here imports
+    torch or pynama_amd), and it never exec()s: the ranks are children.  A
+    rank that fails makes torchrun stop the others; a launch that exceeds the
+    deadline (KLE_BENCH_DEADLINE_S, default 1200 s) is killed as a group and
+    exits 124."""
+    import signal
+    import subprocess
+    import threading
+    if deadline_s is None:
+        deadline_s = float(os.environ.get("KLE_BENCH_DEADLINE_S", "1200"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
+    lines = []
+
+    def pump():
+        for ln in proc.stdout:
+            if ln.startswith("{"):
+                lines.append(ln.strip())
+            else:
+                sys.stderr.write(ln)
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    try:
+        rc = proc.wait(timeout=deadline_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        proc.wait()
+        sys.stderr.write(f"bench: {n}-rank launch exceeded {deadline_s:.0f} s, killed\n")
+        return 124
+    t.join(timeout=10)
+    if rc != 0:
+        sys.stderr.write(f"bench: {n}-rank launch failed (exit {rc})\n")
+        return rc
+    if len(lines) != 1:
+        sys.stderr.write(f"bench: expected one JSON line from rank 0, got {len(lines)}\n")
+        return 1
+    print(lines[0], flush=True)
+    return 0
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     dist = init_dist(args.gpus)
     import numpy as np
 
@@ -177,7 +241,6 @@ def main():
     t_setup = time.perf_counter() - t0
 
     K = mat.K
-    K.setSpmvNontemporal(args.loads == "nt")
     n_global = K.getSize()[0]
     info = K.getInfo()
     nnz_local = info["nz_used"]
@@ -205,33 +268,31 @@ def main():
     pc.setType("jacobi")
     kb.setPC(pc)
     kb.setCGSingleReduction(not args.classic_cg)
-    kb.setFusedDot(args.fused_dot)
     kb.setOperators(K)
     kb.setUp()
     x = K.createVecRight()
-    if args.warmup > 0:
-        kb.setFixedIterations(args.warmup)
-        kb.solve(b, x)
-    kb.setFixedIterations(args.steps)
+    # the warm-up solve starts the recurrence (r = b, w = A u, first scalars);
+    # the timed region continues it for exactly `steps` iterations
+    kb.setFixedIterations(max(args.warmup, 1))
+    kb.solve(b, x)
     ctx.set_profiling(True, only="spmv")  # events around the SpMV launches only
     ctx.reset_stats()
     ctx.barrier()
     if dist is not None:
         dist.barrier()
     t_start = time.perf_counter()
-    kb.solve(b, x)
+    kb.solveContinue(b, x, args.steps)
     ctx.barrier()
     t_loc = time.perf_counter() - t_start
     ctx.set_profiling(False)
     spmv_cnt, spmv_ms = ctx.kernel_stats("spmv")
     # per-kernel breakdown from a separate, untimed pass with every launch timed
     nb_its = min(args.steps, 50)
-    kb.setFixedIterations(nb_its)
     ctx.set_profiling(True)
     ctx.reset_stats()
-    kb.solve(b, x)
+    kb.solveContinue(b, x, nb_its)
     ctx.set_profiling(False)
-    brk = {k: ctx.kernel_stats(k)[1] / nb_its for k in ("spmv", "cg_update", "p_update", "dot", "reduce",
+    brk = {k: ctx.kernel_stats(k)[1] / nb_its for k in ("spmv", "cg_update", "p_update", "reduce",
                                                         "halo", "allreduce")}
     t_max = t_loc
     tot_bytes = spmv_bytes_local
@@ -299,7 +360,7 @@ def main():
             tr = json.load(open(args.traffic))
             key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
                    ("chunk" if args.layout == 1 else f"pad{args.pad}") +
-                   f"-{args.loads}-u1" + ("-struct" if K.isStructured() else "") + ("-fused" if args.fused_dot else ""))
+                   "-nt-u1" + ("-struct" if K.isStructured() else ""))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -342,18 +403,14 @@ def main():
                        ("cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)"),
                        "pc": "jacobi", "matrix_format": info["format"], "value_layout": "chunk16+tail" if args.layout == 1 else f"row streams padded to {args.pad}",
                        "structured_columns": K.isStructured(),
-                       "spmv_loads": args.loads, "spmv_fused_dot": args.fused_dot,
                        "parallelism": (f"z-slab x{nranks} (RCCL halo + allreduce)" if mesh_kind == "box" else
                                        f"cell slabs along the most-layered axis x{nranks} (RCCL halo + allreduce)")},
             # N > 1: bytes of all ranks over the slowest rank's SpMV time,
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
                          "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
-                         "kernel": (("k_nb_spmv_fast<3,3,%d,%s,1,%d>" % (args.layout, "true" if K.isStructured() else "false",
-                                                                          spmv_waves(K, args.layout)))
-                                    if not args.fused_dot and args.loads == "nt" else
-                                    "k_nb_spmv<3,3,%s,64,1,%s>" % ("true" if args.fused_dot else "false",
-                                                                  "true" if args.loads == "nt" else "false")),
+                         "kernel": "k_nb_spmv<3,3,%d,%s,%d>" % (args.layout, "true" if K.isStructured() else "false",
+                                                                 spmv_waves(K, args.layout)),
                          "bytes_per_launch": tot_bytes,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
                          # PMC traffic rate vs this box's measured read-only streaming
@@ -383,11 +440,11 @@ def main():
 
 def spmv_waves(K, layout):
     """Waves per workgroup the default SpMV kernel uses for this rank's K
-    (kle_mat.hip: 8 from 64k node rows up, else 4; KLE_SPMV_WAVES overrides)."""
+    (kle_mat.hip: 8 from 64k node rows up, else 4; KLE_SPMV_WAVES=4|8 overrides)."""
     env = int(os.environ.get("KLE_SPMV_WAVES", "0") or 0)
     if layout != 1:
         return 4
-    if env in (1, 2, 4, 8, 16):
+    if env in (4, 8):
         return env
     lo, hi = K.getOwnershipRange()
     return 8 if (hi - lo) // 3 >= 64000 else 4

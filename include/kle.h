@@ -67,6 +67,11 @@ typedef struct kle_mat kle_mat;
 typedef struct kle_ksp kle_ksp;
 
 const char *kle_last_error(void);
+/* Performance knobs for in-process A/B measurements (tools/cg_ab.py); every
+ * value gives correct results.  Keys: "spmv_waves" (0 auto, 4, 8: rows per
+ * SpMV workgroup of 3x3 chunked matrices). */
+int kle_set_tuning(const char *key, int value);
+int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
 
 /* ---------------------------------------------------------------- context */
@@ -298,25 +303,13 @@ int kle_mat_get_row(const kle_mat *A, int64_t row, int64_t *ncols, int64_t *cols
 int kle_mat_get_csr(const kle_mat *A, int64_t *indptr, int64_t *indices, double *data);
 /* Convert (single rank) to the scalar-CSR device format (the AIJ kernel). */
 int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
-/* SpMV kernel variant of a node-block matrix (tuning): lanes per node row
- * (64|32|16), block columns per lane in flight (1|2), persistent grid (0|1). */
-int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent);
-/* Non-temporal (nt) loads for the value/column streams of the node-block SpMV
- * (default on: fastest together with 128-B row padding, profiles/r01). */
-int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt);
-/* SpMV rows per wavefront (3x3 blocks, unfused): > 1 selects the kernel that
- * prefetches the next row's extent while streaming the current row. */
-int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq);
 /* Structured columns: when every row's columns form a lattice box (K, Rw and
  * the operators on box meshes) the SpMV computes them from 8 B per row instead
  * of streaming 4 B per block (default on; 0 forces the column stream). */
 int kle_mat_set_spmv_structured(kle_mat *A, int on);
 int kle_mat_is_structured(const kle_mat *A, int *on);
-/* 1 (default): the default SpMV variant runs the kernel specialised on layout
- * and structured columns; 0: the generic kernel (same results, bitwise). */
-int kle_mat_set_spmv_fast(kle_mat *A, int on);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
- * flight on a second stream (default on; needs the unfused CG dot). */
+ * flight on a second stream (default on). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);
 /* Row padding quantum (in blocks) of node-block matrices created afterwards:
  * every value stream of a row starts on a multiple of `quantum` doubles
@@ -329,12 +322,6 @@ int kle_get_nb_pad(void);
  * per-stream padding). */
 int kle_set_nb_layout(int layout);
 int kle_get_nb_layout(void);
-/* Buffer-descriptor SpMV variants (cache-policy study): 0 off, 1 aux 0, 2 nt,
- * 3 sc0|nt, 4 sc1, 5 sc1|nt, 6 sc1|sc0|nt, 7 sc1|sc0, 8 nt with the x gather
- * dropped (timing diagnostic only: wrong results). */
-int kle_mat_set_spmv_buffer_variant(kle_mat *A, int variant);
-/* Row -> workgroup mapping: XCD-contiguous chunks (0|1), (x,y)-tiled row order (0|1). */
-int kle_mat_set_spmv_layout(kle_mat *A, int xcd_chunks, int tiled_order);
 /* "nb" (node-block) or "aij". */
 int kle_mat_get_format(const kle_mat *A, char *buf, int buflen);
 /* Bytes one SpMV with this matrix moves (algorithmic: matrix + x + y). */
@@ -351,11 +338,12 @@ int kle_ksp_set_gmres_restart(kle_ksp *k, int restart);
 /* CG with one reduction per iteration (Chronopoulos-Gear), as PETSc's
  * -ksp_cg_single_reduction. */
 int kle_ksp_set_cg_single_reduction(kle_ksp *k, int flag);
-/* 1: the CG dot (p, Ap) is formed inside the SpMV kernel; 0 (default): by a
- * separate streaming pass over p and Ap after a plain SpMV. */
-int kle_ksp_set_fused_dot(kle_ksp *k, int flag);
 /* Run exactly n iterations, no convergence test (benchmarks); 0 = off. */
 int kle_ksp_set_fixed_iterations(kle_ksp *k, int n);
+/* Benchmarks: n more iterations of the preceding fixed-iteration solve's
+ * recurrence on the same (b, x) -- no restart (single-reduction / pipelined
+ * CG), so a timed region holds exactly n iterations. */
+int kle_ksp_continue(kle_ksp *k, kle_vec *b, kle_vec *x, int n);
 int kle_ksp_set_operators(kle_ksp *k, kle_mat *A);
 int kle_ksp_set_up(kle_ksp *k);
 int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x);

@@ -52,6 +52,8 @@ class HostComm(C.Structure):
 _SIGS = {
     "kle_version": [],
     "kle_get_unique_id": [C.c_char_p],
+    "kle_set_tuning": [C.c_char_p, C.c_int],
+    "kle_get_tuning": [C.c_char_p, C.POINTER(C.c_int)],
     "kle_ctx_create": [C.c_int, C.c_int, C.c_int, C.c_char_p, pvp],
     "kle_ctx_create_host_comm": [C.c_int, C.c_int, C.c_int, C.POINTER(HostComm), pvp],
     "kle_ctx_destroy": [vp],
@@ -132,19 +134,13 @@ _SIGS = {
     "kle_mat_get_row": [vp, C.c_int64, C.POINTER(C.c_int64), vp, vp],
     "kle_mat_get_csr": [vp, i64p, i64p, f64p],
     "kle_mat_convert_aij": [vp, pvp],
-    "kle_mat_set_spmv_variant": [vp, C.c_int, C.c_int, C.c_int],
-    "kle_mat_set_spmv_layout": [vp, C.c_int, C.c_int],
-    "kle_mat_set_spmv_buffer_variant": [vp, C.c_int],
     "kle_set_nb_pad": [C.c_int],
     "kle_mat_set_halo_overlap": [vp, C.c_int],
     "kle_mat_set_spmv_structured": [vp, C.c_int],
-    "kle_mat_set_spmv_fast": [vp, C.c_int],
     "kle_mat_is_structured": [vp, C.POINTER(C.c_int)],
-    "kle_mat_set_spmv_rows_per_wave": [vp, C.c_int],
     "kle_get_nb_pad": [],
     "kle_set_nb_layout": [C.c_int],
     "kle_get_nb_layout": [],
-    "kle_mat_set_spmv_nontemporal": [vp, C.c_int],
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],
     "kle_mat_spmv_bytes": [vp, C.POINTER(C.c_double)],
     "kle_ksp_create": [vp, pvp],
@@ -155,8 +151,8 @@ _SIGS = {
     "kle_ksp_set_tolerances": [vp, C.c_double, C.c_double, C.c_double, C.c_int],
     "kle_ksp_set_gmres_restart": [vp, C.c_int],
     "kle_ksp_set_fixed_iterations": [vp, C.c_int],
+    "kle_ksp_continue": [vp, vp, vp, C.c_int],
     "kle_ksp_set_cg_single_reduction": [vp, C.c_int],
-    "kle_ksp_set_fused_dot": [vp, C.c_int],
     "kle_ksp_set_operators": [vp, vp],
     "kle_ksp_set_up": [vp],
     "kle_ksp_solve": [vp, vp, vp],

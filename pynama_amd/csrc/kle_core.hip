@@ -6,6 +6,10 @@
 // setValues+assemble (boundary_conditions.py:252-260), reciprocal
 // (mat_fs.py:256), dot/norm (base_problem.py:334,389).
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -13,6 +17,9 @@
 #include "kle_internal.hpp"
 
 namespace kle {
+
+Tuning g_tune;
+
 
 static thread_local std::string g_err;
 
@@ -262,7 +269,7 @@ static int stage_reserve(kle_ctx *ctx, int64_t n)
 
 int allreduce_sum(kle_ctx *ctx, double *dbuf, int n, hipStream_t st)
 {
-    if (ctx->nranks == 1) return 0;
+    if (ctx->nranks == 1 && !ctx->comm) return 0;
     if (!st) st = ctx->stream;
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("allreduce", &ev, st));
@@ -492,6 +499,28 @@ int kle_ctx::resolve_stats()
 extern "C" {
 
 const char *kle_last_error(void) { return g_err.c_str(); }
+
+int kle_set_tuning(const char *key, int value)
+{
+    KLE_ARG(key, "null key");
+    const std::string k(key);
+    if (k == "spmv_waves") {
+        KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
+        g_tune.spmv_waves = value;
+    } else {
+        return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
+    }
+    return 0;
+}
+
+int kle_get_tuning(const char *key, int *value)
+{
+    KLE_ARG(key && value, "null arg");
+    const std::string k(key);
+    if (k == "spmv_waves") *value = g_tune.spmv_waves;
+    else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
+    return 0;
+}
 int kle_version(void) { return 1; }
 
 int kle_get_unique_id(unsigned char out[128])
@@ -538,18 +567,64 @@ static int ctx_init(int device, int rank, int nranks, kle_ctx **out)
     return 0;
 }
 
+// ncclCommInitRank blocks until every rank has joined; a rank that died
+// before joining would hang this one (and the 8-GPU bench) for ever.  Run the
+// init on a helper thread and give up after KLE_COMM_TIMEOUT_S seconds
+// (default 300): the caller gets KLE_ERR_COMM and exits non-zero; the helper
+// is left blocked (the process is about to end).
+static int comm_init_deadline(kle_ctx *c, int nranks, const ncclUniqueId &id, int rank)
+{
+    struct Job {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false;
+        ncclComm_t comm = nullptr;
+        ncclResult_t r = ncclInternalError;
+    };
+    auto job = std::make_shared<Job>();
+    const int device = c->device;
+    std::thread th([job, device, nranks, id, rank]() {
+        ncclComm_t comm = nullptr;
+        ncclResult_t r = ncclInternalError;
+        if (hipSetDevice(device) == hipSuccess) r = ncclCommInitRank(&comm, nranks, id, rank);
+        std::lock_guard<std::mutex> lk(job->mu);
+        job->comm = comm;
+        job->r = r;
+        job->done = true;
+        job->cv.notify_all();
+    });
+    const char *e = getenv("KLE_COMM_TIMEOUT_S");
+    const double tmo = e && atof(e) > 0 ? atof(e) : 300.0;
+    bool done;
+    {
+        std::unique_lock<std::mutex> lk(job->mu);
+        done = job->cv.wait_for(lk, std::chrono::duration<double>(tmo), [&] { return job->done; });
+    }
+    if (!done) {
+        th.detach();
+        return fail(KLE_ERR_COMM, "ncclCommInitRank (rank %d of %d) did not complete within %.0f s "
+                    "(KLE_COMM_TIMEOUT_S): a peer never joined", rank, nranks, tmo);
+    }
+    th.join();
+    if (job->r != ncclSuccess) return fail(KLE_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(job->r));
+    c->comm = job->comm;
+    return 0;
+}
+
 int kle_ctx_create(int device, int rank, int nranks, const unsigned char *unique_id, kle_ctx **out)
 {
     KLE_ARG(nranks == 1 || unique_id, "nranks > 1 needs an RCCL unique id");
     kle_ctx *c;
     KLE_TRY(ctx_init(device, rank, nranks, &c));
-    if (nranks > 1) {
+    // nranks == 1 with an id: a one-rank communicator, so the RCCL calls of
+    // the solver (allreduce on the compute / comm streams) run on one GPU too
+    if (unique_id) {
         ncclUniqueId id;
         memcpy(&id, unique_id, 128);
-        ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
-        if (r != ncclSuccess) {
+        int rc = comm_init_deadline(c, nranks, id, rank);
+        if (rc) {
             kle_ctx_destroy(c);
-            return fail(KLE_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+            return rc;
         }
     }
     *out = c;

@@ -80,8 +80,10 @@ enum Scal {
     S_TMP0, S_TMP1
 };
 // Device integer state: [0] reason (0 iterating), [1] iterations done,
-// [2] fixed-iteration mode, [3] maxit.
-enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_COUNT = 8 };
+// [2] fixed-iteration mode, [3] maxit, [4] arrival ticket of the fused
+// dot + reduction kernel (zeroed with the rest at every solve start, reset
+// by its last-arriving workgroup).
+enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_TICKET, I_COUNT = 8 };
 
 }  // namespace kle
 
@@ -186,15 +188,8 @@ struct kle_vec {
 struct kle_mat {
     kle_ctx *ctx = nullptr;
     int kind = 0;  // 0 node-block, 1 scalar AIJ
-    int spmv_lpr = 64, spmv_unroll = 1, spmv_persistent = 0;  // SpMV kernel variant (profiles/r01/spmv_ab.jsonl)
-    int spmv_nt = 1;
-    int spmv_seq = 1;              // rows per wavefront (k_nb_spmv_seq when > 1)
     int halo_overlap = 1;          // N>1: interior rows run while the halo is in flight
-    int64_t int_lo = 0, int_hi = 0;  // rows [int_lo, int_hi) read no ghost entries  // non-temporal value/column loads (fastest with padded rows: profiles/r01)
-    int spmv_xcd = 0;          // XCD-chunked workgroup -> row mapping
-    int spmv_buf = 0;          // buffer-load variant (0 off; cache-policy experiments)
-    int spmv_order = 0;        // 0 natural row order, 1 (x,y)-tiled z-columns
-    int *d_order = nullptr;    // processing order of node rows (spmv_order 1)
+    int64_t int_lo = 0, int_hi = 0;  // rows [int_lo, int_hi) read no ghost entries
     int64_t row_lat[3] = {1, 1, 1};  // lattice of the owned rows (x, y, z extents)
     int64_t m_global = 0, n_global = 0, m_local = 0, n_local = 0, row_lo = 0, col_lo = 0;
     // ---- node-block (kind 0)
@@ -216,7 +211,6 @@ struct kle_mat {
     int *d_rowbox = nullptr;
     int64_t box_lx = 0, box_lxy = 0;
     int spmv_struct = 1;  // use d_rowbox when present
-    int spmv_fast = 1;    // specialised default kernel (k_nb_spmv_fast) when the variant allows
     int64_t nblocks_real = 0;
     int pad = 1;
     int *d_bcol = nullptr;     // [nblocks] local ext node index
@@ -259,12 +253,18 @@ int allgather_i64(kle_ctx *ctx, int64_t mine, std::vector<int64_t> &all);
 int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi,
                   int lo_rank, int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t s = nullptr,
                   const HaloPlan *plan = nullptr);
-int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials,
-         int *nparts, const int *istate);
-// true when spmv(A, x, ...) without a fused dot exchanges the halo on ctx->comm_stream
+// y = A x; istate (may be null): no-op once the Krylov reason word is set
+int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
+// true when spmv(A, x, ...) exchanges the halo on ctx->comm_stream
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
+// Performance knobs (kle_set_tuning): every setting gives correct results;
+// they exist for in-process A/B measurements (tools/cg_ab.py).
+struct Tuning {
+    int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
+};
+extern Tuning g_tune;
 extern int g_nb_pad;
 extern int g_nb_layout;  // value layout of new node-block matrices (kle_mat.vlayout)
 extern int g_partitioner;  // unstructured meshes: 0 inertial bisection, 1 slabs (kle_umesh.cpp)

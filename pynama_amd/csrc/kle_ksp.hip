@@ -9,10 +9,12 @@
 //   * convergence is decided on the device: the scalar kernel sets a reason
 //     word and every later kernel of the solve turns into a no-op, so the
 //     host only polls every few iterations and the iteration count is exact;
-//   * the dot(p, A p) partials are fused into the SpMV epilogue, the x/r
-//     update and the r.z / r.r partials are one kernel;
-//   * deterministic two-stage reductions (per-workgroup partials, fixed-order
-//     final sum), RCCL allreduce of the 1-2 scalars across ranks.
+//   * the vector update and its dot partials are one kernel; the dot with the
+//     SpMV output, the fixed-order final sums and the scalar update are one
+//     more (k_dot_finish, last-arriving workgroup): three launches per
+//     single-reduction CG iteration;
+//   * deterministic reductions (per-workgroup partials, fixed-order final
+//     sum), RCCL allreduce of the 1-3 scalars across ranks.
 // PC lu (and KSP preonly) are a dense rocSOLVER factorization for the
 // small sequential systems the reference's own cases use (config 1).
 // GMRES(m) (classical Gram-Schmidt, right Jacobi preconditioning) is the
@@ -245,7 +247,9 @@ __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, doubl
         if (ist[I_REASON] != 0) return;
         const int its = ++ist[I_ITS];
         if (ist[I_FIXED]) {
-            if (its >= ist[I_FIXED]) ist[I_REASON] = KLE_CONVERGED_ITS;
+            // fixed iterations: the host launches exactly I_FIXED of them, so no
+            // kernel has to stop; the recurrence stays complete for kle_ksp_continue
+            if (!isfinite(rn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
         } else if (!isfinite(rn)) {
             ist[I_REASON] = KLE_DIVERGED_NANORINF;
             return;
@@ -305,7 +309,7 @@ __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, doubl
     const int its = ++ist[I_ITS];
     const double rn = sqrt(rr);
     if (ist[I_FIXED]) {
-        if (its >= ist[I_FIXED]) ist[I_REASON] = KLE_CONVERGED_ITS;
+        if (!isfinite(rn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
         return;
     }
     if (!isfinite(rn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
@@ -343,19 +347,120 @@ __global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict_
     if (fuse && threadIdx.x == 0) cg_scalars(stage, scal, ist, rtol, atol);
 }
 
-// partials[blockIdx] = sum x.y over this block's grid-stride slice; no-op once converged
-__global__ __launch_bounds__(KB) void k_dot_part(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
-                                                 double *__restrict__ partials, const int *__restrict__ istate)
-{
-    if (istate && istate[I_REASON] != 0) return;
-    double s[1] = {0.0};
-    for (int64_t i = blockIdx.x * (int64_t)KB + threadIdx.x; i < n; i += (int64_t)gridDim.x * KB) s[0] += x[i] * y[i];
-    block_sums<1>(s, partials, 0);
-}
-
 __global__ void k_scalars(double *scal, int *ist, int stage, double rtol, double atol)
 {
     cg_scalars(stage, scal, ist, rtol, atol);
+}
+
+// Dot + reduction + scalar update in one launch: each workgroup forms its
+// slice of (x, y) (FIN_UNR independent loads in flight per thread) and of the
+// preceding update kernel's NQ0 partial arrays; the last-arriving workgroup
+// sums the per-workgroup partials in a fixed order and (one rank) applies the
+// stage's scalar update.  Replaces a dot pass + two reduction launches.
+// Measured against forming per-row shares of (x, A x) in the SpMV epilogue
+// (8 B per row instead of the 16-B-per-entry pass here): the epilogue slowed
+// the SpMV by 1.3 % at config 2 and tied on the 1/8 slab (tools/cg_ab.py,
+// profiles/r02/cg_ab_rowdot_*.jsonl); 64x1024 / 128x512 shapes were no faster.
+// Hand-off (cdna_hip_programming.md §6 G16, counter form): partials stored
+// write-through (agent-scope atomic store = sc1), the storing wave drains
+// vmcnt, relaxed agent fetch_add on the ticket; the last arriver takes one
+// agent acquire and reads this launch's partials with sc1 loads.  The sum
+// order depends only on the sizes, never on which workgroup arrives last:
+// bitwise deterministic.
+constexpr int FIN_BLOCKS = 256;   // workgroups
+constexpr int FIN_THREADS = 256;  // threads per workgroup
+constexpr int FIN_UNR = 4;
+constexpr int FIN_OFF = PART_STRIDE / 2;  // this launch's per-workgroup partials, slot q
+template <int NQ0, int NT>
+__global__ __launch_bounds__(NT) void k_dot_finish(int64_t n, const double *__restrict__ vx,
+                                                   const double *__restrict__ vy,
+                                                   double *__restrict__ partials, int np0, double *__restrict__ scal,
+                                                   int *__restrict__ ist, int stage, int fuse, double rtol,
+                                                   double atol)
+{
+    if (stage != ST_SR_START && stage != ST_START && ist[I_REASON] != 0) return;
+    constexpr int NQ = NQ0 + 1;
+    __shared__ double lds[NQ][NT / 64];
+    __shared__ int last;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double s[NQ];
+    // this workgroup's slice of (x, y): FIN_UNR independent load pairs in
+    // flight per thread (a grid-stride loop of single loads is latency bound)
+    {
+        double acc = 0.0;
+        const int64_t stride = (int64_t)gridDim.x * NT;
+        for (int64_t i0 = blockIdx.x * (int64_t)NT + threadIdx.x; i0 < n; i0 += stride * FIN_UNR) {
+            double v[FIN_UNR];
+#pragma unroll
+            for (int u = 0; u < FIN_UNR; ++u)
+                v[u] = i0 + u * stride < n ? vx[i0 + u * stride] * vy[i0 + u * stride] : 0.0;
+#pragma unroll
+            for (int u = 0; u < FIN_UNR; ++u) acc += v[u];
+        }
+        s[NQ0] = acc;
+    }
+    // and its slice of the update kernel's partials (visible across the launch boundary)
+    const int chunk = (np0 + (int)gridDim.x - 1) / (int)gridDim.x;
+#pragma unroll
+    for (int q = 0; q < NQ0; ++q) {
+        double acc = 0.0;
+        for (int i = threadIdx.x; i < chunk; i += NT) {
+            const int j = blockIdx.x * chunk + i;
+            if (j < np0) acc += partials[q * PART_STRIDE + j];
+        }
+        s[q] = acc;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] = wsum2(s[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) lds[q][w] = s[q];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            double t = 0.0;
+#pragma unroll
+            for (int i = 0; i < NT / 64; ++i) t += lds[q][i];
+            __hip_atomic_store(partials + q * PART_STRIDE + FIN_OFF + blockIdx.x, t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int tk = __hip_atomic_fetch_add(ist + I_TICKET, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = tk == (int)gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    // last arriver: the per-workgroup partials of this launch (sc1 loads), fixed order
+    const int G = (int)gridDim.x;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        double t = 0.0;
+        for (int i = threadIdx.x; i < G; i += NT)
+            t += __hip_atomic_load(partials + q * PART_STRIDE + FIN_OFF + i, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        s[q] = wsum2(t);
+    }
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) lds[q][w] = s[q];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            double u = 0.0;
+#pragma unroll
+            for (int i = 0; i < NT / 64; ++i) u += lds[q][i];
+            scal[S_SUM0 + q] = u;
+        }
+        if (fuse) cg_scalars(stage, scal, ist, rtol, atol);
+        __hip_atomic_store(ist + I_TICKET, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __global__ void k_invert_diag(int64_t n, const double *__restrict__ d, double *__restrict__ dinv)
@@ -439,7 +544,7 @@ struct kle_ksp {
     kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
     kle_vec *m = nullptr, *nv = nullptr, *z = nullptr;  // pipelined CG
     int single_reduction = 0;
-    int fused_dot = 0;  // 1: SpMV also forms the dot with its input (DOT variant)
+    const kle_vec *last_b = nullptr, *last_x = nullptr;  // last fixed-iteration solve (kle_ksp_continue)
     std::vector<kle_vec *> V;  // GMRES basis
     double **d_Vptr = nullptr;
     double *d_h = nullptr;
@@ -543,23 +648,6 @@ __global__ __launch_bounds__(1024) void k_reduce_l1(double *__restrict__ partial
     }
 }
 
-// y = A x and partials of (x, y): fused into the SpMV (DOT variant) or as a
-// separate streaming pass over x and y (cheaper on gfx950: profiles/r01)
-static int spmv_dot(kle_ksp *k, kle_vec *x, kle_vec *y, double *partials, int *np, const int *istate)
-{
-    if (k->fused_dot) return spmv(k->A, x, y, x, partials, np, istate);
-    KLE_TRY(spmv(k->A, x, y, nullptr, nullptr, nullptr, istate));
-    kle_ctx *c = k->ctx;
-    const int g = grid_for(x->n_local, KB, RED_BLOCKS);
-    std::pair<hipEvent_t, hipEvent_t> ev;
-    KLE_TRY(c->tic("dot", &ev));
-    hipLaunchKernelGGL(k_dot_part, dim3(g), dim3(KB), 0, c->stream, x->n_local, x->d, y->d, partials, istate);
-    KLE_HIP(hipGetLastError());
-    KLE_TRY(c->toc("dot", &ev));
-    *np = g;
-    return 0;
-}
-
 static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage, hipStream_t st = nullptr)
 {
     kle_ctx *c = k->ctx;
@@ -576,7 +664,7 @@ static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage, hipStream_t st
         parts = c->d_partials + PART2_OFF;
         for (int q = 0; q < nq; ++q) np.n[q] = PART2_N;
     }
-    const int fuse = c->nranks == 1;
+    const int fuse = c->nranks == 1 && !c->comm;
     hipLaunchKernelGGL(k_reduce_stage, dim3(1), dim3(1024), 0, st, parts, np, nq, c->d_scal,
                        c->d_istate, stage, fuse, k->rtol, k->atol);
     KLE_HIP(hipGetLastError());
@@ -584,6 +672,33 @@ static int reduce_stage(kle_ksp *k, NParts np, int nq, int stage, hipStream_t st
     if (!fuse) {
         KLE_TRY(allreduce_sum(c, c->d_scal + S_SUM0, nq, st));
         hipLaunchKernelGGL(k_scalars, dim3(1), dim3(1), 0, st, c->d_scal, c->d_istate, stage, k->rtol, k->atol);
+        KLE_HIP(hipGetLastError());
+    }
+    return 0;
+}
+
+// y = A x, then k_dot_finish: (x, y) + the NQ0 update-kernel sums + the
+// scalar stage.  On N ranks (or a one-rank RCCL communicator) the raw sums
+// are allreduced and the scalar stage runs behind them.
+static int spmv_finish(kle_ksp *k, kle_vec *x, kle_vec *y, int nq0, int np0, int stage, const int *istate)
+{
+    kle_ctx *c = k->ctx;
+    KLE_TRY(spmv(k->A, x, y, istate));
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(c->tic("reduce", &ev));
+    const int fuse = c->nranks == 1 && !c->comm;
+    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, FIN_BLOCKS);
+    if (nq0 == 2)
+        hipLaunchKernelGGL((k_dot_finish<2, FIN_THREADS>), dim3(g), dim3(FIN_THREADS), 0, c->stream, x->n_local, x->d,
+                           y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol);
+    else
+        hipLaunchKernelGGL((k_dot_finish<0, FIN_THREADS>), dim3(g), dim3(FIN_THREADS), 0, c->stream, x->n_local, x->d,
+                           y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol);
+    KLE_HIP(hipGetLastError());
+    KLE_TRY(c->toc("reduce", &ev));
+    if (!fuse) {
+        KLE_TRY(allreduce_sum(c, c->d_scal + S_SUM0, nq0 + 1));
+        hipLaunchKernelGGL(k_scalars, dim3(1), dim3(1), 0, c->stream, c->d_scal, c->d_istate, stage, k->rtol, k->atol);
         KLE_HIP(hipGetLastError());
     }
     return 0;
@@ -603,7 +718,7 @@ static int true_residual(kle_ksp *k, kle_vec *b, kle_vec *x)
     kle_ctx *c = k->ctx;
     // q = A x ; q = b - q ; ||q|| / ||b||
     KLE_HIP(hipMemcpyAsync(k->p->d, x->d, sizeof(double) * x->n_local, hipMemcpyDeviceToDevice, c->stream));
-    KLE_TRY(spmv(k->A, k->p, k->q, nullptr, nullptr, nullptr, nullptr));
+    KLE_TRY(spmv(k->A, k->p, k->q, nullptr));
     hipLaunchKernelGGL(k_bmy, dim3(grid_for(b->n_local, KB, RED_BLOCKS)), dim3(KB), 0, c->stream, b->n_local, b->d,
                        k->q->d);
     KLE_HIP(hipGetLastError());
@@ -643,9 +758,7 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
                                c->d_istate);
         KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("p_update", &ev));
-        int np = 0;
-        KLE_TRY(spmv_dot(k, k->p, k->q, c->d_partials, &np, c->d_istate));
-        KLE_TRY(reduce_stage(k, NParts{{np, 0, 0, 0}}, 1, ST_ALPHA));
+        KLE_TRY(spmv_finish(k, k->p, k->q, 0, 0, ST_ALPHA, c->d_istate));
         KLE_TRY(c->tic("cg_update", &ev));
         if (jac)
             hipLaunchKernelGGL(k_cg_update<true>, dim3(g), dim3(KB), 0, c->stream, n, k->p->d, k->q->d, dinv, x->d,
@@ -664,7 +777,7 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(poll_state(k));
     k->its = c->h_istate[I_ITS];
     k->reason = c->h_istate[I_REASON];
-    if (k->reason == 0) k->reason = KLE_DIVERGED_ITS;
+    if (k->reason == 0) k->reason = k->fixed ? KLE_CONVERGED_ITS : KLE_DIVERGED_ITS;
     k->rnorm = std::sqrt(c->h_scal[S_RR]);
     return 0;
 }
@@ -672,7 +785,8 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
 // Chronopoulos-Gear CG (PETSc -ksp_cg_single_reduction): one fused update
 // kernel + one SpMV (with fused (w,u)) + one reduction (three sums) per
 // iteration -> one allreduce per iteration across ranks.
-static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
+// cont: continue the previous fixed-iteration solve's recurrence (no start)
+static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
 {
     kle_ctx *c = k->ctx;
     const int64_t n = b->n_local;
@@ -681,16 +795,16 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
     const int g = grid_for(n, KB, RED_BLOCKS);
     int host_fixed[I_COUNT] = {0, 0, k->fixed, k->fixed ? k->fixed : k->maxit, 0, 0, 0, 0};
     KLE_HIP(hipMemcpyAsync(c->d_istate, host_fixed, sizeof(int) * I_COUNT, hipMemcpyHostToDevice, c->stream));
-    if (jac)
-        hipLaunchKernelGGL(k_sr_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
-                           k->p->d, k->s->d, c->d_partials);
-    else
-        hipLaunchKernelGGL(k_sr_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
-                           k->p->d, k->s->d, c->d_partials);
-    KLE_HIP(hipGetLastError());
-    int np = 0;
-    KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, nullptr));
-    KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR_START));
+    if (!cont) {
+        if (jac)
+            hipLaunchKernelGGL(k_sr_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d,
+                               k->u->d, k->p->d, k->s->d, c->d_partials);
+        else
+            hipLaunchKernelGGL(k_sr_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d,
+                               k->u->d, k->p->d, k->s->d, c->d_partials);
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(spmv_finish(k, k->u, k->w, 2, g, ST_SR_START, nullptr));
+    }
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
     // one iteration: fused update, SpMV w = A u (+ (w, u) partials), reduction
@@ -704,8 +818,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
                                k->s->d, x->d, k->r->d, c->d_partials, c->d_scal, c->d_istate);
         KLE_HIP(hipGetLastError());
         KLE_TRY(c->toc("cg_update", &ev));
-        KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, c->d_istate));
-        KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR));
+        KLE_TRY(spmv_finish(k, k->u, k->w, 2, g, ST_SR, c->d_istate));
         return 0;
     };
     // hipGraph replay (KLE_GRAPH=1; one rank, no per-launch timing): every
@@ -737,13 +850,18 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
         if (gr) (void)hipGraphDestroy(gr);
     }
     if (want_graph && k->graph) {
-        for (int it = 0; it < limit; it += k->graph_len) {
+        // fixed iterations never stop on the device: whole graph blocks, then
+        // the remainder stream-launched
+        int it = 0;
+        for (; it < limit && (!k->fixed || it + k->graph_len <= limit); it += k->graph_len) {
             KLE_HIP(hipGraphLaunch(k->graph, c->stream));
             if (!k->fixed) {
                 KLE_TRY(poll_state(k));
                 if (c->h_istate[I_REASON] != 0) break;
             }
         }
+        if (k->fixed)
+            for (; it < limit; ++it) KLE_TRY(iteration());
     } else {
         for (int it = 0; it < limit; ++it) {
             KLE_TRY(iteration());
@@ -756,7 +874,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(poll_state(k));
     k->its = c->h_istate[I_ITS];
     k->reason = c->h_istate[I_REASON];
-    if (k->reason == 0) k->reason = KLE_DIVERGED_ITS;
+    if (k->reason == 0) k->reason = k->fixed ? KLE_CONVERGED_ITS : KLE_DIVERGED_ITS;
     k->rnorm = std::sqrt(c->h_scal[S_RR]);
     return 0;
 }
@@ -766,7 +884,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x)
 // allreduce across ranks) runs on the comm stream while the SpMV n = A m of
 // the same iteration runs on the compute stream.  Same scalar recurrence as
 // the single-reduction CG (stages ST_SR_START / ST_SR).
-static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
+static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
 {
     kle_ctx *c = k->ctx;
     const int64_t n = b->n_local;
@@ -775,24 +893,24 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
     const int g = grid_for(n, KB, RED_BLOCKS);
     int host_fixed[I_COUNT] = {0, 0, k->fixed, k->fixed ? k->fixed : k->maxit, 0, 0, 0, 0};
     KLE_HIP(hipMemcpyAsync(c->d_istate, host_fixed, sizeof(int) * I_COUNT, hipMemcpyHostToDevice, c->stream));
-    if (jac)
-        hipLaunchKernelGGL(k_sr_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
-                           k->p->d, k->s->d, c->d_partials);
-    else
-        hipLaunchKernelGGL(k_sr_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d, k->u->d,
-                           k->p->d, k->s->d, c->d_partials);
-    KLE_HIP(hipGetLastError());
-    int np = 0;
-    KLE_TRY(spmv_dot(k, k->u, k->w, c->d_partials + 2 * PART_STRIDE, &np, nullptr));  // w = A u, (w,u)
-    KLE_TRY(reduce_stage(k, NParts{{g, g, np, 0}}, 3, ST_SR_START));
-    if (jac)
-        hipLaunchKernelGGL(k_pipe_init<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d, k->z->d,
-                           k->q->d);
-    else
-        hipLaunchKernelGGL(k_pipe_init<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d, k->z->d,
-                           k->q->d);
-    KLE_HIP(hipGetLastError());
-    KLE_TRY(spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, nullptr));  // n = A m
+    if (!cont) {
+        if (jac)
+            hipLaunchKernelGGL(k_sr_start<true>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d,
+                               k->u->d, k->p->d, k->s->d, c->d_partials);
+        else
+            hipLaunchKernelGGL(k_sr_start<false>, dim3(g), dim3(KB), 0, c->stream, n, b->d, dinv, x->d, k->r->d,
+                               k->u->d, k->p->d, k->s->d, c->d_partials);
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(spmv_finish(k, k->u, k->w, 2, g, ST_SR_START, nullptr));  // w = A u, (w,u), scalars
+        if (jac)
+            hipLaunchKernelGGL(k_pipe_init<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d,
+                               k->z->d, k->q->d);
+        else
+            hipLaunchKernelGGL(k_pipe_init<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d,
+                               k->z->d, k->q->d);
+        KLE_HIP(hipGetLastError());
+        KLE_TRY(spmv(k->A, k->m, k->nv, nullptr));  // n = A m
+    }
     // the reduction may run beside the SpMV only where the SpMV's own halo uses
     // the comm stream too (one RCCL stream: halo, then allreduce)
     const bool side = spmv_uses_comm_stream(k->A, k->m);
@@ -821,7 +939,7 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
                 rc = fail(KLE_ERR_DEVICE, "event record/wait failed");
                 break;
             }
-            if ((rc = spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, c->d_istate))) break;
+            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
             if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR, c->comm_stream))) break;
             if (hipEventRecord(ev_red, c->comm_stream) != hipSuccess ||
                 hipStreamWaitEvent(c->stream, ev_red, 0) != hipSuccess) {
@@ -831,12 +949,12 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
         } else if (c->nranks > 1) {
             // no overlap possible on this rank: same collective order as the
             // overlapping ranks (halo, then allreduce), all on one stream
-            if ((rc = spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, c->d_istate))) break;
+            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
             if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
         } else {
             // one rank: the scalar stage first, the SpMV behind it
             if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
-            if ((rc = spmv(k->A, k->m, k->nv, nullptr, nullptr, nullptr, c->d_istate))) break;
+            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
         }
         if (!k->fixed && ((it + 1) % k->check_every == 0)) {
             if ((rc = poll_state(k))) break;
@@ -849,7 +967,7 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
     KLE_TRY(poll_state(k));
     k->its = c->h_istate[I_ITS];
     k->reason = c->h_istate[I_REASON];
-    if (k->reason == 0) k->reason = KLE_DIVERGED_ITS;
+    if (k->reason == 0) k->reason = k->fixed ? KLE_CONVERGED_ITS : KLE_DIVERGED_ITS;
     k->rnorm = std::sqrt(c->h_scal[S_RR]);
     return 0;
 }
@@ -895,7 +1013,7 @@ static int solve_gmres(kle_ksp *k, kle_vec *b, kle_vec *x)
     while (true) {
         // r = b - A x  -> V0
         KLE_HIP(hipMemcpyAsync(k->p->d, x->d, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
-        KLE_TRY(spmv(k->A, k->p, k->V[0], nullptr, nullptr, nullptr, nullptr));
+        KLE_TRY(spmv(k->A, k->p, k->V[0], nullptr));
         hipLaunchKernelGGL(k_bmy, dim3(grid_for(n, KB, RED_BLOCKS)), dim3(KB), 0, c->stream, n, b->d, k->V[0]->d);
         KLE_TRY(kle_vec_norm2(k->V[0], &rn));
         if (rn <= tol) break;
@@ -907,7 +1025,7 @@ static int solve_gmres(kle_ksp *k, kle_vec *b, kle_vec *x)
             // w = A M^-1 v_j
             if (jac) KLE_TRY(kle_vec_pointwise_mult(z, k->dinv, k->V[j]));
             else KLE_TRY(kle_vec_copy(k->V[j], z));
-            KLE_TRY(spmv(k->A, z, k->V[j + 1], nullptr, nullptr, nullptr, nullptr));
+            KLE_TRY(spmv(k->A, z, k->V[j + 1], nullptr));
             // two passes of classical Gram-Schmidt (CGS2)
             std::fill(hcol.begin(), hcol.end(), 0.0);
             for (int pass = 0; pass < 2; ++pass) {
@@ -1125,13 +1243,6 @@ int kle_ksp_set_cg_single_reduction(kle_ksp *k, int flag)
     return 0;
 }
 
-int kle_ksp_set_fused_dot(kle_ksp *k, int flag)
-{
-    KLE_ARG(k, "null ksp");
-    k->fused_dot = flag != 0;
-    return 0;
-}
-
 int kle_ksp_set_fixed_iterations(kle_ksp *k, int n)
 {
     KLE_ARG(k && n >= 0, "bad arg");
@@ -1204,13 +1315,32 @@ int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
     k->true_rel = -1;
     // an exact preconditioner makes any Krylov method converge in one step:
     // PC lu is applied directly whatever the KSP type (gmres + lu, kle_solver.py:57-61)
+    k->last_b = k->last_x = nullptr;
     if (k->pc == "lu" || k->type == "preonly") KLE_TRY(solve_direct(k, b, x));
-    else if (k->type == "pipecg") KLE_TRY(solve_pipecg(k, b, x));
-    else if (k->type == "cg" && k->single_reduction) KLE_TRY(solve_cg_single(k, b, x));
+    else if (k->type == "pipecg") KLE_TRY(solve_pipecg(k, b, x, false));
+    else if (k->type == "cg" && k->single_reduction) KLE_TRY(solve_cg_single(k, b, x, false));
     else if (k->type == "cg") KLE_TRY(solve_cg(k, b, x));
     else KLE_TRY(solve_gmres(k, b, x));
     if (!k->fixed) KLE_TRY(true_residual(k, b, x));
+    else {
+        k->last_b = b;
+        k->last_x = x;
+    }
     return 0;
+}
+
+int kle_ksp_continue(kle_ksp *k, kle_vec *b, kle_vec *x, int n)
+{
+    KLE_ARG(k && b && x && n >= 1, "bad arg");
+    KLE_ARG(k->setup && k->fixed && k->last_b == b && k->last_x == x,
+            "continue needs a preceding fixed-iteration solve with the same b and x");
+    KLE_ARG(k->pc != "lu" && (k->type == "pipecg" || (k->type == "cg" && k->single_reduction)),
+            "continue: single-reduction or pipelined CG only");
+    const int keep = k->fixed;
+    k->fixed = n;
+    const int rc = k->type == "pipecg" ? solve_pipecg(k, b, x, true) : solve_cg_single(k, b, x, true);
+    k->fixed = keep;
+    return rc;
 }
 
 int kle_ksp_get_iteration_number(const kle_ksp *k, int *its)

@@ -42,145 +42,39 @@ __device__ __forceinline__ T ntload(const T *p)
     return __builtin_nontemporal_load(p);
 }
 
-template <bool NT, class T>
-__device__ __forceinline__ T ldv(const T *p)
-{
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-
 constexpr int SPMV_BLOCK = 256;
 constexpr int SPMV_WAVES = SPMV_BLOCK / 64;
 
-// LPR lanes per node row (64: one row per wavefront, 32/16: 2/4 rows per
-// wavefront), UNR block columns per lane issued before the FMAs (memory-level
-// parallelism), persistent: grid-stride over rows with a resident-size grid.
-// xcd: the dispatcher deals workgroups round-robin over the 8 XCDs (b, b+8 on
-// one XCD; MI355X_MICROARCH.md); remapping b -> (b%8)*(G/8) + b/8 gives each
-// XCD one contiguous chunk of the row order, so the x lines a chunk gathers
-// stay in that XCD's L2.  order: optional row permutation (spatially tiled).
 // rows [a0, a0 + na) then [b0, b0 + nb): the whole matrix, or the interior /
 // ghost-dependent split used to overlap the halo exchange (N > 1)
 struct RowMap {
     int64_t a0, na, b0, nb;
 };
 
-template <int R, int C, bool DOT, int LPR, int UNR, bool NT>
-__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv(RowMap rm, const int *__restrict__ rowptr,
-                                                        const int *__restrict__ rowcnt,
-                                                        const int *__restrict__ rowbox, int lx, int lxy,
-                                                        const int64_t *__restrict__ vptr, int lay,
-                                                        const int *__restrict__ bcol,
-                                                        const double *__restrict__ val,
-                                                        const double *__restrict__ x,
-                                                        double *__restrict__ y,
-                                                        const double *__restrict__ pd,
-                                                        double *__restrict__ partials,
-                                                        const int *__restrict__ istate,
-                                                        const int *__restrict__ order, int xcd)
-{
-    if (istate && istate[I_REASON] != 0) return;
-    constexpr int RPW = 64 / LPR;  // rows per wavefront
-    const int lane = threadIdx.x & 63;
-    const int sub = lane / LPR, sl = lane % LPR;
-    const int64_t lb = xcd ? (int64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
-    const int64_t wave0 = lb * SPMV_WAVES + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
-    double dotacc = 0.0;
-    const int64_t nrows = rm.na + rm.nb;
-    for (int64_t base = wave0 * RPW; base < nrows; base += nwaves * RPW) {
-        const int64_t r = base + sub;
-        const bool valid = r < nrows;
-        const int64_t i = !valid ? 0 : order ? order[r] : r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
-        int b0 = 0, m = 0, mp = 0, bbase = 0, bnx = 1, bnxy = 1;
-        if (valid) {
-            b0 = rowptr[i];
-            mp = rowptr[i + 1] - b0;
-            m = rowcnt ? rowcnt[i] : mp;
-            if (rowbox) {
-                bbase = rowbox[2 * i];
-                const int d = rowbox[2 * i + 1];
-                bnx = d & 255;
-                bnxy = bnx * ((d >> 8) & 255);
-            }
-        }
-        const double *v = val + (valid ? vptr[i] : 0);
-        const int *cj = bcol + b0;
-        double acc[R];
-#pragma unroll
-        for (int a = 0; a < R; ++a) acc[a] = 0.0;
-        for (int k = sl; k < m; k += LPR * UNR) {
-            int64_t j[UNR];
-            double vv[UNR][R * C];
-            bool on[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const int ku = k + u * LPR;
-                on[u] = ku < m;
-                if (rowbox) {
-                    // column of block ku inside the row's lattice box (no bcol stream)
-                    const int kz = ku / bnxy, rem = ku - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
-                    j[u] = on[u] ? bbase + kx + lx * ky + lxy * kz : 0;
-                } else {
-                    j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
-                }
-#pragma unroll
-                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + vofs(lay, R * C, t, ku, m, mp)) : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                double xv[C];
-#pragma unroll
-                for (int b = 0; b < C; ++b) xv[b] = on[u] ? x[j[u] * C + b] : 0.0;
-#pragma unroll
-                for (int a = 0; a < R; ++a)
-#pragma unroll
-                    for (int b = 0; b < C; ++b) acc[a] += vv[u][a * C + b] * xv[b];
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-            for (int o = LPR / 2; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-        if (sl < R && valid) {
-            double mine = acc[0];
-#pragma unroll
-            for (int a = 1; a < R; ++a)
-                if (sl == a) mine = acc[a];
-            y[i * R + sl] = mine;
-            if (DOT) dotacc += mine * pd[i * R + sl];
-        }
-    }
-    if (DOT) {
-        __shared__ double lds[SPMV_WAVES];
-        dotacc = wsum(dotacc);
-        if (lane == 0) lds[threadIdx.x >> 6] = dotacc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double s = 0;
-            for (int w = 0; w < SPMV_WAVES; ++w) s += lds[w];
-            partials[blockIdx.x] = s;
-        }
-    }
-}
-
-
-
-// Default SpMV (unfused, one row per wavefront, one block per lane in flight,
-// nt streams), specialised on the value layout and on structured columns so
-// the generic variant's branches cost no registers (occupancy 8 at R = C = 3).
+// Node-block SpMV: one 64-lane wavefront per node row, WV rows per
+// workgroup, one block column per lane in flight, non-temporal value/column
+// loads (read once; they must not evict the gathered x from L2), shuffle
+// reduction of the R row sums.  Specialised on the value layout and on
+// structured columns so no run-time branch costs registers (62 VGPRs at
+// R = C = 3: occupancy 8).
 // LAY 1: while the wave's 64 blocks lie inside the row's full 16-block chunks
 // the RC value loads of a lane share one base address (immediate offsets of
 // 128 B); the last, partial pass uses the packed-tail rule of vofs().
-template <int R, int C, int LAY, bool STRUCT, int UNR, int WV = SPMV_WAVES>
-__global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(RowMap rm, const int *__restrict__ rowptr,
-                                                             const int *__restrict__ rowcnt,
-                                                             const int *__restrict__ rowbox, int lx, int lxy,
-                                                             const int64_t *__restrict__ vptr,
-                                                             const int *__restrict__ bcol,
-                                                             const double *__restrict__ val,
-                                                             const double *__restrict__ x, double *__restrict__ y,
-                                                             const int *__restrict__ istate)
+// STRUCT: the row's columns form a lattice box (K, Rw, operators on box
+// meshes): the column of block k is computed from 8 B per row, no bcol stream.
+// Variants measured and rejected in round 1 (lanes per row 32/16, two blocks
+// per lane in flight, persistent grid, XCD-chunked and (x,y)-tiled row
+// orders, rows-per-wave prefetch, buffer-descriptor cache policies, the dot
+// fused into the epilogue): DESIGN.md §3; code in git history (a54a1e5^).
+template <int R, int C, int LAY, bool STRUCT, int WV>
+__global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMap rm, const int *__restrict__ rowptr,
+                                                        const int *__restrict__ rowcnt,
+                                                        const int *__restrict__ rowbox, int lx, int lxy,
+                                                        const int64_t *__restrict__ vptr,
+                                                        const int *__restrict__ bcol,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, double *__restrict__ y,
+                                                        const int *__restrict__ istate)
 {
     if (istate && istate[I_REASON] != 0) return;
     constexpr int RC = R * C;
@@ -201,48 +95,40 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(
     double acc[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) acc[a] = 0.0;
-    for (int kb = 0; kb < m; kb += 64 * UNR) {
-        int j[UNR];
-        bool on[UNR];
-        double vv[UNR][RC];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const int kbu = kb + 64 * u, k = kbu + lane;
-            on[u] = k < m;
-            j[u] = 0;
-            if (on[u]) {
-                if constexpr (STRUCT) {
-                    const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
-                    j[u] = bbase + kx + lx * ky + lxy * kz;
-                } else {
-                    j[u] = __builtin_nontemporal_load(bcol + b0 + k);
-                }
-            }
-            if (LAY == 1 && kbu + 64 <= q16) {
-                // whole wave inside full chunks: stream t at +16 t doubles
-                const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
-#pragma unroll
-                for (int t = 0; t < RC; ++t) vv[u][t] = __builtin_nontemporal_load(p + t * 16);
-            } else if (on[u]) {
-                const int64_t o0 = vofs(LAY, RC, 0, k, m, mp);
-                const int64_t st = LAY == 1 ? (k < q16 ? 16 : m - q16) : mp;
-#pragma unroll
-                for (int t = 0; t < RC; ++t) vv[u][t] = __builtin_nontemporal_load(v + o0 + t * st);
+    for (int kb = 0; kb < m; kb += 64) {
+        const int k = kb + lane;
+        const bool on = k < m;
+        int j = 0;
+        double vv[RC];
+        if (on) {
+            if constexpr (STRUCT) {
+                const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
+                j = bbase + kx + lx * ky + lxy * kz;
             } else {
-#pragma unroll
-                for (int t = 0; t < RC; ++t) vv[u][t] = 0.0;
+                j = __builtin_nontemporal_load(bcol + b0 + k);
             }
         }
+        if (LAY == 1 && kb + 64 <= q16) {
+            // whole wave inside full chunks: stream t at +16 t doubles
+            const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            double xv[C];
+            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(p + t * 16);
+        } else if (on) {
+            const int64_t o0 = vofs(LAY, RC, 0, k, m, mp);
+            const int64_t st = LAY == 1 ? (k < q16 ? 16 : m - q16) : mp;
 #pragma unroll
-            for (int b = 0; b < C; ++b) xv[b] = on[u] ? x[(int64_t)j[u] * C + b] : 0.0;
+            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
+        } else {
 #pragma unroll
-            for (int a = 0; a < R; ++a)
-#pragma unroll
-                for (int b = 0; b < C; ++b) acc[a] += vv[u][a * C + b] * xv[b];
+            for (int t = 0; t < RC; ++t) vv[t] = 0.0;
         }
+        double xv[C];
+#pragma unroll
+        for (int b = 0; b < C; ++b) xv[b] = on ? x[(int64_t)j * C + b] : 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xv[b];
     }
 #pragma unroll
     for (int a = 0; a < R; ++a)
@@ -257,199 +143,22 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv_fast(
     }
 }
 
-// Variant: each wave takes `seq` consecutive rows and prefetches the next
-// row's (offset, length) while it streams the current one, so the row-start
-// latency overlaps the previous row's loads.  No fused dot / order / XCD map.
-template <int R, int C, int UNR, bool NT>
-__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_seq(RowMap rm, int seq, const int *__restrict__ rowptr,
-                                                            const int *__restrict__ rowcnt,
-                                                            const int64_t *__restrict__ vptr, int lay,
-                                                            const int *__restrict__ bcol,
-                                                            const double *__restrict__ val,
-                                                            const double *__restrict__ x, double *__restrict__ y,
-                                                            const int *__restrict__ istate)
-{
-    if (istate && istate[I_REASON] != 0) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
-    const int64_t nrows = rm.na + rm.nb;
-    const int64_t r0 = wave * seq;
-    if (r0 >= nrows) return;
-    const int64_t r1 = min(r0 + (int64_t)seq, nrows);
-    int64_t i = r0 < rm.na ? rm.a0 + r0 : rm.b0 + (r0 - rm.na);
-    int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
-    for (int64_t r = r0; r < r1; ++r) {
-        int64_t ni = i;
-        int nb0 = 0, nmp = 0, nm = 0;
-        if (r + 1 < r1) {
-            ni = r + 1 < rm.na ? rm.a0 + r + 1 : rm.b0 + (r + 1 - rm.na);
-            nb0 = rowptr[ni];
-            nmp = rowptr[ni + 1] - nb0;
-            nm = rowcnt ? rowcnt[ni] : nmp;
-        }
-        const double *v = val + vptr[i];
-        const int *cj = bcol + b0;
-        double acc[R];
-#pragma unroll
-        for (int a = 0; a < R; ++a) acc[a] = 0.0;
-        for (int k = lane; k < m; k += 64 * UNR) {
-            int64_t j[UNR];
-            double vv[UNR][R * C];
-            bool on[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const int ku = k + u * 64;
-                on[u] = ku < m;
-                j[u] = on[u] ? ldv<NT>(cj + ku) : 0;
-#pragma unroll
-                for (int t = 0; t < R * C; ++t) vv[u][t] = on[u] ? ldv<NT>(v + vofs(lay, R * C, t, ku, m, mp)) : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                double xv[C];
-#pragma unroll
-                for (int b = 0; b < C; ++b) xv[b] = on[u] ? x[j[u] * C + b] : 0.0;
-#pragma unroll
-                for (int a = 0; a < R; ++a)
-#pragma unroll
-                    for (int b = 0; b < C; ++b) acc[a] += vv[u][a * C + b] * xv[b];
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-        if (lane < R) {
-            double mine = acc[0];
-#pragma unroll
-            for (int a = 1; a < R; ++a)
-                if (lane == a) mine = acc[a];
-            y[i * R + lane] = mine;
-        }
-        i = ni;
-        b0 = nb0;
-        mp = nmp;
-        m = nm;
-    }
-}
-
-// Buffer-load variant of the node-block SpMV (one row per wavefront, two
-// block columns per lane in flight): the matrix streams go through a per-row
-// buffer descriptor so the cache-policy bits (aux: bit0 sc0, bit1 nt,
-// bit4 sc1) can be chosen; XDROP=1 prices the x gather (descriptor with 0
-// records: the gathers return 0 -- wrong y, timing diagnostic only).
-template <int R, int C, bool DOT, int AUX, bool XDROP>
-__global__ __launch_bounds__(SPMV_BLOCK) void k_nb_spmv_buf(int64_t nrows, const int *__restrict__ rowptr,
-                                                            const int *__restrict__ rowcnt,
-                                                            const int *__restrict__ bcol,
-                                                            const double *__restrict__ val,
-                                                            const double *__restrict__ x, int64_t xbytes,
-                                                            double *__restrict__ y,
-                                                            const double *__restrict__ pd,
-                                                            double *__restrict__ partials,
-                                                            const int *__restrict__ istate)
-{
-    if (istate && istate[I_REASON] != 0) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
-    double dotacc = 0.0;
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, XDROP ? 0 : (int)min(xbytes, (int64_t)0x7fffffff), 0x00020000);
-    if (i < nrows) {
-        const int b0 = __builtin_amdgcn_readfirstlane(rowptr[i]);
-        const int mp = __builtin_amdgcn_readfirstlane(rowptr[i + 1]) - b0;
-        const int m = rowcnt ? __builtin_amdgcn_readfirstlane(rowcnt[i]) : mp;
-        const __amdgpu_buffer_rsrc_t vr =
-            __builtin_amdgcn_make_buffer_rsrc((void *)(val + (int64_t)b0 * (R * C)), 0, mp * R * C * 8, 0x00020000);
-        const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc((void *)(bcol + b0), 0, m * 4, 0x00020000);
-        double acc[R];
-#pragma unroll
-        for (int a = 0; a < R; ++a) acc[a] = 0.0;
-        for (int k = lane; k < m; k += 128) {
-            int j[2];
-            double vv[2][R * C];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int ku = k + 64 * u;  // out-of-range offsets read 0 (bounds-checked descriptor)
-                j[u] = __builtin_amdgcn_raw_buffer_load_b32(cr, ku * 4, 0, AUX);
-#pragma unroll
-                for (int t = 0; t < R * C; ++t) {
-                    vv[u][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vr, (t * mp + ku) * 8, 0, AUX));
-                }
-                if (ku >= m) {
-#pragma unroll
-                    for (int t = 0; t < R * C; ++t) vv[u][t] = 0.0;
-                    j[u] = 0;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                for (int b = 0; b < C; ++b) {
-                    const double xv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (j[u] * C + b) * 8, 0, 0));
-#pragma unroll
-                    for (int a = 0; a < R; ++a) acc[a] += vv[u][a * C + b] * xv;
-                }
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < R; ++a) acc[a] = wsum(acc[a]);
-        if (lane < R) {
-            double mine = acc[0];
-#pragma unroll
-            for (int a = 1; a < R; ++a)
-                if (lane == a) mine = acc[a];
-            y[i * R + lane] = mine;
-            if (DOT) dotacc += mine * pd[i * R + lane];
-        }
-    }
-    if (DOT) {
-        __shared__ double lds[SPMV_WAVES];
-        dotacc = wsum(dotacc);
-        if (lane == 0) lds[threadIdx.x >> 6] = dotacc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double s = 0;
-            for (int w = 0; w < SPMV_WAVES; ++w) s += lds[w];
-            partials[blockIdx.x] = s;
-        }
-    }
-}
-
-template <bool DOT>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_aij_spmv(int64_t nrows, const int64_t *__restrict__ ptr,
                                                          const int *__restrict__ col,
                                                          const double *__restrict__ val,
                                                          const double *__restrict__ x, double *__restrict__ y,
-                                                         const double *__restrict__ pd,
-                                                         double *__restrict__ partials,
                                                          const int *__restrict__ istate)
 {
     if (istate && istate[I_REASON] != 0) return;
     const int lane = threadIdx.x & 63;
     const int64_t wave0 = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
-    double dotacc = 0.0;
     for (int64_t i = wave0; i < nrows; i += nwaves) {
         const int64_t s = ptr[i], e = ptr[i + 1];
         double acc = 0.0;
         for (int64_t k = s + lane; k < e; k += 64) acc += ntload(val + k) * x[ntload(col + k)];
         acc = wsum(acc);
-        if (lane == 0) {
-            y[i] = acc;
-            if (DOT) dotacc += acc * pd[i];
-        }
-    }
-    if (DOT) {
-        __shared__ double lds[SPMV_WAVES];
-        dotacc = wsum(dotacc);
-        if (lane == 0) lds[threadIdx.x >> 6] = dotacc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double s = 0;
-            for (int w = 0; w < SPMV_WAVES; ++w) s += lds[w];
-            partials[blockIdx.x] = s;
-        }
+        if (lane == 0) y[i] = acc;
     }
 }
 
@@ -538,256 +247,102 @@ __global__ void k_axpy_same(int64_t n, double a, const double *__restrict__ x, d
         y[i] += a * x[i];
 }
 
-// Row processing order: (x,y) tiles of TX x TY nodes, each swept through all
-// owned z planes, so consecutive workgroups reuse the same x window in L2.
-static int nb_build_order(kle_mat *A)
-{
-    const int64_t LX = A->row_lat[0], LY = A->row_lat[1], LZ = A->row_lat[2];
-    if (LX * LY * LZ != A->nrows) return fail(KLE_ERR_STATE, "row lattice does not match the matrix");
-    const int64_t TX = 16, TY = 8;
-    std::vector<int> ord;
-    ord.reserve(A->nrows);
-    for (int64_t ty = 0; ty < LY; ty += TY)
-        for (int64_t tx = 0; tx < LX; tx += TX)
-            for (int64_t z = 0; z < LZ; ++z)
-                for (int64_t yy = ty; yy < std::min(LY, ty + TY); ++yy)
-                    for (int64_t xx = tx; xx < std::min(LX, tx + TX); ++xx) ord.push_back((int)(xx + LX * (yy + LY * z)));
-    KLE_HIP(hipMalloc(&A->d_order, sizeof(int) * std::max<int64_t>(A->nrows, 1)));
-    KLE_HIP(hipMemcpy(A->d_order, ord.data(), sizeof(int) * A->nrows, hipMemcpyHostToDevice));
-    return 0;
-}
-
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
-    return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi && !A->spmv_order &&
-           !A->spmv_buf && !A->spmv_persistent && (x->lo_rank >= 0 || x->hi_rank >= 0 || (x->plan && !x->plan->peers.empty()));
+    return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi &&
+           (x->lo_rank >= 0 || x->hi_rank >= 0 || (x->plan && !x->plan->peers.empty()));
 }
 
-int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const kle_vec *dotvec, double *partials, int *nparts,
-         const int *istate)
+// Waves (rows) per workgroup: 8 for 3x3 chunked matrices of >= 64k node rows
+// -- consecutive rows of one workgroup share most x columns in the CU's L1:
+// config 2 +2.5 %, unstructured 1M mesh +2 %; 4 elsewhere (0.5 % ahead on the
+// 1/8 slab); profiles/r01/spmv_waves_ab.jsonl.  kle_set_tuning("spmv_waves") overrides.
+static int spmv_waves(const kle_mat *A)
+{
+    if (!(A->R == 3 && A->C == 3 && A->vlayout == 1)) return SPMV_WAVES;
+    return g_tune.spmv_waves ? g_tune.spmv_waves : (A->nrows >= 64000 ? 8 : SPMV_WAVES);
+}
+
+template <int R, int C, int LAY, bool STRUCT>
+static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, const kle_vec *x, kle_vec *y,
+                          const int *istate, hipStream_t st)
+{
+    const int64_t nr = rm.na + rm.nb;
+    if (R == 3 && C == 3 && LAY == 1 && wv == 8)
+        hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), 0, st, rm,
+                           A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_bcol,
+                           A->d_val, x->base, y->d, istate);
+    else
+        hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, SPMV_WAVES>), dim3(grid_for(nr, SPMV_WAVES, 1 << 30)),
+                           dim3(SPMV_BLOCK), 0, st, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,
+                           (int)A->box_lxy, A->d_vptr, A->d_bcol, A->d_val, x->base, y->d, istate);
+}
+
+template <int R, int C>
+static void launch_nb(const kle_mat *A, RowMap rm, const int *rbox, const kle_vec *x, kle_vec *y,
+                      const int *istate, hipStream_t st)
+{
+    if (rm.na + rm.nb <= 0) return;
+    const int wv = spmv_waves(A);
+    if (A->vlayout == 1) {
+        if (rbox) launch_nb_lay<R, C, 1, true>(A, rm, wv, rbox, x, y, istate, st);
+        else launch_nb_lay<R, C, 1, false>(A, rm, wv, rbox, x, y, istate, st);
+    } else {
+        if (rbox) launch_nb_lay<R, C, 0, true>(A, rm, wv, rbox, x, y, istate, st);
+        else launch_nb_lay<R, C, 0, false>(A, rm, wv, rbox, x, y, istate, st);
+    }
+}
+
+static int launch_nb_shape(const kle_mat *A, RowMap rm, const int *rbox, const kle_vec *x, kle_vec *y,
+                           const int *istate, hipStream_t st)
+{
+#define NB_SHAPE(RR, CC)                                                  \
+    if (A->R == RR && A->C == CC) {                                       \
+        launch_nb<RR, CC>(A, rm, rbox, x, y, istate, st);                 \
+        KLE_HIP(hipGetLastError());                                       \
+        return 0;                                                         \
+    }
+    NB_SHAPE(3, 3) NB_SHAPE(6, 3) NB_SHAPE(3, 6) NB_SHAPE(2, 2) NB_SHAPE(2, 1) NB_SHAPE(1, 2) NB_SHAPE(3, 1)
+    NB_SHAPE(1, 3) NB_SHAPE(3, 2) NB_SHAPE(2, 3) NB_SHAPE(1, 1)
+#undef NB_SHAPE
+    return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
+}
+
+int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
 {
     kle_ctx *c = A->ctx;
-    const bool dot = dotvec != nullptr;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (A->kind == 0) {
         // N > 1: rows [int_lo, int_hi) read no ghost entry, so they run while the
         // halo is in flight on the comm stream; the ghost-dependent rows follow
-        const bool overlap = !dot && spmv_uses_comm_stream(A, x);
+        const bool overlap = spmv_uses_comm_stream(A, x);
         if (c->nranks > 1 && !overlap)
             KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
                                   x->send_lo, x->send_hi, nullptr, x->plan.get()));
-        const int rpb = SPMV_WAVES * (64 / A->spmv_lpr);  // rows per workgroup
-        int grid;
-        if (A->spmv_persistent) {
-            int occ = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_nb_spmv<3, 3, true, 64, 2, false>,
-                                                             SPMV_BLOCK, 0) != hipSuccess || occ < 1)
-                occ = 4;
-            grid = grid_for(A->nrows, rpb, c->num_cus * occ);
-        } else {
-            grid = grid_for(A->nrows, rpb, PART_STRIDE - 256);
-            if (A->spmv_xcd) grid = (grid + 7) / 8 * 8;  // whole XCD chunks
-        }
-        if (A->spmv_buf && A->R == 3 && A->C == 3 && A->spmv_lpr == 64 && !A->spmv_persistent && !A->spmv_order &&
-            !A->spmv_xcd && A->vlayout == 0) {
-            const int64_t xbytes = (int64_t)(x->ghost_lo + x->n_local + x->ghost_hi) * 8;
-            const int g2 = (int)((A->nrows + SPMV_WAVES - 1) / SPMV_WAVES);
-            if (g2 > PART_STRIDE - 256) return fail(KLE_ERR_SUP, "buffer SpMV variant: matrix too large");
-            if (nparts) *nparts = g2;
-            const double *pd = dot ? dotvec->d : nullptr;
-            KLE_TRY(c->tic("spmv", &ev));
-#define BUF_LAUNCH(AUXV, XD)                                                                              \
-    do {                                                                                                  \
-        if (dot)                                                                                          \
-            hipLaunchKernelGGL((k_nb_spmv_buf<3, 3, true, AUXV, XD>), dim3(g2), dim3(SPMV_BLOCK), 0, c->stream, \
-                               A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
-                               istate);                                                                   \
-        else                                                                                              \
-            hipLaunchKernelGGL((k_nb_spmv_buf<3, 3, false, AUXV, XD>), dim3(g2), dim3(SPMV_BLOCK), 0, c->stream, \
-                               A->nrows, A->d_rowptr, A->d_rowcnt, A->d_bcol, A->d_val, x->base, xbytes, y->d, pd, partials, \
-                               istate);                                                                   \
-    } while (0)
-            switch (A->spmv_buf) {
-            case 1: BUF_LAUNCH(0, false); break;
-            case 2: BUF_LAUNCH(2, false); break;
-            case 3: BUF_LAUNCH(3, false); break;
-            case 4: BUF_LAUNCH(16, false); break;
-            case 5: BUF_LAUNCH(18, false); break;
-            case 6: BUF_LAUNCH(19, false); break;
-            case 7: BUF_LAUNCH(17, false); break;
-            case 8: BUF_LAUNCH(2, true); break;
-            default: return fail(KLE_ERR_ARG, "unknown buffer SpMV variant %d", A->spmv_buf);
-            }
-#undef BUF_LAUNCH
-            KLE_HIP(hipGetLastError());
-            KLE_TRY(c->toc("spmv", &ev));
-            return 0;
-        }
-        const bool seq_ok = A->spmv_seq > 1 && A->R == 3 && A->C == 3 && A->spmv_lpr == 64 && !dot &&
-                            !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
-        const bool fast_shape = (A->R == 3 && A->C == 3) || (A->R == 6 && A->C == 3) || (A->R == 3 && A->C == 6) ||
-                                (A->R == 2 && A->C == 2);
-        // (two blocks per lane in flight spill at 8 waves/SIMD: 112 B scratch -> unroll 1 only)
-        const bool fast_ok = A->spmv_fast && fast_shape && !dot && A->spmv_lpr == 64 && A->spmv_unroll == 1 &&
-                             A->spmv_nt && A->spmv_seq <= 1 && !A->spmv_order && !A->spmv_xcd && !A->spmv_persistent;
-        if (A->spmv_order && !A->d_order) KLE_TRY(nb_build_order(A));
-        const int *order = A->spmv_order ? A->d_order : nullptr;
-        const int xcd = A->spmv_xcd && !A->spmv_persistent;
-        if (nparts) *nparts = grid;
-        const double *pd = dot ? dotvec->d : nullptr;
         KLE_TRY(c->tic("spmv", &ev));
         const int *rbox = A->spmv_struct ? A->d_rowbox : nullptr;
-        RowMap rm{0, A->nrows, 0, 0};
-        if (overlap) {
-            rm = RowMap{A->int_lo, A->int_hi - A->int_lo, 0, 0};
-            grid = grid_for(rm.na, rpb, PART_STRIDE - 256);
+        if (!overlap) {
+            KLE_TRY(launch_nb_shape(A, RowMap{0, A->nrows, 0, 0}, rbox, x, y, istate, c->stream));
+        } else {
             KLE_HIP(hipEventRecord(c->ev_x_ready, c->stream));
             KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
+            KLE_TRY(launch_nb_shape(A, RowMap{A->int_lo, A->int_hi - A->int_lo, 0, 0}, rbox, x, y, istate,
+                                    c->stream));
+            // interior rows are queued; exchange the halo beside them
+            KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
+                                  x->send_lo, x->send_hi, c->comm_stream, x->plan.get()));
+            KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
+            KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
+            KLE_TRY(launch_nb_shape(A, RowMap{0, A->int_lo, A->int_hi, A->nrows - A->int_hi}, rbox, x, y, istate,
+                                    c->stream));
         }
-        for (int pass = 0; pass < (overlap ? 2 : 1); ++pass) {
-            if (pass == 1) {
-                // interior rows are queued; exchange the halo beside them
-                KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank,
-                                      x->send_lo, x->send_hi, c->comm_stream, x->plan.get()));
-                KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
-                KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
-                rm = RowMap{0, A->int_lo, A->int_hi, A->nrows - A->int_hi};
-                grid = grid_for(rm.na + rm.nb, rpb, PART_STRIDE - 256);
-            }
-            if (fast_ok) {
-                // waves per workgroup of the default kernel for the 3x3 node-block
-                // matrices: 8 consecutive rows per workgroup share their x columns in
-                // the CU's L1 -- 2.5 % faster at config 2, 2 % on the unstructured 1M
-                // mesh, 1 % on its 1/4 part (89k rows); 4 stays 0.5 % ahead on the 1/8 slab (47k), 16 is
-                // slower everywhere (profiles/r01/spmv_waves_ab.jsonl).
-                // KLE_SPMV_WAVES=1/2/4/8/16 overrides.
-                static const int wv_env = [] {
-                    const char *e = getenv("KLE_SPMV_WAVES");
-                    const int w = e ? atoi(e) : 0;
-                    return (w == 1 || w == 2 || w == 4 || w == 8 || w == 16) ? w : 0;
-                }();
-                const int wv = (A->R == 3 && A->C == 3 && A->vlayout == 1)
-                                   ? (wv_env ? wv_env : (A->nrows >= 64000 ? 8 : SPMV_WAVES))
-                                   : SPMV_WAVES;
-                if (wv != SPMV_WAVES) {
-                    const int gw = grid_for(rm.na + rm.nb, wv, 1 << 30);
-                    const bool st = rbox != nullptr;
-#define FAST_W(W)                                                                                               \
-    do {                                                                                                        \
-        if (st)                                                                                                 \
-            hipLaunchKernelGGL((k_nb_spmv_fast<3, 3, 1, true, 1, W>), dim3(gw), dim3(64 * W), 0, c->stream, rm, \
-                               A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
-                               A->d_bcol, A->d_val, x->base, y->d, istate);                                     \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_nb_spmv_fast<3, 3, 1, false, 1, W>), dim3(gw), dim3(64 * W), 0, c->stream, rm, \
-                               A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
-                               A->d_bcol, A->d_val, x->base, y->d, istate);                                     \
-    } while (0)
-                    if (wv == 1) FAST_W(1);
-                    else if (wv == 2) FAST_W(2);
-                    else if (wv == 8) FAST_W(8);
-                    else FAST_W(16);
-#undef FAST_W
-                    KLE_HIP(hipGetLastError());
-                    continue;
-                }
-                const int gf = grid_for(rm.na + rm.nb, SPMV_WAVES, 1 << 30);
-                const int st_ = rbox ? 1 : 0;
-#define FAST_LAUNCH(RR, CC, LY, SS)                                                                     \
-    hipLaunchKernelGGL((k_nb_spmv_fast<RR, CC, LY, SS, 1>), dim3(gf), dim3(SPMV_BLOCK), 0, c->stream, rm, \
-                       A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr,       \
-                       A->d_bcol, A->d_val, x->base, y->d, istate)
-#define FAST_SHAPE(RR, CC)                                                                              \
-    if (A->vlayout == 1 && st_) FAST_LAUNCH(RR, CC, 1, true);                                           \
-    else if (A->vlayout == 1) FAST_LAUNCH(RR, CC, 1, false);                                            \
-    else if (st_) FAST_LAUNCH(RR, CC, 0, true);                                                         \
-    else FAST_LAUNCH(RR, CC, 0, false);
-                if (A->R == 3 && A->C == 3) { FAST_SHAPE(3, 3) }
-                else if (A->R == 6 && A->C == 3) { FAST_SHAPE(6, 3) }
-                else if (A->R == 3 && A->C == 6) { FAST_SHAPE(3, 6) }
-                else if (A->R == 2 && A->C == 2) { FAST_SHAPE(2, 2) }
-#undef FAST_SHAPE
-#undef FAST_LAUNCH
-                KLE_HIP(hipGetLastError());
-                continue;
-            }
-            if (seq_ok) {
-                const int64_t nr = rm.na + rm.nb;
-                const int gs = (int)((nr + (int64_t)SPMV_WAVES * A->spmv_seq - 1) / ((int64_t)SPMV_WAVES * A->spmv_seq));
-                if (A->spmv_unroll == 1 && A->spmv_nt)
-                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 1, true>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
-                else if (A->spmv_unroll == 1)
-                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 1, false>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
-                else if (A->spmv_nt)
-                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 2, true>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
-                else
-                    hipLaunchKernelGGL((k_nb_spmv_seq<3, 3, 2, false>), dim3(gs), dim3(SPMV_BLOCK), 0, c->stream, rm,
-                                       A->spmv_seq, A->d_rowptr, A->d_rowcnt, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base, y->d, istate);
-                KLE_HIP(hipGetLastError());
-                continue;
-            }
-#define NB_LAUNCH(RR, CC, LPR, UNR, NT)                                                                   \
-    do {                                                                                                \
-        if (dot)                                                                                        \
-            hipLaunchKernelGGL((k_nb_spmv<RR, CC, true, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0,    \
-                               c->stream, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,           \
-                               (int)A->box_lxy, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base,    \
-                               y->d, pd, partials,                                                      \
-                               istate, order, xcd);                                                     \
-        else                                                                                            \
-            hipLaunchKernelGGL((k_nb_spmv<RR, CC, false, LPR, UNR, NT>), dim3(grid), dim3(SPMV_BLOCK), 0, \
-                               c->stream, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,           \
-                               (int)A->box_lxy, A->d_vptr, A->vlayout, A->d_bcol, A->d_val, x->base,    \
-                               y->d, pd, partials,                                                      \
-                               istate, order, xcd);                                                     \
-    } while (0)
-#define NB_VARIANTS(RR, CC)                                                                             \
-    if (A->spmv_lpr == 64 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 1, true);         \
-    else if (A->spmv_lpr == 64 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 64, 1, false);                 \
-    else if (A->spmv_lpr == 64 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 2, true);                           \
-    else if (A->spmv_lpr == 64) NB_LAUNCH(RR, CC, 64, 2, false);                                        \
-    else if (A->spmv_lpr == 32 && A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 32, 1, false);                 \
-    else if (A->spmv_lpr == 32) NB_LAUNCH(RR, CC, 32, 2, false);                                        \
-    else if (A->spmv_unroll == 1) NB_LAUNCH(RR, CC, 16, 1, false);                                      \
-    else NB_LAUNCH(RR, CC, 16, 2, false);
-#define NB_VARIANTS_33                                                                                  \
-    if (A->spmv_lpr == 32 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(3, 3, 32, 1, true);           \
-    else if (A->spmv_lpr == 32 && A->spmv_nt) NB_LAUNCH(3, 3, 32, 2, true);                             \
-    else if (A->spmv_lpr == 16 && A->spmv_unroll == 1 && A->spmv_nt) NB_LAUNCH(3, 3, 16, 1, true);      \
-    else if (A->spmv_lpr == 16 && A->spmv_nt) NB_LAUNCH(3, 3, 16, 2, true);                             \
-    else { NB_VARIANTS(3, 3) }
-#define NB_CASE(RR, CC)                                                                                 \
-    if (A->R == RR && A->C == CC) {                                                                     \
-        if (RR * CC > 9 && A->spmv_nt) NB_LAUNCH(RR, CC, 64, 1, true);                                  \
-        else if (RR * CC > 9) NB_LAUNCH(RR, CC, 64, 1, false);                                          \
-        else if (RR == 3 && CC == 3) { NB_VARIANTS_33 }                                                 \
-        else { NB_VARIANTS(RR, CC) }                                                                    \
-    } else
-            NB_CASE(3, 3) NB_CASE(2, 2) NB_CASE(2, 1) NB_CASE(1, 2) NB_CASE(3, 1) NB_CASE(1, 3) NB_CASE(6, 3)
-            NB_CASE(3, 2) NB_CASE(2, 3) NB_CASE(3, 6) NB_CASE(1, 1) {
-                return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
-            }
-            KLE_HIP(hipGetLastError());
-        }
-#undef NB_CASE
-#undef NB_VARIANTS
-#undef NB_VARIANTS_33
-#undef NB_LAUNCH
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
     }
     const int grid = grid_for(A->m_local, SPMV_WAVES, PART_STRIDE - 256);
-    if (nparts) *nparts = grid;
     KLE_TRY(c->tic("spmv", &ev));
-    if (dot)
-        hipLaunchKernelGGL(k_aij_spmv<true>, dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, A->m_local, A->d_aptr,
-                           A->d_acol, A->d_aval, x->d, y->d, dotvec->d, partials, istate);
-    else
-        hipLaunchKernelGGL(k_aij_spmv<false>, dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, A->m_local, A->d_aptr,
-                           A->d_acol, A->d_aval, x->d, y->d, nullptr, partials, istate);
+    hipLaunchKernelGGL(k_aij_spmv, dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, A->m_local, A->d_aptr, A->d_acol,
+                       A->d_aval, x->d, y->d, istate);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("spmv", &ev));
     return 0;
@@ -999,7 +554,6 @@ int kle_mat_assemble(kle_mat *A)
 int kle_mat_destroy(kle_mat *A)
 {
     if (!A) return 0;
-    hipFree(A->d_order);
     hipFree(A->d_rowcnt);
     hipFree(A->d_rowbox);
     hipFree(A->d_vptr);
@@ -1064,7 +618,7 @@ int kle_mat_mult(kle_mat *A, kle_vec *x, kle_vec *y)
     KLE_ARG(A && x && y, "null arg");
     if (A->kind == 1 && !A->assembled) return fail(KLE_ERR_STATE, "matrix not assembled");
     KLE_TRY(check_mult_layout(A, x, y));
-    return spmv(A, x, y, nullptr, nullptr, nullptr, nullptr);
+    return spmv(A, x, y, nullptr);
 }
 
 int kle_mat_mult_add(kle_mat *A, kle_vec *x, kle_vec *y, kle_vec *z)
@@ -1321,7 +875,6 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
 {
     KLE_ARG(A && out, "null arg");
     kle_mat *B = new kle_mat(*A);
-    B->d_order = nullptr;
     B->d_rowcnt = nullptr;
     B->d_rowbox = nullptr;
     B->d_vptr = nullptr;
@@ -1361,13 +914,6 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     return 0;
 }
 
-int kle_mat_set_spmv_nontemporal(kle_mat *A, int nt)
-{
-    KLE_ARG(A, "null matrix");
-    A->spmv_nt = nt != 0;
-    return 0;
-}
-
 int kle_get_nb_pad(void) { return g_nb_pad; }
 
 int kle_set_nb_layout(int layout)
@@ -1378,20 +924,6 @@ int kle_set_nb_layout(int layout)
 }
 
 int kle_get_nb_layout(void) { return g_nb_layout; }
-
-int kle_mat_set_spmv_rows_per_wave(kle_mat *A, int seq)
-{
-    KLE_ARG(A && seq >= 1 && seq <= 64, "rows per wave must be in [1,64]");
-    A->spmv_seq = seq;
-    return 0;
-}
-
-int kle_mat_set_spmv_fast(kle_mat *A, int on)
-{
-    KLE_ARG(A, "null matrix");
-    A->spmv_fast = on != 0;
-    return 0;
-}
 
 int kle_mat_set_spmv_structured(kle_mat *A, int on)
 {
@@ -1418,32 +950,6 @@ int kle_set_nb_pad(int quantum)
 {
     KLE_ARG(quantum >= 1 && quantum <= 64, "pad quantum must be in [1,64]");
     g_nb_pad = quantum;
-    return 0;
-}
-
-int kle_mat_set_spmv_buffer_variant(kle_mat *A, int variant)
-{
-    KLE_ARG(A && A->kind == 0 && variant >= 0 && variant <= 8, "bad buffer variant");
-    A->spmv_buf = variant;
-    return 0;
-}
-
-int kle_mat_set_spmv_layout(kle_mat *A, int xcd_chunks, int tiled_order)
-{
-    KLE_ARG(A && A->kind == 0, "node-block matrix expected");
-    A->spmv_xcd = xcd_chunks != 0;
-    A->spmv_order = tiled_order != 0;
-    return 0;
-}
-
-int kle_mat_set_spmv_variant(kle_mat *A, int lanes_per_row, int unroll, int persistent)
-{
-    KLE_ARG(A, "null mat");
-    KLE_ARG(lanes_per_row == 64 || lanes_per_row == 32 || lanes_per_row == 16, "lanes_per_row must be 64/32/16");
-    KLE_ARG(unroll == 1 || unroll == 2, "unroll must be 1 or 2");
-    A->spmv_lpr = lanes_per_row;
-    A->spmv_unroll = unroll;
-    A->spmv_persistent = persistent != 0;
     return 0;
 }
 

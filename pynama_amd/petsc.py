@@ -378,18 +378,6 @@ class Mat:
     def owner_range(self):
         return self.getOwnershipRange()
 
-    def setSpmvVariant(self, lanes_per_row=64, unroll=1, persistent=False):
-        call("kle_mat_set_spmv_variant", self._h, int(lanes_per_row), int(unroll), int(bool(persistent)))
-
-    def setSpmvBufferVariant(self, v):
-        call("kle_mat_set_spmv_buffer_variant", self._h, int(v))
-
-    def setSpmvRowsPerWave(self, seq):
-        call("kle_mat_set_spmv_rows_per_wave", self._h, int(seq))
-
-    def setSpmvFast(self, on=True):
-        call("kle_mat_set_spmv_fast", self._h, int(bool(on)))
-
     def setSpmvStructured(self, on=True):
         call("kle_mat_set_spmv_structured", self._h, int(bool(on)))
 
@@ -400,12 +388,6 @@ class Mat:
 
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))
-
-    def setSpmvNontemporal(self, nt=True):
-        call("kle_mat_set_spmv_nontemporal", self._h, int(bool(nt)))
-
-    def setSpmvLayout(self, xcd_chunks=False, tiled_order=False):
-        call("kle_mat_set_spmv_layout", self._h, int(bool(xcd_chunks)), int(bool(tiled_order)))
 
     def getFormat(self):
         buf = C.create_string_buffer(16)
@@ -594,11 +576,6 @@ class KSP:
         self._ensure()
         call("kle_ksp_set_cg_single_reduction", self._h, int(bool(flag)))
 
-    def setFusedDot(self, flag=True):
-        """Form the CG dot (p, Ap) inside the SpMV kernel instead of a separate pass."""
-        self._ensure()
-        call("kle_ksp_set_fused_dot", self._h, int(bool(flag)))
-
     def setGMRESRestart(self, m):
         self._ensure()
         call("kle_ksp_set_gmres_restart", self._h, int(m))
@@ -630,6 +607,11 @@ class KSP:
 
     def solve(self, b, x):
         call("kle_ksp_solve", self._h, b._h, x._h)
+
+    def solveContinue(self, b, x, n):
+        """n more iterations of the preceding fixed-iteration solve on (b, x),
+        continuing its recurrence without a restart (benchmarks)."""
+        call("kle_ksp_continue", self._h, b._h, x._h, int(n))
 
     def __call__(self, b, x=None):
         if x is None:

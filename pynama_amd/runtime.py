@@ -59,7 +59,10 @@ COMM_WORLD = Comm()
 class Context:
     """transport: "rccl" (default, one GPU per rank) or "host" (collectives
     staged through host memory over torch.distributed/gloo; several ranks may
-    share one GPU -- used to test the distributed path on a single device)."""
+    share one GPU -- used to test the distributed path on a single device).
+    KLE_RCCL_SELF=1 on a single rank creates a one-rank RCCL communicator, so
+    the RCCL calls (init with deadline, allreduce on both streams) run on one
+    GPU; RCCL refuses two ranks on one device."""
 
     def __init__(self, device=None, rank=None, nranks=None, transport=None):
         load()
@@ -78,7 +81,16 @@ class Context:
             self._hc = self._host_comm()
             call("kle_ctx_create_host_comm", device, self.rank, self.nranks, C.byref(self._hc), C.byref(h))
         else:
-            uid = self._bcast_unique_id() if self.nranks > 1 else None
+            if self.nranks > 1:
+                uid = self._bcast_unique_id()
+            elif os.environ.get("KLE_RCCL_SELF") == "1":
+                # a one-rank RCCL communicator: the solver's collectives run
+                # through RCCL on one GPU (tests of the RCCL transport)
+                raw = C.create_string_buffer(128)
+                call("kle_get_unique_id", raw)
+                uid = bytes(raw.raw)
+            else:
+                uid = None
             call("kle_ctx_create", device, self.rank, self.nranks, uid, C.byref(h))
         self.h = h
 
@@ -208,6 +220,8 @@ def get_ctx():
             set_row_padding(int(os.environ["KLE_NB_PAD"]))
         if os.environ.get("KLE_NB_LAYOUT"):
             set_value_layout(int(os.environ["KLE_NB_LAYOUT"]))
+        if os.environ.get("KLE_SPMV_WAVES"):
+            set_tuning("spmv_waves", int(os.environ["KLE_SPMV_WAVES"]))
         _CTX = Context()
     return _CTX
 
@@ -222,6 +236,18 @@ def set_value_layout(layout):
     """Node-block value layout for matrices created afterwards (0 padded
     streams, 1 chunked + packed tail); KLE_NB_LAYOUT sets the initial value."""
     call("kle_set_nb_layout", int(layout))
+
+
+def set_tuning(key, value):
+    """libkle performance knob (kle_set_tuning): "spmv_waves"; every setting
+    gives correct results."""
+    call("kle_set_tuning", key.encode(), int(value))
+
+
+def get_tuning(key):
+    v = C.c_int()
+    call("kle_get_tuning", key.encode(), C.byref(v))
+    return v.value
 
 
 def get_value_layout():

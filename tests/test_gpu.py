@@ -412,7 +412,6 @@ def test_row_padding_and_nt_loads_are_exact(pa, pad):
         set_row_padding(old)
         set_value_layout(old_lay)
     a, b = mats
-    a.K.setSpmvNontemporal(False)
     for nm in ("K", "Krhs", "Rw"):
         for u, v in zip(getattr(a, nm).getValuesCSR(), getattr(b, nm).getValuesCSR()):
             np.testing.assert_array_equal(u, v)
@@ -420,9 +419,7 @@ def test_row_padding_and_nt_loads_are_exact(pa, pad):
     x = a.K.createVecRight()
     x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
     y0 = (a.K * x).getArray()
-    for nt in (False, True):
-        b.K.setSpmvNontemporal(nt)
-        np.testing.assert_array_equal((b.K * x).getArray(), y0)
+    np.testing.assert_array_equal((b.K * x).getArray(), y0)
     np.testing.assert_array_equal(b.K.getDiagonal().getArray(), a.K.getDiagonal().getArray())
     # padding is not useful traffic (only the real-length array, 4 B per row, is added)
     assert 0 <= b.K.spmvBytes() - a.K.spmvBytes() <= 4 * a.K.getSize()[0] / 3
@@ -507,12 +504,17 @@ def test_chunked_value_layout_is_exact(pa):
         np.testing.assert_array_equal(u, v)
 
 
-def test_fast_spmv_kernel_matches_generic(pa):
-    """The specialised default SpMV kernel == the generic one, bitwise, for
-    every (layout, structured) combination and the operator shapes."""
+def test_spmv_layouts_and_column_modes_agree(pa):
+    """The node-block SpMV kernel (k_nb_spmv) for both value layouts and both
+    column modes (structured boxes / streamed bcol) gives bitwise the same
+    product, and equals the exported CSR product to 1e-13, for K/Rw/Krhs and
+    the operator shapes (3x3, 6x3, 3x6)."""
+    import scipy.sparse as sp
+
     from pynama_amd.runtime import get_value_layout, set_value_layout
     g = _golden("tg3d_p4")
     old = get_value_layout()
+    ref = {}
     try:
         for lay in (0, 1):
             set_value_layout(lay)
@@ -521,19 +523,25 @@ def test_fast_spmv_kernel_matches_generic(pa):
             mat.setDomain(dom)
             mat.build()
             op = mat.getOperators()
-            rng = np.random.default_rng(lay)
-            for A in (mat.K, mat.Rw, mat.Krhs, op.SrT, op.DivSrT, op.Curl):
+            for nm, A in (("K", mat.K), ("Rw", mat.Rw), ("Krhs", mat.Krhs), ("SrT", op.SrT),
+                          ("DivSrT", op.DivSrT), ("Curl", op.Curl)):
+                rng = np.random.default_rng(len(nm))
                 x = A.createVecRight()
-                x.setArray(rng.uniform(-1, 1, x.getLocalSize()))
+                xa = rng.uniform(-1, 1, x.getLocalSize())
+                x.setArray(xa)
+                ys = []
                 for st in (True, False):
                     A.setSpmvStructured(st)
-                    A.setSpmvFast(True)
-                    y1 = (A * x).getArray()
-                    A.setSpmvFast(False)
-                    y0 = (A * x).getArray()
-                    np.testing.assert_array_equal(y1, y0)
-                A.setSpmvFast(True)
+                    ys.append((A * x).getArray())
                 A.setSpmvStructured(True)
+                np.testing.assert_array_equal(ys[0], ys[1])
+                if nm in ref:
+                    np.testing.assert_array_equal(ys[0], ref[nm])
+                else:
+                    ref[nm] = ys[0]
+                ip, ix, d = A.getValuesCSR()
+                yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
+                np.testing.assert_allclose(ys[0], yh, rtol=0, atol=1e-13 * max(1.0, np.abs(yh).max()))
     finally:
         set_value_layout(old)
 
@@ -733,6 +741,42 @@ def test_graph_replay_matches_stream_launches(pa):
     np.testing.assert_array_equal(out["1"][3], out["0"][3])
 
 
+def test_fixed_iterations_continue_the_recurrence(pa):
+    """kle_ksp_continue (the bench's timed region): W fixed iterations, then n
+    more continuing the same recurrence == W + n iterations in one solve,
+    bitwise, for single-reduction and pipelined CG (one rank); the iteration
+    count of the continuation is n and the reason CONVERGED_ITS."""
+    from pynama_amd.petsc import KSP, PC
+    g = _golden("tg3d_p4")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    K = mat.K
+    b = K.createVecLeft()
+    b.setArray(np.random.default_rng(5).uniform(-1, 1, b.getLocalSize()))
+    for kt in ("cg", "pipecg"):
+        ksp = KSP().create()
+        ksp.setType(kt)
+        pc = PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setCGSingleReduction(True)
+        ksp.setOperators(K)
+        x = K.createVecRight()
+        ksp.setFixedIterations(17)
+        ksp.solve(b, x)
+        ref = x.getArray().copy()
+        ksp.setFixedIterations(5)
+        ksp.solve(b, x)
+        ksp.solveContinue(b, x, 12)
+        assert ksp.getIterationNumber() == 12 and ksp.getConvergedReason() == 4  # KSP_CONVERGED_ITS
+        np.testing.assert_array_equal(x.getArray(), ref)
+        y = K.createVecRight()
+        with pytest.raises(pa.Error):
+            ksp.solveContinue(b, y, 3)  # not the (b, x) of the last fixed solve
+
+
 def test_config2_full_size_properties(pa):
     """BASELINE config 2 at full size (1,026,675 DoF, p = 4): size-independent
     properties of the device-assembled system.  PETSc's nonzero count
@@ -770,10 +814,6 @@ def test_config2_full_size_properties(pa):
         v.setArray(rng.uniform(-1, 1, v.getLocalSize()))
         np.testing.assert_array_equal((A0 * v).getArray(), (A1 * v).getArray())
     Ax, Ay = K * x, K * y
-    # the default kernel at this size (8 waves per workgroup) == the generic kernel, bitwise
-    K.setSpmvFast(False)
-    np.testing.assert_array_equal((K * x).getArray(), Ax.getArray())
-    K.setSpmvFast(True)
     s = x + y
     np.testing.assert_allclose((K * s).getArray(), Ax.getArray() + Ay.getArray(), rtol=1e-12, atol=1e-9)
     assert abs(y.dot(Ax) - x.dot(Ay)) <= 1e-12 * abs(y.dot(Ax))

@@ -182,3 +182,22 @@ def test_noslip_dof_sets_match_reference():
     assert sorted(dom.getTangDofs(collect=True)) == sorted(g["tang_dofs"].tolist())
     assert sorted(dom.getNormalDofs(collect=True)) == sorted(g["normal_dofs"].tolist())
     assert dom.getNodesNoSlip() == set(int(d) // 2 for d in g["tang_dofs"])
+
+
+def test_bench_launcher_failure_path():
+    """`bench.py --gpus 2` without torchrun starts its own ranks; when they
+    fail (no GPU in this container) the launcher exits non-zero, prints no
+    JSON line, and does not hang; a launch past its deadline is killed (124)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, KLE_COMM_TIMEOUT_S="20")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--nelem", "2,2,2",
+                          "--ngl", "3", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode != 0
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert "2-rank launch failed" in out.stderr
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.launch_ranks(2, ["--nelem", "2,2,2", "--no-cpu-baseline"], deadline_s=0.5) == 124

@@ -1,0 +1,89 @@
+"""In-process A/B of libkle tuning knobs on the CG loop (config 2 by default).
+
+Variants alternate block by block in ONE process on ONE assembled system, so
+box-to-box and process-to-process noise cancels; each block continues the
+same fixed-iteration recurrence (kle_ksp_continue) for --its iterations.
+
+  python tools/cg_ab.py '[{"cg_rowdot":1},{"cg_rowdot":0}]' [--nelem 20,16,16] [--reps 6] [--its 200]
+Prints one JSON line per (rep, variant) and a summary line (median ms/iter).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants")
+    ap.add_argument("--nelem", default="20,16,16")
+    ap.add_argument("--ngl", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--its", type=int, default=200)
+    ap.add_argument("--ksp", default="cg")
+    a = ap.parse_args()
+    variants = json.loads(a.variants)
+    import numpy as np
+
+    import pynama_amd as pa
+    from pynama_amd.petsc import KSP, PC
+    from pynama_amd.runtime import set_tuning
+    ctx = pa.get_ctx()
+    nelem = [int(v) for v in a.nelem.split(",")]
+    cfg = {"domain": {"ngl": a.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * 3, "upper": [1.0] * 3}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    K = mat.K
+    b = K.createVecLeft()
+    b.setArray(np.random.default_rng(1).uniform(-1, 1, b.getLocalSize()))
+    ksp = KSP().create()
+    ksp.setType(a.ksp)
+    pc = PC()
+    pc.setType("jacobi")
+    ksp.setPC(pc)
+    ksp.setCGSingleReduction(True)
+    ksp.setOperators(K)
+    x = K.createVecRight()
+    ksp.setFixedIterations(20)
+    ksp.solve(b, x)
+    res = {i: [] for i in range(len(variants))}
+    for rep in range(a.reps):
+        for i, v in enumerate(variants):
+            prof = False
+            for k, val in v.items():
+                if k == "_prof_spmv":  # HIP events around every SpMV launch (bench.py's roofline timing)
+                    prof = bool(val)
+                elif k == "_graph":  # hipGraph replay of the single-rank loop
+                    os.environ["KLE_GRAPH"] = str(int(val))
+                else:
+                    set_tuning(k, val)
+            ksp.solveContinue(b, x, 10)  # settle
+            ctx.synchronize()
+            if prof:
+                ctx.set_profiling(True, only="spmv")
+                ctx.reset_stats()
+            t = time.perf_counter()
+            ksp.solveContinue(b, x, a.its)
+            ctx.synchronize()
+            ms = (time.perf_counter() - t) / a.its * 1e3
+            if prof:
+                ctx.set_profiling(False)
+            res[i].append(ms)
+            print(json.dumps({"rep": rep, "variant": v, "ms_per_iter": ms}), flush=True)
+    print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]),
+                                   "min_ms": min(res[i])} for i, v in enumerate(variants)],
+                      "nelem": nelem, "ngl": a.ngl, "its": a.its}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
