@@ -275,7 +275,11 @@ def main():
     # the timed region continues it for exactly `steps` iterations
     kb.setFixedIterations(max(args.warmup, 1))
     kb.solve(b, x)
-    ctx.set_profiling(True, only="spmv")  # events around the SpMV launches only
+    # HIP events around one SpMV launch in `every` (sampled live inside the
+    # timed region; timing every launch costs 0.8 % of an iteration at config
+    # 2 and 6 % on a 1/8 slab: profiles/r02/cg_ab_events_*.jsonl)
+    every = max(1, min(8, args.steps // 5))
+    ctx.set_profiling(True, only="spmv", every=every)
     ctx.reset_stats()
     ctx.barrier()
     if dist is not None:

@@ -109,6 +109,9 @@ int kle_ctx_set_profiling(kle_ctx *ctx, int on);
 /* Time only the launches tagged `name` ("spmv", "dot", "cg_update", "reduce",
  * "halo", "allreduce"); NULL or "" times all of them. */
 int kle_ctx_set_profiling_filter(kle_ctx *ctx, const char *name);
+/* Time only one launch in `every` of the profiled tags (1 = all): keeps the
+ * event overhead out of a timed loop while still sampling it live. */
+int kle_ctx_set_profiling_sample(kle_ctx *c, int every);
 /* name: "spmv" | "cg_update" | "p_update" | "reduce" | "halo" | "allreduce" */
 int kle_ctx_get_kernel_stats(kle_ctx *ctx, const char *name, int64_t *count, double *total_ms);
 int kle_ctx_reset_kernel_stats(kle_ctx *ctx);

@@ -60,6 +60,7 @@ _SIGS = {
     "kle_ctx_synchronize": [vp],
     "kle_ctx_barrier": [vp],
     "kle_ctx_set_profiling": [vp, C.c_int],
+    "kle_ctx_set_profiling_sample": [vp, C.c_int],
     "kle_ctx_set_profiling_filter": [vp, C.c_char_p],
     "kle_ctx_get_kernel_stats": [vp, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)],
     "kle_ctx_reset_kernel_stats": [vp],

@@ -461,6 +461,9 @@ int kle_ctx::tic(const char *name, std::pair<hipEvent_t, hipEvent_t> *ev, hipStr
     if (!s) s = stream;
     ev->first = ev->second = nullptr;
     if (!profiling || (!prof_only.empty() && prof_only != name)) return 0;
+    // sampling: time one launch in prof_every (the events cost a few us per
+    // launch on the stream, 6 % of a CG iteration on a 1/8 slab)
+    if (prof_every > 1 && (prof_seq++ % prof_every) != 0) return 0;
     ev->first = get_event();
     ev->second = get_event();
     if (!ev->first || !ev->second) return fail(KLE_ERR_DEVICE, "hipEventCreate failed");
@@ -690,6 +693,14 @@ int kle_ctx_set_profiling_filter(kle_ctx *c, const char *name)
 {
     KLE_ARG(c, "null ctx");
     c->prof_only = name ? name : "";
+    return 0;
+}
+
+int kle_ctx_set_profiling_sample(kle_ctx *c, int every)
+{
+    KLE_ARG(c && every >= 1, "bad arg");
+    c->prof_every = every;
+    c->prof_seq = 0;
     return 0;
 }
 

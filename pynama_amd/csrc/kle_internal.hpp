@@ -98,6 +98,8 @@ struct kle_ctx {
     int64_t h_stage_n = 0;
     bool profiling = false;
     std::string prof_only;  // time only this kernel tag (empty: all)
+    int prof_every = 1;     // time one launch in prof_every (of the filtered tags)
+    int64_t prof_seq = 0;
     struct Stat {
         int64_t count = 0;
         double ms = 0;

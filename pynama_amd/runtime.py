@@ -181,9 +181,11 @@ class Context:
     def barrier(self):
         call("kle_ctx_barrier", self.h)
 
-    def set_profiling(self, on=True, only=None):
-        """Event-time device launches; `only` restricts it to one kernel tag."""
+    def set_profiling(self, on=True, only=None, every=1):
+        """Event-time device launches; `only` restricts it to one kernel tag,
+        `every` > 1 times one launch in `every` (sampled)."""
         call("kle_ctx_set_profiling_filter", self.h, only.encode() if only else None)
+        call("kle_ctx_set_profiling_sample", self.h, int(every))
         call("kle_ctx_set_profiling", self.h, int(bool(on)))
 
     def kernel_stats(self, name):
