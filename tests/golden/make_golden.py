@@ -693,6 +693,32 @@ def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True, u
     print(name, "n =", len(u), "nnz(K) =", len(out["K_data"]), "err =", out["err_l2"])
 
 
+def xdmf_fixtures():
+    """XDMF files from the reference's own XmlGenerator (viewer/xml_generator.py:4-120),
+    driven in the call sequence of Paraviewer (viewer/paraviewer.py:21-70):
+    saveMesh -> setUpDomainNodes(totalNodes) + generateXMLTemplate; each
+    saveData -> generateMeshData("mesh1") + setTimeStamp + per vector a scalar
+    attribute if its size equals the node count, else a vector attribute
+    (saveStepInXML); writeXmf -> writeFile.  Paraviewer itself imports
+    petsc4py, so the sequence is restated here; the element tree is the
+    reference class's."""
+    from viewer.xml_generator import XmlGenerator
+    for dim, n in ((2, 13), (3, 17)):
+        gen = XmlGenerator(dim, "vec-data")
+        gen.setUpDomainNodes(totalNodes=n)
+        gen.generateXMLTemplate()
+        vecs = [("velocity", dim * n), ("vorticity", (1 if dim == 2 else 3) * n), ("num proc", n)]
+        for step, t in ((1, 0.1), (2, 0.2), (10, 1.25)):
+            grid = gen.generateMeshData("mesh1")
+            gen.setTimeStamp(t, grid)
+            for name, size in vecs:
+                if size == gen.dimensions:
+                    gen.setScalarAttribute(name, step, grid)
+                else:
+                    gen.setVectorAttribute(name, step, grid)
+        gen.writeFile(os.path.join(OUT, f"xdmf_{dim}d"))
+
+
 def main(only=()):
     """Regenerate every fixture, or only the named cases (e.g. `gmsh2d`)."""
     uni = {"uniform": {"velocity": [4, 0]}}
@@ -711,6 +737,7 @@ def main(only=()):
     cases = {
         "tables": table_fixtures,
         "elements": element_fixtures,
+        "xdmf": xdmf_fixtures,
         # test_solver.py:7-25  (uniform, 3x3, ngl=3, rho=1, mu=0.01)
         "uniform2d": lambda: assembled_case("uniform2d", 2, [3, 3], 3, uni, 1.0, 0.01, None),
         # test_solver.py:27-37 (Taylor-Green 2-D, 10x10, ngl=5)
