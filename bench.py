@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-solve", action="store_true")
-    ap.add_argument("--aij", action="store_true", help="also time the scalar-CSR (aij) SpMV")
+    ap.add_argument("--no-aij", dest="aij", action="store_false",
+                    help="skip the scalar-CSR (aij) SpMV leg (default: timed at N = 1)")
     ap.add_argument("--layout", type=int, choices=[0, 1], default=1,
                     help="node-block value layout: 1 = 16-block chunks + packed tail, 0 = padded row streams")
     ap.add_argument("--pad", type=int, default=16, help="row padding quantum of layout 0 (blocks)")
@@ -319,6 +320,11 @@ def main():
 
     iters_per_s = args.steps / t_max
     achieved = tot_bytes / (spmv_avg_max * 1e-3) / 1e9 if spmv_avg_max > 0 else None
+    # SURVEY 8(d)'s scalar-CSR bytes for the same product (12 B per nonzero,
+    # int32 row pointers, x and y once): the rate a CSR kernel would need to
+    # match this launch
+    csr_bytes = 12.0 * tot_nnz + 4.0 * (n_global + 1) + 16.0 * n_global
+    csr_equiv = csr_bytes / (spmv_avg_max * 1e-3) / 1e9 if spmv_avg_max > 0 else None
 
     # plain SpMV leg: x = uniform[-1,1) from splitmix64 seeded
     # 0x5EED, 10 warm-ups, 200 timed repetitions of y = K x
@@ -416,6 +422,7 @@ def main():
                          "kernel": "k_nb_spmv<3,3,%d,%s,%d>" % (args.layout, "true" if K.isStructured() else "false",
                                                                  spmv_waves(K, args.layout)),
                          "bytes_per_launch": tot_bytes,
+                         "csr_bytes_per_launch": csr_bytes, "csr_equiv_gbps": csr_equiv,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
                          # PMC traffic rate vs this box's measured read-only streaming
                          # ceiling (per GPU): how close the SpMV is to what HBM delivers here
@@ -467,8 +474,21 @@ def splitmix_uniform(seed, lo, hi):
     return (z >> np.uint64(11)).astype(np.float64) * (2.0 / 9007199254740992.0) - 1.0
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(K, b, seconds):
-    """Oracle CSR CG (OpenMP) on the same matrix: bounded sample of ~`seconds`."""
+    """Oracle CSR CG (OpenMP) on the same matrix: bounded sample of ~`seconds`
+    on all threads the process may use, ~seconds/3 on one thread, plus the
+    host STREAM triad at both thread counts."""
     import numpy as np
 
     from oracle import oracle as O
@@ -477,16 +497,29 @@ def cpu_baseline(K, b, seconds):
     del ip, ix, d
     bb = b.getArray()
     threads = O.num_threads()
-    A.cg(bb, fixed_iters=True, maxit=3)  # first touch of the host pages
-    its, el = 0, 0.0
-    while el < seconds:  # bounded sample: chunks of 10 iterations until ~seconds
-        t = time.perf_counter()
-        A.cg(bb, fixed_iters=True, maxit=10)
-        el += time.perf_counter() - t
-        its += 10
+
+    def sample(secs, chunk):
+        A.cg(bb, fixed_iters=True, maxit=min(chunk, 3))  # first touch of the host pages
+        its, el = 0, 0.0
+        while el < secs:  # bounded sample: chunks of iterations until ~secs
+            A.cg(bb, fixed_iters=True, maxit=chunk)
+            el += A.last_loop_seconds()  # the iteration loop only (no per-call setup)
+            its += chunk
+        return its, el
+
+    its, el = sample(seconds, 10)
+    triad = O.stream_triad_gbps()
+    O.set_threads(1)
+    its1, el1 = sample(seconds / 3, 2)
+    triad1 = O.stream_triad_gbps()
+    O.set_threads(threads)
     return {"value": its / el, "unit": "CG iters/s", "cores": threads, "kind": "port",
             "sample": f"{its} fixed CG+Jacobi iterations of oracle/kle_oracle.c (CSR, OpenMP) on the same "
-                      f"assembled K ({A.nnz} nnz), {el:.1f} s"}
+                      f"assembled K ({A.nnz} nnz), {el:.1f} s; 1 thread: {its1} iterations, {el1:.1f} s",
+            "model": _cpu_model(), "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "value_1core": its1 / el1, "stream_triad_gbps": triad, "stream_triad_gbps_1core": triad1,
+            "spmv_gbps_equiv": 12.0 * A.nnz * its / el / 1e9}
 
 
 if __name__ == "__main__":

@@ -775,11 +775,18 @@ orc_csr *orc_csr_from(int64_t m, int64_t n, const int64_t *indptr, const int64_t
     orc_csr *a = calloc(1, sizeof(orc_csr));
     a->m = m; a->n = n; a->nnz = indptr[m];
     a->indptr = malloc(sizeof(int64_t) * (m + 1));
-    a->indices = malloc(sizeof(int64_t) * a->nnz);
-    a->data = malloc(sizeof(double) * a->nnz);
+    a->indices = malloc(sizeof(int64_t) * (a->nnz ? a->nnz : 1));
+    a->data = malloc(sizeof(double) * (a->nnz ? a->nnz : 1));
     memcpy(a->indptr, indptr, sizeof(int64_t) * (m + 1));
-    memcpy(a->indices, indices, sizeof(int64_t) * a->nnz);
-    memcpy(a->data, data, sizeof(double) * a->nnz);
+    /* first touch by the same static row partition orc_spmv uses, so each
+     * thread's rows sit in its own NUMA node's memory (as with one PETSc rank
+     * per core) */
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t k0 = indptr[r], k1 = indptr[r + 1];
+        memcpy(a->indices + k0, indices + k0, sizeof(int64_t) * (k1 - k0));
+        memcpy(a->data + k0, data + k0, sizeof(double) * (k1 - k0));
+    }
     return a;
 }
 
@@ -804,6 +811,7 @@ static int64_t **node_adjacency(const orc_mesh *m, const int64_t *conn, int *deg
             int64_t i = conn[e * nn + l];
             for (int k = 0; k < nn; ++k) adj[i][deg_out[i]++] = conn[e * nn + k];
         }
+#pragma omp parallel for schedule(dynamic, 1024)
     for (int64_t i = 0; i < N; ++i) {
         qsort(adj[i], deg_out[i], sizeof(int64_t), cmp_i64);
         int u = 0;
@@ -898,25 +906,44 @@ int orc_assemble_fs(const orc_mesh *m, const uint8_t *dir_flag, orc_csr **Kout,
     int nd = dim * nn, nc = 1 << dim;
     double *X = malloc(sizeof(double) * m->E * nc * dim);
     orc_mesh_corners(m, X);
-    double *Ke = malloc(sizeof(double) * nd * nd), *Rwe = malloc(sizeof(double) * nd * dw * nn),
-           *Rde = malloc(sizeof(double) * nd * nn);
-    for (int64_t e = 0; e < m->E; ++e) {
-        orc_elem_kle(el, X + e * nc * dim, Ke, Rwe, Rde);
-        const int64_t *cn = conn + e * nn;
-        for (int li = 0; li < nn; ++li) {
-            int64_t gi = cn[li];
-            if (dir_flag[gi]) continue;
-            for (int a = 0; a < dim; ++a) {
-                int64_t r = gi * dim + a;
-                for (int lj = 0; lj < nn; ++lj) {
-                    int64_t gj = cn[lj];
-                    for (int b = 0; b < dim; ++b) {
-                        double v = Ke[(li * dim + a) * nd + lj * dim + b];
-                        if (dir_flag[gj]) Kr->data[find_col(Kr, r, gj * dim + b)] += -v;
-                        else K->data[find_col(K, r, gj * dim + b)] += v;
+    /* Elements in ascending batches: the batch's element matrices in parallel
+     * (orc_elem_kle is reentrant), then the ADDs in parallel over disjoint
+     * node-row ranges, each range walking the batch in ascending cell order.
+     * Every entry therefore receives the same additions in the same order as
+     * the serial cell loop of MatFS.buildFS: the result is bitwise the serial
+     * one, at any thread count. */
+    const int64_t B = 256;
+    const size_t kes = (size_t)nd * nd, rws = (size_t)nd * dw * nn, rds = (size_t)nd * nn;
+    double *Ke = malloc(sizeof(double) * kes * B), *Rwe = malloc(sizeof(double) * rws * B),
+           *Rde = malloc(sizeof(double) * rds * B);
+    for (int64_t e0 = 0; e0 < m->E; e0 += B) {
+        const int64_t nb = m->E - e0 < B ? m->E - e0 : B;
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int64_t k = 0; k < nb; ++k)
+            orc_elem_kle(el, X + (e0 + k) * nc * dim, Ke + kes * k, Rwe + rws * k, Rde + rds * k);
+#pragma omp parallel
+        {
+            const int T = omp_get_num_threads(), t = omp_get_thread_num();
+            const int64_t nlo = N * t / T, nhi = N * (t + 1) / T;
+            for (int64_t k = 0; k < nb; ++k) {
+                const int64_t *cn = conn + (e0 + k) * nn;
+                const double *ke = Ke + kes * k, *rwe = Rwe + rws * k;
+                for (int li = 0; li < nn; ++li) {
+                    int64_t gi = cn[li];
+                    if (gi < nlo || gi >= nhi || dir_flag[gi]) continue;
+                    for (int a = 0; a < dim; ++a) {
+                        int64_t r = gi * dim + a;
+                        for (int lj = 0; lj < nn; ++lj) {
+                            int64_t gj = cn[lj];
+                            for (int b = 0; b < dim; ++b) {
+                                double v = ke[(li * dim + a) * nd + lj * dim + b];
+                                if (dir_flag[gj]) Kr->data[find_col(Kr, r, gj * dim + b)] += -v;
+                                else K->data[find_col(K, r, gj * dim + b)] += v;
+                            }
+                            for (int c = 0; c < dw; ++c)
+                                Rw->data[find_col(Rw, r, gj * dw + c)] += rwe[(li * dim + a) * dw * nn + lj * dw + c];
+                        }
                     }
-                    for (int c = 0; c < dw; ++c)
-                        Rw->data[find_col(Rw, r, gj * dw + c)] += Rwe[(li * dim + a) * dw * nn + lj * dw + c];
                 }
             }
         }
@@ -1043,6 +1070,11 @@ static double dot(int64_t n, const double *a, const double *b)
     return s;
 }
 
+static double g_cg_loop_seconds = 0.0;
+/* wall time of the last orc_cg's iteration loop (setup and the exit residual
+ * excluded): what the CPU baseline times */
+double orc_cg_loop_seconds(void) { return g_cg_loop_seconds; }
+
 /* KSPSolve_CG (PETSc 3.12, src/ksp/ksp/impls/cg/cg.c; reached through
  * kle_solver.py:35 with -ksp_type cg [-pc_type jacobi|none]); zero initial
  * guess (KSP default), convergence on the UNPRECONDITIONED residual norm:
@@ -1055,6 +1087,7 @@ int orc_cg(const orc_csr *A, const double *b, double *x, double rtol, double ato
     double *r = malloc(sizeof(double) * n), *z = malloc(sizeof(double) * n),
            *p = malloc(sizeof(double) * n), *w = malloc(sizeof(double) * n),
            *dinv = malloc(sizeof(double) * n);
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
         double d = 0;
         for (int64_t k = A->indptr[i]; k < A->indptr[i + 1]; ++k)
@@ -1069,6 +1102,7 @@ int orc_cg(const orc_csr *A, const double *b, double *x, double rtol, double ato
     double beta = dot(n, z, r), betaold = 0;
     int it = 0;
     double rn = sqrt(dot(n, r, r));
+    const double t_loop = omp_get_wtime();
     while (it < maxit && (fixed_iters || rn > tol)) {
         if (it == 0) memcpy(p, z, sizeof(double) * n);
         else {
@@ -1090,6 +1124,7 @@ int orc_cg(const orc_csr *A, const double *b, double *x, double rtol, double ato
         rn = sqrt(dot(n, r, r));
         ++it;
     }
+    g_cg_loop_seconds = omp_get_wtime() - t_loop;
     orc_spmv(A, x, w);
     double s = 0;
     for (int64_t i = 0; i < n; ++i) s += (b[i] - w[i]) * (b[i] - w[i]);
@@ -1114,4 +1149,30 @@ void orc_set_num_threads(int n)
 #else
     (void)n;
 #endif
+}
+
+/* Host STREAM triad a = b + s c (McCalpin's kernel; 24 B moved per element,
+ * the write-allocate read of `a` not counted, as STREAM reports it) over n
+ * doubles per array on the current OpenMP threads, first-touched by the same
+ * static schedule.  Best of `reps` in GB/s: the host memory ceiling the CPU
+ * baseline's CSR CG runs against. */
+double orc_stream_triad(int64_t n, int reps)
+{
+    double *a = malloc(sizeof(double) * n), *b = malloc(sizeof(double) * n), *c = malloc(sizeof(double) * n);
+    if (!a || !b || !c) { free(a); free(b); free(c); return -1.0; }
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) { a[i] = 0.0; b[i] = 1.0; c[i] = 2.0; }
+    double best = 0.0;
+    for (int r = 0; r < reps; ++r) {
+        double t0 = omp_get_wtime();
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < n; ++i) a[i] = b[i] + 3.0 * c[i];
+        double dt = omp_get_wtime() - t0;
+        double gbs = 24.0 * (double)n / dt * 1e-9;
+        if (gbs > best) best = gbs;
+    }
+    volatile double sink = a[n / 2];
+    (void)sink;
+    free(a); free(b); free(c);
+    return best;
 }

@@ -68,6 +68,10 @@ def lib():
                              C.c_int, C.c_int, C.POINTER(C.c_double)]
         L.orc_num_threads.restype = C.c_int
         L.orc_set_num_threads.argtypes = [C.c_int]
+        L.orc_cg_loop_seconds.restype = C.c_double
+        L.orc_cg_loop_seconds.argtypes = []
+        L.orc_stream_triad.restype = C.c_double
+        L.orc_stream_triad.argtypes = [C.c_int64, C.c_int]
         _LIB = L
     return _LIB
 
@@ -170,6 +174,11 @@ class CSR:
         it = lib().orc_cg(self._h, np.ascontiguousarray(b, np.float64), x, rtol, atol, maxit,
                           int(jacobi), int(fixed_iters), C.byref(rr))
         return x, it, rr.value
+
+    @staticmethod
+    def last_loop_seconds():
+        """Wall time of the last cg()'s iteration loop (no setup, no exit residual)."""
+        return lib().orc_cg_loop_seconds()
 
     def dense(self):
         d = np.zeros((self.m, self.n))
@@ -437,6 +446,11 @@ def set_threads(n):
 
 def num_threads():
     return lib().orc_num_threads()
+
+
+def stream_triad_gbps(n=1 << 26, reps=10):
+    """Host STREAM triad (GB/s, best of `reps`) on the current thread count."""
+    return lib().orc_stream_triad(int(n), int(reps))
 
 
 # ------------------------------------------------------------------ no-slip

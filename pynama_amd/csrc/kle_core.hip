@@ -510,6 +510,13 @@ int kle_set_tuning(const char *key, int value)
     if (k == "spmv_waves") {
         KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
         g_tune.spmv_waves = value;
+    } else if (k == "aij_unroll") {
+        KLE_ARG(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16,
+                "aij_unroll: 0 (default), 1, 2, 4, 8 or 16");
+        g_tune.aij_unroll = value;
+    } else if (k == "aij_waves") {
+        KLE_ARG(value == 0 || value == 4 || value == 8, "aij_waves: 0 (default), 4 or 8");
+        g_tune.aij_waves = value;
     } else {
         return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     }
@@ -521,6 +528,8 @@ int kle_get_tuning(const char *key, int *value)
     KLE_ARG(key && value, "null arg");
     const std::string k(key);
     if (k == "spmv_waves") *value = g_tune.spmv_waves;
+    else if (k == "aij_unroll") *value = g_tune.aij_unroll;
+    else if (k == "aij_waves") *value = g_tune.aij_waves;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;
 }

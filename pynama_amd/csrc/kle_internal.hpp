@@ -265,6 +265,8 @@ int grid_for(int64_t work, int per_block, int max_blocks);
 // they exist for in-process A/B measurements (tools/cg_ab.py).
 struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
+    int aij_unroll = 0;  // scalar CSR SpMV: (col, val) pairs in flight per lane: 0 default, 1, 2, 4, 8, 16
+    int aij_waves = 0;   // scalar CSR SpMV: rows (waves) per workgroup: 0 default, 4, 8
 };
 extern Tuning g_tune;
 extern int g_nb_pad;

@@ -143,23 +143,42 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     }
 }
 
-__global__ __launch_bounds__(SPMV_BLOCK) void k_aij_spmv(int64_t nrows, const int64_t *__restrict__ ptr,
-                                                         const int *__restrict__ col,
-                                                         const double *__restrict__ val,
-                                                         const double *__restrict__ x, double *__restrict__ y,
-                                                         const int *__restrict__ istate)
+// Scalar CSR SpMV (MatMult_SeqAIJ): one wavefront per row.  A pass covers
+// 64*U entries from the row start rounded down to 32 entries, so every col
+// load (32 int32 = 128 B) and every val load (16 doubles = 128 B) covers whole
+// cache lines instead of straddling the neighbouring row's, and U independent
+// (col, val) load pairs per lane are in flight before the dependent x gathers
+// (one pair per pass leaves the wave latency bound).  Lanes outside [s, e)
+// load nothing and add nothing.
+template <int U, int WV>
+__global__ __launch_bounds__(64 * WV) void k_aij_spmv(int64_t nrows, const int64_t *__restrict__ ptr,
+                                                      const int *__restrict__ col,
+                                                      const double *__restrict__ val,
+                                                      const double *__restrict__ x, double *__restrict__ y,
+                                                      const int *__restrict__ istate)
 {
     if (istate && istate[I_REASON] != 0) return;
     const int lane = threadIdx.x & 63;
-    const int64_t wave0 = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * SPMV_WAVES;
-    for (int64_t i = wave0; i < nrows; i += nwaves) {
-        const int64_t s = ptr[i], e = ptr[i + 1];
-        double acc = 0.0;
-        for (int64_t k = s + lane; k < e; k += 64) acc += ntload(val + k) * x[ntload(col + k)];
-        acc = wsum(acc);
-        if (lane == 0) y[i] = acc;
+    const int64_t i = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (i >= nrows) return;
+    const int64_t s = ptr[i], e = ptr[i + 1];
+    double acc = 0.0;
+    for (int64_t k0 = s & ~(int64_t)31; k0 < e; k0 += 64 * U) {
+        int c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = k0 + u * 64 + lane;
+            const bool on = k >= s && k < e;
+            c[u] = on ? ntload(col + k) : -1;
+            v[u] = on ? ntload(val + k) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (c[u] >= 0) acc += v[u] * x[c[u]];
     }
+    acc = wsum(acc);
+    if (lane == 0) y[i] = acc;
 }
 
 // diagonal position of each node row (for Jacobi / get_diagonal)
@@ -339,10 +358,19 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
     }
-    const int grid = grid_for(A->m_local, SPMV_WAVES, PART_STRIDE - 256);
     KLE_TRY(c->tic("spmv", &ev));
-    hipLaunchKernelGGL(k_aij_spmv, dim3(grid), dim3(SPMV_BLOCK), 0, c->stream, A->m_local, A->d_aptr, A->d_acol,
-                       A->d_aval, x->d, y->d, istate);
+    const int U = g_tune.aij_unroll ? g_tune.aij_unroll : 8;
+    const int WV = g_tune.aij_waves ? g_tune.aij_waves : 4;
+#define AIJ_U(UU, WW)                                                                                         \
+    if (U == UU && WV == WW) {                                                                                \
+        hipLaunchKernelGGL((k_aij_spmv<UU, WW>), dim3(grid_for(A->m_local, WW, 1 << 30)), dim3(64 * WW), 0,    \
+                           c->stream, A->m_local, A->d_aptr, A->d_acol, A->d_aval, x->d, y->d, istate);        \
+        launched = true;                                                                                      \
+    }
+    bool launched = false;
+    AIJ_U(1, 4) AIJ_U(2, 4) AIJ_U(4, 4) AIJ_U(8, 4) AIJ_U(16, 4) AIJ_U(8, 8) AIJ_U(16, 8)
+#undef AIJ_U
+    if (!launched) return fail(KLE_ERR_SUP, "no aij SpMV kernel for unroll %d x %d waves", U, WV);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("spmv", &ev));
     return 0;

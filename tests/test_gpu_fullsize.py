@@ -1,0 +1,130 @@
+"""BASELINE config 2 at full size against the oracle.
+
+Config 2: box [0,1]^3, nelem [20,16,16], ngl 5 (p = 4), Taylor-Green-3D
+Dirichlet data on every face: 342,225 nodes, 1,026,675 DoF, K 561,335,085
+nonzeros.  The device system (libkle: device patterns, MFMA element kernel,
+node-block gather) is compared with `oracle/kle_oracle.c`'s assembly of the
+same mesh, which restates MatFS.buildFS (mat_fs.py:131-192) cell by cell in
+ascending cell order (OpenMP over elements and disjoint row ranges; bitwise the
+serial loop):
+
+  * connectivity (reference local order, via the golden loc2lat table) and the
+    Dirichlet node set: bit-exact;
+  * K / Krhs / Rw: indptr and indices bit-exact, values <= 1e-12 * max|ref|;
+  * b = Rw w + Krhs u_bc (KleSolver.solve, kle_solver.py:33-37): <= 1e-12 *
+    max|b|;
+  * the device CG solution (rtol 1e-10, the north star's "same residual as
+    PETSc KSP within 1e-10"): true residual with the ORACLE's K and b <=
+    1.05e-10 (the device stops on its recursive residual; 5 % allows the
+    recursive/true drift), and ||u - u_oracle|| / ||u_oracle|| <= 1e-7 against
+    the oracle's Jacobi-CG at rtol 1e-10 (SURVEY 8(d) "Convergence").
+
+Runs for ~2-3 minutes on the GPU box (oracle: ~35 s of element matrices on 16
+host threads, ~70 s of CG); progress goes to stderr so a long step is visible.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+NELEM, NGL = [20, 16, 16], 5
+
+
+def _log(t0, msg):
+    sys.__stderr__.write(f"[config2-parity {time.perf_counter() - t0:7.1f}s] {msg}\n")
+    sys.__stderr__.flush()
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import pynama_amd
+    pynama_amd.load()
+    return pynama_amd
+
+
+@pytest.mark.timeout(900)
+def test_config2_full_size_matches_oracle(pa):
+    from pynama_amd import fields
+    t0 = time.perf_counter()
+    cfg = {"domain": {"ngl": NGL, "box-mesh": {"nelem": NELEM, "lower": [0, 0, 0], "upper": [1, 1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    sol = pa.KleSolver()
+    sol.setMat(mat)
+    sol.setUp()
+    f = fields.get("taylor_green3d")
+    nu = 0.01 / 0.5  # taylor-green3d.yaml: rho 0.5, mu 0.01
+    alpha = f.alpha(nu, 0.0)
+    vort = mat.Rw.createVecRight()
+    vel = sol.getSolution()
+    dom.applyBoundaryConditions(vel, "velocity", 0.0, nu)
+    ksp = sol.getKSP()
+    ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=20000)
+    _log(t0, "device system assembled")
+
+    # ---- oracle mesh: connectivity, coordinates, Dirichlet set
+    om = O.BoxMesh(3, NELEM, [0, 0, 0], [1, 1, 1], NGL)
+    assert om.N == 342225
+    loc2lat = np.load(os.path.join(G, "case_tg3d_p4.npz"))["loc2lat"]
+    assert loc2lat.shape == (NGL ** 3, 3)
+    my_idx = (loc2lat * NGL ** np.arange(3)).sum(1)
+    np.testing.assert_array_equal(dom.mesh.conn()[:, my_idx], om.conn())
+    xo = om.coords()
+    np.testing.assert_allclose(dom.getFullCoordArray().reshape(-1, 3), xo, rtol=0, atol=1e-15)
+    on_bd = ((xo == 0.0) | (xo == 1.0)).any(axis=1)
+    np.testing.assert_array_equal(np.array(sorted(dom.getNodesDirichlet())), np.flatnonzero(on_bd))
+    _log(t0, "connectivity bit-exact, coordinates, Dirichlet set equal")
+
+    vort.setArray(f.vorticity(xo, alpha))
+    b = sol.rhs(vort).copy()
+    bd = b.getArray().copy()
+    sol.solve(vort)
+    assert ksp.getConvergedReason() > 0
+    u_dev = vel.getArray().copy()
+    its_dev = ksp.getIterationNumber()
+    _log(t0, f"device CG: {its_dev} iterations, device true residual {ksp.getTrueRelativeResidual():.3e}")
+
+    # ---- oracle assembly (mat_fs.py:131-192)
+    Ko, Kro, Rwo = om.assemble_fs(on_bd.astype(np.uint8))
+    _log(t0, f"oracle assembly: K {Ko.nnz} nnz, Krhs {Kro.nnz}, Rw {Rwo.nnz}")
+    assert Ko.nnz == 561335085
+    for name, ref in (("K", Ko), ("Krhs", Kro), ("Rw", Rwo)):
+        ip, ix, d = getattr(mat, name).getValuesCSR()
+        np.testing.assert_array_equal(ip, ref.indptr, err_msg=name)
+        np.testing.assert_array_equal(ix, ref.indices, err_msg=name)
+        err = float(np.abs(d - ref.data).max())
+        assert err <= 1e-12 * float(np.abs(ref.data).max()), (name, err)
+        del ip, ix, d
+        _log(t0, f"{name}: pattern bit-exact, max|diff| {err:.3e}")
+
+    # ---- b = Rw w + Krhs u (KleSolver.solve, kle_solver.py:33-37)
+    ubc = np.zeros(om.N * 3)
+    bn = np.flatnonzero(on_bd)
+    ubc[(bn[:, None] * 3 + np.arange(3)).ravel()] = f.velocity(xo[bn], alpha)
+    bo = Rwo.mult(f.vorticity(xo, alpha)) + Kro.mult(ubc)
+    del Kro, Rwo, ref
+    berr = float(np.abs(bd - bo).max())
+    assert berr <= 1e-12 * float(np.abs(bo).max()), berr
+
+    # ---- solution: true residual with the oracle's operator, and the oracle's CG
+    res = float(np.linalg.norm(bo - Ko.mult(u_dev)) / np.linalg.norm(bo))
+    _log(t0, f"b max|diff| {berr:.3e}; true residual of the device solution with the oracle's K, b: {res:.3e}")
+    assert res <= 1.05e-10
+    uo, its_o, rr_o = Ko.cg(bo, rtol=1e-10, jacobi=True)
+    rel = float(np.linalg.norm(u_dev - uo) / np.linalg.norm(uo))
+    _log(t0, f"oracle CG: {its_o} iterations (true residual {rr_o:.3e}); ||u - u_oracle||/||u_oracle|| {rel:.3e}")
+    assert rr_o <= 1.05e-10
+    assert rel <= 1e-7
+    assert abs(its_dev - its_o) <= 4
