@@ -719,6 +719,58 @@ def xdmf_fixtures():
         gen.writeFile(os.path.join(OUT, f"xdmf_{dim}d"))
 
 
+class _Sec:
+    """Duck-typed PetscSection for IndicesManager.getSectionOffset
+    (indices.py:111-118): closure point p owns `dof[p]` nodes from offset[p]."""
+
+    def __init__(self, dofs):
+        self.dof = list(dofs)
+        self.off = list(np.concatenate([[0], np.cumsum(self.dof)[:-1]]).astype(int))
+
+    def getOffset(self, p):
+        return int(self.off[p])
+
+    def getDof(self, p):
+        return int(self.dof[p])
+
+
+def orientation_fixtures():
+    """IndicesManager.mapEntitiesToNodes (indices.py:69-92) on one cell's
+    closure with a duck-typed section, for every orientation code of every
+    edge / face slot (one slot at a time, the others 0) and for all slots at
+    once.  Closure order (DMPlex): 3-D [cell, 6 faces, 12 edges, 8 vertices],
+    2-D [cell, 4 edges, 4 vertices]; point p's nodes are the section range
+    [off[p], off[p] + dof[p]) (dof per entity: getNumCompAndNumDof,
+    indices.py:22-30).  Feeds tests/test_umesh.py's orientation-rule test."""
+    comm = types.SimpleNamespace(rank=0)
+    out = {}
+    for dim, ngls in ((2, (3, 4, 5)), (3, (3, 4, 5))):
+        for ngl in ngls:
+            m = ngl - 2
+            if dim == 3:
+                dofs = [m ** 3] + [m * m] * 6 + [m] * 12 + [1] * 8
+                slots = {"face": range(1, 7), "edge": range(7, 19), "cell": [0]}
+            else:
+                dofs = [m * m] + [m] * 4 + [1] * 4
+                slots = {"edge": range(1, 5), "cell": [0]}
+            im = IndicesManager(dim, ngl, comm)
+            im.setGlobalIndicesSection(_Sec(dofs))
+            ent = np.arange(len(dofs))
+            codes = {"face": range(-4, 4), "edge": range(-2, 2), "cell": range(-1, 2)}
+            k = f"d{dim}_n{ngl}"
+            out[f"{k}_dofs"] = np.array(dofs)
+            out[f"{k}_base"] = np.array(im.mapEntitiesToNodes(ent, np.zeros(len(dofs), int)))
+            for kind, sl in slots.items():
+                for slot in sl:
+                    for o in codes[kind]:
+                        ori = np.zeros(len(dofs), int)
+                        ori[slot] = o
+                        out[f"{k}_{kind}{slot}_o{o}"] = np.array(im.mapEntitiesToNodes(ent, ori))
+            ori = np.array([1] * len(dofs))
+            out[f"{k}_all1"] = np.array(im.mapEntitiesToNodes(ent, ori))
+    np.savez_compressed(os.path.join(OUT, "orientation.npz"), **out)
+
+
 def main(only=()):
     """Regenerate every fixture, or only the named cases (e.g. `gmsh2d`)."""
     uni = {"uniform": {"velocity": [4, 0]}}
@@ -738,6 +790,7 @@ def main(only=()):
         "tables": table_fixtures,
         "elements": element_fixtures,
         "xdmf": xdmf_fixtures,
+        "orientation": orientation_fixtures,
         # test_solver.py:7-25  (uniform, 3x3, ngl=3, rho=1, mu=0.01)
         "uniform2d": lambda: assembled_case("uniform2d", 2, [3, 3], 3, uni, 1.0, 0.01, None),
         # test_solver.py:27-37 (Taylor-Green 2-D, 10x10, ngl=5)

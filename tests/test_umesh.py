@@ -52,7 +52,7 @@ def test_gmsh_fixture_matches_oracle(ngl):
     assert len(m.face_nodes(["up", "left", "right"])) == 0
 
 
-@pytest.mark.parametrize("dim,nelem,ngl,seed", [(2, [5, 4], 4, 1), (3, [3, 3, 2], 3, 2), (3, [3, 2, 2], 5, 3),
+@pytest.mark.parametrize("dim,nelem,ngl,seed", [(2, [5, 4], 4, 1), (3, [3, 3, 2], 3, 2), (3, [2, 2, 2], 4, 5), (3, [3, 2, 2], 5, 3),
                                                 (3, [2, 2, 2], 7, 4)])
 def test_rotated_cells_match_oracle(dim, nelem, ngl, seed):
     V, C, F, T = perturbed_box(dim, nelem, seed=seed)
@@ -236,3 +236,125 @@ def test_oracle_umesh_assembly_matches_reference(case):
         np.testing.assert_array_equal(key[o], rkey, err_msg=nm)
         ref = g[nm + "_data"]
         assert np.abs(A.data[o] - ref).max() <= 1e-13 * np.abs(ref).max(), nm
+
+
+# ---------------------------------------------------------------------------
+# The reference's orientation rule (IndicesManager.mapEntitiesToNodes,
+# indices.py:69-92), pinned by tests/golden/orientation.npz: outputs of the
+# reference's own function on one cell's closure with a duck-typed section,
+# every orientation code of every edge / face / cell slot (make_golden.py).
+def _ref_rule(dim, ngl, ori, dofs):
+    """Restatement of indices.py:69-92 for a closure 0..P-1: entity order
+    vertices | edges | faces | cell (reorderEntities2D/3D, :120-126); 3-D edges
+    at enumerated positions 10,11,14,15,16,18 always reversed, faces and the
+    cell (enu > 19) reversed iff their orientation is nonzero; 2-D edges (and
+    cell) reversed iff nonzero."""
+    P = len(dofs)
+    off = np.concatenate([[0], np.cumsum(dofs)[:-1]])
+    order = list(range(19, 27)) + list(range(7, 19)) + list(range(1, 7)) + [0] if dim == 3 else \
+        list(range(5, 9)) + list(range(1, 5)) + [0]
+    assert len(order) == P
+    out = []
+    for enu, p in enumerate(order):
+        nodes = list(range(off[p], off[p] + dofs[p]))
+        if dim == 2:
+            rev = ori[p] != 0
+        else:
+            rev = enu in (10, 11, 14, 15, 16, 18) or (enu > 19 and ori[p] != 0)
+        out += nodes[::-1] if rev else nodes
+    return np.array(out)
+
+
+def test_reference_orientation_rule_is_pinned():
+    g = np.load(os.path.join(G, "orientation.npz"))
+    seen = 0
+    for key in g.files:
+        if key.endswith("_dofs"):
+            continue
+        dim, ngl = int(key[1]), int(key.split("_")[1][1:])
+        dofs = g[f"d{dim}_n{ngl}_dofs"]
+        ori = np.zeros(len(dofs), int)
+        rest = key.split("_", 2)[2]
+        if rest == "all1":
+            ori[:] = 1
+        elif rest != "base":
+            kind_slot, o = rest.split("_o")
+            slot = int("".join(ch for ch in kind_slot if ch.isdigit()))
+            ori[slot] = int(o)
+        np.testing.assert_array_equal(_ref_rule(dim, ngl, ori, dofs), g[key], err_msg=key)
+        seen += 1
+    assert seen > 300
+
+
+def _d4(m):
+    """The 8 symmetries of an m x m face lattice as permutations of its
+    row-major node list (rotations by 0..3 quarter turns, then reflected)."""
+    u, v = np.divmod(np.arange(m * m), m)
+    out = []
+    for refl in (False, True):
+        a, b = (v, u) if refl else (u, v)
+        for r in range(4):
+            out.append(a * m + b)
+            a, b = b, m - 1 - a
+    return out
+
+
+@pytest.mark.parametrize("ngl", [3, 4, 5])
+def test_reference_orientation_rule_conformity(ngl):
+    """Where the reference's numbering is conforming, and where this build
+    diverges on purpose:
+    * the rule reads only `orientation != 0` for faces / the cell, and never
+      reads edge orientations (pinned against the fixture: every nonzero face
+      code gives the same list, every edge code the base list);
+    * a nonzero face code reverses the face's m x m node list -- the 180-degree
+      rotation of the lattice -- so of the 8 relative orientations in which two
+      hexes can share a face (DMPlex codes -4..3, 0 = as created), the
+      face-interior nodes are numbered conformingly only for identity and the
+      half turn once m = ngl - 2 >= 2; edges only in the fixed box-mesh
+      pattern once they hold >= 2 nodes;
+    * for ngl <= 3 (at most one node per edge / face) the rule is conforming
+      for every orientation -- there this build's entity numbering
+      (kle_umesh.cpp) and the reference's coincide up to relabelling, which
+      test_rotated_cells_match_oracle / the golden umesh cases check; for
+      ngl >= 4 ours stays conforming for all 24 hex orientations (same test at
+      ngl 4, 5, 7) where the reference's does not."""
+    g = np.load(os.path.join(G, "orientation.npz"))
+    k = f"d3_n{ngl}"
+    base = g[f"{k}_base"]
+    m = ngl - 2
+    for slot in range(1, 7):
+        lists = {o: g[f"{k}_face{slot}_o{o}"] for o in range(-4, 4)}
+        for o in range(-4, 4):
+            if o != 0:
+                np.testing.assert_array_equal(lists[o], lists[1])
+        # position of this face's nodes in the element list, in enumeration order
+        start = 8 + 12 * m + (slot - 1) * m * m
+        seg0, seg1 = base[start:start + m * m], lists[1][start:start + m * m]
+        np.testing.assert_array_equal(seg1, seg0[::-1])
+        rot180 = _d4(m)[2]
+        np.testing.assert_array_equal(seg0[rot180], seg1)
+        # symmetries T the rule numbers correctly: identity (code 0) and the
+        # one equal to list reversal (any nonzero code)
+        ok = [T for T in _d4(m) if np.array_equal(seg0[T], seg0) or np.array_equal(seg0[T], seg1)]
+        assert len(ok) == (8 if m == 1 else 2)
+    for slot in range(7, 19):
+        for o in range(-2, 2):
+            np.testing.assert_array_equal(g[f"{k}_edge{slot}_o{o}"], base)
+    if m == 1:
+        np.testing.assert_array_equal(g[f"{k}_all1"], base)
+
+
+@pytest.mark.parametrize("ngl", [3, 4, 5])
+def test_reference_orientation_rule_2d_is_conforming(ngl):
+    """2-D: an edge's node list is reversed iff its orientation is nonzero
+    (indices.py:77-79), and reversal is the only nontrivial symmetry of an
+    edge, so the reference's quad numbering is conforming for every relative
+    orientation -- as this build's (test_rotated_cells_match_oracle, 2-D)."""
+    g = np.load(os.path.join(G, "orientation.npz"))
+    k = f"d2_n{ngl}"
+    base, m = g[f"{k}_base"], ngl - 2
+    for slot in range(1, 5):
+        start = 4 + (slot - 1) * m
+        for o in range(-2, 2):
+            seg = g[f"{k}_edge{slot}_o{o}"][start:start + m]
+            np.testing.assert_array_equal(seg, base[start:start + m][::-1] if o else base[start:start + m])
