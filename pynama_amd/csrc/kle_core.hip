@@ -510,13 +510,9 @@ int kle_set_tuning(const char *key, int value)
     if (k == "spmv_waves") {
         KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
         g_tune.spmv_waves = value;
-    } else if (k == "aij_unroll") {
-        KLE_ARG(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16,
-                "aij_unroll: 0 (default), 1, 2, 4, 8 or 16");
-        g_tune.aij_unroll = value;
-    } else if (k == "aij_waves") {
-        KLE_ARG(value == 0 || value == 4 || value == 8, "aij_waves: 0 (default), 4 or 8");
-        g_tune.aij_waves = value;
+    } else if (k == "spmv_dyn_lds") {
+        KLE_ARG(value >= -1 && value <= 65536, "spmv_dyn_lds: -1 (auto) or 0..65536 bytes");
+        g_tune.spmv_dyn_lds = value;
     } else {
         return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     }
@@ -528,8 +524,7 @@ int kle_get_tuning(const char *key, int *value)
     KLE_ARG(key && value, "null arg");
     const std::string k(key);
     if (k == "spmv_waves") *value = g_tune.spmv_waves;
-    else if (k == "aij_unroll") *value = g_tune.aij_unroll;
-    else if (k == "aij_waves") *value = g_tune.aij_waves;
+    else if (k == "spmv_dyn_lds") *value = g_tune.spmv_dyn_lds;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;
 }
@@ -558,8 +553,15 @@ static int ctx_init(int device, int rank, int nranks, kle_ctx **out)
     c->nranks = nranks;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+    // the comm stream carries the halo exchange and the Krylov reductions /
+    // allreduce that run beside the SpMV; at the highest priority its few
+    // workgroups are dispatched as soon as SpMV workgroups retire instead of
+    // queueing behind the SpMV's whole grid
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
+    const hipError_t se = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (se != hipSuccess ||
+        hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_x_ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_halo_done, hipEventDisableTiming) != hipSuccess) {
         kle_ctx_destroy(c);

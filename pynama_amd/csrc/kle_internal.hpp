@@ -93,6 +93,7 @@ struct kle_ctx {
     hipStream_t comm_stream = nullptr;        // halo exchange overlapped with interior SpMV rows
     hipEvent_t ev_x_ready = nullptr, ev_halo_done = nullptr;
     ncclComm_t comm = nullptr;
+    bool side_busy = false;  // comm-stream kernels run beside the SpMV being launched (kle_mat.hip)
     kle_host_comm hcomm = {};         // host-staged transport (testing), used when comm == nullptr
     double *h_stage = nullptr;        // pinned staging for the host transport
     int64_t h_stage_n = 0;
@@ -265,10 +266,16 @@ int grid_for(int64_t work, int per_block, int max_blocks);
 // they exist for in-process A/B measurements (tools/cg_ab.py).
 struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
-    int aij_unroll = 0;  // scalar CSR SpMV: (col, val) pairs in flight per lane: 0 default, 1, 2, 4, 8, 16
-    int aij_waves = 0;   // scalar CSR SpMV: rows (waves) per workgroup: 0 default, 4, 8
+    int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
 };
 extern Tuning g_tune;
+// marks the SpMV launches inside its scope as running beside comm-stream work
+struct SideBusy {
+    kle_ctx *c;
+    bool prev;
+    explicit SideBusy(kle_ctx *ctx) : c(ctx), prev(ctx->side_busy) { c->side_busy = true; }
+    ~SideBusy() { c->side_busy = prev; }
+};
 extern int g_nb_pad;
 extern int g_nb_layout;  // value layout of new node-block matrices (kle_mat.vlayout)
 extern int g_partitioner;  // unstructured meshes: 0 inertial bisection, 1 slabs (kle_umesh.cpp)

@@ -952,7 +952,11 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
             if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
         } else {
-            // one rank: the scalar stage first, the SpMV behind it
+            // one rank: the scalar stage first, the SpMV behind it.  Running the
+            // reduction on the comm stream beside the SpMV was measured slower at
+            // every size (1/8 slab 95.3 vs 88.9 us, 90.7 with the SpMV's LDS cap;
+            // full size 811 vs 811 us; profiles/r02/pipe_side_*.jsonl): its one
+            // workgroup waits for SpMV workgroups to drain.
             if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
             if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
         }

@@ -287,13 +287,22 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
                           const int *istate, hipStream_t st)
 {
     const int64_t nr = rm.na + rm.nb;
+    // While comm-stream kernels (halo, reductions, allreduce; N > 1 overlap)
+    // run beside this SpMV, 4-wave workgroups reserve 21 KB of (unused) LDS:
+    // 7 instead of 8 fit per CU, so the side kernels find room at once instead
+    // of waiting for the SpMV grid to drain.  Measured on one GPU with a
+    // reduction beside the SpMV of a 1/8 slab: 93.4 -> 90.7 us per iteration,
+    // the capped SpMV itself no slower (profiles/r02/lds_cap_*.jsonl).
+    // kle_set_tuning("spmv_dyn_lds") overrides.
+    const size_t lds = g_tune.spmv_dyn_lds >= 0 ? (size_t)g_tune.spmv_dyn_lds
+                                                 : (A->ctx->side_busy && wv != 8 ? 21504 : 0);
     if (R == 3 && C == 3 && LAY == 1 && wv == 8)
-        hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), 0, st, rm,
+        hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), lds, st, rm,
                            A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_bcol,
                            A->d_val, x->base, y->d, istate);
     else
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, SPMV_WAVES>), dim3(grid_for(nr, SPMV_WAVES, 1 << 30)),
-                           dim3(SPMV_BLOCK), 0, st, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,
+                           dim3(SPMV_BLOCK), lds, st, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,
                            (int)A->box_lxy, A->d_vptr, A->d_bcol, A->d_val, x->base, y->d, istate);
 }
 
@@ -343,6 +352,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
         if (!overlap) {
             KLE_TRY(launch_nb_shape(A, RowMap{0, A->nrows, 0, 0}, rbox, x, y, istate, c->stream));
         } else {
+            SideBusy busy(c);  // the halo (and, in pipecg, the reduction) run beside both launches
             KLE_HIP(hipEventRecord(c->ev_x_ready, c->stream));
             KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
             KLE_TRY(launch_nb_shape(A, RowMap{A->int_lo, A->int_hi - A->int_lo, 0, 0}, rbox, x, y, istate,
@@ -358,19 +368,12 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
         KLE_TRY(c->toc("spmv", &ev));
         return 0;
     }
+    // 8 load pairs in flight per lane, 4 rows per workgroup: 5.50 TB/s at config 2
+    // vs 5.45 (16 pairs), 5.45 (8 rows per workgroup), 4.94 (4 pairs), 3.99 TB/s
+    // (1 pair): profiles/r02/aij_ab_*.jsonl
     KLE_TRY(c->tic("spmv", &ev));
-    const int U = g_tune.aij_unroll ? g_tune.aij_unroll : 8;
-    const int WV = g_tune.aij_waves ? g_tune.aij_waves : 4;
-#define AIJ_U(UU, WW)                                                                                         \
-    if (U == UU && WV == WW) {                                                                                \
-        hipLaunchKernelGGL((k_aij_spmv<UU, WW>), dim3(grid_for(A->m_local, WW, 1 << 30)), dim3(64 * WW), 0,    \
-                           c->stream, A->m_local, A->d_aptr, A->d_acol, A->d_aval, x->d, y->d, istate);        \
-        launched = true;                                                                                      \
-    }
-    bool launched = false;
-    AIJ_U(1, 4) AIJ_U(2, 4) AIJ_U(4, 4) AIJ_U(8, 4) AIJ_U(16, 4) AIJ_U(8, 8) AIJ_U(16, 8)
-#undef AIJ_U
-    if (!launched) return fail(KLE_ERR_SUP, "no aij SpMV kernel for unroll %d x %d waves", U, WV);
+    hipLaunchKernelGGL((k_aij_spmv<8, 4>), dim3(grid_for(A->m_local, 4, 1 << 30)), dim3(256), 0, c->stream,
+                       A->m_local, A->d_aptr, A->d_acol, A->d_aval, x->d, y->d, istate);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("spmv", &ev));
     return 0;

@@ -6,7 +6,10 @@ alternate rep by rep in one process, each rep timing --its launches with HIP
 events.  Prints one JSON line per (rep, variant) and a summary; also checks
 that every variant's y is bitwise the first variant's.
 
-  python tools/aij_ab.py '[{"aij_unroll":1},{"aij_unroll":4}]' [--nelem 20,16,16] [--reps 5] [--its 50]
+  python tools/aij_ab.py '[{}]' [--nelem 20,16,16] [--reps 5] [--its 50]
+(the unroll / waves-per-workgroup knobs of the round-2 A/B,
+profiles/r02/aij_ab_*.jsonl, were removed once k_aij_spmv<8,4> won; a
+variant is a dict of kle_set_tuning keys)
 """
 import argparse
 import json

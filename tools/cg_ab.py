@@ -4,7 +4,7 @@ Variants alternate block by block in ONE process on ONE assembled system, so
 box-to-box and process-to-process noise cancels; each block continues the
 same fixed-iteration recurrence (kle_ksp_continue) for --its iterations.
 
-  python tools/cg_ab.py '[{"cg_rowdot":1},{"cg_rowdot":0}]' [--nelem 20,16,16] [--reps 6] [--its 200]
+  python tools/cg_ab.py '[{"_ksp":"cg"},{"_ksp":"pipecg"}]' [--nelem 20,16,16] [--reps 6] [--its 200]
 Prints one JSON line per (rep, variant) and a summary line (median ms/iter).
 """
 import argparse
@@ -16,6 +16,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1}  # kle_set_tuning defaults
 
 
 def main():
@@ -46,21 +49,30 @@ def main():
     K = mat.K
     b = K.createVecLeft()
     b.setArray(np.random.default_rng(1).uniform(-1, 1, b.getLocalSize()))
-    ksp = KSP().create()
-    ksp.setType(a.ksp)
-    pc = PC()
-    pc.setType("jacobi")
-    ksp.setPC(pc)
-    ksp.setCGSingleReduction(True)
-    ksp.setOperators(K)
-    x = K.createVecRight()
-    ksp.setFixedIterations(20)
-    ksp.solve(b, x)
+    solvers = {}
+
+    def solver(kt):  # one KSP (and x) per Krylov type, its recurrence started once
+        if kt not in solvers:
+            ksp = KSP().create()
+            ksp.setType(kt)
+            pc = PC()
+            pc.setType("jacobi")
+            ksp.setPC(pc)
+            ksp.setCGSingleReduction(True)
+            ksp.setOperators(K)
+            x = K.createVecRight()
+            ksp.setFixedIterations(20)
+            ksp.solve(b, x)
+            solvers[kt] = (ksp, x)
+        return solvers[kt]
     res = {i: [] for i in range(len(variants))}
     for rep in range(a.reps):
         for i, v in enumerate(variants):
             prof = False
+            ksp, x = solver(v.get("_ksp", a.ksp))
             for k, val in v.items():
+                if k == "_ksp":  # Krylov type of this variant (cg | pipecg)
+                    continue
                 if k == "_prof_spmv":  # HIP events around every SpMV launch (bench.py's roofline timing)
                     prof = bool(val)
                 elif k == "_graph":  # hipGraph replay of the single-rank loop
@@ -79,6 +91,10 @@ def main():
             if prof:
                 ctx.set_profiling(False)
             res[i].append(ms)
+            for k in v:  # back to the library defaults before the next variant
+                if k in DEFAULTS:
+                    set_tuning(k, DEFAULTS[k])
+            os.environ.pop("KLE_GRAPH", None)
             print(json.dumps({"rep": rep, "variant": v, "ms_per_iter": ms}), flush=True)
     print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]),
                                    "min_ms": min(res[i])} for i, v in enumerate(variants)],
