@@ -687,7 +687,7 @@ static int spmv_finish(kle_ksp *k, kle_vec *x, kle_vec *y, int nq0, int np0, int
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(c->tic("reduce", &ev));
     const int fuse = c->nranks == 1 && !c->comm;
-    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, FIN_BLOCKS);
+    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, g_tune.fin_blocks ? g_tune.fin_blocks : FIN_BLOCKS);
     if (nq0 == 2)
         hipLaunchKernelGGL((k_dot_finish<2, FIN_THREADS>), dim3(g), dim3(FIN_THREADS), 0, c->stream, x->n_local, x->d,
                            y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol);

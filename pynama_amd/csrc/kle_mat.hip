@@ -51,6 +51,27 @@ struct RowMap {
     int64_t a0, na, b0, nb;
 };
 
+// Logical row block of this workgroup.  Blocks b, b+8, ... share an XCD
+// (round-robin dispatch, MI355X_MICROARCH.md): within each run of 8*ch
+// blocks, XCD slot b%8 takes ch consecutive row blocks, so an XCD's L2 sees
+// compact x footprints while all XCDs stay in the same region of the matrix
+// (balance); the partial last run keeps the round-robin order.  ch = 0: plain
+// round-robin.  ch = 16: config 2 802.7 -> 797.4 us per CG iteration, 1M-DoF
+// unstructured 863.6 -> 853.5, 1/8 slab 90.1 -> 89.1 (one contiguous eighth
+// per XCD: +4 % / +25 % slower from imbalance; profiles/r02/xcd_chunk_*.jsonl).
+__device__ __forceinline__ int64_t xcd_block(int ch)
+{
+    int64_t blk = blockIdx.x;
+    if (ch > 0) {
+        const int64_t k = blk >> 3, xc = blk & 7, S = (int64_t)gridDim.x / (8 * ch);
+        if (k < S * ch) {
+            const int64_t sb = k / ch;
+            blk = sb * 8 * ch + xc * ch + (k - sb * ch);
+        }
+    }
+    return blk;
+}
+
 // Node-block SpMV: one 64-lane wavefront per node row, WV rows per
 // workgroup, one block column per lane in flight, non-temporal value/column
 // loads (read once; they must not evict the gathered x from L2), shuffle
@@ -74,12 +95,13 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
                                                         const int *__restrict__ bcol,
                                                         const double *__restrict__ val,
                                                         const double *__restrict__ x, double *__restrict__ y,
-                                                        const int *__restrict__ istate)
+                                                        const int *__restrict__ istate, int xcd_chunk)
 {
     if (istate && istate[I_REASON] != 0) return;
     constexpr int RC = R * C;
     const int lane = threadIdx.x & 63;
-    const int64_t r = (int64_t)blockIdx.x * WV + (threadIdx.x >> 6);
+    const int64_t blk = xcd_block(xcd_chunk);
+    const int64_t r = blk * WV + (threadIdx.x >> 6);
     if (r >= rm.na + rm.nb) return;
     const int64_t i = r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
     const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
@@ -155,11 +177,11 @@ __global__ __launch_bounds__(64 * WV) void k_aij_spmv(int64_t nrows, const int64
                                                       const int *__restrict__ col,
                                                       const double *__restrict__ val,
                                                       const double *__restrict__ x, double *__restrict__ y,
-                                                      const int *__restrict__ istate)
+                                                      const int *__restrict__ istate, int xcd_chunk)
 {
     if (istate && istate[I_REASON] != 0) return;
     const int lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i = xcd_block(xcd_chunk) * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (i >= nrows) return;
     const int64_t s = ptr[i], e = ptr[i + 1];
     double acc = 0.0;
@@ -299,11 +321,12 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
     if (R == 3 && C == 3 && LAY == 1 && wv == 8)
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), lds, st, rm,
                            A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_bcol,
-                           A->d_val, x->base, y->d, istate);
+                           A->d_val, x->base, y->d, istate, g_tune.spmv_xcd_chunk);
     else
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, SPMV_WAVES>), dim3(grid_for(nr, SPMV_WAVES, 1 << 30)),
                            dim3(SPMV_BLOCK), lds, st, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,
-                           (int)A->box_lxy, A->d_vptr, A->d_bcol, A->d_val, x->base, y->d, istate);
+                           (int)A->box_lxy, A->d_vptr, A->d_bcol, A->d_val, x->base, y->d, istate,
+                           g_tune.spmv_xcd_chunk);
 }
 
 template <int R, int C>
@@ -373,7 +396,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
     // (1 pair): profiles/r02/aij_ab_*.jsonl
     KLE_TRY(c->tic("spmv", &ev));
     hipLaunchKernelGGL((k_aij_spmv<8, 4>), dim3(grid_for(A->m_local, 4, 1 << 30)), dim3(256), 0, c->stream,
-                       A->m_local, A->d_aptr, A->d_acol, A->d_aval, x->d, y->d, istate);
+                       A->m_local, A->d_aptr, A->d_acol, A->d_aval, x->d, y->d, istate, g_tune.spmv_xcd_chunk);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("spmv", &ev));
     return 0;

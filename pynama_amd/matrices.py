@@ -9,6 +9,8 @@ GPU, deterministic gather into node-block CSR, PETSc pattern and ADD order.
 """
 import ctypes as C
 
+import numpy as np
+
 from ._lib import Error, call
 from .petsc import Mat
 from .runtime import get_ctx
@@ -44,7 +46,20 @@ class MatFS:
         self.Rw = Mat._wrap(hRw, ctx, mesh, dim, dim_w)
         for m, n in ((self.K, "K"), (self.Krhs, "Krhs"), (self.Rw, "Rw")):
             m.setName(n)
-        self.kle = [self.K, self.Krhs, self.Rw]
+        # Rd is preallocated but never filled in free slip (preAlloc_Rd_Rw,
+        # mat_fs.py:54-94; buildFS adds no Rd entries): after assembleAll it is
+        # an assembled [dim N x N] matrix without stored entries
+        self.Rd = self._empty(dim)
+        self.kle = [self.K, self.Krhs, self.Rw, self.Rd]
+
+    def _empty(self, dim, name="Rd"):
+        lo, hi = self.dom.getNodesRange()
+        N = self.dom.getMesh().N
+        A = Mat().createAIJ((((hi - lo) * dim, N * dim), (hi - lo, N)),
+                            nnz=(np.zeros((hi - lo) * dim, dtype=np.int32), None))
+        A.assemble()
+        A.setName(name)
+        return A
 
     def buildOperators(self):
         """Curl / SrT / DivSrT on the device (mat_fs.py:194-201)."""

@@ -828,3 +828,22 @@ def test_config2_full_size_properties(pa):
     ksp.solve(Ax, u)
     assert ksp.getConvergedReason() > 0
     assert ksp.getTrueRelativeResidual() <= 2e-10
+
+
+def test_fs_rd_is_preallocated_and_empty(pa):
+    """MatFS.Rd in free slip: preallocated by preAlloc_Rd_Rw (mat_fs.py:54-94),
+    never filled by buildFS, assembled with the rest (assembleAll): a
+    [dim N x N] matrix named "Rd" with no stored entries, in the kle list."""
+    g = _golden("tg2d_small")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    N = dom.getMesh().N
+    Rd = mat.Rd
+    assert Rd is not None and Rd.getName() == "Rd" and Rd in mat.kle
+    assert Rd.getSize() == (2 * N, N)
+    assert Rd.getInfo()["nz_used"] == 0
+    x = Rd.createVecRight()
+    x.setArray(np.random.default_rng(3).uniform(-1, 1, x.getLocalSize()))
+    np.testing.assert_array_equal((Rd * x).getArray(), np.zeros(2 * N))

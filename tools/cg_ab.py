@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1}  # kle_set_tuning defaults
+DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16, "fin_blocks": 0}  # kle_set_tuning defaults
 
 
 def main():
@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--its", type=int, default=200)
     ap.add_argument("--ksp", default="cg")
+    ap.add_argument("--mesh", choices=["box", "unstructured"], default="box",
+                    help="unstructured: the box written as a Gmsh file of perturbed, rotated, shuffled hexes "
+                         "(bench.py --mesh unstructured)")
     a = ap.parse_args()
     variants = json.loads(a.variants)
     import numpy as np
@@ -40,6 +43,13 @@ def main():
     nelem = [int(v) for v in a.nelem.split(",")]
     cfg = {"domain": {"ngl": a.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * 3, "upper": [1.0] * 3}},
            "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    if a.mesh == "unstructured":
+        import tempfile
+        from pynama_amd.meshgen import perturbed_box, write_gmsh
+        V, Cc, F, T = perturbed_box(3, nelem, seed=5)
+        path = os.path.join(tempfile.mkdtemp(prefix="kle_ab_"), "mesh.msh")
+        write_gmsh(path, 3, V, Cc, F, T)
+        cfg["domain"] = {"ngl": a.ngl, "gmsh-file": path}
     dom = pa.Domain()
     dom.configure(cfg)
     dom.setUp()
