@@ -267,7 +267,6 @@ int grid_for(int64_t work, int per_block, int max_blocks);
 struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
-    int fin_blocks = 0;     // k_dot_finish workgroups (0: 256)
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
 };
 extern Tuning g_tune;

@@ -360,7 +360,11 @@ __global__ void k_scalars(double *scal, int *ist, int stage, double rtol, double
 // Measured against forming per-row shares of (x, A x) in the SpMV epilogue
 // (8 B per row instead of the 16-B-per-entry pass here): the epilogue slowed
 // the SpMV by 1.3 % at config 2 and tied on the 1/8 slab (tools/cg_ab.py,
-// profiles/r02/cg_ab_rowdot_*.jsonl); 64x1024 / 128x512 shapes were no faster.
+// profiles/r02/cg_ab_rowdot_*.jsonl); 64x1024 / 128x512 shapes were no faster,
+// nor 64 / 128 / 512 / 1024 workgroups of 256 (config 2: 801.8 us per
+// iteration at 256 vs 803.5-812.4; 1/8 slab 88.9-89.6 for all;
+// profiles/r02/fin_blocks_*.jsonl): the launch is a latency chain (loads,
+// ticket, last-arriver sum), not bandwidth.
 // Hand-off (cdna_hip_programming.md §6 G16, counter form): partials stored
 // write-through (agent-scope atomic store = sc1), the storing wave drains
 // vmcnt, relaxed agent fetch_add on the ticket; the last arriver takes one
@@ -687,7 +691,7 @@ static int spmv_finish(kle_ksp *k, kle_vec *x, kle_vec *y, int nq0, int np0, int
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(c->tic("reduce", &ev));
     const int fuse = c->nranks == 1 && !c->comm;
-    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, g_tune.fin_blocks ? g_tune.fin_blocks : FIN_BLOCKS);
+    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, FIN_BLOCKS);
     if (nq0 == 2)
         hipLaunchKernelGGL((k_dot_finish<2, FIN_THREADS>), dim3(g), dim3(FIN_THREADS), 0, c->stream, x->n_local, x->d,
                            y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol);
