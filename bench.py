@@ -290,6 +290,11 @@ def main():
     ctx.barrier()
     t_loc = time.perf_counter() - t_start
     ctx.set_profiling(False)
+    if kb.getConvergedReason() < 0:
+        # a recurrence continued far past round-off turns its scalars NaN and
+        # every kernel into a no-op: such a timing would not be K iterations
+        raise SystemExit(f"bench: the timed CG recurrence diverged (reason {kb.getConvergedReason()}); "
+                         f"use fewer --steps")
     spmv_cnt, spmv_ms = ctx.kernel_stats("spmv")
     # per-kernel breakdown from a separate, untimed pass with every launch timed
     nb_its = min(args.steps, 50)

@@ -280,6 +280,9 @@ int kle_mat_assemble(kle_mat *A);
 int kle_mat_destroy(kle_mat *A);
 int kle_mat_get_size(const kle_mat *A, int64_t *m_global, int64_t *n_global);
 int kle_mat_get_ownership_range(const kle_mat *A, int64_t *lo, int64_t *hi);
+/* MatGetLocalSize (petsc4py Mat.getLocalSize; the local sizes behind
+ * createVecLeft / createVecRight, base_problem.py:175,184, kle_solver.py:18) */
+int kle_mat_get_local_size(const kle_mat *A, int64_t *m_local, int64_t *n_local);
 int kle_mat_get_local_nnz(const kle_mat *A, int64_t *nnz);
 /* MatGetInfo (+ sizes): PETSc nonzeros of the owned rows, the storage format
  * (0 node-block, 1 scalar AIJ), block shape and the SpMV's algorithmic bytes. */

@@ -122,6 +122,7 @@ _SIGS = {
     "kle_mat_assemble": [vp],
     "kle_mat_destroy": [vp],
     "kle_mat_get_size": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
+    "kle_mat_get_local_size": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "kle_mat_get_ownership_range": [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)],
     "kle_mat_get_local_nnz": [vp, C.POINTER(C.c_int64)],
     "kle_mat_get_info": [vp, C.c_void_p],  # kle_mat_info* (MatInfo below)

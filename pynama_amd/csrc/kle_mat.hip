@@ -492,11 +492,38 @@ int kle_mat_create_aij(kle_ctx *ctx, int64_t m_local, int64_t n_local, int64_t m
 {
     KLE_ARG(ctx && out, "null arg");
     KLE_ARG(m_local >= 0 && n_local >= 0, "negative size");
-    if (ctx->nranks > 1) return fail(KLE_ERR_SUP, "generic AIJ is single-rank; use kle_assemble_kle for MPI layouts");
-    if (m_global < 0) m_global = m_local;
-    if (n_global < 0) n_global = n_local;
-    KLE_ARG(m_global == m_local && n_global == n_local, "single rank: global size must equal local size");
+    int64_t row_lo = 0, col_lo = 0;
+    if (ctx->nranks > 1) {
+        // a distributed generic AIJ is supported only without entries: the
+        // preallocated-but-never-filled matrices of the reference (MatFS.Rd,
+        // mat_fs.py:54-94) -- its product is zero and needs no halo
+        bool empty = d_nnz != nullptr;
+        for (int64_t r = 0; empty && r < m_local; ++r) empty = d_nnz[r] == 0 && (!o_nnz || o_nnz[r] == 0);
+        if (!empty) return fail(KLE_ERR_SUP, "generic AIJ is single-rank; use kle_assemble_kle for MPI layouts");
+        std::vector<int64_t> ms(ctx->nranks), ns(ctx->nranks);
+        KLE_TRY(allgather_i64(ctx, m_local, ms));
+        KLE_TRY(allgather_i64(ctx, n_local, ns));
+        int64_t mt = 0, nt = 0;
+        for (int r = 0; r < ctx->nranks; ++r) {
+            if (r == ctx->rank) {
+                row_lo = mt;
+                col_lo = nt;
+            }
+            mt += ms[r];
+            nt += ns[r];
+        }
+        if (m_global < 0) m_global = mt;
+        if (n_global < 0) n_global = nt;
+        KLE_ARG(m_global == mt && n_global == nt, "global sizes do not match the sum of local sizes");
+    } else {
+        if (m_global < 0) m_global = m_local;
+        if (n_global < 0) n_global = n_local;
+        KLE_ARG(m_global == m_local && n_global == n_local, "single rank: global size must equal local size");
+    }
     kle_mat *A = new kle_mat;
+    A->row_lo = row_lo;
+    A->col_lo = col_lo;
+    A->empty_only = ctx->nranks > 1;
     A->ctx = ctx;
     A->kind = 1;
     A->m_local = m_local;
@@ -555,6 +582,9 @@ int kle_mat_set_values(kle_mat *A, int32_t nr, const int64_t *rows, int32_t nc, 
             if (cols[c] >= A->n_global)
                 return fail(KLE_ERR_OUTOFRANGE, "column %lld out of range", (long long)cols[c]);
             const double val = v[(int64_t)r * nc + c];
+            if (A->empty_only)
+                return fail(KLE_ERR_NEWNZ, "new nonzero at (%lld,%lld) caused a malloc (matrix preallocated empty)",
+                            (long long)rows[r], (long long)cols[c]);
             if (!A->assembled) {
                 A->stash[row].push_back({cols[c], val, addv ? 1 : 0});
             } else {
@@ -618,6 +648,14 @@ int kle_mat_destroy(kle_mat *A)
     hipFree(A->d_acol);
     hipFree(A->d_aval);
     delete A;
+    return 0;
+}
+
+int kle_mat_get_local_size(const kle_mat *A, int64_t *m, int64_t *n)
+{
+    KLE_ARG(A && m && n, "null arg");
+    *m = A->m_local;
+    *n = A->n_local;
     return 0;
 }
 

@@ -369,6 +369,11 @@ class Mat:
         call("kle_mat_get_size", self._h, C.byref(m), C.byref(n))
         return m.value, n.value
 
+    def getLocalSize(self):
+        m, n = C.c_int64(), C.c_int64()
+        call("kle_mat_get_local_size", self._h, C.byref(m), C.byref(n))
+        return m.value, n.value
+
     def getOwnershipRange(self):
         lo, hi = C.c_int64(), C.c_int64()
         call("kle_mat_get_ownership_range", self._h, C.byref(lo), C.byref(hi))
@@ -417,8 +422,8 @@ class Mat:
     def createVecRight(self):
         if self._mesh is not None:
             return Vec.fromMesh(self._mesh, self._cbs)
-        m, n = self.getSize()
-        return Vec().createMPI((n, n))
+        (_, n), (_, nl) = self.getSize(), self.getLocalSize()
+        return Vec().createMPI((nl, n))
 
     def createVecs(self):
         return self.createVecRight(), self.createVecLeft()

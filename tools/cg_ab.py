@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16}  # kle_set_tuning defaults
+DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16, "fin_blocks": 0, "ticket_slots": 8}  # kle_set_tuning defaults
 
 
 def main():
@@ -89,6 +89,11 @@ def main():
                     os.environ["KLE_GRAPH"] = str(int(val))
                 else:
                     set_tuning(k, val)
+            # a fresh fixed-iteration start per block: continuing one recurrence
+            # for thousands of iterations runs it past round-off (the scalars
+            # turn NaN and every kernel becomes a no-op)
+            ksp.setFixedIterations(20)
+            ksp.solve(b, x)
             ksp.solveContinue(b, x, 10)  # settle
             ctx.synchronize()
             if prof:
@@ -100,14 +105,19 @@ def main():
             ms = (time.perf_counter() - t) / a.its * 1e3
             if prof:
                 ctx.set_profiling(False)
-            res[i].append(ms)
             for k in v:  # back to the library defaults before the next variant
                 if k in DEFAULTS:
                     set_tuning(k, DEFAULTS[k])
             os.environ.pop("KLE_GRAPH", None)
+            if ksp.getConvergedReason() < 0:
+                print(json.dumps({"rep": rep, "variant": v, "invalid": "recurrence diverged (reason %d)"
+                                  % ksp.getConvergedReason()}), flush=True)
+                continue
+            res[i].append(ms)
             print(json.dumps({"rep": rep, "variant": v, "ms_per_iter": ms}), flush=True)
-    print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]),
-                                   "min_ms": min(res[i])} for i, v in enumerate(variants)],
+    print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]) if res[i] else None,
+                                   "min_ms": min(res[i]) if res[i] else None, "valid_reps": len(res[i])}
+                                  for i, v in enumerate(variants)],
                       "nelem": nelem, "ngl": a.ngl, "its": a.its}), flush=True)
 
 
