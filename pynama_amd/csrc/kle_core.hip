@@ -513,12 +513,6 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_xcd_chunk") {
         KLE_ARG(value >= 0 && value <= 4096, "spmv_xcd_chunk: 0 (round-robin) or row blocks per XCD run");
         g_tune.spmv_xcd_chunk = value;
-    } else if (k == "ticket_slots") {
-        KLE_ARG(value == 1 || value == 8, "ticket_slots: 1 or 8");
-        g_tune.ticket_slots = value;
-    } else if (k == "fin_blocks") {
-        KLE_ARG(value >= 0 && value <= 4096, "fin_blocks: 0 (default) .. 4096");
-        g_tune.fin_blocks = value;
     } else if (k == "spmv_dyn_lds") {
         KLE_ARG(value >= -1 && value <= 65536, "spmv_dyn_lds: -1 (auto) or 0..65536 bytes");
         g_tune.spmv_dyn_lds = value;
@@ -534,8 +528,6 @@ int kle_get_tuning(const char *key, int *value)
     const std::string k(key);
     if (k == "spmv_waves") *value = g_tune.spmv_waves;
     else if (k == "spmv_dyn_lds") *value = g_tune.spmv_dyn_lds;
-    else if (k == "fin_blocks") *value = g_tune.fin_blocks;
-    else if (k == "ticket_slots") *value = g_tune.ticket_slots;
     else if (k == "spmv_xcd_chunk") *value = g_tune.spmv_xcd_chunk;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

@@ -83,9 +83,9 @@ enum Scal {
 // [2] fixed-iteration mode, [3] maxit, [4] arrival ticket of the fused
 // dot + reduction kernel (zeroed with the rest at every solve start, reset
 // by its last-arriving workgroup).
-// I_TICKET: 9 words of the hierarchical last-arriver ticket (kle_ksp.hip
-// grid_last_arriver): 8 slot counters + 1 global; zeroed at every solve start
-enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_TICKET, I_COUNT = I_TICKET + 9 + 3 };
+// I_TICKET: the last-arriver ticket word (kle_ksp.hip grid_last_arriver),
+// zeroed at every solve start
+enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_TICKET, I_COUNT = 8 };
 
 }  // namespace kle
 
@@ -270,8 +270,6 @@ int grid_for(int64_t work, int per_block, int max_blocks);
 struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
-    int fin_blocks = 0;     // k_dot_finish workgroups (0: FIN_BLOCKS)
-    int ticket_slots = 8;   // last-arriver ticket words: 8 per-slot + global, or 1 (flat)
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
 };
 extern Tuning g_tune;

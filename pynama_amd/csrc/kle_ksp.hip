@@ -65,33 +65,18 @@ enum Stage { ST_START = 0, ST_ALPHA = 1, ST_BETA = 2, ST_SR_START = 3, ST_SR = 4
 __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, double atol);
 
 // Last-arriving workgroup of the grid, as seen by the calling thread (thread 0
-// of each workgroup, after its partials are written through).  Workgroups
-// b, b+8, ... count on slot word b % 8, the last of each slot on the global
-// word: at most ceil(G/8) arrivals per word instead of G (one word saturates
-// near 88 arrivals per us, MI355X_MICROARCH.md "dequeue").  Each word is
-// reset by its last arriver; the next launch that uses them is stream-ordered
-// behind this one.  Visibility: every workgroup's partials are complete
-// (write-through + vmcnt(0)) before its slot increment, every slot's last
-// arriver increments the global word after its slot increment returned, so
-// the global last arriver (after an agent acquire) reads all partials.
-__device__ __forceinline__ bool grid_last_arriver(int *tk, int slots)
+// of each workgroup, after its partials are written through and drained):
+// one ticket word, reset by the last arriver (the next launch that uses it is
+// stream-ordered behind this one).  Eight per-slot words + a global word
+// (fewer arrivals per word) were measured slower: 89.3 vs 88.5 us per CG
+// iteration on the 1/8 slab, 784.9 vs 784.1 at config 2
+// (profiles/r02/ticket_*.jsonl) -- at <= 256 workgroups the second atomic
+// round trip costs more than the contention it removes.
+__device__ __forceinline__ bool grid_last_arriver(int *tk)
 {
-    const int G = (int)gridDim.x, b = (int)blockIdx.x;
-    if (slots <= 1) {  // one word for the whole grid
-        const int t = __hip_atomic_fetch_add(tk + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t != G - 1) return false;
-        __hip_atomic_store(tk + 8, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return true;
-    }
-    const int slot = b & 7;
-    const int nslot = G < 8 ? G : 8;
-    const int inslot = (G - slot + 7) >> 3;
-    const int t = __hip_atomic_fetch_add(tk + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t != inslot - 1) return false;
-    __hip_atomic_store(tk + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int t2 = __hip_atomic_fetch_add(tk + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t2 != nslot - 1) return false;
-    __hip_atomic_store(tk + 8, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != (int)gridDim.x - 1) return false;
+    __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }
 
@@ -417,7 +402,7 @@ __global__ __launch_bounds__(NT) void k_dot_finish(int64_t n, const double *__re
                                                    const double *__restrict__ vy,
                                                    double *__restrict__ partials, int np0, double *__restrict__ scal,
                                                    int *__restrict__ ist, int stage, int fuse, double rtol,
-                                                   double atol, int slots)
+                                                   double atol)
 {
     if (stage != ST_SR_START && stage != ST_START && ist[I_REASON] != 0) return;
     constexpr int NQ = NQ0 + 1;
@@ -467,7 +452,7 @@ __global__ __launch_bounds__(NT) void k_dot_finish(int64_t n, const double *__re
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = grid_last_arriver(ist + I_TICKET, slots);
+        last = grid_last_arriver(ist + I_TICKET);
         if (last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -726,15 +711,13 @@ static int spmv_finish(kle_ksp *k, kle_vec *x, kle_vec *y, int nq0, int np0, int
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(c->tic("reduce", &ev));
     const int fuse = c->nranks == 1 && !c->comm;
-    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, g_tune.fin_blocks ? g_tune.fin_blocks : FIN_BLOCKS);
+    const int g = grid_for(x->n_local, FIN_THREADS * FIN_UNR, FIN_BLOCKS);
     if (nq0 == 2)
         hipLaunchKernelGGL((k_dot_finish<2, FIN_THREADS>), dim3(g), dim3(FIN_THREADS), 0, c->stream, x->n_local, x->d,
-                           y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol,
-                           g_tune.ticket_slots);
+                           y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol);
     else
         hipLaunchKernelGGL((k_dot_finish<0, FIN_THREADS>), dim3(g), dim3(FIN_THREADS), 0, c->stream, x->n_local, x->d,
-                           y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol,
-                           g_tune.ticket_slots);
+                           y->d, c->d_partials, np0, c->d_scal, c->d_istate, stage, fuse, k->rtol, k->atol);
     KLE_HIP(hipGetLastError());
     KLE_TRY(c->toc("reduce", &ev));
     if (!fuse) {
