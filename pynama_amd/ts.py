@@ -110,6 +110,9 @@ class TsSolver:
         if t != "rk":
             raise ValueError("only explicit Runge-Kutta ('rk') is provided")
 
+    def getType(self):
+        return "rk"
+
     def setRKType(self, name):
         if name not in TABLEAUX:
             raise ValueError(f"unknown RK type {name!r} (have {sorted(TABLEAUX)})")

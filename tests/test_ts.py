@@ -44,3 +44,19 @@ def test_tableau_order_conditions(name):
     if fsal:
         np.testing.assert_allclose(A[-1, :-1], b[:-1], atol=0)
         assert b[-1] == 0.0 and c[-1] == 1.0
+
+
+def test_ts_facts_from_reference_tests():
+    """The reference's own TS tests (src/tests/test_ts.py:10-19): the solver is
+    'rk' / '5bs' by default, and setUpTimes sets start, final time and the
+    step limit (ts_solver.py:12-16, MATCHSTEP final time)."""
+    from pynama_amd.ts import TsSolver
+    ts = TsSolver()
+    assert ts.getType() == "rk"
+    assert ts.getRKType() == "5bs"
+    ts.setUpTimes(1.2, 3.4, 50)
+    assert ts.getTime() == 1.2
+    assert ts.getMaxTime() == 3.4
+    assert ts.getMaxSteps() == 50
+    assert ts.exact_final_time == TsSolver.ExactFinalTime.MATCHSTEP
+    assert ts.rk_types == ["3", "5f", "5bs"]
