@@ -150,6 +150,9 @@ class TsSolver:
     def setMaxSteps(self, n):
         self.max_steps = int(n)
 
+    def getMaxSteps(self):
+        return self.max_steps
+
     def getStepNumber(self):
         return self.step_number
 
