@@ -15,29 +15,9 @@ import copy
 
 import numpy as np
 
-from . import fields
+from .boundaries import NORMAL_AXIS, BoundaryConditions
 from .mesh import FACES, BoxMesh, UnstructuredMesh
 from .runtime import world
-
-
-class _Boundary:
-    """One named face with constant values or an analytic function."""
-
-    def __init__(self, name, kind, values=None, func=None):
-        self.name, self.kind, self.values, self.func = name, kind, values or {}, func
-        self.nodes = np.zeros(0, dtype=np.int64)
-        self.coords = None
-
-    def get_values(self, var, dim, t, nu):
-        n = len(self.nodes)
-        if self.func is not None:
-            alpha = self.func.alpha(nu if nu is not None else 0.0, t if t is not None else 0.0)
-            f = self.func.velocity if var == "velocity" else self.func.vorticity
-            return np.asarray(f(self.coords, alpha), dtype=np.float64).ravel()
-        val = self.values.get(var)
-        if val is None:
-            val = [0.0] * (dim if var == "velocity" else (1 if dim == 2 else 3))
-        return np.tile(np.asarray(val, dtype=np.float64), n)
 
 
 class Domain:
@@ -45,7 +25,7 @@ class Domain:
         self.domData = None
         self.bcData = None
         self.mesh = None
-        self._bcs = []
+        self.bcs = None
         self._type = None
         self._type_mesh = None
 
@@ -99,52 +79,30 @@ class Domain:
         return self._type_mesh
 
     def _setup_bcs(self):
+        """BoundaryConditions on the mesh's named faces (domain.py:77-96:
+        setBoundaryConditions, then each face's nodes and, for analytic
+        fields, their coordinates)."""
         if not self.bcData:
             raise ValueError("Boundary Conditions Not defined")
-        names = FACES[self.dim]
-        bc = self.bcData
-        self._bcs = []
-        if "uniform" in bc:
-            self._type = "FS"
-            vals = dict(bc["uniform"])
-            vals.setdefault("vorticity", [0] if self.dim == 2 else [0, 0, 0])
-            for n in names:
-                self._bcs.append(_Boundary(n, "free-slip", vals))
-        elif "custom-func" in bc:
-            self._type = "FS"
-            f = fields.get(bc["custom-func"]["name"])
-            for n in names:
-                self._bcs.append(_Boundary(n, "free-slip", func=f))
-        elif "free-slip" in bc and "no-slip" not in bc:
-            self._type = "FS"
-            for n, v in bc["free-slip"].items():
-                if isinstance(v, dict) and "custom-func" in v:
-                    self._bcs.append(_Boundary(n, "free-slip", func=fields.get(v["custom-func"]["name"])))
-                elif isinstance(v, dict):
-                    self._bcs.append(_Boundary(n, "free-slip", dict(v)))
-                else:
-                    self._bcs.append(_Boundary(n, "free-slip", {"velocity": v}))
-        elif "no-slip" in bc and "free-slip" not in bc:
-            # walls with constant velocity (BoundaryConditions.__setBoundary,
-            # boundary_conditions.py:115-136); dict order = processing order
-            self._type = "NS"
-            zero_w = [0] if self.dim == 2 else [0, 0, 0]
-            for n, v in bc["no-slip"].items():
-                vals = dict(v) if isinstance(v, dict) else {"velocity": v}
-                vals.setdefault("vorticity", zero_w)
-                self._bcs.append(_Boundary(n, "no-slip", vals))
-        else:
+        self.bcs = BoundaryConditions(FACES[self.dim])
+        self.bcs.setBoundaryConditions(self.bcData)
+        self._type = self.bcs.getType()
+        if self._type == "FS-NS":
             # mixed free-slip + no-slip: the reference has no matrix for it either
             # (base_problem.py:161-162, "FSNS Mat not implemented")
             raise NotImplementedError("mixed free-slip / no-slip boundaries (FS-NS)")
-        for b in self._bcs:
-            b.nodes = self.mesh.face_nodes([b.name])
-            lo = self.mesh.node_range[0]
-            b.coords = self._coords[b.nodes - lo] if len(b.nodes) else np.zeros((0, self.dim))
+        lo = self.mesh.node_range[0]
+        needs = set(self.bcs.getBordersNeedsCoords())
+        for name in self.bcs.getNames():
+            nodes = self.mesh.face_nodes([name])
+            self.bcs.setBoundaryNodes(name, nodes)
+            if name in needs:
+                self.bcs.setBoundaryCoords(name, self._coords[nodes - lo] if len(nodes)
+                                           else np.zeros((0, self.dim)))
         if self._type == "NS":
-            self.mesh.set_noslip_faces([b.name for b in self._bcs])
+            self.mesh.set_noslip_faces(self.bcs.getNamesByType("no-slip"))
         else:
-            self.mesh.set_dirichlet_faces([b.name for b in self._bcs])
+            self.mesh.set_dirichlet_faces(self.bcs.getNamesByType("free-slip"))
 
     # ------------------------------------------------------------ queries
     def getMesh(self):
@@ -184,68 +142,43 @@ class Domain:
     def getBorderNodes(self, name):
         return self.mesh.face_nodes([name])
 
-    # no-slip DoF sets (BoundaryConditions.getNoSlip*, boundary_conditions.py:205-238)
-    _AXIS = {"left": 0, "right": 0, "up": 1, "down": 1, "front": 2, "back": 2}
+    # no-slip DoF sets (BoundaryConditions.getNoSlip*, boundary_conditions.py:205-238),
+    # this rank's nodes
+    _AXIS = NORMAL_AXIS
+
+    def getBoundaryConditions(self):
+        return self.bcs
 
     def _ns(self):
-        return [b for b in self._bcs if b.kind == "no-slip"]
+        return [self.bcs.getBoundary(n) for n in self.bcs.getNamesByType("no-slip")]
 
     def getNodesNoSlip(self, collect=False):
-        nodes = set()
-        for b in self._ns():
-            nodes |= set(b.nodes.tolist())
-        return nodes
+        return self.bcs.getNodesByType("no-slip")
 
     def getTangDofs(self, collect=False):
-        dofs = set()
-        for b in self._ns():
-            ax = self._AXIS[b.name]
-            for t in range(self.dim):
-                if t != ax:
-                    dofs |= set((b.nodes * self.dim + t).tolist())
-        return dofs
+        return self.bcs.getNoSlipTangDofs()
 
     def getNormalDofs(self, collect=False):
+        """collect: the corner rule of getNoSlipNormalDofs(allGather=True) --
+        a left / right wall drops its normal DoF where an earlier up / down
+        wall already fixed the node's y DoF -- on this rank's nodes."""
         dofs, remove = set(), set()
         for b in self._ns():
-            ax = self._AXIS[b.name]
-            loc = set((b.nodes * self.dim + ax).tolist())
-            if collect and b.name in ("left", "right"):
+            loc = b.getNormalDofs()
+            if collect and b.getName() in ("left", "right"):
                 remove |= {i for i in loc if i + 1 in dofs}
             dofs |= loc
         return dofs - remove
 
     def getNodesDirichlet(self, collect=False):
-        nodes = set()
-        for b in self._bcs:
-            if b.kind == "free-slip":
-                nodes |= set(b.nodes.tolist())
-        return nodes
+        return self.bcs.getNodesByType("free-slip")
 
     # -------------------------------------------------------------- BCs
     def applyBoundaryConditions(self, vec, varName, t=None, nu=None):
         """BoundaryConditions.setValuesToVec (boundary_conditions.py:252-260)."""
-        for b in self._bcs:
-            if len(b.nodes) == 0:
-                continue
-            vals = b.get_values(varName, self.dim, t, nu)
-            if self.dim == 2 and varName == "vorticity":
-                inds = b.nodes
-            else:
-                comps = self.dim
-                inds = (b.nodes[:, None] * comps + np.arange(comps)[None, :]).ravel()
-            vec.setValues(inds, vals, addv=False)
-        vec.assemble()
+        self.bcs.setValuesToVec(vec, varName, t, nu)
 
     def applyBoundaryConditionsNS(self, vec, varName, t=None, nu=None):
         """BoundaryConditions.setTangentialValuesToVec (boundary_conditions.py:262-278):
         the tangential wall velocity on every no-slip wall."""
-        for b in self._ns():
-            if len(b.nodes) == 0:
-                continue
-            vel = np.asarray(b.values["velocity"], dtype=np.float64)
-            ax = self._AXIS[b.name]
-            for t_ in range(self.dim):
-                if t_ != ax:
-                    vec.setValues(b.nodes * self.dim + t_, np.repeat(vel[t_], len(b.nodes)), addv=False)
-        vec.assemble()
+        self.bcs.setTangentialValuesToVec(vec, varName, t, nu)
