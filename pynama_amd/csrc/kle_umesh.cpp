@@ -92,6 +92,45 @@ inline uint64_t spread3(uint64_t v)  // 21 bits -> every third bit
     return v;
 }
 
+inline uint64_t spread2(uint64_t v)  // 32 bits -> every second bit
+{
+    v &= 0xffffffffull;
+    v = (v | v << 16) & 0x0000ffff0000ffffull;
+    v = (v | v << 8) & 0x00ff00ff00ff00ffull;
+    v = (v | v << 4) & 0x0f0f0f0f0f0f0f0full;
+    v = (v | v << 2) & 0x3333333333333333ull;
+    v = (v | v << 1) & 0x5555555555555555ull;
+    return v;
+}
+
+// Hilbert index of a point with b-bit coordinates q[0..n) (n = 2, 3):
+// Skilling's transform of the axes to the "transposed" index, then the bits
+// interleaved with axis 0 most significant.  Unlike the Morton (Z) order the
+// curve never jumps, so consecutive node rows stay spatially adjacent.
+inline uint64_t hilbert_key(uint32_t q[3], int n, int b)
+{
+    const uint32_t M = 1u << (b - 1);
+    for (uint32_t Q = M; Q > 1; Q >>= 1) {
+        const uint32_t P = Q - 1;
+        for (int i = 0; i < n; ++i) {
+            if (q[i] & Q) {
+                q[0] ^= P;
+            } else {
+                const uint32_t t = (q[0] ^ q[i]) & P;
+                q[0] ^= t;
+                q[i] ^= t;
+            }
+        }
+    }
+    for (int i = 1; i < n; ++i) q[i] ^= q[i - 1];
+    uint32_t t = 0;
+    for (uint32_t Q = M; Q > 1; Q >>= 1)
+        if (q[n - 1] & Q) t ^= Q - 1;
+    for (int i = 0; i < n; ++i) q[i] ^= t;
+    if (n == 2) return spread2(q[0]) << 1 | spread2(q[1]);
+    return spread3(q[0]) << 2 | spread3(q[1]) << 1 | spread3(q[2]);
+}
+
 struct Build {
     int dim, ngl, p, nn, nc;
     int64_t nv, ncell;
@@ -470,14 +509,18 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
         if (used[v]) ord.push_back(v);
     const int64_t N = (int64_t)ord.size();
     std::vector<uint64_t> code(NT, 0);
+    const char *oe = getenv("KLE_UMESH_ORDER");
+    const bool hilbert = oe && atoi(oe) == 1;
     for (int64_t v : ord) {
         uint64_t c = 0;
+        uint32_t q[3] = {0, 0, 0};
         for (int d = 0; d < dim; ++d) {
             const double s = hi[d] > lo[d] ? (X[v * dim + d] - lo[d]) / (hi[d] - lo[d]) : 0.0;
             const uint64_t qd = (uint64_t)std::min(2097151.0, std::max(0.0, s * 2097151.0));
+            q[d] = (uint32_t)qd;
             c |= spread3(qd) << d;
         }
-        code[v] = c;
+        code[v] = hilbert ? hilbert_key(q, dim, 21) : c;
     }
     auto seg = [&](int64_t v) { return seglo[v] ? 0 : seghi[v] ? 2 : 1; };
     std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
