@@ -1008,8 +1008,24 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     int64_t nb = 0;
     for (int64_t i = 0; i < nrows; ++i) nb += info[i].cnt;
     if (nb >= (1ll << 31)) return fail(KLE_ERR_SUP, "pattern too large for int32 block offsets");
+    // structured columns? each row's column list must be exactly a lattice box
+    const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
+    bool is_box = nrows > 0 && m->kind == 0;
+    std::vector<int> box(2 * std::max<int64_t>(nrows, 1), 0);
+    for (int64_t i = 0; i < nrows && is_box; ++i) {
+        if (info[i].box1 < 0) is_box = false;
+        box[2 * i] = info[i].box0;
+        box[2 * i + 1] = info[i].box1;
+    }
     const int lay = g_nb_layout;
-    const int pad = lay == 1 ? 1 : std::max(1, g_nb_pad);
+    // Layout 1 keeps the values' 128-B alignment by chunks (vptr); the column
+    // stream of a row is padded to a multiple of 32 int32 (128 B) unless the
+    // columns are computed from lattice boxes, so every 64-block pass of the
+    // SpMV reads whole 128-B column lines instead of straddling a neighbour's
+    // (KLE_BCOL_PAD overrides; 1 = unpadded).
+    int pad = lay == 1 ? (is_box ? 1 : 32) : std::max(1, g_nb_pad);
+    if (lay == 1)
+        if (const char *e = getenv("KLE_BCOL_PAD")) pad = std::max(1, atoi(e));
     std::vector<int> rp32(nrows + 1), cnt(nrows);
     int64_t nbp = 0;
     for (int64_t i = 0; i < nrows; ++i) {
@@ -1035,15 +1051,6 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     if (first_hi - (last_lo + 1) < first_any) {
         last_lo = -1;
         first_hi = first_any;
-    }
-    // structured columns? each row's column list must be exactly a lattice box
-    const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
-    bool is_box = nrows > 0 && m->kind == 0;
-    std::vector<int> box(2 * std::max<int64_t>(nrows, 1), 0);
-    for (int64_t i = 0; i < nrows && is_box; ++i) {
-        if (info[i].box1 < 0) is_box = false;
-        box[2 * i] = info[i].box0;
-        box[2 * i + 1] = info[i].box1;
     }
     std::vector<int> c32;
     if (!on_dev) {

@@ -24,7 +24,7 @@
 // cells' relative orientation (the role of the reference's orientation rules,
 // indices.py:77-85).  The reference's global numbering is PETSc's section
 // order, which is not reproducible without PETSc; ours is (owner rank,
-// interface segment, Morton order of the coordinates).  Parity tests compare
+// interface segment, Hilbert order of the coordinates).  Parity tests compare
 // through node coordinates.
 //
 // Partition (DMPlexDistribute with the Chaco partitioner, dmplex.py:21).
@@ -32,7 +32,7 @@
 // method: split the cell centroids at the weighted median of their principal
 // axis of inertia, recursively, rank counts proportional to the halves.  A
 // node belongs to the highest rank among its cells.  Owned nodes are ordered
-// [interior | rows that read ghosts] (Morton inside each), so the SpMV's
+// [interior | rows that read ghosts] (Hilbert inside each), so the SpMV's
 // ghost-free rows are one range that runs while the halo is in flight.  A
 // rank's ghosts are grouped by owner rank in ascending global id, lower ranks
 // before the owned range and higher ranks after it, so the vector layout
@@ -502,15 +502,18 @@ int kle_mesh_create_unstructured(int dim, int ngl, int64_t nverts, const double 
             if (used[v] && seglo[v] && seghi[v])
                 return fail(KLE_ERR_ARG, "slab partition too thin: rank %d has a node read by both neighbours "
                                          "(use fewer ranks)", own[v]);
-    // final numbering: (owner, segment, Morton(x), temp id)
+    // final numbering: (owner, segment, Hilbert key of x, temp id)
     std::vector<int64_t> ord;
     ord.reserve(NT);
     for (int64_t v = 0; v < NT; ++v)
         if (used[v]) ord.push_back(v);
     const int64_t N = (int64_t)ord.size();
     std::vector<uint64_t> code(NT, 0);
+    // Hilbert order (default): 1M-DoF unstructured SpMV 0.817 -> 0.810 ms,
+    // config-5 size 6.84 -> 6.67 ms vs Morton (profiles/r02/um_order*.json);
+    // KLE_UMESH_ORDER=0 selects Morton
     const char *oe = getenv("KLE_UMESH_ORDER");
-    const bool hilbert = oe && atoi(oe) == 1;
+    const bool hilbert = !(oe && atoi(oe) == 0);
     for (int64_t v : ord) {
         uint64_t c = 0;
         uint32_t q[3] = {0, 0, 0};
