@@ -513,9 +513,6 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_xcd_chunk") {
         KLE_ARG(value >= 0 && value <= 4096, "spmv_xcd_chunk: 0 (round-robin) or row blocks per XCD run");
         g_tune.spmv_xcd_chunk = value;
-    } else if (k == "spmv_split") {
-        KLE_ARG(value == 1 || value == 2 || value == 4, "spmv_split: 1, 2 or 4");
-        g_tune.spmv_split = value;
     } else if (k == "spmv_dyn_lds") {
         KLE_ARG(value >= -1 && value <= 65536, "spmv_dyn_lds: -1 (auto) or 0..65536 bytes");
         g_tune.spmv_dyn_lds = value;
@@ -531,7 +528,6 @@ int kle_get_tuning(const char *key, int *value)
     const std::string k(key);
     if (k == "spmv_waves") *value = g_tune.spmv_waves;
     else if (k == "spmv_dyn_lds") *value = g_tune.spmv_dyn_lds;
-    else if (k == "spmv_split") *value = g_tune.spmv_split;
     else if (k == "spmv_xcd_chunk") *value = g_tune.spmv_xcd_chunk;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

@@ -270,7 +270,6 @@ int grid_for(int64_t work, int per_block, int max_blocks);
 struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
-    int spmv_split = 1;     // node-block SpMV (3x3, layout 1): waves per row (1, 2, 4)
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
 };
 extern Tuning g_tune;

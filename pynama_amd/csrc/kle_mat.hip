@@ -87,11 +87,7 @@ __device__ __forceinline__ int64_t xcd_block(int ch)
 // per lane in flight, persistent grid, XCD-chunked and (x,y)-tiled row
 // orders, rows-per-wave prefetch, buffer-descriptor cache policies, the dot
 // fused into the epilogue): DESIGN.md §3; code in git history (a54a1e5^).
-// SPL > 1: SPL waves share one row (wave p takes passes p, p + SPL, ...) and
-// their row sums are added in LDS in a fixed order (deterministic): shorter
-// waves, so the grid's tail -- the last long rows running on an emptying GPU --
-// shrinks.
-template <int R, int C, int LAY, bool STRUCT, int WV, int SPL = 1>
+template <int R, int C, int LAY, bool STRUCT, int WV>
 __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMap rm, const int *__restrict__ rowptr,
                                                         const int *__restrict__ rowcnt,
                                                         const int *__restrict__ rowbox, int lx, int lxy,
@@ -105,12 +101,10 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     constexpr int RC = R * C;
     const int lane = threadIdx.x & 63;
     const int64_t blk = xcd_block(xcd_chunk);
-    const int w = threadIdx.x >> 6, part = w % SPL;
-    const int64_t r = blk * (WV / SPL) + w / SPL;
-    const bool active = r < rm.na + rm.nb;
-    if (SPL == 1 && !active) return;  // (SPL > 1: every wave reaches the LDS barrier)
-    const int64_t i = !active ? 0 : r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
-    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = !active ? 0 : rowcnt ? rowcnt[i] : mp;
+    const int64_t r = blk * WV + (threadIdx.x >> 6);
+    if (r >= rm.na + rm.nb) return;
+    const int64_t i = r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
     const double *v = val + vptr[i];
     int bbase = 0, bnx = 1, bnxy = 1;
     if constexpr (STRUCT) {
@@ -123,7 +117,7 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     double acc[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) acc[a] = 0.0;
-    for (int kb = part * 64; kb < m; kb += 64 * SPL) {
+    for (int kb = 0; kb < m; kb += 64) {
         const int k = kb + lane;
         const bool on = k < m;
         int j = 0;
@@ -162,22 +156,12 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-    double mine = acc[0];
+    if (lane < R) {
+        double mine = acc[0];
 #pragma unroll
-    for (int a = 1; a < R; ++a)
-        if (lane == a) mine = acc[a];
-    if constexpr (SPL == 1) {
-        if (lane < R) y[i * R + lane] = mine;
-    } else {
-        __shared__ double sp[WV][R];
-        if (lane < R) sp[w][lane] = mine;
-        __syncthreads();
-        if (active && part == 0 && lane < R) {
-            double t = sp[w][lane];
-#pragma unroll
-            for (int q = 1; q < SPL; ++q) t += sp[w + q][lane];
-            y[i * R + lane] = t;
-        }
+        for (int a = 1; a < R; ++a)
+            if (lane == a) mine = acc[a];
+        y[i * R + lane] = mine;
     }
 }
 
@@ -334,19 +318,6 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
     // kle_set_tuning("spmv_dyn_lds") overrides.
     const size_t lds = g_tune.spmv_dyn_lds >= 0 ? (size_t)g_tune.spmv_dyn_lds
                                                  : (A->ctx->side_busy && wv != 8 ? 21504 : 0);
-    const int spl = g_tune.spmv_split;
-    if (R == 3 && C == 3 && LAY == 1 && spl > 1) {
-#define NB_SPLIT(WW, SS)                                                                                        \
-    if (wv == WW && spl == SS) {                                                                                \
-        hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, WW, SS>), dim3(grid_for(nr, WW / SS, 1 << 30)),      \
-                           dim3(64 * WW), lds, st, rm, A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx,         \
-                           (int)A->box_lxy, A->d_vptr, A->d_bcol, A->d_val, x->base, y->d, istate,             \
-                           g_tune.spmv_xcd_chunk);                                                              \
-        return;                                                                                                 \
-    }
-        NB_SPLIT(8, 2) NB_SPLIT(8, 4) NB_SPLIT(4, 2) NB_SPLIT(4, 4)
-#undef NB_SPLIT
-    }
     if (R == 3 && C == 3 && LAY == 1 && wv == 8)
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), lds, st, rm,
                            A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_bcol,
