@@ -77,7 +77,8 @@ using PlanPtr = std::shared_ptr<HaloPlan>;
 enum Scal {
     S_RHO = 0, S_RHO_OLD, S_PQ, S_ALPHA, S_BETA, S_RR, S_TOL, S_BNORM,
     S_SUM0, S_SUM1, S_SUM2, S_SUM3,  // raw reduction outputs
-    S_TMP0, S_TMP1
+    S_TMP0, S_TMP1,
+    S_PRHO0, S_PRHO1, S_PALPHA0, S_PALPHA1  // pipelined CG: stage inputs, double-buffered by launch parity
 };
 // Device integer state: [0] reason (0 iterating), [1] iterations done,
 // [2] fixed-iteration mode, [3] maxit, [4] arrival ticket of the fused
@@ -85,7 +86,8 @@ enum Scal {
 // by its last-arriving workgroup).
 // I_TICKET: the last-arriver ticket word (kle_ksp.hip grid_last_arriver),
 // zeroed at every solve start
-enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_TICKET, I_COUNT = 8 };
+// I_PITS0/1: pipelined CG iteration count, double-buffered by launch parity
+enum IState { I_REASON = 0, I_ITS, I_FIXED, I_MAXIT, I_TICKET, I_PITS0, I_PITS1, I_COUNT = 8 };
 
 }  // namespace kle
 

@@ -186,53 +186,6 @@ __global__ __launch_bounds__(KB) void k_sr_update(int64_t n, const double *__res
     block_sums<2>(acc, partials, PART_STRIDE);
 }
 
-// Pipelined CG (Ghysels & Vanroose 2014; PETSc KSPPIPECG): with w = A u,
-// u = M r kept by recurrence, one fused pass per iteration
-//   z = n + b z, q = m + b q, s = w + b s, p = u + b p,
-//   x += a p, r -= a s, u -= a q, w -= a z, m = M w
-// partials: [0] r.u, [1] r.r, [2] w.u -- reduced while the SpMV n = A m runs
-// (N > 1), or before it (one rank).  Reducing them in the update kernel's
-// last-arriving workgroup instead was measured slower: the per-workgroup
-// write-through + ticket round trip at the end of every workgroup made the
-// update 6.4 -> 15.7 us on the 1/8 slab and 40 us at config 2, more than the
-// separate reduction launch it saved (profiles/r02/ab_*_fused_pipe.jsonl).
-template <bool JAC>
-__global__ __launch_bounds__(KB) void k_pipe_update(int64_t n, const double *__restrict__ dinv,
-                                                    const double *__restrict__ nv, double *__restrict__ z,
-                                                    double *__restrict__ q, double *__restrict__ sv,
-                                                    double *__restrict__ p, double *__restrict__ x,
-                                                    double *__restrict__ r, double *__restrict__ u,
-                                                    double *__restrict__ w, double *__restrict__ m,
-                                                    double *__restrict__ partials, const double *__restrict__ scal,
-                                                    const int *__restrict__ ist)
-{
-    if (ist[I_REASON] != 0) return;
-    const double alpha = scal[S_ALPHA], beta = scal[S_BETA];
-    double acc[3] = {0.0, 0.0, 0.0};
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double zi = nv[i] + beta * z[i];
-        const double qi = m[i] + beta * q[i];
-        const double si = w[i] + beta * sv[i];
-        const double pi = u[i] + beta * p[i];
-        z[i] = zi;
-        q[i] = qi;
-        sv[i] = si;
-        p[i] = pi;
-        x[i] += alpha * pi;
-        const double ri = r[i] - alpha * si;
-        const double ui = u[i] - alpha * qi;
-        const double wi = w[i] - alpha * zi;
-        r[i] = ri;
-        u[i] = ui;
-        w[i] = wi;
-        m[i] = JAC ? dinv[i] * wi : wi;
-        acc[0] += ri * ui;
-        acc[1] += ri * ri;
-        acc[2] += wi * ui;
-    }
-    block_sums<3>(acc, partials, PART_STRIDE);
-}
-
 // m = M w ; z = q = 0 (start of pipelined CG)
 template <bool JAC>
 __global__ __launch_bounds__(KB) void k_pipe_init(int64_t n, const double *__restrict__ dinv,
@@ -244,6 +197,47 @@ __global__ __launch_bounds__(KB) void k_pipe_init(int64_t n, const double *__res
         z[i] = 0.0;
         q[i] = 0.0;
     }
+}
+
+// One Chronopoulos-Gear scalar stage from the three sums g = (r,u),
+// rn = ||r||, d = (w,u) and the previous rho / alpha / iteration count: the
+// iteration count, a reason (0: go on) and, when the recurrence continues
+// (upd), the new beta, alpha, rho.  Shared by cg_scalars (ST_SR) and the
+// pipelined update's prologue, so both apply the same arithmetic.
+struct SrStep {
+    double alpha, beta, rho;
+    int its, reason;
+    bool upd;
+};
+__device__ __forceinline__ SrStep sr_step(double g, double rn, double d, double rho_prev, double alpha_prev,
+                                          int its_prev, double tol, int fixed, int maxit, double atol)
+{
+    SrStep s{alpha_prev, 0.0, rho_prev, its_prev + 1, 0, false};
+    if (fixed) {
+        // fixed iterations: the host launches exactly I_FIXED of them, so no
+        // kernel has to stop; the recurrence stays complete for kle_ksp_continue
+        if (!isfinite(rn)) s.reason = KLE_DIVERGED_NANORINF;
+    } else if (!isfinite(rn)) {
+        s.reason = KLE_DIVERGED_NANORINF;
+        return s;
+    } else if (rn <= tol) {
+        s.reason = rn <= atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
+        return s;
+    } else if (s.its >= maxit) {
+        s.reason = KLE_DIVERGED_ITS;
+        return s;
+    }
+    const double beta = g / rho_prev;
+    const double den = d - beta * g / alpha_prev;
+    if (den <= 0.0 && !fixed) {
+        s.reason = -8;
+        return s;
+    }
+    s.beta = beta;
+    s.alpha = g / den;
+    s.rho = g;
+    s.upd = true;
+    return s;
 }
 
 __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, double atol)
@@ -267,30 +261,15 @@ __device__ void cg_scalars(int stage, double *scal, int *ist, double rtol, doubl
             return;
         }
         if (ist[I_REASON] != 0) return;
-        const int its = ++ist[I_ITS];
-        if (ist[I_FIXED]) {
-            // fixed iterations: the host launches exactly I_FIXED of them, so no
-            // kernel has to stop; the recurrence stays complete for kle_ksp_continue
-            if (!isfinite(rn)) ist[I_REASON] = KLE_DIVERGED_NANORINF;
-        } else if (!isfinite(rn)) {
-            ist[I_REASON] = KLE_DIVERGED_NANORINF;
-            return;
-        } else if (rn <= scal[S_TOL]) {
-            ist[I_REASON] = rn <= atol ? KLE_CONVERGED_ATOL : KLE_CONVERGED_RTOL;
-            return;
-        } else if (its >= ist[I_MAXIT]) {
-            ist[I_REASON] = KLE_DIVERGED_ITS;
-            return;
+        const SrStep st = sr_step(g, rn, d, scal[S_RHO], scal[S_ALPHA], ist[I_ITS], scal[S_TOL], ist[I_FIXED],
+                                  ist[I_MAXIT], atol);
+        ist[I_ITS] = st.its;
+        if (st.reason) ist[I_REASON] = st.reason;
+        if (st.upd) {
+            scal[S_BETA] = st.beta;
+            scal[S_ALPHA] = st.alpha;
+            scal[S_RHO] = st.rho;
         }
-        const double beta = g / scal[S_RHO];
-        const double den = d - beta * g / scal[S_ALPHA];
-        if (den <= 0.0 && !ist[I_FIXED]) {
-            ist[I_REASON] = -8;
-            return;
-        }
-        scal[S_BETA] = beta;
-        scal[S_ALPHA] = g / den;
-        scal[S_RHO] = g;
         return;
     }
     if (stage == ST_START) {
@@ -372,6 +351,148 @@ __global__ __launch_bounds__(1024) void k_reduce_stage(const double *__restrict_
 __global__ void k_scalars(double *scal, int *ist, int stage, double rtol, double atol)
 {
     cg_scalars(stage, scal, ist, rtol, atol);
+}
+
+// Sums of the [3][G] per-workgroup partials of the previous pipelined update
+// in a fixed order (every caller gets bitwise the same three values).
+__device__ __forceinline__ void pipe_sums(const double *__restrict__ pp, int G, double (&t)[3])
+{
+    __shared__ double red[3][KB / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double a[3] = {0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < G; i += KB) {
+        a[0] += pp[i];
+        a[1] += pp[G + i];
+        a[2] += pp[2 * G + i];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] = wsum2(a[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) red[q][w] = a[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < KB / 64; ++i) s += red[q][i];
+        t[q] = s;
+    }
+}
+
+// One pipelined CG iteration (PETSc KSPPIPECG; Ghysels & Vanroose 2014):
+// with w = A u, u = M r kept by recurrence, one fused pass
+//   z = n + b z, q = m + b q, s = w + b s, p = u + b p,
+//   x += a p, r -= a s, u -= a q, w -= a z, m = M w
+// writing its per-workgroup sums (r,u), (r,r), (w,u) to pp_out [3][G].
+// pro = 1: the prologue first applies the PREVIOUS iteration's scalar stage --
+// every workgroup sums pp_in (the previous launch's partials, allreduced over
+// the ranks) in the same fixed order and runs sr_step, so no reduction or
+// scalar launch sits between two iterations (one rank: update + SpMV per
+// iteration).  The stage's inputs (rho, alpha, iteration count) are
+// double-buffered by launch parity: this launch reads set `par`, workgroup 0
+// writes set par^1 and the reporting slots.  pro = 0 (first launch after a
+// start or a flush): alpha, beta from the scalar slots.  A stage that ends the
+// solve (converged, diverged, NaN) skips the update in every workgroup, as the
+// reason word makes every later launch a no-op.
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_pipe_iter(int64_t n, const double *__restrict__ dinv,
+                                                  const double *__restrict__ nv, double *__restrict__ z,
+                                                  double *__restrict__ q, double *__restrict__ sv,
+                                                  double *__restrict__ p, double *__restrict__ x,
+                                                  double *__restrict__ r, double *__restrict__ u,
+                                                  double *__restrict__ w, double *__restrict__ m,
+                                                  const double *__restrict__ pp_in, double *__restrict__ pp_out,
+                                                  double *__restrict__ scal, int *__restrict__ ist, int pro, int par,
+                                                  double atol)
+{
+    if (ist[I_REASON] != 0) return;
+    __shared__ double ab[2];
+    __shared__ int stop;
+    const bool w0 = blockIdx.x == 0 && threadIdx.x == 0;
+    const int nxt = par ^ 1;
+    if (pro) {
+        double t[3];
+        pipe_sums(pp_in, (int)gridDim.x, t);
+        if (threadIdx.x == 0) {
+            const double rn = sqrt(t[1]);
+            const SrStep st = sr_step(t[0], rn, t[2], scal[S_PRHO0 + par], scal[S_PALPHA0 + par], ist[I_PITS0 + par],
+                                      scal[S_TOL], ist[I_FIXED], ist[I_MAXIT], atol);
+            ab[0] = st.alpha;
+            ab[1] = st.beta;
+            stop = st.reason != 0;
+            if (w0) {
+                scal[S_RR] = t[1];
+                ist[I_ITS] = st.its;
+                if (st.upd) {
+                    scal[S_ALPHA] = st.alpha;
+                    scal[S_BETA] = st.beta;
+                    scal[S_RHO] = st.rho;
+                }
+                scal[S_PRHO0 + nxt] = st.rho;
+                scal[S_PALPHA0 + nxt] = st.alpha;
+                ist[I_PITS0 + nxt] = st.its;
+                if (st.reason) ist[I_REASON] = st.reason;
+            }
+        }
+    } else if (threadIdx.x == 0) {
+        ab[0] = scal[S_ALPHA];
+        ab[1] = scal[S_BETA];
+        stop = 0;
+        if (w0) {
+            scal[S_PRHO0 + nxt] = scal[S_RHO];
+            scal[S_PALPHA0 + nxt] = scal[S_ALPHA];
+            ist[I_PITS0 + nxt] = ist[I_ITS];
+        }
+    }
+    __syncthreads();
+    if (stop) return;
+    const double alpha = ab[0], beta = ab[1];
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double zi = nv[i] + beta * z[i];
+        const double qi = m[i] + beta * q[i];
+        const double si = w[i] + beta * sv[i];
+        const double pi = u[i] + beta * p[i];
+        z[i] = zi;
+        q[i] = qi;
+        sv[i] = si;
+        p[i] = pi;
+        x[i] += alpha * pi;
+        const double ri = r[i] - alpha * si;
+        const double ui = u[i] - alpha * qi;
+        const double wi = w[i] - alpha * zi;
+        r[i] = ri;
+        u[i] = ui;
+        w[i] = wi;
+        m[i] = JAC ? dinv[i] * wi : wi;
+        acc[0] += ri * ui;
+        acc[1] += ri * ri;
+        acc[2] += wi * ui;
+    }
+    block_sums<3>(acc, pp_out, (int)gridDim.x);
+}
+
+// The scalar stage of the last pipelined update of a solve call (its partials
+// are otherwise consumed by the next launch's prologue): leaves the reporting
+// slots (iterations, residual, reason, alpha / beta / rho) consistent.
+__global__ __launch_bounds__(KB) void k_pipe_flush(const double *__restrict__ pp, int G, double *__restrict__ scal,
+                                                   int *__restrict__ ist, int par, double atol)
+{
+    if (ist[I_REASON] != 0) return;  // the last launch stopped: nothing pending
+    double t[3];
+    pipe_sums(pp, G, t);
+    if (threadIdx.x != 0) return;
+    const SrStep st = sr_step(t[0], sqrt(t[1]), t[2], scal[S_PRHO0 + par], scal[S_PALPHA0 + par], ist[I_PITS0 + par],
+                              scal[S_TOL], ist[I_FIXED], ist[I_MAXIT], atol);
+    scal[S_RR] = t[1];
+    ist[I_ITS] = st.its;
+    if (st.upd) {
+        scal[S_ALPHA] = st.alpha;
+        scal[S_BETA] = st.beta;
+        scal[S_RHO] = st.rho;
+    }
+    if (st.reason) ist[I_REASON] = st.reason;
 }
 
 // Dot + reduction + scalar update in one launch: each workgroup forms its
@@ -563,6 +684,7 @@ struct kle_ksp {
     std::string type = "cg", pc = "jacobi";
     double rtol = 1e-5, atol = 1e-50, dtol = 1e5;
     int maxit = 10000, restart = 30, fixed = 0, check_every = 8;
+    int pipe_par = 0;  // pipelined CG: parity of the next update launch (k_pipe_iter)
     kle_mat *A = nullptr;
     kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
     kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
@@ -935,9 +1057,23 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
         KLE_HIP(hipGetLastError());
         KLE_TRY(spmv(k->A, k->m, k->nv, nullptr));  // n = A m
     }
-    // the reduction may run beside the SpMV only where the SpMV's own halo uses
+    // the allreduce may run beside the SpMV only where the SpMV's own halo uses
     // the comm stream too (one RCCL stream: halo, then allreduce)
     const bool side = spmv_uses_comm_stream(k->A, k->m);
+    const int fuse = c->nranks == 1 && !c->comm;
+    // every rank launches the update with the same grid, so the [3][G]
+    // partials allreduce element-wise
+    int G = g;
+    if (c->nranks > 1) {
+        std::vector<int64_t> all;
+        KLE_TRY(allgather_i64(c, g, all));
+        for (int64_t v : all) G = std::max<int>(G, (int)v);
+    }
+    double *const pp[2] = {c->d_partials + 3 * (int64_t)PART_STRIDE, c->d_partials + 3 * (int64_t)PART_STRIDE +
+                                                                          PART_STRIDE / 2};
+    if (!cont) k->pipe_par = 0;
+    int par = k->pipe_par;
+    bool pending = false;  // a launch's partials await the next launch's prologue
     hipEvent_t ev_upd = nullptr, ev_red = nullptr;
     KLE_HIP(hipEventCreateWithFlags(&ev_upd, hipEventDisableTiming));
     KLE_HIP(hipEventCreateWithFlags(&ev_red, hipEventDisableTiming));
@@ -948,47 +1084,52 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
         rc = c->tic("cg_update", &ev);
         if (rc) break;
         if (jac)
-            hipLaunchKernelGGL(k_pipe_update<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
-                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, c->d_partials,
-                               c->d_scal, c->d_istate);
+            hipLaunchKernelGGL(k_pipe_iter<true>, dim3(G), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
+                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, pp[par],
+                               pp[par ^ 1], c->d_scal, c->d_istate, (int)pending, par, k->atol);
         else
-            hipLaunchKernelGGL(k_pipe_update<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
-                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, c->d_partials,
-                               c->d_scal, c->d_istate);
-        if (hipGetLastError() != hipSuccess) { rc = fail(KLE_ERR_DEVICE, "k_pipe_update launch failed"); break; }
+            hipLaunchKernelGGL(k_pipe_iter<false>, dim3(G), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
+                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, pp[par],
+                               pp[par ^ 1], c->d_scal, c->d_istate, (int)pending, par, k->atol);
+        if (hipGetLastError() != hipSuccess) { rc = fail(KLE_ERR_DEVICE, "k_pipe_iter launch failed"); break; }
         if ((rc = c->toc("cg_update", &ev))) break;
-        if (side && c->nranks > 1) {
+        par ^= 1;
+        pending = true;
+        if (fuse) {
+            // one rank: the next launch's prologue reduces these partials
+            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
+        } else if (side && c->nranks > 1) {
+            // the partials' allreduce on the comm stream behind the halo, beside the SpMV
             if (hipEventRecord(ev_upd, c->stream) != hipSuccess ||
                 hipStreamWaitEvent(c->comm_stream, ev_upd, 0) != hipSuccess) {
                 rc = fail(KLE_ERR_DEVICE, "event record/wait failed");
                 break;
             }
             if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
-            if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR, c->comm_stream))) break;
+            if ((rc = allreduce_sum(c, pp[par], 3 * G, c->comm_stream))) break;
             if (hipEventRecord(ev_red, c->comm_stream) != hipSuccess ||
                 hipStreamWaitEvent(c->stream, ev_red, 0) != hipSuccess) {
                 rc = fail(KLE_ERR_DEVICE, "event record/wait failed");
                 break;
             }
-        } else if (c->nranks > 1) {
-            // no overlap possible on this rank: same collective order as the
-            // overlapping ranks (halo, then allreduce), all on one stream
-            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
-            if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
         } else {
-            // one rank: the scalar stage first, the SpMV behind it.  Running the
-            // reduction on the comm stream beside the SpMV was measured slower at
-            // every size (1/8 slab 95.3 vs 88.9 us, 90.7 with the SpMV's LDS cap;
-            // full size 811 vs 811 us; profiles/r02/pipe_side_*.jsonl): its one
-            // workgroup waits for SpMV workgroups to drain.
-            if ((rc = reduce_stage(k, NParts{{g, g, g, 0}}, 3, ST_SR))) break;
+            // no overlap possible on this rank (or a one-rank RCCL
+            // communicator): same collective order as the overlapping ranks
+            // (halo, then allreduce), all on one stream
             if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
+            if ((rc = allreduce_sum(c, pp[par], 3 * G, c->stream))) break;
         }
         if (!k->fixed && ((it + 1) % k->check_every == 0)) {
             if ((rc = poll_state(k))) break;
             if (c->h_istate[I_REASON] != 0) break;
         }
     }
+    if (!rc && pending) {
+        hipLaunchKernelGGL(k_pipe_flush, dim3(1), dim3(KB), 0, c->stream, pp[par], G, c->d_scal, c->d_istate, par,
+                           k->atol);
+        if (hipGetLastError() != hipSuccess) rc = fail(KLE_ERR_DEVICE, "k_pipe_flush launch failed");
+    }
+    k->pipe_par = par;
     hipEventDestroy(ev_upd);
     hipEventDestroy(ev_red);
     if (rc) return rc;
