@@ -9,10 +9,11 @@
 //   * convergence is decided on the device: the scalar kernel sets a reason
 //     word and every later kernel of the solve turns into a no-op, so the
 //     host only polls every few iterations and the iteration count is exact;
-//   * the vector update and its dot partials are one kernel; the dot with the
-//     SpMV output, the fixed-order final sums and the scalar update are one
-//     more (k_dot_finish, last-arriving workgroup): three launches per
-//     single-reduction CG iteration;
+//   * single-reduction and pipelined CG: the vector update, its dot partials
+//     and -- in its prologue -- the previous iteration's fixed-order final
+//     sums and scalar stage are one kernel (k_sr_iter / k_pipe_iter); per
+//     iteration: update, SpMV, and for single-reduction CG a (w, u) partial
+//     launch; N ranks allreduce the partial arrays, not scalars;
 //   * deterministic reductions (per-workgroup partials, fixed-order final
 //     sum), RCCL allreduce of the 1-3 scalars across ranks.
 // PC lu (and KSP preonly) are a dense rocSOLVER factorization for the
@@ -151,35 +152,6 @@ __global__ __launch_bounds__(KB) void k_sr_start(int64_t n, const double *__rest
         u[i] = ui;
         p[i] = 0.0;
         sv[i] = 0.0;
-        acc[0] += ri * ui;
-        acc[1] += ri * ri;
-    }
-    block_sums<2>(acc, partials, PART_STRIDE);
-}
-
-// p = u + beta p ; s = w + beta s ; x += alpha p ; r -= alpha s ; u = M r
-// partials: [0] r.u, [1] r.r   (one pass over 7 inputs, 5 outputs)
-template <bool JAC>
-__global__ __launch_bounds__(KB) void k_sr_update(int64_t n, const double *__restrict__ dinv,
-                                                  const double *__restrict__ w, double *__restrict__ u,
-                                                  double *__restrict__ p, double *__restrict__ sv,
-                                                  double *__restrict__ x, double *__restrict__ r,
-                                                  double *__restrict__ partials, const double *__restrict__ scal,
-                                                  const int *__restrict__ ist)
-{
-    if (ist[I_REASON] != 0) return;
-    const double alpha = scal[S_ALPHA], beta = scal[S_BETA];
-    double acc[2] = {0.0, 0.0};
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double pi = u[i] + beta * p[i];
-        const double si = w[i] + beta * sv[i];
-        p[i] = pi;
-        sv[i] = si;
-        x[i] += alpha * pi;
-        const double ri = r[i] - alpha * si;
-        r[i] = ri;
-        const double ui = JAC ? dinv[i] * ri : ri;
-        u[i] = ui;
         acc[0] += ri * ui;
         acc[1] += ri * ri;
     }
@@ -353,18 +325,20 @@ __global__ void k_scalars(double *scal, int *ist, int stage, double rtol, double
     cg_scalars(stage, scal, ist, rtol, atol);
 }
 
-// Sums of the [3][G] per-workgroup partials of the previous pipelined update
-// in a fixed order (every caller gets bitwise the same three values).
-__device__ __forceinline__ void pipe_sums(const double *__restrict__ pp, int G, double (&t)[3])
+// Three sums of per-workgroup partials in a fixed order (every caller gets
+// bitwise the same values): t0 = sum a0[0..Ga), t1 = sum a1[0..Ga),
+// t2 = sum a2[0..G2).
+__device__ __forceinline__ void sums3(const double *__restrict__ a0, const double *__restrict__ a1, int Ga,
+                                      const double *__restrict__ a2, int G2, double (&t)[3])
 {
     __shared__ double red[3][KB / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double a[3] = {0.0, 0.0, 0.0};
-    for (int i = threadIdx.x; i < G; i += KB) {
-        a[0] += pp[i];
-        a[1] += pp[G + i];
-        a[2] += pp[2 * G + i];
+    for (int i = threadIdx.x; i < Ga; i += KB) {
+        a[0] += a0[i];
+        a[1] += a1[i];
     }
+    for (int i = threadIdx.x; i < G2; i += KB) a[2] += a2[i];
 #pragma unroll
     for (int q = 0; q < 3; ++q) a[q] = wsum2(a[q]);
     if (lane == 0)
@@ -378,6 +352,58 @@ __device__ __forceinline__ void pipe_sums(const double *__restrict__ pp, int G, 
         for (int i = 0; i < KB / 64; ++i) s += red[q][i];
         t[q] = s;
     }
+}
+
+// The prologue shared by the pipelined and the single-reduction CG update
+// kernels: with pro, the previous iteration's scalar stage from the sums t
+// (every workgroup runs the same sr_step; workgroup 0 writes the next
+// parity's stage inputs and the reporting slots); without, alpha / beta from
+// the scalar slots (workgroup 0 seeds the next parity's inputs from them).
+// Returns, in every thread, whether the stage ended the solve; alpha / beta
+// for the update.
+__device__ __forceinline__ bool stage_prologue(int pro, const double (&t)[3], double *__restrict__ scal,
+                                               int *__restrict__ ist, int par, double atol, double &alpha,
+                                               double &beta)
+{
+    __shared__ double ab[2];
+    __shared__ int stop;
+    const bool w0 = blockIdx.x == 0 && threadIdx.x == 0;
+    const int nxt = par ^ 1;
+    if (threadIdx.x == 0) {
+        if (pro) {
+            const SrStep st = sr_step(t[0], sqrt(t[1]), t[2], scal[S_PRHO0 + par], scal[S_PALPHA0 + par],
+                                      ist[I_PITS0 + par], scal[S_TOL], ist[I_FIXED], ist[I_MAXIT], atol);
+            ab[0] = st.alpha;
+            ab[1] = st.beta;
+            stop = st.reason != 0;
+            if (w0) {
+                scal[S_RR] = t[1];
+                ist[I_ITS] = st.its;
+                if (st.upd) {
+                    scal[S_ALPHA] = st.alpha;
+                    scal[S_BETA] = st.beta;
+                    scal[S_RHO] = st.rho;
+                }
+                scal[S_PRHO0 + nxt] = st.rho;
+                scal[S_PALPHA0 + nxt] = st.alpha;
+                ist[I_PITS0 + nxt] = st.its;
+                if (st.reason) ist[I_REASON] = st.reason;
+            }
+        } else {
+            ab[0] = scal[S_ALPHA];
+            ab[1] = scal[S_BETA];
+            stop = 0;
+            if (w0) {
+                scal[S_PRHO0 + nxt] = scal[S_RHO];
+                scal[S_PALPHA0 + nxt] = scal[S_ALPHA];
+                ist[I_PITS0 + nxt] = ist[I_ITS];
+            }
+        }
+    }
+    __syncthreads();
+    alpha = ab[0];
+    beta = ab[1];
+    return stop != 0;
 }
 
 // One pipelined CG iteration (PETSc KSPPIPECG; Ghysels & Vanroose 2014):
@@ -407,47 +433,11 @@ __global__ __launch_bounds__(KB) void k_pipe_iter(int64_t n, const double *__res
                                                   double atol)
 {
     if (ist[I_REASON] != 0) return;
-    __shared__ double ab[2];
-    __shared__ int stop;
-    const bool w0 = blockIdx.x == 0 && threadIdx.x == 0;
-    const int nxt = par ^ 1;
-    if (pro) {
-        double t[3];
-        pipe_sums(pp_in, (int)gridDim.x, t);
-        if (threadIdx.x == 0) {
-            const double rn = sqrt(t[1]);
-            const SrStep st = sr_step(t[0], rn, t[2], scal[S_PRHO0 + par], scal[S_PALPHA0 + par], ist[I_PITS0 + par],
-                                      scal[S_TOL], ist[I_FIXED], ist[I_MAXIT], atol);
-            ab[0] = st.alpha;
-            ab[1] = st.beta;
-            stop = st.reason != 0;
-            if (w0) {
-                scal[S_RR] = t[1];
-                ist[I_ITS] = st.its;
-                if (st.upd) {
-                    scal[S_ALPHA] = st.alpha;
-                    scal[S_BETA] = st.beta;
-                    scal[S_RHO] = st.rho;
-                }
-                scal[S_PRHO0 + nxt] = st.rho;
-                scal[S_PALPHA0 + nxt] = st.alpha;
-                ist[I_PITS0 + nxt] = st.its;
-                if (st.reason) ist[I_REASON] = st.reason;
-            }
-        }
-    } else if (threadIdx.x == 0) {
-        ab[0] = scal[S_ALPHA];
-        ab[1] = scal[S_BETA];
-        stop = 0;
-        if (w0) {
-            scal[S_PRHO0 + nxt] = scal[S_RHO];
-            scal[S_PALPHA0 + nxt] = scal[S_ALPHA];
-            ist[I_PITS0 + nxt] = ist[I_ITS];
-        }
-    }
-    __syncthreads();
-    if (stop) return;
-    const double alpha = ab[0], beta = ab[1];
+    const int G = (int)gridDim.x;
+    double t[3] = {0.0, 0.0, 0.0};
+    if (pro) sums3(pp_in, pp_in + G, G, pp_in + 2 * G, G, t);
+    double alpha, beta;
+    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta)) return;
     double acc[3] = {0.0, 0.0, 0.0};
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double zi = nv[i] + beta * z[i];
@@ -473,15 +463,18 @@ __global__ __launch_bounds__(KB) void k_pipe_iter(int64_t n, const double *__res
     block_sums<3>(acc, pp_out, (int)gridDim.x);
 }
 
-// The scalar stage of the last pipelined update of a solve call (its partials
-// are otherwise consumed by the next launch's prologue): leaves the reporting
-// slots (iterations, residual, reason, alpha / beta / rho) consistent.
-__global__ __launch_bounds__(KB) void k_pipe_flush(const double *__restrict__ pp, int G, double *__restrict__ scal,
-                                                   int *__restrict__ ist, int par, double atol)
+// The scalar stage of the last update of a solve call whose partials would
+// otherwise wait for the next launch's prologue (pipelined / single-reduction
+// CG): leaves the reporting slots (iterations, residual, reason, alpha / beta
+// / rho) consistent.
+__global__ __launch_bounds__(KB) void k_cg_flush(const double *__restrict__ a0, const double *__restrict__ a1,
+                                                 int Ga, const double *__restrict__ a2, int G2,
+                                                 double *__restrict__ scal, int *__restrict__ ist, int par,
+                                                 double atol)
 {
     if (ist[I_REASON] != 0) return;  // the last launch stopped: nothing pending
     double t[3];
-    pipe_sums(pp, G, t);
+    sums3(a0, a1, Ga, a2, G2, t);
     if (threadIdx.x != 0) return;
     const SrStep st = sr_step(t[0], sqrt(t[1]), t[2], scal[S_PRHO0 + par], scal[S_PALPHA0 + par], ist[I_PITS0 + par],
                               scal[S_TOL], ist[I_FIXED], ist[I_MAXIT], atol);
@@ -493,6 +486,62 @@ __global__ __launch_bounds__(KB) void k_pipe_flush(const double *__restrict__ pp
         scal[S_RHO] = st.rho;
     }
     if (st.reason) ist[I_REASON] = st.reason;
+}
+
+// Single-reduction CG iteration with the previous stage in its prologue (one
+// rank): sums (r,u), (r,r) of the previous update [2][G] and (w,u) of the
+// dot launch [Gd], then  p = u + b p ; s = w + b s ; x += a p ; r -= a s ;
+// u = M r  with the new (r,u), (r,r) partials to pu_out [2][G].
+template <bool JAC>
+__global__ __launch_bounds__(KB) void k_sr_iter(int64_t n, const double *__restrict__ dinv,
+                                                const double *__restrict__ w, double *__restrict__ u,
+                                                double *__restrict__ p, double *__restrict__ sv,
+                                                double *__restrict__ x, double *__restrict__ r,
+                                                const double *__restrict__ pu_in, const double *__restrict__ pd,
+                                                int Gd, double *__restrict__ pu_out, double *__restrict__ scal,
+                                                int *__restrict__ ist, int pro, int par, double atol)
+{
+    if (ist[I_REASON] != 0) return;
+    const int G = (int)gridDim.x;
+    double t[3] = {0.0, 0.0, 0.0};
+    if (pro) sums3(pu_in, pu_in + G, G, pd, Gd, t);
+    double alpha, beta;
+    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta)) return;
+    double acc[2] = {0.0, 0.0};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double pi = u[i] + beta * p[i];
+        const double si = w[i] + beta * sv[i];
+        p[i] = pi;
+        sv[i] = si;
+        x[i] += alpha * pi;
+        const double ri = r[i] - alpha * si;
+        r[i] = ri;
+        const double ui = JAC ? dinv[i] * ri : ri;
+        u[i] = ui;
+        acc[0] += ri * ui;
+        acc[1] += ri * ri;
+    }
+    block_sums<2>(acc, pu_out, G);
+}
+
+// (w, u) per workgroup after the SpMV (no last-arriver: the next update's
+// prologue sums the partials); FIN_UNR independent load pairs per thread.
+__global__ __launch_bounds__(KB) void k_dot_part(int64_t n, const double *__restrict__ vx,
+                                                 const double *__restrict__ vy, double *__restrict__ pd,
+                                                 const int *__restrict__ ist)
+{
+    if (ist[I_REASON] != 0) return;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * KB;
+    for (int64_t i0 = blockIdx.x * (int64_t)KB + threadIdx.x; i0 < n; i0 += stride * 4) {
+        double v[4];
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) v[uu] = i0 + uu * stride < n ? vx[i0 + uu * stride] * vy[i0 + uu * stride] : 0.0;
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) acc += v[uu];
+    }
+    double a[1] = {acc};
+    block_sums<1>(a, pd, 0);
 }
 
 // Dot + reduction + scalar update in one launch: each workgroup forms its
@@ -707,7 +756,7 @@ struct kle_ksp {
     // (b, x) pair it was captured with
     hipGraphExec_t graph = nullptr;
     const double *graph_b = nullptr, *graph_x = nullptr;
-    int graph_jac = -1, graph_len = 0;
+    int graph_jac = -1, graph_len = 0, graph_par = -1;
     bool graph_off = false;  // capture failed once: stream-launched from then on
 };
 
@@ -953,35 +1002,83 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     }
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    // one iteration: fused update, SpMV w = A u (+ (w, u) partials), reduction
+    // pro_mode (default): the scalar stage runs in the next update's prologue
+    // (k_sr_iter) and the (w, u) dot is a plain partial launch -- no
+    // last-arriver ticket, no scalar kernel (as the pipelined CG, §3).  Per
+    // parity one buffer [2][G] update partials | [Gd] dot partials; on N ranks
+    // (or a one-rank RCCL communicator) it is allreduced as one array after
+    // the dot (G, Gd equal on every rank), then the next prologue reads it.  A
+    // flush closes the call.  Against update + SpMV + k_dot_finish (last-
+    // arriver sum + stage): config 2 782.3 vs 782.3 us per iteration, 1/8
+    // slab 85.65 vs 88.29 (profiles/r02/sr_prologue_*.jsonl).
+    const bool pro_mode = true;
+    const bool fuse = c->nranks == 1 && !c->comm;
+    int Gu = g, Gd = grid_for(n, KB * 4, 1024);
+    if (pro_mode && c->nranks > 1) {
+        std::vector<int64_t> all;
+        KLE_TRY(allgather_i64(c, ((int64_t)Gu << 20) | Gd, all));
+        for (int64_t v : all) {
+            Gu = std::max<int>(Gu, (int)(v >> 20));
+            Gd = std::max<int>(Gd, (int)(v & ((1 << 20) - 1)));
+        }
+    }
+    double *const pu[2] = {c->d_partials + 3 * (int64_t)PART_STRIDE,
+                           c->d_partials + 3 * (int64_t)PART_STRIDE + PART_STRIDE / 2};
+    if (!cont) k->pipe_par = 0;
+    int par = k->pipe_par;
+    bool pending = false;  // an update's partials await the next launch's prologue
     auto iteration = [&]() -> int {
         KLE_TRY(c->tic("cg_update", &ev));
-        if (jac)
-            hipLaunchKernelGGL(k_sr_update<true>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d, k->p->d,
-                               k->s->d, x->d, k->r->d, c->d_partials, c->d_scal, c->d_istate);
-        else
-            hipLaunchKernelGGL(k_sr_update<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d, k->p->d,
-                               k->s->d, x->d, k->r->d, c->d_partials, c->d_scal, c->d_istate);
-        KLE_HIP(hipGetLastError());
-        KLE_TRY(c->toc("cg_update", &ev));
-        KLE_TRY(spmv_finish(k, k->u, k->w, 2, g, ST_SR, c->d_istate));
+        {
+            if (jac)
+                hipLaunchKernelGGL(k_sr_iter<true>, dim3(Gu), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d,
+                                   k->p->d, k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1],
+                                   c->d_scal, c->d_istate, (int)pending, par, k->atol);
+            else
+                hipLaunchKernelGGL(k_sr_iter<false>, dim3(Gu), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d,
+                                   k->p->d, k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1],
+                                   c->d_scal, c->d_istate, (int)pending, par, k->atol);
+            KLE_HIP(hipGetLastError());
+            KLE_TRY(c->toc("cg_update", &ev));
+            par ^= 1;
+            pending = true;
+            KLE_TRY(spmv(k->A, k->u, k->w, c->d_istate));
+            KLE_TRY(c->tic("reduce", &ev));
+            hipLaunchKernelGGL(k_dot_part, dim3(Gd), dim3(KB), 0, c->stream, n, k->u->d, k->w->d, pu[par] + 2 * Gu,
+                               c->d_istate);
+            KLE_HIP(hipGetLastError());
+            KLE_TRY(c->toc("reduce", &ev));
+            if (!fuse) KLE_TRY(allreduce_sum(c, pu[par], 2 * Gu + Gd));
+            return 0;
+        }
         return 0;
     };
     // hipGraph replay (KLE_GRAPH=1; one rank, no per-launch timing): every
     // kernel of the loop reads its scalars from device memory and turns into a
     // no-op once the reason word is set, so a block of check_every iterations
-    // is a fixed launch sequence; capture it once per (b, x), replay it per
-    // block.  Off by default: the loop is not launch-bound on MI355X
+    // is a fixed launch sequence; capture it once per (b, x, starting parity),
+    // replay it per block (pro_mode: the block starts after one stream
+    // iteration, with a pending stage; an even block length returns to the
+    // same parity).  Off by default: the loop is not launch-bound on MI355X
     // (tools/graph_ab.py: equal time at 1M and 8M DoF, +0.7 % on a 142k-DoF part)
     const char *ge = getenv("KLE_GRAPH");
-    const bool want_graph = c->nranks == 1 && !c->profiling && !k->graph_off && ge && atoi(ge) != 0;
-    if (want_graph && !(k->graph && k->graph_b == b->d && k->graph_x == x->d && k->graph_jac == (int)jac &&
-                        k->graph_len == k->check_every)) {
+    const bool want_graph = fuse && !c->profiling && !k->graph_off && ge && atoi(ge) != 0 &&
+                            (!pro_mode || k->check_every % 2 == 0);
+    int it = 0;
+    if (want_graph && pro_mode && limit > 0) {
+        KLE_TRY(iteration());
+        ++it;
+    }
+    if (want_graph && it < limit &&
+        !(k->graph && k->graph_b == b->d && k->graph_x == x->d && k->graph_jac == (int)jac &&
+          k->graph_len == k->check_every && k->graph_par == (pro_mode ? par : -1))) {
         drop_graph(k);
         hipGraph_t gr = nullptr;
+        const int par0 = par;
         int rc = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess ? 0 : 1;
         for (int j = 0; j < k->check_every && !rc; ++j) rc = iteration();
         const bool ended = hipStreamEndCapture(c->stream, &gr) == hipSuccess;
+        par = par0;  // capture launched nothing
         hipGraphExec_t ex = nullptr;
         if (!rc && ended && gr && hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0) == hipSuccess) {
             k->graph = ex;
@@ -989,34 +1086,41 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             k->graph_x = x->d;
             k->graph_jac = (int)jac;
             k->graph_len = k->check_every;
+            k->graph_par = pro_mode ? par0 : -1;
         } else {
             k->graph_off = true;  // e.g. a matrix whose SpMV path cannot be captured
             (void)hipGetLastError();
         }
         if (gr) (void)hipGraphDestroy(gr);
     }
+    bool stopped = false;
     if (want_graph && k->graph) {
         // fixed iterations never stop on the device: whole graph blocks, then
         // the remainder stream-launched
-        int it = 0;
         for (; it < limit && (!k->fixed || it + k->graph_len <= limit); it += k->graph_len) {
             KLE_HIP(hipGraphLaunch(k->graph, c->stream));
             if (!k->fixed) {
                 KLE_TRY(poll_state(k));
-                if (c->h_istate[I_REASON] != 0) break;
-            }
-        }
-        if (k->fixed)
-            for (; it < limit; ++it) KLE_TRY(iteration());
-    } else {
-        for (int it = 0; it < limit; ++it) {
-            KLE_TRY(iteration());
-            if (!k->fixed && ((it + 1) % k->check_every == 0)) {
-                KLE_TRY(poll_state(k));
-                if (c->h_istate[I_REASON] != 0) break;
+                if (c->h_istate[I_REASON] != 0) {
+                    stopped = true;
+                    break;
+                }
             }
         }
     }
+    for (; it < limit && !stopped; ++it) {
+        KLE_TRY(iteration());
+        if (!k->fixed && ((it + 1) % k->check_every == 0)) {
+            KLE_TRY(poll_state(k));
+            if (c->h_istate[I_REASON] != 0) break;
+        }
+    }
+    if (pro_mode && pending) {
+        hipLaunchKernelGGL(k_cg_flush, dim3(1), dim3(KB), 0, c->stream, pu[par], pu[par] + Gu, Gu, pu[par] + 2 * Gu,
+                           Gd, c->d_scal, c->d_istate, par, k->atol);
+        KLE_HIP(hipGetLastError());
+    }
+    k->pipe_par = par;
     KLE_TRY(poll_state(k));
     k->its = c->h_istate[I_ITS];
     k->reason = c->h_istate[I_REASON];
@@ -1125,9 +1229,9 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
         }
     }
     if (!rc && pending) {
-        hipLaunchKernelGGL(k_pipe_flush, dim3(1), dim3(KB), 0, c->stream, pp[par], G, c->d_scal, c->d_istate, par,
-                           k->atol);
-        if (hipGetLastError() != hipSuccess) rc = fail(KLE_ERR_DEVICE, "k_pipe_flush launch failed");
+        hipLaunchKernelGGL(k_cg_flush, dim3(1), dim3(KB), 0, c->stream, pp[par], pp[par] + G, G, pp[par] + 2 * G, G,
+                           c->d_scal, c->d_istate, par, k->atol);
+        if (hipGetLastError() != hipSuccess) rc = fail(KLE_ERR_DEVICE, "k_cg_flush launch failed");
     }
     k->pipe_par = par;
     hipEventDestroy(ev_upd);
