@@ -7,8 +7,8 @@ BASELINE.json config 2 workload (3-D KLE Laplacian, structured hex mesh
   torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
 A "step" is one CG iteration on the assembled device matrix (single-
-reduction CG + Jacobi: fused vector update with its dot partials, SpMV with
-the row shares of (u, A u), dot finish + scalar update; pipelined CG on N>1);
+reduction CG + Jacobi: the fused vector update whose prologue applies the
+previous scalar stage, the SpMV, the (u, A u) partials; pipelined CG on N>1);
 the warm-up solve starts the recurrence and the K timed steps continue it
 (no restart inside the timed region), between barriers, max over ranks.  Assembly (device
 element kernels + gather) is untimed setup.  A full solve to rtol 1e-10 is
