@@ -406,6 +406,9 @@ __device__ __forceinline__ bool stage_prologue(int pro, const double (&t)[3], do
     return stop != 0;
 }
 
+constexpr int PRO_UPD_BLOCKS = 1024;  // update kernels whose partials a prologue re-sums
+constexpr int PRO_DOT_BLOCKS = 512;
+
 // One pipelined CG iteration (PETSc KSPPIPECG; Ghysels & Vanroose 2014):
 // with w = A u, u = M r kept by recurrence, one fused pass
 //   z = n + b z, q = m + b q, s = w + b s, p = u + b p,
@@ -1013,7 +1016,10 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     // slab 85.65 vs 88.29 (profiles/r02/sr_prologue_*.jsonl).
     const bool pro_mode = true;
     const bool fuse = c->nranks == 1 && !c->comm;
-    int Gu = g, Gd = grid_for(n, KB * 4, 1024);
+    // grids capped at 1024 update / 512 dot workgroups: every prologue reads
+    // all 2 Gu + Gd partials (config 2: 788.5 vs 792.4 us per iteration with
+    // 2048 / 1024; the 1/8 slab is below both caps; profiles/r02/grids_*.jsonl)
+    int Gu = grid_for(n, KB, PRO_UPD_BLOCKS), Gd = grid_for(n, KB * 4, PRO_DOT_BLOCKS);
     if (pro_mode && c->nranks > 1) {
         std::vector<int64_t> all;
         KLE_TRY(allgather_i64(c, ((int64_t)Gu << 20) | Gd, all));
@@ -1166,11 +1172,11 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     const bool side = spmv_uses_comm_stream(k->A, k->m);
     const int fuse = c->nranks == 1 && !c->comm;
     // every rank launches the update with the same grid, so the [3][G]
-    // partials allreduce element-wise
-    int G = g;
+    // partials allreduce element-wise; capped like the single-reduction update
+    int G = grid_for(n, KB, PRO_UPD_BLOCKS);
     if (c->nranks > 1) {
         std::vector<int64_t> all;
-        KLE_TRY(allgather_i64(c, g, all));
+        KLE_TRY(allgather_i64(c, G, all));
         for (int64_t v : all) G = std::max<int>(G, (int)v);
     }
     double *const pp[2] = {c->d_partials + 3 * (int64_t)PART_STRIDE, c->d_partials + 3 * (int64_t)PART_STRIDE +
