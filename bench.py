@@ -318,6 +318,12 @@ def main():
         tot_bytes, tot_nnz = float(sb[0]), int(sb[1])
     else:
         spmv_avg_max = spmv_avg_ms
+    # which device each rank ran on: one distinct GPU per rank under RCCL
+    dev = ctx.device_info()
+    devices = [dev]
+    if dist is not None:
+        devices = [None] * nranks
+        dist.all_gather_object(devices, dev)
     if "torch" in sys.modules:  # torch is only the launcher's plumbing here
         import torch
         if torch.cuda.is_initialized():  # never create a torch context just to sync it
@@ -418,8 +424,12 @@ def main():
                        ("cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)"),
                        "pc": "jacobi", "matrix_format": info["format"], "value_layout": "chunk16+tail" if args.layout == 1 else f"row streams padded to {args.pad}",
                        "structured_columns": K.isStructured(),
-                       "parallelism": (f"z-slab x{nranks} (RCCL halo + allreduce)" if mesh_kind == "box" else
-                                       f"cell slabs along the most-layered axis x{nranks} (RCCL halo + allreduce)")},
+                       "parallelism": ((f"z-slab x{nranks}" if mesh_kind == "box" else
+                                        f"cell slabs along the most-layered axis x{nranks}") +
+                                       ("" if nranks == 1 else
+                                        " (RCCL halo + allreduce)" if dev["transport"] == "rccl" else
+                                        " (host-staged halo + allreduce over gloo, ranks sharing a GPU: test only)")),
+                       "devices": [f"{d['device']}@{d['pci_bus_id']}" for d in devices]},
             # N > 1: bytes of all ranks over the slowest rank's SpMV time,
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",

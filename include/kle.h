@@ -104,6 +104,9 @@ int kle_ctx_create_host_comm(int device, int rank, int nranks, const kle_host_co
 int kle_ctx_destroy(kle_ctx *ctx);
 int kle_ctx_synchronize(kle_ctx *ctx);
 int kle_ctx_barrier(kle_ctx *ctx); /* device-side RCCL barrier + stream sync */
+/* Diagnostics (no reference counterpart): the HIP ordinal, its PCI bus id
+ * (may be NULL) and the transport: 0 single rank, 1 RCCL, 2 host-staged. */
+int kle_ctx_get_device(kle_ctx *ctx, int *device, char *pci_bus_id, int len, int *transport);
 /* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */
 int kle_ctx_set_profiling(kle_ctx *ctx, int on);
 /* Time only the launches tagged `name` ("spmv", "dot", "cg_update", "reduce",

@@ -697,6 +697,15 @@ int kle_ctx_barrier(kle_ctx *c)
     return 0;
 }
 
+int kle_ctx_get_device(kle_ctx *c, int *device, char *pci_bus_id, int len, int *transport)
+{
+    KLE_ARG(c && device && transport && (pci_bus_id == nullptr || len > 0), "bad arg");
+    *device = c->device;
+    *transport = c->comm ? 1 : (c->nranks > 1 ? 2 : 0);
+    if (pci_bus_id) KLE_HIP(hipDeviceGetPCIBusId(pci_bus_id, len, c->device));
+    return 0;
+}
+
 int kle_ctx_set_profiling(kle_ctx *c, int on)
 {
     KLE_ARG(c, "null ctx");

@@ -181,6 +181,15 @@ class Context:
     def barrier(self):
         call("kle_ctx_barrier", self.h)
 
+    def device_info(self):
+        """{"device": HIP ordinal, "pci_bus_id": "0000:..", "transport":
+        "single" | "rccl" | "host"} of this rank."""
+        dev, tr = C.c_int(), C.c_int()
+        pci = C.create_string_buffer(32)
+        call("kle_ctx_get_device", self.h, C.byref(dev), pci, 32, C.byref(tr))
+        return {"device": dev.value, "pci_bus_id": pci.value.decode(),
+                "transport": ("single", "rccl", "host")[tr.value]}
+
     def set_profiling(self, on=True, only=None, every=1):
         """Event-time device launches; `only` restricts it to one kernel tag,
         `every` > 1 times one launch in `every` (sampled)."""

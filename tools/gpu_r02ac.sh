@@ -11,5 +11,5 @@ step bench_default 600 python bench.py || exit 1
 grep '^{' gpurun_out/bench_default.log > gpurun_out/r02ac/bench_default.json
 step prof_bench 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r02ac/prof_bench -o bench --output-format csv -- python3 bench.py --steps 200 --no-cpu-baseline || exit 1
 grep '^{' gpurun_out/prof_bench.log > gpurun_out/r02ac/bench_under_rocprof.json
-step bench_gpus2 300 python bench.py --gpus 2 --steps 50 --warmup 5 --nelem 20,16,4 || exit 1
+KLE_TRANSPORT=host KLE_DEVICE=0 step bench_gpus2 300 python bench.py --gpus 2 --steps 50 --warmup 5 --nelem 20,16,4 || exit 1
 echo done
