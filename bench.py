@@ -381,7 +381,8 @@ def main():
             tr = json.load(open(args.traffic))
             key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
                    ("chunk" if args.layout == 1 else f"pad{args.pad}") +
-                   "-nt-u1" + ("-struct" if K.isStructured() else ""))
+                   "-nt-u1" + ("-struct" if K.isStructured() else "") +
+                   ("-xl" if spmv_kernel(K, args.layout).startswith("k_nb_spmv_xl") else ""))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -434,8 +435,7 @@ def main():
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
                          "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
-                         "kernel": "k_nb_spmv<3,3,%d,%s,%d>" % (args.layout, "true" if K.isStructured() else "false",
-                                                                 spmv_waves(K, args.layout)),
+                         "kernel": spmv_kernel(K, args.layout),
                          "bytes_per_launch": tot_bytes,
                          "csr_bytes_per_launch": csr_bytes, "csr_equiv_gbps": csr_equiv,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
@@ -464,16 +464,22 @@ def main():
         dist.destroy_process_group()
 
 
-def spmv_waves(K, layout):
-    """Waves per workgroup the default SpMV kernel uses for this rank's K
-    (kle_mat.hip: 8 from 64k node rows up, else 4; KLE_SPMV_WAVES=4|8 overrides)."""
-    env = int(os.environ.get("KLE_SPMV_WAVES", "0") or 0)
-    if layout != 1:
-        return 4
-    if env in (4, 8):
-        return env
+def spmv_kernel(K, layout):
+    """Name of the SpMV kernel libkle launches for this rank's K (kle_mat.hip
+    launch_nb_lay / spmv_waves): structured 3x3 chunked rows with x staged in
+    LDS run k_nb_spmv_xl<8> when 8 waves per workgroup apply (from 64k node
+    rows up); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
+    "spmv_waves" / "spmv_x_lds" override)."""
+    from pynama_amd.runtime import get_tuning
+    wv = get_tuning("spmv_waves")
     lo, hi = K.getOwnershipRange()
-    return 8 if (hi - lo) // 3 >= 64000 else 4
+    if layout != 1:
+        wv = 4
+    elif wv not in (4, 8):
+        wv = 8 if (hi - lo) // 3 >= 64000 else 4
+    if layout == 1 and wv == 8 and K.isStructured() and get_tuning("spmv_x_lds"):
+        return "k_nb_spmv_xl<8>"
+    return "k_nb_spmv<3,3,%d,%s,%d>" % (layout, "true" if K.isStructured() else "false", wv)
 
 
 def splitmix_uniform(seed, lo, hi):

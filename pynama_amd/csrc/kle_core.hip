@@ -510,6 +510,9 @@ int kle_set_tuning(const char *key, int value)
     if (k == "spmv_waves") {
         KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
         g_tune.spmv_waves = value;
+    } else if (k == "spmv_x_lds") {
+        KLE_ARG(value == 0 || value == 1, "spmv_x_lds: 0 or 1");
+        g_tune.spmv_x_lds = value;
     } else if (k == "spmv_xcd_chunk") {
         KLE_ARG(value >= 0 && value <= 4096, "spmv_xcd_chunk: 0 (round-robin) or row blocks per XCD run");
         g_tune.spmv_xcd_chunk = value;
@@ -529,6 +532,7 @@ int kle_get_tuning(const char *key, int *value)
     if (k == "spmv_waves") *value = g_tune.spmv_waves;
     else if (k == "spmv_dyn_lds") *value = g_tune.spmv_dyn_lds;
     else if (k == "spmv_xcd_chunk") *value = g_tune.spmv_xcd_chunk;
+    else if (k == "spmv_x_lds") *value = g_tune.spmv_x_lds;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;
 }

@@ -18,6 +18,7 @@
 // the ghosted x vector from L2, shuffle reductions, optional fused dot(y, p)
 // partials for the Krylov loop.
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     constexpr int RC = R * C;
     const int lane = threadIdx.x & 63;
     const int64_t blk = xcd_block(xcd_chunk);
-    const int64_t r = blk * WV + (threadIdx.x >> 6);
+    const int64_t r = blk * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (r >= rm.na + rm.nb) return;
     const int64_t i = r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
     const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
@@ -114,14 +115,11 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
         bnxy = bnx * ((d >> 8) & 255);
     }
     const int q16 = LAY == 1 ? (m & ~15) : 0;
-    double acc[R];
-#pragma unroll
-    for (int a = 0; a < R; ++a) acc[a] = 0.0;
-    for (int kb = 0; kb < m; kb += 64) {
+    // one pass: the values of block kb + lane and the x entries they multiply
+    auto load = [&](int kb, double *vv, double *xv) {
         const int k = kb + lane;
         const bool on = k < m;
         int j = 0;
-        double vv[RC];
         if (on) {
             if constexpr (STRUCT) {
                 const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
@@ -144,13 +142,160 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
 #pragma unroll
             for (int t = 0; t < RC; ++t) vv[t] = 0.0;
         }
-        double xv[C];
 #pragma unroll
         for (int b = 0; b < C; ++b) xv[b] = on ? x[(int64_t)j * C + b] : 0.0;
+    };
+    double acc[R];
 #pragma unroll
-        for (int a = 0; a < R; ++a)
+    for (int a = 0; a < R; ++a) acc[a] = 0.0;
+    {
+        for (int kb = 0; kb < m; kb += 64) {
+            double vv[RC], xv[C];
+            load(kb, vv, xv);
 #pragma unroll
-            for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xv[b];
+            for (int a = 0; a < R; ++a)
+#pragma unroll
+                for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xv[b];
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+    if (lane < R) {
+        double mine = acc[0];
+#pragma unroll
+        for (int a = 1; a < R; ++a)
+            if (lane == a) mine = acc[a];
+        y[i * R + lane] = mine;
+    }
+}
+
+
+// Node-block SpMV with x staged in LDS (3x3 chunked structured rows, the
+// box-mesh K): the WV consecutive rows of a workgroup read nearly the same x
+// columns (their lattice boxes are shifted copies), so the workgroup loads
+// the union of its rows' boxes once -- coalesced x-line segments -- and every
+// wave reads its x entries from LDS instead of gathering them through the
+// L1/L2 (3 gathers per block).  A workgroup whose union exceeds XL_CAP nodes
+// or 21 nodes along x (its rows wrap into the next lattice line, or straddle
+// the two RowMap ranges) gathers from global memory as before.  Row indices
+// are read-first-lane scalars, so the row set-up runs on the scalar unit.
+// Same products in the same order as k_nb_spmv: bitwise identical.
+// Config 2: 0.730 -> 0.708 ms per SpMV, 736.5 -> 716.5 us per CG iteration;
+// a variant with two union boxes for wrapping workgroups and one that loads
+// the first value pass before the fill were slower (profiles/r02/xl_*.jsonl,
+// cg_xl_*.jsonl).
+constexpr int XL_CAP = 16 * 9 * 9;
+template <int WV>
+__global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int *__restrict__ rowptr,
+                                                          const int *__restrict__ rowcnt,
+                                                          const int *__restrict__ rowbox, int lx, int lxy,
+                                                          const int64_t *__restrict__ vptr,
+                                                          const double *__restrict__ val,
+                                                          const double *__restrict__ x, double *__restrict__ y,
+                                                          const int *__restrict__ istate, int xcd_chunk)
+{
+    constexpr int R = 3, C = 3, RC = 9;
+    extern __shared__ double xs[];
+    __shared__ int ub[WV][6];
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t blk = xcd_block(xcd_chunk);
+    const int64_t nr = rm.na + rm.nb;
+    const int64_t r = blk * WV + w;
+    const bool live = r < nr;
+    const int64_t i = !live ? 0 : (r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na));
+    int m = 0, mp = 0, bbase = 0, bnx = 1, bny = 1, bnz = 1;
+    const double *v = val;
+    if (live) {
+        const int b0 = rowptr[i];
+        mp = rowptr[i + 1] - b0;
+        m = rowcnt ? rowcnt[i] : mp;
+        v = val + vptr[i];
+        bbase = rowbox[2 * i];
+        const int d = rowbox[2 * i + 1];
+        bnx = d & 255;
+        bny = (d >> 8) & 255;
+        bnz = (d >> 16) & 255;
+    }
+    const int cz = bbase / lxy, cy = (bbase - cz * lxy) / lx, cx = bbase - cz * lxy - cy * lx;
+    if (lane == 0) {
+        ub[w][0] = live ? cx : INT_MAX;
+        ub[w][1] = live ? cy : INT_MAX;
+        ub[w][2] = live ? cz : INT_MAX;
+        ub[w][3] = live ? cx + bnx : INT_MIN;
+        ub[w][4] = live ? cy + bny : INT_MIN;
+        ub[w][5] = live ? cz + bnz : INT_MIN;
+    }
+    const int bnxy = bnx * bny;
+    const int q16 = m & ~15;
+    auto loadv = [&](int kb, double *vv) {
+        const int k = kb + lane;
+        if (kb + 64 <= q16) {
+            const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
+#pragma unroll
+            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(p + t * 16);
+        } else if (k < m) {
+            const int64_t o0 = vofs(1, RC, 0, k, m, mp);
+            const int64_t st = k < q16 ? 16 : m - q16;
+#pragma unroll
+            for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
+        } else {
+#pragma unroll
+            for (int t = 0; t < RC; ++t) vv[t] = 0.0;
+        }
+    };
+    __syncthreads();
+    int ox = INT_MAX, oy = INT_MAX, oz = INT_MAX, ex = INT_MIN, ey = INT_MIN, ez = INT_MIN;
+#pragma unroll
+    for (int q = 0; q < WV; ++q) {
+        ox = min(ox, ub[q][0]);
+        oy = min(oy, ub[q][1]);
+        oz = min(oz, ub[q][2]);
+        ex = max(ex, ub[q][3]);
+        ey = max(ey, ub[q][4]);
+        ez = max(ez, ub[q][5]);
+    }
+    ox = __builtin_amdgcn_readfirstlane(ox);
+    oy = __builtin_amdgcn_readfirstlane(oy);
+    oz = __builtin_amdgcn_readfirstlane(oz);
+    ex = __builtin_amdgcn_readfirstlane(ex);
+    ey = __builtin_amdgcn_readfirstlane(ey);
+    ez = __builtin_amdgcn_readfirstlane(ez);
+    const int UX = ex - ox, UY = ey - oy, UZ = ez - oz;
+    const bool lds_x = (int64_t)UX * UY * UZ <= XL_CAP && UX * 3 <= 64;
+    if (lds_x) {
+        for (int seg = w; seg < UY * UZ; seg += WV) {
+            const int uz = seg / UY, uy = seg - uz * UY;
+            if (lane < UX * 3)
+                xs[seg * UX * 3 + lane] = x[(int64_t)(ox + lx * (oy + uy) + lxy * (oz + uz)) * 3 + lane];
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    double acc[R] = {0.0, 0.0, 0.0};
+    auto rowloop = [&](auto xat) {
+        for (int kb = 0; kb < m; kb += 64) {
+            double vv[RC];
+            loadv(kb, vv);
+            const int k = kb + lane;
+            if (k < m) {
+                const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
+#pragma unroll
+                for (int a = 0; a < R; ++a)
+#pragma unroll
+                    for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xat(kx, ky, kz, b);
+            }
+        }
+    };
+    if (lds_x) {
+        const int sy = UX * 3, sz = UX * UY * 3;
+        const double *xl = xs + (cx - ox) * 3 + sy * (cy - oy) + sz * (cz - oz);
+        rowloop([&](int kx, int ky, int kz, int b) { return xl[kx * 3 + sy * ky + sz * kz + b]; });
+    } else {
+        const double *xg = x + (int64_t)bbase * 3;
+        rowloop([&](int kx, int ky, int kz, int b) { return xg[(int64_t)(kx + lx * ky + lxy * kz) * 3 + b]; });
     }
 #pragma unroll
     for (int a = 0; a < R; ++a)
@@ -297,7 +442,11 @@ bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 // Waves (rows) per workgroup: 8 for 3x3 chunked matrices of >= 64k node rows
 // -- consecutive rows of one workgroup share most x columns in the CU's L1:
 // config 2 +2.5 %, unstructured 1M mesh +2 %; 4 elsewhere (0.5 % ahead on the
-// 1/8 slab); profiles/r01/spmv_waves_ab.jsonl.  kle_set_tuning("spmv_waves") overrides.
+// 1/8 slab); profiles/r01/spmv_waves_ab.jsonl.  With 8 waves, structured rows
+// run k_nb_spmv_xl (x in LDS).  Below 64k rows 4 plain waves stay: alone the
+// 8-wave LDS kernel is faster on the 1/8 slab (71.3 vs 73.4 us), inside the
+// pipelined CG loop 1 % slower (79.6 vs 78.7 us per iteration,
+// profiles/r02/cg_xl_eighth.jsonl).  kle_set_tuning("spmv_waves") overrides.
 static int spmv_waves(const kle_mat *A)
 {
     if (!(A->R == 3 && A->C == 3 && A->vlayout == 1)) return SPMV_WAVES;
@@ -318,7 +467,12 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
     // kle_set_tuning("spmv_dyn_lds") overrides.
     const size_t lds = g_tune.spmv_dyn_lds >= 0 ? (size_t)g_tune.spmv_dyn_lds
                                                  : (A->ctx->side_busy && wv != 8 ? 21504 : 0);
-    if (R == 3 && C == 3 && LAY == 1 && wv == 8)
+    if (R == 3 && C == 3 && LAY == 1 && STRUCT && wv == 8 && g_tune.spmv_x_lds) {
+        hipLaunchKernelGGL((k_nb_spmv_xl<8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512),
+                           lds + XL_CAP * 3 * sizeof(double), st, rm, A->d_rowptr, A->d_rowcnt, rbox,
+                           (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_val, x->base, y->d, istate,
+                           g_tune.spmv_xcd_chunk);
+    } else if (R == 3 && C == 3 && LAY == 1 && wv == 8)
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), lds, st, rm,
                            A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_bcol,
                            A->d_val, x->base, y->d, istate, g_tune.spmv_xcd_chunk);

@@ -546,6 +546,39 @@ def test_spmv_layouts_and_column_modes_agree(pa):
         set_value_layout(old)
 
 
+@pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([4, 3, 3], 7)])
+def test_spmv_x_in_lds_is_bitwise(pa, nelem, ngl):
+    """k_nb_spmv_xl (x staged in LDS per workgroup of 8 rows) ==
+    k_nb_spmv with global x gathers (spmv_x_lds 0, 4 and 8 waves), bitwise,
+    for the structured K and Rw: lattice lines of 11-49 nodes, so workgroups
+    both fit one union box and wrap into the next line (global fallback)."""
+    from pynama_amd.runtime import get_tuning, set_tuning
+    cfg = {"domain": {"ngl": ngl, "box-mesh": {"nelem": nelem, "lower": [0, 0, 0], "upper": [1, 1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    for A in (mat.K, mat.Rw):
+        assert A.isStructured()
+        x = A.createVecRight()
+        x.setArray(np.random.default_rng(3).uniform(-1, 1, x.getLocalSize()))
+        ys = []
+        try:
+            for xl, wv in ((1, 0), (0, 0), (0, 4), (0, 8)):
+                set_tuning("spmv_x_lds", xl)
+                set_tuning("spmv_waves", wv)
+                ys.append((A * x).getArray().copy())
+        finally:
+            set_tuning("spmv_x_lds", 1)
+            set_tuning("spmv_waves", 0)
+        assert get_tuning("spmv_x_lds") == 1
+        for yv in ys[1:]:
+            np.testing.assert_array_equal(ys[0], yv)
+
+
 @pytest.mark.parametrize("lay", [0, 1])
 def test_device_pattern_matches_host(pa, lay):
     """Box-mesh patterns built on the device (k_pat_count / k_pat_fill) ==

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--ngl", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--its", type=int, default=50)
+    ap.add_argument("--format", choices=["aij", "nb"], default="aij", help="nb: the node-block K itself")
     a = ap.parse_args()
     variants = json.loads(a.variants)
     import numpy as np
@@ -44,7 +45,7 @@ def main():
     mat = pa.MatFS()
     mat.setDomain(dom)
     mat.build(buildOperators=False)
-    A = mat.K.convert("aij")
+    A = mat.K.convert("aij") if a.format == "aij" else mat.K
     nbytes = A.spmvBytes()
     x, y = A.createVecRight(), A.createVecLeft()
     x.setArray(np.random.default_rng(0).uniform(-1, 1, x.getLocalSize()))
@@ -71,7 +72,7 @@ def main():
             print(json.dumps({"rep": rep, "variant": v, "avg_ms": avg, "gbps": nbytes / (avg * 1e-3) / 1e9,
                               "bitwise_equal_first": bitwise}), flush=True)
             for k in v:
-                set_tuning(k, {"spmv_xcd_chunk": 16}.get(k, 0))
+                set_tuning(k, {"spmv_xcd_chunk": 16, "spmv_dyn_lds": -1}.get(k, 0))
     summ = [{"variant": v, "median_ms": statistics.median(res[i]), "min_ms": min(res[i]),
              "gbps_median": nbytes / (statistics.median(res[i]) * 1e-3) / 1e9} for i, v in enumerate(variants)]
     print(json.dumps({"summary": summ, "bytes_per_spmv": nbytes, "nnz": A.getInfo()["nz_used"],
