@@ -382,7 +382,7 @@ def main():
             key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
                    ("chunk" if args.layout == 1 else f"pad{args.pad}") +
                    "-nt-u1" + ("-struct" if K.isStructured() else "") +
-                   ("-xl" if spmv_kernel(K, args.layout).startswith("k_nb_spmv_xl") else ""))
+                   ("-xl" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_xl") else ""))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -435,7 +435,7 @@ def main():
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
                          "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
-                         "kernel": spmv_kernel(K, args.layout),
+                         "kernel": spmv_kernel(K, args.layout, args.ngl),
                          "bytes_per_launch": tot_bytes,
                          "csr_bytes_per_launch": csr_bytes, "csr_equiv_gbps": csr_equiv,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
@@ -464,11 +464,11 @@ def main():
         dist.destroy_process_group()
 
 
-def spmv_kernel(K, layout):
+def spmv_kernel(K, layout, ngl):
     """Name of the SpMV kernel libkle launches for this rank's K (kle_mat.hip
     launch_nb_lay / spmv_waves): structured 3x3 chunked rows with x staged in
     LDS run k_nb_spmv_xl<8> when 8 waves per workgroup apply (from 64k node
-    rows up); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
+    rows up) and 8 rows' union box fits its LDS tile (p <= 4); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
     "spmv_waves" / "spmv_x_lds" override)."""
     from pynama_amd.runtime import get_tuning
     wv = get_tuning("spmv_waves")
@@ -477,7 +477,7 @@ def spmv_kernel(K, layout):
         wv = 4
     elif wv not in (4, 8):
         wv = 8 if (hi - lo) // 3 >= 64000 else 4
-    if layout == 1 and wv == 8 and K.isStructured() and get_tuning("spmv_x_lds"):
+    if layout == 1 and wv == 8 and K.isStructured() and get_tuning("spmv_x_lds") and ngl <= 5:
         return "k_nb_spmv_xl<8>"
     return "k_nb_spmv<3,3,%d,%s,%d>" % (layout, "true" if K.isStructured() else "false", wv)
 

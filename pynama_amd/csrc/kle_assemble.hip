@@ -1012,10 +1012,13 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     const int64_t Lx = m->L[0], Lxy = m->L[0] * m->L[1];
     bool is_box = nrows > 0 && m->kind == 0;
     std::vector<int> box(2 * std::max<int64_t>(nrows, 1), 0);
+    int box_max = 0;
     for (int64_t i = 0; i < nrows && is_box; ++i) {
         if (info[i].box1 < 0) is_box = false;
         box[2 * i] = info[i].box0;
         box[2 * i + 1] = info[i].box1;
+        const int b1 = info[i].box1;
+        box_max = std::max({box_max, b1 & 255, (b1 >> 8) & 255, (b1 >> 16) & 255});
     }
     const int lay = g_nb_layout;
     // Layout 1 keeps the values' 128-B alignment by chunks (vptr); the column
@@ -1082,6 +1085,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     A->int_hi = first_hi;
     A->box_lx = Lx;
     A->box_lxy = Lxy;
+    A->box_max = is_box ? box_max : 0;
     if (const char *e = getenv("KLE_HALO_OVERLAP")) A->halo_overlap = atoi(e) != 0;
     A->node_begin = m->node_begin;
     A->ext_begin = m->ext_begin;

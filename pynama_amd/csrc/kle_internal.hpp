@@ -218,6 +218,7 @@ struct kle_mat {
     // instead of streaming bcol (d_rowbox[2*i] = base, [2*i+1] = nx | ny<<8 | nz<<16)
     int *d_rowbox = nullptr;
     int64_t box_lx = 0, box_lxy = 0;
+    int box_max = 0;  // largest row-box extent along any axis (structured columns)
     int spmv_struct = 1;  // use d_rowbox when present
     int64_t nblocks_real = 0;
     int pad = 1;

@@ -467,7 +467,10 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
     // kle_set_tuning("spmv_dyn_lds") overrides.
     const size_t lds = g_tune.spmv_dyn_lds >= 0 ? (size_t)g_tune.spmv_dyn_lds
                                                  : (A->ctx->side_busy && wv != 8 ? 21504 : 0);
-    if (R == 3 && C == 3 && LAY == 1 && STRUCT && wv == 8 && g_tune.spmv_x_lds) {
+    // x in LDS where 8 rows' union box fits XL_CAP (p <= 4: 16 x 9 x 9 nodes)
+    const bool xl = R == 3 && C == 3 && LAY == 1 && STRUCT && wv == 8 && g_tune.spmv_x_lds &&
+                    (7 + A->box_max) * A->box_max * A->box_max <= XL_CAP;
+    if (xl) {
         hipLaunchKernelGGL((k_nb_spmv_xl<8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512),
                            lds + XL_CAP * 3 * sizeof(double), st, rm, A->d_rowptr, A->d_rowcnt, rbox,
                            (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_val, x->base, y->d, istate,

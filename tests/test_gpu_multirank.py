@@ -21,11 +21,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=None, partitioner=None):
+def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="host",
                       RANK=str(rank), WORLD_SIZE=str(size))
+    if waves:
+        os.environ["KLE_SPMV_WAVES"] = str(waves)
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=size)
@@ -96,14 +98,25 @@ def test_eight_slab_solve_matches_serial(ksp_type):
     _check_box(8, [2, 2, 8], 4, True, ksp_type)
 
 
-def _check_box(size, nelem, ngl, overlap, ksp_type):
+@pytest.mark.parametrize("ksp_type", ["cg", "pipecg"])
+@pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 5), (3, [4, 3, 6], 4)])
+def test_partitioned_solve_x_in_lds(size, nelem, ngl, ksp_type):
+    """8 waves per SpMV workgroup forced at small size, so every rank runs the
+    x-in-LDS SpMV (k_nb_spmv_xl) on its split row ranges (interior rows, then
+    the ghost-dependent rows beside the halo): lattice lines of 13-17 nodes,
+    workgroups inside one line and wrapping ones; same checks as above."""
+    _check_box(size, nelem, ngl, True, ksp_type, waves=8)
+
+
+def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type)) for r in range(size)]
+    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, None, None, waves))
+             for r in range(size)]
     res = _collect(procs, q, size)
     for r in res:
         assert r["overlap_equal"], (r["rank"], r["ov_diff"])
