@@ -68,8 +68,11 @@ typedef struct kle_ksp kle_ksp;
 
 const char *kle_last_error(void);
 /* Performance knobs for in-process A/B measurements (tools/cg_ab.py); every
- * value gives correct results.  Keys: "spmv_waves" (0 auto, 4, 8: rows per
- * SpMV workgroup of 3x3 chunked matrices). */
+ * value gives bitwise the same results.  Keys: "spmv_waves" (0 auto, 4, 8:
+ * rows per SpMV workgroup of 3x3 chunked matrices), "spmv_x_lds" (1 default:
+ * structured 3x3 rows at 8 waves stage x in LDS; 0 off), "spmv_xcd_chunk"
+ * (row blocks per XCD run, 0 round-robin; default 16), "spmv_dyn_lds" (unused
+ * LDS bytes per SpMV workgroup while side-stream work runs, -1 auto). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
