@@ -382,7 +382,7 @@ def main():
             key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
                    ("chunk" if args.layout == 1 else f"pad{args.pad}") +
                    "-nt-u1" + ("-struct" if K.isStructured() else "") +
-                   ("-xl" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_xl") else ""))
+                   {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(spmv_kernel(K, args.layout, args.ngl), ""))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -468,7 +468,9 @@ def spmv_kernel(K, layout, ngl):
     """Name of the SpMV kernel libkle launches for this rank's K (kle_mat.hip
     launch_nb_lay / spmv_waves): structured 3x3 chunked rows with x staged in
     LDS run k_nb_spmv_xl<8> when 8 waves per workgroup apply (from 64k node
-    rows up) and 8 rows' union box fits its LDS tile (p <= 4); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
+    rows up) and 8 rows' union box fits its LDS tile (p <= 4); unstructured
+    3x3 rows there run k_nb_spmv_dict (x through per-group column
+    dictionaries); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
     "spmv_waves" / "spmv_x_lds" override)."""
     from pynama_amd.runtime import get_tuning
     wv = get_tuning("spmv_waves")
@@ -479,6 +481,9 @@ def spmv_kernel(K, layout, ngl):
         wv = 8 if (hi - lo) // 3 >= 64000 else 4
     if layout == 1 and wv == 8 and K.isStructured() and get_tuning("spmv_x_lds") and ngl <= 5:
         return "k_nb_spmv_xl<8>"
+    if (layout == 1 and wv == 8 and not K.isStructured() and get_tuning("spmv_dict")
+            and (hi - lo) // 3 >= get_tuning("spmv_dict_min_rows")):
+        return "k_nb_spmv_dict"
     return "k_nb_spmv<3,3,%d,%s,%d>" % (layout, "true" if K.isStructured() else "false", wv)
 
 

@@ -1150,6 +1150,14 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
     }
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     tm.lap("matrix alloc + uploads + column fill");
+    if (!is_box && R == 3 && C == 3 && lay == 1 && nrows >= g_tune.spmv_dict_min_rows) {
+        const int rc = nb_build_dict(A);
+        if (rc) {
+            kle_mat_destroy(A);
+            return rc;
+        }
+        tm.lap("column dictionaries");
+    }
     *out = A;
     return 0;
 }

@@ -510,6 +510,12 @@ int kle_set_tuning(const char *key, int value)
     if (k == "spmv_waves") {
         KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
         g_tune.spmv_waves = value;
+    } else if (k == "spmv_dict") {
+        KLE_ARG(value == 0 || value == 1, "spmv_dict: 0 or 1");
+        g_tune.spmv_dict = value;
+    } else if (k == "spmv_dict_min_rows") {
+        KLE_ARG(value >= 0, "spmv_dict_min_rows: >= 0");
+        g_tune.spmv_dict_min_rows = value;
     } else if (k == "spmv_x_lds") {
         KLE_ARG(value == 0 || value == 1, "spmv_x_lds: 0 or 1");
         g_tune.spmv_x_lds = value;
@@ -533,6 +539,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_dyn_lds") *value = g_tune.spmv_dyn_lds;
     else if (k == "spmv_xcd_chunk") *value = g_tune.spmv_xcd_chunk;
     else if (k == "spmv_x_lds") *value = g_tune.spmv_x_lds;
+    else if (k == "spmv_dict") *value = g_tune.spmv_dict;
+    else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;
 }

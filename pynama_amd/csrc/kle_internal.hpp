@@ -223,6 +223,14 @@ struct kle_mat {
     int64_t nblocks_real = 0;
     int pad = 1;
     int *d_bcol = nullptr;     // [nblocks] local ext node index
+    // column dictionaries (nb_build_dict; unstructured 3x3 chunked rows): per
+    // group of DICT_GROUP consecutive rows the sorted distinct columns
+    // d_dict[d_dptr[g] .. d_dptr[g+1]), and per block (bcol's indexing) its
+    // position in its group's dictionary
+    int *d_dptr = nullptr;
+    int *d_dict = nullptr;
+    uint16_t *d_lid = nullptr;
+    int64_t dict_len = 0;
     double *d_val = nullptr;   // [nblocks*R*C], per row SoA [a][b][k]
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
     // export: DoF-level entry rule inside the node blocks (no-slip matrices,
@@ -268,13 +276,16 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
+int nb_build_dict(kle_mat *A);  // kle_mat.hip
 // Performance knobs (kle_set_tuning): every setting gives correct results;
 // they exist for in-process A/B measurements (tools/cg_ab.py).
 struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
-    int spmv_x_lds = 1;  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
+    int spmv_x_lds = 1;
+    int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
+    int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
 };
 extern Tuning g_tune;
 // marks the SpMV launches inside its scope as running beside comm-stream work

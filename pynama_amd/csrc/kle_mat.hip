@@ -21,7 +21,9 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <map>
+#include <thread>
 
 #include "kle_internal.hpp"
 
@@ -310,6 +312,91 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
     }
 }
 
+
+// Node-block SpMV through per-group column dictionaries (unstructured 3x3
+// chunked rows, 8 waves): the DICT_GROUP consecutive rows of a workgroup share
+// most of their columns (union = 25 % of their blocks on the 1M-DoF Gmsh
+// mesh, at most 1,053 nodes), so the workgroup gathers its group's distinct
+// x nodes into LDS once (sorted node ids: 24-B records, mostly adjacent) and
+// every block reads x from LDS through a 2-byte dictionary position instead
+// of a 4-byte column (the bcol stream is not read).  Groups are aligned to
+// DICT_GROUP rows in local row numbering; a RowMap range covers the groups
+// that intersect it (waves outside the range idle), so the N > 1 split
+// (interior rows, then ghost-dependent rows) reuses the same dictionaries.  A
+// group whose dictionary exceeds DICT_CAP nodes reads x through it from
+// global memory.  Same products in the same order as k_nb_spmv: bitwise
+// identical.
+constexpr int DICT_GROUP = 8;
+constexpr int DICT_CAP = 16 * 9 * 9;
+__global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
+    RowMap rm, int64_t ga0, int64_t nga, int64_t gb0, int64_t ngb, const int *__restrict__ rowptr,
+    const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr, const uint16_t *__restrict__ lid,
+    const int *__restrict__ dptr, const int *__restrict__ dict, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, const int *__restrict__ istate, int xcd_chunk)
+{
+    constexpr int R = 3, C = 3, RC = 9;
+    extern __shared__ double xs[];
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t blk = xcd_block(xcd_chunk);
+    if (blk >= nga + ngb) return;  // whole workgroup
+    const bool in_a = blk < nga;
+    const int64_t g = in_a ? ga0 + blk : gb0 + (blk - nga);
+    const int64_t lo = in_a ? rm.a0 : rm.b0, hi = in_a ? rm.a0 + rm.na : rm.b0 + rm.nb;
+    const int64_t i = g * DICT_GROUP + w;
+    const bool live = i >= lo && i < hi;
+    const int d0 = dptr[g], U = dptr[g + 1] - d0;
+    const bool lds_x = U <= DICT_CAP;
+    if (lds_x)
+        for (int t = threadIdx.x; t < 3 * U; t += 64 * DICT_GROUP) {
+            const int e = t / 3;
+            xs[t] = x[(int64_t)dict[d0 + e] * 3 + (t - 3 * e)];
+        }
+    __syncthreads();
+    if (!live) return;
+    const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
+    const double *v = val + vptr[i];
+    const uint16_t *lrow = lid + b0;
+    const int q16 = m & ~15;
+    double acc[R] = {0.0, 0.0, 0.0};
+    auto rowloop = [&](auto xat) {
+        for (int kb = 0; kb < m; kb += 64) {
+            const int k = kb + lane;
+            double vv[RC];
+            if (kb + 64 <= q16) {
+                const double *p = v + (k >> 4) * (RC * 16) + (k & 15);
+#pragma unroll
+                for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(p + t * 16);
+            } else if (k < m) {
+                const int64_t o0 = vofs(1, RC, 0, k, m, mp);
+                const int64_t st = k < q16 ? 16 : m - q16;
+#pragma unroll
+                for (int t = 0; t < RC; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
+            }
+            if (k < m) {
+                const int l = __builtin_nontemporal_load(lrow + k);
+#pragma unroll
+                for (int a = 0; a < R; ++a)
+#pragma unroll
+                    for (int b = 0; b < C; ++b) acc[a] += vv[a * C + b] * xat(l, b);
+            }
+        }
+    };
+    if (lds_x) rowloop([&](int l, int b) { return xs[l * 3 + b]; });
+    else rowloop([&](int l, int b) { return x[(int64_t)dict[d0 + l] * 3 + b]; });
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+    if (lane < R) {
+        double mine = acc[0];
+#pragma unroll
+        for (int a = 1; a < R; ++a)
+            if (lane == a) mine = acc[a];
+        y[i * R + lane] = mine;
+    }
+}
+
 // Scalar CSR SpMV (MatMult_SeqAIJ): one wavefront per row.  A pass covers
 // 64*U entries from the row start rounded down to 32 entries, so every col
 // load (32 int32 = 128 B) and every val load (16 doubles = 128 B) covers whole
@@ -433,6 +520,94 @@ __global__ void k_axpy_same(int64_t n, double a, const double *__restrict__ x, d
         y[i] += a * x[i];
 }
 
+// Column dictionaries of an unstructured node-block matrix (k_nb_spmv_dict):
+// built on the host from the device pattern, groups split over threads.
+int nb_build_dict(kle_mat *A)
+{
+    const int64_t nrows = A->nrows, ng = (nrows + DICT_GROUP - 1) / DICT_GROUP;
+    std::vector<int> rp(nrows + 1), cnt, bcol(std::max<int64_t>(A->nblocks, 1));
+    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (nrows + 1), hipMemcpyDeviceToHost));
+    if (A->d_rowcnt) {
+        cnt.resize(nrows);
+        KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * nrows, hipMemcpyDeviceToHost));
+    }
+    KLE_HIP(hipMemcpy(bcol.data(), A->d_bcol, sizeof(int) * bcol.size(), hipMemcpyDeviceToHost));
+    const int64_t ncol = A->ext_nodes;
+    std::vector<int> dptr(ng + 1, 0);
+    std::vector<uint16_t> lid(bcol.size(), 0);
+    std::vector<int> dict;
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto rows_of = [&](int64_t g, int64_t &r0, int64_t &r1) {
+        r0 = g * DICT_GROUP;
+        r1 = std::min(nrows, r0 + DICT_GROUP);
+    };
+    auto len = [&](int64_t r) { return A->d_rowcnt ? cnt[r] : rp[r + 1] - rp[r]; };
+    // pass 1: distinct columns per group
+    std::vector<int> usz(ng, 0);
+    std::atomic<bool> bad{false};
+    auto pass1 = [&](int t) {
+        std::vector<int> stamp(ncol, -1);
+        for (int64_t g = t; g < ng; g += nt) {
+            int64_t r0, r1;
+            rows_of(g, r0, r1);
+            int u = 0;
+            for (int64_t r = r0; r < r1; ++r)
+                for (int k = 0; k < len(r); ++k) {
+                    const int c = bcol[rp[r] + k];
+                    if (c < 0 || c >= ncol) { bad = true; continue; }
+                    if (stamp[c] != (int)g) {
+                        stamp[c] = (int)g;
+                        ++u;
+                    }
+                }
+            usz[g] = u;
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(pass1, t);
+        for (auto &x : th) x.join();
+    }
+    KLE_ARG(!bad, "column out of range in the node-block pattern");
+    for (int64_t g = 0; g < ng; ++g) {
+        KLE_ARG(usz[g] <= 65535, "a row group's dictionary exceeds 16-bit positions");
+        dptr[g + 1] = dptr[g] + usz[g];
+    }
+    dict.resize(std::max(dptr[ng], 1));
+    auto pass2 = [&](int t) {
+        std::vector<int> pos(ncol, 0), list;
+        for (int64_t g = t; g < ng; g += nt) {
+            int64_t r0, r1;
+            rows_of(g, r0, r1);
+            list.clear();
+            for (int64_t r = r0; r < r1; ++r)
+                for (int k = 0; k < len(r); ++k) list.push_back(bcol[rp[r] + k]);
+            std::sort(list.begin(), list.end());
+            list.erase(std::unique(list.begin(), list.end()), list.end());
+            for (size_t j = 0; j < list.size(); ++j) {
+                pos[list[j]] = (int)j;
+                dict[dptr[g] + j] = list[j];
+            }
+            for (int64_t r = r0; r < r1; ++r)
+                for (int k = 0; k < len(r); ++k) lid[rp[r] + k] = (uint16_t)pos[bcol[rp[r] + k]];
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(pass2, t);
+        for (auto &x : th) x.join();
+    }
+    A->dict_len = dptr[ng];
+    if (hipMalloc(&A->d_dptr, sizeof(int) * (ng + 1)) != hipSuccess ||
+        hipMalloc(&A->d_dict, sizeof(int) * dict.size()) != hipSuccess ||
+        hipMalloc(&A->d_lid, sizeof(uint16_t) * lid.size()) != hipSuccess)
+        return fail(KLE_ERR_MEM, "out of device memory for column dictionaries");
+    KLE_HIP(hipMemcpy(A->d_dptr, dptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_dict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_lid, lid.data(), sizeof(uint16_t) * lid.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
     return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi &&
@@ -474,6 +649,19 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
         hipLaunchKernelGGL((k_nb_spmv_xl<8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512),
                            lds + XL_CAP * 3 * sizeof(double), st, rm, A->d_rowptr, A->d_rowcnt, rbox,
                            (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_val, x->base, y->d, istate,
+                           g_tune.spmv_xcd_chunk);
+    } else if (R == 3 && C == 3 && LAY == 1 && !STRUCT && wv == 8 && A->d_lid && g_tune.spmv_dict) {
+        // dictionary groups intersecting each RowMap range
+        auto groups = [](int64_t a0, int64_t na, int64_t &g0, int64_t &ng) {
+            g0 = a0 / DICT_GROUP;
+            ng = na > 0 ? (a0 + na + DICT_GROUP - 1) / DICT_GROUP - g0 : 0;
+        };
+        int64_t ga0, nga, gb0, ngb;
+        groups(rm.a0, rm.na, ga0, nga);
+        groups(rm.b0, rm.nb, gb0, ngb);
+        hipLaunchKernelGGL(k_nb_spmv_dict, dim3((unsigned)(nga + ngb)), dim3(64 * DICT_GROUP),
+                           lds + DICT_CAP * 3 * sizeof(double), st, rm, ga0, nga, gb0, ngb, A->d_rowptr, A->d_rowcnt,
+                           A->d_vptr, A->d_lid, A->d_dptr, A->d_dict, A->d_val, x->base, y->d, istate,
                            g_tune.spmv_xcd_chunk);
     } else if (R == 3 && C == 3 && LAY == 1 && wv == 8)
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), lds, st, rm,
@@ -800,6 +988,9 @@ int kle_mat_destroy(kle_mat *A)
     hipFree(A->d_vptr);
     hipFree(A->d_rowptr);
     hipFree(A->d_bcol);
+    hipFree(A->d_dptr);
+    hipFree(A->d_dict);
+    hipFree(A->d_lid);
     hipFree(A->d_val);
     hipFree(A->d_aptr);
     hipFree(A->d_acol);
@@ -1129,6 +1320,9 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     B->d_vptr = nullptr;
     B->d_rowptr = nullptr;
     B->d_bcol = nullptr;
+    B->d_dptr = nullptr;
+    B->d_dict = nullptr;
+    B->d_lid = nullptr;
     B->d_val = nullptr;
     B->d_aptr = nullptr;
     B->d_acol = nullptr;
@@ -1150,6 +1344,17 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
             KLE_HIP(hipMemcpy(B->d_rowbox, A->d_rowbox, sizeof(int) * 2 * A->nrows, hipMemcpyDeviceToDevice));
         }
         KLE_HIP(hipMemcpy(B->d_bcol, A->d_bcol, sizeof(int) * std::max<int64_t>(A->nblocks, 1), hipMemcpyDeviceToDevice));
+        if (A->d_lid) {
+            const int64_t ng = (A->nrows + DICT_GROUP - 1) / DICT_GROUP;
+            KLE_HIP(hipMalloc(&B->d_dptr, sizeof(int) * (ng + 1)));
+            KLE_HIP(hipMalloc(&B->d_dict, sizeof(int) * std::max<int64_t>(A->dict_len, 1)));
+            KLE_HIP(hipMalloc(&B->d_lid, sizeof(uint16_t) * std::max<int64_t>(A->nblocks, 1)));
+            KLE_HIP(hipMemcpy(B->d_dptr, A->d_dptr, sizeof(int) * (ng + 1), hipMemcpyDeviceToDevice));
+            KLE_HIP(hipMemcpy(B->d_dict, A->d_dict, sizeof(int) * std::max<int64_t>(A->dict_len, 1),
+                              hipMemcpyDeviceToDevice));
+            KLE_HIP(hipMemcpy(B->d_lid, A->d_lid, sizeof(uint16_t) * std::max<int64_t>(A->nblocks, 1),
+                              hipMemcpyDeviceToDevice));
+        }
         if (copy_values) KLE_HIP(hipMemcpy(B->d_val, A->d_val, sizeof(double) * nv, hipMemcpyDeviceToDevice));
         else KLE_HIP(hipMemset(B->d_val, 0, sizeof(double) * nv));
     } else {
@@ -1215,9 +1420,14 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
     if (A->kind == 0) {
         // bytes the SpMV must move: real blocks only (row padding is not counted);
         // the column stream unless the columns are computed from row boxes
+        // (dictionary matrices: a 2-byte position per block plus the
+        // dictionaries and their offsets instead of the column stream)
         const bool sb = A->spmv_struct && A->d_rowbox;
-        *bytes = (double)A->nblocks_real * (A->R * A->C * 8.0 + (sb ? 0.0 : 4.0)) + (A->nrows + 1) * 4.0 +
+        const bool dict = !sb && A->d_lid && g_tune.spmv_dict;
+        const double colb = sb ? 0.0 : dict ? 2.0 : 4.0;
+        *bytes = (double)A->nblocks_real * (A->R * A->C * 8.0 + colb) + (A->nrows + 1) * 4.0 +
                  (A->d_rowcnt ? A->nrows * 4.0 : 0.0) + (sb ? A->nrows * 8.0 : 0.0) +
+                 (dict ? A->dict_len * 4.0 + ((A->nrows + DICT_GROUP - 1) / DICT_GROUP + 1) * 4.0 : 0.0) +
                  (double)A->ext_nodes * A->C * 8.0 + (double)A->m_local * 8.0;
     } else {
         *bytes = (double)A->nnz * 12.0 + (A->m_local + 1) * 8.0 + A->n_local * 8.0 + A->m_local * 8.0;

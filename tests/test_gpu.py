@@ -579,6 +579,49 @@ def test_spmv_x_in_lds_is_bitwise(pa, nelem, ngl):
             np.testing.assert_array_equal(ys[0], yv)
 
 
+@pytest.mark.parametrize("nel,ngl", [([4, 3, 3], 5), ([3, 3, 2], 3), ([2, 2, 2], 7)])
+def test_spmv_column_dictionaries_are_bitwise(pa, nel, ngl, tmp_path):
+    """k_nb_spmv_dict (unstructured 3x3 rows: x staged in LDS through each
+    8-row group's column dictionary, 2-byte positions instead of the column
+    stream) == k_nb_spmv with the bcol stream (spmv_dict 0, 4 and 8
+    waves), bitwise, for K and Rw of a perturbed, rotated, shuffled Gmsh hex
+    mesh; also after Mat.duplicate.  Dictionaries are built for every size
+    here (spmv_dict_min_rows 0)."""
+    from pynama_amd.meshgen import perturbed_box, write_gmsh
+    from pynama_amd.runtime import get_tuning, set_tuning
+    V, Cc, F, T = perturbed_box(3, nel, seed=11)
+    path = tmp_path / "m.msh"
+    write_gmsh(path, 3, V, Cc, F, T)
+    cfg = {"domain": {"ngl": ngl, "gmsh-file": str(path)},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    old = get_tuning("spmv_dict_min_rows")
+    set_tuning("spmv_dict_min_rows", 0)
+    try:
+        dom = pa.Domain()
+        dom.configure(cfg)
+        dom.setUp()
+        mat = pa.MatFS()
+        mat.setDomain(dom)
+        mat.build(buildOperators=False)
+    finally:
+        set_tuning("spmv_dict_min_rows", old)
+    for A in (mat.K, mat.Rw, mat.K.duplicate(copy=True)):
+        assert not A.isStructured()
+        x = A.createVecRight()
+        x.setArray(np.random.default_rng(5).uniform(-1, 1, x.getLocalSize()))
+        ys = []
+        try:
+            for dct, wv in ((1, 8), (0, 8), (0, 4)):
+                set_tuning("spmv_dict", dct)
+                set_tuning("spmv_waves", wv)
+                ys.append((A * x).getArray().copy())
+        finally:
+            set_tuning("spmv_dict", 1)
+            set_tuning("spmv_waves", 0)
+        for yv in ys[1:]:
+            np.testing.assert_array_equal(ys[0], yv)
+
+
 @pytest.mark.parametrize("lay", [0, 1])
 def test_device_pattern_matches_host(pa, lay):
     """Box-mesh patterns built on the device (k_pat_count / k_pat_fill) ==

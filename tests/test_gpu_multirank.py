@@ -26,8 +26,9 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="host",
                       RANK=str(rank), WORLD_SIZE=str(size))
-    if waves:
+    if waves:  # 8: the LDS SpMV kernels (x-in-LDS / column dictionaries) at test sizes
         os.environ["KLE_SPMV_WAVES"] = str(waves)
+        os.environ["KLE_SPMV_DICT_MIN_ROWS"] = "0"
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=size)
@@ -157,12 +158,13 @@ def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0):
     assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
 
 
-def _run(size, nelem, ngl, overlap=True, ksp_type="cg", msh=None, partitioner=None):
+def _run(size, nelem, ngl, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, msh, partitioner))
+    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, msh, partitioner,
+                                               waves))
              for r in range(size)]
     return _collect(procs, q, size)
 
@@ -197,16 +199,18 @@ def _collect(procs, q, size, timeout=100):
     return sorted(res, key=lambda r: r["rank"])
 
 
-@pytest.mark.parametrize("size,partitioner,nel,ksp_type", [
-    (2, "slab", [2, 3, 9], "cg"), (3, "slab", [2, 3, 9], "cg"),
-    (2, "inertial", [3, 3, 4], "cg"), (3, "inertial", [3, 4, 4], "cg"), (4, "inertial", [4, 4, 4], "cg"),
-    (4, "inertial", [4, 4, 4], "pipecg"), (8, "inertial", [4, 4, 6], "pipecg")])
-def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type, tmp_path):
+@pytest.mark.parametrize("size,partitioner,nel,ksp_type,waves", [
+    (2, "slab", [2, 3, 9], "cg", 0), (3, "slab", [2, 3, 9], "cg", 0),
+    (2, "inertial", [3, 3, 4], "cg", 0), (3, "inertial", [3, 4, 4], "cg", 0), (4, "inertial", [4, 4, 4], "cg", 0),
+    (4, "inertial", [4, 4, 4], "pipecg", 0), (8, "inertial", [4, 4, 6], "pipecg", 0),
+    (2, "slab", [2, 3, 9], "cg", 8), (3, "inertial", [3, 4, 4], "pipecg", 8)])
+def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type, waves, tmp_path):
     """SURVEY 8(e) on an unstructured mesh (config 5's path): rotated /
     shuffled hexes in Gmsh format, partitioned into slabs (two-range halo)
     or by inertial bisection (Chaco's method: several neighbours per rank,
     index-list halos); the same halo / overlap / CG code; solution and SpMV
-    vs the oracle's serial system (coordinate numbering)."""
+    vs the oracle's serial system (coordinate numbering).  waves 8: every rank
+    runs the column-dictionary SpMV on its split row ranges."""
     from oracle import oracle as O
     import pynama_amd as pa
     from pynama_amd.meshgen import perturbed_box, write_gmsh
@@ -214,7 +218,7 @@ def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type
     msh = str(tmp_path / "part.msh")
     write_gmsh(msh, 3, V, Cc, F, T)
     ngl = 3
-    res = _run(size, [0, 0, 0], ngl, msh=msh, partitioner=partitioner, ksp_type=ksp_type)
+    res = _run(size, [0, 0, 0], ngl, msh=msh, partitioner=partitioner, ksp_type=ksp_type, waves=waves)
     for r in res:
         assert r["overlap_equal"], (r["rank"], r["ov_diff"])
     um = O.UMesh(3, ngl, V, Cc, F, T)
