@@ -72,7 +72,10 @@ const char *kle_last_error(void);
  * rows per SpMV workgroup of 3x3 chunked matrices), "spmv_x_lds" (1 default:
  * structured 3x3 rows at 8 waves stage x in LDS; 0 off), "spmv_xcd_chunk"
  * (row blocks per XCD run, 0 round-robin; default 16), "spmv_dyn_lds" (unused
- * LDS bytes per SpMV workgroup while side-stream work runs, -1 auto). */
+ * LDS bytes per SpMV workgroup while side-stream work runs, -1 auto),
+ * "spmv_dict" (1 default: unstructured 3x3 rows at 8 waves read x through
+ * per-group column dictionaries; 0 off), "spmv_dict_min_rows" (node rows from
+ * which matrices get dictionaries at creation; default 64000). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
