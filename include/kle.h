@@ -75,7 +75,9 @@ const char *kle_last_error(void);
  * LDS bytes per SpMV workgroup while side-stream work runs, -1 auto),
  * "spmv_dict" (1 default: unstructured 3x3 rows at 8 waves read x through
  * per-group column dictionaries; 0 off), "spmv_dict_min_rows" (node rows from
- * which matrices get dictionaries at creation; default 64000). */
+ * which matrices get dictionaries at creation; default 64000), "upd_preload"
+ * (1 default: CG update kernels load their first element and the stage inputs
+ * before the prologue; 0 off). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);

@@ -283,6 +283,7 @@ struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
+    int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off

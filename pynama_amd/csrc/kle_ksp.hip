@@ -361,18 +361,41 @@ __device__ __forceinline__ void sums3(const double *__restrict__ a0, const doubl
 // the scalar slots (workgroup 0 seeds the next parity's inputs from them).
 // Returns, in every thread, whether the stage ended the solve; alpha / beta
 // for the update.
+// The scalar inputs of the stage, read by thread 0 at kernel entry so their
+// latency overlaps the partial sums.
+struct StageIn {
+    double prho, palpha, tol, alpha, beta, rho;
+    int pits, fixed, maxit, its;
+};
+__device__ __forceinline__ StageIn stage_inputs(const double *__restrict__ scal, const int *__restrict__ ist, int par)
+{
+    StageIn in;
+    in.prho = scal[S_PRHO0 + par];
+    in.palpha = scal[S_PALPHA0 + par];
+    in.tol = scal[S_TOL];
+    in.alpha = scal[S_ALPHA];
+    in.beta = scal[S_BETA];
+    in.rho = scal[S_RHO];
+    in.pits = ist[I_PITS0 + par];
+    in.fixed = ist[I_FIXED];
+    in.maxit = ist[I_MAXIT];
+    in.its = ist[I_ITS];
+    return in;
+}
+
 __device__ __forceinline__ bool stage_prologue(int pro, const double (&t)[3], double *__restrict__ scal,
                                                int *__restrict__ ist, int par, double atol, double &alpha,
-                                               double &beta)
+                                               double &beta, const StageIn *pre = nullptr)
 {
     __shared__ double ab[2];
     __shared__ int stop;
     const bool w0 = blockIdx.x == 0 && threadIdx.x == 0;
     const int nxt = par ^ 1;
     if (threadIdx.x == 0) {
+        const StageIn in = pre ? *pre : stage_inputs(scal, ist, par);
         if (pro) {
-            const SrStep st = sr_step(t[0], sqrt(t[1]), t[2], scal[S_PRHO0 + par], scal[S_PALPHA0 + par],
-                                      ist[I_PITS0 + par], scal[S_TOL], ist[I_FIXED], ist[I_MAXIT], atol);
+            const SrStep st = sr_step(t[0], sqrt(t[1]), t[2], in.prho, in.palpha, in.pits, in.tol, in.fixed,
+                                      in.maxit, atol);
             ab[0] = st.alpha;
             ab[1] = st.beta;
             stop = st.reason != 0;
@@ -390,13 +413,13 @@ __device__ __forceinline__ bool stage_prologue(int pro, const double (&t)[3], do
                 if (st.reason) ist[I_REASON] = st.reason;
             }
         } else {
-            ab[0] = scal[S_ALPHA];
-            ab[1] = scal[S_BETA];
+            ab[0] = in.alpha;
+            ab[1] = in.beta;
             stop = 0;
             if (w0) {
-                scal[S_PRHO0 + nxt] = scal[S_RHO];
-                scal[S_PALPHA0 + nxt] = scal[S_ALPHA];
-                ist[I_PITS0 + nxt] = ist[I_ITS];
+                scal[S_PRHO0 + nxt] = in.rho;
+                scal[S_PALPHA0 + nxt] = in.alpha;
+                ist[I_PITS0 + nxt] = in.its;
             }
         }
     }
@@ -424,7 +447,7 @@ constexpr int PRO_DOT_BLOCKS = 512;
 // start or a flush): alpha, beta from the scalar slots.  A stage that ends the
 // solve (converged, diverged, NaN) skips the update in every workgroup, as the
 // reason word makes every later launch a no-op.
-template <bool JAC>
+template <bool JAC, bool PRE>
 __global__ __launch_bounds__(KB) void k_pipe_iter(int64_t n, const double *__restrict__ dinv,
                                                   const double *__restrict__ nv, double *__restrict__ z,
                                                   double *__restrict__ q, double *__restrict__ sv,
@@ -435,35 +458,52 @@ __global__ __launch_bounds__(KB) void k_pipe_iter(int64_t n, const double *__res
                                                   double *__restrict__ scal, int *__restrict__ ist, int pro, int par,
                                                   double atol)
 {
-    if (ist[I_REASON] != 0) return;
     const int G = (int)gridDim.x;
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    // PRE: this thread's first element and the stage's scalar inputs are
+    // loaded before the reason check and the partial sums, so their latency
+    // overlaps the prologue instead of following it (same arithmetic)
+    double e[11];
+    StageIn in;
+    if constexpr (PRE) {
+        if (i0 < n) {
+            e[0] = nv[i0], e[1] = z[i0], e[2] = m[i0], e[3] = q[i0], e[4] = w[i0], e[5] = sv[i0];
+            e[6] = u[i0], e[7] = p[i0], e[8] = x[i0], e[9] = r[i0], e[10] = JAC ? dinv[i0] : 1.0;
+        }
+        if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
+    }
+    if (ist[I_REASON] != 0) return;
     double t[3] = {0.0, 0.0, 0.0};
     if (pro) sums3(pp_in, pp_in + G, G, pp_in + 2 * G, G, t);
     double alpha, beta;
-    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta)) return;
+    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta, PRE ? &in : nullptr)) return;
     double acc[3] = {0.0, 0.0, 0.0};
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double zi = nv[i] + beta * z[i];
-        const double qi = m[i] + beta * q[i];
-        const double si = w[i] + beta * sv[i];
-        const double pi = u[i] + beta * p[i];
+    for (int64_t i = i0; i < n; i += stride) {
+        if (!PRE || i != i0) {
+            e[0] = nv[i], e[1] = z[i], e[2] = m[i], e[3] = q[i], e[4] = w[i], e[5] = sv[i];
+            e[6] = u[i], e[7] = p[i], e[8] = x[i], e[9] = r[i], e[10] = JAC ? dinv[i] : 1.0;
+        }
+        const double zi = e[0] + beta * e[1];
+        const double qi = e[2] + beta * e[3];
+        const double si = e[4] + beta * e[5];
+        const double pi = e[6] + beta * e[7];
         z[i] = zi;
         q[i] = qi;
         sv[i] = si;
         p[i] = pi;
-        x[i] += alpha * pi;
-        const double ri = r[i] - alpha * si;
-        const double ui = u[i] - alpha * qi;
-        const double wi = w[i] - alpha * zi;
+        x[i] = e[8] + alpha * pi;
+        const double ri = e[9] - alpha * si;
+        const double ui = e[6] - alpha * qi;
+        const double wi = e[4] - alpha * zi;
         r[i] = ri;
         u[i] = ui;
         w[i] = wi;
-        m[i] = JAC ? dinv[i] * wi : wi;
+        m[i] = JAC ? e[10] * wi : wi;
         acc[0] += ri * ui;
         acc[1] += ri * ri;
         acc[2] += wi * ui;
     }
-    block_sums<3>(acc, pp_out, (int)gridDim.x);
+    block_sums<3>(acc, pp_out, G);
 }
 
 // The scalar stage of the last update of a solve call whose partials would
@@ -495,7 +535,7 @@ __global__ __launch_bounds__(KB) void k_cg_flush(const double *__restrict__ a0, 
 // rank): sums (r,u), (r,r) of the previous update [2][G] and (w,u) of the
 // dot launch [Gd], then  p = u + b p ; s = w + b s ; x += a p ; r -= a s ;
 // u = M r  with the new (r,u), (r,r) partials to pu_out [2][G].
-template <bool JAC>
+template <bool JAC, bool PRE>
 __global__ __launch_bounds__(KB) void k_sr_iter(int64_t n, const double *__restrict__ dinv,
                                                 const double *__restrict__ w, double *__restrict__ u,
                                                 double *__restrict__ p, double *__restrict__ sv,
@@ -504,22 +544,36 @@ __global__ __launch_bounds__(KB) void k_sr_iter(int64_t n, const double *__restr
                                                 int Gd, double *__restrict__ pu_out, double *__restrict__ scal,
                                                 int *__restrict__ ist, int pro, int par, double atol)
 {
-    if (ist[I_REASON] != 0) return;
     const int G = (int)gridDim.x;
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    double e[7];  // PRE: first element and stage inputs before the prologue (as k_pipe_iter)
+    StageIn in;
+    if constexpr (PRE) {
+        if (i0 < n) {
+            e[0] = u[i0], e[1] = p[i0], e[2] = w[i0], e[3] = sv[i0], e[4] = x[i0], e[5] = r[i0];
+            e[6] = JAC ? dinv[i0] : 1.0;
+        }
+        if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
+    }
+    if (ist[I_REASON] != 0) return;
     double t[3] = {0.0, 0.0, 0.0};
     if (pro) sums3(pu_in, pu_in + G, G, pd, Gd, t);
     double alpha, beta;
-    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta)) return;
+    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta, PRE ? &in : nullptr)) return;
     double acc[2] = {0.0, 0.0};
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double pi = u[i] + beta * p[i];
-        const double si = w[i] + beta * sv[i];
+    for (int64_t i = i0; i < n; i += stride) {
+        if (!PRE || i != i0) {
+            e[0] = u[i], e[1] = p[i], e[2] = w[i], e[3] = sv[i], e[4] = x[i], e[5] = r[i];
+            e[6] = JAC ? dinv[i] : 1.0;
+        }
+        const double pi = e[0] + beta * e[1];
+        const double si = e[2] + beta * e[3];
         p[i] = pi;
         sv[i] = si;
-        x[i] += alpha * pi;
-        const double ri = r[i] - alpha * si;
+        x[i] = e[4] + alpha * pi;
+        const double ri = e[5] - alpha * si;
         r[i] = ri;
-        const double ui = JAC ? dinv[i] * ri : ri;
+        const double ui = JAC ? e[6] * ri : ri;
         u[i] = ui;
         acc[0] += ri * ui;
         acc[1] += ri * ri;
@@ -1036,14 +1090,13 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     auto iteration = [&]() -> int {
         KLE_TRY(c->tic("cg_update", &ev));
         {
-            if (jac)
-                hipLaunchKernelGGL(k_sr_iter<true>, dim3(Gu), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d,
-                                   k->p->d, k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1],
-                                   c->d_scal, c->d_istate, (int)pending, par, k->atol);
-            else
-                hipLaunchKernelGGL(k_sr_iter<false>, dim3(Gu), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d,
-                                   k->p->d, k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1],
-                                   c->d_scal, c->d_istate, (int)pending, par, k->atol);
+            auto go = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3(Gu), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->u->d, k->p->d,
+                                   k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1], c->d_scal,
+                                   c->d_istate, (int)pending, par, k->atol);
+            };
+            if (jac) go(g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
+            else go(g_tune.upd_preload ? k_sr_iter<false, true> : k_sr_iter<false, false>);
             KLE_HIP(hipGetLastError());
             KLE_TRY(c->toc("cg_update", &ev));
             par ^= 1;
@@ -1193,14 +1246,13 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     for (int it = 0; it < limit && !rc; ++it) {
         rc = c->tic("cg_update", &ev);
         if (rc) break;
-        if (jac)
-            hipLaunchKernelGGL(k_pipe_iter<true>, dim3(G), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
-                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, pp[par],
-                               pp[par ^ 1], c->d_scal, c->d_istate, (int)pending, par, k->atol);
-        else
-            hipLaunchKernelGGL(k_pipe_iter<false>, dim3(G), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d,
-                               k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, pp[par],
-                               pp[par ^ 1], c->d_scal, c->d_istate, (int)pending, par, k->atol);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(G), dim3(KB), 0, c->stream, n, dinv, k->nv->d, k->z->d, k->q->d, k->s->d,
+                               k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, pp[par], pp[par ^ 1], c->d_scal,
+                               c->d_istate, (int)pending, par, k->atol);
+        };
+        if (jac) go(g_tune.upd_preload ? k_pipe_iter<true, true> : k_pipe_iter<true, false>);
+        else go(g_tune.upd_preload ? k_pipe_iter<false, true> : k_pipe_iter<false, false>);
         if (hipGetLastError() != hipSuccess) { rc = fail(KLE_ERR_DEVICE, "k_pipe_iter launch failed"); break; }
         if ((rc = c->toc("cg_update", &ev))) break;
         par ^= 1;
