@@ -72,7 +72,7 @@ def main():
             print(json.dumps({"rep": rep, "variant": v, "avg_ms": avg, "gbps": nbytes / (avg * 1e-3) / 1e9,
                               "bitwise_equal_first": bitwise}), flush=True)
             for k in v:
-                set_tuning(k, {"spmv_xcd_chunk": 16, "spmv_dyn_lds": -1, "spmv_x_lds": 1}.get(k, 0))
+                set_tuning(k, {"spmv_xcd_chunk": 16, "spmv_dyn_lds": -1, "spmv_x_lds": 1, "spmv_dict": 1, "upd_preload": 1}.get(k, 0))
     summ = [{"variant": v, "median_ms": statistics.median(res[i]), "min_ms": min(res[i]),
              "gbps_median": nbytes / (statistics.median(res[i]) * 1e-3) / 1e9} for i, v in enumerate(variants)]
     print(json.dumps({"summary": summ, "bytes_per_spmv": nbytes, "nnz": A.getInfo()["nz_used"],
