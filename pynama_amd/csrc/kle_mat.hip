@@ -570,7 +570,7 @@ int nb_build_dict(kle_mat *A)
     }
     KLE_ARG(!bad, "column out of range in the node-block pattern");
     for (int64_t g = 0; g < ng; ++g) {
-        KLE_ARG(usz[g] <= 65535, "a row group's dictionary exceeds 16-bit positions");
+        if (usz[g] > 65535) return 0;  // positions would not fit 16 bits: keep the column stream
         dptr[g + 1] = dptr[g] + usz[g];
     }
     dict.resize(std::max(dptr[ng], 1));
