@@ -569,9 +569,12 @@ int nb_build_dict(kle_mat *A)
         for (auto &x : th) x.join();
     }
     KLE_ARG(!bad, "column out of range in the node-block pattern");
+    int64_t total = 0;
     for (int64_t g = 0; g < ng; ++g) {
         if (usz[g] > 65535) return 0;  // positions would not fit 16 bits: keep the column stream
-        dptr[g + 1] = dptr[g] + usz[g];
+        total += usz[g];
+        if (total > INT_MAX) return 0;  // int32 dictionary offsets
+        dptr[g + 1] = (int)total;
     }
     dict.resize(std::max(dptr[ng], 1));
     auto pass2 = [&](int t) {
