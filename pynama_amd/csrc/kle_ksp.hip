@@ -1237,8 +1237,7 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     if (!cont) k->pipe_par = 0;
     int par = k->pipe_par;
     bool pending = false;  // a launch's partials await the next launch's prologue
-    hipEvent_t ev_upd = nullptr, ev_red = nullptr;
-    KLE_HIP(hipEventCreateWithFlags(&ev_upd, hipEventDisableTiming));
+    hipEvent_t ev_red = nullptr;
     KLE_HIP(hipEventCreateWithFlags(&ev_red, hipEventDisableTiming));
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
@@ -1261,12 +1260,11 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             // one rank: the next launch's prologue reduces these partials
             if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
         } else if (side && c->nranks > 1) {
-            // the partials' allreduce on the comm stream behind the halo, beside the SpMV
-            if (hipEventRecord(ev_upd, c->stream) != hipSuccess ||
-                hipStreamWaitEvent(c->comm_stream, ev_upd, 0) != hipSuccess) {
-                rc = fail(KLE_ERR_DEVICE, "event record/wait failed");
-                break;
-            }
+            // the partials' allreduce on the comm stream behind the halo, beside
+            // the SpMV; the overlapped SpMV already makes the comm stream wait
+            // for the update (ev_x_ready), so no event of its own: each event
+            // record / cross-stream wait costs ~2.5 us on the critical path
+            // (profiles/r02/sync_cost_eighth.jsonl)
             if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
             if ((rc = allreduce_sum(c, pp[par], 3 * G, c->comm_stream))) break;
             if (hipEventRecord(ev_red, c->comm_stream) != hipSuccess ||
@@ -1292,7 +1290,6 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
         if (hipGetLastError() != hipSuccess) rc = fail(KLE_ERR_DEVICE, "k_cg_flush launch failed");
     }
     k->pipe_par = par;
-    hipEventDestroy(ev_upd);
     hipEventDestroy(ev_red);
     if (rc) return rc;
     KLE_TRY(poll_state(k));
