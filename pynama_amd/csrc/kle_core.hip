@@ -36,6 +36,19 @@ int fail(int code, const char *fmt, ...)
 
 void clear_error() { g_err.clear(); }
 
+// Flags of the events that order the compute and comm streams (N > 1).
+// KLE_EVENT_NO_SYSTEM_FENCE=1 adds hipEventDisableSystemFence: both streams
+// and RCCL's kernels live on this device, so a device-scope release would
+// do, and it halves the cost of a cross-stream round trip (7.8 -> 3.9 us on
+// the 1/8 slab, 7.1 -> 4.3 at config 2; profiles/r02/sync_evflags_*.jsonl).
+// Off by default until a multi-GPU run confirms RCCL never reads our buffers
+// from another device.
+unsigned sync_event_flags()
+{
+    const char *e = getenv("KLE_EVENT_NO_SYSTEM_FENCE");
+    return hipEventDisableTiming | (e && atoi(e) ? hipEventDisableSystemFence : 0u);
+}
+
 int grid_for(int64_t work, int per_block, int max_blocks)
 {
     int64_t g = (work + per_block - 1) / per_block;
@@ -582,8 +595,8 @@ static int ctx_init(int device, int rank, int nranks, kle_ctx **out)
     const hipError_t se = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (se != hipSuccess ||
         hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_x_ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_halo_done, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_x_ready, sync_event_flags()) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_halo_done, sync_event_flags()) != hipSuccess) {
         kle_ctx_destroy(c);
         return fail(KLE_ERR_DEVICE, "hipStreamCreate / hipEventCreate failed");
     }

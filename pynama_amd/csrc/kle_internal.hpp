@@ -276,6 +276,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
+unsigned sync_event_flags();  // kle_core.hip
 int nb_build_dict(kle_mat *A);  // kle_mat.hip
 // Performance knobs (kle_set_tuning): every setting gives correct results;
 // they exist for in-process A/B measurements (tools/cg_ab.py).

@@ -1238,7 +1238,7 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     int par = k->pipe_par;
     bool pending = false;  // a launch's partials await the next launch's prologue
     hipEvent_t ev_red = nullptr;
-    KLE_HIP(hipEventCreateWithFlags(&ev_red, hipEventDisableTiming));
+    KLE_HIP(hipEventCreateWithFlags(&ev_red, sync_event_flags()));
     const int limit = k->fixed ? k->fixed : k->maxit;
     std::pair<hipEvent_t, hipEvent_t> ev;
     int rc = 0;

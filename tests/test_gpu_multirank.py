@@ -91,6 +91,17 @@ def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap, ksp_type):
     _check_box(size, nelem, ngl, overlap, ksp_type)
 
 
+def test_partitioned_solve_without_system_fence_events():
+    """KLE_EVENT_NO_SYSTEM_FENCE=1 (device-scope events between the compute and
+    comm streams, kle_core.hip sync_event_flags): the overlapped pipelined CG
+    on 3 ranks still reproduces the serial oracle."""
+    os.environ["KLE_EVENT_NO_SYSTEM_FENCE"] = "1"  # inherited by the spawned ranks
+    try:
+        _check_box(3, [2, 3, 3], 3, True, "pipecg")
+    finally:
+        del os.environ["KLE_EVENT_NO_SYSTEM_FENCE"]
+
+
 @pytest.mark.parametrize("ksp_type", ["cg", "pipecg"])
 def test_eight_slab_solve_matches_serial(ksp_type):
     """The 8-GPU bench's decomposition (config 3) at small size: 8 ranks of one
