@@ -183,3 +183,83 @@ def test_unstructured_full_size_dictionary_spmv_is_bitwise(pa, tmp_path):
     assert ksp.getTrueRelativeResidual() <= 1.05e-10
     assert abs(ksp.getIterationNumber() - 891) <= 4
     _log(t0, f"solve: {ksp.getIterationNumber()} iterations")
+
+
+@pytest.mark.timeout(900)
+def test_unstructured_full_size_matches_oracle(pa, tmp_path):
+    """Config 5's path at config 2's size against the oracle: the bench's
+    1M-DoF unstructured mesh ([20,16,16] perturbed / rotated / shuffled hexes
+    through Gmsh, p = 4) assembled on the device (kle_umesh.cpp numbering,
+    Hilbert order; column-dictionary SpMV) and by `oracle.UMesh` (nodes
+    identified by coordinates, C assembly of mat_fs.py:131-192 in ascending
+    cell order).  Under the node map: the Dirichlet set equal; K, Krhs and Rw
+    equal as operators (products with two random vectors <= 1e-12 of scale);
+    b <= 1e-12; the device solution's true residual with the oracle's K and b
+    <= 1.05e-10 and within 1e-7 of the oracle's Jacobi-CG solution."""
+    from pynama_amd import fields
+    from pynama_amd.meshgen import perturbed_box, write_gmsh
+    t0 = time.perf_counter()
+    V, Cc, F, T = perturbed_box(3, NELEM, seed=5)
+    path = tmp_path / "mesh.msh"
+    write_gmsh(path, 3, V, Cc, F, T)
+    cfg = {"domain": {"ngl": NGL, "gmsh-file": str(path)},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    sol = pa.KleSolver()
+    sol.setMat(mat)
+    sol.setUp()
+    ksp = sol.getKSP()
+    ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=20000)
+    f = fields.get("taylor_green3d")
+    alpha = f.alpha(0.01 / 0.5, 0.0)
+    xd = dom.getFullCoordArray().reshape(-1, 3)
+    vort = mat.Rw.createVecRight()
+    vort.setArray(f.vorticity(xd, alpha))
+    vel = sol.getSolution()
+    dom.applyBoundaryConditions(vel, "velocity", 0.0, 0.02)
+    b = sol.rhs(vort).copy()
+    bd = b.getArray().copy()
+    sol.solve(vort)
+    assert ksp.getConvergedReason() > 0
+    u_dev = vel.getArray().copy()
+    _log(t0, f"device: {ksp.getIterationNumber()} iterations")
+
+    um = O.UMesh(3, NGL, V, Cc, F, T)
+    assert um.N == 342225
+    mp = O.node_map(xd, um.coords())              # device node -> oracle node
+    xo = um.coords()
+    flag = ((um.tags_ & 0x3f) != 0).astype(np.uint8)
+    np.testing.assert_array_equal(np.sort(mp[np.array(sorted(dom.getNodesDirichlet()))]), np.flatnonzero(flag))
+    _log(t0, "oracle mesh, node map, Dirichlet set equal")
+    Ko, Kro, Rwo = um.assemble_fs(flag)
+    _log(t0, f"oracle assembly: K {Ko.nnz} nnz")
+    dof = (mp[:, None] * 3 + np.arange(3)).ravel()  # device DoF -> oracle DoF
+    rng = np.random.default_rng(3)
+    for name, ref in (("K", Ko), ("Krhs", Kro), ("Rw", Rwo)):
+        A = getattr(mat, name)
+        for _ in range(2):
+            xo_v = rng.uniform(-1, 1, ref.n if hasattr(ref, "n") else um.N * 3)
+            x = A.createVecRight()
+            x.setArray(xo_v[dof])
+            yd = (A * x).getArray()
+            yo = ref.mult(xo_v)[dof]
+            assert np.abs(yd - yo).max() <= 1e-12 * max(1.0, np.abs(yo).max()), name
+        _log(t0, f"{name}: equal as operators under the node map")
+    ubc = np.zeros(um.N * 3)
+    bn = np.flatnonzero(flag)
+    ubc[(bn[:, None] * 3 + np.arange(3)).ravel()] = f.velocity(xo[bn], alpha)
+    bo = Rwo.mult(f.vorticity(xo, alpha)) + Kro.mult(ubc)
+    assert np.abs(bd - bo[dof]).max() <= 1e-12 * np.abs(bo).max()
+    u_o = np.empty_like(u_dev)
+    u_o[dof] = u_dev                                # device solution in oracle numbering
+    res = float(np.linalg.norm(bo - Ko.mult(u_o)) / np.linalg.norm(bo))
+    assert res <= 1.05e-10, res
+    uo, its_o, rr_o = Ko.cg(bo, rtol=1e-10, jacobi=True)
+    rel = float(np.linalg.norm(u_o - uo) / np.linalg.norm(uo))
+    _log(t0, f"true residual {res:.3e}; oracle CG {its_o} iterations; ||u - u_oracle|| / ||u_oracle|| {rel:.3e}")
+    assert rel <= 1e-7
