@@ -325,6 +325,18 @@ int kle_mat_convert_aij(const kle_mat *A, kle_mat **out);
  * of streaming 4 B per block (default on; 0 forces the column stream). */
 int kle_mat_set_spmv_structured(kle_mat *A, int on);
 int kle_mat_is_structured(const kle_mat *A, int *on);
+/* Symmetric storage (MatSetOption(A, MAT_SPD, PETSC_TRUE) with PETSc's
+ * MATSBAIJ layout; kle_solver.py:33-37 solves with the SPD K): keep only each
+ * row's blocks from its diagonal block on and run the SpMV over them, every
+ * stored off-diagonal block serving row i and, transposed, row j.  Needs a
+ * single-rank 3x3 node-block matrix on a box lattice whose blocks are
+ * symmetric (to 1e-12 of the largest entry); otherwise KLE_ERR_SUP.  The full
+ * storage stays (getRow, CSR export); any value change (diagonalScale, axpy,
+ * setValues/assemble) drops the symmetric copy.  kle_assemble_kle turns it on
+ * for K (tuning "spmv_sym", "spmv_sym_min_rows").  Results agree with the
+ * full-storage SpMV to rounding, not bitwise. */
+int kle_mat_set_symmetric(kle_mat *A, int on);
+int kle_mat_get_symmetric(const kle_mat *A, int *on);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

@@ -141,6 +141,8 @@ _SIGS = {
     "kle_mat_set_halo_overlap": [vp, C.c_int],
     "kle_mat_set_spmv_structured": [vp, C.c_int],
     "kle_mat_is_structured": [vp, C.POINTER(C.c_int)],
+    "kle_mat_set_symmetric": [vp, C.c_int],
+    "kle_mat_get_symmetric": [vp, C.POINTER(C.c_int)],
     "kle_get_nb_pad": [],
     "kle_set_nb_layout": [C.c_int],
     "kle_get_nb_layout": [],

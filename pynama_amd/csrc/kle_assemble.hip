@@ -1872,6 +1872,15 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     KLE_HIP(hipStreamSynchronize(ctx->stream));
     tm.lap(nbatch > 1 ? "assemble_kle: element batches + gathers" : "assemble_kle: elements + gathers");
     owned.keep = true;
+    // K is SPD (MatFS.buildFS: free-free blocks + unit Dirichlet diagonal):
+    // one-rank structured K of >= spmv_sym_min_rows rows keeps its upper
+    // triangle only for the SpMV (kle_mat_set_symmetric); a K the symmetric
+    // path cannot take keeps the full-storage kernels
+    if (g_tune.spmv_sym && ctx->nranks == 1 && mK->nrows >= g_tune.spmv_sym_min_rows && mK->R == 3 &&
+        mK->d_rowbox) {
+        if (sym_build(mK)) (void)kle_last_error();
+        tm.lap("assemble_kle: symmetric storage");
+    }
     *K = mK;
     *Krhs = mKr;
     *Rw = mRw;

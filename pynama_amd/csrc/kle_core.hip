@@ -532,6 +532,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_dict_min_rows") {
         KLE_ARG(value >= 0, "spmv_dict_min_rows: >= 0");
         g_tune.spmv_dict_min_rows = value;
+    } else if (k == "spmv_sym") {
+        KLE_ARG(value == 0 || value == 1, "spmv_sym: 0 or 1");
+        g_tune.spmv_sym = value;
+    } else if (k == "spmv_sym_min_rows") {
+        KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
+        g_tune.spmv_sym_min_rows = value;
     } else if (k == "spmv_x_lds") {
         KLE_ARG(value == 0 || value == 1, "spmv_x_lds: 0 or 1");
         g_tune.spmv_x_lds = value;
@@ -558,6 +564,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_dict") *value = g_tune.spmv_dict;
     else if (k == "upd_preload") *value = g_tune.upd_preload;
     else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
+    else if (k == "spmv_sym") *value = g_tune.spmv_sym;
+    else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;
 }

@@ -232,6 +232,14 @@ struct kle_mat {
     uint16_t *d_lid = nullptr;
     int64_t dict_len = 0;
     double *d_val = nullptr;   // [nblocks*R*C], per row SoA [a][b][k]
+    // symmetric storage (kle_mat_set_symmetric = MatSetOption(MAT_SPD), PETSc
+    // SBAIJ; single-rank structured 3x3 rows): each row's blocks from its
+    // diagonal block on, in the chunked layout; per-tile partial sums d_sws
+    double *d_sval = nullptr;
+    int64_t *d_svptr = nullptr;
+    double *d_sws = nullptr;
+    int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries written per SpMV
+    int sym_P = 0;
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
     // export: DoF-level entry rule inside the node blocks (no-slip matrices,
     // MASK_* below) and the ext-range DoF classes it reads
@@ -278,6 +286,8 @@ int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, do
 int grid_for(int64_t work, int per_block, int max_blocks);
 unsigned sync_event_flags();  // kle_core.hip
 int nb_build_dict(kle_mat *A);  // kle_mat.hip
+int sym_build(kle_mat *A);      // kle_mat.hip (symmetric storage)
+void sym_drop(kle_mat *A);
 // Performance knobs (kle_set_tuning): every setting gives correct results;
 // they exist for in-process A/B measurements (tools/cg_ab.py).
 struct Tuning {
@@ -286,6 +296,8 @@ struct Tuning {
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
     int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;
+    int spmv_sym = 1;  // SBAIJ-style symmetric storage for the single-rank KLE K of >= spmv_sym_min_rows rows; 0 off
+    int spmv_sym_min_rows = 64000;
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
 };

@@ -397,6 +397,218 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Symmetric node-block storage (PETSc MATSBAIJ; kle_mat_set_symmetric): on a
+// box lattice a structured row's columns are its box in lexicographic order,
+// so the upper triangle j >= i of row i is the tail [k0, m) of that box from
+// its own (diagonal) block on.  Only those blocks are stored (same 16-block
+// chunk layout, rows 128-B aligned): 31.4 M of config 2's 62.4 M blocks.
+//
+// y = A x as one pass over the stored blocks: block (i, j) adds B x_j to row i
+// and B^T x_i to row j.  A workgroup takes a tile of SYM_TX x SYM_TY rows of
+// one lattice plane z (wave w: lattice line y0 + w, SYM_TX rows in x); every
+// row it touches lies in the tile's region [x0-P, x0+TX+P) x [y0-P, y0+TY+P)
+// x [z, z+P] (P = the largest row-box reach), accumulated in LDS (fp64 LDS
+// adds) and written as the tile's partial sums to a workspace; the gather
+// kernel sums, per row, the partials of the (at most 2 x 2 x (P+1)) tiles whose
+// regions contain it, in a fixed tile order.  HBM: the stored values once
+// (half of the full storage) + the partials written and read once.  The
+// LDS adds of one tile commute in a run-dependent order, so y agrees with the
+// full-storage kernels to rounding (not bitwise).
+constexpr int SYM_TX = 8, SYM_TY = 8;
+struct SymGeo {
+    int Lx, Ly, Lz, P, RX, RY, RZ, ntx, nty;
+};
+
+__device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
+                                        int &by, int &bz, int &bnx, int &bny, int &bnz)
+{
+    const int64_t base = rowbox[2 * i];
+    const int d = rowbox[2 * i + 1];
+    bz = (int)(base / Lxy);
+    const int64_t r = base - (int64_t)bz * Lxy;
+    by = (int)(r / Lx);
+    bx = (int)(r - (int64_t)by * Lx);
+    bnx = d & 255;
+    bny = (d >> 8) & 255;
+    bnz = (d >> 16) & 255;
+}
+
+// Copy each row's upper tail into the symmetric layout and measure
+// max |B_ij - B_ji^T| per row (the stored triangle must describe the matrix).
+__global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly, const int *__restrict__ rowptr,
+                                                   const int *__restrict__ rowcnt, const int *__restrict__ rowbox,
+                                                   const int64_t *__restrict__ vptr, const double *__restrict__ val,
+                                                   const int64_t *__restrict__ svptr, double *__restrict__ sval,
+                                                   double *__restrict__ rowdiff, double *__restrict__ rowmax)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= nrows) return;
+    const int64_t Lxy = (int64_t)Lx * Ly;
+    const int z = (int)(i / Lxy), y = (int)((i - z * Lxy) / Lx), x = (int)(i - z * Lxy - (int64_t)y * Lx);
+    int bx, by, bz, bnx, bny, bnz;
+    sym_box(rowbox, i, Lx, Lxy, bx, by, bz, bnx, bny, bnz);
+    const int m = rowcnt ? rowcnt[i] : rowptr[i + 1] - rowptr[i], mp = rowptr[i + 1] - rowptr[i];
+    const int k0 = (x - bx) + bnx * ((y - by) + bny * (z - bz));
+    const int mu = m - k0;
+    const double *v = val + vptr[i];
+    double *sv = sval + svptr[i];
+    double dmax = 0.0, vmax = 0.0;
+    for (int kk = lane; kk < mu; kk += 64) {
+        const int k = k0 + kk;
+        double b[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            b[t] = v[vofs(1, 9, t, k, m, mp)];
+            sv[vofs(1, 9, t, kk, mu, mu)] = b[t];
+            vmax = fmax(vmax, fabs(b[t]));
+        }
+        if (kk == 0) continue;
+        const int bnxy = bnx * bny;
+        const int kz = k / bnxy, ky = (k - kz * bnxy) / bnx, kx = k - kz * bnxy - ky * bnx;
+        const int64_t j = (bx + kx) + (int64_t)Lx * (by + ky) + Lxy * (bz + kz);
+        int cx, cy, cz, cnx, cny, cnz;
+        sym_box(rowbox, j, Lx, Lxy, cx, cy, cz, cnx, cny, cnz);
+        if (x < cx || x >= cx + cnx || y < cy || y >= cy + cny || z < cz || z >= cz + cnz) {
+            dmax = INFINITY;  // (i, j) stored but (j, i) not in the pattern
+            continue;
+        }
+        const int mj = rowcnt ? rowcnt[j] : rowptr[j + 1] - rowptr[j], mpj = rowptr[j + 1] - rowptr[j];
+        const int kj = (x - cx) + cnx * ((y - cy) + cny * (z - cz));
+        const double *vj = val + vptr[j];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dmax = fmax(dmax, fabs(b[a * 3 + c] - vj[vofs(1, 9, c * 3 + a, kj, mj, mpj)]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
+        vmax = fmax(vmax, __shfl_xor(vmax, o, 64));
+    }
+    if (lane == 0) {
+        rowdiff[i] = dmax;
+        rowmax[i] = vmax;
+    }
+}
+
+template <int TXW>
+__global__ __launch_bounds__(64 * SYM_TY) void k_nb_spmv_sym(SymGeo g, const int *__restrict__ rowbox,
+                                                             const int64_t *__restrict__ svptr,
+                                                             const double *__restrict__ sval,
+                                                             const double *__restrict__ x, double *__restrict__ ws,
+                                                             const int *__restrict__ istate)
+{
+    extern __shared__ double yl[];  // [3][RN]
+    if (istate && istate[I_REASON] != 0) return;
+    const int RN = g.RX * g.RY * g.RZ;
+    const int64_t t = blockIdx.x;
+    const int tix = (int)(t % g.ntx);
+    const int64_t q = t / g.ntx;
+    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty);
+    const int ox = tix * TXW - g.P, oy = tiy * SYM_TY - g.P;
+    for (int k = threadIdx.x; k < 3 * RN; k += 64 * SYM_TY) yl[k] = 0.0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int yy = tiy * SYM_TY + w;
+    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
+    if (yy < g.Ly) {
+        for (int xx = 0; xx < TXW; ++xx) {
+            const int xg = tix * TXW + xx;
+            if (xg >= g.Lx) break;
+            const int64_t i = xg + (int64_t)g.Lx * yy + Lxy * tz;
+            int bx, by, bz, bnx, bny, bnz;
+            sym_box(rowbox, i, g.Lx, Lxy, bx, by, bz, bnx, bny, bnz);
+            const int bnxy = bnx * bny;
+            const int k0 = (xg - bx) + bnx * ((yy - by) + bny * (tz - bz));
+            const int mu = bnxy * bnz - k0;
+            const double *v = sval + svptr[i];
+            const double xi0 = x[3 * i], xi1 = x[3 * i + 1], xi2 = x[3 * i + 2];
+            // region offsets of the box origin
+            const int rx0 = bx - ox, ry0 = by - oy, rz0 = bz - tz;
+            double acc[3] = {0.0, 0.0, 0.0};
+            const int q16 = mu & ~15;
+            for (int kb = 0; kb < mu; kb += 64) {
+                const int kk = kb + lane;
+                double vv[9];
+                if (kb + 64 <= q16) {
+                    const double *p = v + (kk >> 4) * (9 * 16) + (kk & 15);
+#pragma unroll
+                    for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(p + s * 16);
+                } else if (kk < mu) {
+                    const int64_t o0 = vofs(1, 9, 0, kk, mu, mu);
+                    const int64_t st = kk < q16 ? 16 : mu - q16;
+#pragma unroll
+                    for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(v + o0 + s * st);
+                }
+                if (kk < mu) {
+                    const int k = k0 + kk;
+                    const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
+                    const int64_t j = (bx + kx) + (int64_t)g.Lx * (by + ky) + Lxy * (bz + kz);
+                    const double xj0 = x[3 * j], xj1 = x[3 * j + 1], xj2 = x[3 * j + 2];
+                    acc[0] += vv[0] * xj0 + vv[1] * xj1 + vv[2] * xj2;
+                    acc[1] += vv[3] * xj0 + vv[4] * xj1 + vv[5] * xj2;
+                    acc[2] += vv[6] * xj0 + vv[7] * xj1 + vv[8] * xj2;
+                    if (kk > 0) {
+                        const int r = (rx0 + kx) + g.RX * ((ry0 + ky) + g.RY * (rz0 + kz));
+                        atomicAdd(&yl[r], vv[0] * xi0 + vv[3] * xi1 + vv[6] * xi2);
+                        atomicAdd(&yl[RN + r], vv[1] * xi0 + vv[4] * xi1 + vv[7] * xi2);
+                        atomicAdd(&yl[2 * RN + r], vv[2] * xi0 + vv[5] * xi1 + vv[8] * xi2);
+                    }
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a) acc[a] = wsum(acc[a]);
+            if (lane < 3) {
+                const int r = (xg - ox) + g.RX * (yy - oy);
+                atomicAdd(&yl[lane * RN + r], lane == 0 ? acc[0] : lane == 1 ? acc[1] : acc[2]);
+            }
+        }
+    }
+    __syncthreads();
+    // the tile's partial sums: region nodes inside the lattice only
+    double *dst = ws + t * 3 * (int64_t)RN;
+    for (int k = threadIdx.x; k < RN; k += 64 * SYM_TY) {
+        const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
+        const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
+        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) dst[b * RN + k] = yl[b * RN + k];
+    }
+}
+
+// y_j = sum of the partials of the tiles whose regions contain row j, in
+// ascending (z, y, x) tile order.
+template <int TXW>
+__global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *__restrict__ ws, double *__restrict__ y,
+                                                       const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int64_t Lxy = (int64_t)g.Lx * g.Ly, n = Lxy * g.Lz;
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int jz = (int)(j / Lxy), jy = (int)((j - jz * Lxy) / g.Lx), jx = (int)(j - jz * Lxy - (int64_t)jy * g.Lx);
+    const int RN = g.RX * g.RY * g.RZ;
+    // tiles whose [t*T - P, t*T - P + R) contains the coordinate
+    const int x_lo = max(0, (jx + g.P - g.RX + TXW) / TXW), x_hi = min(g.ntx - 1, (jx + g.P) / TXW);
+    const int y_lo = max(0, (jy + g.P - g.RY + SYM_TY) / SYM_TY), y_hi = min(g.nty - 1, (jy + g.P) / SYM_TY);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int tz = max(0, jz - g.P); tz <= jz; ++tz)
+        for (int ty = y_lo; ty <= y_hi; ++ty)
+            for (int tx = x_lo; tx <= x_hi; ++tx) {
+                const int64_t t = ((int64_t)tz * g.nty + ty) * g.ntx + tx;
+                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * SYM_TY - g.P)) + g.RY * (jz - tz));
+                const double *p = ws + t * 3 * (int64_t)RN + r;
+                s0 += p[0];
+                s1 += p[RN];
+                s2 += p[2 * RN];
+            }
+    y[3 * j] = s0;
+    y[3 * j + 1] = s1;
+    y[3 * j + 2] = s2;
+}
+
 // Scalar CSR SpMV (MatMult_SeqAIJ): one wavefront per row.  A pass covers
 // 64*U entries from the row start rounded down to 32 entries, so every col
 // load (32 int32 = 128 B) and every val load (16 doubles = 128 B) covers whole
@@ -611,6 +823,139 @@ int nb_build_dict(kle_mat *A)
     return 0;
 }
 
+void sym_drop(kle_mat *A)
+{
+    if (A->d_sval) (void)hipFree(A->d_sval);
+    if (A->d_svptr) (void)hipFree(A->d_svptr);
+    if (A->d_sws) (void)hipFree(A->d_sws);
+    A->d_sval = nullptr;
+    A->d_svptr = nullptr;
+    A->d_sws = nullptr;
+    A->sblocks = A->snvals = A->sws_entries = 0;
+    A->sym_P = 0;
+}
+
+static SymGeo sym_geo(const kle_mat *A)
+{
+    SymGeo g;
+    g.Lx = (int)A->row_lat[0];
+    g.Ly = (int)A->row_lat[1];
+    g.Lz = (int)A->row_lat[2];
+    g.P = A->sym_P;
+    g.RX = SYM_TX + 2 * g.P;
+    g.RY = SYM_TY + 2 * g.P;
+    g.RZ = g.P + 1;
+    g.ntx = (g.Lx + SYM_TX - 1) / SYM_TX;
+    g.nty = (g.Ly + SYM_TY - 1) / SYM_TY;
+    return g;
+}
+
+// Build the symmetric (upper-triangle) storage of a single-rank structured
+// 3x3 matrix from its full storage; refuses a matrix whose blocks are not
+// symmetric to 1e-12 of its largest entry.
+int sym_build(kle_mat *A)
+{
+    kle_ctx *c = A->ctx;
+    sym_drop(A);
+    if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_rowbox && c->nranks == 1 &&
+          A->ghost_lo == 0 && A->ghost_hi == 0 && A->m_local == A->n_local))
+        return fail(KLE_ERR_SUP, "symmetric storage needs a single-rank 3x3 node-block matrix with box-lattice rows");
+    const int64_t Lx = A->row_lat[0], Ly = A->row_lat[1], Lz = A->row_lat[2], n = A->nrows;
+    if (Lx * Ly * Lz != n || A->box_lx != Lx || A->box_lxy != Lx * Ly || Lx > INT_MAX / 2)
+        return fail(KLE_ERR_SUP, "symmetric storage: the rows are not one box lattice");
+    std::vector<int> rb(2 * n), rp(n + 1), cnt(n);
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    KLE_HIP(hipMemcpy(rb.data(), A->d_rowbox, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
+    if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost));
+    else
+        for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
+    std::vector<int64_t> sv(n + 1);
+    int P = 0;
+    int64_t tot = 0, blocks = 0;
+    const int64_t Lxy = Lx * Ly;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t z = i / Lxy, y = (i - z * Lxy) / Lx, x = i - z * Lxy - y * Lx;
+        const int64_t base = rb[2 * i];
+        const int d = rb[2 * i + 1];
+        const int64_t bz = base / Lxy, by = (base - bz * Lxy) / Lx, bx = base - bz * Lxy - by * Lx;
+        const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
+        if (x < bx || x >= bx + bnx || y < by || y >= by + bny || z < bz || z >= bz + bnz ||
+            cnt[i] != bnx * bny * bnz)
+            return fail(KLE_ERR_SUP, "symmetric storage: row %lld's box does not hold its diagonal", (long long)i);
+        P = std::max<int>(P, (int)std::max({x - bx, bx + bnx - 1 - x, y - by, by + bny - 1 - y, bz + bnz - 1 - z}));
+        const int k0 = (int)((x - bx) + bnx * ((y - by) + (int64_t)bny * (z - bz)));
+        const int64_t mu = cnt[i] - k0;
+        sv[i] = tot;
+        tot += (mu * 9 + 15) & ~int64_t(15);
+        blocks += mu;
+    }
+    sv[n] = tot;
+    if ((int64_t)3 * (SYM_TX + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 > 65536)
+        return fail(KLE_ERR_SUP, "symmetric storage: row boxes reach %d nodes (at most 5 supported)", P);
+    double *rowdiff = nullptr, *rowmax = nullptr;
+    if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
+        hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess) {
+        (void)hipGetLastError();
+        hipFree(rowdiff);
+        hipFree(rowmax);
+        sym_drop(A);
+        return fail(KLE_ERR_MEM, "out of device memory for symmetric storage");
+    }
+    KLE_HIP(hipMemcpy(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_sym_build, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, (int)Lx, (int)Ly,
+                       A->d_rowptr, A->d_rowcnt, A->d_rowbox, A->d_vptr, A->d_val, A->d_svptr, A->d_sval, rowdiff,
+                       rowmax);
+    KLE_HIP(hipGetLastError());
+    std::vector<double> hd(n), hm(n);
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    KLE_HIP(hipMemcpy(hd.data(), rowdiff, sizeof(double) * n, hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(hm.data(), rowmax, sizeof(double) * n, hipMemcpyDeviceToHost));
+    hipFree(rowdiff);
+    hipFree(rowmax);
+    double dmax = 0.0, vmax = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        dmax = std::max(dmax, hd[i]);
+        vmax = std::max(vmax, hm[i]);
+        if (std::isnan(hd[i])) dmax = INFINITY;
+    }
+    if (!(dmax <= 1e-12 * vmax)) {
+        sym_drop(A);
+        return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
+    }
+    A->sym_P = P;
+    const SymGeo g = sym_geo(A);
+    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.Lz, RN = (int64_t)g.RX * g.RY * g.RZ;
+    if (hipMalloc(&A->d_sws, sizeof(double) * 3 * RN * ntiles) != hipSuccess) {
+        (void)hipGetLastError();
+        sym_drop(A);
+        return fail(KLE_ERR_MEM, "out of device memory for the symmetric SpMV workspace");
+    }
+    // lattice entries of every tile region (written by the SpMV, read by the gather)
+    auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
+    int64_t ents = 0;
+    for (int64_t tz = 0; tz < g.Lz; ++tz)
+        for (int ty = 0; ty < g.nty; ++ty)
+            for (int tx = 0; tx < g.ntx; ++tx)
+                ents += span(tx * SYM_TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(tz, g.RZ, Lz);
+    A->sblocks = blocks;
+    A->snvals = tot;
+    A->sws_entries = ents;
+    return 0;
+}
+
+static void launch_sym(const kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, hipStream_t st)
+{
+    const SymGeo g = sym_geo(A);
+    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.Lz, RN = (int64_t)g.RX * g.RY * g.RZ;
+    hipLaunchKernelGGL((k_nb_spmv_sym<SYM_TX>), dim3((unsigned)ntiles), dim3(64 * SYM_TY),
+                       (size_t)(3 * RN * sizeof(double)), st, g, A->d_rowbox, A->d_svptr, A->d_sval, x->base,
+                       A->d_sws, istate);
+    hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
+                       A->d_sws, y->d, istate);
+}
+
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
     return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi &&
@@ -720,7 +1065,10 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
                                   x->send_lo, x->send_hi, nullptr, x->plan.get()));
         KLE_TRY(c->tic("spmv", &ev));
         const int *rbox = A->spmv_struct ? A->d_rowbox : nullptr;
-        if (!overlap) {
+        if (A->d_sval && g_tune.spmv_sym && c->nranks == 1) {
+            launch_sym(A, x, y, istate, c->stream);
+            KLE_HIP(hipGetLastError());
+        } else if (!overlap) {
             KLE_TRY(launch_nb_shape(A, RowMap{0, A->nrows, 0, 0}, rbox, x, y, istate, c->stream));
         } else {
             SideBusy busy(c);  // the halo (and, in pipecg, the reduction) run beside both launches
@@ -918,6 +1266,7 @@ int kle_mat_create_aij_csr(kle_ctx *ctx, int64_t m, int64_t n, const int64_t *in
 int kle_mat_set_values(kle_mat *A, int32_t nr, const int64_t *rows, int32_t nc, const int64_t *cols,
                        const double *v, int addv)
 {
+    if (A) sym_drop(A);
     KLE_ARG(A && rows && cols && v, "null arg");
     if (A->kind != 1) return fail(KLE_ERR_SUP, "setValues on a node-block matrix: assemble with kle_assemble_kle");
     for (int32_t r = 0; r < nr; ++r) {
@@ -952,6 +1301,7 @@ int kle_mat_set_values(kle_mat *A, int32_t nr, const int64_t *rows, int32_t nc, 
 
 int kle_mat_assemble(kle_mat *A)
 {
+    if (A) sym_drop(A);
     KLE_ARG(A, "null mat");
     if (A->kind != 1) return 0;
     if (!A->assembled) {
@@ -995,6 +1345,7 @@ int kle_mat_destroy(kle_mat *A)
     hipFree(A->d_dict);
     hipFree(A->d_lid);
     hipFree(A->d_val);
+    sym_drop(A);
     hipFree(A->d_aptr);
     hipFree(A->d_acol);
     hipFree(A->d_aval);
@@ -1079,6 +1430,7 @@ int kle_mat_mult_add(kle_mat *A, kle_vec *x, kle_vec *y, kle_vec *z)
 int kle_mat_diagonal_scale(kle_mat *A, const kle_vec *L, const kle_vec *Rv)
 {
     KLE_ARG(A, "null mat");
+    sym_drop(A);  // the symmetric copy no longer describes the values
     kle_ctx *c = A->ctx;
     if (L && L->n_local != A->m_local) return fail(KLE_ERR_SIZ, "left scaling vector size mismatch");
     if (A->kind == 0) {
@@ -1279,6 +1631,7 @@ int kle_mat_convert_aij(const kle_mat *A, kle_mat **out)
 int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X)
 {
     KLE_ARG(Y && X, "null arg");
+    sym_drop(Y);
     KLE_ARG(Y->kind == X->kind && Y->m_local == X->m_local && Y->n_local == X->n_local, "layout mismatch");
     kle_ctx *c = Y->ctx;
     if (Y->kind == 0) {
@@ -1389,6 +1742,23 @@ int kle_mat_set_spmv_structured(kle_mat *A, int on)
     return 0;
 }
 
+int kle_mat_set_symmetric(kle_mat *A, int on)
+{
+    KLE_ARG(A, "null matrix");
+    if (!on) {
+        sym_drop(A);
+        return 0;
+    }
+    return sym_build(A);
+}
+
+int kle_mat_get_symmetric(const kle_mat *A, int *on)
+{
+    KLE_ARG(A && on, "null arg");
+    *on = A->d_sval != nullptr;
+    return 0;
+}
+
 int kle_mat_is_structured(const kle_mat *A, int *on)
 {
     KLE_ARG(A && on, "null arg");
@@ -1420,7 +1790,12 @@ int kle_mat_get_format(const kle_mat *A, char *buf, int buflen)
 int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
 {
     KLE_ARG(A && bytes, "null arg");
-    if (A->kind == 0) {
+    if (A->kind == 0 && A->d_sval && g_tune.spmv_sym && A->ctx->nranks == 1) {
+        // symmetric storage: the stored (upper) blocks, per row its value
+        // offset and box, x and y once, the tile partials written and read
+        *bytes = (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 +
+                 (double)A->sws_entries * 48.0;
+    } else if (A->kind == 0) {
         // bytes the SpMV must move: real blocks only (row padding is not counted);
         // the column stream unless the columns are computed from row boxes
         // (dictionary matrices: a 2-byte position per block plus the

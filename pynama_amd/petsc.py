@@ -391,6 +391,32 @@ class Mat:
         call("kle_mat_is_structured", self._h, C.byref(v))
         return bool(v.value)
 
+    class Option:
+        """petsc4py Mat.Option names understood by setOption."""
+        SYMMETRIC = "SYMMETRIC"
+        SPD = "SPD"
+
+    def setOption(self, option, flag):
+        """MatSetOption: SYMMETRIC / SPD switch the SpMV to symmetric (SBAIJ
+        upper-triangle) storage where libkle supports it (single-rank 3x3
+        box-lattice matrices; kle_mat_set_symmetric) and leave other matrices
+        as they are, as PETSc does for options a format ignores."""
+        if option not in (self.Option.SYMMETRIC, self.Option.SPD):
+            raise Error(56, f"Mat option {option!r} not supported")
+        if not flag:
+            call("kle_mat_set_symmetric", self._h, 0)
+            return
+        try:
+            call("kle_mat_set_symmetric", self._h, 1)
+        except Error as e:
+            if e.ierr != 56:
+                raise
+
+    def isSymmetricStorage(self):
+        v = C.c_int()
+        call("kle_mat_get_symmetric", self._h, C.byref(v))
+        return bool(v.value)
+
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))
 

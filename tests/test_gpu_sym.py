@@ -1,0 +1,163 @@
+"""Symmetric (SBAIJ-style upper-triangle) storage of the KLE K
+(kle_mat_set_symmetric / Mat.setOption(SPD)).
+
+The reference solves with the SPD K that MatFS.buildFS assembles
+(mat_fs.py:150-192: free-free element blocks plus a unit Dirichlet diagonal;
+kle_solver.py:33-37).  libkle keeps each row's blocks from its diagonal block
+on and lets every stored block serve row i and, transposed, row j.  The LDS
+accumulation commutes in a run-dependent order, so the tolerances are
+rounding-level, not bitwise:
+  * SpMV vs the full-storage kernel and vs the exported PETSc CSR:
+    <= 1e-14 relative (2-norm), max|diff| <= 1e-13 * max|y|
+  * CG: iterations within 2 of the oracle's Jacobi-CG, solution within 1e-7
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import pynama_amd
+    pynama_amd.load()
+    return pynama_amd
+
+
+def _mat(pa, nelem, ngl):
+    cfg = {"domain": {"ngl": ngl, "box-mesh": {"nelem": nelem, "lower": [0, 0, 0], "upper": [1, 1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    return dom, mat
+
+
+@pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([6, 5, 3], 2),
+                                       ([3, 4, 2], 6), ([1, 1, 1], 4)])
+def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
+    _, mat = _mat(pa, nelem, ngl)
+    K = mat.K
+    assert not K.isSymmetricStorage()  # below spmv_sym_min_rows: full storage
+    x = K.createVecRight()
+    xa = np.random.default_rng(11).uniform(-1, 1, x.getLocalSize())
+    x.setArray(xa)
+    y0 = (K * x).getArray().copy()
+    b0 = K.spmvBytes()
+    K.setOption(K.Option.SPD, True)
+    assert K.isSymmetricStorage()
+    if ngl >= 5 and min(nelem) >= 2:  # (tiny meshes: the tile partials outweigh the halved values)
+        assert K.spmvBytes() < 0.75 * b0
+    ip, ix, d = K.getValuesCSR()
+    yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
+    for _ in range(3):
+        y1 = (K * x).getArray().copy()
+        for ref in (y0, yh):
+            assert np.linalg.norm(y1 - ref) <= 1e-14 * np.linalg.norm(ref)
+            assert np.abs(y1 - ref).max() <= 1e-13 * np.abs(ref).max()
+    K.setOption(K.Option.SPD, False)
+    assert not K.isSymmetricStorage()
+    np.testing.assert_array_equal((K * x).getArray(), y0)
+
+
+def test_symmetric_cg_matches_oracle(pa):
+    """Jacobi-CG on the symmetric storage (single-reduction and pipelined)
+    against the oracle's CG on the exported CSR of the same K."""
+    from pynama_amd import fields
+    dom, mat = _mat(pa, [6, 5, 4], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    assert K.isSymmetricStorage()
+    f = fields.get("taylor_green3d")
+    alpha = f.alpha(0.02, 0.0)
+    sol = pa.KleSolver()
+    sol.setMat(mat)
+    sol.setUp()
+    vort = mat.Rw.createVecRight()
+    vort.setArray(f.vorticity(dom.getFullCoordArray(), alpha))
+    vel = sol.getSolution()
+    dom.applyBoundaryConditions(vel, "velocity", 0.0, 0.02)
+    b = sol.rhs(vort).copy()
+    ip, ix, d = K.getValuesCSR()
+    Ko = O.CSR.from_arrays(ip, ix, d, len(ip) - 1)
+    xo, it_o, _ = Ko.cg(b.getArray(), rtol=1e-10, jacobi=True)
+    for typ, single in (("cg", True), ("cg", False), ("pipecg", True)):
+        ksp = pa.petsc.KSP().create()
+        ksp.setType(typ)
+        pc = pa.petsc.PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+        ksp.setCGSingleReduction(single)
+        ksp.setOperators(K)
+        x = K.createVecRight()
+        ksp.solve(b, x)
+        assert ksp.getConvergedReason() > 0
+        assert abs(ksp.getIterationNumber() - it_o) <= (4 if typ == "pipecg" else 2), (typ, single)
+        assert ksp.getTrueRelativeResidual() <= 1.5e-10
+        assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
+
+
+def test_symmetric_storage_follows_value_changes(pa):
+    """diagonalScale changes the values: the symmetric copy is dropped and the
+    product follows the new values (full storage)."""
+    _, mat = _mat(pa, [4, 3, 3], 5)
+    K = mat.K
+    K.setOption(K.Option.SYMMETRIC, True)
+    assert K.isSymmetricStorage()
+    s = K.createVecLeft()
+    s.setArray(np.random.default_rng(2).uniform(0.5, 2.0, s.getLocalSize()))
+    K.diagonalScale(s, None)
+    assert not K.isSymmetricStorage()
+    x = K.createVecRight()
+    xa = np.random.default_rng(5).uniform(-1, 1, x.getLocalSize())
+    x.setArray(xa)
+    ip, ix, d = K.getValuesCSR()
+    yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
+    y = (K * x).getArray()
+    assert np.abs(y - yh).max() <= 1e-13 * np.abs(yh).max()
+
+
+def test_symmetric_storage_refused_where_it_does_not_apply(pa):
+    """Rw (not symmetric), a 2-D K (2x2 blocks) and a p = 6 K keep the full storage; setOption leaves them as they are,
+    as PETSc ignores options a format does not use."""
+    _, mat = _mat(pa, [3, 3, 2], 4)
+    for A in (mat.Rw,):
+        A.setOption(A.Option.SPD, True)
+        assert not A.isSymmetricStorage()
+    cfg = {"domain": {"ngl": 4, "box-mesh": {"nelem": [5, 4], "lower": [0, 0], "upper": [1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    m2 = pa.MatFS()
+    m2.setDomain(dom)
+    m2.build(buildOperators=False)
+    m2.K.setOption(m2.K.Option.SPD, True)
+    assert not m2.K.isSymmetricStorage()
+    # p = 6 row boxes reach 6 nodes: beyond the tile regions' LDS
+    _, m6 = _mat(pa, [3, 3, 3], 7)
+    m6.K.setOption(m6.K.Option.SPD, True)
+    assert not m6.K.isSymmetricStorage()
+
+
+def test_assembly_turns_symmetric_storage_on_from_the_threshold(pa):
+    from pynama_amd.runtime import get_tuning, set_tuning
+    old = get_tuning("spmv_sym_min_rows")
+    try:
+        set_tuning("spmv_sym_min_rows", 0)
+        _, mat = _mat(pa, [3, 2, 2], 5)
+        assert mat.K.isSymmetricStorage()
+        assert not mat.Rw.isSymmetricStorage()
+        set_tuning("spmv_sym", 0)
+        _, mat = _mat(pa, [3, 2, 2], 5)
+        assert not mat.K.isSymmetricStorage()
+    finally:
+        set_tuning("spmv_sym", 1)
+        set_tuning("spmv_sym_min_rows", old)
