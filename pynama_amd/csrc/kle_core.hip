@@ -535,6 +535,15 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym: 0 or 1");
         g_tune.spmv_sym = value;
+    } else if (k == "spmv_sym_tx") {
+        KLE_ARG(value == 8 || value == 16, "spmv_sym_tx: 8 or 16");
+        g_tune.spmv_sym_tx = value;
+    } else if (k == "spmv_sym_pf") {
+        KLE_ARG(value == 0 || value == 1, "spmv_sym_pf: 0 or 1");
+        g_tune.spmv_sym_pf = value;
+    } else if (k == "spmv_sym_occ") {
+        KLE_ARG(value == 0 || value == 6 || value == 8, "spmv_sym_occ: 0, 6 or 8");
+        g_tune.spmv_sym_occ = value;
     } else if (k == "spmv_sym_min_rows") {
         KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
         g_tune.spmv_sym_min_rows = value;
@@ -565,6 +574,9 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "upd_preload") *value = g_tune.upd_preload;
     else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
     else if (k == "spmv_sym") *value = g_tune.spmv_sym;
+    else if (k == "spmv_sym_tx") *value = g_tune.spmv_sym_tx;
+    else if (k == "spmv_sym_occ") *value = g_tune.spmv_sym_occ;
+    else if (k == "spmv_sym_pf") *value = g_tune.spmv_sym_pf;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

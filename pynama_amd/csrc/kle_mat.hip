@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
 // full-storage kernels to rounding (not bitwise).
 constexpr int SYM_TX = 8, SYM_TY = 8;
 struct SymGeo {
-    int Lx, Ly, Lz, P, RX, RY, RZ, ntx, nty;
+    int Lx, Ly, Lz, P, TX, RX, RY, RZ, ntx, nty;
 };
 
 __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
@@ -493,8 +493,8 @@ __global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly
     }
 }
 
-template <int TXW>
-__global__ __launch_bounds__(64 * SYM_TY) void k_nb_spmv_sym(SymGeo g, const int *__restrict__ rowbox,
+template <int TXW, int OCC>
+__global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym(SymGeo g, const int *__restrict__ rowbox,
                                                              const int64_t *__restrict__ svptr,
                                                              const double *__restrict__ sval,
                                                              const double *__restrict__ x, double *__restrict__ ws,
@@ -568,6 +568,206 @@ __global__ __launch_bounds__(64 * SYM_TY) void k_nb_spmv_sym(SymGeo g, const int
     }
     __syncthreads();
     // the tile's partial sums: region nodes inside the lattice only
+    double *dst = ws + t * 3 * (int64_t)RN;
+    for (int k = threadIdx.x; k < RN; k += 64 * SYM_TY) {
+        const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
+        const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
+        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) dst[b * RN + k] = yl[b * RN + k];
+    }
+}
+
+// Wave sum through DPP row moves (VALU only; __shfl_xor is a ds_bpermute per
+// 32-bit half, i.e. 12 LDS instructions per double): quad swaps, half-row
+// and row mirrors, then row_bcast15 / row_bcast31 carry the row sums into
+// lane 63, which every lane reads back.
+template <int ctrl, int row_mask>
+__device__ __forceinline__ double dpp_step(double v)
+{
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const int l2 = __builtin_amdgcn_update_dpp(0, lo, ctrl, row_mask, 0xF, false);
+    const int h2 = __builtin_amdgcn_update_dpp(0, hi, ctrl, row_mask, 0xF, false);
+    return v + __hiloint2double(h2, l2);
+}
+
+__device__ __forceinline__ double wsum_dpp(double v)
+{
+    v = dpp_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v = dpp_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v = dpp_step<0x141, 0xF>(v);  // row_half_mirror
+    v = dpp_step<0x140, 0xF>(v);  // row_mirror
+    v = dpp_step<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3
+    v = dpp_step<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+    return __hiloint2double(hi, lo);
+}
+
+// Same tile pass with the wave's (row, 64-block pass) items flattened into one
+// software-pipelined loop: the values and x entries of the next item are in
+// flight while the current one is multiplied and accumulated (a wave's rows
+// average 1.4 passes of 64 blocks, so one item at a time leaves it waiting
+// on HBM latency at every row).
+struct SymRow {
+    int64_t i;
+    const double *v;
+    double x0, x1, x2;
+    int bx, by, bz, bnx, bnxy, k0, mu, rx0, ry0, rz0, own;
+    float ibnx, ibnxy;  // 1/bnx, 1/bnxy: quotients of block positions by float multiply + one fix-up
+};
+
+// q = n / d for 0 <= n < 2^20, d >= 1 (block position in its row box)
+__device__ __forceinline__ int sym_div(int n, int d, float inv)
+{
+    int q = (int)((float)n * inv);
+    q += (q + 1) * d <= n;
+    q -= q * d > n;
+    return q;
+}
+
+__device__ __forceinline__ void sym_row(const SymGeo &g, const int *__restrict__ rowbox,
+                                        const int64_t *__restrict__ svptr, const double *__restrict__ sval,
+                                        const double *__restrict__ x, int xg, int yy, int tz, int ox, int oy,
+                                        SymRow &R)
+{
+    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
+    R.i = xg + (int64_t)g.Lx * yy + Lxy * tz;
+    int bny, bnz;
+    sym_box(rowbox, R.i, g.Lx, Lxy, R.bx, R.by, R.bz, R.bnx, bny, bnz);
+    R.bnxy = R.bnx * bny;
+    R.ibnx = 1.0f / (float)R.bnx;
+    R.ibnxy = 1.0f / (float)R.bnxy;
+    R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (tz - R.bz));
+    R.mu = R.bnxy * bnz - R.k0;
+    R.v = sval + svptr[R.i];
+    R.x0 = x[3 * R.i];
+    R.x1 = x[3 * R.i + 1];
+    R.x2 = x[3 * R.i + 2];
+    R.rx0 = R.bx - ox;
+    R.ry0 = R.by - oy;
+    R.rz0 = R.bz - tz;
+    R.own = (xg - ox) + g.RX * (yy - oy);
+}
+
+template <int TXW, int OCC>
+__global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, const int *__restrict__ rowbox,
+                                                                     const int64_t *__restrict__ svptr,
+                                                                     const double *__restrict__ sval,
+                                                                     const double *__restrict__ x,
+                                                                     double *__restrict__ ws,
+                                                                     const int *__restrict__ istate)
+{
+    extern __shared__ double yl[];  // [3][RN]
+    if (istate && istate[I_REASON] != 0) return;
+    const int RN = g.RX * g.RY * g.RZ;
+    const int64_t t = blockIdx.x;
+    const int tix = (int)(t % g.ntx);
+    const int64_t q = t / g.ntx;
+    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty);
+    const int ox = tix * TXW - g.P, oy = tiy * SYM_TY - g.P;
+    for (int k = threadIdx.x; k < 3 * RN; k += 64 * SYM_TY) yl[k] = 0.0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
+    const int nx = min(TXW, g.Lx - tix * TXW);
+    // item = (row, pass kb): values of its 64 blocks and the x entries they multiply
+    auto load = [&](const SymRow &R, int kb, double *vv, double *xv, int &rr) {
+        const int kk = kb + lane;
+        const int q16 = R.mu & ~15;
+        if (kb + 64 <= q16) {
+            const double *p = R.v + (kk >> 4) * (9 * 16) + (kk & 15);
+#pragma unroll
+            for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(p + s * 16);
+        } else if (kk < R.mu) {
+            const int64_t o0 = vofs(1, 9, 0, kk, R.mu, R.mu);
+            const int64_t st = kk < q16 ? 16 : R.mu - q16;
+#pragma unroll
+            for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(R.v + o0 + s * st);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 9; ++s) vv[s] = 0.0;
+        }
+        if (kk < R.mu) {
+            const int k = R.k0 + kk;
+            const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
+            const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
+            const int64_t j = (R.bx + kx) + (int64_t)g.Lx * (R.by + ky) + Lxy * (R.bz + kz);
+            xv[0] = x[3 * j];
+            xv[1] = x[3 * j + 1];
+            xv[2] = x[3 * j + 2];
+            rr = (R.rx0 + kx) + g.RX * ((R.ry0 + ky) + g.RY * (R.rz0 + kz));
+        } else {
+            xv[0] = xv[1] = xv[2] = 0.0;
+            rr = 0;
+        }
+    };
+    // row slots of this wave: slot s is lattice line y0 + s % 8 at x offset
+    // (w + s) % TXW, so every wave takes every line and every x class of the
+    // tile (equal work per wave up to the lattice edges; the workgroup's
+    // barrier waits for its slowest wave)
+    auto slot_ok = [&](int s) {
+        return tiy * SYM_TY + (s & 7) < g.Ly && (w + s) % TXW < nx;
+    };
+    auto next_slot = [&](int s) {
+        while (s < TXW && !slot_ok(s)) ++s;
+        return s;
+    };
+    auto slot_row = [&](int s, SymRow &R) {
+        sym_row(g, rowbox, svptr, sval, x, tix * TXW + (w + s) % TXW, tiy * SYM_TY + (s & 7), tz, ox, oy, R);
+    };
+    int xx = next_slot(0);
+    if (xx < TXW) {
+        SymRow cur, nxt;
+        slot_row(xx, cur);
+        int kb = 0;
+        double vv[9], xv[3], acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        int rr;
+        load(cur, 0, vv, xv, rr);
+        while (true) {
+            int nkb = kb + 64, nxx = xx;
+            bool more = true;
+            if (nkb >= cur.mu) {
+                nkb = 0;
+                nxx = next_slot(xx + 1);
+                more = nxx < TXW;
+                if (more) slot_row(nxx, nxt);
+            } else {
+                nxt = cur;
+            }
+            double vn[9], xn[3];
+            int rn = 0;
+            if (more) load(nxt, nkb, vn, xn, rn);
+            // current item: B x_j into the row, B^T x_i into row j
+            acc0 += vv[0] * xv[0] + vv[1] * xv[1] + vv[2] * xv[2];
+            acc1 += vv[3] * xv[0] + vv[4] * xv[1] + vv[5] * xv[2];
+            acc2 += vv[6] * xv[0] + vv[7] * xv[1] + vv[8] * xv[2];
+            const int kk = kb + lane;
+            if (kk > 0 && kk < cur.mu) {
+                atomicAdd(&yl[rr], vv[0] * cur.x0 + vv[3] * cur.x1 + vv[6] * cur.x2);
+                atomicAdd(&yl[RN + rr], vv[1] * cur.x0 + vv[4] * cur.x1 + vv[7] * cur.x2);
+                atomicAdd(&yl[2 * RN + rr], vv[2] * cur.x0 + vv[5] * cur.x1 + vv[8] * cur.x2);
+            }
+            if (nxx != xx || !more) {
+                acc0 = wsum_dpp(acc0);
+                acc1 = wsum_dpp(acc1);
+                acc2 = wsum_dpp(acc2);
+                if (lane < 3) atomicAdd(&yl[lane * RN + cur.own], lane == 0 ? acc0 : lane == 1 ? acc1 : acc2);
+                acc0 = acc1 = acc2 = 0.0;
+            }
+            if (!more) break;
+            cur = nxt;
+            xx = nxx;
+            kb = nkb;
+#pragma unroll
+            for (int s = 0; s < 9; ++s) vv[s] = vn[s];
+            xv[0] = xn[0];
+            xv[1] = xn[1];
+            xv[2] = xn[2];
+            rr = rn;
+        }
+    }
+    __syncthreads();
     double *dst = ws + t * 3 * (int64_t)RN;
     for (int k = threadIdx.x; k < RN; k += 64 * SYM_TY) {
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
@@ -831,21 +1031,24 @@ void sym_drop(kle_mat *A)
     A->d_sval = nullptr;
     A->d_svptr = nullptr;
     A->d_sws = nullptr;
-    A->sblocks = A->snvals = A->sws_entries = 0;
+    A->sblocks = A->snvals = A->sws_entries[0] = A->sws_entries[1] = 0;
     A->sym_P = 0;
 }
 
-static SymGeo sym_geo(const kle_mat *A)
+static SymGeo sym_geo(const kle_mat *A, int tx = 0)
 {
     SymGeo g;
+    const int P = A->sym_P;
+    const bool fits16 = (int64_t)3 * (16 + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 <= 65536;
+    g.TX = tx ? tx : (g_tune.spmv_sym_tx == 16 && fits16 ? 16 : 8);
     g.Lx = (int)A->row_lat[0];
     g.Ly = (int)A->row_lat[1];
     g.Lz = (int)A->row_lat[2];
     g.P = A->sym_P;
-    g.RX = SYM_TX + 2 * g.P;
+    g.RX = g.TX + 2 * g.P;
     g.RY = SYM_TY + 2 * g.P;
     g.RZ = g.P + 1;
-    g.ntx = (g.Lx + SYM_TX - 1) / SYM_TX;
+    g.ntx = (g.Lx + g.TX - 1) / g.TX;
     g.nty = (g.Ly + SYM_TY - 1) / SYM_TY;
     return g;
 }
@@ -891,7 +1094,7 @@ int sym_build(kle_mat *A)
         blocks += mu;
     }
     sv[n] = tot;
-    if ((int64_t)3 * (SYM_TX + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 > 65536)
+    if ((int64_t)3 * (8 + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 > 65536)
         return fail(KLE_ERR_SUP, "symmetric storage: row boxes reach %d nodes (at most 5 supported)", P);
     double *rowdiff = nullptr, *rowmax = nullptr;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
@@ -925,23 +1128,32 @@ int sym_build(kle_mat *A)
         return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
     }
     A->sym_P = P;
-    const SymGeo g = sym_geo(A);
-    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.Lz, RN = (int64_t)g.RX * g.RY * g.RZ;
-    if (hipMalloc(&A->d_sws, sizeof(double) * 3 * RN * ntiles) != hipSuccess) {
+    // workspace for either tile width (kle_set_tuning "spmv_sym_tx")
+    int64_t wsn = 0;
+    const bool fits16 = (int64_t)3 * (16 + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 <= 65536;
+    for (int tx : {8, 16}) {
+        if (tx == 16 && !fits16) continue;
+        const SymGeo g = sym_geo(A, tx);
+        wsn = std::max(wsn, (int64_t)g.ntx * g.nty * g.Lz * 3 * g.RX * g.RY * g.RZ);
+    }
+    if (hipMalloc(&A->d_sws, sizeof(double) * wsn) != hipSuccess) {
         (void)hipGetLastError();
         sym_drop(A);
         return fail(KLE_ERR_MEM, "out of device memory for the symmetric SpMV workspace");
     }
     // lattice entries of every tile region (written by the SpMV, read by the gather)
     auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
-    int64_t ents = 0;
-    for (int64_t tz = 0; tz < g.Lz; ++tz)
-        for (int ty = 0; ty < g.nty; ++ty)
-            for (int tx = 0; tx < g.ntx; ++tx)
-                ents += span(tx * SYM_TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(tz, g.RZ, Lz);
+    for (int w = 0; w < (fits16 ? 2 : 1); ++w) {
+        const SymGeo g = sym_geo(A, w ? 16 : 8);
+        int64_t ents = 0;
+        for (int64_t tz = 0; tz < g.Lz; ++tz)
+            for (int ty = 0; ty < g.nty; ++ty)
+                for (int tx = 0; tx < g.ntx; ++tx)
+                    ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(tz, g.RZ, Lz);
+        A->sws_entries[w] = ents;
+    }
     A->sblocks = blocks;
     A->snvals = tot;
-    A->sws_entries = ents;
     return 0;
 }
 
@@ -949,11 +1161,31 @@ static void launch_sym(const kle_mat *A, const kle_vec *x, kle_vec *y, const int
 {
     const SymGeo g = sym_geo(A);
     const int64_t ntiles = (int64_t)g.ntx * g.nty * g.Lz, RN = (int64_t)g.RX * g.RY * g.RZ;
-    hipLaunchKernelGGL((k_nb_spmv_sym<SYM_TX>), dim3((unsigned)ntiles), dim3(64 * SYM_TY),
-                       (size_t)(3 * RN * sizeof(double)), st, g, A->d_rowbox, A->d_svptr, A->d_sval, x->base,
-                       A->d_sws, istate);
-    hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
-                       A->d_sws, y->d, istate);
+    const size_t lds = (size_t)(3 * RN * sizeof(double));
+    const dim3 grid((unsigned)ntiles), blk(64 * SYM_TY);
+#define SYM_LAUNCH(TXW, OCC)                                                                                   \
+    do {                                                                                                       \
+        if (g_tune.spmv_sym_pf)                                                                                \
+            hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, OCC>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,   \
+                               A->d_sval, x->base, A->d_sws, istate);                                          \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_nb_spmv_sym<TXW, OCC>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,      \
+                               A->d_sval, x->base, A->d_sws, istate);                                          \
+    } while (0)
+    if (g.TX == 16) {
+        if (g_tune.spmv_sym_occ == 8) SYM_LAUNCH(16, 8);
+        else if (g_tune.spmv_sym_occ == 6) SYM_LAUNCH(16, 6);
+        else SYM_LAUNCH(16, 1);
+        hipLaunchKernelGGL((k_nb_sym_gather<16>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
+                           A->d_sws, y->d, istate);
+    } else {
+        if (g_tune.spmv_sym_occ == 8) SYM_LAUNCH(8, 8);
+        else if (g_tune.spmv_sym_occ == 6) SYM_LAUNCH(8, 6);
+        else SYM_LAUNCH(8, 1);
+        hipLaunchKernelGGL((k_nb_sym_gather<8>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
+                           A->d_sws, y->d, istate);
+    }
+#undef SYM_LAUNCH
 }
 
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
@@ -1794,7 +2026,7 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
         // symmetric storage: the stored (upper) blocks, per row its value
         // offset and box, x and y once, the tile partials written and read
         *bytes = (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 +
-                 (double)A->sws_entries * 48.0;
+                 (double)A->sws_entries[sym_geo(A).TX == 16] * 48.0;
     } else if (A->kind == 0) {
         // bytes the SpMV must move: real blocks only (row padding is not counted);
         // the column stream unless the columns are computed from row boxes
