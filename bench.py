@@ -382,7 +382,8 @@ def main():
             key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
                    ("chunk" if args.layout == 1 else f"pad{args.pad}") +
                    "-nt-u1" + ("-struct" if K.isStructured() else "") +
-                   {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(spmv_kernel(K, args.layout, args.ngl), ""))
+                   ("-sym" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_sym") else
+                    {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(spmv_kernel(K, args.layout, args.ngl), "")))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -425,6 +426,7 @@ def main():
                        ("cg" if args.classic_cg else "cg (single reduction, Chronopoulos-Gear)"),
                        "pc": "jacobi", "matrix_format": info["format"], "value_layout": "chunk16+tail" if args.layout == 1 else f"row streams padded to {args.pad}",
                        "structured_columns": K.isStructured(),
+                       "symmetric_storage": K.isSymmetricStorage(),
                        "parallelism": ((f"z-slab x{nranks}" if mesh_kind == "box" else
                                         f"cell slabs along the most-layered axis x{nranks}") +
                                        ("" if nranks == 1 else
@@ -473,6 +475,10 @@ def spmv_kernel(K, layout, ngl):
     dictionaries); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
     "spmv_waves" / "spmv_x_lds" override)."""
     from pynama_amd.runtime import get_tuning
+    if K.isSymmetricStorage() and get_tuning("spmv_sym"):
+        tx = 16 if get_tuning("spmv_sym_tx") == 16 else 8
+        return (f"k_nb_spmv_sym_pf<{tx},1>+k_nb_sym_gather<{tx}>" if get_tuning("spmv_sym_pf") else
+                f"k_nb_spmv_sym<{tx},1>+k_nb_sym_gather<{tx}>")
     wv = get_tuning("spmv_waves")
     lo, hi = K.getOwnershipRange()
     if layout != 1:

@@ -650,6 +650,13 @@ __device__ __forceinline__ void sym_row(const SymGeo &g, const int *__restrict__
     R.own = (xg - ox) + g.RX * (yy - oy);
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
 template <int TXW, int OCC>
 __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, const int *__restrict__ rowbox,
                                                                      const int64_t *__restrict__ svptr,
@@ -672,35 +679,26 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     const int nx = min(TXW, g.Lx - tix * TXW);
     // item = (row, pass kb): values of its 64 blocks and the x entries they multiply
+    // Branch-free: every lane loads (lanes past the row's end re-read its
+    // last block and are masked when summed), so each item is exactly 12
+    // loads and the wait for the current item leaves the next item's 12 in
+    // flight (conditional loads make the compiler drain the queue).
     auto load = [&](const SymRow &R, int kb, double *vv, double *xv, int &rr) {
-        const int kk = kb + lane;
+        const int kk = min(kb + lane, R.mu - 1);
         const int q16 = R.mu & ~15;
-        if (kb + 64 <= q16) {
-            const double *p = R.v + (kk >> 4) * (9 * 16) + (kk & 15);
+        const bool ch = kk < q16;
+        const int64_t o0 = ch ? (int64_t)((kk >> 4) * 144 + (kk & 15)) : (int64_t)q16 * 9 + (kk - q16);
+        const int st = ch ? 16 : R.mu - q16;
 #pragma unroll
-            for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(p + s * 16);
-        } else if (kk < R.mu) {
-            const int64_t o0 = vofs(1, 9, 0, kk, R.mu, R.mu);
-            const int64_t st = kk < q16 ? 16 : R.mu - q16;
-#pragma unroll
-            for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(R.v + o0 + s * st);
-        } else {
-#pragma unroll
-            for (int s = 0; s < 9; ++s) vv[s] = 0.0;
-        }
-        if (kk < R.mu) {
-            const int k = R.k0 + kk;
-            const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
-            const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
-            const int64_t j = (R.bx + kx) + (int64_t)g.Lx * (R.by + ky) + Lxy * (R.bz + kz);
-            xv[0] = x[3 * j];
-            xv[1] = x[3 * j + 1];
-            xv[2] = x[3 * j + 2];
-            rr = (R.rx0 + kx) + g.RX * ((R.ry0 + ky) + g.RY * (R.rz0 + kz));
-        } else {
-            xv[0] = xv[1] = xv[2] = 0.0;
-            rr = 0;
-        }
+        for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(R.v + o0 + s * st);
+        const int k = R.k0 + kk;
+        const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
+        const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
+        const int64_t j = (R.bx + kx) + (int64_t)g.Lx * (R.by + ky) + Lxy * (R.bz + kz);
+        xv[0] = x[3 * j];
+        xv[1] = x[3 * j + 1];
+        xv[2] = x[3 * j + 2];
+        rr = (R.rx0 + kx) + g.RX * ((R.ry0 + ky) + g.RY * (R.rz0 + kz));
     };
     // row slots of this wave: slot s is lattice line y0 + s % 8 at x offset
     // (w + s) % TXW, so every wave takes every line and every x class of the
@@ -713,18 +711,61 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
         while (s < TXW && !slot_ok(s)) ++s;
         return s;
     };
+    // the wave's row descriptors (box, value offset, x_i) are loaded once, lane
+    // s holding slot s, and read back with readlane when the slot starts: no
+    // dependent scalar-memory round trip at every row
+    int pb = 0, pd = 0, psl = 0, psh = 0;
+    double px0 = 0.0, px1 = 0.0, px2 = 0.0;
+    if (lane < TXW && slot_ok(lane)) {
+        const int64_t i = tix * TXW + (w + lane) % TXW + (int64_t)g.Lx * (tiy * SYM_TY + (lane & 7)) + Lxy * tz;
+        pb = rowbox[2 * i];
+        pd = rowbox[2 * i + 1];
+        const int64_t o = svptr[i];
+        psl = (int)(uint32_t)o;
+        psh = (int)(o >> 32);
+        px0 = x[3 * i];
+        px1 = x[3 * i + 1];
+        px2 = x[3 * i + 2];
+    }
     auto slot_row = [&](int s, SymRow &R) {
-        sym_row(g, rowbox, svptr, sval, x, tix * TXW + (w + s) % TXW, tiy * SYM_TY + (s & 7), tz, ox, oy, R);
+        const int xg = tix * TXW + (w + s) % TXW, yy = tiy * SYM_TY + (s & 7);
+        R.i = xg + (int64_t)g.Lx * yy + Lxy * tz;
+        const int64_t base = __builtin_amdgcn_readlane(pb, s);
+        const int d = __builtin_amdgcn_readlane(pd, s);
+        R.bz = (int)(base / Lxy);
+        const int64_t rem = base - (int64_t)R.bz * Lxy;
+        R.by = (int)(rem / g.Lx);
+        R.bx = (int)(rem - (int64_t)R.by * g.Lx);
+        R.bnx = d & 255;
+        const int bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
+        R.bnxy = R.bnx * bny;
+        R.ibnx = 1.0f / (float)R.bnx;
+        R.ibnxy = 1.0f / (float)R.bnxy;
+        R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (tz - R.bz));
+        R.mu = R.bnxy * bnz - R.k0;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(psl, s);
+        const int64_t hi = __builtin_amdgcn_readlane(psh, s);
+        R.v = sval + ((hi << 32) | lo);
+        R.x0 = readlane_d(px0, s);
+        R.x1 = readlane_d(px1, s);
+        R.x2 = readlane_d(px2, s);
+        R.rx0 = R.bx - ox;
+        R.ry0 = R.by - oy;
+        R.rz0 = R.bz - tz;
+        R.own = (xg - ox) + g.RX * (yy - oy);
     };
     int xx = next_slot(0);
     if (xx < TXW) {
         SymRow cur, nxt;
         slot_row(xx, cur);
         int kb = 0;
-        double vv[9], xv[3], acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-        int rr;
-        load(cur, 0, vv, xv, rr);
-        while (true) {
+        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        // two register sets used in turn (a copy of in-flight registers would
+        // make the compiler wait for the loads at every item)
+        double va[9], xa[3], vb[9], xb[3];
+        int ra, rb;
+        load(cur, 0, va, xa, ra);
+        auto step = [&](const double *vv, const double *xv, const int rr, double *vn, double *xn, int &rn) {
             int nkb = kb + 64, nxx = xx;
             bool more = true;
             if (nkb >= cur.mu) {
@@ -735,14 +776,18 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
             } else {
                 nxt = cur;
             }
-            double vn[9], xn[3];
-            int rn = 0;
-            if (more) load(nxt, nkb, vn, xn, rn);
+            if (!more) {  // no next item: re-read the current one (cache hits) to keep the loads unconditional
+                nxt = cur;
+                nkb = kb;
+            }
+            load(nxt, nkb, vn, xn, rn);
             // current item: B x_j into the row, B^T x_i into row j
-            acc0 += vv[0] * xv[0] + vv[1] * xv[1] + vv[2] * xv[2];
-            acc1 += vv[3] * xv[0] + vv[4] * xv[1] + vv[5] * xv[2];
-            acc2 += vv[6] * xv[0] + vv[7] * xv[1] + vv[8] * xv[2];
             const int kk = kb + lane;
+            if (kk < cur.mu) {
+                acc0 += vv[0] * xv[0] + vv[1] * xv[1] + vv[2] * xv[2];
+                acc1 += vv[3] * xv[0] + vv[4] * xv[1] + vv[5] * xv[2];
+                acc2 += vv[6] * xv[0] + vv[7] * xv[1] + vv[8] * xv[2];
+            }
             if (kk > 0 && kk < cur.mu) {
                 atomicAdd(&yl[rr], vv[0] * cur.x0 + vv[3] * cur.x1 + vv[6] * cur.x2);
                 atomicAdd(&yl[RN + rr], vv[1] * cur.x0 + vv[4] * cur.x1 + vv[7] * cur.x2);
@@ -755,16 +800,13 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
                 if (lane < 3) atomicAdd(&yl[lane * RN + cur.own], lane == 0 ? acc0 : lane == 1 ? acc1 : acc2);
                 acc0 = acc1 = acc2 = 0.0;
             }
-            if (!more) break;
+            if (!more) return false;
             cur = nxt;
             xx = nxx;
             kb = nkb;
-#pragma unroll
-            for (int s = 0; s < 9; ++s) vv[s] = vn[s];
-            xv[0] = xn[0];
-            xv[1] = xn[1];
-            xv[2] = xn[2];
-            rr = rn;
+            return true;
+        };
+        while (step(va, xa, ra, vb, xb, rb) && step(vb, xb, rb, va, xa, ra)) {
         }
     }
     __syncthreads();
