@@ -477,8 +477,10 @@ def spmv_kernel(K, layout, ngl):
     from pynama_amd.runtime import get_tuning
     if K.isSymmetricStorage() and get_tuning("spmv_sym"):
         tx = 16 if get_tuning("spmv_sym_tx") == 16 else 8
-        return (f"k_nb_spmv_sym_pf<{tx},1>+k_nb_sym_gather<{tx}>" if get_tuning("spmv_sym_pf") else
-                f"k_nb_spmv_sym<{tx},1>+k_nb_sym_gather<{tx}>")
+        if not get_tuning("spmv_sym_pf"):
+            return f"k_nb_spmv_sym<{tx},1>+k_nb_sym_gather<{tx},1>"
+        tz, wv = get_tuning("spmv_sym_tz"), get_tuning("spmv_sym_waves")
+        return f"k_nb_spmv_sym_pf<{tx},{tz},{wv}>+k_nb_sym_gather<{tx},{tz}>"
     wv = get_tuning("spmv_waves")
     lo, hi = K.getOwnershipRange()
     if layout != 1:

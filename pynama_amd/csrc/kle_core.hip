@@ -538,6 +538,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tx") {
         KLE_ARG(value == 8 || value == 16, "spmv_sym_tx: 8 or 16");
         g_tune.spmv_sym_tx = value;
+    } else if (k == "spmv_sym_tz") {
+        KLE_ARG(value == 1 || value == 2, "spmv_sym_tz: 1 or 2");
+        g_tune.spmv_sym_tz = value;
+    } else if (k == "spmv_sym_waves") {
+        KLE_ARG(value == 4 || value == 8, "spmv_sym_waves: 4 or 8");
+        g_tune.spmv_sym_waves = value;
     } else if (k == "spmv_sym_pf") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_pf: 0 or 1");
         g_tune.spmv_sym_pf = value;
@@ -577,6 +583,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_tx") *value = g_tune.spmv_sym_tx;
     else if (k == "spmv_sym_occ") *value = g_tune.spmv_sym_occ;
     else if (k == "spmv_sym_pf") *value = g_tune.spmv_sym_pf;
+    else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
+    else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

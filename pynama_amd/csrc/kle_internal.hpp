@@ -238,7 +238,7 @@ struct kle_mat {
     double *d_sval = nullptr;
     int64_t *d_svptr = nullptr;
     double *d_sws = nullptr;
-    int64_t sblocks = 0, snvals = 0, sws_entries[2] = {0, 0};  // lattice entries written per SpMV (tile width 8, 16)
+    int64_t sblocks = 0, snvals = 0, sws_entries[4] = {0, 0, 0, 0};  // lattice entries written per SpMV ([tz 2][tx 16])
     int sym_P = 0;
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
     // export: DoF-level entry rule inside the node blocks (no-slip matrices,
@@ -300,7 +300,9 @@ struct Tuning {
     int spmv_sym_min_rows = 64000;
     int spmv_sym_tx = 8;    // rows per wave (tile width along x) of the symmetric SpMV: 8 or 16
     int spmv_sym_pf = 1;    // symmetric SpMV: next (row, pass) item's loads in flight while the current one is summed
-    int spmv_sym_occ = 0;   // 8: cap the symmetric SpMV at 64 VGPRs (8 waves per SIMD); 0: compiler's choice
+    int spmv_sym_occ = 0;
+    int spmv_sym_tz = 2;    // (2-plane tiles: 12 instead of 20 partials per row)
+    int spmv_sym_waves = 8; // waves per workgroup of the pipelined symmetric SpMV: 8 or 4 (same tile)    // lattice planes per tile of the pipelined symmetric SpMV: 1 or 2   // 8: cap the symmetric SpMV at 64 VGPRs (8 waves per SIMD); 0: compiler's choice
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
 };

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
 // full-storage kernels to rounding (not bitwise).
 constexpr int SYM_TX = 8, SYM_TY = 8;
 struct SymGeo {
-    int Lx, Ly, Lz, P, TX, RX, RY, RZ, ntx, nty;
+    int Lx, Ly, Lz, P, TX, TZ, RX, RY, RZ, ntx, nty, ntz;
 };
 
 __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
@@ -657,8 +657,8 @@ __device__ __forceinline__ double readlane_d(double v, int l)
     return __hiloint2double(hi, lo);
 }
 
-template <int TXW, int OCC>
-__global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, const int *__restrict__ rowbox,
+template <int TXW, int TZ, int WV>
+__global__ __launch_bounds__(64 * WV) void k_nb_spmv_sym_pf(SymGeo g, const int *__restrict__ rowbox,
                                                                      const int64_t *__restrict__ svptr,
                                                                      const double *__restrict__ sval,
                                                                      const double *__restrict__ x,
@@ -671,13 +671,15 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
     const int64_t t = blockIdx.x;
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
-    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty);
+    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;  // first plane of the tile
     const int ox = tix * TXW - g.P, oy = tiy * SYM_TY - g.P;
-    for (int k = threadIdx.x; k < 3 * RN; k += 64 * SYM_TY) yl[k] = 0.0;
+    for (int k = threadIdx.x; k < 3 * RN; k += 64 * WV) yl[k] = 0.0;
     __syncthreads();
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     const int nx = min(TXW, g.Lx - tix * TXW);
+    constexpr int NQ = TXW * SYM_TY / WV;  // row slots per wave and plane
+    constexpr int NS = NQ * TZ;           // row slots per wave
     // item = (row, pass kb): values of its 64 blocks and the x entries they multiply
     // Branch-free: every lane loads (lanes past the row's end re-read its
     // last block and are masked when summed), so each item is exactly 12
@@ -700,15 +702,17 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
         xv[2] = x[3 * j + 2];
         rr = (R.rx0 + kx) + g.RX * ((R.ry0 + ky) + g.RY * (R.rz0 + kz));
     };
-    // row slots of this wave: slot s is lattice line y0 + s % 8 at x offset
-    // (w + s) % TXW, so every wave takes every line and every x class of the
-    // tile (equal work per wave up to the lattice edges; the workgroup's
-    // barrier waits for its slowest wave)
+    // row slots of this wave: slot s = (plane, q) is plane z0 + s / NQ,
+    // lattice line y0 + q % 8, x offset (w + WV (q / 8) + q % 8) % TXW, so
+    // every wave takes every plane, line and x class of the tile (equal work
+    // per wave up to the lattice edges; the workgroup's barrier waits for its
+    // slowest wave)
+    auto slot_x = [&](int s) { return (w + WV * ((s % NQ) >> 3) + (s & 7)) % TXW; };
     auto slot_ok = [&](int s) {
-        return tiy * SYM_TY + (s & 7) < g.Ly && (w + s) % TXW < nx;
+        return tiy * SYM_TY + (s & 7) < g.Ly && slot_x(s) < nx && tz + s / NQ < g.Lz;
     };
     auto next_slot = [&](int s) {
-        while (s < TXW && !slot_ok(s)) ++s;
+        while (s < NS && !slot_ok(s)) ++s;
         return s;
     };
     // the wave's row descriptors (box, value offset, x_i) are loaded once, lane
@@ -716,8 +720,9 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
     // dependent scalar-memory round trip at every row
     int pb = 0, pd = 0, psl = 0, psh = 0;
     double px0 = 0.0, px1 = 0.0, px2 = 0.0;
-    if (lane < TXW && slot_ok(lane)) {
-        const int64_t i = tix * TXW + (w + lane) % TXW + (int64_t)g.Lx * (tiy * SYM_TY + (lane & 7)) + Lxy * tz;
+    if (lane < NS && slot_ok(lane)) {
+        const int64_t i = tix * TXW + slot_x(lane) + (int64_t)g.Lx * (tiy * SYM_TY + (lane & 7)) +
+                          Lxy * (tz + lane / NQ);
         pb = rowbox[2 * i];
         pd = rowbox[2 * i + 1];
         const int64_t o = svptr[i];
@@ -728,8 +733,8 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
         px2 = x[3 * i + 2];
     }
     auto slot_row = [&](int s, SymRow &R) {
-        const int xg = tix * TXW + (w + s) % TXW, yy = tiy * SYM_TY + (s & 7);
-        R.i = xg + (int64_t)g.Lx * yy + Lxy * tz;
+        const int xg = tix * TXW + slot_x(s), yy = tiy * SYM_TY + (s & 7), zz = tz + s / NQ;
+        R.i = xg + (int64_t)g.Lx * yy + Lxy * zz;
         const int64_t base = __builtin_amdgcn_readlane(pb, s);
         const int d = __builtin_amdgcn_readlane(pd, s);
         R.bz = (int)(base / Lxy);
@@ -741,7 +746,7 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
         R.bnxy = R.bnx * bny;
         R.ibnx = 1.0f / (float)R.bnx;
         R.ibnxy = 1.0f / (float)R.bnxy;
-        R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (tz - R.bz));
+        R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (zz - R.bz));
         R.mu = R.bnxy * bnz - R.k0;
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(psl, s);
         const int64_t hi = __builtin_amdgcn_readlane(psh, s);
@@ -752,10 +757,10 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
         R.rx0 = R.bx - ox;
         R.ry0 = R.by - oy;
         R.rz0 = R.bz - tz;
-        R.own = (xg - ox) + g.RX * (yy - oy);
+        R.own = (xg - ox) + g.RX * ((yy - oy) + g.RY * (zz - tz));
     };
     int xx = next_slot(0);
-    if (xx < TXW) {
+    if (xx < NS) {
         SymRow cur, nxt;
         slot_row(xx, cur);
         int kb = 0;
@@ -771,7 +776,7 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
             if (nkb >= cur.mu) {
                 nkb = 0;
                 nxx = next_slot(xx + 1);
-                more = nxx < TXW;
+                more = nxx < NS;
                 if (more) slot_row(nxx, nxt);
             } else {
                 nxt = cur;
@@ -811,7 +816,7 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
     }
     __syncthreads();
     double *dst = ws + t * 3 * (int64_t)RN;
-    for (int k = threadIdx.x; k < RN; k += 64 * SYM_TY) {
+    for (int k = threadIdx.x; k < RN; k += 64 * WV) {
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
         const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
         if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
@@ -822,7 +827,7 @@ __global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym_pf(SymGeo g, c
 
 // y_j = sum of the partials of the tiles whose regions contain row j, in
 // ascending (z, y, x) tile order.
-template <int TXW>
+template <int TXW, int TZ>
 __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *__restrict__ ws, double *__restrict__ y,
                                                        const int *__restrict__ istate)
 {
@@ -835,12 +840,13 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     // tiles whose [t*T - P, t*T - P + R) contains the coordinate
     const int x_lo = max(0, (jx + g.P - g.RX + TXW) / TXW), x_hi = min(g.ntx - 1, (jx + g.P) / TXW);
     const int y_lo = max(0, (jy + g.P - g.RY + SYM_TY) / SYM_TY), y_hi = min(g.nty - 1, (jy + g.P) / SYM_TY);
+    const int z_lo = max(0, (jz - g.RZ + TZ) / TZ), z_hi = min(g.ntz - 1, jz / TZ);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int tz = max(0, jz - g.P); tz <= jz; ++tz)
+    for (int tzi = z_lo; tzi <= z_hi; ++tzi)
         for (int ty = y_lo; ty <= y_hi; ++ty)
             for (int tx = x_lo; tx <= x_hi; ++tx) {
-                const int64_t t = ((int64_t)tz * g.nty + ty) * g.ntx + tx;
-                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * SYM_TY - g.P)) + g.RY * (jz - tz));
+                const int64_t t = ((int64_t)tzi * g.nty + ty) * g.ntx + tx;
+                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * SYM_TY - g.P)) + g.RY * (jz - tzi * TZ));
                 const double *p = ws + t * 3 * (int64_t)RN + r;
                 s0 += p[0];
                 s1 += p[RN];
@@ -1073,25 +1079,34 @@ void sym_drop(kle_mat *A)
     A->d_sval = nullptr;
     A->d_svptr = nullptr;
     A->d_sws = nullptr;
-    A->sblocks = A->snvals = A->sws_entries[0] = A->sws_entries[1] = 0;
+    A->sblocks = A->snvals = 0;
+    for (auto &e : A->sws_entries) e = 0;
     A->sym_P = 0;
 }
 
-static SymGeo sym_geo(const kle_mat *A, int tx = 0)
+static bool sym_fits(int tx, int tz, int P)
+{
+    return (int64_t)3 * (tx + 2 * P) * (SYM_TY + 2 * P) * (tz + P) * 8 <= 65536;
+}
+
+// Tile geometry: tx x 8 rows of tz planes (kle_set_tuning "spmv_sym_tx",
+// "spmv_sym_tz"; the first kernel version, spmv_sym_pf 0, takes one plane)
+static SymGeo sym_geo(const kle_mat *A, int tx = 0, int tz = 0)
 {
     SymGeo g;
     const int P = A->sym_P;
-    const bool fits16 = (int64_t)3 * (16 + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 <= 65536;
-    g.TX = tx ? tx : (g_tune.spmv_sym_tx == 16 && fits16 ? 16 : 8);
+    g.TX = tx ? tx : (g_tune.spmv_sym_tx == 16 && sym_fits(16, 1, P) ? 16 : 8);
+    g.TZ = tz ? tz : (g_tune.spmv_sym_pf && g_tune.spmv_sym_tz == 2 && sym_fits(g.TX, 2, P) ? 2 : 1);
     g.Lx = (int)A->row_lat[0];
     g.Ly = (int)A->row_lat[1];
     g.Lz = (int)A->row_lat[2];
-    g.P = A->sym_P;
-    g.RX = g.TX + 2 * g.P;
-    g.RY = SYM_TY + 2 * g.P;
-    g.RZ = g.P + 1;
+    g.P = P;
+    g.RX = g.TX + 2 * P;
+    g.RY = SYM_TY + 2 * P;
+    g.RZ = g.TZ + P;
     g.ntx = (g.Lx + g.TX - 1) / g.TX;
     g.nty = (g.Ly + SYM_TY - 1) / SYM_TY;
+    g.ntz = (g.Lz + g.TZ - 1) / g.TZ;
     return g;
 }
 
@@ -1136,7 +1151,7 @@ int sym_build(kle_mat *A)
         blocks += mu;
     }
     sv[n] = tot;
-    if ((int64_t)3 * (8 + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 > 65536)
+    if (!sym_fits(8, 1, P))
         return fail(KLE_ERR_SUP, "symmetric storage: row boxes reach %d nodes (at most 5 supported)", P);
     double *rowdiff = nullptr, *rowmax = nullptr;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
@@ -1170,29 +1185,27 @@ int sym_build(kle_mat *A)
         return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
     }
     A->sym_P = P;
-    // workspace for either tile width (kle_set_tuning "spmv_sym_tx")
+    // workspace for every tile shape (kle_set_tuning "spmv_sym_tx" / "spmv_sym_tz")
+    auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
     int64_t wsn = 0;
-    const bool fits16 = (int64_t)3 * (16 + 2 * P) * (SYM_TY + 2 * P) * (P + 1) * 8 <= 65536;
-    for (int tx : {8, 16}) {
-        if (tx == 16 && !fits16) continue;
-        const SymGeo g = sym_geo(A, tx);
-        wsn = std::max(wsn, (int64_t)g.ntx * g.nty * g.Lz * 3 * g.RX * g.RY * g.RZ);
+    for (int w = 0; w < 4; ++w) {
+        const int tx = w & 1 ? 16 : 8, tz = w & 2 ? 2 : 1;
+        A->sws_entries[w] = 0;
+        if (!sym_fits(tx, tz, P)) continue;
+        const SymGeo g = sym_geo(A, tx, tz);
+        wsn = std::max(wsn, (int64_t)g.ntx * g.nty * g.ntz * 3 * g.RX * g.RY * g.RZ);
+        // lattice entries of every tile region (written by the SpMV, read by the gather)
+        int64_t ents = 0;
+        for (int64_t t = 0; t < g.ntz; ++t)
+            for (int ty = 0; ty < g.nty; ++ty)
+                for (int tx2 = 0; tx2 < g.ntx; ++tx2)
+                    ents += span(tx2 * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz);
+        A->sws_entries[w] = ents;
     }
     if (hipMalloc(&A->d_sws, sizeof(double) * wsn) != hipSuccess) {
         (void)hipGetLastError();
         sym_drop(A);
         return fail(KLE_ERR_MEM, "out of device memory for the symmetric SpMV workspace");
-    }
-    // lattice entries of every tile region (written by the SpMV, read by the gather)
-    auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
-    for (int w = 0; w < (fits16 ? 2 : 1); ++w) {
-        const SymGeo g = sym_geo(A, w ? 16 : 8);
-        int64_t ents = 0;
-        for (int64_t tz = 0; tz < g.Lz; ++tz)
-            for (int ty = 0; ty < g.nty; ++ty)
-                for (int tx = 0; tx < g.ntx; ++tx)
-                    ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(tz, g.RZ, Lz);
-        A->sws_entries[w] = ents;
     }
     A->sblocks = blocks;
     A->snvals = tot;
@@ -1202,30 +1215,28 @@ int sym_build(kle_mat *A)
 static void launch_sym(const kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, hipStream_t st)
 {
     const SymGeo g = sym_geo(A);
-    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.Lz, RN = (int64_t)g.RX * g.RY * g.RZ;
+    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz, RN = (int64_t)g.RX * g.RY * g.RZ;
     const size_t lds = (size_t)(3 * RN * sizeof(double));
-    const dim3 grid((unsigned)ntiles), blk(64 * SYM_TY);
-#define SYM_LAUNCH(TXW, OCC)                                                                                   \
-    do {                                                                                                       \
-        if (g_tune.spmv_sym_pf)                                                                                \
-            hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, OCC>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,   \
-                               A->d_sval, x->base, A->d_sws, istate);                                          \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_nb_spmv_sym<TXW, OCC>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,      \
-                               A->d_sval, x->base, A->d_sws, istate);                                          \
+    const dim3 grid((unsigned)ntiles), blk(64 * SYM_TY), ggrid((unsigned)((A->nrows + 255) / 256)), gblk(256);
+#define SYM_LAUNCH(TXW, TZW)                                                                                    \
+    do {                                                                                                        \
+        if (g_tune.spmv_sym_pf && g_tune.spmv_sym_waves == 4)                                                   \
+            hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, TZW, 4>), grid, dim3(256), lds, st, g, A->d_rowbox,       \
+                               A->d_svptr, A->d_sval, x->base, A->d_sws, istate);                               \
+        else if (g_tune.spmv_sym_pf)                                                                            \
+            hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, TZW, 8>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr, \
+                               A->d_sval, x->base, A->d_sws, istate);                                           \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_nb_spmv_sym<TXW, 1>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,         \
+                               A->d_sval, x->base, A->d_sws, istate);                                           \
+        hipLaunchKernelGGL((k_nb_sym_gather<TXW, TZW>), ggrid, gblk, 0, st, g, A->d_sws, y->d, istate);         \
     } while (0)
     if (g.TX == 16) {
-        if (g_tune.spmv_sym_occ == 8) SYM_LAUNCH(16, 8);
-        else if (g_tune.spmv_sym_occ == 6) SYM_LAUNCH(16, 6);
+        if (g.TZ == 2) SYM_LAUNCH(16, 2);
         else SYM_LAUNCH(16, 1);
-        hipLaunchKernelGGL((k_nb_sym_gather<16>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
-                           A->d_sws, y->d, istate);
     } else {
-        if (g_tune.spmv_sym_occ == 8) SYM_LAUNCH(8, 8);
-        else if (g_tune.spmv_sym_occ == 6) SYM_LAUNCH(8, 6);
+        if (g.TZ == 2) SYM_LAUNCH(8, 2);
         else SYM_LAUNCH(8, 1);
-        hipLaunchKernelGGL((k_nb_sym_gather<8>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
-                           A->d_sws, y->d, istate);
     }
 #undef SYM_LAUNCH
 }
@@ -2068,7 +2079,7 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
         // symmetric storage: the stored (upper) blocks, per row its value
         // offset and box, x and y once, the tile partials written and read
         *bytes = (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 +
-                 (double)A->sws_entries[sym_geo(A).TX == 16] * 48.0;
+                 (double)A->sws_entries[(sym_geo(A).TX == 16) + 2 * (sym_geo(A).TZ == 2)] * 48.0;
     } else if (A->kind == 0) {
         // bytes the SpMV must move: real blocks only (row padding is not counted);
         // the column stream unless the columns are computed from row boxes

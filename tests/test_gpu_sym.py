@@ -56,11 +56,25 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         assert K.spmvBytes() < 0.75 * b0
     ip, ix, d = K.getValuesCSR()
     yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
-    for _ in range(3):
-        y1 = (K * x).getArray().copy()
-        for ref in (y0, yh):
-            assert np.linalg.norm(y1 - ref) <= 1e-14 * np.linalg.norm(ref)
-            assert np.abs(y1 - ref).max() <= 1e-13 * np.abs(ref).max()
+    from pynama_amd.runtime import set_tuning
+    try:
+        # tile shapes: 8 x 8 rows of one or two planes (pipelined kernel), the
+        # first kernel version, 16-wide tiles
+        for knobs in ({}, {"spmv_sym_tz": 1}, {"spmv_sym_pf": 0}, {"spmv_sym_tx": 16},
+                      {"spmv_sym_tx": 16, "spmv_sym_tz": 1}, {"spmv_sym_waves": 4},
+                      {"spmv_sym_waves": 4, "spmv_sym_tz": 1}, {"spmv_sym_waves": 4, "spmv_sym_tx": 16}):
+            for k, v in knobs.items():
+                set_tuning(k, v)
+            for _ in range(2):
+                y1 = (K * x).getArray().copy()
+                for ref in (y0, yh):
+                    assert np.linalg.norm(y1 - ref) <= 1e-14 * np.linalg.norm(ref), knobs
+                    assert np.abs(y1 - ref).max() <= 1e-13 * np.abs(ref).max(), knobs
+            for k, v in (("spmv_sym_tz", 2), ("spmv_sym_pf", 1), ("spmv_sym_tx", 8), ("spmv_sym_waves", 8)):
+                set_tuning(k, v)
+    finally:
+        for k, v in (("spmv_sym_tz", 2), ("spmv_sym_pf", 1), ("spmv_sym_tx", 8), ("spmv_sym_waves", 8)):
+            set_tuning(k, v)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)
