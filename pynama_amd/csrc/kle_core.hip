@@ -541,6 +541,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 1 || value == 2, "spmv_sym_tz: 1 or 2");
         g_tune.spmv_sym_tz = value;
+    } else if (k == "spmv_sym_xcd") {
+        KLE_ARG(value >= 0 && value <= 64, "spmv_sym_xcd: 0..64");
+        g_tune.spmv_sym_xcd = value;
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 4 || value == 8, "spmv_sym_waves: 4 or 8");
         g_tune.spmv_sym_waves = value;
@@ -585,6 +588,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_pf") *value = g_tune.spmv_sym_pf;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
+    else if (k == "spmv_sym_xcd") *value = g_tune.spmv_sym_xcd;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

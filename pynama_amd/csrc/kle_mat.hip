@@ -663,12 +663,12 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_sym_pf(SymGeo g, const int 
                                                                      const double *__restrict__ sval,
                                                                      const double *__restrict__ x,
                                                                      double *__restrict__ ws,
-                                                                     const int *__restrict__ istate)
+                                                                     const int *__restrict__ istate, int xcd_chunk)
 {
     extern __shared__ double yl[];  // [3][RN]
     if (istate && istate[I_REASON] != 0) return;
     const int RN = g.RX * g.RY * g.RZ;
-    const int64_t t = blockIdx.x;
+    const int64_t t = xcd_block(xcd_chunk);
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;  // first plane of the tile
@@ -1222,10 +1222,10 @@ static void launch_sym(const kle_mat *A, const kle_vec *x, kle_vec *y, const int
     do {                                                                                                        \
         if (g_tune.spmv_sym_pf && g_tune.spmv_sym_waves == 4)                                                   \
             hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, TZW, 4>), grid, dim3(256), lds, st, g, A->d_rowbox,       \
-                               A->d_svptr, A->d_sval, x->base, A->d_sws, istate);                               \
+                               A->d_svptr, A->d_sval, x->base, A->d_sws, istate, g_tune.spmv_sym_xcd);          \
         else if (g_tune.spmv_sym_pf)                                                                            \
             hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, TZW, 8>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr, \
-                               A->d_sval, x->base, A->d_sws, istate);                                           \
+                               A->d_sval, x->base, A->d_sws, istate, g_tune.spmv_sym_xcd);                      \
         else                                                                                                    \
             hipLaunchKernelGGL((k_nb_spmv_sym<TXW, 1>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,         \
                                A->d_sval, x->base, A->d_sws, istate);                                           \
