@@ -68,7 +68,8 @@ typedef struct kle_ksp kle_ksp;
 
 const char *kle_last_error(void);
 /* Performance knobs for in-process A/B measurements (tools/cg_ab.py); every
- * value gives bitwise the same results.  Keys: "spmv_waves" (0 auto, 4, 8:
+ * value gives bitwise the same results, except the symmetric-storage keys
+ * (the same product to rounding).  Keys: "spmv_waves" (0 auto, 4, 8:
  * rows per SpMV workgroup of 3x3 chunked matrices), "spmv_x_lds" (1 default:
  * structured 3x3 rows at 8 waves stage x in LDS; 0 off), "spmv_xcd_chunk"
  * (row blocks per XCD run, 0 round-robin; default 16), "spmv_dyn_lds" (unused
@@ -77,7 +78,14 @@ const char *kle_last_error(void);
  * per-group column dictionaries; 0 off), "spmv_dict_min_rows" (node rows from
  * which matrices get dictionaries at creation; default 64000), "upd_preload"
  * (1 default: CG update kernels load their first element and the stage inputs
- * before the prologue; 0 off). */
+ * before the prologue; 0 off), "spmv_sym" (1 default: matrices holding
+ * symmetric storage run the symmetric SpMV; 0 the full storage),
+ * "spmv_sym_min_rows" (node rows from which kle_assemble_kle gives the
+ * single-rank K symmetric storage; default 64000), "spmv_sym_pf" (1 default:
+ * software-pipelined symmetric kernel; 0 the first version), "spmv_sym_tx"
+ * (8 default or 16 rows per tile along x), "spmv_sym_tz" (2 default or 1
+ * lattice planes per tile), "spmv_sym_waves" (8 default or 4 waves per
+ * workgroup), "spmv_sym_xcd" (tiles per XCD run, 0 default round-robin). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);

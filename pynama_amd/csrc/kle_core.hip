@@ -550,9 +550,6 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_pf") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_pf: 0 or 1");
         g_tune.spmv_sym_pf = value;
-    } else if (k == "spmv_sym_occ") {
-        KLE_ARG(value == 0 || value == 6 || value == 8, "spmv_sym_occ: 0, 6 or 8");
-        g_tune.spmv_sym_occ = value;
     } else if (k == "spmv_sym_min_rows") {
         KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
         g_tune.spmv_sym_min_rows = value;
@@ -584,7 +581,6 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
     else if (k == "spmv_sym") *value = g_tune.spmv_sym;
     else if (k == "spmv_sym_tx") *value = g_tune.spmv_sym_tx;
-    else if (k == "spmv_sym_occ") *value = g_tune.spmv_sym_occ;
     else if (k == "spmv_sym_pf") *value = g_tune.spmv_sym_pf;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;

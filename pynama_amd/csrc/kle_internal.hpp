@@ -300,7 +300,6 @@ struct Tuning {
     int spmv_sym_min_rows = 64000;
     int spmv_sym_tx = 8;    // rows per wave (tile width along x) of the symmetric SpMV: 8 or 16
     int spmv_sym_pf = 1;    // symmetric SpMV: next (row, pass) item's loads in flight while the current one is summed
-    int spmv_sym_occ = 0;
     int spmv_sym_tz = 2;    // (2-plane tiles: 12 instead of 20 partials per row)
     int spmv_sym_xcd = 0;   // symmetric SpMV tiles per XCD run (xcd_block); 0: round-robin
     int spmv_sym_waves = 8; // waves per workgroup of the pipelined symmetric SpMV: 8 or 4 (same tile)    // lattice planes per tile of the pipelined symmetric SpMV: 1 or 2   // 8: cap the symmetric SpMV at 64 VGPRs (8 waves per SIMD); 0: compiler's choice
