@@ -673,8 +673,6 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_sym_pf(SymGeo g, const int 
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;  // first plane of the tile
     const int ox = tix * TXW - g.P, oy = tiy * SYM_TY - g.P;
-    for (int k = threadIdx.x; k < 3 * RN; k += 64 * WV) yl[k] = 0.0;
-    __syncthreads();
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     const int nx = min(TXW, g.Lx - tix * TXW);
@@ -732,6 +730,11 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_sym_pf(SymGeo g, const int 
         px1 = x[3 * i + 1];
         px2 = x[3 * i + 2];
     }
+    // zero the region while the descriptor loads are in flight; the barrier
+    // waits for the LDS stores only (lgkmcnt 0), not for those loads
+    for (int k = threadIdx.x; k < 3 * RN; k += 64 * WV) yl[k] = 0.0;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
     auto slot_row = [&](int s, SymRow &R) {
         const int xg = tix * TXW + slot_x(s), yy = tiy * SYM_TY + (s & 7), zz = tz + s / NQ;
         R.i = xg + (int64_t)g.Lx * yy + Lxy * zz;
