@@ -175,3 +175,29 @@ def test_noslip_golden():
         np.testing.assert_array_equal(A.indptr, g[k + "_indptr"])
         np.testing.assert_array_equal(A.indices, g[k + "_indices"])
         assert np.abs(A.data - g[k + "_data"]).max() <= 1e-14 * np.abs(g[k + "_data"]).max(), k
+
+
+@pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([2, 2, 2], 3), ([2, 1, 1], 6)])
+def test_kle_k_is_symmetric_with_upper_tails(nelem, ngl):
+    """What the symmetric-storage SpMV relies on, stated on the
+    oracle's K (mat_fs.py:150-192): K == K^T to rounding, and in the box's
+    lexicographic node order each row's columns at or after its own node
+    (the stored upper tail) hold exactly its entries with j >= i."""
+    import scipy.sparse as sp
+    m = O.BoxMesh(3, nelem, [0, 0, 0], [1, 1, 1], ngl)
+    xo = m.coords()
+    flag = ((xo == 0.0) | (xo == 1.0)).any(axis=1).astype(np.uint8)
+    K, _, _ = m.assemble_fs(flag)
+    A = sp.csr_matrix((K.data, K.indices, K.indptr), shape=(K.m, K.m))
+    D = abs(A - A.T)
+    assert D.max() <= 1e-12 * abs(A).max()
+    # upper triangle + strictly lower triangle reconstruct K
+    U = sp.triu(A, 0)
+    assert abs((U + sp.triu(A, 1).T) - A).max() <= 1e-12 * abs(A).max()
+    # half the blocks (plus the diagonal) are kept: 3x3 node blocks
+    n = K.m // 3
+    rows = np.repeat(np.arange(K.m), np.diff(K.indptr)) // 3
+    cols = K.indices // 3
+    blocks = np.unique(rows * n + cols)
+    r, c = blocks // n, blocks % n
+    assert np.count_nonzero(c >= r) == (len(blocks) + n) // 2
