@@ -467,32 +467,9 @@ def main():
 
 
 def spmv_kernel(K, layout, ngl):
-    """Name of the SpMV kernel libkle launches for this rank's K (kle_mat.hip
-    launch_nb_lay / spmv_waves): structured 3x3 chunked rows with x staged in
-    LDS run k_nb_spmv_xl<8> when 8 waves per workgroup apply (from 64k node
-    rows up) and 8 rows' union box fits its LDS tile (p <= 4); unstructured
-    3x3 rows there run k_nb_spmv_dict (x through per-group column
-    dictionaries); otherwise k_nb_spmv with 8 or 4 waves (kle_set_tuning
-    "spmv_waves" / "spmv_x_lds" override)."""
-    from pynama_amd.runtime import get_tuning
-    if K.isSymmetricStorage() and get_tuning("spmv_sym"):
-        tx = 16 if get_tuning("spmv_sym_tx") == 16 else 8
-        if not get_tuning("spmv_sym_pf"):
-            return f"k_nb_spmv_sym<{tx},1>+k_nb_sym_gather<{tx},1>"
-        tz, wv = get_tuning("spmv_sym_tz"), get_tuning("spmv_sym_waves")
-        return f"k_nb_spmv_sym_pf<{tx},{tz},{wv}>+k_nb_sym_gather<{tx},{tz}>"
-    wv = get_tuning("spmv_waves")
-    lo, hi = K.getOwnershipRange()
-    if layout != 1:
-        wv = 4
-    elif wv not in (4, 8):
-        wv = 8 if (hi - lo) // 3 >= 64000 else 4
-    if layout == 1 and wv == 8 and K.isStructured() and get_tuning("spmv_x_lds") and ngl <= 5:
-        return "k_nb_spmv_xl<8>"
-    if (layout == 1 and wv == 8 and not K.isStructured() and get_tuning("spmv_dict")
-            and (hi - lo) // 3 >= get_tuning("spmv_dict_min_rows")):
-        return "k_nb_spmv_dict"
-    return "k_nb_spmv<3,3,%d,%s,%d>" % (layout, "true" if K.isStructured() else "false", wv)
+    """Name of the SpMV kernel(s) libkle launches for this rank's K with the
+    current tuning (kle_mat_spmv_kernel: the library's own launch decision)."""
+    return K.spmvKernel()
 
 
 def splitmix_uniform(seed, lo, hi):

@@ -81,11 +81,11 @@ const char *kle_last_error(void);
  * before the prologue; 0 off), "spmv_sym" (1 default: matrices holding
  * symmetric storage run the symmetric SpMV; 0 the full storage),
  * "spmv_sym_min_rows" (node rows from which kle_assemble_kle gives the
- * single-rank K symmetric storage; default 64000), "spmv_sym_pf" (1 default:
- * software-pipelined symmetric kernel; 0 the first version), "spmv_sym_tx"
- * (8 default or 16 rows per tile along x), "spmv_sym_tz" (2 default or 1
- * lattice planes per tile), "spmv_sym_waves" (8 default or 4 waves per
- * workgroup), "spmv_sym_xcd" (tiles per XCD run, 0 default round-robin). */
+ * single-rank K symmetric storage; default 64000), "spmv_sym_kernel" (2
+ * default: x staged in LDS; 1 the round-2 kernel gathering x from global
+ * memory), "spmv_sym_det" (1 default: the transposed adds as exact
+ * fixed-point sums, y bitwise reproducible; 0 fp64 LDS atomics),
+ * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
@@ -363,6 +363,9 @@ int kle_get_nb_layout(void);
 int kle_mat_get_format(const kle_mat *A, char *buf, int buflen);
 /* Bytes one SpMV with this matrix moves (algorithmic: matrix + x + y). */
 int kle_mat_spmv_bytes(const kle_mat *A, double *bytes);
+/* Name of the kernel(s) y = A x launches with the current tuning, as rocprof
+ * lists them (profile summaries, bench.py's roofline record). */
+int kle_mat_spmv_kernel(const kle_mat *A, char *buf, int buflen);
 
 /* -------------------------------------------------------------------- ksp */
 int kle_ksp_create(kle_ctx *ctx, kle_ksp **out);

@@ -535,21 +535,24 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym: 0 or 1");
         g_tune.spmv_sym = value;
-    } else if (k == "spmv_sym_tx") {
-        KLE_ARG(value == 8 || value == 16, "spmv_sym_tx: 8 or 16");
-        g_tune.spmv_sym_tx = value;
-    } else if (k == "spmv_sym_tz") {
-        KLE_ARG(value == 1 || value == 2, "spmv_sym_tz: 1 or 2");
-        g_tune.spmv_sym_tz = value;
-    } else if (k == "spmv_sym_xcd") {
-        KLE_ARG(value >= 0 && value <= 64, "spmv_sym_xcd: 0..64");
-        g_tune.spmv_sym_xcd = value;
+    } else if (k == "spmv_sym_kernel") {
+        KLE_ARG(value == 2 || value == 3, "spmv_sym_kernel: 2 (tile per workgroup) or 3 (column walk)");
+        g_tune.spmv_sym_kernel = value;
+    } else if (k == "spmv_sym_det") {
+        KLE_ARG(value == 0 || value == 1, "spmv_sym_det: 0 or 1");
+        g_tune.spmv_sym_det = value;
     } else if (k == "spmv_sym_waves") {
-        KLE_ARG(value == 4 || value == 8, "spmv_sym_waves: 4 or 8");
+        KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
-    } else if (k == "spmv_sym_pf") {
-        KLE_ARG(value == 0 || value == 1, "spmv_sym_pf: 0 or 1");
-        g_tune.spmv_sym_pf = value;
+    } else if (k == "spmv_sym_probe") {
+        KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
+        g_tune.spmv_sym_probe = value;
+    } else if (k == "spmv_sym_cw_tile") {
+        KLE_ARG(value >= 0, "spmv_sym_cw_tile: >= 0");
+        g_tune.spmv_sym_cw_tile = value;
+    } else if (k == "spmv_sym_ahead") {
+        KLE_ARG(value == 1 || value == 2, "spmv_sym_ahead: 1 or 2");
+        g_tune.spmv_sym_ahead = value;
     } else if (k == "spmv_sym_min_rows") {
         KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
         g_tune.spmv_sym_min_rows = value;
@@ -580,11 +583,12 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "upd_preload") *value = g_tune.upd_preload;
     else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
     else if (k == "spmv_sym") *value = g_tune.spmv_sym;
-    else if (k == "spmv_sym_tx") *value = g_tune.spmv_sym_tx;
-    else if (k == "spmv_sym_pf") *value = g_tune.spmv_sym_pf;
-    else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
+    else if (k == "spmv_sym_kernel") *value = g_tune.spmv_sym_kernel;
+    else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
-    else if (k == "spmv_sym_xcd") *value = g_tune.spmv_sym_xcd;
+    else if (k == "spmv_sym_ahead") *value = g_tune.spmv_sym_ahead;
+    else if (k == "spmv_sym_cw_tile") *value = g_tune.spmv_sym_cw_tile;
+    else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

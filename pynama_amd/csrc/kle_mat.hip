@@ -23,6 +23,7 @@
 #include <cstring>
 #include <atomic>
 #include <map>
+#include <string>
 #include <thread>
 
 #include "kle_internal.hpp"
@@ -397,469 +398,6 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     }
 }
 
-// ---------------------------------------------------------------------------
-// Symmetric node-block storage (PETSc MATSBAIJ; kle_mat_set_symmetric): on a
-// box lattice a structured row's columns are its box in lexicographic order,
-// so the upper triangle j >= i of row i is the tail [k0, m) of that box from
-// its own (diagonal) block on.  Only those blocks are stored (same 16-block
-// chunk layout, rows 128-B aligned): 31.4 M of config 2's 62.4 M blocks.
-//
-// y = A x as one pass over the stored blocks: block (i, j) adds B x_j to row i
-// and B^T x_i to row j.  A workgroup takes a tile of SYM_TX x SYM_TY rows of
-// one lattice plane z (wave w: lattice line y0 + w, SYM_TX rows in x); every
-// row it touches lies in the tile's region [x0-P, x0+TX+P) x [y0-P, y0+TY+P)
-// x [z, z+P] (P = the largest row-box reach), accumulated in LDS (fp64 LDS
-// adds) and written as the tile's partial sums to a workspace; the gather
-// kernel sums, per row, the partials of the (at most 2 x 2 x (P+1)) tiles whose
-// regions contain it, in a fixed tile order.  HBM: the stored values once
-// (half of the full storage) + the partials written and read once.  The
-// LDS adds of one tile commute in a run-dependent order, so y agrees with the
-// full-storage kernels to rounding (not bitwise).
-constexpr int SYM_TX = 8, SYM_TY = 8;
-struct SymGeo {
-    int Lx, Ly, Lz, P, TX, TZ, RX, RY, RZ, ntx, nty, ntz;
-};
-
-__device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
-                                        int &by, int &bz, int &bnx, int &bny, int &bnz)
-{
-    const int64_t base = rowbox[2 * i];
-    const int d = rowbox[2 * i + 1];
-    bz = (int)(base / Lxy);
-    const int64_t r = base - (int64_t)bz * Lxy;
-    by = (int)(r / Lx);
-    bx = (int)(r - (int64_t)by * Lx);
-    bnx = d & 255;
-    bny = (d >> 8) & 255;
-    bnz = (d >> 16) & 255;
-}
-
-// Copy each row's upper tail into the symmetric layout and measure
-// max |B_ij - B_ji^T| per row (the stored triangle must describe the matrix).
-__global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly, const int *__restrict__ rowptr,
-                                                   const int *__restrict__ rowcnt, const int *__restrict__ rowbox,
-                                                   const int64_t *__restrict__ vptr, const double *__restrict__ val,
-                                                   const int64_t *__restrict__ svptr, double *__restrict__ sval,
-                                                   double *__restrict__ rowdiff, double *__restrict__ rowmax)
-{
-    const int lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= nrows) return;
-    const int64_t Lxy = (int64_t)Lx * Ly;
-    const int z = (int)(i / Lxy), y = (int)((i - z * Lxy) / Lx), x = (int)(i - z * Lxy - (int64_t)y * Lx);
-    int bx, by, bz, bnx, bny, bnz;
-    sym_box(rowbox, i, Lx, Lxy, bx, by, bz, bnx, bny, bnz);
-    const int m = rowcnt ? rowcnt[i] : rowptr[i + 1] - rowptr[i], mp = rowptr[i + 1] - rowptr[i];
-    const int k0 = (x - bx) + bnx * ((y - by) + bny * (z - bz));
-    const int mu = m - k0;
-    const double *v = val + vptr[i];
-    double *sv = sval + svptr[i];
-    double dmax = 0.0, vmax = 0.0;
-    for (int kk = lane; kk < mu; kk += 64) {
-        const int k = k0 + kk;
-        double b[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            b[t] = v[vofs(1, 9, t, k, m, mp)];
-            sv[vofs(1, 9, t, kk, mu, mu)] = b[t];
-            vmax = fmax(vmax, fabs(b[t]));
-        }
-        if (kk == 0) continue;
-        const int bnxy = bnx * bny;
-        const int kz = k / bnxy, ky = (k - kz * bnxy) / bnx, kx = k - kz * bnxy - ky * bnx;
-        const int64_t j = (bx + kx) + (int64_t)Lx * (by + ky) + Lxy * (bz + kz);
-        int cx, cy, cz, cnx, cny, cnz;
-        sym_box(rowbox, j, Lx, Lxy, cx, cy, cz, cnx, cny, cnz);
-        if (x < cx || x >= cx + cnx || y < cy || y >= cy + cny || z < cz || z >= cz + cnz) {
-            dmax = INFINITY;  // (i, j) stored but (j, i) not in the pattern
-            continue;
-        }
-        const int mj = rowcnt ? rowcnt[j] : rowptr[j + 1] - rowptr[j], mpj = rowptr[j + 1] - rowptr[j];
-        const int kj = (x - cx) + cnx * ((y - cy) + cny * (z - cz));
-        const double *vj = val + vptr[j];
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) dmax = fmax(dmax, fabs(b[a * 3 + c] - vj[vofs(1, 9, c * 3 + a, kj, mj, mpj)]));
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
-        vmax = fmax(vmax, __shfl_xor(vmax, o, 64));
-    }
-    if (lane == 0) {
-        rowdiff[i] = dmax;
-        rowmax[i] = vmax;
-    }
-}
-
-template <int TXW, int OCC>
-__global__ __launch_bounds__(64 * SYM_TY, OCC) void k_nb_spmv_sym(SymGeo g, const int *__restrict__ rowbox,
-                                                             const int64_t *__restrict__ svptr,
-                                                             const double *__restrict__ sval,
-                                                             const double *__restrict__ x, double *__restrict__ ws,
-                                                             const int *__restrict__ istate)
-{
-    extern __shared__ double yl[];  // [3][RN]
-    if (istate && istate[I_REASON] != 0) return;
-    const int RN = g.RX * g.RY * g.RZ;
-    const int64_t t = blockIdx.x;
-    const int tix = (int)(t % g.ntx);
-    const int64_t q = t / g.ntx;
-    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty);
-    const int ox = tix * TXW - g.P, oy = tiy * SYM_TY - g.P;
-    for (int k = threadIdx.x; k < 3 * RN; k += 64 * SYM_TY) yl[k] = 0.0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int yy = tiy * SYM_TY + w;
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
-    if (yy < g.Ly) {
-        for (int xx = 0; xx < TXW; ++xx) {
-            const int xg = tix * TXW + xx;
-            if (xg >= g.Lx) break;
-            const int64_t i = xg + (int64_t)g.Lx * yy + Lxy * tz;
-            int bx, by, bz, bnx, bny, bnz;
-            sym_box(rowbox, i, g.Lx, Lxy, bx, by, bz, bnx, bny, bnz);
-            const int bnxy = bnx * bny;
-            const int k0 = (xg - bx) + bnx * ((yy - by) + bny * (tz - bz));
-            const int mu = bnxy * bnz - k0;
-            const double *v = sval + svptr[i];
-            const double xi0 = x[3 * i], xi1 = x[3 * i + 1], xi2 = x[3 * i + 2];
-            // region offsets of the box origin
-            const int rx0 = bx - ox, ry0 = by - oy, rz0 = bz - tz;
-            double acc[3] = {0.0, 0.0, 0.0};
-            const int q16 = mu & ~15;
-            for (int kb = 0; kb < mu; kb += 64) {
-                const int kk = kb + lane;
-                double vv[9];
-                if (kb + 64 <= q16) {
-                    const double *p = v + (kk >> 4) * (9 * 16) + (kk & 15);
-#pragma unroll
-                    for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(p + s * 16);
-                } else if (kk < mu) {
-                    const int64_t o0 = vofs(1, 9, 0, kk, mu, mu);
-                    const int64_t st = kk < q16 ? 16 : mu - q16;
-#pragma unroll
-                    for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(v + o0 + s * st);
-                }
-                if (kk < mu) {
-                    const int k = k0 + kk;
-                    const int kz = k / bnxy, rem = k - kz * bnxy, ky = rem / bnx, kx = rem - ky * bnx;
-                    const int64_t j = (bx + kx) + (int64_t)g.Lx * (by + ky) + Lxy * (bz + kz);
-                    const double xj0 = x[3 * j], xj1 = x[3 * j + 1], xj2 = x[3 * j + 2];
-                    acc[0] += vv[0] * xj0 + vv[1] * xj1 + vv[2] * xj2;
-                    acc[1] += vv[3] * xj0 + vv[4] * xj1 + vv[5] * xj2;
-                    acc[2] += vv[6] * xj0 + vv[7] * xj1 + vv[8] * xj2;
-                    if (kk > 0) {
-                        const int r = (rx0 + kx) + g.RX * ((ry0 + ky) + g.RY * (rz0 + kz));
-                        atomicAdd(&yl[r], vv[0] * xi0 + vv[3] * xi1 + vv[6] * xi2);
-                        atomicAdd(&yl[RN + r], vv[1] * xi0 + vv[4] * xi1 + vv[7] * xi2);
-                        atomicAdd(&yl[2 * RN + r], vv[2] * xi0 + vv[5] * xi1 + vv[8] * xi2);
-                    }
-                }
-            }
-#pragma unroll
-            for (int a = 0; a < 3; ++a) acc[a] = wsum(acc[a]);
-            if (lane < 3) {
-                const int r = (xg - ox) + g.RX * (yy - oy);
-                atomicAdd(&yl[lane * RN + r], lane == 0 ? acc[0] : lane == 1 ? acc[1] : acc[2]);
-            }
-        }
-    }
-    __syncthreads();
-    // the tile's partial sums: region nodes inside the lattice only
-    double *dst = ws + t * 3 * (int64_t)RN;
-    for (int k = threadIdx.x; k < RN; k += 64 * SYM_TY) {
-        const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
-        const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
-        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
-#pragma unroll
-        for (int b = 0; b < 3; ++b) dst[b * RN + k] = yl[b * RN + k];
-    }
-}
-
-// Wave sum through DPP row moves (VALU only; __shfl_xor is a ds_bpermute per
-// 32-bit half, i.e. 12 LDS instructions per double): quad swaps, half-row
-// and row mirrors, then row_bcast15 / row_bcast31 carry the row sums into
-// lane 63, which every lane reads back.
-template <int ctrl, int row_mask>
-__device__ __forceinline__ double dpp_step(double v)
-{
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    const int l2 = __builtin_amdgcn_update_dpp(0, lo, ctrl, row_mask, 0xF, false);
-    const int h2 = __builtin_amdgcn_update_dpp(0, hi, ctrl, row_mask, 0xF, false);
-    return v + __hiloint2double(h2, l2);
-}
-
-__device__ __forceinline__ double wsum_dpp(double v)
-{
-    v = dpp_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-    v = dpp_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-    v = dpp_step<0x141, 0xF>(v);  // row_half_mirror
-    v = dpp_step<0x140, 0xF>(v);  // row_mirror
-    v = dpp_step<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3
-    v = dpp_step<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
-    return __hiloint2double(hi, lo);
-}
-
-// Same tile pass with the wave's (row, 64-block pass) items flattened into one
-// software-pipelined loop: the values and x entries of the next item are in
-// flight while the current one is multiplied and accumulated (a wave's rows
-// average 1.4 passes of 64 blocks, so one item at a time leaves it waiting
-// on HBM latency at every row).
-struct SymRow {
-    int64_t i;
-    const double *v;
-    double x0, x1, x2;
-    int bx, by, bz, bnx, bnxy, k0, mu, rx0, ry0, rz0, own;
-    float ibnx, ibnxy;  // 1/bnx, 1/bnxy: quotients of block positions by float multiply + one fix-up
-};
-
-// q = n / d for 0 <= n < 2^20, d >= 1 (block position in its row box)
-__device__ __forceinline__ int sym_div(int n, int d, float inv)
-{
-    int q = (int)((float)n * inv);
-    q += (q + 1) * d <= n;
-    q -= q * d > n;
-    return q;
-}
-
-__device__ __forceinline__ void sym_row(const SymGeo &g, const int *__restrict__ rowbox,
-                                        const int64_t *__restrict__ svptr, const double *__restrict__ sval,
-                                        const double *__restrict__ x, int xg, int yy, int tz, int ox, int oy,
-                                        SymRow &R)
-{
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
-    R.i = xg + (int64_t)g.Lx * yy + Lxy * tz;
-    int bny, bnz;
-    sym_box(rowbox, R.i, g.Lx, Lxy, R.bx, R.by, R.bz, R.bnx, bny, bnz);
-    R.bnxy = R.bnx * bny;
-    R.ibnx = 1.0f / (float)R.bnx;
-    R.ibnxy = 1.0f / (float)R.bnxy;
-    R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (tz - R.bz));
-    R.mu = R.bnxy * bnz - R.k0;
-    R.v = sval + svptr[R.i];
-    R.x0 = x[3 * R.i];
-    R.x1 = x[3 * R.i + 1];
-    R.x2 = x[3 * R.i + 2];
-    R.rx0 = R.bx - ox;
-    R.ry0 = R.by - oy;
-    R.rz0 = R.bz - tz;
-    R.own = (xg - ox) + g.RX * (yy - oy);
-}
-
-__device__ __forceinline__ double readlane_d(double v, int l)
-{
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-
-template <int TXW, int TZ, int WV>
-__global__ __launch_bounds__(64 * WV) void k_nb_spmv_sym_pf(SymGeo g, const int *__restrict__ rowbox,
-                                                                     const int64_t *__restrict__ svptr,
-                                                                     const double *__restrict__ sval,
-                                                                     const double *__restrict__ x,
-                                                                     double *__restrict__ ws,
-                                                                     const int *__restrict__ istate, int xcd_chunk)
-{
-    extern __shared__ double yl[];  // [3][RN]
-    if (istate && istate[I_REASON] != 0) return;
-    const int RN = g.RX * g.RY * g.RZ;
-    const int64_t t = xcd_block(xcd_chunk);
-    const int tix = (int)(t % g.ntx);
-    const int64_t q = t / g.ntx;
-    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;  // first plane of the tile
-    const int ox = tix * TXW - g.P, oy = tiy * SYM_TY - g.P;
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
-    const int nx = min(TXW, g.Lx - tix * TXW);
-    constexpr int NQ = TXW * SYM_TY / WV;  // row slots per wave and plane
-    constexpr int NS = NQ * TZ;           // row slots per wave
-    // item = (row, pass kb): values of its 64 blocks and the x entries they multiply
-    // Branch-free: every lane loads (lanes past the row's end re-read its
-    // last block and are masked when summed), so each item is exactly 12
-    // loads and the wait for the current item leaves the next item's 12 in
-    // flight (conditional loads make the compiler drain the queue).
-    auto load = [&](const SymRow &R, int kb, double *vv, double *xv, int &rr) {
-        const int kk = min(kb + lane, R.mu - 1);
-        const int q16 = R.mu & ~15;
-        const bool ch = kk < q16;
-        const int64_t o0 = ch ? (int64_t)((kk >> 4) * 144 + (kk & 15)) : (int64_t)q16 * 9 + (kk - q16);
-        const int st = ch ? 16 : R.mu - q16;
-#pragma unroll
-        for (int s = 0; s < 9; ++s) vv[s] = __builtin_nontemporal_load(R.v + o0 + s * st);
-        const int k = R.k0 + kk;
-        const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
-        const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
-        const int64_t j = (R.bx + kx) + (int64_t)g.Lx * (R.by + ky) + Lxy * (R.bz + kz);
-        xv[0] = x[3 * j];
-        xv[1] = x[3 * j + 1];
-        xv[2] = x[3 * j + 2];
-        rr = (R.rx0 + kx) + g.RX * ((R.ry0 + ky) + g.RY * (R.rz0 + kz));
-    };
-    // row slots of this wave: slot s = (plane, q) is plane z0 + s / NQ,
-    // lattice line y0 + q % 8, x offset (w + WV (q / 8) + q % 8) % TXW, so
-    // every wave takes every plane, line and x class of the tile (equal work
-    // per wave up to the lattice edges; the workgroup's barrier waits for its
-    // slowest wave)
-    auto slot_x = [&](int s) { return (w + WV * ((s % NQ) >> 3) + (s & 7)) % TXW; };
-    auto slot_ok = [&](int s) {
-        return tiy * SYM_TY + (s & 7) < g.Ly && slot_x(s) < nx && tz + s / NQ < g.Lz;
-    };
-    auto next_slot = [&](int s) {
-        while (s < NS && !slot_ok(s)) ++s;
-        return s;
-    };
-    // the wave's row descriptors (box, value offset, x_i) are loaded once, lane
-    // s holding slot s, and read back with readlane when the slot starts: no
-    // dependent scalar-memory round trip at every row
-    int pb = 0, pd = 0, psl = 0, psh = 0;
-    double px0 = 0.0, px1 = 0.0, px2 = 0.0;
-    if (lane < NS && slot_ok(lane)) {
-        const int64_t i = tix * TXW + slot_x(lane) + (int64_t)g.Lx * (tiy * SYM_TY + (lane & 7)) +
-                          Lxy * (tz + lane / NQ);
-        pb = rowbox[2 * i];
-        pd = rowbox[2 * i + 1];
-        const int64_t o = svptr[i];
-        psl = (int)(uint32_t)o;
-        psh = (int)(o >> 32);
-        px0 = x[3 * i];
-        px1 = x[3 * i + 1];
-        px2 = x[3 * i + 2];
-    }
-    // zero the region while the descriptor loads are in flight; the barrier
-    // waits for the LDS stores only (lgkmcnt 0), not for those loads
-    for (int k = threadIdx.x; k < 3 * RN; k += 64 * WV) yl[k] = 0.0;
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    auto slot_row = [&](int s, SymRow &R) {
-        const int xg = tix * TXW + slot_x(s), yy = tiy * SYM_TY + (s & 7), zz = tz + s / NQ;
-        R.i = xg + (int64_t)g.Lx * yy + Lxy * zz;
-        const int64_t base = __builtin_amdgcn_readlane(pb, s);
-        const int d = __builtin_amdgcn_readlane(pd, s);
-        R.bz = (int)(base / Lxy);
-        const int64_t rem = base - (int64_t)R.bz * Lxy;
-        R.by = (int)(rem / g.Lx);
-        R.bx = (int)(rem - (int64_t)R.by * g.Lx);
-        R.bnx = d & 255;
-        const int bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
-        R.bnxy = R.bnx * bny;
-        R.ibnx = 1.0f / (float)R.bnx;
-        R.ibnxy = 1.0f / (float)R.bnxy;
-        R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (zz - R.bz));
-        R.mu = R.bnxy * bnz - R.k0;
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(psl, s);
-        const int64_t hi = __builtin_amdgcn_readlane(psh, s);
-        R.v = sval + ((hi << 32) | lo);
-        R.x0 = readlane_d(px0, s);
-        R.x1 = readlane_d(px1, s);
-        R.x2 = readlane_d(px2, s);
-        R.rx0 = R.bx - ox;
-        R.ry0 = R.by - oy;
-        R.rz0 = R.bz - tz;
-        R.own = (xg - ox) + g.RX * ((yy - oy) + g.RY * (zz - tz));
-    };
-    int xx = next_slot(0);
-    if (xx < NS) {
-        SymRow cur, nxt;
-        slot_row(xx, cur);
-        int kb = 0;
-        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-        // two register sets used in turn (a copy of in-flight registers would
-        // make the compiler wait for the loads at every item)
-        double va[9], xa[3], vb[9], xb[3];
-        int ra, rb;
-        load(cur, 0, va, xa, ra);
-        auto step = [&](const double *vv, const double *xv, const int rr, double *vn, double *xn, int &rn) {
-            int nkb = kb + 64, nxx = xx;
-            bool more = true;
-            if (nkb >= cur.mu) {
-                nkb = 0;
-                nxx = next_slot(xx + 1);
-                more = nxx < NS;
-                if (more) slot_row(nxx, nxt);
-            } else {
-                nxt = cur;
-            }
-            if (!more) {  // no next item: re-read the current one (cache hits) to keep the loads unconditional
-                nxt = cur;
-                nkb = kb;
-            }
-            load(nxt, nkb, vn, xn, rn);
-            // current item: B x_j into the row, B^T x_i into row j
-            const int kk = kb + lane;
-            if (kk < cur.mu) {
-                acc0 += vv[0] * xv[0] + vv[1] * xv[1] + vv[2] * xv[2];
-                acc1 += vv[3] * xv[0] + vv[4] * xv[1] + vv[5] * xv[2];
-                acc2 += vv[6] * xv[0] + vv[7] * xv[1] + vv[8] * xv[2];
-            }
-            if (kk > 0 && kk < cur.mu) {
-                atomicAdd(&yl[rr], vv[0] * cur.x0 + vv[3] * cur.x1 + vv[6] * cur.x2);
-                atomicAdd(&yl[RN + rr], vv[1] * cur.x0 + vv[4] * cur.x1 + vv[7] * cur.x2);
-                atomicAdd(&yl[2 * RN + rr], vv[2] * cur.x0 + vv[5] * cur.x1 + vv[8] * cur.x2);
-            }
-            if (nxx != xx || !more) {
-                acc0 = wsum_dpp(acc0);
-                acc1 = wsum_dpp(acc1);
-                acc2 = wsum_dpp(acc2);
-                if (lane < 3) atomicAdd(&yl[lane * RN + cur.own], lane == 0 ? acc0 : lane == 1 ? acc1 : acc2);
-                acc0 = acc1 = acc2 = 0.0;
-            }
-            if (!more) return false;
-            cur = nxt;
-            xx = nxx;
-            kb = nkb;
-            return true;
-        };
-        while (step(va, xa, ra, vb, xb, rb) && step(vb, xb, rb, va, xa, ra)) {
-        }
-    }
-    __syncthreads();
-    double *dst = ws + t * 3 * (int64_t)RN;
-    for (int k = threadIdx.x; k < RN; k += 64 * WV) {
-        const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
-        const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
-        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
-#pragma unroll
-        for (int b = 0; b < 3; ++b) dst[b * RN + k] = yl[b * RN + k];
-    }
-}
-
-// y_j = sum of the partials of the tiles whose regions contain row j, in
-// ascending (z, y, x) tile order.
-template <int TXW, int TZ>
-__global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *__restrict__ ws, double *__restrict__ y,
-                                                       const int *__restrict__ istate)
-{
-    if (istate && istate[I_REASON] != 0) return;
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly, n = Lxy * g.Lz;
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const int jz = (int)(j / Lxy), jy = (int)((j - jz * Lxy) / g.Lx), jx = (int)(j - jz * Lxy - (int64_t)jy * g.Lx);
-    const int RN = g.RX * g.RY * g.RZ;
-    // tiles whose [t*T - P, t*T - P + R) contains the coordinate
-    const int x_lo = max(0, (jx + g.P - g.RX + TXW) / TXW), x_hi = min(g.ntx - 1, (jx + g.P) / TXW);
-    const int y_lo = max(0, (jy + g.P - g.RY + SYM_TY) / SYM_TY), y_hi = min(g.nty - 1, (jy + g.P) / SYM_TY);
-    const int z_lo = max(0, (jz - g.RZ + TZ) / TZ), z_hi = min(g.ntz - 1, jz / TZ);
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int tzi = z_lo; tzi <= z_hi; ++tzi)
-        for (int ty = y_lo; ty <= y_hi; ++ty)
-            for (int tx = x_lo; tx <= x_hi; ++tx) {
-                const int64_t t = ((int64_t)tzi * g.nty + ty) * g.ntx + tx;
-                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * SYM_TY - g.P)) + g.RY * (jz - tzi * TZ));
-                const double *p = ws + t * 3 * (int64_t)RN + r;
-                s0 += p[0];
-                s1 += p[RN];
-                s2 += p[2 * RN];
-            }
-    y[3 * j] = s0;
-    y[3 * j + 1] = s1;
-    y[3 * j + 2] = s2;
-}
-
 // Scalar CSR SpMV (MatMult_SeqAIJ): one wavefront per row.  A pass covers
 // 64*U entries from the row start rounded down to 32 entries, so every col
 // load (32 int32 = 128 B) and every val load (16 doubles = 128 B) covers whole
@@ -1074,176 +612,6 @@ int nb_build_dict(kle_mat *A)
     return 0;
 }
 
-void sym_drop(kle_mat *A)
-{
-    if (A->d_sval) (void)hipFree(A->d_sval);
-    if (A->d_svptr) (void)hipFree(A->d_svptr);
-    if (A->d_sws) (void)hipFree(A->d_sws);
-    A->d_sval = nullptr;
-    A->d_svptr = nullptr;
-    A->d_sws = nullptr;
-    A->sblocks = A->snvals = 0;
-    for (auto &e : A->sws_entries) e = 0;
-    A->sym_P = 0;
-}
-
-static bool sym_fits(int tx, int tz, int P)
-{
-    return (int64_t)3 * (tx + 2 * P) * (SYM_TY + 2 * P) * (tz + P) * 8 <= 65536;
-}
-
-// Tile geometry: tx x 8 rows of tz planes (kle_set_tuning "spmv_sym_tx",
-// "spmv_sym_tz"; the first kernel version, spmv_sym_pf 0, takes one plane)
-static SymGeo sym_geo(const kle_mat *A, int tx = 0, int tz = 0)
-{
-    SymGeo g;
-    const int P = A->sym_P;
-    g.TX = tx ? tx : (g_tune.spmv_sym_tx == 16 && sym_fits(16, 1, P) ? 16 : 8);
-    g.TZ = tz ? tz : (g_tune.spmv_sym_pf && g_tune.spmv_sym_tz == 2 && sym_fits(g.TX, 2, P) ? 2 : 1);
-    g.Lx = (int)A->row_lat[0];
-    g.Ly = (int)A->row_lat[1];
-    g.Lz = (int)A->row_lat[2];
-    g.P = P;
-    g.RX = g.TX + 2 * P;
-    g.RY = SYM_TY + 2 * P;
-    g.RZ = g.TZ + P;
-    g.ntx = (g.Lx + g.TX - 1) / g.TX;
-    g.nty = (g.Ly + SYM_TY - 1) / SYM_TY;
-    g.ntz = (g.Lz + g.TZ - 1) / g.TZ;
-    return g;
-}
-
-// Build the symmetric (upper-triangle) storage of a single-rank structured
-// 3x3 matrix from its full storage; refuses a matrix whose blocks are not
-// symmetric to 1e-12 of its largest entry.
-int sym_build(kle_mat *A)
-{
-    kle_ctx *c = A->ctx;
-    sym_drop(A);
-    if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_rowbox && c->nranks == 1 &&
-          A->ghost_lo == 0 && A->ghost_hi == 0 && A->m_local == A->n_local))
-        return fail(KLE_ERR_SUP, "symmetric storage needs a single-rank 3x3 node-block matrix with box-lattice rows");
-    const int64_t Lx = A->row_lat[0], Ly = A->row_lat[1], Lz = A->row_lat[2], n = A->nrows;
-    if (Lx * Ly * Lz != n || A->box_lx != Lx || A->box_lxy != Lx * Ly || Lx > INT_MAX / 2)
-        return fail(KLE_ERR_SUP, "symmetric storage: the rows are not one box lattice");
-    std::vector<int> rb(2 * n), rp(n + 1), cnt(n);
-    KLE_HIP(hipStreamSynchronize(c->stream));
-    KLE_HIP(hipMemcpy(rb.data(), A->d_rowbox, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
-    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
-    if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost));
-    else
-        for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
-    std::vector<int64_t> sv(n + 1);
-    int P = 0;
-    int64_t tot = 0, blocks = 0;
-    const int64_t Lxy = Lx * Ly;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t z = i / Lxy, y = (i - z * Lxy) / Lx, x = i - z * Lxy - y * Lx;
-        const int64_t base = rb[2 * i];
-        const int d = rb[2 * i + 1];
-        const int64_t bz = base / Lxy, by = (base - bz * Lxy) / Lx, bx = base - bz * Lxy - by * Lx;
-        const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
-        if (x < bx || x >= bx + bnx || y < by || y >= by + bny || z < bz || z >= bz + bnz ||
-            cnt[i] != bnx * bny * bnz)
-            return fail(KLE_ERR_SUP, "symmetric storage: row %lld's box does not hold its diagonal", (long long)i);
-        P = std::max<int>(P, (int)std::max({x - bx, bx + bnx - 1 - x, y - by, by + bny - 1 - y, bz + bnz - 1 - z}));
-        const int k0 = (int)((x - bx) + bnx * ((y - by) + (int64_t)bny * (z - bz)));
-        const int64_t mu = cnt[i] - k0;
-        sv[i] = tot;
-        tot += (mu * 9 + 15) & ~int64_t(15);
-        blocks += mu;
-    }
-    sv[n] = tot;
-    if (!sym_fits(8, 1, P))
-        return fail(KLE_ERR_SUP, "symmetric storage: row boxes reach %d nodes (at most 5 supported)", P);
-    double *rowdiff = nullptr, *rowmax = nullptr;
-    if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
-        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
-        hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess) {
-        (void)hipGetLastError();
-        hipFree(rowdiff);
-        hipFree(rowmax);
-        sym_drop(A);
-        return fail(KLE_ERR_MEM, "out of device memory for symmetric storage");
-    }
-    KLE_HIP(hipMemcpy(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_sym_build, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, (int)Lx, (int)Ly,
-                       A->d_rowptr, A->d_rowcnt, A->d_rowbox, A->d_vptr, A->d_val, A->d_svptr, A->d_sval, rowdiff,
-                       rowmax);
-    KLE_HIP(hipGetLastError());
-    std::vector<double> hd(n), hm(n);
-    KLE_HIP(hipStreamSynchronize(c->stream));
-    KLE_HIP(hipMemcpy(hd.data(), rowdiff, sizeof(double) * n, hipMemcpyDeviceToHost));
-    KLE_HIP(hipMemcpy(hm.data(), rowmax, sizeof(double) * n, hipMemcpyDeviceToHost));
-    hipFree(rowdiff);
-    hipFree(rowmax);
-    double dmax = 0.0, vmax = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        dmax = std::max(dmax, hd[i]);
-        vmax = std::max(vmax, hm[i]);
-        if (std::isnan(hd[i])) dmax = INFINITY;
-    }
-    if (!(dmax <= 1e-12 * vmax)) {
-        sym_drop(A);
-        return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
-    }
-    A->sym_P = P;
-    // workspace for every tile shape (kle_set_tuning "spmv_sym_tx" / "spmv_sym_tz")
-    auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
-    int64_t wsn = 0;
-    for (int w = 0; w < 4; ++w) {
-        const int tx = w & 1 ? 16 : 8, tz = w & 2 ? 2 : 1;
-        A->sws_entries[w] = 0;
-        if (!sym_fits(tx, tz, P)) continue;
-        const SymGeo g = sym_geo(A, tx, tz);
-        wsn = std::max(wsn, (int64_t)g.ntx * g.nty * g.ntz * 3 * g.RX * g.RY * g.RZ);
-        // lattice entries of every tile region (written by the SpMV, read by the gather)
-        int64_t ents = 0;
-        for (int64_t t = 0; t < g.ntz; ++t)
-            for (int ty = 0; ty < g.nty; ++ty)
-                for (int tx2 = 0; tx2 < g.ntx; ++tx2)
-                    ents += span(tx2 * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz);
-        A->sws_entries[w] = ents;
-    }
-    if (hipMalloc(&A->d_sws, sizeof(double) * wsn) != hipSuccess) {
-        (void)hipGetLastError();
-        sym_drop(A);
-        return fail(KLE_ERR_MEM, "out of device memory for the symmetric SpMV workspace");
-    }
-    A->sblocks = blocks;
-    A->snvals = tot;
-    return 0;
-}
-
-static void launch_sym(const kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, hipStream_t st)
-{
-    const SymGeo g = sym_geo(A);
-    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz, RN = (int64_t)g.RX * g.RY * g.RZ;
-    const size_t lds = (size_t)(3 * RN * sizeof(double));
-    const dim3 grid((unsigned)ntiles), blk(64 * SYM_TY), ggrid((unsigned)((A->nrows + 255) / 256)), gblk(256);
-#define SYM_LAUNCH(TXW, TZW)                                                                                    \
-    do {                                                                                                        \
-        if (g_tune.spmv_sym_pf && g_tune.spmv_sym_waves == 4)                                                   \
-            hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, TZW, 4>), grid, dim3(256), lds, st, g, A->d_rowbox,       \
-                               A->d_svptr, A->d_sval, x->base, A->d_sws, istate, g_tune.spmv_sym_xcd);          \
-        else if (g_tune.spmv_sym_pf)                                                                            \
-            hipLaunchKernelGGL((k_nb_spmv_sym_pf<TXW, TZW, 8>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr, \
-                               A->d_sval, x->base, A->d_sws, istate, g_tune.spmv_sym_xcd);                      \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_nb_spmv_sym<TXW, 1>), grid, blk, lds, st, g, A->d_rowbox, A->d_svptr,         \
-                               A->d_sval, x->base, A->d_sws, istate);                                           \
-        hipLaunchKernelGGL((k_nb_sym_gather<TXW, TZW>), ggrid, gblk, 0, st, g, A->d_sws, y->d, istate);         \
-    } while (0)
-    if (g.TX == 16) {
-        if (g.TZ == 2) SYM_LAUNCH(16, 2);
-        else SYM_LAUNCH(16, 1);
-    } else {
-        if (g.TZ == 2) SYM_LAUNCH(8, 2);
-        else SYM_LAUNCH(8, 1);
-    }
-#undef SYM_LAUNCH
-}
-
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
     return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi &&
@@ -1354,8 +722,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
         KLE_TRY(c->tic("spmv", &ev));
         const int *rbox = A->spmv_struct ? A->d_rowbox : nullptr;
         if (A->d_sval && g_tune.spmv_sym && c->nranks == 1) {
-            launch_sym(A, x, y, istate, c->stream);
-            KLE_HIP(hipGetLastError());
+            KLE_TRY(sym_spmv(A, x, y, istate, c->stream));
         } else if (!overlap) {
             KLE_TRY(launch_nb_shape(A, RowMap{0, A->nrows, 0, 0}, rbox, x, y, istate, c->stream));
         } else {
@@ -1971,6 +1338,9 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
     B->d_aptr = nullptr;
     B->d_acol = nullptr;
     B->d_aval = nullptr;
+    // the symmetric copy is A's own: B starts on full storage (rebuilt below
+    // from the copied values when A had one)
+    sym_forget(B);
     if (A->kind == 0) {
         const size_t nv = std::max<int64_t>(A->nvals, 1);
         KLE_HIP(hipMalloc(&B->d_rowptr, sizeof(int) * (A->nrows + 1)));
@@ -2001,6 +1371,7 @@ int kle_mat_duplicate(const kle_mat *A, int copy_values, kle_mat **out)
         }
         if (copy_values) KLE_HIP(hipMemcpy(B->d_val, A->d_val, sizeof(double) * nv, hipMemcpyDeviceToDevice));
         else KLE_HIP(hipMemset(B->d_val, 0, sizeof(double) * nv));
+        if (copy_values && A->d_sval) KLE_TRY(sym_build(B));
     } else {
         if (!copy_values) std::fill(B->h_val.begin(), B->h_val.end(), 0.0);
         if (A->assembled) {
@@ -2075,14 +1446,34 @@ int kle_mat_get_format(const kle_mat *A, char *buf, int buflen)
     return 0;
 }
 
+int kle_mat_spmv_kernel(const kle_mat *A, char *buf, int buflen)
+{
+    KLE_ARG(A && buf && buflen > 0, "bad arg");
+    std::string s;
+    if (A->kind != 0) {
+        s = "k_aij_spmv<8,4>";
+    } else if (A->d_sval && g_tune.spmv_sym && A->ctx->nranks == 1) {
+        s = sym_kernel_name(A);
+    } else {
+        const int wv = spmv_waves(A), lay = A->vlayout;
+        const bool st = A->spmv_struct && A->d_rowbox, n33 = A->R == 3 && A->C == 3 && lay == 1;
+        if (n33 && st && wv == 8 && g_tune.spmv_x_lds && (7 + A->box_max) * A->box_max * A->box_max <= XL_CAP)
+            s = "k_nb_spmv_xl<8>";
+        else if (n33 && !st && wv == 8 && A->d_lid && g_tune.spmv_dict)
+            s = "k_nb_spmv_dict";
+        else
+            s = "k_nb_spmv<" + std::to_string(A->R) + "," + std::to_string(A->C) + "," + std::to_string(lay) + "," +
+                (st ? "true" : "false") + "," + std::to_string(n33 && wv == 8 ? 8 : SPMV_WAVES) + ">";
+    }
+    snprintf(buf, buflen, "%s", s.c_str());
+    return 0;
+}
+
 int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
 {
     KLE_ARG(A && bytes, "null arg");
     if (A->kind == 0 && A->d_sval && g_tune.spmv_sym && A->ctx->nranks == 1) {
-        // symmetric storage: the stored (upper) blocks, per row its value
-        // offset and box, x and y once, the tile partials written and read
-        *bytes = (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 +
-                 (double)A->sws_entries[(sym_geo(A).TX == 16) + 2 * (sym_geo(A).TZ == 2)] * 48.0;
+        *bytes = sym_spmv_bytes(A);
     } else if (A->kind == 0) {
         // bytes the SpMV must move: real blocks only (row padding is not counted);
         // the column stream unless the columns are computed from row boxes

@@ -439,6 +439,12 @@ class Mat:
         call("kle_mat_spmv_bytes", self._h, C.byref(b))
         return b.value
 
+    def spmvKernel(self):
+        """Kernel name(s) MatMult launches with the current tuning (kle_mat_spmv_kernel)."""
+        buf = C.create_string_buffer(96)
+        call("kle_mat_spmv_kernel", self._h, buf, 96)
+        return buf.value.decode()
+
     def createVecLeft(self):
         if self._mesh is not None:
             return Vec.fromMesh(self._mesh, self._rbs)

@@ -4,12 +4,13 @@
 The reference solves with the SPD K that MatFS.buildFS assembles
 (mat_fs.py:150-192: free-free element blocks plus a unit Dirichlet diagonal;
 kle_solver.py:33-37).  libkle keeps each row's blocks from its diagonal block
-on and lets every stored block serve row i and, transposed, row j.  The LDS
-accumulation commutes in a run-dependent order, so the tolerances are
-rounding-level, not bitwise:
+on and lets every stored block serve row i and, transposed, row j.
+Tolerances (the products sum in another order than the full storage):
   * SpMV vs the full-storage kernel and vs the exported PETSc CSR:
     <= 1e-14 relative (2-norm), max|diff| <= 1e-13 * max|y|
   * CG: iterations within 2 of the oracle's Jacobi-CG, solution within 1e-7
+  * the default kernel (spmv_sym_det 1: exact fixed-point transposed sums) is
+    bitwise reproducible: repeated products and solves are identical.
 """
 import numpy as np
 import pytest
@@ -39,8 +40,13 @@ def _mat(pa, nelem, ngl):
     return dom, mat
 
 
+KNOBS = ({}, {"spmv_sym_det": 0}, {"spmv_sym_kernel": 2}, {"spmv_sym_kernel": 2, "spmv_sym_det": 0},
+         {"spmv_sym_kernel": 2, "spmv_sym_ahead": 1}, {"spmv_sym_kernel": 2, "spmv_sym_waves": 16})
+DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_kernel": 2, "spmv_sym_waves": 0, "spmv_sym_ahead": 1}
+
+
 @pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([6, 5, 3], 2),
-                                       ([3, 4, 2], 6), ([1, 1, 1], 4)])
+                                       ([3, 4, 2], 6), ([1, 1, 1], 4), ([3, 3, 2], 7), ([2, 3, 3], 7)])
 def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     _, mat = _mat(pa, nelem, ngl)
     K = mat.K
@@ -58,25 +64,109 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
     from pynama_amd.runtime import set_tuning
     try:
-        # tile shapes: 8 x 8 rows of one or two planes (pipelined kernel), the
-        # first kernel version, 16-wide tiles
-        for knobs in ({}, {"spmv_sym_tz": 1}, {"spmv_sym_pf": 0}, {"spmv_sym_tx": 16},
-                      {"spmv_sym_tx": 16, "spmv_sym_tz": 1}, {"spmv_sym_waves": 4},
-                      {"spmv_sym_waves": 4, "spmv_sym_tz": 1}, {"spmv_sym_waves": 4, "spmv_sym_tx": 16}):
+        # the column walk (P <= 4) and the tile-per-workgroup kernel
+        # (fixed-point and fp64-atomic sums, 1 or 2 items ahead, 8 or 16 waves)
+        for knobs in KNOBS:
             for k, v in knobs.items():
                 set_tuning(k, v)
+            name = K.spmvKernel()
+            assert name.startswith("k_nb_spmv_sym_"), name
+            y1 = (K * x).getArray().copy()
             for _ in range(2):
-                y1 = (K * x).getArray().copy()
+                y2 = (K * x).getArray().copy()
                 for ref in (y0, yh):
-                    assert np.linalg.norm(y1 - ref) <= 1e-14 * np.linalg.norm(ref), knobs
-                    assert np.abs(y1 - ref).max() <= 1e-13 * np.abs(ref).max(), knobs
-            for k, v in (("spmv_sym_tz", 2), ("spmv_sym_pf", 1), ("spmv_sym_tx", 8), ("spmv_sym_waves", 8)):
+                    assert np.linalg.norm(y2 - ref) <= 1e-14 * np.linalg.norm(ref), knobs
+                    assert np.abs(y2 - ref).max() <= 1e-13 * np.abs(ref).max(), knobs
+                if "true" in name:  # fixed-point transposed sums: bitwise reproducible
+                    np.testing.assert_array_equal(y2, y1)
+            for k, v in DEFAULTS.items():
                 set_tuning(k, v)
     finally:
-        for k, v in (("spmv_sym_tz", 2), ("spmv_sym_pf", 1), ("spmv_sym_tx", 8), ("spmv_sym_waves", 8)):
+        for k, v in DEFAULTS.items():
             set_tuning(k, v)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
+    np.testing.assert_array_equal((K * x).getArray(), y0)
+
+
+def test_symmetric_spmv_edge_inputs(pa):
+    """Zero x gives exactly zero; a NaN in x propagates (the fixed-point path
+    must not turn it into a finite number); huge and tiny scales keep their
+    relative accuracy (the per-tile scale follows max|x|)."""
+    _, mat = _mat(pa, [4, 3, 3], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    assert K.isSymmetricStorage()
+    x = K.createVecRight()
+    x.setArray(np.zeros(x.getLocalSize()))
+    assert not np.any((K * x).getArray())
+    xa = np.random.default_rng(3).uniform(-1, 1, x.getLocalSize())
+    ip, ix, d = K.getValuesCSR()
+    A = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa)))
+    for scale in (1e-200, 1e-8, 1.0, 1e150):
+        x.setArray(xa * scale)
+        y = (K * x).getArray()
+        yh = A @ (xa * scale)
+        assert np.linalg.norm(y - yh) <= 1e-14 * np.linalg.norm(yh), scale
+    xb = xa.copy()
+    xb[len(xb) // 2] = np.nan
+    x.setArray(xb)
+    y = (K * x).getArray()
+    assert np.isnan(y).any()
+
+
+def test_symmetric_cg_is_reproducible(pa):
+    """With the fixed-point transposed sums (default) two solves of the same
+    system take the same iterations and give bitwise the same solution."""
+    from pynama_amd.runtime import get_tuning
+    assert get_tuning("spmv_sym_det") == 1
+    _, mat = _mat(pa, [6, 5, 4], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    b = K.createVecLeft()
+    b.setArray(np.random.default_rng(7).uniform(-1, 1, b.getLocalSize()))
+    out = []
+    for _ in range(2):
+        ksp = pa.petsc.KSP().create()
+        ksp.setType("cg")
+        pc = pa.petsc.PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+        ksp.setCGSingleReduction(True)
+        ksp.setOperators(K)
+        x = K.createVecRight()
+        ksp.solve(b, x)
+        out.append((ksp.getIterationNumber(), x.getArray().copy()))
+    assert out[0][0] == out[1][0]
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+def test_duplicate_of_symmetric_matrix_owns_its_storage(pa):
+    """Mat.duplicate(copy=True) of a matrix with symmetric storage gets its
+    own copy (rebuilt from the copied values): axpy on the duplicate drops
+    only the duplicate's, K keeps multiplying correctly, and destroying both
+    frees each buffer once (the copy used to share K's buffers)."""
+    _, mat = _mat(pa, [4, 3, 3], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    x = K.createVecRight()
+    xa = np.random.default_rng(5).uniform(-1, 1, x.getLocalSize())
+    x.setArray(xa)
+    y0 = (K * x).getArray().copy()
+    B = K.duplicate(copy=True)
+    assert B.isSymmetricStorage() and K.isSymmetricStorage()
+    np.testing.assert_array_equal((B * x).getArray(), y0)
+    B.axpy(1.0, K)  # B = 2 K (drops B's symmetric copy)
+    assert not B.isSymmetricStorage() and K.isSymmetricStorage()
+    np.testing.assert_array_equal((K * x).getArray(), y0)
+    yb = (B * x).getArray()
+    assert np.abs(yb - 2 * y0).max() <= 1e-13 * np.abs(y0).max()
+    Z = K.duplicate(copy=False)  # zero values: full storage, product 0
+    assert not Z.isSymmetricStorage()
+    assert not np.any((Z * x).getArray())
+    B.destroy()
+    Z.destroy()
     np.testing.assert_array_equal((K * x).getArray(), y0)
 
 
@@ -139,8 +229,10 @@ def test_symmetric_storage_follows_value_changes(pa):
 
 
 def test_symmetric_storage_refused_where_it_does_not_apply(pa):
-    """Rw (not symmetric), a 2-D K (2x2 blocks) and a p = 6 K keep the full storage; setOption leaves them as they are,
-    as PETSc ignores options a format does not use."""
+    """Rw (not symmetric) and a 2-D K (2x2 blocks) keep the full storage;
+    setOption leaves them as they are, as PETSc ignores options a format does
+    not use.  (p = 6 is supported since round 3: its 20 x 20 x 8-node tile
+    regions take one 16-wave workgroup per CU.)"""
     _, mat = _mat(pa, [3, 3, 2], 4)
     for A in (mat.Rw,):
         A.setOption(A.Option.SPD, True)
@@ -155,10 +247,10 @@ def test_symmetric_storage_refused_where_it_does_not_apply(pa):
     m2.build(buildOperators=False)
     m2.K.setOption(m2.K.Option.SPD, True)
     assert not m2.K.isSymmetricStorage()
-    # p = 6 row boxes reach 6 nodes: beyond the tile regions' LDS
-    _, m6 = _mat(pa, [3, 3, 3], 7)
+    _, m6 = _mat(pa, [2, 2, 2], 7)
     m6.K.setOption(m6.K.Option.SPD, True)
-    assert not m6.K.isSymmetricStorage()
+    assert m6.K.isSymmetricStorage()
+    assert m6.K.spmvKernel().startswith("k_nb_spmv_sym_xl<16,")  # (P = 6: no column walk)
 
 
 def test_assembly_turns_symmetric_storage_on_from_the_threshold(pa):

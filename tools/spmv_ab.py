@@ -1,0 +1,76 @@
+"""In-process A/B of SpMV tuning knobs on config 2's K (or --nelem/--ngl):
+variants alternate block by block in ONE process; each block times --reps
+products with HIP events around every SpMV launch (the gather included).
+Knobs that are timing probes give wrong products on purpose.
+
+  python tools/spmv_ab.py '[{},{"spmv_sym_probe":1}]' [--nelem 20,16,16] [--reps 4] [--its 100]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants")
+    ap.add_argument("--nelem", default="20,16,16")
+    ap.add_argument("--ngl", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--its", type=int, default=100)
+    a = ap.parse_args()
+    import numpy as np
+    import pynama_amd as pa
+    from pynama_amd.runtime import get_tuning, set_tuning
+    from cg_ab import DEFAULTS
+    ctx = pa.get_ctx()
+    nelem = [int(v) for v in a.nelem.split(",")]
+    cfg = {"domain": {"ngl": a.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * 3, "upper": [1.0] * 3}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    x = K.createVecRight()
+    y = K.createVecLeft()
+    x.setArray(np.random.default_rng(1).uniform(-1, 1, x.getLocalSize()))
+    variants = json.loads(a.variants)
+    res = {i: [] for i in range(len(variants))}
+    for rep in range(a.reps):
+        for i, v in enumerate(variants):
+            for k, val in v.items():
+                set_tuning(k, val)
+            name = K.spmvKernel()
+            for _ in range(5):
+                K.mult(x, y)
+            ctx.synchronize()
+            ctx.set_profiling(True, only="spmv")
+            ctx.reset_stats()
+            for _ in range(a.its):
+                K.mult(x, y)
+            ctx.synchronize()
+            c, ms = ctx.kernel_stats("spmv")
+            ctx.set_profiling(False)
+            for k in v:
+                if k in DEFAULTS:
+                    set_tuning(k, DEFAULTS[k])
+                elif k == "spmv_sym_probe":
+                    set_tuning(k, 0)
+            res[i].append(ms / c)
+            print(json.dumps({"rep": rep, "variant": v, "kernel": name, "spmv_ms": ms / c}), flush=True)
+    print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]), "min_ms": min(res[i])}
+                                  for i, v in enumerate(variants)], "nelem": nelem, "ngl": a.ngl,
+                      "spmv_bytes": K.spmvBytes()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
