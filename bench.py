@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--msh", type=str, default=None, help="read this Gmsh 4.1 file instead (implies unstructured)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="OpenMP threads of the CPU baseline: 0 the runtime default (OMP_NUM_THREADS), "
+                         "-1 every thread of the affinity mask")
     ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--no-aij", dest="aij", action="store_false",
                     help="skip the scalar-CSR (aij) SpMV leg (default: timed at N = 1)")
@@ -394,7 +397,7 @@ def main():
 
     cpu = None
     if rank == 0 and nranks == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(K, b, args.cpu_seconds)
+        cpu = cpu_baseline(K, b, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         stream = ctx.stream_copy_gbps(1 << 30, 10)
@@ -496,13 +499,18 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(K, b, seconds):
+def cpu_baseline(K, b, seconds, nthreads=0):
     """Oracle CSR CG (OpenMP) on the same matrix: bounded sample of ~`seconds`
-    on all threads the process may use, ~seconds/3 on one thread, plus the
-    host STREAM triad at both thread counts."""
+    on the OpenMP thread count (nthreads: 0 the runtime default, -1 the
+    affinity mask, else that many), ~seconds/3 on one thread, plus the host
+    STREAM triad at both thread counts."""
     import numpy as np
 
     from oracle import oracle as O
+    if nthreads < 0:
+        nthreads = len(os.sched_getaffinity(0))
+    if nthreads > 0:
+        O.set_threads(nthreads)
     ip, ix, d = K.getValuesCSR()
     A = O.CSR.from_arrays(ip, ix, d, int(ip.shape[0] - 1))
     del ip, ix, d
@@ -524,12 +532,18 @@ def cpu_baseline(K, b, seconds):
     its1, el1 = sample(seconds / 3, 2)
     triad1 = O.stream_triad_gbps()
     O.set_threads(threads)
-    return {"value": its / el, "unit": "CG iters/s", "cores": threads, "kind": "port",
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    reason = None
+    if affinity is not None and threads < affinity:
+        omp = os.environ.get("OMP_NUM_THREADS")
+        reason = (f"OMP_NUM_THREADS={omp} in the environment: the GPU box's CPU share for one GPU "
+                  f"(the affinity mask lists all {affinity} host threads, shared with the other GPUs' jobs)"
+                  if omp else f"OpenMP runtime default of {threads} threads")
+    return {"value": its / el, "unit": "CG iters/s", "cores": threads, "cores_reason": reason, "kind": "port",
             "sample": f"{its} fixed CG+Jacobi iterations of oracle/kle_oracle.c (CSR, OpenMP) on the same "
                       f"assembled K ({A.nnz} nnz), {el:.1f} s; 1 thread: {its1} iterations, {el1:.1f} s",
             "model": _cpu_model(), "nproc": os.cpu_count(),
-            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
-            "value_1core": its1 / el1, "stream_triad_gbps": triad, "stream_triad_gbps_1core": triad1,
+            "affinity": affinity, "value_1core": its1 / el1, "stream_triad_gbps": triad, "stream_triad_gbps_1core": triad1,
             "spmv_gbps_equiv": 12.0 * A.nnz * its / el / 1e9}
 
 

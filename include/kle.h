@@ -81,11 +81,12 @@ const char *kle_last_error(void);
  * before the prologue; 0 off), "spmv_sym" (1 default: matrices holding
  * symmetric storage run the symmetric SpMV; 0 the full storage),
  * "spmv_sym_min_rows" (node rows from which kle_assemble_kle gives the
- * single-rank K symmetric storage; default 64000), "spmv_sym_kernel" (2
- * default: x staged in LDS; 1 the round-2 kernel gathering x from global
- * memory), "spmv_sym_det" (1 default: the transposed adds as exact
- * fixed-point sums, y bitwise reproducible; 0 fp64 LDS atomics),
- * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup). */
+ * single-rank K symmetric storage; default 64000), "spmv_sym_det" (1
+ * default: the transposed adds as exact fixed-point sums, y bitwise
+ * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
+ * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_sym_probe"
+ * (timing probes that skip parts of the symmetric SpMV: wrong results on
+ * purpose; 0 default). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
@@ -342,7 +343,8 @@ int kle_mat_is_structured(const kle_mat *A, int *on);
  * storage stays (getRow, CSR export); any value change (diagonalScale, axpy,
  * setValues/assemble) drops the symmetric copy.  kle_assemble_kle turns it on
  * for K (tuning "spmv_sym", "spmv_sym_min_rows").  Results agree with the
- * full-storage SpMV to rounding, not bitwise. */
+ * full-storage SpMV to rounding (a different summation order); with the
+ * default "spmv_sym_det" they are bitwise reproducible run to run. */
 int kle_mat_set_symmetric(kle_mat *A, int on);
 int kle_mat_get_symmetric(const kle_mat *A, int *on);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in

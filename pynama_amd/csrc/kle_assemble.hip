@@ -1873,11 +1873,11 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     tm.lap(nbatch > 1 ? "assemble_kle: element batches + gathers" : "assemble_kle: elements + gathers");
     owned.keep = true;
     // K is SPD (MatFS.buildFS: free-free blocks + unit Dirichlet diagonal):
-    // one-rank structured K of >= spmv_sym_min_rows rows keeps its upper
-    // triangle only for the SpMV (kle_mat_set_symmetric); a K the symmetric
-    // path cannot take keeps the full-storage kernels
-    if (g_tune.spmv_sym && ctx->nranks == 1 && mK->nrows >= g_tune.spmv_sym_min_rows && mK->R == 3 &&
-        mK->d_rowbox) {
+    // a structured K (one rank or z slabs) of >= spmv_sym_min_rows node rows
+    // in all keeps its upper triangle only for the SpMV
+    // (kle_mat_set_symmetric; collective, the same decision on every rank); a
+    // K the symmetric path cannot take keeps the full-storage kernels
+    if (g_tune.spmv_sym && mK->m_global / 3 >= g_tune.spmv_sym_min_rows && mK->R == 3 && mK->C == 3) {
         if (sym_build(mK)) (void)kle_last_error();
         tm.lap("assemble_kle: symmetric storage");
     }

@@ -452,6 +452,37 @@ int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local,
     return 0;
 }
 
+// Reverse halo of the symmetric SpMV (slab partitions): the partial sums of my
+// upper ghost rows (n_send entries) go to hi_rank, which owns those rows; the
+// lower neighbour's sums for my lowest rows (n_recv entries) arrive from
+// lo_rank.  The forward halo's pairs, one direction each.
+int halo_reverse(kle_ctx *ctx, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
+                 int lo_rank, hipStream_t st)
+{
+    if (ctx->nranks == 1) return 0;
+    if (!st) st = ctx->stream;
+    const int64_t ns = hi_rank >= 0 ? n_send : 0, nr = lo_rank >= 0 ? n_recv : 0;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(ctx->tic("halo_rev", &ev, st));
+    if (ctx->comm) {
+        KLE_NCCL(ncclGroupStart());
+        if (ns) KLE_NCCL(ncclSend(send_hi, ns, ncclDouble, hi_rank, ctx->comm, st));
+        if (nr) KLE_NCCL(ncclRecv(recv_lo, nr, ncclDouble, lo_rank, ctx->comm, st));
+        KLE_NCCL(ncclGroupEnd());
+    } else {
+        KLE_TRY(stage_reserve(ctx, ns + nr));
+        double *hs = ctx->h_stage, *hr = hs + ns;
+        if (ns) KLE_HIP(hipMemcpyAsync(hs, send_hi, sizeof(double) * ns, hipMemcpyDeviceToHost, st));
+        KLE_HIP(hipStreamSynchronize(st));
+        if (ctx->hcomm.halo(nullptr, 0, lo_rank, hs, ns, hi_rank, hr, nr, nullptr, 0, ctx->hcomm.user))
+            return fail(KLE_ERR_COMM, "host halo callback failed (reverse halo)");
+        if (nr) KLE_HIP(hipMemcpyAsync(recv_lo, hr, sizeof(double) * nr, hipMemcpyHostToDevice, st));
+        KLE_HIP(hipStreamSynchronize(st));
+    }
+    KLE_TRY(ctx->toc("halo_rev", &ev, st));
+    return 0;
+}
+
 }  // namespace kle
 
 using namespace kle;
@@ -535,9 +566,6 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym: 0 or 1");
         g_tune.spmv_sym = value;
-    } else if (k == "spmv_sym_kernel") {
-        KLE_ARG(value == 2 || value == 3, "spmv_sym_kernel: 2 (tile per workgroup) or 3 (column walk)");
-        g_tune.spmv_sym_kernel = value;
     } else if (k == "spmv_sym_det") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_det: 0 or 1");
         g_tune.spmv_sym_det = value;
@@ -547,12 +575,6 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_probe") {
         KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
         g_tune.spmv_sym_probe = value;
-    } else if (k == "spmv_sym_cw_tile") {
-        KLE_ARG(value >= 0, "spmv_sym_cw_tile: >= 0");
-        g_tune.spmv_sym_cw_tile = value;
-    } else if (k == "spmv_sym_ahead") {
-        KLE_ARG(value == 1 || value == 2, "spmv_sym_ahead: 1 or 2");
-        g_tune.spmv_sym_ahead = value;
     } else if (k == "spmv_sym_min_rows") {
         KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
         g_tune.spmv_sym_min_rows = value;
@@ -583,11 +605,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "upd_preload") *value = g_tune.upd_preload;
     else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
     else if (k == "spmv_sym") *value = g_tune.spmv_sym;
-    else if (k == "spmv_sym_kernel") *value = g_tune.spmv_sym_kernel;
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
-    else if (k == "spmv_sym_ahead") *value = g_tune.spmv_sym_ahead;
-    else if (k == "spmv_sym_cw_tile") *value = g_tune.spmv_sym_cw_tile;
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);

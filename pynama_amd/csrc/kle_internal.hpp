@@ -233,19 +233,13 @@ struct kle_mat {
     int64_t dict_len = 0;
     double *d_val = nullptr;   // [nblocks*R*C], per row SoA [a][b][k]
     // symmetric storage (kle_mat_set_symmetric = MatSetOption(MAT_SPD), PETSc
-    // SBAIJ; single-rank structured 3x3 rows): each row's blocks from its
-    // diagonal block on, in the chunked layout; per-tile partial sums d_sws
+    // SBAIJ; structured 3x3 rows, one rank or z slabs): each row's blocks from
+    // its diagonal block on, in the chunked layout; per-tile partial sums d_sws
     double *d_sval = nullptr;
     int64_t *d_svptr = nullptr;
     double *d_sws = nullptr;
     int *d_stile_e = nullptr;  // per tile: 2^e bounds its transposed row sums (fixed-point scale, k_sym_bound)
-    // column walk (k_nb_spmv_sym_cw): runs, chunk -> run range, per-run scale
-    // exponents, overlap-slab index per (column, plane), partials
-    void *d_cw_runs = nullptr;
-    int *d_cw_chunk = nullptr, *d_cw_rune = nullptr, *d_cw_ovl = nullptr;
-    double *d_cw_wsA = nullptr, *d_cw_wsB = nullptr;
-    int cw_nchunk = 0;
-    int64_t cw_entries = 0;  // lattice entries of the column partials per SpMV (written, read)
+    double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
     int sym_P = 0;
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
@@ -298,7 +292,9 @@ int nb_build_dict(kle_mat *A);  // kle_mat.hip
 int sym_build(kle_mat *A);
 void sym_drop(kle_mat *A);
 void sym_forget(kle_mat *A);  // null the symmetric-storage pointers of a struct copy (no free)
-int sym_spmv(const kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, hipStream_t st);
+int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);  // N > 1: both halos included
+int halo_reverse(kle_ctx *ctx, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
+                 int lo_rank, hipStream_t st);  // kle_core.hip
 std::string sym_kernel_name(const kle_mat *A);
 double sym_spmv_bytes(const kle_mat *A);
 // Performance knobs (kle_set_tuning): every setting gives correct results;
@@ -309,14 +305,11 @@ struct Tuning {
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
     int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
-    int spmv_sym = 1;  // SBAIJ-style symmetric storage for the single-rank KLE K of >= spmv_sym_min_rows rows; 0 off
+    int spmv_sym = 1;  // SBAIJ-style symmetric storage for the KLE K of >= spmv_sym_min_rows node rows (all ranks); 0 off
     int spmv_sym_min_rows = 64000;
-    int spmv_sym_kernel = 2;  // symmetric SpMV: 2 one tile per workgroup (k_nb_spmv_sym_xl), 3 column walk (k_nb_spmv_sym_cw, P <= 4)
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 4 LDS x reads, 8 partial stores, 16 x fill loads
-    int spmv_sym_ahead = 1;       // items of k_nb_spmv_sym_xl whose value loads are in flight while one is summed: 1 or 2
-    int spmv_sym_cw_tile = 2000;  // column-walk chunking: a tile transition's cost in stored blocks (read at build)
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)
 };

@@ -614,7 +614,10 @@ int nb_build_dict(kle_mat *A)
 
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
-    return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap && A->int_lo < A->int_hi &&
+    // (the symmetric SpMV's two halos run on the comm stream whatever the
+    // slab's interior: sym_spmv)
+    return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap &&
+           (A->int_lo < A->int_hi || (A->d_sval && g_tune.spmv_sym)) &&
            (x->lo_rank >= 0 || x->hi_rank >= 0 || (x->plan && !x->plan->peers.empty()));
 }
 
@@ -712,6 +715,13 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
 {
     kle_ctx *c = A->ctx;
     std::pair<hipEvent_t, hipEvent_t> ev;
+    if (A->kind == 0 && A->d_sval && g_tune.spmv_sym) {
+        // symmetric storage (both halos of N > 1 inside)
+        KLE_TRY(c->tic("spmv", &ev));
+        KLE_TRY(sym_spmv(A, x, y, istate));
+        KLE_TRY(c->toc("spmv", &ev));
+        return 0;
+    }
     if (A->kind == 0) {
         // N > 1: rows [int_lo, int_hi) read no ghost entry, so they run while the
         // halo is in flight on the comm stream; the ghost-dependent rows follow
@@ -721,9 +731,7 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
                                   x->send_lo, x->send_hi, nullptr, x->plan.get()));
         KLE_TRY(c->tic("spmv", &ev));
         const int *rbox = A->spmv_struct ? A->d_rowbox : nullptr;
-        if (A->d_sval && g_tune.spmv_sym && c->nranks == 1) {
-            KLE_TRY(sym_spmv(A, x, y, istate, c->stream));
-        } else if (!overlap) {
+        if (!overlap) {
             KLE_TRY(launch_nb_shape(A, RowMap{0, A->nrows, 0, 0}, rbox, x, y, istate, c->stream));
         } else {
             SideBusy busy(c);  // the halo (and, in pipecg, the reduction) run beside both launches
@@ -1452,7 +1460,7 @@ int kle_mat_spmv_kernel(const kle_mat *A, char *buf, int buflen)
     std::string s;
     if (A->kind != 0) {
         s = "k_aij_spmv<8,4>";
-    } else if (A->d_sval && g_tune.spmv_sym && A->ctx->nranks == 1) {
+    } else if (A->d_sval && g_tune.spmv_sym) {
         s = sym_kernel_name(A);
     } else {
         const int wv = spmv_waves(A), lay = A->vlayout;
@@ -1472,7 +1480,7 @@ int kle_mat_spmv_kernel(const kle_mat *A, char *buf, int buflen)
 int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
 {
     KLE_ARG(A && bytes, "null arg");
-    if (A->kind == 0 && A->d_sval && g_tune.spmv_sym && A->ctx->nranks == 1) {
+    if (A->kind == 0 && A->d_sval && g_tune.spmv_sym) {
         *bytes = sym_spmv_bytes(A);
     } else if (A->kind == 0) {
         // bytes the SpMV must move: real blocks only (row padding is not counted);

@@ -29,8 +29,15 @@ namespace kle {
 // written and read once.
 constexpr int SYM_TX = 8, SYM_TY = 8, SYM_TZ = 2;
 constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (one pass over the region)
+// Lattices: the rows are the owned Lx x Ly x Lz nodes; the columns add zo
+// lattice planes of lower ghosts before them and hp of upper ghosts after
+// them (slab partitions, N > 1: ext layout [lower ghosts | owned | upper]).
+// Row boxes (d_rowbox) are in column (ext) coordinates.  The upper triangle
+// of an owned row never reaches a lower ghost; the blocks that reach upper
+// ghosts add their transposed parts to ghost rows, whose partials go back to
+// the owner (sym_spmv's reverse halo).
 struct SymGeo {
-    int Lx, Ly, Lz, P, TX, TZ, RX, RY, RZ, ntx, nty, ntz;
+    int Lx, Ly, Lz, P, TX, TZ, RX, RY, RZ, ntx, nty, ntz, zo, hp;
 };
 
 __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
@@ -49,7 +56,7 @@ __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t 
 
 // Copy each row's upper tail into the symmetric layout and measure
 // max |B_ij - B_ji^T| per row (the stored triangle must describe the matrix).
-__global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly, const int *__restrict__ rowptr,
+__global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly, int zo, const int *__restrict__ rowptr,
                                                    const int *__restrict__ rowcnt, const int *__restrict__ rowbox,
                                                    const int64_t *__restrict__ vptr, const double *__restrict__ val,
                                                    const int64_t *__restrict__ svptr, double *__restrict__ sval,
@@ -62,6 +69,7 @@ __global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly
     const int z = (int)(i / Lxy), y = (int)((i - z * Lxy) / Lx), x = (int)(i - z * Lxy - (int64_t)y * Lx);
     int bx, by, bz, bnx, bny, bnz;
     sym_box(rowbox, i, Lx, Lxy, bx, by, bz, bnx, bny, bnz);
+    bz -= zo;  // (owned coordinates)
     const int m = rowcnt ? rowcnt[i] : rowptr[i + 1] - rowptr[i], mp = rowptr[i + 1] - rowptr[i];
     const int k0 = (x - bx) + bnx * ((y - by) + bny * (z - bz));
     const int mu = m - k0;
@@ -81,8 +89,10 @@ __global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly
         const int bnxy = bnx * bny;
         const int kz = k / bnxy, ky = (k - kz * bnxy) / bnx, kx = k - kz * bnxy - ky * bnx;
         const int64_t j = (bx + kx) + (int64_t)Lx * (by + ky) + Lxy * (bz + kz);
+        if (j >= nrows) continue;  // an upper ghost row (N > 1): sym_build checks those by a product
         int cx, cy, cz, cnx, cny, cnz;
         sym_box(rowbox, j, Lx, Lxy, cx, cy, cz, cnx, cny, cnz);
+        cz -= zo;
         if (x < cx || x >= cx + cnx || y < cy || y >= cy + cny || z < cz || z >= cz + cnz) {
             dmax = INFINITY;  // (i, j) stored but (j, i) not in the pattern
             continue;
@@ -233,34 +243,13 @@ __device__ __forceinline__ void sym_wait9(double *v)
                  : "i"(N));
 }
 
-// Single loads the compiler does not count (inline asm): uniform base + 32-bit
-// byte offset.  The caller waits with sym_waitn and names the registers.
-__device__ __forceinline__ void asm_ld_f64(double &v, const void *base, unsigned off)
-{
-    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
-}
-__device__ __forceinline__ void asm_ld_i32(int &v, const void *base, unsigned off)
-{
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void sym_waitn()
-{
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-template <class T>
-__device__ __forceinline__ void asm_touch(T &v)  // after a wait: v's register holds the data now
-{
-    asm volatile("" : "+v"(v));
-}
-
-template <int WV, bool DET, int AHEAD>
+template <int WV, bool DET>
 __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const int *__restrict__ rowbox,
                                                              const int64_t *__restrict__ svptr,
                                                              const double *__restrict__ sval,
                                                              const double *__restrict__ x, double *__restrict__ ws,
                                                              const int *__restrict__ tile_e,
-                                                             const int *__restrict__ istate, int probe)
+                                                             const int *__restrict__ istate, int probe, int t0)
 {
     // LDS: x [3][RN] | y [3][RN + 64] (DET: int64; 64 dummy slots per
     // component take the adds of masked lanes) | direct row sums [3][TR]
@@ -271,7 +260,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     constexpr int NS = NQ * TZ;               // row slots per wave
     const int RN = g.RX * g.RY * g.RZ, RS = RN + 64;
     double *xl = lds, *yl = lds + 3 * RN, *yd = lds + 3 * RN + 3 * RS;
-    const int64_t t = blockIdx.x;
+    const int64_t t = (int64_t)blockIdx.x + t0;  // (N > 1: tiles [t0, ...) of one launch)
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;
@@ -319,8 +308,8 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     for (int f = 0; f < SYM_FILL; ++f) {
         const int l = fl0 + f * fstep;
         const int rz = l / g.RY, ry = l - rz * g.RY;
-        const bool ok = fx_ok && l < NL && oy + ry >= 0 && oy + ry < g.Ly && tz + rz < g.Lz;
-        const int64_t node = ok ? (int64_t)(ox + frx) + (int64_t)g.Lx * (oy + ry) + Lxy * (tz + rz) : 0;
+        const bool ok = fx_ok && l < NL && oy + ry >= 0 && oy + ry < g.Ly && tz + rz < g.Lz + g.hp;
+        const int64_t node = ok ? (int64_t)(ox + frx) + (int64_t)g.Lx * (oy + ry) + Lxy * (g.zo + tz + rz) : 0;
         const double v = x[3 * node + fcc];
         fv[f] = ok ? v : 0.0;
     }
@@ -335,6 +324,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const int64_t rem = base - (int64_t)R.bz * Lxy;
         R.by = (int)(rem / g.Lx);
         R.bx = (int)(rem - (int64_t)R.by * g.Lx);
+        R.bz -= g.zo;  // (owned coordinates)
         R.bnx = d & 255;
         const int bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
         R.bnxy = R.bnx * bny;
@@ -390,10 +380,11 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         xv[2] = xl[2 * RN + rr];
     };
     // 3. items = (row, pass of 64 blocks).  The issue cursor (row I, slot xi,
-    // pass ki) runs AHEAD items in front of the compute cursor (row C, slot
-    // xc, pass kc); past the wave's last item it stays there, re-reading it
+    // pass ki) runs one item in front of the compute cursor (row C, slot xc,
+    // pass kc); past the wave's last item it stays there, re-reading it
     // (cache hits), so every step issues exactly 9 loads and the wait for the
-    // item being summed is a fixed vmcnt(9 AHEAD).  A wave without rows in
+    // item being summed is a fixed vmcnt(9).  (Two items ahead measured
+    // slower in rounds 2 and 3.)  A wave without rows in
     // this tile (16-wave tiles on a lattice edge) loads a dummy item.
     int xi = next_slot(0), ki = 0;
     const bool any = xi < NS;
@@ -429,13 +420,9 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const int l = fl0 + f * fstep;  // (unused slots store into a dummy y slot: no branch)
         xl[fl0 < fstep && l < NL ? fcc * RN + frx + g.RX * l : 4 * RN + lane] = fv[f];
     }
-    double v0[9], v1[9], v2[9];
-    int r0, r1 = 0, r2 = 0;
+    double v0[9], v1[9];
+    int r0, r1 = 0;
     load_v(I, ki, v0, r0);  // in flight across the barrier
-    if (AHEAD == 2) {
-        issue_next();
-        load_v(I, ki, v1, r1);
-    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // LDS stores done (lgkmcnt 0); the value loads stay in flight
     __builtin_amdgcn_s_barrier();
     double S = 1.0, invS = 1.0;
@@ -469,8 +456,8 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         int xc = next_slot(0), kc = 0;
         slot_row(xc, C);  // (x_i from LDS, now that the fill has landed)
         double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-        // one item: issue the item AHEAD in front into vn, wait for vv (the
-        // AHEAD items issued after it stay in flight), sum it
+        // one item: issue the next item into vn, wait for vv (the next
+        // item's loads stay in flight), sum it
         auto step = [&](double *vv, const int rr, double *vn, int &rn) {
             issue_next();
             load_v(I, ki, vn, rn);
@@ -479,7 +466,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
                 xv[0] = xv[1] = xv[2] = C.x0;
             else
                 load_x(rr, xv);  // LDS latency overlaps the wait
-            sym_wait9<9 * AHEAD>(vv);
+            sym_wait9<9>(vv);
             // B x_j into the row, B^T x_i into row j (lanes past the row's end
             // and the diagonal block add into their dummy slot)
             const int kk = kc + lane;
@@ -523,18 +510,12 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
             slot_row(xc, C);
             return true;
         };
-        if (AHEAD == 1) {
-            while (step(v0, r0, v1, r1) && step(v1, r1, v0, r0)) {
-            }
-        } else {
-            while (step(v0, r0, v2, r2) && step(v1, r1, v0, r0) && step(v2, r2, v1, r1)) {
-            }
+        while (step(v0, r0, v1, r1) && step(v1, r1, v0, r0)) {
         }
     }
     // the last (re-read) loads land before their registers are reused
     sym_wait9<0>(v0);
     sym_wait9<0>(v1);
-    if (AHEAD == 2) sym_wait9<0>(v2);
     __syncthreads();
     // 4. the tile's partial sums: region nodes inside the lattice
     double *dst = ws + ((probe & 64) ? (t & 7) : t) * 3 * (int64_t)RN;  // (probe 64: every tile into 8 slabs)
@@ -542,7 +523,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     for (int k = (probe & 8) ? RN : threadIdx.x; k < RN; k += NT) {
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
         const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
-        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
+        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz + g.hp) continue;
         const bool own = rx >= g.P && rx < g.P + SYM_TX && ry >= g.P && ry < g.P + SYM_TY && rz < TZ;
         const int sl = (rx - g.P) + SYM_TX * ((ry - g.P) + SYM_TY * rz);
 #pragma unroll
@@ -592,14 +573,14 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
     for (int k = threadIdx.x; k < RN; k += 256) {
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
         const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
-        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz) continue;
+        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz + g.hp) continue;
         double s = 0.0;
         for (int r = 0; r < TR; ++r) {
             const int d = sd[r];
             if (!d) continue;
             const int64_t base = sb[r];
-            const int bz = (int)(base / Lxy), by = (int)((base - bz * Lxy) / g.Lx);
-            const int bx = (int)(base - bz * Lxy - (int64_t)by * g.Lx);
+            const int bze = (int)(base / Lxy), by = (int)((base - bze * Lxy) / g.Lx);
+            const int bx = (int)(base - bze * Lxy - (int64_t)by * g.Lx), bz = bze - g.zo;
             const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
             if (gx < bx || gx >= bx + bnx || gy < by || gy >= by + bny || gz < bz || gz >= bz + bnz) continue;
             const int xi = x0 + (r & 7), yi = y0 + ((r >> 3) & 7), zi = tz + (r >> 6);
@@ -634,15 +615,20 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
 }
 
 // y_j = sum of the partials of the tiles whose regions contain row j, in
-// ascending (z, y, x) tile order.
+// ascending (z, y, x) tile order, for the lattice rows [j0, j1) -- owned rows
+// and (N > 1) the upper ghost rows, whose sums go to gsend (the reverse halo's
+// send buffer, ghost row j at gsend[3 (j - n)]).  The first nrecv entries of y
+// add the lower neighbour's sums for them (grecv, its upper ghost rows) last.
 template <int TXW, int TZ>
 __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *__restrict__ ws, double *__restrict__ y,
+                                                       double *__restrict__ gsend, const double *__restrict__ grecv,
+                                                       int64_t nrecv, int64_t j0, int64_t j1,
                                                        const int *__restrict__ istate)
 {
     if (istate && istate[I_REASON] != 0) return;
     const int64_t Lxy = (int64_t)g.Lx * g.Ly, n = Lxy * g.Lz;
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+    const int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= j1) return;
     const int jz = (int)(j / Lxy), jy = (int)((j - jz * Lxy) / g.Lx), jx = (int)(j - jz * Lxy - (int64_t)jy * g.Lx);
     const int RN = g.RX * g.RY * g.RZ;
     // tiles whose [t*T - P, t*T - P + R) contains the coordinate
@@ -660,551 +646,18 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
                 s1 += p[RN];
                 s2 += p[2 * RN];
             }
-    y[3 * j] = s0;
-    y[3 * j + 1] = s1;
-    y[3 * j + 2] = s2;
-}
-
-// ---------------------------------------------------------------------------
-// Column-walk symmetric SpMV (round 3; default while P <= 4).
-//
-// The tile kernel above writes every tile's whole region partial (16 x 16 x 6
-// nodes at P = 4, 12 partials per node) and its workgroup then ends -- and a
-// wave's s_endpgm waits for its stores to be acknowledged.  Under the full
-// read stream those acknowledgements take tens of microseconds (timing probe:
-// the partial stores cost 45-100 us of a 0.50-0.54 ms SpMV; the same stores
-// into an L2-resident slab cost 11 us).  Here a workgroup walks a column
-// (tix, tiy) of tiles upward in z: consecutive tiles' regions share P of
-// their TZ + P planes, so x and the partial sums live in LDS rings indexed by
-// plane mod RZ, and a tile transition only moves the TZ planes that leave
-// (final for this column: rows above add nothing to them) and the TZ planes
-// that enter.  One helper wave per workgroup does all of that traffic -- it
-// loads the entering x planes a tile ahead and stores the leaving partials --
-// so the 8 compute waves never wait for a store, and a node collects at most
-// 2 x 2 column partials (+ one or two at run boundaries) instead of 12:
-// 33 MB of partials each way per SpMV at config 2 instead of 90 MB.
-//
-// Work: the column-major tile sequence is cut into one chunk per resident
-// workgroup (2 per CU), balanced by stored blocks; a chunk is one or more
-// runs (consecutive tiles of one column).  A run starts cold (whole x
-// window, zeroed y ring) and, where it stops below the column's top, writes
-// the P planes above its last tile to overlap slabs the gather adds.  DET:
-// one fixed-point scale per run, 2^(61-E) with 2^E > W_run max|x| over the
-// run's region (W_run: k_sym_bound_cw), transposed and direct sums alike.
-struct SymRun {
-    int c, kz0, kz1, ovl;  // column, its tiles [kz0, kz1), first overlap slab (-1: none)
-};
-constexpr int CW_WV = 7;                  // compute waves per workgroup (+ the helper: 8 waves, 2 per SIMD x 2 per CU)
-constexpr int CW_NT = 64 * (CW_WV + 1);
-
-__device__ __forceinline__ int cw_ring(int v, int s0, int RZ)
-{
-    const int r = v + s0;
-    return r >= RZ ? r - RZ : r;
-}
-
-template <int P, bool DET>
-__global__ __launch_bounds__(CW_NT, 4) void k_nb_spmv_sym_cw(SymGeo g, const int *__restrict__ rowbox,
-                                                            const int64_t *__restrict__ svptr,
-                                                            const double *__restrict__ sval,
-                                                            const double *__restrict__ x, double *__restrict__ wsA,
-                                                            double *__restrict__ wsB, const SymRun *__restrict__ runs,
-                                                            const int *__restrict__ chunk_run,
-                                                            const int *__restrict__ run_e,
-                                                            const int *__restrict__ istate, int probe)
-{
-    // LDS: x ring [3][RZ][RY][RX] | y ring [3][RZ * RY * RX + 64 dummy] (DET: int64)
-    extern __shared__ double lds[];
-    __shared__ double red[CW_WV + 1];
-    if (istate && istate[I_REASON] != 0) return;
-    constexpr int TZ = SYM_TZ, TR = SYM_TX * SYM_TY * TZ, NS = (TR + CW_WV - 1) / CW_WV;
-    constexpr int RX = SYM_TX + 2 * P, RY = SYM_TY + 2 * P, RZ = TZ + P, RXY = RX * RY, RN = RXY * RZ, RS = RN + 64;
-    constexpr int L3 = 3 * RX;
-    double *xl = lds, *yl = lds + 3 * RN;
-    unsigned long long *yi = reinterpret_cast<unsigned long long *>(yl);
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool helper = w == CW_WV;
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
-    const int r0 = chunk_run[blockIdx.x], r1 = chunk_run[blockIdx.x + 1];
-    // workgroup barrier over LDS only: __syncthreads() would also wait for every
-    // global access in flight (vmcnt(0)) -- the storer's stores and the compute
-    // waves' prefetched loads are exactly what must stay in flight across it
-    auto lds_barrier = []() {
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-    };
-    for (int r = r0; r < r1; ++r) {
-        const SymRun R = runs[r];
-        const int tix = R.c % g.ntx, tiy = R.c / g.ntx;
-        const int x0 = tix * SYM_TX, y0 = tiy * SYM_TY, ox = x0 - P, oy = y0 - P;
-        const int nx = min(SYM_TX, g.Lx - x0);
-        const int zr0 = R.kz0 * TZ, zr1 = min(R.kz1 * TZ, g.Lz), zhi = min(zr1 + P, g.Lz);
-        // global x of region node (rx, ry) in plane z (0 outside the lattice)
-        auto xin = [&](int rx, int ry, int z) {
-            return ox + rx >= 0 && ox + rx < g.Lx && oy + ry >= 0 && oy + ry < g.Ly && z < g.Lz;
-        };
-        auto xaddr = [&](int rx, int ry, int z, int cc) {
-            return 3 * ((int64_t)(ox + rx) + (int64_t)g.Lx * (oy + ry) + Lxy * z) + cc;
-        };
-        // (an opaque copy of the thread id: values derived from it for the
-        // cold start are recomputed per run instead of being hoisted out of the
-        // run loop and spilled)
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        auto olane = [&]() {  // an opaque lane id: derived values are recomputed where used
-            int l = lane;
-            asm volatile("" : "+v"(l));
-            return l;
-        };
-        // ---- cold start: zero the y ring, x window [zr0, zr0 + RZ), DET scale
-        for (int k = tid; k < 3 * RS; k += CW_NT) yl[k] = 0.0;
-        constexpr int CT = CW_WV * 64;  // the compute waves' threads (the storer loads nothing)
-        if (tid < (CT / L3) * L3) {
-            const int f = tid % L3, rx = f / 3, cc = f - 3 * rx;
-            for (int l = tid / L3; l < RZ * RY; l += CT / L3) {
-                const int pz = l / RY, ry = l - pz * RY, z = zr0 + pz;
-                const bool ok = xin(rx, ry, z);
-                const double v = x[ok ? xaddr(rx, ry, z, cc) : 0];
-                xl[cc * RN + (z % RZ) * RXY + ry * RX + rx] = ok ? v : 0.0;
-            }
-        }
-        double S = 1.0, invS = 1.0;
-        if (DET) {
-            double m = 0.0;
-            int bad = 0;
-            if (tid < (CT / L3) * L3) {
-                const int f = tid % L3, rx = f / 3, cc = f - 3 * rx;
-                for (int l = tid / L3; l < (zhi - zr0) * RY; l += CT / L3) {
-                    const int pz = l / RY, ry = l - pz * RY, z = zr0 + pz;
-                    const bool ok = xin(rx, ry, z);
-                    const double a = fabs(x[ok ? xaddr(rx, ry, z, cc) : 0]);
-                    bad |= ok && !(a <= 1.7976931348623157e308);
-                    m = ok ? fmax(m, a) : m;
-                }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-            bad = __ballot(bad) != 0;
-            if (lane == 0) red[w] = bad ? -1.0 : m;
-            __syncthreads();
-            m = 0.0;
-            bad = 0;
-            for (int k = 0; k <= CW_WV; ++k) {
-                bad |= red[k] < 0.0;
-                m = fmax(m, red[k]);
-            }
-            if (bad) {
-                S = 0.0;  // non-finite x: the partials come out NaN, as a floating-point sum would
-                invS = __builtin_nan("");
-            } else if (m > 0.0) {
-                int em;
-                (void)frexp(m, &em);
-                const int E = min(max(run_e[r] + em, -960), 1020);
-                S = ldexp(1.0, 61 - E);
-                invS = ldexp(1.0, E - 61);
-            }
-        }
-        // ---- helper wave: entering x planes a tile ahead (registers), leaving partials out
-        // The TZ planes a tile adds to its predecessor's window are loaded by
-        // the compute waves at the start of the previous tile (in flight during
-        // it) and written into the ring after T1: compute wave w takes the
-        // planes' lattice lines w, w + 7, ... (lane l < 3 RX: position l of the line).
-        constexpr int NLN = TZ * RY, XE = (NLN + CW_WV - 1) / CW_WV;
-        double xe[XE];
-        // (the out-of-lattice mask is applied when storing: a select right
-        // after a load would wait for it)
-        auto xe_ok = [&](int ln0, int rx, int q, int kz, int &ry, int &z) {
-            const int ln = w + CW_WV * q, pz = ln / RY;
-            ry = ln - pz * RY;
-            z = kz * TZ + RZ - TZ + pz;
-            return ln0 < L3 && ox + rx >= 0 && ox + rx < g.Lx && ln < NLN && oy + ry >= 0 && oy + ry < g.Ly &&
-                   z < g.Lz;
-        };
-        // (asm loads: a load the compiler counts makes it wait for everything
-        // in flight before the next barrier; waited with sym_waitn in xe_store)
-        auto xe_load = [&](int kz) {
-            const int ln0 = olane(), rx = ln0 / 3, cc = ln0 - 3 * rx;
-#pragma unroll
-            for (int q = 0; q < XE; ++q) {
-                int ry, z;
-                const bool ok = xe_ok(ln0, rx, q, kz, ry, z);
-                asm_ld_f64(xe[q], x, (uint32_t)(ok ? xaddr(rx, ry, z, cc) : 0) * 8u);
-            }
-        };
-        auto xe_store = [&](int kz) {  // after sym_waitn for the loads
-#pragma unroll
-            for (int q = 0; q < XE; ++q) asm_touch(xe[q]);
-            const int ln0 = olane(), rx = ln0 / 3, cc = ln0 - 3 * rx;
-            if (ln0 < L3) {
-#pragma unroll
-                for (int q = 0; q < XE; ++q) {
-                    int ry, z;
-                    const bool ok = xe_ok(ln0, rx, q, kz, ry, z);
-                    if (w + CW_WV * q < NLN) xl[cc * RN + (z % RZ) * RXY + ry * RX + rx] = ok ? xe[q] : 0.0;
-                }
-            }
-        };
-        // the partials of plane z to global memory (every node of the region
-        // plane, unconditional stores: exact wait counts), its ring slot zeroed
-        auto y_out = [&](int z, double *dst) {
-            const int sl = z % RZ;
-#pragma unroll 1
-            for (int k = lane; k < RXY; k += 64) {
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    const int e = b * RS + sl * RXY + k;
-                    const double v = DET ? fx_to_d(yi[e]) * invS : yl[e];
-                    yl[e] = 0.0;
-                    if (!(probe & 256)) dst[b * RXY + k] = v;  // (timing probe 256: no partial stores)
-                }
-            }
-        };
-        // ---- compute waves: slot s of wave w is the tile's row w + 7 s (row r:
-        // plane r / 64, line (r / 8) % 8, x offset r % 8).  Per tile, lane s
-        // decodes slot s's row once (box, value offset, region offsets, ring
-        // index) into a few VGPRs; a row starts with readlanes, and the valid
-        // slots are a ballot mask (next slot = s_ff1).  zk: the tile's first
-        // plane, s0: its ring slot.
-        int zk = zr0, s0 = zr0 % RZ;
-        int nb = 0, nd = 0, nsl = 0, nsh = 0;  // raw descriptors of a tile (rowbox base, dims, value offset)
-        auto desc_load = [&](int kz) {  // asm loads (see xe_load), waited before desc_decode
-            const int ln0 = olane(), r = w + CW_WV * ln0, z1 = kz * TZ;
-            const bool ok = ln0 < NS && r < TR && y0 + ((r >> 3) & 7) < g.Ly && x0 + (r & 7) < g.Lx &&
-                            z1 + (r >> 6) < g.Lz;
-            const uint32_t i = ok ? (x0 + (r & 7)) + g.Lx * (y0 + ((r >> 3) & 7)) + (uint32_t)Lxy * (z1 + (r >> 6)) : 0;
-            asm_ld_i32(nb, rowbox, i * 8u);
-            asm_ld_i32(nd, rowbox, i * 8u + 4u);
-            asm_ld_i32(nsl, svptr, i * 8u);
-            asm_ld_i32(nsh, svptr, i * 8u + 4u);
-        };
-        auto desc_wait = [&]() {
-            asm_touch(nb);
-            asm_touch(nd);
-            asm_touch(nsl);
-            asm_touch(nsh);
-        };
-        uint64_t smask = 0;                 // valid slots of the tile
-        int qlo = 0, qhi = 0, qa = 0, qb = 0, qc = 0;  // decoded slot records (lane s: slot s)
-        float qix = 1.0f, qixy = 1.0f;
-        auto desc_decode = [&]() {  // after nb.. have landed; zk, s0 of the tile
-            const int ln0 = olane(), r = w + CW_WV * ln0;
-            const int xg = x0 + (r & 7), yy = y0 + ((r >> 3) & 7), zz = zk + (r >> 6);
-            const bool ok = ln0 < NS && r < TR && yy < g.Ly && xg < g.Lx && zz < g.Lz;
-            smask = __ballot(ok);
-            const int64_t base = nb;
-            const int bz = (int)(base / Lxy), by = (int)((base - bz * Lxy) / g.Lx);
-            const int bx = (int)(base - bz * Lxy - (int64_t)by * g.Lx);
-            const int bnx = nd & 255, bny = (nd >> 8) & 255, bnz = (nd >> 16) & 255;
-            const int k0 = (xg - bx) + bnx * ((yy - by) + bny * (zz - bz));
-            const int mu = bnx * bny * bnz - k0;
-            qlo = nsl;
-            qhi = nsh;
-            qa = ok ? (k0 | (mu << 16)) : (0 | (1 << 16));
-            qb = bnx | ((bnx * bny) << 8) | ((bx - ox + 32) << 20);  // rx0 in [-P, RX)
-            qc = (by - oy + 32) | ((bz - zk + 32) << 8) |
-                 (((xg - ox) + RX * ((yy - oy) + RY * cw_ring(zz - zk, s0, RZ))) << 16);  // ry0, rz0, own
-            qix = 1.0f / (float)bnx;
-            qixy = 1.0f / (float)(bnx * bny);
-        };
-        auto next_slot = [&](int s) {  // first valid slot >= s, or NS
-            const uint64_t m = s < 64 ? smask >> s : 0;
-            return m ? s + (int)__builtin_ctzll(m) : NS;
-        };
-        auto slot_row = [&](int s, SymRow &Rw) {
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(qlo, s);
-            const int64_t hi = __builtin_amdgcn_readlane(qhi, s);
-            const int a = __builtin_amdgcn_readlane(qa, s), b = __builtin_amdgcn_readlane(qb, s);
-            const int c = __builtin_amdgcn_readlane(qc, s);
-            Rw.v = sval + ((hi << 32) | lo);
-            Rw.k0 = a & 0xFFFF;
-            Rw.mu = a >> 16;
-            Rw.bnx = b & 255;
-            Rw.bnxy = (b >> 8) & 0xFFF;
-            Rw.rx0 = ((b >> 20) & 255) - 32;
-            Rw.ry0 = (c & 255) - 32;
-            Rw.rz0 = ((c >> 8) & 255) - 32;
-            Rw.own = (c >> 16) & 0xFFFF;
-            Rw.ibnx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, qix), s));
-            Rw.ibnxy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, qixy), s));
-            Rw.x0 = uni_d(xl[Rw.own]);
-            Rw.x1 = uni_d(xl[RN + Rw.own]);
-            Rw.x2 = uni_d(xl[2 * RN + Rw.own]);
-        };
-        auto load_v = [&](const SymRow &Rw, int kb, double *vv, int &rr) {
-            const int kk = min(kb + lane, Rw.mu - 1);
-            const int q16 = Rw.mu & ~15;
-            const bool ch = kk < q16;
-            const int64_t o0 = ch ? (int64_t)((kk >> 4) * 144 + (kk & 15)) : (int64_t)q16 * 9 + (kk - q16);
-            const int st = ch ? 16 : Rw.mu - q16;
-            unsigned o[9];
-#pragma unroll
-            for (int s = 0; s < 9; ++s) o[s] = (unsigned)(o0 + s * st) * 8u;
-            sym_ld9(vv, Rw.v, o);
-            const int k = Rw.k0 + kk;
-            const int kzz = sym_div(k, Rw.bnxy, Rw.ibnxy), rem = k - kzz * Rw.bnxy;
-            const int ky = sym_div(rem, Rw.bnx, Rw.ibnx), kx = rem - ky * Rw.bnx;
-            rr = (Rw.rx0 + kx) + RX * ((Rw.ry0 + ky) + RY * cw_ring(Rw.rz0 + kzz, s0, RZ));
-        };
-        // the issue cursor (row I, slot xi, pass ki) runs one item ahead of the
-        // compute cursor; the first item of a tile is issued before the
-        // transition into it (its rows' x lie in the previous tile's window)
-        int xi = NS, ki = 0;
-        bool any = false, idone = true;
-        SymRow I, C;
-        double v0[9], v1[9];
-        int ra = 0, rb = 0;
-        auto tile_begin = [&]() {  // zk, s0 and the decoded slots of the tile
-            xi = next_slot(0);
-            ki = 0;
-            any = xi < NS;
-            idone = !any;
-            if (any) {
-                slot_row(xi, I);
-            } else {  // no rows of this wave in the tile: a dummy item
-                I.v = sval;
-                I.mu = 1;
-                I.k0 = 0;
-                I.bnx = I.bnxy = 1;
-                I.ibnx = I.ibnxy = 1.0f;
-                I.rx0 = I.ry0 = I.rz0 = 0;
-                I.own = 0;
-            }
-            load_v(I, ki, v0, ra);
-        };
-        auto issue_next = [&]() {
-            if (idone) return;
-            if (ki + 64 < I.mu) {
-                ki += 64;
-                return;
-            }
-            const int nx2 = next_slot(xi + 1);
-            if (nx2 >= NS) {
-                idone = true;
-                return;
-            }
-            xi = nx2;
-            ki = 0;
-            slot_row(xi, I);
-        };
-        // Helper and compute waves run separate loops with the same barrier
-        // sequence (cold start, then T1 / T2 per tile): the helper's entering-x
-        // registers are then not live across the compute waves' item loop.
-        if (helper) {
-            // the storer: it issues no loads, so no wait of its own ever covers
-            // its stores; they drain in the background
-            __syncthreads();  // cold start done
-            for (int kz = R.kz0; kz < R.kz1; ++kz) {
-                const bool last = kz + 1 >= R.kz1;
-                lds_barrier();  // T1: the tile's adds are done
-                // the leaving planes z1 .. z1 + TZ - 1 are final for this column;
-                // at the run's end also the P planes above (overlap slabs)
-                const int z1 = kz * TZ, zo = last ? zhi : min(z1 + TZ, g.Lz);
-                for (int z = z1; z < zo; ++z)
-                    y_out(z, z < zr1 ? wsA + ((int64_t)R.c * g.Lz + z) * 3 * RXY
-                                     : wsB + (int64_t)(R.ovl + z - zr1) * 3 * RXY);
-                lds_barrier();  // T2: the window of tile kz + 1 is in LDS
-            }
-            continue;
-        }
-        desc_load(R.kz0);
-        sym_waitn<0>();
-        desc_wait();
-        __syncthreads();  // cold start done: x window and zeroed y ring in LDS
-        desc_decode();
-        tile_begin();
-        for (int kz = R.kz0; kz < R.kz1; ++kz) {
-            const bool last = kz + 1 >= R.kz1;
-            if (!last) desc_load(kz + 1);  // (in flight during the tile)
-            if (any && !(probe & 1024)) {  // (timing probe 1024: no items)
-                int xc = xi, kc = 0;
-                C = I;
-                C.x0 = uni_d(xl[C.own]);  // (issued before the window was complete)
-                C.x1 = uni_d(xl[RN + C.own]);
-                C.x2 = uni_d(xl[2 * RN + C.own]);
-                double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-                auto step = [&](double *vv, const int rr, double *vn, int &rn) {
-                    issue_next();
-                    load_v(I, ki, vn, rn);
-                    const double xv0 = xl[rr], xv1 = xl[RN + rr], xv2 = xl[2 * RN + rr];
-                    sym_wait9<9>(vv);
-                    const int kk = kc + lane;
-                    const bool live = kk < C.mu;
-                    const int rt = live && kk > 0 ? rr : RN + lane;
-                    const double s0v = vv[0] * xv0 + vv[1] * xv1 + vv[2] * xv2;
-                    const double s1v = vv[3] * xv0 + vv[4] * xv1 + vv[5] * xv2;
-                    const double s2v = vv[6] * xv0 + vv[7] * xv1 + vv[8] * xv2;
-                    acc0 += live ? s0v : 0.0;
-                    acc1 += live ? s1v : 0.0;
-                    acc2 += live ? s2v : 0.0;
-                    const double t0 = vv[0] * C.x0 + vv[3] * C.x1 + vv[6] * C.x2;
-                    const double t1 = vv[1] * C.x0 + vv[4] * C.x1 + vv[7] * C.x2;
-                    const double t2 = vv[2] * C.x0 + vv[5] * C.x1 + vv[8] * C.x2;
-                    if (DET) {
-                        atomicAdd(&yi[rt], fx_of(t0, S));
-                        atomicAdd(&yi[RS + rt], fx_of(t1, S));
-                        atomicAdd(&yi[2 * RS + rt], fx_of(t2, S));
-                    } else {
-                        atomicAdd(&yl[rt], t0);
-                        atomicAdd(&yl[RS + rt], t1);
-                        atomicAdd(&yl[2 * RS + rt], t2);
-                    }
-                    if (kc + 64 < C.mu) {
-                        kc += 64;
-                        return true;
-                    }
-                    // the row is done: its direct sum (fixed-order DPP) into its own node
-                    acc0 = wsum_dpp(acc0);
-                    acc1 = wsum_dpp(acc1);
-                    acc2 = wsum_dpp(acc2);
-                    if (lane < 3) {
-                        const double s = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
-                        if (DET) atomicAdd(&yi[lane * RS + C.own], fx_of(s, S));
-                        else atomicAdd(&yl[lane * RS + C.own], s);
-                    }
-                    acc0 = acc1 = acc2 = 0.0;
-                    const int nx2 = next_slot(xc + 1);
-                    if (nx2 >= NS) return false;
-                    xc = nx2;
-                    kc = 0;
-                    slot_row(xc, C);
-                    return true;
-                };
-                while (step(v0, ra, v1, rb) && step(v1, rb, v0, ra)) {
-                }
-            }
-            sym_wait9<0>(v0);  // (the last, re-read item: L2 hits; the descriptors too)
-            sym_wait9<0>(v1);
-            if (!last) {
-                // tile kz + 1's new x planes, issued once this wave's items are
-                // done (holding them over the whole tile costs spills), and its
-                // first item, both in flight across the transition
-                desc_wait();
-                xe_load(kz + 1);
-                zk += TZ;
-                s0 = zk % RZ;
-                desc_decode();
-                tile_begin();
-            }
-            lds_barrier();  // T1: the tile's adds are done
-            if (!last) {
-                sym_waitn<9>();  // the x planes (the next item's 9 loads stay in flight)
-                xe_store(kz + 1);  // into the slots of planes kz * TZ .. + TZ - 1 (outside tile kz + 1's window)
-            }
-            lds_barrier();  // T2: the window of tile kz + 1 is in LDS
-        }
+    if (j >= n) {
+        double *o = gsend + 3 * (j - n);
+        o[0] = s0;
+        o[1] = s1;
+        o[2] = s2;
+        return;
     }
-}
-
-// W_run of the DET column walk: for each node j of the run's region, the
-// sum over the run's rows i with j in i's stored blocks (j != i) of
-// max_b sum_a |B_ij[a][b]|, plus, when j is a row of the run, the sum over its
-// stored blocks of max_a sum_b |B_jk[a][b]| -- a bound on |partial_j| per
-// unit max|x| over the region; run_e[r] = e with 2^e > max_j.  Fixed order.
-__global__ __launch_bounds__(256) void k_sym_bound_cw(SymGeo g, const int *__restrict__ rowbox,
-                                                      const int64_t *__restrict__ svptr,
-                                                      const double *__restrict__ sval,
-                                                      const SymRun *__restrict__ runs, int *__restrict__ run_e)
-{
-    __shared__ double wred[256];
-    const SymRun R = runs[blockIdx.x];
-    const int TZ = SYM_TZ, P = g.P;
-    const int tix = R.c % g.ntx, tiy = R.c / g.ntx;
-    const int x0 = tix * SYM_TX, y0 = tiy * SYM_TY, ox = x0 - P, oy = y0 - P;
-    const int zr0 = R.kz0 * TZ, zr1 = min(R.kz1 * TZ, g.Lz), zhi = min(zr1 + P, g.Lz);
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly;
-    const int RXY = g.RX * g.RY;
-    auto blk = [&](const double *v, int kk, int mu, bool tr) {
-        double bm = 0.0;
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            double cs = 0.0;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) cs += fabs(v[vofs(1, 9, tr ? a * 3 + b : b * 3 + a, kk, mu, mu)]);
-            bm = fmax(bm, cs);
-        }
-        return bm;
-    };
-    double wm = 0.0;
-    for (int k = threadIdx.x; k < RXY * (zhi - zr0); k += 256) {
-        const int pz = k / RXY, rem = k - pz * RXY, ry = rem / g.RX, rx = rem - ry * g.RX;
-        const int gx = ox + rx, gy = oy + ry, gz = zr0 + pz;
-        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly) continue;
-        double s = 0.0;
-        for (int zi = max(zr0, gz - P); zi <= min(zr1 - 1, gz); ++zi)
-            for (int yi = y0; yi < min(y0 + SYM_TY, g.Ly); ++yi)
-                for (int xi = x0; xi < min(x0 + SYM_TX, g.Lx); ++xi) {
-                    const int64_t i = xi + (int64_t)g.Lx * yi + Lxy * zi;
-                    const int64_t base = rowbox[2 * i];
-                    const int d = rowbox[2 * i + 1];
-                    const int bz = (int)(base / Lxy), by = (int)((base - bz * Lxy) / g.Lx);
-                    const int bx = (int)(base - bz * Lxy - (int64_t)by * g.Lx);
-                    const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
-                    if (gx < bx || gx >= bx + bnx || gy < by || gy >= by + bny || gz < bz || gz >= bz + bnz) continue;
-                    const int k0 = (xi - bx) + bnx * ((yi - by) + bny * (zi - bz));
-                    const int kj = (gx - bx) + bnx * ((gy - by) + bny * (gz - bz));
-                    if (kj <= k0) continue;
-                    const int mu = bnx * bny * bnz - k0;
-                    s += blk(sval + svptr[i], kj - k0, mu, true);
-                }
-        if (gx >= x0 && gx < x0 + SYM_TX && gy >= y0 && gy < y0 + SYM_TY && gz < zr1) {  // j is a row of the run
-            const int64_t j = gx + (int64_t)g.Lx * gy + Lxy * gz;
-            const int d = rowbox[2 * j + 1];
-            const int64_t base = rowbox[2 * j];
-            const int bz = (int)(base / Lxy), by = (int)((base - bz * Lxy) / g.Lx);
-            const int bx = (int)(base - bz * Lxy - (int64_t)by * g.Lx);
-            const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
-            const int k0 = (gx - bx) + bnx * ((gy - by) + bny * (gz - bz)), mu = bnx * bny * bnz - k0;
-            const double *v = sval + svptr[j];
-            for (int kk = 0; kk < mu; ++kk) s += blk(v, kk, mu, false);
-        }
-        wm = fmax(wm, s);
+    if (3 * j < nrecv) {
+        s0 += grecv[3 * j];
+        s1 += grecv[3 * j + 1];
+        s2 += grecv[3 * j + 2];
     }
-    wred[threadIdx.x] = wm;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) wred[threadIdx.x] = fmax(wred[threadIdx.x], wred[threadIdx.x + o]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        int e = -1000;
-        if (wred[0] > 0.0) (void)frexp(wred[0], &e);
-        run_e[blockIdx.x] = e;
-    }
-}
-
-// y_j = the column partials of j's plane (2 x 2 columns whose regions hold
-// it, ascending (y, x)), each followed by its overlap slabs, in that fixed order.
-__global__ __launch_bounds__(256) void k_nb_sym_gather_cw(SymGeo g, const double *__restrict__ wsA,
-                                                          const double *__restrict__ wsB, const int *__restrict__ ovl,
-                                                          double *__restrict__ y, const int *__restrict__ istate)
-{
-    if (istate && istate[I_REASON] != 0) return;
-    const int64_t Lxy = (int64_t)g.Lx * g.Ly, n = Lxy * g.Lz;
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const int jz = (int)(j / Lxy), jy = (int)((j - jz * Lxy) / g.Lx), jx = (int)(j - jz * Lxy - (int64_t)jy * g.Lx);
-    const int RXY = g.RX * g.RY;
-    const int x_lo = max(0, (jx + g.P - g.RX + SYM_TX) / SYM_TX), x_hi = min(g.ntx - 1, (jx + g.P) / SYM_TX);
-    const int y_lo = max(0, (jy + g.P - g.RY + SYM_TY) / SYM_TY), y_hi = min(g.nty - 1, (jy + g.P) / SYM_TY);
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int ty = y_lo; ty <= y_hi; ++ty)
-        for (int tx = x_lo; tx <= x_hi; ++tx) {
-            const int c = ty * g.ntx + tx;
-            const int q = (jy - (ty * SYM_TY - g.P)) * g.RX + (jx - (tx * SYM_TX - g.P));
-            const double *p = wsA + ((int64_t)c * g.Lz + jz) * 3 * RXY + q;
-            s0 += p[0];
-            s1 += p[RXY];
-            s2 += p[2 * RXY];
-#pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                const int k = ovl[((int64_t)c * g.Lz + jz) * 2 + o];
-                if (k < 0) continue;
-                const double *pb = wsB + (int64_t)k * 3 * RXY + q;
-                s0 += pb[0];
-                s1 += pb[RXY];
-                s2 += pb[2 * RXY];
-            }
-        }
     y[3 * j] = s0;
     y[3 * j + 1] = s1;
     y[3 * j + 2] = s2;
@@ -1218,35 +671,17 @@ void sym_forget(kle_mat *A)
     A->d_svptr = nullptr;
     A->d_sws = nullptr;
     A->d_stile_e = nullptr;
-    A->d_cw_runs = nullptr;
-    A->d_cw_chunk = A->d_cw_rune = A->d_cw_ovl = nullptr;
-    A->d_cw_wsA = A->d_cw_wsB = nullptr;
-    A->cw_nchunk = 0;
-    A->cw_entries = 0;
+    A->d_sgsend = A->d_sgrecv = nullptr;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
 }
 
 void sym_drop(kle_mat *A)
 {
-    if (A->d_sval) (void)hipFree(A->d_sval);
-    if (A->d_svptr) (void)hipFree(A->d_svptr);
-    if (A->d_sws) (void)hipFree(A->d_sws);
-    if (A->d_stile_e) (void)hipFree(A->d_stile_e);
-    for (void *q : {A->d_cw_runs, (void *)A->d_cw_chunk, (void *)A->d_cw_rune, (void *)A->d_cw_ovl,
-                    (void *)A->d_cw_wsA, (void *)A->d_cw_wsB})
+    for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
+                    (void *)A->d_sgsend, (void *)A->d_sgrecv})
         if (q) (void)hipFree(q);
-    A->d_cw_runs = nullptr;
-    A->d_cw_chunk = A->d_cw_rune = A->d_cw_ovl = nullptr;
-    A->d_cw_wsA = A->d_cw_wsB = nullptr;
-    A->cw_nchunk = 0;
-    A->cw_entries = 0;
-    A->d_sval = nullptr;
-    A->d_svptr = nullptr;
-    A->d_sws = nullptr;
-    A->d_stile_e = nullptr;
-    A->sblocks = A->snvals = A->sws_entries = 0;
-    A->sym_P = 0;
+    sym_forget(A);
 }
 
 static SymGeo sym_geo(const kle_mat *A)
@@ -1258,6 +693,9 @@ static SymGeo sym_geo(const kle_mat *A)
     g.Lx = (int)A->row_lat[0];
     g.Ly = (int)A->row_lat[1];
     g.Lz = (int)A->row_lat[2];
+    const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
+    g.zo = (int)(A->ghost_lo / plane3);
+    g.hp = (int)(A->ghost_hi / plane3);
     g.P = P;
     g.RX = g.TX + 2 * P;
     g.RY = SYM_TY + 2 * P;
@@ -1276,193 +714,206 @@ static size_t sym_xl_lds(int P)
 }
 constexpr size_t LDS_PER_CU = 163840;
 
-// LDS of the column-walk kernel: x and y rings (y with 64 dummy slots per component)
-static size_t sym_cw_lds(int P)
+// every rank's flag -> whether any rank raised it (one collective; one rank:
+// no communication)
+static int any_rank(kle_ctx *c, int64_t flag, bool &any)
 {
-    const size_t RN = (size_t)(SYM_TX + 2 * P) * (SYM_TY + 2 * P) * (SYM_TZ + P);
-    return (6 * RN + 3 * 64) * sizeof(double);
-}
-
-// Column-walk work plan: the tiles in column-major order (column c =
-// tiy * ntx + tix, tile kz fastest) cut into one chunk per resident
-// workgroup with equal stored blocks (+ 16 per row for the per-row fixed
-// cost), each chunk split into runs at column changes; a run ending below its
-// column's top writes the P planes above it to overlap slabs, which the
-// gather finds through ovl[(c * Lz + z) * 2 + {0, 1}].
-static int cw_build(kle_mat *A, const std::vector<int> &mu_row)
-{
-    const SymGeo g = sym_geo(A);
-    const int P = g.P, TZ = SYM_TZ;
-    const int ncol = g.ntx * g.nty, ntz = g.ntz;
-    const int64_t ntiles = (int64_t)ncol * ntz, Lx = g.Lx, Lxy = (int64_t)g.Lx * g.Ly;
-    std::vector<double> wt(ntiles, 0.0);
-    for (int c = 0; c < ncol; ++c) {
-        const int x0 = (c % g.ntx) * SYM_TX, y0 = (c / g.ntx) * SYM_TY;
-        for (int kz = 0; kz < ntz; ++kz) {
-            double s = 0.0;
-            for (int z = kz * TZ; z < std::min(kz * TZ + TZ, g.Lz); ++z)
-                for (int y = y0; y < std::min(y0 + SYM_TY, g.Ly); ++y)
-                    for (int x = x0; x < std::min(x0 + SYM_TX, g.Lx); ++x) s += mu_row[x + Lx * y + Lxy * z] + 16;
-            wt[(int64_t)c * ntz + kz] = s + g_tune.spmv_sym_cw_tile;  // + a tile's fixed cost (transition)
-        }
-    }
-    const int per_cu = 2 * sym_cw_lds(P) <= LDS_PER_CU ? 2 : 1;
-    int64_t nch = std::min<int64_t>((int64_t)A->ctx->num_cus * per_cu, ntiles);
-    double tot = 0.0;
-    for (double v : wt) tot += v;
-    // cut points: chunk k starts at the first tile whose prefix weight reaches k * tot / nch
-    std::vector<int64_t> cut{0};
-    double pre = 0.0;
-    for (int64_t t = 0, k = 1; t < ntiles && k < nch; ++t) {
-        pre += wt[t];
-        if (pre >= (double)k * tot / nch && t + 1 < ntiles) {
-            cut.push_back(t + 1);
-            while (k < nch && pre >= (double)k * tot / nch) ++k;
-        }
-    }
-    cut.push_back(ntiles);
-    nch = (int64_t)cut.size() - 1;
-    std::vector<SymRun> runs;
-    std::vector<int> chunk_run{0};
-    for (int64_t k = 0; k < nch; ++k) {
-        for (int64_t t = cut[k]; t < cut[k + 1];) {
-            const int c = (int)(t / ntz), kz0 = (int)(t % ntz);
-            const int64_t tend = std::min<int64_t>(cut[k + 1], (int64_t)(c + 1) * ntz);
-            runs.push_back({c, kz0, (int)(tend - (int64_t)c * ntz), -1});
-            t = tend;
-        }
-        chunk_run.push_back((int)runs.size());
-    }
-    // overlap slabs
-    std::vector<int> ovl((size_t)ncol * g.Lz * 2, -1);
-    int nslab = 0;
-    for (auto &R : runs) {
-        const int zr1 = std::min(R.kz1 * TZ, g.Lz), zhi = std::min(zr1 + P, g.Lz);
-        if (zhi <= zr1) continue;
-        R.ovl = nslab;
-        for (int z = zr1; z < zhi; ++z) {
-            int *o = &ovl[((size_t)R.c * g.Lz + z) * 2];
-            if (o[0] < 0) o[0] = nslab + z - zr1;
-            else if (o[1] < 0) o[1] = nslab + z - zr1;
-            else return fail(KLE_ERR_SUP, "symmetric storage: column-walk runs too short for P = %d", P);
-        }
-        nslab += zhi - zr1;
-    }
-    // lattice entries of the column partials (+ overlap slabs): written and read once per SpMV
-    auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
-    int64_t ents = 0;
-    for (int c = 0; c < ncol; ++c) {
-        const int64_t a = span((c % g.ntx) * SYM_TX - P, g.RX, g.Lx) * span((c / g.ntx) * SYM_TY - P, g.RY, g.Ly);
-        int64_t planes = g.Lz;
-        for (int z = 0; z < g.Lz; ++z) planes += (ovl[((size_t)c * g.Lz + z) * 2] >= 0) + (ovl[((size_t)c * g.Lz + z) * 2 + 1] >= 0);
-        ents += a * planes;
-    }
-    const int64_t RXY = (int64_t)g.RX * g.RY;
-    kle_ctx *cx = A->ctx;
-    if (hipMalloc(&A->d_cw_runs, sizeof(SymRun) * runs.size()) != hipSuccess ||
-        hipMalloc(&A->d_cw_chunk, sizeof(int) * chunk_run.size()) != hipSuccess ||
-        hipMalloc(&A->d_cw_rune, sizeof(int) * runs.size()) != hipSuccess ||
-        hipMalloc(&A->d_cw_ovl, sizeof(int) * ovl.size()) != hipSuccess ||
-        hipMalloc(&A->d_cw_wsA, sizeof(double) * (size_t)ncol * g.Lz * 3 * RXY) != hipSuccess ||
-        hipMalloc(&A->d_cw_wsB, sizeof(double) * (size_t)std::max(nslab, 1) * 3 * RXY) != hipSuccess) {
-        (void)hipGetLastError();
-        sym_drop(A);
-        return fail(KLE_ERR_MEM, "out of device memory for the column-walk SpMV workspace");
-    }
-    KLE_HIP(hipMemcpy(A->d_cw_runs, runs.data(), sizeof(SymRun) * runs.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_cw_chunk, chunk_run.data(), sizeof(int) * chunk_run.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_cw_ovl, ovl.data(), sizeof(int) * ovl.size(), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_sym_bound_cw, dim3((unsigned)runs.size()), dim3(256), 0, cx->stream, g, A->d_rowbox,
-                       A->d_svptr, A->d_sval, (const SymRun *)A->d_cw_runs, A->d_cw_rune);
-    KLE_HIP(hipGetLastError());
-    KLE_HIP(hipStreamSynchronize(cx->stream));
-    A->cw_nchunk = (int)nch;
-    A->cw_entries = ents;
+    any = flag != 0;
+    if (c->nranks == 1) return 0;
+    std::vector<int64_t> all;
+    KLE_TRY(allgather_i64(c, flag, all));
+    any = false;
+    for (int64_t v : all) any |= v != 0;
     return 0;
 }
 
-// Build the symmetric (upper-triangle) storage of a single-rank structured
-// 3x3 matrix from its full storage; refuses a matrix whose blocks are not
-// symmetric to 1e-12 of its largest entry or whose pattern is not symmetric.
+// x_i = uniform[-1, 1) of a splitmix64 hash of the global entry index
+__global__ void k_sym_probe_x(int64_t n, int64_t lo, double *__restrict__ x)
+{
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint64_t z = 0x5EED5EEDull + (uint64_t)(lo + k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    x[k] = (double)(z >> 11) * 0x1p-52 - 1.0;
+}
+
+// N > 1: the stored triangle also feeds other ranks' rows (a block (i, j)
+// with j an upper ghost stands in for the neighbour's (j, i)), which
+// k_sym_build cannot compare locally.  One product with a hashed x through
+// both storages checks it: max |A_full x - A_sym x| <= 1e-12 max |A_ij|, the
+// single-rank criterion (a block asymmetric by d changes y by ~d |x_i|).
+static int sym_probe(kle_mat *A, double vmax_all, bool &bad)
+{
+    kle_ctx *c = A->ctx;
+    bad = false;
+    kle_vec *x = nullptr, *y1 = nullptr, *y2 = nullptr;
+    int rc = vec_alloc(c, A->n_local, A->n_global, A->col_lo, A->ghost_lo, A->ghost_hi, &x);
+    if (!rc) rc = vec_alloc(c, A->m_local, A->m_global, A->row_lo, 0, 0, &y1);
+    if (!rc) rc = vec_alloc(c, A->m_local, A->m_global, A->row_lo, 0, 0, &y2);
+    if (!rc) {
+        x->bs = A->C;
+        x->lo_rank = A->lo_rank;
+        x->hi_rank = A->hi_rank;
+        x->send_lo = A->send_lo;
+        x->send_hi = A->send_hi;
+        hipLaunchKernelGGL(k_sym_probe_x, dim3((unsigned)((A->n_local + 255) / 256)), dim3(256), 0, c->stream,
+                           A->n_local, A->col_lo, x->d);
+        rc = hipGetLastError() == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "probe launch failed");
+    }
+    double *sv = A->d_sval;
+    if (!rc) {
+        A->d_sval = nullptr;  // (the full storage)
+        rc = spmv(A, x, y1, nullptr);
+        A->d_sval = sv;
+    }
+    if (!rc) rc = sym_spmv(A, x, y2, nullptr);
+    double dmax = 0.0;
+    if (!rc) {
+        std::vector<double> h1(A->m_local), h2(A->m_local);
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(h1.data(), y1->d, sizeof(double) * A->m_local, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(h2.data(), y2->d, sizeof(double) * A->m_local, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(KLE_ERR_DEVICE, "probe copy failed");
+        for (int64_t k = 0; k < A->m_local && !rc; ++k) {
+            const double d = std::fabs(h1[k] - h2[k]);
+            dmax = std::isnan(d) ? INFINITY : std::max(dmax, d);
+        }
+    }
+    for (kle_vec *v : {x, y1, y2})
+        if (v) {
+            (void)hipFree(v->base);
+            delete v;
+        }
+    if (rc) return rc;
+    // (a flag per rank: an asymmetry anywhere refuses the storage everywhere)
+    return any_rank(c, !(dmax <= 1e-12 * vmax_all), bad);
+}
+
+// Build the symmetric (upper-triangle) storage of a structured 3x3 matrix
+// from its full storage (one rank, or z slabs with lower / upper ghost
+// planes).  Refuses a matrix whose blocks are not symmetric to 1e-12 of its
+// largest entry or whose pattern is not symmetric.  At N > 1 collective: every
+// rank decides the same way (any_rank), so no rank runs the symmetric SpMV
+// and its reverse halo while a neighbour runs the full storage.
 int sym_build(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
     sym_drop(A);
-    if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_rowbox && c->nranks == 1 &&
-          A->ghost_lo == 0 && A->ghost_hi == 0 && A->m_local == A->n_local))
-        return fail(KLE_ERR_SUP, "symmetric storage needs a single-rank 3x3 node-block matrix with box-lattice rows");
-    const int64_t Lx = A->row_lat[0], Ly = A->row_lat[1], Lz = A->row_lat[2], n = A->nrows;
-    if (Lx * Ly * Lz != n || A->box_lx != Lx || A->box_lxy != Lx * Ly || Lx > INT_MAX / 2)
-        return fail(KLE_ERR_SUP, "symmetric storage: the rows are not one box lattice");
-    std::vector<int> rb(2 * n), rp(n + 1), cnt(n);
-    KLE_HIP(hipStreamSynchronize(c->stream));
-    KLE_HIP(hipMemcpy(rb.data(), A->d_rowbox, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
-    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
-    if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost));
-    else
-        for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
-    std::vector<int64_t> sv(n + 1);
-    std::vector<int> mu_row(n);
+    const int64_t Lx = A->row_lat[0], Ly = A->row_lat[1], Lz = A->row_lat[2], n = A->nrows, Lxy = Lx * Ly;
+    std::string why;
+    if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_rowbox && !A->plan &&
+          A->m_local == A->n_local))
+        why = "symmetric storage needs a 3x3 node-block matrix with box-lattice rows (one rank or z slabs)";
+    else if (Lx * Ly * Lz != n || A->box_lx != Lx || A->box_lxy != Lxy || Lx > INT_MAX / 2 ||
+             A->ghost_lo % (3 * Lxy) || A->ghost_hi % (3 * Lxy) || A->send_lo % (3 * Lxy))
+        why = "symmetric storage: the rows are not one box lattice with whole ghost planes";
+    const int64_t zo = why.empty() ? A->ghost_lo / (3 * Lxy) : 0, hp = why.empty() ? A->ghost_hi / (3 * Lxy) : 0;
+    std::vector<int> rb, rp, cnt;
+    std::vector<int64_t> sv;
     int P = 0;
-    int64_t tot = 0, blocks = 0, all = 0;
-    const int64_t Lxy = Lx * Ly;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t z = i / Lxy, y = (i - z * Lxy) / Lx, x = i - z * Lxy - y * Lx;
-        const int64_t base = rb[2 * i];
-        const int d = rb[2 * i + 1];
-        const int64_t bz = base / Lxy, by = (base - bz * Lxy) / Lx, bx = base - bz * Lxy - by * Lx;
-        const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
-        if (x < bx || x >= bx + bnx || y < by || y >= by + bny || z < bz || z >= bz + bnz ||
-            cnt[i] != bnx * bny * bnz)
-            return fail(KLE_ERR_SUP, "symmetric storage: row %lld's box does not hold its diagonal", (long long)i);
-        P = std::max<int>(P, (int)std::max({x - bx, bx + bnx - 1 - x, y - by, by + bny - 1 - y, bz + bnz - 1 - z}));
-        const int k0 = (int)((x - bx) + bnx * ((y - by) + (int64_t)bny * (z - bz)));
-        const int64_t mu = cnt[i] - k0;
-        mu_row[i] = (int)mu;
-        sv[i] = tot;
-        tot += (mu * 9 + 15) & ~int64_t(15);
-        blocks += mu;
-        all += cnt[i];
+    int64_t tot = 0, blocks = 0, all = 0, up_ghost = 0, lo_ghost = 0;
+    if (why.empty()) {
+        rb.resize(2 * n);
+        rp.resize(n + 1);
+        cnt.resize(n);
+        sv.resize(n + 1);
+        KLE_HIP(hipStreamSynchronize(c->stream));
+        KLE_HIP(hipMemcpy(rb.data(), A->d_rowbox, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
+        KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
+        if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost));
+        else
+            for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
+        for (int64_t i = 0; i < n && why.empty(); ++i) {
+            // (x, y, z): the row in column (ext) coordinates
+            const int64_t z = i / Lxy + zo, y = (i % Lxy) / Lx, x = i % Lx;
+            const int64_t base = rb[2 * i];
+            const int d = rb[2 * i + 1];
+            const int64_t bz = base / Lxy, by = (base - bz * Lxy) / Lx, bx = base - bz * Lxy - by * Lx;
+            const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
+            if (x < bx || x >= bx + bnx || y < by || y >= by + bny || z < bz || z >= bz + bnz ||
+                cnt[i] != bnx * bny * bnz || bz + bnz > zo + Lz + hp) {
+                why = "symmetric storage: row " + std::to_string(i) + "'s box does not hold its diagonal";
+                break;
+            }
+            P = std::max<int>(P, (int)std::max({x - bx, bx + bnx - 1 - x, y - by, by + bny - 1 - y, bz + bnz - 1 - z}));
+            const int k0 = (int)((x - bx) + bnx * ((y - by) + (int64_t)bny * (z - bz)));
+            const int64_t mu = cnt[i] - k0;
+            sv[i] = tot;
+            tot += (mu * 9 + 15) & ~int64_t(15);
+            blocks += mu;
+            all += cnt[i];
+            up_ghost += (int64_t)bnx * bny * std::max<int64_t>(0, bz + bnz - std::max<int64_t>(bz, zo + Lz));
+            lo_ghost += (int64_t)bnx * bny * std::max<int64_t>(0, std::min<int64_t>(bz + bnz, zo) - bz);
+        }
+        sv[n] = tot;
+        // k_sym_build checks that every stored (i, j) between owned rows has its
+        // (j, i); with that, a symmetric pattern holds 2 (upper blocks) - n
+        // blocks, less the upper blocks into upper ghosts, plus the blocks into
+        // lower ghosts -- a block without its partner shows up here
+        if (why.empty() && 2 * blocks - n - up_ghost + lo_ghost != all)
+            why = "symmetric storage: the block pattern is not symmetric (" + std::to_string(all) + " blocks, " +
+                  std::to_string(blocks) + " upper)";
+        if (why.empty() && sym_xl_lds(P) > LDS_PER_CU)
+            why = "symmetric storage: row boxes reach " + std::to_string(P) + " nodes (at most 6 supported)";
     }
-    sv[n] = tot;
-    // k_sym_build checks that every stored (i, j) has its (j, i); with that,
-    // a symmetric pattern holds exactly 2 (upper blocks) - n blocks, so a
-    // lower block without its upper partner shows up here
-    if (2 * blocks - n != all)
-        return fail(KLE_ERR_SUP, "symmetric storage: the block pattern is not symmetric (%lld blocks, %lld upper)",
-                    (long long)all, (long long)blocks);
-    if (sym_xl_lds(P) > LDS_PER_CU)
-        return fail(KLE_ERR_SUP, "symmetric storage: row boxes reach %d nodes (at most 6 supported)", P);
+    bool any = false;
+    KLE_TRY(any_rank(c, !why.empty(), any));
+    if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
+    if (c->nranks > 1) {
+        // the slab pattern across a cut: my blocks into the upper ghosts are
+        // the upper neighbour's blocks into its lower ghosts
+        std::vector<int64_t> ups, los;
+        KLE_TRY(allgather_i64(c, up_ghost, ups));
+        KLE_TRY(allgather_i64(c, lo_ghost, los));
+        bool bad = false;
+        if (A->hi_rank >= 0 && ups[c->rank] != los[A->hi_rank]) bad = true;
+        if (A->lo_rank >= 0 && los[c->rank] != ups[A->lo_rank]) bad = true;
+        KLE_TRY(any_rank(c, bad, any));
+        if (any) return fail(KLE_ERR_SUP, "symmetric storage: the block pattern is not symmetric across ranks");
+    }
     double *rowdiff = nullptr, *rowmax = nullptr;
+    int64_t nomem = 0;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
-        hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess) {
-        (void)hipGetLastError();
-        hipFree(rowdiff);
-        hipFree(rowmax);
-        sym_drop(A);
-        return fail(KLE_ERR_MEM, "out of device memory for symmetric storage");
+        hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess)
+        nomem = 1;
+    double dmax = 0.0, vmax = 0.0;
+    if (!nomem) {
+        KLE_HIP(hipMemcpy(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_sym_build, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, (int)Lx, (int)Ly,
+                           (int)zo, A->d_rowptr, A->d_rowcnt, A->d_rowbox, A->d_vptr, A->d_val, A->d_svptr, A->d_sval,
+                           rowdiff, rowmax);
+        KLE_HIP(hipGetLastError());
+        std::vector<double> hd(n), hm(n);
+        KLE_HIP(hipStreamSynchronize(c->stream));
+        KLE_HIP(hipMemcpy(hd.data(), rowdiff, sizeof(double) * n, hipMemcpyDeviceToHost));
+        KLE_HIP(hipMemcpy(hm.data(), rowmax, sizeof(double) * n, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n; ++i) {
+            dmax = std::max(dmax, hd[i]);
+            vmax = std::max(vmax, hm[i]);
+            if (std::isnan(hd[i])) dmax = INFINITY;
+        }
     }
-    KLE_HIP(hipMemcpy(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_sym_build, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, (int)Lx, (int)Ly,
-                       A->d_rowptr, A->d_rowcnt, A->d_rowbox, A->d_vptr, A->d_val, A->d_svptr, A->d_sval, rowdiff,
-                       rowmax);
-    KLE_HIP(hipGetLastError());
-    std::vector<double> hd(n), hm(n);
-    KLE_HIP(hipStreamSynchronize(c->stream));
-    KLE_HIP(hipMemcpy(hd.data(), rowdiff, sizeof(double) * n, hipMemcpyDeviceToHost));
-    KLE_HIP(hipMemcpy(hm.data(), rowmax, sizeof(double) * n, hipMemcpyDeviceToHost));
+    (void)hipGetLastError();
     hipFree(rowdiff);
     hipFree(rowmax);
-    double dmax = 0.0, vmax = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
-        dmax = std::max(dmax, hd[i]);
-        vmax = std::max(vmax, hm[i]);
-        if (std::isnan(hd[i])) dmax = INFINITY;
+    // the largest entry over all ranks (the tolerances' scale): one-hot sums
+    double vmax_all = vmax;
+    if (c->nranks > 1) {
+        std::vector<int64_t> vb;
+        KLE_TRY(allgather_i64(c, (int64_t)std::ilogb(std::max(vmax, 1e-300)), vb));  // exponents (exact)
+        for (int64_t e : vb) vmax_all = std::max(vmax_all, std::ldexp(1.0, (int)e));
     }
-    if (!(dmax <= 1e-12 * vmax)) {
+    const bool asym = !nomem && !(dmax <= 1e-12 * vmax_all);
+    KLE_TRY(any_rank(c, nomem ? 1 : asym ? 2 : 0, any));
+    if (any) {
         sym_drop(A);
-        return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
+        if (nomem) return fail(KLE_ERR_MEM, "out of device memory for symmetric storage");
+        if (asym)
+            return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
+        return fail(KLE_ERR_SUP, "symmetric storage refused on another rank");
     }
     A->sym_P = P;
     const SymGeo g = sym_geo(A);
@@ -1473,10 +924,14 @@ int sym_build(kle_mat *A)
     for (int64_t t = 0; t < g.ntz; ++t)
         for (int ty = 0; ty < g.nty; ++ty)
             for (int tx = 0; tx < g.ntx; ++tx)
-                ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz);
-    if (hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.RX * g.RY * g.RZ) != hipSuccess ||
-        hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess) {
-        (void)hipGetLastError();
+                ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz + hp);
+    nomem = hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.RX * g.RY * g.RZ) != hipSuccess ||
+            hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
+            (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
+            (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess);
+    (void)hipGetLastError();
+    KLE_TRY(any_rank(c, nomem, any));
+    if (any) {
         sym_drop(A);
         return fail(KLE_ERR_MEM, "out of device memory for the symmetric SpMV workspace");
     }
@@ -1487,7 +942,14 @@ int sym_build(kle_mat *A)
     A->sws_entries = ents;
     A->sblocks = blocks;
     A->snvals = tot;
-    if (P >= 1 && P <= 4) KLE_TRY(cw_build(A, mu_row));
+    if (c->nranks > 1) {
+        bool bad = false;
+        KLE_TRY(sym_probe(A, vmax_all, bad));
+        if (bad) {
+            sym_drop(A);
+            return fail(KLE_ERR_SUP, "matrix is not symmetric across ranks (product probe)");
+        }
+    }
     return 0;
 }
 
@@ -1509,94 +971,113 @@ static int sym_waves(const kle_mat *A)
     return 2 * sym_xl_lds(P) <= LDS_PER_CU && sym_fill_fits(P, 8) ? 8 : 16;
 }
 
-template <int WV, bool DET, int AHEAD>
-static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, const int *istate, hipStream_t st)
+template <int WV, bool DET>
+static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,
+                          const int *istate, hipStream_t st)
 {
+    if (t1 <= t0) return;
     const size_t lds = sym_xl_lds(A->sym_P);
     static size_t lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
     if (lds > lds_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, AHEAD>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_set = lds;
     }
-    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz;
-    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, AHEAD>), dim3((unsigned)ntiles), dim3(64 * WV), lds, st, g,
+    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_rowbox, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
-                       g_tune.spmv_sym_probe);
+                       g_tune.spmv_sym_probe, (int)t0);
 }
 
-template <int WV, bool DET>
-static void launch_sym_xl2(const kle_mat *A, const SymGeo &g, const kle_vec *x, const int *istate, hipStream_t st)
+static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,
+                             const int *istate, hipStream_t st)
 {
-    if (g_tune.spmv_sym_ahead == 1) launch_sym_xl<WV, DET, 1>(A, g, x, istate, st);
-    else launch_sym_xl<WV, DET, 2>(A, g, x, istate, st);
-}
-
-static bool sym_use_cw(const kle_mat *A) { return g_tune.spmv_sym_kernel == 3 && A->d_cw_wsA && A->cw_nchunk > 0; }
-
-int sym_spmv(const kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, hipStream_t st)
-{
-    const SymGeo g = sym_geo(A);
     const bool det = g_tune.spmv_sym_det != 0;
-    if (sym_use_cw(A)) {
-        const size_t lds = sym_cw_lds(A->sym_P);
-        const SymRun *runs = (const SymRun *)A->d_cw_runs;
-#define CW_LAUNCH(PP, DD)                                                                                        \
-    do {                                                                                                         \
-        static size_t attr = 0; /* dynamic LDS above 64 KB is declared per kernel (static LDS: red[]) */         \
-        if (lds > attr) {                                                                                        \
-            KLE_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_cw<PP, DD>),               \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                  \
-            attr = lds;                                                                                          \
-        }                                                                                                        \
-        hipLaunchKernelGGL((k_nb_spmv_sym_cw<PP, DD>), dim3((unsigned)A->cw_nchunk), dim3(CW_NT), lds, st, g,    \
-                           A->d_rowbox, A->d_svptr, A->d_sval, x->base, A->d_cw_wsA, A->d_cw_wsB, runs,          \
-                           A->d_cw_chunk, A->d_cw_rune, istate, g_tune.spmv_sym_probe);                          \
-    } while (0)
-        switch (A->sym_P * 2 + det) {
-        case 2: CW_LAUNCH(1, false); break;
-        case 3: CW_LAUNCH(1, true); break;
-        case 4: CW_LAUNCH(2, false); break;
-        case 5: CW_LAUNCH(2, true); break;
-        case 6: CW_LAUNCH(3, false); break;
-        case 7: CW_LAUNCH(3, true); break;
-        case 8: CW_LAUNCH(4, false); break;
-        default: CW_LAUNCH(4, true); break;
-        }
-#undef CW_LAUNCH
-        hipLaunchKernelGGL(k_nb_sym_gather_cw, dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, g,
-                           A->d_cw_wsA, A->d_cw_wsB, A->d_cw_ovl, y->d, istate);
+    if (sym_waves(A) == 16) {
+        if (det) launch_sym_xl<16, true>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<16, false>(A, g, x, t0, t1, istate, st);
+    } else {
+        if (det) launch_sym_xl<8, true>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<8, false>(A, g, x, t0, t1, istate, st);
+    }
+}
+
+static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int64_t j0, int64_t j1, int64_t nrecv,
+                              const int *istate, hipStream_t st)
+{
+    if (j1 <= j0) return;
+    hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, SYM_TZ>), dim3((unsigned)((j1 - j0 + 255) / 256)), dim3(256), 0, st,
+                       g, A->d_sws, y->d, A->d_sgsend, A->d_sgrecv, nrecv, j0, j1, istate);
+}
+
+// y = A x over the symmetric storage.  N > 1 (z slabs), per SpMV:
+//   main: tiles whose regions stay below the upper ghost planes, while the
+//         comm stream exchanges the forward halo (x ghosts);
+//   main: the remaining tiles, then the upper ghost rows' sums -> d_sgsend;
+//   comm: the reverse halo (d_sgsend up, the lower neighbour's sums for my
+//         lowest rows -> d_sgrecv), while main gathers the rows it does not
+//         touch; main: the lowest rows, + d_sgrecv last (fixed order: y stays
+//         bitwise reproducible with spmv_sym_det).
+// All RCCL calls stay on the comm stream, in the same order on every rank.
+int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
+{
+    kle_ctx *c = A->ctx;
+    hipStream_t st = c->stream;
+    const SymGeo g = sym_geo(A);
+    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz, n = A->nrows, Lxy = (int64_t)g.Lx * g.Ly;
+    const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    if (!dist) {
+        launch_sym_tiles(A, g, x, 0, ntiles, istate, st);
+        launch_sym_gather(A, g, y, 0, n, 0, istate, st);
         KLE_HIP(hipGetLastError());
         return 0;
     }
-    if (sym_waves(A) == 16) {
-        if (det) launch_sym_xl2<16, true>(A, g, x, istate, st);
-        else launch_sym_xl2<16, false>(A, g, x, istate, st);
+    // tiles [0, nin): regions below the owned top (no upper ghost x)
+    const int64_t ntz_in = g.Lz >= g.RZ ? (g.Lz - g.RZ) / g.TZ + 1 : 0;
+    const int64_t nin = std::min(ntiles, ntz_in * g.nty * g.ntx);
+    const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0, jr = nrecv / 3;
+    const bool ovl = A->halo_overlap != 0;
+    if (ovl) {
+        KLE_HIP(hipEventRecord(c->ev_x_ready, st));
+        KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
+        launch_sym_tiles(A, g, x, 0, nin, istate, st);
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, c->comm_stream, nullptr));
+        KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
+        KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
+        launch_sym_tiles(A, g, x, nin, ntiles, istate, st);
     } else {
-        if (det) launch_sym_xl2<8, true>(A, g, x, istate, st);
-        else launch_sym_xl2<8, false>(A, g, x, istate, st);
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, st, nullptr));
+        launch_sym_tiles(A, g, x, 0, ntiles, istate, st);
     }
-    hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, SYM_TZ>), dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st,
-                       g, A->d_sws, y->d, istate);
+    launch_sym_gather(A, g, y, n, n + (int64_t)g.hp * Lxy, 0, istate, st);  // upper ghost rows -> d_sgsend
+    KLE_HIP(hipGetLastError());
+    if (ovl) {
+        KLE_HIP(hipEventRecord(c->ev_x_ready, st));
+        KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
+        KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, c->comm_stream));
+        KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
+        launch_sym_gather(A, g, y, jr, n, 0, istate, st);
+        KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
+        launch_sym_gather(A, g, y, 0, jr, nrecv, istate, st);
+    } else {
+        KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, st));
+        launch_sym_gather(A, g, y, 0, n, nrecv, istate, st);
+    }
     KLE_HIP(hipGetLastError());
     return 0;
 }
 
 std::string sym_kernel_name(const kle_mat *A)
 {
-    if (sym_use_cw(A))
-        return std::string("k_nb_spmv_sym_cw<") + (g_tune.spmv_sym_det ? "true" : "false") + ">+k_nb_sym_gather_cw";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
-           (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(g_tune.spmv_sym_ahead == 1 ? 1 : 2) +
-           ">+k_nb_sym_gather<8,2>";
+           (g_tune.spmv_sym_det ? "true" : "false") + ">+k_nb_sym_gather<8,2>";
 }
 
 // symmetric storage: the stored (upper) blocks, per row its value offset and
 // box, x and y once, the tile partials written and read
 double sym_spmv_bytes(const kle_mat *A)
 {
-    if (sym_use_cw(A))  // column walk: the column partials written and read
-        return (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 + (double)A->cw_entries * 48.0;
     return (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 + (double)A->sws_entries * 48.0;
 }
 

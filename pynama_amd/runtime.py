@@ -235,6 +235,8 @@ def get_ctx():
             set_tuning("spmv_waves", int(os.environ["KLE_SPMV_WAVES"]))
         if os.environ.get("KLE_SPMV_SYM"):
             set_tuning("spmv_sym", int(os.environ["KLE_SPMV_SYM"]))
+        if os.environ.get("KLE_SPMV_SYM_MIN_ROWS"):
+            set_tuning("spmv_sym_min_rows", int(os.environ["KLE_SPMV_SYM_MIN_ROWS"]))
         if os.environ.get("KLE_SPMV_DICT_MIN_ROWS"):
             set_tuning("spmv_dict_min_rows", int(os.environ["KLE_SPMV_DICT_MIN_ROWS"]))
         _CTX = Context()

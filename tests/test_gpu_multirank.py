@@ -21,7 +21,8 @@ def _free_port():
     return p
 
 
-def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0):
+def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0,
+            sym=False):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="host",
@@ -29,6 +30,8 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
     if waves:  # 8: the LDS SpMV kernels (x-in-LDS / column dictionaries) at test sizes
         os.environ["KLE_SPMV_WAVES"] = str(waves)
         os.environ["KLE_SPMV_DICT_MIN_ROWS"] = "0"
+    # symmetric storage at every size (kle_assemble_kle: 64000 node rows), or never
+    os.environ["KLE_SPMV_SYM_MIN_ROWS"] = "0" if sym else str(1 << 30)
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=size)
@@ -76,7 +79,8 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
                "vec_range": dn.getOwnershipRange(), "dot": vort.dot(vort),
                "overlap_equal": bool(np.array_equal(y_ov, y_pl)), "y": y_ov, "x": xv.getArray(),
                "coords": dom.getFullCoordArray().reshape(-1, 3),
-               "ov_diff": (np.nonzero(y_ov != y_pl)[0][:12].tolist(), len(y_ov))}
+               "ov_diff": (np.nonzero(y_ov != y_pl)[0][:12].tolist(), len(y_ov)),
+               "sym": mat.K.isSymmetricStorage(), "kernel": mat.K.spmvKernel()}
         q.put(res)
     except Exception as e:  # report instead of hanging the peer
         import traceback
@@ -120,18 +124,37 @@ def test_partitioned_solve_x_in_lds(size, nelem, ngl, ksp_type):
     _check_box(size, nelem, ngl, True, ksp_type, waves=8)
 
 
-def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0):
+@pytest.mark.parametrize("ksp_type,overlap", [("cg", True), ("cg", False), ("pipecg", True)])
+@pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 4), (3, [2, 3, 3], 3), (2, [3, 2, 4], 5),
+                                            (8, [2, 2, 8], 4)])
+def test_partitioned_solve_symmetric_storage(size, nelem, ngl, ksp_type, overlap):
+    """Symmetric (upper-triangle) storage on every rank of a slab partition:
+    each rank streams only its rows' blocks from the diagonal on, the blocks
+    into the upper ghost planes add their transposed parts to ghost rows,
+    whose sums the reverse halo returns to their owner.  Same checks as the
+    full storage: the serial oracle's solution, K's rows, y = K x to rounding,
+    and the overlapped schedule bitwise equal to the plain one."""
+    res = _check_box(size, nelem, ngl, overlap, ksp_type, sym=True)
+    for r in res:
+        assert r["sym"], r["rank"]
+        assert r["kernel"].startswith("k_nb_spmv_sym_xl<"), r["kernel"]
+
+
+def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, None, None, waves))
+    procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, None, None, waves,
+                                               sym))
              for r in range(size)]
     res = _collect(procs, q, size)
     for r in res:
         assert r["overlap_equal"], (r["rank"], r["ov_diff"])
+        if not sym:
+            assert not r["sym"], r["rank"]
     # serial oracle system on the same numbering
     dim = len(nelem)
     om = O.BoxMesh(dim, nelem, [0] * dim, [1] * dim, ngl)
@@ -167,6 +190,7 @@ def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0):
                                    rtol=1e-13, atol=1e-10)
     ranges = [r["vec_range"] for r in res]
     assert ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    return res
 
 
 def _run(size, nelem, ngl, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0):

@@ -40,9 +40,8 @@ def _mat(pa, nelem, ngl):
     return dom, mat
 
 
-KNOBS = ({}, {"spmv_sym_det": 0}, {"spmv_sym_kernel": 2}, {"spmv_sym_kernel": 2, "spmv_sym_det": 0},
-         {"spmv_sym_kernel": 2, "spmv_sym_ahead": 1}, {"spmv_sym_kernel": 2, "spmv_sym_waves": 16})
-DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_kernel": 2, "spmv_sym_waves": 0, "spmv_sym_ahead": 1}
+KNOBS = ({}, {"spmv_sym_det": 0}, {"spmv_sym_waves": 16}, {"spmv_sym_waves": 16, "spmv_sym_det": 0})
+DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_waves": 0}
 
 
 @pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([6, 5, 3], 2),
@@ -250,7 +249,7 @@ def test_symmetric_storage_refused_where_it_does_not_apply(pa):
     _, m6 = _mat(pa, [2, 2, 2], 7)
     m6.K.setOption(m6.K.Option.SPD, True)
     assert m6.K.isSymmetricStorage()
-    assert m6.K.spmvKernel().startswith("k_nb_spmv_sym_xl<16,")  # (P = 6: no column walk)
+    assert m6.K.spmvKernel().startswith("k_nb_spmv_sym_xl<16,")  # (P = 6: 16 waves, one workgroup per CU)
 
 
 def test_assembly_turns_symmetric_storage_on_from_the_threshold(pa):

@@ -140,7 +140,8 @@ def test_rk5bs_steps_match_cpu_restatement(pa):
     the restated algorithm: the increment X_4 - X_0 agrees to 1e-9 relative
     (measured 6.7e-13; CG at rtol 1e-13 on both sides)."""
     from oracle import oracle as O
-    from pynama_amd.ts import TABLEAUX, TsSolver
+    from bs54_tableau import B as B54, C as C54
+    from pynama_amd.ts import TsSolver
     nelem, ngl, h, nsteps = [6, 6], 5, 0.01, 4
     cfg = {"name": "tg", "material-properties": {"rho": 0.5, "mu": 0.01},
            "domain": {"ngl": ngl, "box-mesh": {"nelem": nelem, "lower": [0, 0], "upper": [1, 1]}},
@@ -182,7 +183,9 @@ def test_rk5bs_steps_match_cpu_restatement(pa):
         vel, _, _ = K.cg(Rw.mult(X) + Kr.mult(ubc), rtol=1e-13)
         return O.eval_rhs_chain(Curl, SrT, DivSrT, vel, rho, mu, 2)[2]
 
-    _, _, fsal, c, A, b, _ = TABLEAUX["5bs"]
+    # the published tableau typed into the test (tests/bs54_tableau.py), not
+    # the product's: TSRK5BS is FSAL; the stage-blind RHS reads only c and b
+    fsal, c, b = True, [float(v) for v in C54], [float(v) for v in B54]
     s = len(c)
 
     def integrate(use_fsal):
