@@ -572,6 +572,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
+    } else if (k == "spmv_sym_tz") {
+        KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
+        g_tune.spmv_sym_tz = value;
     } else if (k == "spmv_sym_probe") {
         KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
         g_tune.spmv_sym_probe = value;
@@ -607,6 +610,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym") *value = g_tune.spmv_sym;
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
+    else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);

@@ -239,9 +239,10 @@ struct kle_mat {
     int64_t *d_svptr = nullptr;
     double *d_sws = nullptr;
     int *d_stile_e = nullptr;  // per tile: 2^e bounds its transposed row sums (fixed-point scale, k_sym_bound)
+    int *d_srow = nullptr;     // per row: offset in its box and box extents, 4 bits each (the SpMV's row set-up)
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
-    int sym_P = 0;
+    int sym_P = 0, sym_TZ = 2;
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
     // export: DoF-level entry rule inside the node blocks (no-slip matrices,
     // MASK_* below) and the ext-range DoF classes it reads
@@ -309,7 +310,8 @@ struct Tuning {
     int spmv_sym_min_rows = 64000;
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
-    int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 4 LDS x reads, 8 partial stores, 16 x fill loads
+    int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
+    int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 4 LDS x reads, 8 partial stores, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)
 };

@@ -27,7 +27,7 @@ namespace kle {
 // 2 x 2 x (P/TZ+2)) tiles whose regions contain it, in a fixed tile order.
 // HBM: the stored values once (half of the full storage) + the partials
 // written and read once.
-constexpr int SYM_TX = 8, SYM_TY = 8, SYM_TZ = 2;
+constexpr int SYM_TX = 8;  // tile rows in x; TY x TZ (8 x 2 or 4 x 4) per matrix: sym_TZ
 constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (one pass over the region)
 // Lattices: the rows are the owned Lx x Ly x Lz nodes; the columns add zo
 // lattice planes of lower ghosts before them and hp of upper ghosts after
@@ -37,7 +37,7 @@ constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (on
 // ghosts add their transposed parts to ghost rows, whose partials go back to
 // the owner (sym_spmv's reverse halo).
 struct SymGeo {
-    int Lx, Ly, Lz, P, TX, TZ, RX, RY, RZ, ntx, nty, ntz, zo, hp;
+    int Lx, Ly, Lz, P, TX, TY, TZ, RX, RY, RZ, ntx, nty, ntz, zo, hp;
 };
 
 __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
@@ -148,10 +148,9 @@ __device__ __forceinline__ double wsum_dpp(double v)
 // average 1.4 passes of 64 blocks, so one item at a time leaves it waiting
 // on HBM latency at every row).
 struct SymRow {
-    int64_t i;
     const double *v;
     double x0, x1, x2;
-    int bx, by, bz, bnx, bnxy, k0, mu, rx0, ry0, rz0, own;
+    int bnx, bnxy, k0, mu, rx0, ry0, rz0, own;
     float ibnx, ibnxy;  // 1/bnx, 1/bnxy: quotients of block positions by float multiply + one fix-up
 };
 
@@ -243,8 +242,8 @@ __device__ __forceinline__ void sym_wait9(double *v)
                  : "i"(N));
 }
 
-template <int WV, bool DET>
-__global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const int *__restrict__ rowbox,
+template <int WV, bool DET, int TY, int TZ>
+__global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const int *__restrict__ srow,
                                                              const int64_t *__restrict__ svptr,
                                                              const double *__restrict__ sval,
                                                              const double *__restrict__ x, double *__restrict__ ws,
@@ -255,8 +254,9 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     // component take the adds of masked lanes) | direct row sums [3][TR]
     extern __shared__ double lds[];
     if (istate && istate[I_REASON] != 0) return;
-    constexpr int TZ = SYM_TZ, TR = SYM_TX * SYM_TY * TZ, NT = 64 * WV;
-    constexpr int NQ = SYM_TX * SYM_TY / WV;  // row slots per wave and plane
+    static_assert(TY * TZ == 16, "tiles of 128 rows");
+    constexpr int TR = SYM_TX * TY * TZ, NT = 64 * WV;
+    constexpr int NQ = SYM_TX * TY / WV;  // row slots per wave and plane
     constexpr int NS = NQ * TZ;               // row slots per wave
     const int RN = g.RX * g.RY * g.RZ, RS = RN + 64;
     double *xl = lds, *yl = lds + 3 * RN, *yd = lds + 3 * RN + 3 * RS;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;
-    const int x0 = tix * SYM_TX, y0 = tiy * SYM_TY, ox = x0 - g.P, oy = y0 - g.P;
+    const int x0 = tix * SYM_TX, y0 = tiy * TY, ox = x0 - g.P, oy = y0 - g.P;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     const int nx = min(SYM_TX, g.Lx - x0);
@@ -283,14 +283,13 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     // masked afterwards) and every use of a loaded value is too: a load or a
     // use under a branch makes the compiler's wait counting conservative, and
     // it then drains the whole load queue at every item.
-    // 1. the wave's row descriptors (box, value offset): lane s holds slot s
-    int pb, pd, psl, psh;
+    // 1. the wave's row descriptors (packed box, value offset): lane s holds slot s
+    int pd, psl, psh;
     {
         const bool ok = lane < NS && slot_ok(lane);
         const int64_t i =
             ok ? x0 + slot_x(lane) + (int64_t)g.Lx * (y0 + slot_y(lane)) + Lxy * (tz + lane / NQ) : 0;
-        pb = rowbox[2 * i];
-        pd = rowbox[2 * i + 1];
+        pd = srow[i];
         const int64_t o = svptr[i];
         psl = (int)(uint32_t)o;
         psh = (int)(o >> 32);
@@ -315,31 +314,28 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     }
     for (int k = threadIdx.x; k < 3 * RS; k += NT) yl[k] = 0.0;
     for (int k = threadIdx.x; k < 3 * TR; k += NT) yd[k] = 0.0;
+    // a row from its packed descriptor (sym_row_desc): no divisions -- the
+    // scalar unit is shared by the CU's waves, and 64-bit box arithmetic per
+    // row cost as many instructions as the row's items
     auto slot_row = [&](int s, SymRow &R) {
-        const int xg = x0 + slot_x(s), yy = y0 + slot_y(s), zz = tz + s / NQ;
-        R.i = xg + (int64_t)g.Lx * yy + Lxy * zz;
-        const int64_t base = __builtin_amdgcn_readlane(pb, s);
+        const int sx = slot_x(s), sy = slot_y(s), sz = s / NQ;  // the row in the tile
         const int d = __builtin_amdgcn_readlane(pd, s);
-        R.bz = (int)(base / Lxy);
-        const int64_t rem = base - (int64_t)R.bz * Lxy;
-        R.by = (int)(rem / g.Lx);
-        R.bx = (int)(rem - (int64_t)R.by * g.Lx);
-        R.bz -= g.zo;  // (owned coordinates)
-        R.bnx = d & 255;
-        const int bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
+        const int dbx = d & 15, dby = (d >> 4) & 15, dbz = (d >> 8) & 15;
+        R.bnx = (d >> 12) & 15;
+        const int bny = (d >> 16) & 15, bnz = (d >> 20) & 15;
         R.bnxy = R.bnx * bny;
-        R.ibnx = 1.0f / (float)R.bnx;
-        R.ibnxy = 1.0f / (float)R.bnxy;
-        R.k0 = (xg - R.bx) + R.bnx * ((yy - R.by) + bny * (zz - R.bz));
+        R.ibnx = __builtin_amdgcn_rcpf((float)R.bnx);  // (sym_div fixes the quotient up)
+        R.ibnxy = __builtin_amdgcn_rcpf((float)R.bnxy);
+        R.k0 = dbx + R.bnx * (dby + bny * dbz);
         R.mu = R.bnxy * bnz - R.k0;
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(psl, s);
         const int64_t hi = __builtin_amdgcn_readlane(psh, s);
         R.v = sval + ((hi << 32) | lo);
-        R.rx0 = R.bx - ox;
-        R.ry0 = R.by - oy;
-        R.rz0 = R.bz - tz;
-        R.own = (xg - x0) + SYM_TX * ((yy - y0) + SYM_TY * (zz - tz));  // row slot in the tile
-        const int ir = (xg - ox) + g.RX * ((yy - oy) + g.RY * (zz - tz));  // its region index
+        R.rx0 = g.P + sx - dbx;  // box corner in the region
+        R.ry0 = g.P + sy - dby;
+        R.rz0 = sz - dbz;
+        R.own = sx + SYM_TX * (sy + TY * sz);  // row slot in the tile
+        const int ir = (sx + g.P) + g.RX * ((sy + g.P) + g.RY * sz);  // its region index
         R.x0 = uni_d(xl[ir]);  // (the first row re-reads these once the fill has landed)
         R.x1 = uni_d(xl[RN + ir]);
         R.x2 = uni_d(xl[2 * RN + ir]);
@@ -363,7 +359,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const int kk = min(kb + lane, R.mu - 1);
         const int q16 = R.mu & ~15;
         const bool ch = kk < q16;
-        const int64_t o0 = ch ? (int64_t)((kk >> 4) * 144 + (kk & 15)) : (int64_t)q16 * 9 + (kk - q16);
+        const int o0 = ch ? (kk >> 4) * 144 + (kk & 15) : q16 * 9 + (kk - q16);
         const int st = ch ? 16 : R.mu - q16;
         unsigned o[9];
 #pragma unroll
@@ -431,7 +427,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         double m = 0.0;
         int bad = 0;
         for (int r = lane; r < TR; r += 64) {
-            const int k = (g.P + (r & 7)) + g.RX * ((g.P + ((r >> 3) & 7)) + g.RY * (r >> 6));
+            const int k = (g.P + (r & 7)) + g.RX * ((g.P + (r >> 3) % TY) + g.RY * (r / (SYM_TX * TY)));
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const double a = fabs(xl[c * RN + k]);
@@ -452,7 +448,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
             invS = ldexp(1.0, E - 61);
         }
     }
-    if (any) {
+    if (any && !(probe & 128)) {  // (timing probe 128: no item loop)
         int xc = next_slot(0), kc = 0;
         slot_row(xc, C);  // (x_i from LDS, now that the fill has landed)
         double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
@@ -524,8 +520,8 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
         const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
         if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz + g.hp) continue;
-        const bool own = rx >= g.P && rx < g.P + SYM_TX && ry >= g.P && ry < g.P + SYM_TY && rz < TZ;
-        const int sl = (rx - g.P) + SYM_TX * ((ry - g.P) + SYM_TY * rz);
+        const bool own = rx >= g.P && rx < g.P + SYM_TX && ry >= g.P && ry < g.P + TY && rz < TZ;
+        const int sl = (rx - g.P) + SYM_TX * ((ry - g.P) + TY * rz);
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
             double v = DET ? fx_to_d(yi[b * RS + k]) * invS : yl[b * RS + k];
@@ -547,18 +543,19 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
                                                    const int64_t *__restrict__ svptr,
                                                    const double *__restrict__ sval, int *__restrict__ tile_e)
 {
-    constexpr int TR = SYM_TX * SYM_TY * SYM_TZ;
-    __shared__ int sb[TR], sd[TR];
-    __shared__ int64_t so[TR];
+    constexpr int TRM = 128;  // rows of a tile
+    const int TR = SYM_TX * g.TY * g.TZ;
+    __shared__ int sb[TRM], sd[TRM];
+    __shared__ int64_t so[TRM];
     __shared__ double wred[256];
     const int64_t t = blockIdx.x;
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
-    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * SYM_TZ;
-    const int x0 = tix * SYM_TX, y0 = tiy * SYM_TY, ox = x0 - g.P, oy = y0 - g.P;
+    const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * g.TZ;
+    const int x0 = tix * SYM_TX, y0 = tiy * g.TY, ox = x0 - g.P, oy = y0 - g.P;
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     for (int r = threadIdx.x; r < TR; r += 256) {
-        const int xi = x0 + (r & 7), yi = y0 + ((r >> 3) & 7), zi = tz + (r >> 6);
+        const int xi = x0 + (r & 7), yi = y0 + (r >> 3) % g.TY, zi = tz + r / (SYM_TX * g.TY);
         sd[r] = 0;
         if (xi < g.Lx && yi < g.Ly && zi < g.Lz) {
             const int64_t i = xi + (int64_t)g.Lx * yi + Lxy * zi;
@@ -583,7 +580,7 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
             const int bx = (int)(base - bze * Lxy - (int64_t)by * g.Lx), bz = bze - g.zo;
             const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
             if (gx < bx || gx >= bx + bnx || gy < by || gy >= by + bny || gz < bz || gz >= bz + bnz) continue;
-            const int xi = x0 + (r & 7), yi = y0 + ((r >> 3) & 7), zi = tz + (r >> 6);
+            const int xi = x0 + (r & 7), yi = y0 + (r >> 3) % g.TY, zi = tz + r / (SYM_TX * g.TY);
             const int k0 = (xi - bx) + bnx * ((yi - by) + bny * (zi - bz));
             const int kj = (gx - bx) + bnx * ((gy - by) + bny * (gz - bz));
             if (kj <= k0) continue;
@@ -619,7 +616,7 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
 // and (N > 1) the upper ghost rows, whose sums go to gsend (the reverse halo's
 // send buffer, ghost row j at gsend[3 (j - n)]).  The first nrecv entries of y
 // add the lower neighbour's sums for them (grecv, its upper ghost rows) last.
-template <int TXW, int TZ>
+template <int TXW, int TY, int TZ>
 __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *__restrict__ ws, double *__restrict__ y,
                                                        double *__restrict__ gsend, const double *__restrict__ grecv,
                                                        int64_t nrecv, int64_t j0, int64_t j1,
@@ -633,14 +630,14 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     const int RN = g.RX * g.RY * g.RZ;
     // tiles whose [t*T - P, t*T - P + R) contains the coordinate
     const int x_lo = max(0, (jx + g.P - g.RX + TXW) / TXW), x_hi = min(g.ntx - 1, (jx + g.P) / TXW);
-    const int y_lo = max(0, (jy + g.P - g.RY + SYM_TY) / SYM_TY), y_hi = min(g.nty - 1, (jy + g.P) / SYM_TY);
+    const int y_lo = max(0, (jy + g.P - g.RY + TY) / TY), y_hi = min(g.nty - 1, (jy + g.P) / TY);
     const int z_lo = max(0, (jz - g.RZ + TZ) / TZ), z_hi = min(g.ntz - 1, jz / TZ);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int tzi = z_lo; tzi <= z_hi; ++tzi)
         for (int ty = y_lo; ty <= y_hi; ++ty)
             for (int tx = x_lo; tx <= x_hi; ++tx) {
                 const int64_t t = ((int64_t)tzi * g.nty + ty) * g.ntx + tx;
-                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * SYM_TY - g.P)) + g.RY * (jz - tzi * TZ));
+                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * TY - g.P)) + g.RY * (jz - tzi * TZ));
                 const double *p = ws + t * 3 * (int64_t)RN + r;
                 s0 += p[0];
                 s1 += p[RN];
@@ -672,6 +669,7 @@ void sym_forget(kle_mat *A)
     A->d_sws = nullptr;
     A->d_stile_e = nullptr;
     A->d_sgsend = A->d_sgrecv = nullptr;
+    A->d_srow = nullptr;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
 }
@@ -679,7 +677,7 @@ void sym_forget(kle_mat *A)
 void sym_drop(kle_mat *A)
 {
     for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
-                    (void *)A->d_sgsend, (void *)A->d_sgrecv})
+                    (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow})
         if (q) (void)hipFree(q);
     sym_forget(A);
 }
@@ -689,7 +687,8 @@ static SymGeo sym_geo(const kle_mat *A)
     SymGeo g;
     const int P = A->sym_P;
     g.TX = SYM_TX;
-    g.TZ = SYM_TZ;
+    g.TZ = A->sym_TZ;
+    g.TY = 16 / g.TZ;
     g.Lx = (int)A->row_lat[0];
     g.Ly = (int)A->row_lat[1];
     g.Lz = (int)A->row_lat[2];
@@ -698,21 +697,33 @@ static SymGeo sym_geo(const kle_mat *A)
     g.hp = (int)(A->ghost_hi / plane3);
     g.P = P;
     g.RX = g.TX + 2 * P;
-    g.RY = SYM_TY + 2 * P;
+    g.RY = g.TY + 2 * P;
     g.RZ = g.TZ + P;
     g.ntx = (g.Lx + g.TX - 1) / g.TX;
-    g.nty = (g.Ly + SYM_TY - 1) / SYM_TY;
+    g.nty = (g.Ly + g.TY - 1) / g.TY;
     g.ntz = (g.Lz + g.TZ - 1) / g.TZ;
     return g;
 }
 
 // LDS of the x-in-LDS kernel: x and y of the region, the tile's direct row sums
-static size_t sym_xl_lds(int P)
+static size_t sym_xl_lds(int P, int TZ)
 {
-    const size_t RN = (size_t)(SYM_TX + 2 * P) * (SYM_TY + 2 * P) * (SYM_TZ + P);
-    return (6 * RN + 3 * 64 + 3 * SYM_TX * SYM_TY * SYM_TZ) * sizeof(double);
+    const size_t RN = (size_t)(SYM_TX + 2 * P) * (16 / TZ + 2 * P) * (TZ + P);
+    return (6 * RN + 3 * 64 + 3 * 128) * sizeof(double);
 }
 constexpr size_t LDS_PER_CU = 163840;
+
+// Waves per workgroup of the x-in-LDS kernel: 8 while two workgroups fit a
+// CU's LDS (P <= 4), else 16 (one workgroup of 16 waves per CU);
+// kle_set_tuning("spmv_sym_waves") overrides.
+// The x fill is one pass of SYM_FILL loads per thread: 16 waves where 8 would
+// need more (P >= 5).
+static bool sym_fill_fits(int P, int wv, int TZ)
+{
+    const int RX = SYM_TX + 2 * P, NL = (16 / TZ + 2 * P) * (TZ + P), fstep = 64 * wv / (3 * RX);
+    return NL <= SYM_FILL * fstep;
+}
+
 
 // every rank's flag -> whether any rank raised it (one collective; one rank:
 // no communication)
@@ -812,6 +823,7 @@ int sym_build(kle_mat *A)
     const int64_t zo = why.empty() ? A->ghost_lo / (3 * Lxy) : 0, hp = why.empty() ? A->ghost_hi / (3 * Lxy) : 0;
     std::vector<int> rb, rp, cnt;
     std::vector<int64_t> sv;
+    std::vector<int> srow;  // per row: x-bx, y-by, z-bz, bnx, bny, bnz (4 bits each)
     int P = 0;
     int64_t tot = 0, blocks = 0, all = 0, up_ghost = 0, lo_ghost = 0;
     if (why.empty()) {
@@ -819,6 +831,7 @@ int sym_build(kle_mat *A)
         rp.resize(n + 1);
         cnt.resize(n);
         sv.resize(n + 1);
+        srow.resize(n);
         KLE_HIP(hipStreamSynchronize(c->stream));
         KLE_HIP(hipMemcpy(rb.data(), A->d_rowbox, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
         KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
@@ -838,6 +851,11 @@ int sym_build(kle_mat *A)
                 break;
             }
             P = std::max<int>(P, (int)std::max({x - bx, bx + bnx - 1 - x, y - by, by + bny - 1 - y, bz + bnz - 1 - z}));
+            if (bnx > 15 || bny > 15 || bnz > 15) {
+                why = "symmetric storage: row boxes wider than 15 nodes";
+                break;
+            }
+            srow[i] = (int)((x - bx) | (y - by) << 4 | (z - bz) << 8) | bnx << 12 | bny << 16 | bnz << 20;
             const int k0 = (int)((x - bx) + bnx * ((y - by) + (int64_t)bny * (z - bz)));
             const int64_t mu = cnt[i] - k0;
             sv[i] = tot;
@@ -855,9 +873,16 @@ int sym_build(kle_mat *A)
         if (why.empty() && 2 * blocks - n - up_ghost + lo_ghost != all)
             why = "symmetric storage: the block pattern is not symmetric (" + std::to_string(all) + " blocks, " +
                   std::to_string(blocks) + " upper)";
-        if (why.empty() && sym_xl_lds(P) > LDS_PER_CU)
+        if (why.empty() && sym_xl_lds(P, 2) > LDS_PER_CU)
             why = "symmetric storage: row boxes reach " + std::to_string(P) + " nodes (at most 6 supported)";
     }
+    // tile shape: 8 x 4 x 4 rows (default where two workgroups of 8 waves fit
+    // a CU: P <= 4) or 8 x 8 x 2 -- the same 128 rows and, at P = 4, the same
+    // 1536-node region, but a 4-plane tile spans a whole p = 4 element layer,
+    // so every tile holds the same mix of row lengths (rows on element-
+    // boundary planes carry 4 planes of upper blocks, the next ones 3, 2, 1)
+    const int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(P, 4) <= LDS_PER_CU &&
+                           sym_fill_fits(P, 8, 4) ? 4 : 2;
     bool any = false;
     KLE_TRY(any_rank(c, !why.empty(), any));
     if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
@@ -876,12 +901,14 @@ int sym_build(kle_mat *A)
     double *rowdiff = nullptr, *rowmax = nullptr;
     int64_t nomem = 0;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&A->d_srow, sizeof(int) * std::max<int64_t>(n, 1)) != hipSuccess ||
         hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
         hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess)
         nomem = 1;
     double dmax = 0.0, vmax = 0.0;
     if (!nomem) {
         KLE_HIP(hipMemcpy(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+        KLE_HIP(hipMemcpy(A->d_srow, srow.data(), sizeof(int) * n, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(k_sym_build, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, (int)Lx, (int)Ly,
                            (int)zo, A->d_rowptr, A->d_rowcnt, A->d_rowbox, A->d_vptr, A->d_val, A->d_svptr, A->d_sval,
                            rowdiff, rowmax);
@@ -916,6 +943,7 @@ int sym_build(kle_mat *A)
         return fail(KLE_ERR_SUP, "symmetric storage refused on another rank");
     }
     A->sym_P = P;
+    A->sym_TZ = TZ;
     const SymGeo g = sym_geo(A);
     const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz;
     auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
@@ -924,7 +952,7 @@ int sym_build(kle_mat *A)
     for (int64_t t = 0; t < g.ntz; ++t)
         for (int ty = 0; ty < g.nty; ++ty)
             for (int tx = 0; tx < g.ntx; ++tx)
-                ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * SYM_TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz + hp);
+                ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * g.TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz + hp);
     nomem = hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.RX * g.RY * g.RZ) != hipSuccess ||
             hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
             (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
@@ -953,38 +981,28 @@ int sym_build(kle_mat *A)
     return 0;
 }
 
-// Waves per workgroup of the x-in-LDS kernel: 8 while two workgroups fit a
-// CU's LDS (P <= 4), else 16 (one workgroup of 16 waves per CU);
-// kle_set_tuning("spmv_sym_waves") overrides.
-// The x fill is one pass of SYM_FILL loads per thread: 16 waves where 8 would
-// need more (P >= 5).
-static bool sym_fill_fits(int P, int wv)
-{
-    const int RX = SYM_TX + 2 * P, NL = (SYM_TY + 2 * P) * (SYM_TZ + P), fstep = 64 * wv / (3 * RX);
-    return NL <= SYM_FILL * fstep;
-}
-
 static int sym_waves(const kle_mat *A)
 {
     const int P = A->sym_P;
-    if (g_tune.spmv_sym_waves && sym_fill_fits(P, g_tune.spmv_sym_waves)) return g_tune.spmv_sym_waves;
-    return 2 * sym_xl_lds(P) <= LDS_PER_CU && sym_fill_fits(P, 8) ? 8 : 16;
+    const int TZ = A->sym_TZ;
+    if (g_tune.spmv_sym_waves && sym_fill_fits(P, g_tune.spmv_sym_waves, TZ)) return g_tune.spmv_sym_waves;
+    return 2 * sym_xl_lds(P, TZ) <= LDS_PER_CU && sym_fill_fits(P, 8, TZ) ? 8 : 16;
 }
 
-template <int WV, bool DET>
+template <int WV, bool DET, int TZ>
 static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,
                           const int *istate, hipStream_t st)
 {
     if (t1 <= t0) return;
-    const size_t lds = sym_xl_lds(A->sym_P);
+    const size_t lds = sym_xl_lds(A->sym_P, TZ);
     static size_t lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
     if (lds > lds_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_set = lds;
     }
-    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
-                       A->d_rowbox, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
+    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
+                       A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
                        g_tune.spmv_sym_probe, (int)t0);
 }
 
@@ -992,12 +1010,15 @@ static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x
                              const int *istate, hipStream_t st)
 {
     const bool det = g_tune.spmv_sym_det != 0;
-    if (sym_waves(A) == 16) {
-        if (det) launch_sym_xl<16, true>(A, g, x, t0, t1, istate, st);
-        else launch_sym_xl<16, false>(A, g, x, t0, t1, istate, st);
+    if (g.TZ == 4) {
+        if (det) launch_sym_xl<8, true, 4>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<8, false, 4>(A, g, x, t0, t1, istate, st);
+    } else if (sym_waves(A) == 16) {
+        if (det) launch_sym_xl<16, true, 2>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<16, false, 2>(A, g, x, t0, t1, istate, st);
     } else {
-        if (det) launch_sym_xl<8, true>(A, g, x, t0, t1, istate, st);
-        else launch_sym_xl<8, false>(A, g, x, t0, t1, istate, st);
+        if (det) launch_sym_xl<8, true, 2>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<8, false, 2>(A, g, x, t0, t1, istate, st);
     }
 }
 
@@ -1005,8 +1026,13 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
                               const int *istate, hipStream_t st)
 {
     if (j1 <= j0) return;
-    hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, SYM_TZ>), dim3((unsigned)((j1 - j0 + 255) / 256)), dim3(256), 0, st,
-                       g, A->d_sws, y->d, A->d_sgsend, A->d_sgrecv, nrecv, j0, j1, istate);
+    const dim3 grid((unsigned)((j1 - j0 + 255) / 256));
+    if (g.TZ == 4)
+        hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 4, 4>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
+                           A->d_sgrecv, nrecv, j0, j1, istate);
+    else
+        hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 8, 2>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
+                           A->d_sgrecv, nrecv, j0, j1, istate);
 }
 
 // y = A x over the symmetric storage.  N > 1 (z slabs), per SpMV:
@@ -1071,7 +1097,9 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
 std::string sym_kernel_name(const kle_mat *A)
 {
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
-           (g_tune.spmv_sym_det ? "true" : "false") + ">+k_nb_sym_gather<8,2>";
+           (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(16 / A->sym_TZ) + "," +
+           std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(16 / A->sym_TZ) + "," +
+           std::to_string(A->sym_TZ) + ">";
 }
 
 // symmetric storage: the stored (upper) blocks, per row its value offset and

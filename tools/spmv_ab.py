@@ -11,6 +11,7 @@ import os
 import statistics
 import sys
 
+BUILD_KNOBS = {"spmv_sym_tz"}  # read when the symmetric storage is built
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -49,6 +50,8 @@ def main():
         for i, v in enumerate(variants):
             for k, val in v.items():
                 set_tuning(k, val)
+            if BUILD_KNOBS & set(v):
+                K.setOption(K.Option.SPD, True)  # (re)build the symmetric storage with them
             name = K.spmvKernel()
             for _ in range(5):
                 K.mult(x, y)
@@ -63,8 +66,10 @@ def main():
             for k in v:
                 if k in DEFAULTS:
                     set_tuning(k, DEFAULTS[k])
-                elif k == "spmv_sym_probe":
+                elif k in ("spmv_sym_probe", "spmv_sym_tz"):
                     set_tuning(k, 0)
+            if BUILD_KNOBS & set(v):
+                K.setOption(K.Option.SPD, True)
             res[i].append(ms / c)
             print(json.dumps({"rep": rep, "variant": v, "kernel": name, "spmv_ms": ms / c}), flush=True)
     print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]), "min_ms": min(res[i])}
