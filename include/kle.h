@@ -80,13 +80,15 @@ const char *kle_last_error(void);
  * (1 default: CG update kernels load their first element and the stage inputs
  * before the prologue; 0 off), "spmv_sym" (1 default: matrices holding
  * symmetric storage run the symmetric SpMV; 0 the full storage),
- * "spmv_sym_min_rows" (node rows from which kle_assemble_kle gives the
- * single-rank K symmetric storage; default 64000), "spmv_sym_det" (1
+ * "spmv_sym_min_rows" (node rows per rank from which kle_assemble_kle gives
+ * K symmetric storage; default 64000), "spmv_sym_tz" (read when the storage
+ * is built: 0 auto = 8 x 4 x 4-row tiles where two 8-wave workgroups fit a
+ * CU, 2 = 8 x 8 x 2), "spmv_sym_det" (1
  * default: the transposed adds as exact fixed-point sums, y bitwise
  * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
  * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_sym_probe"
  * (timing probes that skip parts of the symmetric SpMV: wrong results on
- * purpose; 0 default). */
+ * purpose; 0 default; bits in kle_internal.hpp). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
@@ -338,8 +340,11 @@ int kle_mat_is_structured(const kle_mat *A, int *on);
  * MATSBAIJ layout; kle_solver.py:33-37 solves with the SPD K): keep only each
  * row's blocks from its diagonal block on and run the SpMV over them, every
  * stored off-diagonal block serving row i and, transposed, row j.  Needs a
- * single-rank 3x3 node-block matrix on a box lattice whose blocks are
- * symmetric (to 1e-12 of the largest entry); otherwise KLE_ERR_SUP.  The full
+ * 3x3 node-block matrix on a box lattice (one rank, or z slabs: the
+ * transposed sums of upper ghost rows go back to their owner, MPISBAIJ's
+ * reverse scatter) whose blocks are symmetric (to 1e-12 of the largest
+ * entry; across ranks checked by one product through both storages);
+ * otherwise KLE_ERR_SUP.  Collective at N > 1.  The full
  * storage stays (getRow, CSR export); any value change (diagonalScale, axpy,
  * setValues/assemble) drops the symmetric copy.  kle_assemble_kle turns it on
  * for K (tuning "spmv_sym", "spmv_sym_min_rows").  Results agree with the

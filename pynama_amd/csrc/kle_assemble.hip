@@ -1874,10 +1874,16 @@ int kle_assemble_kle(kle_ctx *ctx, kle_mesh *m, kle_mat **K, kle_mat **Krhs, kle
     owned.keep = true;
     // K is SPD (MatFS.buildFS: free-free blocks + unit Dirichlet diagonal):
     // a structured K (one rank or z slabs) of >= spmv_sym_min_rows node rows
-    // in all keeps its upper triangle only for the SpMV
-    // (kle_mat_set_symmetric; collective, the same decision on every rank); a
-    // K the symmetric path cannot take keeps the full-storage kernels
-    if (g_tune.spmv_sym && mK->m_global / 3 >= g_tune.spmv_sym_min_rows && mK->R == 3 && mK->C == 3) {
+    // per rank keeps its upper triangle only for the SpMV
+    // (kle_mat_set_symmetric; collective, the same decision on every rank --
+    // the count is the global one over the ranks); a K the symmetric path
+    // cannot take keeps the full-storage kernels.  Per rank, because the
+    // symmetric SpMV carries ~25 us of tile prologues, partial stores and
+    // the gather that the full-storage SpMV does not: config 2's 1/4 slab
+    // (85k rows) 133.6 vs 165 us, its 1/8 slab (43k rows) 77.6 vs 72.1 us
+    // (profiles/r03/xl/slab_probes.jsonl)
+    if (g_tune.spmv_sym && mK->m_global / 3 / ctx->nranks >= g_tune.spmv_sym_min_rows && mK->R == 3 &&
+        mK->C == 3) {
         if (sym_build(mK)) (void)kle_last_error();
         tm.lap("assemble_kle: symmetric storage");
     }

@@ -306,12 +306,12 @@ struct Tuning {
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
     int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
-    int spmv_sym = 1;  // SBAIJ-style symmetric storage for the KLE K of >= spmv_sym_min_rows node rows (all ranks); 0 off
+    int spmv_sym = 1;  // SBAIJ-style symmetric storage for the KLE K of >= spmv_sym_min_rows node rows per rank; 0 off
     int spmv_sym_min_rows = 64000;
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
-    int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 4 LDS x reads, 8 partial stores, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
+    int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 2 row sums, 4 LDS x reads, 8 partial stores, 16 block -> region arithmetic, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)
 };

@@ -116,30 +116,41 @@ __global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly
     }
 }
 
-// Wave sum through DPP row moves (VALU only; __shfl_xor is a ds_bpermute per
+// Wave sums through DPP row moves (VALU only; __shfl_xor is a ds_bpermute per
 // 32-bit half, i.e. 12 LDS instructions per double): quad swaps, half-row
 // and row mirrors, then row_bcast15 / row_bcast31 carry the row sums into
-// lane 63, which every lane reads back.
+// lane 63, which every lane reads back.  Three sums at once, their steps
+// interleaved (no hazard nops between a step's add and the next step's DPP
+// read); the full-row steps use the source as the unused "old" operand
+// (every lane is written), only the row broadcasts need zeros.
 template <int ctrl, int row_mask>
-__device__ __forceinline__ double dpp_step(double v)
+__device__ __forceinline__ void dpp3(double &a, double &b, double &c)
 {
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    const int l2 = __builtin_amdgcn_update_dpp(0, lo, ctrl, row_mask, 0xF, false);
-    const int h2 = __builtin_amdgcn_update_dpp(0, hi, ctrl, row_mask, 0xF, false);
-    return v + __hiloint2double(h2, l2);
+    constexpr bool all = row_mask == 0xF;
+    const int al = __double2loint(a), ah = __double2hiint(a), bl = __double2loint(b), bh = __double2hiint(b);
+    const int cl = __double2loint(c), ch = __double2hiint(c);
+    const int a2 = __builtin_amdgcn_update_dpp(all ? al : 0, al, ctrl, row_mask, 0xF, false);
+    const int a3 = __builtin_amdgcn_update_dpp(all ? ah : 0, ah, ctrl, row_mask, 0xF, false);
+    const int b2 = __builtin_amdgcn_update_dpp(all ? bl : 0, bl, ctrl, row_mask, 0xF, false);
+    const int b3 = __builtin_amdgcn_update_dpp(all ? bh : 0, bh, ctrl, row_mask, 0xF, false);
+    const int c2 = __builtin_amdgcn_update_dpp(all ? cl : 0, cl, ctrl, row_mask, 0xF, false);
+    const int c3 = __builtin_amdgcn_update_dpp(all ? ch : 0, ch, ctrl, row_mask, 0xF, false);
+    a += __hiloint2double(a3, a2);
+    b += __hiloint2double(b3, b2);
+    c += __hiloint2double(c3, c2);
 }
 
-__device__ __forceinline__ double wsum_dpp(double v)
+__device__ __forceinline__ void wsum3_dpp(double &a, double &b, double &c)
 {
-    v = dpp_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
-    v = dpp_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
-    v = dpp_step<0x141, 0xF>(v);  // row_half_mirror
-    v = dpp_step<0x140, 0xF>(v);  // row_mirror
-    v = dpp_step<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3
-    v = dpp_step<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
-    return __hiloint2double(hi, lo);
+    dpp3<0xB1, 0xF>(a, b, c);   // quad_perm [1,0,3,2]
+    dpp3<0x4E, 0xF>(a, b, c);   // quad_perm [2,3,0,1]
+    dpp3<0x141, 0xF>(a, b, c);  // row_half_mirror
+    dpp3<0x140, 0xF>(a, b, c);  // row_mirror
+    dpp3<0x142, 0xA>(a, b, c);  // row_bcast15 into rows 1, 3
+    dpp3<0x143, 0xC>(a, b, c);  // row_bcast31 into rows 2, 3
+    a = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(a), 63), __builtin_amdgcn_readlane(__double2loint(a), 63));
+    b = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(b), 63), __builtin_amdgcn_readlane(__double2loint(b), 63));
+    c = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(c), 63), __builtin_amdgcn_readlane(__double2loint(c), 63));
 }
 
 // Same tile pass with the wave's (row, 64-block pass) items flattened into one
@@ -369,6 +380,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
         const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
         rr = (R.rx0 + kx) + g.RX * ((R.ry0 + ky) + g.RY * (R.rz0 + kz));
+        if (probe & 16) rr = lane;  // (timing probe 16: no block -> region arithmetic)
     };
     auto load_x = [&](int rr, double *xv) {
         xv[0] = xl[rr];
@@ -494,9 +506,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
                 return true;
             }
             // the row is done: its direct sum (fixed-order DPP), one writer
-            acc0 = wsum_dpp(acc0);
-            acc1 = wsum_dpp(acc1);
-            acc2 = wsum_dpp(acc2);
+            if (!(probe & 2)) wsum3_dpp(acc0, acc1, acc2);  // (timing probe 2: no row sums)
             if (lane < 3) yd[lane * TR + C.own] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
             acc0 = acc1 = acc2 = 0.0;
             const int nx = next_slot(xc + 1);
