@@ -434,6 +434,8 @@ def main():
                                         f"cell slabs along the most-layered axis x{nranks}") +
                                        ("" if nranks == 1 else
                                         " (RCCL halo + allreduce)" if dev["transport"] == "rccl" else
+                                        " (IPC mailbox halo + allreduce: copy engines + stream wait/write-value)"
+                                        if dev["transport"] == "ipc" else
                                         " (host-staged halo + allreduce over gloo, ranks sharing a GPU: test only)")),
                        "devices": [f"{d['device']}@{d['pci_bus_id']}" for d in devices]},
             # N > 1: bytes of all ranks over the slowest rank's SpMV time,

@@ -120,11 +120,22 @@ typedef struct {
 } kle_host_comm;
 int kle_ctx_create_host_comm(int device, int rank, int nranks, const kle_host_comm *comm,
                              kle_ctx **out);
+/* Device-to-device transport for a host-comm context (KLE_TRANSPORT=ipc;
+ * collective): every rank exports one mailbox (hipIpcGetMemHandle, handles
+ * exchanged over the host callbacks) and maps the others'; the slab halos,
+ * the symmetric SpMV's reverse halo and the allreduces then run as
+ * hipMemcpyAsync copies into the peers' mailboxes with stream wait/write-value
+ * signals (no host staging, no RCCL kernels on the SpMV's CUs; the allreduce
+ * sums the ranks' slots in rank order, the same bits on every rank).  Graph-
+ * partition halos keep the host path.  KLE_ERR_COMM when any rank cannot
+ * export or map (then no rank switches). */
+int kle_ctx_enable_ipc(kle_ctx *ctx);
 int kle_ctx_destroy(kle_ctx *ctx);
 int kle_ctx_synchronize(kle_ctx *ctx);
 int kle_ctx_barrier(kle_ctx *ctx); /* device-side RCCL barrier + stream sync */
 /* Diagnostics (no reference counterpart): the HIP ordinal, its PCI bus id
- * (may be NULL) and the transport: 0 single rank, 1 RCCL, 2 host-staged. */
+ * (may be NULL) and the transport: 0 single rank, 1 RCCL, 2 host-staged,
+ * 3 IPC mailboxes (kle_ctx_enable_ipc). */
 int kle_ctx_get_device(kle_ctx *ctx, int *device, char *pci_bus_id, int len, int *transport);
 /* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */
 int kle_ctx_set_profiling(kle_ctx *ctx, int on);

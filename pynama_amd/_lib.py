@@ -60,6 +60,7 @@ _SIGS = {
     "kle_ctx_synchronize": [vp],
     "kle_ctx_barrier": [vp],
     "kle_ctx_get_device": [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int, C.POINTER(C.c_int)],
+    "kle_ctx_enable_ipc": [vp],
     "kle_ctx_set_profiling": [vp, C.c_int],
     "kle_ctx_set_profiling_sample": [vp, C.c_int],
     "kle_ctx_set_profiling_filter": [vp, C.c_char_p],

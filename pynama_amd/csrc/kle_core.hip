@@ -286,7 +286,9 @@ int allreduce_sum(kle_ctx *ctx, double *dbuf, int n, hipStream_t st)
     if (!st) st = ctx->stream;
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("allreduce", &ev, st));
-    if (ctx->comm) {
+    if (ctx->ipc) {
+        KLE_TRY(ipc_allreduce(ctx, dbuf, n, st));
+    } else if (ctx->comm) {
         KLE_NCCL(ncclAllReduce(dbuf, dbuf, n, ncclDouble, ncclSum, ctx->comm, st));
     } else {
         KLE_TRY(stage_reserve(ctx, n));
@@ -418,7 +420,9 @@ int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local,
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("halo", &ev, st));
     double *own = base + ghost_lo;
-    if (ctx->comm) {
+    if (ctx->ipc) {
+        KLE_TRY(ipc_halo(ctx, base, ghost_lo, n_local, ghost_hi, lo_rank, hi_rank, send_lo, send_hi, st));
+    } else if (ctx->comm) {
         KLE_NCCL(ncclGroupStart());
         if (lo_rank >= 0) {
             // my lowest send_lo owned entries are the lower neighbour's upper ghosts
@@ -464,7 +468,9 @@ int halo_reverse(kle_ctx *ctx, const double *send_hi, int64_t n_send, int hi_ran
     const int64_t ns = hi_rank >= 0 ? n_send : 0, nr = lo_rank >= 0 ? n_recv : 0;
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("halo_rev", &ev, st));
-    if (ctx->comm) {
+    if (ctx->ipc) {
+        KLE_TRY(ipc_reverse(ctx, send_hi, ns, hi_rank, recv_lo, nr, lo_rank, st));
+    } else if (ctx->comm) {
         KLE_NCCL(ncclGroupStart());
         if (ns) KLE_NCCL(ncclSend(send_hi, ns, ncclDouble, hi_rank, ctx->comm, st));
         if (nr) KLE_NCCL(ncclRecv(recv_lo, nr, ncclDouble, lo_rank, ctx->comm, st));
@@ -749,6 +755,7 @@ int kle_ctx_destroy(kle_ctx *c)
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     c->resolve_stats();
+    ipc_destroy(c);
     for (auto e : c->event_pool) hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_partials);
@@ -785,7 +792,7 @@ int kle_ctx_get_device(kle_ctx *c, int *device, char *pci_bus_id, int len, int *
 {
     KLE_ARG(c && device && transport && (pci_bus_id == nullptr || len > 0), "bad arg");
     *device = c->device;
-    *transport = c->comm ? 1 : (c->nranks > 1 ? 2 : 0);
+    *transport = c->comm ? 1 : c->ipc ? 3 : (c->nranks > 1 ? 2 : 0);
     if (pci_bus_id) KLE_HIP(hipDeviceGetPCIBusId(pci_bus_id, len, c->device));
     return 0;
 }

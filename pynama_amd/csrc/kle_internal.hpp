@@ -72,6 +72,7 @@ struct HaloPlan {
     ~HaloPlan();
 };
 using PlanPtr = std::shared_ptr<HaloPlan>;
+struct IpcState;  // kle_ipc.hip: IPC-mapped mailboxes (KLE_TRANSPORT=ipc)
 
 // Device scalar slots used by the Krylov kernels.
 enum Scal {
@@ -99,6 +100,7 @@ struct kle_ctx {
     ncclComm_t comm = nullptr;
     bool side_busy = false;  // comm-stream kernels run beside the SpMV being launched (kle_mat.hip)
     kle_host_comm hcomm = {};         // host-staged transport (testing), used when comm == nullptr
+    kle::IpcState *ipc = nullptr;     // device-to-device transport over IPC mailboxes (kle_ctx_enable_ipc)
     double *h_stage = nullptr;        // pinned staging for the host transport
     int64_t h_stage_n = 0;
     bool profiling = false;
@@ -294,6 +296,13 @@ int sym_build(kle_mat *A);
 void sym_drop(kle_mat *A);
 void sym_forget(kle_mat *A);  // null the symmetric-storage pointers of a struct copy (no free)
 int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);  // N > 1: both halos included
+// IPC transport (kle_ipc.hip): slab halos, reverse halo, allreduce
+int ipc_halo(kle_ctx *c, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi, int lo_rank,
+             int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st);
+int ipc_reverse(kle_ctx *c, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
+                int lo_rank, hipStream_t st);
+int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st);
+void ipc_destroy(kle_ctx *c);
 int halo_reverse(kle_ctx *ctx, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
                  int lo_rank, hipStream_t st);  // kle_core.hip
 std::string sym_kernel_name(const kle_mat *A);

@@ -57,9 +57,12 @@ COMM_WORLD = Comm()
 
 
 class Context:
-    """transport: "rccl" (default, one GPU per rank) or "host" (collectives
+    """transport: "rccl" (default, one GPU per rank), "host" (collectives
     staged through host memory over torch.distributed/gloo; several ranks may
-    share one GPU -- used to test the distributed path on a single device).
+    share one GPU -- used to test the distributed path on a single device) or
+    "ipc" (halos and allreduces as copies into IPC-mapped peer mailboxes with
+    stream wait/write-value signals, bootstrapped over gloo;
+    kle_ctx_enable_ipc -- several ranks may share one GPU as well).
     KLE_RCCL_SELF=1 on a single rank creates a one-rank RCCL communicator, so
     the RCCL calls (init with deadline, allreduce on both streams) run on one
     GPU; RCCL refuses two ranks on one device."""
@@ -75,11 +78,19 @@ class Context:
             device = int(os.environ.get("KLE_DEVICE", os.environ.get("LOCAL_RANK", default)))
             if self.transport == "host":
                 device = int(os.environ.get("KLE_DEVICE", 0))
+            elif self.transport == "ipc":  # one GPU per rank under torchrun, else all on 0 (tests)
+                device = int(os.environ.get("KLE_DEVICE", os.environ.get("LOCAL_RANK", 0)))
         self.device = device
         h = C.c_void_p()
-        if self.nranks > 1 and self.transport == "host":
+        if self.nranks > 1 and self.transport in ("host", "ipc"):
             self._hc = self._host_comm()
             call("kle_ctx_create_host_comm", device, self.rank, self.nranks, C.byref(self._hc), C.byref(h))
+            if self.transport == "ipc":
+                try:
+                    call("kle_ctx_enable_ipc", h)
+                except Exception:
+                    call("kle_ctx_destroy", h)
+                    raise
         else:
             if self.nranks > 1:
                 uid = self._bcast_unique_id()
@@ -183,12 +194,12 @@ class Context:
 
     def device_info(self):
         """{"device": HIP ordinal, "pci_bus_id": "0000:..", "transport":
-        "single" | "rccl" | "host"} of this rank."""
+        "single" | "rccl" | "host" | "ipc"} of this rank."""
         dev, tr = C.c_int(), C.c_int()
         pci = C.create_string_buffer(32)
         call("kle_ctx_get_device", self.h, C.byref(dev), pci, 32, C.byref(tr))
         return {"device": dev.value, "pci_bus_id": pci.value.decode(),
-                "transport": ("single", "rccl", "host")[tr.value]}
+                "transport": ("single", "rccl", "host", "ipc")[tr.value]}
 
     def set_profiling(self, on=True, only=None, every=1):
         """Event-time device launches; `only` restricts it to one kernel tag,

@@ -22,10 +22,10 @@ def _free_port():
 
 
 def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0,
-            sym=False):
+            sym=False, transport="host"):
     import sys
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="host",
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT=transport,
                       RANK=str(rank), WORLD_SIZE=str(size))
     if waves:  # 8: the LDS SpMV kernels (x-in-LDS / column dictionaries) at test sizes
         os.environ["KLE_SPMV_WAVES"] = str(waves)
@@ -80,7 +80,8 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
                "overlap_equal": bool(np.array_equal(y_ov, y_pl)), "y": y_ov, "x": xv.getArray(),
                "coords": dom.getFullCoordArray().reshape(-1, 3),
                "ov_diff": (np.nonzero(y_ov != y_pl)[0][:12].tolist(), len(y_ov)),
-               "sym": mat.K.isSymmetricStorage(), "kernel": mat.K.spmvKernel()}
+               "sym": mat.K.isSymmetricStorage(), "kernel": mat.K.spmvKernel(),
+               "transport": pa.get_ctx().device_info()["transport"]}
         q.put(res)
     except Exception as e:  # report instead of hanging the peer
         import traceback
@@ -140,7 +141,29 @@ def test_partitioned_solve_symmetric_storage(size, nelem, ngl, ksp_type, overlap
         assert r["kernel"].startswith("k_nb_spmv_sym_xl<"), r["kernel"]
 
 
-def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False):
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type,overlap,sym", [
+    (2, [3, 2, 4], 4, "cg", True, False), (2, [3, 2, 4], 4, "pipecg", True, True),
+    (2, [3, 2, 4], 4, "cg", False, True), (3, [2, 3, 3], 3, "pipecg", True, False),
+    (3, [2, 3, 3], 3, "cg", True, True), (8, [2, 2, 8], 4, "pipecg", True, False),
+    (8, [2, 2, 8], 4, "pipecg", True, True)])
+def test_partitioned_solve_ipc_transport(size, nelem, ngl, ksp_type, overlap, sym):
+    """KLE_TRANSPORT=ipc (kle_ctx_enable_ipc): the ranks sharing one GPU map
+    each other's mailboxes and run the halos, the symmetric SpMV's reverse
+    halo and every allreduce as copies into the peers' memory with stream
+    wait/write-value signals -- no host staging.  Same checks as the host
+    transport (serial oracle, K's rows, overlapped == plain bitwise), and
+    y = K x bitwise equal to the host transport's (the SpMV does not depend
+    on how its halo travels)."""
+    res = _check_box(size, nelem, ngl, overlap, ksp_type, sym=sym, transport="ipc")
+    ref = _check_box(size, nelem, ngl, overlap, ksp_type, sym=sym)
+    for a, b in zip(res, ref):
+        assert a["transport"] == "ipc" and b["transport"] == "host"
+        assert a["sym"] == sym
+        np.testing.assert_array_equal(a["y"], b["y"])
+        assert abs(a["dot"] - b["dot"]) <= 1e-13 * abs(b["dot"])
+
+
+def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False, transport="host"):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
@@ -148,7 +171,7 @@ def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, None, None, waves,
-                                               sym))
+                                               sym, transport))
              for r in range(size)]
     res = _collect(procs, q, size)
     for r in res:
