@@ -245,6 +245,7 @@ struct kle_mat {
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
     int sym_P = 0, sym_TZ = 2;
+    int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo)
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
     // export: DoF-level entry rule inside the node blocks (no-slip matrices,
     // MASK_* below) and the ext-range DoF classes it reads

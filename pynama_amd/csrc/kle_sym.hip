@@ -36,8 +36,15 @@ constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (on
 // of an owned row never reaches a lower ghost; the blocks that reach upper
 // ghosts add their transposed parts to ghost rows, whose partials go back to
 // the owner (sym_spmv's reverse halo).
+// Region of a tile: [x0 - PX, x0 - PX + RX) x [y0 - PY, y0 - PY + RY) x
+// [z0, z0 + RZ) -- the bounding box, over all tiles, of the rows' upper
+// triangles relative to their tile's origin (sym_build).  On element-aligned
+// tiles an upper triangle reaches back p nodes in x and y (from the planes
+// above) but forward only to the next element boundary, one node past the
+// tile: 13 x 9 x 5 nodes for 8 x 4 x 4 tiles at p = 4, not (8 + 2p) x (4 + 2p)
+// x (4 + p) = 1536.
 struct SymGeo {
-    int Lx, Ly, Lz, P, TX, TY, TZ, RX, RY, RZ, ntx, nty, ntz, zo, hp;
+    int Lx, Ly, Lz, P, TX, TY, TZ, PX, PY, RX, RY, RZ, ntx, nty, ntz, zo, hp;
 };
 
 __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
@@ -275,7 +282,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;
-    const int x0 = tix * SYM_TX, y0 = tiy * TY, ox = x0 - g.P, oy = y0 - g.P;
+    const int x0 = tix * SYM_TX, y0 = tiy * TY, ox = x0 - g.PX, oy = y0 - g.PY;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     const int nx = min(SYM_TX, g.Lx - x0);
@@ -342,11 +349,11 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(psl, s);
         const int64_t hi = __builtin_amdgcn_readlane(psh, s);
         R.v = sval + ((hi << 32) | lo);
-        R.rx0 = g.P + sx - dbx;  // box corner in the region
-        R.ry0 = g.P + sy - dby;
+        R.rx0 = g.PX + sx - dbx;  // box corner in the region
+        R.ry0 = g.PY + sy - dby;
         R.rz0 = sz - dbz;
         R.own = sx + SYM_TX * (sy + TY * sz);  // row slot in the tile
-        const int ir = (sx + g.P) + g.RX * ((sy + g.P) + g.RY * sz);  // its region index
+        const int ir = (sx + g.PX) + g.RX * ((sy + g.PY) + g.RY * sz);  // its region index
         R.x0 = uni_d(xl[ir]);  // (the first row re-reads these once the fill has landed)
         R.x1 = uni_d(xl[RN + ir]);
         R.x2 = uni_d(xl[2 * RN + ir]);
@@ -439,7 +446,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         double m = 0.0;
         int bad = 0;
         for (int r = lane; r < TR; r += 64) {
-            const int k = (g.P + (r & 7)) + g.RX * ((g.P + (r >> 3) % TY) + g.RY * (r / (SYM_TX * TY)));
+            const int k = (g.PX + (r & 7)) + g.RX * ((g.PY + (r >> 3) % TY) + g.RY * (r / (SYM_TX * TY)));
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const double a = fabs(xl[c * RN + k]);
@@ -530,8 +537,8 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
         const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
         if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz + g.hp) continue;
-        const bool own = rx >= g.P && rx < g.P + SYM_TX && ry >= g.P && ry < g.P + TY && rz < TZ;
-        const int sl = (rx - g.P) + SYM_TX * ((ry - g.P) + TY * rz);
+        const bool own = rx >= g.PX && rx < g.PX + SYM_TX && ry >= g.PY && ry < g.PY + TY && rz < TZ;
+        const int sl = (rx - g.PX) + SYM_TX * ((ry - g.PY) + TY * rz);
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
             double v = DET ? fx_to_d(yi[b * RS + k]) * invS : yl[b * RS + k];
@@ -562,7 +569,7 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * g.TZ;
-    const int x0 = tix * SYM_TX, y0 = tiy * g.TY, ox = x0 - g.P, oy = y0 - g.P;
+    const int x0 = tix * SYM_TX, y0 = tiy * g.TY, ox = x0 - g.PX, oy = y0 - g.PY;
     const int64_t Lxy = (int64_t)g.Lx * g.Ly;
     for (int r = threadIdx.x; r < TR; r += 256) {
         const int xi = x0 + (r & 7), yi = y0 + (r >> 3) % g.TY, zi = tz + r / (SYM_TX * g.TY);
@@ -639,15 +646,15 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     const int jz = (int)(j / Lxy), jy = (int)((j - jz * Lxy) / g.Lx), jx = (int)(j - jz * Lxy - (int64_t)jy * g.Lx);
     const int RN = g.RX * g.RY * g.RZ;
     // tiles whose [t*T - P, t*T - P + R) contains the coordinate
-    const int x_lo = max(0, (jx + g.P - g.RX + TXW) / TXW), x_hi = min(g.ntx - 1, (jx + g.P) / TXW);
-    const int y_lo = max(0, (jy + g.P - g.RY + TY) / TY), y_hi = min(g.nty - 1, (jy + g.P) / TY);
+    const int x_lo = max(0, (jx + g.PX - g.RX + TXW) / TXW), x_hi = min(g.ntx - 1, (jx + g.PX) / TXW);
+    const int y_lo = max(0, (jy + g.PY - g.RY + TY) / TY), y_hi = min(g.nty - 1, (jy + g.PY) / TY);
     const int z_lo = max(0, (jz - g.RZ + TZ) / TZ), z_hi = min(g.ntz - 1, jz / TZ);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int tzi = z_lo; tzi <= z_hi; ++tzi)
         for (int ty = y_lo; ty <= y_hi; ++ty)
             for (int tx = x_lo; tx <= x_hi; ++tx) {
                 const int64_t t = ((int64_t)tzi * g.nty + ty) * g.ntx + tx;
-                const int r = (jx - (tx * TXW - g.P)) + g.RX * ((jy - (ty * TY - g.P)) + g.RY * (jz - tzi * TZ));
+                const int r = (jx - (tx * TXW - g.PX)) + g.RX * ((jy - (ty * TY - g.PY)) + g.RY * (jz - tzi * TZ));
                 const double *p = ws + t * 3 * (int64_t)RN + r;
                 s0 += p[0];
                 s1 += p[RN];
@@ -706,9 +713,11 @@ static SymGeo sym_geo(const kle_mat *A)
     g.zo = (int)(A->ghost_lo / plane3);
     g.hp = (int)(A->ghost_hi / plane3);
     g.P = P;
-    g.RX = g.TX + 2 * P;
-    g.RY = g.TY + 2 * P;
-    g.RZ = g.TZ + P;
+    g.PX = A->sym_reg[0];
+    g.RX = A->sym_reg[1];
+    g.PY = A->sym_reg[2];
+    g.RY = A->sym_reg[3];
+    g.RZ = A->sym_reg[4];
     g.ntx = (g.Lx + g.TX - 1) / g.TX;
     g.nty = (g.Ly + g.TY - 1) / g.TY;
     g.ntz = (g.Lz + g.TZ - 1) / g.TZ;
@@ -716,9 +725,18 @@ static SymGeo sym_geo(const kle_mat *A)
 }
 
 // LDS of the x-in-LDS kernel: x and y of the region, the tile's direct row sums
-static size_t sym_xl_lds(int P, int TZ)
+struct SymRegion {
+    int PX, RX, PY, RY, RZ;
+};
+
+static SymRegion sym_region(const kle_mat *A)
 {
-    const size_t RN = (size_t)(SYM_TX + 2 * P) * (16 / TZ + 2 * P) * (TZ + P);
+    return {A->sym_reg[0], A->sym_reg[1], A->sym_reg[2], A->sym_reg[3], A->sym_reg[4]};
+}
+
+static size_t sym_xl_lds(const SymRegion &r)
+{
+    const size_t RN = (size_t)r.RX * r.RY * r.RZ;
     return (6 * RN + 3 * 64 + 3 * 128) * sizeof(double);
 }
 constexpr size_t LDS_PER_CU = 163840;
@@ -728,9 +746,9 @@ constexpr size_t LDS_PER_CU = 163840;
 // kle_set_tuning("spmv_sym_waves") overrides.
 // The x fill is one pass of SYM_FILL loads per thread: 16 waves where 8 would
 // need more (P >= 5).
-static bool sym_fill_fits(int P, int wv, int TZ)
+static bool sym_fill_fits(const SymRegion &r, int wv)
 {
-    const int RX = SYM_TX + 2 * P, NL = (16 / TZ + 2 * P) * (TZ + P), fstep = 64 * wv / (3 * RX);
+    const int NL = r.RY * r.RZ, fstep = 64 * wv / (3 * r.RX);
     return NL <= SYM_FILL * fstep;
 }
 
@@ -835,6 +853,10 @@ int sym_build(kle_mat *A)
     std::vector<int64_t> sv;
     std::vector<int> srow;  // per row: x-bx, y-by, z-bz, bnx, bny, bnz (4 bits each)
     int P = 0;
+    // reach of the rows' upper triangles relative to their tile's origin, per
+    // tile shape (0: 8 x 4 x 4, 1: 8 x 8 x 2): x / y low, x / y / z high
+    const int shape_ty[2] = {4, 8}, shape_tz[2] = {4, 2};
+    int64_t rlo[2][2] = {{0, 0}, {0, 0}}, rhi[2][3] = {{SYM_TX - 1, 3, 3}, {SYM_TX - 1, 7, 1}};
     int64_t tot = 0, blocks = 0, all = 0, up_ghost = 0, lo_ghost = 0;
     if (why.empty()) {
         rb.resize(2 * n);
@@ -866,6 +888,21 @@ int sym_build(kle_mat *A)
                 break;
             }
             srow[i] = (int)((x - bx) | (y - by) << 4 | (z - bz) << 8) | bnx << 12 | bny << 16 | bnz << 20;
+            {
+                // the upper triangle's extent: the planes above take the
+                // whole box, the row's own plane the lines from its own on
+                const int64_t uz1 = bz + bnz - 1, uy1 = by + bny - 1, ux1 = bx + bnx - 1;
+                const int64_t uy0 = uz1 > z ? by : y, ux0 = uz1 > z || uy1 > y ? bx : x;
+                for (int s = 0; s < 2; ++s) {
+                    const int64_t x0 = x / SYM_TX * SYM_TX, y0 = y / shape_ty[s] * shape_ty[s];
+                    const int64_t z0 = (z - zo) / shape_tz[s] * shape_tz[s] + zo;
+                    rlo[s][0] = std::min(rlo[s][0], ux0 - x0);
+                    rlo[s][1] = std::min(rlo[s][1], uy0 - y0);
+                    rhi[s][0] = std::max(rhi[s][0], ux1 - x0);
+                    rhi[s][1] = std::max(rhi[s][1], uy1 - y0);
+                    rhi[s][2] = std::max(rhi[s][2], uz1 - z0);
+                }
+            }
             const int k0 = (int)((x - bx) + bnx * ((y - by) + (int64_t)bny * (z - bz)));
             const int64_t mu = cnt[i] - k0;
             sv[i] = tot;
@@ -883,16 +920,22 @@ int sym_build(kle_mat *A)
         if (why.empty() && 2 * blocks - n - up_ghost + lo_ghost != all)
             why = "symmetric storage: the block pattern is not symmetric (" + std::to_string(all) + " blocks, " +
                   std::to_string(blocks) + " upper)";
-        if (why.empty() && sym_xl_lds(P, 2) > LDS_PER_CU)
-            why = "symmetric storage: row boxes reach " + std::to_string(P) + " nodes (at most 6 supported)";
     }
+    SymRegion reg[2];
+    for (int s = 0; s < 2; ++s)
+        reg[s] = {(int)-rlo[s][0], (int)(rhi[s][0] - rlo[s][0] + 1), (int)-rlo[s][1], (int)(rhi[s][1] - rlo[s][1] + 1),
+                  (int)(rhi[s][2] + 1)};
+    if (why.empty() && sym_xl_lds(reg[1]) > LDS_PER_CU)
+        why = "symmetric storage: row boxes reach " + std::to_string(P) + " nodes (region of " +
+              std::to_string(reg[1].RX * reg[1].RY * reg[1].RZ) + " nodes does not fit the LDS)";
     // tile shape: 8 x 4 x 4 rows (default where two workgroups of 8 waves fit
     // a CU: P <= 4) or 8 x 8 x 2 -- the same 128 rows and, at P = 4, the same
     // 1536-node region, but a 4-plane tile spans a whole p = 4 element layer,
     // so every tile holds the same mix of row lengths (rows on element-
     // boundary planes carry 4 planes of upper blocks, the next ones 3, 2, 1)
-    const int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(P, 4) <= LDS_PER_CU &&
-                           sym_fill_fits(P, 8, 4) ? 4 : 2;
+    const int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(reg[0]) <= LDS_PER_CU &&
+                           sym_fill_fits(reg[0], 8) ? 4 : 2;
+    const SymRegion &rg = reg[TZ == 4 ? 0 : 1];
     bool any = false;
     KLE_TRY(any_rank(c, !why.empty(), any));
     if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
@@ -954,6 +997,11 @@ int sym_build(kle_mat *A)
     }
     A->sym_P = P;
     A->sym_TZ = TZ;
+    A->sym_reg[0] = rg.PX;
+    A->sym_reg[1] = rg.RX;
+    A->sym_reg[2] = rg.PY;
+    A->sym_reg[3] = rg.RY;
+    A->sym_reg[4] = rg.RZ;
     const SymGeo g = sym_geo(A);
     const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz;
     auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
@@ -962,7 +1010,8 @@ int sym_build(kle_mat *A)
     for (int64_t t = 0; t < g.ntz; ++t)
         for (int ty = 0; ty < g.nty; ++ty)
             for (int tx = 0; tx < g.ntx; ++tx)
-                ents += span(tx * g.TX - P, g.RX, Lx) * span(ty * g.TY - P, g.RY, Ly) * span(t * g.TZ, g.RZ, Lz + hp);
+                ents += span(tx * g.TX - g.PX, g.RX, Lx) * span(ty * g.TY - g.PY, g.RY, Ly) *
+                        span(t * g.TZ, g.RZ, Lz + hp);
     nomem = hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.RX * g.RY * g.RZ) != hipSuccess ||
             hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
             (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
@@ -994,9 +1043,10 @@ int sym_build(kle_mat *A)
 static int sym_waves(const kle_mat *A)
 {
     const int P = A->sym_P;
-    const int TZ = A->sym_TZ;
-    if (g_tune.spmv_sym_waves && sym_fill_fits(P, g_tune.spmv_sym_waves, TZ)) return g_tune.spmv_sym_waves;
-    return 2 * sym_xl_lds(P, TZ) <= LDS_PER_CU && sym_fill_fits(P, 8, TZ) ? 8 : 16;
+    const SymRegion r = sym_region(A);
+    if (A->sym_TZ == 4) return 8;
+    if (g_tune.spmv_sym_waves && sym_fill_fits(r, g_tune.spmv_sym_waves)) return g_tune.spmv_sym_waves;
+    return 2 * sym_xl_lds(r) <= LDS_PER_CU && sym_fill_fits(r, 8) ? 8 : 16;
 }
 
 template <int WV, bool DET, int TZ>
@@ -1004,7 +1054,7 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
                           const int *istate, hipStream_t st)
 {
     if (t1 <= t0) return;
-    const size_t lds = sym_xl_lds(A->sym_P, TZ);
+    const size_t lds = sym_xl_lds(sym_region(A));
     static size_t lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
     if (lds > lds_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>),
