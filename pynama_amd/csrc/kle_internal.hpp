@@ -286,6 +286,10 @@ int halo_exchange(kle_ctx *ctx, double *base, int64_t ghost_lo, int64_t n_local,
                   const HaloPlan *plan = nullptr);
 // y = A x; istate (may be null): no-op once the Krylov reason word is set
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
+// y = A x and, where the SpMV can form them, the per-workgroup partials of
+// (y, x) in dpart: *nparts of them (0: none written -- the caller forms them)
+int spmv_dot(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart, int *nparts);
+int spmv_dot_parts(const kle_mat *A);  // what spmv_dot would write (0: none)
 // true when spmv(A, x, ...) exchanges the halo on ctx->comm_stream
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
@@ -296,7 +300,9 @@ int nb_build_dict(kle_mat *A);  // kle_mat.hip
 int sym_build(kle_mat *A);
 void sym_drop(kle_mat *A);
 void sym_forget(kle_mat *A);  // null the symmetric-storage pointers of a struct copy (no free)
-int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);  // N > 1: both halos included
+int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate,
+             double *dpart = nullptr);  // N > 1: both halos included; dpart: (y, x) partials (one rank)
+int sym_dot_parts(const kle_mat *A);  // partials sym_spmv writes with dpart (0: it cannot)
 // IPC transport (kle_ipc.hip): slab halos, reverse halo, allreduce
 int ipc_halo(kle_ctx *c, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi, int lo_rank,
              int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st);

@@ -1074,6 +1074,10 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     // all 2 Gu + Gd partials (config 2: 788.5 vs 792.4 us per iteration with
     // 2048 / 1024; the 1/8 slab is below both caps; profiles/r02/grids_*.jsonl)
     int Gu = grid_for(n, KB, PRO_UPD_BLOCKS), Gd = grid_for(n, KB * 4, PRO_DOT_BLOCKS);
+    // one rank with the symmetric SpMV: its gather forms the (w, u) partials
+    // (spmv_dot), one launch less per iteration
+    const int Gf = c->nranks == 1 && !c->comm ? spmv_dot_parts(k->A) : 0;
+    if (Gf > 0 && 2 * Gu + Gf <= PART_STRIDE / 2) Gd = Gf;
     if (pro_mode && c->nranks > 1) {
         std::vector<int64_t> all;
         KLE_TRY(allgather_i64(c, ((int64_t)Gu << 20) | Gd, all));
@@ -1101,12 +1105,16 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             KLE_TRY(c->toc("cg_update", &ev));
             par ^= 1;
             pending = true;
-            KLE_TRY(spmv(k->A, k->u, k->w, c->d_istate));
-            KLE_TRY(c->tic("reduce", &ev));
-            hipLaunchKernelGGL(k_dot_part, dim3(Gd), dim3(KB), 0, c->stream, n, k->u->d, k->w->d, pu[par] + 2 * Gu,
-                               c->d_istate);
-            KLE_HIP(hipGetLastError());
-            KLE_TRY(c->toc("reduce", &ev));
+            int nd = 0;
+            if (Gd == Gf) KLE_TRY(spmv_dot(k->A, k->u, k->w, c->d_istate, pu[par] + 2 * Gu, &nd));
+            else KLE_TRY(spmv(k->A, k->u, k->w, c->d_istate));
+            if (nd != Gd) {
+                KLE_TRY(c->tic("reduce", &ev));
+                hipLaunchKernelGGL(k_dot_part, dim3(Gd), dim3(KB), 0, c->stream, n, k->u->d, k->w->d,
+                                   pu[par] + 2 * Gu, c->d_istate);
+                KLE_HIP(hipGetLastError());
+                KLE_TRY(c->toc("reduce", &ev));
+            }
             if (!fuse) KLE_TRY(allreduce_sum(c, pu[par], 2 * Gu + Gd));
             return 0;
         }

@@ -761,6 +761,22 @@ int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
     return 0;
 }
 
+int spmv_dot_parts(const kle_mat *A)
+{
+    return A->kind == 0 && A->d_sval && g_tune.spmv_sym ? sym_dot_parts(A) : 0;
+}
+
+int spmv_dot(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart, int *nparts)
+{
+    *nparts = spmv_dot_parts(A);
+    if (!*nparts) return spmv(A, x, y, istate);
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(A->ctx->tic("spmv", &ev));
+    KLE_TRY(sym_spmv(A, x, y, istate, dpart));
+    KLE_TRY(A->ctx->toc("spmv", &ev));
+    return 0;
+}
+
 static int check_mult_layout(const kle_mat *A, const kle_vec *x, const kle_vec *y)
 {
     if (A->kind == 0) {

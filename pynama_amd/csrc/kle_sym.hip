@@ -633,16 +633,24 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
 // and (N > 1) the upper ghost rows, whose sums go to gsend (the reverse halo's
 // send buffer, ghost row j at gsend[3 (j - n)]).  The first nrecv entries of y
 // add the lower neighbour's sums for them (grecv, its upper ghost rows) last.
+// With xdot (one launch over all rows, one rank): also the workgroup's
+// partial of (y, x) in dpart[blockIdx.x] -- the CG's (A u, u), summed in a
+// fixed order (wave sums, then the 4 waves in order), so the single-reduction
+// CG needs no separate dot launch.
 template <int TXW, int TY, int TZ>
 __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *__restrict__ ws, double *__restrict__ y,
                                                        double *__restrict__ gsend, const double *__restrict__ grecv,
                                                        int64_t nrecv, int64_t j0, int64_t j1,
-                                                       const int *__restrict__ istate)
+                                                       const int *__restrict__ istate, const double *__restrict__ xdot,
+                                                       double *__restrict__ dpart)
 {
+    __shared__ double dred[4];
     if (istate && istate[I_REASON] != 0) return;
     const int64_t Lxy = (int64_t)g.Lx * g.Ly, n = Lxy * g.Lz;
     const int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= j1) return;
+    if (j >= j1 && !xdot) return;
+    double dsum = 0.0;
+    if (j < j1) {
     const int jz = (int)(j / Lxy), jy = (int)((j - jz * Lxy) / g.Lx), jx = (int)(j - jz * Lxy - (int64_t)jy * g.Lx);
     const int RN = g.RX * g.RY * g.RZ;
     // tiles whose [t*T - P, t*T - P + R) contains the coordinate
@@ -675,6 +683,14 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     y[3 * j] = s0;
     y[3 * j + 1] = s1;
     y[3 * j + 2] = s2;
+    if (xdot) dsum = s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
+    }
+    if (!xdot) return;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+    if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;
+    __syncthreads();
+    if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
 }
 
 // A copy of a matrix struct (Mat.duplicate) shares none of A's symmetric
@@ -1083,16 +1099,23 @@ static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x
 }
 
 static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int64_t j0, int64_t j1, int64_t nrecv,
-                              const int *istate, hipStream_t st)
+                              const int *istate, hipStream_t st, const double *xdot = nullptr,
+                              double *dpart = nullptr)
 {
     if (j1 <= j0) return;
     const dim3 grid((unsigned)((j1 - j0 + 255) / 256));
     if (g.TZ == 4)
         hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 4, 4>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
-                           A->d_sgrecv, nrecv, j0, j1, istate);
+                           A->d_sgrecv, nrecv, j0, j1, istate, xdot, dpart);
     else
         hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 8, 2>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
-                           A->d_sgrecv, nrecv, j0, j1, istate);
+                           A->d_sgrecv, nrecv, j0, j1, istate, xdot, dpart);
+}
+
+int sym_dot_parts(const kle_mat *A)
+{
+    const bool dist = A->ctx->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    return dist ? 0 : (int)((A->nrows + 255) / 256);
 }
 
 // y = A x over the symmetric storage.  N > 1 (z slabs), per SpMV:
@@ -1104,7 +1127,7 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 //         touch; main: the lowest rows, + d_sgrecv last (fixed order: y stays
 //         bitwise reproducible with spmv_sym_det).
 // All RCCL calls stay on the comm stream, in the same order on every rank.
-int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
+int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
@@ -1113,7 +1136,7 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
     if (!dist) {
         launch_sym_tiles(A, g, x, 0, ntiles, istate, st);
-        launch_sym_gather(A, g, y, 0, n, 0, istate, st);
+        launch_sym_gather(A, g, y, 0, n, 0, istate, st, dpart ? x->d : nullptr, dpart);
         KLE_HIP(hipGetLastError());
         return 0;
     }
