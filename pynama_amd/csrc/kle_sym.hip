@@ -2,9 +2,11 @@
 // the KLE K and its SpMV kernels for gfx950 (kle_mat_set_symmetric =
 // MatSetOption(MAT_SPD); K is SPD: MatFS.buildFS, mat_fs.py:150-192).
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kle_internal.hpp"
@@ -703,16 +705,593 @@ void sym_forget(kle_mat *A)
     A->d_stile_e = nullptr;
     A->d_sgsend = A->d_sgrecv = nullptr;
     A->d_srow = nullptr;
+    A->d_sbp = nullptr;
+    A->d_slid = nullptr;
+    A->d_sdptr = A->d_sdict = A->d_sgptr = A->d_sgidx = nullptr;
+    A->d_sgmask = nullptr;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
+    A->sym_graph = 0;
 }
 
 void sym_drop(kle_mat *A)
 {
     for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
-                    (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow})
+                    (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow, (void *)A->d_sbp,
+                    (void *)A->d_slid, (void *)A->d_sdptr, (void *)A->d_sdict, (void *)A->d_sgptr,
+                    (void *)A->d_sgidx, (void *)A->d_sgmask})
         if (q) (void)hipFree(q);
     sym_forget(A);
+}
+
+// ---------------------------------------------------------------------------
+// Symmetric storage of an unstructured (graph-numbered) 3x3 matrix, one rank.
+// The columns are streamed (bcol ascending per row; node ids in Hilbert order,
+// kle_umesh.cpp), so the upper triangle j >= i of row i is the tail of its
+// column list from the diagonal block on.  Rows go in groups of GSYM_G
+// consecutive rows, one wave per row.  A group's dictionary is the sorted set
+// of its stored blocks' columns; every one is >= the group's first row, so
+// positions 0 .. G-1 are the group's own rows.  The dictionary serves both
+// uses of a block: x_j is read from LDS at the block's 2-byte position and
+// B^T x_i is added to the partial sum at that same position.  The workgroup
+// writes one partial per dictionary entry (its rows' direct sums included) and
+// k_nb_gsym_gather sums, per row, the partials of the dictionary entries that
+// name it, in ascending group order.  HBM per SpMV: the stored values once
+// (half of the full storage), 2 B per stored block, the dictionaries, and
+// the partials written and read once (~25 entries per row at p = 4).  The
+// transposed adds are exact fixed-point sums as in the box kernel (scale per
+// group from k_gsym_bound), so y is bitwise reproducible.
+constexpr int GSYM_G = 8;
+constexpr int GSYM_UCAP = 1536;  // dictionary entries per group (LDS: 48 B each)
+constexpr int GSYM_FILL = 2;  // x-fill entries per thread and batch (3 x 196 entries per group on average)
+
+// kle_mat.hip xcd_block: runs of ch consecutive groups per XCD
+__device__ __forceinline__ int64_t gsym_block(int ch)
+{
+    int64_t blk = blockIdx.x;
+    if (ch > 0) {
+        const int64_t k = blk >> 3, xc = blk & 7, S = (int64_t)gridDim.x / (8 * ch);
+        if (k < S * ch) {
+            const int64_t sb = k / ch;
+            blk = sb * 8 * ch + xc * ch + (k - sb * ch);
+        }
+    }
+    return blk;
+}
+
+// Copy each row's upper tail (from the diagonal block k0 on) into the
+// symmetric layout and measure max |B_ij - B_ji^T| per row over all its
+// off-diagonal blocks; a block whose partner (j, i) is not in the pattern must
+// be zero (it is then dropped from the product with nothing lost).
+__global__ __launch_bounds__(256) void k_gsym_check(int64_t nrows, const int *__restrict__ rowptr,
+                                                    const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
+                                                    const int *__restrict__ bcol, const double *__restrict__ val,
+                                                    const int *__restrict__ sk0, const int64_t *__restrict__ svptr,
+                                                    double *__restrict__ sval, double *__restrict__ rowdiff,
+                                                    double *__restrict__ rowmax)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= nrows) return;
+    const int r0 = rowptr[i], mp = rowptr[i + 1] - r0, m = rowcnt ? rowcnt[i] : mp, k0 = sk0[i], mu = m - k0;
+    const double *v = val + vptr[i];
+    double *sv = sval + svptr[i];
+    double dmax = 0.0, vmax = 0.0;
+    for (int kk = lane; kk < mu; kk += 64)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) sv[vofs(1, 9, t, kk, mu, mu)] = v[vofs(1, 9, t, k0 + kk, m, mp)];
+    for (int k = lane; k < m; k += 64) {
+        double b[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            b[t] = v[vofs(1, 9, t, k, m, mp)];
+            vmax = fmax(vmax, fabs(b[t]));
+        }
+        const int64_t j = bcol[r0 + k];
+        if (j == i) continue;
+        if (j < 0 || j >= nrows) {
+            dmax = INFINITY;
+            continue;
+        }
+        const int s0 = rowptr[j], mpj = rowptr[j + 1] - s0, mj = rowcnt ? rowcnt[j] : mpj;
+        int lo = 0, hi = mj - 1, kj = -1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1, cm = bcol[s0 + mid];
+            if (cm == i) {
+                kj = mid;
+                break;
+            }
+            if (cm < i) lo = mid + 1;
+            else hi = mid - 1;
+        }
+        if (kj < 0) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                if (b[t] != 0.0) dmax = INFINITY;  // (i, j) without (j, i)
+            continue;
+        }
+        const double *vj = val + vptr[j];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dmax = fmax(dmax, fabs(b[a * 3 + c] - vj[vofs(1, 9, c * 3 + a, kj, mj, mpj)]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
+        vmax = fmax(vmax, __shfl_xor(vmax, o, 64));
+    }
+    if (lane == 0) {
+        rowdiff[i] = dmax;
+        rowmax[i] = vmax;
+    }
+}
+
+// Per group: gexp[g] = e with 2^e > the largest, over its dictionary entries
+// e, of the sum over the group's rows of max_b sum_a |B[a][b]| of the block
+// whose transposed part adds to e (k_sym_bound's bound; fixed order).
+__global__ __launch_bounds__(256) void k_gsym_bound(int64_t nrows, const int *__restrict__ dptr,
+                                                    const int *__restrict__ smu, const int64_t *__restrict__ sbp,
+                                                    const uint16_t *__restrict__ slid,
+                                                    const int64_t *__restrict__ svptr,
+                                                    const double *__restrict__ sval, int *__restrict__ gexp)
+{
+    __shared__ double wred[256];
+    const int64_t g = blockIdx.x;
+    const int d0 = dptr[g], U = dptr[g + 1] - d0;
+    const int nr = (int)min<int64_t>(GSYM_G, nrows - g * GSYM_G);
+    double wm = 0.0;
+    for (int e = threadIdx.x; e < U; e += 256) {
+        double s = 0.0;
+        for (int r = 0; r < nr; ++r) {
+            if (e == r) continue;  // (the row's own diagonal block)
+            const int64_t i = g * GSYM_G + r;
+            const int mu = smu[i];
+            const uint16_t *l = slid + sbp[i];
+            int lo = 0, hi = mu - 1, kk = -1;
+            while (lo <= hi) {
+                const int mid = (lo + hi) >> 1, p = l[mid];
+                if (p == e) {
+                    kk = mid;
+                    break;
+                }
+                if (p < e) lo = mid + 1;
+                else hi = mid - 1;
+            }
+            if (kk < 0) continue;
+            const double *v = sval + svptr[i];
+            double bmax = 0.0;
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                double cs = 0.0;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) cs += fabs(v[vofs(1, 9, a * 3 + b, kk, mu, mu)]);
+                bmax = fmax(bmax, cs);
+            }
+            s += bmax;
+        }
+        wm = fmax(wm, s);
+    }
+    wred[threadIdx.x] = wm;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) wred[threadIdx.x] = fmax(wred[threadIdx.x], wred[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int e = -1000;  // no transposed adds in this group
+        if (wred[0] > 0.0) (void)frexp(wred[0], &e);
+        gexp[g] = e;
+    }
+}
+
+// y = A x, pass 1: one workgroup per group, one wave per row.  LDS: x of the
+// dictionary [U][3] | transposed partials [3][US + 64] (DET: int64; 64 dummy
+// slots per component take the adds of masked lanes) | direct row sums [G][3].
+template <bool DET, bool PF>
+__global__ __launch_bounds__(64 * GSYM_G) void k_nb_spmv_gsym(
+    int64_t nrows, int64_t ngroups, int US, const int64_t *__restrict__ svptr, const int *__restrict__ smu,
+    const int64_t *__restrict__ sbp, const uint16_t *__restrict__ slid, const int *__restrict__ dptr,
+    const int *__restrict__ dict, const double *__restrict__ sval, const double *__restrict__ x,
+    double *__restrict__ ws, const int *__restrict__ gexp, const int *__restrict__ istate, int xcd_chunk)
+{
+    extern __shared__ double lds[];
+    if (istate && istate[I_REASON] != 0) return;
+    constexpr int NT = 64 * GSYM_G;
+    const int64_t g = gsym_block(xcd_chunk);
+    if (g >= ngroups) return;  // whole workgroup
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int d0 = dptr[g], U = dptr[g + 1] - d0, RS = US + 64;
+    double *xs = lds, *yl = lds + 3 * US, *yd = yl + 3 * RS;
+    const int64_t i = g * GSYM_G + w;
+    const bool live = i < nrows;
+    // a wave past the last row reads its group's first row (results unused)
+    const int64_t ir = live ? i : g * GSYM_G;
+    const int mu = smu[ir], q16 = mu & ~15;
+    const double *v = sval + svptr[ir];
+    const uint16_t *lr = slid + sbp[ir];
+    // the values of one 64-block pass (lanes past the row's end re-read its
+    // last block; their products are masked) and the blocks' positions
+    auto load_pass = [&](int kb, double *vv, int &l) {
+        const int kk = min(kb + lane, mu - 1);
+        const bool ch = kk < q16;
+        const int o0 = ch ? (kk >> 4) * 144 + (kk & 15) : q16 * 9 + (kk - q16);
+        const int st = ch ? 16 : mu - q16;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
+        l = __builtin_nontemporal_load(lr + kk);
+    };
+    // x of the dictionary in batches of GSYM_FILL entries per thread: the id
+    // loads in flight, (PF, first batch: then both first passes of values,
+    // which stay in flight while the x loads go out), then the x loads
+    double va[9], vb[9];
+    int la = 0, lb = 0;
+    for (int f0 = 0; f0 < 3 * U; f0 += GSYM_FILL * NT) {
+        int id[GSYM_FILL];
+#pragma unroll
+        for (int f = 0; f < GSYM_FILL; ++f) {
+            const int t = min(threadIdx.x + f0 + f * NT, 3 * U - 1);
+            id[f] = dict[d0 + t / 3];
+        }
+        if (PF && f0 == 0) {
+            load_pass(0, va, la);
+            load_pass(64, vb, lb);
+        }
+        double xv[GSYM_FILL];
+#pragma unroll
+        for (int f = 0; f < GSYM_FILL; ++f) {
+            const int t = min(threadIdx.x + f0 + f * NT, 3 * U - 1);
+            xv[f] = x[(int64_t)id[f] * 3 + (t - 3 * (t / 3))];
+        }
+#pragma unroll
+        for (int f = 0; f < GSYM_FILL; ++f) {
+            const int t = threadIdx.x + f0 + f * NT;
+            if (t < 3 * U) xs[t] = xv[f];
+        }
+    }
+    for (int t = threadIdx.x; t < 3 * RS; t += NT) yl[t] = 0.0;  // (0.0 is int64 0)
+    if (threadIdx.x < 3 * GSYM_G) yd[threadIdx.x] = 0.0;
+    __syncthreads();
+    double S = 1.0, invS = 1.0;
+    if (DET) {
+        // max |x_i| over the group's rows: dictionary positions 0 .. nr-1
+        const int nr = (int)min<int64_t>(GSYM_G, nrows - g * GSYM_G);
+        double m = 0.0;
+        int bad = 0;
+        if (lane < 3 * nr) {
+            m = fabs(xs[lane]);
+            bad = !(m <= 1.7976931348623157e308);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+        if (__ballot(bad)) {
+            S = 0.0;  // non-finite x: NaN partials, as a floating-point sum would give
+            invS = __builtin_nan("");
+        } else if (m > 0.0) {
+            int em;
+            (void)frexp(m, &em);
+            const int E = min(max(gexp[g] + em, -960), 1020);
+            S = ldexp(1.0, 61 - E);
+            invS = ldexp(1.0, E - 61);
+        }
+    }
+    if (live) {
+        const double xi0 = xs[3 * w], xi1 = xs[3 * w + 1], xi2 = xs[3 * w + 2];  // (row i is position w)
+        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        unsigned long long *yi = reinterpret_cast<unsigned long long *>(yl);
+        auto pass = [&](int kb, const double *vv, int l) {
+            const int k = kb + lane;
+            const bool on = k < mu;
+            const double x0 = xs[3 * l], x1 = xs[3 * l + 1], x2 = xs[3 * l + 2];
+            const double s0 = vv[0] * x0 + vv[1] * x1 + vv[2] * x2;
+            const double s1 = vv[3] * x0 + vv[4] * x1 + vv[5] * x2;
+            const double s2 = vv[6] * x0 + vv[7] * x1 + vv[8] * x2;
+            acc0 += on ? s0 : 0.0;
+            acc1 += on ? s1 : 0.0;
+            acc2 += on ? s2 : 0.0;
+            const double t0 = vv[0] * xi0 + vv[3] * xi1 + vv[6] * xi2;
+            const double t1 = vv[1] * xi0 + vv[4] * xi1 + vv[7] * xi2;
+            const double t2 = vv[2] * xi0 + vv[5] * xi1 + vv[8] * xi2;
+            const int rt = on && k > 0 ? l : US + lane;  // (the diagonal block is not transposed)
+            if (DET) {
+                atomicAdd(&yi[rt], fx_of(t0, S));
+                atomicAdd(&yi[RS + rt], fx_of(t1, S));
+                atomicAdd(&yi[2 * RS + rt], fx_of(t2, S));
+            } else {
+                atomicAdd(&yl[rt], t0);
+                atomicAdd(&yl[RS + rt], t1);
+                atomicAdd(&yl[2 * RS + rt], t2);
+            }
+        };
+        int kb = 0;
+        if (PF) {
+            pass(0, va, la);
+            if (mu > 64) pass(64, vb, lb);
+            kb = 128;
+        }
+        for (; kb < mu; kb += 64) {
+            load_pass(kb, va, la);
+            pass(kb, va, la);
+        }
+        wsum3_dpp(acc0, acc1, acc2);  // fixed order, one writer per row
+        if (lane < 3) yd[3 * w + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
+    }
+    __syncthreads();
+    // one partial per dictionary entry, [entry][3] (coalesced)
+    const unsigned long long *yi = reinterpret_cast<const unsigned long long *>(yl);
+    double *dst = ws + (int64_t)d0 * 3;
+    for (int t = threadIdx.x; t < 3 * U; t += NT) {
+        const int e = t / 3, c = t - 3 * e;
+        double s = DET ? fx_to_d(yi[c * RS + e]) * invS : yl[c * RS + e];
+        if (e < GSYM_G) s += yd[t];
+        dst[t] = s;
+    }
+}
+
+// y_j = the partials of the dictionary entries naming row j, ascending group
+// order.  A wave takes a slice of 64 consecutive rows.  Each group's
+// dictionary is sorted, so its entries that name rows of the slice are one
+// contiguous run of its partials; a run is stored as (first entry, 64-bit
+// mask of the slice rows it names), the runs of a slice in ascending group
+// order.  Lane j adds the run's entry popcount(mask below j) when its bit is
+// set: the wave's loads of a run are one contiguous stretch of partials
+// (instead of one scattered 24-B read per row and entry), and each row still
+// sums its entries in ascending group order.  With xdot: the workgroup's
+// partial of (y, x) in dpart[blockIdx.x] (k_nb_sym_gather's fixed order).
+__global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, const int *__restrict__ runptr,
+                                                        const int *__restrict__ rstart,
+                                                        const unsigned long long *__restrict__ rmask,
+                                                        const double *__restrict__ ws, double *__restrict__ y,
+                                                        const int *__restrict__ istate, const double *__restrict__ xdot,
+                                                        double *__restrict__ dpart)
+{
+    __shared__ double dred[4];
+    if (istate && istate[I_REASON] != 0) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t sl = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t j = sl * 64 + lane;
+    if (sl * 64 >= nrows && !xdot) return;
+    double dsum = 0.0;
+    if (sl * 64 < nrows) {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        const int r1 = runptr[sl + 1];
+        // (loads unconditional -- absent lanes re-read the run's first entry --
+        // so the unrolled runs' loads are all in flight before the adds)
+#pragma unroll 8
+        for (int r = runptr[sl]; r < r1; ++r) {
+            const unsigned long long m = rmask[r];
+            const bool on = (m >> lane) & 1ull;
+            const double *p = ws + (int64_t)(rstart[r] + (on ? __popcll(m & below) : 0)) * 3;
+            const double a0 = p[0], a1 = p[1], a2 = p[2];
+            s0 += on ? a0 : 0.0;
+            s1 += on ? a1 : 0.0;
+            s2 += on ? a2 : 0.0;
+        }
+        if (j < nrows) {
+            y[3 * j] = s0;
+            y[3 * j + 1] = s1;
+            y[3 * j + 2] = s2;
+            if (xdot) dsum = s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
+        }
+    }
+    if (!xdot) return;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+    if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;
+    __syncthreads();
+    if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
+}
+
+static size_t gsym_lds(int US) { return (size_t)(3 * US + 3 * (US + 64) + 3 * GSYM_G) * sizeof(double); }
+
+// Build the graph symmetric storage (one rank).  Refuses a matrix that is not
+// symmetric to 1e-12 of its largest entry, whose pattern holds a nonzero
+// block without its partner, or whose group dictionaries exceed the LDS.
+static int gsym_build(kle_mat *A)
+{
+    kle_ctx *c = A->ctx;
+    const int64_t n = A->nrows;
+    if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_bcol && !A->d_rowbox &&
+          A->m_local == A->n_local && A->ghost_lo == 0 && A->ghost_hi == 0 && A->lo_rank < 0 && A->hi_rank < 0 &&
+          (!A->plan || A->plan->peers.empty()) && c->nranks == 1 && n > 0))
+        return fail(KLE_ERR_SUP, "symmetric storage of an unstructured matrix needs a 3x3 node-block matrix on one rank");
+    std::vector<int> rp(n + 1), cnt(n), bcol(std::max<int64_t>(A->nblocks, 1));
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
+    if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost));
+    else
+        for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
+    KLE_HIP(hipMemcpy(bcol.data(), A->d_bcol, sizeof(int) * bcol.size(), hipMemcpyDeviceToHost));
+    // per row: the diagonal block's position (columns ascending), stored count
+    std::vector<int> k0(n), smu(n);
+    std::vector<int64_t> svp(n + 1), sbp(n + 1);
+    int64_t tot = 0, blocks = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int *b = bcol.data() + rp[i], *e = b + cnt[i];
+        if (!std::is_sorted(b, e))
+            return fail(KLE_ERR_SUP, "symmetric storage: row %lld's columns are not ascending", (long long)i);
+        const int *d = std::lower_bound(b, e, (int)i);
+        if (d == e || *d != i)
+            return fail(KLE_ERR_SUP, "symmetric storage: row %lld has no diagonal block", (long long)i);
+        k0[i] = (int)(d - b);
+        smu[i] = cnt[i] - k0[i];
+        svp[i] = tot;
+        sbp[i] = blocks;
+        tot += ((int64_t)smu[i] * 9 + 15) & ~int64_t(15);
+        blocks += smu[i];
+    }
+    svp[n] = tot;
+    sbp[n] = blocks;
+    // group dictionaries (threads over groups), then the gather lists
+    const int64_t ng = (n + GSYM_G - 1) / GSYM_G;
+    std::vector<int> usz(ng);
+    std::vector<std::vector<int>> dl(ng);
+    std::vector<uint16_t> slid(std::max<int64_t>(blocks, 1));
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::atomic<bool> big{false};
+    auto work = [&](int t) {
+        for (int64_t g = t; g < ng; g += nt) {
+            const int64_t r0 = g * GSYM_G, r1 = std::min(n, r0 + GSYM_G);
+            std::vector<int> &L = dl[g];
+            for (int64_t r = r0; r < r1; ++r) L.insert(L.end(), bcol.begin() + rp[r] + k0[r], bcol.begin() + rp[r] + cnt[r]);
+            std::sort(L.begin(), L.end());
+            L.erase(std::unique(L.begin(), L.end()), L.end());
+            if ((int64_t)L.size() > GSYM_UCAP) {
+                big = true;
+                continue;
+            }
+            for (int64_t r = r0; r < r1; ++r)
+                for (int k = k0[r]; k < cnt[r]; ++k)
+                    slid[sbp[r] + k - k0[r]] =
+                        (uint16_t)(std::lower_bound(L.begin(), L.end(), bcol[rp[r] + k]) - L.begin());
+            usz[g] = (int)L.size();
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+        for (auto &x : th) x.join();
+    }
+    if (big) return fail(KLE_ERR_SUP, "symmetric storage: a row group's columns exceed %d LDS slots", GSYM_UCAP);
+    std::vector<int> dptr(ng + 1, 0);
+    int US = 0;
+    for (int64_t g = 0; g < ng; ++g) {
+        if ((int64_t)dptr[g] + usz[g] > INT_MAX / 3) return fail(KLE_ERR_SUP, "symmetric storage: dictionaries too large");
+        dptr[g + 1] = dptr[g] + usz[g];
+        US = std::max(US, usz[g]);
+        for (int e = 0; e < usz[g]; ++e) {
+            const int j = dl[g][e];
+            if (e < GSYM_G && g * GSYM_G + e < n && j != g * GSYM_G + e)  // (cannot happen: the rows lead)
+                return fail(KLE_ERR_SUP, "symmetric storage: group %lld does not lead with its rows", (long long)g);
+        }
+    }
+    const int64_t E = dptr[ng];
+    // gather runs: per 64-row slice, the groups naming its rows in ascending
+    // order, each as (first entry, mask of the slice rows) (k_nb_gsym_gather)
+    const int64_t ns = (n + 63) / 64;
+    std::vector<int> dict(std::max<int64_t>(E, 1)), runptr(ns + 1, 0);
+    std::vector<std::vector<std::pair<int, unsigned long long>>> sruns(ns);
+    for (int64_t g = 0; g < ng; ++g)
+        for (int e = 0; e < usz[g];) {
+            const int j0 = dl[g][e], sl = j0 >> 6;
+            unsigned long long m = 0;
+            const int e0 = e;
+            for (; e < usz[g] && (dl[g][e] >> 6) == sl; ++e) {
+                dict[dptr[g] + e] = dl[g][e];
+                m |= 1ull << (dl[g][e] & 63);
+            }
+            sruns[sl].push_back({dptr[g] + e0, m});
+        }
+    for (int64_t sl = 0; sl < ns; ++sl) {
+        if ((int64_t)runptr[sl] + (int64_t)sruns[sl].size() > INT_MAX)
+            return fail(KLE_ERR_SUP, "symmetric storage: gather runs too many");
+        runptr[sl + 1] = runptr[sl] + (int)sruns[sl].size();
+    }
+    const int64_t NR = runptr[ns];
+    std::vector<int> rstart(std::max<int64_t>(NR, 1));
+    std::vector<unsigned long long> rmask(std::max<int64_t>(NR, 1));
+    for (int64_t sl = 0; sl < ns; ++sl)
+        for (size_t k = 0; k < sruns[sl].size(); ++k) {
+            rstart[runptr[sl] + k] = sruns[sl][k].first;
+            rmask[runptr[sl] + k] = sruns[sl][k].second;
+        }
+    sruns.clear();
+    dl.clear();
+    dl.shrink_to_fit();
+    // device arrays; the value copy and the symmetry check
+    int *dk0 = nullptr;
+    double *rowdiff = nullptr, *rowmax = nullptr;
+    const bool nomem =
+        hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
+        hipMalloc(&A->d_srow, sizeof(int) * n) != hipSuccess || hipMalloc(&A->d_sbp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&A->d_slid, sizeof(uint16_t) * slid.size()) != hipSuccess ||
+        hipMalloc(&A->d_sdptr, sizeof(int) * (ng + 1)) != hipSuccess ||
+        hipMalloc(&A->d_sdict, sizeof(int) * dict.size()) != hipSuccess ||
+        hipMalloc(&A->d_sgptr, sizeof(int) * (ns + 1)) != hipSuccess ||
+        hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
+        hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
+        hipMalloc(&A->d_sws, sizeof(double) * 3 * std::max<int64_t>(E, 1)) != hipSuccess ||
+        hipMalloc(&A->d_stile_e, sizeof(int) * ng) != hipSuccess || hipMalloc(&dk0, sizeof(int) * n) != hipSuccess ||
+        hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess;
+    (void)hipGetLastError();
+    auto done = [&](int rc) {
+        (void)hipFree(dk0);
+        (void)hipFree(rowdiff);
+        (void)hipFree(rowmax);
+        if (rc) sym_drop(A);
+        return rc;
+    };
+    if (nomem) return done(fail(KLE_ERR_MEM, "out of device memory for symmetric storage"));
+    A->sym_graph = 1;
+    KLE_HIP(hipMemcpy(A->d_svptr, svp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_srow, smu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sbp, sbp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_slid, slid.data(), sizeof(uint16_t) * slid.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sdptr, dptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sdict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(dk0, k0.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_gsym_check, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, A->d_rowptr,
+                       A->d_rowcnt, A->d_vptr, A->d_bcol, A->d_val, dk0, A->d_svptr, A->d_sval, rowdiff, rowmax);
+    KLE_HIP(hipGetLastError());
+    std::vector<double> hd(n), hm(n);
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    KLE_HIP(hipMemcpy(hd.data(), rowdiff, sizeof(double) * n, hipMemcpyDeviceToHost));
+    KLE_HIP(hipMemcpy(hm.data(), rowmax, sizeof(double) * n, hipMemcpyDeviceToHost));
+    double dmax = 0.0, vmax = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        dmax = std::isnan(hd[i]) ? INFINITY : std::max(dmax, hd[i]);
+        vmax = std::max(vmax, hm[i]);
+    }
+    if (!(dmax <= 1e-12 * vmax))
+        return done(fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax));
+    hipLaunchKernelGGL(k_gsym_bound, dim3((unsigned)ng), dim3(256), 0, c->stream, n, A->d_sdptr, A->d_srow, A->d_sbp,
+                       A->d_slid, A->d_svptr, A->d_sval, A->d_stile_e);
+    KLE_HIP(hipGetLastError());
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    A->sym_reg[0] = US;
+    A->sblocks = blocks;
+    A->snvals = tot;
+    A->sws_entries = E;
+    if (const char *e = getenv("KLE_TIMING"))
+        if (atoi(e))
+            fprintf(stderr, "[kle gsym] rows %lld, stored blocks %lld (of %lld), groups %lld, dictionary entries %lld "
+                            "(%.2f per row, largest group %d), gather runs %lld (%.1f per 64 rows)\n",
+                    (long long)n, (long long)blocks, (long long)A->nblocks_real, (long long)ng, (long long)E,
+                    (double)E / n, US, (long long)NR, (double)NR / ns);
+    return done(0);
+}
+
+static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
+{
+    kle_ctx *c = A->ctx;
+    const int64_t n = A->nrows, ng = (n + GSYM_G - 1) / GSYM_G;
+    const int US = A->sym_reg[0];
+    const size_t lds = gsym_lds(US);
+    const bool det = g_tune.spmv_sym_det != 0, pf = g_tune.spmv_gsym_pf != 0;
+    auto launch = [&](auto kern, int slot) {
+        static size_t lds_set[4] = {0, 0, 0, 0};  // dynamic LDS above 64 KB must be declared per kernel
+        if (lds > lds_set[slot]) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            lds_set[slot] = lds;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)ng), dim3(64 * GSYM_G), lds, c->stream, n, ng, US, A->d_svptr,
+                           A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
+                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk);
+    };
+    if (det && pf) launch(k_nb_spmv_gsym<true, true>, 0);
+    else if (det) launch(k_nb_spmv_gsym<true, false>, 1);
+    else if (pf) launch(k_nb_spmv_gsym<false, true>, 2);
+    else launch(k_nb_spmv_gsym<false, false>, 3);
+    hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, n, A->d_sgptr,
+                       A->d_sgidx, A->d_sgmask, A->d_sws, y->d, istate, dpart ? x->d : nullptr, dpart);
+    KLE_HIP(hipGetLastError());
+    return 0;
 }
 
 static SymGeo sym_geo(const kle_mat *A)
@@ -856,6 +1435,7 @@ int sym_build(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
     sym_drop(A);
+    if (A->kind == 0 && !A->d_rowbox && A->d_bcol) return gsym_build(A);  // unstructured rows
     const int64_t Lx = A->row_lat[0], Ly = A->row_lat[1], Lz = A->row_lat[2], n = A->nrows, Lxy = Lx * Ly;
     std::string why;
     if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_rowbox && !A->plan &&
@@ -1131,6 +1711,7 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
+    if (A->sym_graph) return gsym_spmv(A, x, y, istate, dpart);
     const SymGeo g = sym_geo(A);
     const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz, n = A->nrows, Lxy = (int64_t)g.Lx * g.Ly;
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
@@ -1179,6 +1760,9 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 
 std::string sym_kernel_name(const kle_mat *A)
 {
+    if (A->sym_graph)
+        return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
+               (g_tune.spmv_gsym_pf ? "true" : "false") + ">+k_nb_gsym_gather";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
            (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(16 / A->sym_TZ) + "," +
            std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(16 / A->sym_TZ) + "," +
@@ -1189,6 +1773,12 @@ std::string sym_kernel_name(const kle_mat *A)
 // box, x and y once, the tile partials written and read
 double sym_spmv_bytes(const kle_mat *A)
 {
+    // graph: values + 2-B dictionary positions per stored block; per row its
+    // value offset, slid offset, count, x and y; per dictionary entry its node
+    // id and the partial written and read (the gather runs, 12 B per ~8
+    // entries, are not counted)
+    if (A->sym_graph)
+        return (double)A->sblocks * 74.0 + A->nrows * (8.0 + 8.0 + 4.0 + 48.0) + (double)A->sws_entries * (4.0 + 48.0);
     return (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 + (double)A->sws_entries * 48.0;
 }
 

@@ -266,3 +266,163 @@ def test_assembly_turns_symmetric_storage_on_from_the_threshold(pa):
     finally:
         set_tuning("spmv_sym", 1)
         set_tuning("spmv_sym_min_rows", old)
+
+
+# ---- unstructured (graph-numbered) K: k_nb_spmv_gsym + k_nb_gsym_gather ----
+
+def _umat(pa, tmp_path, nelem, ngl, seed=5):
+    from pynama_amd.meshgen import perturbed_box, write_gmsh
+    dim = len(nelem)
+    V, Cc, F, T = perturbed_box(dim, nelem, seed=seed)
+    path = tmp_path / f"m{seed}.msh"
+    write_gmsh(path, dim, V, Cc, F, T)
+    cfg = {"domain": {"ngl": ngl, "gmsh-file": str(path)},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d" if dim == 3 else "taylor_green"}}}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    return dom, mat
+
+
+@pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([6, 5, 4], 5), ([4, 3, 3], 3), ([5, 4, 3], 2),
+                                       ([2, 2, 2], 7), ([1, 1, 1], 4)])
+def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, nelem, ngl):
+    """Gmsh hexes (perturbed, rotated, shuffled; Hilbert-numbered nodes): the
+    upper-triangle storage with per-group dictionaries equals the
+    column-dictionary full-storage kernel and the exported PETSc CSR to
+    rounding, and repeated products are bitwise equal (fixed-point sums)."""
+    from pynama_amd.runtime import set_tuning
+    _, mat = _umat(pa, tmp_path, nelem, ngl)
+    K = mat.K
+    assert not K.isStructured()
+    assert not K.isSymmetricStorage()  # below spmv_sym_min_rows: full storage
+    x = K.createVecRight()
+    xa = np.random.default_rng(11).uniform(-1, 1, x.getLocalSize())
+    x.setArray(xa)
+    y0 = (K * x).getArray().copy()
+    b0 = K.spmvBytes()
+    K.setOption(K.Option.SPD, True)
+    assert K.isSymmetricStorage()
+    if ngl >= 5 and min(nelem) >= 4:
+        assert K.spmvBytes() < 0.8 * b0
+    ip, ix, d = K.getValuesCSR()
+    yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
+    try:
+        for det in (1, 0):
+            set_tuning("spmv_sym_det", det)
+            name = K.spmvKernel()
+            assert name.startswith("k_nb_spmv_gsym<"), name
+            y1 = (K * x).getArray().copy()
+            for _ in range(2):
+                y2 = (K * x).getArray().copy()
+                for ref in (y0, yh):
+                    assert np.linalg.norm(y2 - ref) <= 1e-14 * np.linalg.norm(ref), det
+                    assert np.abs(y2 - ref).max() <= 1e-13 * np.abs(ref).max(), det
+                if det:
+                    np.testing.assert_array_equal(y2, y1)
+    finally:
+        set_tuning("spmv_sym_det", 1)
+    K.setOption(K.Option.SPD, False)
+    assert not K.isSymmetricStorage()
+    np.testing.assert_array_equal((K * x).getArray(), y0)
+
+
+def test_unstructured_symmetric_spmv_edge_inputs(pa, tmp_path):
+    """Zero x gives exactly zero, a NaN propagates, and the per-group scale
+    follows max|x| from 1e-200 to 1e150."""
+    _, mat = _umat(pa, tmp_path, [4, 3, 3], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    assert K.isSymmetricStorage()
+    x = K.createVecRight()
+    x.setArray(np.zeros(x.getLocalSize()))
+    assert not np.any((K * x).getArray())
+    xa = np.random.default_rng(3).uniform(-1, 1, x.getLocalSize())
+    ip, ix, d = K.getValuesCSR()
+    A = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa)))
+    for scale in (1e-200, 1e-8, 1.0, 1e150):
+        x.setArray(xa * scale)
+        y = (K * x).getArray()
+        yh = A @ (xa * scale)
+        assert np.linalg.norm(y - yh) <= 1e-14 * np.linalg.norm(yh), scale
+    xb = xa.copy()
+    xb[len(xb) // 3] = np.nan
+    x.setArray(xb)
+    assert np.isnan((K * x).getArray()).any()
+
+
+def test_unstructured_symmetric_cg_matches_oracle(pa, tmp_path):
+    """Jacobi-CG through the graph symmetric storage (single-reduction with
+    the gather's fused (w, u) partials, classic, pipelined) against the
+    oracle's CG on the exported CSR; two solves bitwise equal."""
+    from pynama_amd import fields
+    dom, mat = _umat(pa, tmp_path, [6, 5, 4], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    assert K.isSymmetricStorage()
+    f = fields.get("taylor_green3d")
+    alpha = f.alpha(0.02, 0.0)
+    sol = pa.KleSolver()
+    sol.setMat(mat)
+    sol.setUp()
+    vort = mat.Rw.createVecRight()
+    vort.setArray(f.vorticity(dom.getFullCoordArray(), alpha))
+    vel = sol.getSolution()
+    dom.applyBoundaryConditions(vel, "velocity", 0.0, 0.02)
+    b = sol.rhs(vort).copy()
+    ip, ix, d = K.getValuesCSR()
+    Ko = O.CSR.from_arrays(ip, ix, d, len(ip) - 1)
+    xo, it_o, _ = Ko.cg(b.getArray(), rtol=1e-10, jacobi=True)
+    for typ, single in (("cg", True), ("cg", True), ("cg", False), ("pipecg", True)):
+        ksp = pa.petsc.KSP().create()
+        ksp.setType(typ)
+        pc = pa.petsc.PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+        ksp.setCGSingleReduction(single)
+        ksp.setOperators(K)
+        x = K.createVecRight()
+        ksp.solve(b, x)
+        assert ksp.getConvergedReason() > 0
+        assert abs(ksp.getIterationNumber() - it_o) <= (4 if typ == "pipecg" else 2), (typ, single)
+        assert ksp.getTrueRelativeResidual() <= 1.5e-10
+        assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
+        if typ == "cg" and single:
+            if "first" in locals():
+                np.testing.assert_array_equal(x.getArray(), first)
+            first = x.getArray().copy()
+
+
+def test_unstructured_symmetric_storage_refused_where_it_does_not_apply(pa, tmp_path):
+    """Rw (not symmetric) and a 2-D unstructured K (2x2 blocks) keep the full
+    storage; K of the same mesh takes the graph storage."""
+    _, mat = _umat(pa, tmp_path, [3, 3, 2], 4)
+    mat.Rw.setOption(mat.Rw.Option.SPD, True)
+    assert not mat.Rw.isSymmetricStorage()
+    mat.K.setOption(mat.K.Option.SPD, True)
+    assert mat.K.isSymmetricStorage()
+    _, m2 = _umat(pa, tmp_path, [5, 4], 4, seed=6)
+    m2.K.setOption(m2.K.Option.SPD, True)
+    assert not m2.K.isSymmetricStorage()
+
+
+def test_unstructured_duplicate_owns_its_symmetric_storage(pa, tmp_path):
+    _, mat = _umat(pa, tmp_path, [4, 3, 3], 5)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    x = K.createVecRight()
+    x.setArray(np.random.default_rng(5).uniform(-1, 1, x.getLocalSize()))
+    y0 = (K * x).getArray().copy()
+    B = K.duplicate(copy=True)
+    assert B.isSymmetricStorage()
+    np.testing.assert_array_equal((B * x).getArray(), y0)
+    B.axpy(1.0, K)
+    assert not B.isSymmetricStorage() and K.isSymmetricStorage()
+    np.testing.assert_array_equal((K * x).getArray(), y0)
+    assert np.abs((B * x).getArray() - 2 * y0).max() <= 1e-13 * np.abs(y0).max()
+    B.destroy()
+    np.testing.assert_array_equal((K * x).getArray(), y0)

@@ -9,6 +9,7 @@
 #   bench:<bench.py args>   one bench line -> $OUT/bench_<n>.json
 #   prof:<bench.py args>    rocprofv3 kernel trace + stats of a bench run
 #   pmc:<bench.py args>     PMC FETCH_SIZE and WRITE_SIZE passes (separate runs)
+#   sprof:<spmv_ab.py args> rocprofv3 kernel trace + stats of an in-process SpMV A/B
 #   sq:<spmv_ab.py args>    one PMC pass of 8 SQ counters (wave cycles, waits, active VALU/SALU/LDS) over tools/spmv_ab.py
 #   cmd:<command>           any command (env assignments allowed: cmd:KLE_TRANSPORT=host python bench.py --gpus 2)
 #   smoke:                  __graft_entry__.smoke()
@@ -48,6 +49,9 @@ for spec in "$@"; do
       step ${name}_w 400 timeout -s KILL 380 rocprofv3 --pmc WRITE_SIZE -d $OUT/${n}_pmc_w -o w --output-format csv -- python3 bench.py $args || exit 1 ;;
     sq)
       step $name 400 timeout -s KILL 380 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_VALU -d $OUT/${n}_sq -o sq --output-format csv -- python3 tools/spmv_ab.py $args || exit 1 ;;
+    sprof)
+      step $name 600 rocprofv3 --kernel-trace --stats -d $OUT/${n}_sprof -o prof --output-format csv -- python3 tools/spmv_ab.py $args || exit 1
+      grep '^{' "gpurun_out/$name.log" > "$OUT/${n}_sprof.jsonl" || true ;;
     cmd)
       step $name 900 env $args || exit 1
       grep '^{' "gpurun_out/$name.log" > "$OUT/${n}_cmd.jsonl" || true ;;

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--ngl", type=int, default=5)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--its", type=int, default=100)
+    ap.add_argument("--mesh", choices=["box", "unstructured"], default="box",
+                    help="unstructured: the box written as a Gmsh file of perturbed, rotated, shuffled hexes")
     a = ap.parse_args()
     import numpy as np
     import pynama_amd as pa
@@ -33,6 +35,13 @@ def main():
     nelem = [int(v) for v in a.nelem.split(",")]
     cfg = {"domain": {"ngl": a.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * 3, "upper": [1.0] * 3}},
            "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    if a.mesh == "unstructured":
+        import tempfile
+        from pynama_amd.meshgen import perturbed_box, write_gmsh
+        V, Cc, F, T = perturbed_box(3, nelem, seed=5)
+        path = os.path.join(tempfile.mkdtemp(prefix="kle_ab_"), "mesh.msh")
+        write_gmsh(path, 3, V, Cc, F, T)
+        cfg["domain"] = {"ngl": a.ngl, "gmsh-file": path}
     dom = pa.Domain()
     dom.configure(cfg)
     dom.setUp()
@@ -74,7 +83,7 @@ def main():
             print(json.dumps({"rep": rep, "variant": v, "kernel": name, "spmv_ms": ms / c}), flush=True)
     print(json.dumps({"summary": [{"variant": v, "median_ms": statistics.median(res[i]), "min_ms": min(res[i])}
                                   for i, v in enumerate(variants)], "nelem": nelem, "ngl": a.ngl,
-                      "spmv_bytes": K.spmvBytes()}), flush=True)
+                      "mesh": a.mesh, "spmv_bytes": K.spmvBytes()}), flush=True)
 
 
 if __name__ == "__main__":
