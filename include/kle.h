@@ -86,9 +86,10 @@ const char *kle_last_error(void);
  * CU, 2 = 8 x 8 x 2), "spmv_sym_det" (1
  * default: the transposed adds as exact fixed-point sums, y bitwise
  * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
- * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_pf"
- * (unstructured symmetric SpMV: 1 default, a row's first two passes of
- * values issued before the dictionary x fill; 0 after it), "spmv_sym_probe"
+ * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_rows"
+ * (read when the storage of an unstructured K is built: rows per group, 16
+ * default or 8), "spmv_gsym_split" (read at build: the largest dictionary of
+ * the first of its two launches; 0 auto), "spmv_sym_probe"
  * (timing probes that skip parts of the symmetric SpMV: wrong results on
  * purpose; 0 default; bits in kle_internal.hpp). */
 int kle_set_tuning(const char *key, int value);

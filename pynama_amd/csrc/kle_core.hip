@@ -581,9 +581,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
-    } else if (k == "spmv_gsym_pf") {
-        KLE_ARG(value == 0 || value == 1, "spmv_gsym_pf: 0 or 1");
-        g_tune.spmv_gsym_pf = value;
+    } else if (k == "spmv_gsym_rows") {
+        KLE_ARG(value == 8 || value == 16 || value == 32, "spmv_gsym_rows: 8, 16 or 32");
+        g_tune.spmv_gsym_rows = value;
+    } else if (k == "spmv_gsym_split") {
+        KLE_ARG(value >= 0, "spmv_gsym_split: >= 0");
+        g_tune.spmv_gsym_split = value;
     } else if (k == "spmv_sym_probe") {
         KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
         g_tune.spmv_sym_probe = value;
@@ -621,7 +624,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
-    else if (k == "spmv_gsym_pf") *value = g_tune.spmv_gsym_pf;
+    else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
+    else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

@@ -245,14 +245,15 @@ struct kle_mat {
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
     int sym_P = 0, sym_TZ = 2;
-    int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: [0] = LDS dictionary slots
+    int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
     // graph (unstructured) symmetric storage, one rank (kle_sym.hip gsym_build):
     // d_srow = stored blocks per row, d_stile_e = per-group scale exponents,
     // d_sws = one partial per dictionary entry
     int sym_graph = 0;
     int64_t *d_sbp = nullptr;     // per row: its first stored block in d_slid
     uint16_t *d_slid = nullptr;   // per stored block: its column's position in the group dictionary
-    int *d_sdptr = nullptr, *d_sdict = nullptr;  // per group of GSYM_G rows: sorted distinct stored columns
+    int *d_sdptr = nullptr, *d_sdict = nullptr;  // per group of G rows: sorted distinct stored columns
+    int *d_sglist = nullptr;  // group order of the launches: sym_reg[2] groups within sym_reg[0] slots, then the rest
     // gather runs (k_nb_gsym_gather): per 64-row slice s, runs [d_sgptr[s], d_sgptr[s+1]) in ascending
     // group order, each the first dictionary entry (d_sgidx) naming a slice row and the mask of the rows it names
     int *d_sgptr = nullptr, *d_sgidx = nullptr;
@@ -339,7 +340,8 @@ struct Tuning {
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
     int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 2 row sums, 4 LDS x reads, 8 partial stores, 16 block -> region arithmetic, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
-    int spmv_gsym_pf = 1;     // unstructured symmetric SpMV: a row's first two passes of values issued before the x fill; 0 off
+    int spmv_gsym_rows = 16;  // unstructured symmetric storage: rows per group (8 or 16; read at build)
+    int spmv_gsym_split = 0;  // unstructured symmetric storage: dictionary slots of the first launch (0 auto: 4 workgroups per CU; tests)
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)
 };

@@ -707,7 +707,7 @@ void sym_forget(kle_mat *A)
     A->d_srow = nullptr;
     A->d_sbp = nullptr;
     A->d_slid = nullptr;
-    A->d_sdptr = A->d_sdict = A->d_sgptr = A->d_sgidx = nullptr;
+    A->d_sdptr = A->d_sdict = A->d_sgptr = A->d_sgidx = A->d_sglist = nullptr;
     A->d_sgmask = nullptr;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
@@ -719,7 +719,7 @@ void sym_drop(kle_mat *A)
     for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
                     (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow, (void *)A->d_sbp,
                     (void *)A->d_slid, (void *)A->d_sdptr, (void *)A->d_sdict, (void *)A->d_sgptr,
-                    (void *)A->d_sgidx, (void *)A->d_sgmask})
+                    (void *)A->d_sgidx, (void *)A->d_sgmask, (void *)A->d_sglist})
         if (q) (void)hipFree(q);
     sym_forget(A);
 }
@@ -728,7 +728,7 @@ void sym_drop(kle_mat *A)
 // Symmetric storage of an unstructured (graph-numbered) 3x3 matrix, one rank.
 // The columns are streamed (bcol ascending per row; node ids in Hilbert order,
 // kle_umesh.cpp), so the upper triangle j >= i of row i is the tail of its
-// column list from the diagonal block on.  Rows go in groups of GSYM_G
+// column list from the diagonal block on.  Rows go in groups of G
 // consecutive rows, one wave per row.  A group's dictionary is the sorted set
 // of its stored blocks' columns; every one is >= the group's first row, so
 // positions 0 .. G-1 are the group's own rows.  The dictionary serves both
@@ -741,8 +741,8 @@ void sym_drop(kle_mat *A)
 // the partials written and read once (~25 entries per row at p = 4).  The
 // transposed adds are exact fixed-point sums as in the box kernel (scale per
 // group from k_gsym_bound), so y is bitwise reproducible.
-constexpr int GSYM_G = 8;
-constexpr int GSYM_UCAP = 1536;  // dictionary entries per group (LDS: 48 B each)
+constexpr int GSYM_UCAP = 2600;  // dictionary entries per group (LDS: 48 B each)
+constexpr int GSYM_LDS4 = 40960;  // LDS per workgroup while 4 of 8 waves fit a CU
 constexpr int GSYM_FILL = 2;  // x-fill entries per thread and batch (3 x 196 entries per group on average)
 
 // kle_mat.hip xcd_block: runs of ch consecutive groups per XCD
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256) void k_gsym_check(int64_t nrows, const int *__
 // Per group: gexp[g] = e with 2^e > the largest, over its dictionary entries
 // e, of the sum over the group's rows of max_b sum_a |B[a][b]| of the block
 // whose transposed part adds to e (k_sym_bound's bound; fixed order).
-__global__ __launch_bounds__(256) void k_gsym_bound(int64_t nrows, const int *__restrict__ dptr,
+__global__ __launch_bounds__(256) void k_gsym_bound(int64_t nrows, int G, const int *__restrict__ dptr,
                                                     const int *__restrict__ smu, const int64_t *__restrict__ sbp,
                                                     const uint16_t *__restrict__ slid,
                                                     const int64_t *__restrict__ svptr,
@@ -839,13 +839,13 @@ __global__ __launch_bounds__(256) void k_gsym_bound(int64_t nrows, const int *__
     __shared__ double wred[256];
     const int64_t g = blockIdx.x;
     const int d0 = dptr[g], U = dptr[g + 1] - d0;
-    const int nr = (int)min<int64_t>(GSYM_G, nrows - g * GSYM_G);
+    const int nr = (int)min<int64_t>(G, nrows - g * G);
     double wm = 0.0;
     for (int e = threadIdx.x; e < U; e += 256) {
         double s = 0.0;
         for (int r = 0; r < nr; ++r) {
             if (e == r) continue;  // (the row's own diagonal block)
-            const int64_t i = g * GSYM_G + r;
+            const int64_t i = g * G + r;
             const int mu = smu[i];
             const uint16_t *l = slid + sbp[i];
             int lo = 0, hi = mu - 1, kk = -1;
@@ -885,57 +885,38 @@ __global__ __launch_bounds__(256) void k_gsym_bound(int64_t nrows, const int *__
     }
 }
 
-// y = A x, pass 1: one workgroup per group, one wave per row.  LDS: x of the
-// dictionary [U][3] | transposed partials [3][US + 64] (DET: int64; 64 dummy
-// slots per component take the adds of masked lanes) | direct row sums [G][3].
-template <bool DET, bool PF>
-__global__ __launch_bounds__(64 * GSYM_G) void k_nb_spmv_gsym(
-    int64_t nrows, int64_t ngroups, int US, const int64_t *__restrict__ svptr, const int *__restrict__ smu,
-    const int64_t *__restrict__ sbp, const uint16_t *__restrict__ slid, const int *__restrict__ dptr,
-    const int *__restrict__ dict, const double *__restrict__ sval, const double *__restrict__ x,
-    double *__restrict__ ws, const int *__restrict__ gexp, const int *__restrict__ istate, int xcd_chunk)
+// y = A x, pass 1: one workgroup of 8 waves per group of G rows, wave w
+// takes rows w, w + 8, ... (G / 8 rows, one after the other).  The launch
+// runs the groups of glist[] (groups whose dictionaries fit its US slots).
+// LDS: x of the dictionary [U][3] | transposed partials [3][US + 64] (DET:
+// int64; 64 dummy slots per component take the adds of masked lanes) |
+// direct row sums [G][3].
+template <bool DET, int G>
+__global__ __launch_bounds__(512) void k_nb_spmv_gsym(
+    int64_t nrows, int64_t nlist, const int *__restrict__ glist, int US, const int64_t *__restrict__ svptr,
+    const int *__restrict__ smu, const int64_t *__restrict__ sbp, const uint16_t *__restrict__ slid,
+    const int *__restrict__ dptr, const int *__restrict__ dict, const double *__restrict__ sval,
+    const double *__restrict__ x, double *__restrict__ ws, const int *__restrict__ gexp,
+    const int *__restrict__ istate, int xcd_chunk, int probe)
 {
     extern __shared__ double lds[];
     if (istate && istate[I_REASON] != 0) return;
-    constexpr int NT = 64 * GSYM_G;
-    const int64_t g = gsym_block(xcd_chunk);
-    if (g >= ngroups) return;  // whole workgroup
+    constexpr int NT = 512, RW = G / 8;
+    const int64_t blk = gsym_block(xcd_chunk);
+    if (blk >= nlist) return;  // whole workgroup
+    const int64_t g = glist[blk];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int d0 = dptr[g], U = dptr[g + 1] - d0, RS = US + 64;
+    const int nr = (int)min<int64_t>(G, nrows - g * G);
     double *xs = lds, *yl = lds + 3 * US, *yd = yl + 3 * RS;
-    const int64_t i = g * GSYM_G + w;
-    const bool live = i < nrows;
-    // a wave past the last row reads its group's first row (results unused)
-    const int64_t ir = live ? i : g * GSYM_G;
-    const int mu = smu[ir], q16 = mu & ~15;
-    const double *v = sval + svptr[ir];
-    const uint16_t *lr = slid + sbp[ir];
-    // the values of one 64-block pass (lanes past the row's end re-read its
-    // last block; their products are masked) and the blocks' positions
-    auto load_pass = [&](int kb, double *vv, int &l) {
-        const int kk = min(kb + lane, mu - 1);
-        const bool ch = kk < q16;
-        const int o0 = ch ? (kk >> 4) * 144 + (kk & 15) : q16 * 9 + (kk - q16);
-        const int st = ch ? 16 : mu - q16;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
-        l = __builtin_nontemporal_load(lr + kk);
-    };
     // x of the dictionary in batches of GSYM_FILL entries per thread: the id
-    // loads in flight, (PF, first batch: then both first passes of values,
-    // which stay in flight while the x loads go out), then the x loads
-    double va[9], vb[9];
-    int la = 0, lb = 0;
-    for (int f0 = 0; f0 < 3 * U; f0 += GSYM_FILL * NT) {
+    // loads in flight, then the x loads
+    for (int f0 = (probe & 4) ? 3 * U : 0; f0 < 3 * U; f0 += GSYM_FILL * NT) {  // (probe 4: no x fill)
         int id[GSYM_FILL];
 #pragma unroll
         for (int f = 0; f < GSYM_FILL; ++f) {
             const int t = min(threadIdx.x + f0 + f * NT, 3 * U - 1);
             id[f] = dict[d0 + t / 3];
-        }
-        if (PF && f0 == 0) {
-            load_pass(0, va, la);
-            load_pass(64, vb, lb);
         }
         double xv[GSYM_FILL];
 #pragma unroll
@@ -950,17 +931,17 @@ __global__ __launch_bounds__(64 * GSYM_G) void k_nb_spmv_gsym(
         }
     }
     for (int t = threadIdx.x; t < 3 * RS; t += NT) yl[t] = 0.0;  // (0.0 is int64 0)
-    if (threadIdx.x < 3 * GSYM_G) yd[threadIdx.x] = 0.0;
+    if (threadIdx.x < 3 * G) yd[threadIdx.x] = 0.0;
     __syncthreads();
     double S = 1.0, invS = 1.0;
     if (DET) {
         // max |x_i| over the group's rows: dictionary positions 0 .. nr-1
-        const int nr = (int)min<int64_t>(GSYM_G, nrows - g * GSYM_G);
         double m = 0.0;
         int bad = 0;
-        if (lane < 3 * nr) {
-            m = fabs(xs[lane]);
-            bad = !(m <= 1.7976931348623157e308);
+        for (int r = lane; r < 3 * nr; r += 64) {
+            const double a = fabs(xs[r]);
+            bad |= !(a <= 1.7976931348623157e308);
+            m = fmax(m, a);
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
@@ -975,12 +956,27 @@ __global__ __launch_bounds__(64 * GSYM_G) void k_nb_spmv_gsym(
             invS = ldexp(1.0, E - 61);
         }
     }
-    if (live) {
-        const double xi0 = xs[3 * w], xi1 = xs[3 * w + 1], xi2 = xs[3 * w + 2];  // (row i is position w)
+    unsigned long long *yi = reinterpret_cast<unsigned long long *>(yl);
+    for (int rr = 0; rr < RW; ++rr) {
+        const int pos = w + 8 * rr;  // the row's position in the group (and its dictionary)
+        if (pos >= nr) break;
+        const int64_t i = g * G + pos;
+        const int mu = smu[i], q16 = mu & ~15;
+        const double *v = sval + svptr[i];
+        const uint16_t *lr = slid + sbp[i];
+        const double xi0 = xs[3 * pos], xi1 = xs[3 * pos + 1], xi2 = xs[3 * pos + 2];
         double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-        unsigned long long *yi = reinterpret_cast<unsigned long long *>(yl);
-        auto pass = [&](int kb, const double *vv, int l) {
-            const int k = kb + lane;
+        for (int kb = (probe & 128) ? mu : 0; kb < mu; kb += 64) {  // (probe 128: no item loop)
+            // the values of one 64-block pass (lanes past the row's end re-read
+            // its last block; their products are masked) and the blocks' positions
+            const int k = kb + lane, kk = min(k, mu - 1);
+            const bool ch = kk < q16;
+            const int o0 = ch ? (kk >> 4) * 144 + (kk & 15) : q16 * 9 + (kk - q16);
+            const int st = ch ? 16 : mu - q16;
+            double vv[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
+            const int l = __builtin_nontemporal_load(lr + kk);
             const bool on = k < mu;
             const double x0 = xs[3 * l], x1 = xs[3 * l + 1], x2 = xs[3 * l + 2];
             const double s0 = vv[0] * x0 + vv[1] * x1 + vv[2] * x2;
@@ -993,7 +989,9 @@ __global__ __launch_bounds__(64 * GSYM_G) void k_nb_spmv_gsym(
             const double t1 = vv[1] * xi0 + vv[4] * xi1 + vv[7] * xi2;
             const double t2 = vv[2] * xi0 + vv[5] * xi1 + vv[8] * xi2;
             const int rt = on && k > 0 ? l : US + lane;  // (the diagonal block is not transposed)
-            if (DET) {
+            if (probe & 1) {
+                if (!on) yd[lane] = t0 + t1 + t2;  // (probe 1: no transposed adds)
+            } else if (DET) {
                 atomicAdd(&yi[rt], fx_of(t0, S));
                 atomicAdd(&yi[RS + rt], fx_of(t1, S));
                 atomicAdd(&yi[2 * RS + rt], fx_of(t2, S));
@@ -1002,28 +1000,17 @@ __global__ __launch_bounds__(64 * GSYM_G) void k_nb_spmv_gsym(
                 atomicAdd(&yl[RS + rt], t1);
                 atomicAdd(&yl[2 * RS + rt], t2);
             }
-        };
-        int kb = 0;
-        if (PF) {
-            pass(0, va, la);
-            if (mu > 64) pass(64, vb, lb);
-            kb = 128;
-        }
-        for (; kb < mu; kb += 64) {
-            load_pass(kb, va, la);
-            pass(kb, va, la);
         }
         wsum3_dpp(acc0, acc1, acc2);  // fixed order, one writer per row
-        if (lane < 3) yd[3 * w + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
+        if (lane < 3) yd[3 * pos + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
     }
     __syncthreads();
     // one partial per dictionary entry, [entry][3] (coalesced)
-    const unsigned long long *yi = reinterpret_cast<const unsigned long long *>(yl);
     double *dst = ws + (int64_t)d0 * 3;
-    for (int t = threadIdx.x; t < 3 * U; t += NT) {
+    for (int t = (probe & 8) ? 3 * U : threadIdx.x; t < 3 * U; t += NT) {  // (probe 8: no partial stores)
         const int e = t / 3, c = t - 3 * e;
         double s = DET ? fx_to_d(yi[c * RS + e]) * invS : yl[c * RS + e];
-        if (e < GSYM_G) s += yd[t];
+        if (e < G) s += yd[t];
         dst[t] = s;
     }
 }
@@ -1083,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, const int
     if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
 }
 
-static size_t gsym_lds(int US) { return (size_t)(3 * US + 3 * (US + 64) + 3 * GSYM_G) * sizeof(double); }
+static size_t gsym_lds(int US, int G) { return (size_t)(3 * US + 3 * (US + 64) + 3 * G) * sizeof(double); }
 
 // Build the graph symmetric storage (one rank).  Refuses a matrix that is not
 // symmetric to 1e-12 of its largest entry, whose pattern holds a nonzero
@@ -1124,7 +1111,8 @@ static int gsym_build(kle_mat *A)
     svp[n] = tot;
     sbp[n] = blocks;
     // group dictionaries (threads over groups), then the gather lists
-    const int64_t ng = (n + GSYM_G - 1) / GSYM_G;
+    const int G = g_tune.spmv_gsym_rows;
+    const int64_t ng = (n + G - 1) / G;
     std::vector<int> usz(ng);
     std::vector<std::vector<int>> dl(ng);
     std::vector<uint16_t> slid(std::max<int64_t>(blocks, 1));
@@ -1132,7 +1120,7 @@ static int gsym_build(kle_mat *A)
     std::atomic<bool> big{false};
     auto work = [&](int t) {
         for (int64_t g = t; g < ng; g += nt) {
-            const int64_t r0 = g * GSYM_G, r1 = std::min(n, r0 + GSYM_G);
+            const int64_t r0 = g * G, r1 = std::min(n, r0 + G);
             std::vector<int> &L = dl[g];
             for (int64_t r = r0; r < r1; ++r) L.insert(L.end(), bcol.begin() + rp[r] + k0[r], bcol.begin() + rp[r] + cnt[r]);
             std::sort(L.begin(), L.end());
@@ -1162,11 +1150,25 @@ static int gsym_build(kle_mat *A)
         US = std::max(US, usz[g]);
         for (int e = 0; e < usz[g]; ++e) {
             const int j = dl[g][e];
-            if (e < GSYM_G && g * GSYM_G + e < n && j != g * GSYM_G + e)  // (cannot happen: the rows lead)
+            if (e < G && g * G + e < n && j != g * G + e)  // (cannot happen: the rows lead)
                 return fail(KLE_ERR_SUP, "symmetric storage: group %lld does not lead with its rows", (long long)g);
         }
     }
     const int64_t E = dptr[ng];
+    // the launches: groups whose dictionaries fit US1 slots (4 workgroups per
+    // CU), then the rest (US = the largest)
+    int US4 = (int)((GSYM_LDS4 / sizeof(double) - 3 * 64 - 3 * G) / 6);
+    if (g_tune.spmv_gsym_split > 0) US4 = std::min(US4, g_tune.spmv_gsym_split);
+    std::vector<int> glist(ng);
+    int64_t n1 = 0;
+    int US1 = 0;
+    for (int64_t g = 0; g < ng; ++g)
+        if (US <= US4 || usz[g] <= US4) {
+            glist[n1++] = (int)g;
+            US1 = std::max(US1, usz[g]);
+        }
+    for (int64_t g = 0, k = n1; g < ng; ++g)
+        if (!(US <= US4 || usz[g] <= US4)) glist[k++] = (int)g;
     // gather runs: per 64-row slice, the groups naming its rows in ascending
     // order, each as (first entry, mask of the slice rows) (k_nb_gsym_gather)
     const int64_t ns = (n + 63) / 64;
@@ -1209,6 +1211,7 @@ static int gsym_build(kle_mat *A)
         hipMalloc(&A->d_slid, sizeof(uint16_t) * slid.size()) != hipSuccess ||
         hipMalloc(&A->d_sdptr, sizeof(int) * (ng + 1)) != hipSuccess ||
         hipMalloc(&A->d_sdict, sizeof(int) * dict.size()) != hipSuccess ||
+        hipMalloc(&A->d_sglist, sizeof(int) * ng) != hipSuccess ||
         hipMalloc(&A->d_sgptr, sizeof(int) * (ns + 1)) != hipSuccess ||
         hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
         hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
@@ -1231,6 +1234,7 @@ static int gsym_build(kle_mat *A)
     KLE_HIP(hipMemcpy(A->d_slid, slid.data(), sizeof(uint16_t) * slid.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sdptr, dptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sdict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_sglist, glist.data(), sizeof(int) * ng, hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(), hipMemcpyHostToDevice));
@@ -1249,45 +1253,61 @@ static int gsym_build(kle_mat *A)
     }
     if (!(dmax <= 1e-12 * vmax))
         return done(fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax));
-    hipLaunchKernelGGL(k_gsym_bound, dim3((unsigned)ng), dim3(256), 0, c->stream, n, A->d_sdptr, A->d_srow, A->d_sbp,
+    hipLaunchKernelGGL(k_gsym_bound, dim3((unsigned)ng), dim3(256), 0, c->stream, n, G, A->d_sdptr, A->d_srow, A->d_sbp,
                        A->d_slid, A->d_svptr, A->d_sval, A->d_stile_e);
     KLE_HIP(hipGetLastError());
     KLE_HIP(hipStreamSynchronize(c->stream));
-    A->sym_reg[0] = US;
+    A->sym_reg[0] = US1;
+    A->sym_reg[1] = US;
+    A->sym_reg[2] = (int)n1;
+    A->sym_reg[3] = G;
     A->sblocks = blocks;
     A->snvals = tot;
     A->sws_entries = E;
     if (const char *e = getenv("KLE_TIMING"))
         if (atoi(e))
             fprintf(stderr, "[kle gsym] rows %lld, stored blocks %lld (of %lld), groups %lld, dictionary entries %lld "
-                            "(%.2f per row, largest group %d), gather runs %lld (%.1f per 64 rows)\n",
+                            "(%.2f per row, largest group %d; %lld groups within %d slots), gather runs %lld (%.1f per 64 rows)\n",
                     (long long)n, (long long)blocks, (long long)A->nblocks_real, (long long)ng, (long long)E,
-                    (double)E / n, US, (long long)NR, (double)NR / ns);
+                    (double)E / n, US, (long long)n1, US1, (long long)NR, (double)NR / ns);
     return done(0);
 }
 
 static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
-    const int64_t n = A->nrows, ng = (n + GSYM_G - 1) / GSYM_G;
-    const int US = A->sym_reg[0];
-    const size_t lds = gsym_lds(US);
-    const bool det = g_tune.spmv_sym_det != 0, pf = g_tune.spmv_gsym_pf != 0;
-    auto launch = [&](auto kern, int slot) {
-        static size_t lds_set[4] = {0, 0, 0, 0};  // dynamic LDS above 64 KB must be declared per kernel
+    const int G = A->sym_reg[3];
+    const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2];
+    const bool det = g_tune.spmv_sym_det != 0;
+    auto launch = [&](auto kern, int slot, int64_t l0, int64_t nl, int US) {
+        if (nl <= 0) return;
+        const size_t lds = gsym_lds(US, G);
+        static size_t lds_set[12] = {};  // dynamic LDS above 64 KB must be declared per kernel
         if (lds > lds_set[slot]) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
             lds_set[slot] = lds;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)ng), dim3(64 * GSYM_G), lds, c->stream, n, ng, US, A->d_svptr,
-                           A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
-                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk);
+        hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(512), lds, c->stream, n, nl, A->d_sglist + l0, US,
+                           A->d_svptr, A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base,
+                           A->d_sws, A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_probe);
     };
-    if (det && pf) launch(k_nb_spmv_gsym<true, true>, 0);
-    else if (det) launch(k_nb_spmv_gsym<true, false>, 1);
-    else if (pf) launch(k_nb_spmv_gsym<false, true>, 2);
-    else launch(k_nb_spmv_gsym<false, false>, 3);
+    auto launch2 = [&](auto kern, int slot) {
+        launch(kern, slot, 0, n1, A->sym_reg[0]);
+        launch(kern, slot + 1, n1, ng - n1, A->sym_reg[1]);
+    };
+    if (G == 8) {
+        if (det) launch2(k_nb_spmv_gsym<true, 8>, 0);
+        else launch2(k_nb_spmv_gsym<false, 8>, 2);
+    } else if (G == 16) {
+        if (det) launch2(k_nb_spmv_gsym<true, 16>, 4);
+        else launch2(k_nb_spmv_gsym<false, 16>, 6);
+    } else if (G == 32) {
+        if (det) launch2(k_nb_spmv_gsym<true, 32>, 8);
+        else launch2(k_nb_spmv_gsym<false, 32>, 10);
+    } else {
+        return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group", G);
+    }
     hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, n, A->d_sgptr,
                        A->d_sgidx, A->d_sgmask, A->d_sws, y->d, istate, dpart ? x->d : nullptr, dpart);
     KLE_HIP(hipGetLastError());
@@ -1762,7 +1782,7 @@ std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
-               (g_tune.spmv_gsym_pf ? "true" : "false") + ">+k_nb_gsym_gather";
+               std::to_string(A->sym_reg[3]) + ">+k_nb_gsym_gather";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
            (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(16 / A->sym_TZ) + "," +
            std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(16 / A->sym_TZ) + "," +

@@ -311,20 +311,28 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
     ip, ix, d = K.getValuesCSR()
     yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
     try:
-        for det in (1, 0):
-            set_tuning("spmv_sym_det", det)
-            name = K.spmvKernel()
-            assert name.startswith("k_nb_spmv_gsym<"), name
-            y1 = (K * x).getArray().copy()
-            for _ in range(2):
-                y2 = (K * x).getArray().copy()
-                for ref in (y0, yh):
-                    assert np.linalg.norm(y2 - ref) <= 1e-14 * np.linalg.norm(ref), det
-                    assert np.abs(y2 - ref).max() <= 1e-13 * np.abs(ref).max(), det
-                if det:
-                    np.testing.assert_array_equal(y2, y1)
+        # groups of 16 / 8 rows, one launch or the groups split over two
+        # (the larger dictionaries in a second launch with more LDS)
+        for rows, split in ((16, 0), (8, 0), (16, 40), (8, 20)):
+            set_tuning("spmv_gsym_rows", rows)
+            set_tuning("spmv_gsym_split", split)
+            K.setOption(K.Option.SPD, True)
+            for det in (1, 0):
+                set_tuning("spmv_sym_det", det)
+                name = K.spmvKernel()
+                assert name.startswith(f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows}>"), name
+                y1 = (K * x).getArray().copy()
+                for _ in range(2):
+                    y2 = (K * x).getArray().copy()
+                    for ref in (y0, yh):
+                        assert np.linalg.norm(y2 - ref) <= 1e-14 * np.linalg.norm(ref), (rows, split, det)
+                        assert np.abs(y2 - ref).max() <= 1e-13 * np.abs(ref).max(), (rows, split, det)
+                    if det:
+                        np.testing.assert_array_equal(y2, y1)
     finally:
         set_tuning("spmv_sym_det", 1)
+        set_tuning("spmv_gsym_rows", 16)
+        set_tuning("spmv_gsym_split", 0)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)
