@@ -87,8 +87,8 @@ const char *kle_last_error(void);
  * default: the transposed adds as exact fixed-point sums, y bitwise
  * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
  * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_rows"
- * (read when the storage of an unstructured K is built: rows per group, 16
- * default or 8), "spmv_gsym_split" (read at build: the largest dictionary of
+ * (read when the storage of an unstructured K is built: rows per group, 32
+ * default, 16 or 8), "spmv_gsym_split" (read at build: the largest dictionary of
  * the first of its two launches; 0 auto), "spmv_sym_probe"
  * (timing probes that skip parts of the symmetric SpMV: wrong results on
  * purpose; 0 default; bits in kle_internal.hpp). */

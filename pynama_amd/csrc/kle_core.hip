@@ -489,6 +489,56 @@ int halo_reverse(kle_ctx *ctx, const double *send_hi, int64_t n_send, int hi_ran
     return 0;
 }
 
+// Reverse of a graph-partition halo (symmetric storage: MPISBAIJ's reverse
+// scatter with ADD, the transfer only): each peer of higher rank gets the
+// sums of its ghost group (gsend: the upper ghost groups back to back in peer
+// order, from ext node hi0 on, bs entries per node), each peer of lower rank
+// sends the sums for the owned nodes it ghosts into rbuf (the forward halo's
+// send slices of the lower peers, which lead the send list).  The caller adds
+// rbuf into y through the send index lists.
+int halo_reverse_plan(kle_ctx *ctx, const HaloPlan &P, int64_t hi0, int bs, const double *gsend, double *rbuf,
+                      hipStream_t st)
+{
+    if (ctx->nranks == 1 || P.peers.empty()) return 0;
+    if (!st) st = ctx->stream;
+    const size_t np = P.peers.size();
+    std::vector<int64_t> sc(np, 0), rc(np, 0);
+    int64_t ns = 0, nr = 0;
+    for (size_t k = 0; k < np; ++k) {
+        if (P.peers[k] > ctx->rank) sc[k] = P.recv_cnt[k] * bs;
+        if (P.peers[k] < ctx->rank) rc[k] = P.send_cnt[k] * bs;
+        ns += sc[k];
+        nr += rc[k];
+    }
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(ctx->tic("halo_rev", &ev, st));
+    if (ctx->ipc) {
+        return fail(KLE_ERR_SUP, "the IPC transport has no graph-partition reverse halo");
+    } else if (ctx->comm) {
+        KLE_NCCL(ncclGroupStart());
+        for (size_t k = 0; k < np; ++k) {
+            if (sc[k])
+                KLE_NCCL(ncclSend(gsend + (P.recv_off[k] - hi0) * bs, sc[k], ncclDouble, P.peers[k], ctx->comm, st));
+            if (rc[k]) KLE_NCCL(ncclRecv(rbuf + P.send_off[k] * bs, rc[k], ncclDouble, P.peers[k], ctx->comm, st));
+        }
+        KLE_NCCL(ncclGroupEnd());
+    } else {
+        if (!ctx->hcomm.exchange) return fail(KLE_ERR_COMM, "host transport has no exchange callback (reverse halo)");
+        KLE_TRY(stage_reserve(ctx, ns + nr));
+        double *hs = ctx->h_stage, *hr = hs + ns;
+        // (the upper ghost groups are contiguous in peer order, the lower
+        // peers' send slices lead the send list: both buffers are packed)
+        if (ns) KLE_HIP(hipMemcpyAsync(hs, gsend, sizeof(double) * ns, hipMemcpyDeviceToHost, st));
+        KLE_HIP(hipStreamSynchronize(st));
+        if (ctx->hcomm.exchange((int)np, P.peers.data(), hs, sc.data(), hr, rc.data(), ctx->hcomm.user))
+            return fail(KLE_ERR_COMM, "host exchange callback failed (reverse halo)");
+        if (nr) KLE_HIP(hipMemcpyAsync(rbuf, hr, sizeof(double) * nr, hipMemcpyHostToDevice, st));
+        KLE_HIP(hipStreamSynchronize(st));
+    }
+    KLE_TRY(ctx->toc("halo_rev", &ev, st));
+    return 0;
+}
+
 }  // namespace kle
 
 using namespace kle;

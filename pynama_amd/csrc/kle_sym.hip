@@ -763,7 +763,7 @@ __device__ __forceinline__ int64_t gsym_block(int ch)
 // symmetric layout and measure max |B_ij - B_ji^T| per row over all its
 // off-diagonal blocks; a block whose partner (j, i) is not in the pattern must
 // be zero (it is then dropped from the product with nothing lost).
-__global__ __launch_bounds__(256) void k_gsym_check(int64_t nrows, const int *__restrict__ rowptr,
+__global__ __launch_bounds__(256) void k_gsym_check(int64_t nrows, int64_t glo, const int *__restrict__ rowptr,
                                                     const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr,
                                                     const int *__restrict__ bcol, const double *__restrict__ val,
                                                     const int *__restrict__ sk0, const int64_t *__restrict__ svptr,
@@ -787,16 +787,13 @@ __global__ __launch_bounds__(256) void k_gsym_check(int64_t nrows, const int *__
             b[t] = v[vofs(1, 9, t, k, m, mp)];
             vmax = fmax(vmax, fabs(b[t]));
         }
-        const int64_t j = bcol[r0 + k];
-        if (j == i) continue;
-        if (j < 0 || j >= nrows) {
-            dmax = INFINITY;
-            continue;
-        }
+        const int64_t j = bcol[r0 + k] - glo;  // (owned rows: 0 .. nrows-1)
+        if (j == i || j < 0 || j >= nrows) continue;  // (blocks into ghosts: sym_probe checks them)
         const int s0 = rowptr[j], mpj = rowptr[j + 1] - s0, mj = rowcnt ? rowcnt[j] : mpj;
         int lo = 0, hi = mj - 1, kj = -1;
         while (lo <= hi) {
-            const int mid = (lo + hi) >> 1, cm = bcol[s0 + mid];
+            const int mid = (lo + hi) >> 1;
+            const int64_t cm = bcol[s0 + mid] - glo;
             if (cm == i) {
                 kj = mid;
                 break;
@@ -1025,21 +1022,23 @@ __global__ __launch_bounds__(512) void k_nb_spmv_gsym(
 // (instead of one scattered 24-B read per row and entry), and each row still
 // sums its entries in ascending group order.  With xdot: the workgroup's
 // partial of (y, x) in dpart[blockIdx.x] (k_nb_sym_gather's fixed order).
-__global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, const int *__restrict__ runptr,
+// N > 1: the rows past the owned ones (nrows .. ntot-1) are the upper ghost
+// nodes, whose sums go to gsend (the reverse halo's send buffer).
+__global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, int64_t ntot, const int *__restrict__ runptr,
                                                         const int *__restrict__ rstart,
                                                         const unsigned long long *__restrict__ rmask,
                                                         const double *__restrict__ ws, double *__restrict__ y,
-                                                        const int *__restrict__ istate, const double *__restrict__ xdot,
-                                                        double *__restrict__ dpart)
+                                                        double *__restrict__ gsend, const int *__restrict__ istate,
+                                                        const double *__restrict__ xdot, double *__restrict__ dpart)
 {
     __shared__ double dred[4];
     if (istate && istate[I_REASON] != 0) return;
     const int lane = threadIdx.x & 63;
     const int64_t sl = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t j = sl * 64 + lane;
-    if (sl * 64 >= nrows && !xdot) return;
+    if (sl * 64 >= ntot && !xdot) return;
     double dsum = 0.0;
-    if (sl * 64 < nrows) {
+    if (sl * 64 < ntot) {
         const unsigned long long below = (1ull << lane) - 1ull;
         double s0 = 0.0, s1 = 0.0, s2 = 0.0;
         const int r1 = runptr[sl + 1];
@@ -1060,6 +1059,11 @@ __global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, const int
             y[3 * j + 1] = s1;
             y[3 * j + 2] = s2;
             if (xdot) dsum = s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
+        } else if (j < ntot) {
+            double *o = gsend + 3 * (j - nrows);
+            o[0] = s0;
+            o[1] = s1;
+            o[2] = s2;
         }
     }
     if (!xdot) return;
@@ -1070,138 +1074,180 @@ __global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, const int
     if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
 }
 
+// y[0 .. n) += r: the reverse halo's sums for a slab's lowest nodes
+__global__ void k_axpy_first(int64_t n, const double *__restrict__ r, double *__restrict__ y,
+                             const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) y[t] += r[t];
+}
+
+// y[idx[q]] += the reverse halo's sums rbuf[q] (3 entries per node), one
+// launch per lower peer in ascending rank order (fixed order per row)
+__global__ void k_gsym_unpack(int64_t cnt, const int32_t *__restrict__ idx, const double *__restrict__ rbuf,
+                              double *__restrict__ y, const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 3 * cnt) return;
+    const int64_t q = t / 3;
+    y[3 * (int64_t)idx[q] + (t - 3 * q)] += rbuf[t];
+}
+
 static size_t gsym_lds(int US, int G) { return (size_t)(3 * US + 3 * (US + 64) + 3 * G) * sizeof(double); }
 
-// Build the graph symmetric storage (one rank).  Refuses a matrix that is not
-// symmetric to 1e-12 of its largest entry, whose pattern holds a nonzero
-// block without its partner, or whose group dictionaries exceed the LDS.
+static int any_rank(kle_ctx *c, int64_t flag, bool &any);
+static int sym_probe(kle_mat *A, double vmax_all, bool &bad);
+
+// Build the graph symmetric storage: one rank, or a graph partition (the ext
+// columns [lower ranks' ghosts | owned | higher ranks' ghosts], node ids in
+// rank order, so an owned row's upper triangle holds owned columns from its
+// own on and every upper ghost, never a lower ghost).  Refuses a matrix that
+// is not symmetric to 1e-12 of its largest entry, whose pattern holds a
+// nonzero block without its partner, or whose group dictionaries exceed the
+// LDS.  Collective at N > 1: every rank takes the same decision (any_rank),
+// and one hashed product through both storages checks the blocks between
+// ranks (sym_probe).
 static int gsym_build(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
-    const int64_t n = A->nrows;
+    const int64_t n = A->nrows, glo = A->ghost_lo / 3, nhi = A->ghost_hi / 3;
+    const bool dist = c->nranks > 1;
+    const bool slab = dist && !A->plan && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    const bool graph = dist && A->plan && !A->plan->peers.empty();
+    std::string why;
     if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_bcol && !A->d_rowbox &&
-          A->m_local == A->n_local && A->ghost_lo == 0 && A->ghost_hi == 0 && A->lo_rank < 0 && A->hi_rank < 0 &&
-          (!A->plan || A->plan->peers.empty()) && c->nranks == 1 && n > 0))
-        return fail(KLE_ERR_SUP, "symmetric storage of an unstructured matrix needs a 3x3 node-block matrix on one rank");
-    std::vector<int> rp(n + 1), cnt(n), bcol(std::max<int64_t>(A->nblocks, 1));
-    KLE_HIP(hipStreamSynchronize(c->stream));
-    KLE_HIP(hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
-    if (A->d_rowcnt) KLE_HIP(hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost));
-    else
-        for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
-    KLE_HIP(hipMemcpy(bcol.data(), A->d_bcol, sizeof(int) * bcol.size(), hipMemcpyDeviceToHost));
-    // per row: the diagonal block's position (columns ascending), stored count
-    std::vector<int> k0(n), smu(n);
-    std::vector<int64_t> svp(n + 1), sbp(n + 1);
-    int64_t tot = 0, blocks = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const int *b = bcol.data() + rp[i], *e = b + cnt[i];
-        if (!std::is_sorted(b, e))
-            return fail(KLE_ERR_SUP, "symmetric storage: row %lld's columns are not ascending", (long long)i);
-        const int *d = std::lower_bound(b, e, (int)i);
-        if (d == e || *d != i)
-            return fail(KLE_ERR_SUP, "symmetric storage: row %lld has no diagonal block", (long long)i);
-        k0[i] = (int)(d - b);
-        smu[i] = cnt[i] - k0[i];
-        svp[i] = tot;
-        sbp[i] = blocks;
-        tot += ((int64_t)smu[i] * 9 + 15) & ~int64_t(15);
-        blocks += smu[i];
-    }
-    svp[n] = tot;
-    sbp[n] = blocks;
-    // group dictionaries (threads over groups), then the gather lists
+          A->m_local == A->n_local && n > 0 && A->ghost_lo % 3 == 0 && A->ghost_hi % 3 == 0))
+        why = "symmetric storage of an unstructured matrix needs a 3x3 node-block matrix with owned rows";
+    else if (dist && c->ipc && graph)
+        why = "symmetric storage: the IPC transport has no graph-partition reverse halo";
+    else if (slab && (A->send_lo % 3 || A->send_hi % 3))
+        why = "symmetric storage: slab halo of partial nodes";
     const int G = g_tune.spmv_gsym_rows;
-    const int64_t ng = (n + G - 1) / G;
-    std::vector<int> usz(ng);
-    std::vector<std::vector<int>> dl(ng);
-    std::vector<uint16_t> slid(std::max<int64_t>(blocks, 1));
-    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::atomic<bool> big{false};
-    auto work = [&](int t) {
-        for (int64_t g = t; g < ng; g += nt) {
-            const int64_t r0 = g * G, r1 = std::min(n, r0 + G);
-            std::vector<int> &L = dl[g];
-            for (int64_t r = r0; r < r1; ++r) L.insert(L.end(), bcol.begin() + rp[r] + k0[r], bcol.begin() + rp[r] + cnt[r]);
-            std::sort(L.begin(), L.end());
-            L.erase(std::unique(L.begin(), L.end()), L.end());
-            if ((int64_t)L.size() > GSYM_UCAP) {
-                big = true;
-                continue;
-            }
-            for (int64_t r = r0; r < r1; ++r)
-                for (int k = k0[r]; k < cnt[r]; ++k)
-                    slid[sbp[r] + k - k0[r]] =
-                        (uint16_t)(std::lower_bound(L.begin(), L.end(), bcol[rp[r] + k]) - L.begin());
-            usz[g] = (int)L.size();
+    const int64_t ng = (n + G - 1) / G, ntot = n + nhi, ns = (ntot + 63) / 64;
+    std::vector<int> rp, cnt, bcol, k0, smu, usz, dptr(ng + 1, 0), glist(ng), dict, runptr(ns + 1, 0), rstart;
+    std::vector<int64_t> svp, sbp;
+    std::vector<uint16_t> slid;
+    std::vector<unsigned long long> rmask;
+    int64_t tot = 0, blocks = 0, E = 0, n1 = 0, NR = 0;
+    int US = 0, US1 = 0;
+    auto analyse = [&]() -> std::string {
+        rp.resize(n + 1);
+        cnt.resize(n);
+        bcol.resize(std::max<int64_t>(A->nblocks, 1));
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(rp.data(), A->d_rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToHost) != hipSuccess ||
+            (A->d_rowcnt && hipMemcpy(cnt.data(), A->d_rowcnt, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess) ||
+            hipMemcpy(bcol.data(), A->d_bcol, sizeof(int) * bcol.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return "symmetric storage: pattern copy failed";
+        if (!A->d_rowcnt)
+            for (int64_t i = 0; i < n; ++i) cnt[i] = rp[i + 1] - rp[i];
+        // per row: the diagonal block's position (columns ascending), stored count
+        k0.resize(n);
+        smu.resize(n);
+        svp.resize(n + 1);
+        sbp.resize(n + 1);
+        for (int64_t i = 0; i < n; ++i) {
+            const int *b = bcol.data() + rp[i], *e = b + cnt[i];
+            if (!std::is_sorted(b, e)) return "symmetric storage: row " + std::to_string(i) + "'s columns are not ascending";
+            const int *d = std::lower_bound(b, e, (int)(glo + i));
+            if (d == e || *d != glo + i) return "symmetric storage: row " + std::to_string(i) + " has no diagonal block";
+            if (b[cnt[i] - 1] >= glo + ntot) return "symmetric storage: column beyond the ghost range";
+            k0[i] = (int)(d - b);
+            smu[i] = cnt[i] - k0[i];
+            svp[i] = tot;
+            sbp[i] = blocks;
+            tot += ((int64_t)smu[i] * 9 + 15) & ~int64_t(15);
+            blocks += smu[i];
         }
+        svp[n] = tot;
+        sbp[n] = blocks;
+        // group dictionaries (threads over groups; ext column ids)
+        usz.assign(ng, 0);
+        std::vector<std::vector<int>> dl(ng);
+        slid.assign(std::max<int64_t>(blocks, 1), 0);
+        const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::atomic<bool> big{false};
+        auto work = [&](int t) {
+            for (int64_t g = t; g < ng; g += nt) {
+                const int64_t r0 = g * G, r1 = std::min(n, r0 + G);
+                std::vector<int> &L = dl[g];
+                for (int64_t r = r0; r < r1; ++r)
+                    L.insert(L.end(), bcol.begin() + rp[r] + k0[r], bcol.begin() + rp[r] + cnt[r]);
+                std::sort(L.begin(), L.end());
+                L.erase(std::unique(L.begin(), L.end()), L.end());
+                if ((int64_t)L.size() > GSYM_UCAP) {
+                    big = true;
+                    continue;
+                }
+                for (int64_t r = r0; r < r1; ++r)
+                    for (int k = k0[r]; k < cnt[r]; ++k)
+                        slid[sbp[r] + k - k0[r]] =
+                            (uint16_t)(std::lower_bound(L.begin(), L.end(), bcol[rp[r] + k]) - L.begin());
+                usz[g] = (int)L.size();
+            }
+        };
+        {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+            for (auto &x : th) x.join();
+        }
+        if (big) return "symmetric storage: a row group's columns exceed " + std::to_string(GSYM_UCAP) + " LDS slots";
+        for (int64_t g = 0; g < ng; ++g) {
+            if ((int64_t)dptr[g] + usz[g] > INT_MAX / 3) return "symmetric storage: dictionaries too large";
+            dptr[g + 1] = dptr[g] + usz[g];
+            US = std::max(US, usz[g]);
+            for (int e = 0; e < usz[g] && e < G && g * G + e < n; ++e)
+                if (dl[g][e] != glo + g * G + e)  // (cannot happen: the rows lead)
+                    return "symmetric storage: group " + std::to_string(g) + " does not lead with its rows";
+        }
+        E = dptr[ng];
+        // the launches: groups whose dictionaries fit US4 slots (4 workgroups
+        // per CU), then the rest (US = the largest)
+        int US4 = (int)((GSYM_LDS4 / sizeof(double) - 3 * 64 - 3 * G) / 6);
+        if (g_tune.spmv_gsym_split > 0) US4 = std::min(US4, g_tune.spmv_gsym_split);
+        for (int64_t g = 0; g < ng; ++g)
+            if (US <= US4 || usz[g] <= US4) {
+                glist[n1++] = (int)g;
+                US1 = std::max(US1, usz[g]);
+            }
+        for (int64_t g = 0, k = n1; g < ng; ++g)
+            if (!(US <= US4 || usz[g] <= US4)) glist[k++] = (int)g;
+        // gather runs: per 64-node slice of [owned | upper ghosts], the groups
+        // naming its nodes in ascending order, each as (first entry, mask)
+        dict.assign(std::max<int64_t>(E, 1), 0);
+        std::vector<std::vector<std::pair<int, unsigned long long>>> sruns(ns);
+        for (int64_t g = 0; g < ng; ++g)
+            for (int e = 0; e < usz[g];) {
+                const int sl = (int)((dl[g][e] - glo) >> 6), e0 = e;
+                unsigned long long m = 0;
+                for (; e < usz[g] && ((dl[g][e] - glo) >> 6) == sl; ++e) {
+                    dict[dptr[g] + e] = dl[g][e];
+                    m |= 1ull << ((dl[g][e] - glo) & 63);
+                }
+                sruns[sl].push_back({dptr[g] + e0, m});
+            }
+        for (int64_t sl = 0; sl < ns; ++sl) {
+            if ((int64_t)runptr[sl] + (int64_t)sruns[sl].size() > INT_MAX) return "symmetric storage: gather runs too many";
+            runptr[sl + 1] = runptr[sl] + (int)sruns[sl].size();
+        }
+        NR = runptr[ns];
+        rstart.assign(std::max<int64_t>(NR, 1), 0);
+        rmask.assign(std::max<int64_t>(NR, 1), 0);
+        for (int64_t sl = 0; sl < ns; ++sl)
+            for (size_t k = 0; k < sruns[sl].size(); ++k) {
+                rstart[runptr[sl] + k] = sruns[sl][k].first;
+                rmask[runptr[sl] + k] = sruns[sl][k].second;
+            }
+        return "";
     };
-    {
-        std::vector<std::thread> th;
-        for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
-        for (auto &x : th) x.join();
-    }
-    if (big) return fail(KLE_ERR_SUP, "symmetric storage: a row group's columns exceed %d LDS slots", GSYM_UCAP);
-    std::vector<int> dptr(ng + 1, 0);
-    int US = 0;
-    for (int64_t g = 0; g < ng; ++g) {
-        if ((int64_t)dptr[g] + usz[g] > INT_MAX / 3) return fail(KLE_ERR_SUP, "symmetric storage: dictionaries too large");
-        dptr[g + 1] = dptr[g] + usz[g];
-        US = std::max(US, usz[g]);
-        for (int e = 0; e < usz[g]; ++e) {
-            const int j = dl[g][e];
-            if (e < G && g * G + e < n && j != g * G + e)  // (cannot happen: the rows lead)
-                return fail(KLE_ERR_SUP, "symmetric storage: group %lld does not lead with its rows", (long long)g);
-        }
-    }
-    const int64_t E = dptr[ng];
-    // the launches: groups whose dictionaries fit US1 slots (4 workgroups per
-    // CU), then the rest (US = the largest)
-    int US4 = (int)((GSYM_LDS4 / sizeof(double) - 3 * 64 - 3 * G) / 6);
-    if (g_tune.spmv_gsym_split > 0) US4 = std::min(US4, g_tune.spmv_gsym_split);
-    std::vector<int> glist(ng);
-    int64_t n1 = 0;
-    int US1 = 0;
-    for (int64_t g = 0; g < ng; ++g)
-        if (US <= US4 || usz[g] <= US4) {
-            glist[n1++] = (int)g;
-            US1 = std::max(US1, usz[g]);
-        }
-    for (int64_t g = 0, k = n1; g < ng; ++g)
-        if (!(US <= US4 || usz[g] <= US4)) glist[k++] = (int)g;
-    // gather runs: per 64-row slice, the groups naming its rows in ascending
-    // order, each as (first entry, mask of the slice rows) (k_nb_gsym_gather)
-    const int64_t ns = (n + 63) / 64;
-    std::vector<int> dict(std::max<int64_t>(E, 1)), runptr(ns + 1, 0);
-    std::vector<std::vector<std::pair<int, unsigned long long>>> sruns(ns);
-    for (int64_t g = 0; g < ng; ++g)
-        for (int e = 0; e < usz[g];) {
-            const int j0 = dl[g][e], sl = j0 >> 6;
-            unsigned long long m = 0;
-            const int e0 = e;
-            for (; e < usz[g] && (dl[g][e] >> 6) == sl; ++e) {
-                dict[dptr[g] + e] = dl[g][e];
-                m |= 1ull << (dl[g][e] & 63);
-            }
-            sruns[sl].push_back({dptr[g] + e0, m});
-        }
-    for (int64_t sl = 0; sl < ns; ++sl) {
-        if ((int64_t)runptr[sl] + (int64_t)sruns[sl].size() > INT_MAX)
-            return fail(KLE_ERR_SUP, "symmetric storage: gather runs too many");
-        runptr[sl + 1] = runptr[sl] + (int)sruns[sl].size();
-    }
-    const int64_t NR = runptr[ns];
-    std::vector<int> rstart(std::max<int64_t>(NR, 1));
-    std::vector<unsigned long long> rmask(std::max<int64_t>(NR, 1));
-    for (int64_t sl = 0; sl < ns; ++sl)
-        for (size_t k = 0; k < sruns[sl].size(); ++k) {
-            rstart[runptr[sl] + k] = sruns[sl][k].first;
-            rmask[runptr[sl] + k] = sruns[sl][k].second;
-        }
-    sruns.clear();
-    dl.clear();
-    dl.shrink_to_fit();
+    if (why.empty()) why = analyse();
+    bool any = false;
+    KLE_TRY(any_rank(c, !why.empty(), any));
+    if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
     // device arrays; the value copy and the symmetry check
+    const int64_t nsend = graph ? (int64_t)A->plan->send_idx.size() * 3 : slab ? A->send_lo : 0;
     int *dk0 = nullptr;
     double *rowdiff = nullptr, *rowmax = nullptr;
     const bool nomem =
@@ -1217,16 +1263,25 @@ static int gsym_build(kle_mat *A)
         hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
         hipMalloc(&A->d_sws, sizeof(double) * 3 * std::max<int64_t>(E, 1)) != hipSuccess ||
         hipMalloc(&A->d_stile_e, sizeof(int) * ng) != hipSuccess || hipMalloc(&dk0, sizeof(int) * n) != hipSuccess ||
+        (nhi && hipMalloc(&A->d_sgsend, sizeof(double) * 3 * nhi) != hipSuccess) ||
+        (nsend && hipMalloc(&A->d_sgrecv, sizeof(double) * nsend) != hipSuccess) ||
+        (graph && !A->plan->d_send_idx && !A->plan->send_idx.empty() &&
+         hipMalloc(&A->plan->d_send_idx, sizeof(int32_t) * A->plan->send_idx.size()) != hipSuccess) ||
         hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess;
     (void)hipGetLastError();
-    auto done = [&](int rc) {
-        (void)hipFree(dk0);
-        (void)hipFree(rowdiff);
-        (void)hipFree(rowmax);
+    auto done = [&](int rc) {  // the temporaries go; A's storage too on failure
+        for (void *q : {(void *)dk0, (void *)rowdiff, (void *)rowmax})
+            if (q) (void)hipFree(q);
+        dk0 = nullptr;
+        rowdiff = rowmax = nullptr;
         if (rc) sym_drop(A);
         return rc;
     };
-    if (nomem) return done(fail(KLE_ERR_MEM, "out of device memory for symmetric storage"));
+    {
+        const int rc = any_rank(c, nomem, any);
+        if (rc) return done(rc);
+    }
+    if (any) return done(fail(KLE_ERR_MEM, "out of device memory for symmetric storage"));
     A->sym_graph = 1;
     KLE_HIP(hipMemcpy(A->d_svptr, svp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_srow, smu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
@@ -1239,7 +1294,10 @@ static int gsym_build(kle_mat *A)
     KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(dk0, k0.data(), sizeof(int) * n, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_gsym_check, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, A->d_rowptr,
+    if (graph && !A->plan->send_idx.empty())
+        KLE_HIP(hipMemcpy(A->plan->d_send_idx, A->plan->send_idx.data(), sizeof(int32_t) * A->plan->send_idx.size(),
+                          hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_gsym_check, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, glo, A->d_rowptr,
                        A->d_rowcnt, A->d_vptr, A->d_bcol, A->d_val, dk0, A->d_svptr, A->d_sval, rowdiff, rowmax);
     KLE_HIP(hipGetLastError());
     std::vector<double> hd(n), hm(n);
@@ -1251,7 +1309,19 @@ static int gsym_build(kle_mat *A)
         dmax = std::isnan(hd[i]) ? INFINITY : std::max(dmax, hd[i]);
         vmax = std::max(vmax, hm[i]);
     }
-    if (!(dmax <= 1e-12 * vmax))
+    // the largest entry over all ranks (the tolerances' scale): one-hot sums
+    double vmax_all = vmax;
+    if (dist) {
+        std::vector<int64_t> vb;
+        const int rc = allgather_i64(c, (int64_t)std::ilogb(std::max(vmax, 1e-300)), vb);
+        if (rc) return done(rc);
+        for (int64_t e : vb) vmax_all = std::max(vmax_all, std::ldexp(1.0, (int)e));
+    }
+    {
+        const int rc = any_rank(c, !(dmax <= 1e-12 * vmax_all), any);
+        if (rc) return done(rc);
+    }
+    if (any)
         return done(fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax));
     hipLaunchKernelGGL(k_gsym_bound, dim3((unsigned)ng), dim3(256), 0, c->stream, n, G, A->d_sdptr, A->d_srow, A->d_sbp,
                        A->d_slid, A->d_svptr, A->d_sval, A->d_stile_e);
@@ -1264,21 +1334,35 @@ static int gsym_build(kle_mat *A)
     A->sblocks = blocks;
     A->snvals = tot;
     A->sws_entries = E;
+    if (dist) {
+        bool bad = false;
+        const int rc = sym_probe(A, vmax_all, bad);
+        if (rc) return done(rc);
+        if (bad) return done(fail(KLE_ERR_SUP, "matrix is not symmetric across ranks (product probe)"));
+    }
     if (const char *e = getenv("KLE_TIMING"))
         if (atoi(e))
-            fprintf(stderr, "[kle gsym] rows %lld, stored blocks %lld (of %lld), groups %lld, dictionary entries %lld "
-                            "(%.2f per row, largest group %d; %lld groups within %d slots), gather runs %lld (%.1f per 64 rows)\n",
-                    (long long)n, (long long)blocks, (long long)A->nblocks_real, (long long)ng, (long long)E,
-                    (double)E / n, US, (long long)n1, US1, (long long)NR, (double)NR / ns);
+            fprintf(stderr, "[kle gsym r%d] rows %lld (+%lld upper ghosts), stored blocks %lld (of %lld), groups %lld, "
+                            "dictionary entries %lld (%.2f per row, largest group %d; %lld groups within %d slots), "
+                            "gather runs %lld (%.1f per 64 rows)\n",
+                    c->rank, (long long)n, (long long)nhi, (long long)blocks, (long long)A->nblocks_real, (long long)ng,
+                    (long long)E, (double)E / n, US, (long long)n1, US1, (long long)NR, (double)NR / ns);
     return done(0);
 }
 
 static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
+    hipStream_t st = c->stream;
     const int G = A->sym_reg[3];
-    const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2];
+    const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2], nhi = A->ghost_hi / 3;
+    const bool dist = c->nranks > 1;
     const bool det = g_tune.spmv_sym_det != 0;
+    // N > 1: the ghost x first (the groups of rows that read no ghost could
+    // run beside it; not split yet)
+    if (dist)
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, st, x->plan.get()));
     auto launch = [&](auto kern, int slot, int64_t l0, int64_t nl, int US) {
         if (nl <= 0) return;
         const size_t lds = gsym_lds(US, G);
@@ -1288,9 +1372,9 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
                                       (int)lds);
             lds_set[slot] = lds;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(512), lds, c->stream, n, nl, A->d_sglist + l0, US,
-                           A->d_svptr, A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base,
-                           A->d_sws, A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_probe);
+        hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(512), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
+                           A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
+                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_probe);
     };
     auto launch2 = [&](auto kern, int slot) {
         launch(kern, slot, 0, n1, A->sym_reg[0]);
@@ -1308,8 +1392,29 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     } else {
         return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group", G);
     }
-    hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, n, A->d_sgptr,
-                       A->d_sgidx, A->d_sgmask, A->d_sws, y->d, istate, dpart ? x->d : nullptr, dpart);
+    const int64_t ntot = n + (dist ? nhi : 0);
+    hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st, n, ntot, A->d_sgptr,
+                       A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate, dpart && !dist ? x->d : nullptr,
+                       dpart);
+    KLE_HIP(hipGetLastError());
+    if (!dist) return 0;
+    // the upper ghost nodes' sums back to their owners, added in ascending
+    // rank order of the senders (MPISBAIJ's reverse scatter)
+    if (A->plan && !A->plan->peers.empty()) {
+        const HaloPlan &P = *A->plan;
+        KLE_TRY(halo_reverse_plan(c, P, A->ghost_lo / 3 + n, 3, A->d_sgsend, A->d_sgrecv, st));
+        for (size_t k = 0; k < P.peers.size() && P.peers[k] < c->rank; ++k)
+            if (P.send_cnt[k])
+                hipLaunchKernelGGL(k_gsym_unpack, dim3((unsigned)((3 * P.send_cnt[k] + 255) / 256)), dim3(256), 0, st,
+                                   P.send_cnt[k], P.d_send_idx + P.send_off[k], A->d_sgrecv + 3 * P.send_off[k], y->d,
+                                   istate);
+    } else {
+        const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
+        KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, st));
+        if (nrecv)
+            hipLaunchKernelGGL(k_axpy_first, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, st, nrecv,
+                               A->d_sgrecv, y->d, istate);
+    }
     KLE_HIP(hipGetLastError());
     return 0;
 }
@@ -1412,6 +1517,7 @@ static int sym_probe(kle_mat *A, double vmax_all, bool &bad)
         x->hi_rank = A->hi_rank;
         x->send_lo = A->send_lo;
         x->send_hi = A->send_hi;
+        x->plan = A->plan;
         hipLaunchKernelGGL(k_sym_probe_x, dim3((unsigned)((A->n_local + 255) / 256)), dim3(256), 0, c->stream,
                            A->n_local, A->col_lo, x->d);
         rc = hipGetLastError() == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "probe launch failed");
@@ -1714,7 +1820,7 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 
 int sym_dot_parts(const kle_mat *A)
 {
-    const bool dist = A->ctx->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    const bool dist = A->ctx->nranks > 1 && (A->sym_graph || A->lo_rank >= 0 || A->hi_rank >= 0);
     return dist ? 0 : (int)((A->nrows + 255) / 256);
 }
 

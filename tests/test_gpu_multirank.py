@@ -216,13 +216,13 @@ def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False, transpor
     return res
 
 
-def _run(size, nelem, ngl, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0):
+def _run(size, nelem, ngl, overlap=True, ksp_type="cg", msh=None, partitioner=None, waves=0, sym=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, size, port, nelem, ngl, q, overlap, ksp_type, msh, partitioner,
-                                               waves))
+                                               waves, sym))
              for r in range(size)]
     return _collect(procs, q, size)
 
@@ -269,6 +269,29 @@ def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type
     index-list halos); the same halo / overlap / CG code; solution and SpMV
     vs the oracle's serial system (coordinate numbering).  waves 8: every rank
     runs the column-dictionary SpMV on its split row ranges."""
+    res = _check_umesh(size, partitioner, nel, ksp_type, waves, tmp_path)
+    for r in res:
+        assert not r["sym"], r["rank"]
+
+
+@pytest.mark.parametrize("size,partitioner,nel,ksp_type", [
+    (2, "slab", [2, 3, 9], "cg"), (3, "slab", [2, 3, 9], "pipecg"), (2, "inertial", [3, 3, 4], "cg"),
+    (3, "inertial", [3, 4, 4], "cg"), (4, "inertial", [4, 4, 4], "pipecg"), (8, "inertial", [4, 4, 6], "cg")])
+def test_partitioned_umesh_symmetric_storage(size, partitioner, nel, ksp_type, tmp_path):
+    """Graph symmetric storage on every rank of an unstructured partition
+    (config 5's path): each rank keeps its rows' blocks from the diagonal on
+    (owned columns from the row's own, every higher rank's ghost); the
+    partials of the upper ghost nodes go back to their owners over the
+    reverse halo (slab pair or index-list plan) and are added in ascending
+    sender order.  Same checks as the full storage: the serial oracle's
+    solution and y = K x."""
+    res = _check_umesh(size, partitioner, nel, ksp_type, 0, tmp_path, sym=True)
+    for r in res:
+        assert r["sym"], r["rank"]
+        assert r["kernel"].startswith("k_nb_spmv_gsym<"), r["kernel"]
+
+
+def _check_umesh(size, partitioner, nel, ksp_type, waves, tmp_path, sym=False):
     from oracle import oracle as O
     import pynama_amd as pa
     from pynama_amd.meshgen import perturbed_box, write_gmsh
@@ -276,7 +299,7 @@ def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type
     msh = str(tmp_path / "part.msh")
     write_gmsh(msh, 3, V, Cc, F, T)
     ngl = 3
-    res = _run(size, [0, 0, 0], ngl, msh=msh, partitioner=partitioner, ksp_type=ksp_type, waves=waves)
+    res = _run(size, [0, 0, 0], ngl, msh=msh, partitioner=partitioner, ksp_type=ksp_type, waves=waves, sym=sym)
     for r in res:
         assert r["overlap_equal"], (r["rank"], r["ov_diff"])
     um = O.UMesh(3, ngl, V, Cc, F, T)
@@ -303,3 +326,4 @@ def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type
     for r in res:
         assert abs(r["its"] - its) <= (3 if ksp_type == "cg" else 6)
         assert r["true"] < 1e-10
+    return res

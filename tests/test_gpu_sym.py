@@ -313,7 +313,7 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
     try:
         # groups of 16 / 8 rows, one launch or the groups split over two
         # (the larger dictionaries in a second launch with more LDS)
-        for rows, split in ((16, 0), (8, 0), (16, 40), (8, 20)):
+        for rows, split in ((32, 0), (16, 0), (8, 0), (32, 60), (8, 20)):
             set_tuning("spmv_gsym_rows", rows)
             set_tuning("spmv_gsym_split", split)
             K.setOption(K.Option.SPD, True)
@@ -331,7 +331,7 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
                         np.testing.assert_array_equal(y2, y1)
     finally:
         set_tuning("spmv_sym_det", 1)
-        set_tuning("spmv_gsym_rows", 16)
+        set_tuning("spmv_gsym_rows", 32)
         set_tuning("spmv_gsym_split", 0)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()

@@ -78,7 +78,7 @@ def main():
                 elif k in ("spmv_sym_probe", "spmv_sym_tz"):
                     set_tuning(k, 0)
                 elif k == "spmv_gsym_rows":
-                    set_tuning(k, 16)
+                    set_tuning(k, 32)
             if BUILD_KNOBS & set(v):
                 K.setOption(K.Option.SPD, True)
             res[i].append(ms / c)
