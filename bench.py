@@ -386,6 +386,7 @@ def main():
                    ("chunk" if args.layout == 1 else f"pad{args.pad}") +
                    "-nt-u1" + ("-struct" if K.isStructured() else "") +
                    ("-sym" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_sym") else
+                    "-gsym" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_gsym") else
                     {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(spmv_kernel(K, args.layout, args.ngl), "")))
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
