@@ -398,10 +398,11 @@ class Mat:
 
     def setOption(self, option, flag):
         """MatSetOption: SYMMETRIC / SPD switch the SpMV to symmetric (SBAIJ
-        upper-triangle) storage where libkle supports it (3x3 box-lattice
-        matrices on one rank or on z slabs; kle_mat_set_symmetric, collective)
-        and leave other matrices as they are, as PETSc does for options a
-        format ignores."""
+        upper-triangle) storage where libkle supports it (3x3 node-block
+        matrices: box lattices on one rank or z slabs, unstructured rows on
+        one rank or graph partitions; kle_mat_set_symmetric, collective) and
+        leave other matrices as they are, as PETSc does for options a format
+        ignores."""
         if option not in (self.Option.SYMMETRIC, self.Option.SPD):
             raise Error(56, f"Mat option {option!r} not supported")
         if not flag:
