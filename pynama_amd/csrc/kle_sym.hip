@@ -954,6 +954,34 @@ __global__ __launch_bounds__(512) void k_nb_spmv_gsym(
         }
     }
     unsigned long long *yi = reinterpret_cast<unsigned long long *>(yl);
+    // B x_j into the row's sum, B^T x_i into position l (lanes past the row's
+    // end and the diagonal block add into their dummy slot)
+    auto sum_item = [&](const double *vv, int l, int k, int mu, double xi0, double xi1, double xi2, double &acc0,
+                        double &acc1, double &acc2) {
+        const bool on = k < mu;
+        const double x0 = xs[3 * l], x1 = xs[3 * l + 1], x2 = xs[3 * l + 2];
+        const double s0 = vv[0] * x0 + vv[1] * x1 + vv[2] * x2;
+        const double s1 = vv[3] * x0 + vv[4] * x1 + vv[5] * x2;
+        const double s2 = vv[6] * x0 + vv[7] * x1 + vv[8] * x2;
+        acc0 += on ? s0 : 0.0;
+        acc1 += on ? s1 : 0.0;
+        acc2 += on ? s2 : 0.0;
+        const double t0 = vv[0] * xi0 + vv[3] * xi1 + vv[6] * xi2;
+        const double t1 = vv[1] * xi0 + vv[4] * xi1 + vv[7] * xi2;
+        const double t2 = vv[2] * xi0 + vv[5] * xi1 + vv[8] * xi2;
+        const int rt = on && k > 0 ? l : US + lane;
+        if (probe & 1) {
+            if (!on) yd[lane] = t0 + t1 + t2;  // (probe 1: no transposed adds)
+        } else if (DET) {
+            atomicAdd(&yi[rt], fx_of(t0, S));
+            atomicAdd(&yi[RS + rt], fx_of(t1, S));
+            atomicAdd(&yi[2 * RS + rt], fx_of(t2, S));
+        } else {
+            atomicAdd(&yl[rt], t0);
+            atomicAdd(&yl[RS + rt], t1);
+            atomicAdd(&yl[2 * RS + rt], t2);
+        }
+    };
     for (int rr = 0; rr < RW; ++rr) {
         const int pos = w + 8 * rr;  // the row's position in the group (and its dictionary)
         if (pos >= nr) break;
@@ -974,29 +1002,7 @@ __global__ __launch_bounds__(512) void k_nb_spmv_gsym(
 #pragma unroll
             for (int t = 0; t < 9; ++t) vv[t] = __builtin_nontemporal_load(v + o0 + t * st);
             const int l = __builtin_nontemporal_load(lr + kk);
-            const bool on = k < mu;
-            const double x0 = xs[3 * l], x1 = xs[3 * l + 1], x2 = xs[3 * l + 2];
-            const double s0 = vv[0] * x0 + vv[1] * x1 + vv[2] * x2;
-            const double s1 = vv[3] * x0 + vv[4] * x1 + vv[5] * x2;
-            const double s2 = vv[6] * x0 + vv[7] * x1 + vv[8] * x2;
-            acc0 += on ? s0 : 0.0;
-            acc1 += on ? s1 : 0.0;
-            acc2 += on ? s2 : 0.0;
-            const double t0 = vv[0] * xi0 + vv[3] * xi1 + vv[6] * xi2;
-            const double t1 = vv[1] * xi0 + vv[4] * xi1 + vv[7] * xi2;
-            const double t2 = vv[2] * xi0 + vv[5] * xi1 + vv[8] * xi2;
-            const int rt = on && k > 0 ? l : US + lane;  // (the diagonal block is not transposed)
-            if (probe & 1) {
-                if (!on) yd[lane] = t0 + t1 + t2;  // (probe 1: no transposed adds)
-            } else if (DET) {
-                atomicAdd(&yi[rt], fx_of(t0, S));
-                atomicAdd(&yi[RS + rt], fx_of(t1, S));
-                atomicAdd(&yi[2 * RS + rt], fx_of(t2, S));
-            } else {
-                atomicAdd(&yl[rt], t0);
-                atomicAdd(&yl[RS + rt], t1);
-                atomicAdd(&yl[2 * RS + rt], t2);
-            }
+            sum_item(vv, l, k, mu, xi0, xi1, xi2, acc0, acc1, acc2);
         }
         wsum3_dpp(acc0, acc1, acc2);  // fixed order, one writer per row
         if (lane < 3) yd[3 * pos + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;

@@ -320,7 +320,8 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
             for det in (1, 0):
                 set_tuning("spmv_sym_det", det)
                 name = K.spmvKernel()
-                assert name.startswith(f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows}>"), name
+                want = f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows}>"
+                assert name.startswith(want), name
                 y1 = (K * x).getArray().copy()
                 for _ in range(2):
                     y2 = (K * x).getArray().copy()
