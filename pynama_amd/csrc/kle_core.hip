@@ -632,8 +632,11 @@ int kle_set_tuning(const char *key, int value)
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
     } else if (k == "spmv_gsym_rows") {
-        KLE_ARG(value == 8 || value == 16 || value == 32, "spmv_gsym_rows: 8, 16 or 32");
+        KLE_ARG(value == 8 || value == 16 || value == 32 || value == 64, "spmv_gsym_rows: 8, 16, 32 or 64");
         g_tune.spmv_gsym_rows = value;
+    } else if (k == "spmv_gsym_waves") {
+        KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_gsym_waves: 0, 8 or 16");
+        g_tune.spmv_gsym_waves = value;
     } else if (k == "spmv_gsym_split") {
         KLE_ARG(value >= 0, "spmv_gsym_split: >= 0");
         g_tune.spmv_gsym_split = value;
@@ -676,6 +679,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
     else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
+    else if (k == "spmv_gsym_waves") *value = g_tune.spmv_gsym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
     else return fail(KLE_ERR_ARG, "unknown tuning key '%s'", key);
     return 0;

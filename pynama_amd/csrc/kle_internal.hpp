@@ -342,7 +342,8 @@ struct Tuning {
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
     int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 2 row sums, 4 LDS x reads, 8 partial stores, 16 block -> region arithmetic, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
-    int spmv_gsym_rows = 32;  // unstructured symmetric storage: rows per group (8, 16 or 32; read at build)
+    int spmv_gsym_rows = 64;  // unstructured symmetric storage: rows per group (8, 16, 32 or 64; read at build)
+    int spmv_gsym_waves = 0;  // its waves per workgroup (0 auto: 16 for 64-row groups, else 8; 8 or 16; read at build)
     int spmv_gsym_split = 0;  // unstructured symmetric storage: dictionary slots of the first launch (0 auto: 4 workgroups per CU; tests)
     int spmv_dict = 1;  // unstructured 3x3 SpMV: x staged in LDS through the row groups' column dictionaries; 0 off
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)

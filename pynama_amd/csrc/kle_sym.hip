@@ -742,7 +742,8 @@ void sym_drop(kle_mat *A)
 // transposed adds are exact fixed-point sums as in the box kernel (scale per
 // group from k_gsym_bound), so y is bitwise reproducible.
 constexpr int GSYM_UCAP = 2600;  // dictionary entries per group (LDS: 48 B each)
-constexpr int GSYM_LDS4 = 40960;  // LDS per workgroup while 4 of 8 waves fit a CU
+constexpr int GSYM_CU_WAVES = 32;
+constexpr size_t LDS_PER_CU_G = 163840;  // the first launch's LDS budget: this many waves per CU
 constexpr int GSYM_FILL = 2;  // x-fill entries per thread and batch (3 x 196 entries per group on average)
 
 // kle_mat.hip xcd_block: runs of ch consecutive groups per XCD
@@ -882,14 +883,14 @@ __global__ __launch_bounds__(256) void k_gsym_bound(int64_t nrows, int G, const 
     }
 }
 
-// y = A x, pass 1: one workgroup of 8 waves per group of G rows, wave w
-// takes rows w, w + 8, ... (G / 8 rows, one after the other).  The launch
+// y = A x, pass 1: one workgroup of WV waves per group of G rows, wave w
+// takes rows w, w + WV, ... (G / WV rows, one after the other).  The launch
 // runs the groups of glist[] (groups whose dictionaries fit its US slots).
 // LDS: x of the dictionary [U][3] | transposed partials [3][US + 64] (DET:
 // int64; 64 dummy slots per component take the adds of masked lanes) |
 // direct row sums [G][3].
-template <bool DET, int G>
-__global__ __launch_bounds__(512) void k_nb_spmv_gsym(
+template <bool DET, int G, int WV>
+__global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     int64_t nrows, int64_t nlist, const int *__restrict__ glist, int US, const int64_t *__restrict__ svptr,
     const int *__restrict__ smu, const int64_t *__restrict__ sbp, const uint16_t *__restrict__ slid,
     const int *__restrict__ dptr, const int *__restrict__ dict, const double *__restrict__ sval,
@@ -898,7 +899,7 @@ __global__ __launch_bounds__(512) void k_nb_spmv_gsym(
 {
     extern __shared__ double lds[];
     if (istate && istate[I_REASON] != 0) return;
-    constexpr int NT = 512, RW = G / 8;
+    constexpr int NT = 64 * WV, RW = G / WV;
     const int64_t blk = gsym_block(xcd_chunk);
     if (blk >= nlist) return;  // whole workgroup
     const int64_t g = glist[blk];
@@ -983,7 +984,7 @@ __global__ __launch_bounds__(512) void k_nb_spmv_gsym(
         }
     };
     for (int rr = 0; rr < RW; ++rr) {
-        const int pos = w + 8 * rr;  // the row's position in the group (and its dictionary)
+        const int pos = w + WV * rr;  // the row's position in the group (and its dictionary)
         if (pos >= nr) break;
         const int64_t i = g * G + pos;
         const int mu = smu[i], q16 = mu & ~15;
@@ -1131,6 +1132,9 @@ static int gsym_build(kle_mat *A)
     else if (slab && (A->send_lo % 3 || A->send_hi % 3))
         why = "symmetric storage: slab halo of partial nodes";
     const int G = g_tune.spmv_gsym_rows;
+    const int WV = g_tune.spmv_gsym_waves ? g_tune.spmv_gsym_waves : G >= 64 ? 16 : 8;
+    if (why.empty() && !(WV == 8 || (WV == 16 && G >= 32)))  // (the kernels instantiated in gsym_spmv)
+        why = "symmetric storage: " + std::to_string(G) + "-row groups on " + std::to_string(WV) + " waves";
     const int64_t ng = (n + G - 1) / G, ntot = n + nhi, ns = (ntot + 63) / 64;
     std::vector<int> rp, cnt, bcol, k0, smu, usz, dptr(ng + 1, 0), glist(ng), dict, runptr(ns + 1, 0), rstart;
     std::vector<int64_t> svp, sbp;
@@ -1211,7 +1215,8 @@ static int gsym_build(kle_mat *A)
         E = dptr[ng];
         // the launches: groups whose dictionaries fit US4 slots (4 workgroups
         // per CU), then the rest (US = the largest)
-        int US4 = (int)((GSYM_LDS4 / sizeof(double) - 3 * 64 - 3 * G) / 6);
+        const int lds1 = (int)(LDS_PER_CU_G * WV / GSYM_CU_WAVES);  // 4 workgroups of 8 waves or 2 of 16 per CU
+        int US4 = (int)((lds1 / sizeof(double) - 3 * 64 - 3 * G) / 6);
         if (g_tune.spmv_gsym_split > 0) US4 = std::min(US4, g_tune.spmv_gsym_split);
         for (int64_t g = 0; g < ng; ++g)
             if (US <= US4 || usz[g] <= US4) {
@@ -1337,6 +1342,7 @@ static int gsym_build(kle_mat *A)
     A->sym_reg[1] = US;
     A->sym_reg[2] = (int)n1;
     A->sym_reg[3] = G;
+    A->sym_reg[4] = WV;
     A->sblocks = blocks;
     A->snvals = tot;
     A->sws_entries = E;
@@ -1360,7 +1366,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
-    const int G = A->sym_reg[3];
+    const int G = A->sym_reg[3], WV = A->sym_reg[4];
     const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2], nhi = A->ghost_hi / 3;
     const bool dist = c->nranks > 1;
     const bool det = g_tune.spmv_sym_det != 0;
@@ -1372,13 +1378,13 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     auto launch = [&](auto kern, int slot, int64_t l0, int64_t nl, int US) {
         if (nl <= 0) return;
         const size_t lds = gsym_lds(US, G);
-        static size_t lds_set[12] = {};  // dynamic LDS above 64 KB must be declared per kernel
+        static size_t lds_set[24] = {};  // dynamic LDS above 64 KB must be declared per kernel
         if (lds > lds_set[slot]) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
             lds_set[slot] = lds;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(512), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
+        hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(64 * WV), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
                            A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
                            A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_probe);
     };
@@ -1386,17 +1392,15 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         launch(kern, slot, 0, n1, A->sym_reg[0]);
         launch(kern, slot + 1, n1, ng - n1, A->sym_reg[1]);
     };
-    if (G == 8) {
-        if (det) launch2(k_nb_spmv_gsym<true, 8>, 0);
-        else launch2(k_nb_spmv_gsym<false, 8>, 2);
-    } else if (G == 16) {
-        if (det) launch2(k_nb_spmv_gsym<true, 16>, 4);
-        else launch2(k_nb_spmv_gsym<false, 16>, 6);
-    } else if (G == 32) {
-        if (det) launch2(k_nb_spmv_gsym<true, 32>, 8);
-        else launch2(k_nb_spmv_gsym<false, 32>, 10);
-    } else {
-        return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group", G);
+#define GSYM_CASE(GG, WW, SLOT)                                            \
+    if (G == GG && WV == WW) {                                             \
+        if (det) launch2(k_nb_spmv_gsym<true, GG, WW>, SLOT);              \
+        else launch2(k_nb_spmv_gsym<false, GG, WW>, SLOT + 2);             \
+    } else
+    GSYM_CASE(8, 8, 0) GSYM_CASE(16, 8, 4) GSYM_CASE(32, 8, 8) GSYM_CASE(32, 16, 12) GSYM_CASE(64, 8, 16)
+    GSYM_CASE(64, 16, 20) {
+#undef GSYM_CASE
+        return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group on %d waves", G, WV);
     }
     const int64_t ntot = n + (dist ? nhi : 0);
     hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st, n, ntot, A->d_sgptr,
@@ -1894,7 +1898,7 @@ std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
-               std::to_string(A->sym_reg[3]) + ">+k_nb_gsym_gather";
+               std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
            (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(16 / A->sym_TZ) + "," +
            std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(16 / A->sym_TZ) + "," +

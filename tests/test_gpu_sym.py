@@ -313,14 +313,16 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
     try:
         # groups of 16 / 8 rows, one launch or the groups split over two
         # (the larger dictionaries in a second launch with more LDS)
-        for rows, split in ((32, 0), (16, 0), (8, 0), (32, 60), (8, 20)):
+        for rows, waves, split in ((64, 0, 0), (64, 8, 0), (32, 16, 0), (32, 8, 0), (16, 0, 0), (8, 0, 0),
+                                   (64, 0, 120), (32, 8, 60), (8, 0, 20)):
             set_tuning("spmv_gsym_rows", rows)
+            set_tuning("spmv_gsym_waves", waves)
             set_tuning("spmv_gsym_split", split)
             K.setOption(K.Option.SPD, True)
             for det in (1, 0):
                 set_tuning("spmv_sym_det", det)
                 name = K.spmvKernel()
-                want = f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows}>"
+                want = f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows},{waves or (16 if rows == 64 else 8)}>"
                 assert name.startswith(want), name
                 y1 = (K * x).getArray().copy()
                 for _ in range(2):
@@ -332,7 +334,8 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
                         np.testing.assert_array_equal(y2, y1)
     finally:
         set_tuning("spmv_sym_det", 1)
-        set_tuning("spmv_gsym_rows", 32)
+        set_tuning("spmv_gsym_rows", 64)
+        set_tuning("spmv_gsym_waves", 0)
         set_tuning("spmv_gsym_split", 0)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()

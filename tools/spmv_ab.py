@@ -11,7 +11,7 @@ import os
 import statistics
 import sys
 
-BUILD_KNOBS = {"spmv_sym_tz", "spmv_gsym_rows"}  # read when the symmetric storage is built
+BUILD_KNOBS = {"spmv_sym_tz", "spmv_gsym_rows", "spmv_gsym_waves"}  # read when the symmetric storage is built
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -78,7 +78,9 @@ def main():
                 elif k in ("spmv_sym_probe", "spmv_sym_tz"):
                     set_tuning(k, 0)
                 elif k == "spmv_gsym_rows":
-                    set_tuning(k, 32)
+                    set_tuning(k, 64)
+                elif k == "spmv_gsym_waves":
+                    set_tuning(k, 0)
             if BUILD_KNOBS & set(v):
                 K.setOption(K.Option.SPD, True)
             res[i].append(ms / c)
