@@ -1010,12 +1010,15 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     }
     __syncthreads();
     // one partial per dictionary entry, [entry][3] (coalesced)
-    double *dst = ws + (int64_t)d0 * 3;
+    double *dst = ws + ((probe & 64) ? (g & 7) * 3 * 2048 : (int64_t)d0 * 3);  // (probe 64: into 8 slabs)
     for (int t = (probe & 8) ? 3 * U : threadIdx.x; t < 3 * U; t += NT) {  // (probe 8: no partial stores)
         const int e = t / 3, c = t - 3 * e;
         double s = DET ? fx_to_d(yi[c * RS + e]) * invS : yl[c * RS + e];
         if (e < G) s += yd[t];
-        dst[t] = s;
+        if (probe & 32)
+            __builtin_nontemporal_store(s, dst + t);  // (probe 32: nontemporal partial stores)
+        else
+            dst[t] = s;
     }
 }
 
