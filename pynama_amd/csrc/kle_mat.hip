@@ -326,14 +326,18 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
 // (interior rows, then ghost-dependent rows) reuses the same dictionaries.  A
 // group whose dictionary exceeds DICT_CAP nodes reads x through it from
 // global memory.  Same products in the same order as k_nb_spmv: bitwise
-// identical.
+// identical.  xlo / xhi: the ext node range the fill may read -- the interior
+// launch of an overlapped N > 1 SpMV passes the owned range, so no workgroup
+// reads a ghost x entry while the comm stream is receiving it (the group's
+// masked rows outside the range would not have used it; those slots read 0).
 constexpr int DICT_GROUP = 8;
 constexpr int DICT_CAP = 16 * 9 * 9;
 __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     RowMap rm, int64_t ga0, int64_t nga, int64_t gb0, int64_t ngb, const int *__restrict__ rowptr,
     const int *__restrict__ rowcnt, const int64_t *__restrict__ vptr, const uint16_t *__restrict__ lid,
     const int *__restrict__ dptr, const int *__restrict__ dict, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y, const int *__restrict__ istate, int xcd_chunk)
+    const double *__restrict__ x, double *__restrict__ y, const int *__restrict__ istate, int xcd_chunk, int64_t xlo,
+    int64_t xhi)
 {
     constexpr int R = 3, C = 3, RC = 9;
     extern __shared__ double xs[];
@@ -351,7 +355,8 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     if (lds_x)
         for (int t = threadIdx.x; t < 3 * U; t += 64 * DICT_GROUP) {
             const int e = t / 3;
-            xs[t] = x[(int64_t)dict[d0 + e] * 3 + (t - 3 * e)];
+            const int64_t node = dict[d0 + e];
+            xs[t] = node >= xlo && node < xhi ? x[node * 3 + (t - 3 * e)] : 0.0;
         }
     __syncthreads();
     if (!live) return;
@@ -668,10 +673,13 @@ static void launch_nb_lay(const kle_mat *A, RowMap rm, int wv, const int *rbox, 
         int64_t ga0, nga, gb0, ngb;
         groups(rm.a0, rm.na, ga0, nga);
         groups(rm.b0, rm.nb, gb0, ngb);
+        // rows [int_lo, int_hi) read no ghost column: their launch reads owned x only
+        const bool own_only = rm.nb == 0 && rm.a0 >= A->int_lo && rm.a0 + rm.na <= A->int_hi;
+        const int64_t xlo = own_only ? A->ghost_lo / C : 0, xhi = own_only ? xlo + A->n_local / C : INT64_MAX;
         hipLaunchKernelGGL(k_nb_spmv_dict, dim3((unsigned)(nga + ngb)), dim3(64 * DICT_GROUP),
                            lds + DICT_CAP * 3 * sizeof(double), st, rm, ga0, nga, gb0, ngb, A->d_rowptr, A->d_rowcnt,
                            A->d_vptr, A->d_lid, A->d_dptr, A->d_dict, A->d_val, x->base, y->d, istate,
-                           g_tune.spmv_xcd_chunk);
+                           g_tune.spmv_xcd_chunk, xlo, xhi);
     } else if (R == 3 && C == 3 && LAY == 1 && wv == 8)
         hipLaunchKernelGGL((k_nb_spmv<R, C, LAY, STRUCT, 8>), dim3(grid_for(nr, 8, 1 << 30)), dim3(512), lds, st, rm,
                            A->d_rowptr, A->d_rowcnt, rbox, (int)A->box_lx, (int)A->box_lxy, A->d_vptr, A->d_bcol,
