@@ -83,8 +83,7 @@ const char *kle_last_error(void);
  * "spmv_sym_min_rows" (node rows per rank from which kle_assemble_kle gives
  * K symmetric storage; default 64000), "spmv_sym_tz" (read when the storage
  * is built: 0 auto = 8 x 4 x 4-row tiles where two 8-wave workgroups fit a
- * CU, 2 = 8 x 8 x 2), "spmv_sym_ty" (read at build, with 4-plane tiles: 4
- * = 8 x 4 x 4 rows, 8 = 8 x 8 x 4 rows, 32 per wave), "spmv_sym_det" (1
+ * CU, 2 = 8 x 8 x 2), "spmv_sym_det" (1
  * default: the transposed adds as exact fixed-point sums, y bitwise
  * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
  * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_rows"

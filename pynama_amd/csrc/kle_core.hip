@@ -628,9 +628,6 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
-    } else if (k == "spmv_sym_ty") {
-        KLE_ARG(value == 4 || value == 8, "spmv_sym_ty: 4 or 8");
-        g_tune.spmv_sym_ty = value;
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
@@ -679,7 +676,6 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
-    else if (k == "spmv_sym_ty") *value = g_tune.spmv_sym_ty;
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
     else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;

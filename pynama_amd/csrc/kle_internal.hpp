@@ -244,7 +244,7 @@ struct kle_mat {
     int *d_srow = nullptr;     // per row: offset in its box and box extents, 4 bits each (the SpMV's row set-up)
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
-    int sym_P = 0, sym_TZ = 2, sym_TY = 8;
+    int sym_P = 0, sym_TZ = 2;
     int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
     // graph (unstructured) symmetric storage, one rank (kle_sym.hip gsym_build):
     // d_srow = stored blocks per row, d_stile_e = per-group scale exponents,
@@ -341,7 +341,6 @@ struct Tuning {
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
-    int spmv_sym_ty = 4;      // with 4-plane tiles (read at build): 4 (8 x 4 x 4 rows) or 8 (8 x 8 x 4, 32 rows per wave)
     int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 2 row sums, 4 LDS x reads, 8 partial stores, 16 block -> region arithmetic, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
     int spmv_gsym_rows = 64;  // unstructured symmetric storage: rows per group (8, 16, 32 or 64; read at build)
     int spmv_gsym_waves = 0;  // its waves per workgroup (0 auto: 16 for 64-row groups, else 8; 8 or 16; read at build)

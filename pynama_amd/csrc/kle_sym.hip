@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     // component take the adds of masked lanes) | direct row sums [3][TR]
     extern __shared__ double lds[];
     if (istate && istate[I_REASON] != 0) return;
-    static_assert(TY * TZ == 16 || TY * TZ == 32, "tiles of 128 or 256 rows");
+    static_assert(TY * TZ == 16, "tiles of 128 rows");
     constexpr int TR = SYM_TX * TY * TZ, NT = 64 * WV;
     constexpr int NQ = SYM_TX * TY / WV;  // row slots per wave and plane
     constexpr int NS = NQ * TZ;               // row slots per wave
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256) void k_sym_bound(SymGeo g, const int *__restri
                                                    const int64_t *__restrict__ svptr,
                                                    const double *__restrict__ sval, int *__restrict__ tile_e)
 {
-    constexpr int TRM = 256;  // rows of a tile (at most)
+    constexpr int TRM = 128;  // rows of a tile
     const int TR = SYM_TX * g.TY * g.TZ;
     __shared__ int sb[TRM], sd[TRM];
     __shared__ int64_t so[TRM];
@@ -1438,7 +1438,7 @@ static SymGeo sym_geo(const kle_mat *A)
     const int P = A->sym_P;
     g.TX = SYM_TX;
     g.TZ = A->sym_TZ;
-    g.TY = A->sym_TY;
+    g.TY = 16 / g.TZ;
     g.Lx = (int)A->row_lat[0];
     g.Ly = (int)A->row_lat[1];
     g.Lz = (int)A->row_lat[2];
@@ -1470,7 +1470,7 @@ static SymRegion sym_region(const kle_mat *A)
 static size_t sym_xl_lds(const SymRegion &r)
 {
     const size_t RN = (size_t)r.RX * r.RY * r.RZ;
-    return (6 * RN + 3 * 64 + 3 * 256) * sizeof(double);
+    return (6 * RN + 3 * 64 + 3 * 128) * sizeof(double);
 }
 constexpr size_t LDS_PER_CU = 163840;
 
@@ -1589,10 +1589,9 @@ int sym_build(kle_mat *A)
     std::vector<int> srow;  // per row: x-bx, y-by, z-bz, bnx, bny, bnz (4 bits each)
     int P = 0;
     // reach of the rows' upper triangles relative to their tile's origin, per
-    // tile shape (0: 8 x 4 x 4, 1: 8 x 8 x 2, 2: 8 x 8 x 4): x / y low, x / y / z high
-    const int shape_ty[3] = {4, 8, 8}, shape_tz[3] = {4, 2, 4};
-    int64_t rlo[3][2] = {{0, 0}, {0, 0}, {0, 0}},
-            rhi[3][3] = {{SYM_TX - 1, 3, 3}, {SYM_TX - 1, 7, 1}, {SYM_TX - 1, 7, 3}};
+    // tile shape (0: 8 x 4 x 4, 1: 8 x 8 x 2): x / y low, x / y / z high
+    const int shape_ty[2] = {4, 8}, shape_tz[2] = {4, 2};
+    int64_t rlo[2][2] = {{0, 0}, {0, 0}}, rhi[2][3] = {{SYM_TX - 1, 3, 3}, {SYM_TX - 1, 7, 1}};
     int64_t tot = 0, blocks = 0, all = 0, up_ghost = 0, lo_ghost = 0;
     if (why.empty()) {
         rb.resize(2 * n);
@@ -1629,7 +1628,7 @@ int sym_build(kle_mat *A)
                 // whole box, the row's own plane the lines from its own on
                 const int64_t uz1 = bz + bnz - 1, uy1 = by + bny - 1, ux1 = bx + bnx - 1;
                 const int64_t uy0 = uz1 > z ? by : y, ux0 = uz1 > z || uy1 > y ? bx : x;
-                for (int s = 0; s < 3; ++s) {
+                for (int s = 0; s < 2; ++s) {
                     const int64_t x0 = x / SYM_TX * SYM_TX, y0 = y / shape_ty[s] * shape_ty[s];
                     const int64_t z0 = (z - zo) / shape_tz[s] * shape_tz[s] + zo;
                     rlo[s][0] = std::min(rlo[s][0], ux0 - x0);
@@ -1657,8 +1656,8 @@ int sym_build(kle_mat *A)
             why = "symmetric storage: the block pattern is not symmetric (" + std::to_string(all) + " blocks, " +
                   std::to_string(blocks) + " upper)";
     }
-    SymRegion reg[3];
-    for (int s = 0; s < 3; ++s)
+    SymRegion reg[2];
+    for (int s = 0; s < 2; ++s)
         reg[s] = {(int)-rlo[s][0], (int)(rhi[s][0] - rlo[s][0] + 1), (int)-rlo[s][1], (int)(rhi[s][1] - rlo[s][1] + 1),
                   (int)(rhi[s][2] + 1)};
     if (why.empty() && sym_xl_lds(reg[1]) > LDS_PER_CU)
@@ -1669,13 +1668,9 @@ int sym_build(kle_mat *A)
     // 1536-node region, but a 4-plane tile spans a whole p = 4 element layer,
     // so every tile holds the same mix of row lengths (rows on element-
     // boundary planes carry 4 planes of upper blocks, the next ones 3, 2, 1)
-    // (spmv_sym_ty 8: 8 x 8 x 4 tiles of 256 rows, 32 per wave, where two
-    // workgroups still fit a CU -- half the tiles, fewer partials per row)
     const int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(reg[0]) <= LDS_PER_CU &&
                            sym_fill_fits(reg[0], 8) ? 4 : 2;
-    const int TY = TZ == 4 && g_tune.spmv_sym_ty == 8 && 2 * sym_xl_lds(reg[2]) <= LDS_PER_CU &&
-                           sym_fill_fits(reg[2], 8) ? 8 : 16 / TZ;
-    const SymRegion &rg = reg[TZ == 4 ? (TY == 8 ? 2 : 0) : 1];
+    const SymRegion &rg = reg[TZ == 4 ? 0 : 1];
     bool any = false;
     KLE_TRY(any_rank(c, !why.empty(), any));
     if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
@@ -1737,7 +1732,6 @@ int sym_build(kle_mat *A)
     }
     A->sym_P = P;
     A->sym_TZ = TZ;
-    A->sym_TY = TY;
     A->sym_reg[0] = rg.PX;
     A->sym_reg[1] = rg.RX;
     A->sym_reg[2] = rg.PY;
@@ -1790,7 +1784,7 @@ static int sym_waves(const kle_mat *A)
     return 2 * sym_xl_lds(r) <= LDS_PER_CU && sym_fill_fits(r, 8) ? 8 : 16;
 }
 
-template <int WV, bool DET, int TZ, int TY = 16 / TZ>
+template <int WV, bool DET, int TZ>
 static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,
                           const int *istate, hipStream_t st)
 {
@@ -1798,11 +1792,11 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
     const size_t lds = sym_xl_lds(sym_region(A));
     static size_t lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
     if (lds > lds_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, TY, TZ>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_set = lds;
     }
-    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, TY, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
+    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
                        g_tune.spmv_sym_probe, (int)t0);
 }
@@ -1811,10 +1805,7 @@ static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x
                              const int *istate, hipStream_t st)
 {
     const bool det = g_tune.spmv_sym_det != 0;
-    if (g.TZ == 4 && g.TY == 8) {
-        if (det) launch_sym_xl<8, true, 4, 8>(A, g, x, t0, t1, istate, st);
-        else launch_sym_xl<8, false, 4, 8>(A, g, x, t0, t1, istate, st);
-    } else if (g.TZ == 4) {
+    if (g.TZ == 4) {
         if (det) launch_sym_xl<8, true, 4>(A, g, x, t0, t1, istate, st);
         else launch_sym_xl<8, false, 4>(A, g, x, t0, t1, istate, st);
     } else if (sym_waves(A) == 16) {
@@ -1832,10 +1823,7 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 {
     if (j1 <= j0) return;
     const dim3 grid((unsigned)((j1 - j0 + 255) / 256));
-    if (g.TZ == 4 && g.TY == 8)
-        hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 8, 4>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
-                           A->d_sgrecv, nrecv, j0, j1, istate, xdot, dpart);
-    else if (g.TZ == 4)
+    if (g.TZ == 4)
         hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 4, 4>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
                            A->d_sgrecv, nrecv, j0, j1, istate, xdot, dpart);
     else
@@ -1915,8 +1903,8 @@ std::string sym_kernel_name(const kle_mat *A)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
                std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
-           (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(A->sym_TY) + "," +
-           std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(A->sym_TY) + "," +
+           (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(16 / A->sym_TZ) + "," +
+           std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(16 / A->sym_TZ) + "," +
            std::to_string(A->sym_TZ) + ">";
 }
 

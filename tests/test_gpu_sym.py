@@ -80,18 +80,9 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
                     np.testing.assert_array_equal(y2, y1)
             for k, v in DEFAULTS.items():
                 set_tuning(k, v)
-        # 8 x 8 x 4 tiles (256 rows, 32 per wave; read at build)
-        set_tuning("spmv_sym_ty", 8)
-        K.setOption(K.Option.SPD, True)
-        y1 = (K * x).getArray().copy()
-        for ref in (y0, yh):
-            assert np.linalg.norm(y1 - ref) <= 1e-14 * np.linalg.norm(ref), K.spmvKernel()
-            assert np.abs(y1 - ref).max() <= 1e-13 * np.abs(ref).max(), K.spmvKernel()
-        np.testing.assert_array_equal((K * x).getArray(), y1)
     finally:
         for k, v in DEFAULTS.items():
             set_tuning(k, v)
-        set_tuning("spmv_sym_ty", 4)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)

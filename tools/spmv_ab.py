@@ -11,7 +11,7 @@ import os
 import statistics
 import sys
 
-BUILD_KNOBS = {"spmv_sym_tz", "spmv_sym_ty", "spmv_gsym_rows", "spmv_gsym_waves"}  # read when the symmetric storage is built
+BUILD_KNOBS = {"spmv_sym_tz", "spmv_gsym_rows", "spmv_gsym_waves"}  # read when the symmetric storage is built
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -77,8 +77,6 @@ def main():
                     set_tuning(k, DEFAULTS[k])
                 elif k in ("spmv_sym_probe", "spmv_sym_tz"):
                     set_tuning(k, 0)
-                elif k == "spmv_sym_ty":
-                    set_tuning(k, 4)
                 elif k == "spmv_gsym_rows":
                     set_tuning(k, 64)
                 elif k == "spmv_gsym_waves":
