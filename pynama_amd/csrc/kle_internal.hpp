@@ -254,6 +254,7 @@ struct kle_mat {
     uint16_t *d_slid = nullptr;   // per stored block: its column's position in the group dictionary
     int *d_sdptr = nullptr, *d_sdict = nullptr;  // per group of G rows: sorted distinct stored columns
     int *d_sglist = nullptr;  // group order of the launches: sym_reg[2] groups within sym_reg[0] slots, then the rest
+    int64_t gsym_inner[2] = {0, 0};  // groups leading each launch's list that read no ghost column
     // gather runs (k_nb_gsym_gather): per 64-row slice s, runs [d_sgptr[s], d_sgptr[s+1]) in ascending
     // group order, each the first dictionary entry (d_sgidx) naming a slice row and the mask of the rows it names
     int *d_sgptr = nullptr, *d_sgidx = nullptr;

@@ -620,9 +620,10 @@ int nb_build_dict(kle_mat *A)
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x)
 {
     // (the symmetric SpMV's two halos run on the comm stream whatever the
-    // slab's interior: sym_spmv; the graph symmetric SpMV runs its halos on
-    // the compute stream: gsym_spmv)
-    if (A->kind == 0 && A->d_sval && g_tune.spmv_sym && A->sym_graph) return false;
+    // slab's interior: sym_spmv; the graph symmetric SpMV's with overlap on:
+    // gsym_spmv)
+    if (A->kind == 0 && A->d_sval && g_tune.spmv_sym && A->sym_graph)
+        return A->ctx->nranks > 1 && A->halo_overlap != 0;
     return A->kind == 0 && A->ctx->nranks > 1 && A->halo_overlap &&
            (A->int_lo < A->int_hi || (A->d_sval && g_tune.spmv_sym)) &&
            (x->lo_rank >= 0 || x->hi_rank >= 0 || (x->plan && !x->plan->peers.empty()));

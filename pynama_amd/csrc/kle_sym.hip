@@ -1143,7 +1143,7 @@ static int gsym_build(kle_mat *A)
     std::vector<int64_t> svp, sbp;
     std::vector<uint16_t> slid;
     std::vector<unsigned long long> rmask;
-    int64_t tot = 0, blocks = 0, E = 0, n1 = 0, NR = 0;
+    int64_t tot = 0, blocks = 0, E = 0, n1 = 0, n2 = 0, NR = 0, ninner[2] = {0, 0};
     int US = 0, US1 = 0;
     auto analyse = [&]() -> std::string {
         rp.resize(n + 1);
@@ -1221,13 +1221,24 @@ static int gsym_build(kle_mat *A)
         const int lds1 = (int)(LDS_PER_CU_G * WV / GSYM_CU_WAVES);  // 4 workgroups of 8 waves or 2 of 16 per CU
         int US4 = (int)((lds1 / sizeof(double) - 3 * 64 - 3 * G) / 6);
         if (g_tune.spmv_gsym_split > 0) US4 = std::min(US4, g_tune.spmv_gsym_split);
-        for (int64_t g = 0; g < ng; ++g)
-            if (US <= US4 || usz[g] <= US4) {
-                glist[n1++] = (int)g;
-                US1 = std::max(US1, usz[g]);
+        // inside each launch, the groups that read no ghost column first
+        // (N > 1: they run while the halo is in flight)
+        auto tier1 = [&](int64_t g) { return US <= US4 || usz[g] <= US4; };
+        auto inner = [&](int64_t g) { return dl[g].back() < glo + n; };
+        for (int pass = 0; pass < 4; ++pass) {
+            const int64_t k0 = n1 + n2;
+            for (int64_t g = 0; g < ng; ++g)
+                if (tier1(g) == (pass < 2) && inner(g) == (pass % 2 == 0)) glist[n1 + n2++] = (int)g;
+            if (pass == 0) ninner[0] = n2;
+            if (pass == 1) {
+                n1 = n2;
+                n2 = 0;
             }
-        for (int64_t g = 0, k = n1; g < ng; ++g)
-            if (!(US <= US4 || usz[g] <= US4)) glist[k++] = (int)g;
+            if (pass == 2) ninner[1] = n2;
+            (void)k0;
+        }
+        for (int64_t g = 0; g < ng; ++g)
+            if (tier1(g)) US1 = std::max(US1, usz[g]);
         // gather runs: per 64-node slice of [owned | upper ghosts], the groups
         // naming its nodes in ascending order, each as (first entry, mask)
         dict.assign(std::max<int64_t>(E, 1), 0);
@@ -1346,6 +1357,8 @@ static int gsym_build(kle_mat *A)
     A->sym_reg[2] = (int)n1;
     A->sym_reg[3] = G;
     A->sym_reg[4] = WV;
+    A->gsym_inner[0] = ninner[0];
+    A->gsym_inner[1] = ninner[1];
     A->sblocks = blocks;
     A->snvals = tot;
     A->sws_entries = E;
@@ -1373,11 +1386,10 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2], nhi = A->ghost_hi / 3;
     const bool dist = c->nranks > 1;
     const bool det = g_tune.spmv_sym_det != 0;
-    // N > 1: the ghost x first (the groups of rows that read no ghost could
-    // run beside it; not split yet)
-    if (dist)
-        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
-                              x->send_hi, st, x->plan.get()));
+    // N > 1 with overlap: the groups that read no ghost column, then (comm
+    // stream) the halo, then the rest; all RCCL calls on the comm stream
+    const bool ovl = dist && A->halo_overlap != 0;
+    hipStream_t cs = ovl ? c->comm_stream : st;
     auto launch = [&](auto kern, int slot, int64_t l0, int64_t nl, int US) {
         if (nl <= 0) return;
         const size_t lds = gsym_lds(US, G);
@@ -1391,19 +1403,48 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
                            A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
                            A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_probe);
     };
-    auto launch2 = [&](auto kern, int slot) {
-        launch(kern, slot, 0, n1, A->sym_reg[0]);
-        launch(kern, slot + 1, n1, ng - n1, A->sym_reg[1]);
+    // part 0: the inner groups of both launches, part 1: the others (one
+    // rank or no overlap: both parts back to back)
+    const int64_t i1 = A->gsym_inner[0], i2 = A->gsym_inner[1];
+    auto launch2 = [&](auto kern, int slot, int part) {
+        if (part == 0) {
+            launch(kern, slot, 0, i1, A->sym_reg[0]);
+            launch(kern, slot + 1, n1, i2, A->sym_reg[1]);
+        } else {
+            launch(kern, slot, i1, n1 - i1, A->sym_reg[0]);
+            launch(kern, slot + 1, n1 + i2, ng - n1 - i2, A->sym_reg[1]);
+        }
     };
+    auto tiles = [&](int part) -> int {
 #define GSYM_CASE(GG, WW, SLOT)                                            \
     if (G == GG && WV == WW) {                                             \
-        if (det) launch2(k_nb_spmv_gsym<true, GG, WW>, SLOT);              \
-        else launch2(k_nb_spmv_gsym<false, GG, WW>, SLOT + 2);             \
+        if (det) launch2(k_nb_spmv_gsym<true, GG, WW>, SLOT, part);        \
+        else launch2(k_nb_spmv_gsym<false, GG, WW>, SLOT + 2, part);       \
     } else
-    GSYM_CASE(8, 8, 0) GSYM_CASE(16, 8, 4) GSYM_CASE(32, 8, 8) GSYM_CASE(32, 16, 12) GSYM_CASE(64, 8, 16)
-    GSYM_CASE(64, 16, 20) {
+        GSYM_CASE(8, 8, 0) GSYM_CASE(16, 8, 4) GSYM_CASE(32, 8, 8) GSYM_CASE(32, 16, 12) GSYM_CASE(64, 8, 16)
+        GSYM_CASE(64, 16, 20) {
 #undef GSYM_CASE
-        return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group on %d waves", G, WV);
+            return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group on %d waves", G, WV);
+        }
+        return 0;
+    };
+    if (!dist) {
+        KLE_TRY(tiles(0));
+        KLE_TRY(tiles(1));
+    } else if (ovl) {
+        KLE_HIP(hipEventRecord(c->ev_x_ready, st));
+        KLE_HIP(hipStreamWaitEvent(cs, c->ev_x_ready, 0));
+        KLE_TRY(tiles(0));
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, cs, x->plan.get()));
+        KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
+        KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
+        KLE_TRY(tiles(1));
+    } else {
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, st, x->plan.get()));
+        KLE_TRY(tiles(0));
+        KLE_TRY(tiles(1));
     }
     const int64_t ntot = n + (dist ? nhi : 0);
     hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st, n, ntot, A->d_sgptr,
@@ -1413,9 +1454,17 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     if (!dist) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending
     // rank order of the senders (MPISBAIJ's reverse scatter)
+    if (ovl) {
+        KLE_HIP(hipEventRecord(c->ev_x_ready, st));
+        KLE_HIP(hipStreamWaitEvent(cs, c->ev_x_ready, 0));
+    }
     if (A->plan && !A->plan->peers.empty()) {
         const HaloPlan &P = *A->plan;
-        KLE_TRY(halo_reverse_plan(c, P, A->ghost_lo / 3 + n, 3, A->d_sgsend, A->d_sgrecv, st));
+        KLE_TRY(halo_reverse_plan(c, P, A->ghost_lo / 3 + n, 3, A->d_sgsend, A->d_sgrecv, cs));
+        if (ovl) {
+            KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
+            KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
+        }
         for (size_t k = 0; k < P.peers.size() && P.peers[k] < c->rank; ++k)
             if (P.send_cnt[k])
                 hipLaunchKernelGGL(k_gsym_unpack, dim3((unsigned)((3 * P.send_cnt[k] + 255) / 256)), dim3(256), 0, st,
@@ -1423,7 +1472,11 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
                                    istate);
     } else {
         const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
-        KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, st));
+        KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, cs));
+        if (ovl) {
+            KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
+            KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
+        }
         if (nrecv)
             hipLaunchKernelGGL(k_axpy_first, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, st, nrecv,
                                A->d_sgrecv, y->d, istate);
