@@ -207,6 +207,47 @@ def _worker_graph(rank, size, port, nel, ngl, q):
         dist.all_reduce(t)
         return t.numpy()
 
+    # The graph symmetric storage's N > 1 product (kle_sym.hip gsym_spmv),
+    # restated: each rank keeps the blocks of its node rows from the diagonal
+    # on in ext order (owned columns from the row's own, every higher rank's
+    # ghost), adds B x_j to row i and B^T x_i to row j, then returns the upper
+    # ghosts' sums to their owners (halo_reverse_plan: the forward plan
+    # transposed) and adds what the lower peers send, in ascending rank order.
+    xg = np.random.default_rng(11).uniform(-1, 1, K.m)
+    pext = np.zeros(len(g) * bs)
+    pext[glo:glo + nown] = xg[rows_orc]
+    halo(pext)
+    yext = np.zeros(len(g) * bs)
+    n0 = glo // bs
+    for i in range(nown // bs):
+        pi = n0 + i
+        blocks = {}  # node column -> 3x3 block (Dirichlet rows hold their diagonal only)
+        for a in range(bs):
+            for cc, v in zip(cols[ip[i * bs + a]:ip[i * bs + a + 1]], vals[ip[i * bs + a]:ip[i * bs + a + 1]]):
+                blocks.setdefault(cc // bs, np.zeros((bs, bs)))[a, cc % bs] = v
+        for pj, B in sorted(blocks.items()):
+            if pj < pi:
+                continue  # lower triangle: stored by the row pj's owner (here or a lower rank)
+            yext[pi * bs:pi * bs + bs] += B @ pext[pj * bs:pj * bs + bs]
+            if pj != pi:
+                yext[pj * bs:pj * bs + bs] += B.T @ pext[pi * bs:pi * bs + bs]
+    y = yext[glo:glo + nown].reshape(-1, bs)
+    reqs, bufs = [], []
+    for qr, (nrecv, sent) in sorted(peers.items()):
+        if qr > rank:  # my ghosts of a higher rank: their sums go back to it
+            first = int(np.nonzero(owner[g] == qr)[0][0])
+            reqs.append(dist.isend(torch.from_numpy(yext[first * bs:(first + nrecv) * bs].copy()), qr))
+        elif qr < rank:  # the sums a lower rank formed for the nodes it ghosts of mine
+            t = torch.zeros(len(sent) * bs, dtype=torch.float64)
+            reqs.append(dist.irecv(t, qr))
+            bufs.append((sent, t))
+    for rq in reqs:
+        rq.wait()
+    for sent, t in bufs:  # ascending sender rank
+        y[sent] += t.numpy().reshape(-1, bs)
+    y_ref = K.mult(xg)[rows_orc]
+    sym_err = float(np.abs(y.ravel() - y_ref).max() / np.abs(y_ref).max())
+
     rng = np.random.default_rng(7)
     b_glob = rng.uniform(-1, 1, K.m)
     b = b_glob[rows_orc]
@@ -230,13 +271,15 @@ def _worker_graph(rank, size, port, nel, ngl, q):
         it += 1
     xs, its, _ = K.cg(b_glob, rtol=1e-10, jacobi=True)
     err = np.linalg.norm(x - xs[rows_orc]) / max(np.linalg.norm(xs[rows_orc]), 1e-300)
-    q.put((rank, it, its, err, len(peers)))
+    q.put((rank, it, its, err, len(peers), sym_err))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("size,nel", [(2, [3, 3, 4]), (4, [4, 4, 3])])
 def test_graph_partition_cg_matches_serial(size, nel):
+    """Distributed Jacobi-CG on the graph plan == serial oracle; and the graph
+    symmetric storage's product with its reverse halo == K x on every rank."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -248,8 +291,9 @@ def test_graph_partition_cg_matches_serial(size, nel):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, it, its, err, npeers in res:
+    for rank, it, its, err, npeers, sym_err in res:
         assert abs(it - its) <= 1, (rank, it, its)
         assert err < 1e-9, (rank, err)
+        assert sym_err < 1e-13, (rank, sym_err)  # upper-triangle product + reverse halo == K x
     if size == 4:
         assert max(r[4] for r in res) >= 3  # more than a slab chain's two neighbours
