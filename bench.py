@@ -257,12 +257,19 @@ def main():
         ksp.setType("pipecg" if (args.ksp == "pipecg" or (args.ksp == "auto" and nranks > 1)) else "cg")
         ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=200000)
         ksp.setCGSingleReduction(not args.classic_cg)
+        # (pipelined CG stops on its recursive residual, which drifts to
+        # 1.1-1.3e-10; the record asks for the true residual: one correction
+        # solve when it misses rtol, kle_ksp.hip refine_pipecg)
+        from pynama_amd.runtime import set_tuning
+        set_tuning("ksp_refine", 1)
         ctx.barrier()
         ts = time.perf_counter()
         sol.solve(vort)
         ctx.barrier()
+        set_tuning("ksp_refine", 0)
         solve = {"rtol": 1e-10, "iterations": ksp.getIterationNumber(), "reason": ksp.getConvergedReason(),
-                 "true_rel_residual": ksp.getTrueRelativeResidual(), "seconds": time.perf_counter() - ts}
+                 "true_rel_residual": ksp.getTrueRelativeResidual(), "seconds": time.perf_counter() - ts,
+                 "refined_to_true_residual": ksp.getType() == "pipecg"}
 
     # --- timed fixed-iteration CG
     ksp_type = args.ksp if args.ksp != "auto" else ("pipecg" if nranks > 1 else "cg")

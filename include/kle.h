@@ -86,6 +86,8 @@ const char *kle_last_error(void);
  * CU, 2 = 8 x 8 x 2), "spmv_sym_det" (1
  * default: the transposed adds as exact fixed-point sums, y bitwise
  * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
+ * "ksp_refine" (0 default; 1: a pipelined CG whose true residual misses
+ * rtol runs one correction solve on it -- KLE_KSP_REFINE),
  * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_rows"
  * (read when the storage of an unstructured K is built: rows per group, 32
  * default, 16 or 8), "spmv_gsym_split" (read at build: the largest dictionary of

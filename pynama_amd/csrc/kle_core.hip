@@ -631,6 +631,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
+    } else if (k == "ksp_refine") {
+        KLE_ARG(value == 0 || value == 1, "ksp_refine: 0 or 1");
+        g_tune.ksp_refine = value;
     } else if (k == "spmv_gsym_rows") {
         KLE_ARG(value == 8 || value == 16 || value == 32 || value == 64, "spmv_gsym_rows: 8, 16, 32 or 64");
         g_tune.spmv_gsym_rows = value;
@@ -678,6 +681,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
     else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
+    else if (k == "ksp_refine") *value = g_tune.ksp_refine;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
     else if (k == "spmv_gsym_waves") *value = g_tune.spmv_gsym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;
