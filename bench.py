@@ -257,19 +257,17 @@ def main():
         ksp.setType("pipecg" if (args.ksp == "pipecg" or (args.ksp == "auto" and nranks > 1)) else "cg")
         ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=200000)
         ksp.setCGSingleReduction(not args.classic_cg)
-        # (pipelined CG stops on its recursive residual, which drifts to
-        # 1.1-1.3e-10; the record asks for the true residual: one correction
-        # solve when it misses rtol, kle_ksp.hip refine_pipecg)
-        from pynama_amd.runtime import set_tuning
-        set_tuning("ksp_refine", 1)
+        # (CG and pipelined CG stop on their recursive residual; when the
+        # true residual misses rtol -- the pipelined recurrence drifts to
+        # 1.1-1.3e-10 -- libkle's default correction solve brings it under,
+        # kle_ksp.hip refine; its iterations are part of the count)
         ctx.barrier()
         ts = time.perf_counter()
         sol.solve(vort)
         ctx.barrier()
-        set_tuning("ksp_refine", 0)
         solve = {"rtol": 1e-10, "iterations": ksp.getIterationNumber(), "reason": ksp.getConvergedReason(),
                  "true_rel_residual": ksp.getTrueRelativeResidual(), "seconds": time.perf_counter() - ts,
-                 "refined_to_true_residual": ksp.getType() == "pipecg"}
+                 "correction_iterations": ksp.getCorrectionIterations()}
 
     # --- timed fixed-iteration CG
     ksp_type = args.ksp if args.ksp != "auto" else ("pipecg" if nranks > 1 else "cg")
@@ -385,19 +383,14 @@ def main():
                "gbps": ab / (ms / c * 1e-3) / 1e9, "frac": ab / (ms / c * 1e-3) / 1e9 / HBM_PEAK_GBS}
         del A
 
-    traffic = None
-    if os.path.exists(args.traffic):
-        try:
-            tr = json.load(open(args.traffic))
-            key = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
-                   ("chunk" if args.layout == 1 else f"pad{args.pad}") +
-                   "-nt-u1" + ("-struct" if K.isStructured() else "") +
-                   ("-sym" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_sym") else
-                    "-gsym" if spmv_kernel(K, args.layout, args.ngl).startswith("k_nb_spmv_gsym") else
-                    {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(spmv_kernel(K, args.layout, args.ngl), "")))
-            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    kname = spmv_kernel(K, args.layout, args.ngl)
+    tkey = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
+            ("chunk" if args.layout == 1 else f"pad{args.pad}") +
+            "-nt-u1" + ("-struct" if K.isStructured() else "") +
+            ("-sym" if kname.startswith("k_nb_spmv_sym") else
+             "-gsym" if kname.startswith("k_nb_spmv_gsym") else
+             {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(kname, "")))
+    traffic, traffic_status = lookup_traffic(args.traffic, tkey, kname, spmv_bytes_local)
 
     ops = None
     if args.ops:
@@ -450,7 +443,9 @@ def main():
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
                          "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
-                         "kernel": spmv_kernel(K, args.layout, args.ngl),
+                         "traffic_status": traffic_status, "traffic_key": tkey,
+                         "traffic_over_bytes": traffic / spmv_bytes_local if traffic else None,
+                         "kernel": kname,
                          "bytes_per_launch": tot_bytes,
                          "csr_bytes_per_launch": csr_bytes, "csr_equiv_gbps": csr_equiv,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
@@ -483,6 +478,26 @@ def spmv_kernel(K, layout, ngl):
     """Name of the SpMV kernel(s) libkle launches for this rank's K with the
     current tuning (kle_mat_spmv_kernel: the library's own launch decision)."""
     return K.spmvKernel()
+
+
+def lookup_traffic(path, key, kernel, alg_bytes):
+    """HBM bytes per SpMV launch from the rocprofv3 PMC record `key` of
+    profiles/traffic.json (tools/pmc_traffic.py), or None.  A record counts only
+    if it was measured on this kernel: same launch names and the same
+    algorithmic bytes per launch as the kernel running now (a kernel change
+    that moves different bytes makes the old counter stale)."""
+    try:
+        rec = json.load(open(path)).get(key)
+    except (OSError, ValueError):
+        return None, "no traffic file"
+    if rec is None:
+        return None, f"no PMC record {key}"
+    alg = rec.get("algorithmic_bytes_per_launch")
+    if alg is None or rec.get("kernel") != kernel:
+        return None, f"stale: record {key} names no algorithmic bytes or another kernel ({rec.get('kernel')})"
+    if abs(alg - alg_bytes) > 1e-9 * alg_bytes:
+        return None, f"stale: record {key} measured a kernel of {alg:.0f} algorithmic bytes, this one moves {alg_bytes:.0f}"
+    return rec["hbm_bytes_per_launch"], f"measured ({rec.get('source', key)})"
 
 
 def splitmix_uniform(seed, lo, hi):

@@ -83,17 +83,19 @@ const char *kle_last_error(void);
  * "spmv_sym_min_rows" (node rows per rank from which kle_assemble_kle gives
  * K symmetric storage; default 64000), "spmv_sym_tz" (read when the storage
  * is built: 0 auto = 8 x 4 x 4-row tiles where two 8-wave workgroups fit a
- * CU, 2 = 8 x 8 x 2), "spmv_sym_det" (1
+ * CU, 2 = 8 x 8 x 2, 4 = 8 x 4 x 4), "spmv_sym_det" (1
  * default: the transposed adds as exact fixed-point sums, y bitwise
  * reproducible; 0 fp64 LDS atomics, reproducible to rounding),
- * "ksp_refine" (0 default; 1: a pipelined CG whose true residual misses
- * rtol runs one correction solve on it -- KLE_KSP_REFINE),
+ * "ksp_refine" (correction solves of new KSPs, kle_ksp_set_corrections:
+ * default 2, 0 PETSc's plain stop -- KLE_KSP_REFINE),
  * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_rows"
- * (read when the storage of an unstructured K is built: rows per group, 32
- * default, 16 or 8), "spmv_gsym_split" (read at build: the largest dictionary of
- * the first of its two launches; 0 auto), "spmv_sym_probe"
- * (timing probes that skip parts of the symmetric SpMV: wrong results on
- * purpose; 0 default; bits in kle_internal.hpp). */
+ * (read when the storage of an
+ * unstructured K is built: rows per group, 64 default, 32, 16 or 8),
+ * "spmv_gsym_waves" (read at build: 0 auto = 16 for 64-row groups, else 8;
+ * 8 or 16), "spmv_gsym_split" (read at build: the largest dictionary of the
+ * first of its two launches; 0 auto).  Every value gives correct results (the
+ * timing probes of the symmetric SpMV exist only in the tools/ probe build,
+ * `make -C pynama_amd/csrc probe`). */
 int kle_set_tuning(const char *key, int value);
 int kle_get_tuning(const char *key, int *value);
 int kle_version(void);
@@ -415,6 +417,17 @@ int kle_ksp_get_residual_norm(const kle_ksp *k, double *rnorm);
 int kle_ksp_get_converged_reason(const kle_ksp *k, int *reason);
 /* ||b - A x|| / ||b|| recomputed after the last solve. */
 int kle_ksp_get_true_relative_residual(const kle_ksp *k, double *rel);
+/* CG / pipelined CG stop on their recursive residual (KSPSolve,
+ * kle_solver.py:35), which drifts from the true one (pipelined: 1.1-1.3e-10
+ * at rtol 1e-10).  When the true residual misses rtol, up to n correction
+ * solves A e = b - A x (same method) follow, so the solve meets rtol on the
+ * true residual (the north star's "same residual as PETSc KSP within
+ * 1e-10"); n = 0 stops on the recursive residual exactly as PETSc's KSPCG /
+ * KSPPIPECG do.  Default 2 (kle_set_tuning "ksp_refine" for new KSPs). */
+int kle_ksp_set_corrections(kle_ksp *k, int n);
+/* Iterations of the last solve's correction solves (0: none ran); they are
+ * included in kle_ksp_get_iteration_number. */
+int kle_ksp_get_correction_iterations(const kle_ksp *k, int *its);
 
 /* ------------------------------------------------------------ diagnostics */
 /* Streaming read/copy microbenchmark (HBM ceiling for the roofline). */

@@ -9,7 +9,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(_HERE, "libkle.so")
+# KLE_LIBRARY: tools/ A/B scripts point this at the timing-probe build
+# (tools/libkle_probe.so, `make -C pynama_amd/csrc probe`); unset = libkle.so
+LIBPATH = os.environ.get("KLE_LIBRARY") or os.path.join(_HERE, "libkle.so")
 
 
 class Error(RuntimeError):
@@ -167,6 +169,8 @@ _SIGS = {
     "kle_ksp_get_residual_norm": [vp, C.POINTER(C.c_double)],
     "kle_ksp_get_converged_reason": [vp, C.POINTER(C.c_int)],
     "kle_ksp_get_true_relative_residual": [vp, C.POINTER(C.c_double)],
+    "kle_ksp_set_corrections": [vp, C.c_int],
+    "kle_ksp_get_correction_iterations": [vp, C.POINTER(C.c_int)],
     "kle_stream_copy_bench": [vp, C.c_int64, C.c_int, C.POINTER(C.c_double)],
     "kle_stream_bench": [vp, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double)],
 }

@@ -369,6 +369,7 @@ static int halo_exchange_plan(kle_ctx *ctx, double *base, int64_t ghost_lo, int6
     }
     // ghost group of peer k starts at ext node recv_off[k] (relative to base)
     const size_t np = P.peers.size();
+    if (ctx->ipc) return ipc_halo_plan(ctx, base, P, bs, P.d_sbuf, st);
     if (ctx->comm) {
         KLE_NCCL(ncclGroupStart());
         for (size_t k = 0; k < np; ++k) {
@@ -513,7 +514,7 @@ int halo_reverse_plan(kle_ctx *ctx, const HaloPlan &P, int64_t hi0, int bs, cons
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(ctx->tic("halo_rev", &ev, st));
     if (ctx->ipc) {
-        return fail(KLE_ERR_SUP, "the IPC transport has no graph-partition reverse halo");
+        KLE_TRY(ipc_reverse_plan(ctx, P, hi0, bs, gsend, rbuf, st));
     } else if (ctx->comm) {
         KLE_NCCL(ncclGroupStart());
         for (size_t k = 0; k < np; ++k) {
@@ -632,7 +633,7 @@ int kle_set_tuning(const char *key, int value)
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
     } else if (k == "ksp_refine") {
-        KLE_ARG(value == 0 || value == 1, "ksp_refine: 0 or 1");
+        KLE_ARG(value >= 0 && value <= 8, "ksp_refine: 0 .. 8");
         g_tune.ksp_refine = value;
     } else if (k == "spmv_gsym_rows") {
         KLE_ARG(value == 8 || value == 16 || value == 32 || value == 64, "spmv_gsym_rows: 8, 16, 32 or 64");
@@ -643,9 +644,11 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_gsym_split") {
         KLE_ARG(value >= 0, "spmv_gsym_split: >= 0");
         g_tune.spmv_gsym_split = value;
+#ifdef KLE_PROBE_BUILD
     } else if (k == "spmv_sym_probe") {
         KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
         g_tune.spmv_sym_probe = value;
+#endif
     } else if (k == "spmv_sym_min_rows") {
         KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
         g_tune.spmv_sym_min_rows = value;
@@ -679,7 +682,9 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
+#ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
+#endif
     else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
     else if (k == "ksp_refine") *value = g_tune.ksp_refine;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;

@@ -316,12 +316,15 @@ void sym_forget(kle_mat *A);  // null the symmetric-storage pointers of a struct
 int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate,
              double *dpart = nullptr);  // N > 1: both halos included; dpart: (y, x) partials (one rank)
 int sym_dot_parts(const kle_mat *A);  // partials sym_spmv writes with dpart (0: it cannot)
-// IPC transport (kle_ipc.hip): slab halos, reverse halo, allreduce
+// IPC transport (kle_ipc.hip): slab and graph-partition halos, their reverse halos, allreduce
 int ipc_halo(kle_ctx *c, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi, int lo_rank,
              int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st);
 int ipc_reverse(kle_ctx *c, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
                 int lo_rank, hipStream_t st);
 int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st);
+int ipc_halo_plan(kle_ctx *c, double *base, const HaloPlan &H, int bs, const double *sbuf, hipStream_t st);
+int ipc_reverse_plan(kle_ctx *c, const HaloPlan &H, int64_t hi0, int bs, const double *gsend, double *rbuf,
+                     hipStream_t st);
 void ipc_destroy(kle_ctx *c);
 int halo_reverse(kle_ctx *ctx, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
                  int lo_rank, hipStream_t st);  // kle_core.hip
@@ -335,7 +338,7 @@ struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
-    int ksp_refine = 0;  // pipelined CG: one correction solve when the true residual misses rtol (refine_pipecg); 0 off
+    int ksp_refine = 2;  // CG / pipelined CG: up to this many correction solves when the true residual misses rtol (kle_ksp.hip refine; default of new KSPs); 0 PETSc's plain stop
     int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
     int spmv_sym = 1;  // SBAIJ-style symmetric storage for the KLE K of >= spmv_sym_min_rows node rows per rank; 0 off
@@ -343,7 +346,14 @@ struct Tuning {
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
-    int spmv_sym_probe = 0;   // timing probes only (wrong results): skip 1 transposed adds, 2 row sums, 4 LDS x reads, 8 partial stores, 16 block -> region arithmetic, 128 the item loop; 32 nontemporal partial stores, 64 partials into 8 slabs
+#ifdef KLE_PROBE_BUILD
+    // timing probes (wrong results on purpose), compiled only into the probe
+    // build tools/libkle_probe.so (make probe), never into libkle.so: skip 1
+    // transposed adds, 2 row sums, 4 LDS x reads, 8 partial stores, 16 block ->
+    // region arithmetic, 128 the item loop; 32 nontemporal partial stores, 64
+    // partials into 8 slabs
+    int spmv_sym_probe = 0;
+#endif
     int spmv_gsym_rows = 64;  // unstructured symmetric storage: rows per group (8, 16, 32 or 64; read at build)
     int spmv_gsym_waves = 0;  // its waves per workgroup (0 auto: 16 for 64-row groups, else 8; 8 or 16; read at build)
     int spmv_gsym_split = 0;  // unstructured symmetric storage: dictionary slots of the first launch (0 auto: 4 workgroups per CU; tests)
@@ -351,6 +361,17 @@ struct Tuning {
     int spmv_dict_min_rows = 64000;  // matrices with fewer node rows get no dictionaries (read at creation)
 };
 extern Tuning g_tune;
+// The symmetric SpMV kernels' timing-probe argument exists only in the probe
+// build; in libkle.so `probe` is the constant 0 and every probe branch folds away.
+#ifdef KLE_PROBE_BUILD
+#define KLE_PROBE_PARAM , int probe
+#define KLE_PROBE_ARG , g_tune.spmv_sym_probe
+#define KLE_PROBE_CONST
+#else
+#define KLE_PROBE_PARAM
+#define KLE_PROBE_ARG
+#define KLE_PROBE_CONST constexpr int probe = 0;
+#endif
 // marks the SpMV launches inside its scope as running beside comm-stream work
 struct SideBusy {
     kle_ctx *c;

@@ -6,35 +6,61 @@
 // comm stream occupies a CU while the SpMV runs and no host thread takes part
 // in an exchange.  Bootstrap (the IPC handles) goes over the context's host
 // callbacks.  Reference: the VecScatter of MatMult_MPIAIJ and the
-// MPI_Allreduce of KSPSolve behind kle_solver.py:35.
+// MPI_Allreduce of KSPSolve behind kle_solver.py:35, on a slab or a Chaco
+// (graph) partition (dmplex.py:21).
 //
-// Each rank owns one mailbox (device memory, fine-grained where the driver
-// exports it): per channel and peer a data flag (the sequence number of that
-// peer's last delivery) and an ack flag (the last sequence that peer has
-// consumed from its slot), then the slots.  A delivery of sequence s on a
-// channel: the sender's stream waits until the receiver acked s - 1 (the slot
-// is free), copies into the receiver's slot and writes s into the receiver's
-// data flag; the receiver's stream waits for data flag >= s, copies the slot
-// out (or sums it) and writes s into the sender's ack flag.  Every rank calls
-// every collective in the same order, so the per-channel sequence counters
-// agree without communication.
+// Each rank owns one mailbox (fine-grained device memory: peers write into it
+// and its own stream polls flags in it, so writes from other devices must
+// become visible without a kernel boundary; a rank whose driver cannot export
+// fine-grained memory refuses the transport): per channel and peer a data
+// flag (the sequence number of that peer's last delivery) and an ack flag (the
+// last sequence that peer has consumed from its slot), then the slots.  A
+// delivery of sequence s on a channel: the sender's stream waits until the
+// receiver acked s - 1 (the slot is free), copies into the receiver's slot and
+// writes s into the receiver's data flag; the receiver's stream waits for data
+// flag >= s, copies the slot out (or sums it) and writes s into the sender's
+// ack flag.  Every rank calls every collective in the same order, so the
+// per-channel sequence counters agree without communication.
+//
+// Slab partitions use one slot per direction (FWD_LO / FWD_HI / REV_LO);
+// graph partitions (HaloPlan: any number of peers) and the allreduce use one
+// slot per sender.
+//
+// Deadline: a peer that dies or stops calling the collectives leaves this
+// rank's stream waiting on a flag forever (a stream wait has no timeout).
+// Every collective therefore ends with a stream write of its ticket into a
+// host-pinned progress word; a watchdog thread that sees an issued ticket make
+// no progress for KLE_COMM_TIMEOUT_S seconds (default 300, as for
+// ncclCommInitRank) reports the stuck channel and ends the process with exit
+// status KLE_IPC_EXIT (75): the host thread is blocked inside the runtime and
+// cannot return an error, and a process exit is what frees the stuck queue.
+#include <atomic>
+#include <chrono>
 #include <cstring>
+#include <mutex>
+#include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "kle_internal.hpp"
 
 namespace kle {
 
-enum IpcChannel { CH_FWD_LO = 0, CH_FWD_HI, CH_REV_LO, CH_AR, IPC_NCH };
+enum IpcChannel { CH_FWD_LO = 0, CH_FWD_HI, CH_REV_LO, CH_AR, CH_PFWD, CH_PREV, IPC_NCH };
+static const char *const ch_name[IPC_NCH] = {"halo (to lower)", "halo (to upper)", "reverse halo", "allreduce",
+                                              "plan halo", "plan reverse halo"};
 constexpr int IPC_MAXR = 64;
-constexpr size_t IPC_HDR = 8192;                     // flags (2 x 4 x 64 x 8 B = 4 KB), padded
-constexpr int64_t IPC_HALO_CAP = int64_t(1) << 22;   // doubles per halo slot (32 MB)
-constexpr int64_t IPC_AR_CAP = PART_STRIDE;          // doubles per allreduce slot
+constexpr size_t IPC_HDR = 16384;                    // flags (2 x 6 x 64 x 8 B = 6 KB), padded
+constexpr int64_t IPC_HALO_CAP = int64_t(1) << 22;   // doubles per slab halo slot (32 MB)
+constexpr int64_t IPC_AR_CAP = PART_STRIDE;          // doubles per allreduce slot (one per sender)
+constexpr int64_t IPC_PLAN_CAP = int64_t(1) << 19;   // doubles per graph-halo slot (4 MB, one per sender)
+constexpr int KLE_IPC_EXIT = 75;                     // process exit status of a missed deadline
 
 struct IpcFlags {
     uint64_t data[IPC_NCH][IPC_MAXR];  // [channel][sender]
     uint64_t ack[IPC_NCH][IPC_MAXR];   // [channel][receiver]
 };
+static_assert(sizeof(IpcFlags) <= IPC_HDR, "mailbox header");
 
 struct IpcState {
     char *local = nullptr;          // my mailbox
@@ -42,13 +68,32 @@ struct IpcState {
     uint64_t seq[IPC_NCH] = {};
     int nranks = 1;
     size_t bytes = 0;
-    double *slot(int r, IpcChannel c) const
+    // watchdog: progress words per stream (0 compute, 1 comm), host-pinned,
+    // written by the GPU after each collective; issued tickets and what the
+    // newest collective on each stream was waiting for
+    volatile uint64_t *h_prog = nullptr;
+    uint64_t *d_prog = nullptr;
+    std::atomic<uint64_t> issued[2];
+    std::mutex mu;
+    std::string what[2];
+    std::thread wd;
+    std::atomic<bool> stop{false};
+    double deadline_s = 300.0;
+    int rank = 0;
+
+    IpcState() { issued[0] = issued[1] = 0; }
+    double *region(int r, IpcChannel c) const
     {
-        char *b = peer[r] + IPC_HDR;
-        if (c == CH_AR) return reinterpret_cast<double *>(b) + 3 * IPC_HALO_CAP;
-        return reinterpret_cast<double *>(b) + (int64_t)c * IPC_HALO_CAP;
+        double *b = reinterpret_cast<double *>(peer[r] + IPC_HDR);
+        if (c <= CH_REV_LO) return b + (int64_t)c * IPC_HALO_CAP;
+        b += 3 * IPC_HALO_CAP;
+        if (c == CH_AR) return b;
+        b += (int64_t)nranks * IPC_AR_CAP;
+        return b + (c == CH_PFWD ? 0 : (int64_t)nranks * IPC_PLAN_CAP);
     }
-    double *ar_slot(int r, int from) const { return slot(r, CH_AR) + (int64_t)from * IPC_AR_CAP; }
+    double *slot(int r, IpcChannel c) const { return region(r, c); }  // slab channels: one slot
+    double *ar_slot(int r, int from) const { return region(r, CH_AR) + (int64_t)from * IPC_AR_CAP; }
+    double *plan_slot(int r, IpcChannel c, int from) const { return region(r, c) + (int64_t)from * IPC_PLAN_CAP; }
     uint64_t *data_flag(int r, IpcChannel c, int sender) const
     {
         return &reinterpret_cast<IpcFlags *>(peer[r])->data[c][sender];
@@ -84,7 +129,56 @@ static int post(hipStream_t st, uint64_t *flag, uint64_t v)
     return 0;
 }
 
-// one delivery of n doubles from src into rank `to`'s slot of channel c
+// the end of one collective on stream st: its ticket into the progress word
+// the watchdog reads (and what it was, for the report)
+static int ipc_done(kle_ctx *c, hipStream_t st, IpcChannel ch, const std::vector<int> &peers)
+{
+    IpcState &P = *c->ipc;
+    const int k = st == c->comm_stream ? 1 : 0;
+    {
+        std::string w = std::string(ch_name[ch]) + " with rank(s)";
+        for (int q : peers) w += " " + std::to_string(q);
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.what[k] = w;
+    }
+    return post(st, P.d_prog + k, ++P.issued[k]);
+}
+
+static void ipc_watchdog(IpcState *P)
+{
+    using clk = std::chrono::steady_clock;
+    uint64_t seen[2] = {P->h_prog[0], P->h_prog[1]};
+    clk::time_point since[2] = {clk::now(), clk::now()};
+    while (!P->stop.load()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        for (int k = 0; k < 2; ++k) {
+            const uint64_t done = P->h_prog[k], iss = P->issued[k].load();
+            if (done >= iss || done != seen[k]) {
+                seen[k] = done;
+                since[k] = clk::now();
+                continue;
+            }
+            const double idle = std::chrono::duration<double>(clk::now() - since[k]).count();
+            if (idle > P->deadline_s) {
+                std::string w;
+                {
+                    std::lock_guard<std::mutex> lk(P->mu);
+                    w = P->what[k];
+                }
+                fprintf(stderr,
+                        "kle: rank %d: IPC transport made no progress for %.0f s on the %s stream (collective %llu of "
+                        "%llu; newest: %s): a peer died or stopped calling the collectives (KLE_COMM_TIMEOUT_S) -- "
+                        "exiting with status %d\n",
+                        P->rank, idle, k ? "comm" : "compute", (unsigned long long)done + 1,
+                        (unsigned long long)iss, w.c_str(), KLE_IPC_EXIT);
+                fflush(stderr);
+                _exit(KLE_IPC_EXIT);
+            }
+        }
+    }
+}
+
+// one delivery of n doubles from src into dst (rank `to`'s slot of channel c)
 static int ipc_send(kle_ctx *c, IpcChannel ch, int to, const double *src, int64_t n, double *dst, uint64_t s,
                     hipStream_t st)
 {
@@ -94,12 +188,13 @@ static int ipc_send(kle_ctx *c, IpcChannel ch, int to, const double *src, int64_
     return post(st, P.data_flag(to, ch, c->rank), s);
 }
 
-// the matching receive: n doubles from rank `from` out of my slot into dst
-static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, int64_t n, uint64_t s, hipStream_t st)
+// the matching receive: n doubles from rank `from` out of src (my slot) into dst
+static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, const double *src, int64_t n, uint64_t s,
+                    hipStream_t st)
 {
     IpcState &P = *c->ipc;
     KLE_TRY(wait_ge(st, P.data_flag(c->rank, ch, from), s));
-    if (n) KLE_HIP(hipMemcpyAsync(dst, P.slot(c->rank, ch), sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    if (n) KLE_HIP(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     return post(st, P.ack_flag(from, ch, c->rank), s);
 }
 
@@ -107,29 +202,97 @@ int ipc_halo(kle_ctx *c, double *base, int64_t ghost_lo, int64_t n_local, int64_
              int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st)
 {
     IpcState &P = *c->ipc;
+    // (sizes checked before the sequence moves: a refused call leaves the
+    // counters in step with the peers')
+    KLE_ARG(send_lo <= IPC_HALO_CAP && send_hi <= IPC_HALO_CAP && ghost_lo <= IPC_HALO_CAP &&
+                ghost_hi <= IPC_HALO_CAP,
+            "halo of %lld entries exceeds the IPC slot",
+            (long long)std::max(std::max(send_lo, send_hi), std::max(ghost_lo, ghost_hi)));
     const uint64_t s = ++P.seq[CH_FWD_LO];
-    KLE_ARG(send_lo <= IPC_HALO_CAP && send_hi <= IPC_HALO_CAP, "halo of %lld entries exceeds the IPC slot",
-            (long long)std::max(send_lo, send_hi));
     double *own = base + ghost_lo;
     // my lowest entries are the lower neighbour's upper ghosts (its FWD_HI
     // slot), my highest the upper neighbour's lower ghosts (its FWD_LO)
     if (lo_rank >= 0) KLE_TRY(ipc_send(c, CH_FWD_HI, lo_rank, own, send_lo, P.slot(lo_rank, CH_FWD_HI), s, st));
     if (hi_rank >= 0)
         KLE_TRY(ipc_send(c, CH_FWD_LO, hi_rank, own + n_local - send_hi, send_hi, P.slot(hi_rank, CH_FWD_LO), s, st));
-    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_FWD_LO, lo_rank, base, ghost_lo, s, st));
-    if (hi_rank >= 0) KLE_TRY(ipc_recv(c, CH_FWD_HI, hi_rank, own + n_local, ghost_hi, s, st));
-    return 0;
+    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_FWD_LO, lo_rank, base, P.slot(c->rank, CH_FWD_LO), ghost_lo, s, st));
+    if (hi_rank >= 0)
+        KLE_TRY(ipc_recv(c, CH_FWD_HI, hi_rank, own + n_local, P.slot(c->rank, CH_FWD_HI), ghost_hi, s, st));
+    std::vector<int> pr;
+    if (lo_rank >= 0) pr.push_back(lo_rank);
+    if (hi_rank >= 0) pr.push_back(hi_rank);
+    return ipc_done(c, st, CH_FWD_LO, pr);
 }
 
 int ipc_reverse(kle_ctx *c, const double *send_hi, int64_t n_send, int hi_rank, double *recv_lo, int64_t n_recv,
                 int lo_rank, hipStream_t st)
 {
     IpcState &P = *c->ipc;
+    KLE_ARG(n_send <= IPC_HALO_CAP && n_recv <= IPC_HALO_CAP, "reverse halo of %lld entries exceeds the IPC slot",
+            (long long)std::max(n_send, n_recv));
     const uint64_t s = ++P.seq[CH_REV_LO];
-    KLE_ARG(n_send <= IPC_HALO_CAP, "reverse halo of %lld entries exceeds the IPC slot", (long long)n_send);
     if (hi_rank >= 0) KLE_TRY(ipc_send(c, CH_REV_LO, hi_rank, send_hi, n_send, P.slot(hi_rank, CH_REV_LO), s, st));
-    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_REV_LO, lo_rank, recv_lo, n_recv, s, st));
-    return 0;
+    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_REV_LO, lo_rank, recv_lo, P.slot(c->rank, CH_REV_LO), n_recv, s, st));
+    std::vector<int> pr;
+    if (lo_rank >= 0) pr.push_back(lo_rank);
+    if (hi_rank >= 0) pr.push_back(hi_rank);
+    return ipc_done(c, st, CH_REV_LO, pr);
+}
+
+// Graph-partition halo (HaloPlan): sbuf holds the packed sends (peer k's
+// slice at send_off[k] * bs); each peer's ghost group lands in place at ext
+// node recv_off[k].  The plans are symmetric (kle_umesh.cpp: a rank sends to
+// exactly the ranks it receives from), so every pair delivers at every call.
+int ipc_halo_plan(kle_ctx *c, double *base, const HaloPlan &H, int bs, const double *sbuf, hipStream_t st)
+{
+    IpcState &P = *c->ipc;
+    const size_t np = H.peers.size();
+    for (size_t k = 0; k < np; ++k)
+        KLE_ARG(H.send_cnt[k] * bs <= IPC_PLAN_CAP && H.recv_cnt[k] * bs <= IPC_PLAN_CAP,
+                "graph halo of %lld entries (rank %d) exceeds the IPC slot",
+                (long long)(std::max(H.send_cnt[k], H.recv_cnt[k]) * bs), H.peers[k]);
+    const uint64_t s = ++P.seq[CH_PFWD];
+    const int me = c->rank;
+    for (size_t k = 0; k < np; ++k) {
+        const int q = H.peers[k];
+        KLE_TRY(ipc_send(c, CH_PFWD, q, sbuf + H.send_off[k] * bs, H.send_cnt[k] * bs, P.plan_slot(q, CH_PFWD, me), s,
+                         st));
+    }
+    for (size_t k = 0; k < np; ++k) {
+        const int q = H.peers[k];
+        KLE_TRY(ipc_recv(c, CH_PFWD, q, base + H.recv_off[k] * bs, P.plan_slot(me, CH_PFWD, q), H.recv_cnt[k] * bs, s,
+                         st));
+    }
+    return ipc_done(c, st, CH_PFWD, H.peers);
+}
+
+// Reverse of a graph-partition halo (halo_reverse_plan's transfer): to each
+// higher peer the sums of its ghost group (gsend from ext node hi0 on), from
+// each lower peer its sums for the owned nodes of my send slice to it (rbuf).
+int ipc_reverse_plan(kle_ctx *c, const HaloPlan &H, int64_t hi0, int bs, const double *gsend, double *rbuf,
+                     hipStream_t st)
+{
+    IpcState &P = *c->ipc;
+    const size_t np = H.peers.size();
+    const int me = c->rank;
+    for (size_t k = 0; k < np; ++k)
+        KLE_ARG(H.send_cnt[k] * bs <= IPC_PLAN_CAP && H.recv_cnt[k] * bs <= IPC_PLAN_CAP,
+                "reverse graph halo of %lld entries (rank %d) exceeds the IPC slot",
+                (long long)(std::max(H.send_cnt[k], H.recv_cnt[k]) * bs), H.peers[k]);
+    const uint64_t s = ++P.seq[CH_PREV];
+    for (size_t k = 0; k < np; ++k) {
+        const int q = H.peers[k];
+        if (q > me)
+            KLE_TRY(ipc_send(c, CH_PREV, q, gsend + (H.recv_off[k] - hi0) * bs, H.recv_cnt[k] * bs,
+                             P.plan_slot(q, CH_PREV, me), s, st));
+    }
+    for (size_t k = 0; k < np; ++k) {
+        const int q = H.peers[k];
+        if (q < me)
+            KLE_TRY(ipc_recv(c, CH_PREV, q, rbuf + H.send_off[k] * bs, P.plan_slot(me, CH_PREV, q), H.send_cnt[k] * bs,
+                             s, st));
+    }
+    return ipc_done(c, st, CH_PREV, H.peers);
 }
 
 int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st)
@@ -138,8 +301,10 @@ int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st)
     KLE_ARG(n <= IPC_AR_CAP, "allreduce of %d doubles exceeds the IPC slot", n);
     const uint64_t s = ++P.seq[CH_AR];
     const int me = c->rank;
+    std::vector<int> pr;
     for (int q = 0; q < c->nranks; ++q)
         if (q != me) {
+            pr.push_back(q);
             KLE_TRY(wait_ge(st, P.ack_flag(me, CH_AR, q), s - 1));
             KLE_HIP(hipMemcpyAsync(P.ar_slot(q, me), dbuf, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
             KLE_TRY(post(st, P.data_flag(q, CH_AR, me), s));
@@ -147,28 +312,43 @@ int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st)
     for (int q = 0; q < c->nranks; ++q)
         if (q != me) KLE_TRY(wait_ge(st, P.data_flag(me, CH_AR, q), s));
     hipLaunchKernelGGL(k_rank_sum, dim3((unsigned)std::max(1, std::min(64, (n + 255) / 256))), dim3(256), 0, st,
-                       (int64_t)n, c->nranks, me, P.slot(me, CH_AR), IPC_AR_CAP, dbuf);
+                       (int64_t)n, c->nranks, me, P.region(me, CH_AR), IPC_AR_CAP, dbuf);
     KLE_HIP(hipGetLastError());
     for (int q = 0; q < c->nranks; ++q)
         if (q != me) KLE_TRY(post(st, P.ack_flag(q, CH_AR, me), s));
-    return 0;
+    return ipc_done(c, st, CH_AR, pr);
+}
+
+static void ipc_free(IpcState *P, int me, bool unmap)
+{
+    if (P->wd.joinable()) {
+        P->stop = true;
+        P->wd.join();
+    }
+    if (unmap) {
+        for (int r = 0; r < (int)P->peer.size(); ++r)
+            if (r != me && P->peer[r]) (void)hipIpcCloseMemHandle(P->peer[r]);
+        if (P->local) (void)hipFree(P->local);
+    }
+    if (P->h_prog) (void)hipHostFree((void *)P->h_prog);
+    delete P;
 }
 
 void ipc_destroy(kle_ctx *c)
 {
     if (!c->ipc) return;
-    IpcState &P = *c->ipc;
-    // every rank done with every mailbox before any is unmapped
+    // every rank done with every mailbox before any is unmapped (the watchdog
+    // still guards these synchronisations)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    bool barrier = false;
     if (c->hcomm.allreduce) {
         double one = 1.0;
-        (void)c->hcomm.allreduce(&one, 1, c->hcomm.user);
+        barrier = c->hcomm.allreduce(&one, 1, c->hcomm.user) == 0;
     }
-    for (int r = 0; r < (int)P.peer.size(); ++r)
-        if (r != c->rank && P.peer[r]) (void)hipIpcCloseMemHandle(P.peer[r]);
-    if (P.local) (void)hipFree(P.local);
-    delete c->ipc;
+    // without the barrier a peer may still be writing its last acks into my
+    // mailbox: keep it (and my mappings of theirs) rather than free memory in use
+    ipc_free(c->ipc, c->rank, barrier);
     c->ipc = nullptr;
 }
 
@@ -185,33 +365,58 @@ int kle_ctx_enable_ipc(kle_ctx *c)
     int wait_ok = 0;
     KLE_HIP(hipDeviceGetAttribute(&wait_ok, hipDeviceAttributeCanUseStreamWaitValue, c->device));
     int bad = wait_ok ? 0 : 1;
+    const char *why = wait_ok ? "" : "stream wait-value unsupported";
     auto *P = new IpcState;
     P->nranks = c->nranks;
-    P->bytes = IPC_HDR + sizeof(double) * (3 * IPC_HALO_CAP + (int64_t)c->nranks * IPC_AR_CAP);
+    P->rank = c->rank;
+    if (const char *e = getenv("KLE_COMM_TIMEOUT_S"))
+        if (atof(e) > 0) P->deadline_s = atof(e);
+    P->bytes = IPC_HDR + sizeof(double) * (3 * IPC_HALO_CAP + (int64_t)c->nranks * (IPC_AR_CAP + 2 * IPC_PLAN_CAP));
     hipIpcMemHandle_t h{};
     if (!bad) {
+        // fine-grained or nothing: peers on other devices write flags and
+        // data that this rank's stream polls without a kernel boundary
         if (hipExtMallocWithFlags(reinterpret_cast<void **>(&P->local), P->bytes, hipDeviceMallocFinegrained) !=
                 hipSuccess ||
             hipIpcGetMemHandle(&h, P->local) != hipSuccess) {
             (void)hipGetLastError();
-            if (P->local) (void)hipFree(P->local);
-            P->local = nullptr;
-            bad = hipMalloc(reinterpret_cast<void **>(&P->local), P->bytes) != hipSuccess ||
-                  hipIpcGetMemHandle(&h, P->local) != hipSuccess;
-            (void)hipGetLastError();
+            bad = 1;
+            why = "fine-grained mailbox allocation or export failed";
+        } else if (hipMemset(P->local, 0, IPC_HDR) != hipSuccess) {
+            bad = 1;
+            why = "mailbox clear failed";
         }
-        if (!bad && hipMemset(P->local, 0, IPC_HDR) != hipSuccess) bad = 1;
+    }
+    // the watchdog's progress words: host-pinned, written by the GPU; one
+    // write checked here so a driver that cannot target them refuses at once
+    void *hp = nullptr;
+    if (!bad) {
+        if (hipHostMalloc(&hp, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void **>(&P->d_prog), hp, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            bad = 1;
+            why = "pinned progress word allocation failed";
+        } else {
+            P->h_prog = static_cast<volatile uint64_t *>(hp);
+            P->h_prog[0] = P->h_prog[1] = 0;
+            if (hipStreamWriteValue64(c->stream, P->d_prog, 7, 0) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess || P->h_prog[0] != 7) {
+                (void)hipGetLastError();
+                bad = 1;
+                why = "stream write-value into pinned host memory failed";
+            }
+            P->h_prog[0] = 0;
+        }
     }
     // all-gather of the handles over the host callbacks: one byte per
     // double, one-hot sums (exact), plus every rank's failure flag
     const int hb = (int)sizeof(hipIpcMemHandle_t);
     std::vector<double> buf((size_t)c->nranks * (hb + 1), 0.0);
-    const unsigned char *hp = reinterpret_cast<const unsigned char *>(&h);
-    for (int k = 0; k < hb; ++k) buf[(size_t)c->rank * (hb + 1) + k] = hp[k];
+    const unsigned char *hpb = reinterpret_cast<const unsigned char *>(&h);
+    for (int k = 0; k < hb; ++k) buf[(size_t)c->rank * (hb + 1) + k] = hpb[k];
     buf[(size_t)c->rank * (hb + 1) + hb] = bad;
     if (c->hcomm.allreduce(buf.data(), (int)buf.size(), c->hcomm.user)) {
-        if (P->local) (void)hipFree(P->local);
-        delete P;
+        ipc_free(P, c->rank, true);
         return fail(KLE_ERR_COMM, "IPC bootstrap: host allreduce failed");
     }
     int any_bad = 0;
@@ -227,6 +432,7 @@ int kle_ctx_enable_ipc(kle_ctx *c)
         if (hipIpcOpenMemHandle(&m, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
             (void)hipGetLastError();
             any_bad = 1;
+            why = "mapping a peer's mailbox failed";
         }
         P->peer[r] = static_cast<char *>(m);
     }
@@ -234,13 +440,10 @@ int kle_ctx_enable_ipc(kle_ctx *c)
     double ok = any_bad ? 1.0 : 0.0;
     (void)c->hcomm.allreduce(&ok, 1, c->hcomm.user);
     if (ok != 0.0) {
-        for (int r = 0; r < c->nranks; ++r)
-            if (r != c->rank && P->peer[r]) (void)hipIpcCloseMemHandle(P->peer[r]);
-        if (P->local) (void)hipFree(P->local);
-        delete P;
-        return fail(KLE_ERR_COMM, "IPC transport unavailable (stream wait-value %s, mailbox export or mapping failed "
-                                  "on some rank)", wait_ok ? "supported" : "unsupported");
+        ipc_free(P, c->rank, true);
+        return fail(KLE_ERR_COMM, "IPC transport unavailable on some rank (here: %s)", *why ? why : "ok");
     }
+    P->wd = std::thread(ipc_watchdog, P);
     c->ipc = P;
     return 0;
 }

@@ -808,6 +808,8 @@ struct kle_ksp {
     bool setup = false;
     int its = 0, reason = 0;
     double rnorm = 0, true_rel = -1;
+    int max_corr = g_tune.ksp_refine;  // correction solves on a missed true residual (refine)
+    int corr_its = 0;                  // iterations of the last solve's corrections
     // single-rank CG: `check_every` iterations captured as one hipGraph,
     // replayed until the device reason word stops the kernels; valid for the
     // (b, x) pair it was captured with
@@ -1643,39 +1645,51 @@ int kle_ksp_set_up(kle_ksp *k)
     return 0;
 }
 
-// The pipelined recurrence stops on its recursive residual, which drifts from
-// the true one (1.1-1.3e-10 at rtol 1e-10 on 2-8 ranks).  When the true
-// residual b - A x (in k->q after true_residual) misses rtol, one correction
-// solve A e = r to 0.5 rtol ||b|| and x += e bring it under (PETSc's
-// KSPPIPECG stops on the recursive residual alone, so this is opt-in:
-// kle_set_tuning("ksp_refine", 1) / KLE_KSP_REFINE=1); the iterations add up.
-static int refine_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x)
+// CG and pipelined CG stop on their recursive residual, which drifts from
+// the true one: the pipelined recurrence ends at 1.1-1.3e-10 true residual at
+// rtol 1e-10 on 2-8 ranks.  When the true residual b - A x (in k->q after
+// true_residual) misses rtol, a correction solve A e = r to 0.5 rtol ||b||
+// (same method, zero start) and x += e bring it under; at most k->max_corr
+// such passes (default 2: kle_set_tuning("ksp_refine") / KLE_KSP_REFINE for
+// new KSPs, kle_ksp_set_corrections per KSP).  0 is PETSc's KSPCG/KSPPIPECG
+// exactly: stop on the recursive residual whatever the true one.  The
+// correction iterations add to the iteration count;
+// kle_ksp_get_correction_iterations reports them.
+static int refine(kle_ksp *k, kle_vec *b, kle_vec *x)
 {
-    if (!g_tune.ksp_refine || k->type != "pipecg" || k->reason <= 0 || !(k->true_rel > k->rtol) || k->its >= k->maxit) return 0;
+    k->corr_its = 0;
+    if (k->max_corr <= 0 || (k->type != "pipecg" && k->type != "cg") || k->pc == "lu") return 0;
     kle_ctx *c = k->ctx;
-    kle_vec *rv = nullptr, *e = nullptr;
-    int rc = vec_alloc(c, b->n_local, b->n_global, b->lo, 0, 0, &rv);
-    if (!rc) rc = vec_alloc(c, x->n_local, x->n_global, x->lo, 0, 0, &e);
-    const double rtol0 = k->rtol;
-    const int its0 = k->its, maxit0 = k->maxit;
-    if (!rc) rc = kle_vec_copy(k->q, rv);
-    if (!rc) {
-        k->rtol = 0.5 * rtol0 / k->true_rel;  // (relative to ||r|| = true_rel ||b||)
-        k->maxit = maxit0 - its0;
-        rc = solve_pipecg(k, rv, e, false);
-        k->rtol = rtol0;
-        k->maxit = maxit0;
-        k->its += its0;
-    }
-    if (!rc) rc = kle_vec_axpy(x, 1.0, e);
-    for (kle_vec *v : {rv, e})
-        if (v) {
-            (void)hipStreamSynchronize(c->stream);
-            (void)hipFree(v->base);
-            delete v;
+    for (int pass = 0; pass < k->max_corr; ++pass) {
+        if (k->reason <= 0 || !(k->true_rel > k->rtol) || k->its >= k->maxit) return 0;
+        kle_vec *rv = nullptr, *e = nullptr;
+        int rc = vec_alloc(c, b->n_local, b->n_global, b->lo, 0, 0, &rv);
+        if (!rc) rc = vec_alloc(c, x->n_local, x->n_global, x->lo, 0, 0, &e);
+        const double rtol0 = k->rtol;
+        const int its0 = k->its, maxit0 = k->maxit;
+        if (!rc) rc = kle_vec_copy(k->q, rv);
+        if (!rc) {
+            k->rtol = 0.5 * rtol0 / k->true_rel;  // (relative to ||r|| = true_rel ||b||)
+            k->maxit = maxit0 - its0;
+            rc = k->type == "pipecg" ? solve_pipecg(k, rv, e, false)
+                 : k->single_reduction ? solve_cg_single(k, rv, e, false)
+                                       : solve_cg(k, rv, e);
+            k->rtol = rtol0;
+            k->maxit = maxit0;
+            k->corr_its += k->its;
+            k->its += its0;
         }
-    if (rc) return rc;
-    return true_residual(k, b, x);
+        if (!rc) rc = kle_vec_axpy(x, 1.0, e);
+        for (kle_vec *v : {rv, e})
+            if (v) {
+                (void)hipStreamSynchronize(c->stream);
+                (void)hipFree(v->base);
+                delete v;
+            }
+        if (rc) return rc;
+        KLE_TRY(true_residual(k, b, x));
+    }
+    return 0;
 }
 
 int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
@@ -1694,7 +1708,7 @@ int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x)
     else KLE_TRY(solve_gmres(k, b, x));
     if (!k->fixed) {
         KLE_TRY(true_residual(k, b, x));
-        KLE_TRY(refine_pipecg(k, b, x));
+        KLE_TRY(refine(k, b, x));
     } else {
         k->last_b = b;
         k->last_x = x;
@@ -1734,6 +1748,20 @@ int kle_ksp_get_converged_reason(const kle_ksp *k, int *reason)
 {
     KLE_ARG(k && reason, "null arg");
     *reason = k->reason;
+    return 0;
+}
+
+int kle_ksp_set_corrections(kle_ksp *k, int max_corrections)
+{
+    KLE_ARG(k && max_corrections >= 0 && max_corrections <= 8, "corrections: 0 .. 8");
+    k->max_corr = max_corrections;
+    return 0;
+}
+
+int kle_ksp_get_correction_iterations(const kle_ksp *k, int *its)
+{
+    KLE_ARG(k && its, "null arg");
+    *its = k->corr_its;
     return 0;
 }
 

@@ -268,8 +268,9 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
                                                              const double *__restrict__ sval,
                                                              const double *__restrict__ x, double *__restrict__ ws,
                                                              const int *__restrict__ tile_e,
-                                                             const int *__restrict__ istate, int probe, int t0)
+                                                             const int *__restrict__ istate, int t0 KLE_PROBE_PARAM)
 {
+    KLE_PROBE_CONST
     // LDS: x [3][RN] | y [3][RN + 64] (DET: int64; 64 dummy slots per
     // component take the adds of masked lanes) | direct row sums [3][TR]
     extern __shared__ double lds[];
@@ -895,8 +896,9 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     const int *__restrict__ smu, const int64_t *__restrict__ sbp, const uint16_t *__restrict__ slid,
     const int *__restrict__ dptr, const int *__restrict__ dict, const double *__restrict__ sval,
     const double *__restrict__ x, double *__restrict__ ws, const int *__restrict__ gexp,
-    const int *__restrict__ istate, int xcd_chunk, int probe)
+    const int *__restrict__ istate, int xcd_chunk KLE_PROBE_PARAM)
 {
+    KLE_PROBE_CONST
     extern __shared__ double lds[];
     if (istate && istate[I_REASON] != 0) return;
     constexpr int NT = 64 * WV, RW = G / WV;
@@ -1130,8 +1132,6 @@ static int gsym_build(kle_mat *A)
     if (!(A->kind == 0 && A->R == 3 && A->C == 3 && A->vlayout == 1 && A->d_bcol && !A->d_rowbox &&
           A->m_local == A->n_local && n > 0 && A->ghost_lo % 3 == 0 && A->ghost_hi % 3 == 0))
         why = "symmetric storage of an unstructured matrix needs a 3x3 node-block matrix with owned rows";
-    else if (dist && c->ipc && graph)
-        why = "symmetric storage: the IPC transport has no graph-partition reverse halo";
     else if (slab && (A->send_lo % 3 || A->send_hi % 3))
         why = "symmetric storage: slab halo of partial nodes";
     const int G = g_tune.spmv_gsym_rows;
@@ -1401,7 +1401,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(64 * WV), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
                            A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
-                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_probe);
+                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk KLE_PROBE_ARG);
     };
     // part 0: the inner groups of both launches, part 1: the others (one
     // rank or no overlap: both parts back to back)
@@ -1623,7 +1623,19 @@ static int sym_probe(kle_mat *A, double vmax_all, bool &bad)
 // largest entry or whose pattern is not symmetric.  At N > 1 collective: every
 // rank decides the same way (any_rank), so no rank runs the symmetric SpMV
 // and its reverse halo while a neighbour runs the full storage.
+static int sym_build_impl(kle_mat *A);
+
+// Every error return of the builders, wherever it happens (a refused check,
+// a device error between the allocations and the last check), leaves A
+// without symmetric storage: no SpMV can run over a half-built copy.
 int sym_build(kle_mat *A)
+{
+    const int rc = sym_build_impl(A);
+    if (rc) sym_drop(A);
+    return rc;
+}
+
+static int sym_build_impl(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
     sym_drop(A);
@@ -1851,7 +1863,7 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
     }
     hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
-                       g_tune.spmv_sym_probe, (int)t0);
+                       (int)t0 KLE_PROBE_ARG);
 }
 
 static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,

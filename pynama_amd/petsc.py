@@ -680,6 +680,17 @@ class KSP:
         call("kle_ksp_get_true_relative_residual", self._h, C.byref(v))
         return v.value
 
+    def setCorrections(self, n):
+        """Correction solves when the true residual misses rtol (kle.h
+        kle_ksp_set_corrections; default 2, 0 = PETSc's plain recursive stop)."""
+        call("kle_ksp_set_corrections", self._h, int(n))
+
+    def getCorrectionIterations(self):
+        """Iterations of the last solve's correction solves (0: none ran)."""
+        v = C.c_int()
+        call("kle_ksp_get_correction_iterations", self._h, C.byref(v))
+        return v.value
+
     def destroy(self):
         if self._h:
             call("kle_ksp_destroy", self._h)

@@ -172,8 +172,8 @@ def test_cg_iterations_match_oracle(pa, case, single):
     ksp.solve(b, x)
     # pipelined CG: same iterates in exact arithmetic, recurrences drift more in fp64
     tol_its = {False: 1, True: 2, "pipecg": 4}[single]
-    assert abs(ksp.getIterationNumber() - it_o) <= tol_its
-    assert ksp.getTrueRelativeResidual() <= 1.01e-10 * 1.5
+    assert abs(ksp.getIterationNumber() - ksp.getCorrectionIterations() - it_o) <= tol_its
+    assert ksp.getTrueRelativeResidual() <= 1.01e-10  # (default correction solve: the true residual meets rtol)
     assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
 
 

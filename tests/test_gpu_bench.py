@@ -35,6 +35,11 @@ def test_bench_line_contract():
         assert k in r, k
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    # a PMC figure is only quoted for the kernel it was measured on
+    assert r["traffic_status"] and r["traffic_key"]
+    if r["traffic"] is not None:
+        assert r["traffic_status"].startswith("measured")
+        assert abs(r["traffic_over_bytes"] - r["traffic"] / r["bytes_per_launch"]) < 1e-12
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["unit"] == d["unit"]
     s = d["solve"]

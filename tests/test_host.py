@@ -201,3 +201,33 @@ def test_bench_launcher_failure_path():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.launch_ranks(2, ["--nelem", "2,2,2", "--no-cpu-baseline"], deadline_s=0.5) == 124
+
+
+def test_bench_refuses_a_stale_pmc_record(tmp_path):
+    """bench.py's roofline.traffic comes from a PMC record only when that
+    record was measured on the kernel now running: same launch names and the
+    same algorithmic bytes per launch (tools/pmc_traffic.py stores both);
+    otherwise traffic is null and traffic_status says why."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    k = "k_nb_spmv_sym_xl<8,true,4,4>+k_nb_sym_gather<8,4,4>"
+    db = {"cur": {"kernel": k, "hbm_bytes_per_launch": 2.5e9, "algorithmic_bytes_per_launch": 2354103576.0},
+          "old": {"kernel": k, "hbm_bytes_per_launch": 2.6e9},
+          "other": {"kernel": "k_nb_spmv_xl<8>", "hbm_bytes_per_launch": 4.6e9,
+                    "algorithmic_bytes_per_launch": 2354103576.0}}
+    p = tmp_path / "traffic.json"
+    p.write_text(json.dumps(db))
+    assert bench.lookup_traffic(str(p), "cur", k, 2354103576.0)[0] == 2.5e9
+    for key, alg in (("cur", 2461811976.0), ("old", 2354103576.0), ("other", 2354103576.0), ("none", 1.0)):
+        t, why = bench.lookup_traffic(str(p), key, k, alg)
+        assert t is None and why
+    assert bench.lookup_traffic(str(tmp_path / "absent.json"), "cur", k, 1.0)[0] is None
+    # every record of the committed file that bench.py can return names its
+    # algorithmic bytes (older records without them are never used)
+    for key, rec in json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).items():
+        if "algorithmic_bytes_per_launch" in rec:
+            t, _ = bench.lookup_traffic(os.path.join(ROOT, "profiles", "traffic.json"), key, rec["kernel"],
+                                        rec["algorithmic_bytes_per_launch"])
+            assert t == rec["hbm_bytes_per_launch"]

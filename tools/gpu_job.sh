@@ -46,7 +46,10 @@ for spec in "$@"; do
       grep '^{' "gpurun_out/$name.log" | tail -n 1 > "$OUT/${n}_prof_bench.json" ;;
     pmc)
       step ${name}_f 400 timeout -s KILL 380 rocprofv3 --pmc FETCH_SIZE -d $OUT/${n}_pmc_f -o f --output-format csv -- python3 bench.py $args || exit 1
-      step ${name}_w 400 timeout -s KILL 380 rocprofv3 --pmc WRITE_SIZE -d $OUT/${n}_pmc_w -o w --output-format csv -- python3 bench.py $args || exit 1 ;;
+      step ${name}_w 400 timeout -s KILL 380 rocprofv3 --pmc WRITE_SIZE -d $OUT/${n}_pmc_w -o w --output-format csv -- python3 bench.py $args || exit 1
+      # per-launch HBM bytes of the kernel that ran, with its algorithmic bytes (bench line of the FETCH pass)
+      grep '^{' "gpurun_out/${name}_f.log" | tail -n 1 > "$OUT/${n}_pmc_bench.json"
+      step ${name}_t 60 python tools/pmc_traffic.py $OUT/${n}_pmc_f $OUT/${n}_pmc_w $OUT/${n}_pmc_bench.json auto $OUT/${n}_traffic.json || exit 1 ;;
     sq)
       step $name 400 timeout -s KILL 380 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_VALU -d $OUT/${n}_sq -o sq --output-format csv -- python3 tools/spmv_ab.py $args || exit 1 ;;
     sprof)

@@ -1,8 +1,18 @@
 """Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes
-for one kernel, with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
+of one SpMV, with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
 counters are in KiB; FETCH_SIZE reads 1/2 of the bytes of a coalesced
 streaming read (128-B requests tallied as 64 B), so it is doubled.
-Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEY [OUT]"""
+
+  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR BENCH_JSON [KEY|auto] [OUT]
+
+(auto: the key bench.py looks the record up by, roofline.traffic_key)
+
+BENCH_JSON is the bench.py line of the profiled run itself: its
+roofline.kernel names the launches of one SpMV ("a+b": the tile kernel and
+its gather, each counted once) and roofline.bytes_per_launch is the
+algorithmic byte count of that kernel, stored with the record so that
+bench.py can refuse a counter measured on a different kernel (a record whose
+algorithmic bytes differ from the running kernel's is reported as null)."""
 import csv
 import glob
 import json
@@ -10,25 +20,46 @@ import os
 import sys
 
 
-def avg(d, sub):
-    """Median counter over the dispatches of `sub`: the same kernel also runs
-    once each on Krhs and Rw while the right-hand side is formed; the median
-    of the (timed-loop dominated) dispatch list is the bench matrix's value."""
-    f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
-    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if sub in r["Kernel_Name"]]
+def median(d, name):
+    """Median counter over the dispatches of kernel `name` (the template
+    arguments included): the SpMV also runs on Krhs and Rw while the
+    right-hand side is formed; the median of the (timed-loop dominated)
+    dispatch list is the bench matrix's value."""
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
+         if r["Kernel_Name"].replace(" ", "").startswith(name.replace(" ", ""))]
+    if not v:
+        raise SystemExit(f"pmc_traffic: no dispatch of {name} in {f}")
     v.sort()
     return v[len(v) // 2], len(v)
 
 
 def main():
-    fd, wd, sub, key = sys.argv[1:5]
+    fd, wd, bj = sys.argv[1:4]
+    key = sys.argv[4] if len(sys.argv) > 4 else "auto"
     out = sys.argv[5] if len(sys.argv) > 5 else "profiles/traffic.json"
-    fetch, nf = avg(fd, sub)
-    write, nw = avg(wd, sub)
-    rec = {"kernel": sub, "launches": [nf, nw], "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
+    line = [ln for ln in open(bj) if ln.startswith("{")][-1]
+    rl = json.loads(line)["roofline"]
+    if key == "auto":
+        key = rl["traffic_key"]
+    kernels = rl["kernel"].split("+")
+    parts, fetch, write, launches = {}, 0.0, 0.0, []
+    for k in kernels:
+        f, nf = median(fd, k)
+        w, nw = median(wd, k)
+        parts[k] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes": (2 * f + w) * 1024, "launches": [nf, nw]}
+        fetch += f
+        write += w
+        launches.append([nf, nw])
+    hbm = (2 * fetch + write) * 1024
+    alg = rl["bytes_per_launch"]
+    rec = {"kernel": rl["kernel"], "launches": launches, "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "fetch_bytes_corrected": fetch * 1024 * 2, "write_bytes": write * 1024,
-           "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
-           "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied as 64 B), KiB -> B"}
+           "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
+           "traffic_over_algorithmic": hbm / alg, "parts": parts,
+           "source": os.path.dirname(os.path.abspath(fd)),
+           "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied as 64 B), KiB -> B; "
+                         "per-kernel dispatch medians of one SpMV summed"}
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[key] = rec
     json.dump(db, open(out, "w"), indent=1)

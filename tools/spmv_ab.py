@@ -1,7 +1,9 @@
 """In-process A/B of SpMV tuning knobs on config 2's K (or --nelem/--ngl):
 variants alternate block by block in ONE process; each block times --reps
 products with HIP events around every SpMV launch (the gather included).
-Knobs that are timing probes give wrong products on purpose.
+Knobs that are timing probes ("spmv_sym_probe") give wrong products on
+purpose and exist only in the probe build: the script then loads
+tools/libkle_probe.so (`make -C pynama_amd/csrc probe`) instead of libkle.so.
 
   python tools/spmv_ab.py '[{},{"spmv_sym_probe":1}]' [--nelem 20,16,16] [--reps 4] [--its 100]
 """
@@ -11,6 +13,8 @@ import os
 import statistics
 import sys
 
+if "spmv_sym_probe" in " ".join(sys.argv[1:]):
+    os.environ["KLE_LIBRARY"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkle_probe.so")
 BUILD_KNOBS = {"spmv_sym_tz", "spmv_gsym_rows", "spmv_gsym_waves"}  # read when the symmetric storage is built
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
