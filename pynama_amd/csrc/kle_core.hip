@@ -19,6 +19,10 @@
 namespace kle {
 
 Tuning g_tune;
+#ifdef KLE_PROBE_BUILD
+unsigned long long *g_probe_ts = nullptr;
+int64_t g_probe_ts_cap = 0;
+#endif
 
 
 static thread_local std::string g_err;
@@ -648,6 +652,16 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_probe") {
         KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
         g_tune.spmv_sym_probe = value;
+    } else if (k == "spmv_sym_probe_ts") {
+        KLE_ARG(value >= 0, "spmv_sym_probe_ts: workgroup slots (0: off)");
+        if (g_probe_ts) (void)hipFree(g_probe_ts);
+        g_probe_ts = nullptr;
+        g_probe_ts_cap = 0;
+        if (value > 0) {
+            KLE_HIP(hipMalloc(&g_probe_ts, sizeof(unsigned long long) * 8 * (size_t)value));
+            KLE_HIP(hipMemset(g_probe_ts, 0, sizeof(unsigned long long) * 8 * (size_t)value));
+            g_probe_ts_cap = value;
+        }
 #endif
     } else if (k == "spmv_sym_min_rows") {
         KLE_ARG(value >= 0, "spmv_sym_min_rows: >= 0");
@@ -666,6 +680,17 @@ int kle_set_tuning(const char *key, int value)
     }
     return 0;
 }
+
+#ifdef KLE_PROBE_BUILD
+// probe build only: the phase timestamps of the last instrumented launches
+extern "C" int kle_probe_timestamps(unsigned long long *out, int64_t slots)
+{
+    KLE_ARG(out && slots >= 0 && slots <= g_probe_ts_cap, "bad arg");
+    KLE_HIP(hipDeviceSynchronize());
+    KLE_HIP(hipMemcpy(out, g_probe_ts, sizeof(unsigned long long) * 8 * (size_t)slots, hipMemcpyDeviceToHost));
+    return 0;
+}
+#endif
 
 int kle_get_tuning(const char *key, int *value)
 {

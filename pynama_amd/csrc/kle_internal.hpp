@@ -364,13 +364,37 @@ extern Tuning g_tune;
 // The symmetric SpMV kernels' timing-probe argument exists only in the probe
 // build; in libkle.so `probe` is the constant 0 and every probe branch folds away.
 #ifdef KLE_PROBE_BUILD
-#define KLE_PROBE_PARAM , int probe
-#define KLE_PROBE_ARG , g_tune.spmv_sym_probe
+// probe build: also per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+// into g_probe_ts[slot][8] when kle_set_tuning("spmv_sym_probe_ts", slots)
+// allocated it: slot, start, x ready, item loop done, partials stored
+// (after every wave's vmcnt(0)), HW_ID, XCC_ID
+extern unsigned long long *g_probe_ts;
+extern int64_t g_probe_ts_cap;
+#define KLE_PROBE_PARAM , int probe, unsigned long long *probe_ts, int64_t probe_cap
+#define KLE_PROBE_ARG , g_tune.spmv_sym_probe, g_probe_ts, g_probe_ts_cap
 #define KLE_PROBE_CONST
+#define KLE_PROBE_TS(var) unsigned long long var = probe_ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#define KLE_PROBE_TS_END(slot, a, b, c)                                                                 \
+    if (probe_ts) {                                                                                     \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                \
+        __syncthreads();                                                                                \
+        if (threadIdx.x == 0 && (int64_t)(slot) < probe_cap) {                                          \
+            unsigned long long *r = probe_ts + 8 * (int64_t)(slot);                                     \
+            r[0] = (unsigned long long)(slot);                                                          \
+            r[1] = a;                                                                                   \
+            r[2] = b;                                                                                   \
+            r[3] = c;                                                                                   \
+            r[4] = __builtin_amdgcn_s_memrealtime();                                                    \
+            r[5] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                 \
+            r[6] = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));                                \
+        }                                                                                               \
+    }
 #else
 #define KLE_PROBE_PARAM
 #define KLE_PROBE_ARG
 #define KLE_PROBE_CONST constexpr int probe = 0;
+#define KLE_PROBE_TS(var)
+#define KLE_PROBE_TS_END(slot, a, b, c)
 #endif
 // marks the SpMV launches inside its scope as running beside comm-stream work
 struct SideBusy {

@@ -275,6 +275,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     // component take the adds of masked lanes) | direct row sums [3][TR]
     extern __shared__ double lds[];
     if (istate && istate[I_REASON] != 0) return;
+    KLE_PROBE_TS(ts0)
     static_assert(TY * TZ == 16, "tiles of 128 rows");
     constexpr int TR = SYM_TX * TY * TZ, NT = 64 * WV;
     constexpr int NQ = SYM_TX * TY / WV;  // row slots per wave and plane
@@ -443,6 +444,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     load_v(I, ki, v0, r0);  // in flight across the barrier
     __builtin_amdgcn_s_waitcnt(0xC07F);  // LDS stores done (lgkmcnt 0); the value loads stay in flight
     __builtin_amdgcn_s_barrier();
+    KLE_PROBE_TS(ts1)
     double S = 1.0, invS = 1.0;
     if (DET) {
         // max |x_i| over the tile's rows (every wave computes it; max is exact)
@@ -533,6 +535,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     sym_wait9<0>(v0);
     sym_wait9<0>(v1);
     __syncthreads();
+    KLE_PROBE_TS(ts2)
     // 4. the tile's partial sums: region nodes inside the lattice
     double *dst = ws + ((probe & 64) ? (t & 7) : t) * 3 * (int64_t)RN;  // (probe 64: every tile into 8 slabs)
     const unsigned long long *yi = reinterpret_cast<const unsigned long long *>(yl);
@@ -552,6 +555,7 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
                 dst[b * RN + k] = v;
         }
     }
+    KLE_PROBE_TS_END(t, ts0, ts1, ts2)
 }
 
 // W_t of the DET symmetric SpMV, once per build: for each region node j of
@@ -904,6 +908,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     constexpr int NT = 64 * WV, RW = G / WV;
     const int64_t blk = gsym_block(xcd_chunk);
     if (blk >= nlist) return;  // whole workgroup
+    KLE_PROBE_TS(ts0)
     const int64_t g = glist[blk];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int d0 = dptr[g], U = dptr[g + 1] - d0, RS = US + 64;
@@ -933,6 +938,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     for (int t = threadIdx.x; t < 3 * RS; t += NT) yl[t] = 0.0;  // (0.0 is int64 0)
     if (threadIdx.x < 3 * G) yd[threadIdx.x] = 0.0;
     __syncthreads();
+    KLE_PROBE_TS(ts1)
     double S = 1.0, invS = 1.0;
     if (DET) {
         // max |x_i| over the group's rows: dictionary positions 0 .. nr-1
@@ -1011,6 +1017,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
         if (lane < 3) yd[3 * pos + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
     }
     __syncthreads();
+    KLE_PROBE_TS(ts2)
     // one partial per dictionary entry, [entry][3] (coalesced)
     double *dst = ws + ((probe & 64) ? (g & 7) * 3 * 2048 : (int64_t)d0 * 3);  // (probe 64: into 8 slabs)
     for (int t = (probe & 8) ? 3 * U : threadIdx.x; t < 3 * U; t += NT) {  // (probe 8: no partial stores)
@@ -1022,6 +1029,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
         else
             dst[t] = s;
     }
+    KLE_PROBE_TS_END(g, ts0, ts1, ts2)
 }
 
 // y_j = the partials of the dictionary entries naming row j, ascending group

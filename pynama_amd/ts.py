@@ -11,12 +11,15 @@ with the TSAdaptBasic step controller as PETSc 3.12 documents them:
 * stages  Y_i = X + h sum_{j<i} a_ij K_j,  K_i = f(t + c_i h, Y_i)
   (first-same-as-last reuse of K_s for '5bs' / '3bs' after an accepted step);
 * step    X <- X + h sum_j b_j K_j;
-* error   E = h sum_j (b_j - bhat_j) K_j, weighted RMS norm
-  sqrt(mean((E_i / (atol + rtol max(|X_i|, |X_new_i|)))^2)), atol = rtol = 1e-4
-  (PETSc's TS defaults);
-* control h_new = h clip(0.9 err^(-1/(phat+1)), 0.1, 10), reject if err > 1
-  (retry with the reduced h, safety x0.5 after a rejection); -ts_adapt_type
-  none takes fixed steps.
+* error   TSAdaptChoose_Basic: the embedded solution Y = X_new - E,
+  E = h sum_j (b_j - bhat_j) K_j, against X_new in TSErrorWeightedNorm2:
+  sqrt(mean((E_i / (atol + rtol max(|X_new_i|, |Y_i|)))^2)), atol = rtol =
+  1e-4 (PETSc's TS defaults);
+* control h_new = h clip(safety err^(-1/order), 0.1, 10) with order the
+  method's (phat + 1), safety 0.9; reject if err > 1 and retry with h_new;
+  an attempt that fails right after a failed one uses safety x0.5
+  (reject_safety) -- an attempt that passes after a rejection uses 0.9
+  again; -ts_adapt_type none takes fixed steps.
 
 The vector ops run on the device (libkle Vec); the RHS is whatever callable
 the problem installs -- for BaseProblem.evalRHS one KLE solve plus the
@@ -98,6 +101,7 @@ class TsSolver:
         self._rhs = self._post = None
         self._solution = None
         self.converged_reason = 0
+        self.history = []  # adaptive attempts: (t, h, weighted error, accepted)
 
     # ------------------------------------------------------------ setup
     def setProblemType(self, t):
@@ -206,9 +210,11 @@ class TsSolver:
         return self._solution
 
     # ------------------------------------------------------------ solve
-    def _wrms(self, E, X, Y):
-        e, x, y = E.getArray(), X.getArray(), Y.getArray()
-        w = e / (self.atol + self.rtol * np.maximum(np.abs(x), np.abs(y)))
+    def _wrms(self, E, Xn):
+        """TSErrorWeightedNorm2(U = X_new, Y = X_new - E): the embedded
+        solution's distance from the step's, weighted by both."""
+        e, x = E.getArray(), Xn.getArray()
+        w = e / (self.atol + self.rtol * np.maximum(np.abs(x), np.abs(x - e)))
         t = X.duplicate()
         t.setArray(w)
         n = X.getSize()
@@ -227,17 +233,20 @@ class TsSolver:
         Xn = u.duplicate()
         E = u.duplicate() if adaptive else None
         have_fsal = False
-        safety = self.safety
         eps = 1e-12 * max(1.0, abs(self.max_time))
         while self.step_number < self.max_steps and self.time < self.max_time - eps:
             h = min(self.dt, self.dt_max)
             if self.exact_final_time == self.ExactFinalTime.MATCHSTEP and self.time + h > self.max_time:
                 h = self.max_time - self.time
+            accept = True  # (TSStep_RK: the previous attempt's verdict, true at a step's start)
             while True:
                 for i in range(s):
                     if i == 0 and fsal and have_fsal:
                         K[0], K[s - 1] = K[s - 1], K[0]  # K_s of the accepted step is K_1 of this one
+                        have_fsal = False  # (a retry of this step keeps K_1 as it is)
                         continue
+                    if i == 0 and fsal and not accept:
+                        continue  # TSStep_RK with FSAL never recomputes stage 1: a retry reuses it
                     u.copy(Y)
                     for j in range(i):
                         if A[i][j] != 0.0:
@@ -255,17 +264,18 @@ class TsSolver:
                     d = b[j] - bhat[j]
                     if d != 0.0:
                         E.axpy(h * d, K[j])
-                err = self._wrms(E, u, Xn)
+                err = self._wrms(E, Xn)
+                safety = self.safety
+                if err > 1.0 and not accept:
+                    safety *= self.reject_safety  # the last attempt also failed
+                accept = err <= 1.0
                 hfac = safety * (err ** (-1.0 / (pembed + 1)) if err > 0 else np.inf)
                 h_next = min(max(h * min(max(hfac, self.clip[0]), self.clip[1]), self.dt_min), self.dt_max)
-                if err <= 1.0:
-                    accept = True
-                    safety = self.safety
+                self.history.append((self.time, h, err, accept))
+                if accept:
                     break
                 self.reject += 1
-                safety = self.safety * self.reject_safety
                 h = h_next
-                have_fsal = False
             Xn.copy(u)
             self.time += h
             self.step_number += 1

@@ -281,10 +281,23 @@ class _KSP:
         self.A = A
 
     def setUp(self):
-        self._dense = self.A.dense()
+        # direct solve standing in for the makefile's preonly + lu: dense up
+        # to a few thousand unknowns (every fixture before cavity2d_full),
+        # sparse LU (scipy SuperLU) beyond, where a dense copy would not fit
+        if self.A.m <= 5000:
+            self._dense = self.A.dense()
+            self._lu = None
+        else:
+            import scipy.sparse as sp
+            from scipy.sparse.linalg import splu
+            ip, ix, d = self.A.csr()
+            self._lu = splu(sp.csr_matrix((d, ix, ip), shape=(self.A.m, self.A.n)).tocsc())
 
     def __call__(self, b, x):
-        x.a[:] = np.linalg.solve(self._dense, b.a)
+        if self._lu is None:
+            x.a[:] = np.linalg.solve(self._dense, b.a)
+        else:
+            x.a[:] = self._lu.solve(b.a)
 
 
 class _IS:
@@ -618,7 +631,11 @@ def eval_rhs(dom, mat, solver, vort0, rho, mu, dim, t):
     return rec
 
 
-def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True, umesh=None, extra=None):
+def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True, umesh=None, extra=None,
+                   vectors_only=False):
+    """The reference's MatFS / MatNS, KleSolver and evalRHS on one case.
+    vectors_only: keep the solve's vectors and the DoF sets, not the
+    matrices, connectivity or coordinates (a case at a stated config size)."""
     lower = [0.0] * dim
     upper = [1.0] * dim
     dom = FakeDomain(dim, nelem, lower, upper, ngl, bc) if umesh is None else FakeUDomain(umesh, bc)
@@ -689,8 +706,15 @@ def assembled_case(name, dim, nelem, ngl, bc, rho, mu, fn, ns=False, ops=True, u
     out["u"] = u
     out["u_exact"] = u_ex
     out["err_l2"] = np.linalg.norm(u - u_ex)
+    if vectors_only:
+        keep = ("dim", "nelem", "ngl", "lower", "upper", "rho", "mu", "dir_nodes", "vel0", "vort0", "velFS", "bFS",
+                "tang_dofs", "normal_dofs", "b", "u", "rhs_t", "rhs_vort_in", "rhs_vort_bc", "rhs_vel", "rhs_velFS", "rhs_f",
+                "err_l2")
+        out = {k: v for k, v in out.items() if k in keep}
+        out["K_nnz"] = np.array(len(mat.K.csr()[2]))
     np.savez_compressed(os.path.join(OUT, f"case_{name}.npz"), **out)
-    print(name, "n =", len(u), "nnz(K) =", len(out["K_data"]), "err =", out["err_l2"])
+    print(name, "n =", len(u), "nnz(K) =", len(out["K_data"]) if "K_data" in out else int(out["K_nnz"]),
+          "err =", out["err_l2"])
 
 
 def xdmf_fixtures():
@@ -799,6 +823,10 @@ def main(only=()):
         "tg3d": lambda: assembled_case("tg3d", 3, [2, 2, 2], 3, tg3, 0.5, 0.01, tg3d),
         "tg3d_p4": lambda: assembled_case("tg3d_p4", 3, [1, 1, 2], 5, tg3, 0.5, 0.01, tg3d, ops=False),
         "cavity2d": lambda: assembled_case("cavity2d", 2, [4, 4], 3, cav, 0.5, 0.01, None, ns=True),
+        # BASELINE config 1 as stated: src/cases/cavity-2d.yaml as-is (50 x 50,
+        # ngl 3, rho 0.5, mu 0.01, no-slip walls, lid [2, 0]); vectors only
+        "cavity2d_full": lambda: assembled_case("cavity2d_full", 2, [50, 50], 3, cav, 0.5, 0.01, None, ns=True,
+                                                vectors_only=True),
         # unstructured: the reference's Gmsh fixture
         # src/tests/test.msh (copied to tests/golden/test.msh) and a rotated /
         # shuffled / perturbed hex mesh

@@ -143,6 +143,55 @@ def test_eval_rhs_noslip_matches_reference(pa):
     assert np.abs(f.getArray() - g["rhs_f"]).max() <= 1e-6 * scale
 
 
+def test_config1_cavity_at_stated_size_matches_reference(pa):
+    """BASELINE config 1 at its stated size: src/cases/cavity-2d.yaml as-is
+    (50 x 50 cells, ngl 3, rho 0.5, mu 0.01, no-slip walls with the lid at
+    [2, 0]; 20,402 velocity DoF).  Golden vectors from the reference's own
+    MatNS / KleSolver.solveFS + solve / BaseProblem.evalRHS
+    (make_golden.py cavity2d_full: cavity-2d.yaml:1-29, mat_ns.py:47-145,
+    kle_solver.py:39-41, base_problem.py:111-136; direct solves as the
+    makefile's preonly + lu).  Device: free-slip rhs and solution, no-slip
+    solution <= 1e-9 relative, evalRHS <= 1e-6 of its scale; K's nonzero
+    count and the tangential / normal DoF sets exact."""
+    g = np.load(os.path.join(G, "case_cavity2d_full.npz"))
+    cfg = {"name": "cavity", "material-properties": {"rho": float(g["rho"]), "mu": float(g["mu"])},
+           "domain": {"ngl": 3, "box-mesh": {"nelem": [50, 50], "lower": [0, 0], "upper": [1, 1]}},
+           "boundary-conditions": {"no-slip": CAVITY}, "initial-conditions": {"velocity": [0, 0]}}
+    prob = pa.BaseProblem(cfg)
+    prob.setUp()
+    prob.setUpSolver()
+    dom, sol = prob.dom, prob.solverKLE
+    assert sorted(dom.getTangDofs(collect=True)) == sorted(g["tang_dofs"].tolist())
+    assert sorted(dom.getNormalDofs(collect=True)) == sorted(g["normal_dofs"].tolist())
+    sol.getKSP().setTolerances(rtol=1e-13)
+    sol.solverFS.setTolerances(rtol=1e-13)
+    assert prob.mat.K.getInfo()["nz_used"] == int(g["K_nnz"])
+    # solveFS + solve on the initial state (kle_solver.py:33-41)
+    vort = prob.mat.Rw.createVecRight()
+    vort.setArray(g["vort0"])
+    vel = sol.getSolution()
+    vel.setArray(g["vel0"])
+    np.testing.assert_allclose(sol.rhsFS(vort).getArray(), g["bFS"], rtol=0, atol=1e-12 * np.abs(g["bFS"]).max())
+    sol.solveFS(vort)
+    vfs = sol.getFreeSlipSolution().getArray()
+    assert np.linalg.norm(vfs - g["velFS"]) <= 1e-9 * np.linalg.norm(g["velFS"])
+    sol.solve(vort)
+    assert np.linalg.norm(vel.getArray() - g["u"]) <= 1e-9 * np.linalg.norm(g["u"])
+    # one evalRHS (base_problem.py:111-136) at t = rhs_t
+    vel.setArray(g["vel0"])
+    prob.vort.setArray(g["rhs_vort_in"])
+    f = prob.operator.Curl.createVecLeft()
+    prob.evalRHS(None, float(g["rhs_t"]), prob.vort, f)
+    vfs = sol.getFreeSlipSolution().getArray()
+    assert np.linalg.norm(vfs - g["rhs_velFS"]) <= 1e-9 * np.linalg.norm(g["rhs_velFS"])
+    np.testing.assert_allclose(prob.vort.getArray(), g["rhs_vort_bc"], rtol=0,
+                               atol=1e-9 * np.abs(g["rhs_vort_bc"]).max())
+    u = sol.getSolution().getArray()
+    assert np.linalg.norm(u - g["rhs_vel"]) <= 1e-9 * np.linalg.norm(g["rhs_vel"])
+    scale = max(1.0, np.abs(g["rhs_f"]).max())
+    assert np.abs(f.getArray() - g["rhs_f"]).max() <= 1e-6 * scale
+
+
 def test_getrow_matches_csr(pa):
     """Mat.getRow (petsc4py, dmplex.py:332,363) on node-block matrices with and
     without DoF-level masks, and on a scalar AIJ matrix."""

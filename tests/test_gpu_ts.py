@@ -216,3 +216,106 @@ def test_rk5bs_steps_match_cpu_restatement(pa):
     # FSAL reuse (an O(h) change of K_1) is far outside the tolerance
     Xw = integrate(False)
     assert np.linalg.norm((Xg - X0) - (Xw - X0)) > 1e-6 * np.linalg.norm(dc)
+
+
+def _tg2d_cpu_rhs(pa, nelem, ngl, rho=0.5, mu=0.01):
+    """The stage-blind vorticity RHS of BaseProblem.evalRHS restated on the
+    CPU over the oracle's assembly (as in the fixed-step test): refresh the
+    boundary vorticity of X in place at time t, KLE solve with the boundary
+    velocity, operator chain."""
+    from oracle import oracle as O
+    om = O.BoxMesh(2, nelem, [0, 0], [1, 1], ngl)
+    bn = pa.BoxMesh(2, nelem, [0, 0], [1, 1], ngl).face_nodes(pa.mesh.FACES[2])
+    flag = np.zeros(om.N, np.uint8)
+    flag[bn] = 1
+    K, Kr, Rw = om.assemble_fs(flag)
+    Curl, SrT, DivSrT, _ = om.assemble_ops()
+    coords = om.coords()
+    f = pa.fields.get("taylor_green")
+    nu = mu / rho
+    vdofs = (bn[:, None] * 2 + np.arange(2)).ravel()
+
+    def rhs(t, X):
+        a = f.alpha(nu, t)
+        X[bn] = f.vorticity(coords[bn], a)
+        ubc = np.zeros(om.N * 2)
+        ubc[vdofs] = f.velocity(coords[bn], a)
+        vel, _, _ = K.cg(Rw.mult(X) + Kr.mult(ubc), rtol=1e-13)
+        return O.eval_rhs_chain(Curl, SrT, DivSrT, vel, rho, mu, 2)[2]
+    return rhs
+
+
+def test_rk5bs_adaptive_steps_match_tsadapt_basic_restatement(pa):
+    """The adaptive controller the reference's TS runs by default
+    (ts_solver.py:3-23: TSRK 5bs, setFromOptions -> TSAdaptBasic), checked
+    independently of pynama_amd.ts: the published rule is restated here and
+    fed by the CPU RHS above -- embedded error Y = X_new - E against X_new in
+    the weighted RMS norm of TSErrorWeightedNorm2 (atol = rtol = 1e-4, the TS
+    defaults), accept iff err <= 1, h_new = h clip(0.9 err^(-1/5), 0.1, 10),
+    safety x0.5 when an attempt fails right after a failed one, the FSAL stage
+    kept across a retry, MATCHSTEP clamping the last step; the coefficients
+    are the published ones (tests/bs54_tableau.py).  From PETSc's default
+    first step 0.1 to t = 0.5 on the 2-D Taylor-Green case the sequence holds
+    consecutive rejections, an acceptance right after a rejection and a
+    clamped last step.  The device integrator must take the same attempts
+    (same accept / reject verdicts, h and weighted errors to 1e-8) and end
+    on the same vorticity.  Parity with PETSc itself stays unpinned."""
+    from bs54_tableau import B as B54, BHAT as BH54, C as C54
+    from pynama_amd.ts import TsSolver
+    nelem, ngl, tend, h0, tol = [6, 6], 5, 0.5, 0.1, 1e-4
+    cfg = {"name": "tg", "material-properties": {"rho": 0.5, "mu": 0.01},
+           "domain": {"ngl": ngl, "box-mesh": {"nelem": nelem, "lower": [0, 0], "upper": [1, 1]}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green"}},
+           "initial-conditions": {"custom-func": {"name": "taylor_green"}},
+           "time-solver": {"start-time": 0.0, "end-time": tend, "max-steps": 100}}
+    prob = pa.BaseProblem(cfg)
+    prob.setUp()
+    prob.setUpSolver()
+    prob.solverKLE.getKSP().setTolerances(rtol=1e-13)
+    X0 = prob.vort.getArray().copy()
+    ts = TsSolver()
+    ts.setUpTimes(0.0, tend, 100)
+    ts.initSolver(prob.evalRHS, None)
+    ts.setTimeStep(h0)
+    ts.setTolerances(rtol=tol, atol=tol)
+    ts.solve(prob.vort)
+    dev = ts.history
+    Xg = prob.vort.getArray().copy()
+
+    rhs = _tg2d_cpu_rhs(pa, nelem, ngl)
+    c, b, bh = ([float(v) for v in T] for T in (C54, B54, BH54))
+    s = len(c)
+    X, t, h, K1, ref = X0.copy(), 0.0, h0, None, []
+    while t < tend - 1e-12:
+        h = min(h, tend - t)  # MATCHSTEP
+        prev_ok = True
+        while True:
+            Ks = [K1 if K1 is not None else rhs(t, X)] + [None] * (s - 1)
+            for i in range(1, s):
+                Ks[i] = rhs(t + c[i] * h, X)  # (the stage vector is not read)
+            Xn = X.copy()
+            E = np.zeros_like(X)
+            for j in range(s):
+                Xn += (h * b[j]) * Ks[j]
+                E += (h * (b[j] - bh[j])) * Ks[j]
+            Y = Xn - E
+            err = np.sqrt(np.mean((E / (tol + tol * np.maximum(np.abs(Xn), np.abs(Y)))) ** 2))
+            safety = 0.9 * (0.5 if err > 1 and not prev_ok else 1.0)
+            ok = err <= 1.0
+            h_next = h * min(max(safety * err ** -0.2 if err > 0 else np.inf, 0.1), 10.0)
+            ref.append((t, h, err, ok))
+            K1 = Ks[0]
+            if ok:
+                break
+            prev_ok, h = False, h_next
+        X, t, h, K1 = Xn, t + h, h_next, Ks[-1]
+    verdicts = [a for *_, a in ref]
+    assert verdicts.count(False) >= 2 and any(not a and b_ for a, b_ in zip(verdicts, verdicts[1:]))
+    assert any(not a and not b_ for a, b_ in zip(verdicts, verdicts[1:]))  # consecutive rejections
+    assert len(dev) == len(ref), (len(dev), len(ref))
+    for (td, hd, ed, ad), (tr, hr, er, ar) in zip(dev, ref):
+        assert ad == ar
+        assert abs(td - tr) <= 1e-10 and abs(hd - hr) <= 1e-8 * hr
+        assert abs(ed - er) <= 1e-8 * max(er, 1e-3), (ed, er)
+    assert abs(ts.getTime() - tend) < 1e-12
+    np.testing.assert_allclose(Xg, X, rtol=0, atol=1e-9 * np.abs(X).max())

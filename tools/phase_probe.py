@@ -1,0 +1,101 @@
+"""Per-workgroup phase timeline of the symmetric SpMV tile kernels (probe build).
+
+Loads tools/libkle_probe.so (`make -C pynama_amd/csrc probe`), whose
+k_nb_spmv_sym_xl / k_nb_spmv_gsym record per workgroup (s_memrealtime,
+100 MHz): start, x in LDS, item loop done, partials stored (after every
+wave's vmcnt(0) -- the probe adds that wait and a barrier), HW_ID, XCC_ID.
+Prints one JSON summary per run (phase medians / percentiles in us, kernel
+span, workgroup-slot utilisation, per-XCD spans) and saves the raw records.
+
+  python tools/phase_probe.py [--mesh box|unstructured] [--nelem 20,16,16] [--ngl 5] [--reps 3]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["KLE_LIBRARY"] = os.path.join(ROOT, "tools", "libkle_probe.so")
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mesh", default="box", choices=["box", "unstructured"])
+    ap.add_argument("--nelem", default="20,16,16")
+    ap.add_argument("--ngl", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "phase"))
+    ap.add_argument("--tuning", default="{}", help="JSON of kle_set_tuning knobs (probe bits included)")
+    a = ap.parse_args()
+    import numpy as np
+
+    import pynama_amd as pa
+    from pynama_amd._lib import load
+    from pynama_amd.runtime import set_tuning
+    nelem = [int(v) for v in a.nelem.split(",")]
+    cfg = {"domain": {"ngl": a.ngl, "box-mesh": {"nelem": nelem, "lower": [0.0] * 3, "upper": [1.0] * 3}},
+           "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+    if a.mesh == "unstructured":
+        import tempfile
+        from pynama_amd.meshgen import perturbed_box, write_gmsh
+        V, Cc, F, T = perturbed_box(3, nelem, seed=5)
+        path = os.path.join(tempfile.mkdtemp(prefix="kle_phase_"), "mesh.msh")
+        write_gmsh(path, 3, V, Cc, F, T)
+        cfg["domain"] = {"ngl": a.ngl, "gmsh-file": path}
+    dom = pa.Domain()
+    dom.configure(cfg)
+    dom.setUp()
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    K = mat.K
+    kern = K.spmvKernel()
+    for k, v in json.loads(a.tuning).items():
+        set_tuning(k, v)
+    slots = 1 << 20
+    set_tuning("spmv_sym_probe_ts", slots)
+    lib = load()
+    x = K.createVecRight()
+    x.setArray(np.random.default_rng(3).uniform(-1, 1, x.getLocalSize()))
+    y = K.createVecLeft()
+    ctx = pa.get_ctx()
+    os.makedirs(a.out, exist_ok=True)
+    for rep in range(a.reps + 1):
+        K.mult(x, y)
+        ctx.synchronize()
+        buf = np.zeros(slots * 8, dtype=np.uint64)
+        rc = lib.kle_probe_timestamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_int64(slots))
+        assert rc == 0
+        r = buf.reshape(slots, 8)
+        r = r[r[:, 1] != 0]
+        if rep == 0:
+            continue  # (warm-up)
+        t0 = r[:, 1].min()
+        st, xr, lp, en = [(r[:, i].astype(np.int64) - int(t0)) / 100.0 for i in (1, 2, 3, 4)]  # us
+        fill, loop, store, total = xr - st, lp - xr, en - lp, en - st
+        span = en.max()
+        xcc = (r[:, 6] & 0xF).astype(int)
+
+        def pct(v):
+            return {"p10": float(np.percentile(v, 10)), "med": float(np.median(v)), "p90": float(np.percentile(v, 90)),
+                    "mean": float(v.mean())}
+        # mean number of workgroups in flight and per-XCD spans
+        per_xcd = {int(c): {"n": int((xcc == c).sum()), "span_us": float(en[xcc == c].max() - st[xcc == c].min())}
+                   for c in np.unique(xcc)}
+        summ = {"rep": rep, "kernel": kern, "mesh": a.mesh, "nelem": nelem, "ngl": a.ngl, "workgroups": int(len(r)),
+                "span_us": float(span), "sum_total_us": float(total.sum()),
+                "mean_in_flight": float(total.sum() / span),
+                "fill_us": pct(fill), "loop_us": pct(loop), "store_us": pct(store), "total_us": pct(total),
+                "share": {"fill": float(fill.sum() / total.sum()), "loop": float(loop.sum() / total.sum()),
+                          "store": float(store.sum() / total.sum())},
+                "last_start_us": float(st.max()), "first_end_us": float(en.min()),
+                "per_xcd": per_xcd, "tuning": json.loads(a.tuning)}
+        print(json.dumps(summ), flush=True)
+        np.save(os.path.join(a.out, f"phase_{a.mesh}_{rep}.npy"), r)
+    set_tuning("spmv_sym_probe_ts", 0)
+
+
+if __name__ == "__main__":
+    main()
