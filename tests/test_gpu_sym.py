@@ -63,8 +63,8 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
     from pynama_amd.runtime import set_tuning
     try:
-        # the column walk (P <= 4) and the tile-per-workgroup kernel
-        # (fixed-point and fp64-atomic sums, 1 or 2 items ahead, 8 or 16 waves)
+        # the x-in-LDS tile kernel k_nb_spmv_sym_xl under every knob of KNOBS
+        # (fixed-point and fp64-atomic transposed sums, 8 or 16 waves)
         for knobs in KNOBS:
             for k, v in knobs.items():
                 set_tuning(k, v)
