@@ -633,6 +633,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
+    } else if (k == "spmv_sym_early") {
+        KLE_ARG(value == 0 || value == 1, "spmv_sym_early: 0 or 1");
+        g_tune.spmv_sym_early = value;
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
@@ -650,7 +653,7 @@ int kle_set_tuning(const char *key, int value)
         g_tune.spmv_gsym_split = value;
 #ifdef KLE_PROBE_BUILD
     } else if (k == "spmv_sym_probe") {
-        KLE_ARG(value >= 0 && value < 4096, "spmv_sym_probe: bit mask < 4096");
+        KLE_ARG(value >= 0, "spmv_sym_probe: bit mask (< 4096) | ring slots << 12");
         g_tune.spmv_sym_probe = value;
     } else if (k == "spmv_sym_probe_ts") {
         KLE_ARG(value >= 0, "spmv_sym_probe_ts: workgroup slots (0: off)");
@@ -707,6 +710,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
+    else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

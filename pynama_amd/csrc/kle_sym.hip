@@ -268,7 +268,8 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
                                                              const double *__restrict__ sval,
                                                              const double *__restrict__ x, double *__restrict__ ws,
                                                              const int *__restrict__ tile_e,
-                                                             const int *__restrict__ istate, int t0 KLE_PROBE_PARAM)
+                                                             const int *__restrict__ istate, int t0,
+                                                             int early KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
     // LDS: x [3][RN] | y [3][RN + 64] (DET: int64; 64 dummy slots per
@@ -434,14 +435,17 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
         ki = 0;
         slot_row(xi, I);
     };
+    double v0[9], v1[9];
+    int r0, r1 = 0;
+    // early: the first item's value loads go out with the x fill (they do not
+    // read x), so the tile's first round trip overlaps the fill's
+    if (early) load_v(I, ki, v0, r0);
 #pragma unroll
     for (int f = 0; f < SYM_FILL; ++f) {
         const int l = fl0 + f * fstep;  // (unused slots store into a dummy y slot: no branch)
         xl[fl0 < fstep && l < NL ? fcc * RN + frx + g.RX * l : 4 * RN + lane] = fv[f];
     }
-    double v0[9], v1[9];
-    int r0, r1 = 0;
-    load_v(I, ki, v0, r0);  // in flight across the barrier
+    if (!early) load_v(I, ki, v0, r0);  // in flight across the barrier
     __builtin_amdgcn_s_waitcnt(0xC07F);  // LDS stores done (lgkmcnt 0); the value loads stay in flight
     __builtin_amdgcn_s_barrier();
     KLE_PROBE_TS(ts1)
@@ -537,7 +541,8 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     __syncthreads();
     KLE_PROBE_TS(ts2)
     // 4. the tile's partial sums: region nodes inside the lattice
-    double *dst = ws + ((probe & 64) ? (t & 7) : t) * 3 * (int64_t)RN;  // (probe 64: every tile into 8 slabs)
+    // (probe 64: every tile into 8 slabs; probe >> 12 = R > 0: into a ring of R tile slots)
+    double *dst = ws + ((probe & 64) ? (t & 7) : (probe >> 12) ? t % max(1, probe >> 12) : t) * 3 * (int64_t)RN;
     const unsigned long long *yi = reinterpret_cast<const unsigned long long *>(yl);
     for (int k = (probe & 8) ? RN : threadIdx.x; k < RN; k += NT) {
         const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
@@ -1019,7 +1024,8 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     __syncthreads();
     KLE_PROBE_TS(ts2)
     // one partial per dictionary entry, [entry][3] (coalesced)
-    double *dst = ws + ((probe & 64) ? (g & 7) * 3 * 2048 : (int64_t)d0 * 3);  // (probe 64: into 8 slabs)
+    // (probe 64: into 8 slabs; probe >> 12 = R > 0: into a ring of R group slots)
+    double *dst = ws + ((probe & 64) ? (g & 7) * 3 * 2048 : (probe >> 12) ? (g % max(1, probe >> 12)) * 3 * 2048 : (int64_t)d0 * 3);
     for (int t = (probe & 8) ? 3 * U : threadIdx.x; t < 3 * U; t += NT) {  // (probe 8: no partial stores)
         const int e = t / 3, c = t - 3 * e;
         double s = DET ? fx_to_d(yi[c * RS + e]) * invS : yl[c * RS + e];
@@ -1871,7 +1877,7 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
     }
     hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
-                       (int)t0 KLE_PROBE_ARG);
+                       (int)t0, g_tune.spmv_sym_early KLE_PROBE_ARG);
 }
 
 static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,

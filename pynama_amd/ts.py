@@ -215,9 +215,9 @@ class TsSolver:
         solution's distance from the step's, weighted by both."""
         e, x = E.getArray(), Xn.getArray()
         w = e / (self.atol + self.rtol * np.maximum(np.abs(x), np.abs(x - e)))
-        t = X.duplicate()
+        t = Xn.duplicate()
         t.setArray(w)
-        n = X.getSize()
+        n = Xn.getSize()
         return t.norm() / np.sqrt(max(n, 1))
 
     def solve(self, u):
