@@ -633,6 +633,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
+    } else if (k == "spmv_sym_align") {
+        KLE_ARG(value == 0 || value == 1, "spmv_sym_align: 0 or 1");
+        g_tune.spmv_sym_align = value;
     } else if (k == "spmv_sym_early") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_early: 0 or 1");
         g_tune.spmv_sym_early = value;
@@ -711,6 +714,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
+    else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

@@ -245,6 +245,8 @@ struct kle_mat {
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
     int sym_P = 0, sym_TZ = 2;
+    int sym_wn = 0;  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
+    int *d_swptr = nullptr;  // graph: per group, its partials' first double in d_sws (128-B aligned with spmv_sym_align)
     int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
     // graph (unstructured) symmetric storage, one rank (kle_sym.hip gsym_build):
     // d_srow = stored blocks per row, d_stile_e = per-group scale exponents,
@@ -345,6 +347,7 @@ struct Tuning {
     int spmv_sym_min_rows = 64000;
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
+    int spmv_sym_align = 1;   // symmetric SpMV partials (read at build): every tile's / group's slot starts on a 128-B line and its lines are written whole (1) or packed (0)
     int spmv_sym_early = 0;   // symmetric SpMV tiles: the first item's value loads issued with the x fill (1) or after it (0)
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
 #ifdef KLE_PROBE_BUILD

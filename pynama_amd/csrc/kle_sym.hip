@@ -47,6 +47,7 @@ constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (on
 // x (4 + p) = 1536.
 struct SymGeo {
     int Lx, Ly, Lz, P, TX, TY, TZ, PX, PY, RX, RY, RZ, ntx, nty, ntz, zo, hp;
+    int WN;  // per-component stride of a tile's partials in the workspace (>= RX RY RZ)
 };
 
 __device__ __forceinline__ void sym_box(const int *__restrict__ rowbox, int64_t i, int Lx, int64_t Lxy, int &bx,
@@ -542,22 +543,31 @@ __global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const i
     KLE_PROBE_TS(ts2)
     // 4. the tile's partial sums: region nodes inside the lattice
     // (probe 64: every tile into 8 slabs; probe >> 12 = R > 0: into a ring of R tile slots)
-    double *dst = ws + ((probe & 64) ? (t & 7) : (probe >> 12) ? t % max(1, probe >> 12) : t) * 3 * (int64_t)RN;
+    // aligned slots (WN > RN: every slot and component run starts on a 128-B
+    // line): the whole run is written, zeros off the lattice, so every line
+    // leaves L2 written whole by one workgroup -- no partially written lines
+    // for the memory side to merge
+    const int WN = g.WN;
+    const bool whole = WN != RN;
+    double *dst = ws + ((probe & 64) ? (t & 7) : (probe >> 12) ? t % max(1, probe >> 12) : t) * 3 * (int64_t)WN;
     const unsigned long long *yi = reinterpret_cast<const unsigned long long *>(yl);
-    for (int k = (probe & 8) ? RN : threadIdx.x; k < RN; k += NT) {
-        const int rz = k / (g.RX * g.RY), rem = k - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
+    for (int k = (probe & 8) ? WN : threadIdx.x; k < WN; k += NT) {
+        const int kc = min(k, RN - 1);
+        const int rz = kc / (g.RX * g.RY), rem = kc - rz * g.RX * g.RY, ry = rem / g.RX, rx = rem - ry * g.RX;
         const int gx = ox + rx, gy = oy + ry, gz = tz + rz;
-        if (gx < 0 || gx >= g.Lx || gy < 0 || gy >= g.Ly || gz >= g.Lz + g.hp) continue;
+        const bool lat = k < RN && gx >= 0 && gx < g.Lx && gy >= 0 && gy < g.Ly && gz < g.Lz + g.hp;
+        if (!lat && !whole) continue;
         const bool own = rx >= g.PX && rx < g.PX + SYM_TX && ry >= g.PY && ry < g.PY + TY && rz < TZ;
         const int sl = (rx - g.PX) + SYM_TX * ((ry - g.PY) + TY * rz);
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-            double v = DET ? fx_to_d(yi[b * RS + k]) * invS : yl[b * RS + k];
+            double v = DET ? fx_to_d(yi[b * RS + kc]) * invS : yl[b * RS + kc];
             if (own) v += yd[b * TR + sl];
+            if (!lat) v = 0.0;
             if (probe & 32)
-                __builtin_nontemporal_store(v, dst + b * RN + k);
+                __builtin_nontemporal_store(v, dst + b * WN + k);
             else
-                dst[b * RN + k] = v;
+                dst[b * WN + k] = v;
         }
     }
     KLE_PROBE_TS_END(t, ts0, ts1, ts2)
@@ -675,10 +685,10 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
             for (int tx = x_lo; tx <= x_hi; ++tx) {
                 const int64_t t = ((int64_t)tzi * g.nty + ty) * g.ntx + tx;
                 const int r = (jx - (tx * TXW - g.PX)) + g.RX * ((jy - (ty * TY - g.PY)) + g.RY * (jz - tzi * TZ));
-                const double *p = ws + t * 3 * (int64_t)RN + r;
+                const double *p = ws + t * 3 * (int64_t)g.WN + r;
                 s0 += p[0];
-                s1 += p[RN];
-                s2 += p[2 * RN];
+                s1 += p[g.WN];
+                s2 += p[2 * g.WN];
             }
     if (j >= n) {
         double *o = gsend + 3 * (j - n);
@@ -719,6 +729,8 @@ void sym_forget(kle_mat *A)
     A->d_slid = nullptr;
     A->d_sdptr = A->d_sdict = A->d_sgptr = A->d_sgidx = A->d_sglist = nullptr;
     A->d_sgmask = nullptr;
+    A->d_swptr = nullptr;
+    A->sym_wn = 0;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
     A->sym_graph = 0;
@@ -729,7 +741,7 @@ void sym_drop(kle_mat *A)
     for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
                     (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow, (void *)A->d_sbp,
                     (void *)A->d_slid, (void *)A->d_sdptr, (void *)A->d_sdict, (void *)A->d_sgptr,
-                    (void *)A->d_sgidx, (void *)A->d_sgmask, (void *)A->d_sglist})
+                    (void *)A->d_sgidx, (void *)A->d_sgmask, (void *)A->d_sglist, (void *)A->d_swptr})
         if (q) (void)hipFree(q);
     sym_forget(A);
 }
@@ -903,8 +915,9 @@ template <bool DET, int G, int WV>
 __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     int64_t nrows, int64_t nlist, const int *__restrict__ glist, int US, const int64_t *__restrict__ svptr,
     const int *__restrict__ smu, const int64_t *__restrict__ sbp, const uint16_t *__restrict__ slid,
-    const int *__restrict__ dptr, const int *__restrict__ dict, const double *__restrict__ sval,
-    const double *__restrict__ x, double *__restrict__ ws, const int *__restrict__ gexp,
+    const int *__restrict__ dptr, const int *__restrict__ dict, const int *__restrict__ wptr,
+    const double *__restrict__ sval, const double *__restrict__ x, double *__restrict__ ws,
+    const int *__restrict__ gexp,
     const int *__restrict__ istate, int xcd_chunk KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
@@ -1023,13 +1036,20 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     }
     __syncthreads();
     KLE_PROBE_TS(ts2)
-    // one partial per dictionary entry, [entry][3] (coalesced)
+    // one partial per dictionary entry, [entry][3] (coalesced), from the
+    // group's slot start wptr[g]; aligned slots (spmv_sym_align: 128-B slot
+    // starts) are written to the end of their last line, zeros past the
+    // entries, so every line leaves L2 written whole by one workgroup
     // (probe 64: into 8 slabs; probe >> 12 = R > 0: into a ring of R group slots)
-    double *dst = ws + ((probe & 64) ? (g & 7) * 3 * 2048 : (probe >> 12) ? (g % max(1, probe >> 12)) * 3 * 2048 : (int64_t)d0 * 3);
-    for (int t = (probe & 8) ? 3 * U : threadIdx.x; t < 3 * U; t += NT) {  // (probe 8: no partial stores)
-        const int e = t / 3, c = t - 3 * e;
+    const int64_t w0 = wptr[g];
+    const int nw = (int)(wptr[g + 1] - w0);
+    double *dst = ws + ((probe & 64) ? (g & 7) * 3 * 2048 : (probe >> 12) ? (g % max(1, probe >> 12)) * 3 * 2048 : w0);
+    for (int t = (probe & 8) ? nw : threadIdx.x; t < nw; t += NT) {  // (probe 8: no partial stores)
+        const int tc = min(t, 3 * U - 1);
+        const int e = tc / 3, c = tc - 3 * e;
         double s = DET ? fx_to_d(yi[c * RS + e]) * invS : yl[c * RS + e];
-        if (e < G) s += yd[t];
+        if (e < G) s += yd[tc];
+        if (t >= 3 * U) s = 0.0;
         if (probe & 32)
             __builtin_nontemporal_store(s, dst + t);  // (probe 32: nontemporal partial stores)
         else
@@ -1074,7 +1094,7 @@ __global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, int64_t n
         for (int r = runptr[sl]; r < r1; ++r) {
             const unsigned long long m = rmask[r];
             const bool on = (m >> lane) & 1ull;
-            const double *p = ws + (int64_t)(rstart[r] + (on ? __popcll(m & below) : 0)) * 3;
+            const double *p = ws + (int64_t)rstart[r] + (on ? 3 * __popcll(m & below) : 0);
             const double a0 = p[0], a1 = p[1], a2 = p[2];
             s0 += on ? a0 : 0.0;
             s1 += on ? a1 : 0.0;
@@ -1153,7 +1173,8 @@ static int gsym_build(kle_mat *A)
     if (why.empty() && !(WV == 8 || (WV == 16 && G >= 32)))  // (the kernels instantiated in gsym_spmv)
         why = "symmetric storage: " + std::to_string(G) + "-row groups on " + std::to_string(WV) + " waves";
     const int64_t ng = (n + G - 1) / G, ntot = n + nhi, ns = (ntot + 63) / 64;
-    std::vector<int> rp, cnt, bcol, k0, smu, usz, dptr(ng + 1, 0), glist(ng), dict, runptr(ns + 1, 0), rstart;
+    std::vector<int> rp, cnt, bcol, k0, smu, usz, dptr(ng + 1, 0), wptr(ng + 1, 0), glist(ng), dict, runptr(ns + 1, 0),
+        rstart;
     std::vector<int64_t> svp, sbp;
     std::vector<uint16_t> slid;
     std::vector<unsigned long long> rmask;
@@ -1230,6 +1251,12 @@ static int gsym_build(kle_mat *A)
                     return "symmetric storage: group " + std::to_string(g) + " does not lead with its rows";
         }
         E = dptr[ng];
+        // the partials' slots (doubles): packed, or each group's from a 128-B line
+        for (int64_t g = 0; g < ng; ++g) {
+            const int64_t w = g_tune.spmv_sym_align ? ((3 * (int64_t)usz[g] + 15) & ~int64_t(15)) : 3 * (int64_t)usz[g];
+            if ((int64_t)wptr[g] + w > INT_MAX) return "symmetric storage: partial slots too large";
+            wptr[g + 1] = wptr[g] + (int)w;
+        }
         // the launches: groups whose dictionaries fit US4 slots (4 workgroups
         // per CU), then the rest (US = the largest)
         const int lds1 = (int)(LDS_PER_CU_G * WV / GSYM_CU_WAVES);  // 4 workgroups of 8 waves or 2 of 16 per CU
@@ -1265,7 +1292,7 @@ static int gsym_build(kle_mat *A)
                     dict[dptr[g] + e] = dl[g][e];
                     m |= 1ull << ((dl[g][e] - glo) & 63);
                 }
-                sruns[sl].push_back({dptr[g] + e0, m});
+                sruns[sl].push_back({wptr[g] + 3 * e0, m});  // (the run's first partial, in doubles)
             }
         for (int64_t sl = 0; sl < ns; ++sl) {
             if ((int64_t)runptr[sl] + (int64_t)sruns[sl].size() > INT_MAX) return "symmetric storage: gather runs too many";
@@ -1300,7 +1327,8 @@ static int gsym_build(kle_mat *A)
         hipMalloc(&A->d_sgptr, sizeof(int) * (ns + 1)) != hipSuccess ||
         hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
         hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
-        hipMalloc(&A->d_sws, sizeof(double) * 3 * std::max<int64_t>(E, 1)) != hipSuccess ||
+        hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(wptr[ng], 1)) != hipSuccess ||
+        hipMalloc(&A->d_swptr, sizeof(int) * (ng + 1)) != hipSuccess ||
         hipMalloc(&A->d_stile_e, sizeof(int) * ng) != hipSuccess || hipMalloc(&dk0, sizeof(int) * n) != hipSuccess ||
         (nhi && hipMalloc(&A->d_sgsend, sizeof(double) * 3 * nhi) != hipSuccess) ||
         (nsend && hipMalloc(&A->d_sgrecv, sizeof(double) * nsend) != hipSuccess) ||
@@ -1328,6 +1356,7 @@ static int gsym_build(kle_mat *A)
     KLE_HIP(hipMemcpy(A->d_slid, slid.data(), sizeof(uint16_t) * slid.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sdptr, dptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sdict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_swptr, wptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sglist, glist.data(), sizeof(int) * ng, hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
@@ -1414,7 +1443,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
             lds_set[slot] = lds;
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(64 * WV), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
-                           A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_sval, x->base, A->d_sws,
+                           A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_swptr, A->d_sval, x->base, A->d_sws,
                            A->d_stile_e, istate, g_tune.spmv_xcd_chunk KLE_PROBE_ARG);
     };
     // part 0: the inner groups of both launches, part 1: the others (one
@@ -1518,6 +1547,7 @@ static SymGeo sym_geo(const kle_mat *A)
     g.PY = A->sym_reg[2];
     g.RY = A->sym_reg[3];
     g.RZ = A->sym_reg[4];
+    g.WN = A->sym_wn > 0 ? A->sym_wn : g.RX * g.RY * g.RZ;
     g.ntx = (g.Lx + g.TX - 1) / g.TX;
     g.nty = (g.Ly + g.TY - 1) / g.TY;
     g.ntz = (g.Lz + g.TZ - 1) / g.TZ;
@@ -1816,6 +1846,10 @@ static int sym_build_impl(kle_mat *A)
     A->sym_reg[2] = rg.PY;
     A->sym_reg[3] = rg.RY;
     A->sym_reg[4] = rg.RZ;
+    {
+        const int rn = rg.RX * rg.RY * rg.RZ;
+        A->sym_wn = g_tune.spmv_sym_align ? (rn + 15) & ~15 : rn;
+    }
     const SymGeo g = sym_geo(A);
     const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz;
     auto span = [](int64_t o, int64_t r, int64_t L) { return std::max<int64_t>(0, std::min(o + r, L) - std::max<int64_t>(o, 0)); };
@@ -1826,7 +1860,7 @@ static int sym_build_impl(kle_mat *A)
             for (int tx = 0; tx < g.ntx; ++tx)
                 ents += span(tx * g.TX - g.PX, g.RX, Lx) * span(ty * g.TY - g.PY, g.RY, Ly) *
                         span(t * g.TZ, g.RZ, Lz + hp);
-    nomem = hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.RX * g.RY * g.RZ) != hipSuccess ||
+    nomem = hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.WN) != hipSuccess ||
             hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
             (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
             (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess);
