@@ -90,7 +90,7 @@ const char *kle_last_error(void);
  * default 2, 0 PETSc's plain stop -- KLE_KSP_REFINE),
  * "spmv_sym_waves" (0 auto, 8 or 16 waves per workgroup), "spmv_gsym_rows"
  * (read when the storage of an
- * unstructured K is built: rows per group, 64 default, 32, 16 or 8),
+ * unstructured K is built: rows per group, 64 default, 128, 32, 16 or 8),
  * "spmv_gsym_waves" (read at build: 0 auto = 16 for 64-row groups, else 8;
  * 8 or 16), "spmv_gsym_split" (read at build: the largest dictionary of the
  * first of its two launches; 0 auto).  Every value gives correct results (the

@@ -646,7 +646,8 @@ int kle_set_tuning(const char *key, int value)
         KLE_ARG(value >= 0 && value <= 8, "ksp_refine: 0 .. 8");
         g_tune.ksp_refine = value;
     } else if (k == "spmv_gsym_rows") {
-        KLE_ARG(value == 8 || value == 16 || value == 32 || value == 64, "spmv_gsym_rows: 8, 16, 32 or 64");
+        KLE_ARG(value == 8 || value == 16 || value == 32 || value == 64 || value == 128,
+                "spmv_gsym_rows: 8, 16, 32, 64 or 128");
         g_tune.spmv_gsym_rows = value;
     } else if (k == "spmv_gsym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_gsym_waves: 0, 8 or 16");

@@ -447,8 +447,11 @@ constexpr int PRO_DOT_BLOCKS = 512;
 // start or a flush): alpha, beta from the scalar slots.  A stage that ends the
 // solve (converged, diverged, NaN) skips the update in every workgroup, as the
 // reason word makes every later launch a no-op.
+// (SGPRs capped at 64: the HIP runtime admits waves per SIMD as 512 / SGPRs
+// rounded up to 16, so 71-83 SGPRs held these streaming updates at 5-6 waves
+// per SIMD instead of 8; kle_sym.hip SYM_XL_SGPRS)
 template <bool JAC, bool PRE>
-__global__ __launch_bounds__(KB) void k_pipe_iter(int64_t n, const double *__restrict__ dinv,
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_pipe_iter(int64_t n, const double *__restrict__ dinv,
                                                   const double *__restrict__ nv, double *__restrict__ z,
                                                   double *__restrict__ q, double *__restrict__ sv,
                                                   double *__restrict__ p, double *__restrict__ x,
@@ -536,7 +539,7 @@ __global__ __launch_bounds__(KB) void k_cg_flush(const double *__restrict__ a0, 
 // dot launch [Gd], then  p = u + b p ; s = w + b s ; x += a p ; r -= a s ;
 // u = M r  with the new (r,u), (r,r) partials to pu_out [2][G].
 template <bool JAC, bool PRE>
-__global__ __launch_bounds__(KB) void k_sr_iter(int64_t n, const double *__restrict__ dinv,
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_iter(int64_t n, const double *__restrict__ dinv,
                                                 const double *__restrict__ w, double *__restrict__ u,
                                                 double *__restrict__ p, double *__restrict__ sv,
                                                 double *__restrict__ x, double *__restrict__ r,

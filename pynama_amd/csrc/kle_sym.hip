@@ -263,8 +263,16 @@ __device__ __forceinline__ void sym_wait9(double *v)
                  : "i"(N));
 }
 
+// SGPR cap: the HIP runtime admits workgroups per CU by its own register
+// model, 512 SGPRs per SIMD / the kernel's SGPRs rounded up to 16 (the occupancy
+// API and the dispatcher agree: 106 SGPRs -> 4 waves per SIMD = 2 of these
+// 8-wave workgroups per CU, measured with the probe build's phase timestamps);
+// at <= 80 it admits 6 waves per SIMD = 3 workgroups (75 VGPRs allow 6)
+#ifndef SYM_XL_SGPRS
+#define SYM_XL_SGPRS 80
+#endif
 template <int WV, bool DET, int TY, int TZ>
-__global__ __launch_bounds__(64 * WV, 4) void k_nb_spmv_sym_xl(SymGeo g, const int *__restrict__ srow,
+__global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_SGPRS))) void k_nb_spmv_sym_xl(SymGeo g, const int *__restrict__ srow,
                                                              const int64_t *__restrict__ svptr,
                                                              const double *__restrict__ sval,
                                                              const double *__restrict__ x, double *__restrict__ ws,
@@ -1070,7 +1078,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
 // partial of (y, x) in dpart[blockIdx.x] (k_nb_sym_gather's fixed order).
 // N > 1: the rows past the owned ones (nrows .. ntot-1) are the upper ghost
 // nodes, whose sums go to gsend (the reverse halo's send buffer).
-__global__ __launch_bounds__(256) void k_nb_gsym_gather(int64_t nrows, int64_t ntot, const int *__restrict__ runptr,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb_gsym_gather(int64_t nrows, int64_t ntot, const int *__restrict__ runptr,
                                                         const int *__restrict__ rstart,
                                                         const unsigned long long *__restrict__ rmask,
                                                         const double *__restrict__ ws, double *__restrict__ y,
@@ -1170,7 +1178,7 @@ static int gsym_build(kle_mat *A)
         why = "symmetric storage: slab halo of partial nodes";
     const int G = g_tune.spmv_gsym_rows;
     const int WV = g_tune.spmv_gsym_waves ? g_tune.spmv_gsym_waves : G >= 64 ? 16 : 8;
-    if (why.empty() && !(WV == 8 || (WV == 16 && G >= 32)))  // (the kernels instantiated in gsym_spmv)
+    if (why.empty() && !((WV == 8 && G <= 64) || (WV == 16 && G >= 32)))  // (the kernels instantiated in gsym_spmv)
         why = "symmetric storage: " + std::to_string(G) + "-row groups on " + std::to_string(WV) + " waves";
     const int64_t ng = (n + G - 1) / G, ntot = n + nhi, ns = (ntot + 63) / 64;
     std::vector<int> rp, cnt, bcol, k0, smu, usz, dptr(ng + 1, 0), wptr(ng + 1, 0), glist(ng), dict, runptr(ns + 1, 0),
@@ -1436,7 +1444,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     auto launch = [&](auto kern, int slot, int64_t l0, int64_t nl, int US) {
         if (nl <= 0) return;
         const size_t lds = gsym_lds(US, G);
-        static size_t lds_set[24] = {};  // dynamic LDS above 64 KB must be declared per kernel
+        static size_t lds_set[28] = {};  // dynamic LDS above 64 KB must be declared per kernel
         if (lds > lds_set[slot]) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
@@ -1465,7 +1473,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         else launch2(k_nb_spmv_gsym<false, GG, WW>, SLOT + 2, part);       \
     } else
         GSYM_CASE(8, 8, 0) GSYM_CASE(16, 8, 4) GSYM_CASE(32, 8, 8) GSYM_CASE(32, 16, 12) GSYM_CASE(64, 8, 16)
-        GSYM_CASE(64, 16, 20) {
+        GSYM_CASE(64, 16, 20) GSYM_CASE(128, 16, 24) {
 #undef GSYM_CASE
             return fail(KLE_ERR_SUP, "symmetric SpMV: %d rows per group on %d waves", G, WV);
         }
@@ -2035,3 +2043,19 @@ double sym_spmv_bytes(const kle_mat *A)
 }
 
 }  // namespace kle
+
+#ifdef KLE_PROBE_BUILD
+// probe build only: the occupancy API's resident workgroups per CU for the
+// default symmetric tile kernels at a given dynamic LDS (which: 0 box
+// k_nb_spmv_sym_xl<8,true,4,4>, 1 graph k_nb_spmv_gsym<true,64,16>)
+extern "C" int kle_probe_occupancy(int which, int lds_bytes, int *blocks)
+{
+    using namespace kle;
+    KLE_ARG(blocks && lds_bytes >= 0, "bad arg");
+    const void *f = which == 0 ? reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<8, true, 4, 4>)
+                               : reinterpret_cast<const void *>(&k_nb_spmv_gsym<true, 64, 16>);
+    KLE_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+    KLE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, which == 0 ? 512 : 1024, (size_t)lds_bytes));
+    return 0;
+}
+#endif

@@ -83,6 +83,16 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     finally:
         for k, v in DEFAULTS.items():
             set_tuning(k, v)
+    # partial slots aligned to 128-B lines and written whole (build knob
+    # spmv_sym_align): the same sums in the same order, bitwise
+    set_tuning("spmv_sym_align", 1)
+    try:
+        K.setOption(K.Option.SPD, True)
+        ya = (K * x).getArray().copy()
+    finally:
+        set_tuning("spmv_sym_align", 0)
+    K.setOption(K.Option.SPD, True)
+    np.testing.assert_array_equal(ya, (K * x).getArray())
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)
@@ -313,16 +323,20 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
     try:
         # groups of 16 / 8 rows, one launch or the groups split over two
         # (the larger dictionaries in a second launch with more LDS)
-        for rows, waves, split in ((64, 0, 0), (64, 8, 0), (32, 16, 0), (32, 8, 0), (16, 0, 0), (8, 0, 0),
-                                   (64, 0, 120), (32, 8, 60), (8, 0, 20)):
+        # (align: each group's partials from a 128-B line, written whole)
+        for rows, waves, split, align in ((64, 0, 0, 0), (64, 8, 0, 0), (32, 16, 0, 0), (32, 8, 0, 0),
+                                          (16, 0, 0, 0), (8, 0, 0, 0), (128, 0, 0, 0), (64, 0, 120, 0),
+                                          (32, 8, 60, 0), (8, 0, 20, 0), (128, 0, 200, 0), (64, 0, 0, 1),
+                                          (32, 8, 60, 1)):
             set_tuning("spmv_gsym_rows", rows)
             set_tuning("spmv_gsym_waves", waves)
             set_tuning("spmv_gsym_split", split)
+            set_tuning("spmv_sym_align", align)
             K.setOption(K.Option.SPD, True)
             for det in (1, 0):
                 set_tuning("spmv_sym_det", det)
                 name = K.spmvKernel()
-                want = f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows},{waves or (16 if rows == 64 else 8)}>"
+                want = f"k_nb_spmv_gsym<{'true' if det else 'false'},{rows},{waves or (16 if rows >= 64 else 8)}>"
                 assert name.startswith(want), name
                 y1 = (K * x).getArray().copy()
                 for _ in range(2):
@@ -334,6 +348,7 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
                         np.testing.assert_array_equal(y2, y1)
     finally:
         set_tuning("spmv_sym_det", 1)
+        set_tuning("spmv_sym_align", 0)
         set_tuning("spmv_gsym_rows", 64)
         set_tuning("spmv_gsym_waves", 0)
         set_tuning("spmv_gsym_split", 0)

@@ -51,12 +51,20 @@ def main():
     mat.setDomain(dom)
     mat.build(buildOperators=False)
     K = mat.K
+    K.setOption(K.Option.SPD, True)  # (symmetric storage below spmv_sym_min_rows too)
     kern = K.spmvKernel()
     for k, v in json.loads(a.tuning).items():
         set_tuning(k, v)
     slots = 1 << 20
     set_tuning("spmv_sym_probe_ts", slots)
     lib = load()
+    occ = {}
+    for which in (0, 1):
+        for lds in (0, 16384, 32768, 49152, 65536, 81920):
+            b = C.c_int()
+            if lib.kle_probe_occupancy(which, lds, C.byref(b)) == 0:
+                occ[f"{'box' if which == 0 else 'gsym'}@{lds}"] = b.value
+    print(json.dumps({"occupancy_api_blocks_per_cu": occ}), flush=True)
     x = K.createVecRight()
     x.setArray(np.random.default_rng(3).uniform(-1, 1, x.getLocalSize()))
     y = K.createVecLeft()
