@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
                                                         const double *__restrict__ x, double *__restrict__ y,
                                                         const int *__restrict__ istate, int xcd_chunk)
 {
-    if (istate && istate[I_REASON] != 0) return;
+    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
     constexpr int RC = R * C;
     const int lane = threadIdx.x & 63;
     const int64_t blk = xcd_block(xcd_chunk);
@@ -165,6 +165,7 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane < R) {
         double mine = acc[0];
 #pragma unroll
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
     constexpr int R = 3, C = 3, RC = 9;
     extern __shared__ double xs[];
     __shared__ int ub[WV][6];
-    if (istate && istate[I_REASON] != 0) return;
+    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t blk = xcd_block(xcd_chunk);
     const int64_t nr = rm.na + rm.nb;
@@ -304,6 +305,7 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane < R) {
         double mine = acc[0];
 #pragma unroll
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
 {
     constexpr int R = 3, C = 3, RC = 9;
     extern __shared__ double xs[];
-    if (istate && istate[I_REASON] != 0) return;
+    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t blk = xcd_block(xcd_chunk);
     if (blk >= nga + ngb) return;  // whole workgroup
@@ -394,6 +396,7 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
+    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane < R) {
         double mine = acc[0];
 #pragma unroll
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(64 * WV) void k_aij_spmv(int64_t nrows, const int64
                                                       const double *__restrict__ x, double *__restrict__ y,
                                                       const int *__restrict__ istate, int xcd_chunk)
 {
-    if (istate && istate[I_REASON] != 0) return;
+    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
     const int lane = threadIdx.x & 63;
     const int64_t i = xcd_block(xcd_chunk) * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (i >= nrows) return;
@@ -438,6 +441,7 @@ __global__ __launch_bounds__(64 * WV) void k_aij_spmv(int64_t nrows, const int64
             if (c[u] >= 0) acc += v[u] * x[c[u]];
     }
     acc = wsum(acc);
+    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane == 0) y[i] = acc;
 }
 

@@ -284,8 +284,11 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
     // LDS: x [3][RN] | y [3][RN + 64] (DET: int64; 64 dummy slots per
     // component take the adds of masked lanes) | direct row sums [3][TR]
     extern __shared__ double lds[];
-    if (istate && istate[I_REASON] != 0) return;
     KLE_PROBE_TS(ts0)
+    // the solve's reason word (nonzero: the solve has ended, every kernel is a
+    // no-op): loaded first, tested once the tile's descriptor and x loads are
+    // in flight, so its round trip overlaps theirs instead of delaying them
+    const int stop = istate ? istate[I_REASON] : 0;
     static_assert(TY * TZ == 16, "tiles of 128 rows");
     constexpr int TR = SYM_TX * TY * TZ, NT = 64 * WV;
     constexpr int NQ = SYM_TX * TY / WV;  // row slots per wave and plane
@@ -344,6 +347,7 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
         const double v = x[3 * node + fcc];
         fv[f] = ok ? v : 0.0;
     }
+    if (__builtin_amdgcn_readfirstlane(stop) != 0) return;  // (nothing written yet)
     for (int k = threadIdx.x; k < 3 * RS; k += NT) yl[k] = 0.0;
     for (int k = threadIdx.x; k < 3 * TR; k += NT) yd[k] = 0.0;
     // a row from its packed descriptor (sym_row_desc): no divisions -- the
@@ -675,7 +679,9 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
                                                        double *__restrict__ dpart)
 {
     __shared__ double dred[4];
-    if (istate && istate[I_REASON] != 0) return;
+    // (the reason word: loaded first, tested before the first store -- its
+    // round trip overlaps the partials' loads)
+    const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;
     const int64_t Lxy = (int64_t)g.Lx * g.Ly, n = Lxy * g.Lz;
     const int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= j1 && !xdot) return;
@@ -698,6 +704,7 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
                 s1 += p[g.WN];
                 s2 += p[2 * g.WN];
             }
+    if (stop) return;  // (uniform: the whole workgroup)
     if (j >= n) {
         double *o = gsend + 3 * (j - n);
         o[0] = s0;
@@ -715,7 +722,7 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     y[3 * j + 2] = s2;
     if (xdot) dsum = s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
     }
-    if (!xdot) return;
+    if (!xdot || stop) return;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
     if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;
@@ -930,7 +937,9 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
 {
     KLE_PROBE_CONST
     extern __shared__ double lds[];
-    if (istate && istate[I_REASON] != 0) return;
+    // (the reason word: loaded first, tested after the x fill -- nothing is
+    // written to memory before that)
+    const int stop = istate ? istate[I_REASON] : 0;
     constexpr int NT = 64 * WV, RW = G / WV;
     const int64_t blk = gsym_block(xcd_chunk);
     if (blk >= nlist) return;  // whole workgroup
@@ -964,6 +973,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     for (int t = threadIdx.x; t < 3 * RS; t += NT) yl[t] = 0.0;  // (0.0 is int64 0)
     if (threadIdx.x < 3 * G) yd[threadIdx.x] = 0.0;
     __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(stop) != 0) return;
     KLE_PROBE_TS(ts1)
     double S = 1.0, invS = 1.0;
     if (DET) {
@@ -1086,7 +1096,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
                                                         const double *__restrict__ xdot, double *__restrict__ dpart)
 {
     __shared__ double dred[4];
-    if (istate && istate[I_REASON] != 0) return;
+    const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;  // (tested before the first store)
     const int lane = threadIdx.x & 63;
     const int64_t sl = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t j = sl * 64 + lane;
@@ -1108,6 +1118,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
             s1 += on ? a1 : 0.0;
             s2 += on ? a2 : 0.0;
         }
+        if (stop) return;  // (uniform: the whole workgroup)
         if (j < nrows) {
             y[3 * j] = s0;
             y[3 * j + 1] = s1;
@@ -1120,7 +1131,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
             o[2] = s2;
         }
     }
-    if (!xdot) return;
+    if (!xdot || stop) return;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
     if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;

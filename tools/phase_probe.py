@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "phase"))
     ap.add_argument("--tuning", default="{}", help="JSON of kle_set_tuning knobs (probe bits included)")
+    ap.add_argument("--cg", action="store_true",
+                    help="record the last SpMV of 20 single-reduction CG iterations (the bench's loop: x is the "
+                         "vector the update kernel just wrote) instead of repeated products of one x")
     a = ap.parse_args()
     import numpy as np
 
@@ -70,8 +73,26 @@ def main():
     y = K.createVecLeft()
     ctx = pa.get_ctx()
     os.makedirs(a.out, exist_ok=True)
+    ksp = None
+    if a.cg:
+        from pynama_amd.petsc import KSP, PC
+        ksp = KSP().create()
+        ksp.setType("cg")
+        pc = PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setCGSingleReduction(True)
+        ksp.setOperators(K)
+        ksp.setFixedIterations(20)
+        bvec = K.createVecLeft()
+        bvec.setArray(np.random.default_rng(1).uniform(-1, 1, bvec.getLocalSize()))
+        xs = K.createVecRight()
+        ksp.solve(bvec, xs)
     for rep in range(a.reps + 1):
-        K.mult(x, y)
+        if ksp is not None:
+            ksp.solveContinue(bvec, xs, 20)
+        else:
+            K.mult(x, y)
         ctx.synchronize()
         buf = np.zeros(slots * 8, dtype=np.uint64)
         rc = lib.kle_probe_timestamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_int64(slots))
@@ -99,7 +120,7 @@ def main():
                 "share": {"fill": float(fill.sum() / total.sum()), "loop": float(loop.sum() / total.sum()),
                           "store": float(store.sum() / total.sum())},
                 "last_start_us": float(st.max()), "first_end_us": float(en.min()),
-                "per_xcd": per_xcd, "tuning": json.loads(a.tuning)}
+                "per_xcd": per_xcd, "tuning": json.loads(a.tuning), "cg": a.cg}
         print(json.dumps(summ), flush=True)
         np.save(os.path.join(a.out, f"phase_{a.mesh}_{rep}.npy"), r)
     set_tuning("spmv_sym_probe_ts", 0)

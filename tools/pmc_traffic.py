@@ -26,8 +26,9 @@ def median(d, name):
     right-hand side is formed; the median of the (timed-loop dominated)
     dispatch list is the bench matrix's value."""
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    want = name.replace(" ", "") + "("  # (rocprofv3 names carry "void kle::" and the argument list)
     v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-         if r["Kernel_Name"].replace(" ", "").startswith(name.replace(" ", ""))]
+         if want in r["Kernel_Name"].replace(" ", "").replace("voidkle::", "").replace("kle::", "")]
     if not v:
         raise SystemExit(f"pmc_traffic: no dispatch of {name} in {f}")
     v.sort()
