@@ -633,6 +633,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
+    } else if (k == "spmv_sym_stpol") {
+        KLE_ARG(value >= 0 && value <= 3, "spmv_sym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
+        g_tune.spmv_sym_stpol = value;
+    } else if (k == "spmv_sym_alloc") {
+        KLE_ARG(value >= 0 && value <= 3, "spmv_sym_alloc: bits 1 values, 2 partials");
+        g_tune.spmv_sym_alloc = value;
     } else if (k == "spmv_sym_align") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_align: 0 or 1");
         g_tune.spmv_sym_align = value;
@@ -716,6 +722,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
+    else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
+    else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

@@ -31,6 +31,18 @@ namespace kle {
 // written and read once.
 constexpr int SYM_TX = 8;  // tile rows in x; TY x TZ (8 x 2 or 4 x 4) per matrix: sym_TZ
 constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (one pass over the region)
+
+// The symmetric storage's big arrays (values, tile partials): physically
+// contiguous when g_tune.spmv_sym_alloc asks for it (bit 1 values, bit 2
+// partials; hipDeviceMallocContiguous), else -- or when that fails -- plain.
+static hipError_t sym_malloc(void **p, size_t bytes, int bit)
+{
+    if (g_tune.spmv_sym_alloc & bit) {
+        if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+        (void)hipGetLastError();
+    }
+    return hipMalloc(p, bytes);
+}
 // Lattices: the rows are the owned Lx x Ly x Lz nodes; the columns add zo
 // lattice planes of lower ghosts before them and hp of upper ghosts after
 // them (slab partitions, N > 1: ext layout [lower ghosts | owned | upper]).
@@ -228,6 +240,21 @@ __device__ __forceinline__ double fx_to_d(unsigned long long u)
     return (double)(int)((long long)u >> 32) * 0x1p32 + (double)(unsigned)(u & 0xffffffffull);
 }
 
+// A partial store with a cache policy (spmv_sym_stpol): 0 plain (write-back
+// L2), 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through: the line leaves L2
+// with the store instead of at its eviction under the value stream)
+__device__ __forceinline__ void pst(double *p, double v, int pol)
+{
+    if (pol == 1)
+        __builtin_nontemporal_store(v, p);
+    else if (pol == 2)
+        asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if (pol == 3)
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else
+        *p = v;
+}
+
 // Value loads of one item of k_nb_spmv_sym_xl, issued in inline asm so the
 // compiler's wait bookkeeping cannot drain them: it saw the next item's loads
 // as hazards on registers of the current one and put s_waitcnt vmcnt(0) in
@@ -278,7 +305,7 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
                                                              const double *__restrict__ x, double *__restrict__ ws,
                                                              const int *__restrict__ tile_e,
                                                              const int *__restrict__ istate, int t0,
-                                                             int early KLE_PROBE_PARAM)
+                                                             int early, int stpol KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
     // LDS: x [3][RN] | y [3][RN + 64] (DET: int64; 64 dummy slots per
@@ -579,7 +606,7 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
             if (probe & 32)
                 __builtin_nontemporal_store(v, dst + b * WN + k);
             else
-                dst[b * WN + k] = v;
+                pst(dst + b * WN + k, v, stpol);
         }
     }
     KLE_PROBE_TS_END(t, ts0, ts1, ts2)
@@ -933,7 +960,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
     const int *__restrict__ dptr, const int *__restrict__ dict, const int *__restrict__ wptr,
     const double *__restrict__ sval, const double *__restrict__ x, double *__restrict__ ws,
     const int *__restrict__ gexp,
-    const int *__restrict__ istate, int xcd_chunk KLE_PROBE_PARAM)
+    const int *__restrict__ istate, int xcd_chunk, int stpol KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
     extern __shared__ double lds[];
@@ -1071,7 +1098,7 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
         if (probe & 32)
             __builtin_nontemporal_store(s, dst + t);  // (probe 32: nontemporal partial stores)
         else
-            dst[t] = s;
+            pst(dst + t, s, stpol);
     }
     KLE_PROBE_TS_END(g, ts0, ts1, ts2)
 }
@@ -1337,7 +1364,7 @@ static int gsym_build(kle_mat *A)
     double *rowdiff = nullptr, *rowmax = nullptr;
     const bool nomem =
         hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
-        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
+        sym_malloc(reinterpret_cast<void **>(&A->d_sval), sizeof(double) * std::max<int64_t>(tot, 1), 1) != hipSuccess ||
         hipMalloc(&A->d_srow, sizeof(int) * n) != hipSuccess || hipMalloc(&A->d_sbp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_slid, sizeof(uint16_t) * slid.size()) != hipSuccess ||
         hipMalloc(&A->d_sdptr, sizeof(int) * (ng + 1)) != hipSuccess ||
@@ -1346,7 +1373,7 @@ static int gsym_build(kle_mat *A)
         hipMalloc(&A->d_sgptr, sizeof(int) * (ns + 1)) != hipSuccess ||
         hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
         hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
-        hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(wptr[ng], 1)) != hipSuccess ||
+        sym_malloc(reinterpret_cast<void **>(&A->d_sws), sizeof(double) * std::max<int64_t>(wptr[ng], 1), 2) != hipSuccess ||
         hipMalloc(&A->d_swptr, sizeof(int) * (ng + 1)) != hipSuccess ||
         hipMalloc(&A->d_stile_e, sizeof(int) * ng) != hipSuccess || hipMalloc(&dk0, sizeof(int) * n) != hipSuccess ||
         (nhi && hipMalloc(&A->d_sgsend, sizeof(double) * 3 * nhi) != hipSuccess) ||
@@ -1463,7 +1490,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(64 * WV), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
                            A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_swptr, A->d_sval, x->base, A->d_sws,
-                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk KLE_PROBE_ARG);
+                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_stpol KLE_PROBE_ARG);
     };
     // part 0: the inner groups of both launches, part 1: the others (one
     // rank or no overlap: both parts back to back)
@@ -1818,7 +1845,7 @@ static int sym_build_impl(kle_mat *A)
     int64_t nomem = 0;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_srow, sizeof(int) * std::max<int64_t>(n, 1)) != hipSuccess ||
-        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
+        sym_malloc(reinterpret_cast<void **>(&A->d_sval), sizeof(double) * std::max<int64_t>(tot, 1), 1) != hipSuccess ||
         hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess)
         nomem = 1;
     double dmax = 0.0, vmax = 0.0;
@@ -1879,7 +1906,7 @@ static int sym_build_impl(kle_mat *A)
             for (int tx = 0; tx < g.ntx; ++tx)
                 ents += span(tx * g.TX - g.PX, g.RX, Lx) * span(ty * g.TY - g.PY, g.RY, Ly) *
                         span(t * g.TZ, g.RZ, Lz + hp);
-    nomem = hipMalloc(&A->d_sws, sizeof(double) * ntiles * 3 * g.WN) != hipSuccess ||
+    nomem = sym_malloc(reinterpret_cast<void **>(&A->d_sws), sizeof(double) * ntiles * 3 * g.WN, 2) != hipSuccess ||
             hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
             (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
             (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess);
@@ -1930,7 +1957,7 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
     }
     hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
-                       (int)t0, g_tune.spmv_sym_early KLE_PROBE_ARG);
+                       (int)t0, g_tune.spmv_sym_early, g_tune.spmv_sym_stpol KLE_PROBE_ARG);
 }
 
 static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,
@@ -2067,6 +2094,28 @@ extern "C" int kle_probe_occupancy(int which, int lds_bytes, int *blocks)
                                : reinterpret_cast<const void *>(&k_nb_spmv_gsym<true, 64, 16>);
     KLE_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
     KLE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, f, which == 0 ? 512 : 1024, (size_t)lds_bytes));
+    return 0;
+}
+#endif
+
+#ifdef KLE_PROBE_BUILD
+// probe build only: move the box symmetric storage's values (what 1, copied)
+// or tile-partial workspace (what 2) to a fresh allocation, `shift` bytes into
+// it -- does the SpMV's speed depend on where these arrays land?  The old
+// arrays are not freed (probe runs only).
+extern "C" int kle_probe_realloc(kle_mat *A, int what, long long shift)
+{
+    using namespace kle;
+    KLE_ARG(A && A->d_sval && !A->sym_graph && (what == 1 || what == 2) && shift >= 0 && shift % 8 == 0, "bad arg");
+    const SymGeo g = sym_geo(A);
+    const size_t bytes = what == 1 ? sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1)
+                                   : sizeof(double) * (size_t)g.ntx * g.nty * g.ntz * 3 * g.WN;
+    char *raw = nullptr;
+    KLE_HIP(hipMalloc(&raw, bytes + (size_t)shift));
+    double *np = reinterpret_cast<double *>(raw + shift);
+    double **pp = what == 1 ? &A->d_sval : &A->d_sws;
+    KLE_HIP(hipMemcpy(np, *pp, bytes, hipMemcpyDeviceToDevice));
+    *pp = np;
     return 0;
 }
 #endif
