@@ -93,7 +93,15 @@ const char *kle_last_error(void);
  * unstructured K is built: rows per group, 64 default, 128, 32, 16 or 8),
  * "spmv_gsym_waves" (read at build: 0 auto = 16 for 64-row groups, else 8;
  * 8 or 16), "spmv_gsym_split" (read at build: the largest dictionary of the
- * first of its two launches; 0 auto).  Every value gives correct results (the
+ * first of its two launches; 0 auto), "spmv_sym_place" (read at build, one
+ * rank: fresh copies of the symmetric value array timed against the first,
+ * the fastest kept -- the same values at another physical placement; default
+ * 2, 0 off), "spmv_sym_early" (box tile kernel loads its first items before
+ * x is in LDS; 0 default), "spmv_sym_align" (read at build: partial slots
+ * aligned to 128-B lines; 0 default), "spmv_sym_alloc" (read at build: bit 1
+ * values, bit 2 partials physically contiguous; 0 default), "spmv_sym_stpol"
+ * (partial stores: 0 plain default, 1 nontemporal, 2 sc1, 3 sc0 sc1).
+ * Every value gives correct results (the
  * timing probes of the symmetric SpMV exist only in the tools/ probe build,
  * `make -C pynama_amd/csrc probe`). */
 int kle_set_tuning(const char *key, int value);

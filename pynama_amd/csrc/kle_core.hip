@@ -633,6 +633,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
+    } else if (k == "spmv_sym_place") {
+        KLE_ARG(value >= 0 && value <= 8, "spmv_sym_place: 0 .. 8 fresh copies");
+        g_tune.spmv_sym_place = value;
     } else if (k == "spmv_sym_stpol") {
         KLE_ARG(value >= 0 && value <= 3, "spmv_sym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
         g_tune.spmv_sym_stpol = value;
@@ -724,6 +727,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
     else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
+    else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

@@ -245,7 +245,9 @@ struct kle_mat {
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
     int sym_P = 0, sym_TZ = 2;
-    int sym_wn = 0;  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
+    int sym_wn = 0;
+    double sym_place_us = 0;  // SpMV time of the kept value placement (sym_place), one rank
+    int sym_place_kept = 0;   // which fresh copy was kept (0: the first allocation)  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
     int *d_swptr = nullptr;  // graph: per group, its partials' first double in d_sws (128-B aligned with spmv_sym_align)
     int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
     // graph (unstructured) symmetric storage, one rank (kle_sym.hip gsym_build):
@@ -348,6 +350,7 @@ struct Tuning {
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_align = 0;   // symmetric SpMV partials (read at build): every tile's / group's slot starts on a 128-B line and its lines are written whole (1; measured no faster, r04d) or packed (0)
+    int spmv_sym_place = 2;   // symmetric storage (one rank, read at build): fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_stpol = 0;   // symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
     int spmv_sym_alloc = 0;   // symmetric storage (read at build): bit 1 values, bit 2 tile partials physically contiguous (hipDeviceMallocContiguous)
     int spmv_sym_early = 0;   // symmetric SpMV tiles: the first item's value loads issued with the x fill (1) or after it (0)

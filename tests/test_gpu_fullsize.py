@@ -96,6 +96,21 @@ def test_config2_full_size_matches_oracle(pa):
     its_dev = ksp.getIterationNumber() - ksp.getCorrectionIterations()
     _log(t0, f"device CG: {its_dev} iterations, device true residual {ksp.getTrueRelativeResidual():.3e}")
 
+    # ---- the symmetric values' placement (spmv_sym_place, on by default at
+    # this size): a rebuild without it streams the same bits elsewhere
+    from pynama_amd.runtime import set_tuning
+    K = mat.K
+    assert K.isSymmetricStorage()
+    y1 = (K * vel).getArray().copy()
+    set_tuning("spmv_sym_place", 0)
+    try:
+        K.setOption(K.Option.SPD, False)
+        K.setOption(K.Option.SPD, True)
+        np.testing.assert_array_equal((K * vel).getArray(), y1)
+    finally:
+        set_tuning("spmv_sym_place", 2)
+    del y1
+
     # ---- oracle assembly (mat_fs.py:131-192)
     Ko, Kro, Rwo = om.assemble_fs(on_bd.astype(np.uint8))
     _log(t0, f"oracle assembly: K {Ko.nnz} nnz, Krhs {Kro.nnz}, Rw {Rwo.nnz}")

@@ -93,6 +93,14 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         set_tuning("spmv_sym_align", 0)
     K.setOption(K.Option.SPD, True)
     np.testing.assert_array_equal(ya, (K * x).getArray())
+    # value placement off (spmv_sym_place 0; at >= 256 MB of values it moves
+    # them, test_gpu_fullsize): the same bits
+    set_tuning("spmv_sym_place", 0)
+    try:
+        K.setOption(K.Option.SPD, True)
+        np.testing.assert_array_equal(ya, (K * x).getArray())
+    finally:
+        set_tuning("spmv_sym_place", 2)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)

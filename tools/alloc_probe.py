@@ -60,8 +60,13 @@ def main():
         return ms / c * 1e3
 
     y0 = None
-    plan = [("none", 0)] * 3 + [("ws", 0)] * 8 + [("ws", s) for s in (4096, 65536, 1 << 20, (2 << 20) + 4096)] * 2 \
-        + [("values", 0)] * 6 + [("none", 0)] * 2
+    ap_plan = os.environ.get("ALLOC_PLAN", "values")
+    if ap_plan == "ws":
+        plan = [("none", 0)] * 3 + [("ws", 0)] * 8 + [("ws", s) for s in (4096, 65536, 1 << 20, (2 << 20) + 4096)] * 2 \
+            + [("values", 0)] * 6 + [("none", 0)] * 2
+    else:  # the value array at fresh allocations and byte offsets into them
+        plan = [("none", 0)] * 2 + [("values", s) for s in (0, 0, 0, 0, 0, 0, 256, 4096, 65536, 1 << 20,
+                                                             (2 << 20) + 4096, 0, 0, 0, 0, 0)]
     for what, shift in plan:
         if what != "none":
             rc = lib.kle_probe_realloc(K._h, 1 if what == "values" else 2, shift)
