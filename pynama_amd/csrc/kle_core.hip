@@ -636,6 +636,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_place") {
         KLE_ARG(value >= 0 && value <= 8, "spmv_sym_place: 0 .. 8 fresh copies");
         g_tune.spmv_sym_place = value;
+    } else if (k == "spmv_sym_place_gbps") {
+        KLE_ARG(value >= 0 && value <= 100000, "spmv_sym_place_gbps: 0 .. 100000 GB/s");
+        g_tune.spmv_sym_place_gbps = value;
     } else if (k == "spmv_sym_stpol") {
         KLE_ARG(value >= 0 && value <= 3, "spmv_sym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
         g_tune.spmv_sym_stpol = value;
@@ -728,6 +731,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
     else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
+    else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

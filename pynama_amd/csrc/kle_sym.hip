@@ -1716,20 +1716,26 @@ static int sym_probe(kle_mat *A, double vmax_all, bool &bad)
 static int sym_build_impl(kle_mat *A);
 
 // Placement of the value array (one rank): in one process on one box the
-// same storage streams at two speeds, 429 or 493 us per config-2 SpMV, set
-// by where its 2.3 GB land physically -- moving the values alone reproduces
-// both, moving the partials never does (tools/alloc_probe.py,
-// profiles/r04/ab/values_placement.jsonl; round 3 read this as box-to-box
-// variance).  So the build times the product on the first copy and on
-// g_tune.spmv_sym_place fresh copies (the rejected ones held until the end,
-// so each try lands elsewhere) and keeps the fastest: the same bits at other
-// addresses, a few ms of setup.  Collective-free, hence one rank only.
+// same storage streams at two speeds, ~425 or ~490 us per config-2 SpMV, set
+// by where its 2.3 GB land -- moving the values alone reproduces both, moving
+// the partials never does (tools/alloc_probe.py,
+// profiles/r04/ab/values_placement*.jsonl; round 3 read this as box-to-box
+// variance).  Consecutive allocations tend to share the mode (a fresh bench
+// process: the first three copies all slow), so the build keeps allocating
+// fresh copies -- the rejected ones held until the end, so each lands
+// elsewhere -- until one streams at >= spmv_sym_place_gbps of its algorithmic
+// bytes or g_tune.spmv_sym_place copies (and at most 24 GB, 8 copies) are
+// spent, and keeps the fastest: the same bits at another address, a few ms
+// of setup.  Collective-free (the timed products at N > 1 would exchange
+// halos), hence one rank only.
 int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart);
 static int sym_place(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
     if (g_tune.spmv_sym_place <= 0 || c->nranks > 1 || bytes < (size_t(256) << 20)) return 0;
+    const int max_tries = (int)std::min<size_t>((size_t)g_tune.spmv_sym_place, (size_t(24) << 30) / bytes);
+    const double alg = sym_spmv_bytes(A);
     kle_vec *x = nullptr, *y = nullptr;
     KLE_TRY(vec_alloc(c, A->n_local, A->n_global, A->col_lo, A->ghost_lo, A->ghost_hi, &x));
     int rc = vec_alloc(c, A->m_local, A->m_global, A->row_lo, 0, 0, &y);
@@ -1742,41 +1748,44 @@ static int sym_place(kle_mat *A)
                            A->n_local, A->col_lo, x->d);
         rc = hipGetLastError() == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "placement probe launch failed");
     }
-    auto timed = [&](float &ms) -> int {
+    auto timed = [&](float &us) -> int {  // (per product, the gather included)
         for (int k = 0; k < 2; ++k) KLE_TRY(sym_spmv(A, x, y, nullptr, nullptr));
         KLE_HIP(hipEventRecord(e0, c->stream));
         for (int k = 0; k < 4; ++k) KLE_TRY(sym_spmv(A, x, y, nullptr, nullptr));
         KLE_HIP(hipEventRecord(e1, c->stream));
         KLE_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
         KLE_HIP(hipEventElapsedTime(&ms, e0, e1));
+        us = 250.f * ms;
         return 0;
     };
+    auto fast = [&](float us) { return alg / (1e3 * us) >= g_tune.spmv_sym_place_gbps; };
     float best = 0.f, t = 0.f;
     std::vector<double *> held;
+    std::string trail;
     int tries = 0, kept = 0;
     if (!rc) rc = timed(best);
-    for (int k = 0; k < g_tune.spmv_sym_place && !rc; ++k) {
+    trail = std::to_string((int)best);
+    for (int k = 0; k < max_tries && !rc && !fast(best); ++k) {
         double *nv = nullptr;
         if (hipMalloc(&nv, bytes) != hipSuccess) {
             (void)hipGetLastError();
             break;  // (no room for another copy: keep what we have)
         }
+        held.push_back(nv);
         if (hipMemcpy(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice) != hipSuccess) {
-            held.push_back(nv);
             rc = fail(KLE_ERR_DEVICE, "placement copy failed");
             break;
         }
-        double *old = A->d_sval;
-        A->d_sval = nv;
+        std::swap(A->d_sval, held.back());
         ++tries;
         rc = timed(t);
-        if (!rc && t < 0.97f * best) {
-            held.push_back(old);
+        trail += " " + std::to_string((int)t);
+        if (!rc && t < best) {
             best = t;
             kept = tries;
         } else {
-            A->d_sval = old;
-            held.push_back(nv);
+            std::swap(A->d_sval, held.back());
         }
     }
     (void)hipStreamSynchronize(c->stream);
@@ -1790,9 +1799,9 @@ static int sym_place(kle_mat *A)
         }
     if (const char *e = getenv("KLE_TIMING"))
         if (atoi(e))
-            fprintf(stderr, "[kle sym] value placement: %d fresh copies tried, kept %s (%.1f us per SpMV)\n", tries,
-                    kept ? ("copy " + std::to_string(kept)).c_str() : "the first", 1e3f * best / 4);
-    A->sym_place_us = 1e3 * best / 4;
+            fprintf(stderr, "[kle sym] value placement: us per SpMV %s; kept %s (%.0f GB/s)\n", trail.c_str(),
+                    kept ? ("copy " + std::to_string(kept)).c_str() : "the first", alg / (1e3 * best));
+    A->sym_place_us = best;
     A->sym_place_kept = kept;
     return rc;
 }

@@ -108,7 +108,7 @@ def test_config2_full_size_matches_oracle(pa):
         K.setOption(K.Option.SPD, True)
         np.testing.assert_array_equal((K * vel).getArray(), y1)
     finally:
-        set_tuning("spmv_sym_place", 2)
+        set_tuning("spmv_sym_place", 6)
     del y1
 
     # ---- oracle assembly (mat_fs.py:131-192)

@@ -100,7 +100,7 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         K.setOption(K.Option.SPD, True)
         np.testing.assert_array_equal(ya, (K * x).getArray())
     finally:
-        set_tuning("spmv_sym_place", 2)
+        set_tuning("spmv_sym_place", 6)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)
