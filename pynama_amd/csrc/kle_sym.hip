@@ -1724,7 +1724,7 @@ static int sym_build_impl(kle_mat *A);
 // process: the first three copies all slow), so the build keeps allocating
 // fresh copies -- the rejected ones held until the end, so each lands
 // elsewhere -- until one streams at >= spmv_sym_place_gbps of its algorithmic
-// bytes or g_tune.spmv_sym_place copies (and at most 24 GB, 8 copies) are
+// bytes or g_tune.spmv_sym_place copies (at most 64 GB of them) are
 // spent, and keeps the fastest: the same bits at another address, a few ms
 // of setup.  Collective-free (the timed products at N > 1 would exchange
 // halos), hence one rank only.
@@ -1734,7 +1734,7 @@ static int sym_place(kle_mat *A)
     kle_ctx *c = A->ctx;
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
     if (g_tune.spmv_sym_place <= 0 || c->nranks > 1 || bytes < (size_t(256) << 20)) return 0;
-    const int max_tries = (int)std::min<size_t>((size_t)g_tune.spmv_sym_place, (size_t(24) << 30) / bytes);
+    const int max_tries = (int)std::min<size_t>((size_t)g_tune.spmv_sym_place, (size_t(64) << 30) / bytes);
     const double alg = sym_spmv_bytes(A);
     kle_vec *x = nullptr, *y = nullptr;
     KLE_TRY(vec_alloc(c, A->n_local, A->n_global, A->col_lo, A->ghost_lo, A->ghost_hi, &x));
