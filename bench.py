@@ -460,6 +460,7 @@ def main():
             "stream_copy_gbps": stream,
             "stream_read_gbps": stream_rd,  # read-only streaming ceiling (the SpMV is read-dominated)
             "breakdown_ms_per_iter": brk,
+            "symmetric_value_placement": K.getSymmetricPlacement() if K.isSymmetricStorage() else None,
             "assembly_s": t_asm,
             "mesh_generation_s": t_mesh,
             "setup_s": t_setup,

@@ -379,6 +379,11 @@ int kle_mat_is_structured(const kle_mat *A, int *on);
  * default "spmv_sym_det" they are bitwise reproducible run to run. */
 int kle_mat_set_symmetric(kle_mat *A, int on);
 int kle_mat_get_symmetric(const kle_mat *A, int *on);
+/* The value placement kle_mat_set_symmetric kept (tuning "spmv_sym_place",
+ * one rank, symmetric values >= 256 MB): the timed SpMV of the kept array in
+ * microseconds (0: not timed), how many fresh copies were tried and which
+ * one was kept (0: the array as built). */
+int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

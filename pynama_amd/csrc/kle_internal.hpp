@@ -247,7 +247,8 @@ struct kle_mat {
     int sym_P = 0, sym_TZ = 2;
     int sym_wn = 0;
     double sym_place_us = 0;  // SpMV time of the kept value placement (sym_place), one rank
-    int sym_place_kept = 0;   // which fresh copy was kept (0: the first allocation)  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
+    int sym_place_kept = 0;   // which fresh copy was kept (0: the first allocation)
+    int sym_place_tries = 0;  // fresh copies timed  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
     int *d_swptr = nullptr;  // graph: per group, its partials' first double in d_sws (128-B aligned with spmv_sym_align)
     int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
     // graph (unstructured) symmetric storage, one rank (kle_sym.hip gsym_build):

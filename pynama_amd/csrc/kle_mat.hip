@@ -1457,6 +1457,16 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on)
     return 0;
 }
 
+int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept)
+{
+    KLE_ARG(A && us && tries && kept, "null arg");
+    const bool on = A->d_sval != nullptr;
+    *us = on ? A->sym_place_us : 0.0;
+    *tries = on ? A->sym_place_tries : 0;
+    *kept = on ? A->sym_place_kept : 0;
+    return 0;
+}
+
 int kle_mat_is_structured(const kle_mat *A, int *on)
 {
     KLE_ARG(A && on, "null arg");

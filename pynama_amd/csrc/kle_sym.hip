@@ -773,6 +773,8 @@ void sym_forget(kle_mat *A)
     A->d_sgmask = nullptr;
     A->d_swptr = nullptr;
     A->sym_wn = 0;
+    A->sym_place_us = 0;
+    A->sym_place_tries = A->sym_place_kept = 0;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
     A->sym_graph = 0;
@@ -1803,6 +1805,7 @@ static int sym_place(kle_mat *A)
                     kept ? ("copy " + std::to_string(kept)).c_str() : "the first", alg / (1e3 * best));
     A->sym_place_us = best;
     A->sym_place_kept = kept;
+    A->sym_place_tries = tries;
     return rc;
 }
 

@@ -44,6 +44,7 @@ def test_bench_line_contract():
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["unit"] == d["unit"]
     s = d["solve"]
     assert s["reason"] > 0 and s["true_rel_residual"] <= 2e-10
+    assert d["symmetric_value_placement"] is None  # (below spmv_sym_min_rows: full storage)
 
 
 def test_bench_unstructured_line():
