@@ -93,8 +93,7 @@ const char *kle_last_error(void);
  * unstructured K is built: rows per group, 64 default, 128, 32, 16 or 8),
  * "spmv_gsym_waves" (read at build: 0 auto = 16 for 64-row groups, else 8;
  * 8 or 16), "spmv_gsym_split" (read at build: the largest dictionary of the
- * first of its two launches; 0 auto), "spmv_sym_place" (read at build, one
- * rank: up to this many fresh copies of the symmetric value array timed
+ * first of its two launches; 0 auto), "spmv_sym_place" (read at build: up to this many fresh copies of the symmetric value array timed
  * against the first until one streams "spmv_sym_place_gbps" (default 5200)
  * GB/s of its algorithmic bytes, the fastest kept -- the same values at
  * another placement; default 6, 0 off), "spmv_sym_early" (box tile kernel loads its first items before
@@ -380,7 +379,7 @@ int kle_mat_is_structured(const kle_mat *A, int *on);
 int kle_mat_set_symmetric(kle_mat *A, int on);
 int kle_mat_get_symmetric(const kle_mat *A, int *on);
 /* The value placement kle_mat_set_symmetric kept (tuning "spmv_sym_place",
- * one rank, symmetric values >= 256 MB): the timed SpMV of the kept array in
+ * symmetric values >= 256 MB per rank): the timed SpMV of the kept array in
  * microseconds (0: not timed), how many fresh copies were tried and which
  * one was kept (0: the array as built). */
 int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept);

@@ -1469,7 +1469,9 @@ static int gsym_build(kle_mat *A)
     return done(0);
 }
 
-static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
+// local: the rank's own launches only (tiles and gather, no halo in either
+// direction -- sym_place times the product this way at any N)
+static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart, bool local = false)
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
@@ -1519,7 +1521,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         }
         return 0;
     };
-    if (!dist) {
+    if (!dist || local) {
         KLE_TRY(tiles(0));
         KLE_TRY(tiles(1));
     } else if (ovl) {
@@ -1542,7 +1544,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
                        A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate, dpart && !dist ? x->d : nullptr,
                        dpart);
     KLE_HIP(hipGetLastError());
-    if (!dist) return 0;
+    if (!dist || local) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending
     // rank order of the senders (MPISBAIJ's reverse scatter)
     if (ovl) {
@@ -1728,14 +1730,14 @@ static int sym_build_impl(kle_mat *A);
 // elsewhere -- until one streams at >= spmv_sym_place_gbps of its algorithmic
 // bytes or g_tune.spmv_sym_place copies (at most 64 GB of them) are
 // spent, and keeps the fastest: the same bits at another address, a few ms
-// of setup.  Collective-free (the timed products at N > 1 would exchange
-// halos), hence one rank only.
-int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart);
+// of setup.  At N > 1 each rank times its own launches without the halos
+// (sym_spmv_local): no collective, and every rank's choice is its own.
+static int sym_spmv_local(kle_mat *A, const kle_vec *x, kle_vec *y);
 static int sym_place(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
-    if (g_tune.spmv_sym_place <= 0 || c->nranks > 1 || bytes < (size_t(256) << 20)) return 0;
+    if (g_tune.spmv_sym_place <= 0 || bytes < (size_t(256) << 20)) return 0;
     const int max_tries = (int)std::min<size_t>((size_t)g_tune.spmv_sym_place, (size_t(64) << 30) / bytes);
     const double alg = sym_spmv_bytes(A);
     kle_vec *x = nullptr, *y = nullptr;
@@ -1751,9 +1753,9 @@ static int sym_place(kle_mat *A)
         rc = hipGetLastError() == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "placement probe launch failed");
     }
     auto timed = [&](float &us) -> int {  // (per product, the gather included)
-        for (int k = 0; k < 2; ++k) KLE_TRY(sym_spmv(A, x, y, nullptr, nullptr));
+        for (int k = 0; k < 2; ++k) KLE_TRY(sym_spmv_local(A, x, y));
         KLE_HIP(hipEventRecord(e0, c->stream));
-        for (int k = 0; k < 4; ++k) KLE_TRY(sym_spmv(A, x, y, nullptr, nullptr));
+        for (int k = 0; k < 4; ++k) KLE_TRY(sym_spmv_local(A, x, y));
         KLE_HIP(hipEventRecord(e1, c->stream));
         KLE_HIP(hipEventSynchronize(e1));
         float ms = 0.f;
@@ -2100,6 +2102,20 @@ int sym_dot_parts(const kle_mat *A)
 //         touch; main: the lowest rows, + d_sgrecv last (fixed order: y stays
 //         bitwise reproducible with spmv_sym_det).
 // All RCCL calls stay on the comm stream, in the same order on every rank.
+// The rank's own launches of y = A x (tiles, gather; no halo either way, so
+// y lacks the neighbours' contributions at N > 1): sym_place's timed product.
+static int sym_spmv_local(kle_mat *A, const kle_vec *x, kle_vec *y)
+{
+    if (A->sym_graph) return gsym_spmv(A, x, y, nullptr, nullptr, true);
+    const SymGeo g = sym_geo(A);
+    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz;
+    const bool dist = A->ctx->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    launch_sym_tiles(A, g, x, 0, ntiles, nullptr, A->ctx->stream);
+    launch_sym_gather(A, g, y, 0, A->nrows + (dist ? (int64_t)g.hp * g.Lx * g.Ly : 0), 0, nullptr, A->ctx->stream);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
 int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
