@@ -93,10 +93,12 @@ const char *kle_last_error(void);
  * unstructured K is built: rows per group, 64 default, 128, 32, 16 or 8),
  * "spmv_gsym_waves" (read at build: 0 auto = 16 for 64-row groups, else 8;
  * 8 or 16), "spmv_gsym_split" (read at build: the largest dictionary of the
- * first of its two launches; 0 auto), "spmv_sym_place" (read at build: up to this many fresh copies of the symmetric value array timed
- * against the first until one streams "spmv_sym_place_gbps" (default 5200)
- * GB/s of its algorithmic bytes, the fastest kept -- the same values at
- * another placement; default 6, 0 off), "spmv_sym_early" (box tile kernel loads its first items before
+ * first of its two launches; 0 auto), "spmv_sym_place" (read at build: up
+ * to this many fresh copies of a symmetric value array of at least
+ * "spmv_sym_place_min_mb" (256) MB timed against the first until one streams
+ * "spmv_sym_place_gbps" (5200) GB/s of its algorithmic bytes, the fastest
+ * kept -- the same values at another placement; default 6, 0 off),
+ * "spmv_sym_early" (box tile kernel loads its first items before
  * x is in LDS; 0 default), "spmv_sym_align" (read at build: partial slots
  * aligned to 128-B lines; 0 default), "spmv_sym_alloc" (read at build: bit 1
  * values, bit 2 partials physically contiguous; 0 default), "spmv_sym_stpol"

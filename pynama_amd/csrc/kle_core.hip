@@ -636,6 +636,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_place") {
         KLE_ARG(value >= 0 && value <= 8, "spmv_sym_place: 0 .. 8 fresh copies");
         g_tune.spmv_sym_place = value;
+    } else if (k == "spmv_sym_place_min_mb") {
+        KLE_ARG(value >= 0, "spmv_sym_place_min_mb: >= 0");
+        g_tune.spmv_sym_place_min_mb = value;
     } else if (k == "spmv_sym_place_gbps") {
         KLE_ARG(value >= 0 && value <= 100000, "spmv_sym_place_gbps: 0 .. 100000 GB/s");
         g_tune.spmv_sym_place_gbps = value;
@@ -732,6 +735,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
     else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
     else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;
+    else if (k == "spmv_sym_place_min_mb") *value = g_tune.spmv_sym_place_min_mb;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

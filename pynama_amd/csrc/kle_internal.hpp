@@ -352,6 +352,7 @@ struct Tuning {
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_align = 0;   // symmetric SpMV partials (read at build): every tile's / group's slot starts on a 128-B line and its lines are written whole (1; measured no faster, r04d) or packed (0)
     int spmv_sym_place = 6;   // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
+    int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes
     int spmv_sym_stpol = 0;   // symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
     int spmv_sym_alloc = 0;   // symmetric storage (read at build): bit 1 values, bit 2 tile partials physically contiguous (hipDeviceMallocContiguous)

@@ -1737,7 +1737,7 @@ static int sym_place(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
-    if (g_tune.spmv_sym_place <= 0 || bytes < (size_t(256) << 20)) return 0;
+    if (g_tune.spmv_sym_place <= 0 || bytes < ((size_t)g_tune.spmv_sym_place_min_mb << 20)) return 0;
     const int max_tries = (int)std::min<size_t>((size_t)g_tune.spmv_sym_place, (size_t(64) << 30) / bytes);
     const double alg = sym_spmv_bytes(A);
     kle_vec *x = nullptr, *y = nullptr;

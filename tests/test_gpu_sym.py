@@ -93,8 +93,18 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         set_tuning("spmv_sym_align", 0)
     K.setOption(K.Option.SPD, True)
     np.testing.assert_array_equal(ya, (K * x).getArray())
-    # value placement off (spmv_sym_place 0; at >= 256 MB of values it moves
-    # them, test_gpu_fullsize): the same bits
+    # value placement forced at this size (spmv_sym_place_min_mb 0; by
+    # default from 256 MB of values, test_gpu_fullsize): six fresh copies
+    # timed (a small matrix never streams 5.2 TB/s), one kept -- the same bits
+    set_tuning("spmv_sym_place_min_mb", 0)
+    try:
+        K.setOption(K.Option.SPD, True)
+        pl = K.getSymmetricPlacement()
+        assert pl["fresh_copies_tried"] == 6 and pl["spmv_us"] > 0 and 0 <= pl["kept"] <= 6, pl
+        np.testing.assert_array_equal(ya, (K * x).getArray())
+    finally:
+        set_tuning("spmv_sym_place_min_mb", 256)
+    # value placement off: the same bits
     set_tuning("spmv_sym_place", 0)
     try:
         K.setOption(K.Option.SPD, True)
