@@ -1777,7 +1777,7 @@ static int sym_place(kle_mat *A)
             break;  // (no room for another copy: keep what we have)
         }
         held.push_back(nv);
-        if (hipMemcpy(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice) != hipSuccess) {
+        if (hipMemcpyAsync(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
             rc = fail(KLE_ERR_DEVICE, "placement copy failed");
             break;
         }
