@@ -633,6 +633,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_waves") {
         KLE_ARG(value == 0 || value == 8 || value == 16, "spmv_sym_waves: 0 (auto), 8 or 16");
         g_tune.spmv_sym_waves = value;
+    } else if (k == "spmv_sym_tile64") {
+        KLE_ARG(value >= 0 && value <= 2, "spmv_sym_tile64: 0 auto, 1 always, 2 never");
+        g_tune.spmv_sym_tile64 = value;
+    } else if (k == "spmv_sym_tile64_max") {
+        KLE_ARG(value >= 0, "spmv_sym_tile64_max: >= 0 tiles");
+        g_tune.spmv_sym_tile64_max = value;
     } else if (k == "spmv_sym_place") {
         KLE_ARG(value >= 0 && value <= 8, "spmv_sym_place: 0 .. 8 fresh copies");
         g_tune.spmv_sym_place = value;
@@ -734,6 +740,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
     else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
+    else if (k == "spmv_sym_tile64") *value = g_tune.spmv_sym_tile64;
+    else if (k == "spmv_sym_tile64_max") *value = g_tune.spmv_sym_tile64_max;
     else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;
     else if (k == "spmv_sym_place_min_mb") *value = g_tune.spmv_sym_place_min_mb;
 #ifdef KLE_PROBE_BUILD

@@ -244,7 +244,7 @@ struct kle_mat {
     int *d_srow = nullptr;     // per row: offset in its box and box extents, 4 bits each (the SpMV's row set-up)
     double *d_sgsend = nullptr, *d_sgrecv = nullptr;  // N > 1 reverse halo: upper ghost rows' sums out, lowest rows' in
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
-    int sym_P = 0, sym_TZ = 2;
+    int sym_P = 0, sym_TZ = 2, sym_TY = 8;
     int sym_wn = 0;
     double sym_place_us = 0;  // SpMV time of the kept value placement (sym_place), one rank
     int sym_place_kept = 0;   // which fresh copy was kept (0: the first allocation)
@@ -351,6 +351,8 @@ struct Tuning {
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_align = 0;   // symmetric SpMV partials (read at build): every tile's / group's slot starts on a 128-B line and its lines are written whole (1; measured no faster, r04d) or packed (0)
+    int spmv_sym_tile64 = 0;        // symmetric box storage (read at build): 8 x 2 x 4 tiles (64 rows) -- 0 auto (below spmv_sym_tile64_max 128-row tiles), 1 always, 2 never
+    int spmv_sym_tile64_max = 0;    // ... (set from measurements)
     int spmv_sym_place = 6;   // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes

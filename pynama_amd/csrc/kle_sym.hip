@@ -29,7 +29,7 @@ namespace kle {
 // 2 x 2 x (P/TZ+2)) tiles whose regions contain it, in a fixed tile order.
 // HBM: the stored values once (half of the full storage) + the partials
 // written and read once.
-constexpr int SYM_TX = 8;  // tile rows in x; TY x TZ (8 x 2 or 4 x 4) per matrix: sym_TZ
+constexpr int SYM_TX = 8;  // tile rows in x; TY x TZ (8 x 2, 4 x 4 or 2 x 4) per matrix: sym_TY, sym_TZ
 constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (one pass over the region)
 
 // The symmetric storage's big arrays (values, tile partials): physically
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
     // no-op): loaded first, tested once the tile's descriptor and x loads are
     // in flight, so its round trip overlaps theirs instead of delaying them
     const int stop = istate ? istate[I_REASON] : 0;
-    static_assert(TY * TZ == 16, "tiles of 128 rows");
+    static_assert(TY * TZ == 16 || TY * TZ == 8, "tiles of 128 or 64 rows");
     constexpr int TR = SYM_TX * TY * TZ, NT = 64 * WV;
     constexpr int NQ = SYM_TX * TY / WV;  // row slots per wave and plane
     constexpr int NS = NQ * TZ;               // row slots per wave
@@ -1584,7 +1584,7 @@ static SymGeo sym_geo(const kle_mat *A)
     const int P = A->sym_P;
     g.TX = SYM_TX;
     g.TZ = A->sym_TZ;
-    g.TY = 16 / g.TZ;
+    g.TY = A->sym_TY;
     g.Lx = (int)A->row_lat[0];
     g.Ly = (int)A->row_lat[1];
     g.Lz = (int)A->row_lat[2];
@@ -1842,8 +1842,11 @@ static int sym_build_impl(kle_mat *A)
     int P = 0;
     // reach of the rows' upper triangles relative to their tile's origin, per
     // tile shape (0: 8 x 4 x 4, 1: 8 x 8 x 2): x / y low, x / y / z high
-    const int shape_ty[2] = {4, 8}, shape_tz[2] = {4, 2};
-    int64_t rlo[2][2] = {{0, 0}, {0, 0}}, rhi[2][3] = {{SYM_TX - 1, 3, 3}, {SYM_TX - 1, 7, 1}};
+    // tile shapes (rows TX x TY x TZ): 8 x 4 x 4, 8 x 8 x 2, and 8 x 2 x 4 (64 rows)
+    constexpr int NSH = 3;
+    const int shape_ty[NSH] = {4, 8, 2}, shape_tz[NSH] = {4, 2, 4};
+    int64_t rlo[NSH][2] = {{0, 0}, {0, 0}, {0, 0}},
+            rhi[NSH][3] = {{SYM_TX - 1, 3, 3}, {SYM_TX - 1, 7, 1}, {SYM_TX - 1, 1, 3}};
     int64_t tot = 0, blocks = 0, all = 0, up_ghost = 0, lo_ghost = 0;
     if (why.empty()) {
         rb.resize(2 * n);
@@ -1880,7 +1883,7 @@ static int sym_build_impl(kle_mat *A)
                 // whole box, the row's own plane the lines from its own on
                 const int64_t uz1 = bz + bnz - 1, uy1 = by + bny - 1, ux1 = bx + bnx - 1;
                 const int64_t uy0 = uz1 > z ? by : y, ux0 = uz1 > z || uy1 > y ? bx : x;
-                for (int s = 0; s < 2; ++s) {
+                for (int s = 0; s < NSH; ++s) {
                     const int64_t x0 = x / SYM_TX * SYM_TX, y0 = y / shape_ty[s] * shape_ty[s];
                     const int64_t z0 = (z - zo) / shape_tz[s] * shape_tz[s] + zo;
                     rlo[s][0] = std::min(rlo[s][0], ux0 - x0);
@@ -1908,8 +1911,8 @@ static int sym_build_impl(kle_mat *A)
             why = "symmetric storage: the block pattern is not symmetric (" + std::to_string(all) + " blocks, " +
                   std::to_string(blocks) + " upper)";
     }
-    SymRegion reg[2];
-    for (int s = 0; s < 2; ++s)
+    SymRegion reg[NSH];
+    for (int s = 0; s < NSH; ++s)
         reg[s] = {(int)-rlo[s][0], (int)(rhi[s][0] - rlo[s][0] + 1), (int)-rlo[s][1], (int)(rhi[s][1] - rlo[s][1] + 1),
                   (int)(rhi[s][2] + 1)};
     if (why.empty() && sym_xl_lds(reg[1]) > LDS_PER_CU)
@@ -1920,9 +1923,18 @@ static int sym_build_impl(kle_mat *A)
     // 1536-node region, but a 4-plane tile spans a whole p = 4 element layer,
     // so every tile holds the same mix of row lengths (rows on element-
     // boundary planes carry 4 planes of upper blocks, the next ones 3, 2, 1)
+    // 8 x 2 x 4 (64 rows, still a whole element layer deep): where the
+    // 128-row tiles would not fill the chip -- a small part (z slab at N > 1)
+    // whose few heavy tiles set the kernel's length (spmv_sym_tile64: 0 auto
+    // below spmv_sym_tile64_max 128-row tiles, 1 wherever 8 x 4 x 4 fits, 2 never)
     const int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(reg[0]) <= LDS_PER_CU &&
                            sym_fill_fits(reg[0], 8) ? 4 : 2;
-    const SymRegion &rg = reg[TZ == 4 ? 0 : 1];
+    int TY = TZ == 4 ? 4 : 8;
+    if (TZ == 4 && g_tune.spmv_sym_tile64 != 2 && sym_fill_fits(reg[2], 8)) {
+        const int64_t t128 = ((Lx + SYM_TX - 1) / SYM_TX) * ((Ly + 3) / 4) * ((Lz + 3) / 4);
+        if (g_tune.spmv_sym_tile64 == 1 || t128 < g_tune.spmv_sym_tile64_max) TY = 2;
+    }
+    const SymRegion &rg = reg[TZ == 2 ? 1 : TY == 4 ? 0 : 2];
     bool any = false;
     KLE_TRY(any_rank(c, !why.empty(), any));
     if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
@@ -1984,6 +1996,7 @@ static int sym_build_impl(kle_mat *A)
     }
     A->sym_P = P;
     A->sym_TZ = TZ;
+    A->sym_TY = TY;
     A->sym_reg[0] = rg.PX;
     A->sym_reg[1] = rg.RX;
     A->sym_reg[2] = rg.PY;
@@ -2040,7 +2053,7 @@ static int sym_waves(const kle_mat *A)
     return 2 * sym_xl_lds(r) <= LDS_PER_CU && sym_fill_fits(r, 8) ? 8 : 16;
 }
 
-template <int WV, bool DET, int TZ>
+template <int WV, bool DET, int TY, int TZ>
 static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,
                           const int *istate, hipStream_t st)
 {
@@ -2048,11 +2061,11 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
     const size_t lds = sym_xl_lds(sym_region(A));
     static size_t lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
     if (lds > lds_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, TY, TZ>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         lds_set = lds;
     }
-    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, 16 / TZ, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
+    hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, TY, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
                        (int)t0, g_tune.spmv_sym_early, g_tune.spmv_sym_stpol KLE_PROBE_ARG);
 }
@@ -2061,15 +2074,18 @@ static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x
                              const int *istate, hipStream_t st)
 {
     const bool det = g_tune.spmv_sym_det != 0;
-    if (g.TZ == 4) {
-        if (det) launch_sym_xl<8, true, 4>(A, g, x, t0, t1, istate, st);
-        else launch_sym_xl<8, false, 4>(A, g, x, t0, t1, istate, st);
+    if (g.TZ == 4 && g.TY == 2) {
+        if (det) launch_sym_xl<8, true, 2, 4>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<8, false, 2, 4>(A, g, x, t0, t1, istate, st);
+    } else if (g.TZ == 4) {
+        if (det) launch_sym_xl<8, true, 4, 4>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<8, false, 4, 4>(A, g, x, t0, t1, istate, st);
     } else if (sym_waves(A) == 16) {
-        if (det) launch_sym_xl<16, true, 2>(A, g, x, t0, t1, istate, st);
-        else launch_sym_xl<16, false, 2>(A, g, x, t0, t1, istate, st);
+        if (det) launch_sym_xl<16, true, 8, 2>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<16, false, 8, 2>(A, g, x, t0, t1, istate, st);
     } else {
-        if (det) launch_sym_xl<8, true, 2>(A, g, x, t0, t1, istate, st);
-        else launch_sym_xl<8, false, 2>(A, g, x, t0, t1, istate, st);
+        if (det) launch_sym_xl<8, true, 8, 2>(A, g, x, t0, t1, istate, st);
+        else launch_sym_xl<8, false, 8, 2>(A, g, x, t0, t1, istate, st);
     }
 }
 
@@ -2079,7 +2095,10 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 {
     if (j1 <= j0) return;
     const dim3 grid((unsigned)((j1 - j0 + 255) / 256));
-    if (g.TZ == 4)
+    if (g.TZ == 4 && g.TY == 2)
+        hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 2, 4>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
+                           A->d_sgrecv, nrecv, j0, j1, istate, xdot, dpart);
+    else if (g.TZ == 4)
         hipLaunchKernelGGL((k_nb_sym_gather<SYM_TX, 4, 4>), grid, dim3(256), 0, st, g, A->d_sws, y->d, A->d_sgsend,
                            A->d_sgrecv, nrecv, j0, j1, istate, xdot, dpart);
     else
@@ -2173,8 +2192,8 @@ std::string sym_kernel_name(const kle_mat *A)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
                std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
-           (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(16 / A->sym_TZ) + "," +
-           std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(16 / A->sym_TZ) + "," +
+           (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(A->sym_TY) + "," +
+           std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(A->sym_TY) + "," +
            std::to_string(A->sym_TZ) + ">";
 }
 

@@ -93,6 +93,22 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         set_tuning("spmv_sym_align", 0)
     K.setOption(K.Option.SPD, True)
     np.testing.assert_array_equal(ya, (K * x).getArray())
+    # 8 x 2 x 4 tiles (64 rows; spmv_sym_tile64 1 forces them wherever the
+    # 4-plane shape is used, the default picks them for parts of few tiles):
+    # the same products to rounding, bitwise reproducible
+    set_tuning("spmv_sym_tile64", 1)
+    try:
+        K.setOption(K.Option.SPD, True)
+        name = K.spmvKernel()
+        y64 = (K * x).getArray().copy()
+        np.testing.assert_array_equal((K * x).getArray(), y64)
+        for ref in (y0, yh):
+            assert np.linalg.norm(y64 - ref) <= 1e-14 * np.linalg.norm(ref)
+            assert np.abs(y64 - ref).max() <= 1e-13 * np.abs(ref).max()
+        assert ",8,2>" in name or name == "k_nb_spmv_sym_xl<8,true,2,4>+k_nb_sym_gather<8,2,4>", name
+    finally:
+        set_tuning("spmv_sym_tile64", 0)
+    K.setOption(K.Option.SPD, True)
     # value placement forced at this size (spmv_sym_place_min_mb 0; by
     # default from 256 MB of values, test_gpu_fullsize): six fresh copies
     # timed (a small matrix never streams 5.2 TB/s), one kept -- the same bits
