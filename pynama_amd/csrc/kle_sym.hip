@@ -1927,14 +1927,20 @@ static int sym_build_impl(kle_mat *A)
     // 128-row tiles would not fill the chip -- a small part (z slab at N > 1)
     // whose few heavy tiles set the kernel's length (spmv_sym_tile64: 0 auto
     // below spmv_sym_tile64_max 128-row tiles, 1 wherever 8 x 4 x 4 fits, 2 never)
-    const int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(reg[0]) <= LDS_PER_CU &&
-                           sym_fill_fits(reg[0], 8) ? 4 : 2;
+    // (P >= 5, where 8 x 4 x 4 regions do not fit two workgroups per CU, the
+    // 64-row tiles still may: forced only, spmv_sym_tile64 1)
+    int TZ = g_tune.spmv_sym_tz != 2 && why.empty() && 2 * sym_xl_lds(reg[0]) <= LDS_PER_CU &&
+                     sym_fill_fits(reg[0], 8) ? 4 : 2;
     int TY = TZ == 4 ? 4 : 8;
-    if (TZ == 4 && g_tune.spmv_sym_tile64 != 2 && sym_fill_fits(reg[2], 8)) {
+    if (g_tune.spmv_sym_tile64 != 2 && why.empty() && 2 * sym_xl_lds(reg[2]) <= LDS_PER_CU &&
+        sym_fill_fits(reg[2], 8)) {
         const int64_t t128 = ((Lx + SYM_TX - 1) / SYM_TX) * ((Ly + 3) / 4) * ((Lz + 3) / 4);
-        if (g_tune.spmv_sym_tile64 == 1 || t128 < g_tune.spmv_sym_tile64_max) TY = 2;
+        if (g_tune.spmv_sym_tile64 == 1 || (TZ == 4 && t128 < g_tune.spmv_sym_tile64_max)) {
+            TZ = 4;
+            TY = 2;
+        }
     }
-    const SymRegion &rg = reg[TZ == 2 ? 1 : TY == 4 ? 0 : 2];
+    const SymRegion &rg = reg[TY == 2 ? 2 : TZ == 4 ? 0 : 1];
     bool any = false;
     KLE_TRY(any_rank(c, !why.empty(), any));
     if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());

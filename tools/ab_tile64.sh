@@ -11,3 +11,8 @@ for lib in pynama_amd/libkle.so tools/libkle_nocap.so; do
     KLE_LIBRARY=$PWD/$lib timeout -k 10 300 python -u tools/spmv_ab.py "$V" --nelem $ne --reps 4 --its $its
   done
 done
+# config 4 (p = 6): 8 x 8 x 2 tiles on 16 waves (one workgroup per CU) vs 64-row tiles on 8 waves (two per CU)
+for lib in pynama_amd/libkle.so tools/libkle_nocap.so; do
+  echo "{\"lib\": \"$lib\", \"nelem\": \"18,18,18 ngl 7\"}"
+  KLE_LIBRARY=$PWD/$lib timeout -k 10 400 python -u tools/spmv_ab.py '[{},{"spmv_sym_tile64":1}]' --nelem 18,18,18 --ngl 7 --reps 3 --its 20
+done
