@@ -98,7 +98,9 @@ const char *kle_last_error(void);
  * "spmv_sym_place_min_mb" (256) MB timed against the first until one streams
  * "spmv_sym_place_gbps" (5200) GB/s of its algorithmic bytes, the fastest
  * kept -- the same values at another placement; default 6, 0 off),
- * "spmv_sym_early" (box tile kernel loads its first items before
+ * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
+ * "spmv_sym_tile64_max" (800) 128-row tiles; 1 wherever two workgroups fit
+ * a CU; 2 never), "spmv_sym_early" (box tile kernel loads its first items before
  * x is in LDS; 0 default), "spmv_sym_align" (read at build: partial slots
  * aligned to 128-B lines; 0 default), "spmv_sym_alloc" (read at build: bit 1
  * values, bit 2 partials physically contiguous; 0 default), "spmv_sym_stpol"

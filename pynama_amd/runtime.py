@@ -250,6 +250,8 @@ def get_ctx():
             set_tuning("spmv_sym_min_rows", int(os.environ["KLE_SPMV_SYM_MIN_ROWS"]))
         if os.environ.get("KLE_SPMV_DICT_MIN_ROWS"):
             set_tuning("spmv_dict_min_rows", int(os.environ["KLE_SPMV_DICT_MIN_ROWS"]))
+        if os.environ.get("KLE_SPMV_SYM_TILE64"):
+            set_tuning("spmv_sym_tile64", int(os.environ["KLE_SPMV_SYM_TILE64"]))
         if os.environ.get("KLE_SPMV_SYM_PLACE_MIN_MB"):
             set_tuning("spmv_sym_place_min_mb", int(os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"]))
         if os.environ.get("KLE_KSP_REFINE"):

@@ -143,6 +143,20 @@ def test_partitioned_solve_symmetric_storage(size, nelem, ngl, ksp_type, overlap
         assert r["kernel"].startswith("k_nb_spmv_sym_xl<"), r["kernel"]
 
 
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(2, [3, 2, 4], 5, "cg"), (3, [2, 3, 3], 3, "pipecg")])
+def test_partitioned_symmetric_storage_128_row_tiles(size, nelem, ngl, ksp_type):
+    """The 128-row tiles (8 x 4 x 4) on slabs: test-size parts take the 64-row
+    tiles by default (spmv_sym_tile64_max), so KLE_SPMV_SYM_TILE64=2 forces the
+    shape config-2-sized slabs run; same checks as above."""
+    os.environ["KLE_SPMV_SYM_TILE64"] = "2"  # inherited by the spawned ranks
+    try:
+        res = _check_box(size, nelem, ngl, True, ksp_type, sym=True)
+    finally:
+        del os.environ["KLE_SPMV_SYM_TILE64"]
+    for r in res:
+        assert r["kernel"] == "k_nb_spmv_sym_xl<8,true,4,4>+k_nb_sym_gather<8,4,4>", r["kernel"]
+
+
 def test_partitioned_symmetric_value_placement(tmp_path):
     """Value placement (spmv_sym_place) at N > 1, forced at test size
     (KLE_SPMV_SYM_PLACE_MIN_MB=0): every rank times its own tile and gather

@@ -93,21 +93,28 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         set_tuning("spmv_sym_align", 0)
     K.setOption(K.Option.SPD, True)
     np.testing.assert_array_equal(ya, (K * x).getArray())
-    # 8 x 2 x 4 tiles (64 rows; spmv_sym_tile64 1 forces them wherever the
-    # 4-plane shape is used, the default picks them for parts of few tiles):
-    # the same products to rounding, bitwise reproducible
-    set_tuning("spmv_sym_tile64", 1)
-    try:
-        K.setOption(K.Option.SPD, True)
-        name = K.spmvKernel()
-        y64 = (K * x).getArray().copy()
-        np.testing.assert_array_equal((K * x).getArray(), y64)
-        for ref in (y0, yh):
-            assert np.linalg.norm(y64 - ref) <= 1e-14 * np.linalg.norm(ref)
-            assert np.abs(y64 - ref).max() <= 1e-13 * np.abs(ref).max()
-        assert ",8,2>" in name or name == "k_nb_spmv_sym_xl<8,true,2,4>+k_nb_sym_gather<8,2,4>", name
-    finally:
-        set_tuning("spmv_sym_tile64", 0)
+    # tile shapes: 8 x 2 x 4 (64 rows; spmv_sym_tile64 1 forces them where two
+    # workgroups fit a CU, the default picks them for parts of < 800 128-row
+    # tiles -- every matrix here) and never (2: 8 x 4 x 4, or 8 x 8 x 2 at
+    # p >= 5): the same products to rounding, each bitwise reproducible
+    shapes = {}
+    for mode in (1, 2):
+        set_tuning("spmv_sym_tile64", mode)
+        try:
+            K.setOption(K.Option.SPD, True)
+            name = K.spmvKernel()
+            ys = (K * x).getArray().copy()
+            np.testing.assert_array_equal((K * x).getArray(), ys)
+            for ref in (y0, yh):
+                assert np.linalg.norm(ys - ref) <= 1e-14 * np.linalg.norm(ref), name
+                assert np.abs(ys - ref).max() <= 1e-13 * np.abs(ref).max(), name
+            shapes[mode] = name
+        finally:
+            set_tuning("spmv_sym_tile64", 0)
+    assert ",8,2>" in shapes[1] or shapes[1] == "k_nb_spmv_sym_xl<8,true,2,4>+k_nb_sym_gather<8,2,4>", shapes
+    assert shapes[2] in ("k_nb_spmv_sym_xl<8,true,4,4>+k_nb_sym_gather<8,4,4>",
+                         "k_nb_spmv_sym_xl<8,true,8,2>+k_nb_sym_gather<8,8,2>",
+                         "k_nb_spmv_sym_xl<16,true,8,2>+k_nb_sym_gather<8,8,2>"), shapes
     K.setOption(K.Option.SPD, True)
     # value placement forced at this size (spmv_sym_place_min_mb 0; by
     # default from 256 MB of values, test_gpu_fullsize): six fresh copies
