@@ -81,7 +81,7 @@ const char *kle_last_error(void);
  * before the prologue; 0 off), "spmv_sym" (1 default: matrices holding
  * symmetric storage run the symmetric SpMV; 0 the full storage),
  * "spmv_sym_min_rows" (node rows per rank from which kle_assemble_kle gives
- * K symmetric storage; default 64000), "spmv_sym_tz" (read when the storage
+ * K symmetric storage; default 40000), "spmv_sym_tz" (read when the storage
  * is built: 0 auto = 8 x 4 x 4-row tiles where two 8-wave workgroups fit a
  * CU, 2 = 8 x 8 x 2, 4 = 8 x 4 x 4), "spmv_sym_det" (1
  * default: the transposed adds as exact fixed-point sums, y bitwise
@@ -100,7 +100,9 @@ const char *kle_last_error(void);
  * kept -- the same values at another placement; default 6, 0 off),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (800) 128-row tiles; 1 wherever two workgroups fit
- * a CU; 2 never), "spmv_sym_early" (box tile kernel loads its first items before
+ * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo
+ * overlap: the percentage of the interior tiles run beside the reverse halo,
+ * the rest beside the forward halo; default 50), "spmv_sym_early" (box tile kernel loads its first items before
  * x is in LDS; 0 default), "spmv_sym_align" (read at build: partial slots
  * aligned to 128-B lines; 0 default), "spmv_sym_alloc" (read at build: bit 1
  * values, bit 2 partials physically contiguous; 0 default), "spmv_sym_stpol"

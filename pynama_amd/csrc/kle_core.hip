@@ -639,6 +639,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tile64_max") {
         KLE_ARG(value >= 0, "spmv_sym_tile64_max: >= 0 tiles");
         g_tune.spmv_sym_tile64_max = value;
+    } else if (k == "spmv_sym_ovl_b") {
+        KLE_ARG(value >= 0 && value <= 100, "spmv_sym_ovl_b: 0 .. 100 %");
+        g_tune.spmv_sym_ovl_b = value;
     } else if (k == "spmv_sym_place") {
         KLE_ARG(value >= 0 && value <= 8, "spmv_sym_place: 0 .. 8 fresh copies");
         g_tune.spmv_sym_place = value;
@@ -740,6 +743,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
     else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
+    else if (k == "spmv_sym_ovl_b") *value = g_tune.spmv_sym_ovl_b;
     else if (k == "spmv_sym_tile64") *value = g_tune.spmv_sym_tile64;
     else if (k == "spmv_sym_tile64_max") *value = g_tune.spmv_sym_tile64_max;
     else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;

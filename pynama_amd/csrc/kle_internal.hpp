@@ -347,12 +347,13 @@ struct Tuning {
     int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
     int spmv_sym = 1;  // SBAIJ-style symmetric storage for the KLE K of >= spmv_sym_min_rows node rows per rank; 0 off
-    int spmv_sym_min_rows = 64000;
+    int spmv_sym_min_rows = 40000;  // (the 1/8 parts of config 2: box slab 76.75 vs 78.29 us per pipelined CG iteration, unstructured 77.0 vs 79.8 us per SpMV; profiles/r04/ab/small_parts.jsonl)
     int spmv_sym_det = 1;     // symmetric SpMV: transposed adds as exact fixed-point sums (bitwise reproducible); 0 fp64 LDS atomics
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_align = 0;   // symmetric SpMV partials (read at build): every tile's / group's slot starts on a 128-B line and its lines are written whole (1; measured no faster, r04d) or packed (0)
     int spmv_sym_tile64 = 0;        // symmetric box storage (read at build): 8 x 2 x 4 tiles (64 rows) -- 0 auto (below spmv_sym_tile64_max 128-row tiles), 1 always, 2 never
     int spmv_sym_tile64_max = 800;  // ... 1/8 of config 2 (561 tiles) 75.6 -> 70.6 us (full storage 72.4), 1/4 (935) 121.2 vs 127.8 (profiles/r04/ab/tile64_and_sgpr_ab.jsonl)
+    int spmv_sym_ovl_b = 50;        // N > 1 symmetric box SpMV: % of the interior tiles run beside the reverse halo
     int spmv_sym_place = 6;   // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes

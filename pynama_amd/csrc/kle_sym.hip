@@ -2155,15 +2155,23 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
         KLE_HIP(hipGetLastError());
         return 0;
     }
-    // tiles [0, nin): regions below the owned top (no upper ghost x)
+    // tiles [0, nin): regions below the owned top (no upper ghost x).  With
+    // overlap they run in two parts: [0, nA) beside the forward halo, then
+    // the top tiles (the only ones whose regions hold upper ghost rows) and
+    // the ghost rows' sums, then [nA, nin) beside the reverse halo -- so the
+    // reverse halo's latency hides behind tile work too, not only behind the
+    // gather (spmv_sym_ovl_b: the percentage of the interior tiles kept for
+    // the second part).  Tile partials do not depend on the launch order,
+    // and the gather sums them in a fixed order: y is bitwise the plain one.
     const int64_t ntz_in = g.Lz >= g.RZ ? (g.Lz - g.RZ) / g.TZ + 1 : 0;
     const int64_t nin = std::min(ntiles, ntz_in * g.nty * g.ntx);
     const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0, jr = nrecv / 3;
     const bool ovl = A->halo_overlap != 0;
+    const int64_t nA = ovl && A->hi_rank >= 0 ? nin - nin * g_tune.spmv_sym_ovl_b / 100 : nin;
     if (ovl) {
         KLE_HIP(hipEventRecord(c->ev_x_ready, st));
         KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
-        launch_sym_tiles(A, g, x, 0, nin, istate, st);
+        launch_sym_tiles(A, g, x, 0, nA, istate, st);
         KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
                               x->send_hi, c->comm_stream, nullptr));
         KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
@@ -2181,6 +2189,7 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
         KLE_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_x_ready, 0));
         KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, c->comm_stream));
         KLE_HIP(hipEventRecord(c->ev_halo_done, c->comm_stream));
+        launch_sym_tiles(A, g, x, nA, nin, istate, st);
         launch_sym_gather(A, g, y, jr, n, 0, istate, st);
         KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
         launch_sym_gather(A, g, y, 0, jr, nrecv, istate, st);

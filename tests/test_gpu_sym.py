@@ -49,7 +49,11 @@ DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_waves": 0}
 def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     _, mat = _mat(pa, nelem, ngl)
     K = mat.K
-    assert not K.isSymmetricStorage()  # below spmv_sym_min_rows: full storage
+    from pynama_amd.runtime import get_tuning
+    # (assembled with symmetric storage from spmv_sym_min_rows node rows)
+    assert K.isSymmetricStorage() == (K.getSize()[0] // 3 >= get_tuning("spmv_sym_min_rows"))
+    K.setOption(K.Option.SPD, False)
+    assert not K.isSymmetricStorage()
     x = K.createVecRight()
     xa = np.random.default_rng(11).uniform(-1, 1, x.getLocalSize())
     x.setArray(xa)
