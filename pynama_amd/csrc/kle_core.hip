@@ -615,6 +615,9 @@ int kle_set_tuning(const char *key, int value)
     if (k == "spmv_waves") {
         KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
         g_tune.spmv_waves = value;
+    } else if (k == "upd_nt") {
+        KLE_ARG(value == 0 || value == 1, "upd_nt: 0 or 1");
+        g_tune.upd_nt = value;
     } else if (k == "upd_preload") {
         KLE_ARG(value == 0 || value == 1, "upd_preload: 0 or 1");
         g_tune.upd_preload = value;
@@ -733,6 +736,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_x_lds") *value = g_tune.spmv_x_lds;
     else if (k == "spmv_dict") *value = g_tune.spmv_dict;
     else if (k == "upd_preload") *value = g_tune.upd_preload;
+    else if (k == "upd_nt") *value = g_tune.upd_nt;
     else if (k == "spmv_dict_min_rows") *value = g_tune.spmv_dict_min_rows;
     else if (k == "spmv_sym") *value = g_tune.spmv_sym;
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;

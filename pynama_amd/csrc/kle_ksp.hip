@@ -538,7 +538,22 @@ __global__ __launch_bounds__(KB) void k_cg_flush(const double *__restrict__ a0, 
 // rank): sums (r,u), (r,r) of the previous update [2][G] and (w,u) of the
 // dot launch [Gd], then  p = u + b p ; s = w + b s ; x += a p ; r -= a s ;
 // u = M r  with the new (r,u), (r,r) partials to pu_out [2][G].
-template <bool JAC, bool PRE>
+// NT (tuning upd_nt): every vector but u is loaded and stored nontemporal, so
+// that u -- the next SpMV's x -- is what the Infinity Cache keeps of this
+// launch (vectors of 64 MB at 8M DoF: the update's other 704 MB evict it)
+template <bool NT>
+__device__ __forceinline__ double ld_upd(const double *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st_upd(double *p, double v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <bool JAC, bool PRE, bool NT = false>
 __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_iter(int64_t n, const double *__restrict__ dinv,
                                                 const double *__restrict__ w, double *__restrict__ u,
                                                 double *__restrict__ p, double *__restrict__ sv,
@@ -553,8 +568,9 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
     StageIn in;
     if constexpr (PRE) {
         if (i0 < n) {
-            e[0] = u[i0], e[1] = p[i0], e[2] = w[i0], e[3] = sv[i0], e[4] = x[i0], e[5] = r[i0];
-            e[6] = JAC ? dinv[i0] : 1.0;
+            e[0] = u[i0], e[1] = ld_upd<NT>(p + i0), e[2] = ld_upd<NT>(w + i0), e[3] = ld_upd<NT>(sv + i0);
+            e[4] = ld_upd<NT>(x + i0), e[5] = ld_upd<NT>(r + i0);
+            e[6] = JAC ? ld_upd<NT>(dinv + i0) : 1.0;
         }
         if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
     }
@@ -566,16 +582,17 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
     double acc[2] = {0.0, 0.0};
     for (int64_t i = i0; i < n; i += stride) {
         if (!PRE || i != i0) {
-            e[0] = u[i], e[1] = p[i], e[2] = w[i], e[3] = sv[i], e[4] = x[i], e[5] = r[i];
-            e[6] = JAC ? dinv[i] : 1.0;
+            e[0] = u[i], e[1] = ld_upd<NT>(p + i), e[2] = ld_upd<NT>(w + i), e[3] = ld_upd<NT>(sv + i);
+            e[4] = ld_upd<NT>(x + i), e[5] = ld_upd<NT>(r + i);
+            e[6] = JAC ? ld_upd<NT>(dinv + i) : 1.0;
         }
         const double pi = e[0] + beta * e[1];
         const double si = e[2] + beta * e[3];
-        p[i] = pi;
-        sv[i] = si;
-        x[i] = e[4] + alpha * pi;
+        st_upd<NT>(p + i, pi);
+        st_upd<NT>(sv + i, si);
+        st_upd<NT>(x + i, e[4] + alpha * pi);
         const double ri = e[5] - alpha * si;
-        r[i] = ri;
+        st_upd<NT>(r + i, ri);
         const double ui = JAC ? e[6] * ri : ri;
         u[i] = ui;
         acc[0] += ri * ui;
@@ -1104,7 +1121,8 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                                    k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1], c->d_scal,
                                    c->d_istate, (int)pending, par, k->atol);
             };
-            if (jac) go(g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
+            if (jac && g_tune.upd_nt) go(g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
+            else if (jac) go(g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
             else go(g_tune.upd_preload ? k_sr_iter<false, true> : k_sr_iter<false, false>);
             KLE_HIP(hipGetLastError());
             KLE_TRY(c->toc("cg_update", &ev));
