@@ -78,7 +78,9 @@ const char *kle_last_error(void);
  * per-group column dictionaries; 0 off), "spmv_dict_min_rows" (node rows from
  * which matrices get dictionaries at creation; default 64000), "upd_preload"
  * (1 default: CG update kernels load their first element and the stage inputs
- * before the prologue; 0 off), "spmv_sym" (1 default: matrices holding
+ * before the prologue; 0 off), "upd_nt" (single-reduction CG update: every
+ * vector but u loaded and stored nontemporal, so u stays in the Infinity
+ * Cache for the SpMV; 0 off, 1 on, 2 auto = from 2M local entries), "spmv_sym" (1 default: matrices holding
  * symmetric storage run the symmetric SpMV; 0 the full storage),
  * "spmv_sym_min_rows" (node rows per rank from which kle_assemble_kle gives
  * K symmetric storage; default 40000), "spmv_sym_tz" (read when the storage

@@ -616,7 +616,7 @@ int kle_set_tuning(const char *key, int value)
         KLE_ARG(value == 0 || value == 4 || value == 8, "spmv_waves: 0 (auto), 4 or 8");
         g_tune.spmv_waves = value;
     } else if (k == "upd_nt") {
-        KLE_ARG(value == 0 || value == 1, "upd_nt: 0 or 1");
+        KLE_ARG(value >= 0 && value <= 2, "upd_nt: 0 off, 1 on, 2 auto");
         g_tune.upd_nt = value;
     } else if (k == "upd_preload") {
         KLE_ARG(value == 0 || value == 1, "upd_preload: 0 or 1");

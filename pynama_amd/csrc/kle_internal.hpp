@@ -344,7 +344,10 @@ struct Tuning {
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
     int ksp_refine = 2;  // CG / pipelined CG: up to this many correction solves when the true residual misses rtol (kle_ksp.hip refine; default of new KSPs); 0 PETSc's plain stop
-    int upd_nt = 0;       // single-reduction CG update: every vector but u nontemporal (u stays in the Infinity Cache for the SpMV)
+    int upd_nt = 2;       // single-reduction CG update: every vector but u nontemporal (u stays in the Infinity Cache for the
+                          // SpMV) -- 0 off, 1 on, 2 auto: from 2M local entries (12 vectors > the 256 MB cache); per CG
+                          // iteration config 4 4353 -> 4272 us, config-5 size 4019 -> 3907, config 2 448.4 -> 452.1
+                          // (profiles/r04/ab/upd_nt_*.jsonl)
     int upd_preload = 1;  // CG update kernels load their first element and the stage inputs before the prologue; 0 off
     int spmv_x_lds = 1;  // 3x3 structured SpMV: x staged in LDS per workgroup (k_nb_spmv_xl); 0 off
     int spmv_sym = 1;  // SBAIJ-style symmetric storage for the KLE K of >= spmv_sym_min_rows node rows per rank; 0 off

@@ -1121,7 +1121,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                                    k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1], c->d_scal,
                                    c->d_istate, (int)pending, par, k->atol);
             };
-            if (jac && g_tune.upd_nt) go(g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
+            if (jac && (g_tune.upd_nt == 1 || (g_tune.upd_nt == 2 && n >= 2000000))) go(g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
             else if (jac) go(g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
             else go(g_tune.upd_preload ? k_sr_iter<false, true> : k_sr_iter<false, false>);
             KLE_HIP(hipGetLastError());
