@@ -646,7 +646,7 @@ int kle_set_tuning(const char *key, int value)
         KLE_ARG(value >= 0 && value <= 100, "spmv_sym_ovl_b: 0 .. 100 %");
         g_tune.spmv_sym_ovl_b = value;
     } else if (k == "spmv_sym_place") {
-        KLE_ARG(value >= 0 && value <= 8, "spmv_sym_place: 0 .. 8 fresh copies");
+        KLE_ARG(value >= 0 && value <= 32, "spmv_sym_place: 0 .. 32 fresh copies");
         g_tune.spmv_sym_place = value;
     } else if (k == "spmv_sym_place_min_mb") {
         KLE_ARG(value >= 0, "spmv_sym_place_min_mb: >= 0");

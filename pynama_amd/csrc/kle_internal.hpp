@@ -358,7 +358,7 @@ struct Tuning {
     int spmv_sym_tile64 = 0;        // symmetric box storage (read at build): 8 x 2 x 4 tiles (64 rows) -- 0 auto (below spmv_sym_tile64_max 128-row tiles), 1 always, 2 never
     int spmv_sym_tile64_max = 800;  // ... 1/8 of config 2 (561 tiles) 75.6 -> 70.6 us (full storage 72.4), 1/4 (935) 121.2 vs 127.8 (profiles/r04/ab/tile64_and_sgpr_ab.jsonl)
     int spmv_sym_ovl_b = 50;        // N > 1 symmetric box SpMV: % of the interior tiles run beside the reverse halo
-    int spmv_sym_place = 6;   // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
+    int spmv_sym_place = 12;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes
     int spmv_sym_stpol = 0;   // symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
