@@ -642,6 +642,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tile64_max") {
         KLE_ARG(value >= 0, "spmv_sym_tile64_max: >= 0 tiles");
         g_tune.spmv_sym_tile64_max = value;
+    } else if (k == "spmv_sym_xcd") {
+        KLE_ARG(value >= 0 && value <= 4096, "spmv_sym_xcd: 0 .. 4096 tiles");
+        g_tune.spmv_sym_xcd = value;
     } else if (k == "spmv_sym_ovl_b") {
         KLE_ARG(value >= 0 && value <= 100, "spmv_sym_ovl_b: 0 .. 100 %");
         g_tune.spmv_sym_ovl_b = value;
@@ -748,6 +751,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
     else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
     else if (k == "spmv_sym_ovl_b") *value = g_tune.spmv_sym_ovl_b;
+    else if (k == "spmv_sym_xcd") *value = g_tune.spmv_sym_xcd;
     else if (k == "spmv_sym_tile64") *value = g_tune.spmv_sym_tile64;
     else if (k == "spmv_sym_tile64_max") *value = g_tune.spmv_sym_tile64_max;
     else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;

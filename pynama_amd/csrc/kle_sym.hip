@@ -290,6 +290,21 @@ __device__ __forceinline__ void sym_wait9(double *v)
                  : "i"(N));
 }
 
+// launch-local block -> work item: runs of ch consecutive items per XCD
+// (workgroups are dealt round-robin over the 8 XCDs; kle_mat.hip xcd_block)
+__device__ __forceinline__ int64_t gsym_block(int ch)
+{
+    int64_t blk = blockIdx.x;
+    if (ch > 0) {
+        const int64_t k = blk >> 3, xc = blk & 7, S = (int64_t)gridDim.x / (8 * ch);
+        if (k < S * ch) {
+            const int64_t sb = k / ch;
+            blk = sb * 8 * ch + xc * ch + (k - sb * ch);
+        }
+    }
+    return blk;
+}
+
 // SGPR cap: the HIP runtime admits workgroups per CU by its own register
 // model, 512 SGPRs per SIMD / the kernel's SGPRs rounded up to 16 (the occupancy
 // API and the dispatcher agree: 106 SGPRs -> 4 waves per SIMD = 2 of these
@@ -305,7 +320,7 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
                                                              const double *__restrict__ x, double *__restrict__ ws,
                                                              const int *__restrict__ tile_e,
                                                              const int *__restrict__ istate, int t0,
-                                                             int early, int stpol KLE_PROBE_PARAM)
+                                                             int early, int stpol, int xcd KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
     // LDS: x [3][RN] | y [3][RN + 64] (DET: int64; 64 dummy slots per
@@ -322,7 +337,8 @@ __global__ __launch_bounds__(64 * WV, 4) __attribute__((amdgpu_num_sgpr(SYM_XL_S
     constexpr int NS = NQ * TZ;               // row slots per wave
     const int RN = g.RX * g.RY * g.RZ, RS = RN + 64;
     double *xl = lds, *yl = lds + 3 * RN, *yd = lds + 3 * RN + 3 * RS;
-    const int64_t t = (int64_t)blockIdx.x + t0;  // (N > 1: tiles [t0, ...) of one launch)
+    // (N > 1: tiles [t0, ...) of one launch; xcd > 0: runs of xcd tiles per XCD, spmv_sym_xcd)
+    const int64_t t = gsym_block(xcd) + t0;
     const int tix = (int)(t % g.ntx);
     const int64_t q = t / g.ntx;
     const int tiy = (int)(q % g.nty), tz = (int)(q / g.nty) * TZ;
@@ -813,18 +829,6 @@ constexpr size_t LDS_PER_CU_G = 163840;  // the first launch's LDS budget: this 
 constexpr int GSYM_FILL = 2;  // x-fill entries per thread and batch (3 x 196 entries per group on average)
 
 // kle_mat.hip xcd_block: runs of ch consecutive groups per XCD
-__device__ __forceinline__ int64_t gsym_block(int ch)
-{
-    int64_t blk = blockIdx.x;
-    if (ch > 0) {
-        const int64_t k = blk >> 3, xc = blk & 7, S = (int64_t)gridDim.x / (8 * ch);
-        if (k < S * ch) {
-            const int64_t sb = k / ch;
-            blk = sb * 8 * ch + xc * ch + (k - sb * ch);
-        }
-    }
-    return blk;
-}
 
 // Copy each row's upper tail (from the diagonal block k0 on) into the
 // symmetric layout and measure max |B_ij - B_ji^T| per row over all its
@@ -2073,7 +2077,7 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
     }
     hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, TY, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
-                       (int)t0, g_tune.spmv_sym_early, g_tune.spmv_sym_stpol KLE_PROBE_ARG);
+                       (int)t0, g_tune.spmv_sym_early, g_tune.spmv_sym_stpol, g_tune.spmv_sym_xcd KLE_PROBE_ARG);
 }
 
 static void launch_sym_tiles(const kle_mat *A, const SymGeo &g, const kle_vec *x, int64_t t0, int64_t t1,

@@ -40,8 +40,9 @@ def _mat(pa, nelem, ngl):
     return dom, mat
 
 
-KNOBS = ({}, {"spmv_sym_det": 0}, {"spmv_sym_waves": 16}, {"spmv_sym_waves": 16, "spmv_sym_det": 0})
-DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_waves": 0}
+KNOBS = ({}, {"spmv_sym_det": 0}, {"spmv_sym_waves": 16}, {"spmv_sym_waves": 16, "spmv_sym_det": 0},
+         {"spmv_sym_xcd": 3})
+DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_xcd": 0}
 
 
 @pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([6, 5, 3], 2),
