@@ -1821,7 +1821,15 @@ static int sym_place(kle_mat *A)
 int sym_build(kle_mat *A)
 {
     int rc = sym_build_impl(A);
-    if (!rc) rc = sym_place(A);
+    if (!rc) {
+        // (placement is per rank; a failure on one rank drops the storage on
+        // all of them, as every other refusal does, so no rank runs the
+        // reverse halo while a neighbour runs the full storage)
+        const int prc = sym_place(A);
+        bool any = false;
+        const int arc = any_rank(A->ctx, prc != 0, any);
+        rc = prc ? prc : arc ? arc : any ? fail(KLE_ERR_SUP, "symmetric storage: value placement failed on another rank") : 0;
+    }
     if (rc) sym_drop(A);
     return rc;
 }
