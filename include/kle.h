@@ -108,7 +108,8 @@ const char *kle_last_error(void);
  * x is in LDS; 0 default), "spmv_sym_align" (read at build: partial slots
  * aligned to 128-B lines; 0 default), "spmv_sym_alloc" (read at build: bit 1
  * values, bit 2 partials physically contiguous; 0 default), "spmv_sym_stpol"
- * (partial stores: 0 plain default, 1 nontemporal, 2 sc1, 3 sc0 sc1).
+ * (box kernel's partial stores: 0 plain default, 1 nontemporal, 2 sc1, 3 sc0
+ * sc1), "spmv_gsym_stpol" (the same for the graph kernel; default 2).
  * Every value gives correct results (the
  * timing probes of the symmetric SpMV exist only in the tools/ probe build,
  * `make -C pynama_amd/csrc probe`). */

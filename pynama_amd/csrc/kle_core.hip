@@ -660,6 +660,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_stpol") {
         KLE_ARG(value >= 0 && value <= 3, "spmv_sym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
         g_tune.spmv_sym_stpol = value;
+    } else if (k == "spmv_gsym_stpol") {
+        KLE_ARG(value >= 0 && value <= 3, "spmv_gsym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
+        g_tune.spmv_gsym_stpol = value;
     } else if (k == "spmv_sym_alloc") {
         KLE_ARG(value >= 0 && value <= 3, "spmv_sym_alloc: bits 1 values, 2 partials");
         g_tune.spmv_sym_alloc = value;
@@ -749,6 +752,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
     else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
+    else if (k == "spmv_gsym_stpol") *value = g_tune.spmv_gsym_stpol;
     else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
     else if (k == "spmv_sym_ovl_b") *value = g_tune.spmv_sym_ovl_b;
     else if (k == "spmv_sym_xcd") *value = g_tune.spmv_sym_xcd;

@@ -362,7 +362,9 @@ struct Tuning {
     int spmv_sym_place = 12;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes
-    int spmv_sym_stpol = 0;   // symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
+    int spmv_sym_stpol = 0;   // box symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
+    int spmv_gsym_stpol = 2;  // ... of the graph symmetric SpMV: sc1 452.9 -> 449.1 us at 1M DoF (the box kernel: plain 420.5,
+                              // sc1 422.1, nt 426.5; profiles/r04/ab/stpol_*.jsonl)
     int spmv_sym_alloc = 0;   // symmetric storage (read at build): bit 1 values, bit 2 tile partials physically contiguous (hipDeviceMallocContiguous)
     int spmv_sym_early = 0;   // symmetric SpMV tiles: the first item's value loads issued with the x fill (1) or after it (0)
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4

@@ -1498,7 +1498,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(64 * WV), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
                            A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_swptr, A->d_sval, x->base, A->d_sws,
-                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_sym_stpol KLE_PROBE_ARG);
+                           A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_gsym_stpol KLE_PROBE_ARG);
     };
     // part 0: the inner groups of both launches, part 1: the others (one
     // rank or no overlap: both parts back to back)

@@ -41,8 +41,8 @@ def _mat(pa, nelem, ngl):
 
 
 KNOBS = ({}, {"spmv_sym_det": 0}, {"spmv_sym_waves": 16}, {"spmv_sym_waves": 16, "spmv_sym_det": 0},
-         {"spmv_sym_xcd": 3})
-DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_xcd": 0}
+         {"spmv_sym_xcd": 3}, {"spmv_sym_stpol": 1}, {"spmv_sym_stpol": 2}, {"spmv_sym_stpol": 3})
+DEFAULTS = {"spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_xcd": 0, "spmv_sym_stpol": 0}
 
 
 @pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([6, 5, 3], 2),
@@ -398,6 +398,14 @@ def test_unstructured_symmetric_spmv_matches_full_storage_and_csr(pa, tmp_path, 
                         assert np.abs(y2 - ref).max() <= 1e-13 * np.abs(ref).max(), (rows, split, det)
                     if det:
                         np.testing.assert_array_equal(y2, y1)
+                if det and rows == 64 and not split and not align:
+                    # partial-store cache policies (spmv_gsym_stpol; default 2, sc1): the same bits
+                    for pol in (0, 1, 3):
+                        set_tuning("spmv_gsym_stpol", pol)
+                        try:
+                            np.testing.assert_array_equal((K * x).getArray(), y1)
+                        finally:
+                            set_tuning("spmv_gsym_stpol", 2)
     finally:
         set_tuning("spmv_sym_det", 1)
         set_tuning("spmv_sym_align", 0)
