@@ -101,7 +101,7 @@ const char *kle_last_error(void);
  * "spmv_sym_place_gbps" (5200) GB/s of its algorithmic bytes, the fastest
  * kept -- the same values at another placement; default 12, 0 off),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
- * "spmv_sym_tile64_max" (800) 128-row tiles; 1 wherever two workgroups fit
+ * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
  * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo
  * overlap: the percentage of the interior tiles run beside the reverse halo,
  * the rest beside the forward halo; default 50), "spmv_sym_early" (box tile kernel loads its first items before

@@ -356,7 +356,7 @@ struct Tuning {
     int spmv_sym_waves = 0;   // waves per workgroup of k_nb_spmv_sym_xl: 0 auto (8 while 2 workgroups fit a CU), 8, 16
     int spmv_sym_align = 0;   // symmetric SpMV partials (read at build): every tile's / group's slot starts on a 128-B line and its lines are written whole (1; measured no faster, r04d) or packed (0)
     int spmv_sym_tile64 = 0;        // symmetric box storage (read at build): 8 x 2 x 4 tiles (64 rows) -- 0 auto (below spmv_sym_tile64_max 128-row tiles), 1 always, 2 never
-    int spmv_sym_tile64_max = 800;  // ... 1/8 of config 2 (561 tiles) 75.6 -> 70.6 us (full storage 72.4), 1/4 (935) 121.2 vs 127.8 (profiles/r04/ab/tile64_and_sgpr_ab.jsonl)
+    int spmv_sym_tile64_max = 640;  // ... 1/8 of config 2 (561 tiles; 374 per rank at N = 8) 75.6 -> 70.6 us (full storage 72.4), 1/4 (935; 748 per rank at N = 4) 121.2 vs 127.8 (profiles/r04/ab/tile64_and_sgpr_ab.jsonl)
     int spmv_sym_xcd = 0;           // box symmetric tile kernel: runs of this many consecutive tiles per XCD (0: round-robin)
     int spmv_sym_ovl_b = 50;        // N > 1 symmetric box SpMV: % of the interior tiles run beside the reverse halo
     int spmv_sym_place = 12;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off

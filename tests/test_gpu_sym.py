@@ -99,7 +99,7 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     K.setOption(K.Option.SPD, True)
     np.testing.assert_array_equal(ya, (K * x).getArray())
     # tile shapes: 8 x 2 x 4 (64 rows; spmv_sym_tile64 1 forces them where two
-    # workgroups fit a CU, the default picks them for parts of < 800 128-row
+    # workgroups fit a CU, the default picks them for parts of < 640 128-row
     # tiles -- every matrix here) and never (2: 8 x 4 x 4, or 8 x 8 x 2 at
     # p >= 5): the same products to rounding, each bitwise reproducible
     shapes = {}
