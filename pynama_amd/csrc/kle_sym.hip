@@ -2263,18 +2263,23 @@ extern "C" int kle_probe_occupancy(int which, int lds_bytes, int *blocks)
 extern "C" int kle_probe_realloc(kle_mat *A, int what, long long shift)
 {
     using namespace kle;
-    KLE_ARG(A && A->d_sval && !A->sym_graph && (what == 1 || what == 2) && shift >= 0 && shift % 8 == 0, "bad arg");
-    const SymGeo g = sym_geo(A);
-    const size_t bytes = what == 1 ? sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1)
-                                   : sizeof(double) * (size_t)g.ntx * g.nty * g.ntz * 3 * g.WN;
+    // (what 3: the full storage's values, d_val -- does the full-storage SpMV care?)
+    KLE_ARG(A && (what == 3 || (A->d_sval && !A->sym_graph)) && what >= 1 && what <= 3 && shift >= 0 &&
+                shift % 8 == 0, "bad arg");
+    size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->nvals, 1);
+    if (what != 3) {
+        const SymGeo g = sym_geo(A);
+        bytes = what == 1 ? sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1)
+                          : sizeof(double) * (size_t)g.ntx * g.nty * g.ntz * 3 * g.WN;
+    }
     char *raw = nullptr;
     KLE_HIP(hipMalloc(&raw, bytes + (size_t)shift));
     double *np = reinterpret_cast<double *>(raw + shift);
-    double **pp = what == 1 ? &A->d_sval : &A->d_sws;
+    double **pp = what == 1 ? &A->d_sval : what == 2 ? &A->d_sws : &A->d_val;
     KLE_HIP(hipMemcpy(np, *pp, bytes, hipMemcpyDeviceToDevice));
     *pp = np;
-    fprintf(stderr, "[kle probe] moved %s to %p (raw %p, %zu bytes)\n", what == 1 ? "values" : "workspace", (void *)np,
-            (void *)raw, bytes);
+    fprintf(stderr, "[kle probe] moved %s to %p (raw %p, %zu bytes)\n",
+            what == 1 ? "values" : what == 2 ? "workspace" : "full-storage values", (void *)np, (void *)raw, bytes);
     return 0;
 }
 #endif

@@ -61,7 +61,11 @@ def main():
 
     y0 = None
     ap_plan = os.environ.get("ALLOC_PLAN", "values")
-    if ap_plan == "ws":
+    if ap_plan == "full":  # the full-storage SpMV (spmv_sym 0) with its value array moved
+        from pynama_amd.runtime import set_tuning
+        set_tuning("spmv_sym", 0)
+        plan = [("none", 0)] * 2 + [("full", 0)] * 10
+    elif ap_plan == "ws":
         plan = [("none", 0)] * 3 + [("ws", 0)] * 8 + [("ws", s) for s in (4096, 65536, 1 << 20, (2 << 20) + 4096)] * 2 \
             + [("values", 0)] * 6 + [("none", 0)] * 2
     else:  # the value array at fresh allocations and byte offsets into them
@@ -69,7 +73,7 @@ def main():
                                                              (2 << 20) + 4096, 0, 0, 0, 0, 0)]
     for what, shift in plan:
         if what != "none":
-            rc = lib.kle_probe_realloc(K._h, 1 if what == "values" else 2, shift)
+            rc = lib.kle_probe_realloc(K._h, {"values": 1, "ws": 2, "full": 3}[what], shift)
             assert rc == 0
         us = timed()
         yy = y.getArray().copy()
