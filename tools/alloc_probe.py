@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--nelem", default="20,16,16")
     ap.add_argument("--ngl", type=int, default=5)
     ap.add_argument("--its", type=int, default=40)
+    ap.add_argument("--nostore", action="store_true", help="also time each placement without the partial stores")
     a = ap.parse_args()
     import numpy as np
 
@@ -71,6 +72,7 @@ def main():
     else:  # the value array at fresh allocations and byte offsets into them
         plan = [("none", 0)] * 2 + [("values", s) for s in (0, 0, 0, 0, 0, 0, 256, 4096, 65536, 1 << 20,
                                                              (2 << 20) + 4096, 0, 0, 0, 0, 0)]
+    from pynama_amd.runtime import set_tuning
     for what, shift in plan:
         if what != "none":
             rc = lib.kle_probe_realloc(K._h, {"values": 1, "ws": 2, "full": 3}[what], shift)
@@ -79,8 +81,12 @@ def main():
         yy = y.getArray().copy()
         if y0 is None:
             y0 = yy
-        print(json.dumps({"moved": what, "shift": shift, "spmv_us": us, "same_y": bool(np.array_equal(yy, y0))}),
-              flush=True)
+        rec = {"moved": what, "shift": shift, "spmv_us": us, "same_y": bool(np.array_equal(yy, y0))}
+        if a.nostore:  # the same placement without the partial stores (probe 8, wrong y on purpose)
+            set_tuning("spmv_sym_probe", 8)
+            rec["nostore_us"] = timed()
+            set_tuning("spmv_sym_probe", 0)
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
