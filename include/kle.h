@@ -99,7 +99,7 @@ const char *kle_last_error(void);
  * to this many fresh copies of a symmetric value array of at least
  * "spmv_sym_place_min_mb" (256) MB timed against the first until one streams
  * "spmv_sym_place_gbps" (5200) GB/s of its algorithmic bytes, the fastest
- * kept -- the same values at another placement; default 12, 0 off),
+ * kept -- the same values at another placement; default 16, 0 off),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
  * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo

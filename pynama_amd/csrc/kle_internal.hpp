@@ -359,7 +359,7 @@ struct Tuning {
     int spmv_sym_tile64_max = 640;  // ... 1/8 of config 2 (561 tiles; 374 per rank at N = 8) 75.6 -> 70.6 us (full storage 72.4), 1/4 (935; 748 per rank at N = 4) 121.2 vs 127.8 (profiles/r04/ab/tile64_and_sgpr_ab.jsonl)
     int spmv_sym_xcd = 0;           // box symmetric tile kernel: runs of this many consecutive tiles per XCD (0: round-robin)
     int spmv_sym_ovl_b = 50;        // N > 1 symmetric box SpMV: % of the interior tiles run beside the reverse halo
-    int spmv_sym_place = 12;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
+    int spmv_sym_place = 16;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes
     int spmv_sym_stpol = 0;   // box symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
