@@ -1,7 +1,10 @@
 #!/bin/bash
 # 64-row (8 x 2 x 4) vs 128-row symmetric tiles vs full storage on z slabs of
 # config 2 (1/8, 1/4, 1/2) and config 2 itself, with the product library and
-# with the uncapped-SGPR build (tools/libkle_nocap.so).  JSON lines on stdout.
+# with the uncapped-SGPR build (tools/libkle_nocap.so: make -C pynama_amd/csrc
+# OBJDIR=build_nocap OUT=../../tools/libkle_nocap.so
+# HIPFLAGS="--offload-arch=gfx950 -munsafe-fp-atomics -DSYM_XL_SGPRS=128").
+# JSON lines on stdout.
 set -e
 V='[{},{"spmv_sym_tile64":1},{"spmv_sym":0}]'
 for lib in pynama_amd/libkle.so tools/libkle_nocap.so; do
