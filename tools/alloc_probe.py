@@ -62,7 +62,11 @@ def main():
 
     y0 = None
     ap_plan = os.environ.get("ALLOC_PLAN", "values")
-    if ap_plan == "full":  # the full-storage SpMV (spmv_sym 0) with its value array moved
+    if ap_plan == "mix":  # each value placement with four partial-workspace placements
+        plan = [("none", 0)] * 2
+        for _ in range(6):
+            plan += [("values", 0)] + [("ws", 0)] * 4
+    elif ap_plan == "full":  # the full-storage SpMV (spmv_sym 0) with its value array moved
         from pynama_amd.runtime import set_tuning
         set_tuning("spmv_sym", 0)
         plan = [("none", 0)] * 2 + [("full", 0)] * 10
