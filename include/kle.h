@@ -392,6 +392,10 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on);
  * microseconds (0: not timed), how many fresh copies were tried and which
  * one was kept (0: the array as built). */
 int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept);
+/* ... and the partials' workspace placements tried after the value copies
+ * (tuning "spmv_sym_place_ws", only when no copy streamed fast) and the one
+ * kept (0: as built). */
+int kle_mat_get_sym_placement_ws(const kle_mat *A, int *tries, int *kept);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

@@ -147,6 +147,7 @@ _SIGS = {
     "kle_mat_set_symmetric": [vp, C.c_int],
     "kle_mat_get_symmetric": [vp, C.POINTER(C.c_int)],
     "kle_mat_get_sym_placement": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "kle_mat_get_sym_placement_ws": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "kle_get_nb_pad": [],
     "kle_set_nb_layout": [C.c_int],
     "kle_get_nb_layout": [],

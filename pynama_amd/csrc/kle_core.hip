@@ -651,6 +651,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_place") {
         KLE_ARG(value >= 0 && value <= 32, "spmv_sym_place: 0 .. 32 fresh copies");
         g_tune.spmv_sym_place = value;
+    } else if (k == "spmv_sym_place_ws") {
+        KLE_ARG(value >= 0 && value <= 32, "spmv_sym_place_ws: 0 .. 32 workspace placements");
+        g_tune.spmv_sym_place_ws = value;
     } else if (k == "spmv_sym_place_min_mb") {
         KLE_ARG(value >= 0, "spmv_sym_place_min_mb: >= 0");
         g_tune.spmv_sym_place_min_mb = value;
@@ -760,6 +763,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_tile64_max") *value = g_tune.spmv_sym_tile64_max;
     else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;
     else if (k == "spmv_sym_place_min_mb") *value = g_tune.spmv_sym_place_min_mb;
+    else if (k == "spmv_sym_place_ws") *value = g_tune.spmv_sym_place_ws;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif

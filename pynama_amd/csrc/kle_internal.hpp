@@ -248,7 +248,9 @@ struct kle_mat {
     int sym_wn = 0;
     double sym_place_us = 0;  // SpMV time of the kept value placement (sym_place), one rank
     int sym_place_kept = 0;   // which fresh copy was kept (0: the first allocation)
-    int sym_place_tries = 0;  // fresh copies timed  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
+    int sym_place_tries = 0;  // fresh copies timed
+    int sym_place_ws_tries = 0, sym_place_ws_kept = 0;  // workspace placements timed / kept (0: as built)
+    size_t sws_bytes = 0;     // the partials' workspace (d_sws)  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
     int *d_swptr = nullptr;  // graph: per group, its partials' first double in d_sws (128-B aligned with spmv_sym_align)
     int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
     // graph (unstructured) symmetric storage, one rank (kle_sym.hip gsym_build):
@@ -360,6 +362,7 @@ struct Tuning {
     int spmv_sym_xcd = 0;           // box symmetric tile kernel: runs of this many consecutive tiles per XCD (0: round-robin)
     int spmv_sym_ovl_b = 50;        // N > 1 symmetric box SpMV: % of the interior tiles run beside the reverse halo
     int spmv_sym_place = 16;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
+    int spmv_sym_place_ws = 8;       // ... then at most this many workspace placements if no value copy was fast
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
     int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes
     int spmv_sym_stpol = 0;   // box symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)

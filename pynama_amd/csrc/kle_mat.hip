@@ -1457,6 +1457,15 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on)
     return 0;
 }
 
+int kle_mat_get_sym_placement_ws(const kle_mat *A, int *tries, int *kept)
+{
+    KLE_ARG(A && tries && kept, "null arg");
+    const bool on = A->d_sval != nullptr;
+    *tries = on ? A->sym_place_ws_tries : 0;
+    *kept = on ? A->sym_place_ws_kept : 0;
+    return 0;
+}
+
 int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept)
 {
     KLE_ARG(A && us && tries && kept, "null arg");

@@ -791,6 +791,8 @@ void sym_forget(kle_mat *A)
     A->sym_wn = 0;
     A->sym_place_us = 0;
     A->sym_place_tries = A->sym_place_kept = 0;
+    A->sym_place_ws_tries = A->sym_place_ws_kept = 0;
+    A->sws_bytes = 0;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
     A->sym_graph = 0;
@@ -1379,7 +1381,8 @@ static int gsym_build(kle_mat *A)
         hipMalloc(&A->d_sgptr, sizeof(int) * (ns + 1)) != hipSuccess ||
         hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
         hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
-        sym_malloc(reinterpret_cast<void **>(&A->d_sws), sizeof(double) * std::max<int64_t>(wptr[ng], 1), 2) != hipSuccess ||
+        (A->sws_bytes = sizeof(double) * std::max<int64_t>(wptr[ng], 1),
+         sym_malloc(reinterpret_cast<void **>(&A->d_sws), A->sws_bytes, 2) != hipSuccess) ||
         hipMalloc(&A->d_swptr, sizeof(int) * (ng + 1)) != hipSuccess ||
         hipMalloc(&A->d_stile_e, sizeof(int) * ng) != hipSuccess || hipMalloc(&dk0, sizeof(int) * n) != hipSuccess ||
         (nhi && hipMalloc(&A->d_sgsend, sizeof(double) * 3 * nhi) != hipSuccess) ||
@@ -1796,6 +1799,30 @@ static int sym_place(kle_mat *A)
             std::swap(A->d_sval, held.back());
         }
     }
+    // then the partials' workspace, if no value copy streamed fast: the
+    // stores' cost depends on where values and partials lie relative to
+    // each other (placement_with_without_stores.jsonl), and a workspace is
+    // cheap to move -- no copy, every slot the gather reads is written by
+    // the tiles first
+    int wtries = 0, wkept = 0;
+    for (int k = 0; k < g_tune.spmv_sym_place_ws && !rc && !fast(best) && A->sws_bytes; ++k) {
+        double *nw = nullptr;
+        if (hipMalloc(&nw, A->sws_bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        held.push_back(nw);
+        std::swap(A->d_sws, held.back());
+        ++wtries;
+        rc = timed(t);
+        trail += " w" + std::to_string((int)t);
+        if (!rc && t < best) {
+            best = t;
+            wkept = wtries;
+        } else {
+            std::swap(A->d_sws, held.back());
+        }
+    }
     (void)hipStreamSynchronize(c->stream);
     for (double *p : held) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
@@ -1807,11 +1834,14 @@ static int sym_place(kle_mat *A)
         }
     if (const char *e = getenv("KLE_TIMING"))
         if (atoi(e))
-            fprintf(stderr, "[kle sym] value placement: us per SpMV %s; kept %s (%.0f GB/s)\n", trail.c_str(),
-                    kept ? ("copy " + std::to_string(kept)).c_str() : "the first", alg / (1e3 * best));
+            fprintf(stderr, "[kle sym] value placement: us per SpMV %s; kept %s, workspace %s (%.0f GB/s)\n",
+                    trail.c_str(), kept ? ("copy " + std::to_string(kept)).c_str() : "the first",
+                    wkept ? ("move " + std::to_string(wkept)).c_str() : "as built", alg / (1e3 * best));
     A->sym_place_us = best;
     A->sym_place_kept = kept;
     A->sym_place_tries = tries;
+    A->sym_place_ws_tries = wtries;
+    A->sym_place_ws_kept = wkept;
     return rc;
 }
 
@@ -2034,7 +2064,8 @@ static int sym_build_impl(kle_mat *A)
             for (int tx = 0; tx < g.ntx; ++tx)
                 ents += span(tx * g.TX - g.PX, g.RX, Lx) * span(ty * g.TY - g.PY, g.RY, Ly) *
                         span(t * g.TZ, g.RZ, Lz + hp);
-    nomem = sym_malloc(reinterpret_cast<void **>(&A->d_sws), sizeof(double) * ntiles * 3 * g.WN, 2) != hipSuccess ||
+    A->sws_bytes = sizeof(double) * ntiles * 3 * g.WN;
+    nomem = sym_malloc(reinterpret_cast<void **>(&A->d_sws), A->sws_bytes, 2) != hipSuccess ||
             hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
             (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
             (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess);

@@ -423,7 +423,10 @@ class Mat:
         """The value placement the symmetric storage kept (kle_mat_get_sym_placement)."""
         us, tries, kept = C.c_double(), C.c_int(), C.c_int()
         call("kle_mat_get_sym_placement", self._h, C.byref(us), C.byref(tries), C.byref(kept))
-        return {"spmv_us": us.value, "fresh_copies_tried": tries.value, "kept": kept.value}
+        wt, wk = C.c_int(), C.c_int()
+        call("kle_mat_get_sym_placement_ws", self._h, C.byref(wt), C.byref(wk))
+        return {"spmv_us": us.value, "fresh_copies_tried": tries.value, "kept": kept.value,
+                "workspace_moves_tried": wt.value, "workspace_kept": wk.value}
 
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))

@@ -109,7 +109,8 @@ def test_config2_full_size_matches_oracle(pa):
     try:
         K.setOption(K.Option.SPD, False)
         K.setOption(K.Option.SPD, True)
-        assert K.getSymmetricPlacement() == {"spmv_us": 0.0, "fresh_copies_tried": 0, "kept": 0}
+        assert K.getSymmetricPlacement() == {"spmv_us": 0.0, "fresh_copies_tried": 0, "kept": 0,
+                                             "workspace_moves_tried": 0, "workspace_kept": 0}
         np.testing.assert_array_equal((K * vel).getArray(), y1)
     finally:
         set_tuning("spmv_sym_place", 16)

@@ -172,6 +172,7 @@ def test_partitioned_symmetric_value_placement(tmp_path):
     for a, b in zip(res, ref):
         # (test sizes never stream 5.2 TB/s: all sixteen copies are tried)
         assert a["place"]["fresh_copies_tried"] == 16 and a["place"]["spmv_us"] > 0, a["place"]
+        assert a["place"]["workspace_moves_tried"] == 8, a["place"]
         assert b["place"]["fresh_copies_tried"] == 0, b["place"]
         np.testing.assert_array_equal(a["y"], b["y"])
         np.testing.assert_array_equal(a["u"], b["u"])

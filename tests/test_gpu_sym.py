@@ -129,6 +129,7 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
         K.setOption(K.Option.SPD, True)
         pl = K.getSymmetricPlacement()
         assert pl["fresh_copies_tried"] == 16 and pl["spmv_us"] > 0 and 0 <= pl["kept"] <= 16, pl
+        assert pl["workspace_moves_tried"] == 8 and 0 <= pl["workspace_kept"] <= 8, pl  # (then the partials)
         np.testing.assert_array_equal(ya, (K * x).getArray())
     finally:
         set_tuning("spmv_sym_place_min_mb", 256)
