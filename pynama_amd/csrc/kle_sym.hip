@@ -1777,13 +1777,32 @@ static int sym_place(kle_mat *A)
     int tries = 0, kept = 0;
     if (!rc) rc = timed(best);
     trail = std::to_string((int)best);
+    // (slow placements come in runs of consecutive allocations -- 11 fast
+    // copies then 5 slow ones in one process, 16 slow in another: after every
+    // 4 slow copies in a row a 16 GB spacer, held to the end like the
+    // rejected copies, moves the next ones further on; all held memory
+    // stays under 96 GB)
+    size_t held_bytes = 0;
+    int slow_run = 0;
     for (int k = 0; k < max_tries && !rc && !fast(best); ++k) {
         double *nv = nullptr;
+        if (slow_run >= 4 && bytes >= (size_t(256) << 20)) {  // (not for test-size arrays)
+            slow_run = 0;
+            const size_t sp = size_t(16) << 30;
+            if (held_bytes + sp + bytes <= (size_t(96) << 30) && hipMalloc(&nv, sp) == hipSuccess) {
+                held.push_back(nv);
+                held_bytes += sp;
+                trail += " |";
+            }
+            (void)hipGetLastError();
+            nv = nullptr;
+        }
         if (hipMalloc(&nv, bytes) != hipSuccess) {
             (void)hipGetLastError();
             break;  // (no room for another copy: keep what we have)
         }
         held.push_back(nv);
+        held_bytes += bytes;
         if (hipMemcpyAsync(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
             rc = fail(KLE_ERR_DEVICE, "placement copy failed");
             break;
@@ -1792,6 +1811,7 @@ static int sym_place(kle_mat *A)
         ++tries;
         rc = timed(t);
         trail += " " + std::to_string((int)t);
+        slow_run = fast(t) ? 0 : slow_run + 1;
         if (!rc && t < best) {
             best = t;
             kept = tries;
