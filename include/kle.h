@@ -98,7 +98,7 @@ const char *kle_last_error(void);
  * first of its two launches; 0 auto), "spmv_sym_place" (read at build: up
  * to this many fresh copies of a symmetric value array of at least
  * "spmv_sym_place_min_mb" (256) MB timed against the first until one streams
- * "spmv_sym_place_gbps" (5200) GB/s of its algorithmic bytes, the fastest
+ * "spmv_sym_place_gbps" (5450) GB/s of its algorithmic bytes, the fastest
  * kept -- the same values at another placement; default 16, 0 off),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit

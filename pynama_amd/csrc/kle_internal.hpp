@@ -364,7 +364,7 @@ struct Tuning {
     int spmv_sym_place = 16;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
     int spmv_sym_place_ws = 8;       // ... then at most this many workspace placements if no value copy was fast
     int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
-    int spmv_sym_place_gbps = 5200;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes
+    int spmv_sym_place_gbps = 5450;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes (config 2: fast 5.56-5.62, middling 5.41, slow 4.8)
     int spmv_sym_stpol = 0;   // box symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
     int spmv_gsym_stpol = 2;  // ... of the graph symmetric SpMV: sc1 452.9 -> 449.1 us at 1M DoF (the box kernel: plain 420.5,
                               // sc1 422.1, nt 426.5; profiles/r04/ab/stpol_*.jsonl)

@@ -170,7 +170,7 @@ def test_partitioned_symmetric_value_placement(tmp_path):
         del os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"]
     ref = _check_box(3, [2, 3, 3], 3, True, "pipecg", sym=True)
     for a, b in zip(res, ref):
-        # (test sizes never stream 5.2 TB/s: all sixteen copies are tried)
+        # (test sizes never stream 5.45 TB/s: all sixteen copies are tried)
         assert a["place"]["fresh_copies_tried"] == 16 and a["place"]["spmv_us"] > 0, a["place"]
         assert a["place"]["workspace_moves_tried"] == 8, a["place"]
         assert b["place"]["fresh_copies_tried"] == 0, b["place"]

@@ -123,7 +123,7 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
     K.setOption(K.Option.SPD, True)
     # value placement forced at this size (spmv_sym_place_min_mb 0; by
     # default from 256 MB of values, test_gpu_fullsize): sixteen fresh copies
-    # timed (a small matrix never streams 5.2 TB/s), one kept -- the same bits
+    # timed (a small matrix never streams 5.45 TB/s), one kept -- the same bits
     set_tuning("spmv_sym_place_min_mb", 0)
     try:
         K.setOption(K.Option.SPD, True)
