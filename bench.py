@@ -53,8 +53,10 @@ def parse():
     ap.add_argument("--layout", type=int, choices=[0, 1], default=1,
                     help="node-block value layout: 1 = 16-block chunks + packed tail, 0 = padded row streams")
     ap.add_argument("--pad", type=int, default=16, help="row padding quantum of layout 0 (blocks)")
-    ap.add_argument("--ops", action="store_true",
-                    help="also assemble Curl/SrT/DivSrT and time their SpMVs and the evalRHS operator chain")
+    ap.add_argument("--ops", dest="ops", action="store_const", const="on", default="auto",
+                    help="also assemble Curl/SrT/DivSrT and time their SpMVs and the evalRHS operator chain "
+                         "(default: at N = 1)")
+    ap.add_argument("--no-ops", dest="ops", action="store_const", const="off")
     ap.add_argument("--ksp", choices=["auto", "cg", "pipecg"], default="auto",
                     help="auto: single-reduction CG on one GPU, pipelined CG (allreduce beside the SpMV) on N>1")
     ap.add_argument("--classic-cg", action="store_true",
@@ -221,6 +223,9 @@ def main():
             write_gmsh(path, dim, V, Cc, F, T)
             t_mesh = time.perf_counter() - tg
         cfg["domain"] = {"ngl": args.ngl, "gmsh-file": path}
+    # (Domain.create partitions Gmsh meshes by the domain entry's
+    # "partitioner", inertial bisection unless it names another)
+    partitioner = cfg["domain"].get("partitioner", "inertial")
     t0 = time.perf_counter()
     dom = pa.Domain()
     dom.configure(cfg)
@@ -326,8 +331,11 @@ def main():
         tot_bytes, tot_nnz = float(sb[0]), int(sb[1])
     else:
         spmv_avg_max = spmv_avg_ms
-    # which device each rank ran on: one distinct GPU per rank under RCCL
+    # which device each rank ran on (one distinct GPU per rank under RCCL),
+    # what the RCCL communicator itself reports, and each rank's SpMV time
     dev = ctx.device_info()
+    dev["rccl_count"], dev["rccl_rank"] = ctx.comm_info()
+    dev["spmv_ms"] = spmv_avg_ms
     devices = [dev]
     if dist is not None:
         devices = [None] * nranks
@@ -393,7 +401,7 @@ def main():
     traffic, traffic_status = lookup_traffic(args.traffic, tkey, kname, spmv_bytes_local)
 
     ops = None
-    if args.ops:
+    if args.ops == "on" or (args.ops == "auto" and nranks == 1):
         ops = bench_operators(pa, mat, ctx, sol, dim)
 
     cpu = None
@@ -432,13 +440,19 @@ def main():
                        "structured_columns": K.isStructured(),
                        "symmetric_storage": K.isSymmetricStorage(),
                        "parallelism": ((f"z-slab x{nranks}" if mesh_kind == "box" else
-                                        f"cell slabs along the most-layered axis x{nranks}") +
+                                        f"cell slabs along the most-layered axis x{nranks}"
+                                        if partitioner == "slab" else
+                                        f"inertial recursive bisection x{nranks}") +
                                        ("" if nranks == 1 else
                                         " (RCCL halo + allreduce)" if dev["transport"] == "rccl" else
                                         " (IPC mailbox halo + allreduce: copy engines + stream wait/write-value)"
                                         if dev["transport"] == "ipc" else
                                         " (host-staged halo + allreduce over gloo, ranks sharing a GPU: test only)")),
-                       "devices": [f"{d['device']}@{d['pci_bus_id']}" for d in devices]},
+                       "devices": [f"{d['device']}@{d['pci_bus_id']}" for d in devices],
+                       # ncclCommCount / ncclCommUserRank per rank (0 / -1: no RCCL communicator)
+                       "rccl_ranks": devices[0]["rccl_count"],
+                       "rccl_user_ranks": [d["rccl_rank"] for d in devices],
+                       "spmv_ms_per_rank": [d["spmv_ms"] for d in devices]},
             # N > 1: bytes of all ranks over the slowest rank's SpMV time,
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
@@ -449,8 +463,11 @@ def main():
                          "bytes_per_launch": tot_bytes,
                          "csr_bytes_per_launch": csr_bytes, "csr_equiv_gbps": csr_equiv,
                          "avg_launch_ms": spmv_avg_max, "launches": spmv_cnt,
-                         # PMC traffic rate vs this box's measured read-only streaming
-                         # ceiling (per GPU): how close the SpMV is to what HBM delivers here
+                         # this box's measured read-only streaming ceiling (per GPU;
+                         # 16-B nontemporal loads, 4 in flight per lane): what HBM
+                         # delivers here, against the 8 TB/s peak
+                         "achievable_gbps": stream_rd,
+                         "frac_of_achievable": achieved / (stream_rd * nranks) if achieved else None,
                          "read_ceiling_gbps": stream_rd,
                          "traffic_frac_of_read_ceiling": (traffic / (spmv_avg_max * 1e-3) / 1e9 / stream_rd
                                                           if traffic and spmv_avg_max > 0 and nranks == 1
@@ -460,7 +477,7 @@ def main():
             "stream_copy_gbps": stream,
             "stream_read_gbps": stream_rd,  # read-only streaming ceiling (the SpMV is read-dominated)
             "breakdown_ms_per_iter": brk,
-            "symmetric_value_placement": K.getSymmetricPlacement() if K.isSymmetricStorage() else None,
+            "symmetric_bricks": K.getSymmetricBricks() if K.isSymmetricStorage() else None,
             "assembly_s": t_asm,
             "mesh_generation_s": t_mesh,
             "setup_s": t_setup,

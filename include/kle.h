@@ -95,19 +95,20 @@ const char *kle_last_error(void);
  * unstructured K is built: rows per group, 64 default, 128, 32, 16 or 8),
  * "spmv_gsym_waves" (read at build: 0 auto = 16 for 64-row groups, else 8;
  * 8 or 16), "spmv_gsym_split" (read at build: the largest dictionary of the
- * first of its two launches; 0 auto), "spmv_sym_place" (read at build: up
- * to this many fresh copies of a symmetric value array of at least
- * "spmv_sym_place_min_mb" (256) MB timed against the first until one streams
- * "spmv_sym_place_gbps" (5450) GB/s of its algorithmic bytes, the fastest
- * kept -- the same values at another placement; default 16, 0 off),
+ * first of its two launches; 0 auto), "spmv_sym_brick" (read at build:
+ * the box K of one rank on bricks -- one 16-wave workgroup per CU, the
+ * brick region's x and exact sums in LDS for the whole value stream; 1
+ * default, 0 the 128-row tiles), "spmv_brick_ahead" (brick kernel: items in
+ * flight ahead of the summed one, 1 default or 2), "spmv_brick_max" (read at
+ * build: at most this many bricks, 0 = one per CU), "spmv_brick_split" (read
+ * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
  * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo
  * overlap: the percentage of the interior tiles run beside the reverse halo,
  * the rest beside the forward halo; default 50), "spmv_sym_early" (box tile kernel loads its first items before
  * x is in LDS; 0 default), "spmv_sym_align" (read at build: partial slots
- * aligned to 128-B lines; 0 default), "spmv_sym_alloc" (read at build: bit 1
- * values, bit 2 partials physically contiguous; 0 default), "spmv_sym_stpol"
+ * aligned to 128-B lines; 0 default), "spmv_sym_stpol"
  * (box kernel's partial stores: 0 plain default, 1 nontemporal, 2 sc1, 3 sc0
  * sc1), "spmv_gsym_stpol" (the same for the graph kernel; default 2).
  * Every value gives correct results (the
@@ -161,6 +162,17 @@ int kle_ctx_barrier(kle_ctx *ctx); /* device-side RCCL barrier + stream sync */
  * (may be NULL) and the transport: 0 single rank, 1 RCCL, 2 host-staged,
  * 3 IPC mailboxes (kle_ctx_enable_ipc). */
 int kle_ctx_get_device(kle_ctx *ctx, int *device, char *pci_bus_id, int len, int *transport);
+/* What the RCCL communicator itself reports (ncclCommCount /
+ * ncclCommUserRank; the MPI communicator of DMPlex.distribute, dmplex.py:21,
+ * and of KSPSolve's reductions, kle_solver.py:35): *count = 0, *rank = -1
+ * when the context has no RCCL communicator (one rank, host or IPC transport). */
+int kle_ctx_get_comm_info(kle_ctx *ctx, int *count, int *rank);
+/* Diagnostic, host only (no device, no reference counterpart): the brick
+ * plan of the symmetric SpMV for an Lx x Ly x Lz box lattice of p-node
+ * elements (dirichlet: boundary rows the diagonal alone) on ncu CUs (split: forced counts nbx + 100 nby + 10000 nbz, 0
+ * planned).  info: bricks, bricks along x / y / z, LDS bytes; stats: largest
+ * brick's bytes over the mean, region entries per row, stored blocks. */
+int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, int ncu, int split, int *info, double *stats);
 /* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */
 int kle_ctx_set_profiling(kle_ctx *ctx, int on);
 /* Time only the launches tagged `name` ("spmv", "dot", "cg_update", "reduce",
@@ -387,15 +399,11 @@ int kle_mat_is_structured(const kle_mat *A, int *on);
  * default "spmv_sym_det" they are bitwise reproducible run to run. */
 int kle_mat_set_symmetric(kle_mat *A, int on);
 int kle_mat_get_symmetric(const kle_mat *A, int *on);
-/* The value placement kle_mat_set_symmetric kept (tuning "spmv_sym_place",
- * symmetric values >= 256 MB per rank): the timed SpMV of the kept array in
- * microseconds (0: not timed), how many fresh copies were tried and which
- * one was kept (0: the array as built). */
-int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept);
-/* ... and the partials' workspace placements tried after the value copies
- * (tuning "spmv_sym_place_ws", only when no copy streamed fast) and the one
- * kept (0: as built). */
-int kle_mat_get_sym_placement_ws(const kle_mat *A, int *tries, int *kept);
+/* The brick decomposition of A's symmetric storage (kle_brick.hip; 0 bricks:
+ * none -- full storage, tiles or the graph kernel): bricks, bricks along
+ * x / y / z, region entries per row, the planner's modelled product time
+ * (us). */
+int kle_mat_get_sym_bricks(const kle_mat *A, int *nbricks, int *dims, double *entries_per_row, double *model_us);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */
 int kle_mat_set_halo_overlap(kle_mat *A, int on);

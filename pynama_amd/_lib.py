@@ -62,6 +62,9 @@ _SIGS = {
     "kle_ctx_synchronize": [vp],
     "kle_ctx_barrier": [vp],
     "kle_ctx_get_device": [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int, C.POINTER(C.c_int)],
+    "kle_ctx_get_comm_info": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "kle_brick_plan_box": [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                           C.POINTER(C.c_double)],
     "kle_ctx_enable_ipc": [vp],
     "kle_ctx_set_profiling": [vp, C.c_int],
     "kle_ctx_set_profiling_sample": [vp, C.c_int],
@@ -146,8 +149,8 @@ _SIGS = {
     "kle_mat_is_structured": [vp, C.POINTER(C.c_int)],
     "kle_mat_set_symmetric": [vp, C.c_int],
     "kle_mat_get_symmetric": [vp, C.POINTER(C.c_int)],
-    "kle_mat_get_sym_placement": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)],
-    "kle_mat_get_sym_placement_ws": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "kle_mat_get_sym_bricks": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                               C.POINTER(C.c_double)],
     "kle_get_nb_pad": [],
     "kle_set_nb_layout": [C.c_int],
     "kle_get_nb_layout": [],

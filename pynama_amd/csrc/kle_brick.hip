@@ -1,0 +1,664 @@
+// kle_brick.hip -- the box symmetric SpMV on bricks (round 5).
+//
+// Symmetric (SBAIJ-style, upper-triangle) storage of the structured KLE K
+// (kle_mat_set_symmetric = MatSetOption(MAT_SPD); MatFS.buildFS,
+// mat_fs.py:150-192; the product is the MatMult inside KSPSolve,
+// kle_solver.py:35).  Block (i, j), j >= i, serves row i (B x_j) and row j
+// (B^T x_i), so the rows a workgroup touches extend past the rows it owns and
+// their sums meet those of other workgroups.  Rounds 2-4 cut the lattice into
+// 128-row tiles and wrote each tile's region sums to HBM in the middle of the
+// value stream (4.6 partial entries per row, 90 MB per SpMV at config 2);
+// those stores made the stream's speed depend on where the value array lay
+// (424-491 us at config 2).
+//
+// Here the owned lattice is cut into one element-aligned brick per CU (config
+// 2: 4 x 4 x 16 bricks of 20 x 16 x 4 nodes), and one 16-wave workgroup
+// streams a whole brick with x AND the exact int64 fixed-point sums of the
+// brick's region (25 x 21 x 5 nodes: 126 KB) resident in LDS from the first
+// value load to the last.  Nothing is stored while the value array streams;
+// at the end each brick writes its region once (2.05 entries per row, 16 MB),
+// and k_nb_sym_brick_gather adds, per row, the sums of the bricks whose
+// regions hold it in ascending brick order (bitwise reproducible, as the
+// fixed-point sums are order-free).  Inside a brick the waves take rows from
+// an LDS counter, so the brick's end is one row long, not one wave's share.
+// The value array is laid out brick by brick (rows in brick order, each row's
+// upper tail in the 16-block chunk layout), so every CU streams one
+// contiguous range.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "kle_brick.hpp"
+#include "kle_internal.hpp"
+#include "kle_sym_dev.hpp"
+
+namespace kle {
+
+using cint = __attribute__((address_space(4))) const int;
+
+// a row of the brick (every field wave-uniform: SGPRs)
+struct BRow {
+    const double *v;
+    double x0, x1, x2;
+    int bnx, bnxy, k0, mu, rb0, ir, r;
+    float ibnx, ibnxy;
+};
+
+// an issued item: its row (r < 0: a re-read past the brick's last row), the
+// row's stored blocks and region index, the pass's first block
+struct BItem {
+    int r, mu, ir, kb;
+};
+
+// y of brick O's rows from the region sums of the bricks nblist[nbptr[O] ..)
+// (ascending), by NT threads.  (Summing them inside the brick kernel, each
+// brick by the last of its neighbours to finish -- arrival counters, sc1
+// sums -- put the reductions on the slowest CUs: 0.485-0.564 vs 0.399-0.402
+// ms at config 2, profiles/r05/brick_fuse_rejected.jsonl.)
+// nbd: LDS for 8 ints per listed brick; dred: LDS for NT / 64 doubles.
+template <int NT>
+__device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const BrickDesc *__restrict__ bd,
+                                             const int *__restrict__ nbptr, const int *__restrict__ nblist,
+                                             const double *__restrict__ ws, double *__restrict__ y,
+                                             const double *__restrict__ xdot, double *__restrict__ dpart, int *nbd,
+                                             double *dred, int r0 = 0, int r1 = INT_MAX, int dslot = -1)
+{
+    const int x0 = bd[O].x0, y0 = bd[O].y0, z0 = bd[O].z0, nx = bd[O].nx, ny = bd[O].ny, nz = bd[O].nz;
+    const int NR = nx * ny * nz, q0 = nbptr[O], nq = min(nbptr[O + 1] - q0, BG_MAXNB);
+    if ((int)threadIdx.x < nq) {
+        const BrickDesc &E = bd[nblist[q0 + threadIdx.x]];
+        int *o = nbd + 8 * threadIdx.x;
+        o[0] = E.ox;
+        o[1] = E.oy;
+        o[2] = E.oz;
+        o[3] = E.RX;
+        o[4] = E.RY;
+        o[5] = E.RZ;
+        o[6] = (int)(E.wsoff & 0xffffffffll);
+        o[7] = (int)(E.wsoff >> 32);
+    }
+    __syncthreads();
+    const int64_t Lxy = (int64_t)Lx * Ly;
+    double dsum = 0.0;
+    for (int r = r0 + (int)threadIdx.x; r < min(NR, r1); r += NT) {
+        const int rz = r / (nx * ny), rem = r - rz * nx * ny, ry = rem / nx, rx = rem - ry * nx;
+        const int gx = x0 + rx, gy = y0 + ry, gz = z0 + rz;
+        const int64_t j = gx + (int64_t)Lx * gy + Lxy * gz;
+        double s0 = y[3 * j], s1 = y[3 * j + 1], s2 = y[3 * j + 2];  // (the row's direct sum)
+        // (four bricks' loads in flight before their adds, in brick order)
+        for (int q = 0; q < nq; q += 4) {
+            double a[4][3];
+            bool in[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int qq = min(q + u, nq - 1);
+                const int *o = nbd + 8 * qq;
+                const int lx = gx - o[0], ly = gy - o[1], lz = gz - o[2], RX = o[3], RY = o[4], RZ = o[5];
+                in[u] = q + u < nq && lx >= 0 && lx < RX && ly >= 0 && ly < RY && lz >= 0 && lz < RZ;
+                const int64_t wo = (int64_t)(unsigned)o[6] | ((int64_t)o[7] << 32);
+                const int RN = RX * RY * RZ;
+                const double *p = ws + wo + (in[u] ? lx + RX * (ly + RY * lz) : 0);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) a[u][c] = p[c * RN];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s0 += in[u] ? a[u][0] : 0.0;
+                s1 += in[u] ? a[u][1] : 0.0;
+                s2 += in[u] ? a[u][2] : 0.0;
+            }
+        }
+        y[3 * j] = s0;
+        y[3 * j + 1] = s1;
+        y[3 * j + 2] = s2;
+        if (xdot) dsum += s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
+    }
+    if (xdot) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+        if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;
+    }
+    __syncthreads();
+    if (xdot && threadIdx.x == 0) {
+        double t = 0.0;
+        for (int q = 0; q < NT / 64; ++q) t += dred[q];  // (waves in order)
+        dpart[dslot >= 0 ? dslot : O] = t;
+    }
+}
+
+template <int WV, int D>
+__global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp,
+                                                                 const BrickDesc *__restrict__ bd,
+                                                                 const int2 *__restrict__ rowd,
+                                                                 const double *__restrict__ sval,
+                                                                 const double *__restrict__ x,
+                                                                 double *__restrict__ ws, double *__restrict__ y,
+                                                                 const int *__restrict__ istate KLE_PROBE_PARAM)
+{
+    KLE_PROBE_CONST
+    constexpr int NT = 64 * WV;
+    static_assert(D == 1 || D == 2, "one or two items ahead");
+    extern __shared__ double lds[];
+    KLE_PROBE_TS(ts0)
+    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x0 = bd[b].x0, y0 = bd[b].y0, z0 = bd[b].z0, nx = bd[b].nx, ny = bd[b].ny, nz = bd[b].nz;
+    const int ox = bd[b].ox, oy = bd[b].oy, oz = bd[b].oz, RX = bd[b].RX, RY = bd[b].RY, RZ = bd[b].RZ;
+    const int rstart = bd[b].rstart, eb = bd[b].eb;
+    const long long vbase = bd[b].vbase, wsoff = bd[b].wsoff;
+    const int RN = RX * RY * RZ, RS = RN + 64, NR = nx * ny * nz;
+    double *xl = lds;
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(lds + 3 * RN);
+    double *wred = lds + 3 * RN + 3 * RS;
+    int *ctr = reinterpret_cast<int *>(wred + 2 * WV);
+    const int64_t Lxy = (int64_t)Lx * Ly;
+    cint *rdesc = (cint *)(rowd + rstart);  // (address-space cast: scalar loads)
+    const double *vb = sval + vbase;
+    // a row from its descriptor: packed box (dbx, dby, dbz, bnx, bny, bnz: 4
+    // bits each) + the low byte of its region index; value offset / 16
+    // doubles (24 bits) + the high byte
+    auto row_setup = [&](int r, int dw, int vw, BRow &R) {
+        const int dbx = dw & 15, dby = (dw >> 4) & 15, dbz = (dw >> 8) & 15;
+        R.bnx = (dw >> 12) & 15;
+        const int bny = (dw >> 16) & 15, bnz = (dw >> 20) & 15;
+        R.bnxy = R.bnx * bny;
+        R.k0 = dbx + R.bnx * (dby + bny * dbz);
+        R.mu = R.bnxy * bnz - R.k0;
+        R.ir = ((dw >> 24) & 255) | (((vw >> 24) & 255) << 8);
+        R.rb0 = R.ir - (dbx + RX * (dby + RY * dbz));
+        R.v = vb + (int64_t)(vw & 0xFFFFFF) * 16;
+        R.r = r;
+        R.ibnx = __builtin_amdgcn_rcpf((float)R.bnx);
+        R.ibnxy = __builtin_amdgcn_rcpf((float)R.bnxy);
+        R.ibnx = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, R.ibnx)));
+        R.ibnxy = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, R.ibnxy)));
+    };
+    auto row_x = [&](BRow &R) {
+        R.x0 = uni_d(xl[R.ir]);
+        R.x1 = uni_d(xl[RN + R.ir]);
+        R.x2 = uni_d(xl[2 * RN + R.ir]);
+    };
+    // the values of one 64-block pass of a row (lanes past its end re-read
+    // its last block; their results go nowhere) and each block's region index
+    auto load_v = [&](const BRow &R, int kb, double *vv, int &rr) {
+        const int kk = min(kb + lane, R.mu - 1);
+        const int q16 = R.mu & ~15;
+        const bool ch = kk < q16;
+        const int o0 = ch ? (kk >> 4) * 144 + (kk & 15) : q16 * 9 + (kk - q16);
+        const int st = ch ? 16 : R.mu - q16;
+        unsigned o[9];
+#pragma unroll
+        for (int s = 0; s < 9; ++s) o[s] = (unsigned)(o0 + s * st) * 8u;
+        sym_ld9(vv, R.v, o);
+        const int k = R.k0 + kk;
+        const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
+        const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
+        rr = R.rb0 + kx + RX * (ky + RY * kz);
+    };
+    // 1. the wave's first rows are static (w, w + WV, w + 2 WV: the counter
+    // starts past them), so its first D items go out before the fill
+    auto grab = [&]() -> int {
+        int r = 0;
+        if (lane == 0) r = atomicAdd(ctr, 1);
+        return __builtin_amdgcn_readfirstlane(r);
+    };
+    int snext = w + WV;
+    auto take = [&]() -> int {  // (the next row of this wave)
+        if (snext < 3 * WV) {
+            const int r = snext;
+            snext += WV;
+            return r;
+        }
+        return grab();
+    };
+    BRow I;
+    int ki = 0;
+    bool idone = w >= NR;
+    double v0[9], v1[9], v2[9];
+    int r0 = 0, r1 = 0, r2 = 0;
+    BItem i0, i1, i2;
+    if (!idone) {
+        row_setup(w, rdesc[2 * w], rdesc[2 * w + 1], I);
+    } else {
+        I.v = vb;
+        I.mu = 1;
+        I.k0 = 0;
+        I.bnx = I.bnxy = 1;
+        I.ibnx = I.ibnxy = 1.0f;
+        I.rb0 = 0;
+        I.ir = 0;
+        I.r = -1;
+    }
+    load_v(I, 0, v0, r0);
+    i0 = {idone ? -1 : I.r, I.mu, I.ir, 0};
+    // the next row and its descriptor, fetched one row ahead
+    int pend = take();
+    int pdw = rdesc[2 * min(pend, NR - 1)], pvw = rdesc[2 * min(pend, NR - 1) + 1];
+    auto issue = [&](double *vn, int &rn, BItem &itn) {
+        if (!idone) {
+            if (ki + 64 < I.mu) {
+                ki += 64;
+            } else if (pend >= NR) {
+                idone = true;
+            } else {
+                row_setup(pend, pdw, pvw, I);
+                ki = 0;
+                pend = take();
+                pdw = rdesc[2 * min(pend, NR - 1)];
+                pvw = rdesc[2 * min(pend, NR - 1) + 1];
+            }
+        }
+        load_v(I, ki, vn, rn);
+        itn = {idone ? -1 : I.r, I.mu, I.ir, ki};
+    };
+    if (D == 2) issue(v1, r1, i1);
+    // 2. x of the region into LDS (nodes off the lattice read 0), its max |x|;
+    // the sums zeroed.  Line (ry, rz) of the region is 3 RX contiguous doubles
+    // of x; a thread takes one position in a line and every fstep-th line,
+    // FB loads in flight (unconditional: clamped addresses, masked values)
+    double xm = 0.0;
+    int bad = 0;
+    {
+        constexpr int FB = 12;
+        const int L3 = 3 * RX, NL = RY * RZ;
+        const int c3 = threadIdx.x % L3, l0 = threadIdx.x / L3, fstep = NT / L3;
+        const int rx = c3 / 3, c = c3 - 3 * rx, gx = ox + rx;
+        const bool xok = l0 < fstep && gx >= 0 && gx < Lx;
+        for (int lb = l0; lb < NL; lb += FB * fstep) {
+            double fv[FB];
+#pragma unroll
+            for (int f = 0; f < FB; ++f) {
+                const int l = lb + f * fstep;
+                const int rz = l / RY, ry = l - rz * RY, gy = oy + ry, gz = oz + rz;
+                const bool ok = xok && l < NL && gy >= 0 && gy < Ly && gz + zo >= 0 && gz < Lz + hp;
+                const int64_t node = ok ? gx + (int64_t)Lx * gy + Lxy * (gz + zo) : 0;
+                const double v = x[3 * node + c];
+                fv[f] = ok ? v : 0.0;
+            }
+#pragma unroll
+            for (int f = 0; f < FB; ++f) {
+                const int l = lb + f * fstep;
+                const bool st = l0 < fstep && l < NL;
+                xl[st ? c * RN + rx + RX * l : 4 * RN + lane] = fv[f];  // (else a dummy slot of the sums)
+                const double a = fabs(fv[f]);
+                bad |= !(a <= 1.7976931348623157e308);
+                xm = fmax(xm, a);
+            }
+        }
+    }
+    for (int k = threadIdx.x; k < 3 * RS; k += NT) acc[k] = 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) xm = fmax(xm, __shfl_xor(xm, o, 64));
+    const unsigned long long anybad = __ballot(bad);
+    if (lane == 0) {
+        wred[w] = xm;
+        wred[WV + w] = anybad ? 1.0 : 0.0;
+    }
+    if (threadIdx.x == 0) *ctr = 3 * WV;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // LDS stores done (lgkmcnt 0); the value loads stay in flight
+    __builtin_amdgcn_s_barrier();
+    if (__builtin_amdgcn_readfirstlane(stop) != 0) return;  // (nothing written yet)
+    // the brick's scale: 2^(61 - E), 2^E > (its sums' bound, k_brick_bound) x
+    // max |x|, as two factors S1 S2 (and 1 / S as T1 T2), each a normal
+    // double, so that x near the bottom of the exponent range (2^(61 - E) >
+    // 2^1023) keeps its 61 bits too
+    double S1 = 1.0, S2 = 1.0, T1 = 1.0, T2 = 1.0;
+    {
+        double m = 0.0, nb = 0.0;
+#pragma unroll
+        for (int q = 0; q < WV; ++q) {
+            m = fmax(m, wred[q]);
+            nb += wred[WV + q];
+        }
+        if (nb != 0.0) {
+            S1 = 0.0;  // non-finite x: NaN sums, as a floating-point product would give
+            T1 = __builtin_nan("");
+        } else if (m > 0.0) {
+            int em;
+            (void)frexp(m, &em);
+            const int E = min(max(eb + em, -1070), 1020);
+            const int e1 = min(61 - E, 1000), e2 = 61 - E - e1;
+            S1 = ldexp(1.0, e1);
+            S2 = ldexp(1.0, e2);
+            T1 = ldexp(1.0, -e1);
+            T2 = ldexp(1.0, -e2);
+        }
+    }
+    KLE_PROBE_TS(ts1)
+    // 3. items = (row, pass of 64 blocks), rows from the LDS counter.  The
+    // issue cursor runs D items in front of the compute cursor; each issued
+    // item leaves a record (row, its length and region index, first block),
+    // so the compute cursor needs no row state of the issue cursor.  Past the
+    // brick's last row the issue cursor stays on its last item, re-reading it
+    // (cache hits) under a record r = -1, so every step issues 9 loads and the
+    // wait for the summed item is a fixed vmcnt(9 D).
+    if (i0.r >= 0) {
+        double cx0 = 0.0, cx1 = 0.0, cx2 = 0.0;
+        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        // one step: issue the next item into vn, wait for vv (the D newer
+        // items stay in flight), sum it
+        auto step = [&](double *vv, const int rr, const BItem &it, double *vn, int &rn, BItem &itn) {
+            issue(vn, rn, itn);
+            if (it.r < 0) return false;
+            if (it.kb == 0) {  // a new row: x of the row
+                cx0 = uni_d(xl[it.ir]);
+                cx1 = uni_d(xl[RN + it.ir]);
+                cx2 = uni_d(xl[2 * RN + it.ir]);
+            }
+            const double xj0 = xl[rr], xj1 = xl[RN + rr], xj2 = xl[2 * RN + rr];
+            sym_wait9<9 * D>(vv);
+            // B x_j into the row, B^T x_i into row j (lanes past the row's end
+            // and the diagonal block add into their dummy slot)
+            const int kk = it.kb + lane;
+            const bool live = kk < it.mu;
+            const int rt = live && kk > 0 ? rr : RN + lane;
+            const double s0 = vv[0] * xj0 + vv[1] * xj1 + vv[2] * xj2;
+            const double s1 = vv[3] * xj0 + vv[4] * xj1 + vv[5] * xj2;
+            const double s2 = vv[6] * xj0 + vv[7] * xj1 + vv[8] * xj2;
+            acc0 += live ? s0 : 0.0;
+            acc1 += live ? s1 : 0.0;
+            acc2 += live ? s2 : 0.0;
+            const double t0 = vv[0] * cx0 + vv[3] * cx1 + vv[6] * cx2;
+            const double t1 = vv[1] * cx0 + vv[4] * cx1 + vv[7] * cx2;
+            const double t2 = vv[2] * cx0 + vv[5] * cx1 + vv[8] * cx2;
+            if (!(probe & 1)) {  // (timing probe 1: no transposed adds)
+                atomicAdd(&acc[rt], fx_of(t0 * S1, S2));
+                atomicAdd(&acc[RS + rt], fx_of(t1 * S1, S2));
+                atomicAdd(&acc[2 * RS + rt], fx_of(t2 * S1, S2));
+            } else if (!live) {
+                acc[RN + lane] += (unsigned long long)(t0 + t1 + t2);
+            }
+            if (it.kb + 64 >= it.mu) {
+                // the row is done: its direct sum (fixed-order DPP, fp64), one
+                // writer, into y -- the gather adds the bricks' transposed
+                // sums to it, so an identity (Dirichlet) row returns x bit for
+                // bit (8 MB of stores at config 2: the only ones before the end)
+                wsum3_dpp(acc0, acc1, acc2);
+                const int rz = it.r / (nx * ny), rem = it.r - rz * nx * ny, ry = rem / nx, rx = rem - ry * nx;
+                const int64_t j = (x0 + rx) + (int64_t)Lx * (y0 + ry) + Lxy * (z0 + rz);
+                if (lane < 3) y[3 * j + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
+                acc0 = acc1 = acc2 = 0.0;
+            }
+            return true;
+        };
+        if constexpr (D == 1) {
+            while (step(v0, r0, i0, v1, r1, i1) && step(v1, r1, i1, v0, r0, i0)) {
+            }
+        } else {
+            while (step(v0, r0, i0, v2, r2, i2) && step(v1, r1, i1, v0, r0, i0) && step(v2, r2, i2, v1, r1, i1)) {
+            }
+        }
+    }
+    // the last (re-read) loads land before their registers are reused
+    sym_wait9<0>(v0);
+    sym_wait9<0>(v1);
+    if (D == 2) sym_wait9<0>(v2);
+    __syncthreads();
+    KLE_PROBE_TS(ts2)
+    // 4. the region's transposed sums, once (nodes off the lattice are never read)
+    double *dst = ws + wsoff;
+    for (int k = threadIdx.x; k < RN; k += NT) {
+        const int rz = k / (RX * RY), rem = k - rz * RX * RY, ry = rem / RX, rx = rem - ry * RX;
+        const int gx = ox + rx, gy = oy + ry, gz = oz + rz;
+        if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dst[c * RN + k] = fx_to_d(acc[c * RS + k]) * T1 * T2;
+    }
+    KLE_PROBE_TS_END(b, ts0, ts1, ts2)
+}
+
+// y_j = the region sums of the bricks whose regions hold row j, in ascending
+// brick order (brick_reduce), after the brick kernel.
+// Workgroup (brick b, part s) takes b's owned rows [256 s, 256 s + 256);
+// with xdot its (y, x) partial goes to dpart[b * parts + s].
+__global__ __launch_bounds__(256) void k_nb_sym_brick_gather(int Lx, int Ly, int parts, const BrickDesc *__restrict__ bd,
+                                                             const int *__restrict__ nbptr,
+                                                             const int *__restrict__ nblist,
+                                                             const double *__restrict__ ws, double *__restrict__ y,
+                                                             const int *__restrict__ istate,
+                                                             const double *__restrict__ xdot,
+                                                             double *__restrict__ dpart)
+{
+    __shared__ double dred[4];
+    __shared__ int nbd[BG_MAXNB * 8];
+    const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;
+    if (stop) return;  // (uniform)
+    const int b = blockIdx.x / parts, s = blockIdx.x - b * parts;
+    brick_reduce<256>(b, Lx, Ly, bd, nbptr, nblist, ws, y, xdot, dpart, nbd, dred, 256 * s, 256 * s + 256,
+                             (int)blockIdx.x);
+}
+
+// Per brick: eb with 2^eb > the largest, over its region nodes j, of
+//   sum over the brick's rows i != j with j in i's stored blocks of
+//   max_b sum_a |B_ij[a][b]|   (the transposed adds, each <= that x max|x|)
+// + (j owned by the brick) max_a sum over row j's stored blocks of sum_b |B[a][b]|
+// (its direct sum), so no region sum can exceed 2^61 at the scale 2^(61-E),
+// E = eb + (exponent of max |x| over the region).  Fixed summation order.
+__global__ __launch_bounds__(256) void k_brick_bound(int Lx, int Ly, int Lz, int zo, int hp,
+                                                     const BrickDesc *__restrict__ bd, const int *__restrict__ rowbox,
+                                                     const int *__restrict__ smu, const int64_t *__restrict__ svptr,
+                                                     const double *__restrict__ sval, int P, int *__restrict__ ebo)
+{
+    __shared__ double wred[256];
+    const int b = blockIdx.x;
+    const BrickDesc D = bd[b];
+    const int RN = D.RX * D.RY * D.RZ;
+    const int64_t Lxy = (int64_t)Lx * Ly;
+    double wm = 0.0;
+    for (int k = threadIdx.x; k < RN; k += 256) {
+        const int rz = k / (D.RX * D.RY), rem = k - rz * D.RX * D.RY, ry = rem / D.RX, rx = rem - ry * D.RX;
+        const int gx = D.ox + rx, gy = D.oy + ry, gz = D.oz + rz;  // (owned z)
+        if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
+        double s = 0.0;
+        // rows i of the brick whose boxes may hold j: within P of it, not above it
+        for (int iz = max(D.z0, gz - P); iz <= min(D.z0 + D.nz - 1, gz); ++iz)
+            for (int iy = max(D.y0, gy - P); iy <= min(D.y0 + D.ny - 1, gy + P); ++iy)
+                for (int ix = max(D.x0, gx - P); ix <= min(D.x0 + D.nx - 1, gx + P); ++ix) {
+                    const int64_t i = ix + (int64_t)Lx * iy + Lxy * iz;
+                    const int64_t base = rowbox[2 * i];
+                    const int d = rowbox[2 * i + 1];
+                    const int bze = (int)(base / Lxy), by = (int)((base - bze * Lxy) / Lx);
+                    const int bx = (int)(base - bze * Lxy - (int64_t)by * Lx), bz = bze - zo;
+                    const int bnx = d & 255, bny = (d >> 8) & 255, bnz = (d >> 16) & 255;
+                    if (gx < bx || gx >= bx + bnx || gy < by || gy >= by + bny || gz < bz || gz >= bz + bnz) continue;
+                    const int k0 = (ix - bx) + bnx * ((iy - by) + bny * (iz - bz));
+                    const int kj = (gx - bx) + bnx * ((gy - by) + bny * (gz - bz));
+                    if (kj <= k0) continue;  // (lower triangle or the diagonal block)
+                    const int mu = bnx * bny * bnz - k0, kk = kj - k0;
+                    const double *v = sval + svptr[i];
+                    double bmax = 0.0;
+#pragma unroll
+                    for (int bb = 0; bb < 3; ++bb) {
+                        double cs = 0.0;
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) cs += fabs(v[vofs(1, 9, a * 3 + bb, kk, mu, mu)]);
+                        bmax = fmax(bmax, cs);
+                    }
+                    s += bmax;
+                }
+        if (gx >= D.x0 && gx < D.x0 + D.nx && gy >= D.y0 && gy < D.y0 + D.ny && gz >= D.z0 && gz < D.z0 + D.nz) {
+            // the row's own direct sum
+            const int64_t j = gx + (int64_t)Lx * gy + Lxy * gz;
+            const int mu = smu[j];  // (stored blocks of row j)
+            const double *v = sval + svptr[j];
+            double rmax = 0.0;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                double rs = 0.0;
+                for (int kk = 0; kk < mu; ++kk)
+#pragma unroll
+                    for (int bb = 0; bb < 3; ++bb) rs += fabs(v[vofs(1, 9, a * 3 + bb, kk, mu, mu)]);
+                rmax = fmax(rmax, rs);
+            }
+            s += rmax;
+        }
+        wm = fmax(wm, s);
+    }
+    wred[threadIdx.x] = wm;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) wred[threadIdx.x] = fmax(wred[threadIdx.x], wred[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int e = -1000;  // (an all-zero brick)
+        if (wred[0] > 0.0) (void)frexp(wred[0], &e);
+        ebo[b] = e;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+
+int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &cnt, const std::vector<int> &srow,
+                int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out)
+{
+    auto *bp = new BrickPlan;
+    const int ncu = g_tune.spmv_brick_max > 0 ? g_tune.spmv_brick_max : std::max(1, A->ctx->num_cus);
+    why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], ncu, g_tune.spmv_brick_split, cnt,
+                     srow, P, *bp, std::max(1, A->ctx->num_cus));
+    if (!why.empty()) {
+        delete bp;
+        *plan_out = nullptr;
+        return 0;
+    }
+    svptr_out = bp->svb;
+    *plan_out = bp;
+    return 0;
+}
+
+// after the values are in place (d_sval, d_svptr in brick layout): the brick
+// tables on the device, the workspace, the bound exponents
+int brick_finish(kle_mat *A, void *plan)
+{
+    std::unique_ptr<BrickPlan> bp(reinterpret_cast<BrickPlan *>(plan));
+    kle_ctx *c = A->ctx;
+    const int NB = (int)bp->bricks.size();
+    const int64_t n = A->nrows;
+    int *dmu = nullptr;
+    std::vector<int> hmu(n, 0);
+    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NB) != hipSuccess ||
+                 hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
+                 hipMalloc(&A->d_bnbptr, sizeof(int) * (NB + 1)) != hipSuccess ||
+                 hipMalloc(&A->d_bnb, sizeof(int) * std::max<size_t>(bp->nblist.size(), 1)) != hipSuccess ||
+
+                 hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
+                 hipMalloc(&A->d_stile_e, sizeof(int) * NB) != hipSuccess || hipMalloc(&dmu, sizeof(int) * n) != hipSuccess;
+    (void)hipGetLastError();
+    if (nomem) {
+        if (dmu) (void)hipFree(dmu);
+        return fail(KLE_ERR_MEM, "out of device memory for the symmetric SpMV bricks");
+    }
+    A->sws_bytes = sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1);
+    // stored blocks per row (the bound's direct sums) from the row descriptors
+    {
+        for (const BrickDesc &D : bp->bricks)
+            for (int r = 0; r < D.nx * D.ny * D.nz; ++r) {
+                const int d = bp->rowd[2 * ((int64_t)D.rstart + r)];
+                const int dbx = d & 15, dby = (d >> 4) & 15, dbz = (d >> 8) & 15;
+                const int bnx = (d >> 12) & 15, bny = (d >> 16) & 15, bnz = (d >> 20) & 15;
+                const int rz = r / (D.nx * D.ny), rem = r - rz * D.nx * D.ny, ry = rem / D.nx, rx = rem - ry * D.nx;
+                const int64_t i = (D.x0 + rx) + A->row_lat[0] * ((D.y0 + ry) + A->row_lat[1] * (int64_t)(D.z0 + rz));
+                hmu[i] = bnx * bny * bnz - (dbx + bnx * (dby + bny * dbz));
+            }
+    }
+    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_browd, bp->rowd.data(), sizeof(int) * bp->rowd.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_bnbptr, bp->nbptr.data(), sizeof(int) * (NB + 1), hipMemcpyHostToDevice));
+    if (!bp->nblist.empty())
+        KLE_HIP(hipMemcpy(A->d_bnb, bp->nblist.data(), sizeof(int) * bp->nblist.size(), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
+    const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
+    hipLaunchKernelGGL(k_brick_bound, dim3((unsigned)NB), dim3(256), 0, c->stream, (int)A->row_lat[0],
+                       (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, reinterpret_cast<const BrickDesc *>(A->d_bdesc),
+                       A->d_rowbox, dmu, A->d_svptr, A->d_sval, A->sym_P, A->d_stile_e);
+    KLE_HIP(hipGetLastError());
+    // the exponents into the descriptors
+    std::vector<int> eb(NB);
+    KLE_HIP(hipStreamSynchronize(c->stream));
+    KLE_HIP(hipMemcpy(eb.data(), A->d_stile_e, sizeof(int) * NB, hipMemcpyDeviceToHost));
+    (void)hipFree(dmu);
+    for (int q = 0; q < NB; ++q) bp->bricks[q].eb = eb[q];
+    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
+    A->nbricks = NB;
+    for (int k = 0; k < 3; ++k) A->brick_dims[k] = 0;
+    for (const BrickDesc &D : bp->bricks) {
+        A->brick_dims[0] += D.y0 == 0 && D.z0 == 0;
+        A->brick_dims[1] += D.x0 == 0 && D.z0 == 0;
+        A->brick_dims[2] += D.x0 == 0 && D.y0 == 0;
+    }
+    A->brick_model_us = bp->model_us;
+    {
+        int mr = 0;
+        for (const BrickDesc &D : bp->bricks) mr = std::max(mr, D.nx * D.ny * D.nz);
+        A->brick_gparts = (mr + 255) / 256;
+    }
+    A->brick_lds = (int)bp->lds;
+    A->sws_entries = bp->ws_entries;
+    A->sym_brick = 1;
+    if (const char *e = getenv("KLE_TIMING"))
+        if (atoi(e)) {
+            const BrickDesc &D = bp->bricks[0];
+            fprintf(stderr, "[kle brick] %d bricks (first %d x %d x %d rows, region %d x %d x %d), LDS %zu B, "
+                            "region entries %lld (%.2f per row)\n",
+                    NB, D.nx, D.ny, D.nz, D.RX, D.RY, D.RZ, bp->lds, (long long)bp->ws_entries,
+                    (double)bp->ws_entries / n);
+        }
+    return 0;
+}
+
+void brick_plan_free(void *plan) { delete reinterpret_cast<BrickPlan *>(plan); }
+
+void brick_drop(kle_mat *A)
+{
+    for (void *q : {A->d_bdesc, (void *)A->d_browd, (void *)A->d_bnbptr, (void *)A->d_bnb})
+        if (q) (void)hipFree(q);
+    brick_forget(A);
+}
+
+void brick_forget(kle_mat *A)
+{
+    A->d_bdesc = nullptr;
+    A->d_browd = nullptr;
+    A->d_bnbptr = A->d_bnb = nullptr;
+    A->nbricks = 0;
+    A->brick_gparts = 0;
+    A->brick_dims[0] = A->brick_dims[1] = A->brick_dims[2] = 0;
+    A->brick_model_us = 0.0;
+    A->brick_lds = 0;
+    A->sym_brick = 0;
+}
+
+int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
+{
+    kle_ctx *c = A->ctx;
+    const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
+    const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
+    const BrickDesc *bd = reinterpret_cast<const BrickDesc *>(A->d_bdesc);
+    auto go = [&](auto kern, int slot) {
+        static int lds_set[2] = {0, 0};  // dynamic LDS above 64 KB must be declared per kernel
+        if (A->brick_lds > lds_set[slot]) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      A->brick_lds);
+            lds_set[slot] = A->brick_lds;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * BRICK_WV), (size_t)A->brick_lds, c->stream,
+                           (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, bd,
+                           reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
+                           istate KLE_PROBE_ARG);
+    };
+    if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1);
+    else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0);
+    KLE_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_nb_sym_brick_gather, dim3((unsigned)(A->nbricks * A->brick_gparts)), dim3(256), 0,
+                           c->stream, (int)A->row_lat[0], (int)A->row_lat[1], A->brick_gparts, bd, A->d_bnbptr,
+                           A->d_bnb, A->d_sws, y->d, istate, dpart ? x->d : nullptr, dpart);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // namespace kle

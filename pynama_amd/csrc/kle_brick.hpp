@@ -1,0 +1,51 @@
+// kle_brick.hpp -- the brick decomposition of the box symmetric SpMV
+// (kle_brick.hip: kernels and device set-up; kle_brick_plan.cpp: the host
+// planner, also reachable on a CPU through kle_brick_plan_box).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace kle {
+
+// per brick (device, 64 B): owned box in owned-lattice coordinates, the
+// region (bounding box of its rows' upper triangles; z in owned coordinates),
+// its first row descriptor, the bound exponent of its fixed-point sums, where
+// its values and its region sums live
+struct BrickDesc {
+    int x0, y0, z0, nx, ny, nz;
+    int ox, oy, oz, RX, RY, RZ;
+    int rstart, eb;
+    long long vbase, wsoff;
+};
+static_assert(sizeof(BrickDesc) == 72, "BrickDesc layout");
+
+constexpr int BRICK_WV = 16;            // waves per brick workgroup (one workgroup per CU)
+constexpr size_t BRICK_LDS_CAP = 163840;  // LDS per CU
+constexpr size_t BRICK_LDS_MIN = 82 * 1024;  // above half the CU's LDS: never two bricks on one CU
+
+// dynamic LDS of a brick: x [3][RN] | sums [3][RN + 64] (64 dummy slots per
+// component take the adds of masked lanes) | wave maxima, row counter
+
+struct BrickPlan {
+    std::vector<BrickDesc> bricks;
+    std::vector<int> rowd;      // 2 ints per row, brick order
+    std::vector<int64_t> svb;   // per row (natural index): first double of its values, brick layout
+    std::vector<int> nbptr, nblist;  // per brick: the bricks whose regions meet its rows (ascending)
+    int64_t ws_doubles = 0, ws_entries = 0;
+    size_t lds = 0;
+    double model_us = 0.0;  // the planner's time model of the product (us)
+};
+
+// the LDS a brick of RN region nodes needs (x, the transposed sums and their
+// dummy slots, wave maxima, the row counter)
+inline size_t brick_lds(int RN) { return (size_t)(3 * RN + 3 * (RN + 64)) * 8 + 512; }
+constexpr int BG_MAXNB = 64;  // bricks whose regions meet one brick's rows (27 in a regular grid)
+
+// bricks for the owned Lx x Ly x Lz lattice of one rank (rows x-fastest;
+// per row its block count and packed box, kle_sym.hip srow); fs: forced
+// split counts (0: planned), ncu: at most this many bricks.  "" or why not.
+std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vector<int> &cnt,
+                       const std::vector<int> &srow, int P, BrickPlan &bp, int ncu_all = 0);
+
+}  // namespace kle

@@ -237,6 +237,65 @@ __global__ void k_stream_read8(int64_t n, const double *__restrict__ a, double *
     if (s == 1.2345e-300) out[0] = s;
 }
 
+// The streaming ceilings the SpMVs are graded against (verdict r04 item 2):
+// 16 B per lane, U loads in flight per thread (all issued before the first
+// use), each workgroup sweeping contiguous 256 x U x 16-B super-chunks, a
+// grid of a few workgroups per CU.  W = 8: 8-B loads (2U of them) over the
+// same chunk, the symmetric SpMV's value-load width.
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+template <int U, bool NT, int W, int NT_ = 256>
+__global__ __launch_bounds__(NT_) void k_stream_rd(int64_t n16, const dvec2 *__restrict__ a, double *__restrict__ out)
+{
+    double s = 0.0;
+    const int64_t per = (int64_t)NT_ * U;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n16; base += (int64_t)gridDim.x * per) {
+        if (W == 16) {
+            dvec2 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = min(base + u * NT_ + threadIdx.x, n16 - 1);
+                v[u] = NT ? __builtin_nontemporal_load(a + i) : a[i];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) s += v[u].x + v[u].y;
+        } else {
+            const double *d = reinterpret_cast<const double *>(a);
+            double v[2 * U];
+#pragma unroll
+            for (int u = 0; u < 2 * U; ++u) {
+                const int64_t i = min(2 * base + u * NT_ + threadIdx.x, 2 * n16 - 1);
+                v[u] = NT ? __builtin_nontemporal_load(d + i) : d[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 2 * U; ++u) s += v[u];
+        }
+    }
+    if (s == 1.2345e-300) out[0] = s;  // keep the loads alive
+}
+
+// copy with 16-B loads and stores, U in flight; NT: nontemporal stores
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_stream_cp(int64_t n16, const dvec2 *__restrict__ a, dvec2 *__restrict__ b)
+{
+    const int64_t per = (int64_t)256 * U;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n16; base += (int64_t)gridDim.x * per) {
+        dvec2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = min(base + u * 256 + threadIdx.x, n16 - 1);
+            v[u] = __builtin_nontemporal_load(a + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * 256 + threadIdx.x;
+            if (i < n16) {
+                if (NT) __builtin_nontemporal_store(v[u], b + i);
+                else b[i] = v[u];
+            }
+        }
+    }
+}
+
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out)
 {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, ctx->stream, partials, nparts, nq, out);
@@ -648,33 +707,30 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_ovl_b") {
         KLE_ARG(value >= 0 && value <= 100, "spmv_sym_ovl_b: 0 .. 100 %");
         g_tune.spmv_sym_ovl_b = value;
-    } else if (k == "spmv_sym_place") {
-        KLE_ARG(value >= 0 && value <= 32, "spmv_sym_place: 0 .. 32 fresh copies");
-        g_tune.spmv_sym_place = value;
-    } else if (k == "spmv_sym_place_ws") {
-        KLE_ARG(value >= 0 && value <= 32, "spmv_sym_place_ws: 0 .. 32 workspace placements");
-        g_tune.spmv_sym_place_ws = value;
-    } else if (k == "spmv_sym_place_min_mb") {
-        KLE_ARG(value >= 0, "spmv_sym_place_min_mb: >= 0");
-        g_tune.spmv_sym_place_min_mb = value;
-    } else if (k == "spmv_sym_place_gbps") {
-        KLE_ARG(value >= 0 && value <= 100000, "spmv_sym_place_gbps: 0 .. 100000 GB/s");
-        g_tune.spmv_sym_place_gbps = value;
     } else if (k == "spmv_sym_stpol") {
         KLE_ARG(value >= 0 && value <= 3, "spmv_sym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
         g_tune.spmv_sym_stpol = value;
     } else if (k == "spmv_gsym_stpol") {
         KLE_ARG(value >= 0 && value <= 3, "spmv_gsym_stpol: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1");
         g_tune.spmv_gsym_stpol = value;
-    } else if (k == "spmv_sym_alloc") {
-        KLE_ARG(value >= 0 && value <= 3, "spmv_sym_alloc: bits 1 values, 2 partials");
-        g_tune.spmv_sym_alloc = value;
     } else if (k == "spmv_sym_align") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_align: 0 or 1");
         g_tune.spmv_sym_align = value;
     } else if (k == "spmv_sym_early") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_early: 0 or 1");
         g_tune.spmv_sym_early = value;
+    } else if (k == "spmv_brick_ahead") {
+        KLE_ARG(value == 1 || value == 2, "spmv_brick_ahead: 1 or 2");
+        g_tune.spmv_brick_ahead = value;
+    } else if (k == "spmv_brick_split") {
+        KLE_ARG(value >= 0, "spmv_brick_split: nbx + 100 nby + 10000 nbz (0: planned)");
+        g_tune.spmv_brick_split = value;
+    } else if (k == "spmv_brick_max") {
+        KLE_ARG(value >= 0, "spmv_brick_max: >= 0 (0: one brick per CU)");
+        g_tune.spmv_brick_max = value;
+    } else if (k == "spmv_sym_brick") {
+        KLE_ARG(value == 0 || value == 1, "spmv_sym_brick: 0 (128-row tiles) or 1 (bricks)");
+        g_tune.spmv_sym_brick = value;
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
@@ -751,19 +807,18 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_det") *value = g_tune.spmv_sym_det;
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
+    else if (k == "spmv_sym_brick") *value = g_tune.spmv_sym_brick;
+    else if (k == "spmv_brick_ahead") *value = g_tune.spmv_brick_ahead;
+    else if (k == "spmv_brick_max") *value = g_tune.spmv_brick_max;
+    else if (k == "spmv_brick_split") *value = g_tune.spmv_brick_split;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
-    else if (k == "spmv_sym_alloc") *value = g_tune.spmv_sym_alloc;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;
     else if (k == "spmv_gsym_stpol") *value = g_tune.spmv_gsym_stpol;
-    else if (k == "spmv_sym_place") *value = g_tune.spmv_sym_place;
     else if (k == "spmv_sym_ovl_b") *value = g_tune.spmv_sym_ovl_b;
     else if (k == "spmv_sym_xcd") *value = g_tune.spmv_sym_xcd;
     else if (k == "spmv_sym_tile64") *value = g_tune.spmv_sym_tile64;
     else if (k == "spmv_sym_tile64_max") *value = g_tune.spmv_sym_tile64_max;
-    else if (k == "spmv_sym_place_gbps") *value = g_tune.spmv_sym_place_gbps;
-    else if (k == "spmv_sym_place_min_mb") *value = g_tune.spmv_sym_place_min_mb;
-    else if (k == "spmv_sym_place_ws") *value = g_tune.spmv_sym_place_ws;
 #ifdef KLE_PROBE_BUILD
     else if (k == "spmv_sym_probe") *value = g_tune.spmv_sym_probe;
 #endif
@@ -947,6 +1002,18 @@ int kle_ctx_get_device(kle_ctx *c, int *device, char *pci_bus_id, int len, int *
     *device = c->device;
     *transport = c->comm ? 1 : c->ipc ? 3 : (c->nranks > 1 ? 2 : 0);
     if (pci_bus_id) KLE_HIP(hipDeviceGetPCIBusId(pci_bus_id, len, c->device));
+    return 0;
+}
+
+int kle_ctx_get_comm_info(kle_ctx *c, int *count, int *rank)
+{
+    KLE_ARG(c && count && rank, "bad arg");
+    *count = 0;
+    *rank = -1;
+    if (c->comm) {
+        KLE_NCCL(ncclCommCount(c->comm, count));
+        KLE_NCCL(ncclCommUserRank(c->comm, rank));
+    }
     return 0;
 }
 
@@ -1306,16 +1373,37 @@ int kle_stream_bench(kle_ctx *ctx, int64_t bytes, int reps, int mode, double *gb
     int64_t n4 = bytes / 32;
     double4 *a, *b;
     KLE_HIP(hipMalloc(&a, n4 * 32));
-    KLE_HIP(hipMalloc(&b, mode == 0 ? n4 * 32 : 64));
+    const bool copy = mode == 0 || mode == 11 || mode == 12;
+    KLE_HIP(hipMalloc(&b, copy ? n4 * 32 : 64));
     KLE_HIP(hipMemsetAsync(a, 0, n4 * 32, ctx->stream));
-    int g = ctx->num_cus * 8;
+    KLE_ARG(mode >= 0 && mode <= 13, "stream mode 0..13");
+    const int g = ctx->num_cus * 8;
+    // mode 13: 1024-thread workgroups, 16 B x 4 in flight, KLE_STREAM_WGS of
+    // them (default one per CU): the streaming rate of a part of the CUs
+    const char *wg_env = getenv("KLE_STREAM_WGS");
+    const int g13 = wg_env && atoi(wg_env) > 0 ? atoi(wg_env) : ctx->num_cus;
+    const int64_t n16 = n4 * 2;
+    const dvec2 *a2 = reinterpret_cast<const dvec2 *>(a);
+    double *o = reinterpret_cast<double *>(b);
+    // 0 copy (16 B, 4 in flight, nt stores), 1 read (16 B, 4 in flight, nt):
+    // the ceilings bench.py reports; the rest are variants of them
     auto launch = [&]() {
-        if (mode == 0) hipLaunchKernelGGL(k_stream_copy, dim3(g), dim3(256), 0, ctx->stream, n4, a, b);
-        else if (mode == 1) hipLaunchKernelGGL(k_stream_read, dim3(g), dim3(256), 0, ctx->stream, n4, a, (double *)b);
-        else if (mode == 2)
-            hipLaunchKernelGGL(k_stream_read8<true>, dim3(g), dim3(256), 0, ctx->stream, n4 * 4, (const double *)a, (double *)b);
-        else
-            hipLaunchKernelGGL(k_stream_read8<false>, dim3(g), dim3(256), 0, ctx->stream, n4 * 4, (const double *)a, (double *)b);
+        switch (mode) {
+        case 0: hipLaunchKernelGGL((k_stream_cp<4, true>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, reinterpret_cast<dvec2 *>(b)); break;
+        case 1: hipLaunchKernelGGL((k_stream_rd<4, true, 16>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 2: hipLaunchKernelGGL(k_stream_read8<true>, dim3(g), dim3(256), 0, ctx->stream, n4 * 4, (const double *)a, o); break;
+        case 3: hipLaunchKernelGGL(k_stream_read8<false>, dim3(g), dim3(256), 0, ctx->stream, n4 * 4, (const double *)a, o); break;
+        case 4: hipLaunchKernelGGL(k_stream_read, dim3(g), dim3(256), 0, ctx->stream, n4, a, o); break;  // (round 1-4 "read ceiling")
+        case 5: hipLaunchKernelGGL((k_stream_rd<4, false, 16>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 6: hipLaunchKernelGGL((k_stream_rd<8, true, 16>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 7: hipLaunchKernelGGL((k_stream_rd<4, true, 16>), dim3(g / 2), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 8: hipLaunchKernelGGL((k_stream_rd<2, true, 16>), dim3(g * 2), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 9: hipLaunchKernelGGL((k_stream_rd<4, true, 8>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 10: hipLaunchKernelGGL((k_stream_rd<8, true, 8>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, o); break;
+        case 11: hipLaunchKernelGGL(k_stream_copy, dim3(g), dim3(256), 0, ctx->stream, n4, a, b); break;  // (round 1-4 copy)
+        case 13: hipLaunchKernelGGL((k_stream_rd<4, true, 16, 1024>), dim3(g13), dim3(1024), 0, ctx->stream, n16, a2, o); break;
+        default: hipLaunchKernelGGL((k_stream_cp<4, false>), dim3(g), dim3(256), 0, ctx->stream, n16, a2, reinterpret_cast<dvec2 *>(b)); break;
+        }
     };
     launch();
     hipEvent_t e0, e1;
@@ -1327,7 +1415,7 @@ int kle_stream_bench(kle_ctx *ctx, int64_t bytes, int reps, int mode, double *gb
     KLE_HIP(hipEventSynchronize(e1));
     float ms;
     KLE_HIP(hipEventElapsedTime(&ms, e0, e1));
-    *gbps = (mode == 0 ? 2.0 : 1.0) * n4 * 32 * reps / (ms * 1e-3) / 1e9;
+    *gbps = (copy ? 2.0 : 1.0) * n4 * 32 * reps / (ms * 1e-3) / 1e9;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     hipFree(a);

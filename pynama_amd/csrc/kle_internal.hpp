@@ -246,10 +246,6 @@ struct kle_mat {
     int64_t sblocks = 0, snvals = 0, sws_entries = 0;  // sws_entries: lattice entries of the tile partials per SpMV
     int sym_P = 0, sym_TZ = 2, sym_TY = 8;
     int sym_wn = 0;
-    double sym_place_us = 0;  // SpMV time of the kept value placement (sym_place), one rank
-    int sym_place_kept = 0;   // which fresh copy was kept (0: the first allocation)
-    int sym_place_tries = 0;  // fresh copies timed
-    int sym_place_ws_tries = 0, sym_place_ws_kept = 0;  // workspace placements timed / kept (0: as built)
     size_t sws_bytes = 0;     // the partials' workspace (d_sws)  // box: per-component stride of a tile's partials in d_sws (RN, or RN rounded up to 16 doubles)
     int *d_swptr = nullptr;  // graph: per group, its partials' first double in d_sws (128-B aligned with spmv_sym_align)
     int sym_reg[5] = {};  // tile region: PX, RX, PY, RY, RZ (kle_sym.hip SymGeo); graph: slots of launch 1 / 2, groups in launch 1, G
@@ -257,6 +253,16 @@ struct kle_mat {
     // d_srow = stored blocks per row, d_stile_e = per-group scale exponents,
     // d_sws = one partial per dictionary entry
     int sym_graph = 0;
+    // brick decomposition of the box symmetric storage (kle_brick.hip; one
+    // rank): per brick a BrickDesc, per row (brick order) 2 packed ints, per
+    // brick the bricks whose regions meet its rows; d_sws holds the bricks'
+    // region sums, d_stile_e their bound exponents
+    int sym_brick = 0;
+    int nbricks = 0, brick_lds = 0, brick_gparts = 0;  // (gather workgroups per brick)
+    int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
+    double brick_model_us = 0.0;    // the planner's modelled product time
+    void *d_bdesc = nullptr;
+    int *d_browd = nullptr, *d_bnbptr = nullptr, *d_bnb = nullptr;
     int64_t *d_sbp = nullptr;     // per row: its first stored block in d_slid
     uint16_t *d_slid = nullptr;   // per stored block: its column's position in the group dictionary
     int *d_sdptr = nullptr, *d_sdict = nullptr;  // per group of G rows: sorted distinct stored columns
@@ -323,6 +329,16 @@ void sym_forget(kle_mat *A);  // null the symmetric-storage pointers of a struct
 int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate,
              double *dpart = nullptr);  // N > 1: both halos included; dpart: (y, x) partials (one rank)
 int sym_dot_parts(const kle_mat *A);  // partials sym_spmv writes with dpart (0: it cannot)
+// brick symmetric SpMV (kle_brick.hip): plan (values in brick order: svptr
+// out; plan null + why when no brick decomposition applies), finish after the
+// values are copied (takes the plan), product, teardown
+int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &cnt, const std::vector<int> &srow,
+                int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out);
+int brick_finish(kle_mat *A, void *plan);
+void brick_plan_free(void *plan);
+int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart);
+void brick_drop(kle_mat *A);
+void brick_forget(kle_mat *A);
 // IPC transport (kle_ipc.hip): slab and graph-partition halos, their reverse halos, allreduce
 int ipc_halo(kle_ctx *c, double *base, int64_t ghost_lo, int64_t n_local, int64_t ghost_hi, int lo_rank,
              int hi_rank, int64_t send_lo, int64_t send_hi, hipStream_t st);
@@ -361,16 +377,15 @@ struct Tuning {
     int spmv_sym_tile64_max = 640;  // ... 1/8 of config 2 (561 tiles; 374 per rank at N = 8) 75.6 -> 70.6 us (full storage 72.4), 1/4 (935; 748 per rank at N = 4) 121.2 vs 127.8 (profiles/r04/ab/tile64_and_sgpr_ab.jsonl)
     int spmv_sym_xcd = 0;           // box symmetric tile kernel: runs of this many consecutive tiles per XCD (0: round-robin)
     int spmv_sym_ovl_b = 50;        // N > 1 symmetric box SpMV: % of the interior tiles run beside the reverse halo
-    int spmv_sym_place = 16;  // symmetric storage (read at build): at most this many fresh value copies timed against the first, the fastest kept (sym_place); 0 off
-    int spmv_sym_place_ws = 8;       // ... then at most this many workspace placements if no value copy was fast
-    int spmv_sym_place_min_mb = 256;  // ... for value arrays from this size (tests: 0)
-    int spmv_sym_place_gbps = 5450;  // ... stop at the first placement streaming this many GB/s of algorithmic bytes (config 2: fast 5.56-5.62, middling 5.41, slow 4.8)
     int spmv_sym_stpol = 0;   // box symmetric SpMV partial stores: 0 plain, 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through)
     int spmv_gsym_stpol = 2;  // ... of the graph symmetric SpMV: sc1 452.9 -> 449.1 us at 1M DoF (the box kernel: plain 420.5,
                               // sc1 422.1, nt 426.5; profiles/r04/ab/stpol_*.jsonl)
-    int spmv_sym_alloc = 0;   // symmetric storage (read at build): bit 1 values, bit 2 tile partials physically contiguous (hipDeviceMallocContiguous)
     int spmv_sym_early = 0;   // symmetric SpMV tiles: the first item's value loads issued with the x fill (1) or after it (0)
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
+    int spmv_brick_ahead = 1;  // brick SpMV: items in flight ahead of the summed one per wave (1 or 2)
+    int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: one per CU)
+    int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)
+    int spmv_sym_brick = 1;   // box symmetric storage, one rank (read at build): one brick per CU, sums in LDS for the whole stream (kle_brick.hip); 0 the 128-row tiles
 #ifdef KLE_PROBE_BUILD
     // timing probes (wrong results on purpose), compiled only into the probe
     // build tools/libkle_probe.so (make probe), never into libkle.so: skip 1

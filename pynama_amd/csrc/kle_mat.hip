@@ -1440,6 +1440,17 @@ int kle_mat_set_spmv_structured(kle_mat *A, int on)
     return 0;
 }
 
+int kle_mat_get_sym_bricks(const kle_mat *A, int *nbricks, int *dims, double *entries_per_row, double *model_us)
+{
+    KLE_ARG(A && nbricks && dims && entries_per_row && model_us, "null arg");
+    const bool on = A->d_sval && A->sym_brick;
+    *nbricks = on ? A->nbricks : 0;
+    for (int k = 0; k < 3; ++k) dims[k] = on ? A->brick_dims[k] : 0;
+    *entries_per_row = on && A->nrows ? (double)A->sws_entries / A->nrows : 0.0;
+    *model_us = on ? A->brick_model_us : 0.0;
+    return 0;
+}
+
 int kle_mat_set_symmetric(kle_mat *A, int on)
 {
     KLE_ARG(A, "null matrix");
@@ -1457,24 +1468,6 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on)
     return 0;
 }
 
-int kle_mat_get_sym_placement_ws(const kle_mat *A, int *tries, int *kept)
-{
-    KLE_ARG(A && tries && kept, "null arg");
-    const bool on = A->d_sval != nullptr;
-    *tries = on ? A->sym_place_ws_tries : 0;
-    *kept = on ? A->sym_place_ws_kept : 0;
-    return 0;
-}
-
-int kle_mat_get_sym_placement(const kle_mat *A, double *us, int *tries, int *kept)
-{
-    KLE_ARG(A && us && tries && kept, "null arg");
-    const bool on = A->d_sval != nullptr;
-    *us = on ? A->sym_place_us : 0.0;
-    *tries = on ? A->sym_place_tries : 0;
-    *kept = on ? A->sym_place_kept : 0;
-    return 0;
-}
 
 int kle_mat_is_structured(const kle_mat *A, int *on)
 {

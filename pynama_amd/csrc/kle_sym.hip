@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "kle_internal.hpp"
+#include "kle_sym_dev.hpp"
 
 namespace kle {
 
@@ -32,17 +33,6 @@ namespace kle {
 constexpr int SYM_TX = 8;  // tile rows in x; TY x TZ (8 x 2, 4 x 4 or 2 x 4) per matrix: sym_TY, sym_TZ
 constexpr int SYM_FILL = 12;  // x-fill loads per thread of k_nb_spmv_sym_xl (one pass over the region)
 
-// The symmetric storage's big arrays (values, tile partials): physically
-// contiguous when g_tune.spmv_sym_alloc asks for it (bit 1 values, bit 2
-// partials; hipDeviceMallocContiguous), else -- or when that fails -- plain.
-static hipError_t sym_malloc(void **p, size_t bytes, int bit)
-{
-    if (g_tune.spmv_sym_alloc & bit) {
-        if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
-        (void)hipGetLastError();
-    }
-    return hipMalloc(p, bytes);
-}
 // Lattices: the rows are the owned Lx x Ly x Lz nodes; the columns add zo
 // lattice planes of lower ghosts before them and hp of upper ghosts after
 // them (slab partitions, N > 1: ext layout [lower ghosts | owned | upper]).
@@ -138,43 +128,6 @@ __global__ __launch_bounds__(256) void k_sym_build(int64_t nrows, int Lx, int Ly
     }
 }
 
-// Wave sums through DPP row moves (VALU only; __shfl_xor is a ds_bpermute per
-// 32-bit half, i.e. 12 LDS instructions per double): quad swaps, half-row
-// and row mirrors, then row_bcast15 / row_bcast31 carry the row sums into
-// lane 63, which every lane reads back.  Three sums at once, their steps
-// interleaved (no hazard nops between a step's add and the next step's DPP
-// read); the full-row steps use the source as the unused "old" operand
-// (every lane is written), only the row broadcasts need zeros.
-template <int ctrl, int row_mask>
-__device__ __forceinline__ void dpp3(double &a, double &b, double &c)
-{
-    constexpr bool all = row_mask == 0xF;
-    const int al = __double2loint(a), ah = __double2hiint(a), bl = __double2loint(b), bh = __double2hiint(b);
-    const int cl = __double2loint(c), ch = __double2hiint(c);
-    const int a2 = __builtin_amdgcn_update_dpp(all ? al : 0, al, ctrl, row_mask, 0xF, false);
-    const int a3 = __builtin_amdgcn_update_dpp(all ? ah : 0, ah, ctrl, row_mask, 0xF, false);
-    const int b2 = __builtin_amdgcn_update_dpp(all ? bl : 0, bl, ctrl, row_mask, 0xF, false);
-    const int b3 = __builtin_amdgcn_update_dpp(all ? bh : 0, bh, ctrl, row_mask, 0xF, false);
-    const int c2 = __builtin_amdgcn_update_dpp(all ? cl : 0, cl, ctrl, row_mask, 0xF, false);
-    const int c3 = __builtin_amdgcn_update_dpp(all ? ch : 0, ch, ctrl, row_mask, 0xF, false);
-    a += __hiloint2double(a3, a2);
-    b += __hiloint2double(b3, b2);
-    c += __hiloint2double(c3, c2);
-}
-
-__device__ __forceinline__ void wsum3_dpp(double &a, double &b, double &c)
-{
-    dpp3<0xB1, 0xF>(a, b, c);   // quad_perm [1,0,3,2]
-    dpp3<0x4E, 0xF>(a, b, c);   // quad_perm [2,3,0,1]
-    dpp3<0x141, 0xF>(a, b, c);  // row_half_mirror
-    dpp3<0x140, 0xF>(a, b, c);  // row_mirror
-    dpp3<0x142, 0xA>(a, b, c);  // row_bcast15 into rows 1, 3
-    dpp3<0x143, 0xC>(a, b, c);  // row_bcast31 into rows 2, 3
-    a = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(a), 63), __builtin_amdgcn_readlane(__double2loint(a), 63));
-    b = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(b), 63), __builtin_amdgcn_readlane(__double2loint(b), 63));
-    c = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(c), 63), __builtin_amdgcn_readlane(__double2loint(c), 63));
-}
-
 // Same tile pass with the wave's (row, 64-block pass) items flattened into one
 // software-pipelined loop: the values and x entries of the next item are in
 // flight while the current one is multiplied and accumulated (a wave's rows
@@ -186,23 +139,6 @@ struct SymRow {
     int bnx, bnxy, k0, mu, rx0, ry0, rz0, own;
     float ibnx, ibnxy;  // 1/bnx, 1/bnxy: quotients of block positions by float multiply + one fix-up
 };
-
-// q = n / d for 0 <= n < 2^20, d >= 1 (block position in its row box)
-__device__ __forceinline__ int sym_div(int n, int d, float inv)
-{
-    int q = (int)((float)n * inv);
-    q += (q + 1) * d <= n;
-    q -= q * d > n;
-    return q;
-}
-
-__device__ __forceinline__ double uni_d(double v)
-{
-    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
-    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
-    return __hiloint2double(hi, lo);
-}
-
 
 // ---------------------------------------------------------------------------
 // Symmetric SpMV with x staged in LDS (round 3; default).  Every x entry the
@@ -227,19 +163,6 @@ __device__ __forceinline__ double uni_d(double v)
 // DPP sum per row, one writer per row) and are added to the row's partial at
 // the end.  Without DET the transposed adds are fp64 LDS atomics (ds_add_f64),
 // equal to the full-storage product to rounding but run-dependent.
-__device__ __forceinline__ unsigned long long fx_of(double c, double S)
-{
-    const double v = __builtin_rint(c * S);           // |v| <= 2^61: an integer
-    const double hi = __builtin_floor(v * 0x1p-32);  // exact
-    const double lo = __builtin_fma(hi, -0x1p32, v);  // exact, in [0, 2^32)
-    return ((unsigned long long)(unsigned)(int)hi << 32) + (unsigned long long)(unsigned)lo;
-}
-
-__device__ __forceinline__ double fx_to_d(unsigned long long u)
-{
-    return (double)(int)((long long)u >> 32) * 0x1p32 + (double)(unsigned)(u & 0xffffffffull);
-}
-
 // A partial store with a cache policy (spmv_sym_stpol): 0 plain (write-back
 // L2), 1 nontemporal, 2 sc1, 3 sc0 sc1 (write-through: the line leaves L2
 // with the store instead of at its eviction under the value stream)
@@ -253,41 +176,6 @@ __device__ __forceinline__ void pst(double *p, double v, int pol)
         asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
     else
         *p = v;
-}
-
-// Value loads of one item of k_nb_spmv_sym_xl, issued in inline asm so the
-// compiler's wait bookkeeping cannot drain them: it saw the next item's loads
-// as hazards on registers of the current one and put s_waitcnt vmcnt(0) in
-// front of them at every second item.  The wait for an item (vmcnt(9): the
-// next item's 9 loads stay in flight) names its 9 registers as read-write
-// operands, so nothing reads them before the data has landed.
-__device__ __forceinline__ void sym_ld9(double *v, const double *base, const unsigned *o)
-{
-    asm volatile(
-        "s_nop 4\n\t"
-        "global_load_dwordx2 %0, %9, %18 nt\n\t"
-        "global_load_dwordx2 %1, %10, %18 nt\n\t"
-        "global_load_dwordx2 %2, %11, %18 nt\n\t"
-        "global_load_dwordx2 %3, %12, %18 nt\n\t"
-        "global_load_dwordx2 %4, %13, %18 nt\n\t"
-        "global_load_dwordx2 %5, %14, %18 nt\n\t"
-        "global_load_dwordx2 %6, %15, %18 nt\n\t"
-        "global_load_dwordx2 %7, %16, %18 nt\n\t"
-        "global_load_dwordx2 %8, %17, %18 nt"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
-          "=&v"(v[8])
-        : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "v"(o[5]), "v"(o[6]), "v"(o[7]), "v"(o[8]),
-          "s"(base)
-        : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void sym_wait9(double *v)
-{
-    asm volatile("s_waitcnt vmcnt(%9)"
-                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
-                   "+v"(v[8])
-                 : "i"(N));
 }
 
 // launch-local block -> work item: runs of ch consecutive items per XCD
@@ -789,17 +677,16 @@ void sym_forget(kle_mat *A)
     A->d_sgmask = nullptr;
     A->d_swptr = nullptr;
     A->sym_wn = 0;
-    A->sym_place_us = 0;
-    A->sym_place_tries = A->sym_place_kept = 0;
-    A->sym_place_ws_tries = A->sym_place_ws_kept = 0;
     A->sws_bytes = 0;
     A->sblocks = A->snvals = A->sws_entries = 0;
     A->sym_P = 0;
     A->sym_graph = 0;
+    brick_forget(A);
 }
 
 void sym_drop(kle_mat *A)
 {
+    brick_drop(A);
     for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
                     (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow, (void *)A->d_sbp,
                     (void *)A->d_slid, (void *)A->d_sdptr, (void *)A->d_sdict, (void *)A->d_sgptr,
@@ -1372,7 +1259,7 @@ static int gsym_build(kle_mat *A)
     double *rowdiff = nullptr, *rowmax = nullptr;
     const bool nomem =
         hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
-        sym_malloc(reinterpret_cast<void **>(&A->d_sval), sizeof(double) * std::max<int64_t>(tot, 1), 1) != hipSuccess ||
+        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
         hipMalloc(&A->d_srow, sizeof(int) * n) != hipSuccess || hipMalloc(&A->d_sbp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_slid, sizeof(uint16_t) * slid.size()) != hipSuccess ||
         hipMalloc(&A->d_sdptr, sizeof(int) * (ng + 1)) != hipSuccess ||
@@ -1382,7 +1269,7 @@ static int gsym_build(kle_mat *A)
         hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
         hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess ||
         (A->sws_bytes = sizeof(double) * std::max<int64_t>(wptr[ng], 1),
-         sym_malloc(reinterpret_cast<void **>(&A->d_sws), A->sws_bytes, 2) != hipSuccess) ||
+         hipMalloc(&A->d_sws, A->sws_bytes) != hipSuccess) ||
         hipMalloc(&A->d_swptr, sizeof(int) * (ng + 1)) != hipSuccess ||
         hipMalloc(&A->d_stile_e, sizeof(int) * ng) != hipSuccess || hipMalloc(&dk0, sizeof(int) * n) != hipSuccess ||
         (nhi && hipMalloc(&A->d_sgsend, sizeof(double) * 3 * nhi) != hipSuccess) ||
@@ -1476,9 +1363,7 @@ static int gsym_build(kle_mat *A)
     return done(0);
 }
 
-// local: the rank's own launches only (tiles and gather, no halo in either
-// direction -- sym_place times the product this way at any N)
-static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart, bool local = false)
+static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
@@ -1528,7 +1413,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         }
         return 0;
     };
-    if (!dist || local) {
+    if (!dist) {
         KLE_TRY(tiles(0));
         KLE_TRY(tiles(1));
     } else if (ovl) {
@@ -1551,7 +1436,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
                        A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate, dpart && !dist ? x->d : nullptr,
                        dpart);
     KLE_HIP(hipGetLastError());
-    if (!dist || local) return 0;
+    if (!dist) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending
     // rank order of the senders (MPISBAIJ's reverse scatter)
     if (ovl) {
@@ -1726,160 +1611,12 @@ static int sym_probe(kle_mat *A, double vmax_all, bool &bad)
 // and its reverse halo while a neighbour runs the full storage.
 static int sym_build_impl(kle_mat *A);
 
-// Placement of the value array (one rank): in one process on one box the
-// same storage streams at two speeds, ~425 or ~490 us per config-2 SpMV, set
-// by where its 2.3 GB land -- moving the values alone reproduces both, moving
-// the partials never does (tools/alloc_probe.py,
-// profiles/r04/ab/values_placement*.jsonl; round 3 read this as box-to-box
-// variance).  Consecutive allocations tend to share the mode (a fresh bench
-// process: the first three copies all slow), so the build keeps allocating
-// fresh copies -- the rejected ones held until the end, so each lands
-// elsewhere -- until one streams at >= spmv_sym_place_gbps of its algorithmic
-// bytes or g_tune.spmv_sym_place copies (at most 64 GB of them) are
-// spent, and keeps the fastest: the same bits at another address, a few ms
-// of setup.  At N > 1 each rank times its own launches without the halos
-// (sym_spmv_local): no collective, and every rank's choice is its own.
-static int sym_spmv_local(kle_mat *A, const kle_vec *x, kle_vec *y);
-static int sym_place(kle_mat *A)
-{
-    kle_ctx *c = A->ctx;
-    const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
-    if (g_tune.spmv_sym_place <= 0 || bytes < ((size_t)g_tune.spmv_sym_place_min_mb << 20)) return 0;
-    const int max_tries = (int)std::min<size_t>((size_t)g_tune.spmv_sym_place, (size_t(64) << 30) / bytes);
-    const double alg = sym_spmv_bytes(A);
-    kle_vec *x = nullptr, *y = nullptr;
-    KLE_TRY(vec_alloc(c, A->n_local, A->n_global, A->col_lo, A->ghost_lo, A->ghost_hi, &x));
-    int rc = vec_alloc(c, A->m_local, A->m_global, A->row_lo, 0, 0, &y);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (!rc && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess))
-        rc = fail(KLE_ERR_DEVICE, "event create failed");
-    if (!rc) {
-        x->bs = A->C;
-        hipLaunchKernelGGL(k_sym_probe_x, dim3((unsigned)((A->n_local + 255) / 256)), dim3(256), 0, c->stream,
-                           A->n_local, A->col_lo, x->d);
-        rc = hipGetLastError() == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "placement probe launch failed");
-    }
-    auto timed = [&](float &us) -> int {  // (per product, the gather included)
-        for (int k = 0; k < 2; ++k) KLE_TRY(sym_spmv_local(A, x, y));
-        KLE_HIP(hipEventRecord(e0, c->stream));
-        for (int k = 0; k < 4; ++k) KLE_TRY(sym_spmv_local(A, x, y));
-        KLE_HIP(hipEventRecord(e1, c->stream));
-        KLE_HIP(hipEventSynchronize(e1));
-        float ms = 0.f;
-        KLE_HIP(hipEventElapsedTime(&ms, e0, e1));
-        us = 250.f * ms;
-        return 0;
-    };
-    auto fast = [&](float us) { return alg / (1e3 * us) >= g_tune.spmv_sym_place_gbps; };
-    float best = 0.f, t = 0.f;
-    std::vector<double *> held;
-    std::string trail;
-    int tries = 0, kept = 0;
-    if (!rc) rc = timed(best);
-    trail = std::to_string((int)best);
-    // (slow placements come in runs of consecutive allocations -- 11 fast
-    // copies then 5 slow ones in one process, 16 slow in another: after every
-    // 4 slow copies in a row a 16 GB spacer, held to the end like the
-    // rejected copies, moves the next ones further on; all held memory
-    // stays under 96 GB)
-    size_t held_bytes = 0;
-    int slow_run = 0;
-    for (int k = 0; k < max_tries && !rc && !fast(best); ++k) {
-        double *nv = nullptr;
-        if (slow_run >= 4 && bytes >= (size_t(256) << 20)) {  // (not for test-size arrays)
-            slow_run = 0;
-            const size_t sp = size_t(16) << 30;
-            if (held_bytes + sp + bytes <= (size_t(96) << 30) && hipMalloc(&nv, sp) == hipSuccess) {
-                held.push_back(nv);
-                held_bytes += sp;
-                trail += " |";
-            }
-            (void)hipGetLastError();
-            nv = nullptr;
-        }
-        if (hipMalloc(&nv, bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            break;  // (no room for another copy: keep what we have)
-        }
-        held.push_back(nv);
-        held_bytes += bytes;
-        if (hipMemcpyAsync(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
-            rc = fail(KLE_ERR_DEVICE, "placement copy failed");
-            break;
-        }
-        std::swap(A->d_sval, held.back());
-        ++tries;
-        rc = timed(t);
-        trail += " " + std::to_string((int)t);
-        slow_run = fast(t) ? 0 : slow_run + 1;
-        if (!rc && t < best) {
-            best = t;
-            kept = tries;
-        } else {
-            std::swap(A->d_sval, held.back());
-        }
-    }
-    // then the partials' workspace, if no value copy streamed fast: the
-    // stores' cost depends on where values and partials lie relative to
-    // each other (placement_with_without_stores.jsonl), and a workspace is
-    // cheap to move -- no copy, every slot the gather reads is written by
-    // the tiles first
-    int wtries = 0, wkept = 0;
-    for (int k = 0; k < g_tune.spmv_sym_place_ws && !rc && !fast(best) && A->sws_bytes; ++k) {
-        double *nw = nullptr;
-        if (hipMalloc(&nw, A->sws_bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            break;
-        }
-        held.push_back(nw);
-        std::swap(A->d_sws, held.back());
-        ++wtries;
-        rc = timed(t);
-        trail += " w" + std::to_string((int)t);
-        if (!rc && t < best) {
-            best = t;
-            wkept = wtries;
-        } else {
-            std::swap(A->d_sws, held.back());
-        }
-    }
-    (void)hipStreamSynchronize(c->stream);
-    for (double *p : held) (void)hipFree(p);
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    for (kle_vec *v : {x, y})
-        if (v) {
-            (void)hipFree(v->base);
-            delete v;
-        }
-    if (const char *e = getenv("KLE_TIMING"))
-        if (atoi(e))
-            fprintf(stderr, "[kle sym] value placement: us per SpMV %s; kept %s, workspace %s (%.0f GB/s)\n",
-                    trail.c_str(), kept ? ("copy " + std::to_string(kept)).c_str() : "the first",
-                    wkept ? ("move " + std::to_string(wkept)).c_str() : "as built", alg / (1e3 * best));
-    A->sym_place_us = best;
-    A->sym_place_kept = kept;
-    A->sym_place_tries = tries;
-    A->sym_place_ws_tries = wtries;
-    A->sym_place_ws_kept = wkept;
-    return rc;
-}
-
 // Every error return of the builders, wherever it happens (a refused check,
 // a device error between the allocations and the last check), leaves A
 // without symmetric storage: no SpMV can run over a half-built copy.
 int sym_build(kle_mat *A)
 {
-    int rc = sym_build_impl(A);
-    if (!rc) {
-        // (placement is per rank; a failure on one rank drops the storage on
-        // all of them, as every other refusal does, so no rank runs the
-        // reverse halo while a neighbour runs the full storage)
-        const int prc = sym_place(A);
-        bool any = false;
-        const int arc = any_rank(A->ctx, prc != 0, any);
-        rc = prc ? prc : arc ? arc : any ? fail(KLE_ERR_SUP, "symmetric storage: value placement failed on another rank") : 0;
-    }
+    const int rc = sym_build_impl(A);
     if (rc) sym_drop(A);
     return rc;
 }
@@ -1973,11 +1710,26 @@ static int sym_build_impl(kle_mat *A)
             why = "symmetric storage: the block pattern is not symmetric (" + std::to_string(all) + " blocks, " +
                   std::to_string(blocks) + " upper)";
     }
+    // one rank, no ghosts: bricks (kle_brick.hip) -- the values go in brick
+    // order, and none of the tile set-up below is needed
+    void *bplan = nullptr;
+    struct PlanGuard {
+        void *&p;
+        ~PlanGuard() { brick_plan_free(p); }
+    } bguard{bplan};
+    if (why.empty() && g_tune.spmv_sym_brick && g_tune.spmv_sym_det && c->nranks == 1 && zo == 0 && hp == 0) {
+        std::string bwhy;
+        std::vector<int64_t> svb;
+        KLE_TRY(brick_setup(A, rb, cnt, srow, P, svb, bwhy, &bplan));
+        if (bplan) sv.swap(svb);
+        else if (const char *e = getenv("KLE_TIMING"))
+            if (atoi(e)) fprintf(stderr, "[kle brick] not used: %s\n", bwhy.c_str());
+    }
     SymRegion reg[NSH];
     for (int s = 0; s < NSH; ++s)
         reg[s] = {(int)-rlo[s][0], (int)(rhi[s][0] - rlo[s][0] + 1), (int)-rlo[s][1], (int)(rhi[s][1] - rlo[s][1] + 1),
                   (int)(rhi[s][2] + 1)};
-    if (why.empty() && sym_xl_lds(reg[1]) > LDS_PER_CU)
+    if (why.empty() && !bplan && sym_xl_lds(reg[1]) > LDS_PER_CU)
         why = "symmetric storage: row boxes reach " + std::to_string(P) + " nodes (region of " +
               std::to_string(reg[1].RX * reg[1].RY * reg[1].RZ) + " nodes does not fit the LDS)";
     // tile shape: 8 x 4 x 4 rows (default where two workgroups of 8 waves fit
@@ -2022,7 +1774,7 @@ static int sym_build_impl(kle_mat *A)
     int64_t nomem = 0;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_srow, sizeof(int) * std::max<int64_t>(n, 1)) != hipSuccess ||
-        sym_malloc(reinterpret_cast<void **>(&A->d_sval), sizeof(double) * std::max<int64_t>(tot, 1), 1) != hipSuccess ||
+        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
         hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess)
         nomem = 1;
     double dmax = 0.0, vmax = 0.0;
@@ -2062,6 +1814,16 @@ static int sym_build_impl(kle_mat *A)
             return fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax);
         return fail(KLE_ERR_SUP, "symmetric storage refused on another rank");
     }
+    if (bplan) {
+        A->sym_P = P;
+        A->sblocks = blocks;
+        A->snvals = tot;
+        void *p = bplan;
+        bplan = nullptr;  // (brick_finish owns it)
+        const int rc = brick_finish(A, p);
+        if (rc) sym_drop(A);
+        return rc;
+    }
     A->sym_P = P;
     A->sym_TZ = TZ;
     A->sym_TY = TY;
@@ -2085,7 +1847,7 @@ static int sym_build_impl(kle_mat *A)
                 ents += span(tx * g.TX - g.PX, g.RX, Lx) * span(ty * g.TY - g.PY, g.RY, Ly) *
                         span(t * g.TZ, g.RZ, Lz + hp);
     A->sws_bytes = sizeof(double) * ntiles * 3 * g.WN;
-    nomem = sym_malloc(reinterpret_cast<void **>(&A->d_sws), A->sws_bytes, 2) != hipSuccess ||
+    nomem = hipMalloc(&A->d_sws, A->sws_bytes) != hipSuccess ||
             hipMalloc(&A->d_stile_e, sizeof(int) * ntiles) != hipSuccess ||
             (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
             (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess);
@@ -2177,6 +1939,7 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 
 int sym_dot_parts(const kle_mat *A)
 {
+    if (A->sym_brick) return A->nbricks * A->brick_gparts;
     const bool dist = A->ctx->nranks > 1 && (A->sym_graph || A->lo_rank >= 0 || A->hi_rank >= 0);
     return dist ? 0 : (int)((A->nrows + 255) / 256);
 }
@@ -2190,25 +1953,12 @@ int sym_dot_parts(const kle_mat *A)
 //         touch; main: the lowest rows, + d_sgrecv last (fixed order: y stays
 //         bitwise reproducible with spmv_sym_det).
 // All RCCL calls stay on the comm stream, in the same order on every rank.
-// The rank's own launches of y = A x (tiles, gather; no halo either way, so
-// y lacks the neighbours' contributions at N > 1): sym_place's timed product.
-static int sym_spmv_local(kle_mat *A, const kle_vec *x, kle_vec *y)
-{
-    if (A->sym_graph) return gsym_spmv(A, x, y, nullptr, nullptr, true);
-    const SymGeo g = sym_geo(A);
-    const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz;
-    const bool dist = A->ctx->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
-    launch_sym_tiles(A, g, x, 0, ntiles, nullptr, A->ctx->stream);
-    launch_sym_gather(A, g, y, 0, A->nrows + (dist ? (int64_t)g.hp * g.Lx * g.Ly : 0), 0, nullptr, A->ctx->stream);
-    KLE_HIP(hipGetLastError());
-    return 0;
-}
-
 int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
     if (A->sym_graph) return gsym_spmv(A, x, y, istate, dpart);
+    if (A->sym_brick) return brick_spmv(A, x, y, istate, dpart);
     const SymGeo g = sym_geo(A);
     const int64_t ntiles = (int64_t)g.ntx * g.nty * g.ntz, n = A->nrows, Lxy = (int64_t)g.Lx * g.Ly;
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
@@ -2266,6 +2016,9 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 
 std::string sym_kernel_name(const kle_mat *A)
 {
+    if (A->sym_brick)
+        return std::string("k_nb_spmv_sym_brick<16,") + std::to_string(g_tune.spmv_brick_ahead) +
+               ">+k_nb_sym_brick_gather";
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
                std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather";
@@ -2283,6 +2036,9 @@ double sym_spmv_bytes(const kle_mat *A)
     // value offset, slid offset, count, x and y; per dictionary entry its node
     // id and the partial written and read (the gather runs, 12 B per ~8
     // entries, are not counted)
+    // bricks: values, 8 B of row descriptor per row, x and y once, each
+    // brick's region sums written once and read once
+    if (A->sym_brick) return (double)A->sblocks * 72.0 + A->nrows * (8.0 + 48.0) + (double)A->sws_entries * 48.0;
     if (A->sym_graph)
         return (double)A->sblocks * 74.0 + A->nrows * (8.0 + 8.0 + 4.0 + 48.0) + (double)A->sws_entries * (4.0 + 48.0);
     return (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 + (double)A->sws_entries * 48.0;

@@ -419,14 +419,14 @@ class Mat:
         call("kle_mat_get_symmetric", self._h, C.byref(v))
         return bool(v.value)
 
-    def getSymmetricPlacement(self):
-        """The value placement the symmetric storage kept (kle_mat_get_sym_placement)."""
-        us, tries, kept = C.c_double(), C.c_int(), C.c_int()
-        call("kle_mat_get_sym_placement", self._h, C.byref(us), C.byref(tries), C.byref(kept))
-        wt, wk = C.c_int(), C.c_int()
-        call("kle_mat_get_sym_placement_ws", self._h, C.byref(wt), C.byref(wk))
-        return {"spmv_us": us.value, "fresh_copies_tried": tries.value, "kept": kept.value,
-                "workspace_moves_tried": wt.value, "workspace_kept": wk.value}
+    def getSymmetricBricks(self):
+        """The brick decomposition of the symmetric SpMV (kle_mat_get_sym_bricks),
+        or None when the product runs on something else."""
+        n, dims, ent, mus = C.c_int(), (C.c_int * 3)(), C.c_double(), C.c_double()
+        call("kle_mat_get_sym_bricks", self._h, C.byref(n), dims, C.byref(ent), C.byref(mus))
+        if n.value == 0:
+            return None
+        return {"bricks": n.value, "dims": list(dims), "region_entries_per_row": ent.value, "model_us": mus.value}
 
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))

@@ -201,6 +201,13 @@ class Context:
         return {"device": dev.value, "pci_bus_id": pci.value.decode(),
                 "transport": ("single", "rccl", "host", "ipc")[tr.value]}
 
+    def comm_info(self):
+        """(ranks, this rank) as the RCCL communicator reports them
+        (ncclCommCount / ncclCommUserRank), or (0, -1) without one."""
+        cnt, rk = C.c_int(), C.c_int()
+        call("kle_ctx_get_comm_info", self.h, C.byref(cnt), C.byref(rk))
+        return cnt.value, rk.value
+
     def set_profiling(self, on=True, only=None, every=1):
         """Event-time device launches; `only` restricts it to one kernel tag,
         `every` > 1 times one launch in `every` (sampled)."""
@@ -252,8 +259,8 @@ def get_ctx():
             set_tuning("spmv_dict_min_rows", int(os.environ["KLE_SPMV_DICT_MIN_ROWS"]))
         if os.environ.get("KLE_SPMV_SYM_TILE64"):
             set_tuning("spmv_sym_tile64", int(os.environ["KLE_SPMV_SYM_TILE64"]))
-        if os.environ.get("KLE_SPMV_SYM_PLACE_MIN_MB"):
-            set_tuning("spmv_sym_place_min_mb", int(os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"]))
+        if os.environ.get("KLE_SPMV_SYM_BRICK"):
+            set_tuning("spmv_sym_brick", int(os.environ["KLE_SPMV_SYM_BRICK"]))
         if os.environ.get("KLE_KSP_REFINE"):
             set_tuning("ksp_refine", int(os.environ["KLE_KSP_REFINE"]))
         _CTX = Context()

@@ -44,7 +44,20 @@ def test_bench_line_contract():
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["unit"] == d["unit"]
     s = d["solve"]
     assert s["reason"] > 0 and s["true_rel_residual"] <= 2e-10
-    assert d["symmetric_value_placement"] is None  # (below spmv_sym_min_rows: full storage)
+    assert d["symmetric_bricks"] is None  # (below spmv_sym_min_rows: full storage)
+    # the streaming ceiling the SpMV is graded against is this box's own
+    # (16-B nontemporal reads), and the PMC traffic rate cannot exceed it
+    assert r["achievable_gbps"] > 4000.0 and abs(r["frac_of_achievable"] - r["achieved"] / r["achievable_gbps"]) < 1e-12
+    if r["traffic_frac_of_read_ceiling"] is not None:
+        assert r["traffic_frac_of_read_ceiling"] <= 1.0
+    # the (f)#1 operator chain is measured in the default run (N = 1)
+    ops = d["operators"]
+    assert ops is not None and ops["evalRHS_chain_ms"] > 0
+    for nm in ("Curl", "SrT", "DivSrT"):
+        assert ops[nm]["bytes"] > 0 and ops[nm]["avg_ms"] > 0 and 0 < ops[nm]["frac"] < 1
+    # what RCCL itself reports, per rank (one rank: no communicator)
+    cfg = d["config"]
+    assert cfg["rccl_ranks"] == 0 and cfg["rccl_user_ranks"] == [-1] and len(cfg["spmv_ms_per_rank"]) == 1
 
 
 def test_bench_unstructured_line():
@@ -52,3 +65,4 @@ def test_bench_unstructured_line():
              "--no-cpu-baseline")
     assert d["config"]["mesh"] == "unstructured" and d["cpu_baseline"] is None and d["value"] > 0
     assert d["roofline"]["achieved"] > 0
+    assert d["config"]["parallelism"].startswith("inertial recursive bisection")

@@ -96,25 +96,28 @@ def test_config2_full_size_matches_oracle(pa):
     its_dev = ksp.getIterationNumber() - ksp.getCorrectionIterations()
     _log(t0, f"device CG: {its_dev} iterations, device true residual {ksp.getTrueRelativeResidual():.3e}")
 
-    # ---- the symmetric values' placement (spmv_sym_place, on by default at
-    # this size): a rebuild without it streams the same bits elsewhere
+    # ---- the box symmetric SpMV on bricks (default, one rank): its plan, and
+    # the 128-row tile kernel on the same K and u to 1e-14 (both exact
+    # fixed-point transposed sums, other scales and summation orders)
     from pynama_amd.runtime import set_tuning
     K = mat.K
-    assert K.isSymmetricStorage()
-    pl = K.getSymmetricPlacement()
-    assert pl["spmv_us"] > 0 and 0 <= pl["kept"] <= pl["fresh_copies_tried"] <= 16, pl
-    _log(t0, f"value placement: {pl}")
+    assert K.isSymmetricStorage() and K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
+    bk = K.getSymmetricBricks()
+    assert bk["bricks"] == bk["dims"][0] * bk["dims"][1] * bk["dims"][2] and 0 < bk["bricks"] <= 256, bk
+    _log(t0, f"bricks: {bk}")
     y1 = (K * vel).getArray().copy()
-    set_tuning("spmv_sym_place", 0)
+    np.testing.assert_array_equal((K * vel).getArray(), y1)
+    set_tuning("spmv_sym_brick", 0)
     try:
-        K.setOption(K.Option.SPD, False)
         K.setOption(K.Option.SPD, True)
-        assert K.getSymmetricPlacement() == {"spmv_us": 0.0, "fresh_copies_tried": 0, "kept": 0,
-                                             "workspace_moves_tried": 0, "workspace_kept": 0}
-        np.testing.assert_array_equal((K * vel).getArray(), y1)
+        assert K.spmvKernel().startswith("k_nb_spmv_sym_xl"), K.spmvKernel()
+        yt = (K * vel).getArray()
+        assert np.linalg.norm(yt - y1) <= 1e-14 * np.linalg.norm(y1)
     finally:
-        set_tuning("spmv_sym_place", 16)
-    del y1
+        set_tuning("spmv_sym_brick", 1)
+        K.setOption(K.Option.SPD, True)
+    np.testing.assert_array_equal((K * vel).getArray(), y1)
+    del y1, yt
 
     # ---- oracle assembly (mat_fs.py:131-192)
     Ko, Kro, Rwo = om.assemble_fs(on_bd.astype(np.uint8))

@@ -82,7 +82,6 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
                "coords": dom.getFullCoordArray().reshape(-1, 3),
                "ov_diff": (np.nonzero(y_ov != y_pl)[0][:12].tolist(), len(y_ov)),
                "sym": mat.K.isSymmetricStorage(), "kernel": mat.K.spmvKernel(),
-               "place": mat.K.getSymmetricPlacement(),
                "transport": pa.get_ctx().device_info()["transport"]}
         q.put(res)
     except Exception as e:  # report instead of hanging the peer
@@ -155,38 +154,6 @@ def test_partitioned_symmetric_storage_128_row_tiles(size, nelem, ngl, ksp_type)
         del os.environ["KLE_SPMV_SYM_TILE64"]
     for r in res:
         assert r["kernel"] == "k_nb_spmv_sym_xl<8,true,4,4>+k_nb_sym_gather<8,4,4>", r["kernel"]
-
-
-def test_partitioned_symmetric_value_placement(tmp_path):
-    """Value placement (spmv_sym_place) at N > 1, forced at test size
-    (KLE_SPMV_SYM_PLACE_MIN_MB=0): every rank times its own tile and gather
-    launches on fresh copies of its value array, no collective -- the ranks
-    do not wait for each other, and y = K x and the solve are bitwise those of
-    the run without it (box slabs and graph partitions)."""
-    os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"] = "0"  # inherited by the spawned ranks
-    try:
-        res = _check_box(3, [2, 3, 3], 3, True, "pipecg", sym=True)
-    finally:
-        del os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"]
-    ref = _check_box(3, [2, 3, 3], 3, True, "pipecg", sym=True)
-    for a, b in zip(res, ref):
-        # (test sizes never stream 5.45 TB/s: all sixteen copies are tried)
-        assert a["place"]["fresh_copies_tried"] == 16 and a["place"]["spmv_us"] > 0, a["place"]
-        assert a["place"]["workspace_moves_tried"] == 8, a["place"]
-        assert b["place"]["fresh_copies_tried"] == 0, b["place"]
-        np.testing.assert_array_equal(a["y"], b["y"])
-        np.testing.assert_array_equal(a["u"], b["u"])
-        assert a["its"] == b["its"]
-    os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"] = "0"
-    try:
-        res = _check_umesh(3, "inertial", [3, 4, 4], "cg", 0, tmp_path, sym=True)
-    finally:
-        del os.environ["KLE_SPMV_SYM_PLACE_MIN_MB"]
-    ref = _check_umesh(3, "inertial", [3, 4, 4], "cg", 0, tmp_path, sym=True)
-    for a, b in zip(res, ref):
-        assert a["kernel"].startswith("k_nb_spmv_gsym<") and a["place"]["fresh_copies_tried"] == 16, a["place"]
-        np.testing.assert_array_equal(a["y"], b["y"])
-        np.testing.assert_array_equal(a["u"], b["u"])
 
 
 @pytest.mark.parametrize("size,nelem,ngl,ksp_type,overlap,sym", [

@@ -21,6 +21,19 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module", autouse=True)
+def tiles():
+    """The box tests here exercise the 128-row tile kernel (the brick kernel,
+    default for one rank: test_gpu_brick.py); the tiles serve the z slabs of
+    N > 1, larger parts than one brick per CU covers, and spmv_sym_brick 0."""
+    import pynama_amd
+    pynama_amd.load()
+    from pynama_amd.runtime import set_tuning
+    set_tuning("spmv_sym_brick", 0)
+    yield
+    set_tuning("spmv_sym_brick", 1)
+
+
 @pytest.fixture(scope="module")
 def pa():
     import pynama_amd
@@ -121,25 +134,6 @@ def test_symmetric_spmv_matches_full_storage_and_csr(pa, nelem, ngl):
                          "k_nb_spmv_sym_xl<8,true,8,2>+k_nb_sym_gather<8,8,2>",
                          "k_nb_spmv_sym_xl<16,true,8,2>+k_nb_sym_gather<8,8,2>"), shapes
     K.setOption(K.Option.SPD, True)
-    # value placement forced at this size (spmv_sym_place_min_mb 0; by
-    # default from 256 MB of values, test_gpu_fullsize): sixteen fresh copies
-    # timed (a small matrix never streams 5.45 TB/s), one kept -- the same bits
-    set_tuning("spmv_sym_place_min_mb", 0)
-    try:
-        K.setOption(K.Option.SPD, True)
-        pl = K.getSymmetricPlacement()
-        assert pl["fresh_copies_tried"] == 16 and pl["spmv_us"] > 0 and 0 <= pl["kept"] <= 16, pl
-        assert pl["workspace_moves_tried"] == 8 and 0 <= pl["workspace_kept"] <= 8, pl  # (then the partials)
-        np.testing.assert_array_equal(ya, (K * x).getArray())
-    finally:
-        set_tuning("spmv_sym_place_min_mb", 256)
-    # value placement off: the same bits
-    set_tuning("spmv_sym_place", 0)
-    try:
-        K.setOption(K.Option.SPD, True)
-        np.testing.assert_array_equal(ya, (K * x).getArray())
-    finally:
-        set_tuning("spmv_sym_place", 16)
     K.setOption(K.Option.SPD, False)
     assert not K.isSymmetricStorage()
     np.testing.assert_array_equal((K * x).getArray(), y0)

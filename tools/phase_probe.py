@@ -54,10 +54,10 @@ def main():
     mat.setDomain(dom)
     mat.build(buildOperators=False)
     K = mat.K
+    for k, v in json.loads(a.tuning).items():  # (build knobs included: set before the build)
+        set_tuning(k, v)
     K.setOption(K.Option.SPD, True)  # (symmetric storage below spmv_sym_min_rows too)
     kern = K.spmvKernel()
-    for k, v in json.loads(a.tuning).items():
-        set_tuning(k, v)
     slots = 1 << 20
     set_tuning("spmv_sym_probe_ts", slots)
     lib = load()
@@ -120,6 +120,7 @@ def main():
                 "share": {"fill": float(fill.sum() / total.sum()), "loop": float(loop.sum() / total.sum()),
                           "store": float(store.sum() / total.sum())},
                 "last_start_us": float(st.max()), "first_end_us": float(en.min()),
+                "loop_deciles_us": [float(np.percentile(loop, q)) for q in range(0, 101, 10)],
                 "per_xcd": per_xcd, "tuning": json.loads(a.tuning), "cg": a.cg}
         print(json.dumps(summ), flush=True)
         np.save(os.path.join(a.out, f"phase_{a.mesh}_{rep}.npy"), r)
