@@ -100,7 +100,8 @@ const char *kle_last_error(void);
  * brick region's x and exact sums in LDS for the whole value stream; 1
  * default, 0 the 128-row tiles), "spmv_brick_ahead" (brick kernel: items in
  * flight ahead of the summed one, 1 default or 2), "spmv_brick_max" (read at
- * build: at most this many bricks, 0 = one per CU), "spmv_brick_split" (read
+ * build: at most this many bricks, 0 planned), "spmv_brick_rounds" (read at
+ * build: at most this many bricks per CU, default 1), "spmv_brick_split" (read
  * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
@@ -169,10 +170,12 @@ int kle_ctx_get_device(kle_ctx *ctx, int *device, char *pci_bus_id, int len, int
 int kle_ctx_get_comm_info(kle_ctx *ctx, int *count, int *rank);
 /* Diagnostic, host only (no device, no reference counterpart): the brick
  * plan of the symmetric SpMV for an Lx x Ly x Lz box lattice of p-node
- * elements (dirichlet: boundary rows the diagonal alone) on ncu CUs (split: forced counts nbx + 100 nby + 10000 nbz, 0
+ * elements (dirichlet: boundary rows the diagonal alone) on ncu CUs, at
+ * most `rounds` bricks per CU (split: forced counts nbx + 100 nby + 10000 nbz, 0
  * planned).  info: bricks, bricks along x / y / z, LDS bytes; stats: largest
  * brick's bytes over the mean, region entries per row, stored blocks. */
-int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, int ncu, int split, int *info, double *stats);
+int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, int ncu, int rounds, int split, int *info,
+                       double *stats);
 /* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */
 int kle_ctx_set_profiling(kle_ctx *ctx, int on);
 /* Time only the launches tagged `name` ("spmv", "dot", "cg_update", "reduce",

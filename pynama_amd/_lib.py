@@ -63,7 +63,7 @@ _SIGS = {
     "kle_ctx_barrier": [vp],
     "kle_ctx_get_device": [vp, C.POINTER(C.c_int), C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "kle_ctx_get_comm_info": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
-    "kle_brick_plan_box": [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+    "kle_brick_plan_box": [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
                            C.POINTER(C.c_double)],
     "kle_ctx_enable_ipc": [vp],
     "kle_ctx_set_profiling": [vp, C.c_int],

@@ -63,7 +63,7 @@ __device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const BrickD
                                              const int *__restrict__ nbptr, const int *__restrict__ nblist,
                                              const double *__restrict__ ws, double *__restrict__ y,
                                              const double *__restrict__ xdot, double *__restrict__ dpart, int *nbd,
-                                             double *dred, int r0 = 0, int r1 = INT_MAX, int dslot = -1)
+                                             double *dred, int r0, int r1, int dslot, int64_t jofs)
 {
     const int x0 = bd[O].x0, y0 = bd[O].y0, z0 = bd[O].z0, nx = bd[O].nx, ny = bd[O].ny, nz = bd[O].nz;
     const int NR = nx * ny * nz, q0 = nbptr[O], nq = min(nbptr[O + 1] - q0, BG_MAXNB);
@@ -85,8 +85,15 @@ __device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const BrickD
     for (int r = r0 + (int)threadIdx.x; r < min(NR, r1); r += NT) {
         const int rz = r / (nx * ny), rem = r - rz * nx * ny, ry = rem / nx, rx = rem - ry * nx;
         const int gx = x0 + rx, gy = y0 + ry, gz = z0 + rz;
-        const int64_t j = gx + (int64_t)Lx * gy + Lxy * gz;
-        double s0 = y[3 * j], s1 = y[3 * j + 1], s2 = y[3 * j + 2];  // (the row's direct sum)
+        // (an owned row starts from its direct sum; jofs > 0: an upper ghost
+        // node, its sums to the reverse halo's buffer from 0)
+        const int64_t j = gx + (int64_t)Lx * gy + Lxy * gz - jofs;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        if (jofs == 0) {
+            s0 = y[3 * j];
+            s1 = y[3 * j + 1];
+            s2 = y[3 * j + 2];
+        }
         // (four bricks' loads in flight before their adds, in brick order)
         for (int q = 0; q < nq; q += 4) {
             double a[4][3];
@@ -414,11 +421,12 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
 // brick order (brick_reduce), after the brick kernel.
 // Workgroup (brick b, part s) takes b's owned rows [256 s, 256 s + 256);
 // with xdot its (y, x) partial goes to dpart[b * parts + s].
-__global__ __launch_bounds__(256) void k_nb_sym_brick_gather(int Lx, int Ly, int parts, const BrickDesc *__restrict__ bd,
+__global__ __launch_bounds__(256) void k_nb_sym_brick_gather(int Lx, int Ly, int parts, int b0,
+                                                             const BrickDesc *__restrict__ bd,
                                                              const int *__restrict__ nbptr,
                                                              const int *__restrict__ nblist,
                                                              const double *__restrict__ ws, double *__restrict__ y,
-                                                             const int *__restrict__ istate,
+                                                             int64_t jofs, const int *__restrict__ istate,
                                                              const double *__restrict__ xdot,
                                                              double *__restrict__ dpart)
 {
@@ -426,9 +434,19 @@ __global__ __launch_bounds__(256) void k_nb_sym_brick_gather(int Lx, int Ly, int
     __shared__ int nbd[BG_MAXNB * 8];
     const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;
     if (stop) return;  // (uniform)
-    const int b = blockIdx.x / parts, s = blockIdx.x - b * parts;
+    const int b = b0 + (int)blockIdx.x / parts, s = (int)blockIdx.x % parts;
     brick_reduce<256>(b, Lx, Ly, bd, nbptr, nblist, ws, y, xdot, dpart, nbd, dred, 256 * s, 256 * s + 256,
-                             (int)blockIdx.x);
+                      (int)blockIdx.x, jofs);
+}
+
+// y[0 .. n) += r: the lower neighbour's sums for this slab's lowest nodes
+// (the reverse halo), added last -- after the bricks', in a fixed order
+__global__ void k_brick_add_recv(int64_t n, const double *__restrict__ r, double *__restrict__ y,
+                                 const int *__restrict__ istate)
+{
+    if (istate && istate[I_REASON] != 0) return;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) y[t] += r[t];
 }
 
 // Per brick: eb with 2^eb > the largest, over its region nodes j, of
@@ -517,9 +535,10 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
                 int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out)
 {
     auto *bp = new BrickPlan;
-    const int ncu = g_tune.spmv_brick_max > 0 ? g_tune.spmv_brick_max : std::max(1, A->ctx->num_cus);
-    why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], ncu, g_tune.spmv_brick_split, cnt,
-                     srow, P, *bp, std::max(1, A->ctx->num_cus));
+    const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
+    why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
+                     std::max(1, A->ctx->num_cus),
+                     g_tune.spmv_brick_max, g_tune.spmv_brick_rounds, g_tune.spmv_brick_split, cnt, srow, P, *bp);
     if (!why.empty()) {
         delete bp;
         *plan_out = nullptr;
@@ -536,13 +555,15 @@ int brick_finish(kle_mat *A, void *plan)
 {
     std::unique_ptr<BrickPlan> bp(reinterpret_cast<BrickPlan *>(plan));
     kle_ctx *c = A->ctx;
-    const int NB = (int)bp->bricks.size();
+    const int NT = (int)bp->bricks.size(), NB = bp->nreal;  // (all pieces; the bricks with rows)
     const int64_t n = A->nrows;
     int *dmu = nullptr;
     std::vector<int> hmu(n, 0);
-    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NB) != hipSuccess ||
+    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NT) != hipSuccess ||
                  hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
-                 hipMalloc(&A->d_bnbptr, sizeof(int) * (NB + 1)) != hipSuccess ||
+                 hipMalloc(&A->d_bnbptr, sizeof(int) * (NT + 1)) != hipSuccess ||
+                 (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
+                 (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
                  hipMalloc(&A->d_bnb, sizeof(int) * std::max<size_t>(bp->nblist.size(), 1)) != hipSuccess ||
 
                  hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
@@ -555,7 +576,8 @@ int brick_finish(kle_mat *A, void *plan)
     A->sws_bytes = sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1);
     // stored blocks per row (the bound's direct sums) from the row descriptors
     {
-        for (const BrickDesc &D : bp->bricks)
+        for (int q = 0; q < NB; ++q) {
+            const BrickDesc &D = bp->bricks[q];
             for (int r = 0; r < D.nx * D.ny * D.nz; ++r) {
                 const int d = bp->rowd[2 * ((int64_t)D.rstart + r)];
                 const int dbx = d & 15, dby = (d >> 4) & 15, dbz = (d >> 8) & 15;
@@ -564,10 +586,11 @@ int brick_finish(kle_mat *A, void *plan)
                 const int64_t i = (D.x0 + rx) + A->row_lat[0] * ((D.y0 + ry) + A->row_lat[1] * (int64_t)(D.z0 + rz));
                 hmu[i] = bnx * bny * bnz - (dbx + bnx * (dby + bny * dbz));
             }
+        }
     }
-    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NT, hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_browd, bp->rowd.data(), sizeof(int) * bp->rowd.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_bnbptr, bp->nbptr.data(), sizeof(int) * (NB + 1), hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_bnbptr, bp->nbptr.data(), sizeof(int) * (NT + 1), hipMemcpyHostToDevice));
     if (!bp->nblist.empty())
         KLE_HIP(hipMemcpy(A->d_bnb, bp->nblist.data(), sizeof(int) * bp->nblist.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
@@ -583,10 +606,12 @@ int brick_finish(kle_mat *A, void *plan)
     KLE_HIP(hipMemcpy(eb.data(), A->d_stile_e, sizeof(int) * NB, hipMemcpyDeviceToHost));
     (void)hipFree(dmu);
     for (int q = 0; q < NB; ++q) bp->bricks[q].eb = eb[q];
-    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NT, hipMemcpyHostToDevice));
     A->nbricks = NB;
+    A->nbricks_ghost = NT - NB;
     for (int k = 0; k < 3; ++k) A->brick_dims[k] = 0;
-    for (const BrickDesc &D : bp->bricks) {
+    for (int q = 0; q < NB; ++q) {
+        const BrickDesc &D = bp->bricks[q];
         A->brick_dims[0] += D.y0 == 0 && D.z0 == 0;
         A->brick_dims[1] += D.x0 == 0 && D.z0 == 0;
         A->brick_dims[2] += D.x0 == 0 && D.y0 == 0;
@@ -626,6 +651,7 @@ void brick_forget(kle_mat *A)
     A->d_browd = nullptr;
     A->d_bnbptr = A->d_bnb = nullptr;
     A->nbricks = 0;
+    A->nbricks_ghost = 0;
     A->brick_gparts = 0;
     A->brick_dims[0] = A->brick_dims[1] = A->brick_dims[2] = 0;
     A->brick_model_us = 0.0;
@@ -651,12 +677,47 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
                            istate KLE_PROBE_ARG);
     };
+    auto gather = [&](int b0, int nb, double *out, int64_t jofs, double *dp, hipStream_t st) {
+        if (nb <= 0) return;
+        hipLaunchKernelGGL(k_nb_sym_brick_gather, dim3((unsigned)(nb * A->brick_gparts)), dim3(256), 0, st,
+                           (int)A->row_lat[0], (int)A->row_lat[1], A->brick_gparts, b0, bd, A->d_bnbptr, A->d_bnb,
+                           A->d_sws, out, jofs, istate, dp ? x->d : nullptr, dp);
+    };
+    const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    // N > 1 (z slabs): the x ghost planes first (every brick's region fill
+    // may read them); after the bricks, the upper ghost nodes' sums go to the
+    // upper neighbour (MPISBAIJ's reverse scatter) on the comm stream while
+    // the owned rows are summed; the lower neighbour's sums for the lowest
+    // rows are added last (fixed order: y stays bitwise reproducible).  All
+    // RCCL calls in the same order on every rank: forward, then reverse halo.
+    if (dist)
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, c->stream, nullptr));
     if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1);
     else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0);
     KLE_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_nb_sym_brick_gather, dim3((unsigned)(A->nbricks * A->brick_gparts)), dim3(256), 0,
-                           c->stream, (int)A->row_lat[0], (int)A->row_lat[1], A->brick_gparts, bd, A->d_bnbptr,
-                           A->d_bnb, A->d_sws, y->d, istate, dpart ? x->d : nullptr, dpart);
+    if (!dist) {
+        gather(0, A->nbricks, y->d, 0, dpart, c->stream);
+        KLE_HIP(hipGetLastError());
+        return 0;
+    }
+    gather(A->nbricks, A->nbricks_ghost, A->d_sgsend, A->nrows, nullptr, c->stream);
+    KLE_HIP(hipGetLastError());
+    const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
+    const bool ovl = A->halo_overlap != 0;
+    hipStream_t cs = ovl ? c->comm_stream : c->stream;
+    if (ovl) {
+        KLE_HIP(hipEventRecord(c->ev_x_ready, c->stream));
+        KLE_HIP(hipStreamWaitEvent(cs, c->ev_x_ready, 0));
+    }
+    KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, cs));
+    if (ovl) KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
+    gather(0, A->nbricks, y->d, 0, nullptr, c->stream);
+    KLE_HIP(hipGetLastError());
+    if (ovl) KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
+    if (nrecv)
+        hipLaunchKernelGGL(k_brick_add_recv, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream, nrecv,
+                           A->d_sgrecv, y->d, istate);
     KLE_HIP(hipGetLastError());
     return 0;
 }

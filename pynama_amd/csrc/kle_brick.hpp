@@ -28,7 +28,8 @@ constexpr size_t BRICK_LDS_MIN = 82 * 1024;  // above half the CU's LDS: never t
 // component take the adds of masked lanes) | wave maxima, row counter
 
 struct BrickPlan {
-    std::vector<BrickDesc> bricks;
+    std::vector<BrickDesc> bricks;  // nreal bricks, then (N > 1) the ghost pieces the gather sums for the reverse halo
+    int nreal = 0;
     std::vector<int> rowd;      // 2 ints per row, brick order
     std::vector<int64_t> svb;   // per row (natural index): first double of its values, brick layout
     std::vector<int> nbptr, nblist;  // per brick: the bricks whose regions meet its rows (ascending)
@@ -42,10 +43,12 @@ struct BrickPlan {
 inline size_t brick_lds(int RN) { return (size_t)(3 * RN + 3 * (RN + 64)) * 8 + 512; }
 constexpr int BG_MAXNB = 64;  // bricks whose regions meet one brick's rows (27 in a regular grid)
 
-// bricks for the owned Lx x Ly x Lz lattice of one rank (rows x-fastest;
-// per row its block count and packed box, kle_sym.hip srow); fs: forced
-// split counts (0: planned), ncu: at most this many bricks.  "" or why not.
-std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vector<int> &cnt,
-                       const std::vector<int> &srow, int P, BrickPlan &bp, int ncu_all = 0);
+// bricks for the owned Lx x Ly x Lz lattice of a rank (rows x-fastest; per
+// row its block count and packed box, kle_sym.hip srow; hp upper ghost
+// planes, z slabs at N > 1) on ncu CUs: at
+// most `rounds` bricks per CU, or at most nfix bricks (> 0); fs: forced
+// split counts (0: planned).  "" or why not.
+std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int rounds, int fs, const std::vector<int> &cnt,
+                       const std::vector<int> &srow, int P, BrickPlan &bp);
 
 }  // namespace kle

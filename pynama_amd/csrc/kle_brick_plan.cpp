@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <functional>
 
 #include "kle_brick.hpp"
 #include "kle_internal.hpp"
@@ -36,15 +37,27 @@ static bool split_axis(const std::vector<double> &w, int n, int q, std::vector<i
 }
 
 
-// Plan bricks for the owned lattice (one rank, no ghosts): split counts
-// (nbx, nby, nbz) with at most ncu bricks (one round: every brick's sums are
-// written after the whole value stream) and cut variants per axis, whose
-// regions fit the LDS; the shortest modelled time, then the fewest region
-// entries.
-std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vector<int> &cnt,
-                       const std::vector<int> &srow, int P, BrickPlan &bp, int ncu_all)
+// Plan bricks for the owned lattice (one rank, no ghosts) on ncu CUs: up to
+// `rounds` bricks per CU (nfix > 0: exactly at most nfix bricks), from three
+// generators -- one tensor grid of split counts and cut variants per axis,
+// per-slab grids, per-slab recursive bisection -- whose regions fit the
+// LDS; the shortest modelled time, then the fewest region entries.  One
+// brick per CU writes every brick's sums after the whole value stream; more
+// balance the CUs (heaviest first to the first free CU) at the price of a
+// refill and sums written mid-stream.
+// What a row costs a brick, in bytes of streaming: its 64-block passes
+// ("items"), each as if full.  With the memory system saturated every item in
+// flight is served in about the same time whatever its bytes: the measured
+// loop time of 512 config-2 bricks follows their item counts (correlation
+// 0.93, 0.138 us per 1000 items) and not their bytes (0.26), so bricks full
+// of short rows -- the one-block Dirichlet rows of a boundary face -- would
+// end last (profiles/r05/brick_items_vs_bytes.txt).
+static double row_cost(int mu) { return 4608.0 * ((mu + 63) / 64); }
+
+std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int rounds, int fs, const std::vector<int> &cnt,
+                       const std::vector<int> &srow, int P, BrickPlan &bp)
 {
-    if (ncu_all <= 0) ncu_all = ncu;
+    const int ncu_all = ncu;
     const int64_t n = (int64_t)Lx * Ly * Lz, Lxy = (int64_t)Lx * Ly;
     // per row: stored blocks (upper tail) and its byte weight
     std::vector<int> mu(n);
@@ -58,7 +71,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
         const int bnx = (d >> 12) & 15, bny = (d >> 16) & 15, bnz = (d >> 20) & 15;
         const int k0 = dbx + bnx * (dby + bny * dbz);
         mu[i] = cnt[i] - k0;
-        const double wgt = 72.0 * mu[i] + 64.0;
+        const double wgt = row_cost(mu[i]);
         wx[x] += wgt;
         wy[y] += wgt;
         wz[z] += wgt;
@@ -81,7 +94,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
         for (int y = 0; y < Ly; ++y)
             for (int x = 0; x < Lx; ++x) {
                 const int64_t i = x + (int64_t)Lx * y + Lxy * z;
-                const double v = 72.0 * mu[i] + 64.0;
+                const double v = row_cost(mu[i]);
                 const int64_t q = (x + 1) + PX1 * (y + 1) + PXY1 * (z + 1);
                 pw[q] = v + pw[q - 1] + pw[q - PX1] + pw[q - PXY1] - pw[q - 1 - PX1] - pw[q - 1 - PXY1] -
                         pw[q - PX1 - PXY1] + pw[q - 1 - PX1 - PXY1];
@@ -116,21 +129,63 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
         // (per CU, TB/s; the SpMV's item loop itself tops out near 1.06x its
         // all-busy rate: 24.7 -> 27.5 GB/s per CU from 256 to 224 bricks,
         // profiles/r05/phase_bricks_*.jsonl)
-        return std::min(R / std::max(f, 1e-9), 1.06 * 6.87 / 256.0);
+        // (x 1.246: the rates are of bytes, the costs of full-item bytes --
+        // 33.4 GB/s of them per CU with every CU busy, against 26.8 GB/s)
+        return 1.246 * std::min(R / std::max(f, 1e-9), 1.06 * 6.87 / 256.0);
     };
+    // bricks are dispatched in descending bytes to the first free CU (one per
+    // CU: each asks for more than half the LDS); every brick after a CU's
+    // first pays a refill (x fill, first loads) of about 100 KB of streaming
     auto model = [&](std::vector<double> w) {
-        std::sort(w.begin(), w.end());
-        double t = 0.0, done = 0.0;
+        std::sort(w.rbegin(), w.rend());
         const int NB = (int)w.size();
-        for (int j = 0; j < NB; ++j) {
-            t += (w[j] - done) / rate_pc(NB - j);
-            done = w[j];
+        std::vector<double> act;
+        int q = 0;
+        for (; q < NB && q < ncu; ++q) act.push_back(w[q]);
+        double t = 0.0;
+        while (!act.empty()) {
+            const double r = rate_pc((int)act.size());
+            const double m = *std::min_element(act.begin(), act.end());
+            t += m / r;
+            std::vector<double> nx;
+            for (double v : act)
+                if (v - m > 1e-6) nx.push_back(v - m);
+                else if (q < NB) nx.push_back(w[q++] + 1.0e5);
+            act.swap(nx);
         }
         return t;
     };
     double best_t = 1e300;
     int64_t best_ent = INT64_MAX;
-    std::vector<int> bcx, bcy, bcz;
+    struct Box {
+        int x0, x1, y0, y1, z0, z1;
+    };
+    std::vector<Box> best;
+    auto consider = [&](const std::vector<Box> &bx, const std::vector<double> &w, int64_t ent) {
+        const double t = model(w);
+        if (t < best_t * 0.999 || (t <= best_t * 1.001 && ent < best_ent)) {
+            // (the gather stages at most BG_MAXNB neighbouring regions per brick)
+            for (const Box &B : bx) {
+                int o, RX, RY, RZ, ox, oy, oz, nb = 0;
+                (void)o;
+                for (const Box &E : bx) {
+                    region(xlo, xhi, E.x0, E.x1, ox, RX);
+                    region(ylo, yhi, E.y0, E.y1, oy, RY);
+                    region(zlo_none, zhi, E.z0, E.z1, oz, RZ);
+                    nb += ox < B.x1 && B.x0 < ox + RX && oy < B.y1 && B.y0 < oy + RY && oz < B.z1 && B.z0 < oz + RZ;
+                }
+                if (nb > BG_MAXNB) return;
+            }
+            best_t = t;
+            best_ent = ent;
+            // (dispatch order: the heaviest brick first)
+            std::vector<int> ord(bx.size());
+            for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return w[a] > w[b]; });
+            best.clear();
+            for (int k : ord) best.push_back(bx[k]);
+        }
+    };
     // (fs: forced split counts nbx + 100 nby + 10000 nbz; + 1000000: cuts by
     // equal node counts only; + 10000000: weighted cuts at any node only)
     const int fmode = fs / 1000000;
@@ -156,9 +211,11 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
     // neighbouring bricks only)
     const int ex = std::max(1, (Lx - 1) / std::max(P, 1)), ey = std::max(1, (Ly - 1) / std::max(P, 1)),
               ez = std::max(1, (Lz - 1) / std::max(P, 1));
-    for (int nbz = 1; nbz <= std::min(ez, ncu); ++nbz)
-        for (int nby = 1; nby <= std::min(ey, ncu / nbz); ++nby)
-            for (int nbx = 1; nbx <= std::min(ex, ncu / (nbz * nby)); ++nbx) {
+    for (int bpc = 1; bpc <= std::max(1, rounds); ++bpc) {
+        const int nmax = nfix > 0 ? nfix : bpc * ncu;
+    for (int nbz = 1; nbz <= std::min(ez, nmax); ++nbz)
+        for (int nby = 1; nby <= std::min(ey, nmax / nbz); ++nby)
+            for (int nbx = 1; nbx <= std::min(ex, nmax / (nbz * nby)); ++nbx) {
                 if (fs && fs != nbx + 100 * nby + 10000 * nbz) continue;
                 for (const Var &VX : vx)
                     for (const Var &VY : vy)
@@ -187,39 +244,217 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
                                                     72.0 * RN);
                                     }
                             if (!fits) continue;
-                            const double t = model(w);
-                            if (t < best_t * 0.999 || (t <= best_t * 1.001 && ent < best_ent)) {
-                                best_t = t;
-                                best_ent = ent;
-                                bcx = cx;
-                                bcy = cy;
-                                bcz = cz;
-                            }
+                            std::vector<Box> bx;
+                            for (int e = 0; e < nbz; ++e)
+                                for (int c = 0; c < nby; ++c)
+                                    for (int a = 0; a < nbx; ++a)
+                                        bx.push_back({cx[a], cx[a + 1], cy[c], cy[c + 1], cz[e], cz[e + 1]});
+                            consider(bx, w, ent);
                         }
             }
+    // Per-slab grids: z slabs of one or two element layers, each with its own
+    // nbx x nby grid and cuts, the CUs allotted to the slabs by weight (the
+    // Dirichlet top and bottom layers of a box carry 0.66 / 0.71 of an
+    // interior layer's bytes, the x / y face columns 0.91-0.93: one tensor
+    // grid leaves those CUs idle early).  Per slab, the best max brick weight
+    // for every brick count; then greedily more bricks to the slab whose
+    // largest brick is the largest, while the total stays <= nmax.
+    if (fs == 0) {
+        for (int t = 1; t <= 2; ++t) {
+            const int ns = std::max(1, ez / t);
+            std::vector<int> cz;
+            if (!split_axis(uz, ns, P, cz)) continue;
+            struct Opt {
+                double m = 1e300;
+                int64_t ent = 0;
+                std::vector<int> cx, cy;
+            };
+            std::vector<std::vector<Opt>> opt(ns, std::vector<Opt>(nmax + 1));
+            bool ok = true;
+            for (int sl = 0; sl < ns && ok; ++sl) {
+                const int z0 = cz[sl], z1 = cz[sl + 1];
+                int o, RZ;
+                region(zlo_none, zhi, z0, z1, o, RZ);
+                std::vector<double> sx(Lx), sy(Ly);
+                for (int xx = 0; xx < Lx; ++xx) sx[xx] = box_sum(xx, xx + 1, 0, Ly, z0, z1);
+                for (int yy = 0; yy < Ly; ++yy) sy[yy] = box_sum(0, Lx, yy, yy + 1, z0, z1);
+                const std::vector<Var> wvx = {{&sx, P}, {&sx, 1}, {&ux, P}}, wvy = {{&sy, P}, {&sy, 1}, {&uy, P}};
+                for (int nby = 1; nby <= std::min(ey, nmax); ++nby)
+                    for (int nbx = 1; nbx <= std::min(ex, nmax / nby); ++nbx)
+                        for (const Var &VX : wvx)
+                            for (const Var &VY : wvy) {
+                                std::vector<int> cx, cy;
+                                if (!split_axis(*VX.w, nbx, VX.q, cx) || !split_axis(*VY.w, nby, VY.q, cy)) continue;
+                                std::vector<int> RXs(nbx), RYs(nby);
+                                for (int a = 0; a < nbx; ++a) region(xlo, xhi, cx[a], cx[a + 1], o, RXs[a]);
+                                for (int a = 0; a < nby; ++a) region(ylo, yhi, cy[a], cy[a + 1], o, RYs[a]);
+                                double m = 0.0;
+                                int64_t ent = 0;
+                                bool fits = true;
+                                for (int c = 0; c < nby && fits; ++c)
+                                    for (int a = 0; a < nbx && fits; ++a) {
+                                        const int RN = RXs[a] * RYs[c] * RZ;
+                                        if (RN > 65535 || brick_lds(RN) > BRICK_LDS_CAP) fits = false;
+                                        ent += RN;
+                                        m = std::max(m, box_sum(cx[a], cx[a + 1], cy[c], cy[c + 1], z0, z1) + 72.0 * RN);
+                                    }
+                                Opt &O = opt[sl][nbx * nby];
+                                if (fits && (m < O.m * 0.999 || (m <= O.m * 1.001 && ent < O.ent))) {
+                                    O.m = m;
+                                    O.ent = ent;
+                                    O.cx = cx;
+                                    O.cy = cy;
+                                }
+                            }
+                // (prefix minima: the best plan with at most n bricks)
+                int first = -1;
+                for (int k = 1; k <= nmax; ++k) {
+                    if (first < 0 && opt[sl][k].m < 1e300) first = k;
+                    if (k > 1 && opt[sl][k - 1].m < opt[sl][k].m) opt[sl][k] = opt[sl][k - 1];
+                }
+                if (first < 0) ok = false;
+            }
+            if (!ok) continue;
+            std::vector<int> cnt_s(ns);
+            int tot = 0;
+            for (int sl = 0; sl < ns; ++sl) {
+                int k = 1;
+                while (opt[sl][k].m >= 1e300) ++k;
+                cnt_s[sl] = k;
+                tot += k;
+            }
+            if (tot > nmax) continue;
+            for (;;) {
+                int worst = 0;
+                for (int sl = 1; sl < ns; ++sl)
+                    if (opt[sl][cnt_s[sl]].m > opt[worst][cnt_s[worst]].m) worst = sl;
+                int k = cnt_s[worst] + 1;
+                while (k <= nmax && opt[worst][k].m >= opt[worst][cnt_s[worst]].m * 0.9999) ++k;
+                if (k > nmax || tot + k - cnt_s[worst] > nmax) break;
+                tot += k - cnt_s[worst];
+                cnt_s[worst] = k;
+            }
+            std::vector<Box> bx;
+            std::vector<double> w;
+            int64_t ent = 0;
+            for (int sl = 0; sl < ns; ++sl) {
+                const Opt &O = opt[sl][cnt_s[sl]];
+                int o, RZ;
+                region(zlo_none, zhi, cz[sl], cz[sl + 1], o, RZ);
+                for (size_t c = 0; c + 1 < O.cy.size(); ++c)
+                    for (size_t a = 0; a + 1 < O.cx.size(); ++a) {
+                        int RX, RY;
+                        region(xlo, xhi, O.cx[a], O.cx[a + 1], o, RX);
+                        region(ylo, yhi, O.cy[c], O.cy[c + 1], o, RY);
+                        bx.push_back({O.cx[a], O.cx[a + 1], O.cy[c], O.cy[c + 1], cz[sl], cz[sl + 1]});
+                        w.push_back(box_sum(O.cx[a], O.cx[a + 1], O.cy[c], O.cy[c + 1], cz[sl], cz[sl + 1]) +
+                                    72.0 * RX * RY * RZ);
+                        ent += (int64_t)RX * RY * RZ;
+                    }
+            }
+            consider(bx, w, ent);
+        }
+    }
+    // Recursive bisection inside z slabs of one or two element layers: each
+    // slab gets bricks in proportion to its bytes (largest remainders), and a
+    // rectangle of n bricks is cut across its longer side at the node that
+    // splits its bytes n1 : n - n1 -- the face columns' light rows go to
+    // wider bricks without widening the others.
+    if (fs == 0) {
+        for (int t = 1; t <= 2; ++t) {
+            const int ns = std::max(1, ez / t);
+            std::vector<int> cz;
+            if (!split_axis(uz, ns, P, cz) || ns > nmax) continue;
+            const double W = box_sum(0, Lx, 0, Ly, 0, Lz);
+            std::vector<int> nsl(ns);
+            std::vector<std::pair<double, int>> rem;
+            int tot = 0;
+            for (int sl = 0; sl < ns; ++sl) {
+                const double q = box_sum(0, Lx, 0, Ly, cz[sl], cz[sl + 1]) / W * nmax;
+                nsl[sl] = std::max(1, (int)q);
+                tot += nsl[sl];
+                rem.push_back({q - (int)q, sl});
+            }
+            std::sort(rem.rbegin(), rem.rend());
+            for (size_t k = 0; k < rem.size() && tot < nmax; ++k, ++tot) ++nsl[rem[k].second];
+            if (tot > nmax) continue;
+            std::vector<Box> bx;
+            std::function<void(int, int, int, int, int, int, int)> cut = [&](int x0, int x1, int y0, int y1, int z0,
+                                                                            int z1, int nb) {
+                // (both halves keep at least an element along the cut side)
+                const bool cx_ok = x1 - x0 >= 2 * P, cy_ok = y1 - y0 >= 2 * P;
+                if (nb <= 1 || (!cx_ok && !cy_ok)) {
+                    bx.push_back({x0, x1, y0, y1, z0, z1});
+                    return;
+                }
+                const int n1 = nb / 2;
+                const double target = box_sum(x0, x1, y0, y1, z0, z1) * n1 / nb;
+                const bool alongx = cx_ok && (!cy_ok || x1 - x0 >= y1 - y0);
+                const int lo = alongx ? x0 : y0, hi = alongx ? x1 : y1;
+                int bestc = lo + P;
+                double bestd = 1e300;
+                for (int c = lo + P; c <= hi - P; ++c) {
+                    const double wl = alongx ? box_sum(x0, c, y0, y1, z0, z1) : box_sum(x0, x1, y0, c, z0, z1);
+                    if (std::fabs(wl - target) < bestd) {
+                        bestd = std::fabs(wl - target);
+                        bestc = c;
+                    }
+                }
+                if (alongx) {
+                    cut(x0, bestc, y0, y1, z0, z1, n1);
+                    cut(bestc, x1, y0, y1, z0, z1, nb - n1);
+                } else {
+                    cut(x0, x1, y0, bestc, z0, z1, n1);
+                    cut(x0, x1, bestc, y1, z0, z1, nb - n1);
+                }
+            };
+            for (int sl = 0; sl < ns; ++sl) cut(0, Lx, 0, Ly, cz[sl], cz[sl + 1], nsl[sl]);
+            std::vector<double> w;
+            int64_t ent = 0;
+            bool fits = true;
+            for (const Box &B : bx) {
+                int o, RX, RY, RZ;
+                region(xlo, xhi, B.x0, B.x1, o, RX);
+                region(ylo, yhi, B.y0, B.y1, o, RY);
+                region(zlo_none, zhi, B.z0, B.z1, o, RZ);
+                const int RN = RX * RY * RZ;
+                if (RN > 65535 || brick_lds(RN) > BRICK_LDS_CAP) fits = false;
+                ent += RN;
+                w.push_back(box_sum(B.x0, B.x1, B.y0, B.y1, B.z0, B.z1) + 72.0 * RN);
+            }
+            if (getenv("KLE_BRICK_DEBUG")) {
+                double mx = 0, sm = 0;
+                for (double v : w) mx = std::max(mx, v), sm += v;
+                fprintf(stderr, "bisect t=%d bricks %zu fits %d max/mean %.4f model %.1f\n", t, bx.size(), (int)fits,
+                        mx / (sm / w.size()), model(w) * 1e-6);
+            }
+            if (fits) consider(bx, w, ent);
+        }
+    }
+        if (nfix > 0) break;
+    }
     bp.model_us = best_t * 1e-6;  // (bytes / (TB/s) = us)
     (void)total;
-    if (bcx.empty()) return "no brick decomposition fits the LDS";
-    const int nbx = (int)bcx.size() - 1, nby = (int)bcy.size() - 1, nbz = (int)bcz.size() - 1, NB = nbx * nby * nbz;
+    if (best.empty()) return "no brick decomposition fits the LDS";
+    const int NB = (int)best.size();
     bp.bricks.assign(NB, BrickDesc{});
     bp.rowd.assign(2 * n, 0);
     bp.svb.assign(n + 1, 0);
     int64_t voff = 0, rows = 0, wsd = 0;
     bp.lds = 0;
     bp.ws_entries = 0;
-    for (int e = 0; e < nbz; ++e)
-        for (int c = 0; c < nby; ++c)
-            for (int a = 0; a < nbx; ++a) {
-                BrickDesc &D = bp.bricks[((size_t)e * nby + c) * nbx + a];
-                D.x0 = bcx[a];
-                D.nx = bcx[a + 1] - bcx[a];
-                D.y0 = bcy[c];
-                D.ny = bcy[c + 1] - bcy[c];
-                D.z0 = bcz[e];
-                D.nz = bcz[e + 1] - bcz[e];
-                region(xlo, xhi, bcx[a], bcx[a + 1], D.ox, D.RX);
-                region(ylo, yhi, bcy[c], bcy[c + 1], D.oy, D.RY);
-                region(zlo_none, zhi, bcz[e], bcz[e + 1], D.oz, D.RZ);
+    for (int q = 0; q < NB; ++q) {
+                const Box &B = best[q];
+                BrickDesc &D = bp.bricks[q];
+                D.x0 = B.x0;
+                D.nx = B.x1 - B.x0;
+                D.y0 = B.y0;
+                D.ny = B.y1 - B.y0;
+                D.z0 = B.z0;
+                D.nz = B.z1 - B.z0;
+                region(xlo, xhi, B.x0, B.x1, D.ox, D.RX);
+                region(ylo, yhi, B.y0, B.y1, D.oy, D.RY);
+                region(zlo_none, zhi, B.z0, B.z1, D.oz, D.RZ);
                 const int RN = D.RX * D.RY * D.RZ;
                 D.rstart = (int)rows;
                 D.eb = 0;
@@ -244,14 +479,29 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
                 for (int z = D.oz; z < D.oz + D.RZ; ++z)
                     for (int y = D.oy; y < D.oy + D.RY; ++y)
                         for (int x = D.ox; x < D.ox + D.RX; ++x)
-                            bp.ws_entries += x >= 0 && x < Lx && y >= 0 && y < Ly && z >= 0 && z < Lz;
+                            bp.ws_entries += x >= 0 && x < Lx && y >= 0 && y < Ly && z >= 0 && z < Lz + hp;
             }
     bp.svb[n] = voff;
     bp.ws_doubles = wsd;
     // per brick, the bricks whose regions meet its owned box (ascending)
-    bp.nbptr.assign(NB + 1, 0);
+    // N > 1: the upper ghost planes in pieces over the top bricks' footprints
+    // (no rows: the gather sums their region entries into the reverse halo)
+    bp.nreal = NB;
+    if (hp > 0)
+        for (int q = 0; q < NB; ++q)
+            if (bp.bricks[q].z0 + bp.bricks[q].nz == Lz) {
+                BrickDesc G = bp.bricks[q];
+                G.z0 = Lz;
+                G.nz = hp;
+                G.RX = G.RY = G.RZ = 0;
+                G.rstart = 0;
+                G.vbase = G.wsoff = 0;
+                bp.bricks.push_back(G);
+            }
+    const int NT = (int)bp.bricks.size();
+    bp.nbptr.assign(NT + 1, 0);
     bp.nblist.clear();
-    for (int q = 0; q < NB; ++q) {
+    for (int q = 0; q < NT; ++q) {
         const BrickDesc &D = bp.bricks[q];
         for (int q2 = 0; q2 < NB; ++q2) {
             const BrickDesc &E = bp.bricks[q2];
@@ -278,8 +528,8 @@ std::string brick_plan(int Lx, int Ly, int Lz, int ncu, int fs, const std::vecto
 // info[0] bricks, [1] bricks along x, [2] y, [3] z, [4] LDS bytes;
 // stats[0] bytes of the largest brick / the mean, [1] region entries per row,
 // [2] stored blocks, [3] the planner's time model (us).  Returns KLE_ERR_SUP (with the reason) when no plan fits.
-extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, int ncu, int split, int *info,
-                                  double *stats)
+extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, int ncu, int rounds, int split,
+                                  int *info, double *stats)
 {
     using namespace kle;
     KLE_ARG(Lx >= 1 && Ly >= 1 && Lz >= 1 && p >= 1 && p <= 7 && ncu >= 1 && info && stats, "bad arg");
@@ -315,7 +565,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
                 blocks += cnt[i] - ((x - bx) + nx * ((y - by) + ny * (z - bz)));
             }
     BrickPlan bp;
-    const std::string why = brick_plan(Lx, Ly, Lz, ncu, split, cnt, srow, p, bp, ncu);
+    const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();
     double tot = 0.0, mx = 0.0;
@@ -326,7 +576,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
             const int64_t i = (D.x0 + rx) + (int64_t)Lx * ((D.y0 + ry) + (int64_t)Ly * (D.z0 + rz));
             const int d = srow[i];
             const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));
-            w += 72.0 * (cnt[i] - k0) + 64.0;
+            w += row_cost(cnt[i] - k0);
         }
         tot += w;
         mx = std::max(mx, w);
@@ -346,5 +596,18 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     stats[1] = (double)bp.ws_entries / n;
     stats[2] = (double)blocks;
     stats[3] = bp.model_us;
+    if (getenv("KLE_BRICK_DEBUG"))
+        for (const BrickDesc &D : bp.bricks) {
+            double w = 0.0;
+            for (int r = 0; r < D.nx * D.ny * D.nz; ++r) {
+                const int rz = r / (D.nx * D.ny), rem = r - rz * D.nx * D.ny, ry = rem / D.nx, rx = rem - ry * D.nx;
+                const int64_t i = (D.x0 + rx) + (int64_t)Lx * ((D.y0 + ry) + (int64_t)Ly * (D.z0 + rz));
+                const int d = srow[i];
+                const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));
+                w += row_cost(cnt[i] - k0);
+            }
+            fprintf(stderr, "brick %d %d %d  %d %d %d  region %d %d %d  w %.4f\n", D.x0, D.y0, D.z0, D.nx, D.ny, D.nz,
+                    D.RX, D.RY, D.RZ, w / (tot / NB));
+        }
     return 0;
 }

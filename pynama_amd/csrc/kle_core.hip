@@ -725,6 +725,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_split") {
         KLE_ARG(value >= 0, "spmv_brick_split: nbx + 100 nby + 10000 nbz (0: planned)");
         g_tune.spmv_brick_split = value;
+    } else if (k == "spmv_brick_rounds") {
+        KLE_ARG(value >= 1 && value <= 4, "spmv_brick_rounds: 1 .. 4 bricks per CU");
+        g_tune.spmv_brick_rounds = value;
     } else if (k == "spmv_brick_max") {
         KLE_ARG(value >= 0, "spmv_brick_max: >= 0 (0: one brick per CU)");
         g_tune.spmv_brick_max = value;
@@ -810,6 +813,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_brick") *value = g_tune.spmv_sym_brick;
     else if (k == "spmv_brick_ahead") *value = g_tune.spmv_brick_ahead;
     else if (k == "spmv_brick_max") *value = g_tune.spmv_brick_max;
+    else if (k == "spmv_brick_rounds") *value = g_tune.spmv_brick_rounds;
     else if (k == "spmv_brick_split") *value = g_tune.spmv_brick_split;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;

@@ -259,6 +259,7 @@ struct kle_mat {
     // region sums, d_stile_e their bound exponents
     int sym_brick = 0;
     int nbricks = 0, brick_lds = 0, brick_gparts = 0;  // (gather workgroups per brick)
+    int nbricks_ghost = 0;  // N > 1: upper-ghost pieces after the bricks (gather only: the reverse halo's sums)
     int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
     double brick_model_us = 0.0;    // the planner's modelled product time
     void *d_bdesc = nullptr;
@@ -383,7 +384,8 @@ struct Tuning {
     int spmv_sym_early = 0;   // symmetric SpMV tiles: the first item's value loads issued with the x fill (1) or after it (0)
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
     int spmv_brick_ahead = 1;  // brick SpMV: items in flight ahead of the summed one per wave (1 or 2)
-    int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: one per CU)
+    int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: planned, spmv_brick_rounds per CU)
+    int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)
     int spmv_sym_brick = 1;   // box symmetric storage, one rank (read at build): one brick per CU, sums in LDS for the whole stream (kle_brick.hip); 0 the 128-row tiles
 #ifdef KLE_PROBE_BUILD

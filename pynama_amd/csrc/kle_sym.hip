@@ -1717,13 +1717,21 @@ static int sym_build_impl(kle_mat *A)
         void *&p;
         ~PlanGuard() { brick_plan_free(p); }
     } bguard{bplan};
-    if (why.empty() && g_tune.spmv_sym_brick && g_tune.spmv_sym_det && c->nranks == 1 && zo == 0 && hp == 0) {
+    // (one rank, or z slabs; every rank takes the same decision)
+    if (why.empty() && g_tune.spmv_sym_brick && g_tune.spmv_sym_det && (c->nranks == 1 ? zo == 0 && hp == 0 : !A->plan)) {
         std::string bwhy;
         std::vector<int64_t> svb;
         KLE_TRY(brick_setup(A, rb, cnt, srow, P, svb, bwhy, &bplan));
+        bool none = false;
+        KLE_TRY(any_rank(c, !bplan, none));
+        if (none && bplan) {
+            brick_plan_free(bplan);
+            bplan = nullptr;
+            bwhy = "not on every rank";
+        }
         if (bplan) sv.swap(svb);
         else if (const char *e = getenv("KLE_TIMING"))
-            if (atoi(e)) fprintf(stderr, "[kle brick] not used: %s\n", bwhy.c_str());
+            if (atoi(e)) fprintf(stderr, "[kle brick r%d] not used: %s\n", c->rank, bwhy.c_str());
     }
     SymRegion reg[NSH];
     for (int s = 0; s < NSH; ++s)
@@ -1820,7 +1828,18 @@ static int sym_build_impl(kle_mat *A)
         A->snvals = tot;
         void *p = bplan;
         bplan = nullptr;  // (brick_finish owns it)
-        const int rc = brick_finish(A, p);
+        int rc = brick_finish(A, p);
+        bool any_fail = false;
+        if (c->nranks > 1) {
+            const int arc = any_rank(c, rc != 0, any_fail);
+            if (!rc && arc) rc = arc;
+            if (!rc && any_fail) rc = fail(KLE_ERR_MEM, "symmetric storage: bricks failed on another rank");
+            if (!rc) {
+                bool bad = false;
+                rc = sym_probe(A, vmax_all, bad);
+                if (!rc && bad) rc = fail(KLE_ERR_SUP, "matrix is not symmetric across ranks (product probe)");
+            }
+        }
         if (rc) sym_drop(A);
         return rc;
     }
@@ -1939,7 +1958,7 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 
 int sym_dot_parts(const kle_mat *A)
 {
-    if (A->sym_brick) return A->nbricks * A->brick_gparts;
+    if (A->sym_brick) return A->ctx->nranks > 1 ? 0 : A->nbricks * A->brick_gparts;
     const bool dist = A->ctx->nranks > 1 && (A->sym_graph || A->lo_rank >= 0 || A->hi_rank >= 0);
     return dist ? 0 : (int)((A->nrows + 255) / 256);
 }

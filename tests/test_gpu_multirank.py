@@ -139,6 +139,20 @@ def test_partitioned_solve_symmetric_storage(size, nelem, ngl, ksp_type, overlap
     res = _check_box(size, nelem, ngl, overlap, ksp_type, sym=True)
     for r in res:
         assert r["sym"], r["rank"]
+        assert r["kernel"].startswith("k_nb_spmv_sym_brick<"), r["kernel"]
+
+
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(2, [3, 2, 4], 4, "pipecg"), (3, [2, 3, 3], 3, "cg"),
+                                                    (8, [2, 2, 8], 4, "pipecg")])
+def test_partitioned_symmetric_storage_tiles(size, nelem, ngl, ksp_type):
+    """The tile kernel on slabs (KLE_SPMV_SYM_BRICK=0; the bricks are the
+    default at every N): same checks."""
+    os.environ["KLE_SPMV_SYM_BRICK"] = "0"  # inherited by the spawned ranks
+    try:
+        res = _check_box(size, nelem, ngl, True, ksp_type, sym=True)
+    finally:
+        del os.environ["KLE_SPMV_SYM_BRICK"]
+    for r in res:
         assert r["kernel"].startswith("k_nb_spmv_sym_xl<"), r["kernel"]
 
 
@@ -148,10 +162,12 @@ def test_partitioned_symmetric_storage_128_row_tiles(size, nelem, ngl, ksp_type)
     tiles by default (spmv_sym_tile64_max), so KLE_SPMV_SYM_TILE64=2 forces the
     shape config-2-sized slabs run; same checks as above."""
     os.environ["KLE_SPMV_SYM_TILE64"] = "2"  # inherited by the spawned ranks
+    os.environ["KLE_SPMV_SYM_BRICK"] = "0"
     try:
         res = _check_box(size, nelem, ngl, True, ksp_type, sym=True)
     finally:
         del os.environ["KLE_SPMV_SYM_TILE64"]
+        del os.environ["KLE_SPMV_SYM_BRICK"]
     for r in res:
         assert r["kernel"] == "k_nb_spmv_sym_xl<8,true,4,4>+k_nb_sym_gather<8,4,4>", r["kernel"]
 
