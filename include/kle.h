@@ -406,6 +406,11 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on);
  * none -- full storage, tiles or the graph kernel): bricks, bricks along
  * x / y / z, region entries per row, the planner's modelled product time
  * (us). */
+/* Diagnostic: move the symmetric storage's value array to a fresh allocation,
+ * `shift` bytes (a multiple of 8, <= 1 GiB) into it, and free the old one.
+ * The product is unchanged bit for bit; its speed should not depend on where
+ * the array lies (tests/test_gpu_fullsize.py). */
+int kle_mat_move_values(kle_mat *A, long long shift);
 int kle_mat_get_sym_bricks(const kle_mat *A, int *nbricks, int *dims, double *entries_per_row, double *model_us);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */
@@ -462,9 +467,15 @@ int kle_ksp_get_true_relative_residual(const kle_ksp *k, double *rel);
  * 1e-10"); n = 0 stops on the recursive residual exactly as PETSc's KSPCG /
  * KSPPIPECG do.  Default 2 (kle_set_tuning "ksp_refine" for new KSPs). */
 int kle_ksp_set_corrections(kle_ksp *k, int n);
-/* Iterations of the last solve's correction solves (0: none ran); they are
- * included in kle_ksp_get_iteration_number. */
+/* Iterations of the last solve's correction solves (0: none ran).  They are
+ * NOT in kle_ksp_get_iteration_number, and the converged reason and residual
+ * norm stay the main solve's (PETSc's KSPGetIterationNumber /
+ * KSPGetConvergedReason of the recursive stop); each correction has max_it of
+ * its own. */
 int kle_ksp_get_correction_iterations(const kle_ksp *k, int *its);
+/* Converged reason of the last correction solve (0: none ran; < 0: it hit
+ * max_it or broke down and the true residual may still miss rtol). */
+int kle_ksp_get_correction_reason(const kle_ksp *k, int *reason);
 
 /* ------------------------------------------------------------ diagnostics */
 /* Streaming read/copy microbenchmark (HBM ceiling for the roofline). */

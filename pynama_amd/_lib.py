@@ -176,6 +176,8 @@ _SIGS = {
     "kle_ksp_get_true_relative_residual": [vp, C.POINTER(C.c_double)],
     "kle_ksp_set_corrections": [vp, C.c_int],
     "kle_ksp_get_correction_iterations": [vp, C.POINTER(C.c_int)],
+    "kle_ksp_get_correction_reason": [vp, C.POINTER(C.c_int)],
+    "kle_mat_move_values": [vp, C.c_longlong],
     "kle_stream_copy_bench": [vp, C.c_int64, C.c_int, C.POINTER(C.c_double)],
     "kle_stream_bench": [vp, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double)],
 }

@@ -52,34 +52,36 @@ struct BItem {
     int r, mu, ir, kb;
 };
 
-// y of brick O's rows from the region sums of the bricks nblist[nbptr[O] ..)
-// (ascending), by NT threads.  (Summing them inside the brick kernel, each
+// y of brick O's rows from the region sums of the bricks its record lists
+// (ascending), by NT threads.  The record (BG_REC ints at O BG_REC: brick_finish)
+// is one load per thread into LDS, so the sums start one round trip after
+// the launch.  (Summing them inside the brick kernel, each
 // brick by the last of its neighbours to finish -- arrival counters, sc1
 // sums -- put the reductions on the slowest CUs: 0.485-0.564 vs 0.399-0.402
 // ms at config 2, profiles/r05/brick_fuse_rejected.jsonl.)
 // nbd: LDS for 8 ints per listed brick; dred: LDS for NT / 64 doubles.
 template <int NT>
-__device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const BrickDesc *__restrict__ bd,
-                                             const int *__restrict__ nbptr, const int *__restrict__ nblist,
+__device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const int *__restrict__ nbrec,
                                              const double *__restrict__ ws, double *__restrict__ y,
-                                             const double *__restrict__ xdot, double *__restrict__ dpart, int *nbd,
+                                             const double *__restrict__ xdot, double *__restrict__ dpart, int *rec,
                                              double *dred, int r0, int r1, int dslot, int64_t jofs)
 {
-    const int x0 = bd[O].x0, y0 = bd[O].y0, z0 = bd[O].z0, nx = bd[O].nx, ny = bd[O].ny, nz = bd[O].nz;
-    const int NR = nx * ny * nz, q0 = nbptr[O], nq = min(nbptr[O + 1] - q0, BG_MAXNB);
-    if ((int)threadIdx.x < nq) {
-        const BrickDesc &E = bd[nblist[q0 + threadIdx.x]];
-        int *o = nbd + 8 * threadIdx.x;
-        o[0] = E.ox;
-        o[1] = E.oy;
-        o[2] = E.oz;
-        o[3] = E.RX;
-        o[4] = E.RY;
-        o[5] = E.RZ;
-        o[6] = (int)(E.wsoff & 0xffffffffll);
-        o[7] = (int)(E.wsoff >> 32);
+    {
+        constexpr int K = (BG_REC + NT - 1) / NT;
+        int v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = (int)threadIdx.x + k * NT;
+            v[k] = nbrec[(int64_t)O * BG_REC + min(t, BG_REC - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if ((int)threadIdx.x + k * NT < BG_REC) rec[threadIdx.x + k * NT] = v[k];
     }
     __syncthreads();
+    const int nq = rec[0], x0 = rec[1], y0 = rec[2], z0 = rec[3], nx = rec[4], ny = rec[5], nz = rec[6];
+    const int NR = nx * ny * nz;
+    const int *nbd = rec + 8;
     const int64_t Lxy = (int64_t)Lx * Ly;
     double dsum = 0.0;
     for (int r = r0 + (int)threadIdx.x; r < min(NR, r1); r += NT) {
@@ -94,28 +96,42 @@ __device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const BrickD
             s1 = y[3 * j + 1];
             s2 = y[3 * j + 2];
         }
-        // (four bricks' loads in flight before their adds, in brick order)
-        for (int q = 0; q < nq; q += 4) {
-            double a[4][3];
-            bool in[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int qq = min(q + u, nq - 1);
-                const int *o = nbd + 8 * qq;
+        // The listed regions holding the row (about 2 of up to BG_MAXNB: the
+        // tests are LDS reads), up to GK of them with their loads in flight at
+        // once, summed in brick order; more (never on a box of element-wide
+        // bricks: at most 3 x 3 x 2) in further rounds.
+        constexpr int GK = 8;
+        for (int q = 0; q < nq;) {
+            const double *pp[GK];
+            int RNs[GK], k = 0;
+            for (; q < nq && k < GK; ++q) {
+                const int *o = nbd + 8 * q;
                 const int lx = gx - o[0], ly = gy - o[1], lz = gz - o[2], RX = o[3], RY = o[4], RZ = o[5];
-                in[u] = q + u < nq && lx >= 0 && lx < RX && ly >= 0 && ly < RY && lz >= 0 && lz < RZ;
-                const int64_t wo = (int64_t)(unsigned)o[6] | ((int64_t)o[7] << 32);
-                const int RN = RX * RY * RZ;
-                const double *p = ws + wo + (in[u] ? lx + RX * (ly + RY * lz) : 0);
+                if (lx >= 0 && lx < RX && ly >= 0 && ly < RY && lz >= 0 && lz < RZ) {
+                    const int64_t wo = (int64_t)(unsigned)o[6] | ((int64_t)o[7] << 32);
+                    const double *p = ws + wo + lx + RX * (ly + RY * lz);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) a[u][c] = p[c * RN];
+                    for (int u = 0; u < GK; ++u)  // (selects: the slots stay in registers)
+                        if (u == k) {
+                            pp[u] = p;
+                            RNs[u] = RX * RY * RZ;
+                        }
+                    ++k;
+                }
             }
+            double a[GK][3];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                s0 += in[u] ? a[u][0] : 0.0;
-                s1 += in[u] ? a[u][1] : 0.0;
-                s2 += in[u] ? a[u][2] : 0.0;
-            }
+            for (int u = 0; u < GK; ++u)
+                if (u < k)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) a[u][c] = pp[u][c * RNs[u]];
+#pragma unroll
+            for (int u = 0; u < GK; ++u)
+                if (u < k) {
+                    s0 += a[u][0];
+                    s1 += a[u][1];
+                    s2 += a[u][2];
+                }
         }
         y[3 * j] = s0;
         y[3 * j + 1] = s1;
@@ -422,20 +438,18 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
 // Workgroup (brick b, part s) takes b's owned rows [256 s, 256 s + 256);
 // with xdot its (y, x) partial goes to dpart[b * parts + s].
 __global__ __launch_bounds__(256) void k_nb_sym_brick_gather(int Lx, int Ly, int parts, int b0,
-                                                             const BrickDesc *__restrict__ bd,
-                                                             const int *__restrict__ nbptr,
-                                                             const int *__restrict__ nblist,
+                                                             const int *__restrict__ nbrec,
                                                              const double *__restrict__ ws, double *__restrict__ y,
                                                              int64_t jofs, const int *__restrict__ istate,
                                                              const double *__restrict__ xdot,
                                                              double *__restrict__ dpart)
 {
     __shared__ double dred[4];
-    __shared__ int nbd[BG_MAXNB * 8];
+    __shared__ int rec[BG_REC];
     const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;
     if (stop) return;  // (uniform)
     const int b = b0 + (int)blockIdx.x / parts, s = (int)blockIdx.x % parts;
-    brick_reduce<256>(b, Lx, Ly, bd, nbptr, nblist, ws, y, xdot, dpart, nbd, dred, 256 * s, 256 * s + 256,
+    brick_reduce<256>(b, Lx, Ly, nbrec, ws, y, xdot, dpart, rec, dred, 256 * s, 256 * s + 256,
                       (int)blockIdx.x, jofs);
 }
 
@@ -561,11 +575,9 @@ int brick_finish(kle_mat *A, void *plan)
     std::vector<int> hmu(n, 0);
     bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NT) != hipSuccess ||
                  hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
-                 hipMalloc(&A->d_bnbptr, sizeof(int) * (NT + 1)) != hipSuccess ||
+                 hipMalloc(&A->d_bnb, sizeof(int) * BG_REC * (size_t)NT) != hipSuccess ||
                  (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
                  (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
-                 hipMalloc(&A->d_bnb, sizeof(int) * std::max<size_t>(bp->nblist.size(), 1)) != hipSuccess ||
-
                  hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
                  hipMalloc(&A->d_stile_e, sizeof(int) * NB) != hipSuccess || hipMalloc(&dmu, sizeof(int) * n) != hipSuccess;
     (void)hipGetLastError();
@@ -590,9 +602,35 @@ int brick_finish(kle_mat *A, void *plan)
     }
     KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NT, hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_browd, bp->rowd.data(), sizeof(int) * bp->rowd.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_bnbptr, bp->nbptr.data(), sizeof(int) * (NT + 1), hipMemcpyHostToDevice));
-    if (!bp->nblist.empty())
-        KLE_HIP(hipMemcpy(A->d_bnb, bp->nblist.data(), sizeof(int) * bp->nblist.size(), hipMemcpyHostToDevice));
+    {
+        // the gather's records (BG_REC)
+        std::vector<int> rec((size_t)BG_REC * NT, 0);
+        for (int q = 0; q < NT; ++q) {
+            const BrickDesc &D = bp->bricks[q];
+            int *o = rec.data() + (size_t)q * BG_REC;
+            const int q0 = bp->nbptr[q], nq = std::min(bp->nbptr[q + 1] - q0, BG_MAXNB);
+            o[0] = nq;
+            o[1] = D.x0;
+            o[2] = D.y0;
+            o[3] = D.z0;
+            o[4] = D.nx;
+            o[5] = D.ny;
+            o[6] = D.nz;
+            for (int k = 0; k < nq; ++k) {
+                const BrickDesc &E = bp->bricks[bp->nblist[q0 + k]];
+                int *e = o + 8 * (k + 1);
+                e[0] = E.ox;
+                e[1] = E.oy;
+                e[2] = E.oz;
+                e[3] = E.RX;
+                e[4] = E.RY;
+                e[5] = E.RZ;
+                e[6] = (int)(E.wsoff & 0xffffffffll);
+                e[7] = (int)(E.wsoff >> 32);
+            }
+        }
+        KLE_HIP(hipMemcpy(A->d_bnb, rec.data(), sizeof(int) * rec.size(), hipMemcpyHostToDevice));
+    }
     KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
@@ -640,7 +678,7 @@ void brick_plan_free(void *plan) { delete reinterpret_cast<BrickPlan *>(plan); }
 
 void brick_drop(kle_mat *A)
 {
-    for (void *q : {A->d_bdesc, (void *)A->d_browd, (void *)A->d_bnbptr, (void *)A->d_bnb})
+    for (void *q : {A->d_bdesc, (void *)A->d_browd, (void *)A->d_bnb})
         if (q) (void)hipFree(q);
     brick_forget(A);
 }
@@ -649,7 +687,7 @@ void brick_forget(kle_mat *A)
 {
     A->d_bdesc = nullptr;
     A->d_browd = nullptr;
-    A->d_bnbptr = A->d_bnb = nullptr;
+    A->d_bnb = nullptr;
     A->nbricks = 0;
     A->nbricks_ghost = 0;
     A->brick_gparts = 0;
@@ -680,7 +718,7 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     auto gather = [&](int b0, int nb, double *out, int64_t jofs, double *dp, hipStream_t st) {
         if (nb <= 0) return;
         hipLaunchKernelGGL(k_nb_sym_brick_gather, dim3((unsigned)(nb * A->brick_gparts)), dim3(256), 0, st,
-                           (int)A->row_lat[0], (int)A->row_lat[1], A->brick_gparts, b0, bd, A->d_bnbptr, A->d_bnb,
+                           (int)A->row_lat[0], (int)A->row_lat[1], A->brick_gparts, b0, A->d_bnb,
                            A->d_sws, out, jofs, istate, dp ? x->d : nullptr, dp);
     };
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);

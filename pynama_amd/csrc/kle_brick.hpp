@@ -42,6 +42,10 @@ struct BrickPlan {
 // dummy slots, wave maxima, the row counter)
 inline size_t brick_lds(int RN) { return (size_t)(3 * RN + 3 * (RN + 64)) * 8 + 512; }
 constexpr int BG_MAXNB = 64;  // bricks whose regions meet one brick's rows (27 in a regular grid)
+// the gather's record per brick: a header (listed regions, the brick's own
+// box: nq, x0, y0, z0, nx, ny, nz, 0) and per listed region (ascending
+// brick order) ox, oy, oz, RX, RY, RZ and its workspace offset (2 ints)
+constexpr int BG_REC = 8 * (BG_MAXNB + 1);
 
 // bricks for the owned Lx x Ly x Lz lattice of a rank (rows x-fastest; per
 // row its block count and packed box, kle_sym.hip srow; hp upper ghost

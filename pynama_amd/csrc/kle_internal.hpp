@@ -238,6 +238,7 @@ struct kle_mat {
     // SBAIJ; structured 3x3 rows, one rank or z slabs): each row's blocks from
     // its diagonal block on, in the chunked layout; per-tile partial sums d_sws
     double *d_sval = nullptr;
+    void *sval_raw = nullptr;  // kle_mat_move_values: the allocation d_sval lies in (freed instead of it)
     int64_t *d_svptr = nullptr;
     double *d_sws = nullptr;
     int *d_stile_e = nullptr;  // per tile: 2^e bounds its transposed row sums (fixed-point scale, k_sym_bound)
@@ -263,7 +264,7 @@ struct kle_mat {
     int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
     double brick_model_us = 0.0;    // the planner's modelled product time
     void *d_bdesc = nullptr;
-    int *d_browd = nullptr, *d_bnbptr = nullptr, *d_bnb = nullptr;
+    int *d_browd = nullptr, *d_bnb = nullptr;  // (d_bnb: the gather's records, BG_REC ints per brick)
     int64_t *d_sbp = nullptr;     // per row: its first stored block in d_slid
     uint16_t *d_slid = nullptr;   // per stored block: its column's position in the group dictionary
     int *d_sdptr = nullptr, *d_sdict = nullptr;  // per group of G rows: sorted distinct stored columns

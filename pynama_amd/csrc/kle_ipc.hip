@@ -19,8 +19,10 @@
 // receiver acked s - 1 (the slot is free), copies into the receiver's slot and
 // writes s into the receiver's data flag; the receiver's stream waits for data
 // flag >= s, copies the slot out (or sums it) and writes s into the sender's
-// ack flag.  Every rank calls every collective in the same order, so the
-// per-channel sequence counters agree without communication.
+// ack flag.  The sequence numbers count per channel AND per ordered pair
+// (sender -> receiver): a rank whose halo plan has no peers skips the
+// exchange, and only the pairs that exchange advance, so any later plan that
+// pairs it with a peer finds both counters in step.
 //
 // Slab partitions use one slot per direction (FWD_LO / FWD_HI / REV_LO);
 // graph partitions (HaloPlan: any number of peers) and the allreduce use one
@@ -29,13 +31,18 @@
 // Deadline: a peer that dies or stops calling the collectives leaves this
 // rank's stream waiting on a flag forever (a stream wait has no timeout).
 // Every collective therefore ends with a stream write of its ticket into a
-// host-pinned progress word; a watchdog thread that sees an issued ticket make
-// no progress for KLE_COMM_TIMEOUT_S seconds (default 300, as for
-// ncclCommInitRank) reports the stuck channel and ends the process with exit
-// status KLE_IPC_EXIT (75): the host thread is blocked inside the runtime and
-// cannot return an error, and a process exit is what frees the stuck queue.
+// host-pinned progress word, and a watchdog thread watches the issued tickets.
+// When one makes no progress it checks the processes of the peers that
+// collective waits on (their pids are exchanged at bootstrap; IPC peers share
+// the node): a peer that has exited ends this process after IPC_DEAD_GRACE_S.
+// A live peer doing long host-only work between collectives (I/O, CPU
+// assembly) is never cut off -- as with NCCL, operations have no timeout --
+// unless KLE_COMM_TIMEOUT_S > 0 sets one.  The exit status is KLE_IPC_EXIT
+// (75): the host thread is blocked inside the runtime and cannot return an
+// error, and a process exit is what frees the stuck queue.
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -55,6 +62,7 @@ constexpr int64_t IPC_HALO_CAP = int64_t(1) << 22;   // doubles per slab halo sl
 constexpr int64_t IPC_AR_CAP = PART_STRIDE;          // doubles per allreduce slot (one per sender)
 constexpr int64_t IPC_PLAN_CAP = int64_t(1) << 19;   // doubles per graph-halo slot (4 MB, one per sender)
 constexpr int KLE_IPC_EXIT = 75;                     // process exit status of a missed deadline
+constexpr double IPC_DEAD_GRACE_S = 2.0;             // stalled this long with an awaited peer gone: exit
 
 struct IpcFlags {
     uint64_t data[IPC_NCH][IPC_MAXR];  // [channel][sender]
@@ -65,7 +73,9 @@ static_assert(sizeof(IpcFlags) <= IPC_HDR, "mailbox header");
 struct IpcState {
     char *local = nullptr;          // my mailbox
     std::vector<char *> peer;       // every rank's mailbox mapped here (peer[me] = local)
-    uint64_t seq[IPC_NCH] = {};
+    std::vector<long> pid;          // every rank's process id (bootstrap)
+    uint64_t sseq[IPC_NCH][IPC_MAXR] = {};  // deliveries sent to each rank, per channel
+    uint64_t rseq[IPC_NCH][IPC_MAXR] = {};  // deliveries received from each rank, per channel
     int nranks = 1;
     size_t bytes = 0;
     // watchdog: progress words per stream (0 compute, 1 comm), host-pinned,
@@ -76,9 +86,10 @@ struct IpcState {
     std::atomic<uint64_t> issued[2];
     std::mutex mu;
     std::string what[2];
+    std::vector<int> awaited[2];    // peers of the newest collective per stream
     std::thread wd;
     std::atomic<bool> stop{false};
-    double deadline_s = 300.0;
+    double deadline_s = 0.0;        // > 0: also exit on a live peer's stall (KLE_COMM_TIMEOUT_S)
     int rank = 0;
 
     IpcState() { issued[0] = issued[1] = 0; }
@@ -140,8 +151,24 @@ static int ipc_done(kle_ctx *c, hipStream_t st, IpcChannel ch, const std::vector
         for (int q : peers) w += " " + std::to_string(q);
         std::lock_guard<std::mutex> lk(P.mu);
         P.what[k] = w;
+        P.awaited[k] = peers;
     }
     return post(st, P.d_prog + k, ++P.issued[k]);
+}
+
+// has process pid ended?  (gone from /proc, or a zombie not yet reaped)
+static bool pid_dead(long pid)
+{
+    char path[64];
+    snprintf(path, sizeof path, "/proc/%ld/stat", pid);
+    FILE *f = fopen(path, "r");
+    if (!f) return true;
+    char buf[512];
+    const size_t n = fread(buf, 1, sizeof buf - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    const char *e = strrchr(buf, ')');  // (state follows the command name)
+    return e && e[1] == ' ' && (e[2] == 'Z' || e[2] == 'X');
 }
 
 static void ipc_watchdog(IpcState *P)
@@ -159,40 +186,51 @@ static void ipc_watchdog(IpcState *P)
                 continue;
             }
             const double idle = std::chrono::duration<double>(clk::now() - since[k]).count();
-            if (idle > P->deadline_s) {
-                std::string w;
-                {
-                    std::lock_guard<std::mutex> lk(P->mu);
-                    w = P->what[k];
-                }
+            if (idle < IPC_DEAD_GRACE_S) continue;
+            std::string w;
+            int gone = -1;
+            {
+                std::lock_guard<std::mutex> lk(P->mu);
+                w = P->what[k];
+                for (int q : P->awaited[k])
+                    if (q >= 0 && q < (int)P->pid.size() && pid_dead(P->pid[q])) gone = q;
+            }
+            if (gone < 0 && !(P->deadline_s > 0.0 && idle > P->deadline_s)) continue;
+            if (gone >= 0)
+                fprintf(stderr,
+                        "kle: rank %d: IPC transport stalled %.0f s on the %s stream (collective %llu of %llu; newest: "
+                        "%s) and rank %d (pid %ld) has exited -- exiting with status %d\n",
+                        P->rank, idle, k ? "comm" : "compute", (unsigned long long)done + 1, (unsigned long long)iss,
+                        w.c_str(), gone, P->pid[gone], KLE_IPC_EXIT);
+            else
                 fprintf(stderr,
                         "kle: rank %d: IPC transport made no progress for %.0f s on the %s stream (collective %llu of "
-                        "%llu; newest: %s): a peer died or stopped calling the collectives (KLE_COMM_TIMEOUT_S) -- "
-                        "exiting with status %d\n",
+                        "%llu; newest: %s): a peer stopped calling the collectives (KLE_COMM_TIMEOUT_S) -- exiting "
+                        "with status %d\n",
                         P->rank, idle, k ? "comm" : "compute", (unsigned long long)done + 1,
                         (unsigned long long)iss, w.c_str(), KLE_IPC_EXIT);
-                fflush(stderr);
-                _exit(KLE_IPC_EXIT);
-            }
+            fflush(stderr);
+            _exit(KLE_IPC_EXIT);
         }
     }
 }
 
-// one delivery of n doubles from src into dst (rank `to`'s slot of channel c)
-static int ipc_send(kle_ctx *c, IpcChannel ch, int to, const double *src, int64_t n, double *dst, uint64_t s,
-                    hipStream_t st)
+// one delivery of n doubles from src into dst (rank `to`'s slot of channel c),
+// the pair's next sequence number
+static int ipc_send(kle_ctx *c, IpcChannel ch, int to, const double *src, int64_t n, double *dst, hipStream_t st)
 {
     IpcState &P = *c->ipc;
+    const uint64_t s = ++P.sseq[ch][to];
     KLE_TRY(wait_ge(st, P.ack_flag(c->rank, ch, to), s - 1));  // the receiver has consumed s - 1
     if (n) KLE_HIP(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     return post(st, P.data_flag(to, ch, c->rank), s);
 }
 
 // the matching receive: n doubles from rank `from` out of src (my slot) into dst
-static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, const double *src, int64_t n, uint64_t s,
-                    hipStream_t st)
+static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, const double *src, int64_t n, hipStream_t st)
 {
     IpcState &P = *c->ipc;
+    const uint64_t s = ++P.rseq[ch][from];
     KLE_TRY(wait_ge(st, P.data_flag(c->rank, ch, from), s));
     if (n) KLE_HIP(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
     return post(st, P.ack_flag(from, ch, c->rank), s);
@@ -208,16 +246,15 @@ int ipc_halo(kle_ctx *c, double *base, int64_t ghost_lo, int64_t n_local, int64_
                 ghost_hi <= IPC_HALO_CAP,
             "halo of %lld entries exceeds the IPC slot",
             (long long)std::max(std::max(send_lo, send_hi), std::max(ghost_lo, ghost_hi)));
-    const uint64_t s = ++P.seq[CH_FWD_LO];
     double *own = base + ghost_lo;
     // my lowest entries are the lower neighbour's upper ghosts (its FWD_HI
     // slot), my highest the upper neighbour's lower ghosts (its FWD_LO)
-    if (lo_rank >= 0) KLE_TRY(ipc_send(c, CH_FWD_HI, lo_rank, own, send_lo, P.slot(lo_rank, CH_FWD_HI), s, st));
+    if (lo_rank >= 0) KLE_TRY(ipc_send(c, CH_FWD_HI, lo_rank, own, send_lo, P.slot(lo_rank, CH_FWD_HI), st));
     if (hi_rank >= 0)
-        KLE_TRY(ipc_send(c, CH_FWD_LO, hi_rank, own + n_local - send_hi, send_hi, P.slot(hi_rank, CH_FWD_LO), s, st));
-    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_FWD_LO, lo_rank, base, P.slot(c->rank, CH_FWD_LO), ghost_lo, s, st));
+        KLE_TRY(ipc_send(c, CH_FWD_LO, hi_rank, own + n_local - send_hi, send_hi, P.slot(hi_rank, CH_FWD_LO), st));
+    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_FWD_LO, lo_rank, base, P.slot(c->rank, CH_FWD_LO), ghost_lo, st));
     if (hi_rank >= 0)
-        KLE_TRY(ipc_recv(c, CH_FWD_HI, hi_rank, own + n_local, P.slot(c->rank, CH_FWD_HI), ghost_hi, s, st));
+        KLE_TRY(ipc_recv(c, CH_FWD_HI, hi_rank, own + n_local, P.slot(c->rank, CH_FWD_HI), ghost_hi, st));
     std::vector<int> pr;
     if (lo_rank >= 0) pr.push_back(lo_rank);
     if (hi_rank >= 0) pr.push_back(hi_rank);
@@ -230,9 +267,8 @@ int ipc_reverse(kle_ctx *c, const double *send_hi, int64_t n_send, int hi_rank, 
     IpcState &P = *c->ipc;
     KLE_ARG(n_send <= IPC_HALO_CAP && n_recv <= IPC_HALO_CAP, "reverse halo of %lld entries exceeds the IPC slot",
             (long long)std::max(n_send, n_recv));
-    const uint64_t s = ++P.seq[CH_REV_LO];
-    if (hi_rank >= 0) KLE_TRY(ipc_send(c, CH_REV_LO, hi_rank, send_hi, n_send, P.slot(hi_rank, CH_REV_LO), s, st));
-    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_REV_LO, lo_rank, recv_lo, P.slot(c->rank, CH_REV_LO), n_recv, s, st));
+    if (hi_rank >= 0) KLE_TRY(ipc_send(c, CH_REV_LO, hi_rank, send_hi, n_send, P.slot(hi_rank, CH_REV_LO), st));
+    if (lo_rank >= 0) KLE_TRY(ipc_recv(c, CH_REV_LO, lo_rank, recv_lo, P.slot(c->rank, CH_REV_LO), n_recv, st));
     std::vector<int> pr;
     if (lo_rank >= 0) pr.push_back(lo_rank);
     if (hi_rank >= 0) pr.push_back(hi_rank);
@@ -251,16 +287,14 @@ int ipc_halo_plan(kle_ctx *c, double *base, const HaloPlan &H, int bs, const dou
         KLE_ARG(H.send_cnt[k] * bs <= IPC_PLAN_CAP && H.recv_cnt[k] * bs <= IPC_PLAN_CAP,
                 "graph halo of %lld entries (rank %d) exceeds the IPC slot",
                 (long long)(std::max(H.send_cnt[k], H.recv_cnt[k]) * bs), H.peers[k]);
-    const uint64_t s = ++P.seq[CH_PFWD];
     const int me = c->rank;
     for (size_t k = 0; k < np; ++k) {
         const int q = H.peers[k];
-        KLE_TRY(ipc_send(c, CH_PFWD, q, sbuf + H.send_off[k] * bs, H.send_cnt[k] * bs, P.plan_slot(q, CH_PFWD, me), s,
-                         st));
+        KLE_TRY(ipc_send(c, CH_PFWD, q, sbuf + H.send_off[k] * bs, H.send_cnt[k] * bs, P.plan_slot(q, CH_PFWD, me), st));
     }
     for (size_t k = 0; k < np; ++k) {
         const int q = H.peers[k];
-        KLE_TRY(ipc_recv(c, CH_PFWD, q, base + H.recv_off[k] * bs, P.plan_slot(me, CH_PFWD, q), H.recv_cnt[k] * bs, s,
+        KLE_TRY(ipc_recv(c, CH_PFWD, q, base + H.recv_off[k] * bs, P.plan_slot(me, CH_PFWD, q), H.recv_cnt[k] * bs,
                          st));
     }
     return ipc_done(c, st, CH_PFWD, H.peers);
@@ -279,18 +313,17 @@ int ipc_reverse_plan(kle_ctx *c, const HaloPlan &H, int64_t hi0, int bs, const d
         KLE_ARG(H.send_cnt[k] * bs <= IPC_PLAN_CAP && H.recv_cnt[k] * bs <= IPC_PLAN_CAP,
                 "reverse graph halo of %lld entries (rank %d) exceeds the IPC slot",
                 (long long)(std::max(H.send_cnt[k], H.recv_cnt[k]) * bs), H.peers[k]);
-    const uint64_t s = ++P.seq[CH_PREV];
     for (size_t k = 0; k < np; ++k) {
         const int q = H.peers[k];
         if (q > me)
             KLE_TRY(ipc_send(c, CH_PREV, q, gsend + (H.recv_off[k] - hi0) * bs, H.recv_cnt[k] * bs,
-                             P.plan_slot(q, CH_PREV, me), s, st));
+                             P.plan_slot(q, CH_PREV, me), st));
     }
     for (size_t k = 0; k < np; ++k) {
         const int q = H.peers[k];
         if (q < me)
             KLE_TRY(ipc_recv(c, CH_PREV, q, rbuf + H.send_off[k] * bs, P.plan_slot(me, CH_PREV, q), H.send_cnt[k] * bs,
-                             s, st));
+                             st));
     }
     return ipc_done(c, st, CH_PREV, H.peers);
 }
@@ -299,23 +332,23 @@ int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st)
 {
     IpcState &P = *c->ipc;
     KLE_ARG(n <= IPC_AR_CAP, "allreduce of %d doubles exceeds the IPC slot", n);
-    const uint64_t s = ++P.seq[CH_AR];
     const int me = c->rank;
     std::vector<int> pr;
     for (int q = 0; q < c->nranks; ++q)
         if (q != me) {
             pr.push_back(q);
+            const uint64_t s = ++P.sseq[CH_AR][q];
             KLE_TRY(wait_ge(st, P.ack_flag(me, CH_AR, q), s - 1));
             KLE_HIP(hipMemcpyAsync(P.ar_slot(q, me), dbuf, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
             KLE_TRY(post(st, P.data_flag(q, CH_AR, me), s));
         }
     for (int q = 0; q < c->nranks; ++q)
-        if (q != me) KLE_TRY(wait_ge(st, P.data_flag(me, CH_AR, q), s));
+        if (q != me) KLE_TRY(wait_ge(st, P.data_flag(me, CH_AR, q), ++P.rseq[CH_AR][q]));
     hipLaunchKernelGGL(k_rank_sum, dim3((unsigned)std::max(1, std::min(64, (n + 255) / 256))), dim3(256), 0, st,
                        (int64_t)n, c->nranks, me, P.region(me, CH_AR), IPC_AR_CAP, dbuf);
     KLE_HIP(hipGetLastError());
     for (int q = 0; q < c->nranks; ++q)
-        if (q != me) KLE_TRY(post(st, P.ack_flag(q, CH_AR, me), s));
+        if (q != me) KLE_TRY(post(st, P.ack_flag(q, CH_AR, me), P.rseq[CH_AR][q]));
     return ipc_done(c, st, CH_AR, pr);
 }
 
@@ -409,25 +442,30 @@ int kle_ctx_enable_ipc(kle_ctx *c)
         }
     }
     // all-gather of the handles over the host callbacks: one byte per
-    // double, one-hot sums (exact), plus every rank's failure flag
-    const int hb = (int)sizeof(hipIpcMemHandle_t);
-    std::vector<double> buf((size_t)c->nranks * (hb + 1), 0.0);
+    // double, one-hot sums (exact), plus every rank's failure flag and pid
+    const int hb = (int)sizeof(hipIpcMemHandle_t), hs = hb + 2;
+    std::vector<double> buf((size_t)c->nranks * hs, 0.0);
     const unsigned char *hpb = reinterpret_cast<const unsigned char *>(&h);
-    for (int k = 0; k < hb; ++k) buf[(size_t)c->rank * (hb + 1) + k] = hpb[k];
-    buf[(size_t)c->rank * (hb + 1) + hb] = bad;
+    for (int k = 0; k < hb; ++k) buf[(size_t)c->rank * hs + k] = hpb[k];
+    buf[(size_t)c->rank * hs + hb] = bad;
+    buf[(size_t)c->rank * hs + hb + 1] = (double)getpid();
     if (c->hcomm.allreduce(buf.data(), (int)buf.size(), c->hcomm.user)) {
         ipc_free(P, c->rank, true);
         return fail(KLE_ERR_COMM, "IPC bootstrap: host allreduce failed");
     }
     int any_bad = 0;
-    for (int r = 0; r < c->nranks; ++r) any_bad |= buf[(size_t)r * (hb + 1) + hb] != 0.0;
+    P->pid.assign(c->nranks, 0);
+    for (int r = 0; r < c->nranks; ++r) {
+        any_bad |= buf[(size_t)r * hs + hb] != 0.0;
+        P->pid[r] = (long)buf[(size_t)r * hs + hb + 1];
+    }
     P->peer.assign(c->nranks, nullptr);
     P->peer[c->rank] = P->local;
     for (int r = 0; r < c->nranks && !any_bad; ++r) {
         if (r == c->rank) continue;
         hipIpcMemHandle_t ph{};
         unsigned char *pp = reinterpret_cast<unsigned char *>(&ph);
-        for (int k = 0; k < hb; ++k) pp[k] = (unsigned char)buf[(size_t)r * (hb + 1) + k];
+        for (int k = 0; k < hb; ++k) pp[k] = (unsigned char)buf[(size_t)r * hs + k];
         void *m = nullptr;
         if (hipIpcOpenMemHandle(&m, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
             (void)hipGetLastError();

@@ -830,6 +830,7 @@ struct kle_ksp {
     double rnorm = 0, true_rel = -1;
     int max_corr = g_tune.ksp_refine;  // correction solves on a missed true residual (refine)
     int corr_its = 0;                  // iterations of the last solve's corrections
+    int corr_reason = 0;               // converged reason of the last correction (0: none ran)
     // single-rank CG: `check_every` iterations captured as one hipGraph,
     // replayed until the device reason word stops the kernels; valid for the
     // (b, x) pair it was captured with
@@ -1673,32 +1674,38 @@ int kle_ksp_set_up(kle_ksp *k)
 // (same method, zero start) and x += e bring it under; at most k->max_corr
 // such passes (default 2: kle_set_tuning("ksp_refine") / KLE_KSP_REFINE for
 // new KSPs, kle_ksp_set_corrections per KSP).  0 is PETSc's KSPCG/KSPPIPECG
-// exactly: stop on the recursive residual whatever the true one.  The
-// correction iterations add to the iteration count;
-// kle_ksp_get_correction_iterations reports them.
+// exactly: stop on the recursive residual whatever the true one.  The main
+// solve's converged reason, iteration count and residual norm stand as PETSc
+// reports them (a correction that runs out of iterations does not turn a
+// converged solve into DIVERGED_ITS); the corrections are reported apart:
+// kle_ksp_get_correction_iterations / _reason.  Each correction has the
+// KSP's max_it of its own.
 static int refine(kle_ksp *k, kle_vec *b, kle_vec *x)
 {
     k->corr_its = 0;
+    k->corr_reason = 0;
     if (k->max_corr <= 0 || (k->type != "pipecg" && k->type != "cg") || k->pc == "lu") return 0;
     kle_ctx *c = k->ctx;
+    const int reason0 = k->reason, its_main = k->its;
+    const double rnorm0 = k->rnorm;
     for (int pass = 0; pass < k->max_corr; ++pass) {
-        if (k->reason <= 0 || !(k->true_rel > k->rtol) || k->its >= k->maxit) return 0;
+        if (reason0 <= 0 || k->corr_reason < 0 || !(k->true_rel > k->rtol)) return 0;
         kle_vec *rv = nullptr, *e = nullptr;
         int rc = vec_alloc(c, b->n_local, b->n_global, b->lo, 0, 0, &rv);
         if (!rc) rc = vec_alloc(c, x->n_local, x->n_global, x->lo, 0, 0, &e);
         const double rtol0 = k->rtol;
-        const int its0 = k->its, maxit0 = k->maxit;
         if (!rc) rc = kle_vec_copy(k->q, rv);
         if (!rc) {
             k->rtol = 0.5 * rtol0 / k->true_rel;  // (relative to ||r|| = true_rel ||b||)
-            k->maxit = maxit0 - its0;
             rc = k->type == "pipecg" ? solve_pipecg(k, rv, e, false)
                  : k->single_reduction ? solve_cg_single(k, rv, e, false)
                                        : solve_cg(k, rv, e);
             k->rtol = rtol0;
-            k->maxit = maxit0;
             k->corr_its += k->its;
-            k->its += its0;
+            k->corr_reason = k->reason;
+            k->its = its_main;
+            k->reason = reason0;
+            k->rnorm = rnorm0;
         }
         if (!rc) rc = kle_vec_axpy(x, 1.0, e);
         for (kle_vec *v : {rv, e})
@@ -1783,6 +1790,13 @@ int kle_ksp_get_correction_iterations(const kle_ksp *k, int *its)
 {
     KLE_ARG(k && its, "null arg");
     *its = k->corr_its;
+    return 0;
+}
+
+int kle_ksp_get_correction_reason(const kle_ksp *k, int *reason)
+{
+    KLE_ARG(k && reason, "null arg");
+    *reason = k->corr_reason;
     return 0;
 }
 

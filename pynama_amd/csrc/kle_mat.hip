@@ -101,7 +101,9 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
                                                         const double *__restrict__ x, double *__restrict__ y,
                                                         const int *__restrict__ istate, int xcd_chunk)
 {
-    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
+    // the solve has ended (reason word set): every kernel a no-op.  Loaded
+    // with the row's descriptors and tested before its value loads.
+    const int stop = istate ? istate[I_REASON] : 0;
     constexpr int RC = R * C;
     const int lane = threadIdx.x & 63;
     const int64_t blk = xcd_block(xcd_chunk);
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     const int64_t i = r < rm.na ? rm.a0 + r : rm.b0 + (r - rm.na);
     const int b0 = rowptr[i], mp = rowptr[i + 1] - b0, m = rowcnt ? rowcnt[i] : mp;
     const double *v = val + vptr[i];
+    if (stop) return;
     int bbase = 0, bnx = 1, bnxy = 1;
     if constexpr (STRUCT) {
         bbase = rowbox[2 * i];
@@ -165,7 +168,6 @@ __global__ __launch_bounds__(64 * WV, (R * C <= 9 ? 8 : 4)) void k_nb_spmv(RowMa
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane < R) {
         double mine = acc[0];
 #pragma unroll
@@ -203,7 +205,9 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
     constexpr int R = 3, C = 3, RC = 9;
     extern __shared__ double xs[];
     __shared__ int ub[WV][6];
-    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
+    // the solve has ended (reason word set): every kernel a no-op.  Loaded
+    // with the row's descriptors and tested before its value loads.
+    const int stop = istate ? istate[I_REASON] : 0;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t blk = xcd_block(xcd_chunk);
     const int64_t nr = rm.na + rm.nb;
@@ -223,6 +227,7 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
         bny = (d >> 8) & 255;
         bnz = (d >> 16) & 255;
     }
+    if (stop) return;  // (uniform: whole workgroup)
     const int cz = bbase / lxy, cy = (bbase - cz * lxy) / lx, cx = bbase - cz * lxy - cy * lx;
     if (lane == 0) {
         ub[w][0] = live ? cx : INT_MAX;
@@ -305,7 +310,6 @@ __global__ __launch_bounds__(64 * WV, 8) void k_nb_spmv_xl(RowMap rm, const int 
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane < R) {
         double mine = acc[0];
 #pragma unroll
@@ -343,7 +347,9 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
 {
     constexpr int R = 3, C = 3, RC = 9;
     extern __shared__ double xs[];
-    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
+    // the solve has ended (reason word set): every kernel a no-op.  Loaded
+    // with the row's descriptors and tested before its value loads.
+    const int stop = istate ? istate[I_REASON] : 0;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t blk = xcd_block(xcd_chunk);
     if (blk >= nga + ngb) return;  // whole workgroup
@@ -353,6 +359,7 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     const int64_t i = g * DICT_GROUP + w;
     const bool live = i >= lo && i < hi;
     const int d0 = dptr[g], U = dptr[g + 1] - d0;
+    if (stop) return;  // (uniform: whole workgroup)
     const bool lds_x = U <= DICT_CAP;
     if (lds_x)
         for (int t = threadIdx.x; t < 3 * U; t += 64 * DICT_GROUP) {
@@ -396,7 +403,6 @@ __global__ __launch_bounds__(64 * DICT_GROUP, 8) void k_nb_spmv_dict(
     for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc[a] += __shfl_xor(acc[a], o, 64);
-    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane < R) {
         double mine = acc[0];
 #pragma unroll
@@ -420,11 +426,14 @@ __global__ __launch_bounds__(64 * WV) void k_aij_spmv(int64_t nrows, const int64
                                                       const double *__restrict__ x, double *__restrict__ y,
                                                       const int *__restrict__ istate, int xcd_chunk)
 {
-    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the row's store: the load overlaps the row's)
+    // the solve has ended (reason word set): every kernel a no-op.  Loaded
+    // with the row's descriptors and tested before its value loads.
+    const int stop = istate ? istate[I_REASON] : 0;
     const int lane = threadIdx.x & 63;
     const int64_t i = xcd_block(xcd_chunk) * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (i >= nrows) return;
     const int64_t s = ptr[i], e = ptr[i + 1];
+    if (stop) return;
     double acc = 0.0;
     for (int64_t k0 = s & ~(int64_t)31; k0 < e; k0 += 64 * U) {
         int c[U];
@@ -441,7 +450,6 @@ __global__ __launch_bounds__(64 * WV) void k_aij_spmv(int64_t nrows, const int64
             if (c[u] >= 0) acc += v[u] * x[c[u]];
     }
     acc = wsum(acc);
-    if (stop) return;  // (the solve has ended: every kernel a no-op)
     if (lane == 0) y[i] = acc;
 }
 
@@ -1437,6 +1445,26 @@ int kle_mat_set_spmv_structured(kle_mat *A, int on)
 {
     KLE_ARG(A, "null matrix");
     A->spmv_struct = on != 0;
+    return 0;
+}
+
+int kle_mat_move_values(kle_mat *A, long long shift)
+{
+    using namespace kle;
+    KLE_ARG(A && A->d_sval, "no symmetric storage");
+    KLE_ARG(shift >= 0 && shift % 8 == 0 && shift <= (1ll << 30), "shift: a multiple of 8 bytes in [0, 1 GiB]");
+    const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
+    char *raw = nullptr;
+    if (hipMalloc(&raw, bytes + (size_t)shift) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(KLE_ERR_MEM, "out of device memory for the moved values (%zu bytes)", bytes + (size_t)shift);
+    }
+    double *nv = reinterpret_cast<double *>(raw + shift);
+    KLE_HIP(hipStreamSynchronize(A->ctx->stream));
+    KLE_HIP(hipMemcpy(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice));
+    KLE_HIP(hipFree(A->sval_raw ? A->sval_raw : A->d_sval));
+    A->sval_raw = raw;
+    A->d_sval = nv;
     return 0;
 }
 

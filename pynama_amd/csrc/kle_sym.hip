@@ -666,6 +666,7 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
 void sym_forget(kle_mat *A)
 {
     A->d_sval = nullptr;
+    A->sval_raw = nullptr;
     A->d_svptr = nullptr;
     A->d_sws = nullptr;
     A->d_stile_e = nullptr;
@@ -687,7 +688,7 @@ void sym_forget(kle_mat *A)
 void sym_drop(kle_mat *A)
 {
     brick_drop(A);
-    for (void *q : {(void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
+    for (void *q : {A->sval_raw ? A->sval_raw : (void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
                     (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow, (void *)A->d_sbp,
                     (void *)A->d_slid, (void *)A->d_sdptr, (void *)A->d_sdict, (void *)A->d_sgptr,
                     (void *)A->d_sgidx, (void *)A->d_sgmask, (void *)A->d_sglist, (void *)A->d_swptr})

@@ -10,7 +10,13 @@ Mirrors exactly the petsc4py subset Pynama's hot path uses:
   KSP: create, setType, setPC, setFromOptions, setOperators, setUp, solve,
        __call__(b, x)                            (kle_solver.py:49-64)
   PC:  create, setType
+  IS:  createGeneral, createBlock, union, getIndices, getBlockIndices
+                                                 (boundary_conditions.py:1,187-250)
+  COMM_WORLD.tompi4py().allgather                (boundary_conditions.py:201-271)
   Options: getString/getInt/getReal              (run_case.py:9-13)
+The surface the reference's host files use is scanned from their source
+(tools/scan_petsc4py_surface.py -> tests/golden/petsc4py_surface.json) and
+tests/test_host.py checks that every entry exists here.
 Errors raise ``Error`` (ierr = PETSc-style code).  Differences from petsc4py:
 Vec.getArray() returns a host COPY of the owned part (device memory), use
 setArray() to write back.
@@ -31,6 +37,8 @@ def _h(obj):
 
 
 def _i64(a):
+    if isinstance(a, (set, frozenset)):
+        a = sorted(a)
     return np.ascontiguousarray(np.atleast_1d(np.asarray(a, dtype=np.int64)))
 
 
@@ -414,6 +422,28 @@ class Mat:
             if e.ierr != 56:
                 raise
 
+    def isSymmetric(self, tol=0.0):
+        """MatIsSymmetric (printMatsInfo, mat_fs.py:129): |A - A^T| <= tol
+        entry by entry, over every rank's rows (collective).  Symmetric
+        storage holds one triangle: symmetric by construction."""
+        if self.isSymmetricStorage():
+            return True
+        import scipy.sparse as sp
+        from .runtime import COMM_WORLD as W
+        ip, ix, d = self.getValuesCSR()
+        lo, _ = self.getOwnershipRange()
+        rows = np.repeat(np.arange(len(ip) - 1, dtype=np.int64) + lo, np.diff(ip))
+        parts = W.allgather((rows, ix, d))
+        r = np.concatenate([p[0] for p in parts])
+        c = np.concatenate([p[1] for p in parts])
+        v = np.concatenate([p[2] for p in parts])
+        m, n = self.getSize()
+        if m != n:
+            return False
+        A = sp.csr_matrix((v, (r, c)), shape=(m, n))
+        diff = abs(A - A.T)
+        return bool(diff.nnz == 0 or diff.max() <= tol)
+
     def isSymmetricStorage(self):
         v = C.c_int()
         call("kle_mat_get_symmetric", self._h, C.byref(v))
@@ -427,6 +457,11 @@ class Mat:
         if n.value == 0:
             return None
         return {"bricks": n.value, "dims": list(dims), "region_entries_per_row": ent.value, "model_us": mus.value}
+
+    def moveValues(self, shift):
+        """Diagnostic: the symmetric storage's values to a fresh allocation,
+        `shift` bytes into it (kle_mat_move_values)."""
+        call("kle_mat_move_values", self._h, int(shift))
 
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))
@@ -556,6 +591,73 @@ class Mat:
         return ip, ix[: nz.value], d[: nz.value]
 
 
+class IS:
+    """petsc4py IS on the host: the index sets of the boundary-condition code
+    (boundary_conditions.py:187-250 -- unions of the boundaries' node / dof
+    sets, read back with getIndices / getBlockIndices).  Indices are global
+    (owned or not, as the reference's lists are); a block IS of block size bs
+    holds block indices and expands to bs * b + c."""
+
+    def __init__(self):
+        self._idx = np.zeros(0, dtype=np.int64)
+        self._bs = 1
+
+    def createGeneral(self, indices, comm=None):
+        self._idx = np.asarray(list(indices) if isinstance(indices, (set, frozenset)) else indices,
+                               dtype=np.int64).ravel()
+        self._bs = 1
+        return self
+
+    def createBlock(self, bsize, indices, comm=None):
+        if int(bsize) < 1:
+            raise Error(62, "IS block size must be >= 1")
+        self.createGeneral(indices)
+        self._bs = int(bsize)
+        return self
+
+    def createStride(self, size, first=0, step=1, comm=None):
+        return self.createGeneral(np.arange(int(size), dtype=np.int64) * int(step) + int(first))
+
+    def getBlockSize(self):
+        return self._bs
+
+    def getSize(self):
+        return len(self._idx) * self._bs
+
+    getLocalSize = getSize
+
+    def __len__(self):
+        return self.getSize()
+
+    def getIndices(self):
+        """Every index (a block IS expanded: bs * b + c, c < bs)."""
+        if self._bs == 1:
+            return self._idx.copy()
+        return (self._idx[:, None] * self._bs + np.arange(self._bs, dtype=np.int64)).ravel()
+
+    def getBlockIndices(self):
+        """The block indices (ISGetBlockIndices; a general IS: the indices)."""
+        return self._idx.copy()
+
+    @property
+    def indices(self):
+        return self.getIndices()
+
+    def union(self, iset):
+        """ISExpand (petsc4py IS.union): the sorted union without duplicates,
+        block size 1 unless both sets share theirs."""
+        out = IS()
+        if self._bs == iset._bs:
+            out.createBlock(self._bs, np.union1d(self._idx, iset._idx))
+        else:
+            out.createGeneral(np.union1d(self.getIndices(), iset.getIndices()))
+        return out
+
+    def destroy(self):
+        self._idx = np.zeros(0, dtype=np.int64)
+        return self
+
+
 class PC:
     def __init__(self):
         self._type = "jacobi"
@@ -583,6 +685,13 @@ class KSP:
         self._A = None
 
     def create(self, comm=None):
+        # (a subclass whose __init__ does not chain up -- kle_solver.py:49-53
+        # KspSolver(KSP) -- gets its defaults here, as petsc4py's does)
+        for k, v in (("_pc", None), ("_type", "cg"), ("_A", None)):
+            if not hasattr(self, k):
+                setattr(self, k, PC() if k == "_pc" else v)
+        if getattr(self, "_h", None):
+            call("kle_ksp_destroy", self._h)
         ctx = get_ctx()
         h = C.c_void_p()
         call("kle_ksp_create", ctx.h, C.byref(h))
@@ -591,7 +700,7 @@ class KSP:
         return self
 
     def _ensure(self):
-        if self._h is None:
+        if getattr(self, "_h", None) is None:
             self.create()
 
     def setType(self, t):
@@ -695,13 +804,21 @@ class KSP:
         call("kle_ksp_set_corrections", self._h, int(n))
 
     def getCorrectionIterations(self):
-        """Iterations of the last solve's correction solves (0: none ran)."""
+        """Iterations of the last solve's correction solves (0: none ran);
+        not part of getIterationNumber (PETSc's count of the main solve)."""
         v = C.c_int()
         call("kle_ksp_get_correction_iterations", self._h, C.byref(v))
         return v.value
 
+    def getCorrectionReason(self):
+        """Converged reason of the last correction solve (0: none ran); the
+        KSP's own getConvergedReason stays the main solve's."""
+        v = C.c_int()
+        call("kle_ksp_get_correction_reason", self._h, C.byref(v))
+        return v.value
+
     def destroy(self):
-        if self._h:
+        if getattr(self, "_h", None):
             call("kle_ksp_destroy", self._h)
             self._h = None
         return self
@@ -713,4 +830,4 @@ class KSP:
             pass
 
 
-__all__ = ["Mat", "Vec", "KSP", "PC", "Options", "Error", "COMM_WORLD", "INSERT_VALUES", "ADD_VALUES"]
+__all__ = ["Mat", "Vec", "KSP", "PC", "IS", "Options", "Error", "COMM_WORLD", "INSERT_VALUES", "ADD_VALUES"]

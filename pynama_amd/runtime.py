@@ -35,7 +35,11 @@ def world():
 
 
 class Comm:
-    """petsc4py COMM_WORLD stand-in (rank / size only)."""
+    """petsc4py COMM_WORLD stand-in: rank / size, and tompi4py() -> the same
+    object with the mpi4py calls the reference's host code makes on it
+    (allgather of Python objects, boundary_conditions.py:201,221,233,271),
+    over torch.distributed (gloo / RCCL process group) when one is
+    initialised, else a one-rank world."""
 
     @property
     def rank(self):
@@ -45,8 +49,32 @@ class Comm:
     def size(self):
         return world()[1]
 
+    def Get_rank(self):
+        return self.rank
+
+    def Get_size(self):
+        return self.size
+
     def tompi4py(self):
         return self
+
+    def allgather(self, obj):
+        """mpi4py Comm.allgather: every rank's obj, in rank order."""
+        d = _dist()
+        if d is None or d.get_world_size() == 1:
+            return [obj]
+        out = [None] * d.get_world_size()
+        d.all_gather_object(out, obj)
+        return out
+
+    def bcast(self, obj, root=0):
+        """mpi4py Comm.bcast: root's obj on every rank."""
+        d = _dist()
+        if d is None or d.get_world_size() == 1:
+            return obj
+        box = [obj if d.get_rank() == root else None]
+        d.broadcast_object_list(box, src=root)
+        return box[0]
 
     def barrier(self):
         ctx = get_ctx()

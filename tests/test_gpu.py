@@ -172,9 +172,57 @@ def test_cg_iterations_match_oracle(pa, case, single):
     ksp.solve(b, x)
     # pipelined CG: same iterates in exact arithmetic, recurrences drift more in fp64
     tol_its = {False: 1, True: 2, "pipecg": 4}[single]
-    assert abs(ksp.getIterationNumber() - ksp.getCorrectionIterations() - it_o) <= tol_its
+    assert abs(ksp.getIterationNumber() - it_o) <= tol_its
     assert ksp.getTrueRelativeResidual() <= 1.01e-10  # (default correction solve: the true residual meets rtol)
     assert np.linalg.norm(x.getArray() - xo) <= 1e-7 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("typ", ["cg", "pipecg"])
+def test_correction_keeps_main_reason_near_maxit(pa, typ):
+    """A solve that converges on its recursive residual at exactly max_it
+    stays CONVERGED_RTOL with PETSc's iteration count (KSPGetIterationNumber
+    of the recurrence), whatever the correction solve does afterwards; the
+    correction's iterations and reason are reported apart."""
+    g = _golden("tg3d_p4")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    b = mat.K.createVecLeft()
+    b.setArray(g["b"])
+
+    def solve(maxit, corr):
+        ksp = pa.petsc.KSP().create()
+        ksp.setType(typ)
+        pc = pa.petsc.PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=maxit)
+        ksp.setCorrections(corr)
+        ksp.setOperators(mat.K)
+        x = mat.K.createVecRight()
+        ksp.solve(b, x)
+        return ksp
+
+    plain = solve(10000, 0)
+    n = plain.getIterationNumber()
+    assert plain.getConvergedReason() > 0 and plain.getCorrectionIterations() == 0
+    assert plain.getCorrectionReason() == 0
+    for corr in (2, 1):
+        k = solve(n, corr)  # (converges at the last allowed iteration)
+        assert k.getConvergedReason() == plain.getConvergedReason()
+        assert k.getIterationNumber() == n
+        assert k.getResidualNorm() == plain.getResidualNorm()
+        if k.getCorrectionIterations():
+            assert k.getCorrectionReason() != 0
+            if k.getCorrectionReason() > 0:
+                assert k.getTrueRelativeResidual() <= 1.01e-10
+        else:
+            assert plain.getTrueRelativeResidual() <= 1e-10
+    # one iteration short: DIVERGED_ITS from the main solve, no correction runs
+    k = solve(n - 1, 2)
+    assert k.getConvergedReason() < 0 and k.getIterationNumber() == n - 1
+    assert k.getCorrectionIterations() == 0 and k.getCorrectionReason() == 0
 
 
 def test_gmres_and_aij(pa):

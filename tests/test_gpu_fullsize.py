@@ -93,7 +93,7 @@ def test_config2_full_size_matches_oracle(pa):
     sol.solve(vort)
     assert ksp.getConvergedReason() > 0
     u_dev = vel.getArray().copy()
-    its_dev = ksp.getIterationNumber() - ksp.getCorrectionIterations()
+    its_dev = ksp.getIterationNumber()
     _log(t0, f"device CG: {its_dev} iterations, device true residual {ksp.getTrueRelativeResidual():.3e}")
 
     # ---- the box symmetric SpMV on bricks (default, one rank): its plan, and
@@ -103,7 +103,7 @@ def test_config2_full_size_matches_oracle(pa):
     K = mat.K
     assert K.isSymmetricStorage() and K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
     bk = K.getSymmetricBricks()
-    assert bk["bricks"] == bk["dims"][0] * bk["dims"][1] * bk["dims"][2] and 0 < bk["bricks"] <= 256, bk
+    assert 0 < bk["bricks"] <= 256 and min(bk["dims"]) >= 1 and bk["region_entries_per_row"] < 2.5, bk
     _log(t0, f"bricks: {bk}")
     y1 = (K * vel).getArray().copy()
     np.testing.assert_array_equal((K * vel).getArray(), y1)
@@ -117,7 +117,39 @@ def test_config2_full_size_matches_oracle(pa):
         set_tuning("spmv_sym_brick", 1)
         K.setOption(K.Option.SPD, True)
     np.testing.assert_array_equal((K * vel).getArray(), y1)
-    del y1, yt
+    del yt
+    # ---- where the value array lies does not set the speed (VERDICT r04
+    # item 1: the 128-row tiles' mid-stream partial stores made the product
+    # bimodal over placements, 424-491 us, profiles/r04/ab/values_placement.jsonl).
+    # The same offsets, twice each in turn; each placement's faster pass of 20
+    # products (box noise between passes is not the placement's); <= 3 % spread.
+    # (Offsets are multiples of the 128-B cache line, as every allocation is:
+    # a base 64 B off the line splits each 16-block chunk load over two lines
+    # and cost 16 %, 479 vs 413 us, in the r05 run of this test.)
+    from pynama_amd.runtime import get_ctx
+    ctx = get_ctx()
+    yv = K.createVecLeft()
+    offsets = [0, 256, 4096, 65536, 1 << 20, 2101248, 0, (3 << 20) + 384]
+    times = {}
+    for _ in range(2):
+        for k, off in enumerate(offsets):
+            K.moveValues(off)
+            K.mult(vel, yv)
+            np.testing.assert_array_equal(yv.getArray(), y1)
+            ctx.synchronize()
+            ctx.set_profiling(True, only="spmv")
+            ctx.reset_stats()
+            for _ in range(20):
+                K.mult(vel, yv)
+            ctx.synchronize()
+            c, ms = ctx.kernel_stats("spmv")
+            ctx.set_profiling(False)
+            times.setdefault(k, []).append(1e3 * ms / c)
+    best = [min(v) for v in times.values()]
+    spread = (max(best) - min(best)) / min(best)
+    _log(t0, f"value placements {offsets}: SpMV {[round(b, 1) for b in best]} us, spread {spread:.3f}")
+    assert spread <= 0.03, (best, spread)
+    del y1, yv
 
     # ---- oracle assembly (mat_fs.py:131-192)
     Ko, Kro, Rwo = om.assemble_fs(on_bd.astype(np.uint8))
@@ -204,7 +236,7 @@ def test_unstructured_full_size_dictionary_spmv_is_bitwise(pa, tmp_path):
     sol.solve(vort)
     assert ksp.getConvergedReason() > 0
     assert ksp.getTrueRelativeResidual() <= 1.05e-10
-    assert abs(ksp.getIterationNumber() - ksp.getCorrectionIterations() - 891) <= 4
+    assert abs(ksp.getIterationNumber() - 891) <= 4
     _log(t0, f"solve: {ksp.getIterationNumber()} iterations")
 
 

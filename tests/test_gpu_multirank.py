@@ -344,15 +344,20 @@ def test_partitioned_umesh_ipc_transport(size, nel, ksp_type, sym, tmp_path):
         np.testing.assert_array_equal(a["y"], b["y"])
 
 
-def _stall_worker(rank, size, port, q):
+def _stall_worker(rank, size, port, q, mode="stall"):
     """Rank 1 builds the system like its peers and then stops calling the
-    collectives (sleeps); rank 0 runs a product whose halo waits for rank 1."""
+    collectives: "stall" sleeps (alive) under KLE_COMM_TIMEOUT_S=4, "die"
+    exits at once with no timeout set, "slow" does 6 s of host-only work and
+    then its product.  Rank 0 runs a product whose halo waits for rank 1."""
     import sys
     import time
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="ipc",
-                      RANK=str(rank), WORLD_SIZE=str(size), KLE_COMM_TIMEOUT_S="4",
-                      KLE_SPMV_SYM_MIN_ROWS=str(1 << 30))
+                      RANK=str(rank), WORLD_SIZE=str(size), KLE_SPMV_SYM_MIN_ROWS=str(1 << 30))
+    if mode == "stall":
+        os.environ["KLE_COMM_TIMEOUT_S"] = "4"
+    else:
+        os.environ.pop("KLE_COMM_TIMEOUT_S", None)
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=size)
     import pynama_amd as pa
@@ -367,29 +372,37 @@ def _stall_worker(rank, size, port, q):
     x = mat.K.createVecRight()
     x.set(1.0)
     y = mat.K * x  # one halo that completes on both ranks
-    q.put({"rank": rank, "first": float(y.norm())})
+    first = float(y.norm())
+    q.put({"rank": rank, "first": first})
     dist.barrier()
     if rank == 1:
-        time.sleep(40)  # alive, mailbox mapped, but no more collectives
-        os._exit(0)
+        if mode == "stall":
+            time.sleep(40)  # alive, mailbox mapped, but no more collectives
+            os._exit(0)
+        if mode == "die":
+            os._exit(0)
+        time.sleep(6)  # host-only work, then the collective after all
     t0 = time.time()
-    y = mat.K * x  # its halo waits for rank 1's delivery: the watchdog ends the process
+    y = mat.K * x  # its halo waits for rank 1's delivery
     y.getArray()
-    q.put({"rank": rank, "returned_after": time.time() - t0})
+    q.put({"rank": rank, "returned_after": time.time() - t0, "same": float(y.norm()) == first})
+    dist.barrier()
 
 
-def test_ipc_watchdog_ends_a_rank_whose_peer_stops():
+@pytest.mark.parametrize("mode", ["stall", "die"])
+def test_ipc_watchdog_ends_a_rank_whose_peer_stops(mode):
     """A peer that stops calling the collectives leaves this rank's stream
-    waiting on a mailbox flag; the IPC watchdog sees its progress word stall
-    for KLE_COMM_TIMEOUT_S and ends the process with status 75 instead of
-    letting it hang (kle_ipc.hip ipc_watchdog)."""
+    waiting on a mailbox flag.  The IPC watchdog (kle_ipc.hip ipc_watchdog)
+    ends the process with status 75 instead of letting it hang: at once when
+    the awaited peer's process has exited (no timeout needed), after
+    KLE_COMM_TIMEOUT_S when one is set and the peer is alive but silent."""
     import time
 
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -408,6 +421,103 @@ def test_ipc_watchdog_ends_a_rank_whose_peer_stops():
             p.join(timeout=30)
 
 
+def test_ipc_watchdog_spares_a_slow_live_peer():
+    """No KLE_COMM_TIMEOUT_S: a live peer that spends 6 s on host-only work
+    between collectives is waited for (operations have no timeout,
+    as with NCCL); both ranks finish with the same product."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, q, "slow")) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=150) for _ in range(4)]
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    late = [r for r in res if "returned_after" in r]
+    assert len(late) == 2 and all(r["same"] for r in late), late
+    assert max(r["returned_after"] for r in late) >= 4.0
+    assert [p.exitcode for p in procs] == [0, 0]
+
+
+def _pair_worker(rank, size, port, msh_a, msh_b, q):
+    """Two meshes on one IPC context: in the first the last rank owns a box
+    of its own (a halo plan with no peers) while the others exchange; in the
+    second every rank has peers.  Per-pair sequence counters keep the second
+    mesh's exchanges in step (a shared per-channel counter left the isolated
+    rank behind its new peer: a hang)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KLE_TRANSPORT="ipc",
+                      RANK=str(rank), WORLD_SIZE=str(size), KLE_COMM_TIMEOUT_S="30")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        import pynama_amd as pa
+        out = {"rank": rank}
+        for key, msh in (("a", msh_a), ("b", msh_b)):
+            cfg = {"domain": {"ngl": 3, "gmsh-file": msh, "partitioner": "inertial"},
+                   "boundary-conditions": {"custom-func": {"name": "taylor_green3d"}}}
+            dom = pa.Domain()
+            dom.configure(cfg)
+            dom.setUp()
+            mat = pa.MatFS()
+            mat.setDomain(dom)
+            mat.build()
+            ksp = pa.petsc.KSP().create()
+            ksp.setType("cg")
+            pc = pa.petsc.PC()
+            pc.setType("jacobi")
+            ksp.setPC(pc)
+            ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=5000)
+            ksp.setOperators(mat.K)
+            b = mat.K.createVecLeft()
+            lo, hi = b.getOwnershipRange()
+            b.setArray(np.cos(np.arange(lo, hi, dtype=np.float64)))
+            x = mat.K.createVecRight()
+            ksp.solve(b, x)
+            out[key] = {"npeers": len(dom.mesh.peers()), "reason": ksp.getConvergedReason(),
+                        "true": ksp.getTrueRelativeResidual()}
+        q.put(out)
+    except Exception:
+        import traceback
+        q.put({"rank": rank, "error": traceback.format_exc()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ipc_rank_without_peers_then_with_peers(tmp_path):
+    import torch.multiprocessing as mp
+    from pynama_amd.meshgen import perturbed_box, write_gmsh
+    # mesh a: a 4 x 2 x 2 box on x in [0, 2] (ranks 0, 1) and, apart, a
+    # 2 x 2 x 2 box on x in [3, 4] (rank 2); mesh b: one 6 x 2 x 2 box
+    V1, C1, F1, T1 = perturbed_box(3, [4, 2, 2], lower=[0, 0, 0], upper=[2, 1, 1], seed=3, rotate=False,
+                                   shuffle=False)
+    V2, C2, F2, T2 = perturbed_box(3, [2, 2, 2], lower=[3, 0, 0], upper=[4, 1, 1], seed=4, rotate=False,
+                                   shuffle=False)
+    n1 = len(V1)
+    write_gmsh(tmp_path / "a.msh", 3, np.vstack([V1, V2]), np.vstack([C1, C2 + n1]), np.vstack([F1, F2 + n1]),
+               np.concatenate([T1, T2]))
+    write_gmsh(tmp_path / "b.msh", 3, *perturbed_box(3, [6, 2, 2], upper=[3, 1, 1], seed=5))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pair_worker, args=(r, 3, port, str(tmp_path / "a.msh"), str(tmp_path / "b.msh"), q))
+             for r in range(3)]
+    res = _collect(procs, q, 3, timeout=150)
+    assert [r["a"]["npeers"] for r in res] == [1, 1, 0], res
+    assert all(r["b"]["npeers"] >= 1 for r in res), res
+    for r in res:
+        for key in ("a", "b"):
+            assert r[key]["reason"] > 0 and r[key]["true"] <= 1.01e-10, (r["rank"], key, r[key])
+
+
 def test_pipecg_correction_is_default_and_optional(tmp_path):
     """The pipelined CG's true residual drifts above rtol on its recursive
     stop; by default libkle's correction solve (kle_ksp.hip refine) brings it
@@ -422,7 +532,7 @@ def test_pipecg_correction_is_default_and_optional(tmp_path):
     finally:
         del os.environ["KLE_KSP_REFINE"]
     for p_, r in zip(plain, res):
-        assert p_["corr"] == 0 and p_["its"] == r["its"] - r["corr"]
+        assert p_["corr"] == 0 and p_["its"] == r["its"]  # (corrections reported apart)
         assert p_["true"] < 1e-10
 
 

@@ -231,3 +231,111 @@ def test_bench_refuses_a_stale_pmc_record(tmp_path):
             t, _ = bench.lookup_traffic(os.path.join(ROOT, "profiles", "traffic.json"), key, rec["kernel"],
                                         rec["algorithmic_bytes_per_launch"])
             assert t == rec["hbm_bytes_per_launch"]
+
+
+def test_petsc4py_surface_of_the_reference_host_files():
+    """Every petsc4py class, method, operator and import the reference's host
+    files on the path use (mat_fs.py, mat_ns.py, kle_solver.py,
+    base_problem.py:111-222, boundary_conditions.py:1,191-278; scanned from
+    their source by tools/scan_petsc4py_surface.py into
+    tests/golden/petsc4py_surface.json) exists in pynama_amd.petsc / its
+    COMM_WORLD.  tests/test_gpu_petsc_surface.py calls them the reference's way."""
+    import json
+    import pynama_amd.petsc as P
+    from pynama_amd.runtime import COMM_WORLD
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "petsc4py_surface.json")))
+    assert d["unclassified"] == []
+    assert len(d["entries"]) >= 50
+    dunder = {"__mul__", "__add__", "__sub__", "__imul__", "__call__"}
+    missing = []
+    for e in d["entries"]:
+        c, m = e["class"], e["member"]
+        if c == "module":
+            ok = m == "PETSc" or hasattr(P, m)
+        elif c == "Comm":
+            ok = hasattr(COMM_WORLD, m)
+        elif c == "mpi4py.Comm":
+            ok = hasattr(COMM_WORLD.tompi4py(), m)
+        elif m in ("__init__", "__subclass__"):
+            ok = isinstance(getattr(P, c, None), type)
+        else:
+            ok = callable(getattr(getattr(P, c, None), m, None)) or (m in dunder and hasattr(getattr(P, c), m))
+        if not ok:
+            missing.append(f"{c}.{m} ({e['sites'][0]})")
+    assert not missing, missing
+    # the keyword / argument forms the shim's signatures must take
+    import inspect
+    forms = {f"{e['class']}.{e['member']}": e["forms"] for e in d["entries"]}
+    for key, kw in (("Mat.createAIJ", {"nnz", "comm"}), ("Mat.diagonalScale", {"L"}), ("Vec.createMPI", {"comm"}),
+                    ("Vec.setValues", {"addv"}), ("Mat.setValues", {"addv"})):
+        cls, meth = key.split(".")
+        params = set(inspect.signature(getattr(getattr(P, cls), meth)).parameters)
+        used = {k for f in forms[key] for k in f["kwargs"]}
+        assert used <= kw and kw <= params, (key, used, params)
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference sources not present")
+def test_petsc4py_surface_fixture_is_current(tmp_path):
+    """The committed surface is what the scanner reads from the reference now."""
+    import json
+    import subprocess
+    import sys
+    out = tmp_path / "s.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scan_petsc4py_surface.py"), "--out", str(out)],
+                   check=True, capture_output=True)
+    assert json.load(open(out)) == json.load(open(os.path.join(ROOT, "tests", "golden", "petsc4py_surface.json")))
+
+
+def test_index_sets_and_allgather_as_the_boundary_code_uses_them():
+    """IS and COMM_WORLD.tompi4py().allgather the way boundary_conditions.py
+    does (187-250): unions of boundary index sets from an empty general IS,
+    block indices of a block IS, allgather of Python sets on one rank."""
+    from pynama_amd.petsc import IS
+    from pynama_amd.runtime import COMM_WORLD
+    a = IS().createBlock(3, [4, 1, 7])
+    assert list(a.getBlockIndices()) == [4, 1, 7]
+    assert list(a.getIndices()) == [12, 13, 14, 3, 4, 5, 21, 22, 23]
+    inds = IS().createGeneral([])
+    for bc in (IS().createGeneral([5, 2, 9]), IS().createGeneral([2, 11]), IS().createGeneral({9, 0})):
+        inds = bc.union(inds)
+    assert set(inds.getIndices()) == {0, 2, 5, 9, 11} and list(inds.getIndices()) == [0, 2, 5, 9, 11]
+    assert list(IS().createBlock(3, [1]).union(IS().createBlock(3, [0])).getBlockIndices()) == [0, 1]
+    assert list(IS().createBlock(2, [1]).union(IS().createGeneral([0])).getIndices()) == [0, 2, 3]
+    loc = {3, 4}
+    coll = COMM_WORLD.tompi4py().allgather([loc])
+    assert coll == [[{3, 4}]]
+    assert COMM_WORLD.tompi4py().bcast("x") == "x"
+
+
+def _allgather_worker(rank, size, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(size))
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        from pynama_amd.runtime import COMM_WORLD
+        out = COMM_WORLD.tompi4py().allgather({rank * 10, rank * 10 + 1})
+        b = COMM_WORLD.tompi4py().bcast({"from": rank}, root=1)
+        q.put((rank, out, b))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allgather_over_gloo_two_ranks():
+    """getNodesByType(allGather=True) on two ranks: each rank's set, in rank order."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_allgather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    for rank, out, b in res:
+        assert out == [{0, 1}, {10, 11}] and b == {"from": 1}, (rank, out, b)
