@@ -411,6 +411,11 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on);
  * The product is unchanged bit for bit; its speed should not depend on where
  * the array lies (tests/test_gpu_fullsize.py). */
 int kle_mat_move_values(kle_mat *A, long long shift);
+/* Whether the value arrays (the full storage's / the symmetric storage's)
+ * got physically contiguous memory (kle_set_tuning "alloc_contig", default 1:
+ * contiguous first, plain when that fails); sval_addr (may be NULL): the
+ * symmetric values' device address. */
+int kle_mat_get_alloc_info(const kle_mat *A, int *val_contig, int *sval_contig, uint64_t *sval_addr);
 int kle_mat_get_sym_bricks(const kle_mat *A, int *nbricks, int *dims, double *entries_per_row, double *model_us);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */

@@ -549,6 +549,7 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
                 int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out)
 {
     auto *bp = new BrickPlan;
+    bp->pad = g_tune.spmv_brick_pad;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
                      std::max(1, A->ctx->num_cus),

@@ -36,6 +36,7 @@ struct BrickPlan {
     int64_t ws_doubles = 0, ws_entries = 0;
     size_t lds = 0;
     double model_us = 0.0;  // the planner's time model of the product (us)
+    int pad = 0;            // (in) doubles of gap before each brick's values (spmv_brick_pad)
 };
 
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their

@@ -458,6 +458,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
                 const int RN = D.RX * D.RY * D.RZ;
                 D.rstart = (int)rows;
                 D.eb = 0;
+                voff += bp.pad;
                 D.vbase = voff;
                 D.wsoff = wsd;
                 wsd += ((int64_t)3 * RN + 15) & ~int64_t(15);

@@ -18,6 +18,26 @@
 
 namespace kle {
 
+// Matrix value arrays are the SpMVs' whole stream, and where a few GB land
+// moves the same product by a few per cent (config 2 symmetric SpMV over
+// fresh allocations of its values: plain hipMalloc 424-428 us, physically
+// contiguous memory (hipDeviceMallocContiguous) 407-441 us with a lower
+// median, 413-417 against 425 us; profiles/r05/placement_*.jsonl).
+// Contiguous first, plain when the driver cannot find that much in one piece.
+int big_alloc(void **p, size_t bytes)
+{
+    *p = nullptr;
+    if (g_tune.alloc_contig && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return 1;
+    (void)hipGetLastError();
+    *p = nullptr;
+    if (hipMalloc(p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return -1;
+    }
+    return 0;
+}
+
 Tuning g_tune;
 #ifdef KLE_PROBE_BUILD
 unsigned long long *g_probe_ts = nullptr;
@@ -722,6 +742,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_ahead") {
         KLE_ARG(value == 1 || value == 2, "spmv_brick_ahead: 1 or 2");
         g_tune.spmv_brick_ahead = value;
+    } else if (k == "spmv_brick_pad") {
+        KLE_ARG(value >= 0 && value % 16 == 0 && value <= (1 << 20), "spmv_brick_pad: multiple of 16 doubles");
+        g_tune.spmv_brick_pad = value;
+    } else if (k == "alloc_contig") {
+        KLE_ARG(value == 0 || value == 1, "alloc_contig: 0 or 1");
+        g_tune.alloc_contig = value;
     } else if (k == "spmv_brick_split") {
         KLE_ARG(value >= 0, "spmv_brick_split: nbx + 100 nby + 10000 nbz (0: planned)");
         g_tune.spmv_brick_split = value;
@@ -815,6 +841,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_max") *value = g_tune.spmv_brick_max;
     else if (k == "spmv_brick_rounds") *value = g_tune.spmv_brick_rounds;
     else if (k == "spmv_brick_split") *value = g_tune.spmv_brick_split;
+    else if (k == "alloc_contig") *value = g_tune.alloc_contig;
+    else if (k == "spmv_brick_pad") *value = g_tune.spmv_brick_pad;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;

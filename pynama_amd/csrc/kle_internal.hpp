@@ -238,7 +238,9 @@ struct kle_mat {
     // SBAIJ; structured 3x3 rows, one rank or z slabs): each row's blocks from
     // its diagonal block on, in the chunked layout; per-tile partial sums d_sws
     double *d_sval = nullptr;
-    void *sval_raw = nullptr;  // kle_mat_move_values: the allocation d_sval lies in (freed instead of it)
+    void *sval_raw = nullptr;
+    int sval_contig = 0;  // d_sval came from a contiguous allocation (sval_alloc)
+    int val_contig = 0;   // d_val / d_aval likewise (big_alloc)  // kle_mat_move_values: the allocation d_sval lies in (freed instead of it)
     int64_t *d_svptr = nullptr;
     double *d_sws = nullptr;
     int *d_stile_e = nullptr;  // per tile: 2^e bounds its transposed row sums (fixed-point scale, k_sym_bound)
@@ -336,6 +338,11 @@ int sym_dot_parts(const kle_mat *A);  // partials sym_spmv writes with dpart (0:
 // values are copied (takes the plan), product, teardown
 int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &cnt, const std::vector<int> &srow,
                 int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out);
+// the symmetric storage's value array (kle_sym.hip): contiguous first
+int sval_alloc(kle_mat *A, size_t bytes);
+// a streamed array (matrix values): contiguous first (alloc_contig); 1 if
+// the memory is contiguous, 0 plain, -1 out of memory
+int big_alloc(void **p, size_t bytes);
 int brick_finish(kle_mat *A, void *plan);
 void brick_plan_free(void *plan);
 int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart);
@@ -387,6 +394,8 @@ struct Tuning {
     int spmv_brick_ahead = 1;  // brick SpMV: items in flight ahead of the summed one per wave (1 or 2)
     int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: planned, spmv_brick_rounds per CU)
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
+    int alloc_contig = 1;  // matrix value arrays (read at allocation): physically contiguous first (hipDeviceMallocContiguous), 0 plain hipMalloc
+    int spmv_brick_pad = 0;    // brick SpMV (read at build): doubles of gap before each brick's values (multiple of 16; experiments)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)
     int spmv_sym_brick = 1;   // box symmetric storage, one rank (read at build): one brick per CU, sums in LDS for the whole stream (kle_brick.hip); 0 the 128-row tiles
 #ifdef KLE_PROBE_BUILD

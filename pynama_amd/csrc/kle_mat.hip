@@ -870,7 +870,8 @@ static int aij_upload(kle_mat *A)
     for (int64_t k = 0; k < A->nnz; ++k) c32[k] = (int)(A->h_col[k] - A->col_lo);
     KLE_HIP(hipMalloc(&A->d_aptr, sizeof(int64_t) * A->h_ptr.size()));
     KLE_HIP(hipMalloc(&A->d_acol, sizeof(int) * c32.size()));
-    KLE_HIP(hipMalloc(&A->d_aval, sizeof(double) * std::max<int64_t>(A->nnz, 1)));
+    if ((A->val_contig = big_alloc(reinterpret_cast<void **>(&A->d_aval), sizeof(double) * std::max<int64_t>(A->nnz, 1))) < 0)
+        return fail(KLE_ERR_MEM, "out of device memory for the AIJ values");
     KLE_HIP(hipMemcpyAsync(A->d_aptr, A->h_ptr.data(), sizeof(int64_t) * A->h_ptr.size(), hipMemcpyHostToDevice, c->stream));
     KLE_HIP(hipMemcpyAsync(A->d_acol, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice, c->stream));
     if (A->nnz)
@@ -1448,21 +1449,33 @@ int kle_mat_set_spmv_structured(kle_mat *A, int on)
     return 0;
 }
 
+int kle_mat_get_alloc_info(const kle_mat *A, int *val_contig, int *sval_contig, uint64_t *sval_addr)
+{
+    KLE_ARG(A && val_contig && sval_contig, "null arg");
+    *val_contig = A->val_contig > 0;
+    *sval_contig = A->d_sval && A->sval_contig;
+    if (sval_addr) *sval_addr = (uint64_t)(uintptr_t)A->d_sval;
+    return 0;
+}
+
 int kle_mat_move_values(kle_mat *A, long long shift)
 {
     using namespace kle;
     KLE_ARG(A && A->d_sval, "no symmetric storage");
     KLE_ARG(shift >= 0 && shift % 8 == 0 && shift <= (1ll << 30), "shift: a multiple of 8 bytes in [0, 1 GiB]");
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
-    char *raw = nullptr;
-    if (hipMalloc(&raw, bytes + (size_t)shift) != hipSuccess) {
-        (void)hipGetLastError();
+    double *old = A->d_sval;
+    void *old_raw = A->sval_raw ? A->sval_raw : A->d_sval;
+    KLE_HIP(hipStreamSynchronize(A->ctx->stream));
+    if (sval_alloc(A, bytes + (size_t)shift)) {  // (the same allocator as the build's)
+        A->d_sval = old;
+        A->sval_raw = old_raw == old ? nullptr : old_raw;
         return fail(KLE_ERR_MEM, "out of device memory for the moved values (%zu bytes)", bytes + (size_t)shift);
     }
+    char *raw = reinterpret_cast<char *>(A->d_sval);
     double *nv = reinterpret_cast<double *>(raw + shift);
-    KLE_HIP(hipStreamSynchronize(A->ctx->stream));
-    KLE_HIP(hipMemcpy(nv, A->d_sval, bytes, hipMemcpyDeviceToDevice));
-    KLE_HIP(hipFree(A->sval_raw ? A->sval_raw : A->d_sval));
+    KLE_HIP(hipMemcpy(nv, old, bytes, hipMemcpyDeviceToDevice));
+    KLE_HIP(hipFree(old_raw));
     A->sval_raw = raw;
     A->d_sval = nv;
     return 0;

@@ -661,6 +661,18 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
 }
 
+// The value array: big_alloc (contiguous first).  0 on success; d_sval is
+// then set (sval_raw cleared).
+int sval_alloc(kle_mat *A, size_t bytes)
+{
+    A->sval_raw = nullptr;
+    void *p = nullptr;
+    const int r = big_alloc(&p, bytes);
+    A->d_sval = static_cast<double *>(p);
+    A->sval_contig = r > 0;
+    return r < 0 ? KLE_ERR_MEM : 0;
+}
+
 // A copy of a matrix struct (Mat.duplicate) shares none of A's symmetric
 // storage: forget the pointers (without freeing them).
 void sym_forget(kle_mat *A)
@@ -1260,7 +1272,7 @@ static int gsym_build(kle_mat *A)
     double *rowdiff = nullptr, *rowmax = nullptr;
     const bool nomem =
         hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
-        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
+        sval_alloc(A, sizeof(double) * std::max<int64_t>(tot, 1)) != 0 ||
         hipMalloc(&A->d_srow, sizeof(int) * n) != hipSuccess || hipMalloc(&A->d_sbp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_slid, sizeof(uint16_t) * slid.size()) != hipSuccess ||
         hipMalloc(&A->d_sdptr, sizeof(int) * (ng + 1)) != hipSuccess ||
@@ -1730,7 +1742,10 @@ static int sym_build_impl(kle_mat *A)
             bplan = nullptr;
             bwhy = "not on every rank";
         }
-        if (bplan) sv.swap(svb);
+        if (bplan) {
+            sv.swap(svb);
+            tot = std::max<int64_t>(tot, sv[n]);  // (spmv_brick_pad: gaps between the bricks)
+        }
         else if (const char *e = getenv("KLE_TIMING"))
             if (atoi(e)) fprintf(stderr, "[kle brick r%d] not used: %s\n", c->rank, bwhy.c_str());
     }
@@ -1783,7 +1798,7 @@ static int sym_build_impl(kle_mat *A)
     int64_t nomem = 0;
     if (hipMalloc(&A->d_svptr, sizeof(int64_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&A->d_srow, sizeof(int) * std::max<int64_t>(n, 1)) != hipSuccess ||
-        hipMalloc(&A->d_sval, sizeof(double) * std::max<int64_t>(tot, 1)) != hipSuccess ||
+        sval_alloc(A, sizeof(double) * std::max<int64_t>(tot, 1)) != 0 ||
         hipMalloc(&rowdiff, sizeof(double) * n) != hipSuccess || hipMalloc(&rowmax, sizeof(double) * n) != hipSuccess)
         nomem = 1;
     double dmax = 0.0, vmax = 0.0;
