@@ -406,15 +406,18 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on);
  * none -- full storage, tiles or the graph kernel): bricks, bricks along
  * x / y / z, region entries per row, the planner's modelled product time
  * (us). */
-/* Diagnostic: move the symmetric storage's value array to a fresh allocation,
- * `shift` bytes (a multiple of 8, <= 1 GiB) into it, and free the old one.
- * The product is unchanged bit for bit; its speed should not depend on where
- * the array lies (tests/test_gpu_fullsize.py). */
-int kle_mat_move_values(kle_mat *A, long long shift);
+/* Diagnostic: move the symmetric storage's value array.  fresh = 1: to a new
+ * allocation, `shift` bytes (a multiple of 8, <= 1 GiB) into it (the old one
+ * freed).  fresh = 0: `shift` bytes into the allocation of the previous
+ * fresh = 0 move -- the same physical pages, another offset (the first such
+ * call makes that allocation, with 8 MB of room, at offset 0).  The product
+ * is unchanged bit for bit; its speed should not depend on the offset
+ * (tests/test_gpu_fullsize.py). */
+int kle_mat_move_values(kle_mat *A, long long shift, int fresh);
 /* Whether the value arrays (the full storage's / the symmetric storage's)
- * got physically contiguous memory (kle_set_tuning "alloc_contig", default 1:
- * contiguous first, plain when that fails); sval_addr (may be NULL): the
- * symmetric values' device address. */
+ * got physically contiguous memory (kle_set_tuning "alloc_contig": 1
+ * contiguous first, plain when that fails; default 0, plain); sval_addr (may
+ * be NULL): the symmetric values' device address. */
 int kle_mat_get_alloc_info(const kle_mat *A, int *val_contig, int *sval_contig, uint64_t *sval_addr);
 int kle_mat_get_sym_bricks(const kle_mat *A, int *nbricks, int *dims, double *entries_per_row, double *model_us);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in

@@ -1142,8 +1142,10 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
         KLE_HIP(hipMemcpyAsync(A->d_rowcnt, cnt.data(), sizeof(int) * std::max<int64_t>(nrows, 1), hipMemcpyHostToDevice,
                                ctx->stream));
     KLE_HIP(hipMemcpyAsync(A->d_vptr, vptr.data(), sizeof(int64_t) * (nrows + 1), hipMemcpyHostToDevice, ctx->stream));
-    if (pad > 1 || lay == 1)
-        KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(A->nvals, 1), ctx->stream));
+    // (always zeroed: not every fill writes every slot -- pad blocks, chunk
+    // tails, pattern entries no element touches -- and recycled device memory
+    // is not zero)
+    KLE_HIP(hipMemsetAsync(A->d_val, 0, sizeof(double) * std::max<int64_t>(A->nvals, 1), ctx->stream));
     if (is_box) {
         KLE_HIP(hipMalloc(&A->d_rowbox, sizeof(int) * 2 * nrows));
         KLE_HIP(hipMemcpyAsync(A->d_rowbox, box.data(), sizeof(int) * 2 * nrows, hipMemcpyHostToDevice, ctx->stream));

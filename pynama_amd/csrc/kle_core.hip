@@ -23,7 +23,12 @@ namespace kle {
 // fresh allocations of its values: plain hipMalloc 424-428 us, physically
 // contiguous memory (hipDeviceMallocContiguous) 407-441 us with a lower
 // median, 413-417 against 425 us; profiles/r05/placement_*.jsonl).
-// Contiguous first, plain when the driver cannot find that much in one piece.
+// With alloc_contig 1: contiguous first, plain when the driver cannot find
+// that much in one piece.  Off by default: the element-batched assembly,
+// whose gathers add to values an earlier launch stored, missed 41 of 1.4M
+// sums on contiguous memory (tests/test_gpu.py
+// test_batched_element_scratch_is_bitwise, r05) -- a cache-coherence
+// difference of that memory kind this code does not rely on.
 int big_alloc(void **p, size_t bytes)
 {
     *p = nullptr;

@@ -239,6 +239,7 @@ struct kle_mat {
     // its diagonal block on, in the chunked layout; per-tile partial sums d_sws
     double *d_sval = nullptr;
     void *sval_raw = nullptr;
+    size_t sval_cap = 0;  // bytes at sval_raw
     int sval_contig = 0;  // d_sval came from a contiguous allocation (sval_alloc)
     int val_contig = 0;   // d_val / d_aval likewise (big_alloc)  // kle_mat_move_values: the allocation d_sval lies in (freed instead of it)
     int64_t *d_svptr = nullptr;
@@ -394,7 +395,7 @@ struct Tuning {
     int spmv_brick_ahead = 1;  // brick SpMV: items in flight ahead of the summed one per wave (1 or 2)
     int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: planned, spmv_brick_rounds per CU)
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
-    int alloc_contig = 1;  // matrix value arrays (read at allocation): physically contiguous first (hipDeviceMallocContiguous), 0 plain hipMalloc
+    int alloc_contig = 0;  // matrix value arrays (read at allocation): 1 physically contiguous first (hipDeviceMallocContiguous; experiments), 0 plain hipMalloc
     int spmv_brick_pad = 0;    // brick SpMV (read at build): doubles of gap before each brick's values (multiple of 16; experiments)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)
     int spmv_sym_brick = 1;   // box symmetric storage, one rank (read at build): one brick per CU, sums in LDS for the whole stream (kle_brick.hip); 0 the 128-row tiles

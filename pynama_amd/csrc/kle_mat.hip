@@ -1458,20 +1458,39 @@ int kle_mat_get_alloc_info(const kle_mat *A, int *val_contig, int *sval_contig, 
     return 0;
 }
 
-int kle_mat_move_values(kle_mat *A, long long shift)
+int kle_mat_move_values(kle_mat *A, long long shift, int fresh)
 {
     using namespace kle;
     KLE_ARG(A && A->d_sval, "no symmetric storage");
     KLE_ARG(shift >= 0 && shift % 8 == 0 && shift <= (1ll << 30), "shift: a multiple of 8 bytes in [0, 1 GiB]");
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(A->snvals, 1);
+    if (!fresh && A->sval_raw && (size_t)shift + bytes <= A->sval_cap) {
+        // the same allocation (the same physical pages), another offset:
+        // through a scratch copy (the ranges may overlap)
+        double *tmp = nullptr;
+        if (hipMalloc(&tmp, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(KLE_ERR_MEM, "out of device memory for the move's scratch copy");
+        }
+        KLE_HIP(hipStreamSynchronize(A->ctx->stream));
+        KLE_HIP(hipMemcpy(tmp, A->d_sval, bytes, hipMemcpyDeviceToDevice));
+        double *nv = reinterpret_cast<double *>(static_cast<char *>(A->sval_raw) + shift);
+        KLE_HIP(hipMemcpy(nv, tmp, bytes, hipMemcpyDeviceToDevice));
+        KLE_HIP(hipFree(tmp));
+        A->d_sval = nv;
+        return 0;
+    }
+    if (!fresh) shift = 0;  // (a new allocation with room for later offsets: shift applies from the next call)
+    const size_t cap = bytes + (size_t)(fresh ? shift : (8ll << 20));
     double *old = A->d_sval;
     void *old_raw = A->sval_raw ? A->sval_raw : A->d_sval;
     KLE_HIP(hipStreamSynchronize(A->ctx->stream));
-    if (sval_alloc(A, bytes + (size_t)shift)) {  // (the same allocator as the build's)
+    if (sval_alloc(A, cap)) {  // (the same allocator as the build's)
         A->d_sval = old;
         A->sval_raw = old_raw == old ? nullptr : old_raw;
-        return fail(KLE_ERR_MEM, "out of device memory for the moved values (%zu bytes)", bytes + (size_t)shift);
+        return fail(KLE_ERR_MEM, "out of device memory for the moved values (%zu bytes)", cap);
     }
+    A->sval_cap = cap;
     char *raw = reinterpret_cast<char *>(A->d_sval);
     double *nv = reinterpret_cast<double *>(raw + shift);
     KLE_HIP(hipMemcpy(nv, old, bytes, hipMemcpyDeviceToDevice));

@@ -679,6 +679,7 @@ void sym_forget(kle_mat *A)
 {
     A->d_sval = nullptr;
     A->sval_raw = nullptr;
+    A->sval_cap = 0;
     A->d_svptr = nullptr;
     A->d_sws = nullptr;
     A->d_stile_e = nullptr;

@@ -458,10 +458,11 @@ class Mat:
             return None
         return {"bricks": n.value, "dims": list(dims), "region_entries_per_row": ent.value, "model_us": mus.value}
 
-    def moveValues(self, shift):
-        """Diagnostic: the symmetric storage's values to a fresh allocation,
-        `shift` bytes into it (kle_mat_move_values)."""
-        call("kle_mat_move_values", self._h, int(shift))
+    def moveValues(self, shift, fresh=True):
+        """Diagnostic: the symmetric storage's values `shift` bytes into a
+        fresh allocation, or (fresh=False) into the allocation of the previous
+        fresh=False move: same pages, other offset (kle_mat_move_values)."""
+        call("kle_mat_move_values", self._h, int(shift), int(bool(fresh)))
 
     def getAllocInfo(self):
         """{"values_contiguous", "symmetric_values_contiguous"}: whether the
