@@ -704,14 +704,14 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
     const BrickDesc *bd = reinterpret_cast<const BrickDesc *>(A->d_bdesc);
-    auto go = [&](auto kern, int slot) {
-        static int lds_set[2] = {0, 0};  // dynamic LDS above 64 KB must be declared per kernel
+    auto go = [&](auto kern, int slot, int wv) {
+        static int lds_set[4] = {0, 0, 0, 0};  // dynamic LDS above 64 KB must be declared per kernel
         if (A->brick_lds > lds_set[slot]) {
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       A->brick_lds);
             lds_set[slot] = A->brick_lds;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * BRICK_WV), (size_t)A->brick_lds, c->stream,
+        hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * wv), (size_t)A->brick_lds, c->stream,
                            (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, bd,
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
                            istate KLE_PROBE_ARG);
@@ -732,8 +732,11 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     if (dist)
         KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
                               x->send_hi, c->stream, nullptr));
-    if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1);
-    else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0);
+    // (spmv_brick_waves: fewer waves per CU keep fewer loads in flight)
+    if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1, BRICK_WV);
+    else if (g_tune.spmv_brick_waves == 8) go(k_nb_spmv_sym_brick<8, 1>, 2, 8);
+    else if (g_tune.spmv_brick_waves == 12) go(k_nb_spmv_sym_brick<12, 1>, 3, 12);
+    else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0, BRICK_WV);
     KLE_HIP(hipGetLastError());
     if (!dist) {
         gather(0, A->nbricks, y->d, 0, dpart, c->stream);
