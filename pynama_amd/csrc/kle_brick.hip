@@ -696,6 +696,8 @@ void brick_forget(kle_mat *A)
     A->brick_model_us = 0.0;
     A->brick_lds = 0;
     A->sym_brick = 0;
+    A->sym_gbrick = 0;
+    A->brick_lds_u = 0;
 }
 
 int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)

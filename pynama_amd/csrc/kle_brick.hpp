@@ -42,6 +42,16 @@ struct BrickPlan {
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their
 // dummy slots, wave maxima, the row counter)
 inline size_t brick_lds(int RN) { return (size_t)(3 * RN + 3 * (RN + 64)) * 8 + 512; }
+// an unstructured (graph) brick: rows [r0, r0 + nr), its dictionary of U
+// entries from dict[d0] (its rows first), values from sval[vbase], 2-byte
+// positions from slid[sbase], sums to ws[wsoff] ([entry][3]); eb its bound
+// (kle_gbrick.hip)
+struct GBrickDesc {
+    int r0, nr, U, eb;
+    long long d0, vbase, sbase, wsoff;
+};
+// dictionary entries a graph brick may hold (brick_lds <= BRICK_LDS_CAP)
+constexpr int GB_UCAP = (int)((BRICK_LDS_CAP - 2048) / 48);
 constexpr int BG_MAXNB = 64;  // bricks whose regions meet one brick's rows (27 in a regular grid)
 // the gather's record per brick: a header (listed regions, the brick's own
 // box: nq, x0, y0, z0, nx, ny, nz, 0) and per listed region (ascending

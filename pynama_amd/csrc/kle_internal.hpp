@@ -262,6 +262,8 @@ struct kle_mat {
     // brick the bricks whose regions meet its rows; d_sws holds the bricks'
     // region sums, d_stile_e their bound exponents
     int sym_brick = 0;
+    int sym_gbrick = 0;  // unstructured: graph bricks (d_bdesc = GBrickDesc, d_browd = 4 ints per row)
+    int brick_lds_u = 0;  // graph bricks: the largest dictionary
     int nbricks = 0, brick_lds = 0, brick_gparts = 0;  // (gather workgroups per brick)
     int nbricks_ghost = 0;  // N > 1: upper-ghost pieces after the bricks (gather only: the reverse halo's sums)
     int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
@@ -344,6 +346,9 @@ int sval_alloc(kle_mat *A, size_t bytes);
 // a streamed array (matrix values): contiguous first (alloc_contig); 1 if
 // the memory is contiguous, 0 plain, -1 out of memory
 int big_alloc(void **p, size_t bytes);
+// graph bricks (kle_gbrick.hip)
+int gbrick_bound(kle_mat *A, double vmax_all);
+int gbrick_launch(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
 int brick_finish(kle_mat *A, void *plan);
 void brick_plan_free(void *plan);
 int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart);
@@ -396,6 +401,7 @@ struct Tuning {
     int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: planned, spmv_brick_rounds per CU)
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
     int alloc_contig = 0;  // matrix value arrays (read at allocation): 1 physically contiguous first (hipDeviceMallocContiguous; experiments), 0 plain hipMalloc
+    int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
     int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
     int spmv_brick_pad = 0;    // brick SpMV (read at build): doubles of gap before each brick's values (multiple of 16; experiments)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)

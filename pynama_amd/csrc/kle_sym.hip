@@ -9,6 +9,7 @@
 #include <thread>
 #include <vector>
 
+#include "kle_brick.hpp"
 #include "kle_internal.hpp"
 #include "kle_sym_dev.hpp"
 
@@ -1029,7 +1030,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
                                                         const unsigned long long *__restrict__ rmask,
                                                         const double *__restrict__ ws, double *__restrict__ y,
                                                         double *__restrict__ gsend, const int *__restrict__ istate,
-                                                        const double *__restrict__ xdot, double *__restrict__ dpart)
+                                                        const double *__restrict__ xdot, double *__restrict__ dpart,
+                                                        int preload)
 {
     __shared__ double dred[4];
     const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;  // (tested before the first store)
@@ -1056,6 +1058,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
         }
         if (stop) return;  // (uniform: the whole workgroup)
         if (j < nrows) {
+            if (preload) {  // (graph bricks: the rows' direct sums are in y)
+                s0 += y[3 * j];
+                s1 += y[3 * j + 1];
+                s2 += y[3 * j + 2];
+            }
             y[3 * j] = s0;
             y[3 * j + 1] = s1;
             y[3 * j + 2] = s2;
@@ -1110,6 +1117,51 @@ static int sym_probe(kle_mat *A, double vmax_all, bool &bad);
 // LDS.  Collective at N > 1: every rank takes the same decision (any_rank),
 // and one hashed product through both storages checks the blocks between
 // ranks (sym_probe).
+// Graph bricks: contiguous row ranges (Hilbert order: spatially compact) of
+// about equal cost -- a row costs its 64-block passes, each as if full (the
+// box bricks' measured cost model, kle_brick_plan.cpp row_cost) -- one per CU,
+// or k per CU (up to 8) until every range's dictionary (its rows, then the
+// upper-triangle columns past them) fits GB_UCAP LDS entries.  false: none
+// fits (the 64-row groups are used).
+static bool gbrick_ranges(int64_t n, int64_t glo, int64_t ntot, const std::vector<int> &rp,
+                          const std::vector<int> &cnt, const std::vector<int> &bcol, const std::vector<int> &k0,
+                          const std::vector<int> &smu, int ncu, std::vector<int64_t> &gst)
+{
+    if (n <= 0) return false;
+    std::vector<double> P(n + 1, 0.0);
+    for (int64_t i = 0; i < n; ++i) P[i + 1] = P[i] + 4608.0 * ((smu[i] + 63) / 64);
+    std::vector<int> mark(std::max<int64_t>(ntot, 1), -1);
+    // (whole rounds of ncu bricks: a partial last round would leave CUs idle
+    // for one brick's time)
+    for (int NB = ncu; NB <= 8 * ncu; NB += ncu) {
+        gst.assign(1, 0);
+        for (int q = 1; q < NB; ++q) {
+            const double t = P[n] * q / NB;
+            const int64_t r = std::lower_bound(P.begin(), P.end(), t) - P.begin();
+            if (r > gst.back() && r < n) gst.push_back(r);
+        }
+        gst.push_back(n);
+        const int nb = (int)gst.size() - 1;
+        int umax = 0;
+        for (int q = 0; q < nb && umax <= GB_UCAP; ++q) {
+            const int64_t r0 = gst[q], r1 = gst[q + 1];
+            int u = (int)(r1 - r0);
+            for (int64_t i = r0; i < r1; ++i)
+                for (int k = rp[i] + k0[i]; k < rp[i] + cnt[i]; ++k) {
+                    const int64_t col = bcol[k] - glo;
+                    if (col >= r1 && mark[col] != q + NB * 16) {
+                        mark[col] = q + NB * 16;
+                        ++u;
+                    }
+                }
+            umax = std::max(umax, u);
+        }
+        if (umax <= GB_UCAP) return true;
+    }
+    gst.clear();
+    return false;
+}
+
 static int gsym_build(kle_mat *A)
 {
     kle_ctx *c = A->ctx;
@@ -1127,9 +1179,17 @@ static int gsym_build(kle_mat *A)
     const int WV = g_tune.spmv_gsym_waves ? g_tune.spmv_gsym_waves : G >= 64 ? 16 : 8;
     if (why.empty() && !((WV == 8 && G <= 64) || (WV == 16 && G >= 32)))  // (the kernels instantiated in gsym_spmv)
         why = "symmetric storage: " + std::to_string(G) + "-row groups on " + std::to_string(WV) + " waves";
-    const int64_t ng = (n + G - 1) / G, ntot = n + nhi, ns = (ntot + 63) / 64;
+    int64_t ng = (n + G - 1) / G;
+    const int64_t ntot = n + nhi, ns = (ntot + 63) / 64;
     std::vector<int> rp, cnt, bcol, k0, smu, usz, dptr(ng + 1, 0), wptr(ng + 1, 0), glist(ng), dict, runptr(ns + 1, 0),
         rstart;
+    // one rank: graph bricks (kle_gbrick.hip) -- the groups become one
+    // contiguous row range per CU (gst), the rest of the machinery unchanged
+    const bool gb = g_tune.spmv_gsym_brick && g_tune.spmv_sym_det && !dist;
+    bool gb_on = false;
+    std::vector<int64_t> gst;
+    auto gr0 = [&](int64_t g) { return gb_on ? gst[g] : g * G; };
+    auto gr1 = [&](int64_t g) { return gb_on ? gst[g + 1] : std::min<int64_t>(n, (g + 1) * G); };
     std::vector<int64_t> svp, sbp;
     std::vector<uint16_t> slid;
     std::vector<unsigned long long> rmask;
@@ -1166,6 +1226,16 @@ static int gsym_build(kle_mat *A)
         }
         svp[n] = tot;
         sbp[n] = blocks;
+        if (gb) {
+            gb_on = gbrick_ranges(n, glo, ntot, rp, cnt, bcol, k0, smu, std::max(1, c->num_cus), gst);
+            if (gb_on) {
+                ng = (int64_t)gst.size() - 1;
+                dptr.assign(ng + 1, 0);
+                wptr.assign(ng + 1, 0);
+                glist.assign(ng, 0);
+            }
+        }
+        const int ucap = gb_on ? GB_UCAP : GSYM_UCAP;
         // group dictionaries (threads over groups; ext column ids)
         usz.assign(ng, 0);
         std::vector<std::vector<int>> dl(ng);
@@ -1174,13 +1244,13 @@ static int gsym_build(kle_mat *A)
         std::atomic<bool> big{false};
         auto work = [&](int t) {
             for (int64_t g = t; g < ng; g += nt) {
-                const int64_t r0 = g * G, r1 = std::min(n, r0 + G);
+                const int64_t r0 = gr0(g), r1 = gr1(g);
                 std::vector<int> &L = dl[g];
                 for (int64_t r = r0; r < r1; ++r)
                     L.insert(L.end(), bcol.begin() + rp[r] + k0[r], bcol.begin() + rp[r] + cnt[r]);
                 std::sort(L.begin(), L.end());
                 L.erase(std::unique(L.begin(), L.end()), L.end());
-                if ((int64_t)L.size() > GSYM_UCAP) {
+                if ((int64_t)L.size() > ucap) {
                     big = true;
                     continue;
                 }
@@ -1196,13 +1266,13 @@ static int gsym_build(kle_mat *A)
             for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
             for (auto &x : th) x.join();
         }
-        if (big) return "symmetric storage: a row group's columns exceed " + std::to_string(GSYM_UCAP) + " LDS slots";
+        if (big) return "symmetric storage: a row group's columns exceed " + std::to_string(ucap) + " LDS slots";
         for (int64_t g = 0; g < ng; ++g) {
             if ((int64_t)dptr[g] + usz[g] > INT_MAX / 3) return "symmetric storage: dictionaries too large";
             dptr[g + 1] = dptr[g] + usz[g];
             US = std::max(US, usz[g]);
-            for (int e = 0; e < usz[g] && e < G && g * G + e < n; ++e)
-                if (dl[g][e] != glo + g * G + e)  // (cannot happen: the rows lead)
+            for (int64_t e = 0; e < usz[g] && e < gr1(g) - gr0(g); ++e)
+                if (dl[g][e] != glo + gr0(g) + e)  // (cannot happen: the rows lead)
                     return "symmetric storage: group " + std::to_string(g) + " does not lead with its rows";
         }
         E = dptr[ng];
@@ -1347,10 +1417,46 @@ static int gsym_build(kle_mat *A)
     }
     if (any)
         return done(fail(KLE_ERR_SUP, "matrix is not symmetric (max |A_ij - A_ji| = %g, max |A_ij| = %g)", dmax, vmax));
-    hipLaunchKernelGGL(k_gsym_bound, dim3((unsigned)ng), dim3(256), 0, c->stream, n, G, A->d_sdptr, A->d_srow, A->d_sbp,
-                       A->d_slid, A->d_svptr, A->d_sval, A->d_stile_e);
-    KLE_HIP(hipGetLastError());
-    KLE_HIP(hipStreamSynchronize(c->stream));
+    if (gb_on) {
+        // the bricks' descriptors and per-row (value offset / 16, position
+        // offset, stored blocks), then their bounds
+        std::vector<GBrickDesc> hb(ng);
+        std::vector<int> rowd(4 * (size_t)std::max<int64_t>(n, 1), 0);
+        for (int64_t q = 0; q < ng; ++q) {
+            GBrickDesc &B = hb[q];
+            const int64_t r0 = gst[q], r1 = gst[q + 1];
+            B.r0 = (int)r0;
+            B.nr = (int)(r1 - r0);
+            B.U = usz[q];
+            B.eb = 0;
+            B.d0 = dptr[q];
+            B.vbase = svp[r0];
+            B.sbase = sbp[r0];
+            B.wsoff = wptr[q];
+            for (int64_t i = r0; i < r1; ++i) {
+                rowd[4 * i] = (int)((svp[i] - svp[r0]) / 16);
+                rowd[4 * i + 1] = (int)(sbp[i] - sbp[r0]);
+                rowd[4 * i + 2] = smu[i];
+            }
+        }
+        if (hipMalloc(&A->d_bdesc, sizeof(GBrickDesc) * ng) != hipSuccess ||
+            hipMalloc(&A->d_browd, sizeof(int) * rowd.size()) != hipSuccess) {
+            (void)hipGetLastError();
+            return done(fail(KLE_ERR_MEM, "out of device memory for the graph bricks"));
+        }
+        KLE_HIP(hipMemcpy(A->d_bdesc, hb.data(), sizeof(GBrickDesc) * ng, hipMemcpyHostToDevice));
+        KLE_HIP(hipMemcpy(A->d_browd, rowd.data(), sizeof(int) * rowd.size(), hipMemcpyHostToDevice));
+        A->nbricks = (int)ng;
+        A->brick_lds_u = US;
+        A->brick_lds = (int)brick_lds(US);
+        A->sym_gbrick = 1;
+        KLE_TRY(gbrick_bound(A, vmax_all));
+    } else {
+        hipLaunchKernelGGL(k_gsym_bound, dim3((unsigned)ng), dim3(256), 0, c->stream, n, G, A->d_sdptr, A->d_srow,
+                           A->d_sbp, A->d_slid, A->d_svptr, A->d_sval, A->d_stile_e);
+        KLE_HIP(hipGetLastError());
+        KLE_HIP(hipStreamSynchronize(c->stream));
+    }
     A->sym_reg[0] = US1;
     A->sym_reg[1] = US;
     A->sym_reg[2] = (int)n1;
@@ -1369,11 +1475,12 @@ static int gsym_build(kle_mat *A)
     }
     if (const char *e = getenv("KLE_TIMING"))
         if (atoi(e))
-            fprintf(stderr, "[kle gsym r%d] rows %lld (+%lld upper ghosts), stored blocks %lld (of %lld), groups %lld, "
+            fprintf(stderr, "[kle gsym r%d] rows %lld (+%lld upper ghosts), stored blocks %lld (of %lld), %s %lld, "
                             "dictionary entries %lld (%.2f per row, largest group %d; %lld groups within %d slots), "
                             "gather runs %lld (%.1f per 64 rows)\n",
-                    c->rank, (long long)n, (long long)nhi, (long long)blocks, (long long)A->nblocks_real, (long long)ng,
-                    (long long)E, (double)E / n, US, (long long)n1, US1, (long long)NR, (double)NR / ns);
+                    c->rank, (long long)n, (long long)nhi, (long long)blocks, (long long)A->nblocks_real,
+                    gb_on ? "bricks" : "groups", (long long)ng, (long long)E, (double)E / n, US, (long long)n1, US1,
+                    (long long)NR, (double)NR / ns);
     return done(0);
 }
 
@@ -1381,6 +1488,14 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
+    if (A->sym_gbrick) {  // (one rank)
+        KLE_TRY(gbrick_launch(A, x, y, istate));
+        hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, A->nrows,
+                           A->nrows, A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate,
+                           dpart ? x->d : nullptr, dpart, 1);
+        KLE_HIP(hipGetLastError());
+        return 0;
+    }
     const int G = A->sym_reg[3], WV = A->sym_reg[4];
     const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2], nhi = A->ghost_hi / 3;
     const bool dist = c->nranks > 1;
@@ -1448,7 +1563,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     const int64_t ntot = n + (dist ? nhi : 0);
     hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st, n, ntot, A->d_sgptr,
                        A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate, dpart && !dist ? x->d : nullptr,
-                       dpart);
+                       dpart, 0);
     KLE_HIP(hipGetLastError());
     if (!dist) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending
@@ -2055,6 +2170,7 @@ std::string sym_kernel_name(const kle_mat *A)
     if (A->sym_brick)
         return std::string("k_nb_spmv_sym_brick<16,") + std::to_string(g_tune.spmv_brick_ahead) +
                ">+k_nb_sym_brick_gather";
+    if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather";
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
                std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather";
@@ -2075,6 +2191,11 @@ double sym_spmv_bytes(const kle_mat *A)
     // bricks: values, 8 B of row descriptor per row, x and y once, each
     // brick's region sums written once and read once
     if (A->sym_brick) return (double)A->sblocks * 72.0 + A->nrows * (8.0 + 48.0) + (double)A->sws_entries * 48.0;
+    // graph bricks: values + positions, 16 B of row descriptor per row, x
+    // and y once, per dictionary entry its node id and its sums written and
+    // read once
+    if (A->sym_gbrick)
+        return (double)A->sblocks * 74.0 + A->nrows * (16.0 + 48.0) + (double)A->sws_entries * (4.0 + 48.0);
     if (A->sym_graph)
         return (double)A->sblocks * 74.0 + A->nrows * (8.0 + 8.0 + 4.0 + 48.0) + (double)A->sws_entries * (4.0 + 48.0);
     return (double)A->sblocks * 72.0 + A->nrows * 16.0 + (double)A->nrows * 48.0 + (double)A->sws_entries * 48.0;

@@ -118,4 +118,4 @@ def test_config5_mesh_stated_size(pa, tmp_path):
     mat.build(buildOperators=False)
     assert mat.K.getSize()[0] == 8037603
     _log(t0, "config-5 mesh assembled (8,037,603 DoF)")
-    _properties(pa, dom, mat, t0, "k_nb_spmv_gsym<", 1621)
+    _properties(pa, dom, mat, t0, "k_nb_spmv_gsym", 1621)  # (graph bricks, or the 64-row groups)

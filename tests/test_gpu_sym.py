@@ -24,14 +24,18 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module", autouse=True)
 def tiles():
     """The box tests here exercise the 128-row tile kernel (the brick kernel,
-    default for one rank: test_gpu_brick.py); the tiles serve the z slabs of
-    N > 1, larger parts than one brick per CU covers, and spmv_sym_brick 0."""
+    default for one rank: test_gpu_brick.py); the tiles serve p = 6 and
+    spmv_sym_brick 0.  Likewise the unstructured tests exercise the 64-row
+    dictionary groups (graph bricks, default for one rank:
+    test_gpu_gbrick.py), which serve graph partitions at N > 1."""
     import pynama_amd
     pynama_amd.load()
     from pynama_amd.runtime import set_tuning
     set_tuning("spmv_sym_brick", 0)
+    set_tuning("spmv_gsym_brick", 0)
     yield
     set_tuning("spmv_sym_brick", 1)
+    set_tuning("spmv_gsym_brick", 1)
 
 
 @pytest.fixture(scope="module")
