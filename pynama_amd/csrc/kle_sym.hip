@@ -1131,33 +1131,53 @@ static bool gbrick_ranges(int64_t n, int64_t glo, int64_t ntot, const std::vecto
     std::vector<double> P(n + 1, 0.0);
     for (int64_t i = 0; i < n; ++i) P[i + 1] = P[i] + 4608.0 * ((smu[i] + 63) / 64);
     std::vector<int> mark(std::max<int64_t>(ntot, 1), -1);
-    // (whole rounds of ncu bricks: a partial last round would leave CUs idle
-    // for one brick's time)
-    for (int NB = ncu; NB <= 8 * ncu; NB += ncu) {
-        gst.assign(1, 0);
+    int stamp = 0;
+    // k bricks per CU (whole rounds of ncu bricks: a partial last round would
+    // leave CUs idle for one brick's time); the largest dictionary of k
+    auto umax_of = [&](int k, std::vector<int64_t> &st) {
+        const int NB = k * ncu;
+        st.assign(1, 0);
         for (int q = 1; q < NB; ++q) {
             const double t = P[n] * q / NB;
             const int64_t r = std::lower_bound(P.begin(), P.end(), t) - P.begin();
-            if (r > gst.back() && r < n) gst.push_back(r);
+            if (r > st.back() && r < n) st.push_back(r);
         }
-        gst.push_back(n);
-        const int nb = (int)gst.size() - 1;
+        st.push_back(n);
+        const int nb = (int)st.size() - 1;
         int umax = 0;
         for (int q = 0; q < nb && umax <= GB_UCAP; ++q) {
-            const int64_t r0 = gst[q], r1 = gst[q + 1];
+            const int64_t r0 = st[q], r1 = st[q + 1];
             int u = (int)(r1 - r0);
+            ++stamp;
             for (int64_t i = r0; i < r1; ++i)
-                for (int k = rp[i] + k0[i]; k < rp[i] + cnt[i]; ++k) {
-                    const int64_t col = bcol[k] - glo;
-                    if (col >= r1 && mark[col] != q + NB * 16) {
-                        mark[col] = q + NB * 16;
+                for (int kk = rp[i] + k0[i]; kk < rp[i] + cnt[i]; ++kk) {
+                    const int64_t col = bcol[kk] - glo;
+                    if (col >= r1 && mark[col] != stamp) {
+                        mark[col] = stamp;
                         ++u;
                     }
                 }
             umax = std::max(umax, u);
         }
-        if (umax <= GB_UCAP) return true;
+        return umax;
+    };
+    // first guess from the 1M-DoF p = 4 mesh (486-row ranges: 3,230 entries);
+    // then the fewest whole rounds that fit, at most 64 per CU
+    int k = (int)std::max<int64_t>(1, (n + 450LL * ncu - 1) / (450LL * ncu));
+    std::vector<int64_t> st;
+    if (umax_of(k, st) <= GB_UCAP) {
+        gst = st;
+        while (k > 1 && umax_of(k - 1, st) <= GB_UCAP) {
+            gst = st;
+            --k;
+        }
+        return true;
     }
+    for (++k; k <= 64; ++k)
+        if (umax_of(k, st) <= GB_UCAP) {
+            gst = st;
+            return true;
+        }
     gst.clear();
     return false;
 }
