@@ -1205,7 +1205,7 @@ static int gsym_build(kle_mat *A)
         rstart;
     // one rank: graph bricks (kle_gbrick.hip) -- the groups become one
     // contiguous row range per CU (gst), the rest of the machinery unchanged
-    const bool gb = g_tune.spmv_gsym_brick && g_tune.spmv_sym_det && !dist;
+    bool gb = g_tune.spmv_gsym_brick && g_tune.spmv_sym_det;
     bool gb_on = false;
     std::vector<int64_t> gst;
     auto gr0 = [&](int64_t g) { return gb_on ? gst[g] : g * G; };
@@ -1246,15 +1246,14 @@ static int gsym_build(kle_mat *A)
         }
         svp[n] = tot;
         sbp[n] = blocks;
-        if (gb) {
-            gb_on = gbrick_ranges(n, glo, ntot, rp, cnt, bcol, k0, smu, std::max(1, c->num_cus), gst);
-            if (gb_on) {
-                ng = (int64_t)gst.size() - 1;
-                dptr.assign(ng + 1, 0);
-                wptr.assign(ng + 1, 0);
-                glist.assign(ng, 0);
-            }
-        }
+        gb_on = gb && gbrick_ranges(n, glo, ntot, rp, cnt, bcol, k0, smu, std::max(1, c->num_cus), gst);
+        ng = gb_on ? (int64_t)gst.size() - 1 : (n + G - 1) / G;
+        dptr.assign(ng + 1, 0);
+        wptr.assign(ng + 1, 0);
+        glist.assign(ng, 0);
+        US = US1 = 0;
+        n1 = n2 = 0;
+        ninner[0] = ninner[1] = 0;
         const int ucap = gb_on ? GB_UCAP : GSYM_UCAP;
         // group dictionaries (threads over groups; ext column ids)
         usz.assign(ng, 0);
@@ -1355,6 +1354,15 @@ static int gsym_build(kle_mat *A)
     };
     if (why.empty()) why = analyse();
     bool any = false;
+    if (dist && why.empty() && gb) {
+        // every rank runs the same product schedule: bricks everywhere or
+        // groups everywhere
+        KLE_TRY(any_rank(c, !gb_on, any));
+        if (any && gb_on) {
+            gb = false;
+            why = analyse();
+        }
+    }
     KLE_TRY(any_rank(c, !why.empty(), any));
     if (any) return fail(KLE_ERR_SUP, "%s", why.empty() ? "symmetric storage refused on another rank" : why.c_str());
     // device arrays; the value copy and the symmetry check
@@ -1508,7 +1516,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
-    if (A->sym_gbrick) {  // (one rank)
+    if (A->sym_gbrick && c->nranks == 1) {
         KLE_TRY(gbrick_launch(A, x, y, istate));
         hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, A->nrows,
                            A->nrows, A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate,
@@ -1562,7 +1570,22 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         }
         return 0;
     };
-    if (!dist) {
+    if (A->sym_gbrick) {
+        // graph bricks at N > 1: every brick's dictionary may hold ghost
+        // columns, so the forward halo first (comm stream with overlap, as
+        // the group path's RCCL calls), then the bricks
+        if (ovl) {
+            KLE_HIP(hipEventRecord(c->ev_x_ready, st));
+            KLE_HIP(hipStreamWaitEvent(cs, c->ev_x_ready, 0));
+        }
+        KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
+                              x->send_hi, cs, x->plan.get()));
+        if (ovl) {
+            KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
+            KLE_HIP(hipStreamWaitEvent(st, c->ev_halo_done, 0));
+        }
+        KLE_TRY(gbrick_launch(A, x, y, istate));
+    } else if (!dist) {
         KLE_TRY(tiles(0));
         KLE_TRY(tiles(1));
     } else if (ovl) {
@@ -1583,7 +1606,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     const int64_t ntot = n + (dist ? nhi : 0);
     hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st, n, ntot, A->d_sgptr,
                        A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate, dpart && !dist ? x->d : nullptr,
-                       dpart, 0);
+                       dpart, A->sym_gbrick);
     KLE_HIP(hipGetLastError());
     if (!dist) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending

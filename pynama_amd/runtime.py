@@ -291,6 +291,8 @@ def get_ctx():
             set_tuning("spmv_sym_brick", int(os.environ["KLE_SPMV_SYM_BRICK"]))
         if os.environ.get("KLE_KSP_REFINE"):
             set_tuning("ksp_refine", int(os.environ["KLE_KSP_REFINE"]))
+        if os.environ.get("KLE_SPMV_GSYM_BRICK"):
+            set_tuning("spmv_gsym_brick", int(os.environ["KLE_SPMV_GSYM_BRICK"]))
         if os.environ.get("KLE_ALLOC_CONTIG"):
             set_tuning("alloc_contig", int(os.environ["KLE_ALLOC_CONTIG"]))
         _CTX = Context()

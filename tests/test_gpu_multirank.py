@@ -322,6 +322,20 @@ def test_partitioned_umesh_symmetric_storage(size, partitioner, nel, ksp_type, t
     res = _check_umesh(size, partitioner, nel, ksp_type, 0, tmp_path, sym=True)
     for r in res:
         assert r["sym"], r["rank"]
+        assert r["kernel"].startswith("k_nb_spmv_gsym_brick<"), r["kernel"]  # (graph bricks, round 5)
+
+
+@pytest.mark.parametrize("size,partitioner,nel,ksp_type", [
+    (3, "slab", [2, 3, 9], "pipecg"), (4, "inertial", [4, 4, 4], "cg"), (8, "inertial", [4, 4, 6], "pipecg")])
+def test_partitioned_umesh_symmetric_storage_groups(size, partitioner, nel, ksp_type, tmp_path):
+    """The 64-row dictionary groups on the same partitions
+    (KLE_SPMV_GSYM_BRICK=0): same checks."""
+    os.environ["KLE_SPMV_GSYM_BRICK"] = "0"  # inherited by the spawned ranks
+    try:
+        res = _check_umesh(size, partitioner, nel, ksp_type, 0, tmp_path, sym=True)
+    finally:
+        del os.environ["KLE_SPMV_GSYM_BRICK"]
+    for r in res:
         assert r["kernel"].startswith("k_nb_spmv_gsym<"), r["kernel"]
 
 
@@ -340,7 +354,7 @@ def test_partitioned_umesh_ipc_transport(size, nel, ksp_type, sym, tmp_path):
         assert a["transport"] == "ipc" and b["transport"] == "host"
         assert a["sym"] == sym and b["sym"] == sym
         if sym:
-            assert a["kernel"].startswith("k_nb_spmv_gsym<"), a["kernel"]
+            assert a["kernel"].startswith("k_nb_spmv_gsym_brick<"), a["kernel"]
         np.testing.assert_array_equal(a["y"], b["y"])
 
 
