@@ -11,15 +11,18 @@
 // those stores made the stream's speed depend on where the value array lay
 // (424-491 us at config 2).
 //
-// Here the owned lattice is cut into one element-aligned brick per CU (config
-// 2: 4 x 4 x 16 bricks of 20 x 16 x 4 nodes), and one 16-wave workgroup
-// streams a whole brick with x AND the exact int64 fixed-point sums of the
-// brick's region (25 x 21 x 5 nodes: 126 KB) resident in LDS from the first
-// value load to the last.  Nothing is stored while the value array streams;
-// at the end each brick writes its region once (2.05 entries per row, 16 MB),
-// and k_nb_sym_brick_gather adds, per row, the sums of the bricks whose
-// regions hold it in ascending brick order (bitwise reproducible, as the
-// fixed-point sums are order-free).  Inside a brick the waves take rows from
+// Here the owned lattice is cut into at most one element-aligned brick per
+// CU (planner: kle_brick_plan.cpp; config 2: 254 bricks), and one 16-wave
+// workgroup streams a whole brick with x AND the exact int64 fixed-point
+// sums of the brick's region (config 2: about 25 x 21 x 5 nodes, 126 KB)
+// resident in LDS from the first value load to the last.  The rows' direct
+// sums go to y as each row ends (8 MB); nothing else is stored while the
+// value array streams.  At the end each brick writes its region once
+// ([entry][3]; 2.02 entries per row, 16 MB), and the graph kernels' run-mask
+// gather (kle_sym.hip gsym_gather) adds, per row, the sums of the bricks
+// whose regions hold it in ascending brick order (bitwise reproducible, as
+// the fixed-point sums are order-free): per 64-row slice of the lattice, each
+// brick region's stretch of one lattice line is one run of consecutive sums.  Inside a brick the waves take rows from
 // an LDS counter, so the brick's end is one row long, not one wave's share.
 // The value array is laid out brick by brick (rows in brick order, each row's
 // upper tail in the 16-block chunk layout), so every CU streams one
@@ -51,105 +54,6 @@ struct BRow {
 struct BItem {
     int r, mu, ir, kb;
 };
-
-// y of brick O's rows from the region sums of the bricks its record lists
-// (ascending), by NT threads.  The record (BG_REC ints at O BG_REC: brick_finish)
-// is one load per thread into LDS, so the sums start one round trip after
-// the launch.  (Summing them inside the brick kernel, each
-// brick by the last of its neighbours to finish -- arrival counters, sc1
-// sums -- put the reductions on the slowest CUs: 0.485-0.564 vs 0.399-0.402
-// ms at config 2, profiles/r05/brick_fuse_rejected.jsonl.)
-// nbd: LDS for 8 ints per listed brick; dred: LDS for NT / 64 doubles.
-template <int NT>
-__device__ __forceinline__ void brick_reduce(int O, int Lx, int Ly, const int *__restrict__ nbrec,
-                                             const double *__restrict__ ws, double *__restrict__ y,
-                                             const double *__restrict__ xdot, double *__restrict__ dpart, int *rec,
-                                             double *dred, int r0, int r1, int dslot, int64_t jofs)
-{
-    {
-        constexpr int K = (BG_REC + NT - 1) / NT;
-        int v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int t = (int)threadIdx.x + k * NT;
-            v[k] = nbrec[(int64_t)O * BG_REC + min(t, BG_REC - 1)];
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if ((int)threadIdx.x + k * NT < BG_REC) rec[threadIdx.x + k * NT] = v[k];
-    }
-    __syncthreads();
-    const int nq = rec[0], x0 = rec[1], y0 = rec[2], z0 = rec[3], nx = rec[4], ny = rec[5], nz = rec[6];
-    const int NR = nx * ny * nz;
-    const int *nbd = rec + 8;
-    const int64_t Lxy = (int64_t)Lx * Ly;
-    double dsum = 0.0;
-    for (int r = r0 + (int)threadIdx.x; r < min(NR, r1); r += NT) {
-        const int rz = r / (nx * ny), rem = r - rz * nx * ny, ry = rem / nx, rx = rem - ry * nx;
-        const int gx = x0 + rx, gy = y0 + ry, gz = z0 + rz;
-        // (an owned row starts from its direct sum; jofs > 0: an upper ghost
-        // node, its sums to the reverse halo's buffer from 0)
-        const int64_t j = gx + (int64_t)Lx * gy + Lxy * gz - jofs;
-        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-        if (jofs == 0) {
-            s0 = y[3 * j];
-            s1 = y[3 * j + 1];
-            s2 = y[3 * j + 2];
-        }
-        // The listed regions holding the row (about 2 of up to BG_MAXNB: the
-        // tests are LDS reads), up to GK of them with their loads in flight at
-        // once, summed in brick order; more (never on a box of element-wide
-        // bricks: at most 3 x 3 x 2) in further rounds.
-        constexpr int GK = 8;
-        for (int q = 0; q < nq;) {
-            const double *pp[GK];
-            int RNs[GK], k = 0;
-            for (; q < nq && k < GK; ++q) {
-                const int *o = nbd + 8 * q;
-                const int lx = gx - o[0], ly = gy - o[1], lz = gz - o[2], RX = o[3], RY = o[4], RZ = o[5];
-                if (lx >= 0 && lx < RX && ly >= 0 && ly < RY && lz >= 0 && lz < RZ) {
-                    const int64_t wo = (int64_t)(unsigned)o[6] | ((int64_t)o[7] << 32);
-                    const double *p = ws + wo + lx + RX * (ly + RY * lz);
-#pragma unroll
-                    for (int u = 0; u < GK; ++u)  // (selects: the slots stay in registers)
-                        if (u == k) {
-                            pp[u] = p;
-                            RNs[u] = RX * RY * RZ;
-                        }
-                    ++k;
-                }
-            }
-            double a[GK][3];
-#pragma unroll
-            for (int u = 0; u < GK; ++u)
-                if (u < k)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) a[u][c] = pp[u][c * RNs[u]];
-#pragma unroll
-            for (int u = 0; u < GK; ++u)
-                if (u < k) {
-                    s0 += a[u][0];
-                    s1 += a[u][1];
-                    s2 += a[u][2];
-                }
-        }
-        y[3 * j] = s0;
-        y[3 * j + 1] = s1;
-        y[3 * j + 2] = s2;
-        if (xdot) dsum += s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
-    }
-    if (xdot) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
-        if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;
-    }
-    __syncthreads();
-    if (xdot && threadIdx.x == 0) {
-        double t = 0.0;
-        for (int q = 0; q < NT / 64; ++q) t += dred[q];  // (waves in order)
-        dpart[dslot >= 0 ? dslot : O] = t;
-    }
-}
 
 template <int WV, int D>
 __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp,
@@ -421,36 +325,17 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     if (D == 2) sym_wait9<0>(v2);
     __syncthreads();
     KLE_PROBE_TS(ts2)
-    // 4. the region's transposed sums, once (nodes off the lattice are never read)
+    // 4. the region's transposed sums, once, [entry][3] (coalesced; nodes
+    // off the lattice are never read)
     double *dst = ws + wsoff;
-    for (int k = threadIdx.x; k < RN; k += NT) {
+    for (int t = threadIdx.x; t < 3 * RN; t += NT) {
+        const int k = t / 3, c = t - 3 * k;
         const int rz = k / (RX * RY), rem = k - rz * RX * RY, ry = rem / RX, rx = rem - ry * RX;
         const int gx = ox + rx, gy = oy + ry, gz = oz + rz;
         if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) dst[c * RN + k] = fx_to_d(acc[c * RS + k]) * T1 * T2;
+        dst[t] = fx_to_d(acc[c * RS + k]) * T1 * T2;
     }
     KLE_PROBE_TS_END(b, ts0, ts1, ts2)
-}
-
-// y_j = the region sums of the bricks whose regions hold row j, in ascending
-// brick order (brick_reduce), after the brick kernel.
-// Workgroup (brick b, part s) takes b's owned rows [256 s, 256 s + 256);
-// with xdot its (y, x) partial goes to dpart[b * parts + s].
-__global__ __launch_bounds__(256) void k_nb_sym_brick_gather(int Lx, int Ly, int parts, int b0,
-                                                             const int *__restrict__ nbrec,
-                                                             const double *__restrict__ ws, double *__restrict__ y,
-                                                             int64_t jofs, const int *__restrict__ istate,
-                                                             const double *__restrict__ xdot,
-                                                             double *__restrict__ dpart)
-{
-    __shared__ double dred[4];
-    __shared__ int rec[BG_REC];
-    const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;
-    if (stop) return;  // (uniform)
-    const int b = b0 + (int)blockIdx.x / parts, s = (int)blockIdx.x % parts;
-    brick_reduce<256>(b, Lx, Ly, nbrec, ws, y, xdot, dpart, rec, dred, 256 * s, 256 * s + 256,
-                      (int)blockIdx.x, jofs);
 }
 
 // y[0 .. n) += r: the lower neighbour's sums for this slab's lowest nodes
@@ -576,7 +461,6 @@ int brick_finish(kle_mat *A, void *plan)
     std::vector<int> hmu(n, 0);
     bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NT) != hipSuccess ||
                  hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
-                 hipMalloc(&A->d_bnb, sizeof(int) * BG_REC * (size_t)NT) != hipSuccess ||
                  (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
                  (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
                  hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
@@ -604,33 +488,61 @@ int brick_finish(kle_mat *A, void *plan)
     KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NT, hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_browd, bp->rowd.data(), sizeof(int) * bp->rowd.size(), hipMemcpyHostToDevice));
     {
-        // the gather's records (BG_REC)
-        std::vector<int> rec((size_t)BG_REC * NT, 0);
-        for (int q = 0; q < NT; ++q) {
+        // the gather's runs (kle_sym.hip gsym_gather, the graph kernels'
+        // gather): per 64-row slice of [owned | upper ghost planes] in lattice
+        // order, per real brick in ascending order, each stretch of one
+        // lattice line that the brick's region holds -- consecutive region
+        // entries ([entry][3] at wsoff) -- as (first sum, 64-bit row mask)
+        const int64_t Lx = A->row_lat[0], Ly = A->row_lat[1], Lz = A->row_lat[2];
+        const int64_t p3 = 3 * Lx * Ly;
+        const int64_t zo = A->ghost_lo / p3, hp = A->ghost_hi / p3;
+        const int64_t ntot = n + hp * Lx * Ly, ns = (ntot + 63) / 64;
+        std::vector<std::vector<std::pair<int64_t, unsigned long long>>> sr(ns);
+        for (int q = 0; q < NB; ++q) {
             const BrickDesc &D = bp->bricks[q];
-            int *o = rec.data() + (size_t)q * BG_REC;
-            const int q0 = bp->nbptr[q], nq = std::min(bp->nbptr[q + 1] - q0, BG_MAXNB);
-            o[0] = nq;
-            o[1] = D.x0;
-            o[2] = D.y0;
-            o[3] = D.z0;
-            o[4] = D.nx;
-            o[5] = D.ny;
-            o[6] = D.nz;
-            for (int k = 0; k < nq; ++k) {
-                const BrickDesc &E = bp->bricks[bp->nblist[q0 + k]];
-                int *e = o + 8 * (k + 1);
-                e[0] = E.ox;
-                e[1] = E.oy;
-                e[2] = E.oz;
-                e[3] = E.RX;
-                e[4] = E.RY;
-                e[5] = E.RZ;
-                e[6] = (int)(E.wsoff & 0xffffffffll);
-                e[7] = (int)(E.wsoff >> 32);
+            for (int rz = 0; rz < D.RZ; ++rz)
+                for (int ry = 0; ry < D.RY; ++ry) {
+                    const int64_t gy = D.oy + ry, gz = D.oz + rz;
+                    if (gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
+                    const int64_t x0 = std::max<int64_t>(D.ox, 0), x1 = std::min<int64_t>(D.ox + D.RX, Lx);
+                    if (x1 <= x0) continue;
+                    const int64_t j0 = x0 + Lx * (gy + Ly * gz), j1 = j0 + (x1 - x0);
+                    const int64_t k0 = (x0 - D.ox) + (int64_t)D.RX * (ry + (int64_t)D.RY * rz);
+                    for (int64_t a = j0; a < j1;) {
+                        const int64_t sl = a >> 6, b2 = std::min(j1, (sl + 1) * 64);
+                        unsigned long long m = 0;
+                        for (int64_t jj = a; jj < b2; ++jj) m |= 1ull << (jj & 63);
+                        sr[sl].push_back({D.wsoff + 3 * (k0 + (a - j0)), m});
+                        a = b2;
+                    }
+                }
+        }
+        std::vector<int> runptr(ns + 1, 0), rstart;
+        std::vector<unsigned long long> rmask;
+        for (int64_t sl = 0; sl < ns; ++sl) {
+            runptr[sl + 1] = runptr[sl] + (int)sr[sl].size();
+            for (auto &r : sr[sl]) {
+                if (r.first > INT_MAX) return fail(KLE_ERR_SUP, "brick sums beyond 2^31 doubles");
+                rstart.push_back((int)r.first);
+                rmask.push_back(r.second);
             }
         }
-        KLE_HIP(hipMemcpy(A->d_bnb, rec.data(), sizeof(int) * rec.size(), hipMemcpyHostToDevice));
+        if (rstart.empty()) {
+            rstart.push_back(0);
+            rmask.push_back(0);
+        }
+        if (hipMalloc(&A->d_sgptr, sizeof(int) * (ns + 1)) != hipSuccess ||
+            hipMalloc(&A->d_sgidx, sizeof(int) * rstart.size()) != hipSuccess ||
+            hipMalloc(&A->d_sgmask, sizeof(unsigned long long) * rmask.size()) != hipSuccess) {
+            (void)hipGetLastError();
+            if (dmu) (void)hipFree(dmu);
+            return fail(KLE_ERR_MEM, "out of device memory for the brick gather runs");
+        }
+        KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
+        KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
+        KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(),
+                          hipMemcpyHostToDevice));
+        A->brick_gparts = (int)(runptr[ns] / std::max<int64_t>(ns, 1));  // (runs per 64 rows, for the log)
     }
     KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
@@ -656,11 +568,6 @@ int brick_finish(kle_mat *A, void *plan)
         A->brick_dims[2] += D.x0 == 0 && D.y0 == 0;
     }
     A->brick_model_us = bp->model_us;
-    {
-        int mr = 0;
-        for (const BrickDesc &D : bp->bricks) mr = std::max(mr, D.nx * D.ny * D.nz);
-        A->brick_gparts = (mr + 255) / 256;
-    }
     A->brick_lds = (int)bp->lds;
     A->sws_entries = bp->ws_entries;
     A->sym_brick = 1;
@@ -718,12 +625,6 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
                            istate KLE_PROBE_ARG);
     };
-    auto gather = [&](int b0, int nb, double *out, int64_t jofs, double *dp, hipStream_t st) {
-        if (nb <= 0) return;
-        hipLaunchKernelGGL(k_nb_sym_brick_gather, dim3((unsigned)(nb * A->brick_gparts)), dim3(256), 0, st,
-                           (int)A->row_lat[0], (int)A->row_lat[1], A->brick_gparts, b0, A->d_bnb,
-                           A->d_sws, out, jofs, istate, dp ? x->d : nullptr, dp);
-    };
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
     // N > 1 (z slabs): the x ghost planes first (every brick's region fill
     // may read them); after the bricks, the upper ghost nodes' sums go to the
@@ -740,13 +641,12 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     else if (g_tune.spmv_brick_waves == 12) go(k_nb_spmv_sym_brick<12, 1>, 3, 12);
     else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0, BRICK_WV);
     KLE_HIP(hipGetLastError());
-    if (!dist) {
-        gather(0, A->nbricks, y->d, 0, dpart, c->stream);
-        KLE_HIP(hipGetLastError());
-        return 0;
-    }
-    gather(A->nbricks, A->nbricks_ghost, A->d_sgsend, A->nrows, nullptr, c->stream);
-    KLE_HIP(hipGetLastError());
+    // the gather (kle_sym.hip gsym_gather): per row its direct sum in y, then
+    // the runs of the regions holding it, in ascending brick order
+    const int64_t n = A->nrows, ntot = n + A->ghost_hi / 3, nlo = n / 64 * 64;
+    if (!dist) return gsym_gather(A, y->d, 0, n, istate, dpart ? x->d : nullptr, dpart, 1, c->stream);
+    // the slices holding upper ghost rows first (their sums: d_sgsend)
+    KLE_TRY(gsym_gather(A, y->d, nlo, ntot, istate, nullptr, nullptr, 1, c->stream));
     const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
     const bool ovl = A->halo_overlap != 0;
     hipStream_t cs = ovl ? c->comm_stream : c->stream;
@@ -756,8 +656,7 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     }
     KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, cs));
     if (ovl) KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
-    gather(0, A->nbricks, y->d, 0, nullptr, c->stream);
-    KLE_HIP(hipGetLastError());
+    KLE_TRY(gsym_gather(A, y->d, 0, nlo, istate, nullptr, nullptr, 1, c->stream));
     if (ovl) KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
     if (nrecv)
         hipLaunchKernelGGL(k_brick_add_recv, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream, nrecv,

@@ -346,6 +346,8 @@ int sval_alloc(kle_mat *A, size_t bytes);
 // a streamed array (matrix values): contiguous first (alloc_contig); 1 if
 // the memory is contiguous, 0 plain, -1 out of memory
 int big_alloc(void **p, size_t bytes);
+int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
+                int preload, hipStream_t st);
 // graph bricks (kle_gbrick.hip)
 int gbrick_bound(kle_mat *A, double vmax_all);
 int gbrick_launch(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);

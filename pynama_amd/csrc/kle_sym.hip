@@ -1031,16 +1031,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
                                                         const double *__restrict__ ws, double *__restrict__ y,
                                                         double *__restrict__ gsend, const int *__restrict__ istate,
                                                         const double *__restrict__ xdot, double *__restrict__ dpart,
-                                                        int preload)
+                                                        int preload, int64_t sl0, int64_t sl1)
 {
     __shared__ double dred[4];
     const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;  // (tested before the first store)
     const int lane = threadIdx.x & 63;
-    const int64_t sl = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t sl = sl0 + (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t j = sl * 64 + lane;
-    if (sl * 64 >= ntot && !xdot) return;
+    const bool on = sl < sl1 && sl * 64 < ntot;  // (the slices [sl0, sl1) of this launch)
+    if (!on && !xdot) return;
     double dsum = 0.0;
-    if (sl * 64 < ntot) {
+    if (on) {
         const unsigned long long below = (1ull << lane) - 1ull;
         double s0 = 0.0, s1 = 0.0, s2 = 0.0;
         const int r1 = runptr[sl + 1];
@@ -1512,17 +1513,30 @@ static int gsym_build(kle_mat *A)
     return done(0);
 }
 
+// The run-mask gather over the rows [r0, r1) of [owned | upper ghosts]
+// (r0 a multiple of 64; rows past the owned ones go to d_sgsend): per row
+// the runs' sums in stored order, plus y first when preload (the rows'
+// direct sums).  One workgroup per 4 slices of 64 rows; with xdot, its
+// (y, x) partial in dpart[workgroup].
+int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
+                int preload, hipStream_t st)
+{
+    if (r1 <= r0) return 0;
+    const int64_t s0 = r0 / 64, s1 = (r1 + 63) / 64, ntot = A->nrows + A->ghost_hi / 3;
+    hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((s1 - s0 + 3) / 4)), dim3(256), 0, st, A->nrows, ntot,
+                       A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y, A->d_sgsend, istate, xdot, dpart, preload,
+                       s0, s1);
+    KLE_HIP(hipGetLastError());
+    return 0;
+}
+
 static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     kle_ctx *c = A->ctx;
     hipStream_t st = c->stream;
     if (A->sym_gbrick && c->nranks == 1) {
         KLE_TRY(gbrick_launch(A, x, y, istate));
-        hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((A->nrows + 255) / 256)), dim3(256), 0, st, A->nrows,
-                           A->nrows, A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate,
-                           dpart ? x->d : nullptr, dpart, 1);
-        KLE_HIP(hipGetLastError());
-        return 0;
+        return gsym_gather(A, y->d, 0, A->nrows, istate, dpart ? x->d : nullptr, dpart, 1, st);
     }
     const int G = A->sym_reg[3], WV = A->sym_reg[4];
     const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2], nhi = A->ghost_hi / 3;
@@ -1604,9 +1618,7 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         KLE_TRY(tiles(1));
     }
     const int64_t ntot = n + (dist ? nhi : 0);
-    hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st, n, ntot, A->d_sgptr,
-                       A->d_sgidx, A->d_sgmask, A->d_sws, y->d, A->d_sgsend, istate, dpart && !dist ? x->d : nullptr,
-                       dpart, A->sym_gbrick);
+    KLE_TRY(gsym_gather(A, y->d, 0, ntot, istate, dpart && !dist ? x->d : nullptr, dpart, A->sym_gbrick, st));
     KLE_HIP(hipGetLastError());
     if (!dist) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending
@@ -2133,7 +2145,7 @@ static void launch_sym_gather(const kle_mat *A, const SymGeo &g, kle_vec *y, int
 
 int sym_dot_parts(const kle_mat *A)
 {
-    if (A->sym_brick) return A->ctx->nranks > 1 ? 0 : A->nbricks * A->brick_gparts;
+    if (A->sym_brick) return A->ctx->nranks > 1 ? 0 : (int)((A->nrows + 255) / 256);
     const bool dist = A->ctx->nranks > 1 && (A->sym_graph || A->lo_rank >= 0 || A->hi_rank >= 0);
     return dist ? 0 : (int)((A->nrows + 255) / 256);
 }
@@ -2212,7 +2224,7 @@ std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_brick)
         return std::string("k_nb_spmv_sym_brick<16,") + std::to_string(g_tune.spmv_brick_ahead) +
-               ">+k_nb_sym_brick_gather";
+               ">+k_nb_gsym_gather";
     if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather";
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
