@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -72,11 +73,11 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int x0 = bd[b].x0, y0 = bd[b].y0, z0 = bd[b].z0, nx = bd[b].nx, ny = bd[b].ny, nz = bd[b].nz;
+    const int NR = bd[b].nr;
     const int ox = bd[b].ox, oy = bd[b].oy, oz = bd[b].oz, RX = bd[b].RX, RY = bd[b].RY, RZ = bd[b].RZ;
     const int rstart = bd[b].rstart, eb = bd[b].eb;
     const long long vbase = bd[b].vbase, wsoff = bd[b].wsoff;
-    const int RN = RX * RY * RZ, RS = RN + 64, NR = nx * ny * nz;
+    const int RN = RX * RY * RZ, RS = RN + 64, RXY = RX * RY;
     double *xl = lds;
     unsigned long long *acc = reinterpret_cast<unsigned long long *>(lds + 3 * RN);
     double *wred = lds + 3 * RN + 3 * RS;
@@ -304,8 +305,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
                 // sums to it, so an identity (Dirichlet) row returns x bit for
                 // bit (8 MB of stores at config 2: the only ones before the end)
                 wsum3_dpp(acc0, acc1, acc2);
-                const int rz = it.r / (nx * ny), rem = it.r - rz * nx * ny, ry = rem / nx, rx = rem - ry * nx;
-                const int64_t j = (x0 + rx) + (int64_t)Lx * (y0 + ry) + Lxy * (z0 + rz);
+                // (the row's lattice node from its region index: bricks may be
+                // ragged, kle_brick_plan.cpp)
+                const int irz = it.ir / RXY, irem = it.ir - irz * RXY, iry = irem / RX, irx = irem - iry * RX;
+                const int64_t j = (ox + irx) + (int64_t)Lx * (oy + iry) + Lxy * (oz + irz);
                 if (lane < 3) y[3 * j + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
                 acc0 = acc1 = acc2 = 0.0;
             }
@@ -357,7 +360,8 @@ __global__ void k_brick_add_recv(int64_t n, const double *__restrict__ r, double
 __global__ __launch_bounds__(256) void k_brick_bound(int Lx, int Ly, int Lz, int zo, int hp,
                                                      const BrickDesc *__restrict__ bd, const int *__restrict__ rowbox,
                                                      const int *__restrict__ smu, const int64_t *__restrict__ svptr,
-                                                     const double *__restrict__ sval, int P, int *__restrict__ ebo)
+                                                     const double *__restrict__ sval, int P,
+                                                     const int *__restrict__ owner, int *__restrict__ ebo)
 {
     __shared__ double wred[256];
     const int b = blockIdx.x;
@@ -375,6 +379,7 @@ __global__ __launch_bounds__(256) void k_brick_bound(int Lx, int Ly, int Lz, int
             for (int iy = max(D.y0, gy - P); iy <= min(D.y0 + D.ny - 1, gy + P); ++iy)
                 for (int ix = max(D.x0, gx - P); ix <= min(D.x0 + D.nx - 1, gx + P); ++ix) {
                     const int64_t i = ix + (int64_t)Lx * iy + Lxy * iz;
+                    if (owner[i] != b) continue;  // (a ragged brick's bounding box holds others' rows)
                     const int64_t base = rowbox[2 * i];
                     const int d = rowbox[2 * i + 1];
                     const int bze = (int)(base / Lxy), by = (int)((base - bze * Lxy) / Lx);
@@ -396,7 +401,7 @@ __global__ __launch_bounds__(256) void k_brick_bound(int Lx, int Ly, int Lz, int
                     }
                     s += bmax;
                 }
-        if (gx >= D.x0 && gx < D.x0 + D.nx && gy >= D.y0 && gy < D.y0 + D.ny && gz >= D.z0 && gz < D.z0 + D.nz) {
+        if (gz < Lz && owner[gx + (int64_t)Lx * gy + Lxy * gz] == b) {
             // the row's own direct sum
             const int64_t j = gx + (int64_t)Lx * gy + Lxy * gz;
             const int mu = smu[j];  // (stored blocks of row j)
@@ -435,10 +440,15 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
 {
     auto *bp = new BrickPlan;
     bp->pad = g_tune.spmv_brick_pad;
+    bp->bands = g_tune.spmv_brick_bands;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
-    why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
-                     std::max(1, A->ctx->num_cus),
-                     g_tune.spmv_brick_max, g_tune.spmv_brick_rounds, g_tune.spmv_brick_split, cnt, srow, P, *bp);
+    try {  // (no exception may cross the C ABI: a planner failure is a refusal)
+        why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
+                         std::max(1, A->ctx->num_cus), g_tune.spmv_brick_max, g_tune.spmv_brick_rounds,
+                         g_tune.spmv_brick_split, cnt, srow, P, *bp);
+    } catch (const std::exception &e) {
+        why = std::string("brick planner: ") + e.what();
+    }
     if (!why.empty()) {
         delete bp;
         *plan_out = nullptr;
@@ -458,13 +468,14 @@ int brick_finish(kle_mat *A, void *plan)
     const int NT = (int)bp->bricks.size(), NB = bp->nreal;  // (all pieces; the bricks with rows)
     const int64_t n = A->nrows;
     int *dmu = nullptr;
-    std::vector<int> hmu(n, 0);
+    std::vector<int> hmu(2 * n, 0);  // stored blocks per row | owning brick per row
+    int *howner = hmu.data() + n;
     bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NT) != hipSuccess ||
                  hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
                  (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
                  (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
                  hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
-                 hipMalloc(&A->d_stile_e, sizeof(int) * NB) != hipSuccess || hipMalloc(&dmu, sizeof(int) * n) != hipSuccess;
+                 hipMalloc(&A->d_stile_e, sizeof(int) * NB) != hipSuccess || hipMalloc(&dmu, sizeof(int) * 2 * n) != hipSuccess;
     (void)hipGetLastError();
     if (nomem) {
         if (dmu) (void)hipFree(dmu);
@@ -475,13 +486,14 @@ int brick_finish(kle_mat *A, void *plan)
     {
         for (int q = 0; q < NB; ++q) {
             const BrickDesc &D = bp->bricks[q];
-            for (int r = 0; r < D.nx * D.ny * D.nz; ++r) {
-                const int d = bp->rowd[2 * ((int64_t)D.rstart + r)];
+            for (int r = 0; r < D.nr; ++r) {
+                const int64_t rr = (int64_t)D.rstart + r;
+                const int d = bp->rowd[2 * rr];
                 const int dbx = d & 15, dby = (d >> 4) & 15, dbz = (d >> 8) & 15;
                 const int bnx = (d >> 12) & 15, bny = (d >> 16) & 15, bnz = (d >> 20) & 15;
-                const int rz = r / (D.nx * D.ny), rem = r - rz * D.nx * D.ny, ry = rem / D.nx, rx = rem - ry * D.nx;
-                const int64_t i = (D.x0 + rx) + A->row_lat[0] * ((D.y0 + ry) + A->row_lat[1] * (int64_t)(D.z0 + rz));
+                const int64_t i = brick_ir_node(D, brick_row_ir(bp->rowd.data(), rr), A->row_lat[0], A->row_lat[1]);
                 hmu[i] = bnx * bny * bnz - (dbx + bnx * (dby + bny * dbz));
+                howner[i] = q;
             }
         }
     }
@@ -544,12 +556,12 @@ int brick_finish(kle_mat *A, void *plan)
                           hipMemcpyHostToDevice));
         A->brick_gparts = (int)(runptr[ns] / std::max<int64_t>(ns, 1));  // (runs per 64 rows, for the log)
     }
-    KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice));
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
     hipLaunchKernelGGL(k_brick_bound, dim3((unsigned)NB), dim3(256), 0, c->stream, (int)A->row_lat[0],
                        (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, reinterpret_cast<const BrickDesc *>(A->d_bdesc),
-                       A->d_rowbox, dmu, A->d_svptr, A->d_sval, A->sym_P, A->d_stile_e);
+                       A->d_rowbox, dmu, A->d_svptr, A->d_sval, A->sym_P, dmu + n, A->d_stile_e);
     KLE_HIP(hipGetLastError());
     // the exponents into the descriptors
     std::vector<int> eb(NB);

@@ -8,17 +8,31 @@
 
 namespace kle {
 
-// per brick (device, 64 B): owned box in owned-lattice coordinates, the
-// region (bounding box of its rows' upper triangles; z in owned coordinates),
-// its first row descriptor, the bound exponent of its fixed-point sums, where
-// its values and its region sums live
+// per brick (device, 80 B): the bounding box of its rows in owned-lattice
+// coordinates (a box, or a ragged band piece whose first and last x planes /
+// y lines are partial), its row count, the region (bounding box of its rows'
+// upper triangles; z in owned coordinates), its first row descriptor, the
+// bound exponent of its fixed-point sums, where its values and its region
+// sums live
 struct BrickDesc {
     int x0, y0, z0, nx, ny, nz;
     int ox, oy, oz, RX, RY, RZ;
-    int rstart, eb;
+    int rstart, eb, nr, pad_;
     long long vbase, wsoff;
 };
-static_assert(sizeof(BrickDesc) == 72, "BrickDesc layout");
+static_assert(sizeof(BrickDesc) == 80, "BrickDesc layout");
+
+// a row descriptor's region index (the low and high bytes of its two words)
+inline int brick_row_ir(const int *rowd, int64_t r)
+{
+    return ((rowd[2 * r] >> 24) & 255) | (((rowd[2 * r + 1] >> 24) & 255) << 8);
+}
+// the owned-lattice node of region index ir of brick D
+inline int64_t brick_ir_node(const BrickDesc &D, int ir, int64_t Lx, int64_t Ly)
+{
+    const int rxy = D.RX * D.RY, rz = ir / rxy, rem = ir - rz * rxy, ry = rem / D.RX, rx = rem - ry * D.RX;
+    return (D.ox + rx) + Lx * ((D.oy + ry) + Ly * (int64_t)(D.oz + rz));
+}
 
 constexpr int BRICK_WV = 16;            // waves per brick workgroup (one workgroup per CU)
 constexpr size_t BRICK_LDS_CAP = 163840;  // LDS per CU
@@ -32,11 +46,11 @@ struct BrickPlan {
     int nreal = 0;
     std::vector<int> rowd;      // 2 ints per row, brick order
     std::vector<int64_t> svb;   // per row (natural index): first double of its values, brick layout
-    std::vector<int> nbptr, nblist;  // per brick: the bricks whose regions meet its rows (ascending)
     int64_t ws_doubles = 0, ws_entries = 0;
     size_t lds = 0;
     double model_us = 0.0;  // the planner's time model of the product (us)
     int pad = 0;            // (in) doubles of gap before each brick's values (spmv_brick_pad)
+    int bands = 1;          // (in) try the ragged-band generator (spmv_brick_bands)
 };
 
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their
@@ -52,11 +66,6 @@ struct GBrickDesc {
 };
 // dictionary entries a graph brick may hold (brick_lds <= BRICK_LDS_CAP)
 constexpr int GB_UCAP = (int)((BRICK_LDS_CAP - 2048) / 48);
-constexpr int BG_MAXNB = 64;  // bricks whose regions meet one brick's rows (27 in a regular grid)
-// the gather's record per brick: a header (listed regions, the brick's own
-// box: nq, x0, y0, z0, nx, ny, nz, 0) and per listed region (ascending
-// brick order) ox, oy, oz, RX, RY, RZ and its workspace offset (2 ints)
-constexpr int BG_REC = 8 * (BG_MAXNB + 1);
 
 // bricks for the owned Lx x Ly x Lz lattice of a rank (rows x-fastest; per
 // row its block count and packed box, kle_sym.hip srow; hp upper ghost

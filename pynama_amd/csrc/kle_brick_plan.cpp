@@ -160,22 +160,20 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     struct Box {
         int x0, x1, y0, y1, z0, z1;
     };
-    std::vector<Box> best;
-    auto consider = [&](const std::vector<Box> &bx, const std::vector<double> &w, int64_t ent) {
+    // a brick: its rows (lattice indices) in streaming order; boxes and the
+    // ragged bands below are both given this way
+    std::vector<std::vector<int64_t>> best;
+    auto box_rows = [&](const Box &B) {
+        std::vector<int64_t> r;
+        r.reserve((size_t)(B.x1 - B.x0) * (B.y1 - B.y0) * (B.z1 - B.z0));
+        for (int z = B.z0; z < B.z1; ++z)
+            for (int y = B.y0; y < B.y1; ++y)
+                for (int x = B.x0; x < B.x1; ++x) r.push_back(x + (int64_t)Lx * y + Lxy * z);
+        return r;
+    };
+    auto consider_rows = [&](std::vector<std::vector<int64_t>> &&bx, const std::vector<double> &w, int64_t ent) {
         const double t = model(w);
         if (t < best_t * 0.999 || (t <= best_t * 1.001 && ent < best_ent)) {
-            // (the gather stages at most BG_MAXNB neighbouring regions per brick)
-            for (const Box &B : bx) {
-                int o, RX, RY, RZ, ox, oy, oz, nb = 0;
-                (void)o;
-                for (const Box &E : bx) {
-                    region(xlo, xhi, E.x0, E.x1, ox, RX);
-                    region(ylo, yhi, E.y0, E.y1, oy, RY);
-                    region(zlo_none, zhi, E.z0, E.z1, oz, RZ);
-                    nb += ox < B.x1 && B.x0 < ox + RX && oy < B.y1 && B.y0 < oy + RY && oz < B.z1 && B.z0 < oz + RZ;
-                }
-                if (nb > BG_MAXNB) return;
-            }
             best_t = t;
             best_ent = ent;
             // (dispatch order: the heaviest brick first)
@@ -183,8 +181,29 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
             for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
             std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return w[a] > w[b]; });
             best.clear();
-            for (int k : ord) best.push_back(bx[k]);
+            for (int k : ord) best.push_back(std::move(bx[k]));
         }
+    };
+    auto consider = [&](const std::vector<Box> &bx, const std::vector<double> &w, int64_t ent) {
+        const double t = model(w);
+        if (t < best_t * 0.999 || (t <= best_t * 1.001 && ent < best_ent)) {
+            std::vector<std::vector<int64_t>> r;
+            for (const Box &B : bx) r.push_back(box_rows(B));
+            consider_rows(std::move(r), w, ent);
+        }
+    };
+    // the region of a row set: the bounding box of its rows' reach
+    auto row_region = [&](const std::vector<int64_t> &rows, int &ox, int &RX, int &oy, int &RY, int &oz, int &RZ) {
+        int x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN, z0 = INT_MAX, z1 = INT_MIN;
+        for (int64_t i : rows) {
+            const int z = (int)(i / Lxy), y = (int)((i % Lxy) / Lx), x = (int)(i % Lx);
+            x0 = std::min(x0, x), x1 = std::max(x1, x + 1);
+            y0 = std::min(y0, y), y1 = std::max(y1, y + 1);
+            z0 = std::min(z0, z), z1 = std::max(z1, z + 1);
+        }
+        region(xlo, xhi, x0, x1, ox, RX);
+        region(ylo, yhi, y0, y1, oy, RY);
+        region(zlo_none, zhi, z0, z1, oz, RZ);
     };
     // (fs: forced split counts nbx + 100 nby + 10000 nbz; + 1000000: cuts by
     // equal node counts only; + 10000000: weighted cuts at any node only)
@@ -431,6 +450,211 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
             if (fits) consider(bx, w, ent);
         }
     }
+    // Ragged bands inside z slabs of one or two element layers (slab brick
+    // counts by weight, largest remainders): the slab's (y, z) lines in
+    // y-major order are cut into bands of c bricks each at line granularity
+    // (cumulative weight), and a band's rows in x-major order into its c
+    // bricks at row granularity -- every brick of a slab within a row of the
+    // slab's mean weight.  (bp.bands 0: not tried.)  A brick's region grows by at most one node along x
+    // and y over an exact box (its first and last x planes and y lines may be
+    // partial).  The box plans' heaviest brick sets the kernel's time: at
+    // config 2 1.057 x the mean, and the measured loop time of each brick
+    // follows its planned weight with correlation 0.98
+    // (profiles/r05/phase_bricks_weights.txt).
+    if (fs == 0 && bp.bands) {
+        for (int t = 1; t <= 2; ++t) {
+            const int ns = std::max(1, ez / t);
+            std::vector<int> cz;
+            if (!split_axis(uz, ns, P, cz) || ns > nmax) continue;
+            const double W = box_sum(0, Lx, 0, Ly, 0, Lz);
+            std::vector<int> nsl(ns);
+            std::vector<std::pair<double, int>> rem;
+            int tot = 0;
+            for (int sl = 0; sl < ns; ++sl) {
+                const double q = box_sum(0, Lx, 0, Ly, cz[sl], cz[sl + 1]) / W * nmax;
+                nsl[sl] = std::max(1, (int)q);
+                tot += nsl[sl];
+                rem.push_back({q - (int)q, sl});
+            }
+            std::sort(rem.rbegin(), rem.rend());
+            for (size_t k = 0; k < rem.size() && tot < nmax; ++k, ++tot) ++nsl[rem[k].second];
+            if (tot > nmax) continue;
+            // per slab: bands of whole y lines, band (ya, yb) with c bricks cut
+            // from its rows in x-major order at row granularity; the bands and
+            // their brick counts by dynamic programming over y (the heaviest
+            // band brick W(ya, yb) / c smallest), among those whose bricks'
+            // regions fit the LDS (x cuts estimated at plane granularity, then
+            // checked exactly)
+            std::vector<std::vector<int64_t>> bx;
+            std::vector<double> w;
+            int64_t ent = 0;
+            bool all = true;
+            constexpr int CMAX = 12;
+            struct SlabDP {
+                int kmax = 0;
+                std::vector<double> dp;
+                std::vector<int> from, fc;
+            };
+            std::vector<SlabDP> sdp(ns);
+            for (int sl = 0; sl < ns && all; ++sl) {
+                const int z0 = cz[sl], z1 = cz[sl + 1], k = nsl[sl] + 4;
+                int oz, RZ;
+                region(zlo_none, zhi, z0, z1, oz, RZ);
+                // fits[ya][yb][c]
+                auto fidx = [&](int ya, int yb, int c) { return ((size_t)ya * (Ly + 1) + yb) * (CMAX + 1) + c; };
+                std::vector<char> fit((size_t)(Ly + 1) * (Ly + 1) * (CMAX + 1), 0);
+                std::vector<double> px(Lx + 1);
+                for (int ya = 0; ya < Ly; ++ya)
+                    for (int yb = ya + 1; yb <= Ly; ++yb) {
+                        int oy, RY;
+                        region(ylo, yhi, ya, yb, oy, RY);
+                        for (int x = 0; x < Lx; ++x) px[x + 1] = px[x] + box_sum(x, x + 1, ya, yb, z0, z1);
+                        for (int c = 1; c <= CMAX; ++c) {
+                            bool ok = true;
+                            for (int q = 0; q < c && ok; ++q) {
+                                const double ta = px[Lx] * q / c, tb = px[Lx] * (q + 1) / c;
+                                int xa = (int)(std::upper_bound(px.begin(), px.end(), ta) - px.begin()) - 1;
+                                int xb = (int)(std::lower_bound(px.begin(), px.end(), tb) - px.begin());
+                                xa = std::max(0, std::min(xa, Lx - 1));
+                                xb = std::max(xa + 1, std::min(xb, Lx));
+                                int ox, RX;
+                                region(xlo, xhi, xa, xb, ox, RX);
+                                const int RN = RX * RY * RZ;
+                                ok = RN <= 65535 && brick_lds(RN) <= BRICK_LDS_CAP;
+                            }
+                            fit[fidx(ya, yb, c)] = ok;
+                        }
+                    }
+                // dp[y][kk]: the lightest heaviest brick covering lines [0, y) with kk bricks
+                SlabDP &S = sdp[sl];
+                S.kmax = k;
+                S.dp.assign((size_t)(Ly + 1) * (k + 1), 1e300);
+                S.from.assign((size_t)(Ly + 1) * (k + 1), -1);
+                S.fc.assign((size_t)(Ly + 1) * (k + 1), 0);
+                S.dp[0] = 0.0;
+                for (int yb = 1; yb <= Ly; ++yb)
+                    for (int ya = 0; ya < yb; ++ya) {
+                        const double Wb = box_sum(0, Lx, ya, yb, z0, z1);
+                        const int64_t brows = (int64_t)Lx * (yb - ya) * (z1 - z0);
+                        for (int c = 1; c <= CMAX; ++c) {
+                            if (!fit[fidx(ya, yb, c)] || brows < c) continue;  // (at least a row per brick)
+                            for (int kk = c; kk <= k; ++kk) {
+                                const double prev = S.dp[(size_t)ya * (k + 1) + kk - c];
+                                if (prev >= 1e300) continue;
+                                const double v = std::max(prev, Wb / c);
+                                double &cur = S.dp[(size_t)yb * (k + 1) + kk];
+                                if (v < cur) {
+                                    cur = v;
+                                    S.from[(size_t)yb * (k + 1) + kk] = ya;
+                                    S.fc[(size_t)yb * (k + 1) + kk] = c;
+                                }
+                            }
+                        }
+                    }
+            }
+            // brick counts per slab: the smallest threshold T on the heaviest
+            // brick such that every slab's fewest bricks with dp <= T sum to at
+            // most nmax (dp need not fall monotonically with the count)
+            std::vector<int> kc(ns, 0);
+            if (all) {
+                std::vector<double> cand;
+                for (int sl = 0; sl < ns; ++sl)
+                    for (int kk = 1; kk <= sdp[sl].kmax; ++kk) {
+                        const double v = sdp[sl].dp[(size_t)Ly * (sdp[sl].kmax + 1) + kk];
+                        if (v < 1e300) cand.push_back(v);
+                    }
+                std::sort(cand.begin(), cand.end());
+                cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+                auto counts = [&](double T, std::vector<int> &out) {
+                    int tot = 0;
+                    for (int sl = 0; sl < ns; ++sl) {
+                        const SlabDP &S = sdp[sl];
+                        int kk = 1;
+                        while (kk <= S.kmax && S.dp[(size_t)Ly * (S.kmax + 1) + kk] > T) ++kk;
+                        if (kk > S.kmax) return INT_MAX;
+                        out[sl] = kk;
+                        tot += kk;
+                    }
+                    return tot;
+                };
+                size_t lo = 0, hi = cand.size();
+                std::vector<int> tmp(ns);
+                while (lo < hi) {
+                    const size_t mid = (lo + hi) / 2;
+                    if (counts(cand[mid], tmp) <= nmax) hi = mid;
+                    else lo = mid + 1;
+                }
+                if (lo == cand.size() || counts(cand[lo], kc) > nmax) {
+                    all = false;
+                    if (getenv("KLE_BRICK_DEBUG")) fprintf(stderr, "bands t=%d: no slab counts within %d bricks\n", t, nmax);
+                }
+            }
+            for (int sl = 0; sl < ns && all; ++sl) {
+                const int z0 = cz[sl], z1 = cz[sl + 1], k = kc[sl];
+                const SlabDP &S = sdp[sl];
+                const int K1 = S.kmax + 1;
+                std::vector<std::pair<std::pair<int, int>, int>> bands;
+                for (int yb = Ly, kk = k; yb > 0;) {
+                    const int ya = S.from[(size_t)yb * K1 + kk], c = S.fc[(size_t)yb * K1 + kk];
+                    bands.push_back({{ya, yb}, c});
+                    kk -= c;
+                    yb = ya;
+                }
+                std::reverse(bands.begin(), bands.end());
+                if (getenv("KLE_BRICK_DEBUG")) {
+                    fprintf(stderr, "bands t=%d slab %d: %d bricks, heaviest %.4g, bands", t, sl, k,
+                            S.dp[(size_t)Ly * K1 + k]);
+                    for (const auto &bd2 : bands) fprintf(stderr, " [%d,%d)x%d", bd2.first.first, bd2.first.second, bd2.second);
+                    fprintf(stderr, "\n");
+                }
+                for (const auto &bd2 : bands) {
+                    const int ya = bd2.first.first, yb = bd2.first.second, c = bd2.second;
+                    std::vector<int64_t> rows;
+                    rows.reserve((size_t)Lx * (yb - ya) * (z1 - z0));
+                    for (int x = 0; x < Lx; ++x)
+                        for (int y = ya; y < yb; ++y)
+                            for (int z = z0; z < z1; ++z) rows.push_back(x + (int64_t)Lx * y + Lxy * z);
+                    std::vector<double> rp(rows.size() + 1, 0.0);
+                    for (size_t r = 0; r < rows.size(); ++r) rp[r + 1] = rp[r] + row_cost(mu[rows[r]]);
+                    if (rows.size() < (size_t)c) {
+                        all = false;
+                        break;
+                    }
+                    size_t r0 = 0;
+                    for (int q = 0; q < c && all; ++q) {
+                        size_t r1 = rows.size();
+                        if (q < c - 1) {
+                            const double tg = rp.back() * (q + 1) / c;
+                            r1 = std::lower_bound(rp.begin(), rp.end(), tg) - rp.begin();
+                            r1 = std::max(r1, r0 + 1);
+                            r1 = std::min(r1, rows.size() - (size_t)(c - 1 - q));
+                        }
+                        std::vector<int64_t> br(rows.begin() + r0, rows.begin() + r1);
+                        int ox, RX, oy, RY, oz2, RZ2;
+                        row_region(br, ox, RX, oy, RY, oz2, RZ2);
+                        const int RN = RX * RY * RZ2;
+                        if (RN > 65535 || brick_lds(RN) > BRICK_LDS_CAP) {
+                            all = false;
+                            if (getenv("KLE_BRICK_DEBUG"))
+                                fprintf(stderr, "bands t=%d: slab %d band %d..%d: region %d x %d x %d too big\n", t, sl,
+                                        ya, yb, RX, RY, RZ2);
+                        }
+                        ent += RN;
+                        w.push_back(rp[r1] - rp[r0] + 72.0 * RN);
+                        bx.push_back(std::move(br));
+                        r0 = r1;
+                    }
+                }
+            }
+            if (getenv("KLE_BRICK_DEBUG") && all) {
+                double mx = 0, sm = 0;
+                for (double v : w) mx = std::max(mx, v), sm += v;
+                fprintf(stderr, "bands t=%d bricks %zu max/mean %.4f model %.1f\n", t, bx.size(), mx / (sm / w.size()),
+                        model(w) * 1e-6);
+            }
+            if (all && (int)bx.size() <= nmax) consider_rows(std::move(bx), w, ent);
+        }
+    }
         if (nfix > 0) break;
     }
     bp.model_us = best_t * 1e-6;  // (bytes / (TB/s) = us)
@@ -443,76 +667,59 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     int64_t voff = 0, rows = 0, wsd = 0;
     bp.lds = 0;
     bp.ws_entries = 0;
+    std::vector<char> seen(n, 0);
     for (int q = 0; q < NB; ++q) {
-                const Box &B = best[q];
-                BrickDesc &D = bp.bricks[q];
-                D.x0 = B.x0;
-                D.nx = B.x1 - B.x0;
-                D.y0 = B.y0;
-                D.ny = B.y1 - B.y0;
-                D.z0 = B.z0;
-                D.nz = B.z1 - B.z0;
-                region(xlo, xhi, B.x0, B.x1, D.ox, D.RX);
-                region(ylo, yhi, B.y0, B.y1, D.oy, D.RY);
-                region(zlo_none, zhi, B.z0, B.z1, D.oz, D.RZ);
-                const int RN = D.RX * D.RY * D.RZ;
-                D.rstart = (int)rows;
-                D.eb = 0;
-                voff += bp.pad;
-                D.vbase = voff;
-                D.wsoff = wsd;
-                wsd += ((int64_t)3 * RN + 15) & ~int64_t(15);
-                bp.lds = std::max(bp.lds, brick_lds(RN));
-                for (int z = D.z0; z < D.z0 + D.nz; ++z)
-                    for (int y = D.y0; y < D.y0 + D.ny; ++y)
-                        for (int x = D.x0; x < D.x0 + D.nx; ++x) {
-                            const int64_t i = x + (int64_t)Lx * y + Lxy * z;
-                            bp.svb[i] = voff;
-                            const int64_t o = voff - D.vbase;
-                            if ((o >> 4) >= (1 << 24)) return "brick values beyond 2^28 doubles";
-                            const int ir = (x - D.ox) + D.RX * ((y - D.oy) + D.RY * (z - D.oz));
-                            bp.rowd[2 * rows] = (srow[i] & 0xFFFFFF) | ((ir & 255) << 24);
-                            bp.rowd[2 * rows + 1] = (int)((o >> 4) | ((int64_t)((ir >> 8) & 255) << 24));
-                            voff += ((int64_t)mu[i] * 9 + 15) & ~int64_t(15);
-                            ++rows;
-                        }
-                // lattice entries of the region (written by the brick, read by the gather)
-                for (int z = D.oz; z < D.oz + D.RZ; ++z)
-                    for (int y = D.oy; y < D.oy + D.RY; ++y)
-                        for (int x = D.ox; x < D.ox + D.RX; ++x)
-                            bp.ws_entries += x >= 0 && x < Lx && y >= 0 && y < Ly && z >= 0 && z < Lz + hp;
-            }
+        const std::vector<int64_t> &R = best[q];
+        for (int64_t i : R) {  // (each row in exactly one brick, checked before anything is written)
+            if (i < 0 || i >= n || seen[i]) return "bricks overlap or leave the lattice";
+            seen[i] = 1;
+        }
+        BrickDesc &D = bp.bricks[q];
+        row_region(R, D.ox, D.RX, D.oy, D.RY, D.oz, D.RZ);
+        // (the rows' bounding box, informational)
+        int x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN, z0 = INT_MAX, z1 = INT_MIN;
+        for (int64_t i : R) {
+            const int z = (int)(i / Lxy), y = (int)((i % Lxy) / Lx), x = (int)(i % Lx);
+            x0 = std::min(x0, x), x1 = std::max(x1, x + 1);
+            y0 = std::min(y0, y), y1 = std::max(y1, y + 1);
+            z0 = std::min(z0, z), z1 = std::max(z1, z + 1);
+        }
+        D.x0 = x0;
+        D.nx = x1 - x0;
+        D.y0 = y0;
+        D.ny = y1 - y0;
+        D.z0 = z0;
+        D.nz = z1 - z0;
+        D.nr = (int)R.size();
+        const int RN = D.RX * D.RY * D.RZ;
+        D.rstart = (int)rows;
+        D.eb = 0;
+        voff += bp.pad;
+        D.vbase = voff;
+        D.wsoff = wsd;
+        wsd += ((int64_t)3 * RN + 15) & ~int64_t(15);
+        bp.lds = std::max(bp.lds, brick_lds(RN));
+        for (int64_t i : R) {
+            const int z = (int)(i / Lxy), y = (int)((i % Lxy) / Lx), x = (int)(i % Lx);
+            bp.svb[i] = voff;
+            const int64_t o = voff - D.vbase;
+            if ((o >> 4) >= (1 << 24)) return "brick values beyond 2^28 doubles";
+            const int ir = (x - D.ox) + D.RX * ((y - D.oy) + D.RY * (z - D.oz));
+            bp.rowd[2 * rows] = (srow[i] & 0xFFFFFF) | ((ir & 255) << 24);
+            bp.rowd[2 * rows + 1] = (int)((o >> 4) | ((int64_t)((ir >> 8) & 255) << 24));
+            voff += ((int64_t)mu[i] * 9 + 15) & ~int64_t(15);
+            ++rows;
+        }
+        // lattice entries of the region (written by the brick, read by the gather)
+        for (int z = D.oz; z < D.oz + D.RZ; ++z)
+            for (int y = D.oy; y < D.oy + D.RY; ++y)
+                for (int x = D.ox; x < D.ox + D.RX; ++x)
+                    bp.ws_entries += x >= 0 && x < Lx && y >= 0 && y < Ly && z >= 0 && z < Lz + hp;
+    }
+    if (rows != n) return "bricks do not cover the lattice";
     bp.svb[n] = voff;
     bp.ws_doubles = wsd;
-    // per brick, the bricks whose regions meet its owned box (ascending)
-    // N > 1: the upper ghost planes in pieces over the top bricks' footprints
-    // (no rows: the gather sums their region entries into the reverse halo)
     bp.nreal = NB;
-    if (hp > 0)
-        for (int q = 0; q < NB; ++q)
-            if (bp.bricks[q].z0 + bp.bricks[q].nz == Lz) {
-                BrickDesc G = bp.bricks[q];
-                G.z0 = Lz;
-                G.nz = hp;
-                G.RX = G.RY = G.RZ = 0;
-                G.rstart = 0;
-                G.vbase = G.wsoff = 0;
-                bp.bricks.push_back(G);
-            }
-    const int NT = (int)bp.bricks.size();
-    bp.nbptr.assign(NT + 1, 0);
-    bp.nblist.clear();
-    for (int q = 0; q < NT; ++q) {
-        const BrickDesc &D = bp.bricks[q];
-        for (int q2 = 0; q2 < NB; ++q2) {
-            const BrickDesc &E = bp.bricks[q2];
-            const bool meet = E.ox < D.x0 + D.nx && D.x0 < E.ox + E.RX && E.oy < D.y0 + D.ny && D.y0 < E.oy + E.RY &&
-                              E.oz < D.z0 + D.nz && D.z0 < E.oz + E.RZ;
-            if (meet) bp.nblist.push_back(q2);
-        }
-        bp.nbptr[q + 1] = (int)bp.nblist.size();
-        if (bp.nbptr[q + 1] - bp.nbptr[q] > BG_MAXNB) return "a brick's rows meet more than 64 brick regions";
-    }
     bp.lds = std::max(bp.lds, BRICK_LDS_MIN);
     return "";
 }
@@ -556,7 +763,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
                 box(x, Lx, bx, nx);
                 box(y, Ly, by, ny);
                 box(z, Lz, bz, nz);
-                if (dirichlet && (x == 0 || y == 0 || z == 0 || x == Lx - 1 || y == Ly - 1 || z == Lz - 1)) {
+                if (dirichlet == 1 && (x == 0 || y == 0 || z == 0 || x == Lx - 1 || y == Ly - 1 || z == Lz - 1)) {
                     bx = x, by = y, bz = z;
                     nx = ny = nz = 1;
                 }
@@ -569,16 +776,34 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();
+    // every row decodes (descriptor region index -> node) to a distinct node
+    // of the lattice, inside its brick's region (what brick_finish and the
+    // kernel rely on)
+    {
+        std::vector<char> seen(n, 0);
+        for (const BrickDesc &D : bp.bricks)
+            for (int r = 0; r < D.nr; ++r) {
+                const int ir = brick_row_ir(bp.rowd.data(), (int64_t)D.rstart + r);
+                if (ir < 0 || ir >= D.RX * D.RY * D.RZ) return fail(KLE_ERR_SUP, "brick plan: region index out of range");
+                const int64_t i = brick_ir_node(D, ir, Lx, Ly);
+                if (i < 0 || i >= n || seen[i]) return fail(KLE_ERR_SUP, "brick plan: row %lld decodes badly", (long long)i);
+                seen[i] = 1;
+            }
+    }
     double tot = 0.0, mx = 0.0;
-    for (const BrickDesc &D : bp.bricks) {
+    // a brick's weight: its rows' costs (the rows from its descriptors)
+    auto weight = [&](const BrickDesc &D) {
         double w = 0.0;
-        for (int r = 0; r < D.nx * D.ny * D.nz; ++r) {
-            const int rz = r / (D.nx * D.ny), rem = r - rz * D.nx * D.ny, ry = rem / D.nx, rx = rem - ry * D.nx;
-            const int64_t i = (D.x0 + rx) + (int64_t)Lx * ((D.y0 + ry) + (int64_t)Ly * (D.z0 + rz));
+        for (int r = 0; r < D.nr; ++r) {
+            const int64_t i = brick_ir_node(D, brick_row_ir(bp.rowd.data(), (int64_t)D.rstart + r), Lx, Ly);
             const int d = srow[i];
             const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));
             w += row_cost(cnt[i] - k0);
         }
+        return w;
+    };
+    for (const BrickDesc &D : bp.bricks) {
+        const double w = weight(D);
         tot += w;
         mx = std::max(mx, w);
     }
@@ -598,17 +823,8 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     stats[2] = (double)blocks;
     stats[3] = bp.model_us;
     if (getenv("KLE_BRICK_DEBUG"))
-        for (const BrickDesc &D : bp.bricks) {
-            double w = 0.0;
-            for (int r = 0; r < D.nx * D.ny * D.nz; ++r) {
-                const int rz = r / (D.nx * D.ny), rem = r - rz * D.nx * D.ny, ry = rem / D.nx, rx = rem - ry * D.nx;
-                const int64_t i = (D.x0 + rx) + (int64_t)Lx * ((D.y0 + ry) + (int64_t)Ly * (D.z0 + rz));
-                const int d = srow[i];
-                const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));
-                w += row_cost(cnt[i] - k0);
-            }
-            fprintf(stderr, "brick %d %d %d  %d %d %d  region %d %d %d  w %.4f\n", D.x0, D.y0, D.z0, D.nx, D.ny, D.nz,
-                    D.RX, D.RY, D.RZ, w / (tot / NB));
-        }
+        for (const BrickDesc &D : bp.bricks)
+            fprintf(stderr, "brick %d %d %d  %d %d %d  rows %d  region %d %d %d  w %.4f\n", D.x0, D.y0, D.z0, D.nx, D.ny,
+                    D.nz, D.nr, D.RX, D.RY, D.RZ, weight(D) / (tot / NB));
     return 0;
 }

@@ -747,9 +747,15 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_ahead") {
         KLE_ARG(value == 1 || value == 2, "spmv_brick_ahead: 1 or 2");
         g_tune.spmv_brick_ahead = value;
+    } else if (k == "upd_unroll") {
+        KLE_ARG(value == 1 || value == 2, "upd_unroll: 1 or 2");
+        g_tune.upd_unroll = value;
     } else if (k == "spmv_gsym_brick") {
         KLE_ARG(value == 0 || value == 1, "spmv_gsym_brick: 0 or 1");
         g_tune.spmv_gsym_brick = value;
+    } else if (k == "spmv_brick_bands") {
+        KLE_ARG(value == 0 || value == 1, "spmv_brick_bands: 0 or 1");
+        g_tune.spmv_brick_bands = value;
     } else if (k == "spmv_brick_waves") {
         KLE_ARG(value == 8 || value == 12 || value == 16, "spmv_brick_waves: 8, 12 or 16");
         g_tune.spmv_brick_waves = value;
@@ -855,7 +861,9 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "alloc_contig") *value = g_tune.alloc_contig;
     else if (k == "spmv_brick_pad") *value = g_tune.spmv_brick_pad;
     else if (k == "spmv_brick_waves") *value = g_tune.spmv_brick_waves;
+    else if (k == "spmv_brick_bands") *value = g_tune.spmv_brick_bands;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
+    else if (k == "upd_unroll") *value = g_tune.upd_unroll;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
     else if (k == "spmv_sym_align") *value = g_tune.spmv_sym_align;
     else if (k == "spmv_sym_stpol") *value = g_tune.spmv_sym_stpol;

@@ -553,7 +553,7 @@ __device__ __forceinline__ void st_upd(double *p, double v)
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
-template <bool JAC, bool PRE, bool NT = false>
+template <bool JAC, bool PRE, bool NT = false, int SR_UNR = 1>
 __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_iter(int64_t n, const double *__restrict__ dinv,
                                                 const double *__restrict__ w, double *__restrict__ u,
                                                 double *__restrict__ p, double *__restrict__ sv,
@@ -564,14 +564,19 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
 {
     const int G = (int)gridDim.x;
     const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
-    double e[7];  // PRE: first element and stage inputs before the prologue (as k_pipe_iter)
+    // SR_UNR elements of the grid-stride sequence per pass, all their loads
+    // in flight before the first update (upd_unroll; 2: 97 VGPRs, all 4096
+    // waves of config 2 still resident); the elements are summed in the same
+    // order as one at a time (bitwise equal)
+    double e[SR_UNR][7];  // PRE: the first element before the prologue (as k_pipe_iter)
+    auto load = [&](int64_t i, double *f) {
+        f[0] = u[i], f[1] = ld_upd<NT>(p + i), f[2] = ld_upd<NT>(w + i), f[3] = ld_upd<NT>(sv + i);
+        f[4] = ld_upd<NT>(x + i), f[5] = ld_upd<NT>(r + i);
+        f[6] = JAC ? ld_upd<NT>(dinv + i) : 1.0;
+    };
     StageIn in;
     if constexpr (PRE) {
-        if (i0 < n) {
-            e[0] = u[i0], e[1] = ld_upd<NT>(p + i0), e[2] = ld_upd<NT>(w + i0), e[3] = ld_upd<NT>(sv + i0);
-            e[4] = ld_upd<NT>(x + i0), e[5] = ld_upd<NT>(r + i0);
-            e[6] = JAC ? ld_upd<NT>(dinv + i0) : 1.0;
-        }
+        if (i0 < n) load(i0, e[0]);
         if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
     }
     if (ist[I_REASON] != 0) return;
@@ -580,23 +585,28 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
     double alpha, beta;
     if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta, PRE ? &in : nullptr)) return;
     double acc[2] = {0.0, 0.0};
-    for (int64_t i = i0; i < n; i += stride) {
-        if (!PRE || i != i0) {
-            e[0] = u[i], e[1] = ld_upd<NT>(p + i), e[2] = ld_upd<NT>(w + i), e[3] = ld_upd<NT>(sv + i);
-            e[4] = ld_upd<NT>(x + i), e[5] = ld_upd<NT>(r + i);
-            e[6] = JAC ? ld_upd<NT>(dinv + i) : 1.0;
+    for (int64_t ib = i0; ib < n; ib += SR_UNR * stride) {
+#pragma unroll
+        for (int q = 0; q < SR_UNR; ++q) {
+            const int64_t i = ib + q * stride;
+            if (i < n && (!PRE || i != i0)) load(i, e[q]);
         }
-        const double pi = e[0] + beta * e[1];
-        const double si = e[2] + beta * e[3];
-        st_upd<NT>(p + i, pi);
-        st_upd<NT>(sv + i, si);
-        st_upd<NT>(x + i, e[4] + alpha * pi);
-        const double ri = e[5] - alpha * si;
-        st_upd<NT>(r + i, ri);
-        const double ui = JAC ? e[6] * ri : ri;
-        u[i] = ui;
-        acc[0] += ri * ui;
-        acc[1] += ri * ri;
+#pragma unroll
+        for (int q = 0; q < SR_UNR; ++q) {
+            const int64_t i = ib + q * stride;
+            if (i >= n) break;
+            const double pi = e[q][0] + beta * e[q][1];
+            const double si = e[q][2] + beta * e[q][3];
+            st_upd<NT>(p + i, pi);
+            st_upd<NT>(sv + i, si);
+            st_upd<NT>(x + i, e[q][4] + alpha * pi);
+            const double ri = e[q][5] - alpha * si;
+            st_upd<NT>(r + i, ri);
+            const double ui = JAC ? e[q][6] * ri : ri;
+            u[i] = ui;
+            acc[0] += ri * ui;
+            acc[1] += ri * ri;
+        }
     }
     block_sums<2>(acc, pu_out, G);
 }
@@ -1122,8 +1132,10 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                                    k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1], c->d_scal,
                                    c->d_istate, (int)pending, par, k->atol);
             };
-            if (jac && (g_tune.upd_nt == 1 || (g_tune.upd_nt == 2 && n >= 2000000))) go(g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
-            else if (jac) go(g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
+            const bool unr = g_tune.upd_unroll == 2 && g_tune.upd_preload;
+            if (jac && (g_tune.upd_nt == 1 || (g_tune.upd_nt == 2 && n >= 2000000)))
+                go(unr ? k_sr_iter<true, true, true, 2> : g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
+            else if (jac) go(unr ? k_sr_iter<true, true, false, 2> : g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
             else go(g_tune.upd_preload ? k_sr_iter<false, true> : k_sr_iter<false, false>);
             KLE_HIP(hipGetLastError());
             KLE_TRY(c->toc("cg_update", &ev));

@@ -339,3 +339,29 @@ def test_allgather_over_gloo_two_ranks():
         p.join(timeout=60)
     for rank, out, b in res:
         assert out == [{0, 1}, {10, 11}] and b == {"from": 1}, (rank, out, b)
+
+
+@pytest.mark.parametrize("lat,p,ncu,must", [((81, 65, 65), 4, 256, True), ((81, 65, 65), 4, 128, False),
+                                           ((41, 33, 9), 4, 256, True), ((13, 9, 7), 2, 256, True),
+                                           ((41, 33, 33), 4, 128, True), ((25, 21, 13), 6, 64, False),
+                                           ((5, 5, 5), 4, 256, True)])
+def test_brick_planner_covers_the_lattice_and_balances(pa, lat, p, ncu, must):
+    """The box brick planner (kle_brick_plan.cpp, host only): every plan covers
+    the lattice exactly (the planner refuses otherwise), at most ncu bricks,
+    regions within the LDS; at config 2 the ragged-band plan keeps the
+    heaviest brick within 2 % of the mean (the box plans: 5.7 %, and the
+    kernel's time follows the heaviest brick, DESIGN 3 "Bricks")."""
+    lib = pa.load()
+    info = (C.c_int * 8)()
+    st = (C.c_double * 8)()
+    rc = lib.kle_brick_plan_box(lat[0], lat[1], lat[2], p, 1, ncu, 1, 0, info, st)
+    if rc != 0:
+        # (bricks of more rows than one CU-share of config 2, or p = 6: the
+        # regions may not fit the LDS -- the 128-row tiles then)
+        assert not must, (lat, p, ncu)
+        return
+    assert 1 <= info[0] <= ncu
+    assert info[4] <= 163840
+    if lat == (81, 65, 65) and ncu == 256:
+        assert st[0] < 1.02, st[0]
+        assert st[1] < 2.2, st[1]  # (region entries per row)
