@@ -103,6 +103,13 @@ const char *kle_last_error(void);
  * build: at most this many bricks, 0 planned), "spmv_brick_rounds" (read at
  * build: at most this many bricks per CU, default 1), "spmv_brick_split" (read
  * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
+ * "spmv_brick_bands" (read at build: 1 the planner also tries ragged y bands
+ * in z slabs, balanced bricks; 0 default, boxes only), "spmv_brick_pad"
+ * (read at build: doubles of gap before each brick's values; 0 default),
+ * "spmv_brick_waves" (8, 12 or 16 default), "spmv_gsym_brick" (read at
+ * build: graph K on graph bricks, whole rounds per CU; 1 default),
+ * "alloc_contig" (large value arrays from one contiguous allocation; 0
+ * default), "upd_unroll" (CG update kernel: 1 default or 2),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
  * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo

@@ -50,7 +50,7 @@ struct BrickPlan {
     size_t lds = 0;
     double model_us = 0.0;  // the planner's time model of the product (us)
     int pad = 0;            // (in) doubles of gap before each brick's values (spmv_brick_pad)
-    int bands = 1;          // (in) try the ragged-band generator (spmv_brick_bands)
+    int bands = 0;          // (in) try the ragged-band generator (spmv_brick_bands)
 };
 
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their

@@ -630,6 +630,9 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
                             r1 = std::min(r1, rows.size() - (size_t)(c - 1 - q));
                         }
                         std::vector<int64_t> br(rows.begin() + r0, rows.begin() + r1);
+                        // (cut in x-major order for compact bricks, streamed in
+                        // lattice order -- x fastest -- as the boxes are)
+                        std::sort(br.begin(), br.end());
                         int ox, RX, oy, RY, oz2, RZ2;
                         row_region(br, ox, RX, oy, RY, oz2, RZ2);
                         const int RN = RX * RY * RZ2;
@@ -773,6 +776,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
                 blocks += cnt[i] - ((x - bx) + nx * ((y - by) + ny * (z - bz)));
             }
     BrickPlan bp;
+    bp.bands = g_tune.spmv_brick_bands;
     const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();

@@ -406,7 +406,7 @@ struct Tuning {
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
     int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
-    int spmv_brick_bands = 1;  // brick SpMV (read at build): 1 the planner also tries ragged bands (balanced bricks), 0 boxes only
+    int spmv_brick_bands = 0;  // brick SpMV (read at build): 1 the planner also tries ragged bands (balanced bricks; measured no faster), 0 boxes only
     int spmv_brick_pad = 0;    // brick SpMV (read at build): doubles of gap before each brick's values (multiple of 16; experiments)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)
     int spmv_sym_brick = 1;   // box symmetric storage, one rank (read at build): one brick per CU, sums in LDS for the whole stream (kle_brick.hip); 0 the 128-row tiles

@@ -69,6 +69,18 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         np.testing.assert_array_equal((K * x).getArray(), yb)
     finally:
         set_tuning("spmv_brick_ahead", 1)
+    # the ragged-band plans (spmv_brick_bands 1: bricks as row lists, other
+    # regions) -- the same product to rounding
+    set_tuning("spmv_brick_bands", 1)
+    try:
+        K.setOption(K.Option.SPD, True)
+        assert K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
+        ybb = (K * x).getArray().copy()
+    finally:
+        set_tuning("spmv_brick_bands", 0)
+        K.setOption(K.Option.SPD, True)
+    for ref in (y0, yh):
+        _close(ybb, ref)
     set_tuning("spmv_sym_brick", 0)
     try:
         K.setOption(K.Option.SPD, True)
