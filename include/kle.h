@@ -103,7 +103,10 @@ const char *kle_last_error(void);
  * build: at most this many bricks, 0 planned), "spmv_brick_rounds" (read at
  * build: at most this many bricks per CU, default 1), "spmv_brick_split" (read
  * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
- * "spmv_brick_bands" (read at build: 1 the planner also tries ragged y bands
+ * "spmv_brick_tail" / "spmv_brick_tile" (read at build: per mille of the
+ * mean brick cut off every heavier brick into tail tiles of about `tile` per
+ * mille, launched after the bricks; 0 / 20 default), "spmv_brick_bands"
+ * (read at build: 1 the planner also tries ragged y bands
  * in z slabs, balanced bricks; 0 default, boxes only), "spmv_brick_pad"
  * (read at build: doubles of gap before each brick's values; 0 default),
  * "spmv_brick_waves" (8, 12 or 16 default), "spmv_gsym_brick" (read at

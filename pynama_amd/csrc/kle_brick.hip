@@ -441,6 +441,8 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
     auto *bp = new BrickPlan;
     bp->pad = g_tune.spmv_brick_pad;
     bp->bands = g_tune.spmv_brick_bands;
+    bp->tail = g_tune.spmv_brick_tail;
+    bp->tile = g_tune.spmv_brick_tile;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     try {  // (no exception may cross the C ABI: a planner failure is a refusal)
         why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
@@ -465,12 +467,12 @@ int brick_finish(kle_mat *A, void *plan)
 {
     std::unique_ptr<BrickPlan> bp(reinterpret_cast<BrickPlan *>(plan));
     kle_ctx *c = A->ctx;
-    const int NT = (int)bp->bricks.size(), NB = bp->nreal;  // (all pieces; the bricks with rows)
+    const int NB = (int)bp->bricks.size();
     const int64_t n = A->nrows;
     int *dmu = nullptr;
     std::vector<int> hmu(2 * n, 0);  // stored blocks per row | owning brick per row
     int *howner = hmu.data() + n;
-    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NT) != hipSuccess ||
+    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NB) != hipSuccess ||
                  hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
                  (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
                  (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
@@ -497,7 +499,7 @@ int brick_finish(kle_mat *A, void *plan)
             }
         }
     }
-    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NT, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_browd, bp->rowd.data(), sizeof(int) * bp->rowd.size(), hipMemcpyHostToDevice));
     {
         // the gather's runs (kle_sym.hip gsym_gather, the graph kernels'
@@ -569,9 +571,8 @@ int brick_finish(kle_mat *A, void *plan)
     KLE_HIP(hipMemcpy(eb.data(), A->d_stile_e, sizeof(int) * NB, hipMemcpyDeviceToHost));
     (void)hipFree(dmu);
     for (int q = 0; q < NB; ++q) bp->bricks[q].eb = eb[q];
-    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NT, hipMemcpyHostToDevice));
+    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
     A->nbricks = NB;
-    A->nbricks_ghost = NT - NB;
     for (int k = 0; k < 3; ++k) A->brick_dims[k] = 0;
     for (int q = 0; q < NB; ++q) {
         const BrickDesc &D = bp->bricks[q];
@@ -598,7 +599,7 @@ void brick_plan_free(void *plan) { delete reinterpret_cast<BrickPlan *>(plan); }
 
 void brick_drop(kle_mat *A)
 {
-    for (void *q : {A->d_bdesc, (void *)A->d_browd, (void *)A->d_bnb})
+    for (void *q : {A->d_bdesc, (void *)A->d_browd})
         if (q) (void)hipFree(q);
     brick_forget(A);
 }
@@ -607,9 +608,7 @@ void brick_forget(kle_mat *A)
 {
     A->d_bdesc = nullptr;
     A->d_browd = nullptr;
-    A->d_bnb = nullptr;
     A->nbricks = 0;
-    A->nbricks_ghost = 0;
     A->brick_gparts = 0;
     A->brick_dims[0] = A->brick_dims[1] = A->brick_dims[2] = 0;
     A->brick_model_us = 0.0;

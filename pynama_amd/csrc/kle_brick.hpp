@@ -42,8 +42,7 @@ constexpr size_t BRICK_LDS_MIN = 82 * 1024;  // above half the CU's LDS: never t
 // component take the adds of masked lanes) | wave maxima, row counter
 
 struct BrickPlan {
-    std::vector<BrickDesc> bricks;  // nreal bricks, then (N > 1) the ghost pieces the gather sums for the reverse halo
-    int nreal = 0;
+    std::vector<BrickDesc> bricks;  // the bricks (tail tiles last), in launch order
     std::vector<int> rowd;      // 2 ints per row, brick order
     std::vector<int64_t> svb;   // per row (natural index): first double of its values, brick layout
     int64_t ws_doubles = 0, ws_entries = 0;
@@ -51,6 +50,9 @@ struct BrickPlan {
     double model_us = 0.0;  // the planner's time model of the product (us)
     int pad = 0;            // (in) doubles of gap before each brick's values (spmv_brick_pad)
     int bands = 0;          // (in) try the ragged-band generator (spmv_brick_bands)
+    int tail = 0;           // (in) per mille of the mean brick cut off the heavy bricks into tail tiles (spmv_brick_tail)
+    int tile = 20;          // (in) a tail tile's weight, per mille of the mean brick (spmv_brick_tile)
+    int ntail = 0;          // (out) tail tiles (the last ntail bricks)
 };
 
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their

@@ -663,6 +663,75 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     bp.model_us = best_t * 1e-6;  // (bytes / (TB/s) = us)
     (void)total;
     if (best.empty()) return "no brick decomposition fits the LDS";
+    // Tail tiles (bp.tail > 0): every brick heavier than (1 - tail) x the
+    // mean gives the rows past that weight (the end of its streaming order:
+    // x lines of its top plane) to small bricks of about `tile` x the mean,
+    // launched after the bricks.  One brick fills a CU's LDS, so the hardware
+    // dispatches each tile to the first CU of its XCD whose brick has ended:
+    // the CUs of the light bricks take the heavy bricks' tails, and the
+    // kernel ends with the mean brick plus a tile instead of with the
+    // heaviest brick.  A tile is a brick like any other (its region, sums and
+    // gather runs), only small.
+    bp.ntail = 0;
+    if (bp.tail > 0 && best.size() > 1) {
+        const int NB0 = (int)best.size();
+        std::vector<double> wq(NB0, 0.0);
+        double wsum = 0.0;
+        for (int q = 0; q < NB0; ++q) {
+            for (int64_t i : best[q]) wq[q] += row_cost(mu[i]);
+            wsum += wq[q];
+        }
+        const double mean = wsum / NB0, T = mean * (1.0 - 1e-3 * bp.tail), ts = std::max(1e-3 * bp.tile * mean, 1.0);
+        std::vector<std::vector<int64_t>> tiles;
+        for (int q = 0; q < NB0; ++q) {
+            if (wq[q] <= T) continue;
+            std::vector<int64_t> &R = best[q];
+            double w = wq[q];
+            size_t keep = R.size();
+            while (keep > 1 && w - row_cost(mu[R[keep - 1]]) >= T) w -= row_cost(mu[R[--keep]]);
+            if (keep == R.size()) continue;
+            // the cut rows, in streaming order, into nt tiles of about ts
+            // (cuts at the cumulative weights k (cut weight) / nt)
+            const double left = wq[q] - w;
+            const int nt = std::max(1, std::min((int)(R.size() - keep), (int)std::ceil(left / ts - 1e-9)));
+            double cw = 0.0;
+            size_t r = keep;
+            for (int k = 1; k <= nt; ++k) {
+                std::vector<int64_t> t;
+                const double tg = left * k / nt;
+                while (r < R.size() && (k == nt || t.empty() || cw + 0.5 * row_cost(mu[R[r]]) <= tg)) {
+                    cw += row_cost(mu[R[r]]);
+                    t.push_back(R[r++]);
+                }
+                if (t.empty()) continue;
+                std::sort(t.begin(), t.end());
+                tiles.push_back(std::move(t));
+            }
+            R.resize(keep);
+        }
+        // (heaviest tiles first: the last to start are the lightest)
+        std::vector<double> tw(tiles.size(), 0.0);
+        for (size_t k = 0; k < tiles.size(); ++k)
+            for (int64_t i : tiles[k]) tw[k] += row_cost(mu[i]);
+        std::vector<int> ord(tiles.size());
+        for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tw[a] > tw[b]; });
+        bool fits = true;
+        for (int k : ord) {
+            int ox, RX, oy, RY, oz2, RZ2;
+            row_region(tiles[k], ox, RX, oy, RY, oz2, RZ2);
+            if (RX * RY * RZ2 > 65535 || brick_lds(RX * RY * RZ2) > BRICK_LDS_CAP) fits = false;
+        }
+        if (fits) {
+            bp.ntail = (int)tiles.size();
+            for (int k : ord) best.push_back(std::move(tiles[k]));
+        } else {
+            return "tail tiles do not fit the LDS";
+        }
+        if (getenv("KLE_BRICK_DEBUG"))
+            fprintf(stderr, "tail: %d bricks, T %.4f of the mean, %d tiles of ~%.4f\n", NB0, T / mean, bp.ntail,
+                    ts / mean);
+    }
     const int NB = (int)best.size();
     bp.bricks.assign(NB, BrickDesc{});
     bp.rowd.assign(2 * n, 0);
@@ -722,7 +791,6 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     if (rows != n) return "bricks do not cover the lattice";
     bp.svb[n] = voff;
     bp.ws_doubles = wsd;
-    bp.nreal = NB;
     bp.lds = std::max(bp.lds, BRICK_LDS_MIN);
     return "";
 }
@@ -777,6 +845,8 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
             }
     BrickPlan bp;
     bp.bands = g_tune.spmv_brick_bands;
+    bp.tail = g_tune.spmv_brick_tail;
+    bp.tile = g_tune.spmv_brick_tile;
     const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();
@@ -827,8 +897,21 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     stats[2] = (double)blocks;
     stats[3] = bp.model_us;
     if (getenv("KLE_BRICK_DEBUG"))
-        for (const BrickDesc &D : bp.bricks)
-            fprintf(stderr, "brick %d %d %d  %d %d %d  rows %d  region %d %d %d  w %.4f\n", D.x0, D.y0, D.z0, D.nx, D.ny,
-                    D.nz, D.nr, D.RX, D.RY, D.RZ, weight(D) / (tot / NB));
+        for (const BrickDesc &D : bp.bricks) {
+            // (stored blocks, rows of one stored block, rows past one 64-block pass)
+            long long sb = 0;
+            int one = 0, two = 0;
+            for (int r = 0; r < D.nr; ++r) {
+                const int64_t i = brick_ir_node(D, brick_row_ir(bp.rowd.data(), (int64_t)D.rstart + r), Lx, Ly);
+                const int d = srow[i];
+                const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));
+                const int mu = cnt[i] - k0;
+                sb += mu;
+                one += mu == 1;
+                two += mu > 64;
+            }
+            fprintf(stderr, "brick %d %d %d  %d %d %d  rows %d  region %d %d %d  w %.4f  blocks %lld  one %d  multi %d\n",
+                    D.x0, D.y0, D.z0, D.nx, D.ny, D.nz, D.nr, D.RX, D.RY, D.RZ, weight(D) / (tot / NB), sb, one, two);
+        }
     return 0;
 }

@@ -265,11 +265,10 @@ struct kle_mat {
     int sym_gbrick = 0;  // unstructured: graph bricks (d_bdesc = GBrickDesc, d_browd = 4 ints per row)
     int brick_lds_u = 0;  // graph bricks: the largest dictionary
     int nbricks = 0, brick_lds = 0, brick_gparts = 0;  // (gather workgroups per brick)
-    int nbricks_ghost = 0;  // N > 1: upper-ghost pieces after the bricks (gather only: the reverse halo's sums)
     int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
     double brick_model_us = 0.0;    // the planner's modelled product time
     void *d_bdesc = nullptr;
-    int *d_browd = nullptr, *d_bnb = nullptr;  // (d_bnb: the gather's records, BG_REC ints per brick)
+    int *d_browd = nullptr;
     int64_t *d_sbp = nullptr;     // per row: its first stored block in d_slid
     uint16_t *d_slid = nullptr;   // per stored block: its column's position in the group dictionary
     int *d_sdptr = nullptr, *d_sdict = nullptr;  // per group of G rows: sorted distinct stored columns
@@ -406,6 +405,8 @@ struct Tuning {
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
     int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
+    int spmv_brick_tail = 0;   // brick SpMV (read at build): per mille of the mean brick cut off the heavy bricks into tail tiles (0 none)
+    int spmv_brick_tile = 20;  // brick SpMV (read at build): a tail tile's weight, per mille of the mean brick
     int spmv_brick_bands = 0;  // brick SpMV (read at build): 1 the planner also tries ragged bands (balanced bricks; measured no faster), 0 boxes only
     int spmv_brick_pad = 0;    // brick SpMV (read at build): doubles of gap before each brick's values (multiple of 16; experiments)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)

@@ -81,6 +81,21 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         K.setOption(K.Option.SPD, True)
     for ref in (y0, yh):
         _close(ybb, ref)
+    # tail tiles (spmv_brick_tail: the heavy bricks' last rows as small
+    # bricks launched after them) -- the same product to rounding
+    set_tuning("spmv_brick_tail", 30)
+    set_tuning("spmv_brick_tile", 40)
+    try:
+        K.setOption(K.Option.SPD, True)
+        assert K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
+        ybt = (K * x).getArray().copy()
+        np.testing.assert_array_equal((K * x).getArray(), ybt)
+    finally:
+        set_tuning("spmv_brick_tail", 0)
+        set_tuning("spmv_brick_tile", 20)
+        K.setOption(K.Option.SPD, True)
+    for ref in (y0, yh):
+        _close(ybt, ref)
     set_tuning("spmv_sym_brick", 0)
     try:
         K.setOption(K.Option.SPD, True)
