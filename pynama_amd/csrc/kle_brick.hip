@@ -443,6 +443,7 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
     bp->bands = g_tune.spmv_brick_bands;
     bp->tail = g_tune.spmv_brick_tail;
     bp->tile = g_tune.spmv_brick_tile;
+    bp->singles = g_tune.spmv_brick_singles;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     try {  // (no exception may cross the C ABI: a planner failure is a refusal)
         why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
@@ -470,14 +471,17 @@ int brick_finish(kle_mat *A, void *plan)
     const int NB = (int)bp->bricks.size();
     const int64_t n = A->nrows;
     int *dmu = nullptr;
-    std::vector<int> hmu(2 * n, 0);  // stored blocks per row | owning brick per row
+    std::vector<int> hmu(2 * n, 0);  // stored blocks per row | owning brick per row (-1: a one-block row)
     int *howner = hmu.data() + n;
-    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * NB) != hipSuccess ||
+    std::fill(howner, howner + n, -1);
+    for (int64_t i : bp->srows) hmu[i] = 1;
+    bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * std::max(NB, 1)) != hipSuccess ||
                  hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
                  (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
                  (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
                  hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
-                 hipMalloc(&A->d_stile_e, sizeof(int) * NB) != hipSuccess || hipMalloc(&dmu, sizeof(int) * 2 * n) != hipSuccess;
+                 hipMalloc(&A->d_stile_e, sizeof(int) * std::max(NB, 1)) != hipSuccess ||
+                 hipMalloc(&dmu, sizeof(int) * 2 * n) != hipSuccess;
     (void)hipGetLastError();
     if (nomem) {
         if (dmu) (void)hipFree(dmu);
@@ -558,12 +562,28 @@ int brick_finish(kle_mat *A, void *plan)
                           hipMemcpyHostToDevice));
         A->brick_gparts = (int)(runptr[ns] / std::max<int64_t>(ns, 1));  // (runs per 64 rows, for the log)
     }
+    if (!bp->srows.empty()) {
+        // the one-block rows per 64-row slice of the owned rows (the gather
+        // forms their B_ii x_i)
+        const int64_t nso = (n + 63) / 64;
+        std::vector<unsigned long long> sm(nso, 0ull);
+        for (int64_t i : bp->srows) sm[i >> 6] |= 1ull << (i & 63);
+        if (hipMalloc(&A->d_ssingle, sizeof(unsigned long long) * nso) != hipSuccess) {
+            (void)hipGetLastError();
+            A->d_ssingle = nullptr;
+            if (dmu) (void)hipFree(dmu);
+            return fail(KLE_ERR_MEM, "out of device memory for the brick gather's one-block rows");
+        }
+        KLE_HIP(hipMemcpy(A->d_ssingle, sm.data(), sizeof(unsigned long long) * nso, hipMemcpyHostToDevice));
+    }
     KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice));
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
-    hipLaunchKernelGGL(k_brick_bound, dim3((unsigned)NB), dim3(256), 0, c->stream, (int)A->row_lat[0],
-                       (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, reinterpret_cast<const BrickDesc *>(A->d_bdesc),
-                       A->d_rowbox, dmu, A->d_svptr, A->d_sval, A->sym_P, dmu + n, A->d_stile_e);
+    if (NB > 0)  // (every row of one block: no brick at all, the gather forms y)
+        hipLaunchKernelGGL(k_brick_bound, dim3((unsigned)NB), dim3(256), 0, c->stream, (int)A->row_lat[0],
+                           (int)A->row_lat[1], (int)A->row_lat[2], zo, hp,
+                           reinterpret_cast<const BrickDesc *>(A->d_bdesc), A->d_rowbox, dmu, A->d_svptr, A->d_sval,
+                           A->sym_P, dmu + n, A->d_stile_e);
     KLE_HIP(hipGetLastError());
     // the exponents into the descriptors
     std::vector<int> eb(NB);
@@ -573,19 +593,25 @@ int brick_finish(kle_mat *A, void *plan)
     for (int q = 0; q < NB; ++q) bp->bricks[q].eb = eb[q];
     KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
     A->nbricks = NB;
-    for (int k = 0; k < 3; ++k) A->brick_dims[k] = 0;
-    for (int q = 0; q < NB; ++q) {
-        const BrickDesc &D = bp->bricks[q];
-        A->brick_dims[0] += D.y0 == 0 && D.z0 == 0;
-        A->brick_dims[1] += D.x0 == 0 && D.z0 == 0;
-        A->brick_dims[2] += D.x0 == 0 && D.y0 == 0;
+    {
+        // (bricks along each axis: distinct first coordinates)
+        std::vector<int> u[3];
+        for (const BrickDesc &D : bp->bricks) {
+            u[0].push_back(D.x0);
+            u[1].push_back(D.y0);
+            u[2].push_back(D.z0);
+        }
+        for (int k = 0; k < 3; ++k) {
+            std::sort(u[k].begin(), u[k].end());
+            A->brick_dims[k] = (int)(std::unique(u[k].begin(), u[k].end()) - u[k].begin());
+        }
     }
     A->brick_model_us = bp->model_us;
     A->brick_lds = (int)bp->lds;
     A->sws_entries = bp->ws_entries;
     A->sym_brick = 1;
     if (const char *e = getenv("KLE_TIMING"))
-        if (atoi(e)) {
+        if (atoi(e) && NB > 0) {
             const BrickDesc &D = bp->bricks[0];
             fprintf(stderr, "[kle brick] %d bricks (first %d x %d x %d rows, region %d x %d x %d), LDS %zu B, "
                             "region entries %lld (%.2f per row)\n",
@@ -647,7 +673,9 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
         KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
                               x->send_hi, c->stream, nullptr));
     // (spmv_brick_waves: fewer waves per CU keep fewer loads in flight)
-    if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1, BRICK_WV);
+    if (A->nbricks == 0) {
+        // (no brick: every row of one block, formed by the gather)
+    } else if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1, BRICK_WV);
     else if (g_tune.spmv_brick_waves == 8) go(k_nb_spmv_sym_brick<8, 1>, 2, 8);
     else if (g_tune.spmv_brick_waves == 12) go(k_nb_spmv_sym_brick<12, 1>, 3, 12);
     else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0, BRICK_WV);
@@ -655,9 +683,10 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     // the gather (kle_sym.hip gsym_gather): per row its direct sum in y, then
     // the runs of the regions holding it, in ascending brick order
     const int64_t n = A->nrows, ntot = n + A->ghost_hi / 3, nlo = n / 64 * 64;
-    if (!dist) return gsym_gather(A, y->d, 0, n, istate, dpart ? x->d : nullptr, dpart, 1, c->stream);
+    const double *xs = A->d_ssingle ? x->d : nullptr;  // (rows of one stored block: the gather's)
+    if (!dist) return gsym_gather(A, y->d, 0, n, istate, dpart ? x->d : nullptr, dpart, 1, c->stream, xs);
     // the slices holding upper ghost rows first (their sums: d_sgsend)
-    KLE_TRY(gsym_gather(A, y->d, nlo, ntot, istate, nullptr, nullptr, 1, c->stream));
+    KLE_TRY(gsym_gather(A, y->d, nlo, ntot, istate, nullptr, nullptr, 1, c->stream, xs));
     const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
     const bool ovl = A->halo_overlap != 0;
     hipStream_t cs = ovl ? c->comm_stream : c->stream;
@@ -667,7 +696,7 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     }
     KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, cs));
     if (ovl) KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
-    KLE_TRY(gsym_gather(A, y->d, 0, nlo, istate, nullptr, nullptr, 1, c->stream));
+    KLE_TRY(gsym_gather(A, y->d, 0, nlo, istate, nullptr, nullptr, 1, c->stream, xs));
     if (ovl) KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
     if (nrecv)
         hipLaunchKernelGGL(k_brick_add_recv, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream, nrecv,

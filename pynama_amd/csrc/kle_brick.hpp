@@ -53,6 +53,8 @@ struct BrickPlan {
     int tail = 0;           // (in) per mille of the mean brick cut off the heavy bricks into tail tiles (spmv_brick_tail)
     int tile = 20;          // (in) a tail tile's weight, per mille of the mean brick (spmv_brick_tile)
     int ntail = 0;          // (out) tail tiles (the last ntail bricks)
+    int singles = 0;        // (in) rows of one stored block out of the bricks, to the gather (spmv_brick_singles)
+    std::vector<int64_t> srows;  // (out) those rows, ascending; their values (9 doubles each) after the bricks'
 };
 
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their

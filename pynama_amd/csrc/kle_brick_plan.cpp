@@ -61,6 +61,8 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     const int64_t n = (int64_t)Lx * Ly * Lz, Lxy = (int64_t)Lx * Ly;
     // per row: stored blocks (upper tail) and its byte weight
     std::vector<int> mu(n);
+    // (a row of one stored block costs a brick nothing when the gather forms it)
+    auto rcost = [&](int64_t i) { return bp.singles && mu[i] == 1 ? 0.0 : row_cost(mu[i]); };
     std::vector<double> wx(Lx, 0.0), wy(Ly, 0.0), wz(Lz, 0.0);
     std::vector<int> xlo(Lx, INT_MAX), xhi(Lx, INT_MIN), ylo(Ly, INT_MAX), yhi(Ly, INT_MIN), zhi(Lz, INT_MIN);
     double total = 0.0;  // (all rows; KLE_TIMING)
@@ -71,7 +73,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         const int bnx = (d >> 12) & 15, bny = (d >> 16) & 15, bnz = (d >> 20) & 15;
         const int k0 = dbx + bnx * (dby + bny * dbz);
         mu[i] = cnt[i] - k0;
-        const double wgt = row_cost(mu[i]);
+        const double wgt = rcost(i);
         wx[x] += wgt;
         wy[y] += wgt;
         wz[z] += wgt;
@@ -94,7 +96,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         for (int y = 0; y < Ly; ++y)
             for (int x = 0; x < Lx; ++x) {
                 const int64_t i = x + (int64_t)Lx * y + Lxy * z;
-                const double v = row_cost(mu[i]);
+                const double v = rcost(i);
                 const int64_t q = (x + 1) + PX1 * (y + 1) + PXY1 * (z + 1);
                 pw[q] = v + pw[q - 1] + pw[q - PX1] + pw[q - PXY1] - pw[q - 1 - PX1] - pw[q - 1 - PXY1] -
                         pw[q - PX1 - PXY1] + pw[q - 1 - PX1 - PXY1];
@@ -615,7 +617,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
                         for (int y = ya; y < yb; ++y)
                             for (int z = z0; z < z1; ++z) rows.push_back(x + (int64_t)Lx * y + Lxy * z);
                     std::vector<double> rp(rows.size() + 1, 0.0);
-                    for (size_t r = 0; r < rows.size(); ++r) rp[r + 1] = rp[r] + row_cost(mu[rows[r]]);
+                    for (size_t r = 0; r < rows.size(); ++r) rp[r + 1] = rp[r] + rcost(rows[r]);
                     if (rows.size() < (size_t)c) {
                         all = false;
                         break;
@@ -678,7 +680,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         std::vector<double> wq(NB0, 0.0);
         double wsum = 0.0;
         for (int q = 0; q < NB0; ++q) {
-            for (int64_t i : best[q]) wq[q] += row_cost(mu[i]);
+            for (int64_t i : best[q]) wq[q] += rcost(i);
             wsum += wq[q];
         }
         const double mean = wsum / NB0, T = mean * (1.0 - 1e-3 * bp.tail), ts = std::max(1e-3 * bp.tile * mean, 1.0);
@@ -688,7 +690,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
             std::vector<int64_t> &R = best[q];
             double w = wq[q];
             size_t keep = R.size();
-            while (keep > 1 && w - row_cost(mu[R[keep - 1]]) >= T) w -= row_cost(mu[R[--keep]]);
+            while (keep > 1 && w - rcost(R[keep - 1]) >= T) w -= rcost(R[--keep]);
             if (keep == R.size()) continue;
             // the cut rows, in streaming order, into nt tiles of about ts
             // (cuts at the cumulative weights k (cut weight) / nt)
@@ -699,8 +701,8 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
             for (int k = 1; k <= nt; ++k) {
                 std::vector<int64_t> t;
                 const double tg = left * k / nt;
-                while (r < R.size() && (k == nt || t.empty() || cw + 0.5 * row_cost(mu[R[r]]) <= tg)) {
-                    cw += row_cost(mu[R[r]]);
+                while (r < R.size() && (k == nt || t.empty() || cw + 0.5 * rcost(R[r]) <= tg)) {
+                    cw += rcost(R[r]);
                     t.push_back(R[r++]);
                 }
                 if (t.empty()) continue;
@@ -712,7 +714,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         // (heaviest tiles first: the last to start are the lightest)
         std::vector<double> tw(tiles.size(), 0.0);
         for (size_t k = 0; k < tiles.size(); ++k)
-            for (int64_t i : tiles[k]) tw[k] += row_cost(mu[i]);
+            for (int64_t i : tiles[k]) tw[k] += rcost(i);
         std::vector<int> ord(tiles.size());
         for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
         std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tw[a] > tw[b]; });
@@ -731,6 +733,26 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         if (getenv("KLE_BRICK_DEBUG"))
             fprintf(stderr, "tail: %d bricks, T %.4f of the mean, %d tiles of ~%.4f\n", NB0, T / mean, bp.ntail,
                     ts / mean);
+    }
+    // Rows of one stored block (the diagonal: Dirichlet rows and the free rows
+    // at the far corner of their box) leave the bricks (bp.singles): a 64-lane
+    // item would carry one block, and the gather forms B_ii x_i for them
+    // instead (28,675 of 342,225 rows at config 2: 4.3 % of the items, 0.09 %
+    // of the blocks).  Their values follow the bricks', 9 doubles each.
+    bp.srows.clear();
+    if (bp.singles) {
+        std::vector<std::vector<int64_t>> kept;
+        for (std::vector<int64_t> &R : best) {
+            std::vector<int64_t> m;
+            m.reserve(R.size());
+            for (int64_t i : R) {
+                if (i < 0 || i >= n) return "bricks overlap or leave the lattice";
+                (mu[i] == 1 ? bp.srows : m).push_back(i);
+            }
+            if (!m.empty()) kept.push_back(std::move(m));  // (a brick of one-block rows only: none left)
+        }
+        best.swap(kept);
+        std::sort(bp.srows.begin(), bp.srows.end());
     }
     const int NB = (int)best.size();
     bp.bricks.assign(NB, BrickDesc{});
@@ -788,7 +810,15 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
                 for (int x = D.ox; x < D.ox + D.RX; ++x)
                     bp.ws_entries += x >= 0 && x < Lx && y >= 0 && y < Ly && z >= 0 && z < Lz + hp;
     }
-    if (rows != n) return "bricks do not cover the lattice";
+    for (size_t k = 0; k < bp.srows.size(); ++k) {
+        const int64_t i = bp.srows[k];
+        if (seen[i]) return "bricks overlap or leave the lattice";
+        seen[i] = 1;
+        bp.svb[i] = voff;
+        voff += 9;
+    }
+    voff = (voff + 15) & ~int64_t(15);
+    if (rows + (int64_t)bp.srows.size() != n) return "bricks do not cover the lattice";
     bp.svb[n] = voff;
     bp.ws_doubles = wsd;
     bp.lds = std::max(bp.lds, BRICK_LDS_MIN);
@@ -847,6 +877,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     bp.bands = g_tune.spmv_brick_bands;
     bp.tail = g_tune.spmv_brick_tail;
     bp.tile = g_tune.spmv_brick_tile;
+    bp.singles = g_tune.spmv_brick_singles;
     const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();
@@ -881,18 +912,24 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
         tot += w;
         mx = std::max(mx, w);
     }
-    int cx = 0, cy = 0, cz = 0;
+    // (bricks along each axis: distinct first coordinates)
+    std::vector<int> ux, uy, uz;
     for (const BrickDesc &D : bp.bricks) {
-        cx += D.y0 == 0 && D.z0 == 0;
-        cy += D.x0 == 0 && D.z0 == 0;
-        cz += D.x0 == 0 && D.y0 == 0;
+        ux.push_back(D.x0);
+        uy.push_back(D.y0);
+        uz.push_back(D.z0);
     }
+    auto distinct = [](std::vector<int> &v) {
+        std::sort(v.begin(), v.end());
+        return (int)(std::unique(v.begin(), v.end()) - v.begin());
+    };
+    const int cx = distinct(ux), cy = distinct(uy), cz = distinct(uz);
     info[0] = NB;
     info[1] = cx;
     info[2] = cy;
     info[3] = cz;
     info[4] = (int)bp.lds;
-    stats[0] = mx / (tot / NB);
+    stats[0] = NB ? mx / (tot / NB) : 0.0;
     stats[1] = (double)bp.ws_entries / n;
     stats[2] = (double)blocks;
     stats[3] = bp.model_us;

@@ -753,6 +753,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_gsym_brick") {
         KLE_ARG(value == 0 || value == 1, "spmv_gsym_brick: 0 or 1");
         g_tune.spmv_gsym_brick = value;
+    } else if (k == "spmv_brick_singles") {
+        KLE_ARG(value == 0 || value == 1, "spmv_brick_singles: 0 or 1");
+        g_tune.spmv_brick_singles = value;
     } else if (k == "spmv_brick_tail") {
         KLE_ARG(value >= 0 && value <= 500, "spmv_brick_tail: 0..500 per mille");
         g_tune.spmv_brick_tail = value;
@@ -869,6 +872,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_waves") *value = g_tune.spmv_brick_waves;
     else if (k == "spmv_brick_bands") *value = g_tune.spmv_brick_bands;
     else if (k == "spmv_brick_tail") *value = g_tune.spmv_brick_tail;
+    else if (k == "spmv_brick_singles") *value = g_tune.spmv_brick_singles;
     else if (k == "spmv_brick_tile") *value = g_tune.spmv_brick_tile;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
     else if (k == "upd_unroll") *value = g_tune.upd_unroll;

@@ -278,6 +278,9 @@ struct kle_mat {
     // group order, each the first dictionary entry (d_sgidx) naming a slice row and the mask of the rows it names
     int *d_sgptr = nullptr, *d_sgidx = nullptr;
     unsigned long long *d_sgmask = nullptr;
+    // box bricks: per 64-row slice of the owned rows, the rows of one stored
+    // block (the diagonal only), whose product the gather forms (B_ii x_i)
+    unsigned long long *d_ssingle = nullptr;
     std::vector<uint8_t> diag_only_row;  // export: rows whose PETSc pattern is the diagonal
     // export: DoF-level entry rule inside the node blocks (no-slip matrices,
     // MASK_* below) and the ext-range DoF classes it reads
@@ -345,8 +348,9 @@ int sval_alloc(kle_mat *A, size_t bytes);
 // a streamed array (matrix values): contiguous first (alloc_contig); 1 if
 // the memory is contiguous, 0 plain, -1 out of memory
 int big_alloc(void **p, size_t bytes);
+// (xs: the owned x, for the box bricks' one-block rows -- d_ssingle)
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
-                int preload, hipStream_t st);
+                int preload, hipStream_t st, const double *xs = nullptr);
 // graph bricks (kle_gbrick.hip)
 int gbrick_bound(kle_mat *A, double vmax_all);
 int gbrick_launch(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
@@ -405,6 +409,7 @@ struct Tuning {
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
     int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
+    int spmv_brick_singles = 1;  // brick SpMV (read at build): rows of one stored block formed by the gather, not as 64-lane items of the bricks
     int spmv_brick_tail = 0;   // brick SpMV (read at build): per mille of the mean brick cut off the heavy bricks into tail tiles (0 none)
     int spmv_brick_tile = 20;  // brick SpMV (read at build): a tail tile's weight, per mille of the mean brick
     int spmv_brick_bands = 0;  // brick SpMV (read at build): 1 the planner also tries ragged bands (balanced bricks; measured no faster), 0 boxes only

@@ -690,6 +690,7 @@ void sym_forget(kle_mat *A)
     A->d_slid = nullptr;
     A->d_sdptr = A->d_sdict = A->d_sgptr = A->d_sgidx = A->d_sglist = nullptr;
     A->d_sgmask = nullptr;
+    A->d_ssingle = nullptr;
     A->d_swptr = nullptr;
     A->sym_wn = 0;
     A->sws_bytes = 0;
@@ -705,7 +706,8 @@ void sym_drop(kle_mat *A)
     for (void *q : {A->sval_raw ? A->sval_raw : (void *)A->d_sval, (void *)A->d_svptr, (void *)A->d_sws, (void *)A->d_stile_e,
                     (void *)A->d_sgsend, (void *)A->d_sgrecv, (void *)A->d_srow, (void *)A->d_sbp,
                     (void *)A->d_slid, (void *)A->d_sdptr, (void *)A->d_sdict, (void *)A->d_sgptr,
-                    (void *)A->d_sgidx, (void *)A->d_sgmask, (void *)A->d_sglist, (void *)A->d_swptr})
+                    (void *)A->d_sgidx, (void *)A->d_sgmask, (void *)A->d_ssingle, (void *)A->d_sglist,
+                    (void *)A->d_swptr})
         if (q) (void)hipFree(q);
     sym_forget(A);
 }
@@ -1031,7 +1033,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
                                                         const double *__restrict__ ws, double *__restrict__ y,
                                                         double *__restrict__ gsend, const int *__restrict__ istate,
                                                         const double *__restrict__ xdot, double *__restrict__ dpart,
-                                                        int preload, int64_t sl0, int64_t sl1)
+                                                        int preload, int64_t sl0, int64_t sl1,
+                                                        const unsigned long long *__restrict__ single,
+                                                        const double *__restrict__ sval,
+                                                        const int64_t *__restrict__ svptr,
+                                                        const double *__restrict__ xs)
 {
     __shared__ double dred[4];
     const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;  // (tested before the first store)
@@ -1059,7 +1065,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
         }
         if (stop) return;  // (uniform: the whole workgroup)
         if (j < nrows) {
-            if (preload) {  // (graph bricks: the rows' direct sums are in y)
+            // (box bricks: a row of one stored block is no item of its brick;
+            // its direct sum B_ii x_i here, the expression the brick kernel
+            // evaluates -- the same bits)
+            const bool one = single && sl < (nrows + 63) / 64 && ((single[sl] >> lane) & 1ull);
+            if (one) {
+                const double *v = sval + svptr[j];
+                const double x0 = xs[3 * j], x1 = xs[3 * j + 1], x2 = xs[3 * j + 2];
+                s0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
+                s1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
+                s2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+            } else if (preload) {  // (the rows' direct sums are in y)
                 s0 += y[3 * j];
                 s1 += y[3 * j + 1];
                 s2 += y[3 * j + 2];
@@ -1519,13 +1535,13 @@ static int gsym_build(kle_mat *A)
 // direct sums).  One workgroup per 4 slices of 64 rows; with xdot, its
 // (y, x) partial in dpart[workgroup].
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
-                int preload, hipStream_t st)
+                int preload, hipStream_t st, const double *xs)
 {
     if (r1 <= r0) return 0;
     const int64_t s0 = r0 / 64, s1 = (r1 + 63) / 64, ntot = A->nrows + A->ghost_hi / 3;
     hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((s1 - s0 + 3) / 4)), dim3(256), 0, st, A->nrows, ntot,
                        A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y, A->d_sgsend, istate, xdot, dpart, preload,
-                       s0, s1);
+                       s0, s1, xs ? A->d_ssingle : nullptr, A->d_sval, A->d_svptr, xs);
     KLE_HIP(hipGetLastError());
     return 0;
 }

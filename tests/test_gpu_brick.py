@@ -43,7 +43,8 @@ def _close(y, ref):
 
 
 @pytest.mark.parametrize("nelem,ngl", [([3, 2, 2], 5), ([12, 10, 6], 5), ([7, 5, 4], 3), ([6, 5, 3], 2),
-                                       ([3, 4, 2], 6), ([1, 1, 1], 4), ([3, 3, 2], 7), ([9, 7, 5], 4)])
+                                       ([3, 4, 2], 6), ([1, 1, 1], 4), ([3, 3, 2], 7), ([9, 7, 5], 4),
+                                       ([1, 1, 1], 3)])  # (3^3 nodes: every row of one stored block, no brick)
 def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
     from pynama_amd.runtime import set_tuning
     _, mat = _mat(pa, nelem, ngl)
@@ -81,6 +82,18 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         K.setOption(K.Option.SPD, True)
     for ref in (y0, yh):
         _close(ybb, ref)
+    # the one-block rows as items of their bricks (spmv_brick_singles 0)
+    # instead of formed by the gather (another plan: other regions and
+    # scales) -- the same product to rounding
+    set_tuning("spmv_brick_singles", 0)
+    try:
+        K.setOption(K.Option.SPD, True)
+        ys = (K * x).getArray().copy()
+    finally:
+        set_tuning("spmv_brick_singles", 1)
+        K.setOption(K.Option.SPD, True)
+    for ref in (y0, yh):
+        _close(ys, ref)
     # tail tiles (spmv_brick_tail: the heavy bricks' last rows as small
     # bricks launched after them) -- the same product to rounding
     set_tuning("spmv_brick_tail", 30)

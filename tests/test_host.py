@@ -350,7 +350,7 @@ def test_brick_planner_covers_the_lattice_and_balances(pa, lat, p, ncu, must):
     ragged-band generator on (spmv_brick_bands 1): every plan covers the
     lattice exactly (the planner refuses otherwise), at most ncu bricks,
     regions within the LDS; at config 2 the ragged-band plan keeps the
-    heaviest brick within 2 % of the mean (the box plans: 5.7 %; measured no
+    heaviest brick within 3 % of the mean (the box plans: 5.7–10 %; measured no
     faster on the GPU all the same, so off by default -- DESIGN 3 "Bricks")."""
     from pynama_amd.runtime import set_tuning
     lib = pa.load()
@@ -369,5 +369,5 @@ def test_brick_planner_covers_the_lattice_and_balances(pa, lat, p, ncu, must):
     assert 1 <= info[0] <= ncu
     assert info[4] <= 163840
     if lat == (81, 65, 65) and ncu == 256:
-        assert st[0] < 1.02, st[0]
+        assert st[0] < 1.03, st[0]  # (1.026 with the one-block rows out of the bricks)
         assert st[1] < 2.2, st[1]  # (region entries per row)
