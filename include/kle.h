@@ -103,7 +103,10 @@ const char *kle_last_error(void);
  * build: at most this many bricks, 0 planned), "spmv_brick_rounds" (read at
  * build: at most this many bricks per CU, default 1), "spmv_brick_split" (read
  * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
- * "spmv_brick_singles" (read at build: rows of one stored block -- the
+ * "spmv_brick_pair" (read at build: rows in units of two whose last
+ * partial 64-block passes share one item; 1 default), "spmv_brick_fcost"
+ * (read at build: with pairs, plan bricks by blocks instead of passes; 0
+ * default), "spmv_brick_singles" (read at build: rows of one stored block -- the
  * Dirichlet rows and the free rows at the far corner of their box -- formed by
  * the gather instead of as items of the bricks; 1 default),
  * "spmv_brick_tail" / "spmv_brick_tile" (read at build: per mille of the

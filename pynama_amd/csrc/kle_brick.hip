@@ -45,16 +45,24 @@ using cint = __attribute__((address_space(4))) const int;
 // a row of the brick (every field wave-uniform: SGPRs)
 struct BRow {
     const double *v;
-    double x0, x1, x2;
-    int bnx, bnxy, k0, mu, rb0, ir, r;
-    float ibnx, ibnxy;
+    int bnx, bnxy, k0, mu, rb0, ir;
 };
 
-// an issued item: its row (r < 0: a re-read past the brick's last row), the
-// row's stored blocks and region index, the pass's first block
+// an issued item, packed in five words (SGPRs are the kernel's scarce
+// registers): row P on lanes [0, s), row Q on lanes [s, 64) (s = 64: P
+// alone), each from its first block kbP / kbQ; eP / eQ: the item ends row P /
+// Q (its direct sum is complete); ok 0: a re-read past the brick's last unit
 struct BItem {
-    int r, mu, ir, kb;
+    int ok;
+    int ir;  // irP | irQ << 16
+    int mu;  // muP | muQ << 16
+    int kb;  // kbP | kbQ << 16
+    int sf;  // s | eP << 8 | eQ << 9
 };
+__device__ __forceinline__ BItem bitem(int s, int muP, int muQ, int irP, int irQ, int kbP, int kbQ, int eP, int eQ)
+{
+    return {1, irP | irQ << 16, muP | muQ << 16, kbP | kbQ << 16, s | eP << 8 | eQ << 9};
+}
 
 template <int WV, int D>
 __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp,
@@ -73,7 +81,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int NR = bd[b].nr;
+    const int NU = bd[b].nr / 2;  // units of two rows (kle_brick_plan.cpp)
     const int ox = bd[b].ox, oy = bd[b].oy, oz = bd[b].oz, RX = bd[b].RX, RY = bd[b].RY, RZ = bd[b].RZ;
     const int rstart = bd[b].rstart, eb = bd[b].eb;
     const long long vbase = bd[b].vbase, wsoff = bd[b].wsoff;
@@ -85,9 +93,9 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     const int64_t Lxy = (int64_t)Lx * Ly;
     cint *rdesc = (cint *)(rowd + rstart);  // (address-space cast: scalar loads)
     const double *vb = sval + vbase;
-    // a row from its descriptor: packed box (dbx, dby, dbz, bnx, bny, bnz: 4
-    // bits each) + the low byte of its region index; value offset / 16
-    // doubles (24 bits) + the high byte
+    // a row from its descriptor (kle_brick.hpp): packed box (dbx, dby, dbz,
+    // bnx, bny, bnz: 4 bits each) + the low byte of its region index; value
+    // offset / 16 doubles (23 bits) + the high byte
     auto row_setup = [&](int r, int dw, int vw, BRow &R) {
         const int dbx = dw & 15, dby = (dw >> 4) & 15, dbz = (dw >> 8) & 15;
         R.bnx = (dw >> 12) & 15;
@@ -97,91 +105,127 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         R.mu = R.bnxy * bnz - R.k0;
         R.ir = ((dw >> 24) & 255) | (((vw >> 24) & 255) << 8);
         R.rb0 = R.ir - (dbx + RX * (dby + RY * dbz));
-        R.v = vb + (int64_t)(vw & 0xFFFFFF) * 16;
-        R.r = r;
-        R.ibnx = __builtin_amdgcn_rcpf((float)R.bnx);
-        R.ibnxy = __builtin_amdgcn_rcpf((float)R.bnxy);
-        R.ibnx = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, R.ibnx)));
-        R.ibnxy = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, R.ibnxy)));
+        R.v = vb + (int64_t)(vw & (BRICK_ROW_NULL - 1)) * 16;
     };
-    auto row_x = [&](BRow &R) {
-        R.x0 = uni_d(xl[R.ir]);
-        R.x1 = uni_d(xl[RN + R.ir]);
-        R.x2 = uni_d(xl[2 * RN + R.ir]);
-    };
-    // the values of one 64-block pass of a row (lanes past its end re-read
-    // its last block; their results go nowhere) and each block's region index
-    auto load_v = [&](const BRow &R, int kb, double *vv, int &rr) {
-        const int kk = min(kb + lane, R.mu - 1);
-        const int q16 = R.mu & ~15;
+    // the values of one item -- lanes below s from row P's blocks kbP + lane,
+    // the others from row Q's blocks kbQ + lane - s (Q's values follow P's);
+    // lanes past a row's end re-read its last block (their results go
+    // nowhere) -- and each block's region index
+    auto load_v = [&](const BRow &P, const BRow &Q, int kbP, int kbQ, int s, double *vv, int &rr) {
+        const bool q = lane >= s;
+        const int mu = q ? Q.mu : P.mu;
+        const int kk = min(q ? kbQ + lane - s : kbP + lane, mu - 1);
+        const int q16 = mu & ~15;
         const bool ch = kk < q16;
         const int o0 = ch ? (kk >> 4) * 144 + (kk & 15) : q16 * 9 + (kk - q16);
-        const int st = ch ? 16 : R.mu - q16;
+        const int st = ch ? 16 : mu - q16;
+        const unsigned bo = q ? (unsigned)(Q.v - P.v) * 8u : 0u;
         unsigned o[9];
 #pragma unroll
-        for (int s = 0; s < 9; ++s) o[s] = (unsigned)(o0 + s * st) * 8u;
-        sym_ld9(vv, R.v, o);
-        const int k = R.k0 + kk;
-        const int kz = sym_div(k, R.bnxy, R.ibnxy), rem = k - kz * R.bnxy;
-        const int ky = sym_div(rem, R.bnx, R.ibnx), kx = rem - ky * R.bnx;
-        rr = R.rb0 + kx + RX * (ky + RY * kz);
+        for (int t = 0; t < 9; ++t) o[t] = bo + (unsigned)(o0 + t * st) * 8u;
+        // (the base is wave-uniform; said so, as the loads take it in SGPRs)
+        const unsigned long long pb = (unsigned long long)P.v;
+        const unsigned phi = (unsigned)__builtin_amdgcn_readfirstlane((int)(pb >> 32));
+        const unsigned plo = (unsigned)__builtin_amdgcn_readfirstlane((int)(pb & 0xffffffffull));
+        sym_ld9(vv, reinterpret_cast<const double *>(((unsigned long long)phi << 32) | plo), o);
+        const int k = (q ? Q.k0 : P.k0) + kk;
+        const int bnxy = q ? Q.bnxy : P.bnxy, bnx = q ? Q.bnx : P.bnx;
+        const int kz = sym_div(k, bnxy, __builtin_amdgcn_rcpf((float)bnxy)), rem = k - kz * bnxy;
+        const int ky = sym_div(rem, bnx, __builtin_amdgcn_rcpf((float)bnx)), kx = rem - ky * bnx;
+        rr = (q ? Q.rb0 : P.rb0) + kx + RX * (ky + RY * kz);
     };
-    // 1. the wave's first rows are static (w, w + WV, w + 2 WV: the counter
-    // starts past them), so its first D items go out before the fill
+    // 1. units from an LDS counter; each wave's first D + 2 static (w, w + WV,
+    // ...: the counter starts past them -- as many as the D items issued
+    // before the fill can reach), so those go out before the fill
     auto grab = [&]() -> int {
         int r = 0;
         if (lane == 0) r = atomicAdd(ctr, 1);
         return __builtin_amdgcn_readfirstlane(r);
     };
+    constexpr int NSTAT = D + 2;
     int snext = w + WV;
-    auto take = [&]() -> int {  // (the next row of this wave)
-        if (snext < 3 * WV) {
+    auto take = [&]() -> int {  // (the next unit of this wave)
+        if (snext < NSTAT * WV) {
             const int r = snext;
             snext += WV;
             return r;
         }
         return grab();
     };
-    BRow I;
-    int ki = 0;
-    bool idone = w >= NR;
+    // The issue cursor over the wave's units: a unit (A, B) streams A's
+    // passes (B absent: all of them; else its full ones), the item shared by
+    // A's and B's last partial passes, then B's full passes.
+    BRow A, B;
+    bool hasB = false, idone = w >= NU;
+    int ph = 0, ki = 0, aend = 0, bend = 0;
+    auto unit_setup = [&](int u, int d0, int d1, int d2, int d3) {
+        row_setup(2 * u, d0, d1, A);
+        hasB = (d3 & BRICK_ROW_NULL) == 0;
+        if (hasB) row_setup(2 * u + 1, d2, d3, B);
+        else B = A;
+        aend = hasB ? (A.mu & ~63) : A.mu;
+        bend = hasB ? (B.mu & ~63) : 0;
+        ph = aend > 0 ? 0 : 1;
+        ki = 0;
+    };
+    if (!idone) {
+        unit_setup(w, rdesc[4 * w], rdesc[4 * w + 1], rdesc[4 * w + 2], rdesc[4 * w + 3]);
+    } else {
+        A.v = vb;
+        A.mu = 1;
+        A.k0 = 0;
+        A.bnx = A.bnxy = 1;
+        A.rb0 = 0;
+        A.ir = 0;
+        B = A;
+    }
+    // the next unit and its descriptors, fetched one unit ahead
+    int pend = idone ? NU : take();
+    int pd0 = rdesc[4 * min(pend, NU - 1)], pd1 = rdesc[4 * min(pend, NU - 1) + 1];
+    int pd2 = rdesc[4 * min(pend, NU - 1) + 2], pd3 = rdesc[4 * min(pend, NU - 1) + 3];
+    // the item at the cursor: its loads into vn, its record; the cursor then
+    // moves on (past the last unit it stays, re-reading the last item)
+    auto issue = [&](double *vn, int &rn, BItem &itn) {
+        if (idone) {  // (a re-read of A's first pass: cache hits, the results go nowhere)
+            load_v(A, A, 0, 0, 64, vn, rn);
+            itn.ok = 0;
+            return;
+        }
+        if (ph == 0) {  // A's passes
+            load_v(A, A, ki, 0, 64, vn, rn);
+            itn = bitem(64, A.mu, A.mu, A.ir, A.ir, ki, 0, !hasB && ki + 64 >= A.mu, 0);
+            ki += 64;
+            if (ki >= aend) ph = hasB ? 1 : 3;
+        } else if (ph == 1) {  // A's and B's last partial passes
+            const int s = A.mu - aend;
+            load_v(A, B, aend, bend, s, vn, rn);
+            itn = bitem(s, A.mu, B.mu, A.ir, B.ir, aend, bend, 1, bend == 0);
+            ki = 0;
+            ph = bend > 0 ? 2 : 3;
+        } else {  // B's full passes
+            load_v(B, B, ki, 0, 64, vn, rn);
+            itn = bitem(64, B.mu, B.mu, B.ir, B.ir, ki, 0, ki + 64 >= bend, 0);
+            ki += 64;
+            if (ki >= bend) ph = 3;
+        }
+        if (ph == 3) {  // the unit is done: the next one
+            if (pend >= NU) {
+                idone = true;
+            } else {
+                unit_setup(pend, pd0, pd1, pd2, pd3);
+                pend = take();
+                const int u = min(pend, NU - 1);
+                pd0 = rdesc[4 * u];
+                pd1 = rdesc[4 * u + 1];
+                pd2 = rdesc[4 * u + 2];
+                pd3 = rdesc[4 * u + 3];
+            }
+        }
+    };
     double v0[9], v1[9], v2[9];
     int r0 = 0, r1 = 0, r2 = 0;
     BItem i0, i1, i2;
-    if (!idone) {
-        row_setup(w, rdesc[2 * w], rdesc[2 * w + 1], I);
-    } else {
-        I.v = vb;
-        I.mu = 1;
-        I.k0 = 0;
-        I.bnx = I.bnxy = 1;
-        I.ibnx = I.ibnxy = 1.0f;
-        I.rb0 = 0;
-        I.ir = 0;
-        I.r = -1;
-    }
-    load_v(I, 0, v0, r0);
-    i0 = {idone ? -1 : I.r, I.mu, I.ir, 0};
-    // the next row and its descriptor, fetched one row ahead
-    int pend = take();
-    int pdw = rdesc[2 * min(pend, NR - 1)], pvw = rdesc[2 * min(pend, NR - 1) + 1];
-    auto issue = [&](double *vn, int &rn, BItem &itn) {
-        if (!idone) {
-            if (ki + 64 < I.mu) {
-                ki += 64;
-            } else if (pend >= NR) {
-                idone = true;
-            } else {
-                row_setup(pend, pdw, pvw, I);
-                ki = 0;
-                pend = take();
-                pdw = rdesc[2 * min(pend, NR - 1)];
-                pvw = rdesc[2 * min(pend, NR - 1) + 1];
-            }
-        }
-        load_v(I, ki, vn, rn);
-        itn = {idone ? -1 : I.r, I.mu, I.ir, ki};
-    };
+    issue(v0, r0, i0);
     if (D == 2) issue(v1, r1, i1);
     // 2. x of the region into LDS (nodes off the lattice read 0), its max |x|;
     // the sums zeroed.  Line (ry, rz) of the region is 3 RX contiguous doubles
@@ -225,7 +269,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         wred[w] = xm;
         wred[WV + w] = anybad ? 1.0 : 0.0;
     }
-    if (threadIdx.x == 0) *ctr = 3 * WV;
+    if (threadIdx.x == 0) *ctr = NSTAT * WV;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // LDS stores done (lgkmcnt 0); the value loads stay in flight
     __builtin_amdgcn_s_barrier();
     if (__builtin_amdgcn_readfirstlane(stop) != 0) return;  // (nothing written yet)
@@ -256,42 +300,54 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         }
     }
     KLE_PROBE_TS(ts1)
-    // 3. items = (row, pass of 64 blocks), rows from the LDS counter.  The
-    // issue cursor runs D items in front of the compute cursor; each issued
-    // item leaves a record (row, its length and region index, first block),
-    // so the compute cursor needs no row state of the issue cursor.  Past the
-    // brick's last row the issue cursor stays on its last item, re-reading it
-    // (cache hits) under a record r = -1, so every step issues 9 loads and the
-    // wait for the summed item is a fixed vmcnt(9 D).
-    if (i0.r >= 0) {
-        double cx0 = 0.0, cx1 = 0.0, cx2 = 0.0;
+    // 3. The issue cursor runs D items in front of the compute cursor; each
+    // issued item leaves a record (rows, lengths, region indices, first
+    // blocks, which rows it ends), so the compute cursor needs no state of
+    // the issue cursor.  Past the brick's last unit the issue cursor re-reads
+    // its last item under a record r = -1, so every step issues 9 loads and
+    // the wait for the summed item is a fixed vmcnt(9 D).
+    if (i0.ok) {
         double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        // the row's direct sum (fixed-order DPP, fp64), one writer, into y --
+        // the gather adds the bricks' transposed sums to it (8 MB of stores
+        // at config 2: the only ones before the end)
+        auto row_out = [&](int ir, double a0, double a1, double a2) {
+            wsum3_dpp(a0, a1, a2);
+            // (the row's lattice node from its region index: bricks may be
+            // ragged, kle_brick_plan.cpp)
+            const int irz = ir / RXY, irem = ir - irz * RXY, iry = irem / RX, irx = irem - iry * RX;
+            const int64_t j = (ox + irx) + (int64_t)Lx * (oy + iry) + Lxy * (oz + irz);
+            if (lane < 3) y[3 * j + lane] = lane == 0 ? a0 : lane == 1 ? a1 : a2;
+        };
         // one step: issue the next item into vn, wait for vv (the D newer
         // items stay in flight), sum it
         auto step = [&](double *vv, const int rr, const BItem &it, double *vn, int &rn, BItem &itn) {
             issue(vn, rn, itn);
-            if (it.r < 0) return false;
-            if (it.kb == 0) {  // a new row: x of the row
-                cx0 = uni_d(xl[it.ir]);
-                cx1 = uni_d(xl[RN + it.ir]);
-                cx2 = uni_d(xl[2 * RN + it.ir]);
+            if (!it.ok) return false;
+            const int is = it.sf & 255, irP = it.ir & 0xFFFF, irQ = (int)((unsigned)it.ir >> 16);
+            const bool q = lane >= is;
+            // x of the lane's row (P's below s, Q's from s on)
+            const double p0 = uni_d(xl[irP]), p1 = uni_d(xl[RN + irP]), p2 = uni_d(xl[2 * RN + irP]);
+            double c0 = p0, c1 = p1, c2 = p2;
+            if (is < 64) {
+                const double q0 = uni_d(xl[irQ]), q1 = uni_d(xl[RN + irQ]), q2 = uni_d(xl[2 * RN + irQ]);
+                c0 = q ? q0 : p0;
+                c1 = q ? q1 : p1;
+                c2 = q ? q2 : p2;
             }
             const double xj0 = xl[rr], xj1 = xl[RN + rr], xj2 = xl[2 * RN + rr];
             sym_wait9<9 * D>(vv);
             // B x_j into the row, B^T x_i into row j (lanes past the row's end
             // and the diagonal block add into their dummy slot)
-            const int kk = it.kb + lane;
-            const bool live = kk < it.mu;
+            const int kk = q ? (int)((unsigned)it.kb >> 16) + lane - is : (it.kb & 0xFFFF) + lane;
+            const bool live = kk < (q ? (int)((unsigned)it.mu >> 16) : (it.mu & 0xFFFF));
             const int rt = live && kk > 0 ? rr : RN + lane;
             const double s0 = vv[0] * xj0 + vv[1] * xj1 + vv[2] * xj2;
             const double s1 = vv[3] * xj0 + vv[4] * xj1 + vv[5] * xj2;
             const double s2 = vv[6] * xj0 + vv[7] * xj1 + vv[8] * xj2;
-            acc0 += live ? s0 : 0.0;
-            acc1 += live ? s1 : 0.0;
-            acc2 += live ? s2 : 0.0;
-            const double t0 = vv[0] * cx0 + vv[3] * cx1 + vv[6] * cx2;
-            const double t1 = vv[1] * cx0 + vv[4] * cx1 + vv[7] * cx2;
-            const double t2 = vv[2] * cx0 + vv[5] * cx1 + vv[8] * cx2;
+            const double t0 = vv[0] * c0 + vv[3] * c1 + vv[6] * c2;
+            const double t1 = vv[1] * c0 + vv[4] * c1 + vv[7] * c2;
+            const double t2 = vv[2] * c0 + vv[5] * c1 + vv[8] * c2;
             if (!(probe & 1)) {  // (timing probe 1: no transposed adds)
                 atomicAdd(&acc[rt], fx_of(t0 * S1, S2));
                 atomicAdd(&acc[RS + rt], fx_of(t1 * S1, S2));
@@ -299,18 +355,21 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
             } else if (!live) {
                 acc[RN + lane] += (unsigned long long)(t0 + t1 + t2);
             }
-            if (it.kb + 64 >= it.mu) {
-                // the row is done: its direct sum (fixed-order DPP, fp64), one
-                // writer, into y -- the gather adds the bricks' transposed
-                // sums to it, so an identity (Dirichlet) row returns x bit for
-                // bit (8 MB of stores at config 2: the only ones before the end)
-                wsum3_dpp(acc0, acc1, acc2);
-                // (the row's lattice node from its region index: bricks may be
-                // ragged, kle_brick_plan.cpp)
-                const int irz = it.ir / RXY, irem = it.ir - irz * RXY, iry = irem / RX, irx = irem - iry * RX;
-                const int64_t j = (ox + irx) + (int64_t)Lx * (oy + iry) + Lxy * (oz + irz);
-                if (lane < 3) y[3 * j + lane] = lane == 0 ? acc0 : lane == 1 ? acc1 : acc2;
-                acc0 = acc1 = acc2 = 0.0;
+            const bool mine = live && !q;  // (P's lanes)
+            acc0 += mine ? s0 : 0.0;
+            acc1 += mine ? s1 : 0.0;
+            acc2 += mine ? s2 : 0.0;
+            if (it.sf & 256) {
+                row_out(irP, acc0, acc1, acc2);
+                // (Q's lanes start Q's sum)
+                const bool qs = live && q;
+                acc0 = qs ? s0 : 0.0;
+                acc1 = qs ? s1 : 0.0;
+                acc2 = qs ? s2 : 0.0;
+                if (it.sf & 512) {
+                    row_out(irQ, acc0, acc1, acc2);
+                    acc0 = acc1 = acc2 = 0.0;
+                }
             }
             return true;
         };
@@ -444,6 +503,8 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
     bp->tail = g_tune.spmv_brick_tail;
     bp->tile = g_tune.spmv_brick_tile;
     bp->singles = g_tune.spmv_brick_singles;
+    bp->pair = g_tune.spmv_brick_pair;
+    bp->fcost = g_tune.spmv_brick_fcost;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     try {  // (no exception may cross the C ABI: a planner failure is a refusal)
         why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
@@ -494,6 +555,7 @@ int brick_finish(kle_mat *A, void *plan)
             const BrickDesc &D = bp->bricks[q];
             for (int r = 0; r < D.nr; ++r) {
                 const int64_t rr = (int64_t)D.rstart + r;
+                if (brick_row_null(bp->rowd.data(), rr)) continue;
                 const int d = bp->rowd[2 * rr];
                 const int dbx = d & 15, dby = (d >> 4) & 15, dbz = (d >> 8) & 15;
                 const int bnx = (d >> 12) & 15, bny = (d >> 16) & 15, bnz = (d >> 20) & 15;

@@ -22,6 +22,12 @@ struct BrickDesc {
 };
 static_assert(sizeof(BrickDesc) == 80, "BrickDesc layout");
 
+// a row descriptor: word 0 the packed row box (dbx, dby, dbz, bnx, bny, bnz:
+// 4 bits each) + the low byte of its region index; word 1 its value offset
+// / 16 doubles (23 bits), BRICK_ROW_NULL (a unit's absent second row) and the
+// high byte of the region index.  Rows come in units of two (kle_brick_plan.cpp).
+constexpr int BRICK_ROW_NULL = 1 << 23;
+inline bool brick_row_null(const int *rowd, int64_t r) { return (rowd[2 * r + 1] & BRICK_ROW_NULL) != 0; }
 // a row descriptor's region index (the low and high bytes of its two words)
 inline int brick_row_ir(const int *rowd, int64_t r)
 {
@@ -54,6 +60,8 @@ struct BrickPlan {
     int tile = 20;          // (in) a tail tile's weight, per mille of the mean brick (spmv_brick_tile)
     int ntail = 0;          // (out) tail tiles (the last ntail bricks)
     int singles = 0;        // (in) rows of one stored block out of the bricks, to the gather (spmv_brick_singles)
+    int pair = 0;           // (in) units of two rows sharing their tails' item (spmv_brick_pair)
+    int fcost = 0;          // (in) with pair: rows cost their blocks' share of full items (spmv_brick_fcost)
     std::vector<int64_t> srows;  // (out) those rows, ascending; their values (9 doubles each) after the bricks'
 };
 

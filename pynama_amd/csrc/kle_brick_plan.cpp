@@ -61,8 +61,13 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     const int64_t n = (int64_t)Lx * Ly * Lz, Lxy = (int64_t)Lx * Ly;
     // per row: stored blocks (upper tail) and its byte weight
     std::vector<int> mu(n);
-    // (a row of one stored block costs a brick nothing when the gather forms it)
-    auto rcost = [&](int64_t i) { return bp.singles && mu[i] == 1 ? 0.0 : row_cost(mu[i]); };
+    // (a row of one stored block costs a brick nothing when the gather forms
+    // it; with paired tails (bp.pair, bp.fcost) a row costs about its blocks'
+    // share of full items)
+    auto rcost = [&](int64_t i) {
+        if (bp.singles && mu[i] == 1) return 0.0;
+        return bp.pair && bp.fcost ? 4608.0 * (mu[i] / 64.0 + 0.02) : row_cost(mu[i]);
+    };
     std::vector<double> wx(Lx, 0.0), wy(Ly, 0.0), wz(Lz, 0.0);
     std::vector<int> xlo(Lx, INT_MAX), xhi(Lx, INT_MIN), ylo(Ly, INT_MAX), yhi(Ly, INT_MIN), zhi(Lz, INT_MIN);
     double total = 0.0;  // (all rows; KLE_TIMING)
@@ -756,9 +761,9 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     }
     const int NB = (int)best.size();
     bp.bricks.assign(NB, BrickDesc{});
-    bp.rowd.assign(2 * n, 0);
+    bp.rowd.assign(4 * n, 0);  // (units of two rows: a row and its partner or a null row)
     bp.svb.assign(n + 1, 0);
-    int64_t voff = 0, rows = 0, wsd = 0;
+    int64_t voff = 0, rows = 0, wsd = 0, nreal = 0;
     bp.lds = 0;
     bp.ws_entries = 0;
     std::vector<char> seen(n, 0);
@@ -784,7 +789,34 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         D.ny = y1 - y0;
         D.z0 = z0;
         D.nz = z1 - z0;
-        D.nr = (int)R.size();
+        // Units of two rows (bp.pair): row B's last partial pass shares row
+        // A's (tails tA + tB <= 64 -- one 64-lane item instead of two: 22 %
+        // fewer items at config 2), the unit streamed as A's full passes, the
+        // shared item, B's full passes; B's values follow A's.  A row without
+        // a partner takes a null descriptor as its B.  Pairs by two pointers
+        // over the tails (the largest with the smallest that fits); units in
+        // the lattice order of their first row.
+        std::vector<std::pair<int64_t, int64_t>> units;
+        {
+            std::vector<int64_t> tl;
+            for (int64_t i : R)
+                if (bp.pair && mu[i] % 64 != 0) tl.push_back(i);
+                else units.push_back({i, -1});
+            std::stable_sort(tl.begin(), tl.end(), [&](int64_t a, int64_t b) { return mu[a] % 64 < mu[b] % 64; });
+            size_t lo = 0, hi = tl.size();
+            while (lo < hi) {
+                const int64_t big = tl[hi - 1];
+                if (lo + 1 < hi && mu[tl[lo]] % 64 + mu[big] % 64 <= 64) {
+                    units.push_back({std::min(big, tl[lo]), std::max(big, tl[lo])});
+                    ++lo;
+                } else {
+                    units.push_back({big, -1});
+                }
+                --hi;
+            }
+            std::sort(units.begin(), units.end());
+        }
+        D.nr = 2 * (int)units.size();
         const int RN = D.RX * D.RY * D.RZ;
         D.rstart = (int)rows;
         D.eb = 0;
@@ -793,17 +825,25 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         D.wsoff = wsd;
         wsd += ((int64_t)3 * RN + 15) & ~int64_t(15);
         bp.lds = std::max(bp.lds, brick_lds(RN));
-        for (int64_t i : R) {
-            const int z = (int)(i / Lxy), y = (int)((i % Lxy) / Lx), x = (int)(i % Lx);
-            bp.svb[i] = voff;
-            const int64_t o = voff - D.vbase;
-            if ((o >> 4) >= (1 << 24)) return "brick values beyond 2^28 doubles";
-            const int ir = (x - D.ox) + D.RX * ((y - D.oy) + D.RY * (z - D.oz));
-            bp.rowd[2 * rows] = (srow[i] & 0xFFFFFF) | ((ir & 255) << 24);
-            bp.rowd[2 * rows + 1] = (int)((o >> 4) | ((int64_t)((ir >> 8) & 255) << 24));
-            voff += ((int64_t)mu[i] * 9 + 15) & ~int64_t(15);
-            ++rows;
-        }
+        for (const auto &u : units)
+            for (int64_t i : {u.first, u.second}) {
+                if (i < 0) {  // (no partner: the null descriptor)
+                    bp.rowd[2 * rows] = 0;
+                    bp.rowd[2 * rows + 1] = BRICK_ROW_NULL;
+                    ++rows;
+                    continue;
+                }
+                const int z = (int)(i / Lxy), y = (int)((i % Lxy) / Lx), x = (int)(i % Lx);
+                bp.svb[i] = voff;
+                const int64_t o = voff - D.vbase;
+                if ((o >> 4) >= (1 << 23)) return "brick values beyond 2^27 doubles";
+                const int ir = (x - D.ox) + D.RX * ((y - D.oy) + D.RY * (z - D.oz));
+                bp.rowd[2 * rows] = (srow[i] & 0xFFFFFF) | ((ir & 255) << 24);
+                bp.rowd[2 * rows + 1] = (int)((o >> 4) | ((int64_t)((ir >> 8) & 255) << 24));
+                voff += ((int64_t)mu[i] * 9 + 15) & ~int64_t(15);
+                ++rows;
+                ++nreal;
+            }
         // lattice entries of the region (written by the brick, read by the gather)
         for (int z = D.oz; z < D.oz + D.RZ; ++z)
             for (int y = D.oy; y < D.oy + D.RY; ++y)
@@ -818,7 +858,7 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         voff += 9;
     }
     voff = (voff + 15) & ~int64_t(15);
-    if (rows + (int64_t)bp.srows.size() != n) return "bricks do not cover the lattice";
+    if (nreal + (int64_t)bp.srows.size() != n) return "bricks do not cover the lattice";
     bp.svb[n] = voff;
     bp.ws_doubles = wsd;
     bp.lds = std::max(bp.lds, BRICK_LDS_MIN);
@@ -878,6 +918,8 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     bp.tail = g_tune.spmv_brick_tail;
     bp.tile = g_tune.spmv_brick_tile;
     bp.singles = g_tune.spmv_brick_singles;
+    bp.pair = g_tune.spmv_brick_pair;
+    bp.fcost = g_tune.spmv_brick_fcost;
     const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();
@@ -888,6 +930,10 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
         std::vector<char> seen(n, 0);
         for (const BrickDesc &D : bp.bricks)
             for (int r = 0; r < D.nr; ++r) {
+                if (brick_row_null(bp.rowd.data(), (int64_t)D.rstart + r)) {
+                    if (r % 2 == 0) return fail(KLE_ERR_SUP, "brick plan: a unit without its first row");
+                    continue;
+                }
                 const int ir = brick_row_ir(bp.rowd.data(), (int64_t)D.rstart + r);
                 if (ir < 0 || ir >= D.RX * D.RY * D.RZ) return fail(KLE_ERR_SUP, "brick plan: region index out of range");
                 const int64_t i = brick_ir_node(D, ir, Lx, Ly);
@@ -900,6 +946,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     auto weight = [&](const BrickDesc &D) {
         double w = 0.0;
         for (int r = 0; r < D.nr; ++r) {
+            if (brick_row_null(bp.rowd.data(), (int64_t)D.rstart + r)) continue;
             const int64_t i = brick_ir_node(D, brick_row_ir(bp.rowd.data(), (int64_t)D.rstart + r), Lx, Ly);
             const int d = srow[i];
             const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));
@@ -939,6 +986,7 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
             long long sb = 0;
             int one = 0, two = 0;
             for (int r = 0; r < D.nr; ++r) {
+                if (brick_row_null(bp.rowd.data(), (int64_t)D.rstart + r)) continue;
                 const int64_t i = brick_ir_node(D, brick_row_ir(bp.rowd.data(), (int64_t)D.rstart + r), Lx, Ly);
                 const int d = srow[i];
                 const int k0 = (d & 15) + ((d >> 12) & 15) * (((d >> 4) & 15) + ((d >> 16) & 15) * ((d >> 8) & 15));

@@ -753,6 +753,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_gsym_brick") {
         KLE_ARG(value == 0 || value == 1, "spmv_gsym_brick: 0 or 1");
         g_tune.spmv_gsym_brick = value;
+    } else if (k == "spmv_brick_fcost") {
+        KLE_ARG(value == 0 || value == 1, "spmv_brick_fcost: 0 or 1");
+        g_tune.spmv_brick_fcost = value;
+    } else if (k == "spmv_brick_pair") {
+        KLE_ARG(value == 0 || value == 1, "spmv_brick_pair: 0 or 1");
+        g_tune.spmv_brick_pair = value;
     } else if (k == "spmv_brick_singles") {
         KLE_ARG(value == 0 || value == 1, "spmv_brick_singles: 0 or 1");
         g_tune.spmv_brick_singles = value;
@@ -873,6 +879,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_bands") *value = g_tune.spmv_brick_bands;
     else if (k == "spmv_brick_tail") *value = g_tune.spmv_brick_tail;
     else if (k == "spmv_brick_singles") *value = g_tune.spmv_brick_singles;
+    else if (k == "spmv_brick_pair") *value = g_tune.spmv_brick_pair;
+    else if (k == "spmv_brick_fcost") *value = g_tune.spmv_brick_fcost;
     else if (k == "spmv_brick_tile") *value = g_tune.spmv_brick_tile;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
     else if (k == "upd_unroll") *value = g_tune.upd_unroll;

@@ -409,6 +409,8 @@ struct Tuning {
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
     int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
+    int spmv_brick_fcost = 0;  // brick SpMV (read at build): with pairs, plan by blocks (1) or by 64-block passes (0)
+    int spmv_brick_pair = 1;  // brick SpMV (read at build): rows in units of two whose tails share one 64-lane item
     int spmv_brick_singles = 1;  // brick SpMV (read at build): rows of one stored block formed by the gather, not as 64-lane items of the bricks
     int spmv_brick_tail = 0;   // brick SpMV (read at build): per mille of the mean brick cut off the heavy bricks into tail tiles (0 none)
     int spmv_brick_tile = 20;  // brick SpMV (read at build): a tail tile's weight, per mille of the mean brick
