@@ -40,6 +40,7 @@
 // unless KLE_COMM_TIMEOUT_S > 0 sets one.  The exit status is KLE_IPC_EXIT
 // (75): the host thread is blocked inside the runtime and cannot return an
 // error, and a process exit is what frees the stuck queue.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -117,15 +118,29 @@ struct IpcState {
 
 // out[i] = sum over ranks r = 0 .. nr-1 of slot r (my own term from out
 // itself), in rank order: the same value on every rank
+// The peers' slots are read at system scope: their copies land in this
+// rank's fine-grained mailbox from other processes (copy engines, other
+// XCDs' caches), and a plain load may return the line this kernel's
+// previous launch left in its L2 -- last iteration's partials (a rare
+// stale sum, seen as a NaN in an 8-rank pipelined CG on one GPU).
 __global__ void k_rank_sum(int64_t n, int nr, int me, const double *__restrict__ slots, int64_t cap,
                            double *__restrict__ out)
 {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double mine = out[i];
         double s = 0.0;
-        for (int r = 0; r < nr; ++r) s += r == me ? mine : slots[(int64_t)r * cap + i];
+        for (int r = 0; r < nr; ++r)
+            s += r == me ? mine
+                         : __hip_atomic_load(slots + (int64_t)r * cap + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         out[i] = s;
     }
+}
+
+// A slot out of this rank's mailbox at system scope (k_rank_sum's reason)
+__global__ void k_slot_copy(int64_t n, const double *__restrict__ src, double *__restrict__ dst)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 static int wait_ge(hipStream_t st, uint64_t *flag, uint64_t v)
@@ -232,7 +247,11 @@ static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, const doub
     IpcState &P = *c->ipc;
     const uint64_t s = ++P.rseq[ch][from];
     KLE_TRY(wait_ge(st, P.data_flag(c->rank, ch, from), s));
-    if (n) KLE_HIP(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+    if (n) {
+        hipLaunchKernelGGL(k_slot_copy, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (n + 255) / 256))),
+                           dim3(256), 0, st, n, src, dst);
+        KLE_HIP(hipGetLastError());
+    }
     return post(st, P.ack_flag(from, ch, c->rank), s);
 }
 
