@@ -63,6 +63,7 @@ __device__ __forceinline__ BItem bitem(int s, int muP, int muQ, int irP, int irQ
 {
     return {1, irP | irQ << 16, muP | muQ << 16, kbP | kbQ << 16, s | eP << 8 | eQ << 9};
 }
+constexpr int BI_NEWP = 1024;  // (sf: the item starts row P -- its x into the row registers)
 
 template <int WV, int D>
 __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp,
@@ -194,12 +195,14 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         if (ph == 0) {  // A's passes
             load_v(A, A, ki, 0, 64, vn, rn);
             itn = bitem(64, A.mu, A.mu, A.ir, A.ir, ki, 0, !hasB && ki + 64 >= A.mu, 0);
+            if (ki == 0) itn.sf |= BI_NEWP;
             ki += 64;
             if (ki >= aend) ph = hasB ? 1 : 3;
         } else if (ph == 1) {  // A's and B's last partial passes
             const int s = A.mu - aend;
             load_v(A, B, aend, bend, s, vn, rn);
             itn = bitem(s, A.mu, B.mu, A.ir, B.ir, aend, bend, 1, bend == 0);
+            if (aend == 0) itn.sf |= BI_NEWP;
             ki = 0;
             ph = bend > 0 ? 2 : 3;
         } else {  // B's full passes
@@ -308,6 +311,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     // the wait for the summed item is a fixed vmcnt(9 D).
     if (i0.ok) {
         double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        double cx0 = 0.0, cx1 = 0.0, cx2 = 0.0;  // x of the current row, kept across its items
         // the row's direct sum (fixed-order DPP, fp64), one writer, into y --
         // the gather adds the bricks' transposed sums to it (8 MB of stores
         // at config 2: the only ones before the end)
@@ -326,14 +330,25 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
             if (!it.ok) return false;
             const int is = it.sf & 255, irP = it.ir & 0xFFFF, irQ = (int)((unsigned)it.ir >> 16);
             const bool q = lane >= is;
-            // x of the lane's row (P's below s, Q's from s on)
-            const double p0 = uni_d(xl[irP]), p1 = uni_d(xl[RN + irP]), p2 = uni_d(xl[2 * RN + irP]);
+            // x of the lane's row (P's below s, Q's from s on); the row
+            // registers hold P's from its first item on, Q's after a shared
+            // one (0.35 % ahead of reading it per item, profiles/r05/pair/)
+            double p0, p1, p2;
+            if (it.sf & BI_NEWP) {
+                p0 = uni_d(xl[irP]);
+                p1 = uni_d(xl[RN + irP]);
+                p2 = uni_d(xl[2 * RN + irP]);
+                cx0 = p0, cx1 = p1, cx2 = p2;
+            } else {
+                p0 = cx0, p1 = cx1, p2 = cx2;
+            }
             double c0 = p0, c1 = p1, c2 = p2;
             if (is < 64) {
                 const double q0 = uni_d(xl[irQ]), q1 = uni_d(xl[RN + irQ]), q2 = uni_d(xl[2 * RN + irQ]);
                 c0 = q ? q0 : p0;
                 c1 = q ? q1 : p1;
                 c2 = q ? q2 : p2;
+                cx0 = q0, cx1 = q1, cx2 = q2;
             }
             const double xj0 = xl[rr], xj1 = xl[RN + rr], xj2 = xl[2 * RN + rr];
             sym_wait9<9 * D>(vv);
