@@ -188,8 +188,10 @@ int kle_ctx_get_comm_info(kle_ctx *ctx, int *count, int *rank);
  * plan of the symmetric SpMV for an Lx x Ly x Lz box lattice of p-node
  * elements (dirichlet: boundary rows the diagonal alone) on ncu CUs, at
  * most `rounds` bricks per CU (split: forced counts nbx + 100 nby + 10000 nbz, 0
- * planned).  info: bricks, bricks along x / y / z, LDS bytes; stats: largest
- * brick's bytes over the mean, region entries per row, stored blocks. */
+ * planned).  info[5]: bricks, bricks along x / y / z, LDS bytes; stats[6]:
+ * largest brick's bytes over the mean, region entries per row, stored blocks,
+ * modelled microseconds, 64-lane items streamed, share of their lanes that
+ * carry a block. */
 int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, int ncu, int rounds, int split, int *info,
                        double *stats);
 /* Per-kernel HIP-event timing of the hot kernels (SpMV, CG updates). */

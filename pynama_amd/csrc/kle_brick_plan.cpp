@@ -980,6 +980,34 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
     stats[1] = (double)bp.ws_entries / n;
     stats[2] = (double)blocks;
     stats[3] = bp.model_us;
+    // the items the bricks stream (a unit of two rows: their full passes and
+    // one shared item) and the share of their lanes that carry a block
+    {
+        auto rmu = [&](int64_t r) {
+            const int d = bp.rowd[2 * r];
+            const int dbx = d & 15, dby = (d >> 4) & 15, dbz = (d >> 8) & 15;
+            const int bnx = (d >> 12) & 15, bny = (d >> 16) & 15, bnz = (d >> 20) & 15;
+            return bnx * bny * bnz - (dbx + bnx * (dby + bny * dbz));
+        };
+        int64_t items = 0, blocks_b = 0;
+        for (const BrickDesc &D : bp.bricks)
+            for (int u = 0; u < D.nr / 2; ++u) {
+                const int64_t ra = (int64_t)D.rstart + 2 * u, rb = ra + 1;
+                const int ma = rmu(ra);
+                blocks_b += ma;
+                if (brick_row_null(bp.rowd.data(), rb)) {
+                    items += (ma + 63) / 64;
+                } else {
+                    const int mb = rmu(rb);
+                    blocks_b += mb;
+                    if (ma % 64 == 0 || mb % 64 == 0 || ma % 64 + mb % 64 > 64)
+                        return fail(KLE_ERR_SUP, "brick plan: a unit whose tails do not share an item");
+                    items += ma / 64 + mb / 64 + 1;
+                }
+            }
+        stats[4] = (double)items;
+        stats[5] = items ? (double)blocks_b / (64.0 * (double)items) : 0.0;
+    }
     if (getenv("KLE_BRICK_DEBUG"))
         for (const BrickDesc &D : bp.bricks) {
             // (stored blocks, rows of one stored block, rows past one 64-block pass)

@@ -370,4 +370,5 @@ def test_brick_planner_covers_the_lattice_and_balances(pa, lat, p, ncu, must):
     assert info[4] <= 163840
     if lat == (81, 65, 65) and ncu == 256:
         assert st[0] < 1.03, st[0]  # (1.026 with the one-block rows out of the bricks)
+        assert st[5] > 0.95, st[5]  # (paired tails: 97.5 % of the item lanes carry a block, 502k items; unpaired 76.6 %, 640k)
         assert st[1] < 2.2, st[1]  # (region entries per row)
