@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_gsym_brick(const GBrickD
         R.v = vb + (int64_t)rdesc[4 * r] * 16;
         R.s = sb + rdesc[4 * r + 1];
         R.mu = rdesc[4 * r + 2];
-        R.r = r;
+        R.r = rdesc[4 * r + 3];  // (the row's dictionary entry: the brick's rows lead it)
     };
     // the values of one 64-block pass (lanes past the row's end re-read its
     // last block; their results go nowhere) and the blocks' positions

@@ -1146,7 +1146,9 @@ static bool gbrick_ranges(int64_t n, int64_t glo, int64_t ntot, const std::vecto
 {
     if (n <= 0) return false;
     std::vector<double> P(n + 1, 0.0);
-    for (int64_t i = 0; i < n; ++i) P[i + 1] = P[i] + 4608.0 * ((smu[i] + 63) / 64);
+    // (a row of one stored block costs nothing when the gather forms it)
+    for (int64_t i = 0; i < n; ++i)
+        P[i + 1] = P[i] + (g_tune.spmv_brick_singles && smu[i] == 1 ? 0.0 : 4608.0 * ((smu[i] + 63) / 64));
     std::vector<int> mark(std::max<int64_t>(ntot, 1), -1);
     int stamp = 0;
     // k bricks per CU (whole rounds of ncu bricks: a partial last round would
@@ -1467,6 +1469,7 @@ static int gsym_build(kle_mat *A)
         // offset, stored blocks), then their bounds
         std::vector<GBrickDesc> hb(ng);
         std::vector<int> rowd(4 * (size_t)std::max<int64_t>(n, 1), 0);
+        std::vector<unsigned long long> ssm((n + 63) / 64 + 1, 0ull);  // (one-block rows per 64-row slice)
         for (int64_t q = 0; q < ng; ++q) {
             GBrickDesc &B = hb[q];
             const int64_t r0 = gst[q], r1 = gst[q + 1];
@@ -1478,11 +1481,23 @@ static int gsym_build(kle_mat *A)
             B.vbase = svp[r0];
             B.sbase = sbp[r0];
             B.wsoff = wptr[q];
+            // slots of the brick's rows (value offset / 16, position offset,
+            // blocks, the row's dictionary entry); the rows of one stored
+            // block go to the gather instead (spmv_brick_singles; box bricks
+            // alike), so nr counts the others
+            int64_t k = r0;
             for (int64_t i = r0; i < r1; ++i) {
-                rowd[4 * i] = (int)((svp[i] - svp[r0]) / 16);
-                rowd[4 * i + 1] = (int)(sbp[i] - sbp[r0]);
-                rowd[4 * i + 2] = smu[i];
+                if (g_tune.spmv_brick_singles && smu[i] == 1) {
+                    ssm[i >> 6] |= 1ull << (i & 63);
+                    continue;
+                }
+                rowd[4 * k] = (int)((svp[i] - svp[r0]) / 16);
+                rowd[4 * k + 1] = (int)(sbp[i] - sbp[r0]);
+                rowd[4 * k + 2] = smu[i];
+                rowd[4 * k + 3] = (int)(i - r0);
+                ++k;
             }
+            B.nr = (int)(k - r0);
         }
         if (hipMalloc(&A->d_bdesc, sizeof(GBrickDesc) * ng) != hipSuccess ||
             hipMalloc(&A->d_browd, sizeof(int) * rowd.size()) != hipSuccess) {
@@ -1491,6 +1506,14 @@ static int gsym_build(kle_mat *A)
         }
         KLE_HIP(hipMemcpy(A->d_bdesc, hb.data(), sizeof(GBrickDesc) * ng, hipMemcpyHostToDevice));
         KLE_HIP(hipMemcpy(A->d_browd, rowd.data(), sizeof(int) * rowd.size(), hipMemcpyHostToDevice));
+        if (g_tune.spmv_brick_singles) {
+            if (hipMalloc(&A->d_ssingle, sizeof(unsigned long long) * ssm.size()) != hipSuccess) {
+                (void)hipGetLastError();
+                A->d_ssingle = nullptr;
+                return done(fail(KLE_ERR_MEM, "out of device memory for the graph bricks' one-block rows"));
+            }
+            KLE_HIP(hipMemcpy(A->d_ssingle, ssm.data(), sizeof(unsigned long long) * ssm.size(), hipMemcpyHostToDevice));
+        }
         A->nbricks = (int)ng;
         A->brick_lds_u = US;
         A->brick_lds = (int)brick_lds(US);
@@ -1552,7 +1575,8 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     hipStream_t st = c->stream;
     if (A->sym_gbrick && c->nranks == 1) {
         KLE_TRY(gbrick_launch(A, x, y, istate));
-        return gsym_gather(A, y->d, 0, A->nrows, istate, dpart ? x->d : nullptr, dpart, 1, st);
+        return gsym_gather(A, y->d, 0, A->nrows, istate, dpart ? x->d : nullptr, dpart, 1, st,
+                           A->d_ssingle ? x->d : nullptr);
     }
     const int G = A->sym_reg[3], WV = A->sym_reg[4];
     const int64_t n = A->nrows, ng = (n + G - 1) / G, n1 = A->sym_reg[2], nhi = A->ghost_hi / 3;
@@ -1634,7 +1658,8 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
         KLE_TRY(tiles(1));
     }
     const int64_t ntot = n + (dist ? nhi : 0);
-    KLE_TRY(gsym_gather(A, y->d, 0, ntot, istate, dpart && !dist ? x->d : nullptr, dpart, A->sym_gbrick, st));
+    KLE_TRY(gsym_gather(A, y->d, 0, ntot, istate, dpart && !dist ? x->d : nullptr, dpart, A->sym_gbrick, st,
+                        A->sym_gbrick && A->d_ssingle ? x->d : nullptr));
     KLE_HIP(hipGetLastError());
     if (!dist) return 0;
     // the upper ghost nodes' sums back to their owners, added in ascending
