@@ -65,7 +65,11 @@ __device__ __forceinline__ BItem bitem(int s, int muP, int muQ, int irP, int irQ
 }
 constexpr int BI_NEWP = 1024;  // (sf: the item starts row P -- its x into the row registers)
 
-template <int WV, int D>
+// FF: the first item's registers are in flight when the item loop starts,
+// which holds only while the compiler does not copy them on the way there
+// (checked in the ISA; a variant with two items in flight ahead of the summed
+// one -- no faster, round 5 -- had them moved, wrong products, and is gone)
+template <int WV, bool FF = true>
 __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp,
                                                                  const BrickDesc *__restrict__ bd,
                                                                  const int2 *__restrict__ rowd,
@@ -76,10 +80,12 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
 {
     KLE_PROBE_CONST
     constexpr int NT = 64 * WV;
-    static_assert(D == 1 || D == 2, "one or two items ahead");
+    constexpr int D = 1;  // items in flight ahead of the summed one
     extern __shared__ double lds[];
     KLE_PROBE_TS(ts0)
-    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
+#ifdef KLE_PROBE_BUILD
+    __shared__ unsigned pmx[2];
+#endif
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int NU = bd[b].nr / 2;  // units of two rows (kle_brick_plan.cpp)
@@ -92,6 +98,65 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     double *wred = lds + 3 * RN + 3 * RS;
     int *ctr = reinterpret_cast<int *>(wred + 2 * WV);
     const int64_t Lxy = (int64_t)Lx * Ly;
+    // 2a. x of the region into LDS (nodes off the lattice read 0), its max
+    // |x|; the sums zeroed.  Line (ry, rz) of the region is 3 RX contiguous
+    // doubles of x; a thread takes one position in a line and every fstep-th
+    // line, FB loads in flight (unconditional: clamped addresses, masked
+    // values).  FF: the first FB loads go out here, before anything waits on
+    // the row descriptors and before the first items' value loads (asm,
+    // waited for with vmcnt(9 D) in 2b), so they queue neither behind the
+    // descriptor round trip nor behind the whole chip's first value loads.
+    double xm = 0.0;
+    int bad = 0;
+    constexpr int FB = 12;
+    const int L3 = 3 * RX, NL = RY * RZ;
+    const int c3 = threadIdx.x % L3, l0 = threadIdx.x / L3, fstep = NT / L3;
+    const int rx = c3 / 3, c = c3 - 3 * rx, gx = ox + rx;
+    const bool xok = l0 < fstep && gx >= 0 && gx < Lx;
+    // (line l = (ry, rz) and its offset in x stepped by fstep lines without
+    // a division per load; offsets in 32 bits: brick_setup refuses lattices
+    // of 2^29 / 3 or more ext nodes)
+    const int dz = fstep / RY, dy = fstep - dz * RY, sy = 3 * Lx, sz = 3 * Lx * Ly;
+    int fz = l0 / RY, fy = l0 - fz * RY, fo = 3 * gx + c + sy * (oy + fy) + sz * (oz + zo + fz);
+    auto fnode = [&](int l, bool &ok) -> int {
+        const int gy = oy + fy, gz = oz + fz;
+        ok = xok & (l < NL) & (gy >= 0) & (gy < Ly) & (gz + zo >= 0) & (gz < Lz + hp);  // (no branches)
+        const int off = ok ? fo : 0;
+        fy += dy;
+        fz += dz;
+        fo += sy * dy + sz * dz;
+        if (fy >= RY) {
+            fy -= RY;
+            ++fz;
+            fo += sz - sy * RY;
+        }
+        return off;
+    };
+    auto fstore = [&](int lb, double *fv) {
+#pragma unroll
+        for (int f = 0; f < FB; ++f) {
+            const int l = lb + f * fstep;
+            const bool st = l0 < fstep && l < NL;
+            xl[st ? c * RN + rx + RX * l : 4 * RN + lane] = fv[f];  // (else a dummy slot of the sums)
+            const double a = fabs(fv[f]);
+            bad |= !(a <= 1.7976931348623157e308);
+            xm = fmax(xm, a);
+        }
+    };
+    double fv0[FB];
+    unsigned okm = 0;
+    if constexpr (FF) {
+#pragma unroll
+        for (int f = 0; f < FB; ++f) {
+            bool ok;
+            const int off = fnode(l0 + f * fstep, ok);
+            okm |= (unsigned)ok << f;
+            ld_x1(fv0[f], x, 8u * (unsigned)off);
+        }
+    }
+    KLE_PROBE_TS(tsi)
+    // (read after the fill's loads are out: the compiler waits for it at once)
+    const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
     cint *rdesc = (cint *)(rowd + rstart);  // (address-space cast: scalar loads)
     const double *vb = sval + vbase;
     // a row from its descriptor (kle_brick.hpp): packed box (dbx, dby, dbz,
@@ -225,43 +290,41 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
             }
         }
     };
-    double v0[9], v1[9], v2[9];
-    int r0 = 0, r1 = 0, r2 = 0;
-    BItem i0, i1, i2;
-    issue(v0, r0, i0);
-    if (D == 2) issue(v1, r1, i1);
-    // 2. x of the region into LDS (nodes off the lattice read 0), its max |x|;
-    // the sums zeroed.  Line (ry, rz) of the region is 3 RX contiguous doubles
-    // of x; a thread takes one position in a line and every fstep-th line,
-    // FB loads in flight (unconditional: clamped addresses, masked values)
-    double xm = 0.0;
-    int bad = 0;
+    double v0[9], v1[9];
+    int r0 = 0, r1 = 0;
+    BItem i0, i1;
+#ifdef KLE_PROBE_BUILD
+    unsigned long long tsf = 0;
+    if (threadIdx.x == 0) pmx[0] = pmx[1] = 0;
+#endif
+    // 2b. the first item's value loads, then the fill's first loads landed
+    // (vmcnt(9): the value loads stay in flight), into LDS; further lines
+    // (regions of more than FB x fstep lines) after them
     {
-        constexpr int FB = 12;
-        const int L3 = 3 * RX, NL = RY * RZ;
-        const int c3 = threadIdx.x % L3, l0 = threadIdx.x / L3, fstep = NT / L3;
-        const int rx = c3 / 3, c = c3 - 3 * rx, gx = ox + rx;
-        const bool xok = l0 < fstep && gx >= 0 && gx < Lx;
-        for (int lb = l0; lb < NL; lb += FB * fstep) {
+        int lb = l0;
+        if constexpr (FF) {
+            issue(v0, r0, i0);
+            wait_x12<9 * D>(fv0);
+#ifdef KLE_PROBE_BUILD
+            tsf = probe_ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#endif
+#pragma unroll
+            for (int f = 0; f < FB; ++f) fv0[f] = (okm >> f) & 1u ? fv0[f] : 0.0;
+            fstore(lb, fv0);
+            lb += FB * fstep;
+        } else {
+            issue(v0, r0, i0);
+        }
+        for (; lb < NL; lb += FB * fstep) {
             double fv[FB];
 #pragma unroll
             for (int f = 0; f < FB; ++f) {
-                const int l = lb + f * fstep;
-                const int rz = l / RY, ry = l - rz * RY, gy = oy + ry, gz = oz + rz;
-                const bool ok = xok && l < NL && gy >= 0 && gy < Ly && gz + zo >= 0 && gz < Lz + hp;
-                const int64_t node = ok ? gx + (int64_t)Lx * gy + Lxy * (gz + zo) : 0;
-                const double v = x[3 * node + c];
+                bool ok;
+                const int off = fnode(lb + f * fstep, ok);
+                const double v = x[off];
                 fv[f] = ok ? v : 0.0;
             }
-#pragma unroll
-            for (int f = 0; f < FB; ++f) {
-                const int l = lb + f * fstep;
-                const bool st = l0 < fstep && l < NL;
-                xl[st ? c * RN + rx + RX * l : 4 * RN + lane] = fv[f];  // (else a dummy slot of the sums)
-                const double a = fabs(fv[f]);
-                bad |= !(a <= 1.7976931348623157e308);
-                xm = fmax(xm, a);
-            }
+            fstore(lb, fv);
         }
     }
     for (int k = threadIdx.x; k < 3 * RS; k += NT) acc[k] = 0ull;
@@ -273,6 +336,13 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         wred[WV + w] = anybad ? 1.0 : 0.0;
     }
     if (threadIdx.x == 0) *ctr = NSTAT * WV;
+#ifdef KLE_PROBE_BUILD
+    // (probe: the latest wave's fill landed and its arrival at the barrier)
+    if (probe_ts && lane == 0) {
+        atomicMax(&pmx[0], (unsigned)(tsf - ts0));
+        atomicMax(&pmx[1], (unsigned)(__builtin_amdgcn_s_memrealtime() - ts0));
+    }
+#endif
     __builtin_amdgcn_s_waitcnt(0xC07F);  // LDS stores done (lgkmcnt 0); the value loads stay in flight
     __builtin_amdgcn_s_barrier();
     if (__builtin_amdgcn_readfirstlane(stop) != 0) return;  // (nothing written yet)
@@ -388,18 +458,12 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
             }
             return true;
         };
-        if constexpr (D == 1) {
-            while (step(v0, r0, i0, v1, r1, i1) && step(v1, r1, i1, v0, r0, i0)) {
-            }
-        } else {
-            while (step(v0, r0, i0, v2, r2, i2) && step(v1, r1, i1, v0, r0, i0) && step(v2, r2, i2, v1, r1, i1)) {
-            }
+        while (step(v0, r0, i0, v1, r1, i1) && step(v1, r1, i1, v0, r0, i0)) {
         }
     }
     // the last (re-read) loads land before their registers are reused
     sym_wait9<0>(v0);
     sym_wait9<0>(v1);
-    if (D == 2) sym_wait9<0>(v2);
     __syncthreads();
     KLE_PROBE_TS(ts2)
     // 4. the region's transposed sums, once, [entry][3] (coalesced; nodes
@@ -412,7 +476,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
         dst[t] = fx_to_d(acc[c * RS + k]) * T1 * T2;
     }
-    KLE_PROBE_TS_END(b, ts0, ts1, ts2)
+    KLE_PROBE_TS_END4(b, ts0, ts1, ts2, ts0 + pmx[0], ts0 + pmx[1])
 }
 
 // y[0 .. n) += r: the lower neighbour's sums for this slab's lowest nodes
@@ -521,12 +585,34 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
     bp->pair = g_tune.spmv_brick_pair;
     bp->fcost = g_tune.spmv_brick_fcost;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
-    try {  // (no exception may cross the C ABI: a planner failure is a refusal)
-        why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], (int)(A->ghost_hi / plane3),
-                         std::max(1, A->ctx->num_cus), g_tune.spmv_brick_max, g_tune.spmv_brick_rounds,
-                         g_tune.spmv_brick_split, cnt, srow, P, *bp);
-    } catch (const std::exception &e) {
-        why = std::string("brick planner: ") + e.what();
+    if (A->ghost_lo + 3 * A->nrows + A->ghost_hi >= (int64_t)1 << 29) {  // (the fill's 32-bit byte offsets)
+        delete bp;
+        why = "brick SpMV: 2^29 / 3 ext nodes or more";
+        *plan_out = nullptr;
+        return 0;
+    }
+    // k whole rounds of one brick per CU, k from spmv_brick_rounds up to the
+    // fewest whose largest region fits the LDS (config 4, p = 6 on one GPU:
+    // 4 rounds; one round at p = 4 and for p = 6 z slabs of 8 ranks)
+    for (int rounds = std::max(1, g_tune.spmv_brick_rounds); rounds <= BRICK_MAX_ROUNDS; ++rounds) {
+        try {  // (no exception may cross the C ABI: a planner failure is a refusal)
+            why = brick_plan((int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2],
+                             (int)(A->ghost_hi / plane3), std::max(1, A->ctx->num_cus), g_tune.spmv_brick_max, rounds,
+                             g_tune.spmv_brick_split, cnt, srow, P, *bp);
+        } catch (const std::exception &e) {
+            why = std::string("brick planner: ") + e.what();
+        }
+        if (why.empty() || g_tune.spmv_brick_max > 0 || g_tune.spmv_brick_split > 0 ||
+            why.find("fits the LDS") == std::string::npos)
+            break;
+        *bp = BrickPlan{};
+        bp->pad = g_tune.spmv_brick_pad;
+        bp->bands = g_tune.spmv_brick_bands;
+        bp->tail = g_tune.spmv_brick_tail;
+        bp->tile = g_tune.spmv_brick_tile;
+        bp->singles = g_tune.spmv_brick_singles;
+        bp->pair = g_tune.spmv_brick_pair;
+        bp->fcost = g_tune.spmv_brick_fcost;
     }
     if (!why.empty()) {
         delete bp;
@@ -638,6 +724,7 @@ int brick_finish(kle_mat *A, void *plan)
         KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(),
                           hipMemcpyHostToDevice));
         A->brick_gparts = (int)(runptr[ns] / std::max<int64_t>(ns, 1));  // (runs per 64 rows, for the log)
+        A->gather_rps = (int)((runptr[ns] + ns - 1) / std::max<int64_t>(ns, 1));
     }
     if (!bp->srows.empty()) {
         // the one-block rows per 64-row slice of the owned rows (the gather
@@ -752,10 +839,10 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     // (spmv_brick_waves: fewer waves per CU keep fewer loads in flight)
     if (A->nbricks == 0) {
         // (no brick: every row of one block, formed by the gather)
-    } else if (g_tune.spmv_brick_ahead == 2) go(k_nb_spmv_sym_brick<BRICK_WV, 2>, 1, BRICK_WV);
-    else if (g_tune.spmv_brick_waves == 8) go(k_nb_spmv_sym_brick<8, 1>, 2, 8);
-    else if (g_tune.spmv_brick_waves == 12) go(k_nb_spmv_sym_brick<12, 1>, 3, 12);
-    else go(k_nb_spmv_sym_brick<BRICK_WV, 1>, 0, BRICK_WV);
+    } else if (g_tune.spmv_brick_fill == 0) go(k_nb_spmv_sym_brick<BRICK_WV, false>, 1, BRICK_WV);
+    else if (g_tune.spmv_brick_waves == 8) go(k_nb_spmv_sym_brick<8>, 2, 8);
+    else if (g_tune.spmv_brick_waves == 12) go(k_nb_spmv_sym_brick<12>, 3, 12);
+    else go(k_nb_spmv_sym_brick<BRICK_WV>, 0, BRICK_WV);
     KLE_HIP(hipGetLastError());
     // the gather (kle_sym.hip gsym_gather): per row its direct sum in y, then
     // the runs of the regions holding it, in ascending brick order

@@ -40,6 +40,7 @@ inline int64_t brick_ir_node(const BrickDesc &D, int ir, int64_t Lx, int64_t Ly)
     return (D.ox + rx) + Lx * ((D.oy + ry) + Ly * (int64_t)(D.oz + rz));
 }
 
+constexpr int BRICK_MAX_ROUNDS = 8;        // bricks per CU the planner goes up to when fewer do not fit the LDS
 constexpr int BRICK_WV = 16;            // waves per brick workgroup (one workgroup per CU)
 constexpr size_t BRICK_LDS_CAP = 163840;  // LDS per CU
 constexpr size_t BRICK_LDS_MIN = 82 * 1024;  // above half the CU's LDS: never two bricks on one CU

@@ -744,10 +744,7 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_early") {
         KLE_ARG(value == 0 || value == 1, "spmv_sym_early: 0 or 1");
         g_tune.spmv_sym_early = value;
-    } else if (k == "spmv_brick_ahead") {
-        KLE_ARG(value == 1 || value == 2, "spmv_brick_ahead: 1 or 2");
-        g_tune.spmv_brick_ahead = value;
-    } else if (k == "upd_unroll") {
+        } else if (k == "upd_unroll") {
         KLE_ARG(value == 1 || value == 2, "upd_unroll: 1 or 2");
         g_tune.upd_unroll = value;
     } else if (k == "spmv_gsym_brick") {
@@ -771,6 +768,12 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_bands") {
         KLE_ARG(value == 0 || value == 1, "spmv_brick_bands: 0 or 1");
         g_tune.spmv_brick_bands = value;
+    } else if (k == "spmv_brick_fill") {
+        KLE_ARG(value == 0 || value == 1, "spmv_brick_fill: 0 or 1");
+        g_tune.spmv_brick_fill = value;
+    } else if (k == "spmv_gather_wps") {
+        KLE_ARG(value == 0 || value == 1 || value == 2 || value == 4, "spmv_gather_wps: 0 (auto), 1, 2 or 4");
+        g_tune.spmv_gather_wps = value;
     } else if (k == "spmv_brick_waves") {
         KLE_ARG(value == 8 || value == 12 || value == 16, "spmv_brick_waves: 8, 12 or 16");
         g_tune.spmv_brick_waves = value;
@@ -795,6 +798,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
+    } else if (k == "ksp_corr_fault") {
+        KLE_ARG(value == 0 || value == 1, "ksp_corr_fault: 0 or 1 (test hook)");
+        g_tune.ksp_corr_fault = value;
     } else if (k == "ksp_refine") {
         KLE_ARG(value >= 0 && value <= 8, "ksp_refine: 0 .. 8");
         g_tune.ksp_refine = value;
@@ -869,7 +875,6 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_sym_waves") *value = g_tune.spmv_sym_waves;
     else if (k == "spmv_sym_tz") *value = g_tune.spmv_sym_tz;
     else if (k == "spmv_sym_brick") *value = g_tune.spmv_sym_brick;
-    else if (k == "spmv_brick_ahead") *value = g_tune.spmv_brick_ahead;
     else if (k == "spmv_brick_max") *value = g_tune.spmv_brick_max;
     else if (k == "spmv_brick_rounds") *value = g_tune.spmv_brick_rounds;
     else if (k == "spmv_brick_split") *value = g_tune.spmv_brick_split;
@@ -880,6 +885,8 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_tail") *value = g_tune.spmv_brick_tail;
     else if (k == "spmv_brick_singles") *value = g_tune.spmv_brick_singles;
     else if (k == "spmv_brick_pair") *value = g_tune.spmv_brick_pair;
+    else if (k == "spmv_gather_wps") *value = g_tune.spmv_gather_wps;
+    else if (k == "spmv_brick_fill") *value = g_tune.spmv_brick_fill;
     else if (k == "spmv_brick_fcost") *value = g_tune.spmv_brick_fcost;
     else if (k == "spmv_brick_tile") *value = g_tune.spmv_brick_tile;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
@@ -897,6 +904,7 @@ int kle_get_tuning(const char *key, int *value)
 #endif
     else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
     else if (k == "ksp_refine") *value = g_tune.ksp_refine;
+    else if (k == "ksp_corr_fault") *value = g_tune.ksp_corr_fault;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
     else if (k == "spmv_gsym_waves") *value = g_tune.spmv_gsym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;

@@ -264,6 +264,7 @@ struct kle_mat {
     int sym_brick = 0;
     int sym_gbrick = 0;  // unstructured: graph bricks (d_bdesc = GBrickDesc, d_browd = 4 ints per row)
     int brick_lds_u = 0;  // graph bricks: the largest dictionary
+    int gather_rps = 0;  // run-mask gather: runs per 64-row slice (rounded up; picks its waves per slice)
     int nbricks = 0, brick_lds = 0, brick_gparts = 0;  // (gather workgroups per brick)
     int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
     double brick_model_us = 0.0;    // the planner's modelled product time
@@ -381,6 +382,7 @@ struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
+    int ksp_corr_fault = 0;  // test hook: 1 = every correction solve of refine() ends in NaN (DIVERGED_NANORINF), to test that x is kept
     int ksp_refine = 2;  // CG / pipelined CG: up to this many correction solves when the true residual misses rtol (kle_ksp.hip refine; default of new KSPs); 0 PETSc's plain stop
     int upd_nt = 2;       // single-reduction CG update: every vector but u nontemporal (u stays in the Infinity Cache for the
                           // SpMV) -- 0 off, 1 on, 2 auto: from 2M local entries (12 vectors > the 256 MB cache); per CG
@@ -402,12 +404,13 @@ struct Tuning {
                               // sc1 422.1, nt 426.5; profiles/r04/ab/stpol_*.jsonl)
     int spmv_sym_early = 0;   // symmetric SpMV tiles: the first item's value loads issued with the x fill (1) or after it (0)
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
-    int spmv_brick_ahead = 1;  // brick SpMV: items in flight ahead of the summed one per wave (1 or 2)
     int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: planned, spmv_brick_rounds per CU)
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
     int alloc_contig = 0;  // matrix value arrays (read at allocation): 1 physically contiguous first (hipDeviceMallocContiguous; experiments), 0 plain hipMalloc
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
+    int spmv_brick_fill = 1;   // brick SpMV: 1 the region fill's first loads go out before the first items' value loads, 0 after
+    int spmv_gather_wps = 0;   // run-mask gather: waves per 64-row slice (1, 2, 4; 0 auto by the runs per slice)
     int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
     int spmv_brick_fcost = 0;  // brick SpMV (read at build): with pairs, plan by blocks (1) or by 64-block passes (0)
     int spmv_brick_pair = 1;  // brick SpMV (read at build): rows in units of two whose tails share one 64-lane item
@@ -461,7 +464,25 @@ extern int64_t g_probe_ts_cap;
             r[6] = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));                                \
         }                                                                                               \
     }
+// (r[7]: two more points of the workgroup's start, as 32-bit offsets from a)
+#define KLE_PROBE_TS_END4(slot, a, b, c, d, e)                                                         \
+    if (probe_ts) {                                                                                     \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                \
+        __syncthreads();                                                                                \
+        if (threadIdx.x == 0 && (int64_t)(slot) < probe_cap) {                                          \
+            unsigned long long *r = probe_ts + 8 * (int64_t)(slot);                                     \
+            r[0] = (unsigned long long)(slot);                                                          \
+            r[1] = a;                                                                                   \
+            r[2] = b;                                                                                   \
+            r[3] = c;                                                                                   \
+            r[4] = __builtin_amdgcn_s_memrealtime();                                                    \
+            r[5] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                                 \
+            r[6] = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));                                \
+            r[7] = ((d) - (a)) | (((e) - (a)) << 32);                                                   \
+        }                                                                                               \
+    }
 #else
+#define KLE_PROBE_TS_END4(slot, a, b, c, d, e)
 #define KLE_PROBE_PARAM
 #define KLE_PROBE_ARG
 #define KLE_PROBE_CONST constexpr int probe = 0;

@@ -33,8 +33,11 @@
 // Every collective therefore ends with a stream write of its ticket into a
 // host-pinned progress word, and a watchdog thread watches the issued tickets.
 // When one makes no progress it checks the processes of the peers that
-// collective waits on (their pids are exchanged at bootstrap; IPC peers share
-// the node): a peer that has exited ends this process after IPC_DEAD_GRACE_S.
+// collective waits on (pids and process start times are exchanged at
+// bootstrap): a peer that has exited -- or whose pid now names a later
+// process -- ends this process after IPC_DEAD_GRACE_S.  A peer this process
+// cannot see with the start time it reported (another PID namespace) gets no
+// such check.
 // A live peer doing long host-only work between collectives (I/O, CPU
 // assembly) is never cut off -- as with NCCL, operations have no timeout --
 // unless KLE_COMM_TIMEOUT_S > 0 sets one.  The exit status is KLE_IPC_EXIT
@@ -75,6 +78,7 @@ struct IpcState {
     char *local = nullptr;          // my mailbox
     std::vector<char *> peer;       // every rank's mailbox mapped here (peer[me] = local)
     std::vector<long> pid;          // every rank's process id (bootstrap)
+    std::vector<long long> pstart;  // its start time as seen here (-1: not visible, no dead-peer check)
     uint64_t sseq[IPC_NCH][IPC_MAXR] = {};  // deliveries sent to each rank, per channel
     uint64_t rseq[IPC_NCH][IPC_MAXR] = {};  // deliveries received from each rank, per channel
     int nranks = 1;
@@ -171,19 +175,41 @@ static int ipc_done(kle_ctx *c, hipStream_t st, IpcChannel ch, const std::vector
     return post(st, P.d_prog + k, ++P.issued[k]);
 }
 
-// has process pid ended?  (gone from /proc, or a zombie not yet reaped)
-static bool pid_dead(long pid)
+// A process's start time (field 22 of /proc/<pid>/stat, clock ticks after
+// boot) and state letter; -1 when /proc does not show it here
+static long long proc_start(long pid, char *state)
 {
     char path[64];
     snprintf(path, sizeof path, "/proc/%ld/stat", pid);
     FILE *f = fopen(path, "r");
-    if (!f) return true;
-    char buf[512];
+    if (!f) return -1;
+    char buf[1024];
     const size_t n = fread(buf, 1, sizeof buf - 1, f);
     fclose(f);
     buf[n] = 0;
-    const char *e = strrchr(buf, ')');  // (state follows the command name)
-    return e && e[1] == ' ' && (e[2] == 'Z' || e[2] == 'X');
+    const char *e = strrchr(buf, ')');  // (the fields follow the command name)
+    if (!e || e[1] != ' ') return -1;
+    if (state) *state = e[2];
+    const char *q = e + 2;  // field 3 (state)
+    for (int fld = 3; fld < 22 && *q; ++fld) {
+        q = strchr(q, ' ');
+        if (!q) return -1;
+        ++q;
+    }
+    return *q ? atoll(q) : -1;
+}
+
+// has process pid (started at start) ended?  Gone from /proc, a zombie not
+// yet reaped, or the pid reused by a later process.  Only for peers whose
+// pid and start time this process saw at bootstrap: ranks in other PID
+// namespaces (IPC allows containers that share --ipc=host but not --pid)
+// are never taken for dead -- for them only KLE_COMM_TIMEOUT_S applies.
+static bool pid_dead(long pid, long long start)
+{
+    if (pid <= 0 || start < 0) return false;  // (not verifiable from here)
+    char st = 0;
+    const long long s = proc_start(pid, &st);
+    return s < 0 || s != start || st == 'Z' || st == 'X';
 }
 
 static void ipc_watchdog(IpcState *P)
@@ -208,7 +234,7 @@ static void ipc_watchdog(IpcState *P)
                 std::lock_guard<std::mutex> lk(P->mu);
                 w = P->what[k];
                 for (int q : P->awaited[k])
-                    if (q >= 0 && q < (int)P->pid.size() && pid_dead(P->pid[q])) gone = q;
+                    if (q >= 0 && q < (int)P->pid.size() && pid_dead(P->pid[q], P->pstart[q])) gone = q;
             }
             if (gone < 0 && !(P->deadline_s > 0.0 && idle > P->deadline_s)) continue;
             if (gone >= 0)
@@ -462,21 +488,27 @@ int kle_ctx_enable_ipc(kle_ctx *c)
     }
     // all-gather of the handles over the host callbacks: one byte per
     // double, one-hot sums (exact), plus every rank's failure flag and pid
-    const int hb = (int)sizeof(hipIpcMemHandle_t), hs = hb + 2;
+    const int hb = (int)sizeof(hipIpcMemHandle_t), hs = hb + 3;
     std::vector<double> buf((size_t)c->nranks * hs, 0.0);
     const unsigned char *hpb = reinterpret_cast<const unsigned char *>(&h);
     for (int k = 0; k < hb; ++k) buf[(size_t)c->rank * hs + k] = hpb[k];
     buf[(size_t)c->rank * hs + hb] = bad;
     buf[(size_t)c->rank * hs + hb + 1] = (double)getpid();
+    buf[(size_t)c->rank * hs + hb + 2] = (double)proc_start((long)getpid(), nullptr);  // (< 2^53: exact)
     if (c->hcomm.allreduce(buf.data(), (int)buf.size(), c->hcomm.user)) {
         ipc_free(P, c->rank, true);
         return fail(KLE_ERR_COMM, "IPC bootstrap: host allreduce failed");
     }
     int any_bad = 0;
     P->pid.assign(c->nranks, 0);
+    P->pstart.assign(c->nranks, -1);
     for (int r = 0; r < c->nranks; ++r) {
         any_bad |= buf[(size_t)r * hs + hb] != 0.0;
         P->pid[r] = (long)buf[(size_t)r * hs + hb + 1];
+        // (the dead-peer check only for a peer whose pid this process sees
+        // with the start time that peer reported: same PID namespace)
+        const long long st = (long long)buf[(size_t)r * hs + hb + 2];
+        if (st >= 0 && proc_start(P->pid[r], nullptr) == st) P->pstart[r] = st;
     }
     P->peer.assign(c->nranks, nullptr);
     P->peer[c->rank] = P->local;

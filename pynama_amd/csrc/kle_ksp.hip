@@ -1719,7 +1719,32 @@ static int refine(kle_ksp *k, kle_vec *b, kle_vec *x)
             k->reason = reason0;
             k->rnorm = rnorm0;
         }
-        if (!rc) rc = kle_vec_axpy(x, 1.0, e);
+        if (!rc && g_tune.ksp_corr_fault) {  // (test hook: a correction that ends in NaN)
+            rc = kle_vec_set(e, __builtin_nan(""));
+            k->corr_reason = KLE_DIVERGED_NANORINF;
+        }
+        bool kept = false;  // (x left as it was: its true residual in k->q still holds)
+        if (!rc && k->corr_reason > 0) {
+            rc = kle_vec_axpy(x, 1.0, e);
+        } else if (!rc) {
+            // the correction broke down, met NaN/Inf or ran out of iterations:
+            // x + e only if e is finite and the true residual drops, else x
+            // stays as it was -- rv (the correction's right-hand
+            // side, spent) keeps x meanwhile
+            double en = 0.0;
+            rc = kle_vec_norm2(e, &en);
+            kept = true;
+            if (!rc && std::isfinite(en) && en > 0.0) {
+                const double rel0 = k->true_rel;
+                rc = kle_vec_copy(x, rv);
+                if (!rc) rc = kle_vec_axpy(x, 1.0, e);
+                if (!rc) rc = true_residual(k, b, x);
+                if (!rc && !(k->true_rel < rel0)) {
+                    rc = kle_vec_copy(rv, x);
+                    if (!rc) rc = true_residual(k, b, x);
+                }
+            }
+        }
         for (kle_vec *v : {rv, e})
             if (v) {
                 (void)hipStreamSynchronize(c->stream);
@@ -1727,7 +1752,7 @@ static int refine(kle_ksp *k, kle_vec *b, kle_vec *x)
                 delete v;
             }
         if (rc) return rc;
-        KLE_TRY(true_residual(k, b, x));
+        if (!kept) KLE_TRY(true_residual(k, b, x));
     }
     return 0;
 }

@@ -689,6 +689,7 @@ void sym_forget(kle_mat *A)
     A->d_sbp = nullptr;
     A->d_slid = nullptr;
     A->d_sdptr = A->d_sdict = A->d_sgptr = A->d_sgidx = A->d_sglist = nullptr;
+    A->gather_rps = 0;
     A->d_sgmask = nullptr;
     A->d_ssingle = nullptr;
     A->d_swptr = nullptr;
@@ -1027,7 +1028,14 @@ __global__ __launch_bounds__(64 * WV) void k_nb_spmv_gsym(
 // partial of (y, x) in dpart[blockIdx.x] (k_nb_sym_gather's fixed order).
 // N > 1: the rows past the owned ones (nrows .. ntot-1) are the upper ghost
 // nodes, whose sums go to gsend (the reverse halo's send buffer).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb_gsym_gather(int64_t nrows, int64_t ntot, const int *__restrict__ runptr,
+// WPS waves per slice (a workgroup: 4 slices, 256 WPS threads): wave q of a
+// slice sums the q-th WPS-th of its runs, and the slice's first wave adds
+// the WPS parts in order through LDS -- small parts have many short runs per
+// slice (a 1/8 slab about 21), whose loads one wave would chain.  The loads
+// that do not depend on the runs (runptr, the row's direct sum in y, xdot, a
+// one-block row's block and x) go out first.
+template <int WPS>
+__global__ __launch_bounds__(256 * WPS) __attribute__((amdgpu_num_sgpr(64))) void k_nb_gsym_gather(int64_t nrows, int64_t ntot, const int *__restrict__ runptr,
                                                         const int *__restrict__ rstart,
                                                         const unsigned long long *__restrict__ rmask,
                                                         const double *__restrict__ ws, double *__restrict__ y,
@@ -1040,50 +1048,93 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
                                                         const double *__restrict__ xs)
 {
     __shared__ double dred[4];
+    __shared__ double pred[WPS > 1 ? 4 * (WPS - 1) * 3 * 64 : 1];
     const int stop = istate ? __builtin_amdgcn_readfirstlane(istate[I_REASON]) : 0;  // (tested before the first store)
-    const int lane = threadIdx.x & 63;
-    const int64_t sl = sl0 + (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ws4 = wv / WPS, part = wv - ws4 * WPS;  // (slice of the workgroup, part of its runs)
+    const int64_t sl = sl0 + (int64_t)blockIdx.x * 4 + ws4;
     const int64_t j = sl * 64 + lane;
     const bool on = sl < sl1 && sl * 64 < ntot;  // (the slices [sl0, sl1) of this launch)
-    if (!on && !xdot) return;
+    const bool lead = part == 0;
     double dsum = 0.0;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    bool one = false;
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0, e0 = 0.0, e1 = 0.0, e2 = 0.0;
     if (on) {
+        int rb = runptr[sl];
+        const int re = runptr[sl + 1];
+        // (the first wave: the row's own terms, independent of the runs)
+        if (lead && j < nrows) {
+            one = single && sl < (nrows + 63) / 64 && ((single[sl] >> lane) & 1ull);
+            if (one) {
+                // (box bricks: a row of one stored block is no item of its
+                // brick; its direct sum B_ii x_i here, the expression the
+                // brick kernel evaluates -- the same bits)
+                const double *v = sval + svptr[j];
+                const double x0 = xs[3 * j], x1 = xs[3 * j + 1], x2 = xs[3 * j + 2];
+                d0 = v[0] * x0 + v[1] * x1 + v[2] * x2;
+                d1 = v[3] * x0 + v[4] * x1 + v[5] * x2;
+                d2 = v[6] * x0 + v[7] * x1 + v[8] * x2;
+            } else if (preload) {  // (the rows' direct sums are in y)
+                d0 = y[3 * j];
+                d1 = y[3 * j + 1];
+                d2 = y[3 * j + 2];
+            }
+            if (xdot) {
+                e0 = xdot[3 * j];
+                e1 = xdot[3 * j + 1];
+                e2 = xdot[3 * j + 2];
+            }
+        }
+        int r1 = re;
+        if constexpr (WPS > 1) {
+            const int cnt = re - rb;
+            r1 = rb + (cnt * (part + 1)) / WPS;
+            rb += (cnt * part) / WPS;
+        }
         const unsigned long long below = (1ull << lane) - 1ull;
-        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-        const int r1 = runptr[sl + 1];
         // (loads unconditional -- absent lanes re-read the run's first entry --
         // so the unrolled runs' loads are all in flight before the adds)
 #pragma unroll 8
-        for (int r = runptr[sl]; r < r1; ++r) {
+        for (int r = rb; r < r1; ++r) {
             const unsigned long long m = rmask[r];
-            const bool on = (m >> lane) & 1ull;
-            const double *p = ws + (int64_t)rstart[r] + (on ? 3 * __popcll(m & below) : 0);
+            const bool in = (m >> lane) & 1ull;
+            const double *p = ws + (int64_t)rstart[r] + (in ? 3 * __popcll(m & below) : 0);
             const double a0 = p[0], a1 = p[1], a2 = p[2];
-            s0 += on ? a0 : 0.0;
-            s1 += on ? a1 : 0.0;
-            s2 += on ? a2 : 0.0;
+            s0 += in ? a0 : 0.0;
+            s1 += in ? a1 : 0.0;
+            s2 += in ? a2 : 0.0;
         }
-        if (stop) return;  // (uniform: the whole workgroup)
-        if (j < nrows) {
-            // (box bricks: a row of one stored block is no item of its brick;
-            // its direct sum B_ii x_i here, the expression the brick kernel
-            // evaluates -- the same bits)
-            const bool one = single && sl < (nrows + 63) / 64 && ((single[sl] >> lane) & 1ull);
-            if (one) {
-                const double *v = sval + svptr[j];
-                const double x0 = xs[3 * j], x1 = xs[3 * j + 1], x2 = xs[3 * j + 2];
-                s0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
-                s1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
-                s2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
-            } else if (preload) {  // (the rows' direct sums are in y)
-                s0 += y[3 * j];
-                s1 += y[3 * j + 1];
-                s2 += y[3 * j + 2];
+    }
+    if constexpr (WPS > 1) {
+        // the parts in order: the first wave's own, then parts 1 .. WPS-1
+        if (!lead) {
+            double *q = pred + ((ws4 * (WPS - 1) + part - 1) * 3) * 64 + lane;
+            q[0] = s0;
+            q[64] = s1;
+            q[128] = s2;
+        }
+        __syncthreads();
+        if (lead) {
+#pragma unroll
+            for (int pp = 1; pp < WPS; ++pp) {
+                const double *q = pred + ((ws4 * (WPS - 1) + pp - 1) * 3) * 64 + lane;
+                s0 += q[0];
+                s1 += q[64];
+                s2 += q[128];
             }
+        }
+    }
+    if (stop) return;  // (uniform: the whole workgroup)
+    if (on && lead) {
+        if (j < nrows) {
+            s0 += d0;
+            s1 += d1;
+            s2 += d2;
             y[3 * j] = s0;
             y[3 * j + 1] = s1;
             y[3 * j + 2] = s2;
-            if (xdot) dsum = s0 * xdot[3 * j] + s1 * xdot[3 * j + 1] + s2 * xdot[3 * j + 2];
+            if (xdot) dsum = s0 * e0 + s1 * e1 + s2 * e2;
         } else if (j < ntot) {
             double *o = gsend + 3 * (j - nrows);
             o[0] = s0;
@@ -1091,10 +1142,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(64))) void k_nb
             o[2] = s2;
         }
     }
-    if (!xdot || stop) return;
+    if (!xdot) return;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
-    if ((threadIdx.x & 63) == 0) dred[threadIdx.x >> 6] = dsum;
+    if (lane == 0 && lead) dred[ws4] = dsum;
     __syncthreads();
     if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
 }
@@ -1431,6 +1482,7 @@ static int gsym_build(kle_mat *A)
     KLE_HIP(hipMemcpy(A->d_sdict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_swptr, wptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sglist, glist.data(), sizeof(int) * ng, hipMemcpyHostToDevice));
+    A->gather_rps = (int)((runptr[ns] + ns - 1) / std::max<int64_t>(ns, 1));
     KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
     KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(), hipMemcpyHostToDevice));
@@ -1562,9 +1614,17 @@ int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate
 {
     if (r1 <= r0) return 0;
     const int64_t s0 = r0 / 64, s1 = (r1 + 63) / 64, ntot = A->nrows + A->ghost_hi / 3;
-    hipLaunchKernelGGL(k_nb_gsym_gather, dim3((unsigned)((s1 - s0 + 3) / 4)), dim3(256), 0, st, A->nrows, ntot,
-                       A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y, A->d_sgsend, istate, xdot, dpart, preload,
-                       s0, s1, xs ? A->d_ssingle : nullptr, A->d_sval, A->d_svptr, xs);
+    // waves per slice by the runs per slice (spmv_gather_wps: 0 auto)
+    const int rps = A->gather_rps;
+    const int wps = g_tune.spmv_gather_wps ? g_tune.spmv_gather_wps : rps >= 8 ? 2 : 1;
+    auto go = [&](auto kern, int wp) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)((s1 - s0 + 3) / 4)), dim3(256 * wp), 0, st, A->nrows, ntot,
+                           A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y, A->d_sgsend, istate, xdot, dpart,
+                           preload, s0, s1, xs ? A->d_ssingle : nullptr, A->d_sval, A->d_svptr, xs);
+    };
+    if (wps == 4) go(k_nb_gsym_gather<4>, 4);
+    else if (wps == 2) go(k_nb_gsym_gather<2>, 2);
+    else go(k_nb_gsym_gather<1>, 1);
     KLE_HIP(hipGetLastError());
     return 0;
 }
@@ -2264,8 +2324,7 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_brick)
-        return std::string("k_nb_spmv_sym_brick<16,") + std::to_string(g_tune.spmv_brick_ahead) +
-               ">+k_nb_gsym_gather";
+        return std::string("k_nb_spmv_sym_brick<") + std::to_string(g_tune.spmv_brick_waves) + ">+k_nb_gsym_gather";
     if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather";
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +

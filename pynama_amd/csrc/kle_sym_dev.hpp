@@ -109,4 +109,22 @@ __device__ __forceinline__ void sym_wait9(double *v)
                  : "i"(N));
 }
 
+// One load of x for a brick's region fill (SGPR base + 32-bit byte offset),
+// in inline asm like the value loads: issued before the first items' value loads, it is waited for with
+// an explicit vmcnt that leaves those in flight (a compiler load would be
+// waited for with vmcnt(0) once the asm loads follow it).
+__device__ __forceinline__ void ld_x1(double &v, const double *base, unsigned byte_off)
+{
+    asm volatile("global_load_dwordx2 %0, %1, %2" : "=&v"(v) : "v"(byte_off), "s"(base) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_x12(double *v)
+{
+    asm volatile("s_waitcnt vmcnt(%12)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                   "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11])
+                 : "i"(N));
+}
+
 }  // namespace kle

@@ -63,13 +63,24 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         _close(yb, ref)
     for _ in range(3):
         np.testing.assert_array_equal((K * x).getArray(), yb)
-    # two items in flight ahead of the summed one instead of one: the same
-    # sums in the same order, bitwise
-    set_tuning("spmv_brick_ahead", 2)
+    # the region fill after the first items' value loads instead of before
+    # them: the same sums in the same order, bitwise
+    set_tuning("spmv_brick_fill", 0)
     try:
         np.testing.assert_array_equal((K * x).getArray(), yb)
     finally:
-        set_tuning("spmv_brick_ahead", 1)
+        set_tuning("spmv_brick_fill", 1)
+    # the gather with 1, 2 or 4 waves per 64-row slice (its parts summed in
+    # another grouping): the same product to rounding, each bitwise repeatable
+    for wps in (1, 2, 4):
+        set_tuning("spmv_gather_wps", wps)
+        try:
+            yw = (K * x).getArray().copy()
+            np.testing.assert_array_equal((K * x).getArray(), yw)
+        finally:
+            set_tuning("spmv_gather_wps", 0)
+        for ref in (y0, yh):
+            _close(yw, ref)
     # the ragged-band plans (spmv_brick_bands 1: bricks as row lists, other
     # regions) -- the same product to rounding
     set_tuning("spmv_brick_bands", 1)
@@ -119,6 +130,38 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         K.setOption(K.Option.SPD, True)
     assert np.linalg.norm(yb - yt) <= 1e-14 * np.linalg.norm(yt)
     np.testing.assert_array_equal((K * x).getArray(), yb)
+
+
+@pytest.mark.parametrize("nelem,ngl,split", [([12, 10, 6], 5, 12 + 100 * 10 + 10000 * 6),
+                                             ([8, 8, 6], 7, 8 + 100 * 8 + 10000 * 6)])
+def test_brick_spmv_whole_rounds_per_cu(pa, nelem, ngl, split):
+    """More bricks than CUs (k whole rounds of one brick per CU, as the planner
+    takes when one round's regions do not fit the LDS -- config 4 at p = 6):
+    the same product as the full storage and the exported CSR to rounding,
+    bitwise repeatable."""
+    from pynama_amd.runtime import set_tuning
+    _, mat = _mat(pa, nelem, ngl)
+    K = mat.K
+    K.setOption(K.Option.SPD, False)
+    x = K.createVecRight()
+    xa = np.random.default_rng(11).uniform(-1, 1, x.getLocalSize())
+    x.setArray(xa)
+    y0 = (K * x).getArray().copy()
+    ip, ix, d = K.getValuesCSR()
+    yh = sp.csr_matrix((d, ix, ip), shape=(len(ip) - 1, len(xa))) @ xa
+    set_tuning("spmv_brick_rounds", 4)
+    set_tuning("spmv_brick_split", split)
+    try:
+        K.setOption(K.Option.SPD, True)
+        assert K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
+        yb = (K * x).getArray().copy()
+        np.testing.assert_array_equal((K * x).getArray(), yb)
+    finally:
+        set_tuning("spmv_brick_rounds", 1)
+        set_tuning("spmv_brick_split", 0)
+        K.setOption(K.Option.SPD, True)
+    for ref in (y0, yh):
+        _close(yb, ref)
 
 
 def test_brick_spmv_edge_inputs(pa):

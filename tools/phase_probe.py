@@ -113,6 +113,12 @@ def main():
         # mean number of workgroups in flight and per-XCD spans
         per_xcd = {int(c): {"n": int((xcc == c).sum()), "span_us": float(en[xcc == c].max() - st[xcc == c].min())}
                    for c in np.unique(xcc)}
+        if (r[:, 7] != 0).any():  # (the brick kernel: the latest wave's fill landed, its barrier arrival)
+            fi = (r[:, 7] & 0xFFFFFFFF).astype(np.int64) / 100.0
+            fl = (r[:, 7] >> 32).astype(np.int64) / 100.0
+            extra = {"fill_landed_max_wave_us": pct(fi), "barrier_arrival_max_wave_us": pct(fl)}
+        else:
+            extra = {}
         summ = {"rep": rep, "kernel": kern, "mesh": a.mesh, "nelem": nelem, "ngl": a.ngl, "workgroups": int(len(r)),
                 "span_us": float(span), "sum_total_us": float(total.sum()),
                 "mean_in_flight": float(total.sum() / span),
@@ -121,7 +127,7 @@ def main():
                           "store": float(store.sum() / total.sum())},
                 "last_start_us": float(st.max()), "first_end_us": float(en.min()),
                 "loop_deciles_us": [float(np.percentile(loop, q)) for q in range(0, 101, 10)],
-                "per_xcd": per_xcd, "tuning": json.loads(a.tuning), "cg": a.cg}
+                "per_xcd": per_xcd, "tuning": json.loads(a.tuning), "cg": a.cg, **extra}
         print(json.dumps(summ), flush=True)
         np.save(os.path.join(a.out, f"phase_{a.mesh}_{rep}.npy"), r)
     set_tuning("spmv_sym_probe_ts", 0)
