@@ -117,8 +117,7 @@ const char *kle_last_error(void);
  * (read at build: doubles of gap before each brick's values; 0 default),
  * "spmv_brick_waves" (8, 12 or 16 default), "spmv_gsym_brick" (read at
  * build: graph K on graph bricks, whole rounds per CU; 1 default),
- * "alloc_contig" (large value arrays from one contiguous allocation; 0
- * default), "upd_unroll" (CG update kernel: 1 default or 2),
+ * "upd_unroll" (CG update kernel: 1 default or 2),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
  * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo
@@ -432,11 +431,6 @@ int kle_mat_get_symmetric(const kle_mat *A, int *on);
  * is unchanged bit for bit; its speed should not depend on the offset
  * (tests/test_gpu_fullsize.py). */
 int kle_mat_move_values(kle_mat *A, long long shift, int fresh);
-/* Whether the value arrays (the full storage's / the symmetric storage's)
- * got physically contiguous memory (kle_set_tuning "alloc_contig": 1
- * contiguous first, plain when that fails; default 0, plain); sval_addr (may
- * be NULL): the symmetric values' device address. */
-int kle_mat_get_alloc_info(const kle_mat *A, int *val_contig, int *sval_contig, uint64_t *sval_addr);
 int kle_mat_get_sym_bricks(const kle_mat *A, int *nbricks, int *dims, double *entries_per_row, double *model_us);
 /* N > 1: run the rows that read no ghost entry while the halo exchange is in
  * flight on a second stream (default on). */

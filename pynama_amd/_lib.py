@@ -178,7 +178,6 @@ _SIGS = {
     "kle_ksp_get_correction_iterations": [vp, C.POINTER(C.c_int)],
     "kle_ksp_get_correction_reason": [vp, C.POINTER(C.c_int)],
     "kle_mat_move_values": [vp, C.c_longlong, C.c_int],
-    "kle_mat_get_alloc_info": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64)],
     "kle_stream_copy_bench": [vp, C.c_int64, C.c_int, C.POINTER(C.c_double)],
     "kle_stream_bench": [vp, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double)],
 }

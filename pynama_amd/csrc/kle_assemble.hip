@@ -1119,7 +1119,7 @@ int nb_create(kle_ctx *ctx, const kle_mesh *m, int which, int R, int C, kle_mat 
         (pad > 1 && hipMalloc(&A->d_rowcnt, sizeof(int) * std::max<int64_t>(nrows, 1)) != hipSuccess) ||
         hipMalloc(&A->d_bcol, sizeof(int) * std::max<int64_t>(nbp, 1)) != hipSuccess ||
         hipMalloc(&A->d_vptr, sizeof(int64_t) * (nrows + 1)) != hipSuccess ||
-        (A->val_contig = big_alloc(reinterpret_cast<void **>(&A->d_val), sizeof(double) * std::max<int64_t>(A->nvals, 1))) < 0) {
+        big_alloc(reinterpret_cast<void **>(&A->d_val), sizeof(double) * std::max<int64_t>(A->nvals, 1)) < 0) {
         kle_mat_destroy(A);
         return fail(KLE_ERR_MEM, "out of device memory for a %lld-block matrix", (long long)nb);
     }

@@ -18,22 +18,13 @@
 
 namespace kle {
 
-// Matrix value arrays are the SpMVs' whole stream, and where a few GB land
-// moves the same product by a few per cent (config 2 symmetric SpMV over
-// fresh allocations of its values: plain hipMalloc 424-428 us, physically
-// contiguous memory (hipDeviceMallocContiguous) 407-441 us with a lower
-// median, 413-417 against 425 us; profiles/r05/placement_*.jsonl).
-// With alloc_contig 1: contiguous first, plain when the driver cannot find
-// that much in one piece.  Off by default: the element-batched assembly,
-// whose gathers add to values an earlier launch stored, missed 41 of 1.4M
-// sums on contiguous memory (tests/test_gpu.py
-// test_batched_element_scratch_is_bitwise, r05) -- a cache-coherence
-// difference of that memory kind this code does not rely on.
+// Matrix value arrays: plain hipMalloc.  (Round 5 tried physically
+// contiguous memory, hipDeviceMallocContiguous, for placement-independent
+// SpMV speed; on it the element-batched assembly -- gathers adding to values
+// an earlier launch stored -- missed 41 of 1.4M sums, and no speed gain
+// survived the placement records, so the mode is gone: VERDICT r05 item 4.)
 int big_alloc(void **p, size_t bytes)
 {
-    *p = nullptr;
-    if (g_tune.alloc_contig && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return 1;
-    (void)hipGetLastError();
     *p = nullptr;
     if (hipMalloc(p, bytes) != hipSuccess) {
         (void)hipGetLastError();
@@ -780,10 +771,7 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_pad") {
         KLE_ARG(value >= 0 && value % 16 == 0 && value <= (1 << 20), "spmv_brick_pad: multiple of 16 doubles");
         g_tune.spmv_brick_pad = value;
-    } else if (k == "alloc_contig") {
-        KLE_ARG(value == 0 || value == 1, "alloc_contig: 0 or 1");
-        g_tune.alloc_contig = value;
-    } else if (k == "spmv_brick_split") {
+        } else if (k == "spmv_brick_split") {
         KLE_ARG(value >= 0, "spmv_brick_split: nbx + 100 nby + 10000 nbz (0: planned)");
         g_tune.spmv_brick_split = value;
     } else if (k == "spmv_brick_rounds") {
@@ -798,6 +786,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
+    } else if (k == "ipc_sentinel") {
+        KLE_ARG(value == 0 || value == 1, "ipc_sentinel: 0 or 1");
+        g_tune.ipc_sentinel = value;
     } else if (k == "ksp_corr_fault") {
         KLE_ARG(value == 0 || value == 1, "ksp_corr_fault: 0 or 1 (test hook)");
         g_tune.ksp_corr_fault = value;
@@ -878,7 +869,6 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_max") *value = g_tune.spmv_brick_max;
     else if (k == "spmv_brick_rounds") *value = g_tune.spmv_brick_rounds;
     else if (k == "spmv_brick_split") *value = g_tune.spmv_brick_split;
-    else if (k == "alloc_contig") *value = g_tune.alloc_contig;
     else if (k == "spmv_brick_pad") *value = g_tune.spmv_brick_pad;
     else if (k == "spmv_brick_waves") *value = g_tune.spmv_brick_waves;
     else if (k == "spmv_brick_bands") *value = g_tune.spmv_brick_bands;
@@ -905,6 +895,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_gsym_rows") *value = g_tune.spmv_gsym_rows;
     else if (k == "ksp_refine") *value = g_tune.ksp_refine;
     else if (k == "ksp_corr_fault") *value = g_tune.ksp_corr_fault;
+    else if (k == "ipc_sentinel") *value = g_tune.ipc_sentinel;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
     else if (k == "spmv_gsym_waves") *value = g_tune.spmv_gsym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;

@@ -238,10 +238,8 @@ struct kle_mat {
     // SBAIJ; structured 3x3 rows, one rank or z slabs): each row's blocks from
     // its diagonal block on, in the chunked layout; per-tile partial sums d_sws
     double *d_sval = nullptr;
-    void *sval_raw = nullptr;
+    void *sval_raw = nullptr;  // kle_mat_move_values: the allocation d_sval lies in (freed instead of it)
     size_t sval_cap = 0;  // bytes at sval_raw
-    int sval_contig = 0;  // d_sval came from a contiguous allocation (sval_alloc)
-    int val_contig = 0;   // d_val / d_aval likewise (big_alloc)  // kle_mat_move_values: the allocation d_sval lies in (freed instead of it)
     int64_t *d_svptr = nullptr;
     double *d_sws = nullptr;
     int *d_stile_e = nullptr;  // per tile: 2^e bounds its transposed row sums (fixed-point scale, k_sym_bound)
@@ -344,10 +342,9 @@ int sym_dot_parts(const kle_mat *A);  // partials sym_spmv writes with dpart (0:
 // values are copied (takes the plan), product, teardown
 int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &cnt, const std::vector<int> &srow,
                 int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out);
-// the symmetric storage's value array (kle_sym.hip): contiguous first
+// the symmetric storage's value array (kle_sym.hip)
 int sval_alloc(kle_mat *A, size_t bytes);
-// a streamed array (matrix values): contiguous first (alloc_contig); 1 if
-// the memory is contiguous, 0 plain, -1 out of memory
+// a streamed array (matrix values): 0, or -1 out of memory
 int big_alloc(void **p, size_t bytes);
 // (xs: the owned x, for the box bricks' one-block rows -- d_ssingle)
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
@@ -382,7 +379,8 @@ struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
-    int ksp_corr_fault = 0;  // test hook: 1 = every correction solve of refine() ends in NaN (DIVERGED_NANORINF), to test that x is kept
+    int ipc_sentinel = 0;  // IPC transport (debug): consumed mailbox slots overwritten with NaN before the ack (a stale or early slot read shows as NaN)
+    int ksp_corr_fault = 0;  // test hook: 1 = refine() runs its correction solves even when the true residual meets rtol, and each ends in NaN (DIVERGED_NANORINF) -- x must stay as it was
     int ksp_refine = 2;  // CG / pipelined CG: up to this many correction solves when the true residual misses rtol (kle_ksp.hip refine; default of new KSPs); 0 PETSc's plain stop
     int upd_nt = 2;       // single-reduction CG update: every vector but u nontemporal (u stays in the Infinity Cache for the
                           // SpMV) -- 0 off, 1 on, 2 auto: from 2M local entries (12 vectors > the 256 MB cache); per CG
@@ -406,7 +404,6 @@ struct Tuning {
     int spmv_sym_tz = 0;      // symmetric SpMV tiles (read at build): 0 auto (8 x 4 x 4 rows where it fits), 2 (8 x 8 x 2), 4
     int spmv_brick_max = 0;    // brick SpMV (read at build): at most this many bricks (0: planned, spmv_brick_rounds per CU)
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
-    int alloc_contig = 0;  // matrix value arrays (read at allocation): 1 physically contiguous first (hipDeviceMallocContiguous; experiments), 0 plain hipMalloc
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
     int spmv_brick_fill = 1;   // brick SpMV: 1 the region fill's first loads go out before the first items' value loads, 0 after

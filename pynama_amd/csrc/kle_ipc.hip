@@ -127,9 +127,16 @@ struct IpcState {
 // XCDs' caches), and a plain load may return the line this kernel's
 // previous launch left in its L2 -- last iteration's partials (a rare
 // stale sum, seen as a NaN in an 8-rank pipelined CG on one GPU).
-__global__ void k_rank_sum(int64_t n, int nr, int me, const double *__restrict__ slots, int64_t cap,
-                           double *__restrict__ out)
+// Sentinel (tuning ipc_sentinel, a debug mode the multirank tests run once):
+// every consumed slot entry is overwritten with NaN at system scope before the
+// ack goes out, so a read of a slot the peer has not refilled for this
+// sequence -- too early, or a stale line of this GPU's L2 (which the
+// write-through NaN store updates too) -- yields NaN at once instead of last
+// iteration's finite value.
+__global__ void k_rank_sum(int64_t n, int nr, int me, double *__restrict__ slots, int64_t cap,
+                           double *__restrict__ out, int sentinel)
 {
+    const double qnan = __builtin_nan("");
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double mine = out[i];
         double s = 0.0;
@@ -137,14 +144,21 @@ __global__ void k_rank_sum(int64_t n, int nr, int me, const double *__restrict__
             s += r == me ? mine
                          : __hip_atomic_load(slots + (int64_t)r * cap + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         out[i] = s;
+        if (sentinel)
+            for (int r = 0; r < nr; ++r)
+                if (r != me)
+                    __hip_atomic_store(slots + (int64_t)r * cap + i, qnan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 // A slot out of this rank's mailbox at system scope (k_rank_sum's reason)
-__global__ void k_slot_copy(int64_t n, const double *__restrict__ src, double *__restrict__ dst)
+__global__ void k_slot_copy(int64_t n, double *__restrict__ src, double *__restrict__ dst, int sentinel)
 {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    const double qnan = __builtin_nan("");
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sentinel) __hip_atomic_store(src + i, qnan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 static int wait_ge(hipStream_t st, uint64_t *flag, uint64_t v)
@@ -268,14 +282,14 @@ static int ipc_send(kle_ctx *c, IpcChannel ch, int to, const double *src, int64_
 }
 
 // the matching receive: n doubles from rank `from` out of src (my slot) into dst
-static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, const double *src, int64_t n, hipStream_t st)
+static int ipc_recv(kle_ctx *c, IpcChannel ch, int from, double *dst, double *src, int64_t n, hipStream_t st)
 {
     IpcState &P = *c->ipc;
     const uint64_t s = ++P.rseq[ch][from];
     KLE_TRY(wait_ge(st, P.data_flag(c->rank, ch, from), s));
     if (n) {
         hipLaunchKernelGGL(k_slot_copy, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (n + 255) / 256))),
-                           dim3(256), 0, st, n, src, dst);
+                           dim3(256), 0, st, n, src, dst, g_tune.ipc_sentinel);
         KLE_HIP(hipGetLastError());
     }
     return post(st, P.ack_flag(from, ch, c->rank), s);
@@ -390,7 +404,7 @@ int ipc_allreduce(kle_ctx *c, double *dbuf, int n, hipStream_t st)
     for (int q = 0; q < c->nranks; ++q)
         if (q != me) KLE_TRY(wait_ge(st, P.data_flag(me, CH_AR, q), ++P.rseq[CH_AR][q]));
     hipLaunchKernelGGL(k_rank_sum, dim3((unsigned)std::max(1, std::min(64, (n + 255) / 256))), dim3(256), 0, st,
-                       (int64_t)n, c->nranks, me, P.region(me, CH_AR), IPC_AR_CAP, dbuf);
+                       (int64_t)n, c->nranks, me, P.region(me, CH_AR), IPC_AR_CAP, dbuf, g_tune.ipc_sentinel);
     KLE_HIP(hipGetLastError());
     for (int q = 0; q < c->nranks; ++q)
         if (q != me) KLE_TRY(post(st, P.ack_flag(q, CH_AR, me), P.rseq[CH_AR][q]));

@@ -1701,7 +1701,7 @@ static int refine(kle_ksp *k, kle_vec *b, kle_vec *x)
     const int reason0 = k->reason, its_main = k->its;
     const double rnorm0 = k->rnorm;
     for (int pass = 0; pass < k->max_corr; ++pass) {
-        if (reason0 <= 0 || k->corr_reason < 0 || !(k->true_rel > k->rtol)) return 0;
+        if (reason0 <= 0 || k->corr_reason < 0 || (!(k->true_rel > k->rtol) && !g_tune.ksp_corr_fault)) return 0;
         kle_vec *rv = nullptr, *e = nullptr;
         int rc = vec_alloc(c, b->n_local, b->n_global, b->lo, 0, 0, &rv);
         if (!rc) rc = vec_alloc(c, x->n_local, x->n_global, x->lo, 0, 0, &e);

@@ -870,7 +870,7 @@ static int aij_upload(kle_mat *A)
     for (int64_t k = 0; k < A->nnz; ++k) c32[k] = (int)(A->h_col[k] - A->col_lo);
     KLE_HIP(hipMalloc(&A->d_aptr, sizeof(int64_t) * A->h_ptr.size()));
     KLE_HIP(hipMalloc(&A->d_acol, sizeof(int) * c32.size()));
-    if ((A->val_contig = big_alloc(reinterpret_cast<void **>(&A->d_aval), sizeof(double) * std::max<int64_t>(A->nnz, 1))) < 0)
+    if (big_alloc(reinterpret_cast<void **>(&A->d_aval), sizeof(double) * std::max<int64_t>(A->nnz, 1)) < 0)
         return fail(KLE_ERR_MEM, "out of device memory for the AIJ values");
     KLE_HIP(hipMemcpyAsync(A->d_aptr, A->h_ptr.data(), sizeof(int64_t) * A->h_ptr.size(), hipMemcpyHostToDevice, c->stream));
     KLE_HIP(hipMemcpyAsync(A->d_acol, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice, c->stream));
@@ -1446,15 +1446,6 @@ int kle_mat_set_spmv_structured(kle_mat *A, int on)
 {
     KLE_ARG(A, "null matrix");
     A->spmv_struct = on != 0;
-    return 0;
-}
-
-int kle_mat_get_alloc_info(const kle_mat *A, int *val_contig, int *sval_contig, uint64_t *sval_addr)
-{
-    KLE_ARG(A && val_contig && sval_contig, "null arg");
-    *val_contig = A->val_contig > 0;
-    *sval_contig = A->d_sval && A->sval_contig;
-    if (sval_addr) *sval_addr = (uint64_t)(uintptr_t)A->d_sval;
     return 0;
 }
 

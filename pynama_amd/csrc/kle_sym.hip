@@ -662,15 +662,14 @@ __global__ __launch_bounds__(256) void k_nb_sym_gather(SymGeo g, const double *_
     if (threadIdx.x == 0) dpart[blockIdx.x] = ((dred[0] + dred[1]) + dred[2]) + dred[3];
 }
 
-// The value array: big_alloc (contiguous first).  0 on success; d_sval is
-// then set (sval_raw cleared).
+// The value array: big_alloc.  0 on success; d_sval is then set (sval_raw
+// cleared).
 int sval_alloc(kle_mat *A, size_t bytes)
 {
     A->sval_raw = nullptr;
     void *p = nullptr;
     const int r = big_alloc(&p, bytes);
     A->d_sval = static_cast<double *>(p);
-    A->sval_contig = r > 0;
     return r < 0 ? KLE_ERR_MEM : 0;
 }
 
@@ -1609,14 +1608,19 @@ static int gsym_build(kle_mat *A)
 // the runs' sums in stored order, plus y first when preload (the rows'
 // direct sums).  One workgroup per 4 slices of 64 rows; with xdot, its
 // (y, x) partial in dpart[workgroup].
+// the gather's waves per 64-row slice: by the runs per slice (a 1/8 slab of
+// config 2: about 21 -> 2 waves; config 2: 1), or spmv_gather_wps
+static int gather_wps(const kle_mat *A)
+{
+    return g_tune.spmv_gather_wps ? g_tune.spmv_gather_wps : A->gather_rps >= 8 ? 2 : 1;
+}
+
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
                 int preload, hipStream_t st, const double *xs)
 {
     if (r1 <= r0) return 0;
     const int64_t s0 = r0 / 64, s1 = (r1 + 63) / 64, ntot = A->nrows + A->ghost_hi / 3;
-    // waves per slice by the runs per slice (spmv_gather_wps: 0 auto)
-    const int rps = A->gather_rps;
-    const int wps = g_tune.spmv_gather_wps ? g_tune.spmv_gather_wps : rps >= 8 ? 2 : 1;
+    const int wps = gather_wps(A);
     auto go = [&](auto kern, int wp) {
         hipLaunchKernelGGL(kern, dim3((unsigned)((s1 - s0 + 3) / 4)), dim3(256 * wp), 0, st, A->nrows, ntot,
                            A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y, A->d_sgsend, istate, xdot, dpart,
@@ -2324,11 +2328,14 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_brick)
-        return std::string("k_nb_spmv_sym_brick<") + std::to_string(g_tune.spmv_brick_waves) + ">+k_nb_gsym_gather";
-    if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather";
+        return std::string("k_nb_spmv_sym_brick<") + std::to_string(g_tune.spmv_brick_waves) +
+               (g_tune.spmv_brick_fill ? ",true>" : ",false>") + "+k_nb_gsym_gather<" + std::to_string(gather_wps(A)) +
+               ">";
+    if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather<" + std::to_string(gather_wps(A)) + ">";
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +
-               std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather";
+               std::to_string(A->sym_reg[3]) + "," + std::to_string(A->sym_reg[4]) + ">+k_nb_gsym_gather<" +
+               std::to_string(gather_wps(A)) + ">";
     return std::string("k_nb_spmv_sym_xl<") + std::to_string(sym_waves(A)) + "," +
            (g_tune.spmv_sym_det ? "true" : "false") + "," + std::to_string(A->sym_TY) + "," +
            std::to_string(A->sym_TZ) + ">+k_nb_sym_gather<8," + std::to_string(A->sym_TY) + "," +

@@ -464,14 +464,6 @@ class Mat:
         fresh=False move: same pages, other offset (kle_mat_move_values)."""
         call("kle_mat_move_values", self._h, int(shift), int(bool(fresh)))
 
-    def getAllocInfo(self):
-        """{"values_contiguous", "symmetric_values_contiguous"}: whether the
-        value arrays got physically contiguous memory (kle_mat_get_alloc_info)."""
-        a, b, p = C.c_int(), C.c_int(), C.c_uint64()
-        call("kle_mat_get_alloc_info", self._h, C.byref(a), C.byref(b), C.byref(p))
-        return {"values_contiguous": bool(a.value), "symmetric_values_contiguous": bool(b.value),
-                "symmetric_values_address": p.value}
-
     def setHaloOverlap(self, on=True):
         call("kle_mat_set_halo_overlap", self._h, int(bool(on)))
 

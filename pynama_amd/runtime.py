@@ -293,8 +293,6 @@ def get_ctx():
             set_tuning("ksp_refine", int(os.environ["KLE_KSP_REFINE"]))
         if os.environ.get("KLE_SPMV_GSYM_BRICK"):
             set_tuning("spmv_gsym_brick", int(os.environ["KLE_SPMV_GSYM_BRICK"]))
-        if os.environ.get("KLE_ALLOC_CONTIG"):
-            set_tuning("alloc_contig", int(os.environ["KLE_ALLOC_CONTIG"]))
         if os.environ.get("KLE_TUNING"):  # any knobs, as JSON: KLE_TUNING='{"spmv_brick_tail": 10}'
             import json
             for k, v in json.loads(os.environ["KLE_TUNING"]).items():

@@ -225,6 +225,50 @@ def test_correction_keeps_main_reason_near_maxit(pa, typ):
     assert k.getCorrectionIterations() == 0 and k.getCorrectionReason() == 0
 
 
+@pytest.mark.parametrize("typ", ["cg", "pipecg"])
+def test_failed_correction_keeps_x(pa, typ):
+    """A correction solve that ends in NaN (the ksp_corr_fault test hook:
+    refine runs it, then its result is NaN and its reason DIVERGED_NANORINF)
+    leaves x as the main solve made it -- bitwise, finite -- and the main
+    solve's reason, count and residual norm stand; the failed correction is
+    reported apart."""
+    from pynama_amd.runtime import set_tuning
+    g = _golden("tg3d_p4")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build()
+    b = mat.K.createVecLeft()
+    b.setArray(g["b"])
+
+    def solve(corr):
+        ksp = pa.petsc.KSP().create()
+        ksp.setType(typ)
+        pc = pa.petsc.PC()
+        pc.setType("jacobi")
+        ksp.setPC(pc)
+        ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+        ksp.setCorrections(corr)
+        ksp.setOperators(mat.K)
+        x = mat.K.createVecRight()
+        ksp.solve(b, x)
+        return ksp, x.getArray().copy()
+
+    plain, x0 = solve(0)
+    set_tuning("ksp_corr_fault", 1)
+    try:
+        k, x1 = solve(2)
+    finally:
+        set_tuning("ksp_corr_fault", 0)
+    assert np.isfinite(x1).all()
+    np.testing.assert_array_equal(x1, x0)
+    assert k.getConvergedReason() == plain.getConvergedReason() > 0
+    assert k.getIterationNumber() == plain.getIterationNumber()
+    assert k.getResidualNorm() == plain.getResidualNorm()
+    assert k.getCorrectionReason() == -9  # (KSP_DIVERGED_NANORINF)
+    assert k.getTrueRelativeResidual() == plain.getTrueRelativeResidual()
+
+
 def test_gmres_and_aij(pa):
     g = _golden("tg2d_small")
     dom = _domain(pa, g)

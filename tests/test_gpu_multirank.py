@@ -194,6 +194,30 @@ def test_partitioned_solve_ipc_transport(size, nelem, ngl, ksp_type, overlap, sy
         assert abs(a["dot"] - b["dot"]) <= 1e-13 * abs(b["dot"])
 
 
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type,sym", [(2, [3, 2, 4], 4, "pipecg", True),
+                                                    (3, [2, 3, 3], 3, "cg", True),
+                                                    (8, [2, 2, 8], 4, "pipecg", True),
+                                                    (8, [2, 2, 8], 4, "cg", False)])
+def test_ipc_transport_with_slot_sentinel(size, nelem, ngl, ksp_type, sym):
+    """KLE_TRANSPORT=ipc with the NaN slot sentinel (tuning ipc_sentinel:
+    every consumed mailbox slot entry is overwritten with NaN before the ack,
+    kle_ipc.hip): a halo, reverse-halo or allreduce read of a slot the peer has
+    not refilled for this sequence -- early, or a stale line of this GPU's L2
+    -- would turn the product or the solve NaN at once (the round-5
+    8-rank NaN).  Same checks as the other IPC runs: the serial oracle, K's
+    rows, y = K x bitwise equal to the host transport's."""
+    os.environ["KLE_TUNING"] = '{"ipc_sentinel": 1}'  # inherited by the spawned ranks
+    try:
+        res = _check_box(size, nelem, ngl, True, ksp_type, sym=sym, transport="ipc")
+    finally:
+        del os.environ["KLE_TUNING"]
+    ref = _check_box(size, nelem, ngl, True, ksp_type, sym=sym)
+    for a, b in zip(res, ref):
+        assert a["transport"] == "ipc"
+        assert np.isfinite(a["u"]).all() and np.isfinite(a["y"]).all()
+        np.testing.assert_array_equal(a["y"], b["y"])
+
+
 def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False, transport="host", its_extra=0):
     import torch.multiprocessing as mp
     from oracle import oracle as O
@@ -355,6 +379,23 @@ def test_partitioned_umesh_ipc_transport(size, nel, ksp_type, sym, tmp_path):
         assert a["sym"] == sym and b["sym"] == sym
         if sym:
             assert a["kernel"].startswith("k_nb_spmv_gsym_brick<"), a["kernel"]
+        np.testing.assert_array_equal(a["y"], b["y"])
+
+
+@pytest.mark.parametrize("size,nel,ksp_type", [(8, [4, 4, 6], "pipecg"), (4, [4, 4, 4], "cg")])
+def test_partitioned_umesh_ipc_with_slot_sentinel(size, nel, ksp_type, tmp_path):
+    """The round-5 NaN case (8 ranks, graph partition, pipelined CG,
+    symmetric storage; gpurun_out/r05au_1_suite.log) over the IPC transport
+    with the NaN slot sentinel on (test_ipc_transport_with_slot_sentinel):
+    an early or stale slot read shows as NaN on every run, not rarely."""
+    os.environ["KLE_TUNING"] = '{"ipc_sentinel": 1}'  # inherited by the spawned ranks
+    try:
+        res = _check_umesh(size, "inertial", nel, ksp_type, 0, tmp_path, sym=True, transport="ipc")
+    finally:
+        del os.environ["KLE_TUNING"]
+    ref = _check_umesh(size, "inertial", nel, ksp_type, 0, tmp_path, sym=True)
+    for a, b in zip(res, ref):
+        assert a["transport"] == "ipc" and a["sym"]
         np.testing.assert_array_equal(a["y"], b["y"])
 
 

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16, "spmv_x_lds": 1, "spmv_dict": 1, "upd_preload": 1, "upd_nt": 2, "spmv_sym": 1, "spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_early": 0, "spmv_sym_align": 0, "spmv_sym_stpol": 0, "spmv_gsym_stpol": 2, "spmv_sym_tile64": 0, "spmv_sym_tile64_max": 640, "spmv_sym_ovl_b": 50, "spmv_sym_xcd": 0, "spmv_sym_brick": 1, "spmv_brick_fill": 1, "spmv_gather_wps": 0, "spmv_brick_max": 0, "spmv_brick_rounds": 1, "spmv_brick_split": 0, "spmv_brick_waves": 16, "spmv_brick_pad": 0, "alloc_contig": 0, "spmv_gsym_brick": 1, "upd_unroll": 1, "spmv_brick_bands": 0, "spmv_brick_fcost": 0, "spmv_brick_pair": 1, "spmv_brick_singles": 1, "spmv_brick_tail": 0, "spmv_brick_tile": 20}  # kle_set_tuning defaults
+DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16, "spmv_x_lds": 1, "spmv_dict": 1, "upd_preload": 1, "upd_nt": 2, "spmv_sym": 1, "spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_early": 0, "spmv_sym_align": 0, "spmv_sym_stpol": 0, "spmv_gsym_stpol": 2, "spmv_sym_tile64": 0, "spmv_sym_tile64_max": 640, "spmv_sym_ovl_b": 50, "spmv_sym_xcd": 0, "spmv_sym_brick": 1, "spmv_brick_fill": 1, "spmv_gather_wps": 0, "spmv_brick_max": 0, "spmv_brick_rounds": 1, "spmv_brick_split": 0, "spmv_brick_waves": 16, "spmv_brick_pad": 0, "spmv_gsym_brick": 1, "upd_unroll": 1, "spmv_brick_bands": 0, "spmv_brick_fcost": 0, "spmv_brick_pair": 1, "spmv_brick_singles": 1, "spmv_brick_tail": 0, "spmv_brick_tile": 20}  # kle_set_tuning defaults
 
 
 def main():
