@@ -104,19 +104,15 @@ const char *kle_last_error(void);
  * build: at most this many bricks per CU, default 1), "spmv_brick_split" (read
  * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
  * "spmv_brick_pair" (read at build: rows in units of two whose last
- * partial 64-block passes share one item; 1 default), "spmv_brick_fcost"
- * (read at build: with pairs, plan bricks by blocks instead of passes; 0
- * default), "spmv_brick_singles" (read at build: rows of one stored block -- the
- * Dirichlet rows and the free rows at the far corner of their box -- formed by
- * the gather instead of as items of the bricks; 1 default),
- * "spmv_brick_tail" / "spmv_brick_tile" (read at build: per mille of the
- * mean brick cut off every heavier brick into tail tiles of about `tile` per
- * mille, launched after the bricks; 0 / 20 default), "spmv_brick_bands"
- * (read at build: 1 the planner also tries ragged y bands
- * in z slabs, balanced bricks; 0 default, boxes only), "spmv_brick_pad"
- * (read at build: doubles of gap before each brick's values; 0 default),
- * "spmv_brick_waves" (8, 12 or 16 default), "spmv_gsym_brick" (read at
- * build: graph K on graph bricks, whole rounds per CU; 1 default),
+ * partial 64-block passes share one item; 1 default), "spmv_brick_singles"
+ * (read at build: rows of one stored block -- the Dirichlet rows and the
+ * free rows at the far corner of their box -- formed by the gather instead
+ * of as items of the bricks; 1 default), "spmv_gather_wps" (the run-mask
+ * gather's waves per 64-row slice: 1, 2, 4; 0 default, by the runs per
+ * slice), "spmv_gsym_brick" (read at build: graph K on graph bricks, whole
+ * rounds per CU; 1 default), "ipc_sentinel" (IPC transport debug mode:
+ * consumed mailbox slots overwritten with NaN before the ack; 0 default),
+ * "ksp_corr_fault" (test hook: correction solves that end in NaN; 0),
  * "upd_unroll" (CG update kernel: 1 default or 2),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit

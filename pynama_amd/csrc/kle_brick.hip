@@ -577,13 +577,8 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
                 int P, std::vector<int64_t> &svptr_out, std::string &why, void **plan_out)
 {
     auto *bp = new BrickPlan;
-    bp->pad = g_tune.spmv_brick_pad;
-    bp->bands = g_tune.spmv_brick_bands;
-    bp->tail = g_tune.spmv_brick_tail;
-    bp->tile = g_tune.spmv_brick_tile;
     bp->singles = g_tune.spmv_brick_singles;
     bp->pair = g_tune.spmv_brick_pair;
-    bp->fcost = g_tune.spmv_brick_fcost;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     if (A->ghost_lo + 3 * A->nrows + A->ghost_hi >= (int64_t)1 << 29) {  // (the fill's 32-bit byte offsets)
         delete bp;
@@ -606,13 +601,8 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
             why.find("fits the LDS") == std::string::npos)
             break;
         *bp = BrickPlan{};
-        bp->pad = g_tune.spmv_brick_pad;
-        bp->bands = g_tune.spmv_brick_bands;
-        bp->tail = g_tune.spmv_brick_tail;
-        bp->tile = g_tune.spmv_brick_tile;
         bp->singles = g_tune.spmv_brick_singles;
         bp->pair = g_tune.spmv_brick_pair;
-        bp->fcost = g_tune.spmv_brick_fcost;
     }
     if (!why.empty()) {
         delete bp;
@@ -815,12 +805,8 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
     const BrickDesc *bd = reinterpret_cast<const BrickDesc *>(A->d_bdesc);
     auto go = [&](auto kern, int slot, int wv) {
-        static int lds_set[4] = {0, 0, 0, 0};  // dynamic LDS above 64 KB must be declared per kernel
-        if (A->brick_lds > lds_set[slot]) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      A->brick_lds);
-            lds_set[slot] = A->brick_lds;
-        }
+        (void)slot;
+        dyn_lds(c, reinterpret_cast<const void *>(kern), (size_t)A->brick_lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * wv), (size_t)A->brick_lds, c->stream,
                            (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, bd,
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
@@ -836,13 +822,11 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     if (dist)
         KLE_TRY(halo_exchange(c, x->base, x->ghost_lo, x->n_local, x->ghost_hi, x->lo_rank, x->hi_rank, x->send_lo,
                               x->send_hi, c->stream, nullptr));
-    // (spmv_brick_waves: fewer waves per CU keep fewer loads in flight)
     if (A->nbricks == 0) {
         // (no brick: every row of one block, formed by the gather)
-    } else if (g_tune.spmv_brick_fill == 0) go(k_nb_spmv_sym_brick<BRICK_WV, false>, 1, BRICK_WV);
-    else if (g_tune.spmv_brick_waves == 8) go(k_nb_spmv_sym_brick<8>, 2, 8);
-    else if (g_tune.spmv_brick_waves == 12) go(k_nb_spmv_sym_brick<12>, 3, 12);
-    else go(k_nb_spmv_sym_brick<BRICK_WV>, 0, BRICK_WV);
+    } else {
+        go(k_nb_spmv_sym_brick<BRICK_WV>, 0, BRICK_WV);
+    }
     KLE_HIP(hipGetLastError());
     // the gather (kle_sym.hip gsym_gather): per row its direct sum in y, then
     // the runs of the regions holding it, in ascending brick order

@@ -55,14 +55,8 @@ struct BrickPlan {
     int64_t ws_doubles = 0, ws_entries = 0;
     size_t lds = 0;
     double model_us = 0.0;  // the planner's time model of the product (us)
-    int pad = 0;            // (in) doubles of gap before each brick's values (spmv_brick_pad)
-    int bands = 0;          // (in) try the ragged-band generator (spmv_brick_bands)
-    int tail = 0;           // (in) per mille of the mean brick cut off the heavy bricks into tail tiles (spmv_brick_tail)
-    int tile = 20;          // (in) a tail tile's weight, per mille of the mean brick (spmv_brick_tile)
-    int ntail = 0;          // (out) tail tiles (the last ntail bricks)
     int singles = 0;        // (in) rows of one stored block out of the bricks, to the gather (spmv_brick_singles)
     int pair = 0;           // (in) units of two rows sharing their tails' item (spmv_brick_pair)
-    int fcost = 0;          // (in) with pair: rows cost their blocks' share of full items (spmv_brick_fcost)
     std::vector<int64_t> srows;  // (out) those rows, ascending; their values (9 doubles each) after the bricks'
 };
 

@@ -62,11 +62,10 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     // per row: stored blocks (upper tail) and its byte weight
     std::vector<int> mu(n);
     // (a row of one stored block costs a brick nothing when the gather forms
-    // it; with paired tails (bp.pair, bp.fcost) a row costs about its blocks'
-    // share of full items)
+    // it)
     auto rcost = [&](int64_t i) {
         if (bp.singles && mu[i] == 1) return 0.0;
-        return bp.pair && bp.fcost ? 4608.0 * (mu[i] / 64.0 + 0.02) : row_cost(mu[i]);
+        return row_cost(mu[i]);
     };
     std::vector<double> wx(Lx, 0.0), wy(Ly, 0.0), wz(Lz, 0.0);
     std::vector<int> xlo(Lx, INT_MAX), xhi(Lx, INT_MIN), ylo(Ly, INT_MAX), yhi(Ly, INT_MIN), zhi(Lz, INT_MIN);
@@ -457,288 +456,11 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
             if (fits) consider(bx, w, ent);
         }
     }
-    // Ragged bands inside z slabs of one or two element layers (slab brick
-    // counts by weight, largest remainders): the slab's (y, z) lines in
-    // y-major order are cut into bands of c bricks each at line granularity
-    // (cumulative weight), and a band's rows in x-major order into its c
-    // bricks at row granularity -- every brick of a slab within a row of the
-    // slab's mean weight.  (bp.bands 0: not tried.)  A brick's region grows by at most one node along x
-    // and y over an exact box (its first and last x planes and y lines may be
-    // partial).  The box plans' heaviest brick sets the kernel's time: at
-    // config 2 1.057 x the mean, and the measured loop time of each brick
-    // follows its planned weight with correlation 0.98
-    // (profiles/r05/phase_bricks_weights.txt).
-    if (fs == 0 && bp.bands) {
-        for (int t = 1; t <= 2; ++t) {
-            const int ns = std::max(1, ez / t);
-            std::vector<int> cz;
-            if (!split_axis(uz, ns, P, cz) || ns > nmax) continue;
-            const double W = box_sum(0, Lx, 0, Ly, 0, Lz);
-            std::vector<int> nsl(ns);
-            std::vector<std::pair<double, int>> rem;
-            int tot = 0;
-            for (int sl = 0; sl < ns; ++sl) {
-                const double q = box_sum(0, Lx, 0, Ly, cz[sl], cz[sl + 1]) / W * nmax;
-                nsl[sl] = std::max(1, (int)q);
-                tot += nsl[sl];
-                rem.push_back({q - (int)q, sl});
-            }
-            std::sort(rem.rbegin(), rem.rend());
-            for (size_t k = 0; k < rem.size() && tot < nmax; ++k, ++tot) ++nsl[rem[k].second];
-            if (tot > nmax) continue;
-            // per slab: bands of whole y lines, band (ya, yb) with c bricks cut
-            // from its rows in x-major order at row granularity; the bands and
-            // their brick counts by dynamic programming over y (the heaviest
-            // band brick W(ya, yb) / c smallest), among those whose bricks'
-            // regions fit the LDS (x cuts estimated at plane granularity, then
-            // checked exactly)
-            std::vector<std::vector<int64_t>> bx;
-            std::vector<double> w;
-            int64_t ent = 0;
-            bool all = true;
-            constexpr int CMAX = 12;
-            struct SlabDP {
-                int kmax = 0;
-                std::vector<double> dp;
-                std::vector<int> from, fc;
-            };
-            std::vector<SlabDP> sdp(ns);
-            for (int sl = 0; sl < ns && all; ++sl) {
-                const int z0 = cz[sl], z1 = cz[sl + 1], k = nsl[sl] + 4;
-                int oz, RZ;
-                region(zlo_none, zhi, z0, z1, oz, RZ);
-                // fits[ya][yb][c]
-                auto fidx = [&](int ya, int yb, int c) { return ((size_t)ya * (Ly + 1) + yb) * (CMAX + 1) + c; };
-                std::vector<char> fit((size_t)(Ly + 1) * (Ly + 1) * (CMAX + 1), 0);
-                std::vector<double> px(Lx + 1);
-                for (int ya = 0; ya < Ly; ++ya)
-                    for (int yb = ya + 1; yb <= Ly; ++yb) {
-                        int oy, RY;
-                        region(ylo, yhi, ya, yb, oy, RY);
-                        for (int x = 0; x < Lx; ++x) px[x + 1] = px[x] + box_sum(x, x + 1, ya, yb, z0, z1);
-                        for (int c = 1; c <= CMAX; ++c) {
-                            bool ok = true;
-                            for (int q = 0; q < c && ok; ++q) {
-                                const double ta = px[Lx] * q / c, tb = px[Lx] * (q + 1) / c;
-                                int xa = (int)(std::upper_bound(px.begin(), px.end(), ta) - px.begin()) - 1;
-                                int xb = (int)(std::lower_bound(px.begin(), px.end(), tb) - px.begin());
-                                xa = std::max(0, std::min(xa, Lx - 1));
-                                xb = std::max(xa + 1, std::min(xb, Lx));
-                                int ox, RX;
-                                region(xlo, xhi, xa, xb, ox, RX);
-                                const int RN = RX * RY * RZ;
-                                ok = RN <= 65535 && brick_lds(RN) <= BRICK_LDS_CAP;
-                            }
-                            fit[fidx(ya, yb, c)] = ok;
-                        }
-                    }
-                // dp[y][kk]: the lightest heaviest brick covering lines [0, y) with kk bricks
-                SlabDP &S = sdp[sl];
-                S.kmax = k;
-                S.dp.assign((size_t)(Ly + 1) * (k + 1), 1e300);
-                S.from.assign((size_t)(Ly + 1) * (k + 1), -1);
-                S.fc.assign((size_t)(Ly + 1) * (k + 1), 0);
-                S.dp[0] = 0.0;
-                for (int yb = 1; yb <= Ly; ++yb)
-                    for (int ya = 0; ya < yb; ++ya) {
-                        const double Wb = box_sum(0, Lx, ya, yb, z0, z1);
-                        const int64_t brows = (int64_t)Lx * (yb - ya) * (z1 - z0);
-                        for (int c = 1; c <= CMAX; ++c) {
-                            if (!fit[fidx(ya, yb, c)] || brows < c) continue;  // (at least a row per brick)
-                            for (int kk = c; kk <= k; ++kk) {
-                                const double prev = S.dp[(size_t)ya * (k + 1) + kk - c];
-                                if (prev >= 1e300) continue;
-                                const double v = std::max(prev, Wb / c);
-                                double &cur = S.dp[(size_t)yb * (k + 1) + kk];
-                                if (v < cur) {
-                                    cur = v;
-                                    S.from[(size_t)yb * (k + 1) + kk] = ya;
-                                    S.fc[(size_t)yb * (k + 1) + kk] = c;
-                                }
-                            }
-                        }
-                    }
-            }
-            // brick counts per slab: the smallest threshold T on the heaviest
-            // brick such that every slab's fewest bricks with dp <= T sum to at
-            // most nmax (dp need not fall monotonically with the count)
-            std::vector<int> kc(ns, 0);
-            if (all) {
-                std::vector<double> cand;
-                for (int sl = 0; sl < ns; ++sl)
-                    for (int kk = 1; kk <= sdp[sl].kmax; ++kk) {
-                        const double v = sdp[sl].dp[(size_t)Ly * (sdp[sl].kmax + 1) + kk];
-                        if (v < 1e300) cand.push_back(v);
-                    }
-                std::sort(cand.begin(), cand.end());
-                cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-                auto counts = [&](double T, std::vector<int> &out) {
-                    int tot = 0;
-                    for (int sl = 0; sl < ns; ++sl) {
-                        const SlabDP &S = sdp[sl];
-                        int kk = 1;
-                        while (kk <= S.kmax && S.dp[(size_t)Ly * (S.kmax + 1) + kk] > T) ++kk;
-                        if (kk > S.kmax) return INT_MAX;
-                        out[sl] = kk;
-                        tot += kk;
-                    }
-                    return tot;
-                };
-                size_t lo = 0, hi = cand.size();
-                std::vector<int> tmp(ns);
-                while (lo < hi) {
-                    const size_t mid = (lo + hi) / 2;
-                    if (counts(cand[mid], tmp) <= nmax) hi = mid;
-                    else lo = mid + 1;
-                }
-                if (lo == cand.size() || counts(cand[lo], kc) > nmax) {
-                    all = false;
-                    if (getenv("KLE_BRICK_DEBUG")) fprintf(stderr, "bands t=%d: no slab counts within %d bricks\n", t, nmax);
-                }
-            }
-            for (int sl = 0; sl < ns && all; ++sl) {
-                const int z0 = cz[sl], z1 = cz[sl + 1], k = kc[sl];
-                const SlabDP &S = sdp[sl];
-                const int K1 = S.kmax + 1;
-                std::vector<std::pair<std::pair<int, int>, int>> bands;
-                for (int yb = Ly, kk = k; yb > 0;) {
-                    const int ya = S.from[(size_t)yb * K1 + kk], c = S.fc[(size_t)yb * K1 + kk];
-                    bands.push_back({{ya, yb}, c});
-                    kk -= c;
-                    yb = ya;
-                }
-                std::reverse(bands.begin(), bands.end());
-                if (getenv("KLE_BRICK_DEBUG")) {
-                    fprintf(stderr, "bands t=%d slab %d: %d bricks, heaviest %.4g, bands", t, sl, k,
-                            S.dp[(size_t)Ly * K1 + k]);
-                    for (const auto &bd2 : bands) fprintf(stderr, " [%d,%d)x%d", bd2.first.first, bd2.first.second, bd2.second);
-                    fprintf(stderr, "\n");
-                }
-                for (const auto &bd2 : bands) {
-                    const int ya = bd2.first.first, yb = bd2.first.second, c = bd2.second;
-                    std::vector<int64_t> rows;
-                    rows.reserve((size_t)Lx * (yb - ya) * (z1 - z0));
-                    for (int x = 0; x < Lx; ++x)
-                        for (int y = ya; y < yb; ++y)
-                            for (int z = z0; z < z1; ++z) rows.push_back(x + (int64_t)Lx * y + Lxy * z);
-                    std::vector<double> rp(rows.size() + 1, 0.0);
-                    for (size_t r = 0; r < rows.size(); ++r) rp[r + 1] = rp[r] + rcost(rows[r]);
-                    if (rows.size() < (size_t)c) {
-                        all = false;
-                        break;
-                    }
-                    size_t r0 = 0;
-                    for (int q = 0; q < c && all; ++q) {
-                        size_t r1 = rows.size();
-                        if (q < c - 1) {
-                            const double tg = rp.back() * (q + 1) / c;
-                            r1 = std::lower_bound(rp.begin(), rp.end(), tg) - rp.begin();
-                            r1 = std::max(r1, r0 + 1);
-                            r1 = std::min(r1, rows.size() - (size_t)(c - 1 - q));
-                        }
-                        std::vector<int64_t> br(rows.begin() + r0, rows.begin() + r1);
-                        // (cut in x-major order for compact bricks, streamed in
-                        // lattice order -- x fastest -- as the boxes are)
-                        std::sort(br.begin(), br.end());
-                        int ox, RX, oy, RY, oz2, RZ2;
-                        row_region(br, ox, RX, oy, RY, oz2, RZ2);
-                        const int RN = RX * RY * RZ2;
-                        if (RN > 65535 || brick_lds(RN) > BRICK_LDS_CAP) {
-                            all = false;
-                            if (getenv("KLE_BRICK_DEBUG"))
-                                fprintf(stderr, "bands t=%d: slab %d band %d..%d: region %d x %d x %d too big\n", t, sl,
-                                        ya, yb, RX, RY, RZ2);
-                        }
-                        ent += RN;
-                        w.push_back(rp[r1] - rp[r0] + 72.0 * RN);
-                        bx.push_back(std::move(br));
-                        r0 = r1;
-                    }
-                }
-            }
-            if (getenv("KLE_BRICK_DEBUG") && all) {
-                double mx = 0, sm = 0;
-                for (double v : w) mx = std::max(mx, v), sm += v;
-                fprintf(stderr, "bands t=%d bricks %zu max/mean %.4f model %.1f\n", t, bx.size(), mx / (sm / w.size()),
-                        model(w) * 1e-6);
-            }
-            if (all && (int)bx.size() <= nmax) consider_rows(std::move(bx), w, ent);
-        }
-    }
         if (nfix > 0) break;
     }
     bp.model_us = best_t * 1e-6;  // (bytes / (TB/s) = us)
     (void)total;
     if (best.empty()) return "no brick decomposition fits the LDS";
-    // Tail tiles (bp.tail > 0): every brick heavier than (1 - tail) x the
-    // mean gives the rows past that weight (the end of its streaming order:
-    // x lines of its top plane) to small bricks of about `tile` x the mean,
-    // launched after the bricks.  One brick fills a CU's LDS, so the hardware
-    // dispatches each tile to the first CU of its XCD whose brick has ended:
-    // the CUs of the light bricks take the heavy bricks' tails, and the
-    // kernel ends with the mean brick plus a tile instead of with the
-    // heaviest brick.  A tile is a brick like any other (its region, sums and
-    // gather runs), only small.
-    bp.ntail = 0;
-    if (bp.tail > 0 && best.size() > 1) {
-        const int NB0 = (int)best.size();
-        std::vector<double> wq(NB0, 0.0);
-        double wsum = 0.0;
-        for (int q = 0; q < NB0; ++q) {
-            for (int64_t i : best[q]) wq[q] += rcost(i);
-            wsum += wq[q];
-        }
-        const double mean = wsum / NB0, T = mean * (1.0 - 1e-3 * bp.tail), ts = std::max(1e-3 * bp.tile * mean, 1.0);
-        std::vector<std::vector<int64_t>> tiles;
-        for (int q = 0; q < NB0; ++q) {
-            if (wq[q] <= T) continue;
-            std::vector<int64_t> &R = best[q];
-            double w = wq[q];
-            size_t keep = R.size();
-            while (keep > 1 && w - rcost(R[keep - 1]) >= T) w -= rcost(R[--keep]);
-            if (keep == R.size()) continue;
-            // the cut rows, in streaming order, into nt tiles of about ts
-            // (cuts at the cumulative weights k (cut weight) / nt)
-            const double left = wq[q] - w;
-            const int nt = std::max(1, std::min((int)(R.size() - keep), (int)std::ceil(left / ts - 1e-9)));
-            double cw = 0.0;
-            size_t r = keep;
-            for (int k = 1; k <= nt; ++k) {
-                std::vector<int64_t> t;
-                const double tg = left * k / nt;
-                while (r < R.size() && (k == nt || t.empty() || cw + 0.5 * rcost(R[r]) <= tg)) {
-                    cw += rcost(R[r]);
-                    t.push_back(R[r++]);
-                }
-                if (t.empty()) continue;
-                std::sort(t.begin(), t.end());
-                tiles.push_back(std::move(t));
-            }
-            R.resize(keep);
-        }
-        // (heaviest tiles first: the last to start are the lightest)
-        std::vector<double> tw(tiles.size(), 0.0);
-        for (size_t k = 0; k < tiles.size(); ++k)
-            for (int64_t i : tiles[k]) tw[k] += rcost(i);
-        std::vector<int> ord(tiles.size());
-        for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tw[a] > tw[b]; });
-        bool fits = true;
-        for (int k : ord) {
-            int ox, RX, oy, RY, oz2, RZ2;
-            row_region(tiles[k], ox, RX, oy, RY, oz2, RZ2);
-            if (RX * RY * RZ2 > 65535 || brick_lds(RX * RY * RZ2) > BRICK_LDS_CAP) fits = false;
-        }
-        if (fits) {
-            bp.ntail = (int)tiles.size();
-            for (int k : ord) best.push_back(std::move(tiles[k]));
-        } else {
-            return "tail tiles do not fit the LDS";
-        }
-        if (getenv("KLE_BRICK_DEBUG"))
-            fprintf(stderr, "tail: %d bricks, T %.4f of the mean, %d tiles of ~%.4f\n", NB0, T / mean, bp.ntail,
-                    ts / mean);
-    }
     // Rows of one stored block (the diagonal: Dirichlet rows and the free rows
     // at the far corner of their box) leave the bricks (bp.singles): a 64-lane
     // item would carry one block, and the gather forms B_ii x_i for them
@@ -820,7 +542,6 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
         const int RN = D.RX * D.RY * D.RZ;
         D.rstart = (int)rows;
         D.eb = 0;
-        voff += bp.pad;
         D.vbase = voff;
         D.wsoff = wsd;
         wsd += ((int64_t)3 * RN + 15) & ~int64_t(15);
@@ -914,12 +635,8 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
                 blocks += cnt[i] - ((x - bx) + nx * ((y - by) + ny * (z - bz)));
             }
     BrickPlan bp;
-    bp.bands = g_tune.spmv_brick_bands;
-    bp.tail = g_tune.spmv_brick_tail;
-    bp.tile = g_tune.spmv_brick_tile;
     bp.singles = g_tune.spmv_brick_singles;
     bp.pair = g_tune.spmv_brick_pair;
-    bp.fcost = g_tune.spmv_brick_fcost;
     const std::string why = brick_plan(Lx, Ly, Lz, 0, ncu, 0, rounds, split, cnt, srow, p, bp);
     if (!why.empty()) return fail(KLE_ERR_SUP, "%s", why.c_str());
     const int NB = (int)bp.bricks.size();

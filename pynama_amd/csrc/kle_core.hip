@@ -13,6 +13,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "kle_internal.hpp"
 
@@ -32,6 +34,22 @@ int big_alloc(void **p, size_t bytes)
         return -1;
     }
     return 0;
+}
+
+// Dynamic LDS above 64 KB must be declared per kernel (hipFuncSetAttribute);
+// the attribute is per device, so the record of what was declared is keyed
+// by (device, kernel), under a lock (a function-static cache
+// skipped the call for a second context on another device)
+void dyn_lds(const kle_ctx *c, const void *kern, size_t bytes)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, size_t> done;
+    std::lock_guard<std::mutex> lk(mu);
+    size_t &s = done[{c->device, kern}];
+    if (bytes > s) {
+        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        s = bytes;
+    }
 }
 
 Tuning g_tune;
@@ -741,37 +759,16 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_gsym_brick") {
         KLE_ARG(value == 0 || value == 1, "spmv_gsym_brick: 0 or 1");
         g_tune.spmv_gsym_brick = value;
-    } else if (k == "spmv_brick_fcost") {
-        KLE_ARG(value == 0 || value == 1, "spmv_brick_fcost: 0 or 1");
-        g_tune.spmv_brick_fcost = value;
-    } else if (k == "spmv_brick_pair") {
+        } else if (k == "spmv_brick_pair") {
         KLE_ARG(value == 0 || value == 1, "spmv_brick_pair: 0 or 1");
         g_tune.spmv_brick_pair = value;
     } else if (k == "spmv_brick_singles") {
         KLE_ARG(value == 0 || value == 1, "spmv_brick_singles: 0 or 1");
         g_tune.spmv_brick_singles = value;
-    } else if (k == "spmv_brick_tail") {
-        KLE_ARG(value >= 0 && value <= 500, "spmv_brick_tail: 0..500 per mille");
-        g_tune.spmv_brick_tail = value;
-    } else if (k == "spmv_brick_tile") {
-        KLE_ARG(value >= 1 && value <= 1000, "spmv_brick_tile: 1..1000 per mille");
-        g_tune.spmv_brick_tile = value;
-    } else if (k == "spmv_brick_bands") {
-        KLE_ARG(value == 0 || value == 1, "spmv_brick_bands: 0 or 1");
-        g_tune.spmv_brick_bands = value;
-    } else if (k == "spmv_brick_fill") {
-        KLE_ARG(value == 0 || value == 1, "spmv_brick_fill: 0 or 1");
-        g_tune.spmv_brick_fill = value;
-    } else if (k == "spmv_gather_wps") {
+                    } else if (k == "spmv_gather_wps") {
         KLE_ARG(value == 0 || value == 1 || value == 2 || value == 4, "spmv_gather_wps: 0 (auto), 1, 2 or 4");
         g_tune.spmv_gather_wps = value;
-    } else if (k == "spmv_brick_waves") {
-        KLE_ARG(value == 8 || value == 12 || value == 16, "spmv_brick_waves: 8, 12 or 16");
-        g_tune.spmv_brick_waves = value;
-    } else if (k == "spmv_brick_pad") {
-        KLE_ARG(value >= 0 && value % 16 == 0 && value <= (1 << 20), "spmv_brick_pad: multiple of 16 doubles");
-        g_tune.spmv_brick_pad = value;
-        } else if (k == "spmv_brick_split") {
+                } else if (k == "spmv_brick_split") {
         KLE_ARG(value >= 0, "spmv_brick_split: nbx + 100 nby + 10000 nbz (0: planned)");
         g_tune.spmv_brick_split = value;
     } else if (k == "spmv_brick_rounds") {
@@ -869,16 +866,9 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_max") *value = g_tune.spmv_brick_max;
     else if (k == "spmv_brick_rounds") *value = g_tune.spmv_brick_rounds;
     else if (k == "spmv_brick_split") *value = g_tune.spmv_brick_split;
-    else if (k == "spmv_brick_pad") *value = g_tune.spmv_brick_pad;
-    else if (k == "spmv_brick_waves") *value = g_tune.spmv_brick_waves;
-    else if (k == "spmv_brick_bands") *value = g_tune.spmv_brick_bands;
-    else if (k == "spmv_brick_tail") *value = g_tune.spmv_brick_tail;
     else if (k == "spmv_brick_singles") *value = g_tune.spmv_brick_singles;
     else if (k == "spmv_brick_pair") *value = g_tune.spmv_brick_pair;
     else if (k == "spmv_gather_wps") *value = g_tune.spmv_gather_wps;
-    else if (k == "spmv_brick_fill") *value = g_tune.spmv_brick_fill;
-    else if (k == "spmv_brick_fcost") *value = g_tune.spmv_brick_fcost;
-    else if (k == "spmv_brick_tile") *value = g_tune.spmv_brick_tile;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
     else if (k == "upd_unroll") *value = g_tune.upd_unroll;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;

@@ -374,13 +374,8 @@ int gbrick_bound(kle_mat *A, double vmax_all)
 int gbrick_launch(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
 {
     kle_ctx *c = A->ctx;
-    static int lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
     auto kern = k_nb_spmv_gsym_brick<BRICK_WV, 1>;
-    if (A->brick_lds > lds_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  A->brick_lds);
-        lds_set = A->brick_lds;
-    }
+    dyn_lds(c, reinterpret_cast<const void *>(kern), (size_t)A->brick_lds);
     hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * BRICK_WV),
                        (size_t)A->brick_lds, c->stream, reinterpret_cast<const GBrickDesc *>(A->d_bdesc),
                        reinterpret_cast<const int4 *>(A->d_browd), A->d_slid, A->d_sdict, A->d_sval, x->base, A->d_sws,

@@ -346,6 +346,8 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
 int sval_alloc(kle_mat *A, size_t bytes);
 // a streamed array (matrix values): 0, or -1 out of memory
 int big_alloc(void **p, size_t bytes);
+// declare `bytes` of dynamic LDS for kernel `kern` on c's device (once per size)
+void dyn_lds(const kle_ctx *c, const void *kern, size_t bytes);
 // (xs: the owned x, for the box bricks' one-block rows -- d_ssingle)
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
                 int preload, hipStream_t st, const double *xs = nullptr);
@@ -406,16 +408,9 @@ struct Tuning {
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
-    int spmv_brick_fill = 1;   // brick SpMV: 1 the region fill's first loads go out before the first items' value loads, 0 after
     int spmv_gather_wps = 0;   // run-mask gather: waves per 64-row slice (1, 2, 4; 0 auto by the runs per slice)
-    int spmv_brick_waves = 16; // brick SpMV: waves per brick workgroup (8, 12, 16)
-    int spmv_brick_fcost = 0;  // brick SpMV (read at build): with pairs, plan by blocks (1) or by 64-block passes (0)
     int spmv_brick_pair = 1;  // brick SpMV (read at build): rows in units of two whose tails share one 64-lane item
     int spmv_brick_singles = 1;  // brick SpMV (read at build): rows of one stored block formed by the gather, not as 64-lane items of the bricks
-    int spmv_brick_tail = 0;   // brick SpMV (read at build): per mille of the mean brick cut off the heavy bricks into tail tiles (0 none)
-    int spmv_brick_tile = 20;  // brick SpMV (read at build): a tail tile's weight, per mille of the mean brick
-    int spmv_brick_bands = 0;  // brick SpMV (read at build): 1 the planner also tries ragged bands (balanced bricks; measured no faster), 0 boxes only
-    int spmv_brick_pad = 0;    // brick SpMV (read at build): doubles of gap before each brick's values (multiple of 16; experiments)
     int spmv_brick_split = 0;  // brick SpMV (read at build): force nbx + 100 nby + 10000 nbz bricks (0: planned)
     int spmv_sym_brick = 1;   // box symmetric storage, one rank (read at build): one brick per CU, sums in LDS for the whole stream (kle_brick.hip); 0 the 128-row tiles
 #ifdef KLE_PROBE_BUILD

@@ -841,25 +841,10 @@ struct kle_ksp {
     int max_corr = g_tune.ksp_refine;  // correction solves on a missed true residual (refine)
     int corr_its = 0;                  // iterations of the last solve's corrections
     int corr_reason = 0;               // converged reason of the last correction (0: none ran)
-    // single-rank CG: `check_every` iterations captured as one hipGraph,
-    // replayed until the device reason word stops the kernels; valid for the
-    // (b, x) pair it was captured with
-    hipGraphExec_t graph = nullptr;
-    const double *graph_b = nullptr, *graph_x = nullptr;
-    int graph_jac = -1, graph_len = 0, graph_par = -1;
-    bool graph_off = false;  // capture failed once: stream-launched from then on
 };
-
-static void drop_graph(kle_ksp *k)
-{
-    if (k->graph) (void)hipGraphExecDestroy(k->graph);
-    k->graph = nullptr;
-    k->graph_b = k->graph_x = nullptr;
-}
 
 static void free_work(kle_ksp *k)
 {
-    drop_graph(k);
     kle_vec_destroy(k->r);
     kle_vec_destroy(k->p);
     kle_vec_destroy(k->q);
@@ -1156,62 +1141,8 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
         }
         return 0;
     };
-    // hipGraph replay (KLE_GRAPH=1; one rank, no per-launch timing): every
-    // kernel of the loop reads its scalars from device memory and turns into a
-    // no-op once the reason word is set, so a block of check_every iterations
-    // is a fixed launch sequence; capture it once per (b, x, starting parity),
-    // replay it per block (pro_mode: the block starts after one stream
-    // iteration, with a pending stage; an even block length returns to the
-    // same parity).  Off by default: the loop is not launch-bound on MI355X
-    // (tools/graph_ab.py: equal time at 1M and 8M DoF, +0.7 % on a 142k-DoF part)
-    const char *ge = getenv("KLE_GRAPH");
-    const bool want_graph = fuse && !c->profiling && !k->graph_off && ge && atoi(ge) != 0 &&
-                            (!pro_mode || k->check_every % 2 == 0);
     int it = 0;
-    if (want_graph && pro_mode && limit > 0) {
-        KLE_TRY(iteration());
-        ++it;
-    }
-    if (want_graph && it < limit &&
-        !(k->graph && k->graph_b == b->d && k->graph_x == x->d && k->graph_jac == (int)jac &&
-          k->graph_len == k->check_every && k->graph_par == (pro_mode ? par : -1))) {
-        drop_graph(k);
-        hipGraph_t gr = nullptr;
-        const int par0 = par;
-        int rc = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess ? 0 : 1;
-        for (int j = 0; j < k->check_every && !rc; ++j) rc = iteration();
-        const bool ended = hipStreamEndCapture(c->stream, &gr) == hipSuccess;
-        par = par0;  // capture launched nothing
-        hipGraphExec_t ex = nullptr;
-        if (!rc && ended && gr && hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0) == hipSuccess) {
-            k->graph = ex;
-            k->graph_b = b->d;
-            k->graph_x = x->d;
-            k->graph_jac = (int)jac;
-            k->graph_len = k->check_every;
-            k->graph_par = pro_mode ? par0 : -1;
-        } else {
-            k->graph_off = true;  // e.g. a matrix whose SpMV path cannot be captured
-            (void)hipGetLastError();
-        }
-        if (gr) (void)hipGraphDestroy(gr);
-    }
-    bool stopped = false;
-    if (want_graph && k->graph) {
-        // fixed iterations never stop on the device: whole graph blocks, then
-        // the remainder stream-launched
-        for (; it < limit && (!k->fixed || it + k->graph_len <= limit); it += k->graph_len) {
-            KLE_HIP(hipGraphLaunch(k->graph, c->stream));
-            if (!k->fixed) {
-                KLE_TRY(poll_state(k));
-                if (c->h_istate[I_REASON] != 0) {
-                    stopped = true;
-                    break;
-                }
-            }
-        }
-    }
-    for (; it < limit && !stopped; ++it) {
+    for (; it < limit; ++it) {
         KLE_TRY(iteration());
         if (!k->fixed && ((it + 1) % k->check_every == 0)) {
             KLE_TRY(poll_state(k));
@@ -1628,7 +1559,6 @@ int kle_ksp_set_operators(kle_ksp *k, kle_mat *A)
     KLE_ARG(A->m_global == A->n_global, "KSP needs a square operator");
     k->A = A;
     k->setup = false;
-    drop_graph(k);
     return 0;
 }
 

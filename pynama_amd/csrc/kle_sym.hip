@@ -1653,12 +1653,8 @@ static int gsym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate
     auto launch = [&](auto kern, int slot, int64_t l0, int64_t nl, int US) {
         if (nl <= 0) return;
         const size_t lds = gsym_lds(US, G);
-        static size_t lds_set[28] = {};  // dynamic LDS above 64 KB must be declared per kernel
-        if (lds > lds_set[slot]) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            lds_set[slot] = lds;
-        }
+        (void)slot;
+        dyn_lds(A->ctx, reinterpret_cast<const void *>(kern), lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)nl), dim3(64 * WV), lds, st, n, nl, A->d_sglist + l0, US, A->d_svptr,
                            A->d_srow, A->d_sbp, A->d_slid, A->d_sdptr, A->d_sdict, A->d_swptr, A->d_sval, x->base, A->d_sws,
                            A->d_stile_e, istate, g_tune.spmv_xcd_chunk, g_tune.spmv_gsym_stpol KLE_PROBE_ARG);
@@ -2020,7 +2016,7 @@ static int sym_build_impl(kle_mat *A)
         }
         if (bplan) {
             sv.swap(svb);
-            tot = std::max<int64_t>(tot, sv[n]);  // (spmv_brick_pad: gaps between the bricks)
+            tot = std::max<int64_t>(tot, sv[n]);
         }
         else if (const char *e = getenv("KLE_TIMING"))
             if (atoi(e)) fprintf(stderr, "[kle brick r%d] not used: %s\n", c->rank, bwhy.c_str());
@@ -2201,12 +2197,7 @@ static void launch_sym_xl(const kle_mat *A, const SymGeo &g, const kle_vec *x, i
 {
     if (t1 <= t0) return;
     const size_t lds = sym_xl_lds(sym_region(A));
-    static size_t lds_set = 0;  // dynamic LDS above 64 KB must be declared per kernel
-    if (lds > lds_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, TY, TZ>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        lds_set = lds;
-    }
+    dyn_lds(A->ctx, reinterpret_cast<const void *>(&k_nb_spmv_sym_xl<WV, DET, TY, TZ>), lds);
     hipLaunchKernelGGL((k_nb_spmv_sym_xl<WV, DET, TY, TZ>), dim3((unsigned)(t1 - t0)), dim3(64 * WV), lds, st, g,
                        A->d_srow, A->d_svptr, A->d_sval, x->base, A->d_sws, A->d_stile_e, istate,
                        (int)t0, g_tune.spmv_sym_early, g_tune.spmv_sym_stpol, g_tune.spmv_sym_xcd KLE_PROBE_ARG);
@@ -2328,9 +2319,8 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_brick)
-        return std::string("k_nb_spmv_sym_brick<") + std::to_string(g_tune.spmv_brick_waves) +
-               (g_tune.spmv_brick_fill ? ",true>" : ",false>") + "+k_nb_gsym_gather<" + std::to_string(gather_wps(A)) +
-               ">";
+        return std::string("k_nb_spmv_sym_brick<") + std::to_string(BRICK_WV) + ",true>+k_nb_gsym_gather<" +
+               std::to_string(gather_wps(A)) + ">";
     if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather<" + std::to_string(gather_wps(A)) + ">";
     if (A->sym_graph)
         return std::string("k_nb_spmv_gsym<") + (g_tune.spmv_sym_det ? "true," : "false,") +

@@ -293,7 +293,7 @@ def get_ctx():
             set_tuning("ksp_refine", int(os.environ["KLE_KSP_REFINE"]))
         if os.environ.get("KLE_SPMV_GSYM_BRICK"):
             set_tuning("spmv_gsym_brick", int(os.environ["KLE_SPMV_GSYM_BRICK"]))
-        if os.environ.get("KLE_TUNING"):  # any knobs, as JSON: KLE_TUNING='{"spmv_brick_tail": 10}'
+        if os.environ.get("KLE_TUNING"):  # any knobs, as JSON: KLE_TUNING='{"spmv_gather_wps": 2}'
             import json
             for k, v in json.loads(os.environ["KLE_TUNING"]).items():
                 set_tuning(k, int(v))

@@ -870,45 +870,6 @@ def test_device_pattern_matches_host_unstructured(pa, tmp_path):
         np.testing.assert_array_equal((A0 * x).getArray(), (A1 * x).getArray())
 
 
-def test_graph_replay_matches_stream_launches(pa):
-    """Single-rank CG replayed from a captured hipGraph (KLE_GRAPH=1) ==
-    stream-launched CG, bitwise (solution, iteration count), converged and
-    fixed-iteration modes."""
-    from pynama_amd.petsc import KSP, PC
-    g = _golden("tg3d_p4")
-    dom = _domain(pa, g)
-    mat = pa.MatFS()
-    mat.setDomain(dom)
-    mat.build(buildOperators=False)
-    K = mat.K
-    b = K.createVecLeft()
-    b.setArray(np.random.default_rng(3).uniform(-1, 1, b.getLocalSize()))
-    out = {}
-    try:
-        for mode in ("1", "0"):
-            os.environ["KLE_GRAPH"] = mode
-            ksp = KSP().create()
-            ksp.setType("cg")
-            pc = PC()
-            pc.setType("jacobi")
-            ksp.setPC(pc)
-            ksp.setCGSingleReduction(True)
-            ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
-            ksp.setOperators(K)
-            x = K.createVecRight()
-            ksp.solve(b, x)
-            its = ksp.getIterationNumber()
-            x1 = x.getArray().copy()
-            ksp.setFixedIterations(13)  # not a multiple of the 8-iteration graph
-            ksp.solve(b, x)
-            out[mode] = (its, x1, ksp.getIterationNumber(), x.getArray().copy())
-    finally:
-        os.environ.pop("KLE_GRAPH", None)
-    assert out["1"][0] == out["0"][0] and out["1"][2] == out["0"][2] == 13
-    np.testing.assert_array_equal(out["1"][1], out["0"][1])
-    np.testing.assert_array_equal(out["1"][3], out["0"][3])
-
-
 def test_fixed_iterations_continue_the_recurrence(pa):
     """kle_ksp_continue (the bench's timed region): W fixed iterations, then n
     more continuing the same recurrence == W + n iterations in one solve,

@@ -63,13 +63,6 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         _close(yb, ref)
     for _ in range(3):
         np.testing.assert_array_equal((K * x).getArray(), yb)
-    # the region fill after the first items' value loads instead of before
-    # them: the same sums in the same order, bitwise
-    set_tuning("spmv_brick_fill", 0)
-    try:
-        np.testing.assert_array_equal((K * x).getArray(), yb)
-    finally:
-        set_tuning("spmv_brick_fill", 1)
     # the gather with 1, 2 or 4 waves per 64-row slice (its parts summed in
     # another grouping): the same product to rounding, each bitwise repeatable
     for wps in (1, 2, 4):
@@ -81,18 +74,6 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
             set_tuning("spmv_gather_wps", 0)
         for ref in (y0, yh):
             _close(yw, ref)
-    # the ragged-band plans (spmv_brick_bands 1: bricks as row lists, other
-    # regions) -- the same product to rounding
-    set_tuning("spmv_brick_bands", 1)
-    try:
-        K.setOption(K.Option.SPD, True)
-        assert K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
-        ybb = (K * x).getArray().copy()
-    finally:
-        set_tuning("spmv_brick_bands", 0)
-        K.setOption(K.Option.SPD, True)
-    for ref in (y0, yh):
-        _close(ybb, ref)
     # the one-block rows as items of their bricks (spmv_brick_singles 0)
     # instead of formed by the gather (another plan: other regions and
     # scales) -- the same product to rounding
@@ -105,21 +86,6 @@ def test_brick_spmv_matches_full_storage_csr_and_tiles(pa, nelem, ngl):
         K.setOption(K.Option.SPD, True)
     for ref in (y0, yh):
         _close(ys, ref)
-    # tail tiles (spmv_brick_tail: the heavy bricks' last rows as small
-    # bricks launched after them) -- the same product to rounding
-    set_tuning("spmv_brick_tail", 30)
-    set_tuning("spmv_brick_tile", 40)
-    try:
-        K.setOption(K.Option.SPD, True)
-        assert K.spmvKernel().startswith("k_nb_spmv_sym_brick"), K.spmvKernel()
-        ybt = (K * x).getArray().copy()
-        np.testing.assert_array_equal((K * x).getArray(), ybt)
-    finally:
-        set_tuning("spmv_brick_tail", 0)
-        set_tuning("spmv_brick_tile", 20)
-        K.setOption(K.Option.SPD, True)
-    for ref in (y0, yh):
-        _close(ybt, ref)
     set_tuning("spmv_sym_brick", 0)
     try:
         K.setOption(K.Option.SPD, True)

@@ -216,19 +216,30 @@ def test_unstructured_full_size_dictionary_spmv_is_bitwise(pa, tmp_path):
     mat.setDomain(dom)
     mat.build(buildOperators=False)
     _log(t0, "unstructured system assembled")
+    # (K's default product is the symmetric storage on graph bricks, which
+    # spmv_dict does not touch: its full storage is compared with spmv_sym 0,
+    # and the graph bricks with that to rounding)
+    assert mat.K.isSymmetricStorage() and mat.K.spmvKernel().startswith("k_nb_spmv_gsym_brick<")
     for name in ("K", "Rw", "Krhs"):
         A = getattr(mat, name)
         assert not A.isStructured()
         x = A.createVecRight()
         x.setArray(np.random.default_rng(7).uniform(-1, 1, x.getLocalSize()))
         try:
+            ys = (A * x).getArray().copy()
+            set_tuning("spmv_sym", 0)
             y1 = (A * x).getArray().copy()
             set_tuning("spmv_dict", 0)
             y0 = (A * x).getArray().copy()
         finally:
             set_tuning("spmv_dict", 1)
+            set_tuning("spmv_sym", 1)
         np.testing.assert_array_equal(y1, y0, err_msg=name)
-    _log(t0, "K / Rw / Krhs: dictionary SpMV == column-stream SpMV, bitwise")
+        if name == "K":
+            assert np.linalg.norm(ys - y1) <= 1e-14 * np.linalg.norm(y1)
+        else:
+            np.testing.assert_array_equal(ys, y1, err_msg=name)
+    _log(t0, "K / Rw / Krhs: dictionary SpMV == column-stream SpMV, bitwise; K's graph bricks == both to rounding")
     sol = pa.KleSolver()
     sol.setMat(mat)
     sol.setUp()

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16, "spmv_x_lds": 1, "spmv_dict": 1, "upd_preload": 1, "upd_nt": 2, "spmv_sym": 1, "spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_early": 0, "spmv_sym_align": 0, "spmv_sym_stpol": 0, "spmv_gsym_stpol": 2, "spmv_sym_tile64": 0, "spmv_sym_tile64_max": 640, "spmv_sym_ovl_b": 50, "spmv_sym_xcd": 0, "spmv_sym_brick": 1, "spmv_brick_fill": 1, "spmv_gather_wps": 0, "spmv_brick_max": 0, "spmv_brick_rounds": 1, "spmv_brick_split": 0, "spmv_brick_waves": 16, "spmv_brick_pad": 0, "spmv_gsym_brick": 1, "upd_unroll": 1, "spmv_brick_bands": 0, "spmv_brick_fcost": 0, "spmv_brick_pair": 1, "spmv_brick_singles": 1, "spmv_brick_tail": 0, "spmv_brick_tile": 20}  # kle_set_tuning defaults
+DEFAULTS = {"spmv_waves": 0, "spmv_dyn_lds": -1, "spmv_xcd_chunk": 16, "spmv_x_lds": 1, "spmv_dict": 1, "upd_preload": 1, "upd_nt": 2, "spmv_sym": 1, "spmv_sym_det": 1, "spmv_sym_waves": 0, "spmv_sym_early": 0, "spmv_sym_align": 0, "spmv_sym_stpol": 0, "spmv_gsym_stpol": 2, "spmv_sym_tile64": 0, "spmv_sym_tile64_max": 640, "spmv_sym_ovl_b": 50, "spmv_sym_xcd": 0, "spmv_sym_brick": 1, "spmv_gather_wps": 0, "spmv_brick_max": 0, "spmv_brick_rounds": 1, "spmv_brick_split": 0, "spmv_gsym_brick": 1, "upd_unroll": 1, "spmv_brick_pair": 1, "spmv_brick_singles": 1}  # kle_set_tuning defaults
 
 
 def main():
@@ -85,8 +85,6 @@ def main():
                     continue
                 if k == "_prof_spmv":  # HIP events around every SpMV launch (bench.py's roofline timing)
                     prof = bool(val)
-                elif k == "_graph":  # hipGraph replay of the single-rank loop
-                    os.environ["KLE_GRAPH"] = str(int(val))
                 else:
                     set_tuning(k, val)
             # a fresh fixed-iteration start per block: continuing one recurrence
@@ -108,7 +106,6 @@ def main():
             for k in v:  # back to the library defaults before the next variant
                 if k in DEFAULTS:
                     set_tuning(k, DEFAULTS[k])
-            os.environ.pop("KLE_GRAPH", None)
             if ksp.getConvergedReason() < 0:
                 print(json.dumps({"rep": rep, "variant": v, "invalid": "recurrence diverged (reason %d)"
                                   % ksp.getConvergedReason()}), flush=True)

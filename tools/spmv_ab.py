@@ -15,7 +15,7 @@ import sys
 
 if "spmv_sym_probe" in " ".join(sys.argv[1:]):
     os.environ["KLE_LIBRARY"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkle_probe.so")
-BUILD_KNOBS = {"spmv_brick_fcost", "spmv_brick_pair", "spmv_brick_singles", "spmv_brick_tail", "spmv_brick_tile", "spmv_brick_bands", "spmv_gsym_brick", "spmv_brick_pad", "spmv_brick_rounds", "spmv_brick_split", "spmv_brick_max", "spmv_sym_brick", "spmv_sym_tz", "spmv_gsym_rows", "spmv_gsym_waves", "spmv_sym_align", "spmv_sym_tile64", "spmv_sym_tile64_max"}  # read when the symmetric storage is built
+BUILD_KNOBS = {"spmv_brick_pair", "spmv_brick_singles", "spmv_gsym_brick", "spmv_brick_rounds", "spmv_brick_split", "spmv_brick_max", "spmv_sym_brick", "spmv_sym_tz", "spmv_gsym_rows", "spmv_gsym_waves", "spmv_sym_align", "spmv_sym_tile64", "spmv_sym_tile64_max"}  # read when the symmetric storage is built
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
