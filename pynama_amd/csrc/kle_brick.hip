@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
                                                                  const double *__restrict__ sval,
                                                                  const double *__restrict__ x,
                                                                  double *__restrict__ ws, double *__restrict__ y,
-                                                                 const int *__restrict__ istate KLE_PROBE_PARAM)
+                                                                 const int *__restrict__ istate, int xcd KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
     constexpr int NT = 64 * WV;
@@ -84,9 +84,9 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     extern __shared__ double lds[];
     KLE_PROBE_TS(ts0)
 #ifdef KLE_PROBE_BUILD
-    __shared__ unsigned pmx[2];
+    __shared__ unsigned pmx[3];
 #endif
-    const int b = blockIdx.x;
+    const int b = brick_of_wg(blockIdx.x, gridDim.x, xcd);
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int NU = bd[b].nr / 2;  // units of two rows (kle_brick_plan.cpp)
     const int ox = bd[b].ox, oy = bd[b].oy, oz = bd[b].oz, RX = bd[b].RX, RY = bd[b].RY, RZ = bd[b].RZ;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     BItem i0, i1;
 #ifdef KLE_PROBE_BUILD
     unsigned long long tsf = 0;
-    if (threadIdx.x == 0) pmx[0] = pmx[1] = 0;
+    if (threadIdx.x == 0) pmx[0] = pmx[1] = pmx[2] = 0;
 #endif
     // 2b. the first item's value loads, then the fill's first loads landed
     // (vmcnt(9): the value loads stay in flight), into LDS; further lines
@@ -304,6 +304,9 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         int lb = l0;
         if constexpr (FF) {
             issue(v0, r0, i0);
+#ifdef KLE_PROBE_BUILD
+            if (probe_ts && lane == 0) atomicMax(&pmx[2], (unsigned)(__builtin_amdgcn_s_memrealtime() - ts0));
+#endif
             wait_x12<9 * D>(fv0);
 #ifdef KLE_PROBE_BUILD
             tsf = probe_ts ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
         dst[t] = fx_to_d(acc[c * RS + k]) * T1 * T2;
     }
-    KLE_PROBE_TS_END4(b, ts0, ts1, ts2, ts0 + pmx[0], ts0 + pmx[1])
+    KLE_PROBE_TS_END5(b, ts0, ts1, ts2, ts0 + pmx[0], ts0 + pmx[1], ts0 + pmx[2])
 }
 
 // y[0 .. n) += r: the lower neighbour's sums for this slab's lowest nodes
@@ -798,7 +801,7 @@ void brick_forget(kle_mat *A)
     A->brick_lds_u = 0;
 }
 
-int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
+int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart, bool split)
 {
     kle_ctx *c = A->ctx;
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
@@ -810,7 +813,7 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
         hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * wv), (size_t)A->brick_lds, c->stream,
                            (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, bd,
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
-                           istate KLE_PROBE_ARG);
+                           istate, g_tune.spmv_brick_xcd KLE_PROBE_ARG);
     };
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
     // N > 1 (z slabs): the x ghost planes first (every brick's region fill
@@ -832,7 +835,10 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     // the runs of the regions holding it, in ascending brick order
     const int64_t n = A->nrows, ntot = n + A->ghost_hi / 3, nlo = n / 64 * 64;
     const double *xs = A->d_ssingle ? x->d : nullptr;  // (rows of one stored block: the gather's)
-    if (!dist) return gsym_gather(A, y->d, 0, n, istate, dpart ? x->d : nullptr, dpart, 1, c->stream, xs);
+    if (!dist) {
+        if (split) return 0;  // (the consumer gathers every row: BrickGather)
+        return gsym_gather(A, y->d, 0, n, istate, dpart ? x->d : nullptr, dpart, 1, c->stream, xs);
+    }
     // the slices holding upper ghost rows first (their sums: d_sgsend)
     KLE_TRY(gsym_gather(A, y->d, nlo, ntot, istate, nullptr, nullptr, 1, c->stream, xs));
     const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
@@ -844,13 +850,53 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     }
     KLE_TRY(halo_reverse(c, A->d_sgsend, A->ghost_hi, A->hi_rank, A->d_sgrecv, nrecv, A->lo_rank, cs));
     if (ovl) KLE_HIP(hipEventRecord(c->ev_halo_done, cs));
-    KLE_TRY(gsym_gather(A, y->d, 0, nlo, istate, nullptr, nullptr, 1, c->stream, xs));
-    if (ovl) KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
+    if (split) return 0;  // (the owned rows below nlo and the received sums: the consumer's)
+    return brick_gather_rest(A, x, y, istate);
+}
+
+// The rest of a split product (brick_spmv with split): the rows [0, nlo)
+// (every row on one rank) gathered, then the received reverse-halo sums added
+// last -- the same operations, in the same order, as the unsplit product
+// (wps_force 1: each row's runs summed in k_pipe_iter_g's order).
+int brick_gather_rest(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, int wps_force)
+{
+    kle_ctx *c = A->ctx;
+    const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    const int64_t n = A->nrows, nlo = dist ? n / 64 * 64 : n;
+    const double *xs = A->d_ssingle ? x->d : nullptr;
+    KLE_TRY(gsym_gather(A, y->d, 0, nlo, istate, nullptr, nullptr, 1, c->stream, xs, wps_force));
+    if (!dist) return 0;
+    const int64_t nrecv = A->lo_rank >= 0 ? A->send_lo : 0;
+    if (A->halo_overlap) KLE_HIP(hipStreamWaitEvent(c->stream, c->ev_halo_done, 0));
     if (nrecv)
         hipLaunchKernelGGL(k_brick_add_recv, dim3((unsigned)((nrecv + 255) / 256)), dim3(256), 0, c->stream, nrecv,
                            A->d_sgrecv, y->d, istate);
     KLE_HIP(hipGetLastError());
     return 0;
+}
+
+// What a consumer of a split product gathers itself (k_pipe_iter_g,
+// kle_ksp.hip): the run lists of the rows [0, ng), the one-block rows, and
+// the received sums of the lowest rows (after the reverse halo, which the
+// consumer's stream must have waited for: see brick_split_wait)
+BrickGather brick_gather_src(const kle_mat *A, const kle_vec *x)
+{
+    const kle_ctx *c = A->ctx;
+    const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    BrickGather g;
+    g.runptr = A->d_sgptr;
+    g.rstart = A->d_sgidx;
+    g.rmask = A->d_sgmask;
+    g.ws = A->d_sws;
+    g.single = A->d_ssingle;
+    g.sval = A->d_sval;
+    g.svptr = A->d_svptr;
+    g.xs = x->d;
+    g.nrows = A->nrows;
+    g.ng = dist ? A->nrows / 64 * 64 : A->nrows;
+    g.recv = A->d_sgrecv;
+    g.nrecv = dist && A->lo_rank >= 0 ? A->send_lo : 0;
+    return g;
 }
 
 }  // namespace kle

@@ -765,7 +765,10 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_singles") {
         KLE_ARG(value == 0 || value == 1, "spmv_brick_singles: 0 or 1");
         g_tune.spmv_brick_singles = value;
-                    } else if (k == "spmv_gather_wps") {
+                    } else if (k == "spmv_brick_xcd") {
+        KLE_ARG(value == 0 || value == 1, "spmv_brick_xcd: 0 or 1");
+        g_tune.spmv_brick_xcd = value;
+    } else if (k == "spmv_gather_wps") {
         KLE_ARG(value == 0 || value == 1 || value == 2 || value == 4, "spmv_gather_wps: 0 (auto), 1, 2 or 4");
         g_tune.spmv_gather_wps = value;
                 } else if (k == "spmv_brick_split") {
@@ -783,6 +786,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_sym_tz") {
         KLE_ARG(value == 0 || value == 2 || value == 4, "spmv_sym_tz: 0 (auto), 2 or 4");
         g_tune.spmv_sym_tz = value;
+    } else if (k == "ksp_pipe_gather") {
+        KLE_ARG(value == 0 || value == 1, "ksp_pipe_gather: 0 or 1");
+        g_tune.ksp_pipe_gather = value;
     } else if (k == "ipc_sentinel") {
         KLE_ARG(value == 0 || value == 1, "ipc_sentinel: 0 or 1");
         g_tune.ipc_sentinel = value;
@@ -869,6 +875,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_singles") *value = g_tune.spmv_brick_singles;
     else if (k == "spmv_brick_pair") *value = g_tune.spmv_brick_pair;
     else if (k == "spmv_gather_wps") *value = g_tune.spmv_gather_wps;
+    else if (k == "spmv_brick_xcd") *value = g_tune.spmv_brick_xcd;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
     else if (k == "upd_unroll") *value = g_tune.upd_unroll;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;
@@ -886,6 +893,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "ksp_refine") *value = g_tune.ksp_refine;
     else if (k == "ksp_corr_fault") *value = g_tune.ksp_corr_fault;
     else if (k == "ipc_sentinel") *value = g_tune.ipc_sentinel;
+    else if (k == "ksp_pipe_gather") *value = g_tune.ksp_pipe_gather;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
     else if (k == "spmv_gsym_waves") *value = g_tune.spmv_gsym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;

@@ -326,6 +326,8 @@ int spmv_dot(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 int spmv_dot_parts(const kle_mat *A);  // what spmv_dot would write (0: none)
 // true when spmv(A, x, ...) exchanges the halo on ctx->comm_stream
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
+bool spmv_can_split(const kle_mat *A);
+int spmv_split(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
 unsigned sync_event_flags();  // kle_core.hip
@@ -349,14 +351,33 @@ int big_alloc(void **p, size_t bytes);
 // declare `bytes` of dynamic LDS for kernel `kern` on c's device (once per size)
 void dyn_lds(const kle_ctx *c, const void *kern, size_t bytes);
 // (xs: the owned x, for the box bricks' one-block rows -- d_ssingle)
+// (wps_force: the waves per slice, 0 by the runs per slice; 1 sums every
+// row's runs in the order the fused CG update does, k_pipe_iter_g)
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
-                int preload, hipStream_t st, const double *xs = nullptr);
+                int preload, hipStream_t st, const double *xs = nullptr, int wps_force = 0);
 // graph bricks (kle_gbrick.hip)
 int gbrick_bound(kle_mat *A, double vmax_all);
 int gbrick_launch(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
 int brick_finish(kle_mat *A, void *plan);
 void brick_plan_free(void *plan);
-int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart);
+// split: the owned rows' gather and the received reverse-halo sums are left
+// to the consumer (k_pipe_iter_g) or to brick_gather_rest
+int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart, bool split = false);
+int brick_gather_rest(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, int wps_force = 0);
+// a split box-brick product's remaining gather, as the fused CG update does it
+struct BrickGather {
+    const int *runptr, *rstart;
+    const unsigned long long *rmask;
+    const double *ws;
+    const unsigned long long *single;  // one-block rows per 64-row slice (null: none)
+    const double *sval;
+    const int64_t *svptr;
+    const double *xs;     // the product's input (owned part): the one-block rows' B_ii x_i
+    int64_t nrows, ng;    // owned rows; rows [0, ng) gathered by the consumer, [ng, nrows) by the split product
+    const double *recv;   // the lower neighbour's sums for the entries [0, nrecv), added last
+    int64_t nrecv;
+};
+BrickGather brick_gather_src(const kle_mat *A, const kle_vec *x);
 void brick_drop(kle_mat *A);
 void brick_forget(kle_mat *A);
 // IPC transport (kle_ipc.hip): slab and graph-partition halos, their reverse halos, allreduce
@@ -381,6 +402,7 @@ struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
+    int ksp_pipe_gather = 1;  // pipelined CG on box bricks: the product's owned-row gather folded into the next update (k_pipe_iter_g); 0 separate
     int ipc_sentinel = 0;  // IPC transport (debug): consumed mailbox slots overwritten with NaN before the ack (a stale or early slot read shows as NaN)
     int ksp_corr_fault = 0;  // test hook: 1 = refine() runs its correction solves even when the true residual meets rtol, and each ends in NaN (DIVERGED_NANORINF) -- x must stay as it was
     int ksp_refine = 2;  // CG / pipelined CG: up to this many correction solves when the true residual misses rtol (kle_ksp.hip refine; default of new KSPs); 0 PETSc's plain stop
@@ -408,6 +430,7 @@ struct Tuning {
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
+    int spmv_brick_xcd = 0;  // box and graph bricks: 1 each XCD streams a contiguous run of bricks (shared region x in its L2), 0 round-robin
     int spmv_gather_wps = 0;   // run-mask gather: waves per 64-row slice (1, 2, 4; 0 auto by the runs per slice)
     int spmv_brick_pair = 1;  // brick SpMV (read at build): rows in units of two whose tails share one 64-lane item
     int spmv_brick_singles = 1;  // brick SpMV (read at build): rows of one stored block formed by the gather, not as 64-lane items of the bricks
@@ -473,8 +496,14 @@ extern int64_t g_probe_ts_cap;
             r[7] = ((d) - (a)) | (((e) - (a)) << 32);                                                   \
         }                                                                                               \
     }
+// (and a third point in r[5]'s upper half)
+#define KLE_PROBE_TS_END5(slot, a, b, c, d, e, f)                                                      \
+    KLE_PROBE_TS_END4(slot, a, b, c, d, e)                                                              \
+    if (probe_ts && threadIdx.x == 0 && (int64_t)(slot) < probe_cap)                                   \
+        probe_ts[8 * (int64_t)(slot) + 5] |= ((f) - (a)) << 32;
 #else
 #define KLE_PROBE_TS_END4(slot, a, b, c, d, e)
+#define KLE_PROBE_TS_END5(slot, a, b, c, d, e, f)
 #define KLE_PROBE_PARAM
 #define KLE_PROBE_ARG
 #define KLE_PROBE_CONST constexpr int probe = 0;

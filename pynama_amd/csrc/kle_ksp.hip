@@ -509,6 +509,130 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_pip
     block_sums<3>(acc, pp_out, G);
 }
 
+// k_pipe_iter with the gather of a split box-brick product n = A m folded in
+// (kle_brick.hip brick_spmv split): the product left
+// its bricks' region sums in ws and the rows' direct sums in n, and a wave of
+// this update takes one 64-row slice -- it sums the slice's runs (the
+// run-mask gather's order: runs, then the direct sum or a one-block row's
+// B_ii x_i, then the lower neighbour's reverse-halo sum) into LDS and updates
+// the slice's 192 entries from there.  So n's gather costs no launch of its
+// own, and n is neither written nor read back (it is not used after the
+// update).  The slices past ng (the rows the split product gathered with the
+// upper ghost rows) read n.  One-block rows read m before this wave updates
+// it (the same slice).
+template <bool JAC>
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_pipe_iter_g(BrickGather gs, int64_t n,
+                                                  const double *__restrict__ dinv,
+                                                  const double *__restrict__ nv, double *__restrict__ z,
+                                                  double *__restrict__ q, double *__restrict__ sv,
+                                                  double *__restrict__ p, double *__restrict__ x,
+                                                  double *__restrict__ r, double *__restrict__ u,
+                                                  double *__restrict__ w, double *__restrict__ m,
+                                                  const double *__restrict__ pp_in, double *__restrict__ pp_out,
+                                                  double *__restrict__ scal, int *__restrict__ ist, int pro, int par,
+                                                  double atol)
+{
+    constexpr int WPB = KB / 64;
+    __shared__ double nl[WPB][192];
+    const int G = (int)gridDim.x;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nsl = (gs.nrows + 63) / 64, sst = (int64_t)G * WPB;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // n of one slice into nl[wv] (entries 3 j .. 3 j + 2 of its row j)
+    auto gather = [&](int64_t sl) {
+        const int64_t j = sl * 64 + lane;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        if (sl * 64 < gs.ng) {
+            const int rb = gs.runptr[sl], re = gs.runptr[sl + 1];
+            const bool one = j < gs.nrows && gs.single && ((gs.single[sl] >> lane) & 1ull);
+            double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+            if (j < gs.nrows) {
+                if (one) {
+                    const double *v = gs.sval + gs.svptr[j];
+                    const double x0 = gs.xs[3 * j], x1 = gs.xs[3 * j + 1], x2 = gs.xs[3 * j + 2];
+                    d0 = v[0] * x0 + v[1] * x1 + v[2] * x2;
+                    d1 = v[3] * x0 + v[4] * x1 + v[5] * x2;
+                    d2 = v[6] * x0 + v[7] * x1 + v[8] * x2;
+                } else {
+                    d0 = nv[3 * j];
+                    d1 = nv[3 * j + 1];
+                    d2 = nv[3 * j + 2];
+                }
+            }
+#pragma unroll 8
+            for (int rr = rb; rr < re; ++rr) {
+                const unsigned long long mk = gs.rmask[rr];
+                const bool in = (mk >> lane) & 1ull;
+                const double *pw = gs.ws + (int64_t)gs.rstart[rr] + (in ? 3 * __popcll(mk & below) : 0);
+                const double a0 = pw[0], a1 = pw[1], a2 = pw[2];
+                s0 += in ? a0 : 0.0;
+                s1 += in ? a1 : 0.0;
+                s2 += in ? a2 : 0.0;
+            }
+            s0 += d0;
+            s1 += d1;
+            s2 += d2;
+        } else if (j < gs.nrows) {
+            s0 = nv[3 * j];
+            s1 = nv[3 * j + 1];
+            s2 = nv[3 * j + 2];
+        }
+        if (3 * j < gs.nrecv) {  // (the reverse halo's sums, last)
+            s0 += gs.recv[3 * j];
+            s1 += gs.recv[3 * j + 1];
+            s2 += gs.recv[3 * j + 2];
+        }
+        nl[wv][3 * lane] = s0;
+        nl[wv][3 * lane + 1] = s1;
+        nl[wv][3 * lane + 2] = s2;
+        __builtin_amdgcn_wave_barrier();
+    };
+    int64_t sl = (int64_t)blockIdx.x * WPB + wv;
+    // the first slice's gather before the prologue (it needs no scalar)
+    StageIn in;
+    if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
+    if (sl < nsl) gather(sl);
+    if (ist[I_REASON] != 0) return;
+    double t[3] = {0.0, 0.0, 0.0};
+    if (pro) sums3(pp_in, pp_in + G, G, pp_in + 2 * G, G, t);
+    double alpha, beta;
+    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta, &in)) return;
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (; sl < nsl; sl += sst) {
+        if (sl != (int64_t)blockIdx.x * WPB + wv) gather(sl);
+#pragma unroll
+        for (int ps = 0; ps < 3; ++ps) {
+            const int el = ps * 64 + lane;
+            const int64_t i = sl * 192 + el;
+            if (i >= n) break;
+            const double e0 = nl[wv][el];
+            const double zi = e0 + beta * z[i];
+            const double qi = m[i] + beta * q[i];
+            const double wo = w[i];
+            const double si = wo + beta * sv[i];
+            const double uo = u[i];
+            const double pi = uo + beta * p[i];
+            z[i] = zi;
+            q[i] = qi;
+            sv[i] = si;
+            p[i] = pi;
+            x[i] = x[i] + alpha * pi;
+            const double ri = r[i] - alpha * si;
+            const double ui = uo - alpha * qi;
+            const double wi = wo - alpha * zi;
+            r[i] = ri;
+            u[i] = ui;
+            w[i] = wi;
+            m[i] = JAC ? dinv[i] * wi : wi;
+            acc[0] += ri * ui;
+            acc[1] += ri * ri;
+            acc[2] += wi * ui;
+        }
+        __builtin_amdgcn_wave_barrier();  // (nl[wv] read before the next slice's gather writes it)
+    }
+    block_sums<3>(acc, pp_out, G);
+}
+
 // The scalar stage of the last update of a solve call whose partials would
 // otherwise wait for the next launch's prologue (pipelined / single-reduction
 // CG): leaves the reporting slots (iterations, residual, reason, alpha / beta
@@ -1193,8 +1317,19 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             hipLaunchKernelGGL(k_pipe_init<false>, dim3(g), dim3(KB), 0, c->stream, n, dinv, k->w->d, k->m->d,
                                k->z->d, k->q->d);
         KLE_HIP(hipGetLastError());
-        KLE_TRY(spmv(k->A, k->m, k->nv, nullptr));  // n = A m
     }
+    // box bricks: each product n = A m leaves its owned rows' gather to the
+    // next update (k_pipe_iter_g); npend: n awaits that gather
+    const bool gfuse = g_tune.ksp_pipe_gather && spmv_can_split(k->A);
+    const bool gdist = c->nranks > 1 && (k->A->lo_rank >= 0 || k->A->hi_rank >= 0);
+    bool npend = false;
+    auto product = [&](const int *ist) -> int {
+        if (!gfuse) return spmv(k->A, k->m, k->nv, ist);
+        KLE_TRY(spmv_split(k->A, k->m, k->nv, ist));
+        npend = true;
+        return 0;
+    };
+    if (!cont) KLE_TRY(product(nullptr));  // n = A m
     // the allreduce may run beside the SpMV only where the SpMV's own halo uses
     // the comm stream too (one RCCL stream: halo, then allreduce)
     const bool side = spmv_uses_comm_stream(k->A, k->m);
@@ -1225,22 +1360,41 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                                k->p->d, x->d, k->r->d, k->u->d, k->w->d, k->m->d, pp[par], pp[par ^ 1], c->d_scal,
                                c->d_istate, (int)pending, par, k->atol);
         };
-        if (jac) go(g_tune.upd_preload ? k_pipe_iter<true, true> : k_pipe_iter<true, false>);
-        else go(g_tune.upd_preload ? k_pipe_iter<false, true> : k_pipe_iter<false, false>);
+        auto gog = [&](auto kern) {
+            BrickGather gs = brick_gather_src(k->A, k->m);
+            if (!npend) gs.ng = gs.nrecv = 0;  // (n complete: read it)
+            hipLaunchKernelGGL(kern, dim3(G), dim3(KB), 0, c->stream, gs, n, dinv,
+                               k->nv->d, k->z->d, k->q->d, k->s->d, k->p->d, x->d, k->r->d, k->u->d, k->w->d,
+                               k->m->d, pp[par], pp[par ^ 1], c->d_scal, c->d_istate, (int)pending, par, k->atol);
+        };
+        if (gfuse) {
+            // (n complete -- the first update of a continued call -- the
+            // same kernel reads it: the same arithmetic in the same order as
+            // one uninterrupted solve, bitwise)
+            if (jac) gog(k_pipe_iter_g<true>);
+            else gog(k_pipe_iter_g<false>);
+            npend = false;
+        } else if (jac) {
+            go(g_tune.upd_preload ? k_pipe_iter<true, true> : k_pipe_iter<true, false>);
+        } else {
+            go(g_tune.upd_preload ? k_pipe_iter<false, true> : k_pipe_iter<false, false>);
+        }
         if (hipGetLastError() != hipSuccess) { rc = fail(KLE_ERR_DEVICE, "k_pipe_iter launch failed"); break; }
         if ((rc = c->toc("cg_update", &ev))) break;
         par ^= 1;
         pending = true;
         if (fuse) {
             // one rank: the next launch's prologue reduces these partials
-            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
+            if ((rc = product(c->d_istate))) break;
         } else if (side && c->nranks > 1) {
             // the partials' allreduce on the comm stream behind the halo, beside
             // the SpMV; the overlapped SpMV already makes the comm stream wait
             // for the update (ev_x_ready), so no event of its own: each event
             // record / cross-stream wait costs ~2.5 us on the critical path
             // (profiles/r02/sync_cost_eighth.jsonl)
-            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
+            // (a split product's reverse halo went first on the comm stream:
+            // the wait for the allreduce covers the received sums too)
+            if ((rc = product(c->d_istate))) break;
             if ((rc = allreduce_sum(c, pp[par], 3 * G, c->comm_stream))) break;
             if (hipEventRecord(ev_red, c->comm_stream) != hipSuccess ||
                 hipStreamWaitEvent(c->stream, ev_red, 0) != hipSuccess) {
@@ -1251,7 +1405,12 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             // no overlap possible on this rank (or a one-rank RCCL
             // communicator): same collective order as the overlapping ranks
             // (halo, then allreduce), all on one stream
-            if ((rc = spmv(k->A, k->m, k->nv, c->d_istate))) break;
+            if ((rc = product(c->d_istate))) break;
+            if (gfuse && gdist && k->A->halo_overlap &&
+                hipStreamWaitEvent(c->stream, c->ev_halo_done, 0) != hipSuccess) {  // (the received sums)
+                rc = fail(KLE_ERR_DEVICE, "event wait failed");
+                break;
+            }
             if ((rc = allreduce_sum(c, pp[par], 3 * G, c->stream))) break;
         }
         if (!k->fixed && ((it + 1) % k->check_every == 0)) {
@@ -1264,6 +1423,9 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                            c->d_scal, c->d_istate, par, k->atol);
         if (hipGetLastError() != hipSuccess) rc = fail(KLE_ERR_DEVICE, "k_cg_flush launch failed");
     }
+    // (n complete when the call returns: a continuation starts with the plain
+    // update, and nothing may clobber the bricks' sums in between)
+    if (!rc && npend) rc = brick_gather_rest(k->A, k->m, k->nv, c->d_istate, 1);
     k->pipe_par = par;
     hipEventDestroy(ev_red);
     if (rc) return rc;

@@ -734,6 +734,26 @@ static int launch_nb_shape(const kle_mat *A, RowMap rm, const int *rbox, const k
     return fail(KLE_ERR_SUP, "no SpMV kernel for %dx%d blocks", A->R, A->C);
 }
 
+// Whether A's product runs the box bricks, whose owned rows' gather a
+// consumer may take over (spmv_split; k_pipe_iter_g)
+bool spmv_can_split(const kle_mat *A)
+{
+    return A->kind == 0 && A->d_sval && g_tune.spmv_sym && A->sym_brick && !A->sym_graph && A->nbricks > 0;
+}
+
+// y = A x without the owned rows' gather and the received reverse-halo sums
+// (kle_brick.hip brick_spmv split): the consumer adds them (BrickGather), or
+// brick_gather_rest does.  Only where spmv_can_split.
+int spmv_split(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
+{
+    KLE_ARG(spmv_can_split(A), "split product: not a box-brick matrix");
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    KLE_TRY(A->ctx->tic("spmv", &ev));
+    KLE_TRY(brick_spmv(A, x, y, istate, nullptr, true));
+    KLE_TRY(A->ctx->toc("spmv", &ev));
+    return 0;
+}
+
 int spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
 {
     kle_ctx *c = A->ctx;

@@ -1616,11 +1616,11 @@ static int gather_wps(const kle_mat *A)
 }
 
 int gsym_gather(kle_mat *A, double *y, int64_t r0, int64_t r1, const int *istate, const double *xdot, double *dpart,
-                int preload, hipStream_t st, const double *xs)
+                int preload, hipStream_t st, const double *xs, int wps_force)
 {
     if (r1 <= r0) return 0;
     const int64_t s0 = r0 / 64, s1 = (r1 + 63) / 64, ntot = A->nrows + A->ghost_hi / 3;
-    const int wps = gather_wps(A);
+    const int wps = wps_force ? wps_force : gather_wps(A);
     auto go = [&](auto kern, int wp) {
         hipLaunchKernelGGL(kern, dim3((unsigned)((s1 - s0 + 3) / 4)), dim3(256 * wp), 0, st, A->nrows, ntot,
                            A->d_sgptr, A->d_sgidx, A->d_sgmask, A->d_sws, y, A->d_sgsend, istate, xdot, dpart,

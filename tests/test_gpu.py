@@ -884,7 +884,13 @@ def test_fixed_iterations_continue_the_recurrence(pa):
     K = mat.K
     b = K.createVecLeft()
     b.setArray(np.random.default_rng(5).uniform(-1, 1, b.getLocalSize()))
-    for kt in ("cg", "pipecg"):
+    # (symmetric storage on bricks: the pipelined update gathers the split
+    # product itself, k_pipe_iter_g -- a continued call starts from a complete
+    # product, read by the same kernel)
+    for kt, spd in (("cg", False), ("pipecg", False), ("pipecg", True), ("cg", True)):
+        K.setOption(K.Option.SPD, spd)
+        if spd:
+            assert K.spmvKernel().startswith("k_nb_spmv_sym_brick<"), K.spmvKernel()
         ksp = KSP().create()
         ksp.setType(kt)
         pc = PC()
@@ -904,6 +910,52 @@ def test_fixed_iterations_continue_the_recurrence(pa):
         y = K.createVecRight()
         with pytest.raises(pa.Error):
             ksp.solveContinue(b, y, 3)  # not the (b, x) of the last fixed solve
+
+
+def test_pipecg_fused_gather_matches_separate(pa):
+    """Pipelined CG on box bricks: the split product's owned-row gather folded
+    into the next update (k_pipe_iter_g, tuning ksp_pipe_gather 1, default)
+    against the separate gather launch (0): the same iteration count within
+    2, solutions within 1e-9, both at rtol 1e-10 (true residual), and the
+    oracle's CG within 1e-7."""
+    from oracle import oracle as O
+    from pynama_amd.petsc import KSP, PC
+    from pynama_amd.runtime import set_tuning
+    g = _golden("tg3d_p4")
+    dom = _domain(pa, g)
+    mat = pa.MatFS()
+    mat.setDomain(dom)
+    mat.build(buildOperators=False)
+    K = mat.K
+    K.setOption(K.Option.SPD, True)
+    assert K.spmvKernel().startswith("k_nb_spmv_sym_brick<")
+    b = K.createVecLeft()
+    ba = np.random.default_rng(9).uniform(-1, 1, b.getLocalSize())
+    b.setArray(ba)
+    out = {}
+    for fused in (1, 0):
+        set_tuning("ksp_pipe_gather", fused)
+        try:
+            ksp = KSP().create()
+            ksp.setType("pipecg")
+            pc = PC()
+            pc.setType("jacobi")
+            ksp.setPC(pc)
+            ksp.setTolerances(rtol=1e-10, atol=0.0, max_it=10000)
+            ksp.setOperators(K)
+            x = K.createVecRight()
+            ksp.solve(b, x)
+            assert ksp.getConvergedReason() > 0
+            assert ksp.getTrueRelativeResidual() <= 1.01e-10
+            out[fused] = (ksp.getIterationNumber(), x.getArray().copy())
+        finally:
+            set_tuning("ksp_pipe_gather", 1)
+    assert abs(out[1][0] - out[0][0]) <= 2, (out[1][0], out[0][0])
+    assert np.linalg.norm(out[1][1] - out[0][1]) <= 1e-9 * np.linalg.norm(out[0][1])
+    ip, ix, d = K.getValuesCSR()
+    A = O.CSR.from_arrays(ip, ix, d, int(ip.shape[0] - 1))
+    xo, ito, _ = A.cg(ba, rtol=1e-10)
+    assert np.linalg.norm(out[1][1] - xo) <= 1e-7 * np.linalg.norm(xo)
 
 
 def test_config2_full_size_properties(pa):

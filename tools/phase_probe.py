@@ -117,6 +117,8 @@ def main():
             fi = (r[:, 7] & 0xFFFFFFFF).astype(np.int64) / 100.0
             fl = (r[:, 7] >> 32).astype(np.int64) / 100.0
             extra = {"fill_landed_max_wave_us": pct(fi), "barrier_arrival_max_wave_us": pct(fl)}
+            if (r[:, 5] >> 32).any():  # (the latest wave's first item issued: its row descriptors in)
+                extra["first_item_issued_max_wave_us"] = pct((r[:, 5] >> 32).astype(np.int64) / 100.0)
         else:
             extra = {}
         summ = {"rep": rep, "kernel": kern, "mesh": a.mesh, "nelem": nelem, "ngl": a.ngl, "workgroups": int(len(r)),
