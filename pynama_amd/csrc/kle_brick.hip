@@ -70,13 +70,13 @@ constexpr int BI_NEWP = 1024;  // (sf: the item starts row P -- its x into the r
 // (checked in the ISA; a variant with two items in flight ahead of the summed
 // one -- no faster, round 5 -- had them moved, wrong products, and is gone)
 template <int WV, bool FF = true>
-__global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp,
+__global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp, int rstride,
                                                                  const BrickDesc *__restrict__ bd,
                                                                  const int2 *__restrict__ rowd,
                                                                  const double *__restrict__ sval,
                                                                  const double *__restrict__ x,
                                                                  double *__restrict__ ws, double *__restrict__ y,
-                                                                 const int *__restrict__ istate, int xcd KLE_PROBE_PARAM)
+                                                                 const int *__restrict__ istate KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
     constexpr int NT = 64 * WV;
@@ -84,13 +84,13 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     extern __shared__ double lds[];
     KLE_PROBE_TS(ts0)
 #ifdef KLE_PROBE_BUILD
-    __shared__ unsigned pmx[3];
+    __shared__ unsigned pmx[4];
 #endif
-    const int b = brick_of_wg(blockIdx.x, gridDim.x, xcd);
+    const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int NU = bd[b].nr / 2;  // units of two rows (kle_brick_plan.cpp)
     const int ox = bd[b].ox, oy = bd[b].oy, oz = bd[b].oz, RX = bd[b].RX, RY = bd[b].RY, RZ = bd[b].RZ;
-    const int rstart = bd[b].rstart, eb = bd[b].eb;
+    const int eb = bd[b].eb;
     const long long vbase = bd[b].vbase, wsoff = bd[b].wsoff;
     const int RN = RX * RY * RZ, RS = RN + 64, RXY = RX * RY;
     double *xl = lds;
@@ -157,7 +157,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     KLE_PROBE_TS(tsi)
     // (read after the fill's loads are out: the compiler waits for it at once)
     const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
-    cint *rdesc = (cint *)(rowd + rstart);  // (address-space cast: scalar loads)
+    // (the brick's rows at a fixed stride: their descriptors' address needs
+    // no load, so their scalar loads go out beside bd's; address-space
+    // cast: scalar loads)
+    cint *rdesc = (cint *)(rowd + (int64_t)b * rstride);
     const double *vb = sval + vbase;
     // a row from its descriptor (kle_brick.hpp): packed box (dbx, dby, dbz,
     // bnx, bny, bnz: 4 bits each) + the low byte of its region index; value
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     BItem i0, i1;
 #ifdef KLE_PROBE_BUILD
     unsigned long long tsf = 0;
-    if (threadIdx.x == 0) pmx[0] = pmx[1] = pmx[2] = 0;
+    if (threadIdx.x == 0) pmx[0] = pmx[1] = pmx[2] = pmx[3] = 0;
 #endif
     // 2b. the first item's value loads, then the fill's first loads landed
     // (vmcnt(9): the value loads stay in flight), into LDS; further lines
@@ -305,7 +308,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         if constexpr (FF) {
             issue(v0, r0, i0);
 #ifdef KLE_PROBE_BUILD
-            if (probe_ts && lane == 0) atomicMax(&pmx[2], (unsigned)(__builtin_amdgcn_s_memrealtime() - ts0));
+            if (probe_ts && lane == 0) {
+                atomicMax(&pmx[2], (unsigned)(__builtin_amdgcn_s_memrealtime() - ts0));
+                atomicMax(&pmx[3], (unsigned)ts0);  // (the latest wave's start)
+            }
 #endif
             wait_x12<9 * D>(fv0);
 #ifdef KLE_PROBE_BUILD
@@ -480,6 +486,10 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         dst[t] = fx_to_d(acc[c * RS + k]) * T1 * T2;
     }
     KLE_PROBE_TS_END5(b, ts0, ts1, ts2, ts0 + pmx[0], ts0 + pmx[1], ts0 + pmx[2])
+#ifdef KLE_PROBE_BUILD
+    if (probe_ts && threadIdx.x == 0 && (int64_t)b < probe_cap)  // (the waves' start spread, 10 ns units)
+        probe_ts[8 * (int64_t)b] |= (unsigned long long)(pmx[3] - (unsigned)ts0) << 32;
+#endif
 }
 
 // y[0 .. n) += r: the lower neighbour's sums for this slab's lowest nodes
@@ -624,6 +634,8 @@ int brick_finish(kle_mat *A, void *plan)
     std::unique_ptr<BrickPlan> bp(reinterpret_cast<BrickPlan *>(plan));
     kle_ctx *c = A->ctx;
     const int NB = (int)bp->bricks.size();
+    int rstride = 0;  // rows per brick in the descriptor table (the most of any brick)
+    for (const BrickDesc &D : bp->bricks) rstride = std::max(rstride, D.nr);
     const int64_t n = A->nrows;
     int *dmu = nullptr;
     std::vector<int> hmu(2 * n, 0);  // stored blocks per row | owning brick per row (-1: a one-block row)
@@ -631,7 +643,7 @@ int brick_finish(kle_mat *A, void *plan)
     std::fill(howner, howner + n, -1);
     for (int64_t i : bp->srows) hmu[i] = 1;
     bool nomem = hipMalloc(&A->d_bdesc, sizeof(BrickDesc) * std::max(NB, 1)) != hipSuccess ||
-                 hipMalloc(&A->d_browd, sizeof(int) * bp->rowd.size()) != hipSuccess ||
+                 hipMalloc(&A->d_browd, sizeof(int) * 2 * std::max<int64_t>(1, (int64_t)NB * rstride)) != hipSuccess ||
                  (A->ghost_hi && hipMalloc(&A->d_sgsend, sizeof(double) * A->ghost_hi) != hipSuccess) ||
                  (A->send_lo && hipMalloc(&A->d_sgrecv, sizeof(double) * A->send_lo) != hipSuccess) ||
                  hipMalloc(&A->d_sws, sizeof(double) * std::max<int64_t>(bp->ws_doubles, 1)) != hipSuccess ||
@@ -660,7 +672,17 @@ int brick_finish(kle_mat *A, void *plan)
         }
     }
     KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_browd, bp->rowd.data(), sizeof(int) * bp->rowd.size(), hipMemcpyHostToDevice));
+    {
+        // the row descriptors, brick q's at row q rstride (the kernel's
+        // address needs no load)
+        std::vector<int> pad((size_t)2 * std::max<int64_t>(1, (int64_t)NB * rstride), 0);
+        for (int q = 0; q < NB; ++q)
+            std::copy(bp->rowd.begin() + 2 * (int64_t)bp->bricks[q].rstart,
+                      bp->rowd.begin() + 2 * ((int64_t)bp->bricks[q].rstart + bp->bricks[q].nr),
+                      pad.begin() + 2 * (int64_t)q * rstride);
+        KLE_HIP(hipMemcpy(A->d_browd, pad.data(), sizeof(int) * pad.size(), hipMemcpyHostToDevice));
+    }
+    A->brick_rstride = rstride;
     {
         // the gather's runs (kle_sym.hip gsym_gather, the graph kernels'
         // gather): per 64-row slice of [owned | upper ghost planes] in lattice
@@ -811,9 +833,9 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
         (void)slot;
         dyn_lds(c, reinterpret_cast<const void *>(kern), (size_t)A->brick_lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * wv), (size_t)A->brick_lds, c->stream,
-                           (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, bd,
+                           (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, A->brick_rstride, bd,
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
-                           istate, g_tune.spmv_brick_xcd KLE_PROBE_ARG);
+                           istate KLE_PROBE_ARG);
     };
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
     // N > 1 (z slabs): the x ghost planes first (every brick's region fill

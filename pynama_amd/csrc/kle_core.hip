@@ -765,10 +765,7 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "spmv_brick_singles") {
         KLE_ARG(value == 0 || value == 1, "spmv_brick_singles: 0 or 1");
         g_tune.spmv_brick_singles = value;
-                    } else if (k == "spmv_brick_xcd") {
-        KLE_ARG(value == 0 || value == 1, "spmv_brick_xcd: 0 or 1");
-        g_tune.spmv_brick_xcd = value;
-    } else if (k == "spmv_gather_wps") {
+                        } else if (k == "spmv_gather_wps") {
         KLE_ARG(value == 0 || value == 1 || value == 2 || value == 4, "spmv_gather_wps: 0 (auto), 1, 2 or 4");
         g_tune.spmv_gather_wps = value;
                 } else if (k == "spmv_brick_split") {
@@ -875,7 +872,6 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "spmv_brick_singles") *value = g_tune.spmv_brick_singles;
     else if (k == "spmv_brick_pair") *value = g_tune.spmv_brick_pair;
     else if (k == "spmv_gather_wps") *value = g_tune.spmv_gather_wps;
-    else if (k == "spmv_brick_xcd") *value = g_tune.spmv_brick_xcd;
     else if (k == "spmv_gsym_brick") *value = g_tune.spmv_gsym_brick;
     else if (k == "upd_unroll") *value = g_tune.upd_unroll;
     else if (k == "spmv_sym_early") *value = g_tune.spmv_sym_early;

@@ -62,13 +62,13 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_gsym_brick(const GBrickD
                                                                   const double *__restrict__ sval,
                                                                   const double *__restrict__ x,
                                                                   double *__restrict__ ws, double *__restrict__ y,
-                                                                  const int *__restrict__ istate, int xcd)
+                                                                  const int *__restrict__ istate)
 {
     constexpr int NT = 64 * WV;
     static_assert(D == 1 || D == 2, "one or two items ahead");
     extern __shared__ double lds[];
     const int stop = istate ? istate[I_REASON] : 0;  // (tested before the first store)
-    const int b = brick_of_wg(blockIdx.x, gridDim.x, xcd);
+    const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r0 = bd[b].r0, NR = bd[b].nr, U = bd[b].U, eb = bd[b].eb;
     const long long d0 = bd[b].d0, vbase = bd[b].vbase, sbase = bd[b].sbase, wsoff = bd[b].wsoff;
@@ -379,7 +379,7 @@ int gbrick_launch(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
     hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * BRICK_WV),
                        (size_t)A->brick_lds, c->stream, reinterpret_cast<const GBrickDesc *>(A->d_bdesc),
                        reinterpret_cast<const int4 *>(A->d_browd), A->d_slid, A->d_sdict, A->d_sval, x->base, A->d_sws,
-                       y->d, istate, g_tune.spmv_brick_xcd);
+                       y->d, istate);
     KLE_HIP(hipGetLastError());
     return 0;
 }

@@ -263,7 +263,7 @@ struct kle_mat {
     int sym_gbrick = 0;  // unstructured: graph bricks (d_bdesc = GBrickDesc, d_browd = 4 ints per row)
     int brick_lds_u = 0;  // graph bricks: the largest dictionary
     int gather_rps = 0;  // run-mask gather: runs per 64-row slice (rounded up; picks its waves per slice)
-    int nbricks = 0, brick_lds = 0, brick_gparts = 0;  // (gather workgroups per brick)
+    int nbricks = 0, brick_lds = 0, brick_gparts = 0, brick_rstride = 0;  // (gather workgroups per brick)
     int brick_dims[3] = {0, 0, 0};  // bricks along x, y, z
     double brick_model_us = 0.0;    // the planner's modelled product time
     void *d_bdesc = nullptr;
@@ -430,7 +430,6 @@ struct Tuning {
     int spmv_brick_rounds = 1;  // brick SpMV (read at build): at most this many bricks per CU (2: heaviest-first to the first free CU, 0.467 vs 0.460 ms at config 2, profiles/r05/rounds_ab.jsonl)
     int upd_unroll = 1;        // single-reduction CG update: elements per pass with their loads in flight (1, 2; 2 no faster at config 2, profiles/r05/cg_ab_upd_unroll.jsonl)
     int spmv_gsym_brick = 1;   // unstructured symmetric SpMV (read at build): row bricks (kle_gbrick.hip), 0 the 64-row groups
-    int spmv_brick_xcd = 0;  // box and graph bricks: 1 each XCD streams a contiguous run of bricks (shared region x in its L2), 0 round-robin
     int spmv_gather_wps = 0;   // run-mask gather: waves per 64-row slice (1, 2, 4; 0 auto by the runs per slice)
     int spmv_brick_pair = 1;  // brick SpMV (read at build): rows in units of two whose tails share one 64-lane item
     int spmv_brick_singles = 1;  // brick SpMV (read at build): rows of one stored block formed by the gather, not as 64-lane items of the bricks

@@ -127,16 +127,4 @@ __device__ __forceinline__ void wait_x12(double *v)
                  : "i"(N));
 }
 
-// The brick a workgroup streams (spmv_brick_xcd 1): workgroup i runs on XCD
-// (i + c) mod 8 (round-robin dispatch), so workgroups i = k mod 8 take
-// bricks k q + min(k, r) ... -- each XCD a contiguous run of bricks, whose
-// regions / dictionaries overlap, so one XCD's L2 serves the shared x lines
-// of its region fills.  (A bijection of [0, nb).)
-__device__ __forceinline__ int brick_of_wg(int i, int nb, int xcd)
-{
-    if (!xcd) return i;
-    const int k = i & 7, t = i >> 3, q = nb >> 3, r = nb & 7;
-    return k * q + min(k, r) + t;
-}
-
 }  // namespace kle
