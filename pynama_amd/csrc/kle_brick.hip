@@ -85,6 +85,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     KLE_PROBE_TS(ts0)
 #ifdef KLE_PROBE_BUILD
     __shared__ unsigned pmx[4];
+    if (threadIdx.x == 0) pmx[0] = pmx[1] = pmx[2] = pmx[3] = 0;  // (racy by design: the other waves' maxima come microseconds later)
 #endif
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -118,10 +119,16 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     // of 2^29 / 3 or more ext nodes)
     const int dz = fstep / RY, dy = fstep - dz * RY, sy = 3 * Lx, sz = 3 * Lx * Ly;
     int fz = l0 / RY, fy = l0 - fz * RY, fo = 3 * gx + c + sy * (oy + fy) + sz * (oz + zo + fz);
+    // (the unused loads -- lines past the region, threads past fstep lines:
+    // most of a small brick's 12 per thread -- read the brick's first node,
+    // not x[0]: one line of every brick's fill, not one line of the chip,
+    // which every workgroup's dummies made a hot spot at kernel start)
+    const int fdummy = 3 * (min(max(ox, 0), Lx - 1) + Lx * (min(max(oy, 0), Ly - 1) +
+                                                           Ly * min(max(oz + zo, 0), zo + Lz + hp - 1))) + c;
     auto fnode = [&](int l, bool &ok) -> int {
         const int gy = oy + fy, gz = oz + fz;
         ok = xok & (l < NL) & (gy >= 0) & (gy < Ly) & (gz + zo >= 0) & (gz < Lz + hp);  // (no branches)
-        const int off = ok ? fo : 0;
+        const int off = ok ? fo : fdummy;
         fy += dy;
         fz += dz;
         fo += sy * dy + sz * dz;
@@ -248,10 +255,19 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
         A.ir = 0;
         B = A;
     }
+#ifdef KLE_PROBE_BUILD
+    if (probe_ts) {  // (probe: this wave's first row descriptors are in)
+        asm volatile("" ::"s"(A.mu), "s"(A.k0));
+        if (lane == 0) atomicMax(&pmx[0], (unsigned)(__builtin_amdgcn_s_memrealtime() - ts0));
+    }
+#endif
     // the next unit and its descriptors, fetched one unit ahead
     int pend = idone ? NU : take();
-    int pd0 = rdesc[4 * min(pend, NU - 1)], pd1 = rdesc[4 * min(pend, NU - 1) + 1];
-    int pd2 = rdesc[4 * min(pend, NU - 1) + 2], pd3 = rdesc[4 * min(pend, NU - 1) + 3];
+    // (a brick without rows, NU = 0, reads its slot's first unit: the table
+    // holds at least one unit per brick)
+    const int u0 = max(0, min(pend, NU - 1));
+    int pd0 = rdesc[4 * u0], pd1 = rdesc[4 * u0 + 1];
+    int pd2 = rdesc[4 * u0 + 2], pd3 = rdesc[4 * u0 + 3];
     // the item at the cursor: its loads into vn, its record; the cursor then
     // moves on (past the last unit it stays, re-reading the last item)
     auto issue = [&](double *vn, int &rn, BItem &itn) {
@@ -285,7 +301,7 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
             } else {
                 unit_setup(pend, pd0, pd1, pd2, pd3);
                 pend = take();
-                const int u = min(pend, NU - 1);
+                const int u = max(0, min(pend, NU - 1));
                 pd0 = rdesc[4 * u];
                 pd1 = rdesc[4 * u + 1];
                 pd2 = rdesc[4 * u + 2];
@@ -298,7 +314,6 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     BItem i0, i1;
 #ifdef KLE_PROBE_BUILD
     unsigned long long tsf = 0;
-    if (threadIdx.x == 0) pmx[0] = pmx[1] = pmx[2] = pmx[3] = 0;
 #endif
     // 2b. the first item's value loads, then the fill's first loads landed
     // (vmcnt(9): the value loads stay in flight), into LDS; further lines
@@ -348,7 +363,6 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
 #ifdef KLE_PROBE_BUILD
     // (probe: the latest wave's fill landed and its arrival at the barrier)
     if (probe_ts && lane == 0) {
-        atomicMax(&pmx[0], (unsigned)(tsf - ts0));
         atomicMax(&pmx[1], (unsigned)(__builtin_amdgcn_s_memrealtime() - ts0));
     }
 #endif
@@ -634,8 +648,15 @@ int brick_finish(kle_mat *A, void *plan)
     std::unique_ptr<BrickPlan> bp(reinterpret_cast<BrickPlan *>(plan));
     kle_ctx *c = A->ctx;
     const int NB = (int)bp->bricks.size();
+    // every address the kernel forms from the tables, checked on the host
+    // first (a bad plan is an error, never a launch)
+    {
+        const char *bad = brick_validate(*bp, A->row_lat[0], A->row_lat[1], A->row_lat[2], A->snvals, (int64_t)bp->lds);
+        if (bad) return fail(KLE_ERR_SUP, "brick plan: %s", bad);
+    }
     int rstride = 0;  // rows per brick in the descriptor table (the most of any brick)
     for (const BrickDesc &D : bp->bricks) rstride = std::max(rstride, D.nr);
+    rstride = std::max(2, (rstride + 1) & ~1);  // (whole units of two rows, at least one)
     const int64_t n = A->nrows;
     int *dmu = nullptr;
     std::vector<int> hmu(2 * n, 0);  // stored blocks per row | owning brick per row (-1: a one-block row)
@@ -671,16 +692,22 @@ int brick_finish(kle_mat *A, void *plan)
             }
         }
     }
-    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB));
     {
         // the row descriptors, brick q's at row q rstride (the kernel's
-        // address needs no load)
+        // address needs no load); the rows past a brick's own repeat its
+        // last unit (never read: every read is of a unit < nr / 2)
         std::vector<int> pad((size_t)2 * std::max<int64_t>(1, (int64_t)NB * rstride), 0);
-        for (int q = 0; q < NB; ++q)
-            std::copy(bp->rowd.begin() + 2 * (int64_t)bp->bricks[q].rstart,
-                      bp->rowd.begin() + 2 * ((int64_t)bp->bricks[q].rstart + bp->bricks[q].nr),
-                      pad.begin() + 2 * (int64_t)q * rstride);
-        KLE_HIP(hipMemcpy(A->d_browd, pad.data(), sizeof(int) * pad.size(), hipMemcpyHostToDevice));
+        for (int q = 0; q < NB; ++q) {
+            const BrickDesc &D = bp->bricks[q];
+            int *dst = pad.data() + 2 * (int64_t)q * rstride;
+            std::copy(bp->rowd.begin() + 2 * (int64_t)D.rstart, bp->rowd.begin() + 2 * ((int64_t)D.rstart + D.nr), dst);
+            for (int r = D.nr; r < rstride && D.nr >= 2; ++r) {
+                dst[2 * r] = dst[2 * (D.nr - 2 + (r & 1))];
+                dst[2 * r + 1] = dst[2 * (D.nr - 2 + (r & 1)) + 1];
+            }
+        }
+        KLE_TRY(h2d(A->d_browd, pad.data(), sizeof(int) * pad.size()));
     }
     A->brick_rstride = rstride;
     {
@@ -734,10 +761,9 @@ int brick_finish(kle_mat *A, void *plan)
             if (dmu) (void)hipFree(dmu);
             return fail(KLE_ERR_MEM, "out of device memory for the brick gather runs");
         }
-        KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
-        KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
-        KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(),
-                          hipMemcpyHostToDevice));
+        KLE_TRY(h2d(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1)));
+        KLE_TRY(h2d(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size()));
+        KLE_TRY(h2d(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size()));
         A->brick_gparts = (int)(runptr[ns] / std::max<int64_t>(ns, 1));  // (runs per 64 rows, for the log)
         A->gather_rps = (int)((runptr[ns] + ns - 1) / std::max<int64_t>(ns, 1));
     }
@@ -753,9 +779,9 @@ int brick_finish(kle_mat *A, void *plan)
             if (dmu) (void)hipFree(dmu);
             return fail(KLE_ERR_MEM, "out of device memory for the brick gather's one-block rows");
         }
-        KLE_HIP(hipMemcpy(A->d_ssingle, sm.data(), sizeof(unsigned long long) * nso, hipMemcpyHostToDevice));
+        KLE_TRY(h2d(A->d_ssingle, sm.data(), sizeof(unsigned long long) * nso));
     }
-    KLE_HIP(hipMemcpy(dmu, hmu.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(dmu, hmu.data(), sizeof(int) * 2 * n));
     const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
     const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
     if (NB > 0)  // (every row of one block: no brick at all, the gather forms y)
@@ -770,7 +796,7 @@ int brick_finish(kle_mat *A, void *plan)
     KLE_HIP(hipMemcpy(eb.data(), A->d_stile_e, sizeof(int) * NB, hipMemcpyDeviceToHost));
     (void)hipFree(dmu);
     for (int q = 0; q < NB; ++q) bp->bricks[q].eb = eb[q];
-    KLE_HIP(hipMemcpy(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(A->d_bdesc, bp->bricks.data(), sizeof(BrickDesc) * NB));
     A->nbricks = NB;
     {
         // (bricks along each axis: distinct first coordinates)

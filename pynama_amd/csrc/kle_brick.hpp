@@ -60,6 +60,9 @@ struct BrickPlan {
     std::vector<int64_t> srows;  // (out) those rows, ascending; their values (9 doubles each) after the bricks'
 };
 
+// the plan's tables checked against every address the brick kernel forms
+// from them (kle_brick_plan.cpp); nullptr: consistent, else what is wrong
+const char *brick_validate(const BrickPlan &bp, int64_t Lx, int64_t Ly, int64_t Lz, int64_t nvals, int64_t lds_cap);
 // the LDS a brick of RN region nodes needs (x, the transposed sums and their
 // dummy slots, wave maxima, the row counter)
 inline size_t brick_lds(int RN) { return (size_t)(3 * RN + 3 * (RN + 64)) * 8 + 512; }

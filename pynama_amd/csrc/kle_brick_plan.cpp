@@ -586,6 +586,47 @@ std::string brick_plan(int Lx, int Ly, int Lz, int hp, int ncu, int nfix, int ro
     return "";
 }
 
+// The plan's tables against what k_nb_spmv_sym_brick derives from them:
+// units of two rows (the second may be null), every real row's box, first
+// block k0 < its box's size (mu >= 1 stored blocks), region index inside the
+// brick's region and its lattice node inside the owned lattice, its values
+// [off 16, off 16 + 9 mu) inside the value array, a unit's second row's
+// values after its first's; regions within the LDS.  nullptr: consistent.
+const char *brick_validate(const BrickPlan &bp, int64_t Lx, int64_t Ly, int64_t Lz, int64_t nvals,
+                                  int64_t lds_cap)
+{
+    for (const BrickDesc &D : bp.bricks) {
+        const int64_t RN = (int64_t)D.RX * D.RY * D.RZ;
+        if (D.nr < 2 || D.nr % 2 || RN < 1 || RN > 65535) return "a brick's rows or region";
+        if ((int64_t)brick_lds((int)RN) > std::min<int64_t>(lds_cap, (int64_t)BRICK_LDS_CAP))
+            return "a brick's region exceeds the LDS";
+        if (D.rstart < 0 || 2 * ((int64_t)D.rstart + D.nr) > (int64_t)bp.rowd.size()) return "a brick's rows";
+        int64_t a_v0 = 0;
+        for (int r = 0; r < D.nr; ++r) {
+            const int64_t rr = (int64_t)D.rstart + r;
+            const int dw = bp.rowd[2 * rr], vw = bp.rowd[2 * rr + 1];
+            if (vw & BRICK_ROW_NULL) {
+                if (r % 2 == 0) return "a unit's first row is null";
+                continue;
+            }
+            const int dbx = dw & 15, dby = (dw >> 4) & 15, dbz = (dw >> 8) & 15;
+            const int bnx = (dw >> 12) & 15, bny = (dw >> 16) & 15, bnz = (dw >> 20) & 15;
+            const int k0 = dbx + bnx * (dby + bny * dbz), mu = bnx * bny * bnz - k0;
+            if (dbx >= bnx || dby >= bny || dbz >= bnz || mu < 1) return "a row's box";
+            const int ir = brick_row_ir(bp.rowd.data(), rr);
+            if (ir < 0 || ir >= RN) return "a row's region index";
+            const int irz = ir / (D.RX * D.RY), irem = ir - irz * D.RX * D.RY, iry = irem / D.RX, irx = irem - iry * D.RX;
+            const int64_t gx = D.ox + irx, gy = D.oy + iry, gz = D.oz + irz;
+            if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz < 0 || gz >= Lz) return "a row's lattice node";
+            const int64_t v0 = D.vbase + (int64_t)(vw & (BRICK_ROW_NULL - 1)) * 16, v1 = v0 + 9 * (int64_t)mu;
+            if (v0 < 0 || v1 > nvals) return "a row's values";
+            if (r % 2 == 0) a_v0 = v0;
+            else if (v0 < a_v0 || v0 - a_v0 > ((int64_t)1 << 26)) return "a unit's second row's values";
+        }
+    }
+    return nullptr;
+}
+
 }  // namespace kle
 
 // Diagnostic (host only, no device): the brick plan of an Lx x Ly x Lz box
@@ -724,6 +765,12 @@ extern "C" int kle_brick_plan_box(int Lx, int Ly, int Lz, int p, int dirichlet, 
             }
         stats[4] = (double)items;
         stats[5] = items ? (double)blocks_b / (64.0 * (double)items) : 0.0;
+    }
+    {
+        // (the tables checked as brick_finish checks them on the device path;
+        // the values: the plan's own layout)
+        if (const char *bad = brick_validate(bp, Lx, Ly, Lz, bp.svb[n], (int64_t)bp.lds))
+            return fail(KLE_ERR_SUP, "brick plan: %s", bad);
     }
     if (getenv("KLE_BRICK_DEBUG"))
         for (const BrickDesc &D : bp.bricks) {

@@ -36,6 +36,20 @@ int big_alloc(void **p, size_t bytes)
     return 0;
 }
 
+// A host-to-device copy that has landed when it returns.  hipMemcpy from
+// pageable memory may return once the bytes are in a staging buffer, with
+// the DMA still queued on the null stream -- which the context's
+// non-blocking streams do not wait for, so a kernel launched next could read
+// the destination before the copy ends.  The null stream's synchronisation
+// closes that window (setup paths only; round 6 after a fault that
+// serialised kernels could not reproduce).
+int h2d(void *dst, const void *src, size_t bytes)
+{
+    KLE_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    KLE_HIP(hipStreamSynchronize(nullptr));
+    return 0;
+}
+
 // Dynamic LDS above 64 KB must be declared per kernel (hipFuncSetAttribute);
 // the attribute is per device, so the record of what was declared is keyed
 // by (device, kernel), under a lock (a function-static cache
@@ -449,7 +463,7 @@ static int halo_exchange_plan(kle_ctx *ctx, double *base, int64_t ghost_lo, int6
     const int64_t ns = (int64_t)P.send_idx.size() * bs;
     if (!P.d_send_idx && !P.send_idx.empty()) {
         KLE_HIP(hipMalloc(&P.d_send_idx, sizeof(int32_t) * P.send_idx.size()));
-        KLE_HIP(hipMemcpy(P.d_send_idx, P.send_idx.data(), sizeof(int32_t) * P.send_idx.size(), hipMemcpyHostToDevice));
+        KLE_TRY(h2d(P.d_send_idx, P.send_idx.data(), sizeof(int32_t) * P.send_idx.size()));
     }
     if (P.sbuf_cap < ns) {
         KLE_HIP(hipStreamSynchronize(st));

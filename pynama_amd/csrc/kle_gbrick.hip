@@ -367,7 +367,7 @@ int gbrick_bound(kle_mat *A, double vmax_all)
     std::vector<GBrickDesc> hb(NB);
     KLE_HIP(hipMemcpy(hb.data(), A->d_bdesc, sizeof(GBrickDesc) * NB, hipMemcpyDeviceToHost));
     for (int q = 0; q < NB; ++q) hb[q].eb = eb[q];
-    KLE_HIP(hipMemcpy(A->d_bdesc, hb.data(), sizeof(GBrickDesc) * NB, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(A->d_bdesc, hb.data(), sizeof(GBrickDesc) * NB));
     return 0;
 }
 

@@ -348,6 +348,8 @@ int brick_setup(kle_mat *A, const std::vector<int> &rb, const std::vector<int> &
 int sval_alloc(kle_mat *A, size_t bytes);
 // a streamed array (matrix values): 0, or -1 out of memory
 int big_alloc(void **p, size_t bytes);
+// host -> device, landed on return (hipMemcpy + the null stream's sync)
+int h2d(void *dst, const void *src, size_t bytes);
 // declare `bytes` of dynamic LDS for kernel `kern` on c's device (once per size)
 void dyn_lds(const kle_ctx *c, const void *kern, size_t bytes);
 // (xs: the owned x, for the box bricks' one-block rows -- d_ssingle)

@@ -1764,7 +1764,7 @@ int kle_ksp_set_up(kle_ksp *k)
         KLE_HIP(hipMalloc(&k->d_Vptr, sizeof(double *) * ptrs.size()));
         KLE_HIP(hipMalloc(&k->d_h, sizeof(double) * (k->restart + 2)));
         KLE_HIP(hipMalloc(&k->d_gpart, sizeof(double) * (k->restart + 2) * RED_BLOCKS));
-        KLE_HIP(hipMemcpy(k->d_Vptr, ptrs.data(), sizeof(double *) * ptrs.size(), hipMemcpyHostToDevice));
+        KLE_TRY(h2d(k->d_Vptr, ptrs.data(), sizeof(double *) * ptrs.size()));
     }
     KLE_HIP(hipStreamSynchronize(k->ctx->stream));
     k->setup = true;

@@ -623,9 +623,9 @@ int nb_build_dict(kle_mat *A)
         hipMalloc(&A->d_dict, sizeof(int) * dict.size()) != hipSuccess ||
         hipMalloc(&A->d_lid, sizeof(uint16_t) * lid.size()) != hipSuccess)
         return fail(KLE_ERR_MEM, "out of device memory for column dictionaries");
-    KLE_HIP(hipMemcpy(A->d_dptr, dptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_dict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_lid, lid.data(), sizeof(uint16_t) * lid.size(), hipMemcpyHostToDevice));
+    KLE_TRY(h2d(A->d_dptr, dptr.data(), sizeof(int) * (ng + 1)));
+    KLE_TRY(h2d(A->d_dict, dict.data(), sizeof(int) * dict.size()));
+    KLE_TRY(h2d(A->d_lid, lid.data(), sizeof(uint16_t) * lid.size()));
     return 0;
 }
 
@@ -1050,7 +1050,7 @@ int kle_mat_assemble(kle_mat *A)
         return aij_upload(A);
     }
     if (A->dirty) {
-        KLE_HIP(hipMemcpy(A->d_aval, A->h_val.data(), sizeof(double) * A->nnz, hipMemcpyHostToDevice));
+        KLE_TRY(h2d(A->d_aval, A->h_val.data(), sizeof(double) * A->nnz));
         A->dirty = false;
     }
     return 0;
@@ -1386,7 +1386,7 @@ int kle_mat_axpy(kle_mat *Y, double a, const kle_mat *X)
             auto it = std::lower_bound(b, e, X->h_col[k]);
             Y->h_val[it - Y->h_col.begin()] += a * xv[k];
         }
-    KLE_HIP(hipMemcpy(Y->d_aval, Y->h_val.data(), sizeof(double) * Y->nnz, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(Y->d_aval, Y->h_val.data(), sizeof(double) * Y->nnz));
     return 0;
 }
 

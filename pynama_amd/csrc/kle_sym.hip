@@ -1473,22 +1473,21 @@ static int gsym_build(kle_mat *A)
     }
     if (any) return done(fail(KLE_ERR_MEM, "out of device memory for symmetric storage"));
     A->sym_graph = 1;
-    KLE_HIP(hipMemcpy(A->d_svptr, svp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_srow, smu.data(), sizeof(int) * n, hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_sbp, sbp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_slid, slid.data(), sizeof(uint16_t) * slid.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_sdptr, dptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_sdict, dict.data(), sizeof(int) * dict.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_swptr, wptr.data(), sizeof(int) * (ng + 1), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_sglist, glist.data(), sizeof(int) * ng, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(A->d_svptr, svp.data(), sizeof(int64_t) * (n + 1)));
+    KLE_TRY(h2d(A->d_srow, smu.data(), sizeof(int) * n));
+    KLE_TRY(h2d(A->d_sbp, sbp.data(), sizeof(int64_t) * (n + 1)));
+    KLE_TRY(h2d(A->d_slid, slid.data(), sizeof(uint16_t) * slid.size()));
+    KLE_TRY(h2d(A->d_sdptr, dptr.data(), sizeof(int) * (ng + 1)));
+    KLE_TRY(h2d(A->d_sdict, dict.data(), sizeof(int) * dict.size()));
+    KLE_TRY(h2d(A->d_swptr, wptr.data(), sizeof(int) * (ng + 1)));
+    KLE_TRY(h2d(A->d_sglist, glist.data(), sizeof(int) * ng));
     A->gather_rps = (int)((runptr[ns] + ns - 1) / std::max<int64_t>(ns, 1));
-    KLE_HIP(hipMemcpy(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size(), hipMemcpyHostToDevice));
-    KLE_HIP(hipMemcpy(dk0, k0.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    KLE_TRY(h2d(A->d_sgptr, runptr.data(), sizeof(int) * (ns + 1)));
+    KLE_TRY(h2d(A->d_sgidx, rstart.data(), sizeof(int) * rstart.size()));
+    KLE_TRY(h2d(A->d_sgmask, rmask.data(), sizeof(unsigned long long) * rmask.size()));
+    KLE_TRY(h2d(dk0, k0.data(), sizeof(int) * n));
     if (graph && !A->plan->send_idx.empty())
-        KLE_HIP(hipMemcpy(A->plan->d_send_idx, A->plan->send_idx.data(), sizeof(int32_t) * A->plan->send_idx.size(),
-                          hipMemcpyHostToDevice));
+        KLE_TRY(h2d(A->plan->d_send_idx, A->plan->send_idx.data(), sizeof(int32_t) * A->plan->send_idx.size()));
     hipLaunchKernelGGL(k_gsym_check, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, glo, A->d_rowptr,
                        A->d_rowcnt, A->d_vptr, A->d_bcol, A->d_val, dk0, A->d_svptr, A->d_sval, rowdiff, rowmax);
     KLE_HIP(hipGetLastError());
@@ -1555,15 +1554,15 @@ static int gsym_build(kle_mat *A)
             (void)hipGetLastError();
             return done(fail(KLE_ERR_MEM, "out of device memory for the graph bricks"));
         }
-        KLE_HIP(hipMemcpy(A->d_bdesc, hb.data(), sizeof(GBrickDesc) * ng, hipMemcpyHostToDevice));
-        KLE_HIP(hipMemcpy(A->d_browd, rowd.data(), sizeof(int) * rowd.size(), hipMemcpyHostToDevice));
+        KLE_TRY(h2d(A->d_bdesc, hb.data(), sizeof(GBrickDesc) * ng));
+        KLE_TRY(h2d(A->d_browd, rowd.data(), sizeof(int) * rowd.size()));
         if (g_tune.spmv_brick_singles) {
             if (hipMalloc(&A->d_ssingle, sizeof(unsigned long long) * ssm.size()) != hipSuccess) {
                 (void)hipGetLastError();
                 A->d_ssingle = nullptr;
                 return done(fail(KLE_ERR_MEM, "out of device memory for the graph bricks' one-block rows"));
             }
-            KLE_HIP(hipMemcpy(A->d_ssingle, ssm.data(), sizeof(unsigned long long) * ssm.size(), hipMemcpyHostToDevice));
+            KLE_TRY(h2d(A->d_ssingle, ssm.data(), sizeof(unsigned long long) * ssm.size()));
         }
         A->nbricks = (int)ng;
         A->brick_lds_u = US;
@@ -2075,8 +2074,8 @@ static int sym_build_impl(kle_mat *A)
         nomem = 1;
     double dmax = 0.0, vmax = 0.0;
     if (!nomem) {
-        KLE_HIP(hipMemcpy(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-        KLE_HIP(hipMemcpy(A->d_srow, srow.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+        KLE_TRY(h2d(A->d_svptr, sv.data(), sizeof(int64_t) * (n + 1)));
+        KLE_TRY(h2d(A->d_srow, srow.data(), sizeof(int) * n));
         hipLaunchKernelGGL(k_sym_build, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, c->stream, n, (int)Lx, (int)Ly,
                            (int)zo, A->d_rowptr, A->d_rowcnt, A->d_rowbox, A->d_vptr, A->d_val, A->d_svptr, A->d_sval,
                            rowdiff, rowmax);

@@ -116,7 +116,7 @@ def main():
         if (r[:, 7] != 0).any():  # (the brick kernel: the latest wave's fill landed, its barrier arrival)
             fi = (r[:, 7] & 0xFFFFFFFF).astype(np.int64) / 100.0
             fl = (r[:, 7] >> 32).astype(np.int64) / 100.0
-            extra = {"fill_landed_max_wave_us": pct(fi), "barrier_arrival_max_wave_us": pct(fl)}
+            extra = {"descriptors_in_max_wave_us": pct(fi), "barrier_arrival_max_wave_us": pct(fl)}
             if (r[:, 0] >> 32).any():  # (the latest wave's start after wave 0's)
                 extra["wave_start_spread_us"] = pct((r[:, 0] >> 32).astype(np.int64) / 100.0)
             if (r[:, 5] >> 32).any():  # (the latest wave's first item issued: its row descriptors in)
