@@ -62,7 +62,7 @@ for spec in "$@"; do
       step $name 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
       tail -n 3 "gpurun_out/$name.log" > "$OUT/${n}_smoke.txt" ;;
     suite)
-      step $name 1500 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread || exit 1
+      step $name 1500 python -u -m pytest tests -m gpu -x -v --durations=80 --timeout 240 --timeout-method thread || exit 1
       grep -E "passed|failed|PASSED|FAILED|ERROR" "gpurun_out/$name.log" > "$OUT/${n}_suite.txt"
       step ${name}_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     *)
