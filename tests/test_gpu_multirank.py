@@ -218,7 +218,26 @@ def test_ipc_transport_with_slot_sentinel(size, nelem, ngl, ksp_type, sym):
         np.testing.assert_array_equal(a["y"], b["y"])
 
 
+# Checked runs by configuration and knob environment: a test that compares a
+# transport with the host transport's result of an identical run (same ranks,
+# mesh, solver, knobs) reuses the run an earlier test already made and checked.
+_RUNS = {}
+_ENV_KNOBS = ("KLE_TUNING", "KLE_SPMV_SYM_BRICK", "KLE_SPMV_SYM_TILE64", "KLE_SPMV_GSYM_BRICK",
+              "KLE_EVENT_NO_SYSTEM_FENCE", "KLE_KSP_REFINE")
+
+
+def _run_key(*args):
+    return repr(args) + repr([os.environ.get(k) for k in _ENV_KNOBS])
+
+
 def _check_box(size, nelem, ngl, overlap, ksp_type, waves=0, sym=False, transport="host", its_extra=0):
+    key = _run_key("box", size, nelem, ngl, overlap, ksp_type, waves, sym, transport)
+    if key not in _RUNS or _RUNS[key][0] > its_extra:  # (a run checked with a looser count bound is redone)
+        _RUNS[key] = its_extra, _check_box_run(size, nelem, ngl, overlap, ksp_type, waves, sym, transport, its_extra)
+    return _RUNS[key][1]
+
+
+def _check_box_run(size, nelem, ngl, overlap, ksp_type, waves, sym, transport, its_extra):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     import pynama_amd as pa
@@ -334,7 +353,7 @@ def test_partitioned_umesh_solve_matches_serial(size, partitioner, nel, ksp_type
 
 @pytest.mark.parametrize("size,partitioner,nel,ksp_type", [
     (2, "slab", [2, 3, 9], "cg"), (3, "slab", [2, 3, 9], "pipecg"), (2, "inertial", [3, 3, 4], "cg"),
-    (3, "inertial", [3, 4, 4], "cg"), (4, "inertial", [4, 4, 4], "pipecg"), (8, "inertial", [4, 4, 6], "cg")])
+    (3, "inertial", [3, 4, 4], "pipecg"), (4, "inertial", [4, 4, 4], "cg"), (8, "inertial", [4, 4, 6], "pipecg")])
 def test_partitioned_umesh_symmetric_storage(size, partitioner, nel, ksp_type, tmp_path):
     """Graph symmetric storage on every rank of an unstructured partition
     (config 5's path): each rank keeps its rows' blocks from the diagonal on
@@ -592,6 +611,13 @@ def test_pipecg_correction_is_default_and_optional(tmp_path):
 
 
 def _check_umesh(size, partitioner, nel, ksp_type, waves, tmp_path, sym=False, transport="host"):
+    key = _run_key("umesh", size, partitioner, nel, ksp_type, waves, sym, transport)  # (the mesh: seed 31)
+    if key not in _RUNS:
+        _RUNS[key] = _check_umesh_run(size, partitioner, nel, ksp_type, waves, tmp_path, sym, transport)
+    return _RUNS[key]
+
+
+def _check_umesh_run(size, partitioner, nel, ksp_type, waves, tmp_path, sym, transport):
     from oracle import oracle as O
     import pynama_amd as pa
     from pynama_amd.meshgen import perturbed_box, write_gmsh
