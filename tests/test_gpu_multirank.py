@@ -91,8 +91,9 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap,ksp_type", [(True, "cg"), (False, "cg"), (True, "pipecg")])
-@pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 4), (3, [2, 3, 3], 3)])
+@pytest.mark.parametrize("size,nelem,ngl,overlap,ksp_type", [
+    (2, [3, 2, 4], 4, True, "cg"), (2, [3, 2, 4], 4, False, "cg"), (3, [2, 3, 3], 3, False, "cg"),
+    (3, [2, 3, 3], 3, True, "pipecg")])
 def test_partitioned_solve_matches_serial(size, nelem, ngl, overlap, ksp_type):
     _check_box(size, nelem, ngl, overlap, ksp_type)
 
@@ -116,8 +117,7 @@ def test_eight_slab_solve_matches_serial(ksp_type):
     _check_box(8, [2, 2, 8], 4, True, ksp_type)
 
 
-@pytest.mark.parametrize("ksp_type", ["cg", "pipecg"])
-@pytest.mark.parametrize("size,nelem,ngl", [(2, [3, 2, 4], 5), (3, [4, 3, 6], 4)])
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(2, [3, 2, 4], 5, "cg"), (3, [4, 3, 6], 4, "pipecg")])
 def test_partitioned_solve_x_in_lds(size, nelem, ngl, ksp_type):
     """8 waves per SpMV workgroup forced at small size, so every rank runs the
     x-in-LDS SpMV (k_nb_spmv_xl) on its split row ranges (interior rows, then
@@ -142,8 +142,7 @@ def test_partitioned_solve_symmetric_storage(size, nelem, ngl, ksp_type, overlap
         assert r["kernel"].startswith("k_nb_spmv_sym_brick<"), r["kernel"]
 
 
-@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(2, [3, 2, 4], 4, "pipecg"), (3, [2, 3, 3], 3, "cg"),
-                                                    (8, [2, 2, 8], 4, "pipecg")])
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(3, [2, 3, 3], 3, "cg"), (8, [2, 2, 8], 4, "pipecg")])
 def test_partitioned_symmetric_storage_tiles(size, nelem, ngl, ksp_type):
     """The tile kernel on slabs (KLE_SPMV_SYM_BRICK=0; the bricks are the
     default at every N): same checks."""
@@ -156,7 +155,7 @@ def test_partitioned_symmetric_storage_tiles(size, nelem, ngl, ksp_type):
         assert r["kernel"].startswith("k_nb_spmv_sym_xl<"), r["kernel"]
 
 
-@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(2, [3, 2, 4], 5, "cg"), (3, [2, 3, 3], 3, "pipecg")])
+@pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(3, [2, 3, 3], 3, "pipecg")])
 def test_partitioned_symmetric_storage_128_row_tiles(size, nelem, ngl, ksp_type):
     """The 128-row tiles (8 x 4 x 4) on slabs: test-size parts take the 64-row
     tiles by default (spmv_sym_tile64_max), so KLE_SPMV_SYM_TILE64=2 forces the
