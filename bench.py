@@ -367,7 +367,8 @@ def main():
         K.mult(xs, ys)
     pc_, pms = ctx.kernel_stats("spmv")
     ctx.set_profiling(False)
-    spmv_plain = {"reps": pc_, "avg_ms": pms / max(pc_, 1), "bytes": spmv_bytes_local,
+    spmv_plain = {"kernel": spmv_kernel(K, args.layout, args.ngl), "reps": pc_, "avg_ms": pms / max(pc_, 1),
+                  "bytes": spmv_bytes_local,
                   "gbps": spmv_bytes_local / (pms / max(pc_, 1) * 1e-3) / 1e9,
                   "x": "uniform[-1,1) from splitmix64(0x5EED), global index order"}
 
@@ -391,7 +392,9 @@ def main():
                "gbps": ab / (ms / c * 1e-3) / 1e9, "frac": ab / (ms / c * 1e-3) / 1e9 / HBM_PEAK_GBS}
         del A
 
-    kname = spmv_kernel(K, args.layout, args.ngl)
+    # the kernel(s) the timed products ran (the bricks alone where the CG
+    # update gathers the split product itself); the plain leg's is K's own
+    kname = kb.getProductKernel() or spmv_kernel(K, args.layout, args.ngl)
     tkey = (f"{nelem}-{args.ngl}-{nranks}-" + ("umesh-" if mesh_kind != "box" else "") +
             ("chunk" if args.layout == 1 else f"pad{args.pad}") +
             "-nt-u1" + ("-struct" if K.isStructured() else "") +

@@ -471,6 +471,10 @@ int kle_ksp_set_operators(kle_ksp *k, kle_mat *A);
 int kle_ksp_set_up(kle_ksp *k);
 int kle_ksp_solve(kle_ksp *k, kle_vec *b, kle_vec *x);
 int kle_ksp_get_iteration_number(const kle_ksp *k, int *its);
+/* Kernel name(s) of the products inside the last solve call, as rocprof lists
+ * them: kle_mat_spmv_kernel's, or -- where the CG update gathers a split
+ * box-brick product itself -- the brick kernel alone (one rank). */
+int kle_ksp_get_product_kernel(const kle_ksp *k, char *buf, int buflen);
 int kle_ksp_get_residual_norm(const kle_ksp *k, double *rnorm);
 int kle_ksp_get_converged_reason(const kle_ksp *k, int *reason);
 /* ||b - A x|| / ||b|| recomputed after the last solve. */

@@ -69,13 +69,19 @@ constexpr int BI_NEWP = 1024;  // (sf: the item starts row P -- its x into the r
 // which holds only while the compiler does not copy them on the way there
 // (checked in the ISA; a variant with two items in flight ahead of the summed
 // one -- no faster, round 5 -- had them moved, wrong products, and is gone)
-template <int WV, bool FF = true>
+// DOT (one rank, a split product whose gather the CG update does): the
+// brick's share of (A x, x) in dpart[brick] -- its rows' direct sums and its
+// region's transposed sums, each times the x it is added at (the gather adds
+// every one of them to exactly one entry of A x), so the update's prologue
+// has (A x, x) before any row is gathered (kle_ksp.hip k_sr_iter_g)
+template <int WV, bool FF = true, bool DOT = false>
 __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly, int Lz, int zo, int hp, int rstride,
                                                                  const BrickDesc *__restrict__ bd,
                                                                  const int2 *__restrict__ rowd,
                                                                  const double *__restrict__ sval,
                                                                  const double *__restrict__ x,
                                                                  double *__restrict__ ws, double *__restrict__ y,
+                                                                 double *__restrict__ dpart,
                                                                  const int *__restrict__ istate KLE_PROBE_PARAM)
 {
     KLE_PROBE_CONST
@@ -402,13 +408,18 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     // the issue cursor.  Past the brick's last unit the issue cursor re-reads
     // its last item under a record r = -1, so every step issues 9 loads and
     // the wait for the summed item is a fixed vmcnt(9 D).
+    double dr = 0.0;  // DOT: this lane's share of its rows' (direct sum, x)
     if (i0.ok) {
         double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
         double cx0 = 0.0, cx1 = 0.0, cx2 = 0.0;  // x of the current row, kept across its items
         // the row's direct sum (fixed-order DPP, fp64), one writer, into y --
         // the gather adds the bricks' transposed sums to it (8 MB of stores
         // at config 2: the only ones before the end)
-        auto row_out = [&](int ir, double a0, double a1, double a2) {
+        // DOT: each lane's part of the row's sum times the row's x, c (the
+        // lanes of other rows hold 0 of this row's sum), before the lanes'
+        // sum -- all in VGPRs (SGPRs are the kernel's scarce registers)
+        auto row_out = [&](int ir, double a0, double a1, double a2, double xr0, double xr1, double xr2) {
+            if constexpr (DOT) dr += (a0 * xr0 + a1 * xr1) + a2 * xr2;
             wsum3_dpp(a0, a1, a2);
             // (the row's lattice node from its region index: bricks may be
             // ragged, kle_brick_plan.cpp)
@@ -468,14 +479,14 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
             acc1 += mine ? s1 : 0.0;
             acc2 += mine ? s2 : 0.0;
             if (it.sf & 256) {
-                row_out(irP, acc0, acc1, acc2);
+                row_out(irP, acc0, acc1, acc2, c0, c1, c2);
                 // (Q's lanes start Q's sum)
                 const bool qs = live && q;
                 acc0 = qs ? s0 : 0.0;
                 acc1 = qs ? s1 : 0.0;
                 acc2 = qs ? s2 : 0.0;
                 if (it.sf & 512) {
-                    row_out(irQ, acc0, acc1, acc2);
+                    row_out(irQ, acc0, acc1, acc2, c0, c1, c2);
                     acc0 = acc1 = acc2 = 0.0;
                 }
             }
@@ -492,12 +503,29 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     // 4. the region's transposed sums, once, [entry][3] (coalesced; nodes
     // off the lattice are never read)
     double *dst = ws + wsoff;
+    double ds = 0.0;  // DOT: this thread's (region sum, x)
     for (int t = threadIdx.x; t < 3 * RN; t += NT) {
         const int k = t / 3, c = t - 3 * k;
         const int rz = k / (RX * RY), rem = k - rz * RX * RY, ry = rem / RX, rx = rem - ry * RX;
         const int gx = ox + rx, gy = oy + ry, gz = oz + rz;
         if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
-        dst[t] = fx_to_d(acc[c * RS + k]) * T1 * T2;
+        const double v = fx_to_d(acc[c * RS + k]) * T1 * T2;
+        dst[t] = v;
+        if constexpr (DOT) ds += v * xl[c * RN + k];
+    }
+    if constexpr (DOT) {
+        // fixed order: lanes (xor tree), then waves in order
+        double s = ds + dr;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) wred[w] = s;  // (wred's scale inputs were read before the item loop)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+#pragma unroll
+            for (int q = 0; q < WV; ++q) t += wred[q];
+            dpart[b] = t;
+        }
     }
     KLE_PROBE_TS_END5(b, ts0, ts1, ts2, ts0 + pmx[0], ts0 + pmx[1], ts0 + pmx[2])
 #ifdef KLE_PROBE_BUILD
@@ -861,7 +889,7 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
         hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * wv), (size_t)A->brick_lds, c->stream,
                            (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, A->brick_rstride, bd,
                            reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
-                           istate KLE_PROBE_ARG);
+                           dpart, istate KLE_PROBE_ARG);
     };
     const bool dist = c->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
     // N > 1 (z slabs): the x ghost planes first (every brick's region fill
@@ -876,7 +904,9 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     if (A->nbricks == 0) {
         // (no brick: every row of one block, formed by the gather)
     } else {
-        go(k_nb_spmv_sym_brick<BRICK_WV>, 0, BRICK_WV);
+        // (a split product's (A x, x): the bricks' shares, DOT; else the gather's)
+        if (split && dpart && !dist) go(k_nb_spmv_sym_brick<BRICK_WV, true, true>, 0, BRICK_WV);
+        else go(k_nb_spmv_sym_brick<BRICK_WV, true, false>, 0, BRICK_WV);
     }
     KLE_HIP(hipGetLastError());
     // the gather (kle_sym.hip gsym_gather): per row its direct sum in y, then

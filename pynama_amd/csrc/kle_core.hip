@@ -800,6 +800,9 @@ int kle_set_tuning(const char *key, int value)
     } else if (k == "ksp_pipe_gather") {
         KLE_ARG(value == 0 || value == 1, "ksp_pipe_gather: 0 or 1");
         g_tune.ksp_pipe_gather = value;
+    } else if (k == "ksp_sr_gather") {
+        KLE_ARG(value >= 0 && value <= 2, "ksp_sr_gather: 0, 1 or 2");
+        g_tune.ksp_sr_gather = value;
     } else if (k == "ipc_sentinel") {
         KLE_ARG(value == 0 || value == 1, "ipc_sentinel: 0 or 1");
         g_tune.ipc_sentinel = value;
@@ -904,6 +907,7 @@ int kle_get_tuning(const char *key, int *value)
     else if (k == "ksp_corr_fault") *value = g_tune.ksp_corr_fault;
     else if (k == "ipc_sentinel") *value = g_tune.ipc_sentinel;
     else if (k == "ksp_pipe_gather") *value = g_tune.ksp_pipe_gather;
+    else if (k == "ksp_sr_gather") *value = g_tune.ksp_sr_gather;
     else if (k == "spmv_gsym_split") *value = g_tune.spmv_gsym_split;
     else if (k == "spmv_gsym_waves") *value = g_tune.spmv_gsym_waves;
     else if (k == "spmv_sym_min_rows") *value = g_tune.spmv_sym_min_rows;

@@ -327,7 +327,8 @@ int spmv_dot_parts(const kle_mat *A);  // what spmv_dot would write (0: none)
 // true when spmv(A, x, ...) exchanges the halo on ctx->comm_stream
 bool spmv_uses_comm_stream(const kle_mat *A, const kle_vec *x);
 bool spmv_can_split(const kle_mat *A);
-int spmv_split(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate);
+int spmv_split(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate,
+               double *dpart = nullptr);  // dpart (one rank): the bricks' (y, x) partials, A->nbricks of them
 int reduce_partials(kle_ctx *ctx, const double *partials, int nparts, int nq, double *out);
 int grid_for(int64_t work, int per_block, int max_blocks);
 unsigned sync_event_flags();  // kle_core.hip
@@ -404,6 +405,7 @@ struct Tuning {
     int spmv_waves = 0;  // rows per SpMV workgroup for 3x3 chunked matrices: 0 auto (8 from 64k rows, else 4), 4, 8
     int spmv_xcd_chunk = 16;  // SpMV: consecutive row blocks per XCD in each run (0: round-robin), xcd_block()
     int spmv_dyn_lds = -1;  // unused dynamic LDS per SpMV workgroup (bytes), caps SpMV workgroups per CU; -1 auto
+    int ksp_sr_gather = 1;  // single-reduction CG on box bricks, one rank: the same fold (k_sr_iter_g; (A u, u) from the bricks) from 2^17 node rows (1), always (2), never (0)
     int ksp_pipe_gather = 1;  // pipelined CG on box bricks: the product's owned-row gather folded into the next update (k_pipe_iter_g); 0 separate
     int ipc_sentinel = 0;  // IPC transport (debug): consumed mailbox slots overwritten with NaN before the ack (a stale or early slot read shows as NaN)
     int ksp_corr_fault = 0;  // test hook: 1 = refine() runs its correction solves even when the true residual meets rtol, and each ends in NaN (DIVERGED_NANORINF) -- x must stay as it was

@@ -735,6 +735,125 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
     block_sums<2>(acc, pu_out, G);
 }
 
+// k_sr_iter with the gather of a split box-brick product w = A u folded in
+// (one rank; VERDICT r05 item 1a, as k_pipe_iter_g): the product left its
+// bricks' region sums in ws, the rows' direct sums in w and the bricks'
+// shares of (w, u) in the partials after this launch's (k_nb_spmv_sym_brick
+// DOT), so the prologue has the whole (w, u) before any row is gathered.  A
+// wave takes one 64-row slice: it sums the slice's runs (the run-mask
+// gather's order: runs, then the direct sum or a one-block row's B_ii u_i)
+// into LDS and updates the slice's 192 entries from there; w is neither
+// written nor read back.  The one-block rows' share of the NEXT product's
+// (w, u), (B_ii u_i, u_i), is formed here from the new u (those rows are no
+// brick's): partials [3][G] = (r,u) | (r,r) | that share, the bricks' after
+// them (G2 = G + bricks in all).  Without pro (the first update of a call)
+// w is complete and read as it is.
+template <bool JAC>
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_iter_g(BrickGather gs, int64_t n,
+                                                  const double *__restrict__ dinv, const double *__restrict__ w,
+                                                  double *__restrict__ u, double *__restrict__ p,
+                                                  double *__restrict__ sv, double *__restrict__ x,
+                                                  double *__restrict__ r, const double *__restrict__ pu_in, int G2,
+                                                  double *__restrict__ pu_out, double *__restrict__ scal,
+                                                  int *__restrict__ ist, int pro, int par, double atol)
+{
+    constexpr int WPB = KB / 64;
+    __shared__ double nl[WPB][192];
+    const int G = (int)gridDim.x;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nsl = (gs.nrows + 63) / 64, sst = (int64_t)G * WPB;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // w of one slice into nl[wv] (entries 3 j .. 3 j + 2 of its row j)
+    auto gather = [&](int64_t sl) {
+        const int64_t j = sl * 64 + lane;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        if (sl * 64 < gs.ng) {
+            const int rb = gs.runptr[sl], re = gs.runptr[sl + 1];
+            const bool one = j < gs.nrows && gs.single && ((gs.single[sl] >> lane) & 1ull);
+            double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+            if (j < gs.nrows) {
+                if (one) {
+                    const double *v = gs.sval + gs.svptr[j];
+                    const double x0 = gs.xs[3 * j], x1 = gs.xs[3 * j + 1], x2 = gs.xs[3 * j + 2];
+                    d0 = v[0] * x0 + v[1] * x1 + v[2] * x2;
+                    d1 = v[3] * x0 + v[4] * x1 + v[5] * x2;
+                    d2 = v[6] * x0 + v[7] * x1 + v[8] * x2;
+                } else {
+                    d0 = w[3 * j];
+                    d1 = w[3 * j + 1];
+                    d2 = w[3 * j + 2];
+                }
+            }
+#pragma unroll 8
+            for (int rr = rb; rr < re; ++rr) {
+                const unsigned long long mk = gs.rmask[rr];
+                const bool in = (mk >> lane) & 1ull;
+                const double *pw = gs.ws + (int64_t)gs.rstart[rr] + (in ? 3 * __popcll(mk & below) : 0);
+                const double a0 = pw[0], a1 = pw[1], a2 = pw[2];
+                s0 += in ? a0 : 0.0;
+                s1 += in ? a1 : 0.0;
+                s2 += in ? a2 : 0.0;
+            }
+            s0 += d0;
+            s1 += d1;
+            s2 += d2;
+        } else if (j < gs.nrows) {
+            s0 = w[3 * j];
+            s1 = w[3 * j + 1];
+            s2 = w[3 * j + 2];
+        }
+        nl[wv][3 * lane] = s0;
+        nl[wv][3 * lane + 1] = s1;
+        nl[wv][3 * lane + 2] = s2;
+        __builtin_amdgcn_wave_barrier();
+    };
+    int64_t sl = (int64_t)blockIdx.x * WPB + wv;
+    // the first slice's gather before the prologue (it needs no scalar)
+    StageIn in;
+    if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
+    if (sl < nsl) gather(sl);
+    if (ist[I_REASON] != 0) return;
+    double t[3] = {0.0, 0.0, 0.0};
+    if (pro) sums3(pu_in, pu_in + G, G, pu_in + 2 * G, G2, t);
+    double alpha, beta;
+    if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta, &in)) return;
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (; sl < nsl; sl += sst) {
+        if (sl != (int64_t)blockIdx.x * WPB + wv) gather(sl);
+#pragma unroll
+        for (int ps = 0; ps < 3; ++ps) {
+            const int el = ps * 64 + lane;
+            const int64_t i = sl * 192 + el;
+            if (i >= n) break;
+            const double wi = nl[wv][el];
+            const double pi = u[i] + beta * p[i];
+            const double si = wi + beta * sv[i];
+            p[i] = pi;
+            sv[i] = si;
+            x[i] = x[i] + alpha * pi;
+            const double ri = r[i] - alpha * si;
+            r[i] = ri;
+            const double ui = JAC ? dinv[i] * ri : ri;
+            u[i] = ui;
+            nl[wv][el] = ui;  // (this lane's own entry: read above, by this lane only)
+            acc[0] += ri * ui;
+            acc[1] += ri * ri;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int64_t j = sl * 64 + lane;
+        if (gs.single && j < gs.nrows && ((gs.single[sl] >> lane) & 1ull)) {
+            const double *v = gs.sval + gs.svptr[j];
+            const double x0 = nl[wv][3 * lane], x1 = nl[wv][3 * lane + 1], x2 = nl[wv][3 * lane + 2];
+            const double d0 = v[0] * x0 + v[1] * x1 + v[2] * x2;
+            const double d1 = v[3] * x0 + v[4] * x1 + v[5] * x2;
+            const double d2 = v[6] * x0 + v[7] * x1 + v[8] * x2;
+            acc[2] += (d0 * x0 + d1 * x1) + d2 * x2;
+        }
+        __builtin_amdgcn_wave_barrier();  // (nl[wv] read before the next slice's gather writes it)
+    }
+    block_sums<3>(acc, pu_out, G);
+}
+
 // (w, u) per workgroup after the SpMV (no last-arriver: the next update's
 // prologue sums the partials); FIN_UNR independent load pairs per thread.
 __global__ __launch_bounds__(KB) void k_dot_part(int64_t n, const double *__restrict__ vx,
@@ -945,6 +1064,7 @@ struct kle_ksp {
     double rtol = 1e-5, atol = 1e-50, dtol = 1e5;
     int maxit = 10000, restart = 30, fixed = 0, check_every = 8;
     int pipe_par = 0;  // pipelined CG: parity of the next update launch (k_pipe_iter)
+    std::string prod_kernel;  // the kernel(s) of the last call's products (kle_ksp_get_product_kernel)
     kle_mat *A = nullptr;
     kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
     kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
@@ -1176,6 +1296,27 @@ static int solve_cg(kle_ksp *k, kle_vec *b, kle_vec *x)
     return 0;
 }
 
+// The kernel names a solve's products launch, as rocprof lists them: the
+// matrix's own (kle_mat_spmv_kernel), or a split product's -- the bricks
+// (with their (y, x) shares: dot) and, on a slab partition, the ghost
+// slices' gather
+static std::string mat_kernel_name(const kle_mat *A)
+{
+    char buf[160];
+    if (kle_mat_spmv_kernel(A, buf, sizeof buf)) return "?";
+    return buf;
+}
+static std::string split_kernel_name(const kle_mat *A, bool dot)
+{
+    const std::string m = mat_kernel_name(A);
+    const bool dist = A->ctx->nranks > 1 && (A->lo_rank >= 0 || A->hi_rank >= 0);
+    if (dist) return m;
+    const size_t plus = m.find('+');
+    std::string b = plus == std::string::npos ? m : m.substr(0, plus);
+    if (dot) b.replace(b.rfind("false>"), 6, "true>");
+    return b;
+}
+
 // Chronopoulos-Gear CG (PETSc -ksp_cg_single_reduction): one fused update
 // kernel + one SpMV (with fused (w,u)) + one reduction (three sums) per
 // iteration -> one allreduce per iteration across ranks.
@@ -1220,6 +1361,19 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     // (spmv_dot), one launch less per iteration
     const int Gf = c->nranks == 1 && !c->comm ? spmv_dot_parts(k->A) : 0;
     if (Gf > 0 && 2 * Gu + Gf <= PART_STRIDE / 2) Gd = Gf;
+    // one rank on box bricks: the product's gather folded into the next
+    // update (k_sr_iter_g), whose prologue sums (w, u) from the one-block
+    // rows' share (the previous update's) and the bricks' (the product's);
+    // npend: w awaits that gather
+    // From 2^17 node rows (1, default): config 2 (342k rows) 425.3 -> 422.2 us
+    // per iteration, the 1/8 slab (47k rows, a third of the update's waves
+    // with a slice) 59.7 -> 61.2 (profiles/r06/cg_ab_sr_fused_gather_*.jsonl)
+    const bool gfuse = (g_tune.ksp_sr_gather == 2 || (g_tune.ksp_sr_gather == 1 && k->A->nrows >= (1 << 17))) &&
+                       c->nranks == 1 && !c->comm && spmv_can_split(k->A) &&
+                       3 * Gu + k->A->nbricks <= PART_STRIDE / 2;
+    if (gfuse) Gd = Gu + k->A->nbricks;
+    bool npend = false;
+    k->prod_kernel = gfuse ? split_kernel_name(k->A, true) : mat_kernel_name(k->A);
     if (pro_mode && c->nranks > 1) {
         std::vector<int64_t> all;
         KLE_TRY(allgather_i64(c, ((int64_t)Gu << 20) | Gd, all));
@@ -1241,8 +1395,21 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                                    k->s->d, x->d, k->r->d, pu[par], pu[par] + 2 * Gu, Gd, pu[par ^ 1], c->d_scal,
                                    c->d_istate, (int)pending, par, k->atol);
             };
+            auto gog = [&](auto kern) {
+                BrickGather gs = brick_gather_src(k->A, k->u);
+                if (!npend) gs.ng = 0;  // (w complete: read it)
+                hipLaunchKernelGGL(kern, dim3(Gu), dim3(KB), 0, c->stream, gs, n, dinv, k->w->d, k->u->d, k->p->d,
+                                   k->s->d, x->d, k->r->d, pu[par], Gd, pu[par ^ 1], c->d_scal, c->d_istate,
+                                   (int)pending, par, k->atol);
+            };
             const bool unr = g_tune.upd_unroll == 2 && g_tune.upd_preload;
-            if (jac && (g_tune.upd_nt == 1 || (g_tune.upd_nt == 2 && n >= 2000000)))
+            if (gfuse) {
+                // (w complete -- the first update of a call -- the same
+                // kernel reads it: W + n iterations equal one call, bitwise)
+                if (jac) gog(k_sr_iter_g<true>);
+                else gog(k_sr_iter_g<false>);
+                npend = false;
+            } else if (jac && (g_tune.upd_nt == 1 || (g_tune.upd_nt == 2 && n >= 2000000)))
                 go(unr ? k_sr_iter<true, true, true, 2> : g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
             else if (jac) go(unr ? k_sr_iter<true, true, false, 2> : g_tune.upd_preload ? k_sr_iter<true, true> : k_sr_iter<true, false>);
             else go(g_tune.upd_preload ? k_sr_iter<false, true> : k_sr_iter<false, false>);
@@ -1251,7 +1418,11 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             par ^= 1;
             pending = true;
             int nd = 0;
-            if (Gd == Gf) KLE_TRY(spmv_dot(k->A, k->u, k->w, c->d_istate, pu[par] + 2 * Gu, &nd));
+            if (gfuse) {
+                KLE_TRY(spmv_split(k->A, k->u, k->w, c->d_istate, pu[par] + 3 * Gu));
+                npend = true;
+                nd = Gd;  // (the update's one-block share + the bricks')
+            } else if (Gd == Gf) KLE_TRY(spmv_dot(k->A, k->u, k->w, c->d_istate, pu[par] + 2 * Gu, &nd));
             else KLE_TRY(spmv(k->A, k->u, k->w, c->d_istate));
             if (nd != Gd) {
                 KLE_TRY(c->tic("reduce", &ev));
@@ -1278,6 +1449,8 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
                            Gd, c->d_scal, c->d_istate, par, k->atol);
         KLE_HIP(hipGetLastError());
     }
+    // (w complete when the call returns: a continuation's first update reads it)
+    if (npend) KLE_TRY(brick_gather_rest(k->A, k->u, k->w, c->d_istate, 1));
     k->pipe_par = par;
     KLE_TRY(poll_state(k));
     k->its = c->h_istate[I_ITS];
@@ -1322,6 +1495,7 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     // next update (k_pipe_iter_g); npend: n awaits that gather
     const bool gfuse = g_tune.ksp_pipe_gather && spmv_can_split(k->A);
     const bool gdist = c->nranks > 1 && (k->A->lo_rank >= 0 || k->A->hi_rank >= 0);
+    k->prod_kernel = gfuse ? split_kernel_name(k->A, false) : mat_kernel_name(k->A);
     bool npend = false;
     auto product = [&](const int *ist) -> int {
         if (!gfuse) return spmv(k->A, k->m, k->nv, ist);
@@ -1885,6 +2059,13 @@ int kle_ksp_continue(kle_ksp *k, kle_vec *b, kle_vec *x, int n)
     const int rc = k->type == "pipecg" ? solve_pipecg(k, b, x, true) : solve_cg_single(k, b, x, true);
     k->fixed = keep;
     return rc;
+}
+
+int kle_ksp_get_product_kernel(const kle_ksp *k, char *buf, int buflen)
+{
+    KLE_ARG(k && buf && buflen > 0, "bad arg");
+    snprintf(buf, buflen, "%s", k->prod_kernel.c_str());
+    return 0;
 }
 
 int kle_ksp_get_iteration_number(const kle_ksp *k, int *its)

@@ -744,12 +744,12 @@ bool spmv_can_split(const kle_mat *A)
 // y = A x without the owned rows' gather and the received reverse-halo sums
 // (kle_brick.hip brick_spmv split): the consumer adds them (BrickGather), or
 // brick_gather_rest does.  Only where spmv_can_split.
-int spmv_split(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate)
+int spmv_split(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double *dpart)
 {
     KLE_ARG(spmv_can_split(A), "split product: not a box-brick matrix");
     std::pair<hipEvent_t, hipEvent_t> ev;
     KLE_TRY(A->ctx->tic("spmv", &ev));
-    KLE_TRY(brick_spmv(A, x, y, istate, nullptr, true));
+    KLE_TRY(brick_spmv(A, x, y, istate, dpart, true));
     KLE_TRY(A->ctx->toc("spmv", &ev));
     return 0;
 }

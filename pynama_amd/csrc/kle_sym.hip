@@ -2318,7 +2318,7 @@ int sym_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, double
 std::string sym_kernel_name(const kle_mat *A)
 {
     if (A->sym_brick)
-        return std::string("k_nb_spmv_sym_brick<") + std::to_string(BRICK_WV) + ",true>+k_nb_gsym_gather<" +
+        return std::string("k_nb_spmv_sym_brick<") + std::to_string(BRICK_WV) + ",true,false>+k_nb_gsym_gather<" +
                std::to_string(gather_wps(A)) + ">";
     if (A->sym_gbrick) return "k_nb_spmv_gsym_brick<16,1>+k_nb_gsym_gather<" + std::to_string(gather_wps(A)) + ">";
     if (A->sym_graph)

@@ -782,6 +782,14 @@ class KSP:
         call("kle_ksp_get_iteration_number", self._h, C.byref(v))
         return v.value
 
+    def getProductKernel(self):
+        """Kernel name(s) of the last solve call's products (kle_ksp_get_product_kernel):
+        the matrix's (Mat.spmvKernel), or the bricks alone where the CG update
+        gathers the split product itself."""
+        buf = C.create_string_buffer(160)
+        call("kle_ksp_get_product_kernel", self._h, buf, 160)
+        return buf.value.decode()
+
     its = property(getIterationNumber)
 
     def getResidualNorm(self):

@@ -887,7 +887,12 @@ def test_fixed_iterations_continue_the_recurrence(pa):
     # (symmetric storage on bricks: the pipelined update gathers the split
     # product itself, k_pipe_iter_g -- a continued call starts from a complete
     # product, read by the same kernel)
-    for kt, spd in (("cg", False), ("pipecg", False), ("pipecg", True), ("cg", True)):
+    from pynama_amd.runtime import set_tuning
+    # (ksp_sr_gather 2: the single-reduction update gathers the split product
+    # too, k_sr_iter_g -- by default only from 2^17 node rows)
+    for kt, spd, srg in (("cg", False, 1), ("pipecg", False, 1), ("pipecg", True, 1), ("cg", True, 1),
+                         ("cg", True, 2)):
+        set_tuning("ksp_sr_gather", srg)
         K.setOption(K.Option.SPD, spd)
         if spd:
             assert K.spmvKernel().startswith("k_nb_spmv_sym_brick<"), K.spmvKernel()
@@ -910,14 +915,19 @@ def test_fixed_iterations_continue_the_recurrence(pa):
         y = K.createVecRight()
         with pytest.raises(pa.Error):
             ksp.solveContinue(b, y, 3)  # not the (b, x) of the last fixed solve
+    set_tuning("ksp_sr_gather", 1)
 
 
-def test_pipecg_fused_gather_matches_separate(pa):
-    """Pipelined CG on box bricks: the split product's owned-row gather folded
-    into the next update (k_pipe_iter_g, tuning ksp_pipe_gather 1, default)
-    against the separate gather launch (0): the same iteration count within
-    2, solutions within 1e-9, both at rtol 1e-10 (true residual), and the
-    oracle's CG within 1e-7."""
+@pytest.mark.parametrize("kt,knob,on", [("pipecg", "ksp_pipe_gather", 1), ("cg", "ksp_sr_gather", 2)])
+def test_fused_gather_matches_separate(pa, kt, knob, on):
+    """CG on box bricks: the split product's owned-row gather folded into the
+    next update (pipelined: k_pipe_iter_g, tuning ksp_pipe_gather; single
+    reduction, one rank: k_sr_iter_g with (A u, u) from the bricks' and the
+    one-block rows' shares, ksp_sr_gather 2: at every size -- by default
+    from 2^17 node rows) against the separate gather launch (0): the same
+    iteration count within 2, solutions
+    within 1e-9, both at rtol 1e-10 (true residual), and the oracle's CG
+    within 1e-7."""
     from oracle import oracle as O
     from pynama_amd.petsc import KSP, PC
     from pynama_amd.runtime import set_tuning
@@ -933,11 +943,12 @@ def test_pipecg_fused_gather_matches_separate(pa):
     ba = np.random.default_rng(9).uniform(-1, 1, b.getLocalSize())
     b.setArray(ba)
     out = {}
-    for fused in (1, 0):
-        set_tuning("ksp_pipe_gather", fused)
+    for fused in (on, 0):
+        set_tuning(knob, fused)
         try:
             ksp = KSP().create()
-            ksp.setType("pipecg")
+            ksp.setType(kt)
+            ksp.setCGSingleReduction(True)
             pc = PC()
             pc.setType("jacobi")
             ksp.setPC(pc)
@@ -949,13 +960,13 @@ def test_pipecg_fused_gather_matches_separate(pa):
             assert ksp.getTrueRelativeResidual() <= 1.01e-10
             out[fused] = (ksp.getIterationNumber(), x.getArray().copy())
         finally:
-            set_tuning("ksp_pipe_gather", 1)
-    assert abs(out[1][0] - out[0][0]) <= 2, (out[1][0], out[0][0])
-    assert np.linalg.norm(out[1][1] - out[0][1]) <= 1e-9 * np.linalg.norm(out[0][1])
+            set_tuning(knob, 1)
+    assert abs(out[on][0] - out[0][0]) <= 2, (out[on][0], out[0][0])
+    assert np.linalg.norm(out[on][1] - out[0][1]) <= 1e-9 * np.linalg.norm(out[0][1])
     ip, ix, d = K.getValuesCSR()
     A = O.CSR.from_arrays(ip, ix, d, int(ip.shape[0] - 1))
     xo, ito, _ = A.cg(ba, rtol=1e-10)
-    assert np.linalg.norm(out[1][1] - xo) <= 1e-7 * np.linalg.norm(xo)
+    assert np.linalg.norm(out[on][1] - xo) <= 1e-7 * np.linalg.norm(xo)
 
 
 def test_config2_full_size_properties(pa):
