@@ -367,6 +367,22 @@ def main():
         K.mult(xs, ys)
     pc_, pms = ctx.kernel_stats("spmv")
     ctx.set_profiling(False)
+    # each rank's own part alone (no halo; ranks take turns, so ranks that
+    # share a GPU do not slow each other): the per-rank skew of N > 1
+    local_ms = None
+    if dist is not None:
+        for r in range(nranks):
+            dist.barrier()
+            if r == rank:
+                try:
+                    local_ms = K.timeLocalSpmv(xs, ys, 50)
+                except pa.Error:  # (not a box-brick part)
+                    local_ms = None
+        dist.barrier()
+    local_all = [local_ms]
+    if dist is not None:
+        local_all = [None] * nranks
+        dist.all_gather_object(local_all, local_ms)
     spmv_plain = {"kernel": spmv_kernel(K, args.layout, args.ngl), "reps": pc_, "avg_ms": pms / max(pc_, 1),
                   "bytes": spmv_bytes_local,
                   "gbps": spmv_bytes_local / (pms / max(pc_, 1) * 1e-3) / 1e9,
@@ -455,7 +471,9 @@ def main():
                        # ncclCommCount / ncclCommUserRank per rank (0 / -1: no RCCL communicator)
                        "rccl_ranks": devices[0]["rccl_count"],
                        "rccl_user_ranks": [d["rccl_rank"] for d in devices],
-                       "spmv_ms_per_rank": [d["spmv_ms"] for d in devices]},
+                       "spmv_ms_per_rank": [d["spmv_ms"] for d in devices],
+                       # each rank's part alone, ranks in turn (no halo): kle_mat_time_local_spmv
+                       "spmv_local_ms_per_rank": local_all},
             # N > 1: bytes of all ranks over the slowest rank's SpMV time,
             # against N x the per-GPU peak
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",

@@ -449,6 +449,12 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes);
 /* Name of the kernel(s) y = A x launches with the current tuning, as rocprof
  * lists them (profile summaries, bench.py's roofline record). */
 int kle_mat_spmv_kernel(const kle_mat *A, char *buf, int buflen);
+/* Average device time (ms) of `reps` rank-local products y = A x: the bricks
+ * and the gather of every row they touch, with no halo exchange either way
+ * (the ghost x as they are).  A part's own kernel time, free of its
+ * neighbours -- ranks that share a GPU take turns.  Box-brick symmetric
+ * storage only (KLE_ERR_ARG otherwise); y's ghost-row sums are not sent. */
+int kle_mat_time_local_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, int reps, double *ms);
 
 /* -------------------------------------------------------------------- ksp */
 int kle_ksp_create(kle_ctx *ctx, kle_ksp **out);

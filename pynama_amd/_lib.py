@@ -157,6 +157,7 @@ _SIGS = {
     "kle_mat_get_format": [vp, C.c_char_p, C.c_int],
     "kle_mat_spmv_bytes": [vp, C.POINTER(C.c_double)],
     "kle_mat_spmv_kernel": [vp, C.c_char_p, C.c_int],
+    "kle_mat_time_local_spmv": [vp, vp, vp, C.c_int, C.POINTER(C.c_double)],
     "kle_ksp_create": [vp, pvp],
     "kle_ksp_destroy": [vp],
     "kle_ksp_set_type": [vp, C.c_char_p],

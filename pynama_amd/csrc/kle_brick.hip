@@ -932,6 +932,31 @@ int brick_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, const int *istate, doub
     return brick_gather_rest(A, x, y, istate);
 }
 
+// The rank-local part of a box-brick product, for timing it
+// (kle_mat_time_local_spmv): the bricks and the gather of every row they
+// touch, owned and upper ghost, with no halo either way -- the ghost x as
+// they are, the upper ghost rows' sums left in the send buffer.  A slab
+// part's kernel time without its neighbours (ranks sharing one GPU take
+// turns); on one rank the product itself.
+int brick_spmv_local(kle_mat *A, const kle_vec *x, kle_vec *y)
+{
+    kle_ctx *c = A->ctx;
+    const int64_t plane3 = 3 * A->row_lat[0] * A->row_lat[1];
+    const int zo = (int)(A->ghost_lo / plane3), hp = (int)(A->ghost_hi / plane3);
+    if (A->nbricks > 0) {
+        auto kern = k_nb_spmv_sym_brick<BRICK_WV, true, false>;
+        dyn_lds(c, reinterpret_cast<const void *>(kern), (size_t)A->brick_lds);
+        hipLaunchKernelGGL(kern, dim3((unsigned)A->nbricks), dim3(64 * BRICK_WV), (size_t)A->brick_lds, c->stream,
+                           (int)A->row_lat[0], (int)A->row_lat[1], (int)A->row_lat[2], zo, hp, A->brick_rstride,
+                           reinterpret_cast<const BrickDesc *>(A->d_bdesc),
+                           reinterpret_cast<const int2 *>(A->d_browd), A->d_sval, x->base, A->d_sws, y->d,
+                           nullptr, nullptr KLE_PROBE_ARG);
+        KLE_HIP(hipGetLastError());
+    }
+    const int64_t ntot = A->nrows + A->ghost_hi / 3;
+    return gsym_gather(A, y->d, 0, ntot, nullptr, nullptr, nullptr, 1, c->stream, A->d_ssingle ? x->d : nullptr);
+}
+
 // The rest of a split product (brick_spmv with split): the rows [0, nlo)
 // (every row on one rank) gathered, then the received reverse-halo sums added
 // last -- the same operations, in the same order, as the unsplit product

@@ -381,6 +381,7 @@ struct BrickGather {
     int64_t nrecv;
 };
 BrickGather brick_gather_src(const kle_mat *A, const kle_vec *x);
+int brick_spmv_local(kle_mat *A, const kle_vec *x, kle_vec *y);  // the rank-local product, no halos (timing)
 void brick_drop(kle_mat *A);
 void brick_forget(kle_mat *A);
 // IPC transport (kle_ipc.hip): slab and graph-partition halos, their reverse halos, allreduce

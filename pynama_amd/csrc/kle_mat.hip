@@ -1614,4 +1614,26 @@ int kle_mat_spmv_bytes(const kle_mat *A, double *bytes)
     return 0;
 }
 
+int kle_mat_time_local_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, int reps, double *ms)
+{
+    KLE_ARG(A && x && y && ms && reps >= 1, "bad arg");
+    KLE_TRY(check_mult_layout(A, x, y));
+    KLE_ARG(spmv_can_split(A), "local product timing: box-brick symmetric storage only");
+    kle_ctx *c = A->ctx;
+    hipEvent_t e0, e1;
+    KLE_HIP(hipEventCreate(&e0));
+    KLE_HIP(hipEventCreate(&e1));
+    int rc = hipEventRecord(e0, c->stream) == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "event record failed");
+    for (int i = 0; i < reps && !rc; ++i) rc = brick_spmv_local(A, x, y);
+    float t = 0.0f;
+    if (!rc && (hipEventRecord(e1, c->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&t, e0, e1) != hipSuccess))
+        rc = fail(KLE_ERR_DEVICE, "event timing failed");
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (rc) return rc;
+    *ms = (double)t / reps;
+    return 0;
+}
+
 }  // extern "C"

@@ -510,6 +510,14 @@ class Mat:
     def mult(self, x, y):
         call("kle_mat_mult", self._h, x._h, y._h)
 
+    def timeLocalSpmv(self, x, y, reps=50):
+        """Average device ms of `reps` rank-local products (kle_mat_time_local_spmv:
+        the bricks and their gather, no halo either way; no PETSc counterpart) --
+        a part's own kernel time, for ranks that take turns on one GPU."""
+        ms = C.c_double()
+        call("kle_mat_time_local_spmv", self._h, x._h, y._h, int(reps), C.byref(ms))
+        return ms.value
+
     def multAdd(self, x, v2, v3):
         call("kle_mat_mult_add", self._h, x._h, v2._h, v3._h)
 

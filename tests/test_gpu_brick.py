@@ -165,6 +165,25 @@ def test_brick_spmv_edge_inputs(pa):
     assert np.isfinite((K * x).getArray()).all()  # (the next product is clean again)
 
 
+def test_local_product_timing_on_one_rank_is_the_product(pa):
+    """kle_mat_time_local_spmv (bench.py's per-rank part timing at N > 1): on
+    one rank the local product is the product -- y bitwise equal to K x --
+    and the average time is positive; a matrix without bricks is refused."""
+    _, mat = _mat(pa, [6, 5, 4], 5)
+    K = mat.K
+    x = K.createVecRight()
+    x.setArray(np.random.default_rng(4).uniform(-1, 1, x.getLocalSize()))
+    y = K.createVecLeft()
+    K.setOption(K.Option.SPD, False)
+    with pytest.raises(pa.Error):
+        K.timeLocalSpmv(x, y, 3)
+    K.setOption(K.Option.SPD, True)
+    ref = (K * x).getArray().copy()
+    ms = K.timeLocalSpmv(x, y, 7)
+    assert ms > 0.0
+    np.testing.assert_array_equal(y.getArray(), ref)
+
+
 def test_brick_cg_reproducible_and_matches_oracle(pa):
     """CG through the brick SpMV: the oracle's Jacobi-CG iteration count within
     2, the solution within 1e-7, two solves bitwise equal."""

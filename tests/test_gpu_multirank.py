@@ -74,6 +74,14 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
         u = vel.getArray()
         ip, ix, d = mat.K.getValuesCSR()
         dn = pa.petsc.Vec().createMPI((7, None))  # exercise the allgather-based layout
+        local_ms = None
+        if sym:  # each rank's part alone, ranks in turn (bench.py's spmv_local_ms_per_rank)
+            yl = mat.K.createVecLeft()
+            for t in range(size):
+                dist.barrier()
+                if t == rank and mat.K.spmvKernel().startswith("k_nb_spmv_sym_brick<"):
+                    local_ms = mat.K.timeLocalSpmv(xv, yl, 5)
+            dist.barrier()
         res = {"rank": rank, "lo": lo, "hi": hi, "u": u, "its": ksp.getIterationNumber(),
                "corr": ksp.getCorrectionIterations(),
                "true": ksp.getTrueRelativeResidual(), "ip": ip, "ix": ix, "d": d,
@@ -81,7 +89,7 @@ def _worker(rank, size, port, nelem, ngl, q, overlap=True, ksp_type="cg", msh=No
                "overlap_equal": bool(np.array_equal(y_ov, y_pl)), "y": y_ov, "x": xv.getArray(),
                "coords": dom.getFullCoordArray().reshape(-1, 3),
                "ov_diff": (np.nonzero(y_ov != y_pl)[0][:12].tolist(), len(y_ov)),
-               "sym": mat.K.isSymmetricStorage(), "kernel": mat.K.spmvKernel(),
+               "sym": mat.K.isSymmetricStorage(), "kernel": mat.K.spmvKernel(), "local_ms": local_ms,
                "transport": pa.get_ctx().device_info()["transport"]}
         q.put(res)
     except Exception as e:  # report instead of hanging the peer
@@ -140,6 +148,7 @@ def test_partitioned_solve_symmetric_storage(size, nelem, ngl, ksp_type, overlap
     for r in res:
         assert r["sym"], r["rank"]
         assert r["kernel"].startswith("k_nb_spmv_sym_brick<"), r["kernel"]
+        assert r["local_ms"] > 0.0, r["rank"]  # (kle_mat_time_local_spmv on the slab part)
 
 
 @pytest.mark.parametrize("size,nelem,ngl,ksp_type", [(3, [2, 3, 3], 3, "cg"), (8, [2, 2, 8], 4, "pipecg")])

@@ -100,3 +100,4 @@ def test_bench_launches_its_own_ranks():
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 10
     assert d["solve"]["reason"] > 0 and d["solve"]["true_rel_residual"] <= 2e-10
     assert d["roofline"]["peak"] == 16000.0
+    assert len(d["config"]["spmv_local_ms_per_rank"]) == 2  # (null: full-storage parts at this size)
