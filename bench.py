@@ -318,7 +318,10 @@ def main():
     brk = {k: ctx.kernel_stats(k)[1] / nb_its for k in ("spmv", "cg_update", "p_update", "reduce",
                                                         "halo", "allreduce")}
     t_max = t_loc
-    tot_bytes = spmv_bytes_local
+    # the timed products' algorithmic bytes (the bricks' own share where the CG
+    # update gathers a split product; else K's, = the plain leg's)
+    prod_bytes = kb.getProductBytes() or spmv_bytes_local
+    tot_bytes = prod_bytes
     tot_nnz = nnz_local
     spmv_avg_ms = spmv_ms / max(spmv_cnt, 1)
     if dist is not None:
@@ -326,7 +329,7 @@ def main():
         tt = torch.tensor([t_loc, spmv_avg_ms], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max, spmv_avg_max = float(tt[0]), float(tt[1])
-        sb = torch.tensor([spmv_bytes_local, float(nnz_local)], dtype=torch.float64)
+        sb = torch.tensor([prod_bytes, float(nnz_local)], dtype=torch.float64)
         dist.all_reduce(sb, op=dist.ReduceOp.SUM)
         tot_bytes, tot_nnz = float(sb[0]), int(sb[1])
     else:
@@ -417,7 +420,7 @@ def main():
             ("-sym" if kname.startswith("k_nb_spmv_sym") else
              "-gsym" if kname.startswith("k_nb_spmv_gsym") else
              {"k_nb_spmv_xl<8>": "-xl", "k_nb_spmv_dict": "-dict"}.get(kname, "")))
-    traffic, traffic_status = lookup_traffic(args.traffic, tkey, kname, spmv_bytes_local)
+    traffic, traffic_status = lookup_traffic(args.traffic, tkey, kname, prod_bytes)
 
     ops = None
     if args.ops == "on" or (args.ops == "auto" and nranks == 1):
@@ -479,7 +482,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * nranks, "unit": "GB/s",
                          "frac": achieved / (HBM_PEAK_GBS * nranks) if achieved else None, "traffic": traffic,
                          "traffic_status": traffic_status, "traffic_key": tkey,
-                         "traffic_over_bytes": traffic / spmv_bytes_local if traffic else None,
+                         "traffic_over_bytes": traffic / prod_bytes if traffic else None,
                          "kernel": kname,
                          "bytes_per_launch": tot_bytes,
                          "csr_bytes_per_launch": csr_bytes, "csr_equiv_gbps": csr_equiv,

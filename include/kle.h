@@ -481,6 +481,9 @@ int kle_ksp_get_iteration_number(const kle_ksp *k, int *its);
  * them: kle_mat_spmv_kernel's, or -- where the CG update gathers a split
  * box-brick product itself -- the brick kernel alone (one rank). */
 int kle_ksp_get_product_kernel(const kle_ksp *k, char *buf, int buflen);
+/* Algorithmic bytes one of those products moves (kle_mat_spmv_bytes, or the
+ * bricks' own share of a split product: the region sums written, not read). */
+int kle_ksp_get_product_bytes(const kle_ksp *k, double *bytes);
 int kle_ksp_get_residual_norm(const kle_ksp *k, double *rnorm);
 int kle_ksp_get_converged_reason(const kle_ksp *k, int *reason);
 /* ||b - A x|| / ||b|| recomputed after the last solve. */

@@ -173,6 +173,7 @@ _SIGS = {
     "kle_ksp_solve": [vp, vp, vp],
     "kle_ksp_get_iteration_number": [vp, C.POINTER(C.c_int)],
     "kle_ksp_get_product_kernel": [vp, C.c_char_p, C.c_int],
+    "kle_ksp_get_product_bytes": [vp, C.POINTER(C.c_double)],
     "kle_ksp_get_residual_norm": [vp, C.POINTER(C.c_double)],
     "kle_ksp_get_converged_reason": [vp, C.POINTER(C.c_int)],
     "kle_ksp_get_true_relative_residual": [vp, C.POINTER(C.c_double)],

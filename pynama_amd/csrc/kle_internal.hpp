@@ -400,6 +400,7 @@ int halo_reverse_plan(kle_ctx *ctx, const HaloPlan &P, int64_t hi0, int bs, cons
                       hipStream_t st);  // kle_core.hip
 std::string sym_kernel_name(const kle_mat *A);
 double sym_spmv_bytes(const kle_mat *A);
+double brick_split_bytes(const kle_mat *A);  // a split brick product: the bricks alone
 // Performance knobs (kle_set_tuning): every setting gives correct results;
 // they exist for in-process A/B measurements (tools/cg_ab.py).
 struct Tuning {

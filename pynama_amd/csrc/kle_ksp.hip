@@ -1065,6 +1065,7 @@ struct kle_ksp {
     int maxit = 10000, restart = 30, fixed = 0, check_every = 8;
     int pipe_par = 0;  // pipelined CG: parity of the next update launch (k_pipe_iter)
     std::string prod_kernel;  // the kernel(s) of the last call's products (kle_ksp_get_product_kernel)
+    double prod_bytes = 0.0;  // and the algorithmic bytes each moves (kle_ksp_get_product_bytes)
     kle_mat *A = nullptr;
     kle_vec *r = nullptr, *p = nullptr, *q = nullptr, *dinv = nullptr;
     kle_vec *u = nullptr, *w = nullptr, *s = nullptr;  // single-reduction CG
@@ -1306,6 +1307,11 @@ static std::string mat_kernel_name(const kle_mat *A)
     if (kle_mat_spmv_kernel(A, buf, sizeof buf)) return "?";
     return buf;
 }
+static double mat_bytes(const kle_mat *A)
+{
+    double b = 0.0;
+    return kle_mat_spmv_bytes(A, &b) ? 0.0 : b;
+}
 static std::string split_kernel_name(const kle_mat *A, bool dot)
 {
     const std::string m = mat_kernel_name(A);
@@ -1374,6 +1380,7 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     if (gfuse) Gd = Gu + k->A->nbricks;
     bool npend = false;
     k->prod_kernel = gfuse ? split_kernel_name(k->A, true) : mat_kernel_name(k->A);
+    k->prod_bytes = gfuse ? brick_split_bytes(k->A) : mat_bytes(k->A);
     if (pro_mode && c->nranks > 1) {
         std::vector<int64_t> all;
         KLE_TRY(allgather_i64(c, ((int64_t)Gu << 20) | Gd, all));
@@ -1496,6 +1503,7 @@ static int solve_pipecg(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
     const bool gfuse = g_tune.ksp_pipe_gather && spmv_can_split(k->A);
     const bool gdist = c->nranks > 1 && (k->A->lo_rank >= 0 || k->A->hi_rank >= 0);
     k->prod_kernel = gfuse ? split_kernel_name(k->A, false) : mat_kernel_name(k->A);
+    k->prod_bytes = gfuse ? brick_split_bytes(k->A) : mat_bytes(k->A);  // (N > 1: the ghost slices' gather not counted)
     bool npend = false;
     auto product = [&](const int *ist) -> int {
         if (!gfuse) return spmv(k->A, k->m, k->nv, ist);
@@ -2065,6 +2073,13 @@ int kle_ksp_get_product_kernel(const kle_ksp *k, char *buf, int buflen)
 {
     KLE_ARG(k && buf && buflen > 0, "bad arg");
     snprintf(buf, buflen, "%s", k->prod_kernel.c_str());
+    return 0;
+}
+
+int kle_ksp_get_product_bytes(const kle_ksp *k, double *bytes)
+{
+    KLE_ARG(k && bytes, "null arg");
+    *bytes = k->prod_bytes;
     return 0;
 }
 

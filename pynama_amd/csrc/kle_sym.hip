@@ -2333,6 +2333,15 @@ std::string sym_kernel_name(const kle_mat *A)
 
 // symmetric storage: the stored (upper) blocks, per row its value offset and
 // box, x and y once, the tile partials written and read
+// A split box-brick product (brick_spmv split: the CG update gathers it):
+// the bricks alone move the values, the row descriptors, x and y's direct
+// sums once, and write their region sums once -- the sums' read is the
+// update's
+double brick_split_bytes(const kle_mat *A)
+{
+    return (double)A->sblocks * 72.0 + A->nrows * (8.0 + 48.0) + (double)A->sws_entries * 24.0;
+}
+
 double sym_spmv_bytes(const kle_mat *A)
 {
     // graph: values + 2-B dictionary positions per stored block; per row its

@@ -798,6 +798,12 @@ class KSP:
         call("kle_ksp_get_product_kernel", self._h, buf, 160)
         return buf.value.decode()
 
+    def getProductBytes(self):
+        """Algorithmic bytes of one of those products (kle_ksp_get_product_bytes)."""
+        v = C.c_double()
+        call("kle_ksp_get_product_bytes", self._h, C.byref(v))
+        return v.value
+
     its = property(getIterationNumber)
 
     def getResidualNorm(self):
