@@ -504,11 +504,9 @@ __global__ __launch_bounds__(64 * WV, 1) void k_nb_spmv_sym_brick(int Lx, int Ly
     // off the lattice are never read)
     double *dst = ws + wsoff;
     double ds = 0.0;  // DOT: this thread's (region sum, x)
-    const float rxy_inv = __builtin_amdgcn_rcpf((float)RXY), rx_inv = __builtin_amdgcn_rcpf((float)RX);
     for (int t = threadIdx.x; t < 3 * RN; t += NT) {
         const int k = t / 3, c = t - 3 * k;
-        // (exact float-reciprocal quotients: k < 2^20; no integer division loop)
-        const int rz = sym_div(k, RXY, rxy_inv), rem = k - rz * RXY, ry = sym_div(rem, RX, rx_inv), rx = rem - ry * RX;
+        const int rz = k / (RX * RY), rem = k - rz * RX * RY, ry = rem / RX, rx = rem - ry * RX;
         const int gx = ox + rx, gy = oy + ry, gz = oz + rz;
         if (gx < 0 || gx >= Lx || gy < 0 || gy >= Ly || gz + zo < 0 || gz >= Lz + hp) continue;
         const double v = fx_to_d(acc[c * RS + k]) * T1 * T2;
