@@ -424,7 +424,14 @@ def main():
 
     ops = None
     if args.ops == "on" or (args.ops == "auto" and nranks == 1):
-        ops = bench_operators(pa, mat, ctx, sol, dim)
+        try:
+            ops = bench_operators(pa, mat, ctx, sol, dim)
+        except pa.Error as e:
+            # (the reference's full operator matrices at p = 6 on 3.9M DoF do
+            # not fit beside K: reported, not fatal -- they are off the path)
+            if args.ops == "on" or e.ierr != 55:
+                raise
+            ops = {"skipped": str(e)}
 
     cpu = None
     if rank == 0 and nranks == 1 and not args.no_cpu_baseline:
