@@ -959,6 +959,14 @@ def test_fused_gather_matches_separate(pa, kt, knob, on):
             assert ksp.getConvergedReason() > 0
             assert ksp.getTrueRelativeResidual() <= 1.01e-10
             out[fused] = (ksp.getIterationNumber(), x.getArray().copy())
+            # the products the solve timed: the bricks alone (with their (y, x)
+            # shares for the single-reduction fold) and their own bytes, or K's
+            if fused:
+                assert ksp.getProductKernel() == ("k_nb_spmv_sym_brick<16,true,true>" if kt == "cg"
+                                                  else "k_nb_spmv_sym_brick<16,true,false>")
+                assert 0 < ksp.getProductBytes() < K.spmvBytes()
+            else:
+                assert ksp.getProductKernel() == K.spmvKernel() and ksp.getProductBytes() == K.spmvBytes()
         finally:
             set_tuning(knob, 1)
     assert abs(out[on][0] - out[0][0]) <= 2, (out[on][0], out[0][0])
