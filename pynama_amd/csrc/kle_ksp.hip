@@ -748,7 +748,9 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
 // brick's): partials [3][G] = (r,u) | (r,r) | that share, the bricks' after
 // them (G2 = G + bricks in all).  Without pro (the first update of a call)
 // w is complete and read as it is.
-template <bool JAC>
+// PRE (upd_preload): the first slice's vectors are loaded before the
+// prologue too, so their latency overlaps the partial sums (same arithmetic)
+template <bool JAC, bool PRE>
 __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_iter_g(BrickGather gs, int64_t n,
                                                   const double *__restrict__ dinv, const double *__restrict__ w,
                                                   double *__restrict__ u, double *__restrict__ p,
@@ -807,11 +809,27 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
         nl[wv][3 * lane + 2] = s2;
         __builtin_amdgcn_wave_barrier();
     };
-    int64_t sl = (int64_t)blockIdx.x * WPB + wv;
-    // the first slice's gather before the prologue (it needs no scalar)
+    const int64_t sl0 = (int64_t)blockIdx.x * WPB + wv;
+    int64_t sl = sl0;
+    // the first slice's gather (and, PRE, its vectors) before the prologue
+    // (they need no scalar)
     StageIn in;
     if (threadIdx.x == 0) in = stage_inputs(scal, ist, par);
-    if (sl < nsl) gather(sl);
+    double e[3][6];  // u, p, s, x, r, M of the slice's entries
+    auto load = [&](int64_t s0) {
+#pragma unroll
+        for (int ps = 0; ps < 3; ++ps) {
+            const int64_t i = s0 * 192 + ps * 64 + lane;
+            if (i < n) {
+                e[ps][0] = u[i], e[ps][1] = p[i], e[ps][2] = sv[i], e[ps][3] = x[i], e[ps][4] = r[i];
+                e[ps][5] = JAC ? dinv[i] : 1.0;
+            }
+        }
+    };
+    if (sl < nsl) {
+        if constexpr (PRE) load(sl);
+        gather(sl);
+    }
     if (ist[I_REASON] != 0) return;
     double t[3] = {0.0, 0.0, 0.0};
     if (pro) sums3(pu_in, pu_in + G, G, pu_in + 2 * G, G2, t);
@@ -819,21 +837,26 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_num_sgpr(64))) void k_sr_
     if (stage_prologue(pro, t, scal, ist, par, atol, alpha, beta, &in)) return;
     double acc[3] = {0.0, 0.0, 0.0};
     for (; sl < nsl; sl += sst) {
-        if (sl != (int64_t)blockIdx.x * WPB + wv) gather(sl);
+        if (sl != sl0) {
+            load(sl);
+            gather(sl);
+        } else if (!PRE) {
+            load(sl);
+        }
 #pragma unroll
         for (int ps = 0; ps < 3; ++ps) {
             const int el = ps * 64 + lane;
             const int64_t i = sl * 192 + el;
             if (i >= n) break;
             const double wi = nl[wv][el];
-            const double pi = u[i] + beta * p[i];
-            const double si = wi + beta * sv[i];
+            const double pi = e[ps][0] + beta * e[ps][1];
+            const double si = wi + beta * e[ps][2];
             p[i] = pi;
             sv[i] = si;
-            x[i] = x[i] + alpha * pi;
-            const double ri = r[i] - alpha * si;
+            x[i] = e[ps][3] + alpha * pi;
+            const double ri = e[ps][4] - alpha * si;
             r[i] = ri;
-            const double ui = JAC ? dinv[i] * ri : ri;
+            const double ui = JAC ? e[ps][5] * ri : ri;
             u[i] = ui;
             nl[wv][el] = ui;  // (this lane's own entry: read above, by this lane only)
             acc[0] += ri * ui;
@@ -1413,8 +1436,8 @@ static int solve_cg_single(kle_ksp *k, kle_vec *b, kle_vec *x, bool cont)
             if (gfuse) {
                 // (w complete -- the first update of a call -- the same
                 // kernel reads it: W + n iterations equal one call, bitwise)
-                if (jac) gog(k_sr_iter_g<true>);
-                else gog(k_sr_iter_g<false>);
+                if (jac) gog(g_tune.upd_preload ? k_sr_iter_g<true, true> : k_sr_iter_g<true, false>);
+                else gog(g_tune.upd_preload ? k_sr_iter_g<false, true> : k_sr_iter_g<false, false>);
                 npend = false;
             } else if (jac && (g_tune.upd_nt == 1 || (g_tune.upd_nt == 2 && n >= 2000000)))
                 go(unr ? k_sr_iter<true, true, true, 2> : g_tune.upd_preload ? k_sr_iter<true, true, true> : k_sr_iter<true, false, true>);
