@@ -10,6 +10,6 @@ for i in $(seq 1 $TRIES); do
   rc=$?
   st=$(python3 -c "import json;print(json.load(open('/root/repo/gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
   if [ "$st" != "transient" ]; then exit $rc; fi
-  echo "[retry] no box (attempt $i), waiting"; sleep 150
+  echo "[retry] no box (attempt $i), waiting"; sleep ${RETRY_SLEEP:-150}
 done
 exit 3
