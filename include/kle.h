@@ -98,8 +98,7 @@ const char *kle_last_error(void);
  * first of its two launches; 0 auto), "spmv_sym_brick" (read at build:
  * the box K of one rank on bricks -- one 16-wave workgroup per CU, the
  * brick region's x and exact sums in LDS for the whole value stream; 1
- * default, 0 the 128-row tiles), "spmv_brick_ahead" (brick kernel: items in
- * flight ahead of the summed one, 1 default or 2), "spmv_brick_max" (read at
+ * default, 0 the 128-row tiles), "spmv_brick_max" (read at
  * build: at most this many bricks, 0 planned), "spmv_brick_rounds" (read at
  * build: at most this many bricks per CU, default 1), "spmv_brick_split" (read
  * at build: force nbx + 100 nby + 10000 nbz bricks, 0 planned),
@@ -113,7 +112,11 @@ const char *kle_last_error(void);
  * rounds per CU; 1 default), "ipc_sentinel" (IPC transport debug mode:
  * consumed mailbox slots overwritten with NaN before the ack; 0 default),
  * "ksp_corr_fault" (test hook: correction solves that end in NaN; 0),
- * "upd_unroll" (CG update kernel: 1 default or 2),
+ * "upd_unroll" (CG update kernel: 1 default or 2), "ksp_pipe_gather" (box
+ * bricks: the pipelined CG's update gathers the split product itself; 1
+ * default, 0 a separate gather launch), "ksp_sr_gather" (the same for the
+ * single-reduction CG at one rank, the bricks forming (A u, u): 1 default
+ * from 2^17 node rows, 2 always, 0 never),
  * "spmv_sym_tile64" (read at build: 8 x 2 x 4-row tiles -- 0 auto, below
  * "spmv_sym_tile64_max" (640) 128-row tiles; 1 wherever two workgroups fit
  * a CU; 2 never), "spmv_sym_ovl_b" (N > 1, box symmetric SpMV with halo
