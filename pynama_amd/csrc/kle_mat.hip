@@ -1622,7 +1622,10 @@ int kle_mat_time_local_spmv(kle_mat *A, const kle_vec *x, kle_vec *y, int reps, 
     kle_ctx *c = A->ctx;
     hipEvent_t e0, e1;
     KLE_HIP(hipEventCreate(&e0));
-    KLE_HIP(hipEventCreate(&e1));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        hipEventDestroy(e0);
+        return fail(KLE_ERR_DEVICE, "event create failed");
+    }
     int rc = hipEventRecord(e0, c->stream) == hipSuccess ? 0 : fail(KLE_ERR_DEVICE, "event record failed");
     for (int i = 0; i < reps && !rc; ++i) rc = brick_spmv_local(A, x, y);
     float t = 0.0f;
